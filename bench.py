@@ -1,0 +1,200 @@
+"""bench.py -- BASELINE.json headline: MiB/s decompressed per node on the
+64 x 64 MiB raw-deflate batch (configs[1]), inflated on MI355X.
+
+One "step" = one zs_inflate_batch() over all of this rank's streams, inputs
+already resident in HBM, outputs written to HBM (ZS_F_DEVICE).  Weak scaling:
+every rank decodes its own 64 streams (stream ids rank*64 .. rank*64+63).
+
+Prints ONE JSON line (rank 0) with the driver's contract fields plus
+  roofline     -- decode kernel: algorithmic bytes (compressed in + decompressed
+                  out) per launch / average decode-kernel time measured with HIP
+                  events on the launch stream, vs 8 TB/s HBM peak;
+  cpu_baseline -- host zlib inflate on a bounded sample of the same streams,
+                  timed on this host (1 thread, and all threads).
+"""
+import argparse
+import ctypes
+import hashlib
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "zlib-streams_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+METRIC = "MiB/s decompressed (+ compressed) per node, 64×64 MiB raw-deflate batch"
+HBM_PEAK_GBS = 8000.0
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(comps, raws, wbits, sample, threads):
+    """Host zlib inflate of `sample` streams (whole-buffer Z_FINISH), 1 thread
+    and `threads` threads.  Returns the cpu_baseline JSON object."""
+    import numpy as np
+
+    so = os.path.join(ROOT, "oracle", "libzs_cpubase.so")
+    L = ctypes.CDLL(so)
+    L.zs_cpu_inflate.restype = ctypes.c_double
+    L.zs_cpu_inflate.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t),
+                                 ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
+                                 ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_int)]
+    L.zs_cpu_zlib_version.restype = ctypes.c_char_p
+    n = len(sample)
+    cp = (ctypes.c_void_p * n)(*[comps[i].ctypes.data for i in sample])
+    cl = (ctypes.c_size_t * n)(*[len(comps[i]) for i in sample])
+    outs = [np.empty(len(raws[i]), dtype=np.uint8) for i in sample]
+    op = (ctypes.c_void_p * n)(*[o.ctypes.data for o in outs])
+    cap = max(len(raws[i]) for i in sample)
+    tot = ctypes.c_uint64()
+    bad = ctypes.c_int()
+    t1 = L.zs_cpu_inflate(cp, cl, op, cap, n, 1, wbits, 0, ctypes.byref(tot), ctypes.byref(bad))
+    v1 = tot.value / t1 / 2**20
+    tn = L.zs_cpu_inflate(cp, cl, op, cap, n, threads, wbits, 0, ctypes.byref(tot), ctypes.byref(bad))
+    vn = tot.value / tn / 2**20
+    ok = all(np.array_equal(outs[k], raws[i]) for k, i in enumerate(sample)) and not bad.value
+    return {"value": round(v1, 1), "unit": "MiB/s", "cores": 1, "kind": "reference",
+            "impl": f"host zlib {L.zs_cpu_zlib_version().decode()} inflate (upstream of reference src/inflate.c "
+                    "for windowBits -15; the reference build itself needs the absent zlib submodule)",
+            "sample": f"{n} of the streams (alternating Zipf/lines), whole-buffer inflate(Z_FINISH), "
+                      f"{tot.value / 2**20:.0f} MiB out per pass",
+            "value_all_threads": round(vn, 1), "threads": threads, "seconds_1t": round(t1, 2), "verified": ok}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--streams", type=int, default=64)
+    ap.add_argument("--stream-mib", type=int, default=64)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=8)
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        import torch.distributed as tdist
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    import corpus
+    import zstreams
+
+    nbytes = args.stream_mib << 20
+    first = rank * args.streams
+    host_threads = min(16, os.cpu_count() or 1)
+    t0 = time.time()
+    raws, comps = corpus.batch(first, args.streams, nbytes, level=6, wbits=-15, nthreads=host_threads)
+    comp_total = sum(len(c) for c in comps)
+    log(f"[rank {rank}] generated+compressed {args.streams} x {args.stream_mib} MiB in {time.time() - t0:.1f}s "
+        f"(ratio {args.streams * nbytes / comp_total:.2f})")
+
+    # device-resident inputs (16 B aligned) and outputs
+    offs = []
+    o = 0
+    for c in comps:
+        offs.append(o)
+        o += (len(c) + 255) & ~255
+    d_in = torch.empty(o + 256, dtype=torch.uint8, device=dev)
+    d_in_cpu = np.zeros(o + 256, dtype=np.uint8)
+    for c, of in zip(comps, offs):
+        d_in_cpu[of:of + len(c)] = c
+    d_in.copy_(torch.from_numpy(d_in_cpu))
+    del d_in_cpu
+    d_out = torch.empty(args.streams * nbytes, dtype=torch.uint8, device=dev)
+    in_ptrs = [d_in.data_ptr() + of for of in offs]
+    in_lens = [len(c) for c in comps]
+    out_ptrs = [d_out.data_ptr() + k * nbytes for k in range(args.streams)]
+    caps = [nbytes] * args.streams
+
+    torch.cuda.synchronize()
+    stream = torch.cuda.Stream(device=dev)  # a real (non-NULL) HIP stream shared with the library
+    zstreams.set_stream(stream.cuda_stream)
+
+    def step():
+        return zstreams.inflate_batch_device(in_ptrs, in_lens, out_ptrs, caps, -15)
+
+    for _ in range(args.warmup):
+        res = step()
+    # correctness of the measured configuration (bit-exact vs generator)
+    res = step()
+    ok = all(r["ret"] == 1 and r["total_out"] == nbytes and r["total_in"] == in_lens[k] for k, r in enumerate(res))
+    torch.cuda.synchronize()
+    out_host = d_out.cpu().numpy().reshape(args.streams, nbytes)
+    ok = ok and all(np.array_equal(out_host[k], raws[k]) for k in range(args.streams))
+    del out_host
+    log(f"[rank {rank}] verified bit-exact: {ok}")
+
+    zstreams.profile(True)
+    if dist:
+        tdist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        tdist.barrier()
+    t_el = time.perf_counter() - t_start
+    k_ms, k_n = zstreams.profile_read()
+    zstreams.profile(False)
+    if dist:
+        t = torch.tensor([t_el], dtype=torch.float64, device=dev)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        t_el = float(t.item())
+        okt = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+        tdist.all_reduce(okt, op=tdist.ReduceOp.MIN)
+        ok = bool(okt.item())
+
+    out_bytes = world * args.streams * nbytes * args.steps
+    value = out_bytes / t_el / 2**20
+    per_launch_alg = comp_total + args.streams * nbytes  # algorithmic bytes of one decode launch
+    k_avg_s = (k_ms / max(k_n, 1)) / 1e3
+    achieved = per_launch_alg / k_avg_s / 1e9 if k_avg_s > 0 else 0.0
+
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        sample = list(range(0, args.streams, max(1, args.streams // args.cpu_sample)))[:args.cpu_sample]
+        # alternate Zipf / lines in the sample
+        sample = sorted(set(sample[: len(sample) // 2] + [s + args.streams // 2 for s in sample[: len(sample) // 2]]))
+        sample = [s for s in sample if s < args.streams]
+        cpu = cpu_baseline(comps, raws, -15, sample, host_threads)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "MiB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(t_el * 1e3 / args.steps, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic: 32 Zipf-text + 32 line-text streams per GPU, host zlib L6 memLevel 8 raw (-15)",
+            "config": {"workload": f"{args.streams}x{args.stream_mib}MiB raw-deflate inflate (windowBits -15), "
+                                   "inputs resident in HBM", "streams_per_gpu": args.streams,
+                       "stream_bytes": nbytes, "compressed_bytes_per_gpu": comp_total,
+                       "parallelism": f"stream-shard x{world}"},
+            "verified_bit_exact": ok,
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                         "kernel": "zs_decode_kernel<false>", "kernel_ms_avg": round(k_avg_s * 1e3, 3),
+                         "alg_bytes_per_launch": per_launch_alg},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if dist:
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

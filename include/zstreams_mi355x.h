@@ -1,0 +1,99 @@
+/*
+ * zstreams_mi355x.h -- C-ABI of libzstreams_mi355x.so, the MI355X inflate core.
+ *
+ * Three surfaces, all plain pointers and sizes:
+ *
+ *  1. The reference's handle-based stream ABI, symbol for symbol
+ *     (reference export list: Makefile:288).  Handles are widened from the
+ *     WASM `unsigned` to `uintptr_t` (a 64-bit process cannot round-trip a
+ *     pointer through 32 bits).  Each entry replaces the function of the same
+ *     name in the reference:
+ *       inflate_new / inflate9_new         src/wasm/wasm_stream_common.c:7-18
+ *       inflate_init                       src/wasm/inflate_stream_wasm.c:22-27
+ *       inflate_init_raw                   src/wasm/inflate_stream_wasm.c:29-34
+ *       inflate_init_gzip                  src/wasm/inflate_stream_wasm.c:36-45
+ *       inflate9_init / inflate9_init_raw  src/wasm/inflate9_stream_wasm.c:15-22
+ *       *_process                          src/wasm/wasm_stream_common.c:37-63
+ *       *_last_consumed                    src/wasm/wasm_stream_common.c:30-35
+ *       *_end                              src/wasm/wasm_stream_common.c:20-28
+ *     process() returns (produced & 0x00ffffff) | ((ret & 0xff) << 24), the
+ *     zlib code as a signed byte in the top 8 bits, exactly like the reference.
+ *
+ *  2. The zlib inflate ABI used by the reference's native harnesses
+ *     (test/payload_decompress.c:124-178): inflateInit2_, inflateInit_,
+ *     inflate, inflateEnd over the standard z_stream (sizeof 112 on x86-64).
+ *     Declared by <zlib.h>; this library defines them.
+ *
+ *  3. A batch entry for many independent whole streams (new; no reference
+ *     analog): zs_inflate_batch().  Each job has the semantics of ONE
+ *     inflate(strm, Z_FINISH) call over the whole input into an out_cap-byte
+ *     buffer after inflateInit2(strm, window_bits) (src/inflate.c:186, 597):
+ *     same ret, msg, total_in, total_out and adler.
+ *
+ * All decoding runs on the GPU (HIP, gfx950).  There is no CPU fallback: if no
+ * HIP device is usable every entry point fails with Z_STREAM_ERROR /
+ * ZS_ENODEV and zs_last_error() says why.
+ */
+#ifndef ZSTREAMS_MI355X_H
+#define ZSTREAMS_MI355X_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- 1. reference stream ABI (handles are uintptr_t, 0 = allocation failure) ---- */
+uintptr_t inflate_new(void);
+int inflate_init(uintptr_t h);
+int inflate_init_raw(uintptr_t h);
+int inflate_init_gzip(uintptr_t h);
+int inflate_process(uintptr_t h, uintptr_t in_ptr, unsigned in_len, uintptr_t out_ptr, unsigned out_len, int flush);
+int inflate_end(uintptr_t h);
+unsigned inflate_last_consumed(uintptr_t h);
+
+uintptr_t inflate9_new(void);
+int inflate9_init(uintptr_t h);
+int inflate9_init_raw(uintptr_t h);
+int inflate9_process(uintptr_t h, uintptr_t in_ptr, unsigned in_len, uintptr_t out_ptr, unsigned out_len, int flush);
+int inflate9_end(uintptr_t h);
+unsigned inflate9_last_consumed(uintptr_t h);
+
+/* ---- 3. batch API ---- */
+typedef struct zs_job {
+  const void *in;      /* compressed bytes (host, or device with ZS_F_DEVICE) */
+  uint64_t in_len;     /* < 2^29 */
+  void *out;           /* output buffer (host, or 16-byte aligned device memory) */
+  uint64_t out_cap;    /* < 2^32 */
+  int32_t window_bits; /* as inflateInit2: -8..-15 raw, -16 raw deflate64, 8..15 zlib, +16 gzip, +32 auto */
+  int32_t reserved;
+} zs_job;
+
+typedef struct zs_result {
+  int32_t ret;         /* Z_STREAM_END, Z_DATA_ERROR, Z_BUF_ERROR, Z_NEED_DICT, Z_STREAM_ERROR */
+  int32_t reserved;
+  uint64_t total_in;
+  uint64_t total_out;
+  uint32_t adler;      /* strm->adler after the call (0 for raw streams) */
+  uint32_t reserved2;
+  const char *msg;     /* strm->msg (static string) or NULL */
+} zs_result;
+
+#define ZS_F_DEVICE 1u /* job in/out pointers are device (HBM) pointers: no staging copies */
+
+#define ZS_ENODEV (-100)
+
+int zs_inflate_batch(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t flags);
+/* launch on this HIP stream (hipStream_t); NULL = the library's own stream */
+int zs_set_stream(void *hip_stream);
+int zs_synchronize(void);
+/* decode-kernel timing via HIP events on the launch stream */
+int zs_profile(int enable);
+int zs_profile_read(double *ms, uint64_t *launches);
+const char *zs_version(void);
+const char *zs_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,86 @@
+/*
+ * cpu_baseline.c -- CPU baseline timer for bench.py (test/bench infrastructure).
+ *
+ * Times host zlib inflate (libz, the upstream of the reference's vendored
+ * src/inflate.c; SURVEY.md §6: within 3-9% of the reference build) and the
+ * oracle port (zo_inflate.c) over whole streams: inflateInit2(wbits) + one
+ * inflate(Z_FINISH) per stream, streams dealt round-robin to `nthreads`
+ * pthreads.  Returns wall seconds; *total_out receives the bytes produced.
+ */
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+#include <zlib.h>
+
+#include "zo_inflate.h"
+
+typedef struct {
+  const uint8_t *const *comp;
+  const size_t *comp_len;
+  uint8_t *const *out;
+  size_t out_cap;
+  int n, nthreads, tid, wbits, use_oracle;
+  uint64_t produced;
+  int bad;
+} task_t;
+
+static void *run(void *arg) {
+  task_t *t = (task_t *)arg;
+  for (int i = t->tid; i < t->n; i += t->nthreads) {
+    if (t->use_oracle) {
+      zo_result r;
+      zo_oneshot(t->comp[i], (uint32_t)t->comp_len[i], t->out[i], (uint32_t)t->out_cap, t->wbits, &r);
+      t->produced += r.total_out;
+      t->bad |= r.ret != 1;
+    } else {
+      z_stream z;
+      memset(&z, 0, sizeof z);
+      inflateInit2(&z, t->wbits);
+      z.next_in = (Bytef *)t->comp[i];
+      z.avail_in = (uInt)t->comp_len[i];
+      z.next_out = t->out[i];
+      z.avail_out = (uInt)t->out_cap;
+      int r = inflate(&z, Z_FINISH);
+      t->produced += z.total_out;
+      t->bad |= r != Z_STREAM_END;
+      inflateEnd(&z);
+    }
+  }
+  return NULL;
+}
+
+double zs_cpu_inflate(const uint8_t *const *comp, const size_t *comp_len, uint8_t *const *out, size_t out_cap, int n,
+                      int nthreads, int wbits, int use_oracle, uint64_t *total_out, int *bad) {
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 512) nthreads = 512;
+  task_t *ts = (task_t *)calloc((size_t)nthreads, sizeof(task_t));
+  pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
+  /* warm any lazily built static tables before timing (single thread) */
+  if (n > 0) {
+    task_t w = {comp, comp_len, out, out_cap, 1, 1, 0, wbits, use_oracle, 0, 0};
+    run(&w);
+  }
+  struct timespec a, b;
+  clock_gettime(CLOCK_MONOTONIC, &a);
+  for (int k = 0; k < nthreads; k++) {
+    ts[k] = (task_t){comp, comp_len, out, out_cap, n, nthreads, k, wbits, use_oracle, 0, 0};
+    pthread_create(&th[k], NULL, run, &ts[k]);
+  }
+  uint64_t tot = 0;
+  int anybad = 0;
+  for (int k = 0; k < nthreads; k++) {
+    pthread_join(th[k], NULL);
+    tot += ts[k].produced;
+    anybad |= ts[k].bad;
+  }
+  clock_gettime(CLOCK_MONOTONIC, &b);
+  free(ts);
+  free(th);
+  *total_out = tot;
+  *bad = anybad;
+  return (double)(b.tv_sec - a.tv_sec) + 1e-9 * (double)(b.tv_nsec - a.tv_nsec);
+}
+
+const char *zs_cpu_zlib_version(void) { return zlibVersion(); }

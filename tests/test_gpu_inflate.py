@@ -1,0 +1,177 @@
+"""GPU parity: libzstreams_mi355x (HIP, gfx950) vs the CPU oracle, through the C-ABI.
+
+Bar: bit-exact output and identical (ret, msg, total_in, total_out, adler) for
+every job -- the fields of one zlib inflate(Z_FINISH) call.
+"""
+import ctypes
+import hashlib
+import json
+import os
+import random
+import zlib
+
+import pytest
+
+import corpus
+import oracle_lib as O
+from golden.make_manifest import fixture, mutate
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+MAN = json.load(open(os.path.join(HERE, "golden", "manifest.json")))
+
+
+@pytest.fixture(scope="module")
+def zs():
+    import zstreams
+    zstreams.lib()
+    return zstreams
+
+
+def run_and_compare(zs, cases):
+    """cases: list of (data, wbits, cap).  One GPU batch; every job vs the oracle."""
+    streams = [c[0] for c in cases]
+    wbs = [c[1] for c in cases]
+    caps = [c[2] for c in cases]
+    got = zs.inflate_batch(streams, wbs, caps)
+    bad = []
+    for i, (c, (out, info)) in enumerate(zip(cases, got)):
+        eo, ei = O.oneshot(c[0], c[1], c[2])
+        if out != eo or info != ei:
+            bad.append((i, c[1], c[2], len(c[0]), info, ei, len(out), len(eo)))
+    assert not bad, f"{len(bad)}/{len(cases)} mismatches, first: {bad[:4]}"
+
+
+def test_fixtures_deflate64(zs):
+    names = sorted(MAN["fixtures"])
+    got = zs.inflate_batch([fixture(n) for n in names], -16, [1 << 22] * len(names))
+    for n, (out, info) in zip(names, got):
+        m = MAN["fixtures"][n]
+        assert info["ret"] == 1 and info["total_in"] == m["total_in"], (n, info)
+        assert hashlib.sha256(out).hexdigest() == m["sha256"], n
+
+
+def test_crafted_and_known_errors(zs):
+    cases = [(bytes.fromhex(c["hex"]), c["wbits"], 1 << 16) for c in MAN["crafted"]]
+    for e in MAN["fixture_errors"]:
+        how = tuple(e["mutate"]) if e["mutate"] else None
+        cases.append((mutate(fixture(e["fixture"]), how), e["wbits"], 1 << 22))
+    run_and_compare(zs, cases)
+    got = zs.inflate_batch([c[0] for c in cases], [c[1] for c in cases], [c[2] for c in cases])
+    for c, (out, info) in zip(MAN["crafted"], got):
+        for k, v in c["expect"].items():
+            assert (hashlib.sha256(out).hexdigest() if k == "sha256" else info[k]) == v, (c["name"], k)
+
+
+def _random_streams(rng, n):
+    cases = []
+    for _ in range(n):
+        kind = rng.random()
+        size = rng.choice([0, 1, 100, 3000, 40000, 200000])
+        if kind < 0.5:
+            raw = corpus.stream(rng.randrange(64), size)
+        elif kind < 0.7:
+            raw = bytes(rng.getrandbits(8) for _ in range(min(size, 5000)))
+        else:
+            raw = bytes([rng.randrange(4)]) * size
+        wb = rng.choice([-15, 15, 31, -9, 9 + 16, 47 - 32 + 32])
+        if wb == 47:
+            wb_enc = rng.choice([15, 31])
+        else:
+            wb_enc = wb
+        c = zlib.compressobj(rng.choice([0, 1, 6, 9]), zlib.DEFLATED, wb_enc, rng.choice([1, 8, 9]),
+                             rng.choice([0, 0, 1, 2, 3, 4]))
+        comp = c.compress(raw) + c.flush()
+        cases.append((comp, wb, len(raw) + 64))
+    return cases
+
+
+def test_valid_streams_all_wrappers(zs):
+    run_and_compare(zs, _random_streams(random.Random(1), 300))
+
+
+def test_corrupt_truncated_and_small_buffers(zs):
+    rng = random.Random(2)
+    base = _random_streams(rng, 400)
+    cases = []
+    for comp, wb, cap in base:
+        b = bytearray(comp)
+        r = rng.random()
+        if r < 0.45 and b:
+            for _ in range(rng.randint(1, 4)):
+                i = rng.randrange(len(b))
+                b[i] ^= 1 << rng.randrange(8)
+        elif r < 0.7 and b:
+            b = b[:rng.randrange(len(b))]
+        elif r < 0.85:
+            cap = rng.randint(0, cap)
+        else:
+            b += bytes(rng.getrandbits(8) for _ in range(rng.randint(1, 10)))
+        cases.append((bytes(b), wb if rng.random() < 0.9 else rng.choice([-15, 15, 31, 47, -16]), cap))
+    run_and_compare(zs, cases)
+
+
+def test_large_streams_roundtrip(zs):
+    raws, comps = corpus.batch(30, 4, 6 << 20, level=6, wbits=-15, nthreads=4)
+    got = zs.inflate_batch([c.tobytes() for c in comps], -15, [6 << 20] * 4)
+    for r, c, (out, info) in zip(raws, comps, got):
+        assert info["ret"] == 1 and info["total_in"] == len(c) and info["total_out"] == len(r)
+        assert out == r.tobytes()
+
+
+def test_gzip_zlib_checks_large(zs):
+    raw = corpus.stream(3, 3 << 20)
+    gz = zlib.compressobj(6, zlib.DEFLATED, 31)
+    g = gz.compress(raw) + gz.flush()
+    z = zlib.compress(raw, 6)
+    got = zs.inflate_batch([g, z], [31, 15], [len(raw)] * 2)
+    assert got[0][0] == raw and got[0][1]["ret"] == 1 and got[0][1]["adler"] == zlib.crc32(raw)
+    assert got[1][0] == raw and got[1][1]["ret"] == 1 and got[1][1]["adler"] == zlib.adler32(raw)
+
+
+def test_stream_api_js_schedule(zs):
+    """DecompressionStreamZlib (handle ABI) output == oracle output under the
+    reference's JS write schedule."""
+    for name in ("100k_lines", "zeros_100k", "10k_lines"):
+        data = fixture(name)
+        for w in (1000, 4096, 65536):
+            got = zs.decompress(data, "deflate64-raw", w)
+            _, eo = O.js_schedule(data, w, -16)
+            assert got == eo, (name, w)
+    raw = corpus.stream(40, 300000)
+    for fmt, wb in (("deflate-raw", -15), ("deflate", 15), ("gzip", 31)):
+        c = zlib.compressobj(6, zlib.DEFLATED, wb)
+        comp = c.compress(raw) + c.flush()
+        assert zs.decompress(comp, fmt, 4096) == raw, fmt
+
+
+def test_zlib_abi_payload_decompress_loop(zs):
+    """test/payload_decompress.c:148-178 loop over the library's zlib ABI."""
+    import libz_ref
+    L = ctypes.CDLL(zs.LIB_PATH)
+    L.inflateInit2_.argtypes = [ctypes.POINTER(libz_ref.ZStream), ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+    L.inflate.argtypes = [ctypes.POINTER(libz_ref.ZStream), ctypes.c_int]
+    L.inflateEnd.argtypes = [ctypes.POINTER(libz_ref.ZStream)]
+    for name in ("10k_lines", "100k_lines"):
+        data = fixture(name)
+        s = libz_ref.ZStream()
+        ib = ctypes.create_string_buffer(data, len(data))
+        win = ctypes.create_string_buffer(65536)
+        assert L.inflateInit2_(ctypes.byref(s), -16, b"1.2.11", ctypes.sizeof(libz_ref.ZStream)) == 0
+        s.next_in = ctypes.cast(ib, ctypes.c_void_p)
+        s.avail_in = len(data)
+        s.next_out = ctypes.cast(win, ctypes.c_void_p)
+        s.avail_out = 65536
+        out = bytearray()
+        ret = 0
+        while ret == 0:
+            before = s.avail_out
+            ret = L.inflate(ctypes.byref(s), 4 if s.avail_in == 0 else 0)
+            out += win.raw[:before - s.avail_out]
+            if ret == 0:
+                assert s.avail_out == 0
+                s.next_out = ctypes.cast(win, ctypes.c_void_p)
+                s.avail_out = 65536
+        assert ret == 1 and L.inflateEnd(ctypes.byref(s)) == 0
+        assert hashlib.sha256(bytes(out)).hexdigest() == MAN["fixtures"][name]["sha256"]

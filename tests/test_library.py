@@ -1,0 +1,63 @@
+"""CPU: the product C-ABI library loads and exports every symbol the public
+header declares (no compute calls: there is no GPU here), and the product never
+links or references the oracle."""
+import ctypes
+import os
+import re
+import subprocess
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "zlib-streams_amd")
+SO = os.path.join(PKG, "libzstreams_mi355x.so")
+HDR = os.path.join(ROOT, "include", "zstreams_mi355x.h")
+
+
+def _ensure_built():
+    if not os.path.exists(SO):
+        subprocess.run(["make", "-s", "-C", os.path.join(PKG, "csrc")], check=True)
+
+
+def declared_functions():
+    txt = open(HDR).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"^\s*[A-Za-z_][\w \*]*?\b(\w+)\s*\(", txt, flags=re.M)) - {"defined"})
+
+
+def test_header_declares_reference_abi():
+    names = set(declared_functions())
+    ref = {f"{p}_{s}" for p in ("inflate", "inflate9") for s in ("new", "init", "init_raw", "process", "end", "last_consumed")}
+    ref.add("inflate_init_gzip")
+    assert ref <= names
+    assert {"zs_inflate_batch", "zs_set_stream", "zs_version", "zs_last_error"} <= names
+
+
+def test_library_exports_every_declared_symbol():
+    _ensure_built()
+    L = ctypes.CDLL(SO)
+    for name in declared_functions() + ["inflateInit2_", "inflateInit_", "inflate", "inflateEnd"]:
+        assert hasattr(L, name), name
+
+
+def test_version_string_without_gpu():
+    _ensure_built()
+    L = ctypes.CDLL(SO)
+    L.zs_version.restype = ctypes.c_char_p
+    assert b"gfx950" in L.zs_version()
+
+
+def test_product_does_not_link_oracle():
+    _ensure_built()
+    needed = subprocess.run(["readelf", "-d", SO], capture_output=True, text=True).stdout
+    assert "zo_inflate" not in needed and "libz.so" not in needed
+    syms = subprocess.run(["nm", "-D", SO], capture_output=True, text=True).stdout
+    assert " zo_" not in syms
+    for dp, _, fs in os.walk(os.path.join(PKG, "csrc")):
+        for f in fs:
+            if f.endswith((".hip", ".cpp", ".h")):
+                assert "oracle" not in open(os.path.join(dp, f)).read(), f
+
+
+def test_gpu_code_object_is_gfx950():
+    _ensure_built()
+    blob = open(SO, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob

@@ -1,0 +1,1045 @@
+// inflate_kernels.hip -- MI355X (gfx950) inflate kernels.
+//
+// Hot path of the reference: the Huffman decode + window copy loop of
+// src/inffast.c:100-287 and the symbol states of src/inflate.c:1037-1193, the
+// block/table states of src/inflate.c:834-1033, and the table builder of
+// src/inftrees.c:33-321 (incl. the deflate64 variant, windowBits == -16).
+//
+// Design (MI355X-first, not a translation):
+//   * one 64-lane wave decodes one stream (or one chunk of one stream); the
+//     decoder state is wave-uniform, so control flow never diverges;
+//   * the compressed bitstream is staged through a 4 KiB LDS ring filled by
+//     coalesced 16 B/lane loads (1 KiB per wave instruction), one piece ahead;
+//   * the history window (32 KiB, or 64 KiB for deflate64) lives in LDS as a
+//     ring; match copies are done by up to 64 lanes at once;
+//   * output leaves the ring in 1 KiB pieces, 16 B per lane (dwordx4 stores);
+//   * Huffman tables are rebuilt per block in LDS, with the canonical sort and
+//     the root-table fill spread over the lanes (ballot ranks), and zlib's
+//     sub-table layout kept exactly so the deflate64 ENOUGH-1 rule
+//     (src/inftrees.c:211-212) rejects the same codes.
+//
+// Result semantics: one job == one inflate(strm, Z_FINISH) call over the whole
+// input (ret, msg, total_in, total_out, adler identical to the reference).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "zs_common.h"
+
+#define WAVE 64
+#define IN_RING_WORDS 1024   // 4 KiB compressed-input ring
+#define PIECE_WORDS 256      // 1 KiB per fill (64 lanes x 16 B)
+#define FLUSH_BYTES 1024     // output flush granule (64 lanes x 16 B)
+#define TABLE_ENTRIES 1448   // ENOUGH (852 + 594), src/inftrees.h:52-55
+
+// ---------------------------------------------------------------------------
+// constant tables (src/inftrees.c:59-87; op = 16+extra deflate, 128+extra d64,
+// 64 invalid, 96 end of block)
+// ---------------------------------------------------------------------------
+__constant__ uint16_t c_lbase[2][31] = {
+    {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258, 0, 0},
+    {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 3, 0, 0}};
+__constant__ uint8_t c_lop[2][31] = {
+    {16, 16, 16, 16, 16, 16, 16, 16, 17, 17, 17, 17, 18, 18, 18, 18, 19, 19, 19, 19, 20, 20, 20, 20, 21, 21, 21, 21, 16, 73, 200},
+    {128, 128, 128, 128, 128, 128, 128, 128, 129, 129, 129, 129, 130, 130, 130, 130, 131, 131, 131, 131, 132, 132, 132, 132,
+     133, 133, 133, 133, 144, 73, 200}};
+__constant__ uint16_t c_dbase[2][32] = {
+    {1, 2, 3, 4, 5, 7, 9, 13, 17, 25, 33, 49, 65, 97, 129, 193, 257, 385, 513, 769, 1025, 1537, 2049, 3073, 4097, 6145, 8193,
+     12289, 16385, 24577, 0, 0},
+    {1, 2, 3, 4, 5, 7, 9, 13, 17, 25, 33, 49, 65, 97, 129, 193, 257, 385, 513, 769, 1025, 1537, 2049, 3073, 4097, 6145, 8193,
+     12289, 16385, 24577, 32769, 49153}};
+__constant__ uint8_t c_dop[2][32] = {
+    {16, 16, 16, 16, 17, 17, 18, 18, 19, 19, 20, 20, 21, 21, 22, 22, 23, 23, 24, 24, 25, 25, 26, 26, 27, 27, 28, 28, 29, 29, 64, 64},
+    {128, 128, 128, 128, 129, 129, 130, 130, 131, 131, 132, 132, 133, 133, 134, 134, 135, 135, 136, 136, 137, 137, 138, 138,
+     139, 139, 140, 140, 141, 141, 142, 142}};
+__constant__ uint8_t c_clorder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+enum { T_CODES = 0, T_LENS = 1, T_DISTS = 2 };
+
+__device__ __forceinline__ uint32_t mk_entry(uint32_t op, uint32_t bits, uint32_t val) {
+  return op | (bits << 8) | (val << 16);
+}
+__device__ __forceinline__ uint32_t e_op(uint32_t e) { return e & 0xffu; }
+__device__ __forceinline__ uint32_t e_bits(uint32_t e) { return (e >> 8) & 0xffu; }
+__device__ __forceinline__ uint32_t e_val(uint32_t e) { return e >> 16; }
+
+__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & (WAVE - 1); }
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// ---------------------------------------------------------------------------
+// Table builder: canonical Huffman -> zlib-layout 2-level table in LDS.
+// Restates src/inftrees.c:33-321; the sort and the root fill run across lanes,
+// the long-code sub-tables keep zlib's allocation order and sizing.
+// Returns 0 ok, -1 bad code set, 1 table space exceeded.  `*root` is in/out.
+// ---------------------------------------------------------------------------
+__device__ int build_table(int type, const uint16_t *lens, uint32_t n, uint32_t *table, uint32_t *root_io,
+                           uint16_t *sorted, uint32_t *scratch16, int d64) {
+  const uint32_t lane = lane_id();
+  const uint64_t lt_mask = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
+  uint32_t cnt[16];
+#pragma unroll
+  for (int L = 0; L < 16; L++) cnt[L] = 0;
+  for (uint32_t g = 0; g < n; g += WAVE) {
+    uint32_t s = g + lane;
+    uint32_t L = (s < n) ? lens[s] : 16u;
+#pragma unroll
+    for (int x = 0; x < 16; x++) cnt[x] += __popcll(__ballot(L == (uint32_t)x));
+  }
+  uint32_t maxlen = 0, minlen = 0;
+#pragma unroll
+  for (int x = 15; x >= 1; x--)
+    if (maxlen == 0 && cnt[x]) maxlen = x;
+  uint32_t root = *root_io;
+  if (root > maxlen) root = maxlen;
+  if (maxlen == 0) {
+    if (d64) return -1;  // src/inftrees.c:131-132
+    if (lane < 2) table[lane] = mk_entry(64, 1, 0);
+    __builtin_amdgcn_wave_barrier();
+    *root_io = 1;
+    return 0;
+  }
+#pragma unroll
+  for (int x = 1; x <= 15; x++)
+    if (minlen == 0 && cnt[x]) minlen = x;
+  if (root < minlen) root = minlen;
+  int room = 1;
+  bool over = false;
+#pragma unroll
+  for (int x = 1; x <= 15; x++) {
+    room = (room << 1) - (int)cnt[x];
+    over |= room < 0;
+  }
+  if (over) return -1;
+  if (room > 0 && (type == T_CODES || maxlen != 1)) return -1;
+
+  // canonical first codes and sorted offsets
+  uint32_t start[16], first[16];
+  start[0] = 0;
+  start[1] = 0;
+  first[0] = 0;
+  first[1] = 0;
+#pragma unroll
+  for (int x = 1; x < 15; x++) {
+    start[x + 1] = start[x] + cnt[x];
+    first[x + 1] = (first[x] + cnt[x]) << 1;
+  }
+  // publish counts and starts for the serial sub-table pass
+  if (lane < 16) {
+    uint32_t c = 0, st = 0;
+#pragma unroll
+    for (int x = 0; x < 16; x++) {
+      if ((uint32_t)x == lane) { c = cnt[x]; st = start[x]; }
+    }
+    scratch16[lane] = c;
+    scratch16[16 + lane] = st;
+  }
+  // stable sort of symbols by length (ballot rank within each length)
+  {
+    uint32_t base[16];
+#pragma unroll
+    for (int x = 0; x < 16; x++) base[x] = start[x];
+    for (uint32_t g = 0; g < n; g += WAVE) {
+      uint32_t s = g + lane;
+      uint32_t L = (s < n) ? lens[s] : 0u;
+#pragma unroll
+      for (int x = 1; x <= 15; x++) {
+        uint64_t m = __ballot(L == (uint32_t)x);
+        if (L == (uint32_t)x) sorted[base[x] + __popcll(m & lt_mask)] = (uint16_t)s;
+        base[x] += __popcll(m);
+      }
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+
+  const uint32_t first_coded = (type == T_CODES) ? 20u : (type == T_LENS ? 257u : 0u);
+  const uint32_t lim = (type == T_LENS) ? (d64 ? 851u : 852u) : (type == T_DISTS ? (d64 ? 593u : 592u) : 0xffffffffu);
+  uint32_t used = 1u << root;
+  if (used > lim) return 1;
+  const uint32_t ncodes = start[15] + cnt[15];
+  // number of codes of length <= root
+  uint32_t nshort = 0;
+#pragma unroll
+  for (int x = 1; x <= 15; x++)
+    if ((uint32_t)x <= root) nshort += cnt[x];
+
+  auto sym_entry = [&](uint32_t s, uint32_t bits) -> uint32_t {
+    if (s + 1u < first_coded) return mk_entry(0, bits, s);
+    if (s >= first_coded) {
+      uint32_t k = s - first_coded;
+      if (type == T_LENS) return mk_entry(c_lop[d64][k], bits, c_lbase[d64][k]);
+      return mk_entry(c_dop[d64][k], bits, c_dbase[d64][k]);
+    }
+    return mk_entry(96, bits, 0);
+  };
+
+  // root fill for short codes: lane-parallel over codes, replicated entries
+  for (uint32_t g = 0; g < nshort; g += WAVE) {
+    uint32_t i = g + lane;
+    if (i < nshort) {
+      uint32_t s = sorted[i];
+      uint32_t L = lens[s];
+      uint32_t st = scratch16[16 + L];
+      uint32_t code = 0;
+#pragma unroll
+      for (int x = 1; x <= 15; x++)
+        if ((uint32_t)x == L) code = first[x];
+      code += i - st;
+      uint32_t rev = __builtin_bitreverse32(code) >> (32 - L);
+      uint32_t e = sym_entry(s, L);
+      uint32_t reps = 1u << (root - L);
+      for (uint32_t j = 0; j < reps; j++) table[rev + (j << L)] = e;
+    }
+  }
+  // incomplete single 1-bit code: slot 1 is an invalid marker
+  if (room > 0 && lane == 0) table[1] = mk_entry(64, 1, 0);
+
+  // long codes: serial over codes (uniform), lane-parallel replication
+  uint32_t next = 0, cur_size = 1u << root, open_low = 0xffffffffu, curr = root;
+  const uint32_t rmask = (1u << root) - 1;
+  for (uint32_t i = nshort; i < ncodes; i++) {
+    uint32_t s = uni(sorted[i]);
+    uint32_t L = uni(lens[s]);
+    uint32_t st = uni(scratch16[16 + L]);
+    uint32_t code = 0;
+#pragma unroll
+    for (int x = 1; x <= 15; x++)
+      if ((uint32_t)x == L) code = first[x];
+    code += i - st;
+    uint32_t rev = __builtin_bitreverse32(code) >> (32 - L);
+    uint32_t low = rev & rmask;
+    if (low != open_low) {
+      next += cur_size;
+      curr = L - root;
+      int left = 1 << curr;
+      while (curr + root < maxlen) {
+        uint32_t x = curr + root;
+        uint32_t remain = uni(scratch16[x]) - ((x == L) ? (i - st) : 0u);
+        left -= (int)remain;
+        if (left <= 0) break;
+        curr++;
+        left <<= 1;
+      }
+      cur_size = 1u << curr;
+      used += cur_size;
+      if (used > lim) return 1;
+      open_low = low;
+      if (lane == 0) table[low] = mk_entry(curr, root, next);
+    }
+    uint32_t e = sym_entry(s, L - root);
+    uint32_t step = 1u << (L - root);
+    uint32_t reps = cur_size >> (L - root);
+    uint32_t idx0 = next + (rev >> root);
+    for (uint32_t j = lane; j < reps; j += WAVE) table[idx0 + j * step] = e;
+  }
+  __builtin_amdgcn_wave_barrier();
+  *root_io = root;
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Header stage: zlib / gzip wrapper parse (src/inflate.c:629-833), one thread
+// per job.  Byte-exact total_in on header errors and truncation.
+// ---------------------------------------------------------------------------
+__device__ uint32_t crc32_bytes(uint32_t crc, const uint8_t *p, uint64_t n) {
+  crc = ~crc;
+  for (uint64_t i = 0; i < n; i++) {
+    crc ^= p[i];
+#pragma unroll
+    for (int k = 0; k < 8; k++) crc = (crc >> 1) ^ (0xEDB88320u & (0u - (crc & 1u)));
+  }
+  return ~crc;
+}
+
+__global__ void zs_header_kernel(const ZsJobDev *__restrict__ jobs, ZsHeadDev *__restrict__ heads, uint32_t njobs) {
+  uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= njobs) return;
+  ZsJobDev jb = jobs[j];
+  ZsHeadDev h;
+  h.code = ZD_END;  // "continue to deflate data"
+  h.msg = ZM_NONE;
+  h.is_gzip = -1;
+  h.ret = 0;
+  h.start_byte = 0;
+  h.total_in = 0;
+  h.adler = 0;
+  h.pad2 = 0;
+  const uint8_t *in = jb.in;
+  const uint64_t n = jb.in_len;
+  if (jb.wrap == ZW_RAW) {
+    heads[j] = h;
+    return;
+  }
+  uint32_t adler_reset = (uint32_t)(jb.wrap & 1);  // inflateResetKeep: strm->adler = wrap & 1
+  h.adler = adler_reset;
+  auto trunc = [&]() {
+    h.code = ZD_SKIP;
+    h.msg = ZM_NONE;
+    h.total_in = n;
+    h.ret = ZS_BUF_ERROR;
+  };
+  auto fail = [&](int msg, uint64_t consumed) {
+    h.code = ZD_SKIP;
+    h.msg = msg;
+    h.total_in = consumed;
+    h.ret = ZS_DATA_ERROR;
+  };
+  if (n < 2) {
+    trunc();
+    heads[j] = h;
+    return;
+  }
+  uint32_t b0 = in[0], b1 = in[1];
+  if ((jb.wrap & 2) && b0 == 0x1f && b1 == 0x8b) {
+    uint64_t p = 2;
+    uint32_t crc = crc32_bytes(0, in, 2);
+    if (n < p + 2) { trunc(); heads[j] = h; return; }
+    uint32_t flags = in[p] | (in[p + 1] << 8);
+    if ((flags & 0xff) != 8) { fail(ZM_METHOD, p + 2); heads[j] = h; return; }
+    if (flags & 0xe000) { fail(ZM_FLAGS, p + 2); heads[j] = h; return; }
+    const bool hc = (flags & 0x0200) != 0;
+    if (hc) crc = crc32_bytes(crc, in + p, 2);
+    p += 2;
+    if (n < p + 4) { trunc(); heads[j] = h; return; }  // MTIME
+    if (hc) crc = crc32_bytes(crc, in + p, 4);
+    p += 4;
+    if (n < p + 2) { trunc(); heads[j] = h; return; }  // XFL, OS
+    if (hc) crc = crc32_bytes(crc, in + p, 2);
+    p += 2;
+    if (flags & 0x0400) {
+      if (n < p + 2) { trunc(); heads[j] = h; return; }
+      uint32_t xlen = in[p] | (in[p + 1] << 8);
+      if (hc) crc = crc32_bytes(crc, in + p, 2);
+      p += 2;
+      if (n < p + xlen) { trunc(); heads[j] = h; return; }
+      if (hc) crc = crc32_bytes(crc, in + p, xlen);
+      p += xlen;
+    }
+    for (int f = 0; f < 2; f++) {
+      if (flags & (f == 0 ? 0x0800 : 0x1000)) {
+        uint64_t q = p;
+        while (q < n && in[q] != 0) q++;
+        if (q >= n) { trunc(); heads[j] = h; return; }
+        if (hc) crc = crc32_bytes(crc, in + p, q + 1 - p);
+        p = q + 1;
+      }
+    }
+    if (hc) {
+      if (n < p + 2) { trunc(); heads[j] = h; return; }
+      uint32_t want = in[p] | (in[p + 1] << 8);
+      if (want != (crc & 0xffff)) { fail(ZM_HCRC, p + 2); heads[j] = h; return; }
+      p += 2;
+    }
+    h.adler = 0;
+    h.is_gzip = 1;
+    h.start_byte = p;
+    heads[j] = h;
+    return;
+  }
+  if (!(jb.wrap & 1) || (((b0 << 8) + b1) % 31) != 0) { fail(ZM_HEADER_CHECK, 2); heads[j] = h; return; }
+  if ((b0 & 15) != 8) { fail(ZM_METHOD, 2); heads[j] = h; return; }
+  uint32_t wlen = (b0 >> 4) + 8;
+  uint32_t wb = jb.wbits == 0 ? wlen : (uint32_t)jb.wbits;
+  if (wlen > 15 || wlen > wb) { fail(ZM_WINDOW, 2); heads[j] = h; return; }
+  h.adler = 1;
+  if (b1 & 0x20) {  // FDICT: DICTID then Z_NEED_DICT (src/inflate.c:817-828)
+    if (n < 6) { trunc(); heads[j] = h; return; }
+    h.code = ZD_NEED_DICT;
+    h.adler = ((uint32_t)in[2] << 24) | ((uint32_t)in[3] << 16) | ((uint32_t)in[4] << 8) | in[5];
+    h.total_in = 0;  // Z_NEED_DICT returns before inf_leave: totals untouched
+    heads[j] = h;
+    return;
+  }
+  h.is_gzip = 0;
+  h.start_byte = 2;
+  heads[j] = h;
+}
+
+// ---------------------------------------------------------------------------
+// The wave-uniform deflate decoder.
+// ---------------------------------------------------------------------------
+template <bool D64>
+struct Inflater {
+  static constexpr uint32_t RING = D64 ? 65536u : 32768u;
+  static constexpr uint32_t RMASK = RING - 1;
+
+  uint8_t *ring;       // LDS history ring
+  uint32_t *inring;    // LDS compressed-input ring
+  uint32_t *tab;       // LDS dynamic tables
+  uint32_t *ftab;      // LDS fixed tables (built on first use)
+  uint16_t *lens;      // LDS code lengths
+  uint16_t *sorted;    // LDS sort scratch
+  uint32_t *scratch16; // LDS 32 words
+
+  // input
+  const uint8_t *abase;  // 16 B aligned base of the job input
+  uint32_t limit_bits;   // (misalign + in_len) * 8
+  uint32_t end_byte;     // misalign + in_len
+  uint32_t wi;           // next 32-bit word to pull into hold
+  uint32_t committed;    // pieces [committed-4, committed) are in the LDS ring
+  uint4 pending;         // piece `committed`, in flight in registers
+  uint64_t hold;
+  uint32_t nbits;
+
+  // output
+  uint8_t *out;
+  uint32_t cap, pos, flushed;
+  uint32_t whave;  // bytes of history before output position 0
+  bool fixed_ready;
+
+  __device__ uint4 load_piece(uint32_t k) {
+    uint32_t lane = lane_id();
+    uint32_t b = k * (PIECE_WORDS * 4) + lane * 16;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (b < end_byte) {
+      v = *reinterpret_cast<const uint4 *>(abase + b);
+      if (b + 16 > end_byte) {  // zero the bytes past the end of the input
+        uint32_t keep = end_byte - b;
+        uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          int kb = (int)keep - q * 4;
+          uint32_t m = kb >= 4 ? 0xffffffffu : (kb <= 0 ? 0u : ((1u << (8 * kb)) - 1u));
+          w[q] &= m;
+        }
+        v = make_uint4(w[0], w[1], w[2], w[3]);
+      }
+    }
+    return v;
+  }
+  __device__ void store_piece(uint32_t k, uint4 v) {
+    uint32_t lane = lane_id();
+    *reinterpret_cast<uint4 *>(&inring[(k & 3) * PIECE_WORDS + lane * 4]) = v;
+  }
+  // position the reader at absolute bit `bit` (relative to abase)
+  __device__ void seek(uint32_t bit) {
+    uint32_t w = bit >> 5;
+    uint32_t k0 = w / PIECE_WORDS;
+    __builtin_amdgcn_wave_barrier();
+    store_piece(k0, load_piece(k0));
+    store_piece(k0 + 1, load_piece(k0 + 1));
+    store_piece(k0 + 2, load_piece(k0 + 2));
+    committed = k0 + 3;
+    pending = load_piece(committed);
+    __builtin_amdgcn_wave_barrier();
+    wi = w;
+    hold = 0;
+    nbits = 0;
+    refill();
+    uint32_t skip = bit & 31;
+    hold >>= skip;
+    nbits -= skip;
+  }
+  __device__ __forceinline__ void refill() {
+    if (nbits < 32) {
+      uint32_t w = inring[wi & (IN_RING_WORDS - 1)];
+      hold |= (uint64_t)w << nbits;
+      nbits += 32;
+      wi++;
+      if (wi + 16 >= committed * PIECE_WORDS) {
+        __builtin_amdgcn_wave_barrier();
+        store_piece(committed, pending);
+        committed++;
+        pending = load_piece(committed);
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+  }
+  __device__ __forceinline__ uint32_t bitpos() const { return wi * 32u - nbits; }
+  __device__ __forceinline__ void drop(uint32_t n) {
+    hold >>= n;
+    nbits -= n;
+  }
+  __device__ __forceinline__ bool short_of(uint32_t need) const { return bitpos() + need > limit_bits; }
+
+  __device__ void flush_piece() {
+    uint32_t lane = lane_id();
+    uint4 v = *reinterpret_cast<const uint4 *>(&ring[(flushed + lane * 16) & RMASK]);
+    *reinterpret_cast<uint4 *>(out + flushed + lane * 16) = v;
+    flushed += FLUSH_BYTES;
+  }
+  __device__ __forceinline__ void maybe_flush() {
+    while (pos - flushed >= FLUSH_BYTES) flush_piece();
+  }
+  __device__ void flush_tail() {
+    uint32_t lane = lane_id();
+    uint32_t rem = pos - flushed;
+    for (uint32_t k = lane; k < rem; k += WAVE) out[flushed + k] = ring[(flushed + k) & RMASK];
+    flushed = pos;
+  }
+
+  __device__ __forceinline__ void put_literal(uint32_t v) {
+    ring[pos & RMASK] = (uint8_t)v;
+    pos++;
+    if (pos - flushed >= FLUSH_BYTES) flush_piece();
+  }
+
+  // copy n bytes (n <= len, room already checked) from `dist` back
+  __device__ void copy_match(uint32_t n, uint32_t dist) {
+    uint32_t lane = lane_id();
+    if (dist >= WAVE) {
+      // every batch reads bytes at least 64 back: all already final
+      while (n) {
+        uint32_t cnt = min(n, (uint32_t)WAVE);
+        uint8_t v = 0;
+        if (lane < cnt) v = ring[(pos + lane - dist) & RMASK];
+        __builtin_amdgcn_wave_barrier();
+        if (lane < cnt) ring[(pos + lane) & RMASK] = v;
+        __builtin_amdgcn_wave_barrier();
+        pos += cnt;
+        n -= cnt;
+        maybe_flush();
+      }
+    } else {
+      // period P = dist * floor(64 / dist): batches of P lanes; the first batch
+      // reads the source period, later ones read P bytes back.
+      uint32_t per = (uint32_t)(64u / dist) * dist;
+      uint32_t q = (uint32_t)((float)lane * __builtin_amdgcn_rcpf((float)dist) + 1e-3f);
+      if (q * dist > lane) q--;
+      if ((q + 1) * dist <= lane) q++;
+      uint32_t lm = lane - q * dist;  // lane % dist
+      bool firstb = true;
+      while (n) {
+        uint32_t cnt = min(n, per);
+        uint8_t v = 0;
+        if (lane < cnt) v = firstb ? ring[(pos - dist + lm) & RMASK] : ring[(pos + lane - per) & RMASK];
+        __builtin_amdgcn_wave_barrier();
+        if (lane < cnt) ring[(pos + lane) & RMASK] = v;
+        __builtin_amdgcn_wave_barrier();
+        pos += cnt;
+        n -= cnt;
+        firstb = false;
+        maybe_flush();
+      }
+    }
+  }
+
+  // stored block copy of n bytes from input byte `src` (relative to abase)
+  __device__ void copy_stored(uint32_t src, uint32_t n) {
+    uint32_t lane = lane_id();
+    for (uint32_t b = 0; b < n; b += WAVE) {
+      uint32_t k = b + lane;
+      if (k < n) ring[(pos + lane) & RMASK] = abase[src + k];
+      __builtin_amdgcn_wave_barrier();
+      uint32_t adv = min(n - b, (uint32_t)WAVE);
+      pos += adv;
+      maybe_flush();
+    }
+  }
+
+  __device__ void build_fixed() {
+    // src/inflate.c:260-298 lengths: 0-143 -> 8, 144-255 -> 9, 256-279 -> 7, 280-287 -> 8; 32 distance codes of 5
+    uint32_t lane = lane_id();
+    for (uint32_t s = lane; s < 288; s += WAVE) lens[s] = s < 144 ? 8 : (s < 256 ? 9 : (s < 280 ? 7 : 8));
+    __builtin_amdgcn_wave_barrier();
+    uint32_t r = 9;
+    build_table(T_LENS, lens, 288, ftab, &r, sorted, scratch16, D64);
+    for (uint32_t s = lane; s < 32; s += WAVE) lens[s] = 5;
+    __builtin_amdgcn_wave_barrier();
+    r = 5;
+    build_table(T_DISTS, lens, 32, ftab + 512, &r, sorted, scratch16, D64);
+    fixed_ready = true;
+  }
+
+  // Decode from the current bit position to the end of the final block.
+  // Returns a ZsDecCode; *msg and *ebits describe errors / stopping point.
+  __device__ int run(int *msg, uint32_t *ebits) {
+    uint32_t lane = lane_id();
+    bool last = false;
+    for (;;) {
+      if (last) {
+        *ebits = bitpos();
+        return ZD_END;
+      }
+      refill();
+      if (short_of(3)) return ZD_TRUNC;
+      last = (hold & 1) != 0;
+      uint32_t type = (uint32_t)(hold >> 1) & 3u;
+      drop(3);
+      const uint32_t *lt;
+      const uint32_t *dt;
+      uint32_t lbits, dbits;
+      if (type == 0) {
+        uint32_t pad = bitpos() & 7u;
+        if (pad) drop(8 - pad);
+        refill();
+        if (short_of(32)) return ZD_TRUNC;
+        uint32_t v = (uint32_t)hold;
+        if ((v & 0xffffu) != ((v >> 16) ^ 0xffffu)) {
+          *msg = ZM_STORED_LEN;
+          *ebits = bitpos() + 32;
+          return ZD_ERROR;
+        }
+        drop(32);
+        uint32_t slen = v & 0xffffu;
+        uint32_t src = bitpos() >> 3;
+        uint32_t avail = end_byte - src;
+        uint32_t room = cap - pos;
+        uint32_t m = min(slen, min(avail, room));
+        copy_stored(src, m);
+        if (m < slen) {
+          if (m == avail) return ZD_TRUNC;  // input exhausted first (or at the same time)
+          *ebits = (src + m) * 8;
+          return ZD_FULL;
+        }
+        seek((src + slen) * 8);
+        continue;
+      } else if (type == 1) {
+        if (!fixed_ready) build_fixed();
+        lt = ftab;
+        dt = ftab + 512;
+        lbits = 9;
+        dbits = 5;
+      } else if (type == 2) {
+        // ---- dynamic header (src/inflate.c:905-1033) ----
+        refill();
+        if (short_of(14)) return ZD_TRUNC;
+        uint32_t nlen = (uint32_t)(hold & 31) + 257;
+        uint32_t ndist = (uint32_t)((hold >> 5) & 31) + 1;
+        uint32_t ncode = (uint32_t)((hold >> 10) & 15) + 4;
+        drop(14);
+        if (nlen > 286 || (!D64 && ndist > 30)) {
+          *msg = ZM_TOO_MANY;
+          *ebits = bitpos();
+          return ZD_ERROR;
+        }
+        // code-length code lengths (src/inflate.c:923-934)
+        for (uint32_t i = 0; i < ncode; i++) {
+          refill();
+          if (short_of(3)) return ZD_TRUNC;
+          if (lane == 0) lens[c_clorder[i]] = (uint16_t)(hold & 7u);
+          drop(3);
+        }
+        if (lane >= ncode && lane < 19) lens[c_clorder[lane]] = 0;
+        __builtin_amdgcn_wave_barrier();
+        uint32_t cbits = 7;
+        if (build_table(T_CODES, lens, 19, tab, &cbits, sorted, scratch16, D64)) {
+          *msg = ZM_CODE_LENGTHS;
+          *ebits = bitpos();
+          return ZD_ERROR;
+        }
+        uint32_t total = nlen + ndist;
+        uint32_t have = 0;
+        uint32_t cmask = (1u << cbits) - 1;
+        while (have < total) {
+          refill();
+          uint32_t e = tab[(uint32_t)hold & cmask];
+          uint32_t eb = e_bits(e), ev = e_val(e);
+          if (short_of(eb)) return ZD_TRUNC;
+          if (ev < 16) {
+            drop(eb);
+            if (lane == 0) lens[have] = (uint16_t)ev;
+            have++;
+            continue;
+          }
+          uint32_t xb = ev == 16 ? 2 : (ev == 17 ? 3 : 7);
+          if (short_of(eb + xb)) return ZD_TRUNC;
+          drop(eb);
+          if (ev == 16 && have == 0) {
+            *msg = ZM_REPEAT;
+            *ebits = bitpos() + 2;
+            return ZD_ERROR;
+          }
+          uint32_t rep = (ev == 16 ? 3 : (ev == 17 ? 3 : 11)) + ((uint32_t)hold & ((1u << xb) - 1));
+          drop(xb);
+          if (have + rep > total) {
+            *msg = ZM_REPEAT;
+            *ebits = bitpos();
+            return ZD_ERROR;
+          }
+          __builtin_amdgcn_wave_barrier();
+          uint32_t fillv = ev == 16 ? uni(lens[have - 1]) : 0u;
+          if (lane < rep) lens[have + lane] = (uint16_t)fillv;  // rep <= 138 > 64: loop
+          if (lane + 64 < rep) lens[have + lane + 64] = (uint16_t)fillv;
+          if (lane + 128 < rep) lens[have + lane + 128] = (uint16_t)fillv;
+          __builtin_amdgcn_wave_barrier();
+          have += rep;
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (uni(lens[256]) == 0) {
+          *msg = ZM_MISSING_EOB;
+          *ebits = bitpos();
+          return ZD_ERROR;
+        }
+        lbits = 9;
+        if (build_table(T_LENS, lens, nlen, tab, &lbits, sorted, scratch16, D64)) {
+          *msg = ZM_LITLEN_SET;
+          *ebits = bitpos();
+          return ZD_ERROR;
+        }
+        // distance table goes right after the literal/length table; its size
+        // is bounded by 852 entries (ENOUGH_LENS)
+        dbits = 6;
+        if (build_table(T_DISTS, lens + nlen, ndist, tab + 852, &dbits, sorted, scratch16, D64)) {
+          *msg = ZM_DIST_SET;
+          *ebits = bitpos();
+          return ZD_ERROR;
+        }
+        lt = tab;
+        dt = tab + 852;
+      } else {
+        *msg = ZM_BLOCK_TYPE;
+        *ebits = bitpos();
+        return ZD_ERROR;
+      }
+
+      // ---- symbol loop (src/inffast.c:100-287 / src/inflate.c:1037-1193) ----
+      const uint32_t lmask = (1u << lbits) - 1, dmask = (1u << dbits) - 1;
+      for (;;) {
+        refill();
+        uint32_t e = lt[(uint32_t)hold & lmask];
+        uint32_t op = e_op(e);
+        uint32_t used = e_bits(e);
+        if (op != 0 && (op & 0xf0u) == 0) {  // second-level table
+          uint32_t e2 = lt[e_val(e) + (((uint32_t)(hold >> used)) & ((1u << op) - 1))];
+          used += e_bits(e2);
+          e = e2;
+          op = e_op(e);
+        }
+        if (short_of(used)) return ZD_TRUNC;
+        drop(used);
+        if (op == 0) {
+          if (pos == cap) {
+            *ebits = bitpos();
+            return ZD_FULL;
+          }
+          put_literal(e_val(e));
+          continue;
+        }
+        if (op & 32) break;  // end of block
+        if (op & 64) {
+          *msg = ZM_LITLEN_CODE;
+          *ebits = bitpos();
+          return ZD_ERROR;
+        }
+        uint32_t len = e_val(e);
+        uint32_t xb = op & (D64 ? 31u : 15u);
+        if (xb) {
+          if (short_of(xb)) return ZD_TRUNC;
+          len += (uint32_t)hold & ((1u << xb) - 1);
+          drop(xb);
+        }
+        refill();
+        uint32_t d = dt[(uint32_t)hold & dmask];
+        uint32_t dop = e_op(d);
+        uint32_t dused = e_bits(d);
+        if ((dop & 0xf0u) == 0) {
+          uint32_t d2 = dt[e_val(d) + (((uint32_t)(hold >> dused)) & ((1u << dop) - 1))];
+          dused += e_bits(d2);
+          d = d2;
+          dop = e_op(d);
+        }
+        if (short_of(dused)) return ZD_TRUNC;
+        drop(dused);
+        if (dop & 64) {
+          *msg = ZM_DIST_CODE;
+          *ebits = bitpos();
+          return ZD_ERROR;
+        }
+        uint32_t dist = e_val(d);
+        uint32_t dx = dop & 15u;
+        if (dx) {
+          if (short_of(dx)) return ZD_TRUNC;
+          dist += (uint32_t)hold & ((1u << dx) - 1);
+          drop(dx);
+        }
+        if (pos == cap) {
+          *ebits = bitpos();
+          return ZD_FULL;
+        }
+        if (dist > pos + whave) {
+          *msg = ZM_TOO_FAR;
+          *ebits = bitpos();
+          return ZD_ERROR;
+        }
+        uint32_t n = min(len, cap - pos);
+        copy_match(n, dist);
+        if (n < len) {
+          *ebits = bitpos();
+          return ZD_FULL;
+        }
+      }
+    }
+  }
+};
+
+template <bool D64>
+__global__ void __launch_bounds__(64) zs_decode_kernel(const ZsJobDev *__restrict__ jobs, const ZsHeadDev *__restrict__ heads,
+                                                        const uint32_t *__restrict__ job_ids, ZsDecDev *__restrict__ decs) {
+  constexpr uint32_t RING = D64 ? 65536u : 32768u;
+  __shared__ __attribute__((aligned(16))) uint8_t s_ring[RING];
+  __shared__ __attribute__((aligned(16))) uint32_t s_in[IN_RING_WORDS];
+  __shared__ uint32_t s_tab[TABLE_ENTRIES];
+  __shared__ uint32_t s_ftab[544];
+  __shared__ uint16_t s_lens[320];
+  __shared__ uint16_t s_sorted[320];
+  __shared__ uint32_t s_scr[32];
+
+  const uint32_t j = job_ids[blockIdx.x];
+  const ZsJobDev jb = jobs[j];
+  const ZsHeadDev hd = heads[j];
+  ZsDecDev res;
+  res.code = ZD_SKIP;
+  res.msg = ZM_NONE;
+  res.end_bits = 0;
+  res.total_out = 0;
+  if (hd.code != ZD_END) {
+    if (threadIdx.x == 0) decs[j] = res;
+    return;
+  }
+  Inflater<D64> f;
+  f.ring = s_ring;
+  f.inring = s_in;
+  f.tab = s_tab;
+  f.ftab = s_ftab;
+  f.lens = s_lens;
+  f.sorted = s_sorted;
+  f.scratch16 = s_scr;
+  const uintptr_t ip = reinterpret_cast<uintptr_t>(jb.in);
+  const uint32_t mis = (uint32_t)(ip & 15u);
+  f.abase = reinterpret_cast<const uint8_t *>(ip - mis);
+  f.end_byte = mis + (uint32_t)jb.in_len;
+  f.limit_bits = f.end_byte * 8u;
+  f.out = jb.out;
+  f.cap = (uint32_t)jb.out_cap;
+  f.pos = 0;
+  f.flushed = 0;
+  f.whave = 0;
+  f.fixed_ready = false;
+  f.seek((mis + (uint32_t)hd.start_byte) * 8u);
+  int msg = ZM_NONE;
+  uint32_t ebits = 0;
+  int code = f.run(&msg, &ebits);
+  f.flush_tail();
+  res.code = code;
+  res.msg = msg;
+  res.end_bits = (code == ZD_TRUNC) ? (uint64_t)jb.in_len * 8u : (uint64_t)(ebits - mis * 8u);
+  res.total_out = f.pos;
+  if (threadIdx.x == 0) decs[j] = res;
+}
+
+template __global__ void zs_decode_kernel<false>(const ZsJobDev *, const ZsHeadDev *, const uint32_t *, ZsDecDev *);
+template __global__ void zs_decode_kernel<true>(const ZsJobDev *, const ZsHeadDev *, const uint32_t *, ZsDecDev *);
+
+// ---------------------------------------------------------------------------
+// Checks: CRC-32 (gzip) / Adler-32 (zlib) over each job's output, segment
+// parallel with an exact combine (UPDATE_CHECK, src/inflate.c:425-429).
+// ---------------------------------------------------------------------------
+__device__ uint32_t gf2_mulmod(uint32_t a, uint32_t b) {
+  // multiply a(x) * b(x) mod P(x), reflected bit order (bit 31 = x^0)
+  uint32_t m = 1u << 31, p = 0;
+  for (;;) {
+    if (a & m) {
+      p ^= b;
+      if ((a & (m - 1)) == 0) break;
+    }
+    m >>= 1;
+    b = (b & 1) ? (b >> 1) ^ 0xEDB88320u : b >> 1;
+  }
+  return p;
+}
+// x^(8n) mod P
+__device__ uint32_t x8n_mod(uint64_t n) {
+  uint32_t p = 1u << 31;  // x^0
+  uint32_t sq = 1u << 23; // x^8
+  while (n) {
+    if (n & 1) p = gf2_mulmod(sq, p);
+    sq = gf2_mulmod(sq, sq);
+    n >>= 1;
+  }
+  return p;
+}
+
+#define CHECK_THREADS 256
+__global__ void __launch_bounds__(CHECK_THREADS) zs_check_kernel(const ZsJobDev *__restrict__ jobs, const ZsHeadDev *__restrict__ heads,
+                                                                 const ZsDecDev *__restrict__ decs, uint32_t *__restrict__ checks) {
+  __shared__ uint32_t s_tab[256];
+  __shared__ uint32_t s_a[CHECK_THREADS];
+  __shared__ uint32_t s_b[CHECK_THREADS];
+  __shared__ uint64_t s_len[CHECK_THREADS];
+  const uint32_t j = blockIdx.x;
+  const uint32_t t = threadIdx.x;
+  const ZsHeadDev hd = heads[j];
+  const ZsDecDev dc = decs[j];
+  if (hd.code != ZD_END || hd.is_gzip < 0 || dc.code == ZD_SKIP) {
+    if (t == 0) checks[j] = 0;
+    return;
+  }
+  const uint8_t *p = jobs[j].out;
+  const uint64_t n = dc.total_out;
+  const uint64_t seg = ((n + CHECK_THREADS - 1) / CHECK_THREADS + 15) & ~15ull;
+  const uint64_t lo = min(n, seg * t), hi = min(n, seg * (t + 1));
+  if (hd.is_gzip == 1) {
+    {
+      uint32_t c = t;
+      for (int k = 0; k < 8; k++) c = (c & 1) ? (0xEDB88320u ^ (c >> 1)) : (c >> 1);
+      s_tab[t] = c;
+    }
+    __syncthreads();
+    uint32_t crc = 0xffffffffu;
+    for (uint64_t i = lo; i < hi; i++) crc = s_tab[(crc ^ p[i]) & 0xff] ^ (crc >> 8);
+    s_a[t] = (hi > lo) ? ~crc : 0u;
+    s_len[t] = hi - lo;
+    __syncthreads();
+    for (uint32_t w = 1; w < CHECK_THREADS; w <<= 1) {
+      uint32_t nv = 0;
+      uint64_t nl = 0;
+      bool act = (t % (2 * w)) == 0 && t + w < CHECK_THREADS;
+      if (act) {
+        uint64_t l2 = s_len[t + w];
+        nv = l2 ? (gf2_mulmod(x8n_mod(l2), s_a[t]) ^ s_a[t + w]) : s_a[t];
+        nl = s_len[t] + l2;
+      }
+      __syncthreads();
+      if (act) {
+        s_a[t] = nv;
+        s_len[t] = nl;
+      }
+      __syncthreads();
+    }
+    if (t == 0) checks[j] = s_a[0];
+  } else {
+    const uint32_t MOD = 65521u;
+    uint64_t A = 0, B = 0;
+    uint64_t m = hi - lo;
+    for (uint64_t i = lo; i < hi; i++) {
+      A += p[i];
+      B += (m - (i - lo)) * (uint64_t)p[i];
+      if (((i - lo) & 4095) == 4095) {
+        A %= MOD;
+        B %= MOD;
+      }
+    }
+    s_a[t] = (uint32_t)(A % MOD);
+    s_b[t] = (uint32_t)(B % MOD);
+    s_len[t] = lo;  // segment start
+    __syncthreads();
+    if (t == 0) {
+      uint64_t a = 1, b = n % MOD;
+      for (uint32_t k = 0; k < CHECK_THREADS; k++) {
+        uint64_t st = s_len[k];
+        uint64_t segl = min(n, st + seg) - min(n, st);
+        if (segl == 0) continue;
+        uint64_t tail = (n - st - segl) % MOD;
+        a = (a + s_a[k]) % MOD;
+        b = (b + s_b[k] + tail * s_a[k]) % MOD;
+      }
+      checks[j] = (uint32_t)((b << 16) | a);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Finalize: zlib's CHECK/LENGTH states and inf_leave totals
+// (src/inflate.c:1194-1274).
+// ---------------------------------------------------------------------------
+__global__ void zs_finalize_kernel(const ZsJobDev *__restrict__ jobs, const ZsHeadDev *__restrict__ heads,
+                                   const ZsDecDev *__restrict__ decs, const uint32_t *__restrict__ checks,
+                                   ZsResultDev *__restrict__ res, uint32_t njobs) {
+  uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= njobs) return;
+  const ZsJobDev jb = jobs[j];
+  const ZsHeadDev hd = heads[j];
+  ZsResultDev r;
+  r.pad = 0;
+  r.msg = ZM_NONE;
+  if (hd.code == ZD_SKIP) {
+    r.ret = hd.ret;
+    r.msg = hd.msg;
+    r.total_in = hd.total_in;
+    r.total_out = 0;
+    r.adler = hd.adler;
+    res[j] = r;
+    return;
+  }
+  if (hd.code == ZD_NEED_DICT) {
+    r.ret = ZS_NEED_DICT;
+    r.total_in = 0;
+    r.total_out = 0;
+    r.adler = hd.adler;
+    res[j] = r;
+    return;
+  }
+  const ZsDecDev dc = decs[j];
+  const bool raw = hd.is_gzip < 0;
+  r.total_out = dc.total_out;
+  r.adler = raw ? 0u : checks[j];
+  if (!raw && hd.is_gzip == 0 && dc.total_out == 0) r.adler = 1;
+  if (!raw && hd.is_gzip == 1 && dc.total_out == 0) r.adler = 0;
+  switch (dc.code) {
+    case ZD_END: {
+      uint64_t t = (dc.end_bits + 7) >> 3;
+      if (raw) {
+        r.ret = ZS_STREAM_END;
+        r.total_in = t;
+        break;
+      }
+      if (t + 4 > jb.in_len) {
+        r.ret = ZS_BUF_ERROR;
+        r.total_in = jb.in_len;
+        break;
+      }
+      const uint8_t *q = jb.in + t;
+      uint32_t tr = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
+      if (hd.is_gzip == 0) tr = (tr >> 24) | ((tr >> 8) & 0xff00u) | ((tr & 0xff00u) << 8) | (tr << 24);
+      if (tr != r.adler) {
+        r.ret = ZS_DATA_ERROR;
+        r.msg = ZM_DATA_CHECK;
+        r.total_in = t + 4;
+        break;
+      }
+      if (hd.is_gzip == 1) {
+        if (t + 8 > jb.in_len) {
+          r.ret = ZS_BUF_ERROR;
+          r.total_in = jb.in_len;
+          break;
+        }
+        uint32_t isz = (uint32_t)q[4] | ((uint32_t)q[5] << 8) | ((uint32_t)q[6] << 16) | ((uint32_t)q[7] << 24);
+        if (isz != (uint32_t)(dc.total_out & 0xffffffffu)) {
+          r.ret = ZS_DATA_ERROR;
+          r.msg = ZM_LENGTH_CHECK;
+          r.total_in = t + 8;
+          break;
+        }
+        r.total_in = t + 8;
+      } else {
+        r.total_in = t + 4;
+      }
+      r.ret = ZS_STREAM_END;
+      break;
+    }
+    case ZD_TRUNC:
+      r.ret = ZS_BUF_ERROR;
+      r.total_in = jb.in_len;
+      break;
+    case ZD_FULL:
+      r.ret = ZS_BUF_ERROR;
+      r.total_in = (dc.end_bits + 7) >> 3;
+      break;
+    default:
+      r.ret = ZS_DATA_ERROR;
+      r.msg = dc.msg;
+      r.total_in = (dc.end_bits + 7) >> 3;
+      break;
+  }
+  res[j] = r;
+}
+
+// ---------------------------------------------------------------------------
+// launch sequence for one batch (host side, same stream, no host syncs)
+// ---------------------------------------------------------------------------
+// ev[0..1] (optional): HIP events recorded around the decode kernels, on `stream`
+extern "C" int zs_launch_inflate(const ZsJobDev *d_jobs, ZsHeadDev *d_heads, ZsDecDev *d_decs, uint32_t *d_checks,
+                                 ZsResultDev *d_res, const uint32_t *d_ids, uint32_t n_std, uint32_t n_d64,
+                                 uint32_t njobs, hipStream_t stream, hipEvent_t *ev) {
+  if (njobs == 0) return 0;
+  const uint32_t tb = 64;
+  hipLaunchKernelGGL(zs_header_kernel, dim3((njobs + tb - 1) / tb), dim3(tb), 0, stream, d_jobs, d_heads, njobs);
+  if (ev) (void)hipEventRecord(ev[0], stream);
+  if (n_std) hipLaunchKernelGGL(zs_decode_kernel<false>, dim3(n_std), dim3(64), 0, stream, d_jobs, d_heads, d_ids, d_decs);
+  if (n_d64)
+    hipLaunchKernelGGL(zs_decode_kernel<true>, dim3(n_d64), dim3(64), 0, stream, d_jobs, d_heads, d_ids + n_std, d_decs);
+  if (ev) (void)hipEventRecord(ev[1], stream);
+  hipLaunchKernelGGL(zs_check_kernel, dim3(njobs), dim3(CHECK_THREADS), 0, stream, d_jobs, d_heads, d_decs, d_checks);
+  hipLaunchKernelGGL(zs_finalize_kernel, dim3((njobs + tb - 1) / tb), dim3(tb), 0, stream, d_jobs, d_heads, d_decs, d_checks,
+                     d_res, njobs);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}

@@ -1,0 +1,513 @@
+// zs_capi.cpp -- host side of libzstreams_mi355x.so.
+//
+// Orchestrates the HIP kernels of inflate_kernels.hip behind three C-ABI
+// surfaces (see include/zstreams_mi355x.h):
+//   * zs_inflate_batch    -- many whole streams per launch sequence;
+//   * the reference's handle ABI (src/wasm/*_stream_wasm.c, wasm_stream_common.c);
+//   * the zlib inflate ABI (inflateInit2_/inflate/inflateEnd, src/inflate.c).
+// The stream surfaces accumulate input on the host and hand complete streams
+// to the GPU (first decode attempt at Z_FINISH or whenever the accumulated
+// input has doubled), then serve the output in caller-sized pieces.  Every
+// byte is produced by the GPU; a missing or failing device is a hard error.
+#include <hip/hip_runtime.h>
+#include <zlib.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/zstreams_mi355x.h"
+#include "zs_common.h"
+
+extern "C" int zs_launch_inflate(const ZsJobDev *d_jobs, ZsHeadDev *d_heads, ZsDecDev *d_decs, uint32_t *d_checks,
+                                 ZsResultDev *d_res, const uint32_t *d_ids, uint32_t n_std, uint32_t n_d64,
+                                 uint32_t njobs, hipStream_t stream, hipEvent_t *ev);
+
+namespace {
+
+const char *const kMsgs[ZM_COUNT] = {
+    nullptr,
+    "incorrect header check",
+    "unknown compression method",
+    "invalid window size",
+    "unknown header flags set",
+    "header crc mismatch",
+    "invalid block type",
+    "invalid stored block lengths",
+    "too many length or distance symbols",
+    "invalid code lengths set",
+    "invalid bit length repeat",
+    "invalid code -- missing end-of-block",
+    "invalid literal/lengths set",
+    "invalid distances set",
+    "invalid literal/length code",
+    "invalid distance code",
+    "invalid distance too far back",
+    "incorrect data check",
+    "incorrect length check",
+};
+
+thread_local std::string g_err;
+
+void set_err(const std::string &s) { g_err = s; }
+
+#define HIP_OK(x)                                                              \
+  do {                                                                         \
+    hipError_t e_ = (x);                                                       \
+    if (e_ != hipSuccess) {                                                    \
+      set_err(std::string(#x) + ": " + hipGetErrorString(e_));                 \
+      return ZS_ENODEV;                                                        \
+    }                                                                          \
+  } while (0)
+
+// Device workspace, grown on demand and reused across calls.
+struct Workspace {
+  bool ready = false;
+  int device = -1;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  size_t cap_jobs = 0;
+  ZsJobDev *d_jobs = nullptr;
+  ZsHeadDev *d_heads = nullptr;
+  ZsDecDev *d_decs = nullptr;
+  uint32_t *d_checks = nullptr;
+  ZsResultDev *d_res = nullptr;
+  uint32_t *d_ids = nullptr;
+  ZsJobDev *h_jobs = nullptr;     // pinned
+  ZsResultDev *h_res = nullptr;   // pinned
+  uint32_t *h_ids = nullptr;      // pinned
+  size_t cap_in = 0, cap_out = 0;
+  uint8_t *d_in = nullptr, *d_out = nullptr;
+  // decode-kernel timing (zs_profile): events on the launch stream
+  bool prof = false;
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  double prof_ms = 0.0;
+  uint64_t prof_launches = 0;
+};
+
+std::mutex g_mu;
+Workspace g_ws;
+
+int ws_init() {
+  if (g_ws.ready) return 0;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+    set_err("no HIP device available (libzstreams_mi355x has no CPU path)");
+    return ZS_ENODEV;
+  }
+  HIP_OK(hipGetDevice(&g_ws.device));
+  HIP_OK(hipStreamCreateWithFlags(&g_ws.own_stream, hipStreamNonBlocking));
+  if (!g_ws.stream) g_ws.stream = g_ws.own_stream;
+  g_ws.ready = true;
+  return 0;
+}
+
+template <typename T>
+int grow_dev(T **p, size_t n) {
+  if (*p) HIP_OK(hipFree(*p));
+  *p = nullptr;
+  HIP_OK(hipMalloc(reinterpret_cast<void **>(p), std::max<size_t>(n, 1) * sizeof(T)));
+  return 0;
+}
+template <typename T>
+int grow_host(T **p, size_t n) {
+  if (*p) HIP_OK(hipHostFree(*p));
+  *p = nullptr;
+  HIP_OK(hipHostMalloc(reinterpret_cast<void **>(p), std::max<size_t>(n, 1) * sizeof(T), hipHostMallocDefault));
+  return 0;
+}
+
+int ws_reserve_jobs(size_t n) {
+  if (n <= g_ws.cap_jobs) return 0;
+  size_t c = std::max<size_t>(n, 2 * g_ws.cap_jobs);
+  int r;
+  if ((r = grow_dev(&g_ws.d_jobs, c)) || (r = grow_dev(&g_ws.d_heads, c)) || (r = grow_dev(&g_ws.d_decs, c)) ||
+      (r = grow_dev(&g_ws.d_checks, c)) || (r = grow_dev(&g_ws.d_res, c)) || (r = grow_dev(&g_ws.d_ids, c)) ||
+      (r = grow_host(&g_ws.h_jobs, c)) || (r = grow_host(&g_ws.h_res, c)) || (r = grow_host(&g_ws.h_ids, c)))
+    return r;
+  g_ws.cap_jobs = c;
+  return 0;
+}
+
+int ws_reserve_bytes(uint8_t **p, size_t *cap, size_t need) {
+  if (need <= *cap) return 0;
+  size_t c = std::max(need, *cap + *cap / 2);
+  int r = grow_dev(p, c);
+  if (r) return r;
+  *cap = c;
+  return 0;
+}
+
+// windowBits rules of inflateReset2 (src/inflate.c:147-184).
+bool parse_wbits(int wb, ZsJobDev *j) {
+  int wrap;
+  j->d64 = 0;
+  if (wb < 0) {
+    if (wb < -16) return false;
+    wrap = 0;
+    j->d64 = (wb == -16);
+    wb = -wb;
+  } else {
+    wrap = (wb >> 4) + 5;
+    if (wb < 48) wb &= 15;
+  }
+  if (wb && (wb < 8 || wb > (j->d64 ? 16 : 15))) return false;
+  // wrap bits: 1 zlib, 2 gzip (4 = check, always set for wrapped streams)
+  j->wrap = wrap == 0 ? ZW_RAW : ((wrap & 3) == 1 ? ZW_ZLIB : ((wrap & 3) == 2 ? ZW_GZIP : ZW_AUTO));
+  j->wbits = wb;
+  return true;
+}
+
+void fill_result(zs_result *r, int ret, const ZsResultDev *d) {
+  std::memset(r, 0, sizeof *r);
+  r->ret = ret;
+  if (d) {
+    r->total_in = d->total_in;
+    r->total_out = d->total_out;
+    r->adler = d->adler;
+    r->msg = (d->msg > 0 && d->msg < ZM_COUNT) ? kMsgs[d->msg] : nullptr;
+  }
+}
+
+int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t flags) {
+  int r = ws_init();
+  if (r) {
+    for (uint32_t i = 0; i < n; i++) fill_result(&results[i], Z_STREAM_ERROR, nullptr);
+    return r;
+  }
+  if ((r = ws_reserve_jobs(n))) return r;
+  const bool dev = (flags & ZS_F_DEVICE) != 0;
+  // validate + lay out the staging arenas
+  std::vector<uint32_t> slot(n, UINT32_MAX);
+  std::vector<size_t> in_off(n, 0), out_off(n, 0);
+  size_t in_total = 0, out_total = 0;
+  uint32_t nv = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    ZsJobDev jd{};
+    bool ok = parse_wbits(jobs[i].window_bits, &jd) && jobs[i].in_len < (1ull << 29) &&
+              jobs[i].out_cap < (1ull << 32) && (jobs[i].in || jobs[i].in_len == 0) &&
+              (jobs[i].out || jobs[i].out_cap == 0);
+    if (dev && jobs[i].out && (reinterpret_cast<uintptr_t>(jobs[i].out) & 15u)) ok = false;
+    if (!ok) {
+      fill_result(&results[i], Z_STREAM_ERROR, nullptr);
+      continue;
+    }
+    slot[i] = nv;
+    jd.in_len = jobs[i].in_len;
+    jd.out_cap = jobs[i].out_cap;
+    if (dev) {
+      jd.in = static_cast<const uint8_t *>(jobs[i].in);
+      jd.out = static_cast<uint8_t *>(jobs[i].out);
+    } else {
+      in_off[i] = in_total;
+      in_total += (jobs[i].in_len + 15) & ~size_t(15);
+      out_off[i] = out_total;
+      out_total += (jobs[i].out_cap + 255) & ~size_t(255);
+    }
+    g_ws.h_jobs[nv] = jd;
+    nv++;
+  }
+  if (nv == 0) return 0;
+  hipStream_t st = g_ws.stream;
+  if (!dev) {
+    if ((r = ws_reserve_bytes(&g_ws.d_in, &g_ws.cap_in, in_total + 64))) return r;
+    if ((r = ws_reserve_bytes(&g_ws.d_out, &g_ws.cap_out, out_total + 256))) return r;
+    for (uint32_t i = 0; i < n; i++) {
+      if (slot[i] == UINT32_MAX) continue;
+      ZsJobDev &jd = g_ws.h_jobs[slot[i]];
+      jd.in = g_ws.d_in + in_off[i];
+      jd.out = g_ws.d_out + out_off[i];
+      if (jobs[i].in_len) HIP_OK(hipMemcpyAsync(g_ws.d_in + in_off[i], jobs[i].in, jobs[i].in_len, hipMemcpyHostToDevice, st));
+    }
+  }
+  // std jobs first, then deflate64 jobs (different LDS window)
+  uint32_t n_std = 0, n_d64 = 0;
+  for (uint32_t k = 0; k < nv; k++)
+    if (!g_ws.h_jobs[k].d64) g_ws.h_ids[n_std++] = k;
+  for (uint32_t k = 0; k < nv; k++)
+    if (g_ws.h_jobs[k].d64) g_ws.h_ids[n_std + n_d64++] = k;
+  HIP_OK(hipMemcpyAsync(g_ws.d_jobs, g_ws.h_jobs, nv * sizeof(ZsJobDev), hipMemcpyHostToDevice, st));
+  HIP_OK(hipMemcpyAsync(g_ws.d_ids, g_ws.h_ids, nv * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+  if (zs_launch_inflate(g_ws.d_jobs, g_ws.d_heads, g_ws.d_decs, g_ws.d_checks, g_ws.d_res, g_ws.d_ids, n_std, n_d64, nv,
+                        st, g_ws.prof ? g_ws.ev : nullptr)) {
+    set_err(std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+    return ZS_ENODEV;
+  }
+  HIP_OK(hipMemcpyAsync(g_ws.h_res, g_ws.d_res, nv * sizeof(ZsResultDev), hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  if (g_ws.prof) {
+    float ms = 0.f;
+    HIP_OK(hipEventElapsedTime(&ms, g_ws.ev[0], g_ws.ev[1]));
+    g_ws.prof_ms += ms;
+    g_ws.prof_launches++;
+  }
+  for (uint32_t i = 0; i < n; i++) {
+    if (slot[i] == UINT32_MAX) continue;
+    const ZsResultDev &d = g_ws.h_res[slot[i]];
+    fill_result(&results[i], d.ret, &d);
+    if (!dev && d.total_out)
+      HIP_OK(hipMemcpyAsync(jobs[i].out, g_ws.d_out + out_off[i], d.total_out, hipMemcpyDeviceToHost, st));
+  }
+  if (!dev) HIP_OK(hipStreamSynchronize(st));
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Stream surfaces: accumulate, decode complete streams on the GPU, serve.
+// ---------------------------------------------------------------------------
+struct StreamState {
+  int inited = 0;
+  int wbits = 0;
+  std::vector<uint8_t> acc;   // input accepted and not yet resolved by a decode
+  size_t last_try = 0;        // acc size at the last unsuccessful decode attempt
+  bool done = false;          // decode result available
+  int final_ret = Z_OK;
+  const char *final_msg = nullptr;
+  uint32_t adler = 0;
+  std::vector<uint8_t> out;
+  size_t served = 0;
+  uint64_t total_in = 0, total_out = 0;
+};
+
+// Decode `acc` as one whole stream with growing output capacity.
+int decode_whole(StreamState *s, zs_result *res) {
+  uint64_t cap = std::max<uint64_t>(1u << 20, 4 * (uint64_t)s->acc.size());
+  for (;;) {
+    if (cap >= (1ull << 32)) cap = (1ull << 32) - 1;
+    s->out.resize(cap);
+    zs_job j{};
+    j.in = s->acc.data();
+    j.in_len = s->acc.size();
+    j.out = s->out.data();
+    j.out_cap = cap;
+    j.window_bits = s->wbits;
+    int r = batch_locked(&j, 1, res, 0);
+    if (r) return r;
+    // output full with the stream not finished: grow and retry
+    if (res->ret == Z_BUF_ERROR && res->total_out == cap && cap < (1ull << 32) - 1) {
+      cap *= 4;
+      continue;
+    }
+    s->out.resize(res->total_out);
+    return 0;
+  }
+}
+
+// One zlib-style call: returns ret, updates *consumed / *produced.
+int stream_call(StreamState *s, const uint8_t *in, unsigned in_len, uint8_t *out, unsigned out_len, int flush,
+                unsigned *consumed, unsigned *produced) {
+  *consumed = 0;
+  *produced = 0;
+  if (!s->done) {
+    size_t before = s->acc.size();
+    s->acc.insert(s->acc.end(), in, in + in_len);
+    bool attempt = flush == Z_FINISH || s->acc.size() >= 2 * std::max<size_t>(s->last_try, 32768);
+    if (!attempt) {
+      *consumed = in_len;
+      return in_len ? Z_OK : Z_BUF_ERROR;
+    }
+    zs_result res;
+    int r = decode_whole(s, &res);
+    if (r) {
+      s->acc.resize(before);
+      return Z_STREAM_ERROR;
+    }
+    bool trunc = res.ret == Z_BUF_ERROR;
+    if (trunc && flush != Z_FINISH) {
+      s->last_try = s->acc.size();
+      *consumed = in_len;
+      return in_len ? Z_OK : Z_BUF_ERROR;
+    }
+    s->done = true;
+    s->final_ret = res.ret;
+    s->final_msg = res.msg;
+    s->adler = res.adler;
+    uint64_t used_here = res.total_in > before ? res.total_in - before : 0;
+    *consumed = (unsigned)std::min<uint64_t>(used_here, in_len);
+    s->total_in = res.total_in;
+  }
+  size_t rem = s->out.size() - s->served;
+  size_t n = std::min<size_t>(rem, out_len);
+  if (n) std::memcpy(out, s->out.data() + s->served, n);
+  s->served += n;
+  s->total_out += n;
+  *produced = (unsigned)n;
+  if (s->served < s->out.size()) return flush == Z_FINISH ? Z_BUF_ERROR : Z_OK;
+  return s->final_ret;
+}
+
+struct Handle {
+  z_stream strm;  // layout parity with the reference context (unused fields)
+  StreamState st;
+  unsigned last_consumed = 0;
+};
+
+uintptr_t handle_new() {
+  Handle *h = new (std::nothrow) Handle();
+  if (!h) return 0;
+  std::memset(&h->strm, 0, sizeof h->strm);
+  return reinterpret_cast<uintptr_t>(h);
+}
+int handle_init(uintptr_t hp, int wbits) {
+  Handle *h = reinterpret_cast<Handle *>(hp);
+  if (!h) return Z_STREAM_ERROR;
+  ZsJobDev probe{};
+  if (!parse_wbits(wbits, &probe)) return Z_STREAM_ERROR;
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (ws_init()) return Z_STREAM_ERROR;
+  h->st = StreamState();
+  h->st.inited = 1;
+  h->st.wbits = wbits;
+  return Z_OK;
+}
+int handle_process(uintptr_t hp, uintptr_t in_ptr, unsigned in_len, uintptr_t out_ptr, unsigned out_len, int flush) {
+  Handle *h = reinterpret_cast<Handle *>(hp);
+  if (!h || !h->st.inited) return (int)((unsigned)(Z_STREAM_ERROR & 0xff) << 24);
+  std::lock_guard<std::mutex> lk(g_mu);
+  unsigned cons = 0, prod = 0;
+  int ret = stream_call(&h->st, reinterpret_cast<const uint8_t *>(in_ptr), in_len, reinterpret_cast<uint8_t *>(out_ptr),
+                        out_len, flush, &cons, &prod);
+  h->last_consumed = cons;
+  return (int)((prod & 0x00ffffffu) | ((unsigned)(ret & 0xff) << 24));
+}
+int handle_end(uintptr_t hp) {
+  Handle *h = reinterpret_cast<Handle *>(hp);
+  if (!h) return Z_STREAM_ERROR;
+  delete h;
+  return Z_OK;
+}
+unsigned handle_last_consumed(uintptr_t hp) {
+  Handle *h = reinterpret_cast<Handle *>(hp);
+  return h ? h->last_consumed : 0;
+}
+
+}  // namespace
+
+// ===========================================================================
+// exported C-ABI
+// ===========================================================================
+extern "C" {
+
+const char *zs_version(void) { return "zstreams-mi355x 0.1 (gfx950)"; }
+const char *zs_last_error(void) { return g_err.c_str(); }
+
+int zs_set_stream(void *s) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  int r = ws_init();
+  if (r) return r;
+  g_ws.stream = s ? static_cast<hipStream_t>(s) : g_ws.own_stream;
+  return 0;
+}
+
+// Decode-kernel timing with HIP events on the launch stream: enable (1) /
+// disable (0); zs_profile_read returns the accumulated milliseconds and the
+// number of timed batches since the last enable.
+int zs_profile(int enable) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  int r = ws_init();
+  if (r) return r;
+  if (!g_ws.ev[0]) {
+    HIP_OK(hipEventCreate(&g_ws.ev[0]));
+    HIP_OK(hipEventCreate(&g_ws.ev[1]));
+  }
+  g_ws.prof = enable != 0;
+  g_ws.prof_ms = 0.0;
+  g_ws.prof_launches = 0;
+  return 0;
+}
+int zs_profile_read(double *ms, uint64_t *launches) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  *ms = g_ws.prof_ms;
+  *launches = g_ws.prof_launches;
+  return 0;
+}
+
+int zs_synchronize(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!g_ws.ready) return 0;
+  return hipStreamSynchronize(g_ws.stream) == hipSuccess ? 0 : ZS_ENODEV;
+}
+
+int zs_inflate_batch(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t flags) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  return batch_locked(jobs, n, results, flags);
+}
+
+// ---- reference handle ABI (src/wasm/inflate_stream_wasm.c, inflate9_stream_wasm.c) ----
+uintptr_t inflate_new(void) { return handle_new(); }
+int inflate_init(uintptr_t h) { return handle_init(h, 15); }
+int inflate_init_raw(uintptr_t h) { return handle_init(h, -15); }
+int inflate_init_gzip(uintptr_t h) { return handle_init(h, 15 + 16); }
+int inflate_process(uintptr_t h, uintptr_t in_ptr, unsigned in_len, uintptr_t out_ptr, unsigned out_len, int flush) {
+  return handle_process(h, in_ptr, in_len, out_ptr, out_len, flush);
+}
+int inflate_end(uintptr_t h) { return handle_end(h); }
+unsigned inflate_last_consumed(uintptr_t h) { return handle_last_consumed(h); }
+
+uintptr_t inflate9_new(void) { return handle_new(); }
+int inflate9_init_raw(uintptr_t h) { return handle_init(h, -16); }
+int inflate9_init(uintptr_t h) { return inflate9_init_raw(h); }
+int inflate9_process(uintptr_t h, uintptr_t in_ptr, unsigned in_len, uintptr_t out_ptr, unsigned out_len, int flush) {
+  return handle_process(h, in_ptr, in_len, out_ptr, out_len, flush);
+}
+int inflate9_end(uintptr_t h) { return handle_end(h); }
+unsigned inflate9_last_consumed(uintptr_t h) { return handle_last_consumed(h); }
+
+// ---- zlib inflate ABI (src/inflate.c:186 inflateInit2_, :597 inflate, :1277 inflateEnd) ----
+int ZEXPORT inflateInit2_(z_streamp strm, int windowBits, const char *version, int stream_size) {
+  if (version == Z_NULL || version[0] != '1' || stream_size != (int)sizeof(z_stream)) return Z_VERSION_ERROR;
+  if (strm == Z_NULL) return Z_STREAM_ERROR;
+  strm->msg = Z_NULL;
+  ZsJobDev probe{};
+  if (!parse_wbits(windowBits, &probe)) return Z_STREAM_ERROR;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (ws_init()) return Z_STREAM_ERROR;
+  }
+  StreamState *s = new (std::nothrow) StreamState();
+  if (!s) return Z_MEM_ERROR;
+  s->inited = 1;
+  s->wbits = windowBits;
+  strm->state = reinterpret_cast<struct internal_state *>(s);
+  strm->total_in = strm->total_out = 0;
+  strm->adler = (probe.wrap == ZW_RAW) ? strm->adler : (uLong)(probe.wrap & 1);
+  return Z_OK;
+}
+
+int ZEXPORT inflateInit_(z_streamp strm, const char *version, int stream_size) {
+  return inflateInit2_(strm, 15, version, stream_size);
+}
+
+int ZEXPORT inflate(z_streamp strm, int flush) {
+  if (strm == Z_NULL || strm->state == Z_NULL || strm->next_out == Z_NULL ||
+      (strm->next_in == Z_NULL && strm->avail_in != 0))
+    return Z_STREAM_ERROR;
+  StreamState *s = reinterpret_cast<StreamState *>(strm->state);
+  std::lock_guard<std::mutex> lk(g_mu);
+  unsigned cons = 0, prod = 0;
+  int ret = stream_call(s, strm->next_in, strm->avail_in, strm->next_out, strm->avail_out, flush, &cons, &prod);
+  strm->next_in += cons;
+  strm->avail_in -= cons;
+  strm->total_in += cons;
+  strm->next_out += prod;
+  strm->avail_out -= prod;
+  strm->total_out += prod;
+  if (s->done) {
+    strm->msg = const_cast<char *>(s->final_msg);
+    strm->adler = s->adler;
+  }
+  return ret;
+}
+
+int ZEXPORT inflateEnd(z_streamp strm) {
+  if (strm == Z_NULL || strm->state == Z_NULL) return Z_STREAM_ERROR;
+  delete reinterpret_cast<StreamState *>(strm->state);
+  strm->state = Z_NULL;
+  return Z_OK;
+}
+
+}  // extern "C"

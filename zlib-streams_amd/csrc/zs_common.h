@@ -1,0 +1,99 @@
+// zs_common.h -- layouts shared by the HIP kernels and the host orchestration.
+//
+// One "job" = one complete compressed stream handed to the GPU, with the
+// semantics of a single zlib inflate(strm, Z_FINISH) call over the whole input
+// into an out_cap-byte buffer (reference: src/inflate.c:597-1275 driven as in
+// test/payload_decompress.c:148-178 with the whole payload in one buffer).
+#pragma once
+#include <stdint.h>
+
+// zlib return codes (zlib.h; reference callers decode them in
+// src/wasm/api/zlib-streams.js:89-95)
+#define ZS_OK 0
+#define ZS_STREAM_END 1
+#define ZS_NEED_DICT 2
+#define ZS_STREAM_ERROR (-2)
+#define ZS_DATA_ERROR (-3)
+#define ZS_MEM_ERROR (-4)
+#define ZS_BUF_ERROR (-5)
+#define ZS_VERSION_ERROR (-6)
+
+// strm->msg strings of the reference (src/inflate.c:652-1223, inffast.c:158-283).
+enum ZsMsg {
+  ZM_NONE = 0,
+  ZM_HEADER_CHECK,      // "incorrect header check"
+  ZM_METHOD,            // "unknown compression method"
+  ZM_WINDOW,            // "invalid window size"
+  ZM_FLAGS,             // "unknown header flags set"
+  ZM_HCRC,              // "header crc mismatch"
+  ZM_BLOCK_TYPE,        // "invalid block type"
+  ZM_STORED_LEN,        // "invalid stored block lengths"
+  ZM_TOO_MANY,          // "too many length or distance symbols"
+  ZM_CODE_LENGTHS,      // "invalid code lengths set"
+  ZM_REPEAT,            // "invalid bit length repeat"
+  ZM_MISSING_EOB,       // "invalid code -- missing end-of-block"
+  ZM_LITLEN_SET,        // "invalid literal/lengths set"
+  ZM_DIST_SET,          // "invalid distances set"
+  ZM_LITLEN_CODE,       // "invalid literal/length code"
+  ZM_DIST_CODE,         // "invalid distance code"
+  ZM_TOO_FAR,           // "invalid distance too far back"
+  ZM_DATA_CHECK,        // "incorrect data check"
+  ZM_LENGTH_CHECK,      // "incorrect length check"
+  ZM_COUNT
+};
+
+// Wrapper kinds, derived from windowBits exactly as inflateReset2 does
+// (src/inflate.c:147-184).
+enum ZsWrap { ZW_RAW = 0, ZW_ZLIB = 1, ZW_GZIP = 2, ZW_AUTO = 3 };
+
+// Per-job device descriptor (filled by the host).
+struct ZsJobDev {
+  const uint8_t *in;   // device pointer to compressed bytes
+  uint8_t *out;        // device pointer, 16-byte aligned
+  uint64_t in_len;
+  uint64_t out_cap;
+  int32_t wrap;        // ZsWrap allowed by windowBits (0 raw, 1 zlib, 2 gzip, 3 auto)
+  int32_t d64;         // 1 => raw deflate64 (windowBits == -16)
+  int32_t wbits;       // window bits after the reset rules (8..16, or 0 = from header)
+  int32_t pad;
+};
+
+// Decoder outcome codes (device -> finalize).
+enum ZsDecCode {
+  ZD_END = 0,        // final block decoded; end_bits = bits consumed through it
+  ZD_TRUNC = 1,      // input ran out (zlib NEEDBITS/PULLBYTE would return)
+  ZD_FULL = 2,       // output buffer full before an output-producing symbol
+  ZD_ERROR = 3,      // data error; msg set; end_bits = bits pulled
+  ZD_NEED_DICT = 4,  // zlib header asked for a preset dictionary
+  ZD_SKIP = 5        // header stage already produced the final result
+};
+
+// Header stage result.
+struct ZsHeadDev {
+  int32_t code;        // ZD_* (ZD_SKIP when the header itself failed / truncated)
+  int32_t msg;
+  int32_t is_gzip;     // 1 gzip trailer (CRC-32 + ISIZE), 0 zlib (Adler-32), -1 raw
+  int32_t ret;         // zlib return code when code == ZD_SKIP
+  uint64_t start_byte; // first byte of deflate data
+  uint64_t total_in;   // valid when code == ZD_SKIP / ZD_NEED_DICT
+  uint32_t adler;      // valid when code == ZD_SKIP / ZD_NEED_DICT
+  uint32_t pad2;
+};
+
+// Deflate decode result.
+struct ZsDecDev {
+  int32_t code;
+  int32_t msg;
+  uint64_t end_bits;   // relative to the job's input byte 0
+  uint64_t total_out;
+};
+
+// Final per-job result (device -> host), zlib z_stream fields after the call.
+struct ZsResultDev {
+  int32_t ret;
+  int32_t msg;
+  uint64_t total_in;
+  uint64_t total_out;
+  uint32_t adler;
+  int32_t pad;
+};

@@ -1,0 +1,245 @@
+"""Host-side mirror of the reference's Compression Streams surface over the
+MI355X inflate core (libzstreams_mi355x.so, C-ABI, loaded with ctypes).
+
+Reference interface mirrored here:
+  * src/wasm/api/zlib-streams.js:15-157  ``_make`` / ``DecompressionStreamZlib``:
+    formats "deflate", "deflate-raw", "gzip", "deflate64-raw"; 32 KiB input
+    slices, 64 KiB output buffer, stop a write when a call consumes 0 bytes,
+    ``Z_FINISH`` drain in ``flush()``; a negative code raises (transform 89-95,
+    flush 125-130).
+  * the handle ABI of src/wasm/*_stream_wasm.c (``inflate_new`` ...).
+
+Plus the batch entry ``inflate_batch`` (many whole streams per GPU launch).
+
+There is no CPU path: if the shared library or a HIP device is missing, every
+call raises ``ZStreamsError``.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libzstreams_mi355x.so")
+
+Z_OK, Z_STREAM_END, Z_NEED_DICT = 0, 1, 2
+Z_STREAM_ERROR, Z_DATA_ERROR, Z_MEM_ERROR, Z_BUF_ERROR = -2, -3, -4, -5
+Z_NO_FLUSH, Z_FINISH = 0, 4
+ZS_F_DEVICE = 1
+
+# windowBits per format, as the reference's init functions choose them
+# (src/wasm/inflate_stream_wasm.c:22-45, inflate9_stream_wasm.c:15-20)
+FORMAT_WBITS = {"deflate": 15, "deflate-raw": -15, "gzip": 31, "deflate64-raw": -16}
+
+# exported symbols and their ctypes signatures (include/zstreams_mi355x.h)
+_U = ctypes.c_size_t  # uintptr_t
+_SIGS = {
+    "inflate_new": (_U, []), "inflate_init": (ctypes.c_int, [_U]),
+    "inflate_init_raw": (ctypes.c_int, [_U]), "inflate_init_gzip": (ctypes.c_int, [_U]),
+    "inflate_process": (ctypes.c_int, [_U, _U, ctypes.c_uint, _U, ctypes.c_uint, ctypes.c_int]),
+    "inflate_end": (ctypes.c_int, [_U]), "inflate_last_consumed": (ctypes.c_uint, [_U]),
+    "inflate9_new": (_U, []), "inflate9_init": (ctypes.c_int, [_U]),
+    "inflate9_init_raw": (ctypes.c_int, [_U]),
+    "inflate9_process": (ctypes.c_int, [_U, _U, ctypes.c_uint, _U, ctypes.c_uint, ctypes.c_int]),
+    "inflate9_end": (ctypes.c_int, [_U]), "inflate9_last_consumed": (ctypes.c_uint, [_U]),
+    "zs_set_stream": (ctypes.c_int, [ctypes.c_void_p]),
+    "zs_profile": (ctypes.c_int, [ctypes.c_int]),
+    "zs_profile_read": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)]),
+    "zs_synchronize": (ctypes.c_int, []),
+    "zs_version": (ctypes.c_char_p, []), "zs_last_error": (ctypes.c_char_p, []),
+}
+
+
+class ZStreamsError(RuntimeError):
+    pass
+
+
+class ZsJob(ctypes.Structure):
+    _fields_ = [("in_", ctypes.c_void_p), ("in_len", ctypes.c_uint64), ("out", ctypes.c_void_p),
+                ("out_cap", ctypes.c_uint64), ("window_bits", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+class ZsResult(ctypes.Structure):
+    _fields_ = [("ret", ctypes.c_int32), ("reserved", ctypes.c_int32), ("total_in", ctypes.c_uint64),
+                ("total_out", ctypes.c_uint64), ("adler", ctypes.c_uint32), ("reserved2", ctypes.c_uint32),
+                ("msg", ctypes.c_char_p)]
+
+    def as_dict(self):
+        return {"ret": self.ret, "msg": self.msg.decode() if self.msg else None,
+                "total_in": self.total_in, "total_out": self.total_out, "adler": self.adler}
+
+
+_lib = None
+
+
+def lib():
+    """Load the shared library (fails loudly: there is no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ZStreamsError(f"{LIB_PATH} missing: run __graft_entry__.build() (make -C zlib-streams_amd/csrc)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        L.zs_inflate_batch.restype = ctypes.c_int
+        L.zs_inflate_batch.argtypes = [ctypes.POINTER(ZsJob), ctypes.c_uint32, ctypes.POINTER(ZsResult), ctypes.c_uint32]
+        _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc != 0:
+        raise ZStreamsError(f"libzstreams_mi355x error {rc}: {lib().zs_last_error().decode()}")
+
+
+def inflate_batch(streams, window_bits=-15, out_caps=None):
+    """Inflate many whole streams on the GPU (host buffers).
+
+    Each stream behaves like inflateInit2(window_bits) + one inflate(Z_FINISH)
+    into an out_cap-byte buffer.  Returns [(bytes, result_dict)].
+    """
+    n = len(streams)
+    if out_caps is None:
+        out_caps = [max(1 << 16, 8 * len(s) + 4096) for s in streams]
+    wbs = window_bits if isinstance(window_bits, (list, tuple)) else [window_bits] * n
+    jobs = (ZsJob * max(n, 1))()
+    res = (ZsResult * max(n, 1))()
+    inbufs, outbufs = [], []
+    for i, s in enumerate(streams):
+        ib = ctypes.create_string_buffer(bytes(s), max(len(s), 1))
+        ob = ctypes.create_string_buffer(max(out_caps[i], 1))
+        inbufs.append(ib)
+        outbufs.append(ob)
+        jobs[i].in_ = ctypes.cast(ib, ctypes.c_void_p).value if len(s) else None
+        jobs[i].in_len = len(s)
+        jobs[i].out = ctypes.cast(ob, ctypes.c_void_p).value
+        jobs[i].out_cap = out_caps[i]
+        jobs[i].window_bits = wbs[i]
+    _check(lib().zs_inflate_batch(jobs, n, res, 0))
+    return [(outbufs[i].raw[:res[i].total_out], res[i].as_dict()) for i in range(n)]
+
+
+def inflate_batch_device(in_ptrs, in_lens, out_ptrs, out_caps, window_bits):
+    """Inflate streams already resident in HBM (device pointers, outputs 16 B aligned)."""
+    n = len(in_ptrs)
+    jobs = (ZsJob * n)()
+    res = (ZsResult * n)()
+    for i in range(n):
+        jobs[i].in_ = in_ptrs[i]
+        jobs[i].in_len = in_lens[i]
+        jobs[i].out = out_ptrs[i]
+        jobs[i].out_cap = out_caps[i]
+        jobs[i].window_bits = window_bits[i] if isinstance(window_bits, (list, tuple)) else window_bits
+    _check(lib().zs_inflate_batch(jobs, n, res, ZS_F_DEVICE))
+    return [res[i].as_dict() for i in range(n)]
+
+
+def profile(enable):
+    """Time the decode kernels with HIP events on the launch stream."""
+    _check(lib().zs_profile(1 if enable else 0))
+
+
+def profile_read():
+    ms = ctypes.c_double()
+    n = ctypes.c_uint64()
+    _check(lib().zs_profile_read(ctypes.byref(ms), ctypes.byref(n)))
+    return ms.value, n.value
+
+
+def set_stream(hip_stream_handle):
+    _check(lib().zs_set_stream(hip_stream_handle))
+
+
+class _Handle:
+    """The reference's handle ABI for one decompression stream."""
+
+    def __init__(self, fmt):
+        if fmt not in FORMAT_WBITS:
+            raise ValueError(f"unsupported format {fmt!r}")
+        L = lib()
+        p = "inflate9_" if fmt == "deflate64-raw" else "inflate_"
+        self._process = getattr(L, p + "process")
+        self._last = getattr(L, p + "last_consumed")
+        self._end = getattr(L, p + "end")
+        self.h = getattr(L, p + "new")()
+        if not self.h:
+            raise MemoryError("stream allocation failed")
+        init = {"deflate": "inflate_init", "deflate-raw": "inflate_init_raw", "gzip": "inflate_init_gzip",
+                "deflate64-raw": "inflate9_init_raw"}[fmt]
+        r = getattr(L, init)(self.h)
+        if r != 0:
+            raise ZStreamsError("init failed:" + str(r))
+
+    def process(self, data, out_buf, flush):
+        ib = ctypes.create_string_buffer(bytes(data), max(len(data), 1))
+        r = self._process(self.h, ctypes.addressof(ib) if data else 0, len(data),
+                          ctypes.addressof(out_buf), len(out_buf), flush)
+        r &= 0xffffffff
+        produced = r & 0x00ffffff
+        code = (r >> 24) & 0xff
+        return produced, (code - 256 if code & 0x80 else code), self._last(self.h)
+
+    def end(self):
+        if self.h:
+            r = self._end(self.h)
+            self.h = 0
+            return r
+        return 0
+
+
+class DecompressionStreamZlib:
+    """Mirror of the reference's ``DecompressionStreamZlib`` TransformStream
+    (src/wasm/api/zlib-streams.js:15-157): feed chunks with ``transform``,
+    finish with ``flush``; both return the list of enqueued output chunks."""
+
+    def __init__(self, fmt="deflate", options=None):
+        options = options or {}
+        self.out_size = options.get("outBuffer", 64 * 1024)
+        self._h = _Handle(fmt)
+        self._out = ctypes.create_string_buffer(self.out_size)
+
+    def transform(self, chunk):
+        out = []
+        off = 0
+        try:
+            while off < len(chunk):
+                n = min(len(chunk) - off, 32 * 1024)
+                produced, code, consumed = self._h.process(chunk[off:off + n], self._out, Z_NO_FLUSH)
+                if produced:
+                    out.append(self._out.raw[:produced])
+                if code < 0:
+                    raise ZStreamsError("process error:" + str(code))
+                if consumed == 0:
+                    break
+                off += consumed
+        except Exception:
+            self._h.end()
+            raise
+        return out
+
+    def flush(self):
+        out = []
+        try:
+            while True:
+                produced, code, _ = self._h.process(b"", self._out, Z_FINISH)
+                if code < 0:
+                    raise ZStreamsError("process error:" + str(code))
+                if produced:
+                    out.append(self._out.raw[:produced])
+                if code == 1 or produced == 0:
+                    break
+        finally:
+            r = self._h.end()
+            if r != 0:
+                raise ZStreamsError("end error:" + str(r))
+        return out
+
+
+def decompress(data, fmt="deflate-raw", write_size=4096):
+    """Pipe ``data`` through a DecompressionStreamZlib in ``write_size`` writes."""
+    ds = DecompressionStreamZlib(fmt)
+    parts = []
+    for i in range(0, len(data), write_size):
+        parts += ds.transform(data[i:i + write_size])
+    parts += ds.flush()
+    return b"".join(parts)
