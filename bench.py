@@ -150,7 +150,8 @@ def main():
     if dist:
         tdist.barrier()
     t_el = time.perf_counter() - t_start
-    k_ms, k_n = zstreams.profile_read()
+    k_ms, b_ms, k_n = zstreams.profile_read()
+    stats = zstreams.last_stats()
     zstreams.profile(False)
     if dist:
         t = torch.tensor([t_el], dtype=torch.float64, device=dev)
@@ -187,9 +188,11 @@ def main():
             "verified_bit_exact": ok,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                         "kernel": "zs_decode_kernel<false>", "kernel_ms_avg": round(k_avg_s * 1e3, 3),
+                         "kernel": "zs_lane_kernel" if stats["chunked_jobs"] else "zs_decode_kernel<false>",
+                         "kernel_ms_avg": round(k_avg_s * 1e3, 3), "batch_ms_avg": round(b_ms / max(k_n, 1), 3),
                          "alg_bytes_per_launch": per_launch_alg},
             "cpu_baseline": cpu,
+            "path_stats": stats,
         }
         print(json.dumps(line), flush=True)
     if dist:

@@ -89,7 +89,10 @@ int zs_set_stream(void *hip_stream);
 int zs_synchronize(void);
 /* decode-kernel timing via HIP events on the launch stream */
 int zs_profile(int enable);
-int zs_profile_read(double *ms, uint64_t *launches);
+int zs_profile_read(double *decode_ms, double *batch_ms, uint64_t *launches);
+/* last batch: [jobs on the chunked path, chunks, chunked jobs that fell back
+   to the serial decoder, jobs on the serial path] */
+int zs_last_stats(uint32_t out[4]);
 const char *zs_version(void);
 const char *zs_last_error(void);
 

@@ -175,3 +175,57 @@ def test_zlib_abi_payload_decompress_loop(zs):
                 s.avail_out = 65536
         assert ret == 1 and L.inflateEnd(ctypes.byref(s)) == 0
         assert hashlib.sha256(bytes(out)).hexdigest() == MAN["fixtures"][name]["sha256"]
+
+
+# ---------------------------------------------------------------------------
+# speculative chunked path (streams >= 4 chunks of compressed data)
+# ---------------------------------------------------------------------------
+def _big_cases(rng, n, lo=1 << 20, hi=6 << 20):
+    cases = []
+    for i in range(n):
+        size = rng.randint(lo, hi)
+        raw = corpus.stream(rng.randrange(64), size)
+        wb = rng.choice([-15, -15, 15, 31])
+        c = zlib.compressobj(rng.choice([1, 6, 6, 9]), zlib.DEFLATED, wb, 8, rng.choice([0, 0, 0, 1]))
+        cases.append((raw, c.compress(raw) + c.flush(), wb))
+    return cases
+
+
+def test_chunked_path_exact_and_taken(zs):
+    cases = _big_cases(random.Random(5), 8)
+    got = zs.inflate_batch([c[1] for c in cases], [c[2] for c in cases], [len(c[0]) for c in cases])
+    st = zs.last_stats()
+    assert st["chunked_jobs"] == len(cases), st
+    for (raw, comp, wb), (out, info) in zip(cases, got):
+        assert info["ret"] == 1 and info["total_in"] == len(comp) and out == raw, (wb, info)
+    # text streams at the default strategy must not need the serial fallback
+    assert st["fallback_jobs"] == 0, st
+
+
+def test_chunked_path_errors_match_oracle(zs):
+    rng = random.Random(6)
+    base = _big_cases(rng, 6, 600 << 10, 2 << 20)
+    cases = []
+    for raw, comp, wb in base:
+        b = bytearray(comp)
+        r = rng.random()
+        if r < 0.4:
+            i = rng.randrange(len(b) // 2, len(b))
+            b[i] ^= 1 << rng.randrange(8)
+        elif r < 0.7:
+            b = b[:rng.randrange(len(b) // 2, len(b))]
+        cap = len(raw) if rng.random() < 0.7 else rng.randint(len(raw) // 2, len(raw))
+        cases.append((bytes(b), wb, cap))
+    run_and_compare(zs, cases)
+
+
+def test_chunked_random_and_stored(zs):
+    rng = random.Random(7)
+    raw = bytes(rng.getrandbits(8) for _ in range(1 << 20)) + corpus.stream(5, 1 << 20)
+    comps = []
+    for lvl in (0, 1, 6):
+        c = zlib.compressobj(lvl, zlib.DEFLATED, -15)
+        comps.append(c.compress(raw) + c.flush())
+    got = zs.inflate_batch(comps, -15, [len(raw)] * 3)
+    for (out, info), comp in zip(got, comps):
+        assert info["ret"] == 1 and info["total_in"] == len(comp) and out == raw

@@ -24,216 +24,11 @@
 #include <stdint.h>
 
 #include "zs_common.h"
+#include "zs_device.h"
 
-#define WAVE 64
 #define IN_RING_WORDS 1024   // 4 KiB compressed-input ring
 #define PIECE_WORDS 256      // 1 KiB per fill (64 lanes x 16 B)
 #define FLUSH_BYTES 1024     // output flush granule (64 lanes x 16 B)
-#define TABLE_ENTRIES 1448   // ENOUGH (852 + 594), src/inftrees.h:52-55
-
-// ---------------------------------------------------------------------------
-// constant tables (src/inftrees.c:59-87; op = 16+extra deflate, 128+extra d64,
-// 64 invalid, 96 end of block)
-// ---------------------------------------------------------------------------
-__constant__ uint16_t c_lbase[2][31] = {
-    {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258, 0, 0},
-    {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 3, 0, 0}};
-__constant__ uint8_t c_lop[2][31] = {
-    {16, 16, 16, 16, 16, 16, 16, 16, 17, 17, 17, 17, 18, 18, 18, 18, 19, 19, 19, 19, 20, 20, 20, 20, 21, 21, 21, 21, 16, 73, 200},
-    {128, 128, 128, 128, 128, 128, 128, 128, 129, 129, 129, 129, 130, 130, 130, 130, 131, 131, 131, 131, 132, 132, 132, 132,
-     133, 133, 133, 133, 144, 73, 200}};
-__constant__ uint16_t c_dbase[2][32] = {
-    {1, 2, 3, 4, 5, 7, 9, 13, 17, 25, 33, 49, 65, 97, 129, 193, 257, 385, 513, 769, 1025, 1537, 2049, 3073, 4097, 6145, 8193,
-     12289, 16385, 24577, 0, 0},
-    {1, 2, 3, 4, 5, 7, 9, 13, 17, 25, 33, 49, 65, 97, 129, 193, 257, 385, 513, 769, 1025, 1537, 2049, 3073, 4097, 6145, 8193,
-     12289, 16385, 24577, 32769, 49153}};
-__constant__ uint8_t c_dop[2][32] = {
-    {16, 16, 16, 16, 17, 17, 18, 18, 19, 19, 20, 20, 21, 21, 22, 22, 23, 23, 24, 24, 25, 25, 26, 26, 27, 27, 28, 28, 29, 29, 64, 64},
-    {128, 128, 128, 128, 129, 129, 130, 130, 131, 131, 132, 132, 133, 133, 134, 134, 135, 135, 136, 136, 137, 137, 138, 138,
-     139, 139, 140, 140, 141, 141, 142, 142}};
-__constant__ uint8_t c_clorder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
-
-enum { T_CODES = 0, T_LENS = 1, T_DISTS = 2 };
-
-__device__ __forceinline__ uint32_t mk_entry(uint32_t op, uint32_t bits, uint32_t val) {
-  return op | (bits << 8) | (val << 16);
-}
-__device__ __forceinline__ uint32_t e_op(uint32_t e) { return e & 0xffu; }
-__device__ __forceinline__ uint32_t e_bits(uint32_t e) { return (e >> 8) & 0xffu; }
-__device__ __forceinline__ uint32_t e_val(uint32_t e) { return e >> 16; }
-
-__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & (WAVE - 1); }
-__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
-
-// ---------------------------------------------------------------------------
-// Table builder: canonical Huffman -> zlib-layout 2-level table in LDS.
-// Restates src/inftrees.c:33-321; the sort and the root fill run across lanes,
-// the long-code sub-tables keep zlib's allocation order and sizing.
-// Returns 0 ok, -1 bad code set, 1 table space exceeded.  `*root` is in/out.
-// ---------------------------------------------------------------------------
-__device__ int build_table(int type, const uint16_t *lens, uint32_t n, uint32_t *table, uint32_t *root_io,
-                           uint16_t *sorted, uint32_t *scratch16, int d64) {
-  const uint32_t lane = lane_id();
-  const uint64_t lt_mask = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
-  uint32_t cnt[16];
-#pragma unroll
-  for (int L = 0; L < 16; L++) cnt[L] = 0;
-  for (uint32_t g = 0; g < n; g += WAVE) {
-    uint32_t s = g + lane;
-    uint32_t L = (s < n) ? lens[s] : 16u;
-#pragma unroll
-    for (int x = 0; x < 16; x++) cnt[x] += __popcll(__ballot(L == (uint32_t)x));
-  }
-  uint32_t maxlen = 0, minlen = 0;
-#pragma unroll
-  for (int x = 15; x >= 1; x--)
-    if (maxlen == 0 && cnt[x]) maxlen = x;
-  uint32_t root = *root_io;
-  if (root > maxlen) root = maxlen;
-  if (maxlen == 0) {
-    if (d64) return -1;  // src/inftrees.c:131-132
-    if (lane < 2) table[lane] = mk_entry(64, 1, 0);
-    __builtin_amdgcn_wave_barrier();
-    *root_io = 1;
-    return 0;
-  }
-#pragma unroll
-  for (int x = 1; x <= 15; x++)
-    if (minlen == 0 && cnt[x]) minlen = x;
-  if (root < minlen) root = minlen;
-  int room = 1;
-  bool over = false;
-#pragma unroll
-  for (int x = 1; x <= 15; x++) {
-    room = (room << 1) - (int)cnt[x];
-    over |= room < 0;
-  }
-  if (over) return -1;
-  if (room > 0 && (type == T_CODES || maxlen != 1)) return -1;
-
-  // canonical first codes and sorted offsets
-  uint32_t start[16], first[16];
-  start[0] = 0;
-  start[1] = 0;
-  first[0] = 0;
-  first[1] = 0;
-#pragma unroll
-  for (int x = 1; x < 15; x++) {
-    start[x + 1] = start[x] + cnt[x];
-    first[x + 1] = (first[x] + cnt[x]) << 1;
-  }
-  // publish counts and starts for the serial sub-table pass
-  if (lane < 16) {
-    uint32_t c = 0, st = 0;
-#pragma unroll
-    for (int x = 0; x < 16; x++) {
-      if ((uint32_t)x == lane) { c = cnt[x]; st = start[x]; }
-    }
-    scratch16[lane] = c;
-    scratch16[16 + lane] = st;
-  }
-  // stable sort of symbols by length (ballot rank within each length)
-  {
-    uint32_t base[16];
-#pragma unroll
-    for (int x = 0; x < 16; x++) base[x] = start[x];
-    for (uint32_t g = 0; g < n; g += WAVE) {
-      uint32_t s = g + lane;
-      uint32_t L = (s < n) ? lens[s] : 0u;
-#pragma unroll
-      for (int x = 1; x <= 15; x++) {
-        uint64_t m = __ballot(L == (uint32_t)x);
-        if (L == (uint32_t)x) sorted[base[x] + __popcll(m & lt_mask)] = (uint16_t)s;
-        base[x] += __popcll(m);
-      }
-    }
-  }
-  __builtin_amdgcn_wave_barrier();
-
-  const uint32_t first_coded = (type == T_CODES) ? 20u : (type == T_LENS ? 257u : 0u);
-  const uint32_t lim = (type == T_LENS) ? (d64 ? 851u : 852u) : (type == T_DISTS ? (d64 ? 593u : 592u) : 0xffffffffu);
-  uint32_t used = 1u << root;
-  if (used > lim) return 1;
-  const uint32_t ncodes = start[15] + cnt[15];
-  // number of codes of length <= root
-  uint32_t nshort = 0;
-#pragma unroll
-  for (int x = 1; x <= 15; x++)
-    if ((uint32_t)x <= root) nshort += cnt[x];
-
-  auto sym_entry = [&](uint32_t s, uint32_t bits) -> uint32_t {
-    if (s + 1u < first_coded) return mk_entry(0, bits, s);
-    if (s >= first_coded) {
-      uint32_t k = s - first_coded;
-      if (type == T_LENS) return mk_entry(c_lop[d64][k], bits, c_lbase[d64][k]);
-      return mk_entry(c_dop[d64][k], bits, c_dbase[d64][k]);
-    }
-    return mk_entry(96, bits, 0);
-  };
-
-  // root fill for short codes: lane-parallel over codes, replicated entries
-  for (uint32_t g = 0; g < nshort; g += WAVE) {
-    uint32_t i = g + lane;
-    if (i < nshort) {
-      uint32_t s = sorted[i];
-      uint32_t L = lens[s];
-      uint32_t st = scratch16[16 + L];
-      uint32_t code = 0;
-#pragma unroll
-      for (int x = 1; x <= 15; x++)
-        if ((uint32_t)x == L) code = first[x];
-      code += i - st;
-      uint32_t rev = __builtin_bitreverse32(code) >> (32 - L);
-      uint32_t e = sym_entry(s, L);
-      uint32_t reps = 1u << (root - L);
-      for (uint32_t j = 0; j < reps; j++) table[rev + (j << L)] = e;
-    }
-  }
-  // incomplete single 1-bit code: slot 1 is an invalid marker
-  if (room > 0 && lane == 0) table[1] = mk_entry(64, 1, 0);
-
-  // long codes: serial over codes (uniform), lane-parallel replication
-  uint32_t next = 0, cur_size = 1u << root, open_low = 0xffffffffu, curr = root;
-  const uint32_t rmask = (1u << root) - 1;
-  for (uint32_t i = nshort; i < ncodes; i++) {
-    uint32_t s = uni(sorted[i]);
-    uint32_t L = uni(lens[s]);
-    uint32_t st = uni(scratch16[16 + L]);
-    uint32_t code = 0;
-#pragma unroll
-    for (int x = 1; x <= 15; x++)
-      if ((uint32_t)x == L) code = first[x];
-    code += i - st;
-    uint32_t rev = __builtin_bitreverse32(code) >> (32 - L);
-    uint32_t low = rev & rmask;
-    if (low != open_low) {
-      next += cur_size;
-      curr = L - root;
-      int left = 1 << curr;
-      while (curr + root < maxlen) {
-        uint32_t x = curr + root;
-        uint32_t remain = uni(scratch16[x]) - ((x == L) ? (i - st) : 0u);
-        left -= (int)remain;
-        if (left <= 0) break;
-        curr++;
-        left <<= 1;
-      }
-      cur_size = 1u << curr;
-      used += cur_size;
-      if (used > lim) return 1;
-      open_low = low;
-      if (lane == 0) table[low] = mk_entry(curr, root, next);
-    }
-    uint32_t e = sym_entry(s, L - root);
-    uint32_t step = 1u << (L - root);
-    uint32_t reps = cur_size >> (L - root);
-    uint32_t idx0 = next + (rev >> root);
-    for (uint32_t j = lane; j < reps; j += WAVE) table[idx0 + j * step] = e;
-  }
-  __builtin_amdgcn_wave_barrier();
-  *root_io = root;
-  return 0;
-}
 
 // ---------------------------------------------------------------------------
 // Header stage: zlib / gzip wrapper parse (src/inflate.c:629-833), one thread
@@ -539,14 +334,16 @@ struct Inflater {
     fixed_ready = true;
   }
 
+  uint32_t stop_bits;  // end bit of the last decoded element (errors / FULL / END)
+
   // Decode from the current bit position to the end of the final block.
-  // Returns a ZsDecCode; *msg and *ebits describe errors / stopping point.
-  __device__ int run(int *msg, uint32_t *ebits) {
+  // Returns ZsDecCode | (ZsMsg << 8); stop_bits describes where it stopped.
+  __device__ int run() {
     uint32_t lane = lane_id();
     bool last = false;
     for (;;) {
       if (last) {
-        *ebits = bitpos();
+        stop_bits = bitpos();
         return ZD_END;
       }
       refill();
@@ -564,9 +361,8 @@ struct Inflater {
         if (short_of(32)) return ZD_TRUNC;
         uint32_t v = (uint32_t)hold;
         if ((v & 0xffffu) != ((v >> 16) ^ 0xffffu)) {
-          *msg = ZM_STORED_LEN;
-          *ebits = bitpos() + 32;
-          return ZD_ERROR;
+          stop_bits = bitpos() + 32;
+          return ZD_ERROR | (ZM_STORED_LEN << 8);
         }
         drop(32);
         uint32_t slen = v & 0xffffu;
@@ -577,7 +373,7 @@ struct Inflater {
         copy_stored(src, m);
         if (m < slen) {
           if (m == avail) return ZD_TRUNC;  // input exhausted first (or at the same time)
-          *ebits = (src + m) * 8;
+          stop_bits = (src + m) * 8;
           return ZD_FULL;
         }
         seek((src + slen) * 8);
@@ -597,9 +393,8 @@ struct Inflater {
         uint32_t ncode = (uint32_t)((hold >> 10) & 15) + 4;
         drop(14);
         if (nlen > 286 || (!D64 && ndist > 30)) {
-          *msg = ZM_TOO_MANY;
-          *ebits = bitpos();
-          return ZD_ERROR;
+          stop_bits = bitpos();
+          return ZD_ERROR | (ZM_TOO_MANY << 8);
         }
         // code-length code lengths (src/inflate.c:923-934)
         for (uint32_t i = 0; i < ncode; i++) {
@@ -612,9 +407,8 @@ struct Inflater {
         __builtin_amdgcn_wave_barrier();
         uint32_t cbits = 7;
         if (build_table(T_CODES, lens, 19, tab, &cbits, sorted, scratch16, D64)) {
-          *msg = ZM_CODE_LENGTHS;
-          *ebits = bitpos();
-          return ZD_ERROR;
+          stop_bits = bitpos();
+          return ZD_ERROR | (ZM_CODE_LENGTHS << 8);
         }
         uint32_t total = nlen + ndist;
         uint32_t have = 0;
@@ -634,16 +428,14 @@ struct Inflater {
           if (short_of(eb + xb)) return ZD_TRUNC;
           drop(eb);
           if (ev == 16 && have == 0) {
-            *msg = ZM_REPEAT;
-            *ebits = bitpos() + 2;
-            return ZD_ERROR;
+            stop_bits = bitpos() + 2;
+            return ZD_ERROR | (ZM_REPEAT << 8);
           }
           uint32_t rep = (ev == 16 ? 3 : (ev == 17 ? 3 : 11)) + ((uint32_t)hold & ((1u << xb) - 1));
           drop(xb);
           if (have + rep > total) {
-            *msg = ZM_REPEAT;
-            *ebits = bitpos();
-            return ZD_ERROR;
+            stop_bits = bitpos();
+            return ZD_ERROR | (ZM_REPEAT << 8);
           }
           __builtin_amdgcn_wave_barrier();
           uint32_t fillv = ev == 16 ? uni(lens[have - 1]) : 0u;
@@ -655,30 +447,26 @@ struct Inflater {
         }
         __builtin_amdgcn_wave_barrier();
         if (uni(lens[256]) == 0) {
-          *msg = ZM_MISSING_EOB;
-          *ebits = bitpos();
-          return ZD_ERROR;
+          stop_bits = bitpos();
+          return ZD_ERROR | (ZM_MISSING_EOB << 8);
         }
         lbits = 9;
         if (build_table(T_LENS, lens, nlen, tab, &lbits, sorted, scratch16, D64)) {
-          *msg = ZM_LITLEN_SET;
-          *ebits = bitpos();
-          return ZD_ERROR;
+          stop_bits = bitpos();
+          return ZD_ERROR | (ZM_LITLEN_SET << 8);
         }
         // distance table goes right after the literal/length table; its size
         // is bounded by 852 entries (ENOUGH_LENS)
         dbits = 6;
         if (build_table(T_DISTS, lens + nlen, ndist, tab + 852, &dbits, sorted, scratch16, D64)) {
-          *msg = ZM_DIST_SET;
-          *ebits = bitpos();
-          return ZD_ERROR;
+          stop_bits = bitpos();
+          return ZD_ERROR | (ZM_DIST_SET << 8);
         }
         lt = tab;
         dt = tab + 852;
       } else {
-        *msg = ZM_BLOCK_TYPE;
-        *ebits = bitpos();
-        return ZD_ERROR;
+        stop_bits = bitpos();
+        return ZD_ERROR | (ZM_BLOCK_TYPE << 8);
       }
 
       // ---- symbol loop (src/inffast.c:100-287 / src/inflate.c:1037-1193) ----
@@ -698,7 +486,7 @@ struct Inflater {
         drop(used);
         if (op == 0) {
           if (pos == cap) {
-            *ebits = bitpos();
+            stop_bits = bitpos();
             return ZD_FULL;
           }
           put_literal(e_val(e));
@@ -706,9 +494,8 @@ struct Inflater {
         }
         if (op & 32) break;  // end of block
         if (op & 64) {
-          *msg = ZM_LITLEN_CODE;
-          *ebits = bitpos();
-          return ZD_ERROR;
+          stop_bits = bitpos();
+          return ZD_ERROR | (ZM_LITLEN_CODE << 8);
         }
         uint32_t len = e_val(e);
         uint32_t xb = op & (D64 ? 31u : 15u);
@@ -730,9 +517,8 @@ struct Inflater {
         if (short_of(dused)) return ZD_TRUNC;
         drop(dused);
         if (dop & 64) {
-          *msg = ZM_DIST_CODE;
-          *ebits = bitpos();
-          return ZD_ERROR;
+          stop_bits = bitpos();
+          return ZD_ERROR | (ZM_DIST_CODE << 8);
         }
         uint32_t dist = e_val(d);
         uint32_t dx = dop & 15u;
@@ -742,18 +528,17 @@ struct Inflater {
           drop(dx);
         }
         if (pos == cap) {
-          *ebits = bitpos();
+          stop_bits = bitpos();
           return ZD_FULL;
         }
         if (dist > pos + whave) {
-          *msg = ZM_TOO_FAR;
-          *ebits = bitpos();
-          return ZD_ERROR;
+          stop_bits = bitpos();
+          return ZD_ERROR | (ZM_TOO_FAR << 8);
         }
         uint32_t n = min(len, cap - pos);
         copy_match(n, dist);
         if (n < len) {
-          *ebits = bitpos();
+          stop_bits = bitpos();
           return ZD_FULL;
         }
       }
@@ -763,8 +548,12 @@ struct Inflater {
 
 template <bool D64>
 __global__ void __launch_bounds__(64) zs_decode_kernel(const ZsJobDev *__restrict__ jobs, const ZsHeadDev *__restrict__ heads,
-                                                        const uint32_t *__restrict__ job_ids, ZsDecDev *__restrict__ decs) {
+                                                        const uint32_t *__restrict__ job_ids, ZsDecDev *__restrict__ decs,
+                                                        const uint32_t *__restrict__ run_only) {
   constexpr uint32_t RING = D64 ? 65536u : 32768u;
+  // run_only (optional, indexed by job): decode only flagged jobs -- the exact
+  // serial decoder as the fallback of the speculative chunked path
+  if (run_only && run_only[job_ids[blockIdx.x]] == 0) return;
   __shared__ __attribute__((aligned(16))) uint8_t s_ring[RING];
   __shared__ __attribute__((aligned(16))) uint32_t s_in[IN_RING_WORDS];
   __shared__ uint32_t s_tab[TABLE_ENTRIES];
@@ -805,19 +594,21 @@ __global__ void __launch_bounds__(64) zs_decode_kernel(const ZsJobDev *__restric
   f.whave = 0;
   f.fixed_ready = false;
   f.seek((mis + (uint32_t)hd.start_byte) * 8u);
-  int msg = ZM_NONE;
-  uint32_t ebits = 0;
-  int code = f.run(&msg, &ebits);
+  f.stop_bits = 0;
+  const int packed = f.run();
+  const int code = packed & 0xff;
   f.flush_tail();
   res.code = code;
-  res.msg = msg;
-  res.end_bits = (code == ZD_TRUNC) ? (uint64_t)jb.in_len * 8u : (uint64_t)(ebits - mis * 8u);
+  res.msg = packed >> 8;
+  res.end_bits = (code == ZD_TRUNC) ? (uint64_t)jb.in_len * 8u : (uint64_t)(f.stop_bits - mis * 8u);
   res.total_out = f.pos;
   if (threadIdx.x == 0) decs[j] = res;
 }
 
-template __global__ void zs_decode_kernel<false>(const ZsJobDev *, const ZsHeadDev *, const uint32_t *, ZsDecDev *);
-template __global__ void zs_decode_kernel<true>(const ZsJobDev *, const ZsHeadDev *, const uint32_t *, ZsDecDev *);
+template __global__ void zs_decode_kernel<false>(const ZsJobDev *, const ZsHeadDev *, const uint32_t *, ZsDecDev *,
+                                                 const uint32_t *);
+template __global__ void zs_decode_kernel<true>(const ZsJobDev *, const ZsHeadDev *, const uint32_t *, ZsDecDev *,
+                                                const uint32_t *);
 
 // ---------------------------------------------------------------------------
 // Checks: CRC-32 (gzip) / Adler-32 (zlib) over each job's output, segment
@@ -1024,22 +815,27 @@ __global__ void zs_finalize_kernel(const ZsJobDev *__restrict__ jobs, const ZsHe
 }
 
 // ---------------------------------------------------------------------------
-// launch sequence for one batch (host side, same stream, no host syncs)
+// launch helpers (host side; every launch on `stream`, no host syncs)
 // ---------------------------------------------------------------------------
-// ev[0..1] (optional): HIP events recorded around the decode kernels, on `stream`
-extern "C" int zs_launch_inflate(const ZsJobDev *d_jobs, ZsHeadDev *d_heads, ZsDecDev *d_decs, uint32_t *d_checks,
-                                 ZsResultDev *d_res, const uint32_t *d_ids, uint32_t n_std, uint32_t n_d64,
-                                 uint32_t njobs, hipStream_t stream, hipEvent_t *ev) {
-  if (njobs == 0) return 0;
+extern "C" void zs_launch_header(const ZsJobDev *d_jobs, ZsHeadDev *d_heads, uint32_t njobs, hipStream_t stream) {
   const uint32_t tb = 64;
   hipLaunchKernelGGL(zs_header_kernel, dim3((njobs + tb - 1) / tb), dim3(tb), 0, stream, d_jobs, d_heads, njobs);
-  if (ev) (void)hipEventRecord(ev[0], stream);
-  if (n_std) hipLaunchKernelGGL(zs_decode_kernel<false>, dim3(n_std), dim3(64), 0, stream, d_jobs, d_heads, d_ids, d_decs);
-  if (n_d64)
-    hipLaunchKernelGGL(zs_decode_kernel<true>, dim3(n_d64), dim3(64), 0, stream, d_jobs, d_heads, d_ids + n_std, d_decs);
-  if (ev) (void)hipEventRecord(ev[1], stream);
+}
+
+// serial (wave-per-stream) decode of the jobs listed in d_ids; run_only filters
+extern "C" void zs_launch_decode(int d64, const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, const uint32_t *d_ids,
+                                 uint32_t n, ZsDecDev *d_decs, const uint32_t *run_only, hipStream_t stream) {
+  if (!n) return;
+  if (d64)
+    hipLaunchKernelGGL(zs_decode_kernel<true>, dim3(n), dim3(64), 0, stream, d_jobs, d_heads, d_ids, d_decs, run_only);
+  else
+    hipLaunchKernelGGL(zs_decode_kernel<false>, dim3(n), dim3(64), 0, stream, d_jobs, d_heads, d_ids, d_decs, run_only);
+}
+
+extern "C" void zs_launch_finish(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, const ZsDecDev *d_decs,
+                                 uint32_t *d_checks, ZsResultDev *d_res, uint32_t njobs, hipStream_t stream) {
+  const uint32_t tb = 64;
   hipLaunchKernelGGL(zs_check_kernel, dim3(njobs), dim3(CHECK_THREADS), 0, stream, d_jobs, d_heads, d_decs, d_checks);
   hipLaunchKernelGGL(zs_finalize_kernel, dim3((njobs + tb - 1) / tb), dim3(tb), 0, stream, d_jobs, d_heads, d_decs, d_checks,
                      d_res, njobs);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -23,11 +23,20 @@
 #include "../../include/zstreams_mi355x.h"
 #include "zs_common.h"
 
-extern "C" int zs_launch_inflate(const ZsJobDev *d_jobs, ZsHeadDev *d_heads, ZsDecDev *d_decs, uint32_t *d_checks,
-                                 ZsResultDev *d_res, const uint32_t *d_ids, uint32_t n_std, uint32_t n_d64,
-                                 uint32_t njobs, hipStream_t stream, hipEvent_t *ev);
+extern "C" void zs_launch_header(const ZsJobDev *d_jobs, ZsHeadDev *d_heads, uint32_t njobs, hipStream_t stream);
+extern "C" void zs_launch_decode(int d64, const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, const uint32_t *d_ids,
+                                 uint32_t n, ZsDecDev *d_decs, const uint32_t *run_only, hipStream_t stream);
+extern "C" void zs_launch_finish(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, const ZsDecDev *d_decs,
+                                 uint32_t *d_checks, ZsResultDev *d_res, uint32_t njobs, hipStream_t stream);
+extern "C" void zs_launch_fixed_tables(uint32_t *fixed, hipStream_t st);
+extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, ZsChunkDev *d_chunks, uint32_t nchunks,
+                                  const uint32_t *d_find_ids, uint32_t nfind, const ZsCJobDev *d_cjobs, uint32_t ncjobs,
+                                  uint16_t *d_scratch, uint32_t *d_tables, const uint32_t *d_fixed, uint8_t *d_windows,
+                                  ZsDecDev *d_decs, uint32_t *d_fallback, hipStream_t st, hipEvent_t *ev);
 
 namespace {
+
+constexpr size_t TABLE_ENTRIES_HOST = 1448;  // must match TABLE_ENTRIES (zs_device.h)
 
 const char *const kMsgs[ZM_COUNT] = {
     nullptr,
@@ -82,12 +91,44 @@ struct Workspace {
   uint32_t *h_ids = nullptr;      // pinned
   size_t cap_in = 0, cap_out = 0;
   uint8_t *d_in = nullptr, *d_out = nullptr;
-  // decode-kernel timing (zs_profile): events on the launch stream
+  uint32_t *d_fallback = nullptr;  // per job (cap_jobs)
+  ZsCJobDev *d_cjobs = nullptr, *h_cjobs = nullptr;  // per job (cap_jobs)
+  // chunked path
+  size_t cap_chunks = 0;
+  ZsChunkDev *d_chunks = nullptr, *h_chunks = nullptr;
+  uint32_t *d_find = nullptr, *h_find = nullptr;
+  uint32_t *d_tables = nullptr;  // TABLE_ENTRIES per chunk
+  uint8_t *d_windows = nullptr;  // 32 KiB per chunk
+  size_t cap_scratch = 0;        // u16 entries
+  uint16_t *d_scratch = nullptr;
+  uint32_t *d_fixed = nullptr;
+  // timing (zs_profile): events on the launch stream
   bool prof = false;
-  hipEvent_t ev[2] = {nullptr, nullptr};
-  double prof_ms = 0.0;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  double prof_ms = 0.0, prof_batch_ms = 0.0;
   uint64_t prof_launches = 0;
+  // last batch: chunked jobs, chunks, chunked jobs that fell back, serial jobs
+  uint32_t stats[4] = {0, 0, 0, 0};
 };
+
+// chunked-path tuning (env: ZS_CHUNK_KB, ZS_NO_CHUNK)
+uint32_t chunk_bytes() {
+  static uint32_t v = [] {
+    const char *e = std::getenv("ZS_CHUNK_KB");
+    long kb = e ? std::atol(e) : 32;
+    if (kb < 4) kb = 4;
+    if (kb > 65536) kb = 65536;
+    return (uint32_t)(kb * 1024);
+  }();
+  return v;
+}
+bool chunking_enabled() {
+  static bool v = [] {
+    const char *e = std::getenv("ZS_NO_CHUNK");
+    return !(e && e[0] == '1');
+  }();
+  return v;
+}
 
 std::mutex g_mu;
 Workspace g_ws;
@@ -126,10 +167,33 @@ int ws_reserve_jobs(size_t n) {
   size_t c = std::max<size_t>(n, 2 * g_ws.cap_jobs);
   int r;
   if ((r = grow_dev(&g_ws.d_jobs, c)) || (r = grow_dev(&g_ws.d_heads, c)) || (r = grow_dev(&g_ws.d_decs, c)) ||
-      (r = grow_dev(&g_ws.d_checks, c)) || (r = grow_dev(&g_ws.d_res, c)) || (r = grow_dev(&g_ws.d_ids, c)) ||
-      (r = grow_host(&g_ws.h_jobs, c)) || (r = grow_host(&g_ws.h_res, c)) || (r = grow_host(&g_ws.h_ids, c)))
+      (r = grow_dev(&g_ws.d_checks, c)) || (r = grow_dev(&g_ws.d_res, c)) || (r = grow_dev(&g_ws.d_ids, 3 * c)) ||
+      (r = grow_dev(&g_ws.d_fallback, c)) || (r = grow_dev(&g_ws.d_cjobs, c)) || (r = grow_host(&g_ws.h_cjobs, c)) ||
+      (r = grow_host(&g_ws.h_jobs, c)) || (r = grow_host(&g_ws.h_res, c)) || (r = grow_host(&g_ws.h_ids, 3 * c)))
     return r;
   g_ws.cap_jobs = c;
+  return 0;
+}
+
+int ws_reserve_chunks(size_t n, size_t scratch_entries) {
+  int r;
+  if (n > g_ws.cap_chunks) {
+    size_t c = std::max(n, g_ws.cap_chunks + g_ws.cap_chunks / 2);
+    if ((r = grow_dev(&g_ws.d_chunks, c)) || (r = grow_host(&g_ws.h_chunks, c)) || (r = grow_dev(&g_ws.d_find, c)) ||
+        (r = grow_host(&g_ws.h_find, c)) || (r = grow_dev(&g_ws.d_tables, c * TABLE_ENTRIES_HOST)) ||
+        (r = grow_dev(&g_ws.d_windows, c * 32768)))
+      return r;
+    g_ws.cap_chunks = c;
+  }
+  if (scratch_entries > g_ws.cap_scratch) {
+    size_t c = std::max(scratch_entries, g_ws.cap_scratch + g_ws.cap_scratch / 4);
+    if ((r = grow_dev(&g_ws.d_scratch, c))) return r;
+    g_ws.cap_scratch = c;
+  }
+  if (!g_ws.d_fixed) {
+    if ((r = grow_dev(&g_ws.d_fixed, 544))) return r;
+    zs_launch_fixed_tables(g_ws.d_fixed, g_ws.stream);
+  }
   return 0;
 }
 
@@ -224,26 +288,122 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
       if (jobs[i].in_len) HIP_OK(hipMemcpyAsync(g_ws.d_in + in_off[i], jobs[i].in, jobs[i].in_len, hipMemcpyHostToDevice, st));
     }
   }
-  // std jobs first, then deflate64 jobs (different LDS window)
-  uint32_t n_std = 0, n_d64 = 0;
+  // Route each job: large raw/zlib/gzip streams -> speculative chunked path
+  // (with the serial decoder as exact fallback); small ones and deflate64 ->
+  // the wave-per-stream serial decoder.  Lists in h_ids: [serial std | d64 | chunked].
+  const uint32_t C = chunk_bytes();
+  uint32_t n_std = 0, n_d64 = 0, n_cj = 0;
+  size_t nchunks = 0, scratch_need = 0;
+  std::vector<uint32_t> cj_list;
+  for (uint32_t k = 0; k < nv; k++) {
+    const ZsJobDev &jd = g_ws.h_jobs[k];
+    const double ratio = jd.in_len ? (double)jd.out_cap / (double)jd.in_len : 0.0;
+    const bool chunk = chunking_enabled() && !jd.d64 && jd.in_len >= 4ull * C && ratio <= 64.0;
+    if (chunk) {
+      cj_list.push_back(k);
+      nchunks += (jd.in_len + C - 1) / C;
+    }
+  }
   for (uint32_t k = 0; k < nv; k++)
-    if (!g_ws.h_jobs[k].d64) g_ws.h_ids[n_std++] = k;
+    if (!g_ws.h_jobs[k].d64 && std::find(cj_list.begin(), cj_list.end(), k) == cj_list.end()) g_ws.h_ids[n_std++] = k;
   for (uint32_t k = 0; k < nv; k++)
     if (g_ws.h_jobs[k].d64) g_ws.h_ids[n_std + n_d64++] = k;
+  for (uint32_t k : cj_list) g_ws.h_ids[n_std + n_d64 + n_cj++] = k;
+  uint32_t nfind = 0;
+  if (n_cj) {
+    if ((r = ws_reserve_chunks(nchunks, 0))) return r;
+    size_t ci = 0;
+    for (uint32_t q = 0; q < n_cj; q++) {
+      const uint32_t k = cj_list[q];
+      const ZsJobDev &jd = g_ws.h_jobs[k];
+      const uint32_t nc = (uint32_t)((jd.in_len + C - 1) / C);
+      const double ratio = std::max(1.0, (double)jd.out_cap / (double)jd.in_len);
+      // scratch per chunk: 2.5x the expected output of a nominal chunk plus one
+      // block of slack; a chunk that overflows sends its stream to the fallback
+      const uint32_t cap = (uint32_t)std::min<double>(4.0e9, 2.5 * C * ratio + 65536.0);
+      g_ws.h_cjobs[q] = ZsCJobDev{k, (uint32_t)ci, nc, 0};
+      for (uint32_t o = 0; o < nc; o++, ci++) {
+        ZsChunkDev ch{};
+        ch.job = k;
+        ch.ord = o;
+        ch.first = (uint32_t)(ci - o);
+        ch.nchunks = nc;
+        ch.s_byte = o * C;
+        ch.e_byte = (uint32_t)std::min<uint64_t>((uint64_t)(o + 1) * C, jd.in_len);
+        ch.start_bit = ZS_NONE;
+        ch.scratch = scratch_need;
+        ch.cap = cap;
+        ch.chain_next = ZS_NONE;
+        scratch_need += ((size_t)cap + 64 + 7) & ~size_t(7);
+        g_ws.h_chunks[ci] = ch;
+        if (o) g_ws.h_find[nfind++] = (uint32_t)ci;
+      }
+    }
+    if ((r = ws_reserve_chunks(nchunks, scratch_need))) return r;
+    HIP_OK(hipMemcpyAsync(g_ws.d_chunks, g_ws.h_chunks, nchunks * sizeof(ZsChunkDev), hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemcpyAsync(g_ws.d_find, g_ws.h_find, nfind * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemcpyAsync(g_ws.d_cjobs, g_ws.h_cjobs, n_cj * sizeof(ZsCJobDev), hipMemcpyHostToDevice, st));
+  }
   HIP_OK(hipMemcpyAsync(g_ws.d_jobs, g_ws.h_jobs, nv * sizeof(ZsJobDev), hipMemcpyHostToDevice, st));
   HIP_OK(hipMemcpyAsync(g_ws.d_ids, g_ws.h_ids, nv * sizeof(uint32_t), hipMemcpyHostToDevice, st));
-  if (zs_launch_inflate(g_ws.d_jobs, g_ws.d_heads, g_ws.d_decs, g_ws.d_checks, g_ws.d_res, g_ws.d_ids, n_std, n_d64, nv,
-                        st, g_ws.prof ? g_ws.ev : nullptr)) {
-    set_err(std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
-    return ZS_ENODEV;
+  hipEvent_t *ev = g_ws.prof ? g_ws.ev : nullptr;
+  if (ev) HIP_OK(hipEventRecord(ev[2], st));
+  zs_launch_header(g_ws.d_jobs, g_ws.d_heads, nv, st);
+  if (n_cj)
+    zs_launch_chunked(g_ws.d_jobs, g_ws.d_heads, g_ws.d_chunks, (uint32_t)nchunks, g_ws.d_find, nfind, g_ws.d_cjobs, n_cj,
+                      g_ws.d_scratch, g_ws.d_tables, g_ws.d_fixed, g_ws.d_windows, g_ws.d_decs, g_ws.d_fallback, st, ev);
+  else if (ev) {
+    HIP_OK(hipEventRecord(ev[0], st));
+  }
+  zs_launch_decode(0, g_ws.d_jobs, g_ws.d_heads, g_ws.d_ids, n_std, g_ws.d_decs, nullptr, st);
+  zs_launch_decode(1, g_ws.d_jobs, g_ws.d_heads, g_ws.d_ids + n_std, n_d64, g_ws.d_decs, nullptr, st);
+  if (n_cj) zs_launch_decode(0, g_ws.d_jobs, g_ws.d_heads, g_ws.d_ids + n_std + n_d64, n_cj, g_ws.d_decs, g_ws.d_fallback, st);
+  if (ev && !n_cj) HIP_OK(hipEventRecord(ev[1], st));
+  zs_launch_finish(g_ws.d_jobs, g_ws.d_heads, g_ws.d_decs, g_ws.d_checks, g_ws.d_res, nv, st);
+  if (ev) HIP_OK(hipEventRecord(ev[3], st));
+  {
+    hipError_t le = hipGetLastError();
+    if (le != hipSuccess) {
+      set_err(std::string("kernel launch failed: ") + hipGetErrorString(le));
+      return ZS_ENODEV;
+    }
   }
   HIP_OK(hipMemcpyAsync(g_ws.h_res, g_ws.d_res, nv * sizeof(ZsResultDev), hipMemcpyDeviceToHost, st));
   HIP_OK(hipStreamSynchronize(st));
-  if (g_ws.prof) {
-    float ms = 0.f;
-    HIP_OK(hipEventElapsedTime(&ms, g_ws.ev[0], g_ws.ev[1]));
+  if (ev) {
+    float ms = 0.f, bms = 0.f;
+    HIP_OK(hipEventElapsedTime(&ms, ev[0], ev[1]));
+    HIP_OK(hipEventElapsedTime(&bms, ev[2], ev[3]));
     g_ws.prof_ms += ms;
+    g_ws.prof_batch_ms += bms;
     g_ws.prof_launches++;
+  }
+  g_ws.stats[0] = n_cj;
+  g_ws.stats[1] = (uint32_t)nchunks;
+  g_ws.stats[2] = 0;
+  g_ws.stats[3] = n_std + n_d64;
+  if (n_cj) {
+    std::vector<uint32_t> fb(nv);
+    HIP_OK(hipMemcpy(fb.data(), g_ws.d_fallback, nv * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    for (uint32_t k : cj_list) g_ws.stats[2] += fb[k];
+  }
+  if (std::getenv("ZS_DEBUG_CHUNKS") && n_cj) {
+    std::vector<uint32_t> fb(nv);
+    HIP_OK(hipMemcpy(fb.data(), g_ws.d_fallback, nv * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(g_ws.h_chunks, g_ws.d_chunks, nchunks * sizeof(ZsChunkDev), hipMemcpyDeviceToHost));
+    size_t found = 0, inch = 0;
+    for (size_t i = 0; i < nchunks; i++) {
+      found += g_ws.h_chunks[i].start_bit != ZS_NONE;
+      inch += g_ws.h_chunks[i].in_chain;
+    }
+    uint32_t nfb = 0;
+    for (uint32_t k : cj_list) nfb += fb[k];
+    std::fprintf(stderr, "[zs] chunked jobs %u chunks %zu found %zu in_chain %zu fallback %u\n", n_cj, nchunks, found, inch, nfb);
+    for (size_t i = 0; i < nchunks && i < 8; i++) {
+      const ZsChunkDev &c = g_ws.h_chunks[i];
+      std::fprintf(stderr, "  chunk %zu ord %u start %u end %u code %d n_out %u chain %u\n", i, c.ord, c.start_bit, c.end_bit,
+                   c.code, c.n_out, c.in_chain);
+    }
   }
   for (uint32_t i = 0; i < n; i++) {
     if (slot[i] == UINT32_MAX) continue;
@@ -403,26 +563,33 @@ int zs_set_stream(void *s) {
   return 0;
 }
 
-// Decode-kernel timing with HIP events on the launch stream: enable (1) /
-// disable (0); zs_profile_read returns the accumulated milliseconds and the
-// number of timed batches since the last enable.
+// Timing with HIP events on the launch stream: enable (1) / disable (0).
+// zs_profile_read returns the accumulated milliseconds of the dominant decode
+// kernel (the lane decoder when any job took the chunked path, else the serial
+// decoder), of whole batches (header .. finalize), and the number of batches.
 int zs_profile(int enable) {
   std::lock_guard<std::mutex> lk(g_mu);
   int r = ws_init();
   if (r) return r;
-  if (!g_ws.ev[0]) {
-    HIP_OK(hipEventCreate(&g_ws.ev[0]));
-    HIP_OK(hipEventCreate(&g_ws.ev[1]));
-  }
+  if (!g_ws.ev[0])
+    for (int i = 0; i < 4; i++) HIP_OK(hipEventCreate(&g_ws.ev[i]));
   g_ws.prof = enable != 0;
   g_ws.prof_ms = 0.0;
+  g_ws.prof_batch_ms = 0.0;
   g_ws.prof_launches = 0;
   return 0;
 }
-int zs_profile_read(double *ms, uint64_t *launches) {
+int zs_profile_read(double *decode_ms, double *batch_ms, uint64_t *launches) {
   std::lock_guard<std::mutex> lk(g_mu);
-  *ms = g_ws.prof_ms;
+  *decode_ms = g_ws.prof_ms;
+  *batch_ms = g_ws.prof_batch_ms;
   *launches = g_ws.prof_launches;
+  return 0;
+}
+
+int zs_last_stats(uint32_t out[4]) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  for (int i = 0; i < 4; i++) out[i] = g_ws.stats[i];
   return 0;
 }
 

@@ -88,6 +88,47 @@ struct ZsDecDev {
   uint64_t total_out;
 };
 
+// ---------------------------------------------------------------------------
+// Speculative chunking of large raw/zlib/gzip streams (one lane per chunk).
+// A stream's deflate data is cut into fixed-size compressed chunks; each chunk
+// >= 1 searches its range for a dynamic-block header (zs_find_kernel), every
+// chunk with a start decodes up to the first block end at or past the next
+// chunk's start, emitting u16 entries where values >= 256 name bytes of the
+// unknown 32 KiB history before the chunk (markers).  zs_link_kernel verifies
+// that the chunks tile the stream exactly (chunk j ends where chunk j+1
+// starts), resolves the history windows in order, and zs_emit_kernel writes
+// the final bytes.  Any inconsistency sends the whole stream to the exact
+// serial decoder, so results never depend on the speculation.
+// ---------------------------------------------------------------------------
+#define ZS_NONE 0xffffffffu
+#define ZD_STOP 6  // chunk decode reached its stop bit at a block boundary
+
+struct ZsChunkDev {
+  uint32_t job;        // job index
+  uint32_t ord;        // ordinal of the chunk within its job
+  uint32_t first;      // index of the job's chunk 0 in the chunk array
+  uint32_t nchunks;    // chunks of this job
+  uint32_t s_byte;     // block-search range [s_byte, e_byte) of the job input
+  uint32_t e_byte;
+  uint32_t start_bit;  // decode start (bits from the 4-byte-aligned input base), ZS_NONE if none
+  uint32_t end_bit;    // where decoding stopped
+  int32_t code;        // ZD_* | (ZsMsg << 8)
+  uint32_t n_out;      // u16 entries produced
+  uint64_t scratch;    // entry offset of this chunk's u16 scratch region
+  uint32_t cap;        // scratch capacity (entries)
+  uint32_t chain_next; // next chunk in the verified chain (ZS_NONE at the end)
+  uint64_t out_off;    // output byte offset (verified chain members)
+  uint32_t in_chain;   // 1 = member of the verified chain of a non-fallback job
+  uint32_t pad;
+};
+
+struct ZsCJobDev {
+  uint32_t job;        // job index
+  uint32_t first;      // first chunk
+  uint32_t nchunks;
+  uint32_t pad;
+};
+
 // Final per-job result (device -> host), zlib z_stream fields after the call.
 struct ZsResultDev {
   int32_t ret;

@@ -42,7 +42,9 @@ _SIGS = {
     "inflate9_end": (ctypes.c_int, [_U]), "inflate9_last_consumed": (ctypes.c_uint, [_U]),
     "zs_set_stream": (ctypes.c_int, [ctypes.c_void_p]),
     "zs_profile": (ctypes.c_int, [ctypes.c_int]),
-    "zs_profile_read": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)]),
+    "zs_profile_read": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                       ctypes.POINTER(ctypes.c_uint64)]),
+    "zs_last_stats": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint32)]),
     "zs_synchronize": (ctypes.c_int, []),
     "zs_version": (ctypes.c_char_p, []), "zs_last_error": (ctypes.c_char_p, []),
 }
@@ -140,10 +142,19 @@ def profile(enable):
 
 
 def profile_read():
+    """(decode-kernel ms, whole-batch ms, batches) accumulated since profile(True)."""
     ms = ctypes.c_double()
+    bms = ctypes.c_double()
     n = ctypes.c_uint64()
-    _check(lib().zs_profile_read(ctypes.byref(ms), ctypes.byref(n)))
-    return ms.value, n.value
+    _check(lib().zs_profile_read(ctypes.byref(ms), ctypes.byref(bms), ctypes.byref(n)))
+    return ms.value, bms.value, n.value
+
+
+def last_stats():
+    """Last batch: chunked jobs, chunks, chunked jobs that fell back, serial jobs."""
+    a = (ctypes.c_uint32 * 4)()
+    _check(lib().zs_last_stats(a))
+    return {"chunked_jobs": a[0], "chunks": a[1], "fallback_jobs": a[2], "serial_jobs": a[3]}
 
 
 def set_stream(hip_stream_handle):
