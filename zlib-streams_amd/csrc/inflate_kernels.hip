@@ -755,61 +755,45 @@ __global__ void zs_finalize_kernel(const ZsJobDev *__restrict__ jobs, const ZsHe
   r.adler = raw ? 0u : checks[j];
   if (!raw && hd.is_gzip == 0 && dc.total_out == 0) r.adler = 1;
   if (!raw && hd.is_gzip == 1 && dc.total_out == 0) r.adler = 0;
-  switch (dc.code) {
-    case ZD_END: {
-      uint64_t t = (dc.end_bits + 7) >> 3;
-      if (raw) {
-        r.ret = ZS_STREAM_END;
-        r.total_in = t;
-        break;
-      }
-      if (t + 4 > jb.in_len) {
-        r.ret = ZS_BUF_ERROR;
-        r.total_in = jb.in_len;
-        break;
-      }
+  // (an if-chain, not a switch: hipcc 7.2 dropped the msg copy of the default
+  // arm of the equivalent switch for codes > ZD_FULL)
+  const int code = dc.code;
+  const uint64_t t = (dc.end_bits + 7) >> 3;  // bytes pulled (slow path) / not returned (fast path)
+  r.msg = (code == ZD_END || code == ZD_TRUNC || code == ZD_FULL) ? (int32_t)ZM_NONE : dc.msg;
+  r.ret = ZS_DATA_ERROR;
+  r.total_in = t;
+  if (code == ZD_TRUNC) {
+    r.ret = ZS_BUF_ERROR;
+    r.total_in = jb.in_len;
+  } else if (code == ZD_FULL) {
+    r.ret = ZS_BUF_ERROR;
+  } else if (code == ZD_END) {
+    if (raw) {
+      r.ret = ZS_STREAM_END;
+    } else if (t + 4 > jb.in_len) {  // CHECK: NEEDBITS(32) runs out of input
+      r.ret = ZS_BUF_ERROR;
+      r.total_in = jb.in_len;
+    } else {
       const uint8_t *q = jb.in + t;
       uint32_t tr = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
       if (hd.is_gzip == 0) tr = (tr >> 24) | ((tr >> 8) & 0xff00u) | ((tr & 0xff00u) << 8) | (tr << 24);
+      r.total_in = t + 4;
       if (tr != r.adler) {
-        r.ret = ZS_DATA_ERROR;
         r.msg = ZM_DATA_CHECK;
-        r.total_in = t + 4;
-        break;
-      }
-      if (hd.is_gzip == 1) {
-        if (t + 8 > jb.in_len) {
-          r.ret = ZS_BUF_ERROR;
-          r.total_in = jb.in_len;
-          break;
-        }
-        uint32_t isz = (uint32_t)q[4] | ((uint32_t)q[5] << 8) | ((uint32_t)q[6] << 16) | ((uint32_t)q[7] << 24);
-        if (isz != (uint32_t)(dc.total_out & 0xffffffffu)) {
-          r.ret = ZS_DATA_ERROR;
-          r.msg = ZM_LENGTH_CHECK;
-          r.total_in = t + 8;
-          break;
-        }
-        r.total_in = t + 8;
+      } else if (hd.is_gzip != 1) {
+        r.ret = ZS_STREAM_END;
+      } else if (t + 8 > jb.in_len) {  // LENGTH: NEEDBITS(32) runs out of input
+        r.ret = ZS_BUF_ERROR;
+        r.total_in = jb.in_len;
       } else {
-        r.total_in = t + 4;
+        const uint32_t isz = (uint32_t)q[4] | ((uint32_t)q[5] << 8) | ((uint32_t)q[6] << 16) | ((uint32_t)q[7] << 24);
+        r.total_in = t + 8;
+        if (isz != (uint32_t)(dc.total_out & 0xffffffffu))
+          r.msg = ZM_LENGTH_CHECK;
+        else
+          r.ret = ZS_STREAM_END;
       }
-      r.ret = ZS_STREAM_END;
-      break;
     }
-    case ZD_TRUNC:
-      r.ret = ZS_BUF_ERROR;
-      r.total_in = jb.in_len;
-      break;
-    case ZD_FULL:
-      r.ret = ZS_BUF_ERROR;
-      r.total_in = (dc.end_bits + 7) >> 3;
-      break;
-    default:
-      r.ret = ZS_DATA_ERROR;
-      r.msg = dc.msg;
-      r.total_in = (dc.end_bits + 7) >> 3;
-      break;
   }
   res[j] = r;
 }

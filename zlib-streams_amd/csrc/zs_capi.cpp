@@ -465,7 +465,9 @@ int stream_call(StreamState *s, const uint8_t *in, unsigned in_len, uint8_t *out
   if (!s->done) {
     size_t before = s->acc.size();
     s->acc.insert(s->acc.end(), in, in + in_len);
-    bool attempt = flush == Z_FINISH || s->acc.size() >= 2 * std::max<size_t>(s->last_try, 32768);
+    // decode at Z_FINISH, on the first call with data, and whenever the
+    // accumulated input has doubled since the last (truncated) attempt
+    bool attempt = flush == Z_FINISH || (!s->acc.empty() && s->acc.size() >= 2 * s->last_try);
     if (!attempt) {
       *consumed = in_len;
       return in_len ? Z_OK : Z_BUF_ERROR;
@@ -496,7 +498,9 @@ int stream_call(StreamState *s, const uint8_t *in, unsigned in_len, uint8_t *out
   s->served += n;
   s->total_out += n;
   *produced = (unsigned)n;
-  if (s->served < s->out.size()) return flush == Z_FINISH ? Z_BUF_ERROR : Z_OK;
+  // more decoded output pending: Z_OK (also under Z_FINISH, so the reference's
+  // flush() drain loop, src/wasm/api/zlib-streams.js:119-136, keeps pulling)
+  if (s->served < s->out.size()) return Z_OK;
   return s->final_ret;
 }
 
