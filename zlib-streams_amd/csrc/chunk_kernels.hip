@@ -31,17 +31,6 @@
 #define STAGE_WORDS 256  // 1 KiB of staged header bits per cooperative step
 
 // ---------------------------------------------------------------------------
-// masked 32-bit input word (bytes at or past end_byte read as zero)
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t in_word(const uint32_t *w, uint32_t wi, uint32_t end_byte) {
-  uint32_t b = wi * 4u;
-  if (b + 4u <= end_byte) return w[wi];
-  if (b >= end_byte) return 0u;
-  uint32_t keep = end_byte - b;  // 1..3
-  return w[wi] & ((1u << (8u * keep)) - 1u);
-}
-
-// ---------------------------------------------------------------------------
 // Full dynamic-header validation for one candidate (per lane, rare path).
 // Mirrors the acceptance rules of src/inflate.c:905-1033 + src/inftrees.c
 // (complete code-length code, repeat rules, end-of-block present, literal and
@@ -243,429 +232,16 @@ __global__ void __launch_bounds__(64) zs_fixed_tables_kernel(uint32_t *__restric
 }
 
 // ---------------------------------------------------------------------------
-// Lane decoder
-// ---------------------------------------------------------------------------
-enum { LM_SYM = 0, LM_BLOCK = 1, LM_DONE = 2 };
-
-struct LaneState {
-  const uint32_t *w;   // 4-byte aligned input base
-  uint32_t end_byte, limit;
-  uint32_t wi, nw, nbits;
-  uint64_t hold;
-  uint16_t *out;
-  uint32_t pos, cap;
-  const uint32_t *lt, *dt;
-  uint32_t lmask, dmask;
-  uint32_t stop, bit, whave;
-  int mode, code, last;
-};
-
-__device__ __forceinline__ void lane_prime(LaneState &s, uint32_t bit) {
-  s.wi = bit >> 5;
-  uint32_t w0 = in_word(s.w, s.wi, s.end_byte);
-  s.nw = in_word(s.w, s.wi + 1, s.end_byte);
-  s.hold = (uint64_t)w0 >> (bit & 31);
-  s.nbits = 32 - (bit & 31);
-  s.wi += 1;
-}
-__device__ __forceinline__ void lane_refill(LaneState &s) {
-  if (s.nbits < 32) {
-    s.hold |= (uint64_t)s.nw << s.nbits;
-    s.nbits += 32;
-    s.wi++;
-    s.nw = in_word(s.w, s.wi, s.end_byte);
-  }
-}
-__device__ __forceinline__ uint32_t lane_pos(const LaneState &s) { return s.wi * 32u - s.nbits; }
-
-// one symbol; returns true when the lane left symbol mode
-__device__ __forceinline__ bool lane_step(LaneState &s) {
-  lane_refill(s);
-  uint32_t e = s.lt[(uint32_t)s.hold & s.lmask];
-  uint32_t op = e_op(e);
-  uint32_t used = e_bits(e);
-  if (op != 0 && (op & 0xf0u) == 0) {
-    e = s.lt[e_val(e) + ((uint32_t)(s.hold >> used) & ((1u << op) - 1u))];
-    used += e_bits(e);
-    op = e_op(e);
-  }
-  if (lane_pos(s) + used > s.limit) {
-    s.code = ZD_TRUNC;
-    s.mode = LM_DONE;
-    return true;
-  }
-  s.hold >>= used;
-  s.nbits -= used;
-  if (op == 0) {
-    if (s.pos >= s.cap) {
-      s.code = ZD_FULL;
-      s.mode = LM_DONE;
-      return true;
-    }
-    s.out[s.pos++] = (uint16_t)e_val(e);
-    return false;
-  }
-  if (op & 32) {  // end of block
-    s.bit = lane_pos(s);
-    s.mode = LM_BLOCK;
-    return true;
-  }
-  if (op & 64) {
-    s.code = ZD_ERROR | (ZM_LITLEN_CODE << 8);
-    s.mode = LM_DONE;
-    return true;
-  }
-  uint32_t len = e_val(e);
-  const uint32_t xb = op & 15u;
-  len += (uint32_t)s.hold & ((1u << xb) - 1u);
-  s.hold >>= xb;
-  s.nbits -= xb;
-  lane_refill(s);
-  uint32_t d = s.dt[(uint32_t)s.hold & s.dmask];
-  uint32_t dop = e_op(d);
-  uint32_t dused = e_bits(d);
-  if ((dop & 0xf0u) == 0) {
-    d = s.dt[e_val(d) + ((uint32_t)(s.hold >> dused) & ((1u << dop) - 1u))];
-    dused += e_bits(d);
-    dop = e_op(d);
-  }
-  const uint32_t dx = dop & 15u;
-  if (lane_pos(s) + dused + dx > s.limit) {
-    s.code = ZD_TRUNC;
-    s.mode = LM_DONE;
-    return true;
-  }
-  s.hold >>= dused;
-  s.nbits -= dused;
-  if (dop & 64) {
-    s.code = ZD_ERROR | (ZM_DIST_CODE << 8);
-    s.mode = LM_DONE;
-    return true;
-  }
-  const uint32_t dist = e_val(d) + ((uint32_t)s.hold & ((1u << dx) - 1u));
-  s.hold >>= dx;
-  s.nbits -= dx;
-  if (s.pos + len > s.cap) {
-    s.code = ZD_FULL;
-    s.mode = LM_DONE;
-    return true;
-  }
-  const int q = (int)s.pos - (int)dist;
-  if (q < -(int)s.whave) {
-    s.code = ZD_ERROR | (ZM_TOO_FAR << 8);
-    s.mode = LM_DONE;
-    return true;
-  }
-  // copy: entry k comes from q + (k mod dist) (always before pos, so the group
-  // loads never depend on this match's own stores); q < 0 -> history marker
-  uint16_t *o = s.out + s.pos;
-  uint32_t m = 0;
-  for (uint32_t k = 0; k < len; k += 8) {
-    uint16_t v[8];
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      const int idx = q + (int)m;
-      v[i] = (idx < 0) ? (uint16_t)(MARK_BASE + HIST + idx) : ((k + i < len) ? s.out[idx] : (uint16_t)0);
-      m = (m + 1 == dist) ? 0u : m + 1;
-    }
-#pragma unroll
-    for (int i = 0; i < 8; i++)
-      if (k + i < len) o[k + i] = v[i];
-  }
-  s.pos += len;
-  return false;
-}
-
-// Wave-uniform bit reader over the LDS-staged header bits.
-struct StageBits {
-  const uint32_t *st;  // LDS words
-  uint32_t base;       // bit index of st[0] in the input
-  __device__ __forceinline__ uint32_t peek(uint32_t bit, uint32_t n) const {
-    uint32_t r = bit - base;
-    uint64_t v = (uint64_t)st[r >> 5] | ((uint64_t)st[(r >> 5) + 1] << 32);
-    return (uint32_t)(v >> (r & 31)) & ((n >= 32) ? 0xffffffffu : ((1u << n) - 1u));
-  }
-};
-
-struct CoopLDS {
-  uint32_t stage[STAGE_WORDS + 4];
-  uint32_t tab[TABLE_ENTRIES];
-  uint16_t lens[320];
-  uint16_t sorted[320];
-  uint32_t scr[32];
-};
-
-// Stage 1 KiB of input starting at the 16-byte boundary at or below `bit`.
-__device__ void stage_bits(CoopLDS &L, const uint32_t *w, uint32_t end_byte, uint32_t bit, StageBits &sb) {
-  const uint32_t lane = lane_id();
-  const uint32_t b16 = (bit >> 7) << 4;  // byte offset, multiple of 16
-  const uint32_t wi = (b16 >> 2) + lane * 4;
-#pragma unroll
-  for (int k = 0; k < 4; k++) L.stage[lane * 4 + k] = in_word(w, wi + k, end_byte);
-  if (lane < 4) L.stage[STAGE_WORDS + lane] = 0;
-  __builtin_amdgcn_wave_barrier();
-  sb.st = L.stage;
-  sb.base = b16 * 8u;
-}
-
-__device__ __forceinline__ uintptr_t readlane_ptr(const void *p, uint32_t ln) {
-  const uint64_t v = reinterpret_cast<uintptr_t>(p);
-  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, ln);
-  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), ln);
-  return (uintptr_t)(((uint64_t)hi << 32) | lo);
-}
-
-// Cooperative block-boundary processing for lane `ln` (all lanes call it with
-// the same ln).  Handles end/stop checks, stored blocks, fixed and dynamic
-// headers; installs the lane's tables.  Mirrors src/inflate.c:834-1033.
-__device__ void coop_block(LaneState &s, uint32_t ln, CoopLDS &L, uint32_t *lane_tab, const uint32_t *fixed) {
-  const uint32_t lane = lane_id();
-  const uint32_t *w = reinterpret_cast<const uint32_t *>(readlane_ptr(s.w, ln));
-  uint16_t *out = reinterpret_cast<uint16_t *>(readlane_ptr(s.out, ln));
-  uint32_t *tabg = reinterpret_cast<uint32_t *>(readlane_ptr(lane_tab, ln));
-  const uint32_t end_byte = __builtin_amdgcn_readlane(s.end_byte, ln);
-  const uint32_t limit = end_byte * 8u;
-  const uint32_t stop = __builtin_amdgcn_readlane(s.stop, ln);
-  const uint32_t cap = __builtin_amdgcn_readlane(s.cap, ln);
-  uint32_t bit = __builtin_amdgcn_readlane(s.bit, ln);
-  uint32_t pos = __builtin_amdgcn_readlane(s.pos, ln);
-  int last = __builtin_amdgcn_readlane(s.last, ln);
-  int mode = LM_DONE, code = 0;
-  const uint32_t *lt = nullptr, *dt = nullptr;
-  uint32_t lbits = 0, dbits = 0;
-  for (;;) {
-    if (last) {
-      code = ZD_END;
-      break;
-    }
-    if (bit >= stop) {
-      code = ZD_STOP;
-      break;
-    }
-    if (bit + 3 > limit) {
-      code = ZD_TRUNC;
-      break;
-    }
-    StageBits sb;
-    stage_bits(L, w, end_byte, bit, sb);
-    const uint32_t hdr = sb.peek(bit, 3);
-    last = hdr & 1;
-    const uint32_t type = hdr >> 1;
-    bit += 3;
-    if (type == 0) {  // stored (src/inflate.c:870-904)
-      bit = (bit + 7) & ~7u;
-      if (bit + 32 > limit) {
-        code = ZD_TRUNC;
-        break;
-      }
-      stage_bits(L, w, end_byte, bit, sb);
-      const uint32_t v = sb.peek(bit, 32);
-      if ((v & 0xffffu) != ((v >> 16) ^ 0xffffu)) {
-        code = ZD_ERROR | (ZM_STORED_LEN << 8);
-        break;
-      }
-      bit += 32;
-      const uint32_t n = v & 0xffffu;
-      if (bit / 8 + n > end_byte) {
-        code = ZD_TRUNC;
-        break;
-      }
-      if (pos + n > cap) {
-        code = ZD_FULL;
-        break;
-      }
-      const uint8_t *src = reinterpret_cast<const uint8_t *>(w) + bit / 8;
-      for (uint32_t k = lane; k < n; k += WAVE) out[pos + k] = src[k];
-      pos += n;
-      bit += n * 8;
-      continue;
-    }
-    if (type == 1) {
-      lt = fixed;
-      dt = fixed + 512;
-      lbits = 9;
-      dbits = 5;
-      mode = LM_SYM;
-      break;
-    }
-    if (type == 3) {
-      code = ZD_ERROR | (ZM_BLOCK_TYPE << 8);
-      break;
-    }
-    // dynamic header
-    if (bit + 14 > limit) {
-      code = ZD_TRUNC;
-      break;
-    }
-    const uint32_t h = sb.peek(bit, 14);
-    const uint32_t nlen = (h & 31) + 257, ndist = ((h >> 5) & 31) + 1, ncode = ((h >> 10) & 15) + 4;
-    bit += 14;
-    if (nlen > 286 || ndist > 30) {
-      code = ZD_ERROR | (ZM_TOO_MANY << 8);
-      break;
-    }
-    if (bit + 3 * ncode > limit) {
-      code = ZD_TRUNC;
-      break;
-    }
-    if (lane < 19) L.lens[c_clorder[lane]] = lane < ncode ? (uint16_t)sb.peek(bit + 3 * lane, 3) : (uint16_t)0;
-    bit += 3 * ncode;
-    __builtin_amdgcn_wave_barrier();
-    uint32_t cbits = 7;
-    if (build_table(T_CODES, L.lens, 19, L.tab, &cbits, L.sorted, L.scr, 0)) {
-      code = ZD_ERROR | (ZM_CODE_LENGTHS << 8);
-      break;
-    }
-    const uint32_t total = nlen + ndist;
-    const uint32_t cmask = (1u << cbits) - 1u;
-    uint32_t have = 0;
-    bool bad = false;
-    while (have < total) {
-      if (bit - sb.base > (STAGE_WORDS - 2) * 32u - 64u) stage_bits(L, w, end_byte, bit, sb);
-      const uint32_t x = sb.peek(bit, 14);
-      const uint32_t e = L.tab[x & cmask];
-      const uint32_t eb = e_bits(e), ev = e_val(e);
-      if (ev < 16) {
-        if (bit + eb > limit) { bad = true; code = ZD_TRUNC; break; }
-        bit += eb;
-        if (lane == 0) L.lens[have] = (uint16_t)ev;
-        have++;
-        continue;
-      }
-      const uint32_t xb = ev == 16 ? 2u : (ev == 17 ? 3u : 7u);
-      if (bit + eb + xb > limit) { bad = true; code = ZD_TRUNC; break; }
-      if (ev == 16 && have == 0) { bad = true; code = ZD_ERROR | (ZM_REPEAT << 8); break; }
-      const uint32_t rep = (ev == 18 ? 11u : 3u) + ((x >> eb) & ((1u << xb) - 1u));
-      bit += eb + xb;
-      if (have + rep > total) { bad = true; code = ZD_ERROR | (ZM_REPEAT << 8); break; }
-      __builtin_amdgcn_wave_barrier();
-      const uint32_t fillv = ev == 16 ? uni(L.lens[have - 1]) : 0u;
-      for (uint32_t k = lane; k < rep; k += WAVE) L.lens[have + k] = (uint16_t)fillv;
-      __builtin_amdgcn_wave_barrier();
-      have += rep;
-    }
-    if (bad) break;
-    __builtin_amdgcn_wave_barrier();
-    if (uni(L.lens[256]) == 0) {
-      code = ZD_ERROR | (ZM_MISSING_EOB << 8);
-      break;
-    }
-    lbits = 9;
-    if (build_table(T_LENS, L.lens, nlen, L.tab, &lbits, L.sorted, L.scr, 0)) {
-      code = ZD_ERROR | (ZM_LITLEN_SET << 8);
-      break;
-    }
-    dbits = 6;
-    if (build_table(T_DISTS, L.lens + nlen, ndist, L.tab + DIST_TABLE_OFF, &dbits, L.sorted, L.scr, 0)) {
-      code = ZD_ERROR | (ZM_DIST_SET << 8);
-      break;
-    }
-    __builtin_amdgcn_wave_barrier();
-    for (uint32_t i = lane; i < TABLE_ENTRIES; i += WAVE) tabg[i] = L.tab[i];
-    lt = tabg;
-    dt = tabg + DIST_TABLE_OFF;
-    mode = LM_SYM;
-    break;
-  }
-  if (lane == ln) {
-    s.pos = pos;
-    s.last = last;
-    s.bit = bit;
-    s.mode = mode;
-    if (mode == LM_SYM) {
-      s.lt = lt;
-      s.dt = dt;
-      s.lmask = (1u << lbits) - 1u;
-      s.dmask = (1u << dbits) - 1u;
-      lane_prime(s, bit);
-    } else {
-      s.code = code;
-    }
-  }
-}
-
-__global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict__ jobs, const ZsHeadDev *__restrict__ heads,
-                                                      ZsChunkDev *__restrict__ chunks, uint32_t nchunks,
-                                                      uint16_t *__restrict__ scratch, uint32_t *__restrict__ tables,
-                                                      const uint32_t *__restrict__ fixed) {
-  __shared__ CoopLDS L;
-  const uint32_t lane = threadIdx.x;
-  const uint32_t c = blockIdx.x * WAVE + lane;
-  LaneState s;
-  s.mode = LM_DONE;
-  s.code = ZD_SKIP;
-  s.pos = 0;
-  s.last = 0;
-  s.bit = 0;
-  s.stop = ZS_NONE;
-  s.w = nullptr;
-  s.out = nullptr;
-  s.end_byte = 0;
-  s.limit = 0;
-  s.cap = 0;
-  s.whave = 0;
-  s.lt = s.dt = fixed;
-  s.lmask = s.dmask = 0;
-  s.wi = s.nw = s.nbits = 0;
-  s.hold = 0;
-  uint32_t *lane_tab = tables + (size_t)min(c, nchunks - 1) * TABLE_ENTRIES;
-  if (c < nchunks) {
-    const ZsChunkDev ch = chunks[c];
-    const ZsHeadDev hd = heads[ch.job];
-    const ZsJobDev jb = jobs[ch.job];
-    const uintptr_t ip = reinterpret_cast<uintptr_t>(jb.in);
-    const uint32_t mis = (uint32_t)(ip & 3u);
-    uint32_t start = ch.ord == 0 ? (mis + (uint32_t)hd.start_byte) * 8u : ch.start_bit;
-    if (hd.code == ZD_END && start != ZS_NONE) {
-      s.w = reinterpret_cast<const uint32_t *>(ip - mis);
-      s.end_byte = mis + (uint32_t)jb.in_len;
-      s.limit = s.end_byte * 8u;
-      s.out = scratch + ch.scratch;
-      s.cap = ch.cap;
-      s.whave = ch.ord == 0 ? 0u : HIST;
-      s.bit = start;
-      s.mode = LM_BLOCK;
-      s.code = 0;
-      for (uint32_t k = ch.ord + 1; k < ch.nchunks; k++) {
-        uint32_t sb = chunks[ch.first + k].start_bit;
-        if (sb != ZS_NONE) {
-          s.stop = sb;
-          break;
-        }
-      }
-    }
-  }
-  for (;;) {
-    uint64_t need = __ballot(s.mode == LM_BLOCK);
-    while (need) {
-      const uint32_t ln = (uint32_t)__builtin_ctzll(need);
-      need &= need - 1;
-      coop_block(s, ln, L, lane_tab, fixed);
-    }
-    if (__ballot(s.mode == LM_SYM) == 0) break;
-    if (s.mode == LM_SYM) {
-      for (int it = 0; it < 64; it++)
-        if (lane_step(s)) break;
-    }
-  }
-  if (c < nchunks) {
-    ZsChunkDev *ch = &chunks[c];
-    ch->code = s.code;
-    ch->end_bit = (s.code == ZD_END || s.code == ZD_STOP) ? s.bit : 0u;
-    ch->n_out = s.pos;
-  }
-}
-
-// ---------------------------------------------------------------------------
 // Link: verify the chain, offsets, history windows (one workgroup per stream)
 // ---------------------------------------------------------------------------
-#define LINK_THREADS 256
+#define LINK_THREADS 1024
+#define LINK_PER (HIST / LINK_THREADS)  // window entries per thread and chain step
 __global__ void __launch_bounds__(LINK_THREADS) zs_link_kernel(const ZsJobDev *__restrict__ jobs, const ZsHeadDev *__restrict__ heads,
                                                                ZsChunkDev *__restrict__ chunks, const ZsCJobDev *__restrict__ cjobs,
                                                                const uint16_t *__restrict__ scratch, uint8_t *__restrict__ windows,
                                                                ZsDecDev *__restrict__ decs, uint32_t *__restrict__ fallback) {
   __shared__ uint8_t s_win[2][HIST];
-  __shared__ uint32_t s_ok, s_cur, s_next;
+  __shared__ uint32_t s_ok, s_cur;
   __shared__ uint32_t s_end_bit;
   __shared__ uint64_t s_total;
   const uint32_t t = threadIdx.x;
@@ -743,20 +319,33 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_link_kernel(const ZsJobDev *_
     const uint32_t n = ch.n_out;
     const uint16_t *e = scratch + ch.scratch;
     const uint32_t keep = n < HIST ? HIST - n : 0u;  // old history bytes still inside the new window
-    for (uint32_t i = t; i < keep; i += LINK_THREADS) W2[i] = W[i + n];
-    const uint32_t lowest = HIST - wv;  // first valid history index
-    for (uint32_t i = keep + t; i < HIST; i += LINK_THREADS) {
-      const uint32_t v = e[n - HIST + i];
+    const uint32_t lowest = HIST - wv;                // first valid history index
+    // window index i = k * LINK_THREADS + t; all LINK_PER loads are issued
+    // before any is consumed (one memory latency per chain step)
+    uint16_t v[LINK_PER];
+#pragma unroll
+    for (int k = 0; k < LINK_PER; k++) {
+      const uint32_t i = (uint32_t)k * LINK_THREADS + t;
+      v[k] = (i >= keep) ? e[n - HIST + i] : (uint16_t)0;
+    }
+    bool bad = false;
+#pragma unroll
+    for (int k = 0; k < LINK_PER; k++) {
+      const uint32_t i = (uint32_t)k * LINK_THREADS + t;
       uint32_t b;
-      if (v < MARK_BASE) {
-        b = v;
+      if (i < keep) {
+        b = W[i + n];
+      } else if (v[k] < MARK_BASE) {
+        b = v[k];
       } else {
-        const uint32_t wx = v - MARK_BASE;
-        if (wx < lowest) s_ok = 0;  // reaches before the stream start
+        const uint32_t wx = v[k] - MARK_BASE;
+        bad |= wx < lowest;  // reaches before the stream start
         b = W[wx & (HIST - 1)];
       }
       W2[i] = (uint8_t)b;
     }
+    if (bad) s_ok = 0;
+    if (t == 0) chunks[c].in_chain = 1;
     wv = min(HIST, wv + n);
     cur ^= 1;
     __syncthreads();
@@ -775,12 +364,6 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_link_kernel(const ZsJobDev *_
       d.end_bits = s_end_bit - mis * 8u;
       d.total_out = s_total;
       decs[cj.job] = d;
-      // mark chain members for the emit pass
-      uint32_t k = cj.first;
-      while (k != ZS_NONE) {
-        chunks[k].in_chain = 1;
-        k = chunks[k].chain_next;
-      }
     }
   }
 }
@@ -837,14 +420,16 @@ extern "C" void zs_launch_fixed_tables(uint32_t *fixed, hipStream_t st) {
   hipLaunchKernelGGL(zs_fixed_tables_kernel, dim3(1), dim3(64), 0, st, fixed);
 }
 
+extern "C" void zs_launch_lane(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, ZsChunkDev *d_chunks, uint32_t nchunks,
+                               uint16_t *d_scratch, uint32_t *d_tables, const uint32_t *d_fixed, hipStream_t st);
+
 extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, ZsChunkDev *d_chunks, uint32_t nchunks,
                                   const uint32_t *d_find_ids, uint32_t nfind, const ZsCJobDev *d_cjobs, uint32_t ncjobs,
                                   uint16_t *d_scratch, uint32_t *d_tables, const uint32_t *d_fixed, uint8_t *d_windows,
                                   ZsDecDev *d_decs, uint32_t *d_fallback, hipStream_t st, hipEvent_t *ev) {
   if (nfind) hipLaunchKernelGGL(zs_find_kernel, dim3(nfind), dim3(64), 0, st, d_jobs, d_heads, d_chunks, d_find_ids);
   if (ev) (void)hipEventRecord(ev[0], st);
-  hipLaunchKernelGGL(zs_lane_kernel, dim3((nchunks + WAVE - 1) / WAVE), dim3(WAVE), 0, st, d_jobs, d_heads, d_chunks,
-                     nchunks, d_scratch, d_tables, d_fixed);
+  zs_launch_lane(d_jobs, d_heads, d_chunks, nchunks, d_scratch, d_tables, d_fixed, st);
   if (ev) (void)hipEventRecord(ev[1], st);
   hipLaunchKernelGGL(zs_link_kernel, dim3(ncjobs), dim3(LINK_THREADS), 0, st, d_jobs, d_heads, d_chunks, d_cjobs,
                      d_scratch, d_windows, d_decs, d_fallback);

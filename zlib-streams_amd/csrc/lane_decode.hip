@@ -1,0 +1,572 @@
+// lane_decode.hip -- one lane per chunk: the speculative chunk decoder.
+//
+// Reference hot loop: src/inffast.c:100-287 (literal/length/distance decode +
+// copy), with block headers from src/inflate.c:834-1033 and tables from
+// src/inftrees.c:33-321.
+//
+// MI355X layout (one 64-lane wave = 64 independent chunk decoders):
+//   * LDS holds every lane's ROOT tables as compact 16-bit entries: a 9-bit
+//     literal/length root (1 KiB per lane) and a 6-bit distance root (128 B),
+//     72 KiB per wave -> 2 waves per CU.  Codes longer than the root, and
+//     invalid codes, take a slow path through the lane's full zlib-layout table
+//     in global memory (rare: only the least frequent symbols);
+//   * length/distance base and extra-bit counts are computed arithmetically
+//     from the code index (no table loads);
+//   * the lane writes u16 entries to its own scratch: values < 256 are bytes,
+//     256 + w names byte w of the 32 KiB history before the chunk (markers);
+//   * match copies move 8 entries (16 B) per load/store when the source lies
+//     at least 8 entries back inside the chunk, and emit whole marker runs
+//     arithmetically when the source lies entirely before the chunk;
+//   * block headers / stored blocks are processed cooperatively: the whole
+//     wave works on one lane's header (bits staged in LDS, ballot-parallel
+//     table build), then writes that lane's compact roots.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "zs_common.h"
+#include "zs_device.h"
+
+#define MARK_BASE 256u
+#define HIST 32768u
+#define STAGE_WORDS 256  // 1 KiB of staged header bits per cooperative step
+#define LROOT_N 512      // 9-bit literal/length root
+#define DROOT_N 64       // 6-bit distance root
+#define ZBUILD 852       // zlib build area (ENOUGH_LENS; the distance table reuses it)
+
+// compact root entry (u16): [1:0] kind, [5:2] code bits, [15:6] symbol
+enum { CK_SYM = 0, CK_LEN = 1, CK_EOB = 2, CK_SLOW = 3 };
+
+__device__ __forceinline__ uint16_t compact_len_entry(uint32_t z) {
+  const uint32_t op = e_op(z), bits = e_bits(z), val = e_val(z);
+  if (op == 0) return (uint16_t)(CK_SYM | (bits << 2) | (val << 6));
+  if (op & 32) return (uint16_t)(CK_EOB | (bits << 2));  // 96 = end of block
+  if (op & 64) return (uint16_t)CK_SLOW;                 // invalid code
+  if ((op & 0xf0u) == 0) return (uint16_t)CK_SLOW;       // link to a sub-table
+  // length base -> code index k (lbase of src/inftrees.c:59-61)
+  const uint32_t e = op & 15u;
+  uint32_t k;
+  if (val == 258) k = 28;
+  else if (e == 0) k = val - 3;
+  else k = 4 * (e + 1) + ((val - 3) >> e) - 4;
+  return (uint16_t)(CK_LEN | (bits << 2) | (k << 6));
+}
+__device__ __forceinline__ uint16_t compact_dist_entry(uint32_t z) {
+  const uint32_t op = e_op(z), bits = e_bits(z), val = e_val(z);
+  if ((op & 64) || (op & 0xf0u) == 0) return (uint16_t)CK_SLOW;
+  const uint32_t e = op & 15u;
+  const uint32_t d = (e == 0) ? val - 1 : 2 * (e + 1) + ((val - 1) >> e) - 2;
+  return (uint16_t)(CK_SYM | (bits << 2) | (d << 6));
+}
+
+enum { LM_SYM = 0, LM_BLOCK = 1, LM_DONE = 2 };
+
+struct LaneState {
+  const uint32_t *w;  // 4-byte aligned input base
+  uint32_t end_byte, limit;
+  uint32_t wi, nw, nbits;
+  uint64_t hold;
+  uint16_t *out;
+  uint32_t pos, cap;
+  const uint32_t *zl, *zd;  // full zlib tables (global): slow path
+  uint32_t zlmask, zdmask;
+  uint32_t stop, bit, whave;
+  int mode, code, last;
+};
+
+__device__ __forceinline__ void lane_prime(LaneState &s, uint32_t bit) {
+  s.wi = bit >> 5;
+  const uint32_t w0 = in_word(s.w, s.wi, s.end_byte);
+  s.nw = in_word(s.w, s.wi + 1, s.end_byte);
+  s.hold = (uint64_t)w0 >> (bit & 31);
+  s.nbits = 32 - (bit & 31);
+  s.wi += 1;
+}
+__device__ __forceinline__ void lane_refill(LaneState &s) {
+  if (s.nbits < 32) {
+    s.hold |= (uint64_t)s.nw << s.nbits;
+    s.nbits += 32;
+    s.wi++;
+    s.nw = in_word(s.w, s.wi, s.end_byte);
+  }
+}
+__device__ __forceinline__ uint32_t lane_pos(const LaneState &s) { return s.wi * 32u - s.nbits; }
+
+// zlib-table slow path: returns a compact-format entry whose bits field is the
+// TOTAL code length (may exceed 15 for the encoding; carried separately)
+__device__ __forceinline__ uint32_t slow_lookup(const uint32_t *zt, uint32_t zmask, uint64_t hold, bool lens,
+                                                uint32_t *total_bits) {
+  uint32_t z = zt[(uint32_t)hold & zmask];
+  uint32_t used = e_bits(z);
+  if (e_op(z) != 0 && (e_op(z) & 0xf0u) == 0) {
+    z = zt[e_val(z) + ((uint32_t)(hold >> used) & ((1u << e_op(z)) - 1u))];
+    used += e_bits(z);
+  }
+  *total_bits = used;
+  const uint32_t op = e_op(z);
+  if (lens) {
+    if (op & 32) return CK_EOB;
+    if (op & 64) return CK_SLOW;  // invalid literal/length code
+    return compact_len_entry(z) & ~(15u << 2);
+  }
+  if (op & 64) return CK_SLOW;  // invalid distance code
+  return compact_dist_entry(z) & ~(15u << 2);
+}
+
+// one symbol; returns true when the lane left symbol mode
+__device__ __forceinline__ bool lane_step(LaneState &s, const uint16_t *__restrict__ lt, const uint16_t *__restrict__ dt) {
+  lane_refill(s);
+  uint32_t e = lt[(uint32_t)s.hold & (LROOT_N - 1)];
+  uint32_t used = (e >> 2) & 15u;
+  if ((e & 3u) == CK_SLOW) {
+    e = slow_lookup(s.zl, s.zlmask, s.hold, true, &used);
+    if ((e & 3u) == CK_SLOW) {
+      if (lane_pos(s) + used > s.limit) {
+        s.code = ZD_TRUNC;
+      } else {
+        s.code = ZD_ERROR | (ZM_LITLEN_CODE << 8);
+      }
+      s.mode = LM_DONE;
+      return true;
+    }
+  }
+  if (lane_pos(s) + used > s.limit) {
+    s.code = ZD_TRUNC;
+    s.mode = LM_DONE;
+    return true;
+  }
+  s.hold >>= used;
+  s.nbits -= used;
+  const uint32_t kind = e & 3u, sym = e >> 6;
+  if (kind == CK_SYM) {  // literal
+    if (s.pos >= s.cap) {
+      s.code = ZD_FULL;
+      s.mode = LM_DONE;
+      return true;
+    }
+    s.out[s.pos++] = (uint16_t)sym;
+    return false;
+  }
+  if (kind == CK_EOB) {
+    s.bit = lane_pos(s);
+    s.mode = LM_BLOCK;
+    return true;
+  }
+  // length code sym (0..28): base/extra of src/inftrees.c:59-64, computed
+  uint32_t len, xb;
+  if (sym < 8) {
+    len = sym + 3;
+    xb = 0;
+  } else if (sym < 28) {
+    xb = (sym >> 2) - 1;
+    len = ((4u + (sym & 3u)) << xb) + 3u;
+  } else {
+    len = 258;
+    xb = 0;
+  }
+  len += (uint32_t)s.hold & ((1u << xb) - 1u);
+  s.hold >>= xb;
+  s.nbits -= xb;
+  lane_refill(s);
+  uint32_t d = dt[(uint32_t)s.hold & (DROOT_N - 1)];
+  uint32_t dused = (d >> 2) & 15u;
+  if ((d & 3u) == CK_SLOW) {
+    d = slow_lookup(s.zd, s.zdmask, s.hold, false, &dused);
+    if ((d & 3u) == CK_SLOW) {
+      if (lane_pos(s) + dused > s.limit) {
+        s.code = ZD_TRUNC;
+      } else {
+        s.code = ZD_ERROR | (ZM_DIST_CODE << 8);
+      }
+      s.mode = LM_DONE;
+      return true;
+    }
+  }
+  const uint32_t dsym = d >> 6;
+  uint32_t dist, dx;
+  if (dsym < 4) {
+    dist = dsym + 1;
+    dx = 0;
+  } else {
+    dx = (dsym >> 1) - 1;
+    dist = ((2u + (dsym & 1u)) << dx) + 1u;
+  }
+  if (lane_pos(s) + dused + dx > s.limit) {
+    s.code = ZD_TRUNC;
+    s.mode = LM_DONE;
+    return true;
+  }
+  s.hold >>= dused;
+  s.nbits -= dused;
+  dist += (uint32_t)s.hold & ((1u << dx) - 1u);
+  s.hold >>= dx;
+  s.nbits -= dx;
+  if (s.pos + len > s.cap) {
+    s.code = ZD_FULL;
+    s.mode = LM_DONE;
+    return true;
+  }
+  const int q = (int)s.pos - (int)dist;
+  if (q < -(int)s.whave) {
+    s.code = ZD_ERROR | (ZM_TOO_FAR << 8);
+    s.mode = LM_DONE;
+    return true;
+  }
+  uint16_t *o = s.out + s.pos;
+  if (q >= 0 && dist >= 8) {
+    // 16-byte groups; every group reads entries at least 8 back, so at most
+    // the previous group's stores are read (same lane: program order)
+    const uint16_t *src = s.out + q;
+    for (uint32_t k = 0; k < len; k += 8) {
+      uint4 v;
+      __builtin_memcpy(&v, src + k, 16);
+      __builtin_memcpy(o + k, &v, 16);
+    }
+  } else if (q + (int)len <= 0) {
+    // source entirely in the unknown history: a run of consecutive markers
+    uint32_t m = MARK_BASE + HIST + (uint32_t)q;
+    for (uint32_t k = 0; k < len; k += 8, m += 8) {
+      const uint32_t a = m | ((m + 1) << 16);
+      uint4 v = make_uint4(a, a + 0x00020002u, a + 0x00040004u, a + 0x00060006u);
+      __builtin_memcpy(o + k, &v, 16);
+    }
+  } else {
+    // general case: entry k comes from q + (k mod dist) (always before pos)
+    uint32_t m = 0;
+    for (uint32_t k = 0; k < len; k += 8) {
+      uint16_t v[8];
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        const int idx = q + (int)m;
+        v[i] = (idx < 0) ? (uint16_t)(MARK_BASE + HIST + idx) : ((k + i < len) ? s.out[idx] : (uint16_t)0);
+        m = (m + 1 == dist) ? 0u : m + 1;
+      }
+#pragma unroll
+      for (int i = 0; i < 8; i++)
+        if (k + i < len) o[k + i] = v[i];
+    }
+  }
+  s.pos += len;
+  return false;
+}
+
+// Wave-uniform bit reader over the LDS-staged header bits.
+struct StageBits {
+  const uint32_t *st;
+  uint32_t base;  // bit index of st[0] in the input
+  __device__ __forceinline__ uint32_t peek(uint32_t bit, uint32_t n) const {
+    const uint32_t r = bit - base;
+    const uint64_t v = (uint64_t)st[r >> 5] | ((uint64_t)st[(r >> 5) + 1] << 32);
+    return (uint32_t)(v >> (r & 31)) & ((n >= 32) ? 0xffffffffu : ((1u << n) - 1u));
+  }
+};
+
+struct LaneLDS {
+  uint16_t lroot[WAVE][LROOT_N];
+  uint16_t droot[WAVE][DROOT_N];
+  uint32_t stage[STAGE_WORDS + 4];
+  uint32_t tab[ZBUILD];
+  uint16_t lens[320];
+  uint16_t sorted[320];
+  uint32_t scr[32];
+};
+
+__device__ void stage_bits(LaneLDS &L, const uint32_t *w, uint32_t end_byte, uint32_t bit, StageBits &sb) {
+  const uint32_t lane = lane_id();
+  const uint32_t b16 = (bit >> 7) << 4;  // byte offset, multiple of 16
+  const uint32_t wi = (b16 >> 2) + lane * 4;
+#pragma unroll
+  for (int k = 0; k < 4; k++) L.stage[lane * 4 + k] = in_word(w, wi + k, end_byte);
+  if (lane < 4) L.stage[STAGE_WORDS + lane] = 0;
+  __builtin_amdgcn_wave_barrier();
+  sb.st = L.stage;
+  sb.base = b16 * 8u;
+}
+
+__device__ __forceinline__ uintptr_t readlane_ptr(const void *p, uint32_t ln) {
+  const uint64_t v = reinterpret_cast<uintptr_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, ln);
+  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), ln);
+  return (uintptr_t)(((uint64_t)hi << 32) | lo);
+}
+
+// Install compact roots for lane ln from zlib tables zl (root bits lb) and zd (db).
+__device__ void install_roots(LaneLDS &L, uint32_t ln, const uint32_t *zl, uint32_t lb, const uint32_t *zd, uint32_t db) {
+  const uint32_t lane = lane_id();
+  for (uint32_t i = lane; i < LROOT_N; i += WAVE) L.lroot[ln][i] = compact_len_entry(zl[i & ((1u << lb) - 1u)]);
+  L.droot[ln][lane] = compact_dist_entry(zd[lane & ((1u << db) - 1u)]);
+  __builtin_amdgcn_wave_barrier();
+}
+
+// Cooperative block-boundary processing for lane `ln` (all lanes call it with
+// the same ln): end/stop checks, stored blocks, fixed and dynamic headers
+// (src/inflate.c:834-1033); installs the lane's tables.
+__device__ void coop_block(LaneState &s, uint32_t ln, LaneLDS &L, uint32_t *lane_tab, const uint32_t *fixed) {
+  const uint32_t lane = lane_id();
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(readlane_ptr(s.w, ln));
+  uint16_t *out = reinterpret_cast<uint16_t *>(readlane_ptr(s.out, ln));
+  uint32_t *tabg = reinterpret_cast<uint32_t *>(readlane_ptr(lane_tab, ln));
+  const uint32_t end_byte = __builtin_amdgcn_readlane(s.end_byte, ln);
+  const uint32_t limit = end_byte * 8u;
+  const uint32_t stop = __builtin_amdgcn_readlane(s.stop, ln);
+  const uint32_t cap = __builtin_amdgcn_readlane(s.cap, ln);
+  uint32_t bit = __builtin_amdgcn_readlane(s.bit, ln);
+  uint32_t pos = __builtin_amdgcn_readlane(s.pos, ln);
+  int last = __builtin_amdgcn_readlane(s.last, ln);
+  int mode = LM_DONE, code = 0;
+  const uint32_t *zl = fixed, *zd = fixed + 512;
+  uint32_t lbits = 9, dbits = 5;
+  for (;;) {
+    if (last) {
+      code = ZD_END;
+      break;
+    }
+    if (bit >= stop) {
+      code = ZD_STOP;
+      break;
+    }
+    if (bit + 3 > limit) {
+      code = ZD_TRUNC;
+      break;
+    }
+    StageBits sb;
+    stage_bits(L, w, end_byte, bit, sb);
+    const uint32_t hdr = sb.peek(bit, 3);
+    last = hdr & 1;
+    const uint32_t type = hdr >> 1;
+    bit += 3;
+    if (type == 0) {  // stored (src/inflate.c:870-904)
+      bit = (bit + 7) & ~7u;
+      if (bit + 32 > limit) {
+        code = ZD_TRUNC;
+        break;
+      }
+      stage_bits(L, w, end_byte, bit, sb);
+      const uint32_t v = sb.peek(bit, 32);
+      if ((v & 0xffffu) != ((v >> 16) ^ 0xffffu)) {
+        code = ZD_ERROR | (ZM_STORED_LEN << 8);
+        break;
+      }
+      bit += 32;
+      const uint32_t n = v & 0xffffu;
+      if (bit / 8 + n > end_byte) {
+        code = ZD_TRUNC;
+        break;
+      }
+      if (pos + n > cap) {
+        code = ZD_FULL;
+        break;
+      }
+      const uint8_t *src = reinterpret_cast<const uint8_t *>(w) + bit / 8;
+      for (uint32_t k = lane; k < n; k += WAVE) out[pos + k] = src[k];
+      pos += n;
+      bit += n * 8;
+      continue;
+    }
+    if (type == 1) {  // fixed: global fixed tables (lit root 9, dist root 5)
+      zl = fixed;
+      zd = fixed + 512;
+      lbits = 9;
+      dbits = 5;
+      install_roots(L, ln, zl, lbits, zd, dbits);
+      mode = LM_SYM;
+      break;
+    }
+    if (type == 3) {
+      code = ZD_ERROR | (ZM_BLOCK_TYPE << 8);
+      break;
+    }
+    if (bit + 14 > limit) {
+      code = ZD_TRUNC;
+      break;
+    }
+    const uint32_t h = sb.peek(bit, 14);
+    const uint32_t nlen = (h & 31) + 257, ndist = ((h >> 5) & 31) + 1, ncode = ((h >> 10) & 15) + 4;
+    bit += 14;
+    if (nlen > 286 || ndist > 30) {
+      code = ZD_ERROR | (ZM_TOO_MANY << 8);
+      break;
+    }
+    if (bit + 3 * ncode > limit) {
+      code = ZD_TRUNC;
+      break;
+    }
+    if (lane < 19) L.lens[c_clorder[lane]] = lane < ncode ? (uint16_t)sb.peek(bit + 3 * lane, 3) : (uint16_t)0;
+    bit += 3 * ncode;
+    __builtin_amdgcn_wave_barrier();
+    uint32_t cbits = 7;
+    if (build_table(T_CODES, L.lens, 19, L.tab, &cbits, L.sorted, L.scr, 0)) {
+      code = ZD_ERROR | (ZM_CODE_LENGTHS << 8);
+      break;
+    }
+    const uint32_t total = nlen + ndist;
+    const uint32_t cmask = (1u << cbits) - 1u;
+    uint32_t have = 0;
+    bool bad = false;
+    while (have < total) {
+      if (bit - sb.base > (STAGE_WORDS - 2) * 32u - 64u) stage_bits(L, w, end_byte, bit, sb);
+      const uint32_t x = sb.peek(bit, 14);
+      const uint32_t e = L.tab[x & cmask];
+      const uint32_t eb = e_bits(e), ev = e_val(e);
+      if (ev < 16) {
+        if (bit + eb > limit) {
+          bad = true;
+          code = ZD_TRUNC;
+          break;
+        }
+        bit += eb;
+        if (lane == 0) L.lens[have] = (uint16_t)ev;
+        have++;
+        continue;
+      }
+      const uint32_t xb = ev == 16 ? 2u : (ev == 17 ? 3u : 7u);
+      if (bit + eb + xb > limit) {
+        bad = true;
+        code = ZD_TRUNC;
+        break;
+      }
+      if (ev == 16 && have == 0) {
+        bad = true;
+        code = ZD_ERROR | (ZM_REPEAT << 8);
+        break;
+      }
+      const uint32_t rep = (ev == 18 ? 11u : 3u) + ((x >> eb) & ((1u << xb) - 1u));
+      bit += eb + xb;
+      if (have + rep > total) {
+        bad = true;
+        code = ZD_ERROR | (ZM_REPEAT << 8);
+        break;
+      }
+      __builtin_amdgcn_wave_barrier();
+      const uint32_t fillv = ev == 16 ? uni(L.lens[have - 1]) : 0u;
+      for (uint32_t k = lane; k < rep; k += WAVE) L.lens[have + k] = (uint16_t)fillv;
+      __builtin_amdgcn_wave_barrier();
+      have += rep;
+    }
+    if (bad) break;
+    __builtin_amdgcn_wave_barrier();
+    if (uni(L.lens[256]) == 0) {
+      code = ZD_ERROR | (ZM_MISSING_EOB << 8);
+      break;
+    }
+    // literal/length table: build in LDS, keep the full zlib table in global
+    // (slow path), compact root into the lane's LDS slot
+    lbits = 9;
+    if (build_table(T_LENS, L.lens, nlen, L.tab, &lbits, L.sorted, L.scr, 0)) {
+      code = ZD_ERROR | (ZM_LITLEN_SET << 8);
+      break;
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t i = lane; i < ZBUILD; i += WAVE) tabg[i] = L.tab[i];
+    for (uint32_t i = lane; i < LROOT_N; i += WAVE) L.lroot[ln][i] = compact_len_entry(L.tab[i & ((1u << lbits) - 1u)]);
+    __builtin_amdgcn_wave_barrier();
+    dbits = 6;
+    if (build_table(T_DISTS, L.lens + nlen, ndist, L.tab, &dbits, L.sorted, L.scr, 0)) {
+      code = ZD_ERROR | (ZM_DIST_SET << 8);
+      break;
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t i = lane; i < 592; i += WAVE) tabg[DIST_TABLE_OFF + i] = L.tab[i];
+    L.droot[ln][lane] = compact_dist_entry(L.tab[lane & ((1u << dbits) - 1u)]);
+    __builtin_amdgcn_wave_barrier();
+    zl = tabg;
+    zd = tabg + DIST_TABLE_OFF;
+    mode = LM_SYM;
+    break;
+  }
+  if (lane == ln) {
+    s.pos = pos;
+    s.last = last;
+    s.bit = bit;
+    s.mode = mode;
+    if (mode == LM_SYM) {
+      s.zl = zl;
+      s.zd = zd;
+      s.zlmask = (1u << lbits) - 1u;
+      s.zdmask = (1u << dbits) - 1u;
+      lane_prime(s, bit);
+    } else {
+      s.code = code;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict__ jobs, const ZsHeadDev *__restrict__ heads,
+                                                      ZsChunkDev *__restrict__ chunks, uint32_t nchunks,
+                                                      uint16_t *__restrict__ scratch, uint32_t *__restrict__ tables,
+                                                      const uint32_t *__restrict__ fixed) {
+  __shared__ LaneLDS L;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t c = blockIdx.x * WAVE + lane;
+  LaneState s;
+  s.mode = LM_DONE;
+  s.code = ZD_SKIP;
+  s.pos = 0;
+  s.last = 0;
+  s.bit = 0;
+  s.stop = ZS_NONE;
+  s.w = nullptr;
+  s.out = nullptr;
+  s.end_byte = 0;
+  s.limit = 0;
+  s.cap = 0;
+  s.whave = 0;
+  s.zl = fixed;
+  s.zd = fixed + 512;
+  s.zlmask = s.zdmask = 0;
+  s.wi = s.nw = s.nbits = 0;
+  s.hold = 0;
+  uint32_t *lane_tab = tables + (size_t)min(c, nchunks - 1) * TABLE_ENTRIES;
+  if (c < nchunks) {
+    const ZsChunkDev ch = chunks[c];
+    const ZsHeadDev hd = heads[ch.job];
+    const ZsJobDev jb = jobs[ch.job];
+    const uintptr_t ip = reinterpret_cast<uintptr_t>(jb.in);
+    const uint32_t mis = (uint32_t)(ip & 3u);
+    const uint32_t start = ch.ord == 0 ? (mis + (uint32_t)hd.start_byte) * 8u : ch.start_bit;
+    if (hd.code == ZD_END && start != ZS_NONE) {
+      s.w = reinterpret_cast<const uint32_t *>(ip - mis);
+      s.end_byte = mis + (uint32_t)jb.in_len;
+      s.limit = s.end_byte * 8u;
+      s.out = scratch + ch.scratch;
+      s.cap = ch.cap;
+      s.whave = ch.ord == 0 ? 0u : HIST;
+      s.bit = start;
+      s.mode = LM_BLOCK;
+      s.code = 0;
+      for (uint32_t k = ch.ord + 1; k < ch.nchunks; k++) {
+        const uint32_t sb = chunks[ch.first + k].start_bit;
+        if (sb != ZS_NONE) {
+          s.stop = sb;
+          break;
+        }
+      }
+    }
+  }
+  const uint16_t *lt = L.lroot[lane];
+  const uint16_t *dt = L.droot[lane];
+  for (;;) {
+    uint64_t need = __ballot(s.mode == LM_BLOCK);
+    while (need) {
+      const uint32_t ln = (uint32_t)__builtin_ctzll(need);
+      need &= need - 1;
+      coop_block(s, ln, L, lane_tab, fixed);
+    }
+    if (__ballot(s.mode == LM_SYM) == 0) break;
+    if (s.mode == LM_SYM) {
+      for (int it = 0; it < 64; it++)
+        if (lane_step(s, lt, dt)) break;
+    }
+  }
+  if (c < nchunks) {
+    ZsChunkDev *ch = &chunks[c];
+    ch->code = s.code;
+    ch->end_bit = (s.code == ZD_END || s.code == ZD_STOP) ? s.bit : 0u;
+    ch->n_out = s.pos;
+  }
+}
+
+extern "C" void zs_launch_lane(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, ZsChunkDev *d_chunks, uint32_t nchunks,
+                               uint16_t *d_scratch, uint32_t *d_tables, const uint32_t *d_fixed, hipStream_t st) {
+  hipLaunchKernelGGL(zs_lane_kernel, dim3((nchunks + WAVE - 1) / WAVE), dim3(WAVE), 0, st, d_jobs, d_heads, d_chunks,
+                     nchunks, d_scratch, d_tables, d_fixed);
+}

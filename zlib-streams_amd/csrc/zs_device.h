@@ -211,3 +211,12 @@ static __device__ __attribute__((noinline)) int build_table(int type, const uint
   return 0;
 }
 
+
+// masked 32-bit input word (bytes at or past end_byte read as zero)
+static __device__ __forceinline__ uint32_t in_word(const uint32_t *w, uint32_t wi, uint32_t end_byte) {
+  uint32_t b = wi * 4u;
+  if (b + 4u <= end_byte) return w[wi];
+  if (b >= end_byte) return 0u;
+  uint32_t keep = end_byte - b;  // 1..3
+  return w[wi] & ((1u << (8u * keep)) - 1u);
+}
