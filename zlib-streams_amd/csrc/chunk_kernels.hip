@@ -421,16 +421,16 @@ extern "C" void zs_launch_fixed_tables(uint32_t *fixed, hipStream_t st) {
 }
 
 extern "C" void zs_launch_lane(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, ZsChunkDev *d_chunks, uint32_t nchunks,
-                               uint16_t *d_scratch, uint32_t *d_tables, const uint32_t *d_fixed, hipStream_t st);
+                               uint16_t *d_scratch, uint32_t *d_tokens, uint32_t *d_tables, const uint32_t *d_fixed,
+                               hipStream_t st, hipEvent_t *ev);
 
 extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, ZsChunkDev *d_chunks, uint32_t nchunks,
                                   const uint32_t *d_find_ids, uint32_t nfind, const ZsCJobDev *d_cjobs, uint32_t ncjobs,
-                                  uint16_t *d_scratch, uint32_t *d_tables, const uint32_t *d_fixed, uint8_t *d_windows,
-                                  ZsDecDev *d_decs, uint32_t *d_fallback, hipStream_t st, hipEvent_t *ev) {
+                                  uint16_t *d_scratch, uint32_t *d_tokens, uint32_t *d_tables, const uint32_t *d_fixed,
+                                  uint8_t *d_windows, ZsDecDev *d_decs, uint32_t *d_fallback, hipStream_t st,
+                                  hipEvent_t *ev) {
   if (nfind) hipLaunchKernelGGL(zs_find_kernel, dim3(nfind), dim3(64), 0, st, d_jobs, d_heads, d_chunks, d_find_ids);
-  if (ev) (void)hipEventRecord(ev[0], st);
-  zs_launch_lane(d_jobs, d_heads, d_chunks, nchunks, d_scratch, d_tables, d_fixed, st);
-  if (ev) (void)hipEventRecord(ev[1], st);
+  zs_launch_lane(d_jobs, d_heads, d_chunks, nchunks, d_scratch, d_tokens, d_tables, d_fixed, st, ev);
   hipLaunchKernelGGL(zs_link_kernel, dim3(ncjobs), dim3(LINK_THREADS), 0, st, d_jobs, d_heads, d_chunks, d_cjobs,
                      d_scratch, d_windows, d_decs, d_fallback);
   hipLaunchKernelGGL(zs_emit_kernel, dim3(nchunks), dim3(EMIT_THREADS), 0, st, d_jobs, d_chunks, d_scratch, d_windows,

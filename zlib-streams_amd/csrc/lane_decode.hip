@@ -65,8 +65,9 @@ struct LaneState {
   uint32_t end_byte, limit;
   uint32_t wi, nw, nbits;
   uint64_t hold;
-  uint16_t *out;
-  uint32_t pos, cap;
+  uint32_t *tok;      // token output (parse pass)
+  uint32_t ntok, tcap;
+  uint32_t pos, cap;  // entries the tokens expand to / entry capacity
   const uint32_t *zl, *zd;  // full zlib tables (global): slow path
   uint32_t zlmask, zdmask;
   uint32_t stop, bit, whave;
@@ -138,12 +139,13 @@ __device__ __forceinline__ bool lane_step(LaneState &s, const uint16_t *__restri
   s.nbits -= used;
   const uint32_t kind = e & 3u, sym = e >> 6;
   if (kind == CK_SYM) {  // literal
-    if (s.pos >= s.cap) {
+    if (s.pos >= s.cap || s.ntok >= s.tcap) {
       s.code = ZD_FULL;
       s.mode = LM_DONE;
       return true;
     }
-    s.out[s.pos++] = (uint16_t)sym;
+    s.tok[s.ntok++] = sym;
+    s.pos++;
     return false;
   }
   if (kind == CK_EOB) {
@@ -200,51 +202,17 @@ __device__ __forceinline__ bool lane_step(LaneState &s, const uint16_t *__restri
   dist += (uint32_t)s.hold & ((1u << dx) - 1u);
   s.hold >>= dx;
   s.nbits -= dx;
-  if (s.pos + len > s.cap) {
+  if (s.pos + len > s.cap || s.ntok >= s.tcap) {
     s.code = ZD_FULL;
     s.mode = LM_DONE;
     return true;
   }
-  const int q = (int)s.pos - (int)dist;
-  if (q < -(int)s.whave) {
+  if (dist > s.pos + s.whave) {
     s.code = ZD_ERROR | (ZM_TOO_FAR << 8);
     s.mode = LM_DONE;
     return true;
   }
-  uint16_t *o = s.out + s.pos;
-  if (q >= 0 && dist >= 8) {
-    // 16-byte groups; every group reads entries at least 8 back, so at most
-    // the previous group's stores are read (same lane: program order)
-    const uint16_t *src = s.out + q;
-    for (uint32_t k = 0; k < len; k += 8) {
-      uint4 v;
-      __builtin_memcpy(&v, src + k, 16);
-      __builtin_memcpy(o + k, &v, 16);
-    }
-  } else if (q + (int)len <= 0) {
-    // source entirely in the unknown history: a run of consecutive markers
-    uint32_t m = MARK_BASE + HIST + (uint32_t)q;
-    for (uint32_t k = 0; k < len; k += 8, m += 8) {
-      const uint32_t a = m | ((m + 1) << 16);
-      uint4 v = make_uint4(a, a + 0x00020002u, a + 0x00040004u, a + 0x00060006u);
-      __builtin_memcpy(o + k, &v, 16);
-    }
-  } else {
-    // general case: entry k comes from q + (k mod dist) (always before pos)
-    uint32_t m = 0;
-    for (uint32_t k = 0; k < len; k += 8) {
-      uint16_t v[8];
-#pragma unroll
-      for (int i = 0; i < 8; i++) {
-        const int idx = q + (int)m;
-        v[i] = (idx < 0) ? (uint16_t)(MARK_BASE + HIST + idx) : ((k + i < len) ? s.out[idx] : (uint16_t)0);
-        m = (m + 1 == dist) ? 0u : m + 1;
-      }
-#pragma unroll
-      for (int i = 0; i < 8; i++)
-        if (k + i < len) o[k + i] = v[i];
-    }
-  }
+  s.tok[s.ntok++] = (len << 16) | (dist - 1u);
   s.pos += len;
   return false;
 }
@@ -303,8 +271,10 @@ __device__ void install_roots(LaneLDS &L, uint32_t ln, const uint32_t *zl, uint3
 __device__ void coop_block(LaneState &s, uint32_t ln, LaneLDS &L, uint32_t *lane_tab, const uint32_t *fixed) {
   const uint32_t lane = lane_id();
   const uint32_t *w = reinterpret_cast<const uint32_t *>(readlane_ptr(s.w, ln));
-  uint16_t *out = reinterpret_cast<uint16_t *>(readlane_ptr(s.out, ln));
+  uint32_t *tok = reinterpret_cast<uint32_t *>(readlane_ptr(s.tok, ln));
   uint32_t *tabg = reinterpret_cast<uint32_t *>(readlane_ptr(lane_tab, ln));
+  uint32_t ntok = __builtin_amdgcn_readlane(s.ntok, ln);
+  const uint32_t tcap = __builtin_amdgcn_readlane(s.tcap, ln);
   const uint32_t end_byte = __builtin_amdgcn_readlane(s.end_byte, ln);
   const uint32_t limit = end_byte * 8u;
   const uint32_t stop = __builtin_amdgcn_readlane(s.stop, ln);
@@ -352,12 +322,17 @@ __device__ void coop_block(LaneState &s, uint32_t ln, LaneLDS &L, uint32_t *lane
         code = ZD_TRUNC;
         break;
       }
-      if (pos + n > cap) {
+      if (pos + n > cap || ntok + 2 > tcap) {
         code = ZD_FULL;
         break;
       }
-      const uint8_t *src = reinterpret_cast<const uint8_t *>(w) + bit / 8;
-      for (uint32_t k = lane; k < n; k += WAVE) out[pos + k] = src[k];
+      if (n) {  // stored run token + input byte offset (expanded by zs_expand_kernel)
+        if (lane == 0) {
+          tok[ntok] = (TOK_STORED << 16) | (n - 1u);
+          tok[ntok + 1] = bit / 8;
+        }
+        ntok += 2;
+      }
       pos += n;
       bit += n * 8;
       continue;
@@ -475,6 +450,7 @@ __device__ void coop_block(LaneState &s, uint32_t ln, LaneLDS &L, uint32_t *lane
   }
   if (lane == ln) {
     s.pos = pos;
+    s.ntok = ntok;
     s.last = last;
     s.bit = bit;
     s.mode = mode;
@@ -490,9 +466,10 @@ __device__ void coop_block(LaneState &s, uint32_t ln, LaneLDS &L, uint32_t *lane
   }
 }
 
+// Parse pass: one lane per chunk, symbols -> tokens (no history reads at all).
 __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict__ jobs, const ZsHeadDev *__restrict__ heads,
                                                       ZsChunkDev *__restrict__ chunks, uint32_t nchunks,
-                                                      uint16_t *__restrict__ scratch, uint32_t *__restrict__ tables,
+                                                      uint32_t *__restrict__ tokens, uint32_t *__restrict__ tables,
                                                       const uint32_t *__restrict__ fixed) {
   __shared__ LaneLDS L;
   const uint32_t lane = threadIdx.x;
@@ -505,7 +482,9 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
   s.bit = 0;
   s.stop = ZS_NONE;
   s.w = nullptr;
-  s.out = nullptr;
+  s.tok = nullptr;
+  s.ntok = 0;
+  s.tcap = 0;
   s.end_byte = 0;
   s.limit = 0;
   s.cap = 0;
@@ -527,7 +506,8 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
       s.w = reinterpret_cast<const uint32_t *>(ip - mis);
       s.end_byte = mis + (uint32_t)jb.in_len;
       s.limit = s.end_byte * 8u;
-      s.out = scratch + ch.scratch;
+      s.tok = tokens + ch.tok;
+      s.tcap = ch.tcap;
       s.cap = ch.cap;
       s.whave = ch.ord == 0 ? 0u : HIST;
       s.bit = start;
@@ -562,11 +542,180 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
     ch->code = s.code;
     ch->end_bit = (s.code == ZD_END || s.code == ZD_STOP) ? s.bit : 0u;
     ch->n_out = s.pos;
+    ch->n_tok = s.ntok;
   }
 }
 
+// ---------------------------------------------------------------------------
+// Expand pass: one 256-thread workgroup (4 waves) per chunk, tokens -> u16
+// entries.  The last 32 Ki entries live in an LDS ring; every round the 256
+// threads produce 256 consecutive entries in parallel: a max-scan over
+// round-stamped token-start marks finds each entry's token, sources before the
+// round come from the ring (markers 256 + w for positions before the chunk),
+// sources inside the round are resolved by pointer jumping through LDS (rare:
+// only distances shorter than the round reach into it).  Output leaves the ring
+// in 4 KiB pieces (16 B per thread).
+// ---------------------------------------------------------------------------
+#define EXP_T 256       // threads = tokens per batch = entries per round
+#define EXP_W (EXP_T / WAVE)
+#define EXP_FLUSH 2048  // entries per flush piece (8 per thread)
+
+__device__ __forceinline__ uint32_t wave_scan_add(uint32_t v) {  // inclusive, wave64
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_scan_max(uint32_t v) {  // inclusive, wave64, values >= 0
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));
+  return v;
+}
+
+__global__ void __launch_bounds__(EXP_T) zs_expand_kernel(const ZsJobDev *__restrict__ jobs,
+                                                           const ZsChunkDev *__restrict__ chunks,
+                                                           uint16_t *__restrict__ scratch,
+                                                           const uint32_t *__restrict__ tokens) {
+  __shared__ __attribute__((aligned(16))) uint16_t ring[HIST];
+  __shared__ uint32_t s_tstart[EXP_T], s_tval[EXP_T], s_mark[EXP_T];
+  __shared__ uint8_t s_tkind[EXP_T];
+  __shared__ uint32_t s_red[EXP_W];
+  __shared__ uint32_t s_jv[EXP_T];
+  __shared__ int32_t s_jp[EXP_T];
+  const uint32_t tid = threadIdx.x, lane = tid & (WAVE - 1), wv = tid / WAVE;
+  const ZsChunkDev ch = chunks[blockIdx.x];
+  const int code = ch.code & 0xff;
+  if (!(code == ZD_STOP || code == ZD_END)) return;
+  const uint32_t *tk = tokens + ch.tok;
+  const uint32_t ntok = ch.n_tok;
+  uint16_t *out = scratch + ch.scratch;
+  const uint8_t *inb = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(jobs[ch.job].in) & ~(uintptr_t)3);
+  if (ch.ord != 0) {  // history before the chunk: markers 256 + w for position w - HIST
+    uint32_t *r32 = reinterpret_cast<uint32_t *>(ring);
+    for (uint32_t i = tid; i < HIST / 2; i += EXP_T) r32[i] = (MARK_BASE + 2 * i) | ((MARK_BASE + 2 * i + 1) << 16);
+  }
+  for (uint32_t i = tid; i < EXP_T; i += EXP_T) s_mark[i] = 0;
+  uint32_t pos = 0, flushed = 0, stamp = 0;
+  for (uint32_t tb = 0; tb < ntok; tb += EXP_T) {
+    const uint32_t i = tb + tid;
+    const bool valid = i < ntok;
+    const uint32_t t = valid ? tk[i] : 0u;
+    // an offset word follows a stored-run token (offsets never reach 0xffff0000)
+    const bool is_off = valid && i > 0 && (tk[i - 1] >> 16) == TOK_STORED;
+    const uint32_t hi = t >> 16;
+    uint32_t len = 0, kind = 3, val = 0;
+    if (valid && !is_off) {
+      if (hi == 0) {
+        len = 1;
+        kind = 0;
+        val = t & 0xffu;
+      } else if (hi == TOK_STORED) {
+        len = (t & 0xffffu) + 1u;
+        kind = 2;
+        val = tk[i + 1];
+      } else {
+        len = hi;
+        kind = 1;
+        val = (t & 0xffffu) + 1u;
+      }
+    }
+    const uint32_t incl = wave_scan_add(len);
+    if (lane == WAVE - 1) s_red[wv] = incl;
+    __syncthreads();
+    uint32_t before = 0, S = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < EXP_W; w++) {
+      const uint32_t x = s_red[w];
+      before += w < wv ? x : 0u;
+      S += x;
+    }
+    const uint32_t tstart = pos + before + incl - len;
+    s_tstart[tid] = tstart;
+    s_tval[tid] = val;
+    s_tkind[tid] = (uint8_t)kind;
+    uint32_t own_carry = 0;
+    for (uint32_t R = pos; R < pos + S; R += EXP_T) {
+      if ((++stamp & 0x7fffffu) == 0) {  // stamp wrap: drop stale marks
+        s_mark[tid] = 0;
+        __syncthreads();
+        stamp++;
+      }
+      if (len && tstart >= R && tstart < R + EXP_T) s_mark[tstart - R] = (stamp << 9) | (tid + 1);
+      __syncthreads();  // marks (and the batch's token table) visible; s_red free
+      const uint32_t m = s_mark[tid];
+      const uint32_t wmax = wave_scan_max((m >> 9) == (stamp & 0x7fffffu) ? (m & 511u) : 0u);
+      if (lane == WAVE - 1) s_red[wv] = wmax;
+      __syncthreads();
+      uint32_t own = max(own_carry, wmax), all = own_carry;
+#pragma unroll
+      for (uint32_t w = 0; w < EXP_W; w++) {
+        const uint32_t x = s_red[w];
+        own = w < wv ? max(own, x) : own;
+        all = max(all, x);
+      }
+      own_carry = all;
+      const uint32_t e = R + tid;
+      const bool act = e < pos + S;
+      const uint32_t j = (own ? own : 1u) - 1u;
+      const uint32_t kj = s_tkind[j], vj = s_tval[j], sj = s_tstart[j];
+      uint32_t v = 0;
+      int p = 0;
+      bool res = true;
+      if (act) {
+        if (kj == 0) {
+          v = vj;
+        } else if (kj == 2) {
+          v = inb[vj + (e - sj)];
+        } else {
+          p = (int)e - (int)vj;
+          if (p < (int)R) v = ring[(uint32_t)p & (HIST - 1)];
+          else res = false;
+        }
+      }
+      // every ring read of this round happens before any ring write below
+      while (__syncthreads_or(!res)) {  // in-round sources: pointer jumping through LDS
+        s_jv[tid] = v;
+        s_jp[tid] = res ? -1 : p - (int)R;
+        __syncthreads();
+        if (!res) {
+          const uint32_t q = (uint32_t)(p - (int)R);
+          const int tq = s_jp[q];
+          if (tq < 0) {
+            v = s_jv[q];
+            res = true;
+          } else {
+            p = (int)R + tq;
+          }
+        }
+      }
+      if (act) ring[e & (HIST - 1)] = (uint16_t)v;
+      __syncthreads();
+      const uint32_t rend = min(R + EXP_T, pos + S);
+      while (rend - flushed >= EXP_FLUSH) {
+        const uint4 v4 = *reinterpret_cast<const uint4 *>(&ring[(flushed + tid * 8) & (HIST - 1)]);
+        *reinterpret_cast<uint4 *>(out + flushed + tid * 8) = v4;
+        flushed += EXP_FLUSH;
+      }
+    }
+    pos += S;
+    __syncthreads();  // token table reads done before the next batch rewrites it
+  }
+  for (uint32_t k = tid; k < pos - flushed; k += EXP_T) out[flushed + k] = ring[(flushed + k) & (HIST - 1)];
+}
+
 extern "C" void zs_launch_lane(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, ZsChunkDev *d_chunks, uint32_t nchunks,
-                               uint16_t *d_scratch, uint32_t *d_tables, const uint32_t *d_fixed, hipStream_t st) {
+                               uint16_t *d_scratch, uint32_t *d_tokens, uint32_t *d_tables, const uint32_t *d_fixed,
+                               hipStream_t st, hipEvent_t *ev) {
+  if (ev) (void)hipEventRecord(ev[0], st);
   hipLaunchKernelGGL(zs_lane_kernel, dim3((nchunks + WAVE - 1) / WAVE), dim3(WAVE), 0, st, d_jobs, d_heads, d_chunks,
-                     nchunks, d_scratch, d_tables, d_fixed);
+                     nchunks, d_tokens, d_tables, d_fixed);
+  hipLaunchKernelGGL(zs_expand_kernel, dim3(nchunks), dim3(EXP_T), 0, st, d_jobs, d_chunks, d_scratch, d_tokens);
+  if (ev) (void)hipEventRecord(ev[1], st);
 }

@@ -31,8 +31,9 @@ extern "C" void zs_launch_finish(const ZsJobDev *d_jobs, const ZsHeadDev *d_head
 extern "C" void zs_launch_fixed_tables(uint32_t *fixed, hipStream_t st);
 extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, ZsChunkDev *d_chunks, uint32_t nchunks,
                                   const uint32_t *d_find_ids, uint32_t nfind, const ZsCJobDev *d_cjobs, uint32_t ncjobs,
-                                  uint16_t *d_scratch, uint32_t *d_tables, const uint32_t *d_fixed, uint8_t *d_windows,
-                                  ZsDecDev *d_decs, uint32_t *d_fallback, hipStream_t st, hipEvent_t *ev);
+                                  uint16_t *d_scratch, uint32_t *d_tokens, uint32_t *d_tables, const uint32_t *d_fixed,
+                                  uint8_t *d_windows, ZsDecDev *d_decs, uint32_t *d_fallback, hipStream_t st,
+                                  hipEvent_t *ev);
 
 namespace {
 
@@ -99,8 +100,9 @@ struct Workspace {
   uint32_t *d_find = nullptr, *h_find = nullptr;
   uint32_t *d_tables = nullptr;  // TABLE_ENTRIES per chunk
   uint8_t *d_windows = nullptr;  // 32 KiB per chunk
-  size_t cap_scratch = 0;        // u16 entries
+  size_t cap_scratch = 0;        // u16 entries (and u32 parse tokens, same count)
   uint16_t *d_scratch = nullptr;
+  uint32_t *d_tokens = nullptr;
   uint32_t *d_fixed = nullptr;
   // timing (zs_profile): events on the launch stream
   bool prof = false;
@@ -187,7 +189,7 @@ int ws_reserve_chunks(size_t n, size_t scratch_entries) {
   }
   if (scratch_entries > g_ws.cap_scratch) {
     size_t c = std::max(scratch_entries, g_ws.cap_scratch + g_ws.cap_scratch / 4);
-    if ((r = grow_dev(&g_ws.d_scratch, c))) return r;
+    if ((r = grow_dev(&g_ws.d_scratch, c)) || (r = grow_dev(&g_ws.d_tokens, c))) return r;
     g_ws.cap_scratch = c;
   }
   if (!g_ws.d_fixed) {
@@ -320,7 +322,7 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
       const double ratio = std::max(1.0, (double)jd.out_cap / (double)jd.in_len);
       // scratch per chunk: 2.5x the expected output of a nominal chunk plus one
       // block of slack; a chunk that overflows sends its stream to the fallback
-      const uint32_t cap = (uint32_t)std::min<double>(4.0e9, 2.5 * C * ratio + 65536.0);
+      const uint32_t cap = (uint32_t)std::min<double>(4.0e9, 2.0 * C * ratio + 49152.0);
       g_ws.h_cjobs[q] = ZsCJobDev{k, (uint32_t)ci, nc, 0};
       for (uint32_t o = 0; o < nc; o++, ci++) {
         ZsChunkDev ch{};
@@ -333,6 +335,8 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
         ch.start_bit = ZS_NONE;
         ch.scratch = scratch_need;
         ch.cap = cap;
+        ch.tok = scratch_need;  // tokens: same offsets, u32 units (one token yields >= 1 entry)
+        ch.tcap = cap;
         ch.chain_next = ZS_NONE;
         scratch_need += ((size_t)cap + 64 + 7) & ~size_t(7);
         g_ws.h_chunks[ci] = ch;
@@ -351,7 +355,8 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
   zs_launch_header(g_ws.d_jobs, g_ws.d_heads, nv, st);
   if (n_cj)
     zs_launch_chunked(g_ws.d_jobs, g_ws.d_heads, g_ws.d_chunks, (uint32_t)nchunks, g_ws.d_find, nfind, g_ws.d_cjobs, n_cj,
-                      g_ws.d_scratch, g_ws.d_tables, g_ws.d_fixed, g_ws.d_windows, g_ws.d_decs, g_ws.d_fallback, st, ev);
+                      g_ws.d_scratch, g_ws.d_tokens, g_ws.d_tables, g_ws.d_fixed, g_ws.d_windows, g_ws.d_decs,
+                      g_ws.d_fallback, st, ev);
   else if (ev) {
     HIP_OK(hipEventRecord(ev[0], st));
   }

@@ -119,8 +119,18 @@ struct ZsChunkDev {
   uint32_t chain_next; // next chunk in the verified chain (ZS_NONE at the end)
   uint64_t out_off;    // output byte offset (verified chain members)
   uint32_t in_chain;   // 1 = member of the verified chain of a non-fallback job
+  uint32_t n_tok;      // tokens produced by the parse pass
+  uint64_t tok;        // offset of this chunk's token region (u32 units)
+  uint32_t tcap;       // token capacity
   uint32_t pad;
 };
+
+// Parse-pass tokens (u32), consumed by the expand pass:
+//   hi16 == 0          literal, byte in bits 0-7
+//   hi16 in [3, 258]   match: length = hi16, distance = lo16 + 1
+//   hi16 == 0xffff     stored run of lo16 + 1 bytes; the next word is the byte
+//                      offset of the run in the job input (from its 4-byte-aligned base)
+#define TOK_STORED 0xffffu
 
 struct ZsCJobDev {
   uint32_t job;        // job index
