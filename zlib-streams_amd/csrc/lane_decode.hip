@@ -1,25 +1,24 @@
-// lane_decode.hip -- one lane per chunk: the speculative chunk decoder.
+// lane_decode.hip -- the speculative chunk decoder: parse pass + expand pass.
 //
 // Reference hot loop: src/inffast.c:100-287 (literal/length/distance decode +
 // copy), with block headers from src/inflate.c:834-1033 and tables from
 // src/inftrees.c:33-321.
 //
-// MI355X layout (one 64-lane wave = 64 independent chunk decoders):
+// Parse pass (zs_lane_kernel, one 64-lane wave = 64 independent chunk decoders):
 //   * LDS holds every lane's ROOT tables as compact 16-bit entries: a 9-bit
 //     literal/length root (1 KiB per lane) and a 6-bit distance root (128 B),
-//     72 KiB per wave -> 2 waves per CU.  Codes longer than the root, and
-//     invalid codes, take a slow path through the lane's full zlib-layout table
-//     in global memory (rare: only the least frequent symbols);
+//     ~80 KiB per wave.  A root entry for a code longer than the root carries
+//     the offset and index width of its sub-table, which lives as compact
+//     16-bit entries in the lane's global table area (one dependent load);
+//     invalid codes re-run zlib's two-level lookup on the lane's zlib-layout
+//     table to report exactly what inflate reports;
 //   * length/distance base and extra-bit counts are computed arithmetically
 //     from the code index (no table loads);
-//   * the lane writes u16 entries to its own scratch: values < 256 are bytes,
-//     256 + w names byte w of the 32 KiB history before the chunk (markers);
-//   * match copies move 8 entries (16 B) per load/store when the source lies
-//     at least 8 entries back inside the chunk, and emit whole marker runs
-//     arithmetically when the source lies entirely before the chunk;
+//   * every symbol becomes one u32 token (no history reads at all);
 //   * block headers / stored blocks are processed cooperatively: the whole
 //     wave works on one lane's header (bits staged in LDS, ballot-parallel
-//     table build), then writes that lane's compact roots.
+//     table build), then writes that lane's compact roots and sub-tables.
+// Expand pass (zs_expand_kernel): see below.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -33,15 +32,18 @@
 #define DROOT_N 64       // 6-bit distance root
 #define ZBUILD 852       // zlib build area (ENOUGH_LENS; the distance table reuses it)
 
-// compact root entry (u16): [1:0] kind, [5:2] code bits, [15:6] symbol
+// compact entry (u16): [1:0] kind, [5:2] code bits, [15:6] symbol.
+// CK_SLOW: [5:2] = sub-table index bits (0 = invalid code), [15:6] = sub-table
+// offset (zlib's link entry, src/inftrees.c:250-262); sub-table entries carry
+// the TOTAL code length in [5:2] (root bits + sub bits <= 15).
 enum { CK_SYM = 0, CK_LEN = 1, CK_EOB = 2, CK_SLOW = 3 };
 
-__device__ __forceinline__ uint16_t compact_len_entry(uint32_t z) {
-  const uint32_t op = e_op(z), bits = e_bits(z), val = e_val(z);
+__device__ __forceinline__ uint16_t compact_len_entry(uint32_t z, uint32_t add_bits = 0) {
+  const uint32_t op = e_op(z), bits = e_bits(z) + add_bits, val = e_val(z);
   if (op == 0) return (uint16_t)(CK_SYM | (bits << 2) | (val << 6));
   if (op & 32) return (uint16_t)(CK_EOB | (bits << 2));  // 96 = end of block
   if (op & 64) return (uint16_t)CK_SLOW;                 // invalid code
-  if ((op & 0xf0u) == 0) return (uint16_t)CK_SLOW;       // link to a sub-table
+  if ((op & 0xf0u) == 0) return (uint16_t)(CK_SLOW | (op << 2) | (val << 6));  // sub-table link
   // length base -> code index k (lbase of src/inftrees.c:59-61)
   const uint32_t e = op & 15u;
   uint32_t k;
@@ -50,159 +52,168 @@ __device__ __forceinline__ uint16_t compact_len_entry(uint32_t z) {
   else k = 4 * (e + 1) + ((val - 3) >> e) - 4;
   return (uint16_t)(CK_LEN | (bits << 2) | (k << 6));
 }
-__device__ __forceinline__ uint16_t compact_dist_entry(uint32_t z) {
-  const uint32_t op = e_op(z), bits = e_bits(z), val = e_val(z);
-  if ((op & 64) || (op & 0xf0u) == 0) return (uint16_t)CK_SLOW;
+__device__ __forceinline__ uint16_t compact_dist_entry(uint32_t z, uint32_t add_bits = 0) {
+  const uint32_t op = e_op(z), bits = e_bits(z) + add_bits, val = e_val(z);
+  if (op & 64) return (uint16_t)CK_SLOW;
+  if ((op & 0xf0u) == 0) return (uint16_t)(CK_SLOW | (op << 2) | (val << 6));
   const uint32_t e = op & 15u;
   const uint32_t d = (e == 0) ? val - 1 : 2 * (e + 1) + ((val - 1) >> e) - 2;
   return (uint16_t)(CK_SYM | (bits << 2) | (d << 6));
 }
 
+typedef __attribute__((address_space(1))) const uint32_t gcu32;
+typedef __attribute__((address_space(1))) uint32_t gu32;
+typedef __attribute__((address_space(1))) const uint16_t gcu16;
+
+// masked input word: bytes at or past end_byte read as zero; never reads a
+// word that holds no input byte
+__device__ __forceinline__ uint32_t in_word_g(gcu32 *w, uint32_t wi, uint32_t end_byte) {
+  const uint32_t v = w[min(wi, (end_byte - 1u) >> 2)];
+  const uint32_t b = wi * 4u;
+  const uint32_t keep = b >= end_byte ? 0u : end_byte - b;
+  return keep >= 4u ? v : __builtin_amdgcn_ubfe(v, 0, 8u * keep);
+}
+
 enum { LM_SYM = 0, LM_BLOCK = 1, LM_DONE = 2 };
 
 struct LaneState {
-  const uint32_t *w;  // 4-byte aligned input base
+  gcu32 *w;           // 4-byte aligned input base
   uint32_t end_byte, limit;
-  uint32_t wi, nw, nbits;
+  uint32_t wi, nw, nkeep, nbits;  // nw: next input word, raw; nkeep: its valid bytes (0..4)
+  uint32_t lastw;     // last word index holding input
   uint64_t hold;
-  uint32_t *tok;      // token output (parse pass)
+  gu32 *tok;          // token output (parse pass)
   uint32_t ntok, tcap;
+  uint32_t gk;        // tokens of the current group (in LDS)
   uint32_t pos, cap;  // entries the tokens expand to / entry capacity
-  const uint32_t *zl, *zd;  // full zlib tables (global): slow path
+  uint32_t capx;      // min(cap, pos + tcap - ntok) at block start: one check covers both
+  gcu16 *cl, *cd;     // compact sub-tables (global) of the current block
+  const uint32_t *zl, *zd;  // zlib-layout tables (global): invalid-code reporting
   uint32_t zlmask, zdmask;
+  uint32_t lbits, dbits;    // root widths of the current block's zlib tables
   uint32_t stop, bit, whave;
   int mode, code, last;
 };
 
+// prefetch word wi raw; the end-of-input mask is applied when it is used, so
+// the load's latency hides behind the current symbol
+__device__ __forceinline__ void lane_fetch(LaneState &s) {
+  s.nw = s.w[min(s.wi, s.lastw)];
+  const uint32_t b = s.wi * 4u;
+  s.nkeep = b >= s.end_byte ? 0u : min(s.end_byte - b, 4u);
+}
+__device__ __forceinline__ uint32_t lane_take(const LaneState &s) {
+  return s.nkeep >= 4u ? s.nw : __builtin_amdgcn_ubfe(s.nw, 0, 8u * s.nkeep);
+}
 __device__ __forceinline__ void lane_prime(LaneState &s, uint32_t bit) {
+  s.lastw = (s.end_byte - 1u) >> 2;
   s.wi = bit >> 5;
-  const uint32_t w0 = in_word(s.w, s.wi, s.end_byte);
-  s.nw = in_word(s.w, s.wi + 1, s.end_byte);
+  const uint32_t w0 = in_word_g(s.w, s.wi, s.end_byte);
+  s.wi += 1;
+  lane_fetch(s);
   s.hold = (uint64_t)w0 >> (bit & 31);
   s.nbits = 32 - (bit & 31);
-  s.wi += 1;
 }
 __device__ __forceinline__ void lane_refill(LaneState &s) {
   if (s.nbits < 32) {
-    s.hold |= (uint64_t)s.nw << s.nbits;
+    s.hold |= (uint64_t)lane_take(s) << s.nbits;
     s.nbits += 32;
     s.wi++;
-    s.nw = in_word(s.w, s.wi, s.end_byte);
+    lane_fetch(s);
   }
 }
+// bit position of the next unconsumed bit (wi = index of the prefetched word)
 __device__ __forceinline__ uint32_t lane_pos(const LaneState &s) { return s.wi * 32u - s.nbits; }
 
-// zlib-table slow path: returns a compact-format entry whose bits field is the
-// TOTAL code length (may exceed 15 for the encoding; carried separately)
-__device__ __forceinline__ uint32_t slow_lookup(const uint32_t *zt, uint32_t zmask, uint64_t hold, bool lens,
-                                                uint32_t *total_bits) {
-  uint32_t z = zt[(uint32_t)hold & zmask];
+// zlib's two-level lookup (src/inffast.c:125-135) on the zlib-layout table;
+// used only to size an invalid code for the truncated-vs-invalid decision
+__device__ __noinline__ uint32_t invalid_code_bits(const uint32_t *zt, uint32_t zmask, uint32_t hold) {
+  uint32_t z = zt[hold & zmask];
   uint32_t used = e_bits(z);
   if (e_op(z) != 0 && (e_op(z) & 0xf0u) == 0) {
-    z = zt[e_val(z) + ((uint32_t)(hold >> used) & ((1u << e_op(z)) - 1u))];
+    z = zt[e_val(z) + ((hold >> used) & ((1u << e_op(z)) - 1u))];
     used += e_bits(z);
   }
-  *total_bits = used;
-  const uint32_t op = e_op(z);
-  if (lens) {
-    if (op & 32) return CK_EOB;
-    if (op & 64) return CK_SLOW;  // invalid literal/length code
-    return compact_len_entry(z) & ~(15u << 2);
-  }
-  if (op & 64) return CK_SLOW;  // invalid distance code
-  return compact_dist_entry(z) & ~(15u << 2);
+  return used;
 }
 
-// one symbol; returns true when the lane left symbol mode
-__device__ __forceinline__ bool lane_step(LaneState &s, const uint16_t *__restrict__ lt, const uint16_t *__restrict__ dt) {
+// one symbol; returns true when the lane left symbol mode.  Bits past the end
+// of the input read as zero; truncation is decided once the symbol is
+// complete (or, for an invalid code, from zlib's code length), which gives
+// the same ZD_TRUNC / error split as checking before every bit pull.
+__device__ __forceinline__ bool lane_step(LaneState &s, const uint16_t *__restrict__ lt, const uint16_t *__restrict__ dt,
+                                          uint32_t *__restrict__ tb) {
   lane_refill(s);
   uint32_t e = lt[(uint32_t)s.hold & (LROOT_N - 1)];
-  uint32_t used = (e >> 2) & 15u;
   if ((e & 3u) == CK_SLOW) {
-    e = slow_lookup(s.zl, s.zlmask, s.hold, true, &used);
-    if ((e & 3u) == CK_SLOW) {
-      if (lane_pos(s) + used > s.limit) {
-        s.code = ZD_TRUNC;
-      } else {
-        s.code = ZD_ERROR | (ZM_LITLEN_CODE << 8);
-      }
+    const uint32_t op = (e >> 2) & 15u;
+    uint32_t e2 = CK_SLOW;
+    if (op) e2 = s.cl[(e >> 6) + (((uint32_t)s.hold >> s.lbits) & ((1u << op) - 1u))];
+    if ((e2 & 3u) == CK_SLOW) {
+      const uint32_t used = invalid_code_bits(s.zl, s.zlmask, (uint32_t)s.hold);
+      s.code = lane_pos(s) + used > s.limit ? ZD_TRUNC : (ZD_ERROR | (ZM_LITLEN_CODE << 8));
       s.mode = LM_DONE;
       return true;
     }
+    e = e2;
   }
-  if (lane_pos(s) + used > s.limit) {
-    s.code = ZD_TRUNC;
-    s.mode = LM_DONE;
-    return true;
-  }
+  const uint32_t used = (e >> 2) & 15u;
   s.hold >>= used;
   s.nbits -= used;
   const uint32_t kind = e & 3u, sym = e >> 6;
-  if (kind == CK_SYM) {  // literal
-    if (s.pos >= s.cap || s.ntok >= s.tcap) {
-      s.code = ZD_FULL;
-      s.mode = LM_DONE;
-      return true;
+  uint32_t len = 1, dist = 0;
+  if (kind == CK_LEN) {
+    // length code sym (0..28): base/extra of src/inftrees.c:59-64, computed
+    uint32_t xb = 0;
+    if (sym < 8) {
+      len = sym + 3;
+    } else if (sym < 28) {
+      xb = (sym >> 2) - 1;
+      len = ((4u + (sym & 3u)) << xb) + 3u;
+    } else {
+      len = 258;
     }
-    s.tok[s.ntok++] = sym;
-    s.pos++;
-    return false;
+    len += (uint32_t)s.hold & ((1u << xb) - 1u);
+    s.hold >>= xb;
+    s.nbits -= xb;
+    lane_refill(s);
+    uint32_t d = dt[(uint32_t)s.hold & (DROOT_N - 1)];
+    if ((d & 3u) == CK_SLOW) {
+      const uint32_t op = (d >> 2) & 15u;
+      uint32_t d2 = CK_SLOW;
+      if (op) d2 = s.cd[(d >> 6) + (((uint32_t)s.hold >> s.dbits) & ((1u << op) - 1u))];
+      if ((d2 & 3u) == CK_SLOW) {
+        const uint32_t dused = invalid_code_bits(s.zd, s.zdmask, (uint32_t)s.hold);
+        s.code = lane_pos(s) + dused > s.limit ? ZD_TRUNC : (ZD_ERROR | (ZM_DIST_CODE << 8));
+        s.mode = LM_DONE;
+        return true;
+      }
+      d = d2;
+    }
+    const uint32_t dused = (d >> 2) & 15u, dsym = d >> 6;
+    uint32_t dx = 0;
+    if (dsym < 4) {
+      dist = dsym + 1;
+    } else {
+      dx = (dsym >> 1) - 1;
+      dist = ((2u + (dsym & 1u)) << dx) + 1u;
+    }
+    s.hold >>= dused;
+    dist += (uint32_t)s.hold & ((1u << dx) - 1u);
+    s.hold >>= dx;
+    s.nbits -= dused + dx;
+  }
+  if (lane_pos(s) > s.limit) {
+    s.code = ZD_TRUNC;
+    s.mode = LM_DONE;
+    return true;
   }
   if (kind == CK_EOB) {
     s.bit = lane_pos(s);
     s.mode = LM_BLOCK;
     return true;
   }
-  // length code sym (0..28): base/extra of src/inftrees.c:59-64, computed
-  uint32_t len, xb;
-  if (sym < 8) {
-    len = sym + 3;
-    xb = 0;
-  } else if (sym < 28) {
-    xb = (sym >> 2) - 1;
-    len = ((4u + (sym & 3u)) << xb) + 3u;
-  } else {
-    len = 258;
-    xb = 0;
-  }
-  len += (uint32_t)s.hold & ((1u << xb) - 1u);
-  s.hold >>= xb;
-  s.nbits -= xb;
-  lane_refill(s);
-  uint32_t d = dt[(uint32_t)s.hold & (DROOT_N - 1)];
-  uint32_t dused = (d >> 2) & 15u;
-  if ((d & 3u) == CK_SLOW) {
-    d = slow_lookup(s.zd, s.zdmask, s.hold, false, &dused);
-    if ((d & 3u) == CK_SLOW) {
-      if (lane_pos(s) + dused > s.limit) {
-        s.code = ZD_TRUNC;
-      } else {
-        s.code = ZD_ERROR | (ZM_DIST_CODE << 8);
-      }
-      s.mode = LM_DONE;
-      return true;
-    }
-  }
-  const uint32_t dsym = d >> 6;
-  uint32_t dist, dx;
-  if (dsym < 4) {
-    dist = dsym + 1;
-    dx = 0;
-  } else {
-    dx = (dsym >> 1) - 1;
-    dist = ((2u + (dsym & 1u)) << dx) + 1u;
-  }
-  if (lane_pos(s) + dused + dx > s.limit) {
-    s.code = ZD_TRUNC;
-    s.mode = LM_DONE;
-    return true;
-  }
-  s.hold >>= dused;
-  s.nbits -= dused;
-  dist += (uint32_t)s.hold & ((1u << dx) - 1u);
-  s.hold >>= dx;
-  s.nbits -= dx;
-  if (s.pos + len > s.cap || s.ntok >= s.tcap) {
+  if (s.pos + len > s.capx) {
     s.code = ZD_FULL;
     s.mode = LM_DONE;
     return true;
@@ -212,7 +223,9 @@ __device__ __forceinline__ bool lane_step(LaneState &s, const uint16_t *__restri
     s.mode = LM_DONE;
     return true;
   }
-  s.tok[s.ntok++] = (len << 16) | (dist - 1u);
+  tb[s.gk * WAVE] = kind == CK_SYM ? sym : ((len << 16) | (dist - 1u));
+  s.gk++;
+  s.ntok++;
   s.pos += len;
   return false;
 }
@@ -228,14 +241,26 @@ struct StageBits {
   }
 };
 
+// Symbol steps run in groups of GROUP; each lane's tokens of a group wait in
+// LDS (tokbuf, which shares space with the header build area: headers are
+// only processed between groups) and leave in one flush, so the step loop
+// itself issues no global stores (vmcnt is in-order: a store in the loop
+// would make every input refill wait for it).
+#define GROUP 16
+
 struct LaneLDS {
   uint16_t lroot[WAVE][LROOT_N];
   uint16_t droot[WAVE][DROOT_N];
-  uint32_t stage[STAGE_WORDS + 4];
-  uint32_t tab[ZBUILD];
-  uint16_t lens[320];
-  uint16_t sorted[320];
-  uint32_t scr[32];
+  union {
+    struct {
+      uint32_t stage[STAGE_WORDS + 4];
+      uint32_t tab[ZBUILD];
+      uint16_t lens[320];
+      uint16_t sorted[320];
+      uint32_t scr[32];
+    };
+    uint32_t tokbuf[GROUP][WAVE];
+  };
 };
 
 __device__ void stage_bits(LaneLDS &L, const uint32_t *w, uint32_t end_byte, uint32_t bit, StageBits &sb) {
@@ -270,9 +295,10 @@ __device__ void install_roots(LaneLDS &L, uint32_t ln, const uint32_t *zl, uint3
 // (src/inflate.c:834-1033); installs the lane's tables.
 __device__ void coop_block(LaneState &s, uint32_t ln, LaneLDS &L, uint32_t *lane_tab, const uint32_t *fixed) {
   const uint32_t lane = lane_id();
-  const uint32_t *w = reinterpret_cast<const uint32_t *>(readlane_ptr(s.w, ln));
-  uint32_t *tok = reinterpret_cast<uint32_t *>(readlane_ptr(s.tok, ln));
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(readlane_ptr((const void *)(uintptr_t)s.w, ln));
+  uint32_t *tok = reinterpret_cast<uint32_t *>(readlane_ptr((const void *)(uintptr_t)s.tok, ln));
   uint32_t *tabg = reinterpret_cast<uint32_t *>(readlane_ptr(lane_tab, ln));
+  uint16_t *ctab = reinterpret_cast<uint16_t *>(tabg + TABLE_ENTRIES);  // compact sub-tables
   uint32_t ntok = __builtin_amdgcn_readlane(s.ntok, ln);
   const uint32_t tcap = __builtin_amdgcn_readlane(s.tcap, ln);
   const uint32_t end_byte = __builtin_amdgcn_readlane(s.end_byte, ln);
@@ -431,7 +457,10 @@ __device__ void coop_block(LaneState &s, uint32_t ln, LaneLDS &L, uint32_t *lane
       break;
     }
     __builtin_amdgcn_wave_barrier();
-    for (uint32_t i = lane; i < ZBUILD; i += WAVE) tabg[i] = L.tab[i];
+    for (uint32_t i = lane; i < ZBUILD; i += WAVE) {
+      tabg[i] = L.tab[i];
+      ctab[i] = compact_len_entry(L.tab[i], lbits);
+    }
     for (uint32_t i = lane; i < LROOT_N; i += WAVE) L.lroot[ln][i] = compact_len_entry(L.tab[i & ((1u << lbits) - 1u)]);
     __builtin_amdgcn_wave_barrier();
     dbits = 6;
@@ -440,7 +469,10 @@ __device__ void coop_block(LaneState &s, uint32_t ln, LaneLDS &L, uint32_t *lane
       break;
     }
     __builtin_amdgcn_wave_barrier();
-    for (uint32_t i = lane; i < 592; i += WAVE) tabg[DIST_TABLE_OFF + i] = L.tab[i];
+    for (uint32_t i = lane; i < 592; i += WAVE) {
+      tabg[DIST_TABLE_OFF + i] = L.tab[i];
+      ctab[DIST_TABLE_OFF + i] = compact_dist_entry(L.tab[i], dbits);
+    }
     L.droot[ln][lane] = compact_dist_entry(L.tab[lane & ((1u << dbits) - 1u)]);
     __builtin_amdgcn_wave_barrier();
     zl = tabg;
@@ -459,6 +491,11 @@ __device__ void coop_block(LaneState &s, uint32_t ln, LaneLDS &L, uint32_t *lane
       s.zd = zd;
       s.zlmask = (1u << lbits) - 1u;
       s.zdmask = (1u << dbits) - 1u;
+      s.lbits = lbits;
+      s.dbits = dbits;
+      s.cl = (gcu16 *)ctab;
+      s.cd = (gcu16 *)(ctab + DIST_TABLE_OFF);
+      s.capx = min(cap, pos + (tcap - ntok));
       lane_prime(s, bit);
     } else {
       s.code = code;
@@ -492,9 +529,12 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
   s.zl = fixed;
   s.zd = fixed + 512;
   s.zlmask = s.zdmask = 0;
-  s.wi = s.nw = s.nbits = 0;
+  s.lbits = s.dbits = 0;
+  s.capx = 0;
+  s.wi = s.nw = s.nkeep = s.nbits = s.lastw = s.gk = 0;
   s.hold = 0;
-  uint32_t *lane_tab = tables + (size_t)min(c, nchunks - 1) * TABLE_ENTRIES;
+  uint32_t *lane_tab = tables + (size_t)min(c, nchunks - 1) * TABLE_STRIDE;
+  s.cl = s.cd = (gcu16 *)(lane_tab + TABLE_ENTRIES);
   if (c < nchunks) {
     const ZsChunkDev ch = chunks[c];
     const ZsHeadDev hd = heads[ch.job];
@@ -503,10 +543,10 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
     const uint32_t mis = (uint32_t)(ip & 3u);
     const uint32_t start = ch.ord == 0 ? (mis + (uint32_t)hd.start_byte) * 8u : ch.start_bit;
     if (hd.code == ZD_END && start != ZS_NONE) {
-      s.w = reinterpret_cast<const uint32_t *>(ip - mis);
+      s.w = (gcu32 *)(ip - mis);
       s.end_byte = mis + (uint32_t)jb.in_len;
       s.limit = s.end_byte * 8u;
-      s.tok = tokens + ch.tok;
+      s.tok = (gu32 *)(tokens + ch.tok);
       s.tcap = ch.tcap;
       s.cap = ch.cap;
       s.whave = ch.ord == 0 ? 0u : HIST;
@@ -524,6 +564,7 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
   }
   const uint16_t *lt = L.lroot[lane];
   const uint16_t *dt = L.droot[lane];
+  uint32_t *tb = &L.tokbuf[0][lane];
   for (;;) {
     uint64_t need = __ballot(s.mode == LM_BLOCK);
     while (need) {
@@ -532,10 +573,17 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
       coop_block(s, ln, L, lane_tab, fixed);
     }
     if (__ballot(s.mode == LM_SYM) == 0) break;
+    s.gk = 0;
     if (s.mode == LM_SYM) {
-      for (int it = 0; it < 64; it++)
-        if (lane_step(s, lt, dt)) break;
+      for (int it = 0; it < GROUP; it++)
+        if (lane_step(s, lt, dt, tb)) break;
     }
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t g0 = s.ntok - s.gk;
+#pragma unroll
+    for (uint32_t j = 0; j < GROUP; j++)
+      if (j < s.gk) s.tok[g0 + j] = L.tokbuf[j][lane];
+    __builtin_amdgcn_wave_barrier();  // tokbuf area is reused by the next header build
   }
   if (c < nchunks) {
     ZsChunkDev *ch = &chunks[c];

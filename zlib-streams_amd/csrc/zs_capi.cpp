@@ -37,7 +37,7 @@ extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_hea
 
 namespace {
 
-constexpr size_t TABLE_ENTRIES_HOST = 1448;  // must match TABLE_ENTRIES (zs_device.h)
+constexpr size_t TABLE_ENTRIES_HOST = 1448 + 724;  // must match TABLE_STRIDE (zs_device.h)
 
 const char *const kMsgs[ZM_COUNT] = {
     nullptr,
@@ -98,7 +98,7 @@ struct Workspace {
   size_t cap_chunks = 0;
   ZsChunkDev *d_chunks = nullptr, *h_chunks = nullptr;
   uint32_t *d_find = nullptr, *h_find = nullptr;
-  uint32_t *d_tables = nullptr;  // TABLE_ENTRIES per chunk
+  uint32_t *d_tables = nullptr;  // TABLE_STRIDE words per chunk
   uint8_t *d_windows = nullptr;  // 32 KiB per chunk
   size_t cap_scratch = 0;        // u16 entries (and u32 parse tokens, same count)
   uint16_t *d_scratch = nullptr;

@@ -5,6 +5,7 @@
 
 #define WAVE 64
 #define TABLE_ENTRIES 1448   // ENOUGH (852 + 594), src/inftrees.h:52-55
+#define TABLE_STRIDE (TABLE_ENTRIES + TABLE_ENTRIES / 2)  // + compact u16 copy (lane decoder)
 #define DIST_TABLE_OFF 852   // distance table follows the literal/length table
 
 // ---------------------------------------------------------------------------
