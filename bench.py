@@ -9,8 +9,9 @@ Prints ONE JSON line (rank 0) with the driver's contract fields plus
   roofline     -- decode kernel: algorithmic bytes (compressed in + decompressed
                   out) per launch / average decode-kernel time measured with HIP
                   events on the launch stream, vs 8 TB/s HBM peak;
-  cpu_baseline -- host zlib inflate on a bounded sample of the same streams,
-                  timed on this host (1 thread, and all threads).
+  cpu_baseline -- host zlib inflate on a bounded sample of the same streams
+                  (>= --cpu-seconds of 1-thread work), timed on this host on
+                  1 thread and on all threads, plus the oracle port on 1 thread.
 """
 import argparse
 import ctypes
@@ -32,9 +33,11 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(comps, raws, wbits, sample, threads):
-    """Host zlib inflate of `sample` streams (whole-buffer Z_FINISH), 1 thread
-    and `threads` threads.  Returns the cpu_baseline JSON object."""
+def cpu_baseline(comps, raws, wbits, sample, threads, min_seconds):
+    """Host zlib inflate of `sample` streams (whole-buffer Z_FINISH) on 1 thread,
+    repeated until `min_seconds` of CPU work, then on `threads` threads; plus
+    the oracle's C restatement (oracle/zo_inflate.c) on 1 thread over the first
+    8 sample streams.  Returns the cpu_baseline JSON object."""
     import numpy as np
 
     so = os.path.join(ROOT, "oracle", "libzs_cpubase.so")
@@ -44,25 +47,41 @@ def cpu_baseline(comps, raws, wbits, sample, threads):
                                  ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
                                  ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_int)]
     L.zs_cpu_zlib_version.restype = ctypes.c_char_p
-    n = len(sample)
-    cp = (ctypes.c_void_p * n)(*[comps[i].ctypes.data for i in sample])
-    cl = (ctypes.c_size_t * n)(*[len(comps[i]) for i in sample])
-    outs = [np.empty(len(raws[i]), dtype=np.uint8) for i in sample]
-    op = (ctypes.c_void_p * n)(*[o.ctypes.data for o in outs])
-    cap = max(len(raws[i]) for i in sample)
-    tot = ctypes.c_uint64()
-    bad = ctypes.c_int()
-    t1 = L.zs_cpu_inflate(cp, cl, op, cap, n, 1, wbits, 0, ctypes.byref(tot), ctypes.byref(bad))
-    v1 = tot.value / t1 / 2**20
-    tn = L.zs_cpu_inflate(cp, cl, op, cap, n, threads, wbits, 0, ctypes.byref(tot), ctypes.byref(bad))
-    vn = tot.value / tn / 2**20
-    ok = all(np.array_equal(outs[k], raws[i]) for k, i in enumerate(sample)) and not bad.value
-    return {"value": round(v1, 1), "unit": "MiB/s", "cores": 1, "kind": "reference",
-            "impl": f"host zlib {L.zs_cpu_zlib_version().decode()} inflate (upstream of reference src/inflate.c "
-                    "for windowBits -15; the reference build itself needs the absent zlib submodule)",
-            "sample": f"{n} of the streams (alternating Zipf/lines), whole-buffer inflate(Z_FINISH), "
-                      f"{tot.value / 2**20:.0f} MiB out per pass",
-            "value_all_threads": round(vn, 1), "threads": threads, "seconds_1t": round(t1, 2), "verified": ok}
+
+    def run(ids, nthreads, use_oracle, outs):
+        n = len(ids)
+        cp = (ctypes.c_void_p * n)(*[comps[i].ctypes.data for i in ids])
+        cl = (ctypes.c_size_t * n)(*[len(comps[i]) for i in ids])
+        op = (ctypes.c_void_p * n)(*[outs[i].ctypes.data for i in ids])
+        cap = max(len(raws[i]) for i in ids)
+        tot = ctypes.c_uint64()
+        bad = ctypes.c_int()
+        t = L.zs_cpu_inflate(cp, cl, op, cap, n, nthreads, wbits, use_oracle, ctypes.byref(tot), ctypes.byref(bad))
+        ok = not bad.value and all(np.array_equal(outs[i], raws[i]) for i in ids)
+        return t, tot.value, ok
+
+    outs = {i: np.empty(len(raws[i]), dtype=np.uint8) for i in sample}
+    t1 = b1 = 0
+    passes = 0
+    ok = True
+    while t1 < min_seconds or passes == 0:
+        t, b, k = run(sample, 1, 0, outs)
+        t1, b1, ok, passes = t1 + t, b1 + b, ok and k, passes + 1
+    tn = bn = 0
+    for _ in range(passes):
+        t, b, k = run(sample, threads, 0, outs)
+        tn, bn, ok = tn + t, bn + b, ok and k
+    psample = sample[:8]
+    tp, bp, kp = run(psample, 1, 1, outs)
+    return {"value": round(b1 / t1 / 2**20, 1), "unit": "MiB/s", "cores": 1, "kind": "reference",
+            "impl": f"host zlib {L.zs_cpu_zlib_version().decode()} inflate: upstream of the reference's src/inflate.c "
+                    "for windowBits -15 (the reference build needs its absent zlib submodule headers)",
+            "sample": f"{len(sample)} streams x {passes} pass(es), whole-buffer inflate(Z_FINISH), "
+                      f"{b1 / 2**20:.0f} MiB out, {t1:.1f} s on 1 thread",
+            "value_all_threads": round(bn / tn / 2**20, 1), "threads": threads,
+            "value_port_1t": round(bp / tp / 2**20, 1),
+            "port_sample": f"oracle/zo_inflate.c (C restatement) on {len(psample)} streams, 1 thread",
+            "verified": bool(ok and kp)}
 
 
 def main():
@@ -73,7 +92,10 @@ def main():
     ap.add_argument("--streams", type=int, default=64)
     ap.add_argument("--stream-mib", type=int, default=64)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=8)
+    ap.add_argument("--cpu-sample", type=int, default=64, help="streams in the CPU baseline sample")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="minimum 1-thread CPU baseline work")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json"),
+                    help="PMC-derived HBM bytes per pipeline launch (null in the line when absent)")
     args = ap.parse_args()
 
     import numpy as np
@@ -92,6 +114,7 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
 
     import corpus
+    import shard
     import zstreams
 
     nbytes = args.stream_mib << 20
@@ -151,29 +174,29 @@ def main():
         tdist.barrier()
     t_el = time.perf_counter() - t_start
     k_ms, b_ms, k_n = zstreams.profile_read()
+    stage_ms = zstreams.profile_stages()
     stats = zstreams.last_stats()
     zstreams.profile(False)
-    if dist:
-        t = torch.tensor([t_el], dtype=torch.float64, device=dev)
-        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        t_el = float(t.item())
-        okt = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
-        tdist.all_reduce(okt, op=tdist.ReduceOp.MIN)
-        ok = bool(okt.item())
+    # max elapsed over ranks, summed decompressed bytes, all ranks verified
+    t_el, out_bytes, ok = shard.reduce_counters(t_el, args.streams * nbytes * args.steps, ok, device=dev)
 
-    out_bytes = world * args.streams * nbytes * args.steps
     value = out_bytes / t_el / 2**20
     per_launch_alg = comp_total + args.streams * nbytes  # algorithmic bytes of one decode launch
     k_avg_s = (k_ms / max(k_n, 1)) / 1e3
     achieved = per_launch_alg / k_avg_s / 1e9 if k_avg_s > 0 else 0.0
 
+    traffic = None
+    if args.traffic_json and os.path.exists(args.traffic_json):
+        # HBM bytes per launch from rocprofv3 PMC passes (tools/pmc_traffic.py)
+        traffic = json.load(open(args.traffic_json)).get("hbm_bytes_per_launch")
+
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
-        sample = list(range(0, args.streams, max(1, args.streams // args.cpu_sample)))[:args.cpu_sample]
-        # alternate Zipf / lines in the sample
-        sample = sorted(set(sample[: len(sample) // 2] + [s + args.streams // 2 for s in sample[: len(sample) // 2]]))
-        sample = [s for s in sample if s < args.streams]
-        cpu = cpu_baseline(comps, raws, -15, sample, host_threads)
+        # interleave Zipf (first half) and lines (second half) streams
+        half = args.streams // 2
+        order = [x for k in range(half) for x in (k, k + half)] + list(range(2 * half, args.streams))
+        sample = order[:max(1, args.cpu_sample)]
+        cpu = cpu_baseline(comps, raws, -15, sample, host_threads, args.cpu_seconds)
 
     if rank == 0:
         line = {
@@ -187,10 +210,12 @@ def main():
                        "parallelism": f"stream-shard x{world}"},
             "verified_bit_exact": ok,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                         "kernel": "zs_lane_kernel" if stats["chunked_jobs"] else "zs_decode_kernel<false>",
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                         "kernel": "inflate pipeline (find+parse+expand+link+emit+serial decode)",
                          "kernel_ms_avg": round(k_avg_s * 1e3, 3), "batch_ms_avg": round(b_ms / max(k_n, 1), 3),
-                         "alg_bytes_per_launch": per_launch_alg},
+                         "alg_bytes_per_launch": per_launch_alg,
+                         "stages_ms_avg": {k: round(v / max(k_n, 1), 3) for k, v in stage_ms.items()},
+                         "stage_kernels": zstreams.STAGE_KERNELS},
             "cpu_baseline": cpu,
             "path_stats": stats,
         }

@@ -87,9 +87,14 @@ int zs_inflate_batch(const zs_job *jobs, uint32_t n, zs_result *results, uint32_
 /* launch on this HIP stream (hipStream_t); NULL = the library's own stream */
 int zs_set_stream(void *hip_stream);
 int zs_synchronize(void);
-/* decode-kernel timing via HIP events on the launch stream */
+/* kernel timing via HIP events on the launch stream (enable resets the sums) */
 int zs_profile(int enable);
+/* accumulated ms: inflate pipeline (find .. serial decode), whole batches; batch count */
 int zs_profile_read(double *decode_ms, double *batch_ms, uint64_t *launches);
+/* accumulated ms per stage, in this order: header, find, parse, expand, link,
+   emit, serial decode, finalize.  Returns the number of entries written. */
+#define ZS_PROF_STAGES 8
+int zs_profile_stages(double *ms, uint32_t n);
 /* last batch: [jobs on the chunked path, chunks, chunked jobs that fell back
    to the serial decoder, jobs on the serial path] */
 int zs_last_stats(uint32_t out[4]);

@@ -1,0 +1,87 @@
+"""Multi-GPU sharding logic on CPU: LPT partition properties and a
+world_size-2 gloo run (every rank derives the same partition independently,
+the shards tile the job list, and the counter reduction gives max time /
+summed bytes / all-ok).  SURVEY.md §8e."""
+import os
+import random
+import socket
+
+import pytest
+
+import shard
+
+
+def test_lpt_partition_tiles_jobs():
+    rng = random.Random(7)
+    costs = [rng.randint(1, 1 << 22) for _ in range(4096)]
+    for world in (1, 2, 4, 8):
+        shards = shard.lpt_partition(costs, world)
+        flat = sorted(i for s in shards for i in s)
+        assert flat == list(range(len(costs)))
+        loads = shard.shard_loads(costs, shards)
+        # LPT bound: max load <= avg + largest job
+        assert max(loads) <= sum(costs) / world + max(costs)
+
+
+def test_lpt_partition_deterministic_and_balanced():
+    costs = [5, 5, 4, 4, 3, 3, 3]
+    a = shard.lpt_partition(costs, 2)
+    b = shard.lpt_partition(list(costs), 2)
+    assert a == b
+    loads = shard.shard_loads(costs, a)
+    assert max(loads) - min(loads) <= 3
+    assert shard.lpt_partition([], 3) == [[], [], []]
+    with pytest.raises(ValueError):
+        shard.lpt_partition(costs, 0)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, costs, q):
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        mine = shard.my_shard(costs, rank, world)
+        gathered = [None] * world
+        dist.all_gather_object(gathered, mine)
+        nbytes = sum(costs[i] for i in mine)
+        t, b, ok = shard.reduce_counters(0.5 + rank, nbytes, True)
+        _, _, ok_one_bad = shard.reduce_counters(0.0, 0, rank == 0)
+        q.put((rank, gathered, t, b, ok and not ok_one_bad))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_shards_and_counters():
+    import torch.multiprocessing as mp
+
+    rng = random.Random(11)
+    costs = [rng.randint(1, 1 << 20) for _ in range(257)]
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, costs, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res.sort()
+    g0 = res[0][1]
+    assert all(r[1] == g0 for r in res)  # every rank derived the same partition
+    assert sorted(i for s in g0 for i in s) == list(range(len(costs)))
+    for rank, _, t, b, ok in res:
+        assert t == 1.5  # max over ranks
+        assert b == sum(costs)
+        assert ok

@@ -429,10 +429,16 @@ extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_hea
                                   uint16_t *d_scratch, uint32_t *d_tokens, uint32_t *d_tables, const uint32_t *d_fixed,
                                   uint8_t *d_windows, ZsDecDev *d_decs, uint32_t *d_fallback, hipStream_t st,
                                   hipEvent_t *ev) {
+  // ev (profiling, optional): [0] before find, [1] after find, [2] after parse,
+  // [3] after expand, [4] after link, [5] after emit
+  if (ev) (void)hipEventRecord(ev[0], st);
   if (nfind) hipLaunchKernelGGL(zs_find_kernel, dim3(nfind), dim3(64), 0, st, d_jobs, d_heads, d_chunks, d_find_ids);
-  zs_launch_lane(d_jobs, d_heads, d_chunks, nchunks, d_scratch, d_tokens, d_tables, d_fixed, st, ev);
+  if (ev) (void)hipEventRecord(ev[1], st);
+  zs_launch_lane(d_jobs, d_heads, d_chunks, nchunks, d_scratch, d_tokens, d_tables, d_fixed, st, ev ? ev + 2 : nullptr);
   hipLaunchKernelGGL(zs_link_kernel, dim3(ncjobs), dim3(LINK_THREADS), 0, st, d_jobs, d_heads, d_chunks, d_cjobs,
                      d_scratch, d_windows, d_decs, d_fallback);
+  if (ev) (void)hipEventRecord(ev[4], st);
   hipLaunchKernelGGL(zs_emit_kernel, dim3(nchunks), dim3(EMIT_THREADS), 0, st, d_jobs, d_chunks, d_scratch, d_windows,
                      d_fallback);
+  if (ev) (void)hipEventRecord(ev[5], st);
 }

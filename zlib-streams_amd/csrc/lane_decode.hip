@@ -761,9 +761,10 @@ __global__ void __launch_bounds__(EXP_T) zs_expand_kernel(const ZsJobDev *__rest
 extern "C" void zs_launch_lane(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, ZsChunkDev *d_chunks, uint32_t nchunks,
                                uint16_t *d_scratch, uint32_t *d_tokens, uint32_t *d_tables, const uint32_t *d_fixed,
                                hipStream_t st, hipEvent_t *ev) {
-  if (ev) (void)hipEventRecord(ev[0], st);
+  // ev (profiling, optional): [0] after parse, [1] after expand
   hipLaunchKernelGGL(zs_lane_kernel, dim3((nchunks + WAVE - 1) / WAVE), dim3(WAVE), 0, st, d_jobs, d_heads, d_chunks,
                      nchunks, d_tokens, d_tables, d_fixed);
+  if (ev) (void)hipEventRecord(ev[0], st);
   hipLaunchKernelGGL(zs_expand_kernel, dim3(nchunks), dim3(EXP_T), 0, st, d_jobs, d_chunks, d_scratch, d_tokens);
   if (ev) (void)hipEventRecord(ev[1], st);
 }

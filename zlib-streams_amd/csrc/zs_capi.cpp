@@ -106,7 +106,11 @@ struct Workspace {
   uint32_t *d_fixed = nullptr;
   // timing (zs_profile): events on the launch stream
   bool prof = false;
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  // boundaries: [0] batch start, [1] after header, [2] after find, [3] after
+  // parse, [4] after expand, [5] after link, [6] after emit, [7] after the
+  // serial decoders, [8] after finalize
+  hipEvent_t ev[ZS_PROF_STAGES + 1] = {};
+  double prof_stage[ZS_PROF_STAGES] = {};
   double prof_ms = 0.0, prof_batch_ms = 0.0;
   uint64_t prof_launches = 0;
   // last batch: chunked jobs, chunks, chunked jobs that fell back, serial jobs
@@ -351,21 +355,20 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
   HIP_OK(hipMemcpyAsync(g_ws.d_jobs, g_ws.h_jobs, nv * sizeof(ZsJobDev), hipMemcpyHostToDevice, st));
   HIP_OK(hipMemcpyAsync(g_ws.d_ids, g_ws.h_ids, nv * sizeof(uint32_t), hipMemcpyHostToDevice, st));
   hipEvent_t *ev = g_ws.prof ? g_ws.ev : nullptr;
-  if (ev) HIP_OK(hipEventRecord(ev[2], st));
+  if (ev) HIP_OK(hipEventRecord(ev[0], st));
   zs_launch_header(g_ws.d_jobs, g_ws.d_heads, nv, st);
   if (n_cj)
     zs_launch_chunked(g_ws.d_jobs, g_ws.d_heads, g_ws.d_chunks, (uint32_t)nchunks, g_ws.d_find, nfind, g_ws.d_cjobs, n_cj,
                       g_ws.d_scratch, g_ws.d_tokens, g_ws.d_tables, g_ws.d_fixed, g_ws.d_windows, g_ws.d_decs,
-                      g_ws.d_fallback, st, ev);
-  else if (ev) {
-    HIP_OK(hipEventRecord(ev[0], st));
-  }
+                      g_ws.d_fallback, st, ev ? ev + 1 : nullptr);
+  else if (ev)
+    for (int i = 1; i <= 6; i++) HIP_OK(hipEventRecord(ev[i], st));
   zs_launch_decode(0, g_ws.d_jobs, g_ws.d_heads, g_ws.d_ids, n_std, g_ws.d_decs, nullptr, st);
   zs_launch_decode(1, g_ws.d_jobs, g_ws.d_heads, g_ws.d_ids + n_std, n_d64, g_ws.d_decs, nullptr, st);
   if (n_cj) zs_launch_decode(0, g_ws.d_jobs, g_ws.d_heads, g_ws.d_ids + n_std + n_d64, n_cj, g_ws.d_decs, g_ws.d_fallback, st);
-  if (ev && !n_cj) HIP_OK(hipEventRecord(ev[1], st));
+  if (ev) HIP_OK(hipEventRecord(ev[7], st));
   zs_launch_finish(g_ws.d_jobs, g_ws.d_heads, g_ws.d_decs, g_ws.d_checks, g_ws.d_res, nv, st);
-  if (ev) HIP_OK(hipEventRecord(ev[3], st));
+  if (ev) HIP_OK(hipEventRecord(ev[8], st));
   {
     hipError_t le = hipGetLastError();
     if (le != hipSuccess) {
@@ -377,8 +380,13 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
   HIP_OK(hipStreamSynchronize(st));
   if (ev) {
     float ms = 0.f, bms = 0.f;
-    HIP_OK(hipEventElapsedTime(&ms, ev[0], ev[1]));
-    HIP_OK(hipEventElapsedTime(&bms, ev[2], ev[3]));
+    HIP_OK(hipEventElapsedTime(&ms, ev[1], ev[7]));
+    HIP_OK(hipEventElapsedTime(&bms, ev[0], ev[8]));
+    for (int i = 0; i < ZS_PROF_STAGES; i++) {
+      float sm = 0.f;
+      HIP_OK(hipEventElapsedTime(&sm, ev[i], ev[i + 1]));
+      g_ws.prof_stage[i] += sm;
+    }
     g_ws.prof_ms += ms;
     g_ws.prof_batch_ms += bms;
     g_ws.prof_launches++;
@@ -573,16 +581,19 @@ int zs_set_stream(void *s) {
 }
 
 // Timing with HIP events on the launch stream: enable (1) / disable (0).
-// zs_profile_read returns the accumulated milliseconds of the dominant decode
-// kernel (the lane decoder when any job took the chunked path, else the serial
-// decoder), of whole batches (header .. finalize), and the number of batches.
+// zs_profile_read returns the accumulated milliseconds of the inflate pipeline
+// (find .. serial decoders: everything between header parse and finalize), of
+// whole batches (header .. finalize), and the number of batches;
+// zs_profile_stages the per-kernel split (ZS_PROF_STAGES entries, order in the
+// public header).
 int zs_profile(int enable) {
   std::lock_guard<std::mutex> lk(g_mu);
   int r = ws_init();
   if (r) return r;
   if (!g_ws.ev[0])
-    for (int i = 0; i < 4; i++) HIP_OK(hipEventCreate(&g_ws.ev[i]));
+    for (int i = 0; i <= ZS_PROF_STAGES; i++) HIP_OK(hipEventCreate(&g_ws.ev[i]));
   g_ws.prof = enable != 0;
+  for (int i = 0; i < ZS_PROF_STAGES; i++) g_ws.prof_stage[i] = 0.0;
   g_ws.prof_ms = 0.0;
   g_ws.prof_batch_ms = 0.0;
   g_ws.prof_launches = 0;
@@ -594,6 +605,13 @@ int zs_profile_read(double *decode_ms, double *batch_ms, uint64_t *launches) {
   *batch_ms = g_ws.prof_batch_ms;
   *launches = g_ws.prof_launches;
   return 0;
+}
+
+int zs_profile_stages(double *ms, uint32_t n) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  const uint32_t k = n < ZS_PROF_STAGES ? n : ZS_PROF_STAGES;
+  for (uint32_t i = 0; i < k; i++) ms[i] = g_ws.prof_stage[i];
+  return (int)k;
 }
 
 int zs_last_stats(uint32_t out[4]) {

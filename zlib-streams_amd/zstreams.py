@@ -44,6 +44,7 @@ _SIGS = {
     "zs_profile": (ctypes.c_int, [ctypes.c_int]),
     "zs_profile_read": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                        ctypes.POINTER(ctypes.c_uint64)]),
+    "zs_profile_stages": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.c_uint32]),
     "zs_last_stats": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint32)]),
     "zs_synchronize": (ctypes.c_int, []),
     "zs_version": (ctypes.c_char_p, []), "zs_last_error": (ctypes.c_char_p, []),
@@ -142,12 +143,30 @@ def profile(enable):
 
 
 def profile_read():
-    """(decode-kernel ms, whole-batch ms, batches) accumulated since profile(True)."""
+    """(inflate-pipeline ms, whole-batch ms, batches) accumulated since profile(True).
+
+    The pipeline is every kernel between the header parse and the finalize
+    (find, parse, expand, link, emit, serial decode)."""
     ms = ctypes.c_double()
     bms = ctypes.c_double()
     n = ctypes.c_uint64()
     _check(lib().zs_profile_read(ctypes.byref(ms), ctypes.byref(bms), ctypes.byref(n)))
     return ms.value, bms.value, n.value
+
+
+PROFILE_STAGES = ("header", "find", "parse", "expand", "link", "emit", "serial_decode", "finalize")
+STAGE_KERNELS = {"header": "zs_header_kernel", "find": "zs_find_kernel", "parse": "zs_lane_kernel",
+                 "expand": "zs_expand_kernel", "link": "zs_link_kernel", "emit": "zs_emit_kernel",
+                 "serial_decode": "zs_decode_kernel", "finalize": "zs_check_kernel + zs_finalize_kernel"}
+
+
+def profile_stages():
+    """Accumulated ms per pipeline stage since profile(True), keyed by PROFILE_STAGES."""
+    a = (ctypes.c_double * len(PROFILE_STAGES))()
+    k = lib().zs_profile_stages(a, len(PROFILE_STAGES))
+    if k < 0:
+        _check(k)
+    return {PROFILE_STAGES[i]: a[i] for i in range(k)}
 
 
 def last_stats():
