@@ -348,16 +348,17 @@ __device__ void coop_block(LaneState &s, uint32_t ln, LaneLDS &L, uint32_t *lane
         code = ZD_TRUNC;
         break;
       }
-      if (pos + n > cap || ntok + 2 > tcap) {
+      if (pos + n > cap || ntok + n > tcap) {
         code = ZD_FULL;
         break;
       }
-      if (n) {  // stored run token + input byte offset (expanded by zs_expand_kernel)
-        if (lane == 0) {
-          tok[ntok] = (TOK_STORED << 16) | (n - 1u);
-          tok[ntok + 1] = bit / 8;
+      {  // stored bytes become literal tokens (coalesced: 64 per store)
+        const uint32_t b0 = bit / 8;
+        for (uint32_t k = lane; k < n; k += WAVE) {
+          const uint32_t b = b0 + k;
+          tok[ntok + k] = (w[b >> 2] >> (8u * (b & 3u))) & 0xffu;
         }
-        ntok += 2;
+        ntok += n;
       }
       pos += n;
       bit += n * 8;
@@ -600,9 +601,13 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
 // threads produce 256 consecutive entries in parallel: a max-scan over
 // round-stamped token-start marks finds each entry's token, sources before the
 // round come from the ring (markers 256 + w for positions before the chunk),
-// sources inside the round are resolved by pointer jumping through LDS (rare:
-// only distances shorter than the round reach into it).  Output leaves the ring
-// in 4 KiB pieces (16 B per thread).
+// sources inside the round are resolved by pointer jumping through LDS (only
+// distances shorter than the round reach into it).  Three barriers per round:
+//   B1 marks visible (and the previous round's ring writes),
+//   B2 per-wave max-scan totals visible,
+//   B3 every ring read of the round done + per-wave "unresolved" flags visible.
+// Output leaves the ring in 4 KiB pieces (16 B per thread) after B1, when every
+// entry before the round is in the ring.
 // ---------------------------------------------------------------------------
 #define EXP_T 256       // threads = tokens per batch = entries per round
 #define EXP_W (EXP_T / WAVE)
@@ -626,6 +631,13 @@ __device__ __forceinline__ uint32_t wave_scan_max(uint32_t v) {  // inclusive, w
   v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));
   return v;
 }
+__device__ __forceinline__ void exp_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+#define TV_LIT 0x80000000u  // s_tval: literal byte | TV_LIT, else match distance
 
 __global__ void __launch_bounds__(EXP_T) zs_expand_kernel(const ZsJobDev *__restrict__ jobs,
                                                            const ZsChunkDev *__restrict__ chunks,
@@ -633,50 +645,33 @@ __global__ void __launch_bounds__(EXP_T) zs_expand_kernel(const ZsJobDev *__rest
                                                            const uint32_t *__restrict__ tokens) {
   __shared__ __attribute__((aligned(16))) uint16_t ring[HIST];
   __shared__ uint32_t s_tstart[EXP_T], s_tval[EXP_T], s_mark[EXP_T];
-  __shared__ uint8_t s_tkind[EXP_T];
-  __shared__ uint32_t s_red[EXP_W];
-  __shared__ uint32_t s_jv[EXP_T];
-  __shared__ int32_t s_jp[EXP_T];
+  __shared__ uint32_t s_red[EXP_W], s_flag[EXP_W];
+  __shared__ uint32_t s_jv[2][EXP_T], s_jf[2][EXP_W];
+  __shared__ int32_t s_jp[2][EXP_T];
   const uint32_t tid = threadIdx.x, lane = tid & (WAVE - 1), wv = tid / WAVE;
   const ZsChunkDev ch = chunks[blockIdx.x];
   const int code = ch.code & 0xff;
   if (!(code == ZD_STOP || code == ZD_END)) return;
-  const uint32_t *tk = tokens + ch.tok;
+  gcu32 *tk = (gcu32 *)(tokens + ch.tok);
   const uint32_t ntok = ch.n_tok;
   uint16_t *out = scratch + ch.scratch;
-  const uint8_t *inb = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(jobs[ch.job].in) & ~(uintptr_t)3);
   if (ch.ord != 0) {  // history before the chunk: markers 256 + w for position w - HIST
     uint32_t *r32 = reinterpret_cast<uint32_t *>(ring);
     for (uint32_t i = tid; i < HIST / 2; i += EXP_T) r32[i] = (MARK_BASE + 2 * i) | ((MARK_BASE + 2 * i + 1) << 16);
   }
-  for (uint32_t i = tid; i < EXP_T; i += EXP_T) s_mark[i] = 0;
+  s_mark[tid] = 0;
   uint32_t pos = 0, flushed = 0, stamp = 0;
+  uint32_t tnext = tid < ntok ? tk[tid] : 0u;
   for (uint32_t tb = 0; tb < ntok; tb += EXP_T) {
-    const uint32_t i = tb + tid;
-    const bool valid = i < ntok;
-    const uint32_t t = valid ? tk[i] : 0u;
-    // an offset word follows a stored-run token (offsets never reach 0xffff0000)
-    const bool is_off = valid && i > 0 && (tk[i - 1] >> 16) == TOK_STORED;
+    const uint32_t t = tnext;
+    if (tb + EXP_T + tid < ntok) tnext = tk[tb + EXP_T + tid];  // next batch, in flight during this one
+    const bool valid = tb + tid < ntok;
     const uint32_t hi = t >> 16;
-    uint32_t len = 0, kind = 3, val = 0;
-    if (valid && !is_off) {
-      if (hi == 0) {
-        len = 1;
-        kind = 0;
-        val = t & 0xffu;
-      } else if (hi == TOK_STORED) {
-        len = (t & 0xffffu) + 1u;
-        kind = 2;
-        val = tk[i + 1];
-      } else {
-        len = hi;
-        kind = 1;
-        val = (t & 0xffffu) + 1u;
-      }
-    }
+    const uint32_t len = valid ? (hi ? hi : 1u) : 0u;
+    const uint32_t val = hi ? (t & 0xffffu) + 1u : (TV_LIT | (t & 0xffu));
     const uint32_t incl = wave_scan_add(len);
     if (lane == WAVE - 1) s_red[wv] = incl;
-    __syncthreads();
+    exp_barrier();
     uint32_t before = 0, S = 0;
 #pragma unroll
     for (uint32_t w = 0; w < EXP_W; w++) {
@@ -687,20 +682,24 @@ __global__ void __launch_bounds__(EXP_T) zs_expand_kernel(const ZsJobDev *__rest
     const uint32_t tstart = pos + before + incl - len;
     s_tstart[tid] = tstart;
     s_tval[tid] = val;
-    s_tkind[tid] = (uint8_t)kind;
     uint32_t own_carry = 0;
     for (uint32_t R = pos; R < pos + S; R += EXP_T) {
       if ((++stamp & 0x7fffffu) == 0) {  // stamp wrap: drop stale marks
         s_mark[tid] = 0;
-        __syncthreads();
+        exp_barrier();
         stamp++;
       }
       if (len && tstart >= R && tstart < R + EXP_T) s_mark[tstart - R] = (stamp << 9) | (tid + 1);
-      __syncthreads();  // marks (and the batch's token table) visible; s_red free
+      exp_barrier();  // B1
+      while (R - flushed >= EXP_FLUSH) {  // entries before R are final in the ring
+        const uint4 v4 = *reinterpret_cast<const uint4 *>(&ring[(flushed + tid * 8) & (HIST - 1)]);
+        *reinterpret_cast<uint4 *>(out + flushed + tid * 8) = v4;
+        flushed += EXP_FLUSH;
+      }
       const uint32_t m = s_mark[tid];
       const uint32_t wmax = wave_scan_max((m >> 9) == (stamp & 0x7fffffu) ? (m & 511u) : 0u);
       if (lane == WAVE - 1) s_red[wv] = wmax;
-      __syncthreads();
+      exp_barrier();  // B2
       uint32_t own = max(own_carry, wmax), all = own_carry;
 #pragma unroll
       for (uint32_t w = 0; w < EXP_W; w++) {
@@ -712,48 +711,55 @@ __global__ void __launch_bounds__(EXP_T) zs_expand_kernel(const ZsJobDev *__rest
       const uint32_t e = R + tid;
       const bool act = e < pos + S;
       const uint32_t j = (own ? own : 1u) - 1u;
-      const uint32_t kj = s_tkind[j], vj = s_tval[j], sj = s_tstart[j];
-      uint32_t v = 0;
+      const uint32_t vj = s_tval[j], sj = s_tstart[j];
+      (void)sj;
+      uint32_t v = vj & 0xffu;
       int p = 0;
       bool res = true;
-      if (act) {
-        if (kj == 0) {
-          v = vj;
-        } else if (kj == 2) {
-          v = inb[vj + (e - sj)];
-        } else {
-          p = (int)e - (int)vj;
-          if (p < (int)R) v = ring[(uint32_t)p & (HIST - 1)];
-          else res = false;
-        }
+      if (act && !(vj & TV_LIT)) {
+        p = (int)e - (int)vj;
+        if (p < (int)R) v = ring[(uint32_t)p & (HIST - 1)];
+        else res = false;
       }
-      // every ring read of this round happens before any ring write below
-      while (__syncthreads_or(!res)) {  // in-round sources: pointer jumping through LDS
-        s_jv[tid] = v;
-        s_jp[tid] = res ? -1 : p - (int)R;
-        __syncthreads();
-        if (!res) {
-          const uint32_t q = (uint32_t)(p - (int)R);
-          const int tq = s_jp[q];
-          if (tq < 0) {
-            v = s_jv[q];
-            res = true;
-          } else {
-            p = (int)R + tq;
+      const bool wave_unres = __ballot(!res) != 0;
+      if (lane == 0) s_flag[wv] = wave_unres;
+      exp_barrier();  // B3: ring reads done, flags visible
+      bool any = false;
+#pragma unroll
+      for (uint32_t w = 0; w < EXP_W; w++) any |= s_flag[w] != 0;
+      if (any) {  // in-round sources: pointer jumping through LDS, one barrier per step
+        for (uint32_t it = 0;; it++) {
+          const uint32_t b = it & 1u;
+          s_jv[b][tid] = v;
+          s_jp[b][tid] = res ? -1 : p - (int)R;
+          const bool wu = __ballot(!res) != 0;
+          if (lane == 0) s_jf[b][wv] = wu;
+          exp_barrier();
+          bool more = false;
+#pragma unroll
+          for (uint32_t w = 0; w < EXP_W; w++) more |= s_jf[b][w] != 0;
+          if (!more) break;
+          if (!res) {
+            const uint32_t q = (uint32_t)(p - (int)R);
+            const int tq = s_jp[b][q];
+            if (tq < 0) {
+              v = s_jv[b][q];
+              res = true;
+            } else {
+              p = (int)R + tq;
+            }
           }
         }
       }
       if (act) ring[e & (HIST - 1)] = (uint16_t)v;
-      __syncthreads();
-      const uint32_t rend = min(R + EXP_T, pos + S);
-      while (rend - flushed >= EXP_FLUSH) {
-        const uint4 v4 = *reinterpret_cast<const uint4 *>(&ring[(flushed + tid * 8) & (HIST - 1)]);
-        *reinterpret_cast<uint4 *>(out + flushed + tid * 8) = v4;
-        flushed += EXP_FLUSH;
-      }
     }
     pos += S;
-    __syncthreads();  // token table reads done before the next batch rewrites it
+  }
+  exp_barrier();
+  while (pos - flushed >= EXP_FLUSH) {
+    const uint4 v4 = *reinterpret_cast<const uint4 *>(&ring[(flushed + tid * 8) & (HIST - 1)]);
+    *reinterpret_cast<uint4 *>(out + flushed + tid * 8) = v4;
+    flushed += EXP_FLUSH;
   }
   for (uint32_t k = tid; k < pos - flushed; k += EXP_T) out[flushed + k] = ring[(flushed + k) & (HIST - 1)];
 }

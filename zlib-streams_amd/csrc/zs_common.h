@@ -126,11 +126,8 @@ struct ZsChunkDev {
 };
 
 // Parse-pass tokens (u32), consumed by the expand pass:
-//   hi16 == 0          literal, byte in bits 0-7
+//   hi16 == 0          literal, byte in bits 0-7 (stored-block bytes included)
 //   hi16 in [3, 258]   match: length = hi16, distance = lo16 + 1
-//   hi16 == 0xffff     stored run of lo16 + 1 bytes; the next word is the byte
-//                      offset of the run in the job input (from its 4-byte-aligned base)
-#define TOK_STORED 0xffffu
 
 struct ZsCJobDev {
   uint32_t job;        // job index
