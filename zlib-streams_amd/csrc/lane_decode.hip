@@ -609,9 +609,11 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
 // Output leaves the ring in 4 KiB pieces (16 B per thread) after B1, when every
 // entry before the round is in the ring.
 // ---------------------------------------------------------------------------
-#define EXP_T 256       // threads = tokens per batch = entries per round
+#define EXP_T 256                 // threads = tokens per batch
 #define EXP_W (EXP_T / WAVE)
-#define EXP_FLUSH 2048  // entries per flush piece (8 per thread)
+#define EXP_E 4                   // consecutive entries per thread per round
+#define EXP_N (EXP_T * EXP_E)     // entries per round
+#define EXP_FLUSH 2048            // entries per flush piece (8 per thread)
 
 __device__ __forceinline__ uint32_t wave_scan_add(uint32_t v) {  // inclusive, wave64
   v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
@@ -638,16 +640,18 @@ __device__ __forceinline__ void exp_barrier() {
 }
 
 #define TV_LIT 0x80000000u  // s_tval: literal byte | TV_LIT, else match distance
+#define JR 0x80000000u      // s_j: resolved value | JR, else index of the source in the round
 
 __global__ void __launch_bounds__(EXP_T) zs_expand_kernel(const ZsJobDev *__restrict__ jobs,
                                                            const ZsChunkDev *__restrict__ chunks,
                                                            uint16_t *__restrict__ scratch,
                                                            const uint32_t *__restrict__ tokens) {
   __shared__ __attribute__((aligned(16))) uint16_t ring[HIST];
-  __shared__ uint32_t s_tstart[EXP_T], s_tval[EXP_T], s_mark[EXP_T];
+  __shared__ __attribute__((aligned(16))) uint32_t s_mark[EXP_N];
+  __shared__ uint32_t s_tval[EXP_T];
   __shared__ uint32_t s_red[EXP_W], s_flag[EXP_W];
-  __shared__ uint32_t s_jv[2][EXP_T], s_jf[2][EXP_W];
-  __shared__ int32_t s_jp[2][EXP_T];
+  __shared__ __attribute__((aligned(16))) uint32_t s_j[2][EXP_N];
+  __shared__ uint32_t s_jf[2][EXP_W];
   const uint32_t tid = threadIdx.x, lane = tid & (WAVE - 1), wv = tid / WAVE;
   const ZsChunkDev ch = chunks[blockIdx.x];
   const int code = ch.code & 0xff;
@@ -655,11 +659,12 @@ __global__ void __launch_bounds__(EXP_T) zs_expand_kernel(const ZsJobDev *__rest
   gcu32 *tk = (gcu32 *)(tokens + ch.tok);
   const uint32_t ntok = ch.n_tok;
   uint16_t *out = scratch + ch.scratch;
+  (void)jobs;
   if (ch.ord != 0) {  // history before the chunk: markers 256 + w for position w - HIST
     uint32_t *r32 = reinterpret_cast<uint32_t *>(ring);
     for (uint32_t i = tid; i < HIST / 2; i += EXP_T) r32[i] = (MARK_BASE + 2 * i) | ((MARK_BASE + 2 * i + 1) << 16);
   }
-  s_mark[tid] = 0;
+  for (uint32_t i = tid; i < EXP_N; i += EXP_T) s_mark[i] = 0;
   uint32_t pos = 0, flushed = 0, stamp = 0;
   uint32_t tnext = tid < ntok ? tk[tid] : 0u;
   for (uint32_t tb = 0; tb < ntok; tb += EXP_T) {
@@ -668,7 +673,6 @@ __global__ void __launch_bounds__(EXP_T) zs_expand_kernel(const ZsJobDev *__rest
     const bool valid = tb + tid < ntok;
     const uint32_t hi = t >> 16;
     const uint32_t len = valid ? (hi ? hi : 1u) : 0u;
-    const uint32_t val = hi ? (t & 0xffffu) + 1u : (TV_LIT | (t & 0xffu));
     const uint32_t incl = wave_scan_add(len);
     if (lane == WAVE - 1) s_red[wv] = incl;
     exp_barrier();
@@ -680,78 +684,112 @@ __global__ void __launch_bounds__(EXP_T) zs_expand_kernel(const ZsJobDev *__rest
       S += x;
     }
     const uint32_t tstart = pos + before + incl - len;
-    s_tstart[tid] = tstart;
-    s_tval[tid] = val;
+    s_tval[tid] = hi ? (t & 0xffffu) + 1u : (TV_LIT | (t & 0xffu));
     uint32_t own_carry = 0;
-    for (uint32_t R = pos; R < pos + S; R += EXP_T) {
+    // rounds start 4-aligned (8-byte ring stores); entries below pos are the
+    // previous batch's, already final in the ring, and stay inactive
+    for (uint32_t R = pos & ~(uint32_t)(EXP_E - 1); R < pos + S; R += EXP_N) {
+      const uint32_t lo = max(R, pos);  // entries below lo are final in the ring
       if ((++stamp & 0x7fffffu) == 0) {  // stamp wrap: drop stale marks
-        s_mark[tid] = 0;
+        for (uint32_t i = tid; i < EXP_N; i += EXP_T) s_mark[i] = 0;
         exp_barrier();
         stamp++;
       }
-      if (len && tstart >= R && tstart < R + EXP_T) s_mark[tstart - R] = (stamp << 9) | (tid + 1);
-      exp_barrier();  // B1
-      while (R - flushed >= EXP_FLUSH) {  // entries before R are final in the ring
+      const uint32_t st = stamp & 0x7fffffu;
+      if (len && tstart >= R && tstart < R + EXP_N) s_mark[tstart - R] = (st << 9) | (tid + 1);
+      exp_barrier();  // B1: marks, token values and the previous round's ring writes visible
+      while (lo - flushed >= EXP_FLUSH) {
         const uint4 v4 = *reinterpret_cast<const uint4 *>(&ring[(flushed + tid * 8) & (HIST - 1)]);
         *reinterpret_cast<uint4 *>(out + flushed + tid * 8) = v4;
         flushed += EXP_FLUSH;
       }
-      const uint32_t m = s_mark[tid];
-      const uint32_t wmax = wave_scan_max((m >> 9) == (stamp & 0x7fffffu) ? (m & 511u) : 0u);
-      if (lane == WAVE - 1) s_red[wv] = wmax;
+      // owner token of each of this thread's entries: running max of marks
+      const uint4 m4 = *reinterpret_cast<const uint4 *>(&s_mark[tid * EXP_E]);
+      uint32_t mk[EXP_E] = {m4.x, m4.y, m4.z, m4.w};
+      uint32_t run[EXP_E];
+#pragma unroll
+      for (int k = 0; k < EXP_E; k++) {
+        const uint32_t x = (mk[k] >> 9) == st ? (mk[k] & 511u) : 0u;
+        run[k] = k ? max(run[k - 1], x) : x;
+      }
+      const uint32_t winc = wave_scan_max(run[EXP_E - 1]);
+      const uint32_t wexc = __shfl_up(winc, 1);
+      if (lane == WAVE - 1) s_red[wv] = winc;
       exp_barrier();  // B2
-      uint32_t own = max(own_carry, wmax), all = own_carry;
+      uint32_t base = max(own_carry, lane ? wexc : 0u), all = own_carry;
 #pragma unroll
       for (uint32_t w = 0; w < EXP_W; w++) {
         const uint32_t x = s_red[w];
-        own = w < wv ? max(own, x) : own;
+        base = w < wv ? max(base, x) : base;
         all = max(all, x);
       }
       own_carry = all;
-      const uint32_t e = R + tid;
-      const bool act = e < pos + S;
-      const uint32_t j = (own ? own : 1u) - 1u;
-      const uint32_t vj = s_tval[j], sj = s_tstart[j];
-      (void)sj;
-      uint32_t v = vj & 0xffu;
-      int p = 0;
-      bool res = true;
-      if (act && !(vj & TV_LIT)) {
-        p = (int)e - (int)vj;
-        if (p < (int)R) v = ring[(uint32_t)p & (HIST - 1)];
-        else res = false;
+      const uint32_t e0 = R + tid * EXP_E;
+      uint32_t v[EXP_E], q[EXP_E];
+      uint32_t unres = 0;
+#pragma unroll
+      for (int k = 0; k < EXP_E; k++) {
+        const uint32_t e = e0 + k;
+        const uint32_t own = max(base, run[k]);
+        const uint32_t vj = s_tval[(own ? own : 1u) - 1u];
+        v[k] = vj & 0xffffu;
+        q[k] = 0;
+        if (e >= lo && e < pos + S && !(vj & TV_LIT)) {
+          const int p = (int)e - (int)vj;
+          if (p < (int)lo) {
+            v[k] = ring[(uint32_t)p & (HIST - 1)];
+          } else {
+            q[k] = (uint32_t)(p - (int)R);
+            unres |= 1u << k;
+          }
+        }
       }
-      const bool wave_unres = __ballot(!res) != 0;
+      const bool wave_unres = __ballot(unres != 0) != 0;
       if (lane == 0) s_flag[wv] = wave_unres;
-      exp_barrier();  // B3: ring reads done, flags visible
+      exp_barrier();  // B3: every ring read of the round done, flags visible
       bool any = false;
 #pragma unroll
       for (uint32_t w = 0; w < EXP_W; w++) any |= s_flag[w] != 0;
       if (any) {  // in-round sources: pointer jumping through LDS, one barrier per step
         for (uint32_t it = 0;; it++) {
           const uint32_t b = it & 1u;
-          s_jv[b][tid] = v;
-          s_jp[b][tid] = res ? -1 : p - (int)R;
-          const bool wu = __ballot(!res) != 0;
+          uint4 o;
+          o.x = (unres & 1u) ? q[0] : (JR | v[0]);
+          o.y = (unres & 2u) ? q[1] : (JR | v[1]);
+          o.z = (unres & 4u) ? q[2] : (JR | v[2]);
+          o.w = (unres & 8u) ? q[3] : (JR | v[3]);
+          *reinterpret_cast<uint4 *>(&s_j[b][tid * EXP_E]) = o;
+          const bool wu = __ballot(unres != 0) != 0;
           if (lane == 0) s_jf[b][wv] = wu;
           exp_barrier();
           bool more = false;
 #pragma unroll
           for (uint32_t w = 0; w < EXP_W; w++) more |= s_jf[b][w] != 0;
           if (!more) break;
-          if (!res) {
-            const uint32_t q = (uint32_t)(p - (int)R);
-            const int tq = s_jp[b][q];
-            if (tq < 0) {
-              v = s_jv[b][q];
-              res = true;
-            } else {
-              p = (int)R + tq;
+#pragma unroll
+          for (int k = 0; k < EXP_E; k++) {
+            if (unres & (1u << k)) {
+              const uint32_t x = s_j[b][q[k]];
+              if (x & JR) {
+                v[k] = x & 0xffffu;
+                unres &= ~(1u << k);
+              } else {
+                q[k] = x;
+              }
             }
           }
         }
       }
-      if (act) ring[e & (HIST - 1)] = (uint16_t)v;
+      if (e0 >= lo && e0 + EXP_E <= pos + S) {
+        uint2 w2;
+        w2.x = v[0] | (v[1] << 16);
+        w2.y = v[2] | (v[3] << 16);
+        *reinterpret_cast<uint2 *>(&ring[e0 & (HIST - 1)]) = w2;
+      } else {
+#pragma unroll
+        for (int k = 0; k < EXP_E; k++)
+          if (e0 + k >= lo && e0 + k < pos + S) ring[(e0 + k) & (HIST - 1)] = (uint16_t)v[k];
+      }
     }
     pos += S;
   }
