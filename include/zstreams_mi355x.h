@@ -95,6 +95,10 @@ int zs_profile_read(double *decode_ms, double *batch_ms, uint64_t *launches);
    emit, serial decode, finalize.  Returns the number of entries written. */
 #define ZS_PROF_STAGES 8
 int zs_profile_stages(double *ms, uint32_t n);
+/* in-kernel phase counters of the profiling build (libzstreams_mi355x_prof.so,
+   `make prof`); the product library returns 0 (no counters).  reset != 0
+   zeroes them after the read.  Returns the number of counters written. */
+int zs_kprof_read(uint64_t *out, uint32_t n, int reset);
 /* last batch: [jobs on the chunked path, chunks, chunked jobs that fell back
    to the serial decoder, jobs on the serial path] */
 int zs_last_stats(uint32_t out[4]);

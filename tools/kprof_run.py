@@ -1,0 +1,65 @@
+"""Run the bench workload once through the profiling build and print the
+in-kernel counters (zs_kprof.h) as per-phase figures.
+
+usage (GPU box): ZS_LIB=$PWD/zlib-streams_amd/libzstreams_mi355x_prof.so \
+                 python3 tools/kprof_run.py [--streams 64] [--out FILE.json]
+"""
+import argparse, json, os, sys, time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "zlib-streams_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+NAMES = {0: "p_waves", 1: "p_cyc_total", 2: "p_cyc_coop", 3: "p_cyc_steps", 4: "p_cyc_flush", 5: "p_groups",
+         6: "p_coop_calls", 7: "p_lane_steps", 8: "p_wave_steps", 9: "p_slow_lit", 10: "p_slow_dist",
+         11: "p_cyc_max", 12: "p_cyc_init", 13: "p_refills",
+         16: "e_blocks", 17: "e_cyc_total", 18: "e_rounds", 19: "e_jump_iters", 20: "e_cyc_jump", 21: "e_batches",
+         22: "e_cyc_max", 23: "e_cyc_init", 24: "e_jump_rounds"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--streams", type=int, default=64)
+    ap.add_argument("--stream-mib", type=int, default=64)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    import numpy as np
+    import corpus
+    import zstreams
+    raws, comps = corpus.batch(0, a.streams, a.stream_mib << 20, 6, -15, 16, True)
+    zstreams.kprof_read(reset=True)
+    res = zstreams.inflate_batch([bytes(c) for c in comps], -15, [a.stream_mib << 20] * a.streams)
+    c = zstreams.kprof_read(reset=True)
+    if not c:
+        sys.exit("no counters: ZS_LIB must point at libzstreams_mi355x_prof.so")
+    ok = all(r["ret"] == 1 and bytes(o) == bytes(raws[k]) for k, (o, r) in enumerate(res))
+    d = {NAMES[i]: v for i, v in enumerate(c) if i in NAMES}
+    w = max(d["p_waves"], 1)
+    b = max(d["e_blocks"], 1)
+    derived = {
+        "ok": ok,
+        "parse_cycles_per_wave": d["p_cyc_total"] / w, "parse_cycles_max": d["p_cyc_max"],
+        "parse_frac_coop": d["p_cyc_coop"] / max(d["p_cyc_total"], 1),
+        "parse_frac_steps": d["p_cyc_steps"] / max(d["p_cyc_total"], 1),
+        "parse_frac_flush": d["p_cyc_flush"] / max(d["p_cyc_total"], 1),
+        "parse_cycles_per_wave_step": d["p_cyc_steps"] / max(d["p_wave_steps"], 1),
+        "parse_lane_util": d["p_lane_steps"] / max(64 * d["p_wave_steps"], 1),
+        "parse_coop_cycles_per_call": d["p_cyc_coop"] / max(d["p_coop_calls"], 1),
+        "parse_slow_lit_per_step": d["p_slow_lit"] / max(d["p_lane_steps"], 1),
+        "parse_slow_dist_per_step": d["p_slow_dist"] / max(d["p_lane_steps"], 1),
+        "parse_refills_per_step": d["p_refills"] / max(d["p_lane_steps"], 1),
+        "expand_cycles_per_block": d["e_cyc_total"] / b, "expand_cycles_max": d["e_cyc_max"],
+        "expand_cycles_per_round": d["e_cyc_total"] / max(d["e_rounds"], 1),
+        "expand_frac_jump": d["e_cyc_jump"] / max(d["e_cyc_total"], 1),
+        "expand_jump_rounds_frac": d["e_jump_rounds"] / max(d["e_rounds"], 1),
+        "expand_jump_iters_per_jround": d["e_jump_iters"] / max(d["e_jump_rounds"], 1),
+        "expand_frac_init": d["e_cyc_init"] / max(d["e_cyc_total"], 1),
+    }
+    out = {"raw": d, "derived": derived}
+    print(json.dumps(out, indent=1))
+    if a.out:
+        json.dump(out, open(a.out, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()

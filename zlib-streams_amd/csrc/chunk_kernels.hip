@@ -3,23 +3,21 @@
 // Hot loop of the reference: src/inffast.c:100-287 (symbol decode + copy), fed
 // by the block/table states of src/inflate.c:834-1033 and src/inftrees.c.
 // MI355X design:
-//   zs_find_kernel   one wave per chunk; each lane tests 32 bit offsets per
-//                    step with bit-parallel filters (BFINAL=0, BTYPE=2, HLIT,
-//                    HDIST, complete code-length code), survivors get a full
-//                    header validation; the lowest valid offset wins.
-//   zs_lane_kernel   ONE LANE PER CHUNK: 64 independent decoders per wave.
-//                    Each lane decodes symbols with its own zlib-layout tables
-//                    (global, per chunk) and writes u16 entries; matches that
-//                    reach before the chunk start emit markers 256+w naming
-//                    byte w of the unknown 32 KiB history.  Block headers and
-//                    stored blocks are handled cooperatively: the whole wave
-//                    works on one lane's header at a time (bits staged in LDS,
-//                    ballot-parallel table build), then the lane resumes.
-//   zs_link_kernel   one workgroup per stream: verifies the chunk chain,
+//   zs_find_kernel   one wave per search segment: bit-parallel filters queue
+//                    candidate block starts in LDS; the queue is validated 64
+//                    at a time (one candidate per lane); up to SEG_SLOTS starts
+//                    are recorded per segment.
+//   zs_plan_kernel   one workgroup per stream: stream start + recorded starts
+//                    -> ordered decode units with stops and scratch ranges.
+//   zs_lane_kernel / zs_expand_kernel (lane_decode.hip): one lane per unit
+//                    parses symbols to tokens; one workgroup per unit expands
+//                    tokens to u16 entries (markers 256+w for the unknown
+//                    32 KiB history before the unit).
+//   zs_link_kernel   one workgroup per stream: follows the unit chain,
 //                    computes output offsets, resolves the 32 KiB history of
-//                    every chunk in order (LDS double buffer).
-//   zs_emit_kernel   one workgroup per chunk: entries -> bytes at their final
-//                    offsets (markers looked up in the chunk's window in LDS).
+//                    every chained unit in order (LDS double buffer).
+//   zs_emit_kernel   one workgroup per unit: entries -> bytes at their final
+//                    offsets (markers looked up in the unit's window in LDS).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -148,67 +146,232 @@ __device__ bool validate_header(const uint32_t *w, uint32_t end_byte, uint32_t b
 }
 
 // ---------------------------------------------------------------------------
-// Block finder
+// Block finder: one wave per search segment; records the first SEG_SLOTS
+// dynamic-block starts in [s_byte, e_byte).
+//   1. every lane tests 32 bit offsets per step with bit-parallel filters
+//      (BFINAL = 0, BTYPE = 2, HLIT <= 29, HDIST <= 29, complete code-length
+//      code) and appends the survivors, in offset order, to an LDS queue;
+//   2. the queue is drained 64 candidates at a time, ONE candidate per lane,
+//      through the full header validation, so the expensive check runs
+//      SIMD-parallel instead of stalling the wave lane by lane.
 // ---------------------------------------------------------------------------
+#define FQ 1024  // candidate queue (ring) per wave
+
+__device__ __forceinline__ uint32_t find_scan_excl(uint32_t v, uint32_t *total) {
+  uint32_t x = v;
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);
+  *total = __builtin_amdgcn_readlane(x, WAVE - 1);
+  return x - v;
+}
+
 __global__ void __launch_bounds__(64) zs_find_kernel(const ZsJobDev *__restrict__ jobs, const ZsHeadDev *__restrict__ heads,
-                                                      ZsChunkDev *__restrict__ chunks, const uint32_t *__restrict__ ids) {
+                                                      ZsSegDev *__restrict__ segs) {
   __shared__ uint8_t s_lut[WAVE][128];
+  __shared__ uint32_t s_q[FQ];
   const uint32_t lane = threadIdx.x;
-  const uint32_t c = ids[blockIdx.x];
-  const ZsChunkDev ch = chunks[c];
-  const ZsJobDev jb = jobs[ch.job];
-  const ZsHeadDev hd = heads[ch.job];
-  if (hd.code != ZD_END) {
-    if (lane == 0) chunks[c].start_bit = ZS_NONE;
-    return;
-  }
-  const uintptr_t ip = reinterpret_cast<uintptr_t>(jb.in);
-  const uint32_t mis = (uint32_t)(ip & 3u);
-  const uint32_t *w = reinterpret_cast<const uint32_t *>(ip - mis);
-  const uint32_t end_byte = mis + (uint32_t)jb.in_len;
-  uint32_t lo = (mis + max(ch.s_byte, (uint32_t)hd.start_byte)) * 8u;
-  const uint32_t hi = (mis + ch.e_byte) * 8u;
-  for (uint32_t base = lo & ~31u; base < hi; base += WAVE * 32u) {
-    const uint32_t b0 = base + lane * 32u;
-    uint32_t found = ZS_NONE;
-    if (b0 < hi) {
-      const uint32_t wi = b0 >> 5;
-      const uint64_t lo64 = (uint64_t)in_word(w, wi, end_byte) | ((uint64_t)in_word(w, wi + 1, end_byte) << 32);
-      const uint64_t hi64 = (uint64_t)in_word(w, wi + 2, end_byte) | ((uint64_t)in_word(w, wi + 3, end_byte) << 32);
-      // BFINAL = 0, BTYPE = 2 at offset p: bit p = 0, bit p+1 = 0, bit p+2 = 1
-      uint32_t cand = (uint32_t)(~lo64 & ~(lo64 >> 1) & (lo64 >> 2));
-      if (b0 < lo) cand &= ~0u << (lo - b0);
-      if (hi - b0 < 32u) cand &= (1u << (hi - b0)) - 1u;
-      while (cand) {
-        const uint32_t p = __builtin_ctz(cand);
-        cand &= cand - 1u;
-        const uint64_t h = lo64 >> (p + 3);
-        if ((h & 31) > 29 || ((h >> 5) & 31) > 29) continue;
-        const uint32_t ncode = (uint32_t)((h >> 10) & 15) + 4;
-        const uint32_t s = p + 17;  // 17..48
-        const uint64_t clb = (lo64 >> s) | (hi64 << (64 - s));
-        uint32_t kraft = 0;
+  const uint32_t sg = blockIdx.x;
+  const ZsSegDev seg = segs[sg];
+  const ZsJobDev jb = jobs[seg.job];
+  const ZsHeadDev hd = heads[seg.job];
+  uint32_t nfound = 0;
+  if (hd.code == ZD_END) {
+    const uintptr_t ip = reinterpret_cast<uintptr_t>(jb.in);
+    const uint32_t mis = (uint32_t)(ip & 3u);
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(ip - mis);
+    const uint32_t end_byte = mis + (uint32_t)jb.in_len;
+    // strictly after the stream's first block (that start is unit 0)
+    const uint32_t lo = max((mis + seg.s_byte) * 8u, (mis + (uint32_t)hd.start_byte) * 8u + 1u);
+    const uint32_t hi = (mis + seg.e_byte) * 8u;
+    uint32_t qh = 0, qt = 0;
+    for (uint32_t base = lo & ~31u;; base += WAVE * 32u) {
+      const bool more = base < hi;
+      const uint32_t b0 = base + lane * 32u;
+      uint32_t surv = 0;
+      if (more && b0 < hi) {
+        const uint32_t wi = b0 >> 5;
+        const uint64_t lo64 = (uint64_t)in_word(w, wi, end_byte) | ((uint64_t)in_word(w, wi + 1, end_byte) << 32);
+        const uint64_t hi64 = (uint64_t)in_word(w, wi + 2, end_byte) | ((uint64_t)in_word(w, wi + 3, end_byte) << 32);
+        // BFINAL = 0, BTYPE = 2 at offset p: bit p = 0, bit p+1 = 0, bit p+2 = 1
+        uint32_t cand = (uint32_t)(~lo64 & ~(lo64 >> 1) & (lo64 >> 2));
+        if (b0 < lo) cand &= ~0u << (lo - b0);
+        if (hi - b0 < 32u) cand &= (1u << (hi - b0)) - 1u;
+        while (cand) {
+          const uint32_t p = __builtin_ctz(cand);
+          cand &= cand - 1u;
+          const uint64_t h = lo64 >> (p + 3);
+          if ((h & 31) > 29 || ((h >> 5) & 31) > 29) continue;
+          const uint32_t ncode = (uint32_t)((h >> 10) & 15) + 4;
+          const uint32_t sh = p + 17;  // 17..48
+          const uint64_t clb = (lo64 >> sh) | (hi64 << (64 - sh));
+          uint32_t kraft = 0;
 #pragma unroll
-        for (int i = 0; i < 19; i++) {
-          uint32_t L = (uint32_t)(clb >> (3 * i)) & 7u;
-          if ((uint32_t)i < ncode && L) kraft += 128u >> L;
-        }
-        if (kraft != 128u) continue;
-        if (validate_header(w, end_byte, b0 + p, s_lut[lane])) {
-          found = b0 + p;
-          break;
+          for (int i = 0; i < 19; i++) {
+            const uint32_t L = (uint32_t)(clb >> (3 * i)) & 7u;
+            if ((uint32_t)i < ncode && L) kraft += 128u >> L;
+          }
+          if (kraft == 128u) surv |= 1u << p;
         }
       }
-    }
-    const uint64_t m = __ballot(found != ZS_NONE);
-    if (m) {
-      const uint32_t first_lane = (uint32_t)__builtin_ctzll(m);
-      const uint32_t f = __builtin_amdgcn_readlane(found, first_lane);
-      if (lane == 0) chunks[c].start_bit = f;
-      return;
+      uint32_t tot;
+      const uint32_t at = find_scan_excl((uint32_t)__builtin_popcount(surv), &tot);
+      for (uint32_t k = 0; surv; k++) {
+        s_q[(qt + at + k) & (FQ - 1)] = b0 + (uint32_t)__builtin_ctz(surv);
+        surv &= surv - 1u;
+      }
+      qt += tot;
+      __builtin_amdgcn_wave_barrier();
+      while (qt - qh >= WAVE || (!more && qt != qh)) {
+        const uint32_t take = min(qt - qh, (uint32_t)WAVE);
+        uint32_t cb = 0;
+        bool ok = false;
+        if (lane < take) {
+          cb = s_q[(qh + lane) & (FQ - 1)];
+          ok = validate_header(w, end_byte, cb, s_lut[lane]);
+        }
+        uint64_t m = __ballot(ok);
+        while (m && nfound < SEG_SLOTS) {
+          const uint32_t l = (uint32_t)__builtin_ctzll(m);
+          m &= m - 1;
+          const uint32_t f = __builtin_amdgcn_readlane(cb, l);
+          if (lane == 0) segs[sg].cand[nfound] = f;
+          nfound++;
+        }
+        qh += take;
+        if (nfound == SEG_SLOTS) break;
+      }
+      if (!more || nfound == SEG_SLOTS) break;
     }
   }
-  if (lane == 0) chunks[c].start_bit = ZS_NONE;
+  if (lane == 0) segs[sg].ncand = nfound;
+}
+
+// ---------------------------------------------------------------------------
+// Plan: one workgroup per chunked job.  Units = the stream's first block +
+// every recorded start, in order; each unit's stop is the next unit's start;
+// scratch/token capacity per unit = 2 x its compressed span x the job's
+// output/input ratio + slack, carved from the job's host-reserved range.
+// Unused unit slots of the job are marked inactive.
+// ---------------------------------------------------------------------------
+#define PLAN_T 256
+#define UNIT_SLACK 8192u  // entries of slack per unit
+
+__device__ uint32_t plan_block_scan(uint32_t v, uint32_t *s_tmp, uint32_t *total) {  // exclusive, PLAN_T threads
+  const uint32_t t = threadIdx.x, lane = t & (WAVE - 1), wv = t / WAVE;
+  uint32_t wt;
+  const uint32_t ex = find_scan_excl(v, &wt);
+  if (lane == 0) s_tmp[wv] = wt;
+  __syncthreads();
+  uint32_t before = 0, all = 0;
+  for (uint32_t k = 0; k < PLAN_T / WAVE; k++) {
+    const uint32_t x = s_tmp[k];
+    before += k < wv ? x : 0u;
+    all += x;
+  }
+  __syncthreads();
+  *total = all;
+  return before + ex;
+}
+
+__global__ void __launch_bounds__(PLAN_T) zs_plan_kernel(const ZsJobDev *__restrict__ jobs, const ZsHeadDev *__restrict__ heads,
+                                                          const ZsSegDev *__restrict__ segs, ZsCJobDev *__restrict__ cjobs,
+                                                          ZsChunkDev *__restrict__ units) {
+  __shared__ uint32_t s_tmp[PLAN_T / WAVE];
+  __shared__ uint64_t s_cap_base;
+  __shared__ uint64_t s_c[PLAN_T];
+  const uint32_t t = threadIdx.x;
+  const ZsCJobDev cj = cjobs[blockIdx.x];
+  const ZsJobDev jb = jobs[cj.job];
+  const ZsHeadDev hd = heads[cj.job];
+  const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(jb.in) & 3u);
+  const uint32_t end_bit = (mis + (uint32_t)jb.in_len) * 8u;
+  const double ratio = fmax(1.0, (double)jb.out_cap / fmax(1.0, (double)jb.in_len));
+  uint32_t nunits = 0;
+  if (hd.code == ZD_END) {
+    // unit index of each segment's first candidate (unit 0 = stream start)
+    uint32_t run = 1;
+    if (t == 0) s_cap_base = 0;
+    for (uint32_t s0 = 0; s0 < cj.nseg; s0 += PLAN_T) {
+      const uint32_t sg = s0 + t;
+      const uint32_t c = sg < cj.nseg ? segs[cj.first_seg + sg].ncand : 0u;
+      uint32_t tot;
+      const uint32_t ex = plan_block_scan(c, s_tmp, &tot);
+      for (uint32_t k = 0; k < c; k++) {
+        ZsChunkDev u{};
+        u.start_bit = segs[cj.first_seg + sg].cand[k];
+        units[cj.unit0 + run + ex + k] = u;  // start only; completed below
+      }
+      run += tot;
+    }
+    nunits = run;
+    if (t == 0) {
+      ZsChunkDev u{};
+      u.start_bit = (mis + (uint32_t)hd.start_byte) * 8u;
+      units[cj.unit0] = u;
+    }
+    __syncthreads();
+    // stops, spans, capacities (scanned in u64 through per-thread sums)
+    for (uint32_t u0 = 0; u0 < nunits; u0 += PLAN_T) {
+      const uint32_t i = u0 + t;
+      uint64_t cap = 0;
+      uint32_t st = 0, sp = ZS_NONE;
+      if (i < nunits) {
+        st = units[cj.unit0 + i].start_bit;
+        sp = i + 1 < nunits ? units[cj.unit0 + i + 1].start_bit : ZS_NONE;
+        const uint32_t span_bytes = ((sp == ZS_NONE ? end_bit : sp) - st + 7u) / 8u;
+        cap = ((uint64_t)(2.0 * span_bytes * ratio) + UNIT_SLACK + 7u) & ~7ull;
+        if (cap > 0xfff00000ull) cap = 0xfff00000ull;
+      }
+      // exclusive u64 prefix of the capacities (thread 0 walks the tile)
+      s_c[t] = cap;
+      __syncthreads();
+      if (t == 0) {
+        uint64_t acc = s_cap_base;
+        for (uint32_t k = 0; k < PLAN_T; k++) {
+          const uint64_t x = s_c[k];
+          s_c[k] = acc;
+          acc += x;
+        }
+        s_cap_base = acc;
+      }
+      __syncthreads();
+      const uint64_t pre = s_c[t];
+      if (i < nunits) {
+        ZsChunkDev u{};
+        u.job = cj.job;
+        u.ord = i;
+        u.first = cj.unit0;
+        u.nunits = nunits;
+        u.start_bit = st;
+        u.stop_bit = sp;
+        u.end_bit = 0;
+        u.code = ZD_SKIP;
+        u.cap = (uint32_t)cap;
+        u.tcap = (uint32_t)cap;
+        u.scratch = cj.scratch0 + pre;
+        u.tok = cj.scratch0 + pre;
+        u.chain_next = ZS_NONE;
+        u.in_chain = 0;
+        units[cj.unit0 + i] = u;  // start_bit unchanged: neighbours' reads stay valid
+      }
+      __syncthreads();
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = nunits + t; i < cj.max_units; i += PLAN_T) {
+    ZsChunkDev u{};
+    u.job = cj.job;
+    u.start_bit = ZS_NONE;
+    u.stop_bit = ZS_NONE;
+    u.code = ZD_SKIP;
+    u.chain_next = ZS_NONE;
+    units[cj.unit0 + i] = u;
+  }
+  if (t == 0) cjobs[blockIdx.x].nunits = nunits;
 }
 
 // ---------------------------------------------------------------------------
@@ -261,8 +424,11 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_link_kernel(const ZsJobDev *_
     return;
   }
   if (t == 0) {
-    // walk the chain from chunk 0
-    uint32_t c = cj.first;
+    // walk the chain from unit 0: a unit's end must be the start of a later
+    // unit (starts ascend; recorded starts that are not block boundaries are
+    // skipped and never enter the chain)
+    const uint32_t last = cj.unit0 + cj.nunits;
+    uint32_t c = cj.unit0;
     uint64_t total = 0;
     uint32_t ok = 1, end_bit = 0;
     for (;;) {
@@ -280,12 +446,15 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_link_kernel(const ZsJobDev *_
         break;
       }
       uint32_t k = ZS_NONE;
-      for (uint32_t o = ch.ord + 1; o < cj.nchunks; o++)
-        if (chunks[cj.first + o].start_bit != ZS_NONE) {
-          k = cj.first + o;
+      for (uint32_t o = c + 1; o < last; o++) {
+        const uint32_t sb = chunks[o].start_bit;
+        if (sb == ch.end_bit) {
+          k = o;
           break;
         }
-      if (k == ZS_NONE || chunks[k].start_bit != ch.end_bit) {
+        if (sb > ch.end_bit) break;
+      }
+      if (k == ZS_NONE) {
         ok = 0;
         break;
       }
@@ -296,7 +465,7 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_link_kernel(const ZsJobDev *_
     s_ok = ok;
     s_total = total;
     s_end_bit = end_bit;
-    s_cur = cj.first;
+    s_cur = cj.unit0;
   }
   __syncthreads();
   if (!s_ok) {
@@ -424,21 +593,22 @@ extern "C" void zs_launch_lane(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads,
                                uint16_t *d_scratch, uint32_t *d_tokens, uint32_t *d_tables, const uint32_t *d_fixed,
                                hipStream_t st, hipEvent_t *ev);
 
-extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, ZsChunkDev *d_chunks, uint32_t nchunks,
-                                  const uint32_t *d_find_ids, uint32_t nfind, const ZsCJobDev *d_cjobs, uint32_t ncjobs,
+extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, ZsSegDev *d_segs, uint32_t nseg,
+                                  ZsCJobDev *d_cjobs, uint32_t ncjobs, ZsChunkDev *d_units, uint32_t nunit_slots,
                                   uint16_t *d_scratch, uint32_t *d_tokens, uint32_t *d_tables, const uint32_t *d_fixed,
                                   uint8_t *d_windows, ZsDecDev *d_decs, uint32_t *d_fallback, hipStream_t st,
                                   hipEvent_t *ev) {
-  // ev (profiling, optional): [0] before find, [1] after find, [2] after parse,
-  // [3] after expand, [4] after link, [5] after emit
+  // ev (profiling, optional): [0] before find, [1] after find + plan, [2] after
+  // parse, [3] after expand, [4] after link, [5] after emit
   if (ev) (void)hipEventRecord(ev[0], st);
-  if (nfind) hipLaunchKernelGGL(zs_find_kernel, dim3(nfind), dim3(64), 0, st, d_jobs, d_heads, d_chunks, d_find_ids);
+  hipLaunchKernelGGL(zs_find_kernel, dim3(nseg), dim3(64), 0, st, d_jobs, d_heads, d_segs);
+  hipLaunchKernelGGL(zs_plan_kernel, dim3(ncjobs), dim3(PLAN_T), 0, st, d_jobs, d_heads, d_segs, d_cjobs, d_units);
   if (ev) (void)hipEventRecord(ev[1], st);
-  zs_launch_lane(d_jobs, d_heads, d_chunks, nchunks, d_scratch, d_tokens, d_tables, d_fixed, st, ev ? ev + 2 : nullptr);
-  hipLaunchKernelGGL(zs_link_kernel, dim3(ncjobs), dim3(LINK_THREADS), 0, st, d_jobs, d_heads, d_chunks, d_cjobs,
+  zs_launch_lane(d_jobs, d_heads, d_units, nunit_slots, d_scratch, d_tokens, d_tables, d_fixed, st, ev ? ev + 2 : nullptr);
+  hipLaunchKernelGGL(zs_link_kernel, dim3(ncjobs), dim3(LINK_THREADS), 0, st, d_jobs, d_heads, d_units, d_cjobs,
                      d_scratch, d_windows, d_decs, d_fallback);
   if (ev) (void)hipEventRecord(ev[4], st);
-  hipLaunchKernelGGL(zs_emit_kernel, dim3(nchunks), dim3(EMIT_THREADS), 0, st, d_jobs, d_chunks, d_scratch, d_windows,
+  hipLaunchKernelGGL(zs_emit_kernel, dim3(nunit_slots), dim3(EMIT_THREADS), 0, st, d_jobs, d_units, d_scratch, d_windows,
                      d_fallback);
   if (ev) (void)hipEventRecord(ev[5], st);
 }

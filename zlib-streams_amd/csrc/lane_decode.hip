@@ -24,18 +24,45 @@
 
 #include "zs_common.h"
 #include "zs_device.h"
+#include "zs_kprof.h"
+
+#if KP_ON
+__device__ unsigned long long g_kprof[KP_COUNT];
+// wave-uniform value, added once per wave
+#define KP_ADD(i, v)                                                       \
+  do {                                                                     \
+    if (lane_id() == 0) atomicAdd(&g_kprof[i], (unsigned long long)(v));  \
+  } while (0)
+#define KP_MAX(i, v)                                                       \
+  do {                                                                     \
+    if (lane_id() == 0) atomicMax(&g_kprof[i], (unsigned long long)(v));  \
+  } while (0)
+__device__ __forceinline__ uint32_t kp_wave_sum(uint32_t v) {
+  for (int o = 32; o; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+__device__ __forceinline__ uint32_t kp_wave_max(uint32_t v) {
+  for (int o = 32; o; o >>= 1) v = max(v, (uint32_t)__shfl_xor(v, o));
+  return v;
+}
+#else
+#define KP_ADD(i, v) ((void)0)
+#define KP_MAX(i, v) ((void)0)
+#endif
 
 #define MARK_BASE 256u
 #define HIST 32768u
 #define STAGE_WORDS 256  // 1 KiB of staged header bits per cooperative step
-#define LROOT_N 512      // 9-bit literal/length root
+#define LROOT_N 256      // 8-bit literal/length root (LDS)
 #define DROOT_N 64       // 6-bit distance root
 #define ZBUILD 852       // zlib build area (ENOUGH_LENS; the distance table reuses it)
 
 // compact entry (u16): [1:0] kind, [5:2] code bits, [15:6] symbol.
 // CK_SLOW: [5:2] = sub-table index bits (0 = invalid code), [15:6] = sub-table
 // offset (zlib's link entry, src/inftrees.c:250-262); sub-table entries carry
-// the TOTAL code length in [5:2] (root bits + sub bits <= 15).
+// the TOTAL code length in [5:2] (root bits + sub bits <= 15).  In the 8-bit
+// LDS literal/length root, [5:2] = 15 means "look up zlib's 9-bit root in the
+// lane's global compact table" (the prefix covers 9-bit or longer codes).
 enum { CK_SYM = 0, CK_LEN = 1, CK_EOB = 2, CK_SLOW = 3 };
 
 __device__ __forceinline__ uint16_t compact_len_entry(uint32_t z, uint32_t add_bits = 0) {
@@ -59,6 +86,18 @@ __device__ __forceinline__ uint16_t compact_dist_entry(uint32_t z, uint32_t add_
   const uint32_t e = op & 15u;
   const uint32_t d = (e == 0) ? val - 1 : 2 * (e + 1) + ((val - 1) >> e) - 2;
   return (uint16_t)(CK_SYM | (bits << 2) | (d << 6));
+}
+
+#define OP_ROOT9 15u
+
+// LDS root entry for 8-bit prefix i from a zlib literal/length table with
+// lbits-bit root (lbits <= 9)
+__device__ __forceinline__ uint16_t lds_len_root(const uint32_t *zt, uint32_t lbits, uint32_t i) {
+  if (lbits <= 8) return compact_len_entry(zt[i & ((1u << lbits) - 1u)]);
+  const uint32_t z0 = zt[i], z1 = zt[i | 256u];
+  const bool link = e_op(z0) != 0 && (e_op(z0) & 0xf0u) == 0;
+  if (z0 == z1 && !link) return compact_len_entry(z0);  // code of <= 8 bits (or invalid both ways)
+  return (uint16_t)(CK_SLOW | (OP_ROOT9 << 2));
 }
 
 typedef __attribute__((address_space(1))) const uint32_t gcu32;
@@ -85,6 +124,9 @@ struct LaneState {
   gu32 *tok;          // token output (parse pass)
   uint32_t ntok, tcap;
   uint32_t gk;        // tokens of the current group (in LDS)
+#if KP_ON
+  uint32_t kp_steps, kp_slow_l, kp_slow_d, kp_refills;
+#endif
   uint32_t pos, cap;  // entries the tokens expand to / entry capacity
   uint32_t capx;      // min(cap, pos + tcap - ntok) at block start: one check covers both
   gcu16 *cl, *cd;     // compact sub-tables (global) of the current block
@@ -116,6 +158,9 @@ __device__ __forceinline__ void lane_prime(LaneState &s, uint32_t bit) {
 }
 __device__ __forceinline__ void lane_refill(LaneState &s) {
   if (s.nbits < 32) {
+#if KP_ON
+    s.kp_refills++;
+#endif
     s.hold |= (uint64_t)lane_take(s) << s.nbits;
     s.nbits += 32;
     s.wi++;
@@ -145,10 +190,22 @@ __device__ __forceinline__ bool lane_step(LaneState &s, const uint16_t *__restri
                                           uint32_t *__restrict__ tb) {
   lane_refill(s);
   uint32_t e = lt[(uint32_t)s.hold & (LROOT_N - 1)];
+#if KP_ON
+  s.kp_steps++;
+#endif
   if ((e & 3u) == CK_SLOW) {
+#if KP_ON
+    s.kp_slow_l++;
+#endif
     const uint32_t op = (e >> 2) & 15u;
     uint32_t e2 = CK_SLOW;
-    if (op) e2 = s.cl[(e >> 6) + (((uint32_t)s.hold >> s.lbits) & ((1u << op) - 1u))];
+    if (op == OP_ROOT9) {  // zlib's 9-bit root (compact, global), then its sub-table
+      e2 = s.cl[(uint32_t)s.hold & 511u];
+      const uint32_t op2 = (e2 >> 2) & 15u;
+      if ((e2 & 3u) == CK_SLOW && op2) e2 = s.cl[(e2 >> 6) + (((uint32_t)s.hold >> 9) & ((1u << op2) - 1u))];
+    } else if (op) {
+      e2 = s.cl[(e >> 6) + (((uint32_t)s.hold >> s.lbits) & ((1u << op) - 1u))];
+    }
     if ((e2 & 3u) == CK_SLOW) {
       const uint32_t used = invalid_code_bits(s.zl, s.zlmask, (uint32_t)s.hold);
       s.code = lane_pos(s) + used > s.limit ? ZD_TRUNC : (ZD_ERROR | (ZM_LITLEN_CODE << 8));
@@ -179,6 +236,9 @@ __device__ __forceinline__ bool lane_step(LaneState &s, const uint16_t *__restri
     lane_refill(s);
     uint32_t d = dt[(uint32_t)s.hold & (DROOT_N - 1)];
     if ((d & 3u) == CK_SLOW) {
+#if KP_ON
+      s.kp_slow_d++;
+#endif
       const uint32_t op = (d >> 2) & 15u;
       uint32_t d2 = CK_SLOW;
       if (op) d2 = s.cd[(d >> 6) + (((uint32_t)s.hold >> s.dbits) & ((1u << op) - 1u))];
@@ -248,22 +308,24 @@ struct StageBits {
 // would make every input refill wait for it).
 #define GROUP 16
 
+struct BuildLDS {  // one wave's header-decode / table-build area
+  uint32_t stage[STAGE_WORDS + 4];
+  uint32_t tab[ZBUILD];
+  uint16_t lens[320];
+  uint16_t sorted[320];
+  uint32_t scr[32];
+};
+
 struct LaneLDS {
   uint16_t lroot[WAVE][LROOT_N];
   uint16_t droot[WAVE][DROOT_N];
   union {
-    struct {
-      uint32_t stage[STAGE_WORDS + 4];
-      uint32_t tab[ZBUILD];
-      uint16_t lens[320];
-      uint16_t sorted[320];
-      uint32_t scr[32];
-    };
+    BuildLDS b;
     uint32_t tokbuf[GROUP][WAVE];
   };
 };
 
-__device__ void stage_bits(LaneLDS &L, const uint32_t *w, uint32_t end_byte, uint32_t bit, StageBits &sb) {
+__device__ void stage_bits(BuildLDS &L, const uint32_t *w, uint32_t end_byte, uint32_t bit, StageBits &sb) {
   const uint32_t lane = lane_id();
   const uint32_t b16 = (bit >> 7) << 4;  // byte offset, multiple of 16
   const uint32_t wi = (b16 >> 2) + lane * 4;
@@ -282,10 +344,108 @@ __device__ __forceinline__ uintptr_t readlane_ptr(const void *p, uint32_t ln) {
   return (uintptr_t)(((uint64_t)hi << 32) | lo);
 }
 
+// Dynamic block header after the 3 block-type bits (src/inflate.c:905-1033):
+// code-length code, code lengths, then the literal/length and distance tables
+// (src/inftrees.c restated in build_table) into the unit's global table area
+// (zlib layout + compact copy) and the compact root images lroot_out (256 u16)
+// and droot_out (64 u16), which may be LDS or global.  Wave-cooperative: every
+// lane calls it with the same arguments.  Returns 0, or ZD_* | msg << 8.
+__device__ int wave_dyn_header(BuildLDS &B, const uint32_t *w, uint32_t end_byte, uint32_t &bit, uint32_t *tabg,
+                               uint16_t *ctab, uint32_t &lbits, uint32_t &dbits, uint16_t *lroot_out,
+                               uint16_t *droot_out) {
+  const uint32_t lane = lane_id();
+  const uint32_t limit = end_byte * 8u;
+  StageBits sb;
+  stage_bits(B, w, end_byte, bit, sb);
+  if (bit + 14 > limit) {
+    return ZD_TRUNC;
+  }
+  const uint32_t h = sb.peek(bit, 14);
+  const uint32_t nlen = (h & 31) + 257, ndist = ((h >> 5) & 31) + 1, ncode = ((h >> 10) & 15) + 4;
+  bit += 14;
+  if (nlen > 286 || ndist > 30) {
+    return ZD_ERROR | (ZM_TOO_MANY << 8);
+  }
+  if (bit + 3 * ncode > limit) {
+    return ZD_TRUNC;
+  }
+  if (lane < 19) B.lens[c_clorder[lane]] = lane < ncode ? (uint16_t)sb.peek(bit + 3 * lane, 3) : (uint16_t)0;
+  bit += 3 * ncode;
+  __builtin_amdgcn_wave_barrier();
+  uint32_t cbits = 7;
+  if (build_table(T_CODES, B.lens, 19, B.tab, &cbits, B.sorted, B.scr, 0)) {
+    return ZD_ERROR | (ZM_CODE_LENGTHS << 8);
+  }
+  const uint32_t total = nlen + ndist;
+  const uint32_t cmask = (1u << cbits) - 1u;
+  uint32_t have = 0;
+  while (have < total) {
+    if (bit - sb.base > (STAGE_WORDS - 2) * 32u - 64u) stage_bits(B, w, end_byte, bit, sb);
+    const uint32_t x = sb.peek(bit, 14);
+    const uint32_t e = B.tab[x & cmask];
+    const uint32_t eb = e_bits(e), ev = e_val(e);
+    if (ev < 16) {
+      if (bit + eb > limit) {
+        return ZD_TRUNC;
+      }
+      bit += eb;
+      if (lane == 0) B.lens[have] = (uint16_t)ev;
+      have++;
+      continue;
+    }
+    const uint32_t xb = ev == 16 ? 2u : (ev == 17 ? 3u : 7u);
+    if (bit + eb + xb > limit) {
+      return ZD_TRUNC;
+    }
+    if (ev == 16 && have == 0) {
+      return ZD_ERROR | (ZM_REPEAT << 8);
+    }
+    const uint32_t rep = (ev == 18 ? 11u : 3u) + ((x >> eb) & ((1u << xb) - 1u));
+    bit += eb + xb;
+    if (have + rep > total) {
+      return ZD_ERROR | (ZM_REPEAT << 8);
+    }
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t fillv = ev == 16 ? uni(B.lens[have - 1]) : 0u;
+    for (uint32_t k = lane; k < rep; k += WAVE) B.lens[have + k] = (uint16_t)fillv;
+    __builtin_amdgcn_wave_barrier();
+    have += rep;
+  }
+  __builtin_amdgcn_wave_barrier();
+  if (uni(B.lens[256]) == 0) {
+    return ZD_ERROR | (ZM_MISSING_EOB << 8);
+  }
+  // literal/length table: build in LDS, keep the full zlib table in global
+  // (slow path), compact root into the lane's LDS slot
+  lbits = 9;
+  if (build_table(T_LENS, B.lens, nlen, B.tab, &lbits, B.sorted, B.scr, 0)) {
+    return ZD_ERROR | (ZM_LITLEN_SET << 8);
+  }
+  __builtin_amdgcn_wave_barrier();
+  for (uint32_t i = lane; i < ZBUILD; i += WAVE) {
+    tabg[i] = B.tab[i];
+    ctab[i] = compact_len_entry(B.tab[i], i < (1u << lbits) ? 0u : lbits);
+  }
+  for (uint32_t i = lane; i < LROOT_N; i += WAVE) lroot_out[i] = lds_len_root(B.tab, lbits, i);
+  __builtin_amdgcn_wave_barrier();
+  dbits = 6;
+  if (build_table(T_DISTS, B.lens + nlen, ndist, B.tab, &dbits, B.sorted, B.scr, 0)) {
+    return ZD_ERROR | (ZM_DIST_SET << 8);
+  }
+  __builtin_amdgcn_wave_barrier();
+  for (uint32_t i = lane; i < 592; i += WAVE) {
+    tabg[DIST_TABLE_OFF + i] = B.tab[i];
+    ctab[DIST_TABLE_OFF + i] = compact_dist_entry(B.tab[i], i < (1u << dbits) ? 0u : dbits);
+  }
+  droot_out[lane] = compact_dist_entry(B.tab[lane & ((1u << dbits) - 1u)]);
+  __builtin_amdgcn_wave_barrier();
+  return 0;
+}
+
 // Install compact roots for lane ln from zlib tables zl (root bits lb) and zd (db).
 __device__ void install_roots(LaneLDS &L, uint32_t ln, const uint32_t *zl, uint32_t lb, const uint32_t *zd, uint32_t db) {
   const uint32_t lane = lane_id();
-  for (uint32_t i = lane; i < LROOT_N; i += WAVE) L.lroot[ln][i] = compact_len_entry(zl[i & ((1u << lb) - 1u)]);
+  for (uint32_t i = lane; i < LROOT_N; i += WAVE) L.lroot[ln][i] = lds_len_root(zl, lb, i);
   L.droot[ln][lane] = compact_dist_entry(zd[lane & ((1u << db) - 1u)]);
   __builtin_amdgcn_wave_barrier();
 }
@@ -298,7 +458,8 @@ __device__ void coop_block(LaneState &s, uint32_t ln, LaneLDS &L, uint32_t *lane
   const uint32_t *w = reinterpret_cast<const uint32_t *>(readlane_ptr((const void *)(uintptr_t)s.w, ln));
   uint32_t *tok = reinterpret_cast<uint32_t *>(readlane_ptr((const void *)(uintptr_t)s.tok, ln));
   uint32_t *tabg = reinterpret_cast<uint32_t *>(readlane_ptr(lane_tab, ln));
-  uint16_t *ctab = reinterpret_cast<uint16_t *>(tabg + TABLE_ENTRIES);  // compact sub-tables
+  uint16_t *ctab = reinterpret_cast<uint16_t *>(tabg + TABLE_ENTRIES);  // compact copy (roots + sub-tables)
+  const uint16_t *cl = ctab, *cd = ctab + DIST_TABLE_OFF;
   uint32_t ntok = __builtin_amdgcn_readlane(s.ntok, ln);
   const uint32_t tcap = __builtin_amdgcn_readlane(s.tcap, ln);
   const uint32_t end_byte = __builtin_amdgcn_readlane(s.end_byte, ln);
@@ -325,7 +486,7 @@ __device__ void coop_block(LaneState &s, uint32_t ln, LaneLDS &L, uint32_t *lane
       break;
     }
     StageBits sb;
-    stage_bits(L, w, end_byte, bit, sb);
+    stage_bits(L.b, w, end_byte, bit, sb);
     const uint32_t hdr = sb.peek(bit, 3);
     last = hdr & 1;
     const uint32_t type = hdr >> 1;
@@ -336,7 +497,7 @@ __device__ void coop_block(LaneState &s, uint32_t ln, LaneLDS &L, uint32_t *lane
         code = ZD_TRUNC;
         break;
       }
-      stage_bits(L, w, end_byte, bit, sb);
+      stage_bits(L.b, w, end_byte, bit, sb);
       const uint32_t v = sb.peek(bit, 32);
       if ((v & 0xffffu) != ((v >> 16) ^ 0xffffu)) {
         code = ZD_ERROR | (ZM_STORED_LEN << 8);
@@ -367,6 +528,8 @@ __device__ void coop_block(LaneState &s, uint32_t ln, LaneLDS &L, uint32_t *lane
     if (type == 1) {  // fixed: global fixed tables (lit root 9, dist root 5)
       zl = fixed;
       zd = fixed + 512;
+      cl = reinterpret_cast<const uint16_t *>(fixed + FIXED_ZLIB_WORDS);
+      cd = cl + 512;
       lbits = 9;
       dbits = 5;
       install_roots(L, ln, zl, lbits, zd, dbits);
@@ -377,107 +540,17 @@ __device__ void coop_block(LaneState &s, uint32_t ln, LaneLDS &L, uint32_t *lane
       code = ZD_ERROR | (ZM_BLOCK_TYPE << 8);
       break;
     }
-    if (bit + 14 > limit) {
-      code = ZD_TRUNC;
-      break;
-    }
-    const uint32_t h = sb.peek(bit, 14);
-    const uint32_t nlen = (h & 31) + 257, ndist = ((h >> 5) & 31) + 1, ncode = ((h >> 10) & 15) + 4;
-    bit += 14;
-    if (nlen > 286 || ndist > 30) {
-      code = ZD_ERROR | (ZM_TOO_MANY << 8);
-      break;
-    }
-    if (bit + 3 * ncode > limit) {
-      code = ZD_TRUNC;
-      break;
-    }
-    if (lane < 19) L.lens[c_clorder[lane]] = lane < ncode ? (uint16_t)sb.peek(bit + 3 * lane, 3) : (uint16_t)0;
-    bit += 3 * ncode;
-    __builtin_amdgcn_wave_barrier();
-    uint32_t cbits = 7;
-    if (build_table(T_CODES, L.lens, 19, L.tab, &cbits, L.sorted, L.scr, 0)) {
-      code = ZD_ERROR | (ZM_CODE_LENGTHS << 8);
-      break;
-    }
-    const uint32_t total = nlen + ndist;
-    const uint32_t cmask = (1u << cbits) - 1u;
-    uint32_t have = 0;
-    bool bad = false;
-    while (have < total) {
-      if (bit - sb.base > (STAGE_WORDS - 2) * 32u - 64u) stage_bits(L, w, end_byte, bit, sb);
-      const uint32_t x = sb.peek(bit, 14);
-      const uint32_t e = L.tab[x & cmask];
-      const uint32_t eb = e_bits(e), ev = e_val(e);
-      if (ev < 16) {
-        if (bit + eb > limit) {
-          bad = true;
-          code = ZD_TRUNC;
-          break;
-        }
-        bit += eb;
-        if (lane == 0) L.lens[have] = (uint16_t)ev;
-        have++;
-        continue;
-      }
-      const uint32_t xb = ev == 16 ? 2u : (ev == 17 ? 3u : 7u);
-      if (bit + eb + xb > limit) {
-        bad = true;
-        code = ZD_TRUNC;
+    {
+      const int hc = wave_dyn_header(L.b, w, end_byte, bit, tabg, ctab, lbits, dbits, L.lroot[ln], L.droot[ln]);
+      if (hc) {
+        code = hc;
         break;
       }
-      if (ev == 16 && have == 0) {
-        bad = true;
-        code = ZD_ERROR | (ZM_REPEAT << 8);
-        break;
-      }
-      const uint32_t rep = (ev == 18 ? 11u : 3u) + ((x >> eb) & ((1u << xb) - 1u));
-      bit += eb + xb;
-      if (have + rep > total) {
-        bad = true;
-        code = ZD_ERROR | (ZM_REPEAT << 8);
-        break;
-      }
-      __builtin_amdgcn_wave_barrier();
-      const uint32_t fillv = ev == 16 ? uni(L.lens[have - 1]) : 0u;
-      for (uint32_t k = lane; k < rep; k += WAVE) L.lens[have + k] = (uint16_t)fillv;
-      __builtin_amdgcn_wave_barrier();
-      have += rep;
     }
-    if (bad) break;
-    __builtin_amdgcn_wave_barrier();
-    if (uni(L.lens[256]) == 0) {
-      code = ZD_ERROR | (ZM_MISSING_EOB << 8);
-      break;
-    }
-    // literal/length table: build in LDS, keep the full zlib table in global
-    // (slow path), compact root into the lane's LDS slot
-    lbits = 9;
-    if (build_table(T_LENS, L.lens, nlen, L.tab, &lbits, L.sorted, L.scr, 0)) {
-      code = ZD_ERROR | (ZM_LITLEN_SET << 8);
-      break;
-    }
-    __builtin_amdgcn_wave_barrier();
-    for (uint32_t i = lane; i < ZBUILD; i += WAVE) {
-      tabg[i] = L.tab[i];
-      ctab[i] = compact_len_entry(L.tab[i], lbits);
-    }
-    for (uint32_t i = lane; i < LROOT_N; i += WAVE) L.lroot[ln][i] = compact_len_entry(L.tab[i & ((1u << lbits) - 1u)]);
-    __builtin_amdgcn_wave_barrier();
-    dbits = 6;
-    if (build_table(T_DISTS, L.lens + nlen, ndist, L.tab, &dbits, L.sorted, L.scr, 0)) {
-      code = ZD_ERROR | (ZM_DIST_SET << 8);
-      break;
-    }
-    __builtin_amdgcn_wave_barrier();
-    for (uint32_t i = lane; i < 592; i += WAVE) {
-      tabg[DIST_TABLE_OFF + i] = L.tab[i];
-      ctab[DIST_TABLE_OFF + i] = compact_dist_entry(L.tab[i], dbits);
-    }
-    L.droot[ln][lane] = compact_dist_entry(L.tab[lane & ((1u << dbits) - 1u)]);
-    __builtin_amdgcn_wave_barrier();
     zl = tabg;
     zd = tabg + DIST_TABLE_OFF;
+    cl = ctab;
+    cd = ctab + DIST_TABLE_OFF;
     mode = LM_SYM;
     break;
   }
@@ -494,8 +567,8 @@ __device__ void coop_block(LaneState &s, uint32_t ln, LaneLDS &L, uint32_t *lane
       s.zdmask = (1u << dbits) - 1u;
       s.lbits = lbits;
       s.dbits = dbits;
-      s.cl = (gcu16 *)ctab;
-      s.cd = (gcu16 *)(ctab + DIST_TABLE_OFF);
+      s.cl = (gcu16 *)cl;
+      s.cd = (gcu16 *)cd;
       s.capx = min(cap, pos + (tcap - ntok));
       lane_prime(s, bit);
     } else {
@@ -533,17 +606,21 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
   s.lbits = s.dbits = 0;
   s.capx = 0;
   s.wi = s.nw = s.nkeep = s.nbits = s.lastw = s.gk = 0;
+#if KP_ON
+  const uint64_t kp_t0 = KP_NOW();
+  uint64_t kp_coop = 0, kp_steps_c = 0, kp_flush = 0, kp_init = 0;
+  uint32_t kp_groups = 0, kp_coopn = 0, kp_wsteps = 0;
+  s.kp_steps = s.kp_slow_l = s.kp_slow_d = s.kp_refills = 0;
+#endif
   s.hold = 0;
   uint32_t *lane_tab = tables + (size_t)min(c, nchunks - 1) * TABLE_STRIDE;
   s.cl = s.cd = (gcu16 *)(lane_tab + TABLE_ENTRIES);
   if (c < nchunks) {
     const ZsChunkDev ch = chunks[c];
-    const ZsHeadDev hd = heads[ch.job];
-    const ZsJobDev jb = jobs[ch.job];
-    const uintptr_t ip = reinterpret_cast<uintptr_t>(jb.in);
-    const uint32_t mis = (uint32_t)(ip & 3u);
-    const uint32_t start = ch.ord == 0 ? (mis + (uint32_t)hd.start_byte) * 8u : ch.start_bit;
-    if (hd.code == ZD_END && start != ZS_NONE) {
+    if (ch.start_bit != ZS_NONE && heads[ch.job].code == ZD_END) {
+      const ZsJobDev jb = jobs[ch.job];
+      const uintptr_t ip = reinterpret_cast<uintptr_t>(jb.in);
+      const uint32_t mis = (uint32_t)(ip & 3u);
       s.w = (gcu32 *)(ip - mis);
       s.end_byte = mis + (uint32_t)jb.in_len;
       s.limit = s.end_byte * 8u;
@@ -551,28 +628,59 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
       s.tcap = ch.tcap;
       s.cap = ch.cap;
       s.whave = ch.ord == 0 ? 0u : HIST;
-      s.bit = start;
+      s.bit = ch.start_bit;
+      s.stop = ch.stop_bit;
       s.mode = LM_BLOCK;
       s.code = 0;
-      for (uint32_t k = ch.ord + 1; k < ch.nchunks; k++) {
-        const uint32_t sb = chunks[ch.first + k].start_bit;
-        if (sb != ZS_NONE) {
-          s.stop = sb;
-          break;
-        }
+      if (ch.hdr_info & 1u) {  // first header prebuilt by zs_unit_header_kernel: straight to symbols
+        const uint32_t lb = (ch.hdr_info >> 8) & 15u, db = (ch.hdr_info >> 12) & 15u;
+        uint32_t *tabg = lane_tab;
+        const uint16_t *ctab = reinterpret_cast<const uint16_t *>(tabg + TABLE_ENTRIES);
+        const uint4 *img = reinterpret_cast<const uint4 *>(tabg + TABLE_ENTRIES + TABLE_ENTRIES / 2);
+        uint4 *lr = reinterpret_cast<uint4 *>(L.lroot[lane]);
+        uint4 *dr = reinterpret_cast<uint4 *>(L.droot[lane]);
+#pragma unroll 4
+        for (int k = 0; k < LROOT_N * 2 / 16; k++) lr[k] = img[k];
+#pragma unroll
+        for (int k = 0; k < DROOT_N * 2 / 16; k++) dr[k] = img[LROOT_N * 2 / 16 + k];
+        s.mode = LM_SYM;
+        s.bit = ch.hdr_bit;
+        s.zl = tabg;
+        s.zd = tabg + DIST_TABLE_OFF;
+        s.zlmask = (1u << lb) - 1u;
+        s.zdmask = (1u << db) - 1u;
+        s.lbits = lb;
+        s.dbits = db;
+        s.cl = (gcu16 *)ctab;
+        s.cd = (gcu16 *)(ctab + DIST_TABLE_OFF);
+        s.capx = min(s.cap, s.tcap);
+        lane_prime(s, s.bit);
       }
     }
   }
+  __builtin_amdgcn_wave_barrier();
   const uint16_t *lt = L.lroot[lane];
   const uint16_t *dt = L.droot[lane];
   uint32_t *tb = &L.tokbuf[0][lane];
+#if KP_ON
+  kp_init = KP_NOW() - kp_t0;
+#endif
   for (;;) {
     uint64_t need = __ballot(s.mode == LM_BLOCK);
+#if KP_ON
+    const uint64_t kc0 = KP_NOW();
+    kp_coopn += __builtin_popcountll(need);
+#endif
     while (need) {
       const uint32_t ln = (uint32_t)__builtin_ctzll(need);
       need &= need - 1;
       coop_block(s, ln, L, lane_tab, fixed);
     }
+#if KP_ON
+    const uint64_t kc1 = KP_NOW();
+    kp_coop += kc1 - kc0;
+    const uint32_t kp_st0 = s.kp_steps;
+#endif
     if (__ballot(s.mode == LM_SYM) == 0) break;
     s.gk = 0;
     if (s.mode == LM_SYM) {
@@ -580,12 +688,42 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
         if (lane_step(s, lt, dt, tb)) break;
     }
     __builtin_amdgcn_wave_barrier();
+#if KP_ON
+    const uint64_t kc2 = KP_NOW();
+    kp_steps_c += kc2 - kc1;
+    kp_groups++;
+    kp_wsteps += kp_wave_max(s.kp_steps - kp_st0);
+#endif
     const uint32_t g0 = s.ntok - s.gk;
 #pragma unroll
     for (uint32_t j = 0; j < GROUP; j++)
       if (j < s.gk) s.tok[g0 + j] = L.tokbuf[j][lane];
     __builtin_amdgcn_wave_barrier();  // tokbuf area is reused by the next header build
+#if KP_ON
+    kp_flush += KP_NOW() - kc2;
+#endif
   }
+#if KP_ON
+  {
+    const uint64_t tot = KP_NOW() - kp_t0;
+    KP_ADD(KP_P_WAVES, 1);
+    KP_ADD(KP_P_CYC_TOTAL, tot);
+    KP_MAX(KP_P_CYC_MAX, tot);
+    KP_ADD(KP_P_CYC_INIT, kp_init);
+    KP_ADD(KP_P_CYC_COOP, kp_coop);
+    KP_ADD(KP_P_CYC_STEPS, kp_steps_c);
+    KP_ADD(KP_P_CYC_FLUSH, kp_flush);
+    KP_ADD(KP_P_GROUPS, kp_groups);
+    KP_ADD(KP_P_COOP, kp_coopn);
+    KP_ADD(KP_P_WAVE_STEPS, kp_wsteps);
+    const uint32_t ls = kp_wave_sum(s.kp_steps), sl = kp_wave_sum(s.kp_slow_l), sd = kp_wave_sum(s.kp_slow_d),
+                   rf = kp_wave_sum(s.kp_refills);
+    KP_ADD(KP_P_LANE_STEPS, ls);
+    KP_ADD(KP_P_SLOW_LIT, sl);
+    KP_ADD(KP_P_SLOW_DIST, sd);
+    KP_ADD(KP_P_REFILLS, rf);
+  }
+#endif
   if (c < nchunks) {
     ZsChunkDev *ch = &chunks[c];
     ch->code = s.code;
@@ -660,11 +798,19 @@ __global__ void __launch_bounds__(EXP_T) zs_expand_kernel(const ZsJobDev *__rest
   const uint32_t ntok = ch.n_tok;
   uint16_t *out = scratch + ch.scratch;
   (void)jobs;
+#if KP_ON
+  const uint64_t kp_t0 = KP_NOW();
+  uint64_t kp_jump = 0;
+  uint32_t kp_rounds = 0, kp_jits = 0, kp_jrounds = 0, kp_batches = 0;
+#endif
   if (ch.ord != 0) {  // history before the chunk: markers 256 + w for position w - HIST
     uint32_t *r32 = reinterpret_cast<uint32_t *>(ring);
     for (uint32_t i = tid; i < HIST / 2; i += EXP_T) r32[i] = (MARK_BASE + 2 * i) | ((MARK_BASE + 2 * i + 1) << 16);
   }
   for (uint32_t i = tid; i < EXP_N; i += EXP_T) s_mark[i] = 0;
+#if KP_ON
+  const uint64_t kp_init = KP_NOW() - kp_t0;
+#endif
   uint32_t pos = 0, flushed = 0, stamp = 0;
   uint32_t tnext = tid < ntok ? tk[tid] : 0u;
   for (uint32_t tb = 0; tb < ntok; tb += EXP_T) {
@@ -750,8 +896,18 @@ __global__ void __launch_bounds__(EXP_T) zs_expand_kernel(const ZsJobDev *__rest
       bool any = false;
 #pragma unroll
       for (uint32_t w = 0; w < EXP_W; w++) any |= s_flag[w] != 0;
+#if KP_ON
+      kp_rounds++;
+      const uint64_t kj0 = KP_NOW();
+#endif
       if (any) {  // in-round sources: pointer jumping through LDS, one barrier per step
+#if KP_ON
+        kp_jrounds++;
+#endif
         for (uint32_t it = 0;; it++) {
+#if KP_ON
+          kp_jits++;
+#endif
           const uint32_t b = it & 1u;
           uint4 o;
           o.x = (unres & 1u) ? q[0] : (JR | v[0]);
@@ -780,6 +936,9 @@ __global__ void __launch_bounds__(EXP_T) zs_expand_kernel(const ZsJobDev *__rest
           }
         }
       }
+#if KP_ON
+      kp_jump += KP_NOW() - kj0;
+#endif
       if (e0 >= lo && e0 + EXP_E <= pos + S) {
         uint2 w2;
         w2.x = v[0] | (v[1] << 16);
@@ -792,6 +951,9 @@ __global__ void __launch_bounds__(EXP_T) zs_expand_kernel(const ZsJobDev *__rest
       }
     }
     pos += S;
+#if KP_ON
+    kp_batches++;
+#endif
   }
   exp_barrier();
   while (pos - flushed >= EXP_FLUSH) {
@@ -800,15 +962,93 @@ __global__ void __launch_bounds__(EXP_T) zs_expand_kernel(const ZsJobDev *__rest
     flushed += EXP_FLUSH;
   }
   for (uint32_t k = tid; k < pos - flushed; k += EXP_T) out[flushed + k] = ring[(flushed + k) & (HIST - 1)];
+#if KP_ON
+  if (wv == 0) {
+    const uint64_t tot = KP_NOW() - kp_t0;
+    KP_ADD(KP_E_BLOCKS, 1);
+    KP_ADD(KP_E_CYC_TOTAL, tot);
+    KP_MAX(KP_E_CYC_MAX, tot);
+    KP_ADD(KP_E_CYC_INIT, kp_init);
+    KP_ADD(KP_E_ROUNDS, kp_rounds);
+    KP_ADD(KP_E_JUMP_ITERS, kp_jits);
+    KP_ADD(KP_E_JUMP_ROUNDS, kp_jrounds);
+    KP_ADD(KP_E_CYC_JUMP, kp_jump);
+    KP_ADD(KP_E_BATCHES, kp_batches);
+  }
+#endif
+}
+
+// First dynamic header of every unit after the stream's first (the finder
+// only records BFINAL = 0, BTYPE = 2 starts whose header validated), one wave
+// per unit across the whole GPU: tables go to the unit's global table area and
+// the compact root image next to them; the parse pass then starts each lane
+// directly in symbol mode.  A header that does not decode is left to the parse
+// pass, which redoes it cooperatively and reports exactly.
+__global__ void __launch_bounds__(64) zs_unit_header_kernel(const ZsJobDev *__restrict__ jobs,
+                                                             const ZsHeadDev *__restrict__ heads,
+                                                             ZsChunkDev *__restrict__ units, uint32_t *__restrict__ tables) {
+  __shared__ BuildLDS B;
+  const uint32_t c = blockIdx.x;
+  const uint32_t lane = threadIdx.x;
+  const ZsChunkDev ch = units[c];
+  if (ch.start_bit == ZS_NONE || ch.ord == 0 || heads[ch.job].code != ZD_END) return;
+  const ZsJobDev jb = jobs[ch.job];
+  const uintptr_t ip = reinterpret_cast<uintptr_t>(jb.in);
+  const uint32_t mis = (uint32_t)(ip & 3u);
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(ip - mis);
+  const uint32_t end_byte = mis + (uint32_t)jb.in_len;
+  StageBits sb;
+  stage_bits(B, w, end_byte, ch.start_bit, sb);
+  if (ch.start_bit + 3 > end_byte * 8u || sb.peek(ch.start_bit, 3) != 4u) return;  // BFINAL 0, BTYPE 2
+  uint32_t bit = ch.start_bit + 3;
+  uint32_t *tabg = tables + (size_t)c * TABLE_STRIDE;
+  uint16_t *ctab = reinterpret_cast<uint16_t *>(tabg + TABLE_ENTRIES);
+  uint16_t *img = reinterpret_cast<uint16_t *>(tabg + TABLE_ENTRIES + TABLE_ENTRIES / 2);
+  uint32_t lbits = 9, dbits = 6;
+  if (wave_dyn_header(B, w, end_byte, bit, tabg, ctab, lbits, dbits, img, img + LROOT_N)) return;
+  if (lane == 0) {
+    units[c].hdr_bit = bit;
+    units[c].hdr_info = 1u | (lbits << 8) | (dbits << 12);
+  }
+}
+
+// compact copies of the fixed tables (after zs_fixed_tables_kernel's zlib layout)
+__global__ void __launch_bounds__(64) zs_fixed_compact_kernel(uint32_t *__restrict__ fixed) {
+  uint16_t *fc = reinterpret_cast<uint16_t *>(fixed + FIXED_ZLIB_WORDS);
+  for (uint32_t i = threadIdx.x; i < 512; i += WAVE) fc[i] = compact_len_entry(fixed[i]);
+  for (uint32_t i = threadIdx.x; i < 32; i += WAVE) fc[512 + i] = compact_dist_entry(fixed[512 + i]);
+}
+extern "C" void zs_launch_fixed_compact(uint32_t *fixed, hipStream_t st) {
+  hipLaunchKernelGGL(zs_fixed_compact_kernel, dim3(1), dim3(64), 0, st, fixed);
 }
 
 extern "C" void zs_launch_lane(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, ZsChunkDev *d_chunks, uint32_t nchunks,
                                uint16_t *d_scratch, uint32_t *d_tokens, uint32_t *d_tables, const uint32_t *d_fixed,
                                hipStream_t st, hipEvent_t *ev) {
   // ev (profiling, optional): [0] after parse, [1] after expand
+  hipLaunchKernelGGL(zs_unit_header_kernel, dim3(nchunks), dim3(WAVE), 0, st, d_jobs, d_heads, d_chunks, d_tables);
   hipLaunchKernelGGL(zs_lane_kernel, dim3((nchunks + WAVE - 1) / WAVE), dim3(WAVE), 0, st, d_jobs, d_heads, d_chunks,
                      nchunks, d_tokens, d_tables, d_fixed);
   if (ev) (void)hipEventRecord(ev[0], st);
   hipLaunchKernelGGL(zs_expand_kernel, dim3(nchunks), dim3(EXP_T), 0, st, d_jobs, d_chunks, d_scratch, d_tokens);
   if (ev) (void)hipEventRecord(ev[1], st);
+}
+
+// Counter readback (profiling builds only; product builds report 0 counters).
+extern "C" int zs_kprof_read(uint64_t *out, uint32_t n, int reset) {
+#if KP_ON
+  const uint32_t k = n < KP_COUNT ? n : KP_COUNT;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_kprof), k * sizeof(uint64_t)) != hipSuccess) return -1;
+  if (reset) {
+    static const unsigned long long z[KP_COUNT] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_kprof), z, sizeof z) != hipSuccess) return -1;
+  }
+  return (int)k;
+#else
+  (void)out;
+  (void)n;
+  (void)reset;
+  return 0;
+#endif
 }

@@ -29,15 +29,18 @@ extern "C" void zs_launch_decode(int d64, const ZsJobDev *d_jobs, const ZsHeadDe
 extern "C" void zs_launch_finish(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, const ZsDecDev *d_decs,
                                  uint32_t *d_checks, ZsResultDev *d_res, uint32_t njobs, hipStream_t stream);
 extern "C" void zs_launch_fixed_tables(uint32_t *fixed, hipStream_t st);
-extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, ZsChunkDev *d_chunks, uint32_t nchunks,
-                                  const uint32_t *d_find_ids, uint32_t nfind, const ZsCJobDev *d_cjobs, uint32_t ncjobs,
+extern "C" void zs_launch_fixed_compact(uint32_t *fixed, hipStream_t st);
+extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, ZsSegDev *d_segs, uint32_t nseg,
+                                  ZsCJobDev *d_cjobs, uint32_t ncjobs, ZsChunkDev *d_units, uint32_t nunit_slots,
                                   uint16_t *d_scratch, uint32_t *d_tokens, uint32_t *d_tables, const uint32_t *d_fixed,
                                   uint8_t *d_windows, ZsDecDev *d_decs, uint32_t *d_fallback, hipStream_t st,
                                   hipEvent_t *ev);
 
 namespace {
 
-constexpr size_t TABLE_ENTRIES_HOST = 1448 + 724;  // must match TABLE_STRIDE (zs_device.h)
+constexpr size_t TABLE_ENTRIES_HOST = 1448 + 724 + 160;  // must match TABLE_STRIDE (zs_device.h)
+constexpr size_t FIXED_WORDS_HOST = 544 + 272;      // must match FIXED_WORDS (zs_device.h)
+constexpr double UNIT_SLACK_HOST = 8192.0;          // must match UNIT_SLACK (chunk_kernels.hip)
 
 const char *const kMsgs[ZM_COUNT] = {
     nullptr,
@@ -94,12 +97,12 @@ struct Workspace {
   uint8_t *d_in = nullptr, *d_out = nullptr;
   uint32_t *d_fallback = nullptr;  // per job (cap_jobs)
   ZsCJobDev *d_cjobs = nullptr, *h_cjobs = nullptr;  // per job (cap_jobs)
-  // chunked path
-  size_t cap_chunks = 0;
-  ZsChunkDev *d_chunks = nullptr, *h_chunks = nullptr;
-  uint32_t *d_find = nullptr, *h_find = nullptr;
-  uint32_t *d_tables = nullptr;  // TABLE_STRIDE words per chunk
-  uint8_t *d_windows = nullptr;  // 32 KiB per chunk
+  // chunked path: search segments and decode-unit slots
+  size_t cap_segs = 0, cap_units = 0;
+  ZsSegDev *d_segs = nullptr, *h_segs = nullptr;
+  ZsChunkDev *d_chunks = nullptr, *h_chunks = nullptr;  // unit slots
+  uint32_t *d_tables = nullptr;  // TABLE_STRIDE words per unit slot
+  uint8_t *d_windows = nullptr;  // 32 KiB per unit slot
   size_t cap_scratch = 0;        // u16 entries (and u32 parse tokens, same count)
   uint16_t *d_scratch = nullptr;
   uint32_t *d_tokens = nullptr;
@@ -181,15 +184,19 @@ int ws_reserve_jobs(size_t n) {
   return 0;
 }
 
-int ws_reserve_chunks(size_t n, size_t scratch_entries) {
+int ws_reserve_chunks(size_t nseg, size_t nunits, size_t scratch_entries) {
   int r;
-  if (n > g_ws.cap_chunks) {
-    size_t c = std::max(n, g_ws.cap_chunks + g_ws.cap_chunks / 2);
-    if ((r = grow_dev(&g_ws.d_chunks, c)) || (r = grow_host(&g_ws.h_chunks, c)) || (r = grow_dev(&g_ws.d_find, c)) ||
-        (r = grow_host(&g_ws.h_find, c)) || (r = grow_dev(&g_ws.d_tables, c * TABLE_ENTRIES_HOST)) ||
-        (r = grow_dev(&g_ws.d_windows, c * 32768)))
+  if (nseg > g_ws.cap_segs) {
+    size_t c = std::max(nseg, g_ws.cap_segs + g_ws.cap_segs / 2);
+    if ((r = grow_dev(&g_ws.d_segs, c)) || (r = grow_host(&g_ws.h_segs, c))) return r;
+    g_ws.cap_segs = c;
+  }
+  if (nunits > g_ws.cap_units) {
+    size_t c = std::max(nunits, g_ws.cap_units + g_ws.cap_units / 2);
+    if ((r = grow_dev(&g_ws.d_chunks, c)) || (r = grow_host(&g_ws.h_chunks, c)) ||
+        (r = grow_dev(&g_ws.d_tables, c * TABLE_ENTRIES_HOST)) || (r = grow_dev(&g_ws.d_windows, c * 32768)))
       return r;
-    g_ws.cap_chunks = c;
+    g_ws.cap_units = c;
   }
   if (scratch_entries > g_ws.cap_scratch) {
     size_t c = std::max(scratch_entries, g_ws.cap_scratch + g_ws.cap_scratch / 4);
@@ -197,8 +204,9 @@ int ws_reserve_chunks(size_t n, size_t scratch_entries) {
     g_ws.cap_scratch = c;
   }
   if (!g_ws.d_fixed) {
-    if ((r = grow_dev(&g_ws.d_fixed, 544))) return r;
+    if ((r = grow_dev(&g_ws.d_fixed, FIXED_WORDS_HOST))) return r;
     zs_launch_fixed_tables(g_ws.d_fixed, g_ws.stream);
+    zs_launch_fixed_compact(g_ws.d_fixed, g_ws.stream);
   }
   return 0;
 }
@@ -299,7 +307,7 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
   // the wave-per-stream serial decoder.  Lists in h_ids: [serial std | d64 | chunked].
   const uint32_t C = chunk_bytes();
   uint32_t n_std = 0, n_d64 = 0, n_cj = 0;
-  size_t nchunks = 0, scratch_need = 0;
+  size_t nseg = 0, nunit_slots = 0, scratch_need = 0;
   std::vector<uint32_t> cj_list;
   for (uint32_t k = 0; k < nv; k++) {
     const ZsJobDev &jd = g_ws.h_jobs[k];
@@ -307,7 +315,7 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
     const bool chunk = chunking_enabled() && !jd.d64 && jd.in_len >= 4ull * C && ratio <= 64.0;
     if (chunk) {
       cj_list.push_back(k);
-      nchunks += (jd.in_len + C - 1) / C;
+      nseg += (jd.in_len + C - 1) / C;
     }
   }
   for (uint32_t k = 0; k < nv; k++)
@@ -315,41 +323,41 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
   for (uint32_t k = 0; k < nv; k++)
     if (g_ws.h_jobs[k].d64) g_ws.h_ids[n_std + n_d64++] = k;
   for (uint32_t k : cj_list) g_ws.h_ids[n_std + n_d64 + n_cj++] = k;
-  uint32_t nfind = 0;
   if (n_cj) {
-    if ((r = ws_reserve_chunks(nchunks, 0))) return r;
-    size_t ci = 0;
+    if ((r = ws_reserve_chunks(nseg, 0, 0))) return r;
+    size_t si = 0;
     for (uint32_t q = 0; q < n_cj; q++) {
       const uint32_t k = cj_list[q];
       const ZsJobDev &jd = g_ws.h_jobs[k];
-      const uint32_t nc = (uint32_t)((jd.in_len + C - 1) / C);
+      const uint32_t ns = (uint32_t)((jd.in_len + C - 1) / C);
       const double ratio = std::max(1.0, (double)jd.out_cap / (double)jd.in_len);
-      // scratch per chunk: 2.5x the expected output of a nominal chunk plus one
-      // block of slack; a chunk that overflows sends its stream to the fallback
-      const uint32_t cap = (uint32_t)std::min<double>(4.0e9, 2.0 * C * ratio + 49152.0);
-      g_ws.h_cjobs[q] = ZsCJobDev{k, (uint32_t)ci, nc, 0};
-      for (uint32_t o = 0; o < nc; o++, ci++) {
-        ZsChunkDev ch{};
-        ch.job = k;
-        ch.ord = o;
-        ch.first = (uint32_t)(ci - o);
-        ch.nchunks = nc;
-        ch.s_byte = o * C;
-        ch.e_byte = (uint32_t)std::min<uint64_t>((uint64_t)(o + 1) * C, jd.in_len);
-        ch.start_bit = ZS_NONE;
-        ch.scratch = scratch_need;
-        ch.cap = cap;
-        ch.tok = scratch_need;  // tokens: same offsets, u32 units (one token yields >= 1 entry)
-        ch.tcap = cap;
-        ch.chain_next = ZS_NONE;
-        scratch_need += ((size_t)cap + 64 + 7) & ~size_t(7);
-        g_ws.h_chunks[ci] = ch;
-        if (o) g_ws.h_find[nfind++] = (uint32_t)ci;
+      const uint32_t max_units = ns * SEG_SLOTS + 1;
+      // zs_plan_kernel gives each unit 2 x span x ratio + slack entries; spans
+      // of a job's units sum to at most its input (+1 byte of rounding each)
+      const size_t reserve = (size_t)(2.0 * ratio * ((double)jd.in_len + max_units)) +
+                             (size_t)max_units * ((size_t)UNIT_SLACK_HOST + 8) + 64;
+      ZsCJobDev cj{};
+      cj.job = k;
+      cj.first_seg = (uint32_t)si;
+      cj.nseg = ns;
+      cj.unit0 = (uint32_t)nunit_slots;
+      cj.max_units = max_units;
+      cj.scratch0 = scratch_need;
+      cj.scratch_n = reserve;
+      g_ws.h_cjobs[q] = cj;
+      for (uint32_t o = 0; o < ns; o++, si++) {
+        ZsSegDev sg{};
+        sg.job = k;
+        sg.ord = o;
+        sg.s_byte = o * C;
+        sg.e_byte = (uint32_t)std::min<uint64_t>((uint64_t)(o + 1) * C, jd.in_len);
+        g_ws.h_segs[si] = sg;
       }
+      nunit_slots += max_units;
+      scratch_need += (reserve + 7) & ~size_t(7);
     }
-    if ((r = ws_reserve_chunks(nchunks, scratch_need))) return r;
-    HIP_OK(hipMemcpyAsync(g_ws.d_chunks, g_ws.h_chunks, nchunks * sizeof(ZsChunkDev), hipMemcpyHostToDevice, st));
-    HIP_OK(hipMemcpyAsync(g_ws.d_find, g_ws.h_find, nfind * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+    if ((r = ws_reserve_chunks(nseg, nunit_slots, scratch_need))) return r;
+    HIP_OK(hipMemcpyAsync(g_ws.d_segs, g_ws.h_segs, nseg * sizeof(ZsSegDev), hipMemcpyHostToDevice, st));
     HIP_OK(hipMemcpyAsync(g_ws.d_cjobs, g_ws.h_cjobs, n_cj * sizeof(ZsCJobDev), hipMemcpyHostToDevice, st));
   }
   HIP_OK(hipMemcpyAsync(g_ws.d_jobs, g_ws.h_jobs, nv * sizeof(ZsJobDev), hipMemcpyHostToDevice, st));
@@ -358,7 +366,8 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
   if (ev) HIP_OK(hipEventRecord(ev[0], st));
   zs_launch_header(g_ws.d_jobs, g_ws.d_heads, nv, st);
   if (n_cj)
-    zs_launch_chunked(g_ws.d_jobs, g_ws.d_heads, g_ws.d_chunks, (uint32_t)nchunks, g_ws.d_find, nfind, g_ws.d_cjobs, n_cj,
+    zs_launch_chunked(g_ws.d_jobs, g_ws.d_heads, g_ws.d_segs, (uint32_t)nseg, g_ws.d_cjobs, n_cj, g_ws.d_chunks,
+                      (uint32_t)nunit_slots,
                       g_ws.d_scratch, g_ws.d_tokens, g_ws.d_tables, g_ws.d_fixed, g_ws.d_windows, g_ws.d_decs,
                       g_ws.d_fallback, st, ev ? ev + 1 : nullptr);
   else if (ev)
@@ -392,30 +401,29 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
     g_ws.prof_launches++;
   }
   g_ws.stats[0] = n_cj;
-  g_ws.stats[1] = (uint32_t)nchunks;
+  g_ws.stats[1] = 0;
   g_ws.stats[2] = 0;
   g_ws.stats[3] = n_std + n_d64;
   if (n_cj) {
     std::vector<uint32_t> fb(nv);
     HIP_OK(hipMemcpy(fb.data(), g_ws.d_fallback, nv * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(g_ws.h_cjobs, g_ws.d_cjobs, n_cj * sizeof(ZsCJobDev), hipMemcpyDeviceToHost));
     for (uint32_t k : cj_list) g_ws.stats[2] += fb[k];
-  }
-  if (std::getenv("ZS_DEBUG_CHUNKS") && n_cj) {
-    std::vector<uint32_t> fb(nv);
-    HIP_OK(hipMemcpy(fb.data(), g_ws.d_fallback, nv * sizeof(uint32_t), hipMemcpyDeviceToHost));
-    HIP_OK(hipMemcpy(g_ws.h_chunks, g_ws.d_chunks, nchunks * sizeof(ZsChunkDev), hipMemcpyDeviceToHost));
-    size_t found = 0, inch = 0;
-    for (size_t i = 0; i < nchunks; i++) {
-      found += g_ws.h_chunks[i].start_bit != ZS_NONE;
-      inch += g_ws.h_chunks[i].in_chain;
-    }
-    uint32_t nfb = 0;
-    for (uint32_t k : cj_list) nfb += fb[k];
-    std::fprintf(stderr, "[zs] chunked jobs %u chunks %zu found %zu in_chain %zu fallback %u\n", n_cj, nchunks, found, inch, nfb);
-    for (size_t i = 0; i < nchunks && i < 8; i++) {
-      const ZsChunkDev &c = g_ws.h_chunks[i];
-      std::fprintf(stderr, "  chunk %zu ord %u start %u end %u code %d n_out %u chain %u\n", i, c.ord, c.start_bit, c.end_bit,
-                   c.code, c.n_out, c.in_chain);
+    for (uint32_t q = 0; q < n_cj; q++) g_ws.stats[1] += g_ws.h_cjobs[q].nunits;
+    if (std::getenv("ZS_DEBUG_CHUNKS")) {
+      HIP_OK(hipMemcpy(g_ws.h_chunks, g_ws.d_chunks, nunit_slots * sizeof(ZsChunkDev), hipMemcpyDeviceToHost));
+      size_t inch = 0, stopped = 0;
+      for (size_t i = 0; i < nunit_slots; i++) {
+        inch += g_ws.h_chunks[i].in_chain;
+        stopped += (g_ws.h_chunks[i].code & 0xff) == ZD_STOP;
+      }
+      std::fprintf(stderr, "[zs] chunked jobs %u segments %zu units %u in_chain %zu stopped %zu fallback %u\n", n_cj, nseg,
+                   g_ws.stats[1], inch, stopped, g_ws.stats[2]);
+      for (size_t i = 0; i < nunit_slots && i < 8; i++) {
+        const ZsChunkDev &c = g_ws.h_chunks[i];
+        std::fprintf(stderr, "  unit %zu ord %u start %u stop %u end %u code %d n_out %u ntok %u cap %u chain %u\n", i, c.ord,
+                     c.start_bit, c.stop_bit, c.end_bit, c.code, c.n_out, c.n_tok, c.cap, c.in_chain);
+      }
     }
   }
   for (uint32_t i = 0; i < n; i++) {

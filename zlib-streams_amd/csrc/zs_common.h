@@ -89,51 +89,69 @@ struct ZsDecDev {
 };
 
 // ---------------------------------------------------------------------------
-// Speculative chunking of large raw/zlib/gzip streams (one lane per chunk).
-// A stream's deflate data is cut into fixed-size compressed chunks; each chunk
-// >= 1 searches its range for a dynamic-block header (zs_find_kernel), every
-// chunk with a start decodes up to the first block end at or past the next
-// chunk's start, emitting u16 entries where values >= 256 name bytes of the
-// unknown 32 KiB history before the chunk (markers).  zs_link_kernel verifies
-// that the chunks tile the stream exactly (chunk j ends where chunk j+1
-// starts), resolves the history windows in order, and zs_emit_kernel writes
-// the final bytes.  Any inconsistency sends the whole stream to the exact
-// serial decoder, so results never depend on the speculation.
+// Speculative chunking of large raw/zlib/gzip streams.
+// A stream's deflate data is cut into fixed-size search SEGMENTS; the block
+// finder (zs_find_kernel) records up to SEG_SLOTS dynamic-block starts per
+// segment, and zs_plan_kernel turns the stream start plus every recorded start
+// into an ordered list of decode UNITS (ZsChunkDev), each decoding from its
+// start to the first block end at or past the next unit's start.  Unit outputs
+// are u16 entries where values >= 256 name bytes of the unknown 32 KiB history
+// before the unit (markers).  zs_link_kernel follows the chain (a unit's end
+// must be the start of a later unit; starts that are not true block
+// boundaries are skipped), resolves the history windows in order, and
+// zs_emit_kernel writes the final bytes.  A stream whose chain breaks goes to
+// the exact serial decoder, so results never depend on the speculation.
 // ---------------------------------------------------------------------------
 #define ZS_NONE 0xffffffffu
-#define ZD_STOP 6  // chunk decode reached its stop bit at a block boundary
+#define ZD_STOP 6     // unit decode reached its stop bit at a block boundary
+#define SEG_SLOTS 4   // block starts recorded per search segment
 
-struct ZsChunkDev {
+struct ZsSegDev {
   uint32_t job;        // job index
-  uint32_t ord;        // ordinal of the chunk within its job
-  uint32_t first;      // index of the job's chunk 0 in the chunk array
-  uint32_t nchunks;    // chunks of this job
-  uint32_t s_byte;     // block-search range [s_byte, e_byte) of the job input
+  uint32_t ord;        // ordinal of the segment within its job
+  uint32_t s_byte;     // search range [s_byte, e_byte) of the job input
   uint32_t e_byte;
-  uint32_t start_bit;  // decode start (bits from the 4-byte-aligned input base), ZS_NONE if none
+  uint32_t ncand;      // block starts found (<= SEG_SLOTS), ascending
+  uint32_t cand[SEG_SLOTS];  // bit offsets from the 4-byte-aligned input base
+  uint32_t pad[3];
+};
+
+struct ZsChunkDev {    // one decode unit
+  uint32_t job;        // job index
+  uint32_t ord;        // 0 = the stream's first unit (no history before it)
+  uint32_t first;      // first unit of this job
+  uint32_t nunits;     // units of this job
+  uint32_t start_bit;  // decode start (bits from the 4-byte-aligned input base)
+  uint32_t stop_bit;   // next unit's start (ZS_NONE: decode to the final block)
   uint32_t end_bit;    // where decoding stopped
   int32_t code;        // ZD_* | (ZsMsg << 8)
   uint32_t n_out;      // u16 entries produced
-  uint64_t scratch;    // entry offset of this chunk's u16 scratch region
   uint32_t cap;        // scratch capacity (entries)
-  uint32_t chain_next; // next chunk in the verified chain (ZS_NONE at the end)
-  uint64_t out_off;    // output byte offset (verified chain members)
+  uint64_t scratch;    // entry offset of this unit's u16 scratch region
+  uint32_t chain_next; // next unit in the verified chain (ZS_NONE at the end)
   uint32_t in_chain;   // 1 = member of the verified chain of a non-fallback job
+  uint64_t out_off;    // output byte offset (verified chain members)
   uint32_t n_tok;      // tokens produced by the parse pass
-  uint64_t tok;        // offset of this chunk's token region (u32 units)
   uint32_t tcap;       // token capacity
-  uint32_t pad;
+  uint64_t tok;        // offset of this unit's token region (u32 units)
+  uint32_t hdr_bit;    // bit after the first block's header (when prebuilt)
+  uint32_t hdr_info;   // bit 0: first header prebuilt by zs_unit_header_kernel;
+                       // bits 8-11 / 12-15: lit/len and distance root bits
 };
 
 // Parse-pass tokens (u32), consumed by the expand pass:
 //   hi16 == 0          literal, byte in bits 0-7 (stored-block bytes included)
 //   hi16 in [3, 258]   match: length = hi16, distance = lo16 + 1
 
-struct ZsCJobDev {
+struct ZsCJobDev {     // a job on the chunked path
   uint32_t job;        // job index
-  uint32_t first;      // first chunk
-  uint32_t nchunks;
-  uint32_t pad;
+  uint32_t first_seg;  // first search segment
+  uint32_t nseg;
+  uint32_t unit0;      // first unit slot reserved for this job (host)
+  uint32_t max_units;  // unit slots reserved (nseg * SEG_SLOTS + 1)
+  uint32_t nunits;     // units planned (zs_plan_kernel)
+  uint64_t scratch0;   // first scratch entry reserved for this job (host)
+  uint64_t scratch_n;  // scratch entries reserved
 };
 
 // Final per-job result (device -> host), zlib z_stream fields after the call.

@@ -1,0 +1,24 @@
+// zs_kprof.h -- optional in-kernel phase counters (build with -DZS_KPROF, i.e.
+// `make prof` -> libzstreams_mi355x_prof.so).  Product builds compile every
+// macro to nothing.  Counters are u64 sums over waves (cycles from s_memtime,
+// event counts), read back with zs_kprof_read().
+#pragma once
+#include <stdint.h>
+
+enum ZsKprof {
+  // parse pass (zs_lane_kernel), per wave
+  KP_P_WAVES = 0, KP_P_CYC_TOTAL, KP_P_CYC_COOP, KP_P_CYC_STEPS, KP_P_CYC_FLUSH, KP_P_GROUPS, KP_P_COOP,
+  KP_P_LANE_STEPS, KP_P_WAVE_STEPS, KP_P_SLOW_LIT, KP_P_SLOW_DIST, KP_P_CYC_MAX, KP_P_CYC_INIT, KP_P_REFILLS,
+  // expand pass (zs_expand_kernel), per workgroup (wave 0)
+  KP_E_BLOCKS = 16, KP_E_CYC_TOTAL, KP_E_ROUNDS, KP_E_JUMP_ITERS, KP_E_CYC_JUMP, KP_E_BATCHES, KP_E_CYC_MAX,
+  KP_E_CYC_INIT, KP_E_JUMP_ROUNDS,
+  KP_COUNT = 64
+};
+
+#ifdef ZS_KPROF
+#define KP_ON 1
+#define KP_NOW() ((uint64_t)__builtin_amdgcn_s_memtime())
+#else
+#define KP_ON 0
+#define KP_NOW() ((uint64_t)0)
+#endif

@@ -18,7 +18,8 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libzstreams_mi355x.so")
+# ZS_LIB selects another build of the same library (e.g. the profiling build)
+LIB_PATH = os.environ.get("ZS_LIB") or os.path.join(HERE, "libzstreams_mi355x.so")
 
 Z_OK, Z_STREAM_END, Z_NEED_DICT = 0, 1, 2
 Z_STREAM_ERROR, Z_DATA_ERROR, Z_MEM_ERROR, Z_BUF_ERROR = -2, -3, -4, -5
@@ -45,6 +46,7 @@ _SIGS = {
     "zs_profile_read": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                        ctypes.POINTER(ctypes.c_uint64)]),
     "zs_profile_stages": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.c_uint32]),
+    "zs_kprof_read": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32, ctypes.c_int]),
     "zs_last_stats": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint32)]),
     "zs_synchronize": (ctypes.c_int, []),
     "zs_version": (ctypes.c_char_p, []), "zs_last_error": (ctypes.c_char_p, []),
@@ -167,6 +169,16 @@ def profile_stages():
     if k < 0:
         _check(k)
     return {PROFILE_STAGES[i]: a[i] for i in range(k)}
+
+
+def kprof_read(reset=True):
+    """In-kernel counters of the profiling build (ZS_LIB=.../libzstreams_mi355x_prof.so);
+    an empty list with the product library."""
+    a = (ctypes.c_uint64 * 64)()
+    k = lib().zs_kprof_read(a, 64, 1 if reset else 0)
+    if k < 0:
+        raise ZStreamsError("zs_kprof_read failed")
+    return list(a[:k])
 
 
 def last_stats():
