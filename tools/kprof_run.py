@@ -14,7 +14,8 @@ NAMES = {0: "p_waves", 1: "p_cyc_total", 2: "p_cyc_coop", 3: "p_cyc_steps", 4: "
          6: "p_coop_calls", 7: "p_lane_steps", 8: "p_wave_steps", 9: "p_slow_lit", 10: "p_slow_dist",
          11: "p_cyc_max", 12: "p_cyc_init", 13: "p_refills",
          16: "e_blocks", 17: "e_cyc_total", 18: "e_rounds", 19: "e_jump_iters", 20: "e_cyc_jump", 21: "e_batches",
-         22: "e_cyc_max", 23: "e_cyc_init", 24: "e_jump_rounds"}
+         22: "e_cyc_max", 23: "e_cyc_init", 24: "e_jump_rounds",
+         40: "s_refill1", 41: "s_lit", 42: "s_refill2", 43: "s_dist", 44: "s_tail"}
 
 
 def main():
@@ -54,6 +55,8 @@ def main():
         "expand_jump_rounds_frac": d["e_jump_rounds"] / max(d["e_rounds"], 1),
         "expand_jump_iters_per_jround": d["e_jump_iters"] / max(d["e_jump_rounds"], 1),
         "expand_frac_init": d["e_cyc_init"] / max(d["e_cyc_total"], 1),
+        "step_phase_cycles_per_wave_step": {k: d[k] / max(d["p_wave_steps"], 1)
+                                            for k in ("s_refill1", "s_lit", "s_refill2", "s_dist", "s_tail")},
     }
     out = {"raw": d, "derived": derived}
     print(json.dumps(out, indent=1))

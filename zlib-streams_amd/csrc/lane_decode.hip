@@ -56,6 +56,7 @@ __device__ __forceinline__ uint32_t kp_wave_max(uint32_t v) {
 #define LROOT_N 256      // 8-bit literal/length root (LDS)
 #define DROOT_N 64       // 6-bit distance root
 #define ZBUILD 852       // zlib build area (ENOUGH_LENS; the distance table reuses it)
+#define RING 16          // input words per lane staged in LDS for a group of steps
 
 // compact entry (u16): [1:0] kind, [5:2] code bits, [15:6] symbol.
 // CK_SLOW: [5:2] = sub-table index bits (0 = invalid code), [15:6] = sub-table
@@ -115,10 +116,15 @@ __device__ __forceinline__ uint32_t in_word_g(gcu32 *w, uint32_t wi, uint32_t en
 
 enum { LM_SYM = 0, LM_BLOCK = 1, LM_DONE = 2 };
 
+struct KpPhase {
+  uint64_t t[5];
+};
+
 struct LaneState {
   gcu32 *w;           // 4-byte aligned input base
   uint32_t end_byte, limit;
-  uint32_t wi, nw, nkeep, nbits;  // nw: next input word, raw; nkeep: its valid bytes (0..4)
+  uint32_t wi, nw, nkeep, nbits;  // nw: next input word (index wi); nkeep: its valid bytes (0..4)
+  uint32_t rk;        // ring index of nw during a group
   uint32_t lastw;     // last word index holding input
   uint64_t hold;
   gu32 *tok;          // token output (parse pass)
@@ -156,16 +162,41 @@ __device__ __forceinline__ void lane_prime(LaneState &s, uint32_t bit) {
   s.hold = (uint64_t)w0 >> (bit & 31);
   s.nbits = 32 - (bit & 31);
 }
-__device__ __forceinline__ void lane_refill(LaneState &s) {
+// refill from the group's LDS ring (words are masked at fill time)
+__device__ __forceinline__ void lane_refill(LaneState &s, const uint32_t *__restrict__ rp) {
   if (s.nbits < 32) {
 #if KP_ON
     s.kp_refills++;
 #endif
-    s.hold |= (uint64_t)lane_take(s) << s.nbits;
+    s.hold |= (uint64_t)s.nw << s.nbits;
     s.nbits += 32;
     s.wi++;
-    lane_fetch(s);
+    s.rk++;
+    s.nw = rp[s.rk * WAVE];
   }
+}
+// group start: ring[0..RING) = input words wi .. wi + RING - 1 (masked)
+__device__ __forceinline__ void lane_fill_ring(LaneState &s, uint32_t *__restrict__ rp) {
+  uint32_t v[RING];
+  if (s.wi + RING <= s.lastw) {  // all full words: 16-byte loads
+    const uint32_t *src = (const uint32_t *)(s.w + s.wi);
+#pragma unroll
+    for (int q = 0; q < RING / 4; q++) {
+      uint4 x;
+      __builtin_memcpy(&x, src + 4 * q, 16);
+      v[4 * q] = x.x;
+      v[4 * q + 1] = x.y;
+      v[4 * q + 2] = x.z;
+      v[4 * q + 3] = x.w;
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < RING; q++) v[q] = in_word_g(s.w, s.wi + q, s.end_byte);
+  }
+#pragma unroll
+  for (int q = 0; q < RING; q++) rp[q * WAVE] = v[q];
+  s.nw = v[0];
+  s.rk = 0;
 }
 // bit position of the next unconsumed bit (wi = index of the prefetched word)
 __device__ __forceinline__ uint32_t lane_pos(const LaneState &s) { return s.wi * 32u - s.nbits; }
@@ -186,9 +217,52 @@ __device__ __noinline__ uint32_t invalid_code_bits(const uint32_t *zt, uint32_t 
 // of the input read as zero; truncation is decided once the symbol is
 // complete (or, for an invalid code, from zlib's code length), which gives
 // the same ZD_TRUNC / error split as checking before every bit pull.
+// code longer than the 6-bit distance root: canonical decode from the lane's
+// 64-byte tail (two LDS round trips); returns a compact entry (total length)
+__device__ __forceinline__ uint32_t dist_tail(const uint32_t *__restrict__ dtl, uint32_t hold) {
+  const uint4 a = *reinterpret_cast<const uint4 *>(dtl);
+  const uint4 b = *reinterpret_cast<const uint4 *>(dtl + 4);
+  const uint32_t rev = __builtin_bitreverse32(hold) >> 17;  // next 15 bits, first bit highest
+  const uint32_t lw[5] = {a.x, a.y, a.z, a.w, b.x};
+  uint32_t L = 7, fl = lw[0] & 0xffffu, of = (b.x >> 16) & 0xffu;  // lim[0], offs[0]
+#pragma unroll
+  for (int k = 1; k < 9; k++) {
+    const uint32_t lim = (lw[k >> 1] >> (16 * (k & 1))) & 0xffffu;
+    // offs[k] lives at byte 18 + k: word 4 + (2 + k) / 4 of the 32 bytes read
+    const uint32_t ob = 18 + k;
+    const uint32_t ow = ob < 20 ? b.x : (ob < 24 ? b.y : b.z);
+    const uint32_t ofk = (ow >> (8 * (ob & 3))) & 0xffu;
+    const bool ge = rev >= lim;
+    L += ge ? 1u : 0u;
+    fl = ge ? lim : fl;
+    of = ge ? ofk : of;
+  }
+  const uint32_t idx = of + ((rev - fl) >> (15u - L));
+  const uint32_t sym = reinterpret_cast<const uint8_t *>(dtl)[27 + min(idx, 29u)];
+  return CK_SYM | (L << 2) | (sym << 6);
+}
+
+#if KP_ON
+#define KPT(i)                       \
+  do {                               \
+    const uint64_t now_ = KP_NOW();  \
+    kp.t[i] += now_ - kp_last;       \
+    kp_last = now_;                  \
+  } while (0)
+#else
+#define KPT(i) ((void)0)
+#endif
+
 __device__ __forceinline__ bool lane_step(LaneState &s, const uint16_t *__restrict__ lt, const uint16_t *__restrict__ dt,
-                                          uint32_t *__restrict__ tb) {
-  lane_refill(s);
+                                          uint32_t *__restrict__ tb, const uint32_t *__restrict__ dtl,
+                                          const uint32_t *__restrict__ rp, KpPhase &kp) {
+#if KP_ON
+  uint64_t kp_last = KP_NOW();
+#else
+  (void)kp;
+#endif
+  lane_refill(s, rp);
+  KPT(0);
   uint32_t e = lt[(uint32_t)s.hold & (LROOT_N - 1)];
 #if KP_ON
   s.kp_steps++;
@@ -214,6 +288,7 @@ __device__ __forceinline__ bool lane_step(LaneState &s, const uint16_t *__restri
     }
     e = e2;
   }
+  KPT(1);
   const uint32_t used = (e >> 2) & 15u;
   s.hold >>= used;
   s.nbits -= used;
@@ -233,7 +308,7 @@ __device__ __forceinline__ bool lane_step(LaneState &s, const uint16_t *__restri
     len += (uint32_t)s.hold & ((1u << xb) - 1u);
     s.hold >>= xb;
     s.nbits -= xb;
-    lane_refill(s);
+    lane_refill(s, rp);
     uint32_t d = dt[(uint32_t)s.hold & (DROOT_N - 1)];
     if ((d & 3u) == CK_SLOW) {
 #if KP_ON
@@ -241,7 +316,7 @@ __device__ __forceinline__ bool lane_step(LaneState &s, const uint16_t *__restri
 #endif
       const uint32_t op = (d >> 2) & 15u;
       uint32_t d2 = CK_SLOW;
-      if (op) d2 = s.cd[(d >> 6) + (((uint32_t)s.hold >> s.dbits) & ((1u << op) - 1u))];
+      if (op) d2 = dist_tail(dtl, (uint32_t)s.hold);
       if ((d2 & 3u) == CK_SLOW) {
         const uint32_t dused = invalid_code_bits(s.zd, s.zdmask, (uint32_t)s.hold);
         s.code = lane_pos(s) + dused > s.limit ? ZD_TRUNC : (ZD_ERROR | (ZM_DIST_CODE << 8));
@@ -263,11 +338,13 @@ __device__ __forceinline__ bool lane_step(LaneState &s, const uint16_t *__restri
     s.hold >>= dx;
     s.nbits -= dused + dx;
   }
+  KPT(2);
   if (lane_pos(s) > s.limit) {
     s.code = ZD_TRUNC;
     s.mode = LM_DONE;
     return true;
   }
+  KPT(3);
   if (kind == CK_EOB) {
     s.bit = lane_pos(s);
     s.mode = LM_BLOCK;
@@ -284,6 +361,7 @@ __device__ __forceinline__ bool lane_step(LaneState &s, const uint16_t *__restri
     return true;
   }
   tb[s.gk * WAVE] = kind == CK_SYM ? sym : ((len << 16) | (dist - 1u));
+  KPT(4);
   s.gk++;
   s.ntok++;
   s.pos += len;
@@ -316,12 +394,30 @@ struct BuildLDS {  // one wave's header-decode / table-build area
   uint32_t scr[32];
 };
 
+// Distance codes longer than the 6-bit root decode canonically from 64 bytes
+// per lane (src/inftrees.c assigns codes canonically: consecutive values in
+// symbol order within a length, lengths in increasing order):
+//   [0, 18)  u16 lim[k]: left-aligned 15-bit end of the length-(6+k) codes
+//   [18, 27) u8 offs[k]: rank of the first length-(7+k) code among tail codes
+//   [27, 57) u8 sym[]:   tail symbols (length >= 7) in canonical order
+#define DTAIL_BYTES 64
+
+// Input ring: at every group start each lane loads its next RING input words
+// into ring[k][lane] (lane-interleaved: conflict-free whatever k each lane
+// reads); the steps refill from it, one word prefetched ahead, so a refill
+// never waits on global memory.  Like tokbuf it lives only during a group and
+// shares space with the header build area.
+
 struct LaneLDS {
   uint16_t lroot[WAVE][LROOT_N];
   uint16_t droot[WAVE][DROOT_N];
+  uint32_t dtail[WAVE][DTAIL_BYTES / 4];
   union {
     BuildLDS b;
-    uint32_t tokbuf[GROUP][WAVE];
+    struct {
+      uint32_t tokbuf[GROUP][WAVE];
+      uint32_t ring[RING][WAVE];
+    } g;
   };
 };
 
@@ -344,6 +440,36 @@ __device__ __forceinline__ uintptr_t readlane_ptr(const void *p, uint32_t ln) {
   return (uintptr_t)(((uint64_t)hi << 32) | lo);
 }
 
+// canonical tail of a distance code (lengths dl[0..n)); one lane writes it
+__device__ void build_dist_tail(const uint16_t *dl, uint32_t n, uint8_t *out) {
+  uint32_t count[16];
+#pragma unroll
+  for (int L = 0; L < 16; L++) count[L] = 0;
+  for (uint32_t i = 0; i < n; i++) count[dl[i] & 15u]++;
+  count[0] = 0;
+  uint32_t code = 0, first[16];
+  first[0] = 0;
+  for (int L = 1; L < 16; L++) {
+    code = (code + count[L - 1]) << 1;
+    first[L] = code;
+  }
+  uint16_t *lim = reinterpret_cast<uint16_t *>(out);
+  for (int k = 0; k < 9; k++) {
+    const int L = 6 + k;
+    const uint32_t v = (first[L] + count[L]) << (15 - L);
+    lim[k] = (uint16_t)min(v, 0xffffu);
+  }
+  uint32_t rank = 0;
+  for (int k = 0; k < 9; k++) {
+    out[18 + k] = (uint8_t)rank;
+    rank += count[7 + k];
+  }
+  uint32_t r = 0;
+  for (int L = 7; L < 16; L++)
+    for (uint32_t i = 0; i < n; i++)
+      if (dl[i] == (uint32_t)L && r < 30) out[27 + r++] = (uint8_t)i;
+}
+
 // Dynamic block header after the 3 block-type bits (src/inflate.c:905-1033):
 // code-length code, code lengths, then the literal/length and distance tables
 // (src/inftrees.c restated in build_table) into the unit's global table area
@@ -352,7 +478,7 @@ __device__ __forceinline__ uintptr_t readlane_ptr(const void *p, uint32_t ln) {
 // lane calls it with the same arguments.  Returns 0, or ZD_* | msg << 8.
 __device__ int wave_dyn_header(BuildLDS &B, const uint32_t *w, uint32_t end_byte, uint32_t &bit, uint32_t *tabg,
                                uint16_t *ctab, uint32_t &lbits, uint32_t &dbits, uint16_t *lroot_out,
-                               uint16_t *droot_out) {
+                               uint16_t *droot_out, uint8_t *dtail_out) {
   const uint32_t lane = lane_id();
   const uint32_t limit = end_byte * 8u;
   StageBits sb;
@@ -438,6 +564,7 @@ __device__ int wave_dyn_header(BuildLDS &B, const uint32_t *w, uint32_t end_byte
     ctab[DIST_TABLE_OFF + i] = compact_dist_entry(B.tab[i], i < (1u << dbits) ? 0u : dbits);
   }
   droot_out[lane] = compact_dist_entry(B.tab[lane & ((1u << dbits) - 1u)]);
+  if (lane == 0) build_dist_tail(B.lens + nlen, ndist, dtail_out);
   __builtin_amdgcn_wave_barrier();
   return 0;
 }
@@ -541,7 +668,8 @@ __device__ void coop_block(LaneState &s, uint32_t ln, LaneLDS &L, uint32_t *lane
       break;
     }
     {
-      const int hc = wave_dyn_header(L.b, w, end_byte, bit, tabg, ctab, lbits, dbits, L.lroot[ln], L.droot[ln]);
+      const int hc = wave_dyn_header(L.b, w, end_byte, bit, tabg, ctab, lbits, dbits, L.lroot[ln], L.droot[ln],
+                                     reinterpret_cast<uint8_t *>(L.dtail[ln]));
       if (hc) {
         code = hc;
         break;
@@ -605,7 +733,7 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
   s.zlmask = s.zdmask = 0;
   s.lbits = s.dbits = 0;
   s.capx = 0;
-  s.wi = s.nw = s.nkeep = s.nbits = s.lastw = s.gk = 0;
+  s.wi = s.nw = s.nkeep = s.nbits = s.lastw = s.gk = s.rk = 0;
 #if KP_ON
   const uint64_t kp_t0 = KP_NOW();
   uint64_t kp_coop = 0, kp_steps_c = 0, kp_flush = 0, kp_init = 0;
@@ -643,6 +771,9 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
         for (int k = 0; k < LROOT_N * 2 / 16; k++) lr[k] = img[k];
 #pragma unroll
         for (int k = 0; k < DROOT_N * 2 / 16; k++) dr[k] = img[LROOT_N * 2 / 16 + k];
+        uint4 *dt4 = reinterpret_cast<uint4 *>(L.dtail[lane]);
+#pragma unroll
+        for (int k = 0; k < DTAIL_BYTES / 16; k++) dt4[k] = img[(LROOT_N + DROOT_N) * 2 / 16 + k];
         s.mode = LM_SYM;
         s.bit = ch.hdr_bit;
         s.zl = tabg;
@@ -661,7 +792,10 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
   __builtin_amdgcn_wave_barrier();
   const uint16_t *lt = L.lroot[lane];
   const uint16_t *dt = L.droot[lane];
-  uint32_t *tb = &L.tokbuf[0][lane];
+  uint32_t *tb = &L.g.tokbuf[0][lane];
+  uint32_t *rp = &L.g.ring[0][lane];
+  const uint32_t *dtl = L.dtail[lane];
+  KpPhase kph = {{0, 0, 0, 0, 0}};
 #if KP_ON
   kp_init = KP_NOW() - kp_t0;
 #endif
@@ -684,8 +818,10 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
     if (__ballot(s.mode == LM_SYM) == 0) break;
     s.gk = 0;
     if (s.mode == LM_SYM) {
-      for (int it = 0; it < GROUP; it++)
-        if (lane_step(s, lt, dt, tb)) break;
+      lane_fill_ring(s, rp);
+      // a step reads at most 2 more ring words
+      for (int it = 0; it < GROUP && s.rk + 2 < RING; it++)
+        if (lane_step(s, lt, dt, tb, dtl, rp, kph)) break;
     }
     __builtin_amdgcn_wave_barrier();
 #if KP_ON
@@ -697,7 +833,7 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
     const uint32_t g0 = s.ntok - s.gk;
 #pragma unroll
     for (uint32_t j = 0; j < GROUP; j++)
-      if (j < s.gk) s.tok[g0 + j] = L.tokbuf[j][lane];
+      if (j < s.gk) s.tok[g0 + j] = L.g.tokbuf[j][lane];
     __builtin_amdgcn_wave_barrier();  // tokbuf area is reused by the next header build
 #if KP_ON
     kp_flush += KP_NOW() - kc2;
@@ -722,6 +858,7 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
     KP_ADD(KP_P_SLOW_LIT, sl);
     KP_ADD(KP_P_SLOW_DIST, sd);
     KP_ADD(KP_P_REFILLS, rf);
+    for (int i = 0; i < 5; i++) KP_ADD(KP_S_REFILL1 + i, kph.t[i]);
   }
 #endif
   if (c < nchunks) {
@@ -1005,7 +1142,9 @@ __global__ void __launch_bounds__(64) zs_unit_header_kernel(const ZsJobDev *__re
   uint16_t *ctab = reinterpret_cast<uint16_t *>(tabg + TABLE_ENTRIES);
   uint16_t *img = reinterpret_cast<uint16_t *>(tabg + TABLE_ENTRIES + TABLE_ENTRIES / 2);
   uint32_t lbits = 9, dbits = 6;
-  if (wave_dyn_header(B, w, end_byte, bit, tabg, ctab, lbits, dbits, img, img + LROOT_N)) return;
+  if (wave_dyn_header(B, w, end_byte, bit, tabg, ctab, lbits, dbits, img, img + LROOT_N,
+                      reinterpret_cast<uint8_t *>(img + LROOT_N + DROOT_N)))
+    return;
   if (lane == 0) {
     units[c].hdr_bit = bit;
     units[c].hdr_info = 1u | (lbits << 8) | (dbits << 12);

@@ -5,7 +5,7 @@
 
 #define WAVE 64
 #define TABLE_ENTRIES 1448   // ENOUGH (852 + 594), src/inftrees.h:52-55
-#define TABLE_STRIDE (TABLE_ENTRIES + TABLE_ENTRIES / 2 + 160)  // + compact u16 copy + LDS-root image (256 + 64 u16)
+#define TABLE_STRIDE (TABLE_ENTRIES + TABLE_ENTRIES / 2 + 176)  // + compact u16 copy + LDS image (256 + 64 u16 roots, 64 B dist tail)
 #define FIXED_ZLIB_WORDS 544                              // fixed tables: 512 lit/len + 32 dist (zlib layout)
 #define FIXED_WORDS (FIXED_ZLIB_WORDS + FIXED_ZLIB_WORDS / 2)  // + compact u16 copy
 #define DIST_TABLE_OFF 852   // distance table follows the literal/length table

@@ -12,6 +12,10 @@ enum ZsKprof {
   // expand pass (zs_expand_kernel), per workgroup (wave 0)
   KP_E_BLOCKS = 16, KP_E_CYC_TOTAL, KP_E_ROUNDS, KP_E_JUMP_ITERS, KP_E_CYC_JUMP, KP_E_BATCHES, KP_E_CYC_MAX,
   KP_E_CYC_INIT, KP_E_JUMP_ROUNDS,
+  // parse step phases (s_memtime, wave-uniform): refill 1, literal/length
+  // lookup (+ slow path), length extra + refill 2, distance lookup (+ slow
+  // path), checks + token write
+  KP_S_REFILL1 = 40, KP_S_LIT, KP_S_REFILL2, KP_S_DIST, KP_S_TAIL,
   KP_COUNT = 64
 };
 
