@@ -149,7 +149,8 @@ __device__ bool validate_header(const uint32_t *w, uint32_t end_byte, uint32_t b
 // Block finder: one wave per search segment; records the first SEG_SLOTS
 // dynamic-block starts in [s_byte, e_byte).
 //   1. every lane tests 32 bit offsets per step with bit-parallel filters
-//      (BFINAL = 0, BTYPE = 2, HLIT <= 29, HDIST <= 29, complete code-length
+//      (BFINAL = 0 -- or 1 in a stream's last segments --, BTYPE = 2,
+//      HLIT <= 29, HDIST <= 29, complete code-length
 //      code) and appends the survivors, in offset order, to an LDS queue;
 //   2. the queue is drained 64 candidates at a time, ONE candidate per lane,
 //      through the full header validation, so the expensive check runs
@@ -196,8 +197,10 @@ __global__ void __launch_bounds__(64) zs_find_kernel(const ZsJobDev *__restrict_
         const uint32_t wi = b0 >> 5;
         const uint64_t lo64 = (uint64_t)in_word(w, wi, end_byte) | ((uint64_t)in_word(w, wi + 1, end_byte) << 32);
         const uint64_t hi64 = (uint64_t)in_word(w, wi + 2, end_byte) | ((uint64_t)in_word(w, wi + 3, end_byte) << 32);
-        // BFINAL = 0, BTYPE = 2 at offset p: bit p = 0, bit p+1 = 0, bit p+2 = 1
-        uint32_t cand = (uint32_t)(~lo64 & ~(lo64 >> 1) & (lo64 >> 2));
+        // BTYPE = 2 at offset p: bit p+1 = 0, bit p+2 = 1; BFINAL (bit p) = 0,
+        // or either value in the stream's last segments (its final block)
+        const uint64_t bt = ~(lo64 >> 1) & (lo64 >> 2);
+        uint32_t cand = (uint32_t)(seg.final_ok ? bt : (bt & ~lo64));
         if (b0 < lo) cand &= ~0u << (lo - b0);
         if (hi - b0 < 32u) cand &= (1u << (hi - b0)) - 1u;
         while (cand) {

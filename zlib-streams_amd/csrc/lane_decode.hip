@@ -775,6 +775,7 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
 #pragma unroll
         for (int k = 0; k < DTAIL_BYTES / 16; k++) dt4[k] = img[(LROOT_N + DROOT_N) * 2 / 16 + k];
         s.mode = LM_SYM;
+        s.last = (ch.hdr_info >> 1) & 1u;
         s.bit = ch.hdr_bit;
         s.zl = tabg;
         s.zd = tabg + DIST_TABLE_OFF;
@@ -1136,7 +1137,9 @@ __global__ void __launch_bounds__(64) zs_unit_header_kernel(const ZsJobDev *__re
   const uint32_t end_byte = mis + (uint32_t)jb.in_len;
   StageBits sb;
   stage_bits(B, w, end_byte, ch.start_bit, sb);
-  if (ch.start_bit + 3 > end_byte * 8u || sb.peek(ch.start_bit, 3) != 4u) return;  // BFINAL 0, BTYPE 2
+  if (ch.start_bit + 3 > end_byte * 8u) return;
+  const uint32_t hdr3 = sb.peek(ch.start_bit, 3);
+  if ((hdr3 >> 1) != 2u) return;  // BTYPE 2 (BFINAL either way)
   uint32_t bit = ch.start_bit + 3;
   uint32_t *tabg = tables + (size_t)c * TABLE_STRIDE;
   uint16_t *ctab = reinterpret_cast<uint16_t *>(tabg + TABLE_ENTRIES);
@@ -1147,7 +1150,7 @@ __global__ void __launch_bounds__(64) zs_unit_header_kernel(const ZsJobDev *__re
     return;
   if (lane == 0) {
     units[c].hdr_bit = bit;
-    units[c].hdr_info = 1u | (lbits << 8) | (dbits << 12);
+    units[c].hdr_info = 1u | ((hdr3 & 1u) << 1) | (lbits << 8) | (dbits << 12);
   }
 }
 

@@ -351,6 +351,7 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
         sg.ord = o;
         sg.s_byte = o * C;
         sg.e_byte = (uint32_t)std::min<uint64_t>((uint64_t)(o + 1) * C, jd.in_len);
+        sg.final_ok = o + 2 >= ns;  // the final block lies within the last segments
         g_ws.h_segs[si] = sg;
       }
       nunit_slots += max_units;

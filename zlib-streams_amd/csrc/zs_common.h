@@ -113,7 +113,8 @@ struct ZsSegDev {
   uint32_t e_byte;
   uint32_t ncand;      // block starts found (<= SEG_SLOTS), ascending
   uint32_t cand[SEG_SLOTS];  // bit offsets from the 4-byte-aligned input base
-  uint32_t pad[3];
+  uint32_t final_ok;   // 1: BFINAL = 1 starts count too (the stream's last segments)
+  uint32_t pad[2];
 };
 
 struct ZsChunkDev {    // one decode unit
@@ -136,7 +137,7 @@ struct ZsChunkDev {    // one decode unit
   uint64_t tok;        // offset of this unit's token region (u32 units)
   uint32_t hdr_bit;    // bit after the first block's header (when prebuilt)
   uint32_t hdr_info;   // bit 0: first header prebuilt by zs_unit_header_kernel;
-                       // bits 8-11 / 12-15: lit/len and distance root bits
+                       // bit 1: its BFINAL; bits 8-11 / 12-15: lit/len and distance root bits
 };
 
 // Parse-pass tokens (u32), consumed by the expand pass:
