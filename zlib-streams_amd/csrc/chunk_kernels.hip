@@ -398,23 +398,54 @@ __global__ void __launch_bounds__(64) zs_fixed_tables_kernel(uint32_t *__restric
 }
 
 // ---------------------------------------------------------------------------
-// Link: verify the chain, offsets, history windows (one workgroup per stream)
+// Link (one 1024-thread workgroup per stream):
+//   A. in parallel, every unit finds its successor: the first later unit whose
+//      start is its end bit (recorded starts that are not block boundaries
+//      are skipped; starts ascend, so the search stops early);
+//   B. thread 0 walks the successors (in LDS for up to LINK_MAXU units),
+//      assigning output offsets and writing the chain in order to `info`;
+//   C. the 32 KiB history windows are resolved in chain order from each
+//      unit's last HIST entries; the entries of the next chain member are
+//      loaded into registers while the current one resolves (one memory
+//      latency per step is hidden behind the LDS work).
 // ---------------------------------------------------------------------------
 #define LINK_THREADS 1024
 #define LINK_PER (HIST / LINK_THREADS)  // window entries per thread and chain step
+#define LINK_MAXU 4096                  // units per stream with the successor walk in LDS
+
+struct ZsLinkInfo {
+  uint64_t scratch;
+  uint32_t n_out;
+  uint32_t unit;  // unit index (ord 0 <=> first of the job)
+};
+
+__device__ __forceinline__ void link_load(const uint16_t *__restrict__ scratch, const ZsLinkInfo &li, uint32_t t,
+                                          uint16_t (&v)[LINK_PER]) {
+  const uint32_t n = li.n_out;
+  const uint32_t keep = n < HIST ? HIST - n : 0u;
+  const uint16_t *e = scratch + li.scratch;
+#pragma unroll
+  for (int k = 0; k < LINK_PER; k++) {
+    const uint32_t i = (uint32_t)k * LINK_THREADS + t;
+    v[k] = (i >= keep) ? e[n - HIST + i] : (uint16_t)0;
+  }
+}
+
 __global__ void __launch_bounds__(LINK_THREADS) zs_link_kernel(const ZsJobDev *__restrict__ jobs, const ZsHeadDev *__restrict__ heads,
                                                                ZsChunkDev *__restrict__ chunks, const ZsCJobDev *__restrict__ cjobs,
                                                                const uint16_t *__restrict__ scratch, uint8_t *__restrict__ windows,
-                                                               ZsDecDev *__restrict__ decs, uint32_t *__restrict__ fallback) {
+                                                               ZsLinkInfo *__restrict__ info, ZsDecDev *__restrict__ decs,
+                                                               uint32_t *__restrict__ fallback) {
   __shared__ uint8_t s_win[2][HIST];
-  __shared__ uint32_t s_ok, s_cur;
+  __shared__ uint16_t s_succ[LINK_MAXU];  // successor - unit (0: none / end)
+  __shared__ uint32_t s_ok, s_len;
   __shared__ uint32_t s_end_bit;
   __shared__ uint64_t s_total;
   const uint32_t t = threadIdx.x;
   const ZsCJobDev cj = cjobs[blockIdx.x];
   const ZsJobDev jb = jobs[cj.job];
   const ZsHeadDev hd = heads[cj.job];
-  if (hd.code != ZD_END) {
+  if (hd.code != ZD_END || cj.nunits == 0) {
     if (t == 0) {
       fallback[cj.job] = 0;
       ZsDecDev d;
@@ -426,30 +457,15 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_link_kernel(const ZsJobDev *_
     }
     return;
   }
-  if (t == 0) {
-    // walk the chain from unit 0: a unit's end must be the start of a later
-    // unit (starts ascend; recorded starts that are not block boundaries are
-    // skipped and never enter the chain)
-    const uint32_t last = cj.unit0 + cj.nunits;
-    uint32_t c = cj.unit0;
-    uint64_t total = 0;
-    uint32_t ok = 1, end_bit = 0;
-    for (;;) {
-      ZsChunkDev ch = chunks[c];
-      chunks[c].out_off = total;
-      total += ch.n_out;
-      const int code = ch.code & 0xff;
-      if (code == ZD_END) {
-        chunks[c].chain_next = ZS_NONE;
-        end_bit = ch.end_bit;
-        break;
-      }
-      if (code != ZD_STOP) {
-        ok = 0;
-        break;
-      }
-      uint32_t k = ZS_NONE;
-      for (uint32_t o = c + 1; o < last; o++) {
+  const uint32_t u0 = cj.unit0, nu = cj.nunits, last = u0 + nu;
+  const bool small = nu <= LINK_MAXU;
+  // A: successors
+  for (uint32_t i = u0 + t; i < last; i += LINK_THREADS) {
+    const ZsChunkDev ch = chunks[i];
+    const int code = ch.code & 0xff;
+    uint32_t k = ZS_NONE;
+    if (code == ZD_STOP) {
+      for (uint32_t o = i + 1; o < last; o++) {
         const uint32_t sb = chunks[o].start_bit;
         if (sb == ch.end_bit) {
           k = o;
@@ -457,50 +473,86 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_link_kernel(const ZsJobDev *_
         }
         if (sb > ch.end_bit) break;
       }
+    }
+    chunks[i].chain_next = k;
+    if (small) s_succ[i - u0] = (k == ZS_NONE || k - i > 0xffffu) ? (uint16_t)0 : (uint16_t)(k - i);
+  }
+  __syncthreads();
+  // B: walk the chain
+  if (t == 0) {
+    uint32_t c = u0, len = 0, ok = 1, end_bit = 0;
+    uint64_t total = 0;
+    for (;;) {
+      const ZsChunkDev ch = chunks[c];
+      const int code = ch.code & 0xff;
+      if (code != ZD_STOP && code != ZD_END) {
+        ok = 0;
+        break;
+      }
+      ZsLinkInfo li;
+      li.scratch = ch.scratch;
+      li.n_out = ch.n_out;
+      li.unit = c;
+      info[u0 + len] = li;
+      len++;
+      chunks[c].out_off = total;
+      chunks[c].in_chain = 1;
+      total += ch.n_out;
+      if (code == ZD_END) {
+        end_bit = ch.end_bit;
+        break;
+      }
+      uint32_t k;
+      if (small) {
+        const uint32_t d = s_succ[c - u0];
+        k = d ? c + d : ZS_NONE;
+      } else {
+        k = ch.chain_next;
+      }
       if (k == ZS_NONE) {
         ok = 0;
         break;
       }
-      chunks[c].chain_next = k;
       c = k;
     }
     if (total > jb.out_cap) ok = 0;
     s_ok = ok;
     s_total = total;
     s_end_bit = end_bit;
-    s_cur = cj.unit0;
+    s_len = len;
   }
   __syncthreads();
   if (!s_ok) {
     if (t == 0) fallback[cj.job] = 1;
     return;
   }
-  // history windows in chain order: W holds the last HIST bytes before chunk c
+  // C: history windows in chain order: W holds the last HIST bytes before unit c
+  const uint32_t len = s_len;
   uint32_t wv = 0;  // valid bytes of history
   int cur = 0;
-  uint32_t c = s_cur;
-  for (;;) {
-    const ZsChunkDev ch = chunks[c];
+  uint16_t v[LINK_PER], vn[LINK_PER];
+  ZsLinkInfo li = info[u0];
+  link_load(scratch, li, t, v);
+  ZsLinkInfo lin = len > 1 ? info[u0 + 1] : li;
+  bool bad = false;
+  for (uint32_t j = 0; j < len; j++) {
+    // next member's entries (and the one after's descriptor) in flight now
+    ZsLinkInfo li2 = lin;
+    if (j + 1 < len) {
+      link_load(scratch, lin, t, vn);
+      if (j + 2 < len) li2 = info[u0 + j + 2];
+    }
+    const uint32_t c = li.unit;
     uint8_t *W = s_win[cur];
     uint8_t *W2 = s_win[cur ^ 1];
-    if (ch.ord != 0) {
+    if (c != u0) {
       uint8_t *g = windows + (size_t)c * HIST;
       for (uint32_t i = t * 16; i < HIST; i += LINK_THREADS * 16)
         *reinterpret_cast<uint4 *>(g + i) = *reinterpret_cast<const uint4 *>(W + i);
     }
-    const uint32_t n = ch.n_out;
-    const uint16_t *e = scratch + ch.scratch;
+    const uint32_t n = li.n_out;
     const uint32_t keep = n < HIST ? HIST - n : 0u;  // old history bytes still inside the new window
     const uint32_t lowest = HIST - wv;                // first valid history index
-    // window index i = k * LINK_THREADS + t; all LINK_PER loads are issued
-    // before any is consumed (one memory latency per chain step)
-    uint16_t v[LINK_PER];
-#pragma unroll
-    for (int k = 0; k < LINK_PER; k++) {
-      const uint32_t i = (uint32_t)k * LINK_THREADS + t;
-      v[k] = (i >= keep) ? e[n - HIST + i] : (uint16_t)0;
-    }
-    bool bad = false;
 #pragma unroll
     for (int k = 0; k < LINK_PER; k++) {
       const uint32_t i = (uint32_t)k * LINK_THREADS + t;
@@ -516,14 +568,16 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_link_kernel(const ZsJobDev *_
       }
       W2[i] = (uint8_t)b;
     }
-    if (bad) s_ok = 0;
-    if (t == 0) chunks[c].in_chain = 1;
     wv = min(HIST, wv + n);
     cur ^= 1;
     __syncthreads();
-    if (ch.chain_next == ZS_NONE) break;
-    c = ch.chain_next;
+    li = lin;
+    lin = li2;
+#pragma unroll
+    for (int k = 0; k < LINK_PER; k++) v[k] = vn[k];
   }
+  if (bad) s_ok = 0;
+  __syncthreads();
   if (t == 0) {
     if (!s_ok) {
       fallback[cj.job] = 1;
@@ -561,27 +615,38 @@ __global__ void __launch_bounds__(EMIT_THREADS) zs_emit_kernel(const ZsJobDev *_
   uint8_t *out = jobs[ch.job].out + ch.out_off;
   const uint16_t *e = scratch + ch.scratch;
   const uint32_t n = ch.n_out;
-  // bytes [0, head) and the tail are written byte-wise so no 8-byte word is
-  // shared with a neighbouring chunk; the body uses aligned 8-byte stores
-  const uint32_t head = min(n, (uint32_t)((8u - (uint32_t)(reinterpret_cast<uintptr_t>(out) & 7u)) & 7u));
-  for (uint32_t i = t; i < head; i += EMIT_THREADS) {
-    uint32_t v = e[i];
-    out[i] = (uint8_t)(v < MARK_BASE ? v : s_w[v - MARK_BASE]);
-  }
-  const uint32_t body = (n - head) & ~7u;
-  for (uint32_t i = head + t * 8; i < head + body; i += EMIT_THREADS * 8) {
-    uint64_t word = 0;
+  // 16-byte output groups aligned in memory; group g covers unit bytes
+  // [16 g - mis, 16 g - mis + 16).  Groups straddling the unit's ends are
+  // written bytewise (neighbouring units own the other bytes).
+  const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(out) & 15u);
+  const uint32_t ngroups = (n + mis + 15u) / 16u;
+  for (uint32_t g = t; g < ngroups; g += EMIT_THREADS) {
+    const int32_t i0 = (int32_t)(g * 16u) - (int32_t)mis;  // unit byte of the group's first byte
+    uint32_t b[16];
+    if (i0 >= 0 && (uint32_t)i0 + 16u <= n) {
+      uint4 lo, hi;
+      __builtin_memcpy(&lo, e + i0, 16);
+      __builtin_memcpy(&hi, e + i0 + 8, 16);
+      const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
-      uint32_t v = e[i + k];
-      uint32_t b = v < MARK_BASE ? v : s_w[v - MARK_BASE];
-      word |= (uint64_t)b << (8 * k);
+      for (int k = 0; k < 16; k++) {
+        const uint32_t v = (w[k >> 1] >> (16 * (k & 1))) & 0xffffu;
+        b[k] = v < MARK_BASE ? v : s_w[v - MARK_BASE];
+      }
+      uint4 o;
+      o.x = b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
+      o.y = b[4] | (b[5] << 8) | (b[6] << 16) | (b[7] << 24);
+      o.z = b[8] | (b[9] << 8) | (b[10] << 16) | (b[11] << 24);
+      o.w = b[12] | (b[13] << 8) | (b[14] << 16) | (b[15] << 24);
+      *reinterpret_cast<uint4 *>(out + i0) = o;
+    } else {
+      for (int k = 0; k < 16; k++) {
+        const int32_t i = i0 + k;
+        if (i < 0 || (uint32_t)i >= n) continue;
+        const uint32_t v = e[i];
+        out[i] = (uint8_t)(v < MARK_BASE ? v : s_w[v - MARK_BASE]);
+      }
     }
-    *reinterpret_cast<uint64_t *>(out + i) = word;
-  }
-  for (uint32_t i = head + body + t; i < n; i += EMIT_THREADS) {
-    uint32_t v = e[i];
-    out[i] = (uint8_t)(v < MARK_BASE ? v : s_w[v - MARK_BASE]);
   }
 }
 
@@ -599,8 +664,8 @@ extern "C" void zs_launch_lane(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads,
 extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, ZsSegDev *d_segs, uint32_t nseg,
                                   ZsCJobDev *d_cjobs, uint32_t ncjobs, ZsChunkDev *d_units, uint32_t nunit_slots,
                                   uint16_t *d_scratch, uint32_t *d_tokens, uint32_t *d_tables, const uint32_t *d_fixed,
-                                  uint8_t *d_windows, ZsDecDev *d_decs, uint32_t *d_fallback, hipStream_t st,
-                                  hipEvent_t *ev) {
+                                  uint8_t *d_windows, void *d_linkinfo, ZsDecDev *d_decs, uint32_t *d_fallback,
+                                  hipStream_t st, hipEvent_t *ev) {
   // ev (profiling, optional): [0] before find, [1] after find + plan, [2] after
   // parse, [3] after expand, [4] after link, [5] after emit
   if (ev) (void)hipEventRecord(ev[0], st);
@@ -609,7 +674,7 @@ extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_hea
   if (ev) (void)hipEventRecord(ev[1], st);
   zs_launch_lane(d_jobs, d_heads, d_units, nunit_slots, d_scratch, d_tokens, d_tables, d_fixed, st, ev ? ev + 2 : nullptr);
   hipLaunchKernelGGL(zs_link_kernel, dim3(ncjobs), dim3(LINK_THREADS), 0, st, d_jobs, d_heads, d_units, d_cjobs,
-                     d_scratch, d_windows, d_decs, d_fallback);
+                     d_scratch, d_windows, reinterpret_cast<ZsLinkInfo *>(d_linkinfo), d_decs, d_fallback);
   if (ev) (void)hipEventRecord(ev[4], st);
   hipLaunchKernelGGL(zs_emit_kernel, dim3(nunit_slots), dim3(EMIT_THREADS), 0, st, d_jobs, d_units, d_scratch, d_windows,
                      d_fallback);

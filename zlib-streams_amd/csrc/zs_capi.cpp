@@ -33,8 +33,8 @@ extern "C" void zs_launch_fixed_compact(uint32_t *fixed, hipStream_t st);
 extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, ZsSegDev *d_segs, uint32_t nseg,
                                   ZsCJobDev *d_cjobs, uint32_t ncjobs, ZsChunkDev *d_units, uint32_t nunit_slots,
                                   uint16_t *d_scratch, uint32_t *d_tokens, uint32_t *d_tables, const uint32_t *d_fixed,
-                                  uint8_t *d_windows, ZsDecDev *d_decs, uint32_t *d_fallback, hipStream_t st,
-                                  hipEvent_t *ev);
+                                  uint8_t *d_windows, void *d_linkinfo, ZsDecDev *d_decs, uint32_t *d_fallback,
+                                  hipStream_t st, hipEvent_t *ev);
 
 namespace {
 
@@ -103,6 +103,7 @@ struct Workspace {
   ZsChunkDev *d_chunks = nullptr, *h_chunks = nullptr;  // unit slots
   uint32_t *d_tables = nullptr;  // TABLE_STRIDE words per unit slot
   uint8_t *d_windows = nullptr;  // 32 KiB per unit slot
+  uint64_t *d_linkinfo = nullptr;  // zs_link_kernel chain order: 16 B per unit slot
   size_t cap_scratch = 0;        // u16 entries (and u32 parse tokens, same count)
   uint16_t *d_scratch = nullptr;
   uint32_t *d_tokens = nullptr;
@@ -194,7 +195,8 @@ int ws_reserve_chunks(size_t nseg, size_t nunits, size_t scratch_entries) {
   if (nunits > g_ws.cap_units) {
     size_t c = std::max(nunits, g_ws.cap_units + g_ws.cap_units / 2);
     if ((r = grow_dev(&g_ws.d_chunks, c)) || (r = grow_host(&g_ws.h_chunks, c)) ||
-        (r = grow_dev(&g_ws.d_tables, c * TABLE_ENTRIES_HOST)) || (r = grow_dev(&g_ws.d_windows, c * 32768)))
+        (r = grow_dev(&g_ws.d_tables, c * TABLE_ENTRIES_HOST)) || (r = grow_dev(&g_ws.d_windows, c * 32768)) ||
+        (r = grow_dev(&g_ws.d_linkinfo, c * 2)))
       return r;
     g_ws.cap_units = c;
   }
@@ -369,7 +371,8 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
   if (n_cj)
     zs_launch_chunked(g_ws.d_jobs, g_ws.d_heads, g_ws.d_segs, (uint32_t)nseg, g_ws.d_cjobs, n_cj, g_ws.d_chunks,
                       (uint32_t)nunit_slots,
-                      g_ws.d_scratch, g_ws.d_tokens, g_ws.d_tables, g_ws.d_fixed, g_ws.d_windows, g_ws.d_decs,
+                      g_ws.d_scratch, g_ws.d_tokens, g_ws.d_tables, g_ws.d_fixed, g_ws.d_windows, g_ws.d_linkinfo,
+                      g_ws.d_decs,
                       g_ws.d_fallback, st, ev ? ev + 1 : nullptr);
   else if (ev)
     for (int i = 1; i <= 6; i++) HIP_OK(hipEventRecord(ev[i], st));
