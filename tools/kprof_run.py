@@ -15,7 +15,9 @@ NAMES = {0: "p_waves", 1: "p_cyc_total", 2: "p_cyc_coop", 3: "p_cyc_steps", 4: "
          11: "p_cyc_max", 12: "p_cyc_init", 13: "p_refills",
          16: "e_blocks", 17: "e_cyc_total", 18: "e_rounds", 19: "e_jump_iters", 20: "e_cyc_jump", 21: "e_batches",
          22: "e_cyc_max", 23: "e_cyc_init", 24: "e_jump_rounds",
-         40: "s_refill1", 41: "s_lit", 42: "s_refill2", 43: "s_dist", 44: "s_tail"}
+         40: "s_refill1", 41: "s_lit", 42: "s_refill2", 43: "s_dist", 44: "s_tail",
+         48: "l_streams", 49: "l_steps", 50: "l_cyc_succ", 51: "l_cyc_walk", 52: "l_cyc_winwrite", 53: "l_cyc_resolve",
+         54: "l_cyc_barrier", 55: "l_markers_sample", 56: "l_cyc_total", 57: "l_cyc_max"}
 
 
 def main():
@@ -55,6 +57,10 @@ def main():
         "expand_jump_rounds_frac": d["e_jump_rounds"] / max(d["e_rounds"], 1),
         "expand_jump_iters_per_jround": d["e_jump_iters"] / max(d["e_jump_rounds"], 1),
         "expand_frac_init": d["e_cyc_init"] / max(d["e_cyc_total"], 1),
+        "link_cycles_per_step": {k: d[k] / max(d["l_steps"], 1) for k in
+                                 ("l_cyc_succ", "l_cyc_walk", "l_cyc_winwrite", "l_cyc_resolve", "l_cyc_barrier",
+                                  "l_cyc_total")},
+        "link_marker_frac_sample": d["l_markers_sample"] / max(d["l_steps"] * 16 * 32, 1),
         "step_phase_cycles_per_wave_step": {k: d[k] / max(d["p_wave_steps"], 1)
                                             for k in ("s_refill1", "s_lit", "s_refill2", "s_dist", "s_tail")},
     }

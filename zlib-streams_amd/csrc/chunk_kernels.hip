@@ -23,6 +23,13 @@
 
 #include "zs_common.h"
 #include "zs_device.h"
+#include "zs_kprof.h"
+
+#if KP_ON
+__device__ unsigned long long g_kprof_ck[16];  // KP_L_* - 48
+#define KPC_ADD(i, v) atomicAdd(&g_kprof_ck[(i) - 48], (unsigned long long)(v))
+#define KPC_MAX(i, v) atomicMax(&g_kprof_ck[(i) - 48], (unsigned long long)(v))
+#endif
 
 #define MARK_BASE 256u
 #define HIST 32768u
@@ -419,15 +426,23 @@ struct ZsLinkInfo {
   uint32_t unit;  // unit index (ord 0 <=> first of the job)
 };
 
+// thread t owns window entries 4t + 4096 g + {0..3}, g < LINK_PER / 4; entry
+// pairs are packed in u32 (2 per word, 2 words per group)
+#define LINK_G (LINK_PER / 4)
 __device__ __forceinline__ void link_load(const uint16_t *__restrict__ scratch, const ZsLinkInfo &li, uint32_t t,
-                                          uint16_t (&v)[LINK_PER]) {
+                                          uint2 (&v)[LINK_G]) {
   const uint32_t n = li.n_out;
-  const uint32_t keep = n < HIST ? HIST - n : 0u;
   const uint16_t *e = scratch + li.scratch;
 #pragma unroll
-  for (int k = 0; k < LINK_PER; k++) {
-    const uint32_t i = (uint32_t)k * LINK_THREADS + t;
-    v[k] = (i >= keep) ? e[n - HIST + i] : (uint16_t)0;
+  for (int g = 0; g < LINK_G; g++) {
+    const uint32_t i = (uint32_t)g * (LINK_THREADS * 4) + t * 4;
+    if (n >= HIST) {
+      __builtin_memcpy(&v[g], e + (n - HIST) + i, 8);
+    } else {  // short unit: entry i exists only for i >= HIST - n
+      uint16_t x[4];
+      for (int k = 0; k < 4; k++) x[k] = (i + k >= HIST - n) ? e[i + k - (HIST - n)] : (uint16_t)0;
+      __builtin_memcpy(&v[g], x, 8);
+    }
   }
 }
 
@@ -459,6 +474,11 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_link_kernel(const ZsJobDev *_
   }
   const uint32_t u0 = cj.unit0, nu = cj.nunits, last = u0 + nu;
   const bool small = nu <= LINK_MAXU;
+#if KP_ON
+  const uint64_t kt0 = KP_NOW();
+  uint64_t kt_ww = 0, kt_res = 0, kt_bar = 0;
+  uint32_t kmark = 0;
+#endif
   // A: successors
   for (uint32_t i = u0 + t; i < last; i += LINK_THREADS) {
     const ZsChunkDev ch = chunks[i];
@@ -478,6 +498,9 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_link_kernel(const ZsJobDev *_
     if (small) s_succ[i - u0] = (k == ZS_NONE || k - i > 0xffffu) ? (uint16_t)0 : (uint16_t)(k - i);
   }
   __syncthreads();
+#if KP_ON
+  const uint64_t kt1 = KP_NOW();
+#endif
   // B: walk the chain
   if (t == 0) {
     uint32_t c = u0, len = 0, ok = 1, end_bit = 0;
@@ -522,6 +545,9 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_link_kernel(const ZsJobDev *_
     s_len = len;
   }
   __syncthreads();
+#if KP_ON
+  const uint64_t kt2 = KP_NOW();
+#endif
   if (!s_ok) {
     if (t == 0) fallback[cj.job] = 1;
     return;
@@ -530,7 +556,7 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_link_kernel(const ZsJobDev *_
   const uint32_t len = s_len;
   uint32_t wv = 0;  // valid bytes of history
   int cur = 0;
-  uint16_t v[LINK_PER], vn[LINK_PER];
+  uint2 v[LINK_G], vn[LINK_G];
   ZsLinkInfo li = info[u0];
   link_load(scratch, li, t, v);
   ZsLinkInfo lin = len > 1 ? info[u0 + 1] : li;
@@ -545,39 +571,91 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_link_kernel(const ZsJobDev *_
     const uint32_t c = li.unit;
     uint8_t *W = s_win[cur];
     uint8_t *W2 = s_win[cur ^ 1];
+#if KP_ON
+    const uint64_t ka = KP_NOW();
+#endif
     if (c != u0) {
       uint8_t *g = windows + (size_t)c * HIST;
       for (uint32_t i = t * 16; i < HIST; i += LINK_THREADS * 16)
         *reinterpret_cast<uint4 *>(g + i) = *reinterpret_cast<const uint4 *>(W + i);
     }
+#if KP_ON
+    const uint64_t kb = KP_NOW();
+    kt_ww += kb - ka;
+#endif
     const uint32_t n = li.n_out;
     const uint32_t keep = n < HIST ? HIST - n : 0u;  // old history bytes still inside the new window
     const uint32_t lowest = HIST - wv;                // first valid history index
+    if (keep == 0 && lowest == 0) {
+      // common case (full window, unit >= 32 KiB): branch-free gather, every
+      // entry reads the window and selects literal or history byte
 #pragma unroll
-    for (int k = 0; k < LINK_PER; k++) {
-      const uint32_t i = (uint32_t)k * LINK_THREADS + t;
-      uint32_t b;
-      if (i < keep) {
-        b = W[i + n];
-      } else if (v[k] < MARK_BASE) {
-        b = v[k];
-      } else {
-        const uint32_t wx = v[k] - MARK_BASE;
-        bad |= wx < lowest;  // reaches before the stream start
-        b = W[wx & (HIST - 1)];
+      for (int g = 0; g < LINK_G; g++) {
+        const uint32_t i = (uint32_t)g * (LINK_THREADS * 4) + t * 4;
+        const uint32_t x0 = v[g].x & 0xffffu, x1 = v[g].x >> 16, x2 = v[g].y & 0xffffu, x3 = v[g].y >> 16;
+        const uint32_t r0 = W[(x0 - MARK_BASE) & (HIST - 1)], r1 = W[(x1 - MARK_BASE) & (HIST - 1)];
+        const uint32_t r2 = W[(x2 - MARK_BASE) & (HIST - 1)], r3 = W[(x3 - MARK_BASE) & (HIST - 1)];
+        const uint32_t b0 = x0 < MARK_BASE ? x0 : r0, b1 = x1 < MARK_BASE ? x1 : r1;
+        const uint32_t b2 = x2 < MARK_BASE ? x2 : r2, b3 = x3 < MARK_BASE ? x3 : r3;
+        *reinterpret_cast<uint32_t *>(W2 + i) = b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
+#if KP_ON
+        kmark += (x0 >= MARK_BASE) + (x1 >= MARK_BASE) + (x2 >= MARK_BASE) + (x3 >= MARK_BASE);
+#endif
       }
-      W2[i] = (uint8_t)b;
+    } else {
+#pragma unroll
+      for (int g = 0; g < LINK_G; g++) {
+        const uint32_t xs[4] = {v[g].x & 0xffffu, v[g].x >> 16, v[g].y & 0xffffu, v[g].y >> 16};
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const uint32_t i = (uint32_t)g * (LINK_THREADS * 4) + t * 4 + k;
+          const uint32_t x = xs[k];
+          uint32_t b;
+          if (i < keep) {
+            b = W[i + n];
+          } else if (x < MARK_BASE) {
+            b = x;
+          } else {
+            const uint32_t wx = x - MARK_BASE;
+            bad |= wx < lowest;  // reaches before the stream start
+            b = W[wx & (HIST - 1)];
+          }
+          W2[i] = (uint8_t)b;
+        }
+      }
     }
     wv = min(HIST, wv + n);
     cur ^= 1;
+#if KP_ON
+    const uint64_t kc = KP_NOW();
+    kt_res += kc - kb;
+#endif
     __syncthreads();
+#if KP_ON
+    kt_bar += KP_NOW() - kc;
+#endif
     li = lin;
     lin = li2;
 #pragma unroll
-    for (int k = 0; k < LINK_PER; k++) v[k] = vn[k];
+    for (int g = 0; g < LINK_G; g++) v[g] = vn[g];
   }
   if (bad) s_ok = 0;
   __syncthreads();
+#if KP_ON
+  if ((t & 63) == 0) KPC_ADD(KP_L_MARKERS, kmark);  // lane 0 of each wave: a sample
+  if (t == 0) {
+    const uint64_t tot = KP_NOW() - kt0;
+    KPC_ADD(KP_L_STREAMS, 1);
+    KPC_ADD(KP_L_STEPS, len);
+    KPC_ADD(KP_L_CYC_SUCC, kt1 - kt0);
+    KPC_ADD(KP_L_CYC_WALK, kt2 - kt1);
+    KPC_ADD(KP_L_CYC_WINWRITE, kt_ww);
+    KPC_ADD(KP_L_CYC_RESOLVE, kt_res);
+    KPC_ADD(KP_L_CYC_BARRIER, kt_bar);
+    KPC_ADD(KP_L_CYC_TOTAL, tot);
+    KPC_MAX(KP_L_CYC_MAX, tot);
+  }
+#endif
   if (t == 0) {
     if (!s_ok) {
       fallback[cj.job] = 1;
@@ -679,4 +757,20 @@ extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_hea
   hipLaunchKernelGGL(zs_emit_kernel, dim3(nunit_slots), dim3(EMIT_THREADS), 0, st, d_jobs, d_units, d_scratch, d_windows,
                      d_fallback);
   if (ev) (void)hipEventRecord(ev[5], st);
+}
+
+// link counters of the profiling build (merged into zs_kprof_read's 48..63)
+extern "C" int zs_kprof_read_ck(uint64_t *out16, int reset) {
+#if KP_ON
+  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_kprof_ck), 16 * sizeof(uint64_t)) != hipSuccess) return -1;
+  if (reset) {
+    static const unsigned long long z[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_kprof_ck), z, sizeof z) != hipSuccess) return -1;
+  }
+  return 16;
+#else
+  (void)out16;
+  (void)reset;
+  return 0;
+#endif
 }

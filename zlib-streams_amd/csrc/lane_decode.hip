@@ -1176,12 +1176,18 @@ extern "C" void zs_launch_lane(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads,
   if (ev) (void)hipEventRecord(ev[1], st);
 }
 
+extern "C" int zs_kprof_read_ck(uint64_t *out16, int reset);
 // Counter readback (profiling builds only; product builds report 0 counters).
 extern "C" int zs_kprof_read(uint64_t *out, uint32_t n, int reset) {
 #if KP_ON
   const uint32_t k = n < KP_COUNT ? n : KP_COUNT;
   if (hipDeviceSynchronize() != hipSuccess) return -1;
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_kprof), k * sizeof(uint64_t)) != hipSuccess) return -1;
+  if (k >= 64) {
+    uint64_t ck[16];
+    if (zs_kprof_read_ck(ck, reset) == 16)
+      for (int i = 0; i < 16; i++) out[48 + i] = ck[i];
+  }
   if (reset) {
     static const unsigned long long z[KP_COUNT] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_kprof), z, sizeof z) != hipSuccess) return -1;

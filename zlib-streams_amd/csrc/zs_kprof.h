@@ -16,6 +16,9 @@ enum ZsKprof {
   // lookup (+ slow path), length extra + refill 2, distance lookup (+ slow
   // path), checks + token write
   KP_S_REFILL1 = 40, KP_S_LIT, KP_S_REFILL2, KP_S_DIST, KP_S_TAIL,
+  // link (chunk_kernels.hip; its own counter array, copied into 48..63)
+  KP_L_STREAMS = 48, KP_L_STEPS, KP_L_CYC_SUCC, KP_L_CYC_WALK, KP_L_CYC_WINWRITE, KP_L_CYC_RESOLVE,
+  KP_L_CYC_BARRIER, KP_L_MARKERS, KP_L_CYC_TOTAL, KP_L_CYC_MAX,
   KP_COUNT = 64
 };
 
