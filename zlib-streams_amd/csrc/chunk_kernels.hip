@@ -163,7 +163,7 @@ __device__ bool validate_header(const uint32_t *w, uint32_t end_byte, uint32_t b
 //      through the full header validation, so the expensive check runs
 //      SIMD-parallel instead of stalling the wave lane by lane.
 // ---------------------------------------------------------------------------
-#define FQ 1024  // candidate queue (ring) per wave
+#define FQ 512  // validation queue (ring) per wave
 
 __device__ __forceinline__ uint32_t find_scan_excl(uint32_t v, uint32_t *total) {
   uint32_t x = v;
@@ -177,10 +177,32 @@ __device__ __forceinline__ uint32_t find_scan_excl(uint32_t v, uint32_t *total) 
   return x - v;
 }
 
+// code-length-code completeness (Kraft sum == 2^7) of the candidate header at
+// bit p (p - base < 2048): HCLEN at p+13, 3-bit lengths from p+17; the bits
+// come from the step's LDS stage st (words of the input from bit base)
+__device__ __forceinline__ bool cl_complete(const uint32_t *st, uint32_t base, uint32_t p) {
+  const uint32_t r = p - base, wi = r >> 5, sh = r & 31u;
+  const uint64_t a = (uint64_t)st[wi] | ((uint64_t)st[wi + 1] << 32);
+  const uint64_t b = (uint64_t)st[wi + 2] | ((uint64_t)st[wi + 3] << 32);
+  const uint64_t h = sh ? ((a >> sh) | (b << (64 - sh))) : a;  // bits p .. p+63 (74 needed: 17 + 57)
+  const uint64_t h2 = sh ? ((b >> sh) | ((uint64_t)st[wi + 4] << (64 - sh))) : b;  // p+64 ..
+  const uint32_t ncode = (uint32_t)((h >> 13) & 15) + 4;
+  const uint64_t clb = (h >> 17) | (h2 << 47);  // lengths: 57 bits from p+17
+  uint32_t kraft = 0;
+#pragma unroll
+  for (int i = 0; i < 19; i++) {
+    const uint32_t L = (uint32_t)(clb >> (3 * i)) & 7u;
+    if ((uint32_t)i < ncode && L) kraft += 128u >> L;
+  }
+  return kraft == 128u;
+}
+
 __global__ void __launch_bounds__(64) zs_find_kernel(const ZsJobDev *__restrict__ jobs, const ZsHeadDev *__restrict__ heads,
                                                       ZsSegDev *__restrict__ segs) {
   __shared__ uint8_t s_lut[WAVE][128];
-  __shared__ uint32_t s_q[FQ];
+  __shared__ uint32_t s_st[WAVE + 8];  // this step's input words (2048 bits + overlap)
+  __shared__ uint32_t s_q[WAVE * 12]; // this step's candidates passing the bit-parallel filters
+  __shared__ uint32_t s_v[FQ];        // ... and the code-length-code completeness check
   const uint32_t lane = threadIdx.x;
   const uint32_t sg = blockIdx.x;
   const ZsSegDev seg = segs[sg];
@@ -195,52 +217,68 @@ __global__ void __launch_bounds__(64) zs_find_kernel(const ZsJobDev *__restrict_
     // strictly after the stream's first block (that start is unit 0)
     const uint32_t lo = max((mis + seg.s_byte) * 8u, (mis + (uint32_t)hd.start_byte) * 8u + 1u);
     const uint32_t hi = (mis + seg.e_byte) * 8u;
-    uint32_t qh = 0, qt = 0;
+    uint32_t vh = 0, vt = 0;
+    // input words of a step: lane word (base/32 + lane), the next one, and 8
+    // overlap words (lanes < 8); the next step's are loaded one step ahead
+    auto fetch = [&](uint32_t bs, uint32_t &a0, uint32_t &a1, uint32_t &a2) {
+      const uint32_t wi = (bs >> 5) + lane;
+      a0 = in_word(w, wi, end_byte);
+      a1 = in_word(w, wi + 1, end_byte);
+      a2 = lane < 8 ? in_word(w, (bs >> 5) + WAVE + lane, end_byte) : 0u;
+    };
+    uint32_t nx0, nx1, nx2;
+    fetch(lo & ~31u, nx0, nx1, nx2);
     for (uint32_t base = lo & ~31u;; base += WAVE * 32u) {
       const bool more = base < hi;
       const uint32_t b0 = base + lane * 32u;
-      uint32_t surv = 0;
+      const uint32_t x0 = nx0, x1 = nx1, x2 = nx2;
+      if (more) fetch(base + WAVE * 32u, nx0, nx1, nx2);
+      s_st[lane] = x0;
+      if (lane < 8) s_st[WAVE + lane] = x2;
+      uint32_t cand = 0;
       if (more && b0 < hi) {
-        const uint32_t wi = b0 >> 5;
-        const uint64_t lo64 = (uint64_t)in_word(w, wi, end_byte) | ((uint64_t)in_word(w, wi + 1, end_byte) << 32);
-        const uint64_t hi64 = (uint64_t)in_word(w, wi + 2, end_byte) | ((uint64_t)in_word(w, wi + 3, end_byte) << 32);
-        // BTYPE = 2 at offset p: bit p+1 = 0, bit p+2 = 1; BFINAL (bit p) = 0,
-        // or either value in the stream's last segments (its final block)
-        const uint64_t bt = ~(lo64 >> 1) & (lo64 >> 2);
-        uint32_t cand = (uint32_t)(seg.final_ok ? bt : (bt & ~lo64));
+        const uint64_t x = (uint64_t)x0 | ((uint64_t)x1 << 32);
+        // bit-parallel over the lane's 32 offsets p: BTYPE = 2 (bit p+1 = 0,
+        // bit p+2 = 1), BFINAL (bit p) = 0 unless this is one of the stream's
+        // last segments, HLIT <= 29 (not bits p+4..p+7 all set), HDIST <= 29
+        // (not bits p+9..p+12 all set)
+        const uint64_t bt = ~(x >> 1) & (x >> 2);
+        const uint64_t hlit_bad = (x >> 4) & (x >> 5) & (x >> 6) & (x >> 7);
+        const uint64_t hdist_bad = (x >> 9) & (x >> 10) & (x >> 11) & (x >> 12);
+        cand = (uint32_t)((seg.final_ok ? bt : (bt & ~x)) & ~hlit_bad & ~hdist_bad);
         if (b0 < lo) cand &= ~0u << (lo - b0);
         if (hi - b0 < 32u) cand &= (1u << (hi - b0)) - 1u;
-        while (cand) {
-          const uint32_t p = __builtin_ctz(cand);
-          cand &= cand - 1u;
-          const uint64_t h = lo64 >> (p + 3);
-          if ((h & 31) > 29 || ((h >> 5) & 31) > 29) continue;
-          const uint32_t ncode = (uint32_t)((h >> 10) & 15) + 4;
-          const uint32_t sh = p + 17;  // 17..48
-          const uint64_t clb = (lo64 >> sh) | (hi64 << (64 - sh));
-          uint32_t kraft = 0;
-#pragma unroll
-          for (int i = 0; i < 19; i++) {
-            const uint32_t L = (uint32_t)(clb >> (3 * i)) & 7u;
-            if ((uint32_t)i < ncode && L) kraft += 128u >> L;
-          }
-          if (kraft == 128u) surv |= 1u << p;
-        }
       }
       uint32_t tot;
-      const uint32_t at = find_scan_excl((uint32_t)__builtin_popcount(surv), &tot);
-      for (uint32_t k = 0; surv; k++) {
-        s_q[(qt + at + k) & (FQ - 1)] = b0 + (uint32_t)__builtin_ctz(surv);
-        surv &= surv - 1u;
+      const uint32_t at = find_scan_excl((uint32_t)__builtin_popcount(cand), &tot);
+      for (uint32_t k = 0; cand; k++) {
+        s_q[at + k] = b0 + (uint32_t)__builtin_ctz(cand);
+        cand &= cand - 1u;
       }
-      qt += tot;
       __builtin_amdgcn_wave_barrier();
-      while (qt - qh >= WAVE || (!more && qt != qh)) {
-        const uint32_t take = min(qt - qh, (uint32_t)WAVE);
+      // completeness check on this step's candidates, one per lane; survivors
+      // keep their order in the validation queue
+      for (uint32_t q0 = 0; q0 < tot; q0 += WAVE) {
+        const uint32_t take = min(tot - q0, (uint32_t)WAVE);
         uint32_t cb = 0;
         bool ok = false;
         if (lane < take) {
-          cb = s_q[(qh + lane) & (FQ - 1)];
+          cb = s_q[q0 + lane];
+          ok = cl_complete(s_st, base, cb);
+        }
+        uint32_t vtot;
+        const uint32_t vat = find_scan_excl(ok ? 1u : 0u, &vtot);
+        if (ok) s_v[(vt + vat) & (FQ - 1)] = cb;
+        vt += vtot;
+      }
+      __builtin_amdgcn_wave_barrier();
+      // full header validation, one candidate per lane
+      while (vt - vh >= WAVE || (!more && vt != vh)) {
+        const uint32_t take = min(vt - vh, (uint32_t)WAVE);
+        uint32_t cb = 0;
+        bool ok = false;
+        if (lane < take) {
+          cb = s_v[(vh + lane) & (FQ - 1)];
           ok = validate_header(w, end_byte, cb, s_lut[lane]);
         }
         uint64_t m = __ballot(ok);
@@ -251,7 +289,7 @@ __global__ void __launch_bounds__(64) zs_find_kernel(const ZsJobDev *__restrict_
           if (lane == 0) segs[sg].cand[nfound] = f;
           nfound++;
         }
-        qh += take;
+        vh += take;
         if (nfound == SEG_SLOTS) break;
       }
       if (!more || nfound == SEG_SLOTS) break;
