@@ -52,6 +52,14 @@ int inflate_process(uintptr_t h, uintptr_t in_ptr, unsigned in_len, uintptr_t ou
 int inflate_end(uintptr_t h);
 unsigned inflate_last_consumed(uintptr_t h);
 
+uintptr_t deflate_new(void);
+int deflate_init(uintptr_t h, int level);       /* src/wasm/deflate_stream_wasm.c:22-29 (level < 0 -> default) */
+int deflate_init_raw(uintptr_t h, int level);   /* :31-39 */
+int deflate_init_gzip(uintptr_t h, int level);  /* :41-49; deflate_process :51-55, _end :57-65, _last_consumed :67-69 */
+int deflate_process(uintptr_t h, uintptr_t in_ptr, unsigned in_len, uintptr_t out_ptr, unsigned out_len, int flush);
+int deflate_end(uintptr_t h);
+unsigned deflate_last_consumed(uintptr_t h);
+
 uintptr_t inflate9_new(void);
 int inflate9_init(uintptr_t h);
 int inflate9_init_raw(uintptr_t h);
@@ -84,6 +92,28 @@ typedef struct zs_result {
 #define ZS_ENODEV (-100)
 
 int zs_inflate_batch(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t flags);
+
+/* ---- GPU deflate ---- */
+typedef struct zs_djob {
+  const void *in;      /* bytes to compress (host, or device with ZS_F_DEVICE) */
+  uint64_t in_len;     /* < 2^32 */
+  void *out;           /* compressed output (host, or device with ZS_F_DEVICE) */
+  uint64_t out_cap;    /* zs_deflate_bound(in_len, window_bits) always suffices */
+  int32_t window_bits; /* as deflateInit2: -9..-15 raw, 9..15 zlib, 25..31 gzip */
+  int32_t level;       /* 0 stored, 1..9, or -1 (Z_DEFAULT_COMPRESSION = 6) */
+} zs_djob;
+/* Each job = deflateInit2(level, Z_DEFLATED, window_bits, 8, Z_DEFAULT_STRATEGY)
+   + one deflate(Z_FINISH) over the whole input: ret Z_STREAM_END (Z_OK when
+   out_cap was too small: total_out = out_cap bytes of the stream), total_in,
+   total_out, adler (CRC-32 for gzip, Adler-32 for zlib, 1 for raw).  The
+   stream is valid deflate that any inflater decodes to the input; its bytes
+   are not zlib's. */
+int zs_deflate_batch(const zs_djob *jobs, uint32_t n, zs_result *results, uint32_t flags);
+uint64_t zs_deflate_bound(uint64_t in_len, int32_t window_bits);
+/* accumulated deflate timing (zs_profile(1) enables): [0] whole pipeline ms,
+   [1] match, [2] parse, [3] blocks + checks, [4] offsets + stitch + trailer,
+   [5] batches.  Returns the number of entries written. */
+int zs_profile_deflate(double *ms, uint32_t n);
 /* launch on this HIP stream (hipStream_t); NULL = the library's own stream */
 int zs_set_stream(void *hip_stream);
 int zs_synchronize(void);

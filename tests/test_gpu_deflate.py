@@ -1,0 +1,201 @@
+"""GPU deflate (LZ77 match-find + Huffman emission)
+through the C-ABI.
+
+Bar: every GPU stream is valid deflate that the
+CPU oracle (and, independently, host zlib 1.2.11) inflates to the input, with
+Z_STREAM_END, the whole stream consumed and the wrapper check value matching.
+The wrapper bytes (zlib CMF/FLG, gzip header) are pinned against host zlib's
+deflate, which is byte-identical to the reference's.  The
+compressed body is not zlib's bytes (no sequential hash chains): its size is
+reported against zlib at the same level, and bounded.
+"""
+import ctypes
+import random
+import zlib
+
+import numpy as np
+import pytest
+
+import corpus
+import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def zs():
+    import zstreams
+    zstreams.lib()
+    return zstreams
+
+
+def expected_check(data, wbits):
+    if wbits > 15:
+        return zlib.crc32(data)
+    if wbits > 0:
+        return zlib.adler32(data)
+    return 1  # raw: strm->adler keeps adler32(0) (deflateResetKeep)
+
+
+def check_stream(data, wbits, level, comp, info):
+    assert info["ret"] == 1, info
+    assert info["total_in"] == len(data) and info["total_out"] == len(comp), info
+    assert info["adler"] == expected_check(data, wbits), info
+    # zlib turns deflate windowBits 8 into 9 and writes CINFO 1, which an
+    # inflateInit2(8) rejects ("invalid window size"): inflate those with 9
+    iw = 9 if wbits == 8 else wbits
+    out, oi = O.oneshot(comp, iw, max(len(data), 1) + 1024)
+    assert oi["ret"] == 1 and oi["total_in"] == len(comp) and out == data, (len(data), wbits, level, oi)
+    assert zlib.decompress(comp, iw) == data
+    # wrapper header as host zlib writes it for the same parameters
+    if wbits > 0:
+        c = zlib.compressobj(level, zlib.DEFLATED, wbits)
+        ref = c.compress(b"") + c.flush(zlib.Z_SYNC_FLUSH)
+        hl = 10 if wbits > 15 else 2
+        assert comp[:hl] == ref[:hl], (comp[:hl], ref[:hl])
+
+
+def _patterns(rng):
+    text = corpus.stream(1, 300000)
+    lines = corpus.stream(33, 300000)
+    rnd = bytes(rng.getrandbits(8) for _ in range(70000))
+    return {
+        "text": text, "lines": lines, "random": rnd, "zeros": bytes(200000),
+        "abc": b"abc" * 70000, "mixed": text[:50000] + rnd[:30000] + bytes(40000) + lines[:50000],
+    }
+
+
+SIZES = [0, 1, 2, 3, 4, 5, 17, 258, 259, 4095, 32768, 65535, 65536, 65537, 131079, 200000]
+
+
+def test_deflate_small_all_wrappers_levels(zs):
+    rng = random.Random(3)
+    pats = _patterns(rng)
+    cases = []
+    for name, p in pats.items():
+        for n in SIZES:
+            if n > len(p):
+                continue
+            for wb in (-15, 15, 31):
+                for lv in (0, 1, 6, 9):
+                    cases.append((p[:n], wb, lv))
+    rng.shuffle(cases)
+    got = zs.deflate_batch([c[0] for c in cases], [c[1] for c in cases], [c[2] for c in cases])
+    for (data, wb, lv), (comp, info) in zip(cases, got):
+        check_stream(data, wb, lv, comp, info)
+
+
+def test_deflate_window_bits_and_levels(zs):
+    data = corpus.stream(5, 150000)
+    cases = [(data, wb, lv) for wb in (-9, -12, 9, 8, 13, 25, 28) for lv in (-1, 2, 3, 4, 5, 7, 8)]
+    got = zs.deflate_batch([c[0] for c in cases], [c[1] for c in cases], [c[2] for c in cases])
+    for (d, wb, lv), (comp, info) in zip(cases, got):
+        check_stream(d, wb, 6 if lv == -1 else lv, comp, info)
+
+
+def test_deflate_invalid_parameters(zs):
+    data = b"hello hello hello"
+    bad = [(-8, 6), (24, 6), (7, 6), (16, 6), (32, 6), (-16, 6), (15, 10), (15, -2)]
+    got = zs.deflate_batch([data] * len(bad), [b[0] for b in bad], [b[1] for b in bad], [64] * len(bad))
+    for b, (comp, info) in zip(bad, got):
+        assert info["ret"] == -2 and comp == b"", (b, info)
+
+
+def test_deflate_small_out_cap(zs):
+    data = corpus.stream(7, 100000)
+    full, _ = zs.deflate_batch([data], 31, 6)[0]
+    part, info = zs.deflate_batch([data], 31, 6, [1000])[0]
+    assert info["ret"] == 0 and info["total_out"] == 1000 and part == full[:1000]
+
+
+def test_deflate_large_corpus_ratio_and_gpu_roundtrip(zs):
+    """C3 shape at reduced size: gzip L6 GPU compress -> oracle + GPU inflate."""
+    raws, _ = corpus.batch(0, 4, 8 << 20, compress=False)
+    raws += corpus.batch(32, 2, 8 << 20, compress=False)[0]
+    datas = [r.tobytes() for r in raws]
+    got = zs.deflate_batch(datas, 31, 6)
+    comps = [g[0] for g in got]
+    for d, (comp, info) in zip(datas, got):
+        assert info["ret"] == 1 and info["adler"] == zlib.crc32(d)
+        out, oi = O.oneshot(comp, 31, len(d) + 1024)
+        assert oi["ret"] == 1 and out == d
+        zl = len(zlib.compress(d, 6))
+        # quality bar: within 25% of zlib L6 on these corpora
+        assert len(comp) <= 1.25 * zl, (len(comp), zl)
+    back = zs.inflate_batch(comps, 31, [len(d) for d in datas])
+    for d, (out, info) in zip(datas, back):
+        assert info["ret"] == 1 and info["adler"] == zlib.crc32(d) and out == d
+
+
+def test_deflate_deterministic(zs):
+    data = corpus.stream(9, 1 << 20)
+    a = zs.deflate_batch([data] * 3, -15, 6)
+    assert a[0][0] == a[1][0] == a[2][0]
+
+
+def test_compression_stream_js_schedule(zs):
+    """CompressionStreamZlib (handle ABI, JS write schedule) == batch output,
+    and the stream round-trips through DecompressionStreamZlib."""
+    data = corpus.stream(40, 300000)
+    for fmt, wb in (("deflate-raw", -15), ("deflate", 15), ("gzip", 31)):
+        for level in (-1, 1, 9):
+            ref, _ = zs.deflate_batch([data], wb, level)[0]
+            for w in (4096, 65536):
+                got = zs.compress(data, fmt, level, w)
+                assert got == ref, (fmt, level, w)
+            assert zs.decompress(ref, fmt, 4096) == data
+    # empty input: flush alone gives a complete stream
+    assert zlib.decompress(zs.compress(b"", "gzip"), 31) == b""
+    # the reference's round-trip test shape: 24 000 random bytes, 4096-B writes
+    rnd = bytes(random.Random(1).getrandbits(8) for _ in range(24000))
+    assert zs.decompress(zs.compress(rnd, "deflate", -1, 4096), "deflate", 4096) == rnd
+
+
+def test_zlib_abi_deflate_loop(zs):
+    """deflateInit2_ / deflate / deflateEnd / deflateBound over the library's
+    zlib ABI with a small output buffer (Z_FINISH, served in pieces)."""
+    import libz_ref
+    Z = libz_ref.ZStream
+    L = ctypes.CDLL(zs.LIB_PATH)
+    L.deflateInit2_.argtypes = [ctypes.POINTER(Z), ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+    L.deflate.argtypes = [ctypes.POINTER(Z), ctypes.c_int]
+    L.deflateEnd.argtypes = [ctypes.POINTER(Z)]
+    L.deflateBound.argtypes = [ctypes.POINTER(Z), ctypes.c_ulong]
+    L.deflateBound.restype = ctypes.c_ulong
+    sz = ctypes.sizeof(Z)
+    s = Z()
+    assert L.deflateInit2_(ctypes.byref(s), 6, 8, 15, 8, 0, b"2.0", sz) == -6  # Z_VERSION_ERROR
+    for bad in ((6, 9, 15, 8, 0), (6, 8, -8, 8, 0), (6, 8, 15, 0, 0), (6, 8, 15, 8, 5), (10, 8, 15, 8, 0)):
+        assert L.deflateInit2_(ctypes.byref(s), *bad, b"1.2.11", sz) == -2, bad
+    data = corpus.stream(12, 500000)
+    for wb in (-15, 15, 31):
+        ref, _ = zs.deflate_batch([data], wb, 6)[0]
+        s = Z()
+        assert L.deflateInit2_(ctypes.byref(s), 6, 8, wb, 8, 0, b"1.2.11", sz) == 0
+        assert L.deflateBound(ctypes.byref(s), len(data)) >= len(ref)
+        ib = ctypes.create_string_buffer(data, len(data))
+        ob = ctypes.create_string_buffer(7000)
+        s.next_in = ctypes.cast(ib, ctypes.c_void_p)
+        s.avail_in = len(data)
+        out = bytearray()
+        ret = 0
+        while ret == 0:
+            s.next_out = ctypes.cast(ob, ctypes.c_void_p)
+            s.avail_out = len(ob)
+            ret = L.deflate(ctypes.byref(s), 4)
+            out += ob.raw[:len(ob) - s.avail_out]
+        assert ret == 1 and bytes(out) == ref
+        assert s.total_in == len(data) and s.total_out == len(ref) and s.adler == expected_check(data, wb)
+        assert L.deflateEnd(ctypes.byref(s)) == 0
+
+
+def test_deflate_device_pointers(zs):
+    import torch
+    data = corpus.stream(20, 3 << 20)
+    ref, _ = zs.deflate_batch([data], -15, 6)[0]
+    src = torch.from_numpy(np.frombuffer(data, dtype=np.uint8).copy()).cuda()
+    cap = zs.deflate_bound(len(data), -15)
+    dst = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+    info = zs.deflate_batch_device([src.data_ptr()], [len(data)], [dst.data_ptr()], [cap], -15, 6)[0]
+    assert info["ret"] == 1 and dst[:info["total_out"]].cpu().numpy().tobytes() == ref

@@ -30,6 +30,8 @@ extern "C" void zs_launch_finish(const ZsJobDev *d_jobs, const ZsHeadDev *d_head
                                  uint32_t *d_checks, ZsResultDev *d_res, uint32_t njobs, hipStream_t stream);
 extern "C" void zs_launch_fixed_tables(uint32_t *fixed, hipStream_t st);
 extern "C" void zs_launch_fixed_compact(uint32_t *fixed, hipStream_t st);
+extern "C" void zs_launch_deflate(ZsDJobDev *d_jobs, uint32_t njobs, ZsDSegDev *d_segs, uint32_t nseg, uint32_t *d_tokens,
+                                  uint32_t *d_obuf, uint8_t *d_stage, hipStream_t st, hipEvent_t *ev);
 extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, ZsSegDev *d_segs, uint32_t nseg,
                                   ZsCJobDev *d_cjobs, uint32_t ncjobs, ZsChunkDev *d_units, uint32_t nunit_slots,
                                   uint16_t *d_scratch, uint32_t *d_tokens, uint32_t *d_tables, const uint32_t *d_fixed,
@@ -574,6 +576,271 @@ unsigned handle_last_consumed(uintptr_t hp) {
   return h ? h->last_consumed : 0;
 }
 
+
+// ---------------------------------------------------------------------------
+// GPU deflate (deflate_kernels.hip): batch of whole streams
+// ---------------------------------------------------------------------------
+constexpr uint64_t DZ_SEG_HOST = 65536;   // must match DZ_SEG
+constexpr uint64_t DZ_OUTW_HOST = 18440;  // must match DZ_OUTW
+
+struct DzWorkspace {
+  size_t cap_jobs = 0, cap_segs = 0, cap_tok = 0, cap_obuf = 0, cap_stage = 0, cap_in = 0;
+  ZsDJobDev *d_jobs = nullptr, *h_jobs = nullptr;
+  ZsDSegDev *d_segs = nullptr, *h_segs = nullptr;
+  uint32_t *d_tok = nullptr, *d_obuf = nullptr;
+  uint8_t *d_stage = nullptr, *d_in = nullptr;
+  hipEvent_t ev[5] = {};
+  double stage_ms[4] = {};
+  double ms = 0.0;
+  uint64_t launches = 0;
+};
+DzWorkspace g_dz;
+
+// deflateInit2 windowBits as zlib 1.2.11 deflate.c checks them: 9..15 zlib,
+// -9..-15 raw, 25..31 gzip; 8 only with the zlib wrapper, where it becomes 9
+bool parse_dz_wbits(int wb, int *wrap, uint32_t *w) {
+  int x = wb;
+  if (x < 0) {
+    *wrap = 0;
+    x = -x;
+  } else if (x > 15) {
+    *wrap = 2;
+    x -= 16;
+  } else {
+    *wrap = 1;
+  }
+  if (x < 8 || x > 15 || (x == 8 && *wrap != 1)) return false;
+  *w = x == 8 ? 9u : (uint32_t)x;
+  return true;
+}
+
+uint64_t dz_bound(uint64_t in_len, int wrap) {
+  const uint64_t nseg = std::max<uint64_t>(1, (in_len + DZ_SEG_HOST - 1) / DZ_SEG_HOST);
+  return in_len + in_len / 8 + nseg * 16 + 64 + (wrap == 2 ? 18 : 6);
+}
+
+template <typename T>
+int dz_grow(T **p, size_t *cap, size_t need) {
+  if (need <= *cap) return 0;
+  const size_t c = std::max(need, *cap + *cap / 4);
+  int r = grow_dev(p, c);
+  if (r) return r;
+  *cap = c;
+  return 0;
+}
+
+int deflate_batch_locked(const zs_djob *jobs, uint32_t n, zs_result *results, uint32_t flags) {
+  int r = ws_init();
+  if (r) {
+    for (uint32_t i = 0; i < n; i++) fill_result(&results[i], Z_STREAM_ERROR, nullptr);
+    return r;
+  }
+  const bool dev = (flags & ZS_F_DEVICE) != 0;
+  if (n > g_dz.cap_jobs) {
+    const size_t c = std::max<size_t>(n, 2 * g_dz.cap_jobs);
+    if ((r = grow_dev(&g_dz.d_jobs, c)) || (r = grow_host(&g_dz.h_jobs, c))) return r;
+    g_dz.cap_jobs = c;
+  }
+  std::vector<uint32_t> slot(n, UINT32_MAX);
+  std::vector<size_t> in_off(n, 0);
+  size_t nseg = 0, stage_total = 0, in_total = 0;
+  uint32_t nv = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    int wrap = 0;
+    uint32_t w = 15;
+    int level = jobs[i].level == Z_DEFAULT_COMPRESSION ? 6 : jobs[i].level;
+    const bool ok = parse_dz_wbits(jobs[i].window_bits, &wrap, &w) && level >= 0 && level <= 9 &&
+                    jobs[i].in_len < (1ull << 32) && (jobs[i].in || jobs[i].in_len == 0) &&
+                    (jobs[i].out || jobs[i].out_cap == 0);
+    if (!ok) {
+      fill_result(&results[i], Z_STREAM_ERROR, nullptr);
+      continue;
+    }
+    ZsDJobDev jd{};
+    jd.in_len = jobs[i].in_len;
+    jd.wrap = wrap;
+    jd.level = level;
+    jd.wbits = w;
+    jd.seg0 = (uint32_t)nseg;
+    jd.nseg = (uint32_t)std::max<uint64_t>(1, (jd.in_len + DZ_SEG_HOST - 1) / DZ_SEG_HOST);
+    jd.stage = stage_total;
+    stage_total += (dz_bound(jd.in_len, wrap) + 4095) & ~size_t(4095);
+    nseg += jd.nseg;
+    if (dev) {
+      jd.in = static_cast<const uint8_t *>(jobs[i].in);
+    } else {
+      in_off[i] = in_total;
+      in_total += (jobs[i].in_len + 15) & ~size_t(15);
+    }
+    slot[i] = nv;
+    g_dz.h_jobs[nv++] = jd;
+  }
+  if (nv == 0) return 0;
+  hipStream_t st = g_ws.stream;
+  if (nseg > g_dz.cap_segs) {
+    const size_t c = std::max(nseg, g_dz.cap_segs + g_dz.cap_segs / 2);
+    if ((r = grow_dev(&g_dz.d_segs, c)) || (r = grow_host(&g_dz.h_segs, c))) return r;
+    g_dz.cap_segs = c;
+  }
+  if ((r = dz_grow(&g_dz.d_tok, &g_dz.cap_tok, nseg * DZ_SEG_HOST)) ||
+      (r = dz_grow(&g_dz.d_obuf, &g_dz.cap_obuf, nseg * DZ_OUTW_HOST)) ||
+      (r = dz_grow(&g_dz.d_stage, &g_dz.cap_stage, stage_total)))
+    return r;
+  if (!dev) {
+    if ((r = dz_grow(&g_dz.d_in, &g_dz.cap_in, in_total + 64))) return r;
+    for (uint32_t i = 0; i < n; i++) {
+      if (slot[i] == UINT32_MAX) continue;
+      g_dz.h_jobs[slot[i]].in = g_dz.d_in + in_off[i];
+      if (jobs[i].in_len)
+        HIP_OK(hipMemcpyAsync(g_dz.d_in + in_off[i], jobs[i].in, jobs[i].in_len, hipMemcpyHostToDevice, st));
+    }
+  }
+  size_t si = 0;
+  for (uint32_t k = 0; k < nv; k++) {
+    const ZsDJobDev &jd = g_dz.h_jobs[k];
+    for (uint32_t o = 0; o < jd.nseg; o++, si++) {
+      ZsDSegDev sg{};
+      sg.job = k;
+      sg.last = o + 1 == jd.nseg;
+      sg.start = (uint64_t)o * DZ_SEG_HOST;
+      sg.len = (uint32_t)std::min<uint64_t>(DZ_SEG_HOST, jd.in_len - std::min<uint64_t>(jd.in_len, sg.start));
+      sg.tok = (uint64_t)si * DZ_SEG_HOST;
+      sg.obuf = (uint64_t)si * DZ_OUTW_HOST * 4;
+      g_dz.h_segs[si] = sg;
+    }
+  }
+  HIP_OK(hipMemsetAsync(g_dz.d_stage, 0, stage_total, st));
+  HIP_OK(hipMemcpyAsync(g_dz.d_jobs, g_dz.h_jobs, nv * sizeof(ZsDJobDev), hipMemcpyHostToDevice, st));
+  HIP_OK(hipMemcpyAsync(g_dz.d_segs, g_dz.h_segs, nseg * sizeof(ZsDSegDev), hipMemcpyHostToDevice, st));
+  hipEvent_t *ev = nullptr;
+  if (g_ws.prof) {
+    if (!g_dz.ev[0])
+      for (int i = 0; i < 5; i++) HIP_OK(hipEventCreate(&g_dz.ev[i]));
+    ev = g_dz.ev;
+  }
+  zs_launch_deflate(g_dz.d_jobs, nv, g_dz.d_segs, (uint32_t)nseg, g_dz.d_tok, g_dz.d_obuf, g_dz.d_stage, st, ev);
+  {
+    hipError_t le = hipGetLastError();
+    if (le != hipSuccess) {
+      set_err(std::string("kernel launch failed: ") + hipGetErrorString(le));
+      return ZS_ENODEV;
+    }
+  }
+  HIP_OK(hipMemcpyAsync(g_dz.h_jobs, g_dz.d_jobs, nv * sizeof(ZsDJobDev), hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  if (ev) {
+    float t = 0.f;
+    HIP_OK(hipEventElapsedTime(&t, ev[0], ev[4]));
+    g_dz.ms += t;
+    for (int i = 0; i < 4; i++) {
+      HIP_OK(hipEventElapsedTime(&t, ev[i], ev[i + 1]));
+      g_dz.stage_ms[i] += t;
+    }
+    g_dz.launches++;
+  }
+  for (uint32_t i = 0; i < n; i++) {
+    if (slot[i] == UINT32_MAX) continue;
+    const ZsDJobDev &jd = g_dz.h_jobs[slot[i]];
+    const uint64_t tot = jd.total_out;
+    const uint64_t give = std::min<uint64_t>(tot, jobs[i].out_cap);
+    if (give)
+      HIP_OK(hipMemcpyAsync(jobs[i].out, g_dz.d_stage + jd.stage, give,
+                            dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, st));
+    zs_result &res = results[i];
+    std::memset(&res, 0, sizeof res);
+    res.ret = give == tot ? Z_STREAM_END : Z_OK;  // Z_OK: output space ran out (deflate(Z_FINISH) semantics)
+    res.total_in = jd.in_len;
+    res.total_out = give;
+    res.adler = jd.wrap ? jd.check : 1u;  // deflateResetKeep: adler32(0) for raw/zlib, crc32(0) for gzip
+    res.msg = nullptr;
+  }
+  HIP_OK(hipStreamSynchronize(st));
+  return 0;
+}
+
+// stream surface for deflate: accept all input, compress at Z_FINISH, serve
+struct DStreamState {
+  int inited = 0;
+  int wbits = 15, level = 6;
+  std::vector<uint8_t> acc;
+  std::vector<uint8_t> out;
+  bool done = false;
+  size_t served = 0;
+  uint32_t adler = 1;
+};
+
+int dstream_call(DStreamState *s, const uint8_t *in, unsigned in_len, uint8_t *out, unsigned out_len, int flush,
+                 unsigned *consumed, unsigned *produced) {
+  *consumed = 0;
+  *produced = 0;
+  if (!s->done) {
+    s->acc.insert(s->acc.end(), in, in + in_len);
+    *consumed = in_len;
+    if (flush != Z_FINISH) return in_len ? Z_OK : Z_BUF_ERROR;
+    int wrap = 0;
+    uint32_t w = 15;
+    parse_dz_wbits(s->wbits, &wrap, &w);
+    s->out.resize(dz_bound(s->acc.size(), wrap));
+    zs_djob j{};
+    j.in = s->acc.data();
+    j.in_len = s->acc.size();
+    j.out = s->out.data();
+    j.out_cap = s->out.size();
+    j.window_bits = s->wbits;
+    j.level = s->level;
+    zs_result res;
+    if (deflate_batch_locked(&j, 1, &res, 0) || res.ret != Z_STREAM_END) return Z_STREAM_ERROR;
+    s->out.resize(res.total_out);
+    s->adler = res.adler;
+    s->done = true;
+  }
+  const size_t rem = s->out.size() - s->served;
+  const size_t k = std::min<size_t>(rem, out_len);
+  if (k) std::memcpy(out, s->out.data() + s->served, k);
+  s->served += k;
+  *produced = (unsigned)k;
+  if (s->served < s->out.size()) return Z_OK;
+  return Z_STREAM_END;
+}
+
+struct DHandle {
+  z_stream strm;  // layout parity with the reference context (unused fields)
+  DStreamState st;
+  unsigned last_consumed = 0;
+};
+
+uintptr_t dhandle_new() {
+  DHandle *h = new (std::nothrow) DHandle();
+  if (!h) return 0;
+  std::memset(&h->strm, 0, sizeof h->strm);
+  return reinterpret_cast<uintptr_t>(h);
+}
+// src/wasm/deflate_stream_wasm.c:22-49: level < 0 -> Z_DEFAULT_COMPRESSION
+int dhandle_init(uintptr_t hp, int level, int wbits) {
+  DHandle *h = reinterpret_cast<DHandle *>(hp);
+  if (!h) return Z_STREAM_ERROR;
+  int wrap;
+  uint32_t w;
+  if (level < 0) level = 6;
+  if (level > 9 || !parse_dz_wbits(wbits, &wrap, &w)) return Z_STREAM_ERROR;
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (ws_init()) return Z_STREAM_ERROR;
+  h->st = DStreamState();
+  h->st.inited = 1;
+  h->st.level = level;
+  h->st.wbits = wbits;
+  return Z_OK;
+}
+int dhandle_process(uintptr_t hp, uintptr_t in_ptr, unsigned in_len, uintptr_t out_ptr, unsigned out_len, int flush) {
+  DHandle *h = reinterpret_cast<DHandle *>(hp);
+  if (!h || !h->st.inited) return (int)((unsigned)(Z_STREAM_ERROR & 0xff) << 24);
+  std::lock_guard<std::mutex> lk(g_mu);
+  unsigned cons = 0, prod = 0;
+  const int ret = dstream_call(&h->st, reinterpret_cast<const uint8_t *>(in_ptr), in_len,
+                               reinterpret_cast<uint8_t *>(out_ptr), out_len, flush, &cons, &prod);
+  h->last_consumed = cons;
+  return (int)((prod & 0x00ffffffu) | ((unsigned)(ret & 0xff) << 24));
+}
 }  // namespace
 
 // ===========================================================================
@@ -609,6 +876,9 @@ int zs_profile(int enable) {
   g_ws.prof_ms = 0.0;
   g_ws.prof_batch_ms = 0.0;
   g_ws.prof_launches = 0;
+  g_dz.ms = 0.0;
+  for (double &x : g_dz.stage_ms) x = 0.0;
+  g_dz.launches = 0;
   return 0;
 }
 int zs_profile_read(double *decode_ms, double *batch_ms, uint64_t *launches) {
@@ -716,4 +986,101 @@ int ZEXPORT inflateEnd(z_streamp strm) {
   return Z_OK;
 }
 
+
+// ---- deflate: batch, reference stream ABI, zlib ABI ----
+int zs_deflate_batch(const zs_djob *jobs, uint32_t n, zs_result *results, uint32_t flags) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  return deflate_batch_locked(jobs, n, results, flags);
+}
+uint64_t zs_deflate_bound(uint64_t in_len, int32_t window_bits) {
+  int wrap = 0;
+  uint32_t w = 15;
+  if (!parse_dz_wbits(window_bits, &wrap, &w)) wrap = 2;
+  return dz_bound(in_len, wrap);
+}
+int zs_profile_deflate(double *ms, uint32_t n) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (n > 0) ms[0] = g_dz.ms;
+  for (uint32_t i = 1; i < n && i < 5; i++) ms[i] = g_dz.stage_ms[i - 1];
+  if (n > 5) ms[5] = (double)g_dz.launches;
+  return (int)std::min<uint32_t>(n, 6);
+}
+
+uintptr_t deflate_new(void) { return dhandle_new(); }
+int deflate_init(uintptr_t h, int level) { return dhandle_init(h, level, 15); }
+int deflate_init_raw(uintptr_t h, int level) { return dhandle_init(h, level, -15); }
+int deflate_init_gzip(uintptr_t h, int level) { return dhandle_init(h, level, 15 + 16); }
+int deflate_process(uintptr_t h, uintptr_t in_ptr, unsigned in_len, uintptr_t out_ptr, unsigned out_len, int flush) {
+  return dhandle_process(h, in_ptr, in_len, out_ptr, out_len, flush);
+}
+int deflate_end(uintptr_t h) {
+  DHandle *d = reinterpret_cast<DHandle *>(h);
+  if (!d) return Z_STREAM_ERROR;
+  delete d;
+  return Z_OK;
+}
+unsigned deflate_last_consumed(uintptr_t h) {
+  DHandle *d = reinterpret_cast<DHandle *>(h);
+  return d ? d->last_consumed : 0;
+}
+
+// zlib deflate ABI (deflate.c deflateInit2_ / deflate / deflateEnd / deflateBound)
+int ZEXPORT deflateInit2_(z_streamp strm, int level, int method, int windowBits, int memLevel, int strategy,
+                          const char *version, int stream_size) {
+  if (version == Z_NULL || version[0] != '1' || stream_size != (int)sizeof(z_stream)) return Z_VERSION_ERROR;
+  if (strm == Z_NULL) return Z_STREAM_ERROR;
+  strm->msg = Z_NULL;
+  int wrap;
+  uint32_t w;
+  if (level == Z_DEFAULT_COMPRESSION) level = 6;
+  if (method != Z_DEFLATED || memLevel < 1 || memLevel > 9 || level < 0 || level > 9 || strategy < 0 ||
+      strategy > Z_FIXED || !parse_dz_wbits(windowBits, &wrap, &w))
+    return Z_STREAM_ERROR;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (ws_init()) return Z_STREAM_ERROR;
+  }
+  DStreamState *s = new (std::nothrow) DStreamState();
+  if (!s) return Z_MEM_ERROR;
+  s->inited = 1;
+  s->level = level;
+  s->wbits = windowBits;
+  strm->state = reinterpret_cast<struct internal_state *>(s);
+  strm->total_in = strm->total_out = 0;
+  strm->adler = wrap == 2 ? 0u : 1u;
+  return Z_OK;
+}
+int ZEXPORT deflateInit_(z_streamp strm, int level, const char *version, int stream_size) {
+  return deflateInit2_(strm, level, Z_DEFLATED, 15, 8, Z_DEFAULT_STRATEGY, version, stream_size);
+}
+int ZEXPORT deflate(z_streamp strm, int flush) {
+  if (strm == Z_NULL || strm->state == Z_NULL || strm->next_out == Z_NULL ||
+      (strm->next_in == Z_NULL && strm->avail_in != 0) || flush < 0 || flush > Z_BLOCK)
+    return Z_STREAM_ERROR;
+  if (strm->avail_out == 0) return Z_BUF_ERROR;
+  DStreamState *s = reinterpret_cast<DStreamState *>(strm->state);
+  std::lock_guard<std::mutex> lk(g_mu);
+  unsigned cons = 0, prod = 0;
+  const int ret = dstream_call(s, strm->next_in, strm->avail_in, strm->next_out, strm->avail_out, flush, &cons, &prod);
+  strm->next_in += cons;
+  strm->avail_in -= cons;
+  strm->total_in += cons;
+  strm->next_out += prod;
+  strm->avail_out -= prod;
+  strm->total_out += prod;
+  if (s->done) strm->adler = s->adler;
+  return ret;
+}
+int ZEXPORT deflateEnd(z_streamp strm) {
+  if (strm == Z_NULL || strm->state == Z_NULL) return Z_STREAM_ERROR;
+  delete reinterpret_cast<DStreamState *>(strm->state);
+  strm->state = Z_NULL;
+  return Z_OK;
+}
+uLong ZEXPORT deflateBound(z_streamp strm, uLong sourceLen) {
+  int wrap = 1;
+  uint32_t w = 15;
+  if (strm && strm->state) parse_dz_wbits(reinterpret_cast<DStreamState *>(strm->state)->wbits, &wrap, &w);
+  return (uLong)dz_bound(sourceLen, wrap);
+}
 }  // extern "C"

@@ -155,6 +155,38 @@ struct ZsCJobDev {     // a job on the chunked path
   uint64_t scratch_n;  // scratch entries reserved
 };
 
+// ---------------------------------------------------------------------------
+// GPU deflate (deflate_kernels.hip): one job = one whole stream compressed as
+// with deflateInit2(level, Z_DEFLATED, window_bits) + deflate(Z_FINISH).
+// ---------------------------------------------------------------------------
+struct ZsDJobDev {
+  const uint8_t *in;
+  uint64_t in_len;
+  int32_t wrap;        // 0 raw, 1 zlib, 2 gzip
+  int32_t level;       // 0 stored, 1..9
+  uint32_t seg0;       // first segment
+  uint32_t nseg;       // segments (>= 1)
+  uint64_t stage;      // byte offset of the job's 4 KiB-aligned staging area
+  uint64_t total_out;  // compressed bytes (zs_dz_offsets_kernel)
+  uint32_t check;      // CRC-32 (gzip) / Adler-32 (zlib) of the input
+  uint32_t wbits;      // window bits 9..15 (match distances <= 2^wbits; zlib CINFO = wbits - 8)
+};
+
+struct ZsDSegDev {
+  uint32_t job;
+  uint32_t last;       // 1: the job's last segment (BFINAL)
+  uint64_t start;      // input byte offset
+  uint32_t len;        // input bytes (<= 64 KiB)
+  uint32_t ntok;       // tokens (parse)
+  uint64_t tok;        // offset of the segment's match/token region (u32 units)
+  uint64_t obuf;       // byte offset of the segment's block buffer
+  uint64_t bitoff;     // bit offset of the block in the job's stream
+  uint32_t nbits;      // block bits
+  uint32_t ck_a;       // CRC-32 of the segment, or Adler sum a
+  uint32_t ck_b;       // Adler weighted sum b (to the segment end)
+  uint32_t pad;
+};
+
 // Final per-job result (device -> host), zlib z_stream fields after the call.
 struct ZsResultDev {
   int32_t ret;

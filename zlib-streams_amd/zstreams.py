@@ -7,9 +7,14 @@ Reference interface mirrored here:
     slices, 64 KiB output buffer, stop a write when a call consumes 0 bytes,
     ``Z_FINISH`` drain in ``flush()``; a negative code raises (transform 89-95,
     flush 125-130).
-  * the handle ABI of src/wasm/*_stream_wasm.c (``inflate_new`` ...).
+  * ``CompressionStreamZlib`` (zlib-streams.js:159-163, same ``_make`` with
+    isCompress): formats "deflate", "deflate-raw", "gzip"; ``options.level``
+    (default -1); process codes are not checked while compressing (:89, :123).
+  * the handle ABI of src/wasm/*_stream_wasm.c (``inflate_new``,
+    ``deflate_new`` ...).
 
-Plus the batch entry ``inflate_batch`` (many whole streams per GPU launch).
+Plus the batch entries ``inflate_batch`` / ``deflate_batch`` (many whole
+streams per GPU launch).
 
 There is no CPU path: if the shared library or a HIP device is missing, every
 call raises ``ZStreamsError``.
@@ -29,6 +34,8 @@ ZS_F_DEVICE = 1
 # windowBits per format, as the reference's init functions choose them
 # (src/wasm/inflate_stream_wasm.c:22-45, inflate9_stream_wasm.c:15-20)
 FORMAT_WBITS = {"deflate": 15, "deflate-raw": -15, "gzip": 31, "deflate64-raw": -16}
+# deflateInit2 windowBits per compression format (src/wasm/deflate_stream_wasm.c:22-49)
+DEFLATE_FORMAT_WBITS = {"deflate": 15, "deflate-raw": -15, "gzip": 31}
 
 # exported symbols and their ctypes signatures (include/zstreams_mi355x.h)
 _U = ctypes.c_size_t  # uintptr_t
@@ -41,6 +48,12 @@ _SIGS = {
     "inflate9_init_raw": (ctypes.c_int, [_U]),
     "inflate9_process": (ctypes.c_int, [_U, _U, ctypes.c_uint, _U, ctypes.c_uint, ctypes.c_int]),
     "inflate9_end": (ctypes.c_int, [_U]), "inflate9_last_consumed": (ctypes.c_uint, [_U]),
+    "deflate_new": (_U, []), "deflate_init": (ctypes.c_int, [_U, ctypes.c_int]),
+    "deflate_init_raw": (ctypes.c_int, [_U, ctypes.c_int]), "deflate_init_gzip": (ctypes.c_int, [_U, ctypes.c_int]),
+    "deflate_process": (ctypes.c_int, [_U, _U, ctypes.c_uint, _U, ctypes.c_uint, ctypes.c_int]),
+    "deflate_end": (ctypes.c_int, [_U]), "deflate_last_consumed": (ctypes.c_uint, [_U]),
+    "zs_deflate_bound": (ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_int32]),
+    "zs_profile_deflate": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.c_uint32]),
     "zs_set_stream": (ctypes.c_int, [ctypes.c_void_p]),
     "zs_profile": (ctypes.c_int, [ctypes.c_int]),
     "zs_profile_read": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
@@ -60,6 +73,11 @@ class ZStreamsError(RuntimeError):
 class ZsJob(ctypes.Structure):
     _fields_ = [("in_", ctypes.c_void_p), ("in_len", ctypes.c_uint64), ("out", ctypes.c_void_p),
                 ("out_cap", ctypes.c_uint64), ("window_bits", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+class ZsDJob(ctypes.Structure):
+    _fields_ = [("in_", ctypes.c_void_p), ("in_len", ctypes.c_uint64), ("out", ctypes.c_void_p),
+                ("out_cap", ctypes.c_uint64), ("window_bits", ctypes.c_int32), ("level", ctypes.c_int32)]
 
 
 class ZsResult(ctypes.Structure):
@@ -88,6 +106,8 @@ def lib():
             fn.argtypes = args
         L.zs_inflate_batch.restype = ctypes.c_int
         L.zs_inflate_batch.argtypes = [ctypes.POINTER(ZsJob), ctypes.c_uint32, ctypes.POINTER(ZsResult), ctypes.c_uint32]
+        L.zs_deflate_batch.restype = ctypes.c_int
+        L.zs_deflate_batch.argtypes = [ctypes.POINTER(ZsDJob), ctypes.c_uint32, ctypes.POINTER(ZsResult), ctypes.c_uint32]
         _lib = L
     return _lib
 
@@ -137,6 +157,71 @@ def inflate_batch_device(in_ptrs, in_lens, out_ptrs, out_caps, window_bits):
         jobs[i].window_bits = window_bits[i] if isinstance(window_bits, (list, tuple)) else window_bits
     _check(lib().zs_inflate_batch(jobs, n, res, ZS_F_DEVICE))
     return [res[i].as_dict() for i in range(n)]
+
+
+def deflate_bound(n, window_bits=-15):
+    """Output capacity that always holds one GPU-deflated stream of n bytes."""
+    return int(lib().zs_deflate_bound(n, window_bits))
+
+
+def deflate_batch(streams, window_bits=-15, level=-1, out_caps=None):
+    """Deflate many whole buffers on the GPU (host buffers).
+
+    Each job behaves like deflateInit2(level, Z_DEFLATED, window_bits, 8,
+    Z_DEFAULT_STRATEGY) + one deflate(Z_FINISH).  Returns [(bytes, result_dict)].
+    """
+    n = len(streams)
+    wbs = window_bits if isinstance(window_bits, (list, tuple)) else [window_bits] * n
+    lvs = level if isinstance(level, (list, tuple)) else [level] * n
+    if out_caps is None:
+        out_caps = [deflate_bound(len(s), wbs[i]) if -15 <= wbs[i] <= 31 else 64 for i, s in enumerate(streams)]
+    jobs = (ZsDJob * max(n, 1))()
+    res = (ZsResult * max(n, 1))()
+    inbufs, outbufs = [], []
+    for i, s in enumerate(streams):
+        ib = ctypes.create_string_buffer(bytes(s), max(len(s), 1))
+        ob = ctypes.create_string_buffer(max(out_caps[i], 1))
+        inbufs.append(ib)
+        outbufs.append(ob)
+        jobs[i].in_ = ctypes.cast(ib, ctypes.c_void_p).value if len(s) else None
+        jobs[i].in_len = len(s)
+        jobs[i].out = ctypes.cast(ob, ctypes.c_void_p).value
+        jobs[i].out_cap = out_caps[i]
+        jobs[i].window_bits = wbs[i]
+        jobs[i].level = lvs[i]
+    _check(lib().zs_deflate_batch(jobs, n, res, 0))
+    return [(outbufs[i].raw[:res[i].total_out], res[i].as_dict()) for i in range(n)]
+
+
+def deflate_batch_device(in_ptrs, in_lens, out_ptrs, out_caps, window_bits, level=-1):
+    """Deflate buffers already resident in HBM (device pointers)."""
+    n = len(in_ptrs)
+    jobs = (ZsDJob * n)()
+    res = (ZsResult * n)()
+    for i in range(n):
+        jobs[i].in_ = in_ptrs[i]
+        jobs[i].in_len = in_lens[i]
+        jobs[i].out = out_ptrs[i]
+        jobs[i].out_cap = out_caps[i]
+        jobs[i].window_bits = window_bits[i] if isinstance(window_bits, (list, tuple)) else window_bits
+        jobs[i].level = level[i] if isinstance(level, (list, tuple)) else level
+    _check(lib().zs_deflate_batch(jobs, n, res, ZS_F_DEVICE))
+    return [res[i].as_dict() for i in range(n)]
+
+
+DEFLATE_STAGES = ("match", "parse", "blocks", "stitch")
+DEFLATE_STAGE_KERNELS = {"match": "zs_dz_match_kernel", "parse": "zs_dz_parse_kernel",
+                         "blocks": "zs_dz_block_kernel + zs_dz_check_kernel",
+                         "stitch": "zs_dz_offsets_kernel + zs_dz_stitch_kernel + zs_dz_trailer_kernel"}
+
+
+def profile_deflate():
+    """Accumulated deflate timing since profile(True): (pipeline ms, {stage: ms}, batches)."""
+    a = (ctypes.c_double * 6)()
+    k = lib().zs_profile_deflate(a, 6)
+    if k < 0:
+        _check(k)
+    return a[0], {DEFLATE_STAGES[i]: a[1 + i] for i in range(4)}, int(a[5])
 
 
 def profile(enable):
@@ -193,22 +278,23 @@ def set_stream(hip_stream_handle):
 
 
 class _Handle:
-    """The reference's handle ABI for one decompression stream."""
+    """The reference's handle ABI for one (de)compression stream."""
 
-    def __init__(self, fmt):
-        if fmt not in FORMAT_WBITS:
+    def __init__(self, fmt, compress=False, level=-1):
+        if fmt not in (DEFLATE_FORMAT_WBITS if compress else FORMAT_WBITS):
             raise ValueError(f"unsupported format {fmt!r}")
         L = lib()
-        p = "inflate9_" if fmt == "deflate64-raw" else "inflate_"
+        p = "deflate_" if compress else "inflate9_" if fmt == "deflate64-raw" else "inflate_"
         self._process = getattr(L, p + "process")
         self._last = getattr(L, p + "last_consumed")
         self._end = getattr(L, p + "end")
         self.h = getattr(L, p + "new")()
         if not self.h:
             raise MemoryError("stream allocation failed")
-        init = {"deflate": "inflate_init", "deflate-raw": "inflate_init_raw", "gzip": "inflate_init_gzip",
-                "deflate64-raw": "inflate9_init_raw"}[fmt]
-        r = getattr(L, init)(self.h)
+        init = {"deflate": "init", "deflate-raw": "init_raw", "gzip": "init_gzip",
+                "deflate64-raw": "init_raw"}[fmt]
+        args = (self.h, level) if compress else (self.h,)
+        r = getattr(L, p + init)(*args)
         if r != 0:
             raise ZStreamsError("init failed:" + str(r))
 
@@ -275,6 +361,61 @@ class DecompressionStreamZlib:
             if r != 0:
                 raise ZStreamsError("end error:" + str(r))
         return out
+
+
+class CompressionStreamZlib:
+    """Mirror of the reference's ``CompressionStreamZlib``
+    (src/wasm/api/zlib-streams.js:159-163 over ``_make(true, ...)``).  As in the
+    reference, process codes are not checked while compressing (:89, :123)."""
+
+    def __init__(self, fmt="deflate", options=None):
+        options = options or {}
+        level = options.get("level", -1)
+        self.out_size = options.get("outBuffer", 64 * 1024)
+        self._h = _Handle(fmt, compress=True, level=level if isinstance(level, int) else -1)
+        self._out = ctypes.create_string_buffer(self.out_size)
+
+    def transform(self, chunk):
+        out = []
+        off = 0
+        try:
+            while off < len(chunk):
+                n = min(len(chunk) - off, 32 * 1024)
+                produced, _, consumed = self._h.process(chunk[off:off + n], self._out, Z_NO_FLUSH)
+                if produced:
+                    out.append(self._out.raw[:produced])
+                if consumed == 0:
+                    break
+                off += consumed
+        except Exception:
+            self._h.end()
+            raise
+        return out
+
+    def flush(self):
+        out = []
+        try:
+            while True:
+                produced, code, _ = self._h.process(b"", self._out, Z_FINISH)
+                if produced:
+                    out.append(self._out.raw[:produced])
+                if code == 1 or produced == 0:
+                    break
+        finally:
+            r = self._h.end()
+            if r != 0:
+                raise ZStreamsError("end error:" + str(r))
+        return out
+
+
+def compress(data, fmt="deflate-raw", level=-1, write_size=65536):
+    """Pipe ``data`` through a CompressionStreamZlib in ``write_size`` writes."""
+    cs = CompressionStreamZlib(fmt, {"level": level})
+    parts = []
+    for i in range(0, len(data), write_size):
+        parts += cs.transform(data[i:i + write_size])
+    parts += cs.flush()
+    return b"".join(parts)
 
 
 def decompress(data, fmt="deflate-raw", write_size=4096):
