@@ -5,6 +5,12 @@ One "step" = one zs_inflate_batch() over all of this rank's streams, inputs
 already resident in HBM, outputs written to HBM (ZS_F_DEVICE).  Weak scaling:
 every rank decodes its own 64 streams (stream ids rank*64 .. rank*64+63).
 
+The "(+ compressed)" half of the metric (configs[2]): after the inflate
+measurement the 64 decompressed streams, still in HBM, are gzip-compressed
+(level 6) by one zs_deflate_batch() per step; the line's "compress" object
+holds that rate (input MiB/s), the size against host zlib L6 on the same
+streams, the GPU inflate round trip check and a host zlib L6 deflate baseline.
+
 Prints ONE JSON line (rank 0) with the driver's contract fields plus
   roofline     -- decode kernel: algorithmic bytes (compressed in + decompressed
                   out) per launch / average decode-kernel time measured with HIP
@@ -84,6 +90,46 @@ def cpu_baseline(comps, raws, wbits, sample, threads, min_seconds):
             "verified": bool(ok and kp)}
 
 
+def cpu_deflate_baseline(raws, sample, threads, level, wbits, min_seconds):
+    """Host zlib deflate (the reference's deflate, byte-identical) of `sample`
+    streams on 1 thread (repeated to >= min_seconds) and on `threads` threads."""
+    import numpy as np
+
+    L = ctypes.CDLL(os.path.join(ROOT, "oracle", "libzs_cpubase.so"))
+    L.zs_cpu_deflate.restype = ctypes.c_double
+    L.zs_cpu_zlib_version.restype = ctypes.c_char_p
+    L.zs_cpu_deflate.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t),
+                                 ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t), ctypes.c_size_t,
+                                 ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                 ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_int)]
+    cap = max(len(raws[i]) for i in sample) * 11 // 10 + 65536
+    bufs = {i: np.empty(cap, dtype=np.uint8) for i in sample}
+
+    def run(ids, nthreads):
+        n = len(ids)
+        rp = (ctypes.c_void_p * n)(*[raws[i].ctypes.data for i in ids])
+        rl = (ctypes.c_size_t * n)(*[len(raws[i]) for i in ids])
+        cp = (ctypes.c_void_p * n)(*[bufs[i].ctypes.data for i in ids])
+        cl = (ctypes.c_size_t * n)()
+        tot = ctypes.c_uint64()
+        bad = ctypes.c_int()
+        t = L.zs_cpu_deflate(rp, rl, cp, cl, cap, n, nthreads, level, wbits, ctypes.byref(tot), ctypes.byref(bad))
+        return t, tot.value, not bad.value, sum(cl)
+
+    t1 = b1 = c1 = passes = 0
+    ok = True
+    while t1 < min_seconds or passes == 0:
+        t, b, k, c = run(sample, 1)
+        t1, b1, c1, ok, passes = t1 + t, b1 + b, c1 + c, ok and k, passes + 1
+    tn, bn, kn, _ = run(sample * max(1, threads // len(sample)), threads)
+    return {"value": round(b1 / t1 / 2**20, 2), "unit": "MiB/s (input)", "cores": 1, "kind": "reference",
+            "impl": f"host zlib {L.zs_cpu_zlib_version().decode()} deflate level {level} memLevel 8 "
+                    "(byte-identical to the reference's deflate)",
+            "sample": f"{len(sample)} streams x {passes} pass(es), {b1 / 2**20:.0f} MiB in, {t1:.1f} s on 1 thread",
+            "ratio": round(b1 / c1, 3) if c1 else None,
+            "value_all_threads": round(bn / tn / 2**20, 1), "threads": threads, "verified": bool(ok and kn)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -94,6 +140,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=64, help="streams in the CPU baseline sample")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="minimum 1-thread CPU baseline work")
+    ap.add_argument("--no-compress", action="store_true", help="skip the GPU deflate leg")
+    ap.add_argument("--compress-level", type=int, default=6)
+    ap.add_argument("--cpu-deflate-seconds", type=float, default=10.0)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json"),
                     help="PMC-derived HBM bytes per pipeline launch (null in the line when absent)")
     args = ap.parse_args()
@@ -190,6 +239,11 @@ def main():
         # HBM bytes per launch from rocprofv3 PMC passes (tools/pmc_traffic.py)
         traffic = json.load(open(args.traffic_json)).get("hbm_bytes_per_launch")
 
+    comp_leg = None
+    if not args.no_compress:
+        comp_leg = compress_leg(args, zstreams, shard, torch, np, dev, dist, raws, d_out, out_ptrs, nbytes,
+                                comp_total, host_threads, rank)
+
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
         # interleave Zipf (first half) and lines (second half) streams
@@ -218,10 +272,78 @@ def main():
                          "stage_kernels": zstreams.STAGE_KERNELS},
             "cpu_baseline": cpu,
             "path_stats": stats,
+            "compress": comp_leg,
         }
         print(json.dumps(line), flush=True)
     if dist:
         tdist.destroy_process_group()
+
+
+def compress_leg(args, zstreams, shard, torch, np, dev, dist, raws, d_out, raw_ptrs, nbytes, zlib_raw_total,
+                 host_threads, rank):
+    """configs[2]: gzip (windowBits 31) level-L GPU deflate of the decompressed
+    streams resident in HBM, then a GPU inflate round trip of its output."""
+    n = len(raw_ptrs)
+    level = args.compress_level
+    bound = zstreams.deflate_bound(nbytes, 31)
+    slot = (bound + 4095) & ~4095
+    d_cz = torch.empty(n * slot, dtype=torch.uint8, device=dev)
+    cz_ptrs = [d_cz.data_ptr() + k * slot for k in range(n)]
+
+    def step():
+        return zstreams.deflate_batch_device(raw_ptrs, [nbytes] * n, cz_ptrs, [bound] * n, 31, level)
+
+    for _ in range(args.warmup):
+        res = step()
+    res = step()
+    zstreams.profile(True)
+    if dist:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        torch.distributed.barrier()
+    t_el = time.perf_counter() - t0
+    k_ms, stages, k_n = zstreams.profile_deflate()
+    zstreams.profile(False)
+    sizes = [r["total_out"] for r in res]
+    ok = all(r["ret"] == 1 and r["total_in"] == nbytes for r in res)
+    # round trip: GPU inflate of the GPU gzip streams into the zeroed raw buffers
+    d_out.zero_()
+    back = zstreams.inflate_batch_device(cz_ptrs, sizes, raw_ptrs, [nbytes] * n, 31)
+    torch.cuda.synchronize()
+    ok = ok and all(b["ret"] == 1 and b["total_out"] == nbytes and b["adler"] == r["adler"]
+                    for b, r in zip(back, res))
+    out_host = d_out.cpu().numpy().reshape(n, nbytes)
+    ok = ok and all(np.array_equal(out_host[k], raws[k]) for k in range(n))
+    del out_host
+    log(f"[rank {rank}] GPU gzip L{level}: {sum(sizes)} bytes, round trip ok: {ok}")
+    t_el, in_bytes, ok = shard.reduce_counters(t_el, n * nbytes * args.steps, ok, device=dev)
+    comp_total = sum(sizes)
+    zlib_total = zlib_raw_total + 18 * n  # host zlib L6 raw streams + gzip wrapper
+    k_avg_s = (k_ms / max(k_n, 1)) / 1e3
+    alg = n * nbytes + comp_total
+    achieved = alg / k_avg_s / 1e9 if k_avg_s > 0 else 0.0
+    leg = {"metric": "MiB/s compressed (input bytes), gzip level %d" % level,
+           "value": round(in_bytes / t_el / 2**20, 1), "unit": "MiB/s", "ms_per_step": round(t_el * 1e3 / args.steps, 3),
+           "workload": f"{n}x{nbytes >> 20}MiB gzip (windowBits 31) level {level} deflate, inputs resident in HBM",
+           "compressed_bytes": comp_total, "ratio": round(n * nbytes / comp_total, 3),
+           "zlib_l6_bytes": zlib_total, "size_vs_zlib_l6": round(comp_total / zlib_total, 4),
+           "roundtrip_verified": ok,
+           "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(achieved / HBM_PEAK_GBS, 5), "kernel": "deflate pipeline",
+                        "kernel_ms_avg": round(k_avg_s * 1e3, 3), "alg_bytes_per_launch": alg,
+                        "stages_ms_avg": {k: round(v / max(k_n, 1), 3) for k, v in stages.items()},
+                        "stage_kernels": zstreams.DEFLATE_STAGE_KERNELS}}
+    if rank == 0 and not args.no_cpu_baseline:
+        half = n // 2
+        sample = [0, half, 1, half + 1][:max(1, min(4, n))]
+        leg["cpu_baseline"] = cpu_deflate_baseline(raws, sample, host_threads, level, 31, args.cpu_deflate_seconds)
+    del d_cz
+    return leg
 
 
 if __name__ == "__main__":

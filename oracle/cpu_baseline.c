@@ -84,3 +84,65 @@ double zs_cpu_inflate(const uint8_t *const *comp, const size_t *comp_len, uint8_
 }
 
 const char *zs_cpu_zlib_version(void) { return zlibVersion(); }
+
+/* host zlib deflate (deflateInit2(level, Z_DEFLATED, wbits, 8,
+ * Z_DEFAULT_STRATEGY) + one deflate(Z_FINISH) per buffer, byte-identical to the
+ * reference's shipped deflate), buffers dealt round-robin to
+ * `nthreads` pthreads.  Returns wall seconds; *total_in receives the bytes
+ * consumed, comp_len[i] each output size. */
+typedef struct {
+  const uint8_t *const *raw;
+  const size_t *raw_len;
+  uint8_t *const *comp;
+  size_t *comp_len;
+  size_t comp_cap;
+  int n, nthreads, tid, level, wbits;
+  uint64_t consumed;
+  int bad;
+} dtask_t;
+
+static void *drun(void *arg) {
+  dtask_t *t = (dtask_t *)arg;
+  for (int i = t->tid; i < t->n; i += t->nthreads) {
+    z_stream z;
+    memset(&z, 0, sizeof z);
+    deflateInit2(&z, t->level, Z_DEFLATED, t->wbits, 8, Z_DEFAULT_STRATEGY);
+    z.next_in = (Bytef *)t->raw[i];
+    z.avail_in = (uInt)t->raw_len[i];
+    z.next_out = t->comp[i];
+    z.avail_out = (uInt)t->comp_cap;
+    int r = deflate(&z, Z_FINISH);
+    t->consumed += z.total_in;
+    t->comp_len[i] = z.total_out;
+    t->bad |= r != Z_STREAM_END;
+    deflateEnd(&z);
+  }
+  return NULL;
+}
+
+double zs_cpu_deflate(const uint8_t *const *raw, const size_t *raw_len, uint8_t *const *comp, size_t *comp_len,
+                      size_t comp_cap, int n, int nthreads, int level, int wbits, uint64_t *total_in, int *bad) {
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 512) nthreads = 512;
+  dtask_t *ts = (dtask_t *)calloc((size_t)nthreads, sizeof(dtask_t));
+  pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
+  struct timespec a, b;
+  clock_gettime(CLOCK_MONOTONIC, &a);
+  for (int k = 0; k < nthreads; k++) {
+    ts[k] = (dtask_t){raw, raw_len, comp, comp_len, comp_cap, n, nthreads, k, level, wbits, 0, 0};
+    pthread_create(&th[k], NULL, drun, &ts[k]);
+  }
+  uint64_t tot = 0;
+  int anybad = 0;
+  for (int k = 0; k < nthreads; k++) {
+    pthread_join(th[k], NULL);
+    tot += ts[k].consumed;
+    anybad |= ts[k].bad;
+  }
+  clock_gettime(CLOCK_MONOTONIC, &b);
+  free(ts);
+  free(th);
+  *total_in = tot;
+  *bad = anybad;
+  return (double)(b.tv_sec - a.tv_sec) + 1e-9 * (double)(b.tv_nsec - a.tv_nsec);
+}
