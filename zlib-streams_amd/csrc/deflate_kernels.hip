@@ -36,6 +36,7 @@
 
 #include "zs_common.h"
 #include "zs_device.h"
+#include "zs_check.h"
 
 #define DZ_SEG 65536u        // input bytes per segment
 #define DZ_T 256u            // threads per workgroup
@@ -47,10 +48,25 @@
 // ---------------------------------------------------------------------------
 // helpers
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t dz_load32(const uint8_t *p) {
+typedef __attribute__((address_space(1))) const uint8_t gcu8;  // global loads, not flat
+__device__ __forceinline__ uint32_t dz_load32(gcu8 *p) {
   uint32_t v;
   __builtin_memcpy(&v, p, 4);
   return v;
+}
+__device__ __forceinline__ uint4 dz_load128(gcu8 *p) {  // unaligned 16-byte load
+  uint4 v;
+  __builtin_memcpy(&v, p, 16);
+  return v;
+}
+// bytes equal at the start of a and b (0..16)
+__device__ __forceinline__ uint32_t dz_eq16(uint4 a, uint4 b) {
+  const uint32_t x0 = a.x ^ b.x, x1 = a.y ^ b.y, x2 = a.z ^ b.z, x3 = a.w ^ b.w;
+  if (x0) return (uint32_t)__builtin_ctz(x0) >> 3;
+  if (x1) return 4u + ((uint32_t)__builtin_ctz(x1) >> 3);
+  if (x2) return 8u + ((uint32_t)__builtin_ctz(x2) >> 3);
+  if (x3) return 12u + ((uint32_t)__builtin_ctz(x3) >> 3);
+  return 16u;
 }
 __device__ __forceinline__ uint32_t dz_hash(uint32_t v) { return (v * 2654435761u) >> (32 - 13); }
 
@@ -98,7 +114,7 @@ __global__ void __launch_bounds__(DZ_T) zs_dz_match_kernel(const ZsDJobDev *__re
   const ZsDSegDev sg = segs[blockIdx.x];
   const ZsDJobDev jb = jobs[sg.job];
   if (jb.level == 0) return;  // stored blocks: no matches
-  const uint8_t *in = jb.in;
+  gcu8 *in = (gcu8 *)jb.in;
   const uint64_t n = jb.in_len;
   const uint64_t s = sg.start, e = s + sg.len;
   uint32_t *mo = matches + sg.tok;
@@ -115,39 +131,65 @@ __global__ void __launch_bounds__(DZ_T) zs_dz_match_kernel(const ZsDJobDev *__re
     if (p < s && p + 4 <= n) tab[dz_hash(dz_load32(in + p))][way] = (uint16_t)p;
   }
   __syncthreads();
-  const uint32_t max_chain_len = 258u;
   const uint32_t maxd = 1u << jb.wbits;
   for (uint64_t P = s; P < e; P += DZ_T) {
     const uint64_t p = P + tid;
     uint32_t h = 0;
     uint32_t best = 0, bd = 0;
     if (p < e && p + 4 <= n) {
-      const uint32_t v = dz_load32(in + p);
-      h = dz_hash(v);
-      const uint32_t lim = (uint32_t)min<uint64_t>(max_chain_len, e - p);
+      const uint32_t lim = (uint32_t)min<uint64_t>(258u, e - p);
+      if (p + 16 <= n) {
+        // 16-byte compares: one load round for the common (short) match
+        const uint4 cur = dz_load128(in + p);
+        h = dz_hash(cur.x);
+        const uint2 ent = *reinterpret_cast<const uint2 *>(&tab[h][0]);
+        const uint32_t c4[4] = {ent.x & 0xffffu, ent.x >> 16, ent.y & 0xffffu, ent.y >> 16};
+        uint32_t dd[4];
+        uint4 cv[4];
 #pragma unroll
-      for (uint32_t w = 0; w < DZ_WAYS; w++) {
-        const uint32_t c16 = tab[h][w];
-        if (c16 == 0xffffu) continue;
-        const uint32_t d = ((uint32_t)p - c16) & 0xffffu;
-        if (d == 0 || d > maxd || d > p) continue;
-        const uint8_t *q = in + (p - d);
-        if (dz_load32(q) != v) continue;
-        uint32_t L = 4;
-        while (L + 4 <= lim) {
-          const uint32_t x = dz_load32(q + L) ^ dz_load32(in + p + L);
-          if (x) {
-            L += (uint32_t)__builtin_ctz(x) >> 3;
-            break;
-          }
-          L += 4;
+        for (uint32_t w = 0; w < DZ_WAYS; w++) {
+          const uint32_t d = ((uint32_t)p - c4[w]) & 0xffffu;
+          dd[w] = (c4[w] == 0xffffu || d == 0 || d > maxd || d > p) ? 0u : d;
+          if (dd[w]) cv[w] = dz_load128(in + (p - dd[w]));
         }
-        if (L + 4 > lim)
+#pragma unroll
+        for (uint32_t w = 0; w < DZ_WAYS; w++) {
+          if (!dd[w]) continue;
+          uint32_t L = dz_eq16(cv[w], cur);
+          if (L < 4u) continue;
+          if (L == 16u) {
+            gcu8 *q = in + (p - dd[w]);
+            while (L + 16u <= lim) {
+              const uint32_t k = dz_eq16(dz_load128(q + L), dz_load128(in + p + L));
+              L += k;
+              if (k < 16u) break;
+            }
+            if (L + 16u > lim)
+              while (L < lim && q[L] == in[p + L]) L++;
+          }
+          L = min(L, lim);
+          if (L > best || (L == best && dd[w] < bd)) {
+            best = L;
+            bd = dd[w];
+          }
+        }
+      } else {  // the last 15 bytes of the input: byte compares
+        const uint32_t v = dz_load32(in + p);
+        h = dz_hash(v);
+#pragma unroll
+        for (uint32_t w = 0; w < DZ_WAYS; w++) {
+          const uint32_t c16 = tab[h][w];
+          if (c16 == 0xffffu) continue;
+          const uint32_t d = ((uint32_t)p - c16) & 0xffffu;
+          if (d == 0 || d > maxd || d > p) continue;
+          gcu8 *q = in + (p - d);
+          uint32_t L = 0;
           while (L < lim && q[L] == in[p + L]) L++;
-        L = min(L, lim);
-        if (L > best || (L == best && d < bd)) {
-          best = L;
-          bd = d;
+          if (L < 4u) continue;
+          if (L > best || (L == best && d < bd)) {
+            best = L;
+            bd = d;
+          }
         }
       }
     }
@@ -571,94 +613,30 @@ __global__ void __launch_bounds__(DZ_T) zs_dz_block_kernel(const ZsDJobDev *__re
 }
 
 // ---------------------------------------------------------------------------
-// D4: per-job bit offsets (scan over segments) and checksums of the input
+// D4: checksums of the input (zs_check.h: every segment adds its contribution
+// to the job's accumulators, in any order) and per-job bit offsets
 // ---------------------------------------------------------------------------
-__device__ uint32_t dz_gf2_mulmod(uint32_t a, uint32_t b) {
-  uint32_t m = 1u << 31, p = 0;
-  for (;;) {
-    if (a & m) {
-      p ^= b;
-      if ((a & (m - 1)) == 0) break;
-    }
-    m >>= 1;
-    b = (b & 1) ? (b >> 1) ^ 0xEDB88320u : b >> 1;
-  }
-  return p;
-}
-__device__ uint32_t dz_x8n_mod(uint64_t n) {
-  uint32_t p = 1u << 31, sq = 1u << 23;
-  while (n) {
-    if (n & 1) p = dz_gf2_mulmod(sq, p);
-    sq = dz_gf2_mulmod(sq, sq);
-    n >>= 1;
-  }
-  return p;
-}
-
-// per segment: CRC-32 (gzip) or Adler-32 sums (zlib) of its input, 256 threads
-__global__ void __launch_bounds__(DZ_T) zs_dz_check_kernel(const ZsDJobDev *__restrict__ jobs, ZsDSegDev *__restrict__ segs) {
-  __shared__ uint32_t s_tab[256], s_a[DZ_T], s_b[DZ_T];
-  __shared__ uint32_t s_len[DZ_T];
+__global__ void __launch_bounds__(DZ_T) zs_dz_check_kernel(ZsDJobDev *__restrict__ jobs, const ZsDSegDev *__restrict__ segs) {
+  __shared__ uint32_t s_tab[4][256];
+  __shared__ uint64_t s_red[16];
   const uint32_t t = threadIdx.x;
   const ZsDSegDev sg = segs[blockIdx.x];
   const ZsDJobDev jb = jobs[sg.job];
-  if (jb.wrap == 0) return;
-  const uint8_t *p = jb.in + sg.start;
-  const uint32_t n = sg.len;
-  const uint32_t per = (n + DZ_T - 1) / DZ_T;
-  const uint32_t lo = min(n, per * t), hi = min(n, per * (t + 1));
+  if (jb.wrap == 0 || sg.len == 0) return;
+  const uint32_t per = ((sg.len + DZ_T - 1) / DZ_T + 3u) & ~3u;
+  const uint64_t lo = sg.start + min(sg.len, per * t), hi = sg.start + min(sg.len, per * (t + 1));
   if (jb.wrap == 2) {
-    uint32_t c = t;
-    for (int k = 0; k < 8; k++) c = (c & 1) ? (0xEDB88320u ^ (c >> 1)) : (c >> 1);
-    s_tab[t] = c;
-    __syncthreads();
-    uint32_t crc = 0xffffffffu;
-    for (uint32_t i = lo; i < hi; i++) crc = s_tab[(crc ^ p[i]) & 0xff] ^ (crc >> 8);
-    s_a[t] = hi > lo ? ~crc : 0u;
-    s_len[t] = hi - lo;
-    __syncthreads();
-    for (uint32_t w = 1; w < DZ_T; w <<= 1) {
-      uint32_t nv = 0, nl = 0;
-      const bool act = (t % (2 * w)) == 0 && t + w < DZ_T;
-      if (act) {
-        const uint32_t l2 = s_len[t + w];
-        nv = l2 ? (dz_gf2_mulmod(dz_x8n_mod(l2), s_a[t]) ^ s_a[t + w]) : s_a[t];
-        nl = s_len[t] + l2;
-      }
-      __syncthreads();
-      if (act) {
-        s_a[t] = nv;
-        s_len[t] = nl;
-      }
-      __syncthreads();
-    }
-    if (t == 0) segs[blockIdx.x].ck_a = s_a[0];
+    zs_crc_tables(s_tab);
+    const uint32_t v = zs_block_xor(zs_crc_piece(jb.in, lo, hi, jb.in_len, s_tab), reinterpret_cast<uint32_t *>(s_red));
+    if (t == 0 && v) atomicXor(reinterpret_cast<unsigned long long *>(&jobs[sg.job].ck_a), (unsigned long long)v);
   } else {
-    const uint32_t MOD = 65521u;
-    uint64_t A = 0, B = 0;
-    const uint32_t m = hi - lo;
-    for (uint32_t i = lo; i < hi; i++) {
-      A += p[i];
-      B += (uint64_t)(m - (i - lo)) * p[i];
-      if (((i - lo) & 4095) == 4095) {
-        A %= MOD;
-        B %= MOD;
-      }
-    }
-    s_a[t] = (uint32_t)(A % MOD);
-    s_b[t] = (uint32_t)(B % MOD);
-    __syncthreads();
-    if (t == 0) {  // segment sums: A = sum, B = sum of (bytes to the segment end, inclusive) weights
-      uint64_t a = 0, b = 0;
-      for (uint32_t k = 0; k < DZ_T; k++) {
-        const uint32_t st = min(n, per * k), en = min(n, per * (k + 1));
-        if (en <= st) continue;
-        const uint64_t tail = (n - en) % MOD;
-        a = (a + s_a[k]) % MOD;
-        b = (b + s_b[k] + tail * s_a[k]) % MOD;
-      }
-      segs[blockIdx.x].ck_a = (uint32_t)a;
-      segs[blockIdx.x].ck_b = (uint32_t)b;
+    uint32_t A = 0, B = 0;
+    if (hi > lo) zs_adler_piece(jb.in, lo, hi, jb.in_len, &A, &B);
+    const uint64_t sa = zs_block_sum(A, s_red);
+    const uint64_t sb = zs_block_sum(B, s_red);
+    if (t == 0) {
+      atomicAdd(reinterpret_cast<unsigned long long *>(&jobs[sg.job].ck_a), (unsigned long long)sa);
+      atomicAdd(reinterpret_cast<unsigned long long *>(&jobs[sg.job].ck_b), (unsigned long long)sb);
     }
   }
 }
@@ -669,8 +647,6 @@ __global__ void __launch_bounds__(DZ_T) zs_dz_check_kernel(const ZsDJobDev *__re
 __global__ void __launch_bounds__(DZ_JT) zs_dz_offsets_kernel(ZsDJobDev *__restrict__ jobs, ZsDSegDev *__restrict__ segs,
                                                                uint8_t *__restrict__ stage) {
   __shared__ uint64_t s_sum[DZ_JT];
-  __shared__ uint32_t s_ck[DZ_JT];
-  __shared__ uint64_t s_cl[DZ_JT];
   const uint32_t t = threadIdx.x;
   ZsDJobDev jb = jobs[blockIdx.x];
   const uint32_t hdr = jb.wrap == 2 ? 10u : (jb.wrap == 1 ? 2u : 0u);
@@ -699,46 +675,10 @@ __global__ void __launch_bounds__(DZ_JT) zs_dz_offsets_kernel(ZsDJobDev *__restr
     segs[jb.seg0 + k].bitoff = off;
     off += segs[jb.seg0 + k].nbits;
   }
-  // checksum combine over segments (in order)
-  if (jb.wrap == 2) {
-    uint32_t crc = 0;
-    uint64_t len = 0;
-    for (uint32_t k = k0; k < k1; k++) {
-      const ZsDSegDev sg = segs[jb.seg0 + k];
-      crc = sg.len ? (len ? (dz_gf2_mulmod(dz_x8n_mod(sg.len), crc) ^ sg.ck_a) : sg.ck_a) : crc;
-      len += sg.len;
-    }
-    s_ck[t] = crc;
-    s_cl[t] = len;
-    __syncthreads();
-    if (t == 0) {
-      uint32_t c = 0;
-      uint64_t l = 0;
-      for (uint32_t k = 0; k < DZ_JT; k++) {
-        if (!s_cl[k]) continue;
-        c = l ? (dz_gf2_mulmod(dz_x8n_mod(s_cl[k]), c) ^ s_ck[k]) : s_ck[k];
-        l += s_cl[k];
-      }
-      jobs[blockIdx.x].check = c;
-    }
-  } else if (jb.wrap == 1) {
-    if (t == 0) {  // Adler-32 combine of segment pieces (a = sum, b = weighted sum to each piece's end)
-      const uint32_t MOD = 65521u;
-      uint64_t a = 1, b = 0;
-      const uint64_t n = jb.in_len;
-      for (uint32_t k = 0; k < ns; k++) {
-        const ZsDSegDev sg = segs[jb.seg0 + k];
-        if (!sg.len) continue;
-        const uint64_t tail = (n - sg.start - sg.len) % MOD;
-        a = (a + sg.ck_a) % MOD;
-        b = (b + sg.ck_b + tail * sg.ck_a) % MOD;
-      }
-      b = (b + (n % MOD)) % MOD;  // the initial a = 1 contributes n to b
-      jobs[blockIdx.x].check = (uint32_t)((b << 16) | a);
-    }
-  } else if (t == 0) {
-    jobs[blockIdx.x].check = 0;
-  }
+  if (t == 0)
+    jobs[blockIdx.x].check = jb.wrap == 2   ? zs_crc_final((uint32_t)jb.ck_a, jb.in_len)
+                             : jb.wrap == 1 ? zs_adler_final(jb.ck_a, jb.ck_b, jb.in_len)
+                                            : 0u;
   if (t == 0) {
     uint8_t *o = stage + jb.stage;
     if (jb.wrap == 2) {  // gzip header as zlib writes it with no options (mtime 0, OS 3)

@@ -25,6 +25,7 @@
 
 #include "zs_common.h"
 #include "zs_device.h"
+#include "zs_check.h"
 
 #define IN_RING_WORDS 1024   // 4 KiB compressed-input ring
 #define PIECE_WORDS 256      // 1 KiB per fill (64 lanes x 16 B)
@@ -614,106 +615,39 @@ template __global__ void zs_decode_kernel<true>(const ZsJobDev *, const ZsHeadDe
 // Checks: CRC-32 (gzip) / Adler-32 (zlib) over each job's output, segment
 // parallel with an exact combine (UPDATE_CHECK, src/inflate.c:425-429).
 // ---------------------------------------------------------------------------
-__device__ uint32_t gf2_mulmod(uint32_t a, uint32_t b) {
-  // multiply a(x) * b(x) mod P(x), reflected bit order (bit 31 = x^0)
-  uint32_t m = 1u << 31, p = 0;
-  for (;;) {
-    if (a & m) {
-      p ^= b;
-      if ((a & (m - 1)) == 0) break;
-    }
-    m >>= 1;
-    b = (b & 1) ? (b >> 1) ^ 0xEDB88320u : b >> 1;
-  }
-  return p;
-}
-// x^(8n) mod P
-__device__ uint32_t x8n_mod(uint64_t n) {
-  uint32_t p = 1u << 31;  // x^0
-  uint32_t sq = 1u << 23; // x^8
-  while (n) {
-    if (n & 1) p = gf2_mulmod(sq, p);
-    sq = gf2_mulmod(sq, sq);
-    n >>= 1;
-  }
-  return p;
-}
-
+// One workgroup per (job, piece): a piece of P = max(64 KiB, n / gridDim.y)
+// bytes (4-byte multiple) adds its contribution to the job's accumulators
+// (zs_check.h), so a 64 MiB output is checked by hundreds of workgroups.
 #define CHECK_THREADS 256
 __global__ void __launch_bounds__(CHECK_THREADS) zs_check_kernel(const ZsJobDev *__restrict__ jobs, const ZsHeadDev *__restrict__ heads,
-                                                                 const ZsDecDev *__restrict__ decs, uint32_t *__restrict__ checks) {
-  __shared__ uint32_t s_tab[256];
-  __shared__ uint32_t s_a[CHECK_THREADS];
-  __shared__ uint32_t s_b[CHECK_THREADS];
-  __shared__ uint64_t s_len[CHECK_THREADS];
+                                                                 const ZsDecDev *__restrict__ decs, uint64_t *__restrict__ checks) {
+  __shared__ uint32_t s_tab[4][256];
+  __shared__ uint64_t s_red[16];
   const uint32_t j = blockIdx.x;
   const uint32_t t = threadIdx.x;
   const ZsHeadDev hd = heads[j];
   const ZsDecDev dc = decs[j];
-  if (hd.code != ZD_END || hd.is_gzip < 0 || dc.code == ZD_SKIP) {
-    if (t == 0) checks[j] = 0;
-    return;
-  }
+  if (hd.code != ZD_END || hd.is_gzip < 0 || dc.code == ZD_SKIP) return;
   const uint8_t *p = jobs[j].out;
   const uint64_t n = dc.total_out;
-  const uint64_t seg = ((n + CHECK_THREADS - 1) / CHECK_THREADS + 15) & ~15ull;
-  const uint64_t lo = min(n, seg * t), hi = min(n, seg * (t + 1));
+  const uint64_t piece = max<uint64_t>(65536u, ((n + gridDim.y - 1) / gridDim.y + 1023u) & ~1023ull);
+  const uint64_t p0 = (uint64_t)blockIdx.y * piece;
+  if (p0 >= n) return;
+  const uint64_t plen = min(piece, n - p0);
+  const uint64_t per = ((plen + CHECK_THREADS - 1) / CHECK_THREADS + 3u) & ~3ull;
+  const uint64_t lo = p0 + min(plen, per * t), hi = p0 + min(plen, per * (t + 1));
   if (hd.is_gzip == 1) {
-    {
-      uint32_t c = t;
-      for (int k = 0; k < 8; k++) c = (c & 1) ? (0xEDB88320u ^ (c >> 1)) : (c >> 1);
-      s_tab[t] = c;
-    }
-    __syncthreads();
-    uint32_t crc = 0xffffffffu;
-    for (uint64_t i = lo; i < hi; i++) crc = s_tab[(crc ^ p[i]) & 0xff] ^ (crc >> 8);
-    s_a[t] = (hi > lo) ? ~crc : 0u;
-    s_len[t] = hi - lo;
-    __syncthreads();
-    for (uint32_t w = 1; w < CHECK_THREADS; w <<= 1) {
-      uint32_t nv = 0;
-      uint64_t nl = 0;
-      bool act = (t % (2 * w)) == 0 && t + w < CHECK_THREADS;
-      if (act) {
-        uint64_t l2 = s_len[t + w];
-        nv = l2 ? (gf2_mulmod(x8n_mod(l2), s_a[t]) ^ s_a[t + w]) : s_a[t];
-        nl = s_len[t] + l2;
-      }
-      __syncthreads();
-      if (act) {
-        s_a[t] = nv;
-        s_len[t] = nl;
-      }
-      __syncthreads();
-    }
-    if (t == 0) checks[j] = s_a[0];
+    zs_crc_tables(s_tab);
+    const uint32_t v = zs_block_xor(zs_crc_piece(p, lo, hi, n, s_tab), reinterpret_cast<uint32_t *>(s_red));
+    if (t == 0 && v) atomicXor(reinterpret_cast<unsigned long long *>(&checks[2 * j]), (unsigned long long)v);
   } else {
-    const uint32_t MOD = 65521u;
-    uint64_t A = 0, B = 0;
-    uint64_t m = hi - lo;
-    for (uint64_t i = lo; i < hi; i++) {
-      A += p[i];
-      B += (m - (i - lo)) * (uint64_t)p[i];
-      if (((i - lo) & 4095) == 4095) {
-        A %= MOD;
-        B %= MOD;
-      }
-    }
-    s_a[t] = (uint32_t)(A % MOD);
-    s_b[t] = (uint32_t)(B % MOD);
-    s_len[t] = lo;  // segment start
-    __syncthreads();
+    uint32_t A = 0, B = 0;
+    if (hi > lo) zs_adler_piece(p, lo, hi, n, &A, &B);
+    const uint64_t sa = zs_block_sum(A, s_red);
+    const uint64_t sb = zs_block_sum(B, s_red);
     if (t == 0) {
-      uint64_t a = 1, b = n % MOD;
-      for (uint32_t k = 0; k < CHECK_THREADS; k++) {
-        uint64_t st = s_len[k];
-        uint64_t segl = min(n, st + seg) - min(n, st);
-        if (segl == 0) continue;
-        uint64_t tail = (n - st - segl) % MOD;
-        a = (a + s_a[k]) % MOD;
-        b = (b + s_b[k] + tail * s_a[k]) % MOD;
-      }
-      checks[j] = (uint32_t)((b << 16) | a);
+      atomicAdd(reinterpret_cast<unsigned long long *>(&checks[2 * j]), (unsigned long long)sa);
+      atomicAdd(reinterpret_cast<unsigned long long *>(&checks[2 * j + 1]), (unsigned long long)sb);
     }
   }
 }
@@ -723,7 +657,7 @@ __global__ void __launch_bounds__(CHECK_THREADS) zs_check_kernel(const ZsJobDev 
 // (src/inflate.c:1194-1274).
 // ---------------------------------------------------------------------------
 __global__ void zs_finalize_kernel(const ZsJobDev *__restrict__ jobs, const ZsHeadDev *__restrict__ heads,
-                                   const ZsDecDev *__restrict__ decs, const uint32_t *__restrict__ checks,
+                                   const ZsDecDev *__restrict__ decs, const uint64_t *__restrict__ checks,
                                    ZsResultDev *__restrict__ res, uint32_t njobs) {
   uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= njobs) return;
@@ -752,9 +686,9 @@ __global__ void zs_finalize_kernel(const ZsJobDev *__restrict__ jobs, const ZsHe
   const ZsDecDev dc = decs[j];
   const bool raw = hd.is_gzip < 0;
   r.total_out = dc.total_out;
-  r.adler = raw ? 0u : checks[j];
-  if (!raw && hd.is_gzip == 0 && dc.total_out == 0) r.adler = 1;
-  if (!raw && hd.is_gzip == 1 && dc.total_out == 0) r.adler = 0;
+  r.adler = raw ? 0u
+                : hd.is_gzip == 1 ? zs_crc_final((uint32_t)checks[2 * j], dc.total_out)
+                                  : zs_adler_final(checks[2 * j], checks[2 * j + 1], dc.total_out);
   // (an if-chain, not a switch: hipcc 7.2 dropped the msg copy of the default
   // arm of the equivalent switch for codes > ZD_FULL)
   const int code = dc.code;
@@ -816,10 +750,13 @@ extern "C" void zs_launch_decode(int d64, const ZsJobDev *d_jobs, const ZsHeadDe
     hipLaunchKernelGGL(zs_decode_kernel<false>, dim3(n), dim3(64), 0, stream, d_jobs, d_heads, d_ids, d_decs, run_only);
 }
 
+// max_out: the largest out_cap of the batch (sizes the piece grid)
 extern "C" void zs_launch_finish(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, const ZsDecDev *d_decs,
-                                 uint32_t *d_checks, ZsResultDev *d_res, uint32_t njobs, hipStream_t stream) {
+                                 uint64_t *d_checks, ZsResultDev *d_res, uint32_t njobs, uint64_t max_out, hipStream_t stream) {
   const uint32_t tb = 64;
-  hipLaunchKernelGGL(zs_check_kernel, dim3(njobs), dim3(CHECK_THREADS), 0, stream, d_jobs, d_heads, d_decs, d_checks);
+  const uint32_t pieces = (uint32_t)std::min<uint64_t>(1024, std::max<uint64_t>(1, (max_out + 262143) / 262144));
+  (void)hipMemsetAsync(d_checks, 0, 2 * sizeof(uint64_t) * njobs, stream);
+  hipLaunchKernelGGL(zs_check_kernel, dim3(njobs, pieces), dim3(CHECK_THREADS), 0, stream, d_jobs, d_heads, d_decs, d_checks);
   hipLaunchKernelGGL(zs_finalize_kernel, dim3((njobs + tb - 1) / tb), dim3(tb), 0, stream, d_jobs, d_heads, d_decs, d_checks,
                      d_res, njobs);
 }

@@ -27,7 +27,8 @@ extern "C" void zs_launch_header(const ZsJobDev *d_jobs, ZsHeadDev *d_heads, uin
 extern "C" void zs_launch_decode(int d64, const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, const uint32_t *d_ids,
                                  uint32_t n, ZsDecDev *d_decs, const uint32_t *run_only, hipStream_t stream);
 extern "C" void zs_launch_finish(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, const ZsDecDev *d_decs,
-                                 uint32_t *d_checks, ZsResultDev *d_res, uint32_t njobs, hipStream_t stream);
+                                 uint64_t *d_checks, ZsResultDev *d_res, uint32_t njobs, uint64_t max_out,
+                                 hipStream_t stream);
 extern "C" void zs_launch_fixed_tables(uint32_t *fixed, hipStream_t st);
 extern "C" void zs_launch_fixed_compact(uint32_t *fixed, hipStream_t st);
 extern "C" void zs_launch_deflate(ZsDJobDev *d_jobs, uint32_t njobs, ZsDSegDev *d_segs, uint32_t nseg, uint32_t *d_tokens,
@@ -89,7 +90,7 @@ struct Workspace {
   ZsJobDev *d_jobs = nullptr;
   ZsHeadDev *d_heads = nullptr;
   ZsDecDev *d_decs = nullptr;
-  uint32_t *d_checks = nullptr;
+  uint64_t *d_checks = nullptr;  // 2 per job: check accumulators (zs_check.h)
   ZsResultDev *d_res = nullptr;
   uint32_t *d_ids = nullptr;
   ZsJobDev *h_jobs = nullptr;     // pinned
@@ -179,7 +180,7 @@ int ws_reserve_jobs(size_t n) {
   size_t c = std::max<size_t>(n, 2 * g_ws.cap_jobs);
   int r;
   if ((r = grow_dev(&g_ws.d_jobs, c)) || (r = grow_dev(&g_ws.d_heads, c)) || (r = grow_dev(&g_ws.d_decs, c)) ||
-      (r = grow_dev(&g_ws.d_checks, c)) || (r = grow_dev(&g_ws.d_res, c)) || (r = grow_dev(&g_ws.d_ids, 3 * c)) ||
+      (r = grow_dev(&g_ws.d_checks, 2 * c)) || (r = grow_dev(&g_ws.d_res, c)) || (r = grow_dev(&g_ws.d_ids, 3 * c)) ||
       (r = grow_dev(&g_ws.d_fallback, c)) || (r = grow_dev(&g_ws.d_cjobs, c)) || (r = grow_host(&g_ws.h_cjobs, c)) ||
       (r = grow_host(&g_ws.h_jobs, c)) || (r = grow_host(&g_ws.h_res, c)) || (r = grow_host(&g_ws.h_ids, 3 * c)))
     return r;
@@ -267,6 +268,7 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
   std::vector<uint32_t> slot(n, UINT32_MAX);
   std::vector<size_t> in_off(n, 0), out_off(n, 0);
   size_t in_total = 0, out_total = 0;
+  uint64_t max_out = 0;
   uint32_t nv = 0;
   for (uint32_t i = 0; i < n; i++) {
     ZsJobDev jd{};
@@ -281,6 +283,7 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
     slot[i] = nv;
     jd.in_len = jobs[i].in_len;
     jd.out_cap = jobs[i].out_cap;
+    max_out = std::max<uint64_t>(max_out, jd.out_cap);
     if (dev) {
       jd.in = static_cast<const uint8_t *>(jobs[i].in);
       jd.out = static_cast<uint8_t *>(jobs[i].out);
@@ -382,7 +385,7 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
   zs_launch_decode(1, g_ws.d_jobs, g_ws.d_heads, g_ws.d_ids + n_std, n_d64, g_ws.d_decs, nullptr, st);
   if (n_cj) zs_launch_decode(0, g_ws.d_jobs, g_ws.d_heads, g_ws.d_ids + n_std + n_d64, n_cj, g_ws.d_decs, g_ws.d_fallback, st);
   if (ev) HIP_OK(hipEventRecord(ev[7], st));
-  zs_launch_finish(g_ws.d_jobs, g_ws.d_heads, g_ws.d_decs, g_ws.d_checks, g_ws.d_res, nv, st);
+  zs_launch_finish(g_ws.d_jobs, g_ws.d_heads, g_ws.d_decs, g_ws.d_checks, g_ws.d_res, nv, max_out, st);
   if (ev) HIP_OK(hipEventRecord(ev[8], st));
   {
     hipError_t le = hipGetLastError();

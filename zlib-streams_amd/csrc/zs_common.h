@@ -170,6 +170,8 @@ struct ZsDJobDev {
   uint64_t total_out;  // compressed bytes (zs_dz_offsets_kernel)
   uint32_t check;      // CRC-32 (gzip) / Adler-32 (zlib) of the input
   uint32_t wbits;      // window bits 9..15 (match distances <= 2^wbits; zlib CINFO = wbits - 8)
+  uint64_t ck_a;       // check accumulators (zs_check.h): CRC XOR / Adler sum A (zeroed by the host)
+  uint64_t ck_b;       // Adler weighted sum B
 };
 
 struct ZsDSegDev {
