@@ -16,6 +16,8 @@ NAMES = {0: "p_waves", 1: "p_cyc_total", 2: "p_cyc_coop", 3: "p_cyc_steps", 4: "
          16: "e_blocks", 17: "e_cyc_total", 18: "e_rounds", 19: "e_jump_iters", 20: "e_cyc_jump", 21: "e_batches",
          22: "e_cyc_max", 23: "e_cyc_init", 24: "e_jump_rounds",
          40: "s_refill1", 41: "s_lit", 42: "s_refill2", 43: "s_dist", 44: "s_tail",
+         26: "d_blocks", 27: "d_cyc_total", 28: "d_cyc_hist", 29: "d_cyc_build", 30: "d_cyc_hdr", 31: "d_cyc_emit",
+         32: "d_cyc_out", 33: "d_chunks",
          48: "l_streams", 49: "l_steps", 50: "l_cyc_succ", 51: "l_cyc_walk", 52: "l_cyc_winwrite", 53: "l_cyc_resolve",
          54: "l_cyc_barrier", 55: "l_markers_sample", 56: "l_cyc_total", 57: "l_cyc_max"}
 
@@ -25,6 +27,7 @@ def main():
     ap.add_argument("--streams", type=int, default=64)
     ap.add_argument("--stream-mib", type=int, default=64)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--deflate", action="store_true", help="also run gzip L6 deflate and report the block kernel")
     a = ap.parse_args()
     import numpy as np
     import corpus
@@ -33,6 +36,12 @@ def main():
     zstreams.kprof_read(reset=True)
     res = zstreams.inflate_batch([bytes(c) for c in comps], -15, [a.stream_mib << 20] * a.streams)
     c = zstreams.kprof_read(reset=True)
+    if a.deflate:  # deflate block-kernel counters (gzip level 6 over the raw streams)
+        zstreams.deflate_batch([bytes(r) for r in raws], 31, 6)
+        cd = zstreams.kprof_read(reset=True)
+        c = list(c)
+        for i in range(26, 34):
+            c[i] = cd[i]
     if not c:
         sys.exit("no counters: ZS_LIB must point at libzstreams_mi355x_prof.so")
     ok = all(r["ret"] == 1 and bytes(o) == bytes(raws[k]) for k, (o, r) in enumerate(res))
@@ -61,6 +70,9 @@ def main():
                                  ("l_cyc_succ", "l_cyc_walk", "l_cyc_winwrite", "l_cyc_resolve", "l_cyc_barrier",
                                   "l_cyc_total")},
         "link_marker_frac_sample": d["l_markers_sample"] / max(d["l_steps"] * 16 * 32, 1),
+        "deflate_block_cycles_per_block": {k: d[k] / max(d["d_blocks"], 1) for k in
+                                           ("d_cyc_total", "d_cyc_hist", "d_cyc_build", "d_cyc_hdr", "d_cyc_emit",
+                                            "d_cyc_out", "d_chunks")},
         "step_phase_cycles_per_wave_step": {k: d[k] / max(d["p_wave_steps"], 1)
                                             for k in ("s_refill1", "s_lit", "s_refill2", "s_dist", "s_tail")},
     }

@@ -37,6 +37,14 @@
 #include "zs_common.h"
 #include "zs_device.h"
 #include "zs_check.h"
+#include "zs_kprof.h"
+
+#if KP_ON
+__device__ unsigned long long g_kprof_dz[12];  // KP_D_* - 26
+#define KPD_ADD(i, v) atomicAdd(&g_kprof_dz[(i) - 26], (unsigned long long)(v))
+#else
+#define KPD_ADD(i, v) ((void)0)
+#endif
 
 #define DZ_SEG 65536u        // input bytes per segment
 #define DZ_T 256u            // threads per workgroup
@@ -108,7 +116,7 @@ __device__ __forceinline__ uint32_t dz_dist_sym(uint32_t dist, uint32_t *xb, uin
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(DZ_T) zs_dz_match_kernel(const ZsDJobDev *__restrict__ jobs,
                                                             const ZsDSegDev *__restrict__ segs,
-                                                            uint32_t *__restrict__ matches) {
+                                                            uint16_t *__restrict__ dist16, uint8_t *__restrict__ len8) {
   __shared__ uint16_t tab[DZ_HB][DZ_WAYS];
   const uint32_t tid = threadIdx.x;
   const ZsDSegDev sg = segs[blockIdx.x];
@@ -117,7 +125,9 @@ __global__ void __launch_bounds__(DZ_T) zs_dz_match_kernel(const ZsDJobDev *__re
   gcu8 *in = (gcu8 *)jb.in;
   const uint64_t n = jb.in_len;
   const uint64_t s = sg.start, e = s + sg.len;
-  uint32_t *mo = matches + sg.tok;
+  // per position: length - 3 (4..258 -> 1..255; 0 = no match) and distance - 1
+  uint16_t *do16 = dist16 + sg.tok;
+  uint8_t *lo8 = len8 + sg.tok;
   for (uint32_t i = tid; i < DZ_HB * DZ_WAYS / 2; i += DZ_T) reinterpret_cast<uint32_t *>(tab)[i] = 0xffffffffu;
   __syncthreads();
   // Way w of a bucket belongs to wave w: the waves of a step never store to
@@ -193,7 +203,10 @@ __global__ void __launch_bounds__(DZ_T) zs_dz_match_kernel(const ZsDJobDev *__re
         }
       }
     }
-    if (p < e) mo[p - s] = best >= 3u ? ((best << 16) | (bd - 1u)) : 0u;
+    if (p < e) {  // candidates need 4 equal bytes; the segment-end clamp can leave fewer
+      lo8[p - s] = (uint8_t)(best >= 4u ? best - 3u : 0u);
+      do16[p - s] = (uint16_t)(best >= 4u ? bd - 1u : 0u);
+    }
     __syncthreads();  // every lookup of the step before its inserts
     if (p < e && p + 4 <= n) tab[h][way] = (uint16_t)p;
     __syncthreads();
@@ -201,67 +214,177 @@ __global__ void __launch_bounds__(DZ_T) zs_dz_match_kernel(const ZsDJobDev *__re
 }
 
 // ---------------------------------------------------------------------------
-// D2: lazy parse (one lane per segment), tokens written over the matches
-// (zlib deflate_slow semantics: a match is deferred by one byte when the next
-// position has a longer one and the current is shorter than max_lazy)
+// D2: lazy parse (zlib deflate_slow semantics: a match is deferred by one byte
+// when the next position has a longer one and the current is shorter than
+// max_lazy; greedy below level 4), one workgroup per segment.
+//
+// The parse is the path from position 0 under next(p), a function of m[p] and
+// m[p+1] only.  Thread i owns positions [256 i, 256 i + 256): it walks from
+// its own first position (speculation) and marks the positions it visits.
+// Paths under next() merge within a few tokens, so the exit of range i rarely
+// depends on where the true path enters it: every thread re-walks from its
+// predecessor's exit until it meets a marked position (then its speculative
+// exit holds) or leaves the range, and the rounds repeat until no exit
+// changes (usually one).  The result is two bitmaps per segment: token
+// starts (S) and match starts (T), read by the block kernel.
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(64) zs_dz_parse_kernel(const ZsDJobDev *__restrict__ jobs, ZsDSegDev *__restrict__ segs,
-                                                          uint32_t nseg, uint32_t *__restrict__ matches) {
-  const uint32_t c = blockIdx.x * 64u + threadIdx.x;
-  if (c >= nseg) return;
-  const ZsDSegDev sg = segs[c];
+typedef __attribute__((address_space(1))) const uint32_t gcu32;
+#define DZ_BMW (DZ_SEG / 32u)  // start-bitmap words per segment
+
+// next(p) over the LDS length stage (length - 3, 0 = no match)
+__device__ __forceinline__ uint32_t dz_next(const uint8_t *sl, uint32_t p, uint32_t len, uint32_t max_lazy) {
+  const uint32_t l8 = sl[p];
+  const uint32_t n8 = p + 1 < len ? sl[p + 1] : 0u;
+  const uint32_t L = l8 + 3u, NL8 = n8 + 3u;
+  return (l8 && !(L < max_lazy && n8 && NL8 > L)) ? p + L : p + 1;
+}
+
+__global__ void __launch_bounds__(DZ_T) zs_dz_parse_kernel(const ZsDJobDev *__restrict__ jobs, ZsDSegDev *__restrict__ segs,
+                                                            const uint8_t *__restrict__ len8, uint32_t *__restrict__ bm) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_len[DZ_SEG];
+  __shared__ uint32_t s_vis[DZ_BMW];  // speculative marks, then the token starts
+  __shared__ uint32_t s_ex[DZ_T];
+  const uint32_t t = threadIdx.x;
+  const ZsDSegDev sg = segs[blockIdx.x];
   const ZsDJobDev jb = jobs[sg.job];
-  uint32_t *m = matches + sg.tok;
-  const uint8_t *in = jb.in + sg.start;
+  if (jb.level == 0) return;
   const uint32_t len = sg.len;
-  uint32_t nt = 0;
-  if (jb.level == 0) {
-    segs[c].ntok = 0;
-    return;
+  {
+    const uint4 *src = reinterpret_cast<const uint4 *>(len8 + sg.tok);
+    uint4 *dst = reinterpret_cast<uint4 *>(s_len);
+    const uint32_t n16 = (len + 15u) / 16u;
+    for (uint32_t k = t; k < n16; k += DZ_T) dst[k] = src[k];
   }
   const uint32_t max_lazy = jb.level >= 4 ? 16u : 0u;
-  uint32_t p = 0;
-  uint32_t cur = len ? m[0] : 0u;
-  while (p < len) {
-    const uint32_t nxt = p + 1 < len ? m[p + 1] : 0u;
-    const uint32_t L = cur >> 16;
-    if (L >= 3u && !(L < max_lazy && (nxt >> 16) > L)) {
-      m[nt++] = cur;
-      p += L;
-      cur = p < len ? m[p] : 0u;
-    } else {
-      m[nt++] = in[p];
-      p++;
-      cur = nxt;
+  const uint32_t a = t * 256u, b = min(len, a + 256u);
+  const bool active = a < len;
+  for (uint32_t k = 0; k < 8; k++) s_vis[t * 8 + k] = 0;
+  __syncthreads();
+  // speculative walk from the range start (own bitmap words only)
+  uint32_t p = a;
+  while (p < b) {
+    s_vis[p >> 5] |= 1u << (p & 31u);
+    p = dz_next(s_len, p, len, max_lazy);
+  }
+  const uint32_t spec = active ? p : a;
+  s_ex[t] = spec;
+  __syncthreads();
+  for (;;) {
+    const uint32_t e = t == 0 ? 0u : s_ex[t - 1];
+    uint32_t r = s_ex[t];
+    if (active) {
+      uint32_t q = e;
+      r = q;
+      while (q < b) {
+        if (s_vis[q >> 5] & (1u << (q & 31u))) {
+          r = spec;
+          break;
+        }
+        q = dz_next(s_len, q, len, max_lazy);
+        r = q;
+      }
+    }
+    __syncthreads();
+    const bool changed = active && r != s_ex[t];
+    if (changed) s_ex[t] = r;
+    if (!__syncthreads_or(changed)) break;
+  }
+  // final walk from the true entry; the marks are the owner's alone, so they
+  // are cleared and reused for the token starts
+  for (uint32_t k = 0; k < 8; k++) s_vis[t * 8 + k] = 0;
+  uint32_t cnt = 0;
+  if (active) {
+    uint32_t q = t == 0 ? 0u : s_ex[t - 1];
+    while (q < b) {
+      s_vis[q >> 5] |= 1u << (q & 31u);
+      cnt++;
+      q = dz_next(s_len, q, len, max_lazy);
     }
   }
-  segs[c].ntok = nt;
+  __syncthreads();
+  uint32_t *o = bm + (uint64_t)blockIdx.x * DZ_BMW;
+  for (uint32_t k = t; k < DZ_BMW; k += DZ_T) o[k] = s_vis[k];
+  uint32_t c = cnt;  // token count: wave sums into segs[].ntok (zeroed by the host)
+  for (int off = 32; off >= 1; off >>= 1) c += __shfl_xor(c, off);
+  if ((t & 63u) == 0) atomicAdd(&segs[blockIdx.x].ntok, c);
+}
+
+// the 16 positions q0 .. q0 + 15 of one block-kernel thread: token starts
+// (S), match starts (a start whose successor position is not a start; the
+// segment end counts as a start), lengths, distances (loaded only for the
+// halves holding a match start) and literal bytes
+struct DzTok16 {
+  uint32_t s16, t16;
+  uint4 l8, lit;
+  uint4 d[2];
+};
+__device__ __forceinline__ void dz_load_tok16(DzTok16 &k, gcu32 *bS, gcu8 *l8, const uint16_t *d16, gcu8 *in, uint32_t q0,
+                                              uint32_t len) {
+  k.s16 = 0;
+  k.t16 = 0;
+  if (q0 >= len) return;
+  const uint32_t w = bS[q0 >> 5];
+  const uint32_t sh = q0 & 16u;
+  const uint32_t real = (w >> sh) & 0xffffu;  // positions >= len are 0
+  const uint32_t nb = q0 + 16u < len ? (sh ? bS[(q0 >> 5) + 1] & 1u : (w >> 16) & 1u) : 0u;
+  uint32_t s17 = real | (nb << 16);
+  if (len - q0 <= 16u) s17 |= 1u << (len - q0);  // the segment end
+  k.s16 = real;
+  k.t16 = real & ~(s17 >> 1);
+  __builtin_memcpy(&k.l8, l8 + q0, 16);
+  typedef __attribute__((address_space(1))) const uint16_t gcu16;
+  gcu16 *dp = (gcu16 *)(d16 + q0);
+  if (k.t16 & 0x00ffu) __builtin_memcpy(&k.d[0], dp, 16);
+  if (k.t16 & 0xff00u) __builtin_memcpy(&k.d[1], dp + 8, 16);
+  if (q0 + 16u <= len) {
+    k.lit = dz_load128(in + q0);
+  } else {
+    uint32_t b[4] = {0, 0, 0, 0};
+    for (uint32_t i = 0; q0 + i < len; i++) b[i >> 2] |= (uint32_t)in[q0 + i] << (8u * (i & 3u));
+    k.lit = make_uint4(b[0], b[1], b[2], b[3]);
+  }
+}
+__device__ __forceinline__ uint32_t dz_u4_byte(uint4 v, uint32_t i) {
+  const uint32_t w = i < 4 ? v.x : i < 8 ? v.y : i < 12 ? v.z : v.w;
+  return (w >> (8u * (i & 3u))) & 0xffu;
+}
+// the token word at position i: (length << 16) | (distance - 1), or the literal
+__device__ __forceinline__ uint32_t dz_tok16_at(const DzTok16 &k, uint32_t i) {
+  if ((k.t16 >> i) & 1u) {
+    const uint4 dv = k.d[i >> 3];
+    const uint32_t j = i & 7u;
+    const uint32_t w = j < 2 ? dv.x : j < 4 ? dv.y : j < 6 ? dv.z : dv.w;
+    return ((dz_u4_byte(k.l8, i) + 3u) << 16) | ((w >> (16u * (j & 1u))) & 0xffffu);
+  }
+  return dz_u4_byte(k.lit, i);
 }
 
 // ---------------------------------------------------------------------------
-// D3: Huffman codes + block emission (one workgroup per segment)
+// D3: Huffman codes and block emission (src/trees.c _tr_flush_block 931-1023),
+// three kernels:
+//   zs_dz_hist_kernel   one workgroup per segment: symbol histograms, extra
+//                       bits and the fixed-code cost;
+//   zs_dz_codes_kernel  one THREAD per segment: the serial code build (sort,
+//                       two-queue Huffman, length limit, canonical codes),
+//                       header RLE and code-length code, the dynamic / fixed
+//                       choice and the header bits.  Every segment builds at
+//                       once (scratch rows laid out SoA in HBM, so a wave's
+//                       accesses coalesce), instead of one thread per
+//                       workgroup holding a CU's LDS;
+//   zs_dz_emit_kernel   one workgroup per segment: token bits at scanned
+//                       offsets, atomicOr-packed into a 16 KiB LDS ring that
+//                       is flushed to the segment's output after every chunk.
 // ---------------------------------------------------------------------------
 #define NL 286
 #define ND 30
 #define NC 19
-
-struct DzLDS {
-  union {
-    uint32_t out[DZ_OUTW];     // block bits (LSB-first), atomicOr-packed (zeroed after the code builds)
-    struct {                   // code-build scratch, dead before out is used
-      uint16_t order[NL + 2];  // symbols by (freq, symbol)
-      uint32_t w[2 * (NL + 2)];
-      uint16_t par[2 * (NL + 2)];
-      uint8_t depth[2 * (NL + 2)];
-    };
-  };
-  uint32_t fl[NL + 2], fd[ND + 2], fc[NC + 1];
-  uint32_t cl[NL + 2], cd[ND + 2], cc[NC + 1];  // code | len << 16 (code bit-reversed)
-  uint8_t lens[NL + ND + 4]; // concatenated lit + dist lengths for the header
-  uint16_t rle[NL + ND + 4]; // header symbols: sym | extra << 8
-  uint32_t scan[DZ_T / WAVE + 1];
-  uint32_t misc[16];
-};
+#define DZ_HROWS 320u  // histogram rows per segment (SoA): lit/len 0..285, dist 286..315, extra bits 316, fixed bits 317
+#define DZ_CROW 320u   // code words per segment (AoS): lit/len 0..285, dist 286..315 (code | len << 16, code bit-reversed)
+#define DZ_HDRW 192u   // header words per segment (AoS); word 191 = header bit count
+#define DZ_SCR 2400u   // build scratch rows per segment (SoA)
+#define DZ_AUXW (DZ_HROWS + DZ_CROW + DZ_HDRW + DZ_SCR)  // aux words per segment
+#define DZ_RING 4096u  // emit ring words (16 KiB); a chunk emits <= 4096 x 15 bits
+typedef __attribute__((address_space(1))) uint32_t gu32;
 
 __device__ __forceinline__ uint32_t dz_scan_excl(uint32_t v, uint32_t *s_tmp, uint32_t *total) {
   const uint32_t t = threadIdx.x, lane = t & (WAVE - 1), wv = t / WAVE;
@@ -283,110 +406,6 @@ __device__ __forceinline__ uint32_t dz_scan_excl(uint32_t v, uint32_t *s_tmp, ui
   __syncthreads();
   *total = all;
   return before + x - v;
-}
-
-// Length-limited Huffman code lengths for freq[0..n) (every used symbol gets a
-// length 1..maxbits; at least two symbols are forced used, as trees.c:610-620
-// does, so every code is complete), then canonical codes (gen_codes,
-// trees.c:205) bit-reversed for LSB-first output.  Whole workgroup.
-__device__ void dz_build_code(DzLDS &L, uint32_t *freq, uint32_t n, uint32_t maxbits, uint32_t *codes) {
-  const uint32_t t = threadIdx.x;
-  if (t == 0) {
-    uint32_t used = 0;
-    for (uint32_t i = 0; i < n; i++) used += freq[i] != 0;
-    for (uint32_t i = 0; used < 2 && i < n; i++)
-      if (freq[i] == 0) {
-        freq[i] = 1;
-        used++;
-      }
-  }
-  __syncthreads();
-  // rank sort of the used symbols by (freq, symbol)
-  uint32_t nu = 0;
-  for (uint32_t i = 0; i < n; i++) nu += freq[i] != 0;
-  for (uint32_t i = t; i < n; i += DZ_T) {
-    const uint32_t f = freq[i];
-    if (!f) continue;
-    uint32_t r = 0;
-    for (uint32_t j = 0; j < n; j++) {
-      const uint32_t g = freq[j];
-      r += (g != 0) && (g < f || (g == f && j < i));
-    }
-    L.order[r] = (uint16_t)i;
-  }
-  __syncthreads();
-  if (t == 0) {
-    // two-queue Huffman: leaves 0..nu-1 (sorted), internal nodes nu.. in order
-    for (uint32_t i = 0; i < nu; i++) L.w[i] = freq[L.order[i]];
-    uint32_t li = 0, ii = nu, in_end = nu;
-    for (uint32_t k = 0; k + 1 < nu; k++) {
-      uint32_t a, b;
-      for (int pick = 0; pick < 2; pick++) {
-        uint32_t x;
-        if (li < nu && (ii >= in_end || L.w[li] <= L.w[ii])) x = li++;
-        else x = ii++;
-        if (pick == 0) a = x;
-        else b = x;
-      }
-      L.w[in_end] = L.w[a] + L.w[b];
-      L.par[a] = (uint16_t)in_end;
-      L.par[b] = (uint16_t)in_end;
-      in_end++;
-    }
-    // depths: root = in_end - 1
-    const uint32_t root = in_end - 1;
-    L.depth[root] = 0;
-    for (int x = (int)root - 1; x >= 0; x--) L.depth[x] = (uint8_t)min(255u, L.depth[L.par[x]] + 1u);
-    uint32_t count[32];
-    for (int b = 0; b < 32; b++) count[b] = 0;
-    uint32_t maxd = 0;
-    for (uint32_t i = 0; i < nu; i++) {
-      const uint32_t d = min(31u, (uint32_t)L.depth[i]);
-      count[d]++;
-      maxd = max(maxd, d);
-    }
-    // limit to maxbits (bl_count adjustment; cf. gen_bitlen overflow, trees.c:474-559)
-    for (uint32_t i = maxd; i > maxbits; i--) {
-      while (count[i] > 0) {
-        uint32_t j = i - 2;
-        while (count[j] == 0) j--;
-        count[i] -= 2;
-        count[i - 1] += 1;
-        count[j + 1] += 2;
-        count[j] -= 1;
-      }
-    }
-    // least frequent symbols get the longest codes
-    uint32_t k = 0;
-    for (uint32_t b = min(maxd, maxbits); b >= 1; b--)
-      for (uint32_t c = 0; c < count[b]; c++) codes[L.order[k++]] = b << 16;
-    for (uint32_t i = 0; i < n; i++)
-      if (freq[i] == 0) codes[i] = 0;
-    // canonical codes
-    uint32_t bl[16];
-    for (int b = 0; b < 16; b++) bl[b] = 0;
-    for (uint32_t i = 0; i < n; i++) bl[codes[i] >> 16]++;
-    bl[0] = 0;
-    uint32_t nextc[16], code = 0;
-    for (int b = 1; b < 16; b++) {
-      code = (code + bl[b - 1]) << 1;
-      nextc[b] = code;
-    }
-    for (uint32_t i = 0; i < n; i++) {
-      const uint32_t len = codes[i] >> 16;
-      if (!len) continue;
-      const uint32_t cv = nextc[len]++;
-      codes[i] = (len << 16) | (__builtin_bitreverse32(cv) >> (32 - len));
-    }
-  }
-  __syncthreads();
-}
-
-__device__ __forceinline__ void dz_put(uint32_t *out, uint32_t bit, uint32_t v, uint32_t nb) {  // nb <= 32
-  if (!nb) return;
-  const uint64_t x = (uint64_t)(v & (nb == 32 ? 0xffffffffu : ((1u << nb) - 1u))) << (bit & 31);
-  atomicOr(&out[bit >> 5], (uint32_t)x);
-  if ((bit & 31) + nb > 32) atomicOr(&out[(bit >> 5) + 1], (uint32_t)(x >> 32));
 }
 
 __device__ __forceinline__ uint32_t dz_tok_bits(uint32_t tk, const uint32_t *cl, const uint32_t *cd, uint32_t *v0,
@@ -412,14 +431,327 @@ __device__ __forceinline__ uint32_t dz_tok_bits(uint32_t tk, const uint32_t *cl,
   return *n0 + *n1;
 }
 
-__global__ void __launch_bounds__(DZ_T) zs_dz_block_kernel(const ZsDJobDev *__restrict__ jobs, ZsDSegDev *__restrict__ segs,
-                                                            const uint32_t *__restrict__ tokens, uint32_t *__restrict__ obuf) {
-  __shared__ DzLDS L;
+__device__ __forceinline__ void dz_put_ring(uint32_t *ring, uint32_t bit, uint32_t v, uint32_t nb) {  // nb <= 32
+  if (!nb) return;
+  const uint64_t x = (uint64_t)(v & (nb == 32 ? 0xffffffffu : ((1u << nb) - 1u))) << (bit & 31);
+  const uint32_t w = bit >> 5;
+  atomicOr(&ring[w & (DZ_RING - 1)], (uint32_t)x);
+  if ((bit & 31) + nb > 32) atomicOr(&ring[(w + 1) & (DZ_RING - 1)], (uint32_t)(x >> 32));
+}
+
+// D3a: histograms
+__global__ void __launch_bounds__(DZ_T) zs_dz_hist_kernel(const ZsDJobDev *__restrict__ jobs, const ZsDSegDev *__restrict__ segs,
+                                                           uint32_t nseg, const uint16_t *__restrict__ dist16,
+                                                           const uint8_t *__restrict__ len8, const uint32_t *__restrict__ bm,
+                                                           uint32_t *__restrict__ hist) {
+  __shared__ uint32_t fl[NL + 2], fd[ND + 2];
+  __shared__ uint64_t s_red[16];
   const uint32_t t = threadIdx.x;
   const ZsDSegDev sg = segs[blockIdx.x];
   const ZsDJobDev jb = jobs[sg.job];
-  const uint32_t *tk = tokens + sg.tok;
-  const uint32_t nt = sg.ntok;
+  if (jb.level == 0) return;
+  gcu8 *l8 = (gcu8 *)(len8 + sg.tok);
+  const uint16_t *d16 = dist16 + sg.tok;
+  gcu8 *in = (gcu8 *)(jb.in + sg.start);
+  gcu32 *bS = (gcu32 *)(bm + (uint64_t)blockIdx.x * DZ_BMW);
+  const uint32_t nch = (sg.len + 4095u) / 4096u;
+  for (uint32_t i = t; i < NL + 2; i += DZ_T) fl[i] = 0;
+  if (t < ND + 2) fd[t] = 0;
+  __syncthreads();
+  uint32_t xbits = 0, fix = 0;  // length/distance extra bits; fixed-code cost
+  for (uint32_t c = 0; c < nch; c++) {
+    DzTok16 k;
+    dz_load_tok16(k, bS, l8, d16, in, c * 4096u + 16u * t, sg.len);
+#pragma unroll
+    for (uint32_t i = 0; i < 16; i++) {
+      if (!((k.s16 >> i) & 1u)) continue;
+      const uint32_t x = dz_tok16_at(k, i);
+      if ((x >> 16) == 0) {
+        atomicAdd(&fl[x], 1u);
+        fix += x < 144u ? 8u : 9u;
+      } else {
+        uint32_t lx, lv, dx, dv;
+        const uint32_t ls = dz_len_sym(x >> 16, &lx, &lv);
+        atomicAdd(&fl[257 + ls], 1u);
+        atomicAdd(&fd[dz_dist_sym((x & 0xffffu) + 1u, &dx, &dv)], 1u);
+        xbits += lx + dx;
+        fix += (257u + ls < 280u ? 7u : 8u) + lx + 5u + dx;
+      }
+    }
+  }
+  const uint64_t xs = zs_block_sum(xbits, s_red);
+  const uint64_t fs = zs_block_sum(fix, s_red);
+  gu32 *h = (gu32 *)hist + blockIdx.x;  // row r at h[r * nseg]
+  for (uint32_t i = t; i < NL; i += DZ_T) h[(uint64_t)i * nseg] = i == 256 ? 1u : fl[i];  // one end-of-block
+  if (t < ND) h[(uint64_t)(NL + t) * nseg] = fd[t];
+  if (t == 0) {
+    h[(uint64_t)316 * nseg] = (uint32_t)xs;
+    h[(uint64_t)317 * nseg] = (uint32_t)fs;
+  }
+}
+
+// D3b: one thread per segment
+struct DzRows {  // SoA rows of one segment
+  gu32 *b;
+  uint64_t stride;
+  __device__ __forceinline__ gu32 &operator[](uint32_t r) const { return b[(uint64_t)r * stride]; }
+};
+#define DZS_KEY 0u
+#define DZS_TMP 288u
+#define DZS_W 576u
+#define DZS_P 1152u
+#define DZS_LEN 1728u  // lit/len 1728..2013, dist 2014..2043, code-length 2044..2062
+#define DZS_RLE 2064u  // header symbols: sym | extra << 8
+
+// Code lengths (1..maxbits, 0 = unused) of the n frequencies freq(i) into
+// scratch rows LEN0 .. LEN0 + n: at least two symbols used (trees.c:610-620),
+// leaves sorted by (freq, symbol), two-queue Huffman, depth limit by the
+// bl_count adjustment (cf. gen_bitlen, trees.c:474-559), longest codes to the
+// least frequent symbols.  cnt: 32 words of LDS.
+template <typename F>
+__device__ void dz_huff_lengths(const DzRows &S, F freq, uint32_t n, uint32_t maxbits, uint32_t len0, uint32_t *cnt) {
+  uint32_t m = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    const uint32_t f = freq(i);
+    S[len0 + i] = 0;
+    if (f) S[DZS_KEY + m++] = (f << 9) | i;
+  }
+  for (uint32_t i = 0; m < 2 && i < n; i++)
+    if (!freq(i)) S[DZS_KEY + m++] = (1u << 9) | i;
+  // bottom-up merge sort of the keys (unique: the symbol is in the low bits)
+  uint32_t src = DZS_KEY, dst = DZS_TMP;
+  for (uint32_t w = 1; w < m; w <<= 1) {
+    for (uint32_t lo = 0; lo < m; lo += 2 * w) {
+      const uint32_t mid = min(lo + w, m), hi = min(lo + 2 * w, m);
+      uint32_t i = lo, j = mid;
+      uint32_t a = i < mid ? S[src + i] : 0xffffffffu, b = j < hi ? S[src + j] : 0xffffffffu;
+      for (uint32_t k = lo; k < hi; k++) {
+        if (a <= b) {
+          S[dst + k] = a;
+          i++;
+          a = i < mid ? S[src + i] : 0xffffffffu;
+        } else {
+          S[dst + k] = b;
+          j++;
+          b = j < hi ? S[src + j] : 0xffffffffu;
+        }
+      }
+    }
+    const uint32_t x = src;
+    src = dst;
+    dst = x;
+  }
+  // two-queue Huffman: leaves 0..m-1 (sorted weights), internal nodes from m
+  for (uint32_t i = 0; i < m; i++) S[DZS_W + i] = S[src + i] >> 9;
+  uint32_t li = 0, ii = m, end = m;
+  uint32_t wl = S[DZS_W], wi = 0;
+  for (uint32_t k = 0; k + 1 < m; k++) {
+    uint32_t x[2], wx[2];
+    for (int q = 0; q < 2; q++) {
+      if (li < m && (ii >= end || wl <= wi)) {
+        x[q] = li;
+        wx[q] = wl;
+        li++;
+        wl = li < m ? S[DZS_W + li] : 0u;
+      } else {
+        x[q] = ii;
+        wx[q] = wi;
+        ii++;
+        wi = ii < end ? S[DZS_W + ii] : 0u;
+      }
+    }
+    const uint32_t sum = wx[0] + wx[1];
+    S[DZS_W + end] = sum;
+    S[DZS_P + x[0]] = end;
+    S[DZS_P + x[1]] = end;
+    if (ii == end) wi = sum;
+    end++;
+  }
+  // depths (parents have higher indices); W is reused for them
+  const uint32_t root = end - 1;
+  S[DZS_W + root] = 0;
+  for (uint32_t x = root; x-- > 0;) S[DZS_W + x] = min(31u, S[DZS_W + S[DZS_P + x]] + 1u);
+  for (uint32_t b = 0; b < 32; b++) cnt[b] = 0;
+  uint32_t maxd = 0;
+  for (uint32_t i = 0; i < m; i++) {
+    const uint32_t d = S[DZS_W + i];
+    cnt[d]++;
+    maxd = max(maxd, d);
+  }
+  for (uint32_t i = maxd; i > maxbits; i--) {
+    while (cnt[i] > 0) {
+      uint32_t j = i - 2;
+      while (cnt[j] == 0) j--;
+      cnt[i] -= 2;
+      cnt[i - 1] += 1;
+      cnt[j + 1] += 2;
+      cnt[j] -= 1;
+    }
+  }
+  uint32_t k = 0;
+  for (uint32_t b = min(maxd, maxbits); b >= 1; b--)
+    for (uint32_t c = 0; c < cnt[b]; c++) S[len0 + (S[src + k++] & 511u)] = b;
+}
+
+// canonical codes (gen_codes, trees.c:205) of lengths len(i), bit-reversed for
+// LSB-first output; put(i, code | len << 16).  bl: 16 words of LDS.
+template <typename L, typename P>
+__device__ void dz_canonical(L len, P put, uint32_t n, uint32_t *bl) {
+  for (uint32_t b = 0; b < 16; b++) bl[b] = 0;
+  for (uint32_t i = 0; i < n; i++) bl[len(i)]++;
+  bl[0] = 0;
+  uint32_t code = 0, prev = 0;
+  for (uint32_t b = 1; b < 16; b++) {
+    code = (code + prev) << 1;
+    prev = bl[b];
+    bl[b] = code;  // next code of length b
+  }
+  for (uint32_t i = 0; i < n; i++) {
+    const uint32_t l = len(i);
+    if (!l) {
+      put(i, 0u);
+      continue;
+    }
+    const uint32_t cv = bl[l]++;
+    put(i, (l << 16) | (__builtin_bitreverse32(cv) >> (32 - l)));
+  }
+}
+
+struct DzBitW {  // LSB-first bit writer into global words
+  gu32 *o;
+  uint64_t acc;
+  uint32_t n, w;
+  __device__ __forceinline__ void put(uint32_t v, uint32_t nb) {
+    acc |= (uint64_t)(v & ((1u << nb) - 1u)) << n;
+    n += nb;
+    if (n >= 32) {
+      o[w++] = (uint32_t)acc;
+      acc >>= 32;
+      n -= 32;
+    }
+  }
+  __device__ __forceinline__ uint32_t flush() {
+    const uint32_t bits = w * 32u + n;
+    if (n) o[w] = (uint32_t)acc;
+    return bits;
+  }
+};
+
+__global__ void __launch_bounds__(WAVE) zs_dz_codes_kernel(const ZsDJobDev *__restrict__ jobs, const ZsDSegDev *__restrict__ segs,
+                                                            uint32_t nseg, uint32_t *__restrict__ aux) {
+  __shared__ uint32_t s_cnt[WAVE][32];
+  __shared__ uint32_t s_bl[WAVE][16];
+  __shared__ uint32_t s_fc[WAVE][20];
+  __shared__ uint32_t s_cc[WAVE][20];
+  const uint32_t s = blockIdx.x * WAVE + threadIdx.x;
+  if (s >= nseg) return;
+  const ZsDSegDev sg = segs[s];
+  const ZsDJobDev jb = jobs[sg.job];
+  if (jb.level == 0) return;
+  const uint32_t lane = threadIdx.x;
+  gu32 *A = (gu32 *)aux;
+  const DzRows H{A + s, nseg};                                              // histograms
+  gu32 *C = A + (uint64_t)DZ_HROWS * nseg + (uint64_t)s * DZ_CROW;          // codes (AoS)
+  gu32 *HB = A + (uint64_t)(DZ_HROWS + DZ_CROW) * nseg + (uint64_t)s * DZ_HDRW;  // header bits (AoS)
+  const DzRows S{A + (uint64_t)(DZ_HROWS + DZ_CROW + DZ_HDRW) * nseg + s, nseg};  // scratch
+  uint32_t *cnt = s_cnt[lane], *bl = s_bl[lane], *fc = s_fc[lane], *cc = s_cc[lane];
+  dz_huff_lengths(S, [&](uint32_t i) -> uint32_t { return H[i]; }, NL, 15, DZS_LEN, cnt);
+  dz_huff_lengths(S, [&](uint32_t i) -> uint32_t { return H[NL + i]; }, ND, 15, DZS_LEN + NL, cnt);
+  // header: lengths RLE (scan_tree / send_tree, trees.c:682-766)
+  uint32_t hlit = NL;
+  while (hlit > 257 && S[DZS_LEN + hlit - 1] == 0) hlit--;
+  uint32_t hdist = ND;
+  while (hdist > 1 && S[DZS_LEN + NL + hdist - 1] == 0) hdist--;
+  const uint32_t tot = hlit + hdist;
+  auto lenat = [&](uint32_t i) -> uint32_t { return i < hlit ? S[DZS_LEN + i] : S[DZS_LEN + NL + (i - hlit)]; };
+  for (uint32_t i = 0; i < 20; i++) fc[i] = 0;
+  uint32_t nr = 0;
+  for (uint32_t i = 0; i < tot;) {
+    const uint32_t v = lenat(i);
+    uint32_t r = 1;
+    while (i + r < tot && r < 138 && lenat(i + r) == v) r++;
+    if (v == 0 && r >= 3) {
+      const uint32_t sym = r >= 11 ? 18u : 17u;
+      S[DZS_RLE + nr++] = sym | ((r - (sym == 18 ? 11u : 3u)) << 8);
+      fc[sym]++;
+      i += r;
+    } else if (v != 0 && r >= 4) {
+      S[DZS_RLE + nr++] = v;
+      fc[v]++;
+      uint32_t rem = r - 1;
+      i += 1;
+      while (rem >= 3) {
+        const uint32_t q = min(rem, 6u);
+        S[DZS_RLE + nr++] = 16u | ((q - 3u) << 8);
+        fc[16]++;
+        rem -= q;
+        i += q;
+      }
+    } else {
+      S[DZS_RLE + nr++] = v;
+      fc[v]++;
+      i++;
+    }
+  }
+  dz_huff_lengths(S, [&](uint32_t i) -> uint32_t { return fc[i]; }, NC, 7, DZS_LEN + NL + ND, cnt);
+  dz_canonical([&](uint32_t i) -> uint32_t { return S[DZS_LEN + NL + ND + i]; }, [&](uint32_t i, uint32_t c) { cc[i] = c; },
+               NC, bl);
+  static constexpr uint8_t ordr[NC] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+  uint32_t hclen = NC;
+  while (hclen > 4 && (cc[ordr[hclen - 1]] >> 16) == 0) hclen--;
+  uint32_t hb = 3 + 5 + 5 + 4 + 3 * hclen;
+  for (uint32_t i = 0; i < nr; i++) {
+    const uint32_t sym = S[DZS_RLE + i] & 0xffu;
+    hb += (cc[sym] >> 16) + (sym == 16 ? 2u : sym == 17 ? 3u : sym == 18 ? 7u : 0u);
+  }
+  uint64_t dyn = (uint64_t)hb + H[316];
+  for (uint32_t i = 0; i < NL; i++) dyn += (uint64_t)H[i] * S[DZS_LEN + i];
+  for (uint32_t i = 0; i < ND; i++) dyn += (uint64_t)H[NL + i] * S[DZS_LEN + NL + i];
+  const uint64_t fix = 3ull + H[317] + 7ull;
+  DzBitW bw{HB, 0, 0, 0};
+  bw.put(sg.last ? 1u : 0u, 1);
+  if (dyn < fix) {
+    dz_canonical([&](uint32_t i) -> uint32_t { return S[DZS_LEN + i]; }, [&](uint32_t i, uint32_t c) { C[i] = c; }, NL, bl);
+    dz_canonical([&](uint32_t i) -> uint32_t { return S[DZS_LEN + NL + i]; }, [&](uint32_t i, uint32_t c) { C[NL + i] = c; },
+                 ND, bl);
+    bw.put(2u, 2);
+    bw.put(hlit - 257u, 5);
+    bw.put(hdist - 1u, 5);
+    bw.put(hclen - 4u, 4);
+    for (uint32_t i = 0; i < hclen; i++) bw.put(cc[ordr[i]] >> 16, 3);
+    for (uint32_t i = 0; i < nr; i++) {
+      const uint32_t e = S[DZS_RLE + i];
+      const uint32_t sym = e & 0xffu, c = cc[sym];
+      bw.put(c & 0xffffu, c >> 16);
+      const uint32_t xb = sym == 16 ? 2u : sym == 17 ? 3u : sym == 18 ? 7u : 0u;
+      if (xb) bw.put(e >> 8, xb);
+    }
+  } else {
+    // fixed codes (src/trees.c tr_static_init): lit 0-143 8 bits from 0x30,
+    // 144-255 9 bits from 0x190, 256-279 7 bits from 0, 280-287 8 bits from
+    // 0xc0; distances 5 bits
+    for (uint32_t i = 0; i < NL; i++) {
+      const uint32_t len = i < 144 ? 8u : i < 256 ? 9u : i < 280 ? 7u : 8u;
+      const uint32_t code = i < 144 ? 0x30u + i : i < 256 ? 0x190u + (i - 144u) : i < 280 ? i - 256u : 0xc0u + (i - 280u);
+      C[i] = (len << 16) | (__builtin_bitreverse32(code) >> (32 - len));
+    }
+    for (uint32_t i = 0; i < ND; i++) C[NL + i] = (5u << 16) | (__builtin_bitreverse32(i) >> 27);
+    bw.put(1u, 2);
+  }
+  HB[DZ_HDRW - 1] = bw.flush();
+}
+
+// D3c: emission
+__global__ void __launch_bounds__(DZ_T) zs_dz_emit_kernel(const ZsDJobDev *__restrict__ jobs, ZsDSegDev *__restrict__ segs,
+                                                           uint32_t nseg, const uint16_t *__restrict__ dist16,
+                                                           const uint8_t *__restrict__ len8, const uint32_t *__restrict__ bm,
+                                                           const uint32_t *__restrict__ aux, uint32_t *__restrict__ obuf) {
+  __shared__ uint32_t ring[DZ_RING];
+  __shared__ uint32_t s_cl[NL + 2], s_cd[ND + 2];
+  __shared__ uint32_t s_scan[DZ_T / WAVE + 1];
+  const uint32_t t = threadIdx.x;
+  const ZsDSegDev sg = segs[blockIdx.x];
+  const ZsDJobDev jb = jobs[sg.job];
   uint32_t *gout = obuf + sg.obuf / 4;
   const uint32_t last = sg.last;
   if (jb.level == 0) {  // stored blocks of <= 65535 bytes, byte-aligned (every block is stored)
@@ -442,174 +774,58 @@ __global__ void __launch_bounds__(DZ_T) zs_dz_block_kernel(const ZsDJobDev *__re
     if (t == 0) segs[blockIdx.x].nbits = 8u * (n + 5u * nblk);
     return;
   }
-  for (uint32_t i = t; i < NL + 2; i += DZ_T) L.fl[i] = 0;
-  if (t < ND + 2) L.fd[t] = 0;
-  if (t < NC + 1) L.fc[t] = 0;
+  const uint32_t *C = aux + (uint64_t)DZ_HROWS * nseg + (uint64_t)blockIdx.x * DZ_CROW;
+  const uint32_t *HB = aux + (uint64_t)(DZ_HROWS + DZ_CROW) * nseg + (uint64_t)blockIdx.x * DZ_HDRW;
+  const uint32_t hbits = HB[DZ_HDRW - 1];
+  for (uint32_t i = t; i < NL; i += DZ_T) s_cl[i] = C[i];
+  if (t < ND) s_cd[t] = C[NL + t];
+  for (uint32_t i = t; i < DZ_RING; i += DZ_T) ring[i] = i < (hbits + 31u) / 32u ? HB[i] : 0u;
   __syncthreads();
-  for (uint32_t i = t; i < nt; i += DZ_T) {
-    const uint32_t x = tk[i];
-    if ((x >> 16) == 0) {
-      atomicAdd(&L.fl[x & 0xffu], 1u);
-    } else {
-      uint32_t a, b;
-      atomicAdd(&L.fl[257 + dz_len_sym(x >> 16, &a, &b)], 1u);
-      atomicAdd(&L.fd[dz_dist_sym((x & 0xffffu) + 1u, &a, &b)], 1u);
+  gcu8 *l8 = (gcu8 *)(len8 + sg.tok);
+  const uint16_t *d16 = dist16 + sg.tok;
+  gcu8 *in = (gcu8 *)(jb.in + sg.start);
+  gcu32 *bS = (gcu32 *)(bm + (uint64_t)blockIdx.x * DZ_BMW);
+  const uint32_t nch = (sg.len + 4095u) / 4096u;
+  uint32_t base = hbits, flushed = 0;  // bits emitted; words written to gout
+  for (uint32_t c = 0; c < nch; c++) {
+    DzTok16 k;
+    dz_load_tok16(k, bS, l8, d16, in, c * 4096u + 16u * t, sg.len);
+    uint32_t nb = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 16; i++) {
+      if (!((k.s16 >> i) & 1u)) continue;
+      uint32_t v0, n0, v1, n1;
+      nb += dz_tok_bits(dz_tok16_at(k, i), s_cl, s_cd, &v0, &n0, &v1, &n1);
     }
-  }
-  if (t == 0) L.fl[256] = 1;
-  __syncthreads();
-  // fixed-code cost (src/trees.c static_ltree / static_dtree) vs dynamic
-  dz_build_code(L, L.fl, NL, 15, L.cl);
-  dz_build_code(L, L.fd, ND, 15, L.cd);
-  // dynamic header: lengths RLE (send_tree/scan_tree, trees.c:682-766)
-  if (t == 0) {
-    uint32_t hlit = NL;
-    while (hlit > 257 && (L.cl[hlit - 1] >> 16) == 0) hlit--;
-    uint32_t hdist = ND;
-    while (hdist > 1 && (L.cd[hdist - 1] >> 16) == 0) hdist--;
-    const uint32_t tot = hlit + hdist;
-    for (uint32_t i = 0; i < hlit; i++) L.lens[i] = (uint8_t)(L.cl[i] >> 16);
-    for (uint32_t i = 0; i < hdist; i++) L.lens[hlit + i] = (uint8_t)(L.cd[i] >> 16);
-    uint32_t nr = 0;
-    for (uint32_t i = 0; i < tot;) {
-      const uint32_t v = L.lens[i];
-      uint32_t r = 1;
-      while (i + r < tot && L.lens[i + r] == v) r++;
-      if (v == 0 && r >= 3) {
-        const uint32_t k = min(r, 138u);
-        if (k >= 11) L.rle[nr++] = (uint16_t)(18 | ((k - 11) << 8));
-        else L.rle[nr++] = (uint16_t)(17 | ((k - 3) << 8));
-        i += k;
-      } else if (v != 0 && r >= 4) {
-        L.rle[nr++] = (uint16_t)v;
-        uint32_t rem = r - 1, used = 1;
-        while (rem >= 3) {
-          const uint32_t k = min(rem, 6u);
-          L.rle[nr++] = (uint16_t)(16 | ((k - 3) << 8));
-          rem -= k;
-          used += k;
-        }
-        i += used;
-      } else {
-        L.rle[nr++] = (uint16_t)v;
-        i++;
-      }
-    }
-    for (uint32_t i = 0; i < nr; i++) L.fc[L.rle[i] & 0xffu]++;
-    L.misc[0] = hlit;
-    L.misc[1] = hdist;
-    L.misc[2] = nr;
-  }
-  __syncthreads();
-  dz_build_code(L, L.fc, NC, 7, L.cc);
-  for (uint32_t i = t; i < DZ_OUTW; i += DZ_T) L.out[i] = 0;
-  __syncthreads();
-  // sizes
-  uint32_t dyn_tok = 0, fix_tok = 0;
-  for (uint32_t i = t; i < nt; i += DZ_T) {
-    const uint32_t x = tk[i];
-    uint32_t a, b, c, d;
-    dyn_tok += dz_tok_bits(x, L.cl, L.cd, &a, &b, &c, &d);
-    if ((x >> 16) == 0) {
-      fix_tok += (x & 0xffu) < 144u ? 8u : 9u;
-    } else {
-      uint32_t lx, lv, dx, dv;
-      const uint32_t ls = dz_len_sym(x >> 16, &lx, &lv);
-      dz_dist_sym((x & 0xffffu) + 1u, &dx, &dv);
-      fix_tok += (257u + ls < 280u ? 7u : 8u) + lx + 5u + dx;
-    }
-  }
-  uint32_t dyn_all, fix_all;
-  dz_scan_excl(dyn_tok, L.scan, &dyn_all);
-  dz_scan_excl(fix_tok, L.scan, &fix_all);
-  __shared__ uint32_t s_hdr_bits, s_dynamic;
-  if (t == 0) {
-    static const uint8_t ordr[NC] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
-    uint32_t hclen = NC;
-    while (hclen > 4 && (L.cc[ordr[hclen - 1]] >> 16) == 0) hclen--;
-    uint32_t hb = 3 + 5 + 5 + 4 + 3 * hclen;
-    for (uint32_t i = 0; i < L.misc[2]; i++) {
-      const uint32_t sym = L.rle[i] & 0xffu;
-      hb += (L.cc[sym] >> 16) + (sym == 16 ? 2u : sym == 17 ? 3u : sym == 18 ? 7u : 0u);
-    }
-    const uint64_t dyn = (uint64_t)hb + dyn_all + (L.cl[256] >> 16);
-    const uint64_t fix = 3ull + fix_all + 7ull;
-    s_dynamic = dyn < fix;
-    // block header + (dynamic) code description
-    uint32_t bit = 0;
-    dz_put(L.out, bit, last ? 1u : 0u, 1);
-    bit += 1;
-    if (s_dynamic) {
-      dz_put(L.out, bit, 2u, 2);
-      bit += 2;
-      dz_put(L.out, bit, L.misc[0] - 257u, 5);
-      bit += 5;
-      dz_put(L.out, bit, L.misc[1] - 1u, 5);
-      bit += 5;
-      dz_put(L.out, bit, hclen - 4u, 4);
-      bit += 4;
-      for (uint32_t i = 0; i < hclen; i++) {
-        dz_put(L.out, bit, L.cc[ordr[i]] >> 16, 3);
-        bit += 3;
-      }
-      for (uint32_t i = 0; i < L.misc[2]; i++) {
-        const uint32_t sym = L.rle[i] & 0xffu, xv = L.rle[i] >> 8;
-        const uint32_t c = L.cc[sym];
-        dz_put(L.out, bit, c & 0xffffu, c >> 16);
-        bit += c >> 16;
-        const uint32_t xb = sym == 16 ? 2u : sym == 17 ? 3u : sym == 18 ? 7u : 0u;
-        dz_put(L.out, bit, xv, xb);
-        bit += xb;
-      }
-    } else {
-      dz_put(L.out, bit, 1u, 2);
-      bit += 2;
-      // fixed codes (src/trees.c tr_static_init): lit 0-143: 8 bits 0x30+, 144-255: 9 bits
-      // 0x190+, 256-279: 7 bits 0+, 280-287: 8 bits 0xc0+; distances 5 bits
-      for (uint32_t i = 0; i < NL; i++) {
-        uint32_t len, code;
-        if (i < 144) {
-          len = 8;
-          code = 0x30 + i;
-        } else if (i < 256) {
-          len = 9;
-          code = 0x190 + (i - 144);
-        } else if (i < 280) {
-          len = 7;
-          code = i - 256;
-        } else {
-          len = 8;
-          code = 0xc0 + (i - 280);
-        }
-        L.cl[i] = (len << 16) | (__builtin_bitreverse32(code) >> (32 - len));
-      }
-      for (uint32_t i = 0; i < ND; i++) L.cd[i] = (5u << 16) | (__builtin_bitreverse32(i) >> 27);
-    }
-    s_hdr_bits = bit;
-  }
-  __syncthreads();
-  // tokens: bit offsets by a block scan over 256-token batches
-  uint32_t base = s_hdr_bits;
-  for (uint32_t b0 = 0; b0 < nt; b0 += DZ_T) {
-    const uint32_t i = b0 + t;
-    uint32_t v0 = 0, n0 = 0, v1 = 0, n1 = 0, nb = 0;
-    if (i < nt) nb = dz_tok_bits(tk[i], L.cl, L.cd, &v0, &n0, &v1, &n1);
     uint32_t all;
-    const uint32_t off = dz_scan_excl(nb, L.scan, &all) + base;
-    if (i < nt) {
-      dz_put(L.out, off, v0, n0);
-      dz_put(L.out, off + n0, v1, n1);
+    uint32_t off = dz_scan_excl(nb, s_scan, &all) + base;
+#pragma unroll
+    for (uint32_t i = 0; i < 16; i++) {
+      if (!((k.s16 >> i) & 1u)) continue;
+      uint32_t v0, n0, v1, n1;
+      dz_tok_bits(dz_tok16_at(k, i), s_cl, s_cd, &v0, &n0, &v1, &n1);
+      dz_put_ring(ring, off, v0, n0);
+      dz_put_ring(ring, off + n0, v1, n1);
+      off += n0 + n1;
     }
     base += all;
+    __syncthreads();
+    const uint32_t full = base >> 5;  // words complete after this chunk
+    for (uint32_t w = flushed + t; w < full; w += DZ_T) {
+      gout[w] = ring[w & (DZ_RING - 1)];
+      ring[w & (DZ_RING - 1)] = 0;
+    }
+    flushed = full;
+    __syncthreads();
   }
   if (t == 0) {
-    const uint32_t c = L.cl[256];
-    dz_put(L.out, base, c & 0xffffu, c >> 16);
-    segs[blockIdx.x].nbits = base + (c >> 16);
+    const uint32_t e = s_cl[256];
+    dz_put_ring(ring, base, e & 0xffffu, e >> 16);
+    segs[blockIdx.x].nbits = base + (e >> 16);
   }
   __syncthreads();
-  const uint32_t nw = (base + 32u + 31u) / 32u;
-  for (uint32_t i = t; i < nw; i += DZ_T) gout[i] = L.out[i];
+  const uint32_t endw = (base + (s_cl[256] >> 16) + 31u) >> 5;
+  for (uint32_t w = flushed + t; w < endw; w += DZ_T) gout[w] = ring[w & (DZ_RING - 1)];
 }
 
 // ---------------------------------------------------------------------------
@@ -756,18 +972,39 @@ __global__ void zs_dz_trailer_kernel(const ZsDJobDev *__restrict__ jobs, uint32_
 // ---------------------------------------------------------------------------
 // launcher
 // ---------------------------------------------------------------------------
-extern "C" void zs_launch_deflate(ZsDJobDev *d_jobs, uint32_t njobs, ZsDSegDev *d_segs, uint32_t nseg, uint32_t *d_tokens,
-                                  uint32_t *d_obuf, uint8_t *d_stage, hipStream_t st, hipEvent_t *ev) {
+// per segment: d_dist16 / d_len8 DZ_SEG entries, d_bm DZ_BMW bitmap words, d_aux DZ_AUXW words
+extern "C" void zs_launch_deflate(ZsDJobDev *d_jobs, uint32_t njobs, ZsDSegDev *d_segs, uint32_t nseg, uint16_t *d_dist16,
+                                  uint8_t *d_len8, uint32_t *d_bm, uint32_t *d_aux, uint32_t *d_obuf, uint8_t *d_stage,
+                                  hipStream_t st, hipEvent_t *ev) {
   if (ev) (void)hipEventRecord(ev[0], st);
-  hipLaunchKernelGGL(zs_dz_match_kernel, dim3(nseg), dim3(DZ_T), 0, st, d_jobs, d_segs, d_tokens);
+  hipLaunchKernelGGL(zs_dz_match_kernel, dim3(nseg), dim3(DZ_T), 0, st, d_jobs, d_segs, d_dist16, d_len8);
   if (ev) (void)hipEventRecord(ev[1], st);
-  hipLaunchKernelGGL(zs_dz_parse_kernel, dim3((nseg + 63) / 64), dim3(64), 0, st, d_jobs, d_segs, nseg, d_tokens);
+  hipLaunchKernelGGL(zs_dz_parse_kernel, dim3(nseg), dim3(DZ_T), 0, st, d_jobs, d_segs, d_len8, d_bm);
   if (ev) (void)hipEventRecord(ev[2], st);
-  hipLaunchKernelGGL(zs_dz_block_kernel, dim3(nseg), dim3(DZ_T), 0, st, d_jobs, d_segs, d_tokens, d_obuf);
+  hipLaunchKernelGGL(zs_dz_hist_kernel, dim3(nseg), dim3(DZ_T), 0, st, d_jobs, d_segs, nseg, d_dist16, d_len8, d_bm, d_aux);
+  hipLaunchKernelGGL(zs_dz_codes_kernel, dim3((nseg + WAVE - 1) / WAVE), dim3(WAVE), 0, st, d_jobs, d_segs, nseg, d_aux);
+  hipLaunchKernelGGL(zs_dz_emit_kernel, dim3(nseg), dim3(DZ_T), 0, st, d_jobs, d_segs, nseg, d_dist16, d_len8, d_bm, d_aux,
+                     d_obuf);
   hipLaunchKernelGGL(zs_dz_check_kernel, dim3(nseg), dim3(DZ_T), 0, st, d_jobs, d_segs);
   if (ev) (void)hipEventRecord(ev[3], st);
   hipLaunchKernelGGL(zs_dz_offsets_kernel, dim3(njobs), dim3(DZ_JT), 0, st, d_jobs, d_segs, d_stage);
   hipLaunchKernelGGL(zs_dz_stitch_kernel, dim3(nseg), dim3(DZ_T), 0, st, d_jobs, d_segs, d_obuf, d_stage);
   hipLaunchKernelGGL(zs_dz_trailer_kernel, dim3((njobs + 63) / 64), dim3(64), 0, st, d_jobs, njobs, d_stage);
   if (ev) (void)hipEventRecord(ev[4], st);
+}
+
+// block-kernel counters of the profiling build (merged into zs_kprof_read's 26..37)
+extern "C" int zs_kprof_read_dz(uint64_t *out12, int reset) {
+#if KP_ON
+  if (hipMemcpyFromSymbol(out12, HIP_SYMBOL(g_kprof_dz), 12 * sizeof(uint64_t)) != hipSuccess) return -1;
+  if (reset) {
+    static const unsigned long long z[12] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_kprof_dz), z, sizeof z) != hipSuccess) return -1;
+  }
+  return 12;
+#else
+  (void)out12;
+  (void)reset;
+  return 0;
+#endif
 }

@@ -1177,6 +1177,7 @@ extern "C" void zs_launch_lane(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads,
 }
 
 extern "C" int zs_kprof_read_ck(uint64_t *out16, int reset);
+extern "C" int zs_kprof_read_dz(uint64_t *out12, int reset);
 // Counter readback (profiling builds only; product builds report 0 counters).
 extern "C" int zs_kprof_read(uint64_t *out, uint32_t n, int reset) {
 #if KP_ON
@@ -1187,6 +1188,9 @@ extern "C" int zs_kprof_read(uint64_t *out, uint32_t n, int reset) {
     uint64_t ck[16];
     if (zs_kprof_read_ck(ck, reset) == 16)
       for (int i = 0; i < 16; i++) out[48 + i] = ck[i];
+    uint64_t dz[12];
+    if (zs_kprof_read_dz(dz, reset) == 12)
+      for (int i = 0; i < 12; i++) out[26 + i] = dz[i];
   }
   if (reset) {
     static const unsigned long long z[KP_COUNT] = {};

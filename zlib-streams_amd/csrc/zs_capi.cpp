@@ -31,8 +31,9 @@ extern "C" void zs_launch_finish(const ZsJobDev *d_jobs, const ZsHeadDev *d_head
                                  hipStream_t stream);
 extern "C" void zs_launch_fixed_tables(uint32_t *fixed, hipStream_t st);
 extern "C" void zs_launch_fixed_compact(uint32_t *fixed, hipStream_t st);
-extern "C" void zs_launch_deflate(ZsDJobDev *d_jobs, uint32_t njobs, ZsDSegDev *d_segs, uint32_t nseg, uint32_t *d_tokens,
-                                  uint32_t *d_obuf, uint8_t *d_stage, hipStream_t st, hipEvent_t *ev);
+extern "C" void zs_launch_deflate(ZsDJobDev *d_jobs, uint32_t njobs, ZsDSegDev *d_segs, uint32_t nseg, uint16_t *d_dist16,
+                                  uint8_t *d_len8, uint32_t *d_bm, uint32_t *d_aux, uint32_t *d_obuf, uint8_t *d_stage,
+                                  hipStream_t st, hipEvent_t *ev);
 extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, ZsSegDev *d_segs, uint32_t nseg,
                                   ZsCJobDev *d_cjobs, uint32_t ncjobs, ZsChunkDev *d_units, uint32_t nunit_slots,
                                   uint16_t *d_scratch, uint32_t *d_tokens, uint32_t *d_tables, const uint32_t *d_fixed,
@@ -585,12 +586,16 @@ unsigned handle_last_consumed(uintptr_t hp) {
 // ---------------------------------------------------------------------------
 constexpr uint64_t DZ_SEG_HOST = 65536;   // must match DZ_SEG
 constexpr uint64_t DZ_OUTW_HOST = 18440;  // must match DZ_OUTW
+constexpr uint64_t DZ_AUXW_HOST = 320 + 320 + 192 + 2400;  // must match DZ_AUXW
 
 struct DzWorkspace {
   size_t cap_jobs = 0, cap_segs = 0, cap_tok = 0, cap_obuf = 0, cap_stage = 0, cap_in = 0;
   ZsDJobDev *d_jobs = nullptr, *h_jobs = nullptr;
   ZsDSegDev *d_segs = nullptr, *h_segs = nullptr;
-  uint32_t *d_tok = nullptr, *d_obuf = nullptr;
+  uint16_t *d_tok = nullptr;  // distance - 1 per position
+  uint32_t *d_obuf = nullptr, *d_bm = nullptr, *d_aux = nullptr;
+  uint8_t *d_len8 = nullptr;
+  size_t cap_bm = 0, cap_len8 = 0, cap_aux = 0;
   uint8_t *d_stage = nullptr, *d_in = nullptr;
   hipEvent_t ev[5] = {};
   double stage_ms[4] = {};
@@ -687,6 +692,9 @@ int deflate_batch_locked(const zs_djob *jobs, uint32_t n, zs_result *results, ui
   }
   if ((r = dz_grow(&g_dz.d_tok, &g_dz.cap_tok, nseg * DZ_SEG_HOST)) ||
       (r = dz_grow(&g_dz.d_obuf, &g_dz.cap_obuf, nseg * DZ_OUTW_HOST)) ||
+      (r = dz_grow(&g_dz.d_bm, &g_dz.cap_bm, nseg * (DZ_SEG_HOST / 32))) ||
+      (r = dz_grow(&g_dz.d_len8, &g_dz.cap_len8, nseg * DZ_SEG_HOST)) ||
+      (r = dz_grow(&g_dz.d_aux, &g_dz.cap_aux, nseg * DZ_AUXW_HOST)) ||
       (r = dz_grow(&g_dz.d_stage, &g_dz.cap_stage, stage_total)))
     return r;
   if (!dev) {
@@ -721,7 +729,8 @@ int deflate_batch_locked(const zs_djob *jobs, uint32_t n, zs_result *results, ui
       for (int i = 0; i < 5; i++) HIP_OK(hipEventCreate(&g_dz.ev[i]));
     ev = g_dz.ev;
   }
-  zs_launch_deflate(g_dz.d_jobs, nv, g_dz.d_segs, (uint32_t)nseg, g_dz.d_tok, g_dz.d_obuf, g_dz.d_stage, st, ev);
+  zs_launch_deflate(g_dz.d_jobs, nv, g_dz.d_segs, (uint32_t)nseg, g_dz.d_tok, g_dz.d_len8, g_dz.d_bm, g_dz.d_aux, g_dz.d_obuf, g_dz.d_stage, st,
+                    ev);
   {
     hipError_t le = hipGetLastError();
     if (le != hipSuccess) {

@@ -12,6 +12,9 @@ enum ZsKprof {
   // expand pass (zs_expand_kernel), per workgroup (wave 0)
   KP_E_BLOCKS = 16, KP_E_CYC_TOTAL, KP_E_ROUNDS, KP_E_JUMP_ITERS, KP_E_CYC_JUMP, KP_E_BATCHES, KP_E_CYC_MAX,
   KP_E_CYC_INIT, KP_E_JUMP_ROUNDS,
+  // deflate block kernel (deflate_kernels.hip; its own array, copied into 26..37), per workgroup
+  KP_D_BLOCKS = 26, KP_D_CYC_TOTAL, KP_D_CYC_HIST, KP_D_CYC_BUILD, KP_D_CYC_HDR, KP_D_CYC_EMIT, KP_D_CYC_OUT,
+  KP_D_CHUNKS,
   // parse step phases (s_memtime, wave-uniform): refill 1, literal/length
   // lookup (+ slow path), length extra + refill 2, distance lookup (+ slow
   // path), checks + token write
