@@ -114,92 +114,110 @@ __device__ __forceinline__ uint32_t dz_dist_sym(uint32_t dist, uint32_t *xb, uin
 // ---------------------------------------------------------------------------
 // D1: match finding
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(DZ_T) zs_dz_match_kernel(const ZsDJobDev *__restrict__ jobs,
-                                                            const ZsDSegDev *__restrict__ segs,
-                                                            uint16_t *__restrict__ dist16, uint8_t *__restrict__ len8) {
+// One 512-thread workgroup per HALF segment (32 KiB of positions).  The half,
+// the 32 KiB of history before it and the longest match past its end are
+// staged in LDS next to the hash table (8192 buckets x 4 ways of 16-bit
+// window offsets, 0 = empty): candidate compares read LDS, not HBM.  A step
+// looks up 512 positions at once, then inserts them; positions 128 k ..
+// 128 k + 127 of a step go to way k, the even wave of the pair first and the
+// odd (later) one after a barrier, and within one store the higher lane lands
+// last -- the table, and so the output, is deterministic.
+#define DZ_MT 512u
+#define DZ_HALF 32768u
+#define DZ_MWIN (DZ_WIN + DZ_HALF + 288u)  // window bytes: history, the half, matches running past it
+
+__device__ __forceinline__ uint32_t dz_lds32(const uint32_t *w, uint32_t a) {
+  return __builtin_amdgcn_alignbyte(w[(a >> 2) + 1], w[a >> 2], a & 3u);
+}
+__device__ __forceinline__ uint4 dz_lds128(const uint32_t *w, uint32_t a) {
+  const uint32_t k = a >> 2, b = a & 3u;
+  const uint32_t x0 = w[k], x1 = w[k + 1], x2 = w[k + 2], x3 = w[k + 3], x4 = w[k + 4];
+  return make_uint4(__builtin_amdgcn_alignbyte(x1, x0, b), __builtin_amdgcn_alignbyte(x2, x1, b),
+                    __builtin_amdgcn_alignbyte(x3, x2, b), __builtin_amdgcn_alignbyte(x4, x3, b));
+}
+
+__global__ void __launch_bounds__(DZ_MT) zs_dz_match_kernel(const ZsDJobDev *__restrict__ jobs,
+                                                             const ZsDSegDev *__restrict__ segs,
+                                                             uint16_t *__restrict__ dist16, uint8_t *__restrict__ len8) {
   __shared__ uint16_t tab[DZ_HB][DZ_WAYS];
+  __shared__ __attribute__((aligned(16))) uint32_t win[DZ_MWIN / 4 + 8];
   const uint32_t tid = threadIdx.x;
-  const ZsDSegDev sg = segs[blockIdx.x];
+  const ZsDSegDev sg = segs[blockIdx.x >> 1];
+  const uint32_t half = blockIdx.x & 1u;
   const ZsDJobDev jb = jobs[sg.job];
-  if (jb.level == 0) return;  // stored blocks: no matches
+  if (jb.level == 0 || half * DZ_HALF >= sg.len) return;  // stored blocks / no positions
   gcu8 *in = (gcu8 *)jb.in;
   const uint64_t n = jb.in_len;
-  const uint64_t s = sg.start, e = s + sg.len;
-  // per position: length - 3 (4..258 -> 1..255; 0 = no match) and distance - 1
-  uint16_t *do16 = dist16 + sg.tok;
-  uint8_t *lo8 = len8 + sg.tok;
-  for (uint32_t i = tid; i < DZ_HB * DZ_WAYS / 2; i += DZ_T) reinterpret_cast<uint32_t *>(tab)[i] = 0xffffffffu;
-  __syncthreads();
-  // Way w of a bucket belongs to wave w: the waves of a step never store to
-  // the same slot, and within one store instruction the higher lane (the later
-  // position) lands last, so the table -- and the output -- is deterministic.
-  const uint32_t way = tid / WAVE;
-  // prime with the window before the segment
+  const uint64_t s = sg.start + half * DZ_HALF;
+  const uint64_t segend = sg.start + sg.len;  // matches stop at the segment end
+  const uint64_t e = min<uint64_t>(segend, s + DZ_HALF);
   const uint64_t hs = s > DZ_WIN ? s - DZ_WIN : 0;
-  for (uint64_t P = hs; P < s; P += DZ_T) {
-    const uint64_t p = P + tid;
-    if (p < s && p + 4 <= n) tab[dz_hash(dz_load32(in + p))][way] = (uint16_t)p;
+  const uint64_t we = min<uint64_t>(segend, e + 272u);
+  // per position: length - 3 (4..258 -> 1..255; 0 = no match) and distance - 1
+  uint16_t *do16 = dist16 + sg.tok + half * DZ_HALF;
+  uint8_t *lo8 = len8 + sg.tok + half * DZ_HALF;
+  for (uint32_t i = tid; i < DZ_HB * DZ_WAYS / 2; i += DZ_MT) reinterpret_cast<uint32_t *>(tab)[i] = 0u;
+  {
+    const uint32_t nb = (uint32_t)(we - hs), n16 = (nb + 15u) / 16u;
+    for (uint32_t k = tid; k < n16; k += DZ_MT) {
+      const uint64_t a = hs + 16ull * k;
+      uint4 v;
+      if (a + 16 <= n) {
+        v = dz_load128(in + a);
+      } else {
+        uint32_t b[4] = {0, 0, 0, 0};
+        for (uint32_t i = 0; a + i < n && i < 16; i++) b[i >> 2] |= (uint32_t)in[a + i] << (8u * (i & 3u));
+        v = make_uint4(b[0], b[1], b[2], b[3]);
+      }
+      *reinterpret_cast<uint4 *>(&win[4 * k]) = v;
+    }
   }
   __syncthreads();
-  const uint32_t maxd = 1u << jb.wbits;
-  for (uint64_t P = s; P < e; P += DZ_T) {
+  const uint32_t way = (tid >> 7) & 3u;
+  const bool odd = (tid >> 6) & 1u;
+  // prime with the history
+  for (uint64_t P = hs; P < s; P += DZ_MT) {
     const uint64_t p = P + tid;
-    uint32_t h = 0;
-    uint32_t best = 0, bd = 0;
-    if (p < e && p + 4 <= n) {
-      const uint32_t lim = (uint32_t)min<uint64_t>(258u, e - p);
-      if (p + 16 <= n) {
-        // 16-byte compares: one load round for the common (short) match
-        const uint4 cur = dz_load128(in + p);
-        h = dz_hash(cur.x);
-        const uint2 ent = *reinterpret_cast<const uint2 *>(&tab[h][0]);
-        const uint32_t c4[4] = {ent.x & 0xffffu, ent.x >> 16, ent.y & 0xffffu, ent.y >> 16};
-        uint32_t dd[4];
-        uint4 cv[4];
+    const bool ok = p < s && p + 4 <= n;
+    const uint32_t rel = (uint32_t)(p - hs);
+    const uint32_t h = ok ? dz_hash(dz_lds32(win, rel)) : 0u;
+    if (ok && !odd) tab[h][way] = (uint16_t)(rel + 1u);
+    __syncthreads();
+    if (ok && odd) tab[h][way] = (uint16_t)(rel + 1u);
+    __syncthreads();
+  }
+  const uint32_t maxd = 1u << jb.wbits;
+  for (uint64_t P = s; P < e; P += DZ_MT) {
+    const uint64_t p = P + tid;
+    const bool ok = p < e && p + 4 <= n;
+    const uint32_t rel = (uint32_t)(p - hs);
+    uint32_t h = 0, best = 0, bd = 0;
+    if (ok) {
+      const uint32_t lim = (uint32_t)min<uint64_t>(258u, segend - p);
+      const uint4 cur = dz_lds128(win, rel);
+      h = dz_hash(cur.x);
+      const uint2 ent = *reinterpret_cast<const uint2 *>(&tab[h][0]);
+      const uint32_t c4[4] = {ent.x & 0xffffu, ent.x >> 16, ent.y & 0xffffu, ent.y >> 16};
 #pragma unroll
-        for (uint32_t w = 0; w < DZ_WAYS; w++) {
-          const uint32_t d = ((uint32_t)p - c4[w]) & 0xffffu;
-          dd[w] = (c4[w] == 0xffffu || d == 0 || d > maxd || d > p) ? 0u : d;
-          if (dd[w]) cv[w] = dz_load128(in + (p - dd[w]));
+      for (uint32_t w = 0; w < DZ_WAYS; w++) {
+        if (!c4[w]) continue;
+        const uint32_t crel = c4[w] - 1u;
+        const uint32_t d = rel - crel;
+        if (crel >= rel || d > maxd) continue;
+        uint32_t L = dz_eq16(dz_lds128(win, crel), cur);
+        if (L < 4u) continue;
+        if (L == 16u) {
+          while (L + 16u <= lim) {
+            const uint32_t k = dz_eq16(dz_lds128(win, crel + L), dz_lds128(win, rel + L));
+            L += k;
+            if (k < 16u) break;
+          }
+          if (L + 16u > lim && L < lim) L += dz_eq16(dz_lds128(win, crel + L), dz_lds128(win, rel + L));
         }
-#pragma unroll
-        for (uint32_t w = 0; w < DZ_WAYS; w++) {
-          if (!dd[w]) continue;
-          uint32_t L = dz_eq16(cv[w], cur);
-          if (L < 4u) continue;
-          if (L == 16u) {
-            gcu8 *q = in + (p - dd[w]);
-            while (L + 16u <= lim) {
-              const uint32_t k = dz_eq16(dz_load128(q + L), dz_load128(in + p + L));
-              L += k;
-              if (k < 16u) break;
-            }
-            if (L + 16u > lim)
-              while (L < lim && q[L] == in[p + L]) L++;
-          }
-          L = min(L, lim);
-          if (L > best || (L == best && dd[w] < bd)) {
-            best = L;
-            bd = dd[w];
-          }
-        }
-      } else {  // the last 15 bytes of the input: byte compares
-        const uint32_t v = dz_load32(in + p);
-        h = dz_hash(v);
-#pragma unroll
-        for (uint32_t w = 0; w < DZ_WAYS; w++) {
-          const uint32_t c16 = tab[h][w];
-          if (c16 == 0xffffu) continue;
-          const uint32_t d = ((uint32_t)p - c16) & 0xffffu;
-          if (d == 0 || d > maxd || d > p) continue;
-          gcu8 *q = in + (p - d);
-          uint32_t L = 0;
-          while (L < lim && q[L] == in[p + L]) L++;
-          if (L < 4u) continue;
-          if (L > best || (L == best && d < bd)) {
-            best = L;
-            bd = d;
-          }
+        L = min(L, lim);
+        if (L > best || (L == best && d < bd)) {
+          best = L;
+          bd = d;
         }
       }
     }
@@ -207,8 +225,11 @@ __global__ void __launch_bounds__(DZ_T) zs_dz_match_kernel(const ZsDJobDev *__re
       lo8[p - s] = (uint8_t)(best >= 4u ? best - 3u : 0u);
       do16[p - s] = (uint16_t)(best >= 4u ? bd - 1u : 0u);
     }
+    const bool ins = ok && rel + 1u <= 0xffffu;
     __syncthreads();  // every lookup of the step before its inserts
-    if (p < e && p + 4 <= n) tab[h][way] = (uint16_t)p;
+    if (ins && !odd) tab[h][way] = (uint16_t)(rel + 1u);
+    __syncthreads();
+    if (ins && odd) tab[h][way] = (uint16_t)(rel + 1u);
     __syncthreads();
   }
 }
@@ -977,7 +998,7 @@ extern "C" void zs_launch_deflate(ZsDJobDev *d_jobs, uint32_t njobs, ZsDSegDev *
                                   uint8_t *d_len8, uint32_t *d_bm, uint32_t *d_aux, uint32_t *d_obuf, uint8_t *d_stage,
                                   hipStream_t st, hipEvent_t *ev) {
   if (ev) (void)hipEventRecord(ev[0], st);
-  hipLaunchKernelGGL(zs_dz_match_kernel, dim3(nseg), dim3(DZ_T), 0, st, d_jobs, d_segs, d_dist16, d_len8);
+  hipLaunchKernelGGL(zs_dz_match_kernel, dim3(2 * nseg), dim3(DZ_MT), 0, st, d_jobs, d_segs, d_dist16, d_len8);
   if (ev) (void)hipEventRecord(ev[1], st);
   hipLaunchKernelGGL(zs_dz_parse_kernel, dim3(nseg), dim3(DZ_T), 0, st, d_jobs, d_segs, d_len8, d_bm);
   if (ev) (void)hipEventRecord(ev[2], st);
