@@ -26,6 +26,9 @@
 #include "zs_device.h"
 #include "zs_kprof.h"
 
+#include <hipcub/device/device_radix_sort.hpp>
+#include <algorithm>
+
 #if KP_ON
 __device__ unsigned long long g_kprof[KP_COUNT];
 // wave-uniform value, added once per wave
@@ -709,10 +712,12 @@ __device__ void coop_block(LaneState &s, uint32_t ln, LaneLDS &L, uint32_t *lane
 __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict__ jobs, const ZsHeadDev *__restrict__ heads,
                                                       ZsChunkDev *__restrict__ chunks, uint32_t nchunks,
                                                       uint32_t *__restrict__ tokens, uint32_t *__restrict__ tables,
-                                                      const uint32_t *__restrict__ fixed) {
+                                                      const uint32_t *__restrict__ fixed, const uint32_t *__restrict__ order) {
   __shared__ LaneLDS L;
   const uint32_t lane = threadIdx.x;
-  const uint32_t c = blockIdx.x * WAVE + lane;
+  // units by decreasing span: a wave's lanes run similar lengths, the longest first
+  const uint32_t ci = blockIdx.x * WAVE + lane;
+  const uint32_t c = ci < nchunks ? order[ci] : ci;
   LaneState s;
   s.mode = LM_DONE;
   s.code = ZD_SKIP;
@@ -921,7 +926,8 @@ __device__ __forceinline__ void exp_barrier() {
 __global__ void __launch_bounds__(EXP_T) zs_expand_kernel(const ZsJobDev *__restrict__ jobs,
                                                            const ZsChunkDev *__restrict__ chunks,
                                                            uint16_t *__restrict__ scratch,
-                                                           const uint32_t *__restrict__ tokens) {
+                                                           const uint32_t *__restrict__ tokens,
+                                                           const uint32_t *__restrict__ order) {
   __shared__ __attribute__((aligned(16))) uint16_t ring[HIST];
   __shared__ __attribute__((aligned(16))) uint32_t s_mark[EXP_N];
   __shared__ uint32_t s_tval[EXP_T];
@@ -929,7 +935,7 @@ __global__ void __launch_bounds__(EXP_T) zs_expand_kernel(const ZsJobDev *__rest
   __shared__ __attribute__((aligned(16))) uint32_t s_j[2][EXP_N];
   __shared__ uint32_t s_jf[2][EXP_W];
   const uint32_t tid = threadIdx.x, lane = tid & (WAVE - 1), wv = tid / WAVE;
-  const ZsChunkDev ch = chunks[blockIdx.x];
+  const ZsChunkDev ch = chunks[order[blockIdx.x]];  // units by decreasing output (longest first)
   const int code = ch.code & 0xff;
   if (!(code == ZD_STOP || code == ZD_END)) return;
   gcu32 *tk = (gcu32 *)(tokens + ch.tok);
@@ -1164,15 +1170,76 @@ extern "C" void zs_launch_fixed_compact(uint32_t *fixed, hipStream_t st) {
   hipLaunchKernelGGL(zs_fixed_compact_kernel, dim3(1), dim3(64), 0, st, fixed);
 }
 
+// Schedule keys of every unit slot: the compressed span before the parse, the
+// output entries before the expand (0 for inactive or failed slots).
+__global__ void zs_unit_keys_kernel(const ZsJobDev *__restrict__ jobs, const ZsChunkDev *__restrict__ chunks, uint32_t n,
+                                    int after_parse, uint32_t *__restrict__ keys, uint32_t *__restrict__ ids) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const ZsChunkDev ch = chunks[i];
+  uint32_t k = 0;
+  if (ch.start_bit != ZS_NONE) {
+    if (after_parse) {
+      const int code = ch.code & 0xff;
+      k = (code == ZD_STOP || code == ZD_END) ? ch.n_out : 0u;
+    } else {
+      const uint64_t end = ch.stop_bit != ZS_NONE ? ch.stop_bit : (uint64_t)jobs[ch.job].in_len * 8u + 32u;
+      k = (uint32_t)min<uint64_t>(end > ch.start_bit ? end - ch.start_bit : 1u, 0xffffffffu);
+      k = max(k, 1u);
+    }
+  }
+  keys[i] = k;
+  ids[i] = i;
+}
+
+namespace {
+struct SortWs {  // grown on demand; the library serializes batches
+  uint32_t *buf = nullptr;  // keys in/out, ids in/out
+  void *tmp = nullptr;
+  size_t cap = 0, tmp_bytes = 0;
+};
+SortWs g_sort;
+// order[0..n) = unit slots by decreasing key (stable)
+int sort_units(const ZsJobDev *d_jobs, const ZsChunkDev *d_chunks, uint32_t n, int after_parse, uint32_t **order,
+               hipStream_t st) {
+  if (n > g_sort.cap) {
+    if (g_sort.buf) (void)hipFree(g_sort.buf);
+    if (g_sort.tmp) (void)hipFree(g_sort.tmp);
+    g_sort.buf = nullptr;
+    g_sort.tmp = nullptr;
+    const size_t c = std::max<size_t>(n, 2 * g_sort.cap);
+    size_t tb = 0;
+    (void)hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tb, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                                                 (const uint32_t *)nullptr, (uint32_t *)nullptr, (int)c, 0, 32, st);
+    if (hipMalloc(&g_sort.buf, 4 * c * sizeof(uint32_t)) != hipSuccess || hipMalloc(&g_sort.tmp, tb) != hipSuccess)
+      return -1;
+    g_sort.cap = c;
+    g_sort.tmp_bytes = tb;
+  }
+  uint32_t *kin = g_sort.buf, *kout = kin + g_sort.cap, *vin = kout + g_sort.cap, *vout = vin + g_sort.cap;
+  hipLaunchKernelGGL(zs_unit_keys_kernel, dim3((n + 255) / 256), dim3(256), 0, st, d_jobs, d_chunks, n, after_parse, kin,
+                     vin);
+  size_t tb = g_sort.tmp_bytes;
+  if (hipcub::DeviceRadixSort::SortPairsDescending(g_sort.tmp, tb, kin, kout, vin, vout, (int)n, 0, 32, st) != hipSuccess)
+    return -1;
+  *order = vout;
+  return 0;
+}
+}  // namespace
+
 extern "C" void zs_launch_lane(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, ZsChunkDev *d_chunks, uint32_t nchunks,
                                uint16_t *d_scratch, uint32_t *d_tokens, uint32_t *d_tables, const uint32_t *d_fixed,
                                hipStream_t st, hipEvent_t *ev) {
   // ev (profiling, optional): [0] after parse, [1] after expand
+  if (!nchunks) return;
   hipLaunchKernelGGL(zs_unit_header_kernel, dim3(nchunks), dim3(WAVE), 0, st, d_jobs, d_heads, d_chunks, d_tables);
+  uint32_t *order = nullptr;
+  if (sort_units(d_jobs, d_chunks, nchunks, 0, &order, st)) return;
   hipLaunchKernelGGL(zs_lane_kernel, dim3((nchunks + WAVE - 1) / WAVE), dim3(WAVE), 0, st, d_jobs, d_heads, d_chunks,
-                     nchunks, d_tokens, d_tables, d_fixed);
+                     nchunks, d_tokens, d_tables, d_fixed, order);
   if (ev) (void)hipEventRecord(ev[0], st);
-  hipLaunchKernelGGL(zs_expand_kernel, dim3(nchunks), dim3(EXP_T), 0, st, d_jobs, d_chunks, d_scratch, d_tokens);
+  if (sort_units(d_jobs, d_chunks, nchunks, 1, &order, st)) return;
+  hipLaunchKernelGGL(zs_expand_kernel, dim3(nchunks), dim3(EXP_T), 0, st, d_jobs, d_chunks, d_scratch, d_tokens, order);
   if (ev) (void)hipEventRecord(ev[1], st);
 }
 
