@@ -73,3 +73,28 @@ def js_schedule(data, w, wbits, out_cap=1 << 26):
     ol = ctypes.c_size_t(0)
     n = lib().zo_js_schedule(bytes(data), len(data), w, wbits, tr, len(tr), out, out_cap, ctypes.byref(ol))
     return tr.raw[:n].decode(), out.raw[:ol.value]
+
+
+class Stream:
+    """Call-by-call driver of the oracle's zlib-style inflate (zo_inflate):
+    the reference's per-call contract (consumed, produced, ret, msg, adler)."""
+
+    def __init__(self, wbits):
+        self.z = ZoStream()
+        self.rc = lib().zo_inflate_init2(ctypes.byref(self.z), wbits)
+
+    def call(self, data, out_len, flush):
+        ib = ctypes.create_string_buffer(bytes(data), max(len(data), 1))
+        ob = ctypes.create_string_buffer(max(out_len, 1))
+        self.z.next_in = ctypes.addressof(ib) if data else None
+        self.z.avail_in = len(data)
+        self.z.next_out = ctypes.addressof(ob)
+        self.z.avail_out = out_len
+        r = lib().zo_inflate(ctypes.byref(self.z), flush)
+        prod = out_len - self.z.avail_out
+        return {"ret": r, "consumed": len(data) - self.z.avail_in, "produced": prod, "out": ob.raw[:prod],
+                "msg": self.z.msg.decode() if self.z.msg else None, "total_in": self.z.total_in,
+                "total_out": self.z.total_out, "adler": self.z.adler}
+
+    def end(self):
+        lib().zo_inflate_end(ctypes.byref(self.z))

@@ -136,9 +136,11 @@ def test_stream_api_js_schedule(zs):
     for name in ("100k_lines", "zeros_100k", "10k_lines"):
         data = fixture(name)
         for w in (1000, 4096, 65536):
-            got = zs.decompress(data, "deflate64-raw", w)
-            _, eo = O.js_schedule(data, w, -16)
-            assert got == eo, (name, w)
+            tr, out = zs.js_schedule(data, "deflate64-raw", w)
+            etr, eo = O.js_schedule(data, w, -16)
+            assert (tr, out) == (etr, eo), (name, w)
+            if " -" not in etr:  # no negative code: the mirror's TransformStream completes
+                assert zs.decompress(data, "deflate64-raw", w) == eo, (name, w)
     raw = corpus.stream(40, 300000)
     for fmt, wb in (("deflate-raw", -15), ("deflate", 15), ("gzip", 31)):
         c = zlib.compressobj(6, zlib.DEFLATED, wb)

@@ -1,0 +1,210 @@
+"""GPU parity of the streaming surfaces, call by call (SURVEY.md §8b Tier 2).
+
+Every call of the handle ABI (src/wasm/wasm_stream_common.c:37-63) and of the
+zlib ABI (inflate(strm, flush), src/inflate.c:597) must return what the
+reference's zlib state machine returns for the same call: consumed, produced,
+the bytes, ret, msg, total_in/total_out and adler.  The oracle
+(oracle/zo_inflate.c, pinned by tests/test_oracle.py) is the checker; the
+reference's own call schedule is pinned by the Appendix C trace hashes.
+"""
+import ctypes
+import hashlib
+import json
+import os
+import random
+import struct
+import zlib
+
+import pytest
+
+import corpus
+import libz_ref
+import oracle_lib as O
+from golden.make_manifest import fixture
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+MAN = json.load(open(os.path.join(HERE, "golden", "manifest.json")))
+FMT = {-15: "deflate-raw", 15: "deflate", 31: "gzip", -16: "deflate64-raw"}
+
+
+@pytest.fixture(scope="module")
+def zs():
+    import zstreams
+    zstreams.lib()
+    return zstreams
+
+
+def _comp(data, wbits, level=6, mem=8, strategy=zlib.Z_DEFAULT_STRATEGY):
+    c = zlib.compressobj(level, zlib.DEFLATED, wbits, mem, strategy)
+    return c.compress(data) + c.flush()
+
+
+@pytest.mark.parametrize("case", MAN["traces"], ids=lambda c: f'{c["fixture"]}{c["wbits"]}w{c["write"]}')
+def test_appendix_c_traces(zs, case):
+    """The reference's JS schedule on the GPU reproduces the per-call traces
+    captured from the reference."""
+    tr, out = zs.js_schedule(fixture(case["fixture"]), FMT[case["wbits"]], case["write"])
+    assert tr.count("\n") == case["calls"]
+    assert hashlib.sha256(tr.encode()).hexdigest()[:16] == case["sha256_16"], tr
+    etr, eout = O.js_schedule(fixture(case["fixture"]), case["write"], case["wbits"])
+    assert tr == etr and out == eout
+
+
+def _schedule_cases():
+    rng = random.Random(7)
+    text = corpus.stream(3, 400000)
+    lines = corpus.stream(40, 300000)
+    rnd = bytes(rng.getrandbits(8) for _ in range(150000))
+    cases = []
+    for name in ("100k_lines", "zeros_100k", "payload_64k", "rand_block_gap"):
+        cases.append((fixture(name), -16))
+    cases.append((fixture("10k_lines"), -15))
+    for wb in (-15, 15, 31):
+        cases.append((_comp(text, wb), wb))
+        cases.append((_comp(lines, wb, 9), wb))
+        cases.append((_comp(rnd, wb, 6), wb))          # stored blocks
+        cases.append((_comp(text[:60000], wb, 0), wb))  # level 0
+        cases.append((_comp(text[:20000], wb, 1, strategy=zlib.Z_FIXED), wb))
+        cases.append((_comp(text[:90000], wb, 6, strategy=zlib.Z_HUFFMAN_ONLY), wb))
+        cases.append((_comp(b"", wb), wb))
+    # corrupt / truncated
+    g = _comp(text[:100000], 31)
+    cases.append((g[:len(g) - 3], 31))
+    b = bytearray(g)
+    b[len(b) - 6] ^= 0x55  # CRC mismatch
+    cases.append((bytes(b), 31))
+    z = _comp(lines[:100000], 15)
+    b = bytearray(z)
+    b[len(b) // 2] ^= 0x10
+    cases.append((bytes(b), 15))
+    return cases
+
+
+@pytest.mark.parametrize("write", [1000, 4096, 65536])
+def test_js_schedule_traces_match_oracle(zs, write):
+    """Per-call (n, produced, code, consumed) traces and output, GPU vs oracle."""
+    bad = []
+    for i, (data, wb) in enumerate(_schedule_cases()):
+        tr, out = zs.js_schedule(data, FMT[wb], write)
+        etr, eout = O.js_schedule(data, write, wb)
+        if tr != etr or out != eout:
+            bad.append((i, wb, len(data), tr[:300], etr[:300]))
+    assert not bad, bad[:3]
+
+
+def _gzip_header_all_fields(body_raw):
+    """gzip member with FEXTRA, FNAME, FCOMMENT and FHCRC set."""
+    hdr = bytearray(b"\x1f\x8b\x08\x1e") + struct.pack("<I", 12345) + b"\x00\x03"
+    hdr += struct.pack("<H", 7) + b"extra!!" + b"name.txt\x00" + b"a comment\x00"
+    hdr += struct.pack("<H", zlib.crc32(bytes(hdr)) & 0xffff)
+    return bytes(hdr)
+
+
+def _random_call_cases():
+    rng = random.Random(11)
+    text = corpus.stream(5, 200000)
+    cases = []
+    for wb in (-15, 15, 31, 47):
+        cases.append((_comp(text, wb if wb != 47 else 31), wb))
+    raw = text[:80000]
+    gz = _gzip_header_all_fields(raw) + _comp(raw, -15) + struct.pack("<II", zlib.crc32(raw), len(raw))
+    cases.append((gz, 31))
+    cases.append((gz, 47))
+    cases.append((fixture("100k_lines")[:60000], -16))
+    cases.append((fixture("payload_65k"), -16))
+    cases.append((bytes.fromhex("4b1c451f0000"), -16))  # len-285
+    cases.append((_comp(bytes(rng.getrandbits(8) for _ in range(70000)), -15, 1), -15))
+    cases.append((_comp(text[:50000], -15, 0), -15))
+    # distances beyond a small window: legal in one call, too far once split
+    cases.append((_comp(text[:60000], -15), -9))
+    cases.append((_comp(text[:60000], -9), -9))
+    # zlib FDICT header -> Z_NEED_DICT
+    zd = zlib.compressobj(6, zlib.DEFLATED, 15, 8, zlib.Z_DEFAULT_STRATEGY, b"dictionary words")
+    cases.append((zd.compress(text[:5000]) + zd.flush(), 15))
+    # corruptions in headers / data / trailers
+    for k in range(6):
+        b = bytearray(_comp(text[:30000], 31))
+        b[rng.randrange(len(b))] ^= 1 << rng.randrange(8)
+        cases.append((bytes(b), 31))
+    return cases
+
+
+class _GpuZ:
+    """The library's zlib ABI (inflateInit2_ / inflate / inflateEnd)."""
+
+    def __init__(self, L, wbits):
+        self.L = L
+        self.s = libz_ref.ZStream()
+        self.rc = L.inflateInit2_(ctypes.byref(self.s), wbits, b"1.2.11", ctypes.sizeof(libz_ref.ZStream))
+
+    def call(self, data, out_len, flush):
+        ib = ctypes.create_string_buffer(bytes(data), max(len(data), 1))
+        ob = ctypes.create_string_buffer(max(out_len, 1))
+        self.s.next_in = ctypes.addressof(ib) if data else None
+        self.s.avail_in = len(data)
+        self.s.next_out = ctypes.addressof(ob)
+        self.s.avail_out = out_len
+        r = self.L.inflate(ctypes.byref(self.s), flush)
+        prod = out_len - self.s.avail_out
+        return {"ret": r, "consumed": len(data) - self.s.avail_in, "produced": prod, "out": ob.raw[:prod],
+                "msg": self.s.msg.decode() if self.s.msg else None, "total_in": self.s.total_in,
+                "total_out": self.s.total_out, "adler": self.s.adler & 0xffffffff}
+
+    def end(self):
+        return self.L.inflateEnd(ctypes.byref(self.s))
+
+
+def test_zlib_abi_random_call_schedules(zs):
+    """Random avail_in / avail_out / flush per call (0 and 1 included), every
+    call's result vs the oracle's zlib-style inflate."""
+    L = ctypes.CDLL(zs.LIB_PATH)
+    L.inflateInit2_.argtypes = [ctypes.POINTER(libz_ref.ZStream), ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+    L.inflate.argtypes = [ctypes.POINTER(libz_ref.ZStream), ctypes.c_int]
+    L.inflateEnd.argtypes = [ctypes.POINTER(libz_ref.ZStream)]
+    rng = random.Random(2024)
+    ins = [0, 1, 2, 3, 5, 9, 64, 700, 4096, 32768, 200000]
+    outs = [0, 1, 2, 7, 258, 1000, 4096, 65536, 65536, 1 << 20]
+    ncalls = 0
+    for ci, (data, wb) in enumerate(_random_call_cases()):
+        g, o = _GpuZ(L, wb), O.Stream(wb)
+        assert g.rc == o.rc == 0
+        off, idle = 0, 0
+        for k in range(400):
+            n = min(rng.choice(ins), len(data) - off)
+            m = rng.choice(outs)
+            fl = 4 if rng.random() < 0.2 else 0
+            rg, ro = g.call(data[off:off + n], m, fl), o.call(data[off:off + n], m, fl)
+            ncalls += 1
+            assert rg == ro, (ci, wb, k, off, n, m, fl, {x: (rg[x], ro[x]) for x in rg if rg[x] != ro[x] and x != "out"})
+            off += ro["consumed"]
+            if ro["ret"] in (1, 2, -3):
+                break
+            idle = idle + 1 if ro["consumed"] == 0 and ro["produced"] == 0 else 0
+            if idle > 6 and off >= len(data):
+                break
+        g.end()
+        o.end()
+    assert ncalls > 500
+
+
+def test_zlib_abi_one_shot_fast_path(zs):
+    """A fresh stream offered whole (>= 1 MiB) goes through the batch pipeline;
+    the call's results still equal zlib's single inflate() call."""
+    L = ctypes.CDLL(zs.LIB_PATH)
+    L.inflateInit2_.argtypes = [ctypes.POINTER(libz_ref.ZStream), ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+    L.inflate.argtypes = [ctypes.POINTER(libz_ref.ZStream), ctypes.c_int]
+    L.inflateEnd.argtypes = [ctypes.POINTER(libz_ref.ZStream)]
+    raw = corpus.stream(9, 6 << 20)
+    for wb in (-15, 15, 31):
+        data = _comp(raw, wb)
+        for out_len, fl in ((len(raw) + 10, 4), (len(raw), 0), (len(raw) // 2, 0), (len(raw) // 2, 4)):
+            g, o = _GpuZ(L, wb), O.Stream(wb)
+            rg, ro = g.call(data, out_len, fl), o.call(data, out_len, fl)
+            assert rg == ro, (wb, out_len, fl)
+            if ro["ret"] == 0:  # continue from a FULL stop through the resumable path
+                rg, ro = g.call(data[ro["consumed"]:], 1 << 23, 4), o.call(data[ro["consumed"]:], 1 << 23, 4)
+                assert rg == ro
+            g.end()
+            o.end()

@@ -57,7 +57,7 @@ __global__ void zs_header_kernel(const ZsJobDev *__restrict__ jobs, ZsHeadDev *_
   h.start_byte = 0;
   h.total_in = 0;
   h.adler = 0;
-  h.pad2 = 0;
+  h.wbits = jb.wbits;
   const uint8_t *in = jb.in;
   const uint64_t n = jb.in_len;
   if (jb.wrap == ZW_RAW) {
@@ -126,6 +126,7 @@ __global__ void zs_header_kernel(const ZsJobDev *__restrict__ jobs, ZsHeadDev *_
     }
     h.adler = 0;
     h.is_gzip = 1;
+    if (h.wbits == 0) h.wbits = 15;  // src/inflate.c HEAD: gzip with windowBits 0 uses 15
     h.start_byte = p;
     heads[j] = h;
     return;
@@ -145,6 +146,7 @@ __global__ void zs_header_kernel(const ZsJobDev *__restrict__ jobs, ZsHeadDev *_
     return;
   }
   h.is_gzip = 0;
+  h.wbits = wb;
   h.start_byte = 2;
   heads[j] = h;
 }
@@ -337,212 +339,305 @@ struct Inflater {
 
   uint32_t stop_bits;  // end bit of the last decoded element (errors / FULL / END)
 
-  // Decode from the current bit position to the end of the final block.
-  // Returns ZsDecCode | (ZsMsg << 8); stop_bits describes where it stopped.
-  __device__ int run() {
+  // Resume bookkeeping (ZsStreamDev): the state a later call continues from.
+  // r_bit is the restart bit of the element in progress: a block header
+  // restarts at its first bit, a symbol at its first bit (zlib keeps the
+  // partial header / length / distance in its state instead; both resume to
+  // the same bits and output).
+  uint32_t r_mode, r_bit, r_len, r_dist, r_btype, r_nlen, r_ndist;
+  bool blast;  // BFINAL of the current block
+
+  // stored bytes [src, src + slen) (src/inflate.c:885-904 COPY); -1 = complete
+  __device__ int stored_copy(uint32_t src, uint32_t slen) {
+    uint32_t avail = end_byte - src;
+    uint32_t room = cap - pos;
+    uint32_t m = min(slen, min(avail, room));
+    copy_stored(src, m);
+    if (m < slen) {
+      r_mode = ZSM_STORED;
+      r_len = slen - m;
+      r_bit = (src + m) * 8;
+      if (m == avail) return ZD_TRUNC;  // input exhausted first (or at the same time)
+      stop_bits = (src + m) * 8;
+      return ZD_FULL;
+    }
+    seek((src + slen) * 8);
+    return -1;
+  }
+
+  // dynamic tables from lens[0, nlen + ndist) (src/inflate.c:1010-1032)
+  __device__ int dyn_tables(uint32_t nlen, uint32_t ndist, const uint32_t **lt, const uint32_t **dt, uint32_t *lbits,
+                            uint32_t *dbits) {
+    *lbits = 9;
+    if (build_table(T_LENS, lens, nlen, tab, lbits, sorted, scratch16, D64)) return ZD_ERROR | (ZM_LITLEN_SET << 8);
+    // distance table goes right after the literal/length table; its size
+    // is bounded by 852 entries (ENOUGH_LENS)
+    *dbits = 6;
+    if (build_table(T_DISTS, lens + nlen, ndist, tab + 852, dbits, sorted, scratch16, D64))
+      return ZD_ERROR | (ZM_DIST_SET << 8);
+    *lt = tab;
+    *dt = tab + 852;
+    return -1;
+  }
+
+  // Block header (src/inflate.c:834-1033).  -1: symbols follow with *lt/*dt;
+  // -2: a stored block was copied whole; otherwise a ZD_* code.
+  __device__ int block_header(const uint32_t **lt, const uint32_t **dt, uint32_t *lbits, uint32_t *dbits) {
     uint32_t lane = lane_id();
-    bool last = false;
-    for (;;) {
-      if (last) {
-        stop_bits = bitpos();
-        return ZD_END;
+    r_mode = ZSM_TYPE;
+    r_bit = bitpos();
+    refill();
+    if (short_of(3)) return ZD_TRUNC;
+    blast = (hold & 1) != 0;
+    uint32_t type = (uint32_t)(hold >> 1) & 3u;
+    drop(3);
+    if (type == 0) {
+      uint32_t pad = bitpos() & 7u;
+      if (pad) drop(8 - pad);
+      refill();
+      if (short_of(32)) return ZD_TRUNC;
+      uint32_t v = (uint32_t)hold;
+      if ((v & 0xffffu) != ((v >> 16) ^ 0xffffu)) {
+        stop_bits = bitpos() + 32;
+        return ZD_ERROR | (ZM_STORED_LEN << 8);
       }
+      drop(32);
+      int rc = stored_copy(bitpos() >> 3, v & 0xffffu);
+      return rc < 0 ? -2 : rc;
+    }
+    if (type == 1) {
+      if (!fixed_ready) build_fixed();
+      *lt = ftab;
+      *dt = ftab + 512;
+      *lbits = 9;
+      *dbits = 5;
+      r_btype = 1;
+      return -1;
+    }
+    if (type != 2) {
+      stop_bits = bitpos();
+      return ZD_ERROR | (ZM_BLOCK_TYPE << 8);
+    }
+    // ---- dynamic header (src/inflate.c:905-1033) ----
+    refill();
+    if (short_of(14)) return ZD_TRUNC;
+    uint32_t nlen = (uint32_t)(hold & 31) + 257;
+    uint32_t ndist = (uint32_t)((hold >> 5) & 31) + 1;
+    uint32_t ncode = (uint32_t)((hold >> 10) & 15) + 4;
+    drop(14);
+    if (nlen > 286 || (!D64 && ndist > 30)) {
+      stop_bits = bitpos();
+      return ZD_ERROR | (ZM_TOO_MANY << 8);
+    }
+    // code-length code lengths (src/inflate.c:923-934)
+    for (uint32_t i = 0; i < ncode; i++) {
       refill();
       if (short_of(3)) return ZD_TRUNC;
-      last = (hold & 1) != 0;
-      uint32_t type = (uint32_t)(hold >> 1) & 3u;
+      if (lane == 0) lens[c_clorder[i]] = (uint16_t)(hold & 7u);
       drop(3);
-      const uint32_t *lt;
-      const uint32_t *dt;
-      uint32_t lbits, dbits;
-      if (type == 0) {
-        uint32_t pad = bitpos() & 7u;
-        if (pad) drop(8 - pad);
-        refill();
-        if (short_of(32)) return ZD_TRUNC;
-        uint32_t v = (uint32_t)hold;
-        if ((v & 0xffffu) != ((v >> 16) ^ 0xffffu)) {
-          stop_bits = bitpos() + 32;
-          return ZD_ERROR | (ZM_STORED_LEN << 8);
-        }
-        drop(32);
-        uint32_t slen = v & 0xffffu;
-        uint32_t src = bitpos() >> 3;
-        uint32_t avail = end_byte - src;
-        uint32_t room = cap - pos;
-        uint32_t m = min(slen, min(avail, room));
-        copy_stored(src, m);
-        if (m < slen) {
-          if (m == avail) return ZD_TRUNC;  // input exhausted first (or at the same time)
-          stop_bits = (src + m) * 8;
+    }
+    if (lane >= ncode && lane < 19) lens[c_clorder[lane]] = 0;
+    __builtin_amdgcn_wave_barrier();
+    uint32_t cbits = 7;
+    if (build_table(T_CODES, lens, 19, tab, &cbits, sorted, scratch16, D64)) {
+      stop_bits = bitpos();
+      return ZD_ERROR | (ZM_CODE_LENGTHS << 8);
+    }
+    uint32_t total = nlen + ndist;
+    uint32_t have = 0;
+    uint32_t cmask = (1u << cbits) - 1;
+    while (have < total) {
+      refill();
+      uint32_t e = tab[(uint32_t)hold & cmask];
+      uint32_t eb = e_bits(e), ev = e_val(e);
+      if (short_of(eb)) return ZD_TRUNC;
+      if (ev < 16) {
+        drop(eb);
+        if (lane == 0) lens[have] = (uint16_t)ev;
+        have++;
+        continue;
+      }
+      uint32_t xb = ev == 16 ? 2 : (ev == 17 ? 3 : 7);
+      if (short_of(eb + xb)) return ZD_TRUNC;
+      drop(eb);
+      if (ev == 16 && have == 0) {
+        stop_bits = bitpos() + 2;
+        return ZD_ERROR | (ZM_REPEAT << 8);
+      }
+      uint32_t rep = (ev == 16 ? 3 : (ev == 17 ? 3 : 11)) + ((uint32_t)hold & ((1u << xb) - 1));
+      drop(xb);
+      if (have + rep > total) {
+        stop_bits = bitpos();
+        return ZD_ERROR | (ZM_REPEAT << 8);
+      }
+      __builtin_amdgcn_wave_barrier();
+      uint32_t fillv = ev == 16 ? uni(lens[have - 1]) : 0u;
+      if (lane < rep) lens[have + lane] = (uint16_t)fillv;  // rep <= 138 > 64: loop
+      if (lane + 64 < rep) lens[have + lane + 64] = (uint16_t)fillv;
+      if (lane + 128 < rep) lens[have + lane + 128] = (uint16_t)fillv;
+      __builtin_amdgcn_wave_barrier();
+      have += rep;
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (uni(lens[256]) == 0) {
+      stop_bits = bitpos();
+      return ZD_ERROR | (ZM_MISSING_EOB << 8);
+    }
+    int rc = dyn_tables(nlen, ndist, lt, dt, lbits, dbits);
+    if (rc >= 0) {
+      stop_bits = bitpos();
+      return rc;
+    }
+    r_btype = 2;
+    r_nlen = nlen;
+    r_ndist = ndist;
+    return -1;
+  }
+
+  // MATCH state (src/inflate.c:1142-1187): a decoded match, or the pending
+  // rest of one in a resumed call; -1 = copied whole.  left == 0 is tested
+  // before the distance, so a too-far distance met with a full output is
+  // reported by the next call (whave then counts the earlier calls' output,
+  // capped at the window size, as updatewindow keeps it).
+  __device__ int finish_match(uint32_t len, uint32_t dist) {
+    if (pos == cap) {
+      r_mode = ZSM_MATCH;
+      r_len = len;
+      r_dist = dist;
+      r_bit = stop_bits = bitpos();
+      return ZD_FULL;
+    }
+    if (dist > pos + whave) {
+      stop_bits = bitpos();
+      r_mode = ZSM_BAD;
+      return ZD_ERROR | (ZM_TOO_FAR << 8);
+    }
+    uint32_t n = min(len, cap - pos);
+    copy_match(n, dist);
+    if (n < len) {
+      r_mode = ZSM_MATCH;
+      r_len = len - n;
+      r_dist = dist;
+      r_bit = stop_bits = bitpos();
+      return ZD_FULL;
+    }
+    return -1;
+  }
+
+  // ---- symbol loop (src/inffast.c:100-287 / src/inflate.c:1037-1193) ----
+  // -1 at the end of the block, otherwise a ZD_* code
+  __device__ int symbols(const uint32_t *lt, const uint32_t *dt, uint32_t lbits, uint32_t dbits) {
+    r_mode = ZSM_SYMS;
+    const uint32_t lmask = (1u << lbits) - 1, dmask = (1u << dbits) - 1;
+    for (;;) {
+      refill();
+      r_bit = bitpos();
+      uint32_t e = lt[(uint32_t)hold & lmask];
+      uint32_t op = e_op(e);
+      uint32_t used = e_bits(e);
+      if (op != 0 && (op & 0xf0u) == 0) {  // second-level table
+        uint32_t e2 = lt[e_val(e) + (((uint32_t)(hold >> used)) & ((1u << op) - 1))];
+        used += e_bits(e2);
+        e = e2;
+        op = e_op(e);
+      }
+      if (short_of(used)) return ZD_TRUNC;
+      drop(used);
+      if (op == 0) {
+        if (pos == cap) {
+          r_mode = ZSM_LIT;
+          r_len = e_val(e);
+          r_bit = stop_bits = bitpos();
           return ZD_FULL;
         }
-        seek((src + slen) * 8);
+        put_literal(e_val(e));
         continue;
-      } else if (type == 1) {
-        if (!fixed_ready) build_fixed();
-        lt = ftab;
-        dt = ftab + 512;
-        lbits = 9;
-        dbits = 5;
-      } else if (type == 2) {
-        // ---- dynamic header (src/inflate.c:905-1033) ----
-        refill();
-        if (short_of(14)) return ZD_TRUNC;
-        uint32_t nlen = (uint32_t)(hold & 31) + 257;
-        uint32_t ndist = (uint32_t)((hold >> 5) & 31) + 1;
-        uint32_t ncode = (uint32_t)((hold >> 10) & 15) + 4;
-        drop(14);
-        if (nlen > 286 || (!D64 && ndist > 30)) {
-          stop_bits = bitpos();
-          return ZD_ERROR | (ZM_TOO_MANY << 8);
-        }
-        // code-length code lengths (src/inflate.c:923-934)
-        for (uint32_t i = 0; i < ncode; i++) {
-          refill();
-          if (short_of(3)) return ZD_TRUNC;
-          if (lane == 0) lens[c_clorder[i]] = (uint16_t)(hold & 7u);
-          drop(3);
-        }
-        if (lane >= ncode && lane < 19) lens[c_clorder[lane]] = 0;
-        __builtin_amdgcn_wave_barrier();
-        uint32_t cbits = 7;
-        if (build_table(T_CODES, lens, 19, tab, &cbits, sorted, scratch16, D64)) {
-          stop_bits = bitpos();
-          return ZD_ERROR | (ZM_CODE_LENGTHS << 8);
-        }
-        uint32_t total = nlen + ndist;
-        uint32_t have = 0;
-        uint32_t cmask = (1u << cbits) - 1;
-        while (have < total) {
-          refill();
-          uint32_t e = tab[(uint32_t)hold & cmask];
-          uint32_t eb = e_bits(e), ev = e_val(e);
-          if (short_of(eb)) return ZD_TRUNC;
-          if (ev < 16) {
-            drop(eb);
-            if (lane == 0) lens[have] = (uint16_t)ev;
-            have++;
-            continue;
-          }
-          uint32_t xb = ev == 16 ? 2 : (ev == 17 ? 3 : 7);
-          if (short_of(eb + xb)) return ZD_TRUNC;
-          drop(eb);
-          if (ev == 16 && have == 0) {
-            stop_bits = bitpos() + 2;
-            return ZD_ERROR | (ZM_REPEAT << 8);
-          }
-          uint32_t rep = (ev == 16 ? 3 : (ev == 17 ? 3 : 11)) + ((uint32_t)hold & ((1u << xb) - 1));
-          drop(xb);
-          if (have + rep > total) {
-            stop_bits = bitpos();
-            return ZD_ERROR | (ZM_REPEAT << 8);
-          }
-          __builtin_amdgcn_wave_barrier();
-          uint32_t fillv = ev == 16 ? uni(lens[have - 1]) : 0u;
-          if (lane < rep) lens[have + lane] = (uint16_t)fillv;  // rep <= 138 > 64: loop
-          if (lane + 64 < rep) lens[have + lane + 64] = (uint16_t)fillv;
-          if (lane + 128 < rep) lens[have + lane + 128] = (uint16_t)fillv;
-          __builtin_amdgcn_wave_barrier();
-          have += rep;
-        }
-        __builtin_amdgcn_wave_barrier();
-        if (uni(lens[256]) == 0) {
-          stop_bits = bitpos();
-          return ZD_ERROR | (ZM_MISSING_EOB << 8);
-        }
-        lbits = 9;
-        if (build_table(T_LENS, lens, nlen, tab, &lbits, sorted, scratch16, D64)) {
-          stop_bits = bitpos();
-          return ZD_ERROR | (ZM_LITLEN_SET << 8);
-        }
-        // distance table goes right after the literal/length table; its size
-        // is bounded by 852 entries (ENOUGH_LENS)
-        dbits = 6;
-        if (build_table(T_DISTS, lens + nlen, ndist, tab + 852, &dbits, sorted, scratch16, D64)) {
-          stop_bits = bitpos();
-          return ZD_ERROR | (ZM_DIST_SET << 8);
-        }
-        lt = tab;
-        dt = tab + 852;
-      } else {
-        stop_bits = bitpos();
-        return ZD_ERROR | (ZM_BLOCK_TYPE << 8);
       }
+      if (op & 32) return -1;  // end of block
+      if (op & 64) {
+        stop_bits = bitpos();
+        return ZD_ERROR | (ZM_LITLEN_CODE << 8);
+      }
+      uint32_t len = e_val(e);
+      uint32_t xb = op & (D64 ? 31u : 15u);
+      if (xb) {
+        if (short_of(xb)) return ZD_TRUNC;
+        len += (uint32_t)hold & ((1u << xb) - 1);
+        drop(xb);
+      }
+      refill();
+      uint32_t d = dt[(uint32_t)hold & dmask];
+      uint32_t dop = e_op(d);
+      uint32_t dused = e_bits(d);
+      if ((dop & 0xf0u) == 0) {
+        uint32_t d2 = dt[e_val(d) + (((uint32_t)(hold >> dused)) & ((1u << dop) - 1))];
+        dused += e_bits(d2);
+        d = d2;
+        dop = e_op(d);
+      }
+      if (short_of(dused)) return ZD_TRUNC;
+      drop(dused);
+      if (dop & 64) {
+        stop_bits = bitpos();
+        return ZD_ERROR | (ZM_DIST_CODE << 8);
+      }
+      uint32_t dist = e_val(d);
+      uint32_t dx = dop & 15u;
+      if (dx) {
+        if (short_of(dx)) return ZD_TRUNC;
+        dist += (uint32_t)hold & ((1u << dx) - 1);
+        drop(dx);
+      }
+      int rc = finish_match(len, dist);
+      if (rc >= 0) return rc;
+    }
+  }
 
-      // ---- symbol loop (src/inffast.c:100-287 / src/inflate.c:1037-1193) ----
-      const uint32_t lmask = (1u << lbits) - 1, dmask = (1u << dbits) - 1;
-      for (;;) {
-        refill();
-        uint32_t e = lt[(uint32_t)hold & lmask];
-        uint32_t op = e_op(e);
-        uint32_t used = e_bits(e);
-        if (op != 0 && (op & 0xf0u) == 0) {  // second-level table
-          uint32_t e2 = lt[e_val(e) + (((uint32_t)(hold >> used)) & ((1u << op) - 1))];
-          used += e_bits(e2);
-          e = e2;
-          op = e_op(e);
-        }
-        if (short_of(used)) return ZD_TRUNC;
-        drop(used);
-        if (op == 0) {
-          if (pos == cap) {
-            stop_bits = bitpos();
-            return ZD_FULL;
-          }
-          put_literal(e_val(e));
-          continue;
-        }
-        if (op & 32) break;  // end of block
-        if (op & 64) {
-          stop_bits = bitpos();
-          return ZD_ERROR | (ZM_LITLEN_CODE << 8);
-        }
-        uint32_t len = e_val(e);
-        uint32_t xb = op & (D64 ? 31u : 15u);
-        if (xb) {
-          if (short_of(xb)) return ZD_TRUNC;
-          len += (uint32_t)hold & ((1u << xb) - 1);
-          drop(xb);
-        }
-        refill();
-        uint32_t d = dt[(uint32_t)hold & dmask];
-        uint32_t dop = e_op(d);
-        uint32_t dused = e_bits(d);
-        if ((dop & 0xf0u) == 0) {
-          uint32_t d2 = dt[e_val(d) + (((uint32_t)(hold >> dused)) & ((1u << dop) - 1))];
-          dused += e_bits(d2);
-          d = d2;
-          dop = e_op(d);
-        }
-        if (short_of(dused)) return ZD_TRUNC;
-        drop(dused);
-        if (dop & 64) {
-          stop_bits = bitpos();
-          return ZD_ERROR | (ZM_DIST_CODE << 8);
-        }
-        uint32_t dist = e_val(d);
-        uint32_t dx = dop & 15u;
-        if (dx) {
-          if (short_of(dx)) return ZD_TRUNC;
-          dist += (uint32_t)hold & ((1u << dx) - 1);
-          drop(dx);
-        }
+  // Decode from the current bit position to the end of the final block, or
+  // until the input or the output runs out.  `mode` is where a resumed call
+  // starts (ZSM_TYPE for a whole stream).  Returns ZsDecCode | (ZsMsg << 8);
+  // stop_bits says where it stopped and r_* where a next call resumes.
+  __device__ int run(uint32_t mode) {
+    const uint32_t *lt = ftab, *dt = ftab + 512;
+    uint32_t lbits = 9, dbits = 5;
+    bool in_block = false;
+    int rc;
+    if (mode == ZSM_STORED) {
+      rc = stored_copy(bitpos() >> 3, r_len);
+      if (rc >= 0) return rc;
+    } else if (mode == ZSM_SYMS || mode == ZSM_LIT || mode == ZSM_MATCH) {
+      if (r_btype == 1) {
+        if (!fixed_ready) build_fixed();
+      } else {
+        dyn_tables(r_nlen, r_ndist, &lt, &dt, &lbits, &dbits);  // built once already: cannot fail
+      }
+      if (mode == ZSM_LIT) {
         if (pos == cap) {
           stop_bits = bitpos();
           return ZD_FULL;
         }
-        if (dist > pos + whave) {
-          stop_bits = bitpos();
-          return ZD_ERROR | (ZM_TOO_FAR << 8);
-        }
-        uint32_t n = min(len, cap - pos);
-        copy_match(n, dist);
-        if (n < len) {
-          stop_bits = bitpos();
-          return ZD_FULL;
-        }
+        put_literal(r_len);
+      } else if (mode == ZSM_MATCH) {
+        rc = finish_match(r_len, r_dist);
+        if (rc >= 0) return rc;
       }
+      in_block = true;
+    }
+    for (;;) {
+      if (!in_block) {
+        if (blast) {
+          stop_bits = bitpos();
+          r_mode = ZSM_CHECK;
+          r_bit = (stop_bits + 7u) & ~7u;
+          return ZD_END;
+        }
+        rc = block_header(&lt, &dt, &lbits, &dbits);
+        if (rc == -2) continue;
+        if (rc >= 0) return rc;
+      }
+      in_block = false;
+      rc = symbols(lt, dt, lbits, dbits);
+      if (rc >= 0) return rc;
     }
   }
 };
@@ -594,9 +689,10 @@ __global__ void __launch_bounds__(64) zs_decode_kernel(const ZsJobDev *__restric
   f.flushed = 0;
   f.whave = 0;
   f.fixed_ready = false;
+  f.blast = false;
   f.seek((mis + (uint32_t)hd.start_byte) * 8u);
   f.stop_bits = 0;
-  const int packed = f.run();
+  const int packed = f.run(ZSM_TYPE);
   const int code = packed & 0xff;
   f.flush_tail();
   res.code = code;
@@ -610,6 +706,249 @@ template __global__ void zs_decode_kernel<false>(const ZsJobDev *, const ZsHeadD
                                                  const uint32_t *);
 template __global__ void zs_decode_kernel<true>(const ZsJobDev *, const ZsHeadDev *, const uint32_t *, ZsDecDev *,
                                                 const uint32_t *);
+
+// ---------------------------------------------------------------------------
+// Exact streaming inflate: one call of the handle / zlib ABI
+// (src/wasm/wasm_stream_common.c:37-63 -> inflate(strm, flush)), resumed from
+// the handle's device state.  The job holds the call buffer (bytes carried
+// over from earlier calls + the new input) and the call's output buffer.
+// ---------------------------------------------------------------------------
+template <bool D64>
+__global__ void __launch_bounds__(64) zs_stream_kernel(ZsStreamDev *__restrict__ st, const ZsJobDev *__restrict__ job,
+                                                        const ZsHeadDev *__restrict__ head) {
+  constexpr uint32_t RING = D64 ? 65536u : 32768u;
+  constexpr uint32_t WOFF = 65536u - RING;  // window bytes used: the newest RING
+  __shared__ __attribute__((aligned(16))) uint8_t s_ring[RING];
+  __shared__ __attribute__((aligned(16))) uint32_t s_in[IN_RING_WORDS];
+  __shared__ uint32_t s_tab[TABLE_ENTRIES];
+  __shared__ uint32_t s_ftab[544];
+  __shared__ uint16_t s_lens[320];
+  __shared__ uint16_t s_sorted[320];
+  __shared__ uint32_t s_scr[32];
+
+  const uint32_t lane = lane_id();
+  const ZsJobDev jb = *job;
+  int32_t mode = st->mode;
+  uint32_t rbit = st->rbit;
+  int code = ZD_END, msg = ZM_NONE;
+  uint32_t stop = rbit, produced = 0;
+  if (mode == ZSM_HEAD) {
+    const ZsHeadDev hd = *head;
+    if (hd.code == ZD_SKIP) {
+      if (hd.ret == ZS_BUF_ERROR) {
+        code = ZD_TRUNC;
+      } else {
+        code = ZD_ERROR;
+        msg = hd.msg;
+        mode = ZSM_BAD;
+        stop = (uint32_t)hd.total_in * 8u;
+      }
+    } else if (hd.code == ZD_NEED_DICT) {
+      code = ZD_NEED_DICT;
+      mode = ZSM_DICT;
+      stop = 6u * 8u;
+      if (lane == 0) st->check = hd.adler;
+    } else {
+      mode = ZSM_TYPE;
+      rbit = (uint32_t)hd.start_byte * 8u;
+      if (lane == 0) {
+        st->is_gzip = hd.is_gzip;
+        st->wbits = hd.wbits;
+        st->ck_a = hd.is_gzip == 0 ? 1u : 0u;  // adler32(0, Z_NULL, 0) = 1 / CRC register 0
+        st->ck_b = 0;
+      }
+    }
+  }
+  __syncthreads();
+  if (mode >= ZSM_TYPE && mode <= ZSM_STORED) {
+    Inflater<D64> f;
+    f.ring = s_ring;
+    f.inring = s_in;
+    f.tab = s_tab;
+    f.ftab = s_ftab;
+    f.lens = s_lens;
+    f.sorted = s_sorted;
+    f.scratch16 = s_scr;
+    const uintptr_t ip = reinterpret_cast<uintptr_t>(jb.in);
+    const uint32_t mis = (uint32_t)(ip & 15u);
+    f.abase = reinterpret_cast<const uint8_t *>(ip - mis);
+    f.end_byte = mis + (uint32_t)jb.in_len;
+    f.limit_bits = f.end_byte * 8u;
+    f.out = jb.out;
+    f.cap = (uint32_t)jb.out_cap;
+    f.pos = 0;
+    f.flushed = 0;
+    const uint64_t total = st->total_out;
+    const uint32_t wbits = st->wbits ? st->wbits : 15u;
+    f.whave = (uint32_t)min<uint64_t>(total, 1ull << wbits);
+    if (total) {  // history: window[WOFF + k] is ring position k - RING
+      for (uint32_t k = lane * 16u; k < RING; k += WAVE * 16u)
+        *reinterpret_cast<uint4 *>(&s_ring[k]) = *reinterpret_cast<const uint4 *>(&st->window[WOFF + k]);
+    }
+    f.fixed_ready = false;
+    f.r_mode = (uint32_t)mode;
+    f.r_bit = mis * 8u + rbit;
+    f.r_len = st->len;
+    f.r_dist = st->dist;
+    f.r_btype = st->btype;
+    f.r_nlen = st->nlen;
+    f.r_ndist = st->ndist;
+    f.blast = st->last != 0;
+    if (mode != ZSM_TYPE && mode != ZSM_STORED && f.r_btype == 2)
+      for (uint32_t k = lane; k < f.r_nlen + f.r_ndist; k += WAVE) s_lens[k] = st->lens[k];
+    __syncthreads();
+    f.seek(mis * 8u + rbit);
+    f.stop_bits = 0;
+    const int packed = f.run((uint32_t)mode);
+    f.flush_tail();
+    __syncthreads();
+    code = packed & 0xff;
+    msg = packed >> 8;
+    mode = code == ZD_ERROR ? (int32_t)ZSM_BAD : (int32_t)f.r_mode;
+    stop = code == ZD_TRUNC ? (uint32_t)jb.in_len * 8u : f.stop_bits - mis * 8u;
+    rbit = f.r_bit - mis * 8u;
+    produced = f.pos;
+    // window for the next call: the newest RING bytes, oldest first
+    for (uint32_t k = lane; k < RING; k += WAVE) st->window[WOFF + k] = s_ring[(f.pos + k) & (RING - 1u)];
+    const bool dyn = (mode == ZSM_SYMS || mode == ZSM_LIT || mode == ZSM_MATCH) && f.r_btype == 2;
+    if (dyn)
+      for (uint32_t k = lane; k < f.r_nlen + f.r_ndist; k += WAVE) st->lens[k] = (uint8_t)s_lens[k];
+    if (lane == 0) {
+      st->len = f.r_len;
+      st->dist = f.r_dist;
+      st->btype = f.r_btype;
+      st->nlen = f.r_nlen;
+      st->ndist = f.r_ndist;
+      st->last = (f.blast && f.r_mode != ZSM_TYPE) ? 1u : 0u;  // at a block header the previous block was not final
+    }
+  }
+  if (lane == 0) {
+    st->mode = mode;
+    st->rbit = rbit;
+    st->code = code;
+    st->msg = msg;
+    st->stop_bits = stop;
+    st->produced = produced;
+    st->acc_a = 0;
+    st->acc_b = 0;
+  }
+}
+
+template __global__ void zs_stream_kernel<false>(ZsStreamDev *, const ZsJobDev *, const ZsHeadDev *);
+template __global__ void zs_stream_kernel<true>(ZsStreamDev *, const ZsJobDev *, const ZsHeadDev *);
+
+// check contributions of the call's output (zs_check.h accumulators)
+#define SCHECK_THREADS 256
+__global__ void __launch_bounds__(SCHECK_THREADS) zs_stream_check_kernel(ZsStreamDev *__restrict__ st,
+                                                                         const ZsJobDev *__restrict__ job) {
+  __shared__ uint32_t s_tab[4][256];
+  __shared__ uint64_t s_red[16];
+  const uint32_t t = threadIdx.x;
+  const int gz = st->is_gzip;
+  const uint64_t n = st->produced;
+  if (gz < 0 || n == 0 || st->mode == ZSM_HEAD) return;
+  const uint8_t *p = job->out;
+  const uint64_t piece = max<uint64_t>(4096u, ((n + gridDim.x - 1) / gridDim.x + 1023u) & ~1023ull);
+  const uint64_t p0 = (uint64_t)blockIdx.x * piece;
+  if (p0 >= n) return;
+  const uint64_t plen = min(piece, n - p0);
+  const uint64_t per = ((plen + SCHECK_THREADS - 1) / SCHECK_THREADS + 3u) & ~3ull;
+  const uint64_t lo = p0 + min(plen, per * t), hi = p0 + min(plen, per * (t + 1));
+  if (gz == 1) {
+    zs_crc_tables(s_tab);
+    const uint32_t v = zs_block_xor(zs_crc_piece(p, lo, hi, n, s_tab), reinterpret_cast<uint32_t *>(s_red));
+    if (t == 0 && v) atomicXor(reinterpret_cast<unsigned long long *>(&st->acc_a), (unsigned long long)v);
+  } else {
+    uint32_t A = 0, B = 0;
+    if (hi > lo) zs_adler_piece(p, lo, hi, n, &A, &B);
+    const uint64_t sa = zs_block_sum(A, s_red);
+    const uint64_t sb = zs_block_sum(B, s_red);
+    if (t == 0) {
+      atomicAdd(reinterpret_cast<unsigned long long *>(&st->acc_a), (unsigned long long)sa);
+      atomicAdd(reinterpret_cast<unsigned long long *>(&st->acc_b), (unsigned long long)sb);
+    }
+  }
+}
+
+// Running check, then the CHECK / LENGTH trailer states (src/inflate.c:1194-1232).
+__global__ void zs_stream_finish_kernel(ZsStreamDev *__restrict__ st, const ZsJobDev *__restrict__ job) {
+  if (threadIdx.x != 0) return;
+  ZsStreamDev &s = *st;
+  if (s.mode == ZSM_HEAD || s.mode == ZSM_DICT || s.code == ZD_NEED_DICT) return;
+  const int gz = s.is_gzip;
+  const uint64_t n = s.produced;
+  if (n && gz == 1) {
+    s.ck_a = zs_gf2_mul(zs_x8n(n), s.ck_a) ^ (uint32_t)s.acc_a;
+  } else if (n && gz == 0) {
+    const uint64_t a = s.ck_a, b = s.ck_b;
+    s.ck_b = (uint32_t)((b + (n % ZS_ADLER_MOD) * a + s.acc_b % ZS_ADLER_MOD) % ZS_ADLER_MOD);
+    s.ck_a = (uint32_t)((a + s.acc_a % ZS_ADLER_MOD) % ZS_ADLER_MOD);
+  }
+  s.total_out += n;
+  uint32_t check = 0;
+  if (gz == 1) check = ~(s.ck_a ^ zs_gf2_mul(zs_x8n(s.total_out), 0xffffffffu));
+  else if (gz == 0) check = (s.ck_b << 16) | s.ck_a;
+  if (gz >= 0) s.check = check;
+  const uint8_t *in = job->in;
+  const uint32_t len = (uint32_t)job->in_len;
+  if (s.mode == ZSM_CHECK) {
+    const uint32_t P = s.rbit >> 3;
+    if (gz < 0) {
+      s.mode = ZSM_DONE;
+      s.code = ZD_END;
+      s.stop_bits = s.rbit;
+    } else if (P + 4 > len) {
+      s.code = ZD_TRUNC;
+      s.stop_bits = len * 8u;
+    } else {
+      uint32_t tr = (uint32_t)in[P] | ((uint32_t)in[P + 1] << 8) | ((uint32_t)in[P + 2] << 16) | ((uint32_t)in[P + 3] << 24);
+      if (gz == 0) tr = (tr >> 24) | ((tr >> 8) & 0xff00u) | ((tr & 0xff00u) << 8) | (tr << 24);
+      s.stop_bits = (P + 4) * 8u;
+      s.rbit = (P + 4) * 8u;
+      if (tr != check) {
+        s.mode = ZSM_BAD;
+        s.code = ZD_ERROR;
+        s.msg = ZM_DATA_CHECK;
+      } else if (gz == 1) {
+        s.mode = ZSM_LENGTH;
+      } else {
+        s.mode = ZSM_DONE;
+        s.code = ZD_END;
+      }
+    }
+  }
+  if (s.mode == ZSM_LENGTH) {
+    const uint32_t P = s.rbit >> 3;
+    if (P + 4 > len) {
+      s.code = ZD_TRUNC;
+      s.stop_bits = len * 8u;
+    } else {
+      const uint32_t isz = (uint32_t)in[P] | ((uint32_t)in[P + 1] << 8) | ((uint32_t)in[P + 2] << 16) | ((uint32_t)in[P + 3] << 24);
+      s.stop_bits = (P + 4) * 8u;
+      if (isz != (uint32_t)(s.total_out & 0xffffffffu)) {
+        s.mode = ZSM_BAD;
+        s.code = ZD_ERROR;
+        s.msg = ZM_LENGTH_CHECK;
+      } else {
+        s.mode = ZSM_DONE;
+        s.code = ZD_END;
+      }
+    }
+  }
+}
+
+// One call: [wrapper header] -> resumable decode -> check -> trailers.
+extern "C" void zs_launch_stream(int d64, int run_header, ZsStreamDev *d_st, const ZsJobDev *d_job, ZsHeadDev *d_head,
+                                 uint64_t out_cap, hipStream_t stream) {
+  if (run_header) hipLaunchKernelGGL(zs_header_kernel, dim3(1), dim3(64), 0, stream, d_job, d_head, 1u);
+  if (d64)
+    hipLaunchKernelGGL(zs_stream_kernel<true>, dim3(1), dim3(64), 0, stream, d_st, d_job, d_head);
+  else
+    hipLaunchKernelGGL(zs_stream_kernel<false>, dim3(1), dim3(64), 0, stream, d_st, d_job, d_head);
+  const uint32_t pieces = (uint32_t)std::min<uint64_t>(1024, std::max<uint64_t>(1, (out_cap + 65535) / 65536));
+  hipLaunchKernelGGL(zs_stream_check_kernel, dim3(pieces), dim3(SCHECK_THREADS), 0, stream, d_st, d_job);
+  hipLaunchKernelGGL(zs_stream_finish_kernel, dim3(1), dim3(64), 0, stream, d_st, d_job);
+}
 
 // ---------------------------------------------------------------------------
 // Checks: CRC-32 (gzip) / Adler-32 (zlib) over each job's output, segment

@@ -5,10 +5,9 @@
 //   * zs_inflate_batch    -- many whole streams per launch sequence;
 //   * the reference's handle ABI (src/wasm/*_stream_wasm.c, wasm_stream_common.c);
 //   * the zlib inflate ABI (inflateInit2_/inflate/inflateEnd, src/inflate.c).
-// The stream surfaces accumulate input on the host and hand complete streams
-// to the GPU (first decode attempt at Z_FINISH or whenever the accumulated
-// input has doubled), then serve the output in caller-sized pieces.  Every
-// byte is produced by the GPU; a missing or failing device is a hard error.
+// The stream surfaces run every call as one exact, resumable inflate() on the
+// GPU (zlib's per-call consumed / produced / ret, see "Stream surfaces").
+// Every byte is produced by the GPU; a missing or failing device is a hard error.
 #include <hip/hip_runtime.h>
 #include <zlib.h>
 
@@ -29,6 +28,8 @@ extern "C" void zs_launch_decode(int d64, const ZsJobDev *d_jobs, const ZsHeadDe
 extern "C" void zs_launch_finish(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, const ZsDecDev *d_decs,
                                  uint64_t *d_checks, ZsResultDev *d_res, uint32_t njobs, uint64_t max_out,
                                  hipStream_t stream);
+extern "C" void zs_launch_stream(int d64, int run_header, ZsStreamDev *d_st, const ZsJobDev *d_job, ZsHeadDev *d_head,
+                                 uint64_t out_cap, hipStream_t stream);
 extern "C" void zs_launch_fixed_tables(uint32_t *fixed, hipStream_t st);
 extern "C" void zs_launch_fixed_compact(uint32_t *fixed, hipStream_t st);
 extern "C" void zs_launch_deflate(ZsDJobDev *d_jobs, uint32_t njobs, ZsDSegDev *d_segs, uint32_t nseg, uint16_t *d_dist16,
@@ -448,92 +449,209 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
 }
 
 // ---------------------------------------------------------------------------
-// Stream surfaces: accumulate, decode complete streams on the GPU, serve.
+// Stream surfaces: every call is one exact inflate(strm, flush) on the GPU.
+//
+// A handle's decoder state (ZsStreamDev: mode, pending literal / match /
+// stored bytes, current code lengths, the last 32 / 64 KiB of output, the
+// running check) stays in device memory between calls.  zlib pulls input on
+// demand (src/inflate.c:481-495, inffast.c:289-293): bytes it has pulled but
+// not turned into output yet live in its bit buffer / partial state.  Here
+// they are the host `carry` (at most a partial element: a symbol, a block
+// header, a wrapper header or trailer, plus the partial byte of a FULL stop),
+// put in front of the next call's new input.  So every call returns zlib's
+// (consumed, produced, ret, msg, adler) -- SURVEY §8b Tier 2.
+//
+// A fresh stream offered >= ZS_STREAM_FAST_KB of input in one call (the
+// zlib-ABI one-shot pattern) is first decoded by the batch pipeline (the
+// chunk-parallel path for large standard streams); when that run ends the
+// stream (STREAM_END or a data error) its result IS the call's result, as
+// it is one inflate() over the same input and output space.  Otherwise the
+// call runs on the resumable decoder.
 // ---------------------------------------------------------------------------
+constexpr size_t STREAM_SLICE = 64u << 20;  // input bytes per resumable launch (32-bit bit offsets)
+
 struct StreamState {
   int inited = 0;
   int wbits = 0;
-  std::vector<uint8_t> acc;   // input accepted and not yet resolved by a decode
-  size_t last_try = 0;        // acc size at the last unsuccessful decode attempt
-  bool done = false;          // decode result available
-  int final_ret = Z_OK;
-  const char *final_msg = nullptr;
-  uint32_t adler = 0;
-  std::vector<uint8_t> out;
-  size_t served = 0;
+  ZsJobDev cfg{};               // wrap / d64 / wbits from parse_wbits
+  int mode = ZSM_HEAD;          // host mirror of the device mode after the last call
+  std::vector<uint8_t> carry;   // pulled, not yet consumed into output (see above)
+  uint32_t carry_bit = 0;       // restart bit within carry[0]
   uint64_t total_in = 0, total_out = 0;
+  const char *msg = nullptr;
+  uint32_t adler = 0;
+  ZsStreamDev *d_st = nullptr;
 };
 
-// Decode `acc` as one whole stream with growing output capacity.
-int decode_whole(StreamState *s, zs_result *res) {
-  uint64_t cap = std::max<uint64_t>(1u << 20, 4 * (uint64_t)s->acc.size());
-  for (;;) {
-    if (cap >= (1ull << 32)) cap = (1ull << 32) - 1;
-    s->out.resize(cap);
-    zs_job j{};
-    j.in = s->acc.data();
-    j.in_len = s->acc.size();
-    j.out = s->out.data();
-    j.out_cap = cap;
-    j.window_bits = s->wbits;
-    int r = batch_locked(&j, 1, res, 0);
-    if (r) return r;
-    // output full with the stream not finished: grow and retry
-    if (res->ret == Z_BUF_ERROR && res->total_out == cap && cap < (1ull << 32) - 1) {
-      cap *= 4;
-      continue;
-    }
-    s->out.resize(res->total_out);
-    return 0;
-  }
+size_t stream_fast_min() {
+  static size_t v = [] {
+    const char *e = std::getenv("ZS_STREAM_FAST_KB");
+    return (size_t)(e ? std::atoll(e) : 1024) << 10;
+  }();
+  return v;
 }
 
-// One zlib-style call: returns ret, updates *consumed / *produced.
+struct StreamBufs {
+  ZsJobDev *d_job = nullptr;
+  ZsHeadDev *d_head = nullptr;
+  uint8_t *d_in = nullptr, *d_out = nullptr;
+  size_t cap_in = 0, cap_out = 0;
+} g_sb;
+
+int stream_init(StreamState *s, int wbits) {
+  ZsJobDev cfg{};
+  if (!parse_wbits(wbits, &cfg)) return Z_STREAM_ERROR;
+  if (ws_init()) return Z_STREAM_ERROR;
+  if (!g_sb.d_job) {
+    if (hipMalloc(&g_sb.d_job, sizeof(ZsJobDev)) != hipSuccess || hipMalloc(&g_sb.d_head, sizeof(ZsHeadDev)) != hipSuccess) {
+      set_err("stream: device allocation failed");
+      return Z_MEM_ERROR;
+    }
+  }
+  if (!s->d_st && hipMalloc(&s->d_st, sizeof(ZsStreamDev)) != hipSuccess) {
+    s->d_st = nullptr;
+    set_err("stream: device state allocation failed");
+    return Z_MEM_ERROR;
+  }
+  ZsStreamDev h;
+  std::memset(&h, 0, offsetof(ZsStreamDev, lens));
+  h.mode = cfg.wrap == ZW_RAW ? ZSM_TYPE : ZSM_HEAD;
+  h.wbits = (uint32_t)cfg.wbits;
+  h.is_gzip = -1;
+  if (hipMemcpy(s->d_st, &h, offsetof(ZsStreamDev, lens), hipMemcpyHostToDevice) != hipSuccess) {
+    set_err("stream: state upload failed");
+    return Z_STREAM_ERROR;
+  }
+  ZsStreamDev *keep = s->d_st;
+  *s = StreamState();
+  s->d_st = keep;
+  s->inited = 1;
+  s->wbits = wbits;
+  s->cfg = cfg;
+  s->mode = h.mode;
+  s->adler = (uint32_t)(cfg.wrap == ZW_RAW ? 0 : (cfg.wrap & 1));  // inflateResetKeep: strm->adler = wrap & 1
+  return Z_OK;
+}
+
+void stream_free(StreamState *s) {
+  if (s->d_st) (void)hipFree(s->d_st);
+  s->d_st = nullptr;
+}
+
+// Whole-stream attempt through the batch pipeline; true when it settled the call.
+bool stream_fast(StreamState *s, const uint8_t *in, unsigned in_len, uint8_t *out, unsigned out_len, unsigned *consumed,
+                 unsigned *produced, int *ret) {
+  zs_job j{};
+  j.in = in;
+  j.in_len = in_len;
+  j.out = out;
+  j.out_cap = out_len;
+  j.window_bits = s->wbits;
+  zs_result r;
+  if (batch_locked(&j, 1, &r, 0) || (r.ret != Z_STREAM_END && r.ret != Z_DATA_ERROR)) return false;
+  *consumed = (unsigned)r.total_in;
+  *produced = (unsigned)r.total_out;
+  *ret = r.ret;
+  s->mode = r.ret == Z_STREAM_END ? ZSM_DONE : ZSM_BAD;
+  s->msg = r.msg;
+  if (s->cfg.wrap != ZW_RAW) s->adler = r.adler;
+  // the device state is left behind: DONE / BAD never launch again
+  return true;
+}
+
+// One zlib inflate(strm, flush) call.  *need_dict: Z_NEED_DICT returns before
+// inf_leave, so total_in is not advanced (src/inflate.c:1325-1328).
 int stream_call(StreamState *s, const uint8_t *in, unsigned in_len, uint8_t *out, unsigned out_len, int flush,
                 unsigned *consumed, unsigned *produced) {
   *consumed = 0;
   *produced = 0;
-  if (!s->done) {
-    size_t before = s->acc.size();
-    s->acc.insert(s->acc.end(), in, in + in_len);
-    // decode at Z_FINISH, on the first call with data, and whenever the
-    // accumulated input has doubled since the last (truncated) attempt
-    bool attempt = flush == Z_FINISH || (!s->acc.empty() && s->acc.size() >= 2 * s->last_try);
-    if (!attempt) {
-      *consumed = in_len;
-      return in_len ? Z_OK : Z_BUF_ERROR;
-    }
-    zs_result res;
-    int r = decode_whole(s, &res);
-    if (r) {
-      s->acc.resize(before);
-      return Z_STREAM_ERROR;
-    }
-    bool trunc = res.ret == Z_BUF_ERROR;
-    if (trunc && flush != Z_FINISH) {
-      s->last_try = s->acc.size();
-      *consumed = in_len;
-      return in_len ? Z_OK : Z_BUF_ERROR;
-    }
-    s->done = true;
-    s->final_ret = res.ret;
-    s->final_msg = res.msg;
-    s->adler = res.adler;
-    uint64_t used_here = res.total_in > before ? res.total_in - before : 0;
-    *consumed = (unsigned)std::min<uint64_t>(used_here, in_len);
-    s->total_in = res.total_in;
+  if (s->mode == ZSM_DONE) return Z_STREAM_END;
+  if (s->mode == ZSM_BAD) return Z_DATA_ERROR;
+  if (s->mode == ZSM_DICT) return Z_NEED_DICT;
+  int fret;
+  if (s->total_in == 0 && s->total_out == 0 && s->carry.empty() && !s->cfg.d64 && in_len >= stream_fast_min() &&
+      stream_fast(s, in, in_len, out, out_len, consumed, produced, &fret)) {
+    s->total_in += *consumed;
+    s->total_out += *produced;
+    return fret;
   }
-  size_t rem = s->out.size() - s->served;
-  size_t n = std::min<size_t>(rem, out_len);
-  if (n) std::memcpy(out, s->out.data() + s->served, n);
-  s->served += n;
-  s->total_out += n;
-  *produced = (unsigned)n;
-  // more decoded output pending: Z_OK (also under Z_FINISH, so the reference's
-  // flush() drain loop, src/wasm/api/zlib-streams.js:119-136, keeps pulling)
-  if (s->served < s->out.size()) return Z_OK;
-  return s->final_ret;
+  const hipStream_t st = g_ws.stream;
+  ZsStreamDev h;
+  size_t off = 0;
+  uint64_t cons = 0, prod = 0;
+  for (;;) {
+    const size_t take = std::min<size_t>(in_len - off, STREAM_SLICE);
+    const size_t clen = s->carry.size();
+    const size_t blen = clen + take;
+    if (ws_reserve_bytes(&g_sb.d_in, &g_sb.cap_in, std::max<size_t>(blen, 64)) ||
+        ws_reserve_bytes(&g_sb.d_out, &g_sb.cap_out, std::max<size_t>((size_t)out_len - prod, 64))) {
+      set_err("stream: device buffer allocation failed");
+      return Z_MEM_ERROR;
+    }
+    if (clen) HIP_OK(hipMemcpyAsync(g_sb.d_in, s->carry.data(), clen, hipMemcpyHostToDevice, st));
+    if (take) HIP_OK(hipMemcpyAsync(g_sb.d_in + clen, in + off, take, hipMemcpyHostToDevice, st));
+    ZsJobDev jb = s->cfg;
+    jb.in = g_sb.d_in;
+    jb.in_len = blen;
+    jb.out = g_sb.d_out;
+    jb.out_cap = (uint64_t)out_len - prod;
+    HIP_OK(hipMemcpyAsync(g_sb.d_job, &jb, sizeof jb, hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemcpyAsync(&s->d_st->rbit, &s->carry_bit, sizeof(uint32_t), hipMemcpyHostToDevice, st));
+    zs_launch_stream(s->cfg.d64, s->mode == ZSM_HEAD, s->d_st, g_sb.d_job, g_sb.d_head, jb.out_cap, st);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipMemcpyAsync(&h, s->d_st, offsetof(ZsStreamDev, lens), hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    if (h.produced) HIP_OK(hipMemcpy(out + prod, g_sb.d_out, h.produced, hipMemcpyDeviceToHost));
+    prod += h.produced;
+    s->mode = h.mode;
+    if (h.is_gzip >= 0) s->adler = h.check;
+    if (h.code == ZD_TRUNC) {
+      // everything offered is pulled; keep the element in progress
+      cons += take;
+      const size_t rb = h.rbit >> 3;
+      std::vector<uint8_t> nc;
+      nc.reserve(blen - std::min(rb, blen));
+      if (rb < clen) nc.insert(nc.end(), s->carry.begin() + rb, s->carry.end());
+      const size_t from = rb > clen ? rb - clen : 0;
+      nc.insert(nc.end(), in + off + from, in + off + take);
+      s->carry.swap(nc);
+      s->carry_bit = h.rbit & 7u;
+      off += take;
+      if (off < in_len && prod < out_len) continue;
+      break;
+    }
+    const size_t pulled = (h.stop_bits + 7u) >> 3;
+    cons += pulled > clen ? pulled - clen : 0;
+    if (h.code == ZD_FULL) {
+      // resume at rbit (== stop_bits): keep its partial byte
+      const size_t rb = h.rbit >> 3;
+      std::vector<uint8_t> nc;
+      for (size_t k = rb; k < pulled; k++) nc.push_back(k < clen ? s->carry[k] : in[off + (k - clen)]);
+      s->carry.swap(nc);
+      s->carry_bit = h.rbit & 7u;
+    } else {
+      s->carry.clear();
+      s->carry_bit = 0;
+    }
+    break;
+  }
+  *consumed = (unsigned)cons;
+  *produced = (unsigned)prod;
+  s->total_out += prod;
+  if (h.code == ZD_NEED_DICT) {
+    s->adler = h.check;
+    return Z_NEED_DICT;
+  }
+  s->total_in += cons;
+  if (h.code == ZD_ERROR) {
+    s->msg = (h.msg > 0 && h.msg < ZM_COUNT) ? kMsgs[h.msg] : nullptr;
+    return Z_DATA_ERROR;
+  }
+  if (s->mode == ZSM_DONE) return Z_STREAM_END;
+  if ((cons == 0 && prod == 0) || flush == Z_FINISH) return Z_BUF_ERROR;
+  return Z_OK;
 }
+
 
 struct Handle {
   z_stream strm;  // layout parity with the reference context (unused fields)
@@ -550,14 +668,8 @@ uintptr_t handle_new() {
 int handle_init(uintptr_t hp, int wbits) {
   Handle *h = reinterpret_cast<Handle *>(hp);
   if (!h) return Z_STREAM_ERROR;
-  ZsJobDev probe{};
-  if (!parse_wbits(wbits, &probe)) return Z_STREAM_ERROR;
   std::lock_guard<std::mutex> lk(g_mu);
-  if (ws_init()) return Z_STREAM_ERROR;
-  h->st = StreamState();
-  h->st.inited = 1;
-  h->st.wbits = wbits;
-  return Z_OK;
+  return stream_init(&h->st, wbits);
 }
 int handle_process(uintptr_t hp, uintptr_t in_ptr, unsigned in_len, uintptr_t out_ptr, unsigned out_len, int flush) {
   Handle *h = reinterpret_cast<Handle *>(hp);
@@ -572,6 +684,10 @@ int handle_process(uintptr_t hp, uintptr_t in_ptr, unsigned in_len, uintptr_t ou
 int handle_end(uintptr_t hp) {
   Handle *h = reinterpret_cast<Handle *>(hp);
   if (!h) return Z_STREAM_ERROR;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    stream_free(&h->st);
+  }
   delete h;
   return Z_OK;
 }
@@ -952,17 +1068,21 @@ int ZEXPORT inflateInit2_(z_streamp strm, int windowBits, const char *version, i
   strm->msg = Z_NULL;
   ZsJobDev probe{};
   if (!parse_wbits(windowBits, &probe)) return Z_STREAM_ERROR;
-  {
-    std::lock_guard<std::mutex> lk(g_mu);
-    if (ws_init()) return Z_STREAM_ERROR;
-  }
   StreamState *s = new (std::nothrow) StreamState();
   if (!s) return Z_MEM_ERROR;
-  s->inited = 1;
-  s->wbits = windowBits;
+  int r;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    r = stream_init(s, windowBits);
+    if (r != Z_OK) stream_free(s);
+  }
+  if (r != Z_OK) {
+    delete s;
+    return r;
+  }
   strm->state = reinterpret_cast<struct internal_state *>(s);
   strm->total_in = strm->total_out = 0;
-  strm->adler = (probe.wrap == ZW_RAW) ? strm->adler : (uLong)(probe.wrap & 1);
+  if (probe.wrap != ZW_RAW) strm->adler = s->adler;
   return Z_OK;
 }
 
@@ -980,20 +1100,23 @@ int ZEXPORT inflate(z_streamp strm, int flush) {
   int ret = stream_call(s, strm->next_in, strm->avail_in, strm->next_out, strm->avail_out, flush, &cons, &prod);
   strm->next_in += cons;
   strm->avail_in -= cons;
-  strm->total_in += cons;
+  if (ret != Z_NEED_DICT) strm->total_in += cons;  // Z_NEED_DICT returns before inf_leave
   strm->next_out += prod;
   strm->avail_out -= prod;
   strm->total_out += prod;
-  if (s->done) {
-    strm->msg = const_cast<char *>(s->final_msg);
-    strm->adler = s->adler;
-  }
+  if (s->msg) strm->msg = const_cast<char *>(s->msg);
+  if (s->cfg.wrap != ZW_RAW) strm->adler = s->adler;
   return ret;
 }
 
 int ZEXPORT inflateEnd(z_streamp strm) {
   if (strm == Z_NULL || strm->state == Z_NULL) return Z_STREAM_ERROR;
-  delete reinterpret_cast<StreamState *>(strm->state);
+  StreamState *s = reinterpret_cast<StreamState *>(strm->state);
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    stream_free(s);
+  }
+  delete s;
   strm->state = Z_NULL;
   return Z_OK;
 }

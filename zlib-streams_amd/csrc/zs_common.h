@@ -77,7 +77,7 @@ struct ZsHeadDev {
   uint64_t start_byte; // first byte of deflate data
   uint64_t total_in;   // valid when code == ZD_SKIP / ZD_NEED_DICT
   uint32_t adler;      // valid when code == ZD_SKIP / ZD_NEED_DICT
-  uint32_t pad2;
+  uint32_t wbits;      // window bits in force after the header (zlib: CINFO when windowBits was 0)
 };
 
 // Deflate decode result.
@@ -187,6 +187,52 @@ struct ZsDSegDev {
   uint32_t ck_a;       // CRC-32 of the segment, or Adler sum a
   uint32_t ck_b;       // Adler weighted sum b (to the segment end)
   uint32_t pad;
+};
+
+// ---------------------------------------------------------------------------
+// Exact streaming inflate (the reference's per-call contract, SURVEY §8b
+// Tier 2): one handle's decoder state lives in device memory between calls,
+// so each inflate(strm, flush) call of the handle / zlib ABI is one resumable
+// decode on the GPU with zlib's pull-on-demand accounting.  The modes name
+// the states of src/inflate.c (inflate.h:21-54) where a call can return.
+// ---------------------------------------------------------------------------
+enum ZsStreamMode {
+  ZSM_HEAD = 0,    // wrapper header not complete yet (re-parsed from byte 0 of the carry)
+  ZSM_TYPE = 1,    // at a block header (TYPE..CODELENS restart here)
+  ZSM_SYMS = 2,    // inside a fixed/dynamic block at a symbol (LEN..DISTEXT restart here)
+  ZSM_LIT = 3,     // LIT with left == 0: literal `len` pending
+  ZSM_MATCH = 4,   // MATCH with left == 0: `len` bytes at `dist` pending
+  ZSM_STORED = 5,  // COPY: `len` stored bytes pending
+  ZSM_CHECK = 6,   // trailer CHECK (byte aligned)
+  ZSM_LENGTH = 7,  // gzip trailer LENGTH
+  ZSM_DONE = 8,
+  ZSM_BAD = 9,
+  ZSM_DICT = 10    // zlib FDICT: Z_NEED_DICT on every call
+};
+
+struct ZsStreamDev {
+  // resume point, in and out of every call; bit offsets relative to the
+  // call buffer (the host rebases them onto the bytes it carries over)
+  int32_t mode;        // ZsStreamMode
+  uint32_t rbit;       // restart bit
+  uint32_t last;       // BFINAL of the current block
+  uint32_t btype;      // 1 fixed, 2 dynamic (SYMS / LIT / MATCH)
+  uint32_t nlen, ndist;
+  uint32_t len, dist;  // LIT literal; MATCH remaining length + distance; STORED remaining bytes
+  uint32_t wbits;      // window bits (0: from the zlib header)
+  int32_t is_gzip;     // -1 raw, 0 zlib, 1 gzip (set by the header)
+  uint64_t total_out;  // bytes produced by earlier calls
+  uint32_t ck_a, ck_b; // running check: CRC-32 register f(0, out) (zs_check.h) / Adler a, b
+  // outcome of the last call
+  int32_t code;        // ZD_END / ZD_TRUNC / ZD_FULL / ZD_ERROR / ZD_NEED_DICT
+  int32_t msg;         // ZsMsg
+  uint32_t stop_bits;  // bits pulled (FULL / END / ERROR / trailer): zlib total_in = ceil(/8)
+  uint32_t produced;   // bytes written this call
+  uint32_t check;      // strm->adler after the call
+  uint32_t pad;
+  uint64_t acc_a, acc_b;  // check accumulators of this call's output
+  uint8_t lens[320];   // code lengths of the current dynamic block
+  __attribute__((aligned(16))) uint8_t window[65536];  // last 64 KiB (32 KiB used unless deflate64) of output, oldest first
 };
 
 // Final per-job result (device -> host), zlib z_stream fields after the call.

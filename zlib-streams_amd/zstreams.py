@@ -418,6 +418,44 @@ def compress(data, fmt="deflate-raw", level=-1, write_size=65536):
     return b"".join(parts)
 
 
+def js_schedule(data, fmt="deflate-raw", write_size=4096):
+    """The reference's DecompressionStreamZlib call schedule
+    (src/wasm/api/zlib-streams.js:64-136) over the handle ABI, recording every
+    process() call as "T n produced code consumed" / "F 0 produced code 0"
+    lines.  Returns (trace, output); stops at the first
+    negative code where the reference would throw."""
+    h = _Handle(fmt)
+    ob = ctypes.create_string_buffer(65536)
+    lines, out = [], []
+    failed = False
+    try:
+        for w in range(0, len(data), write_size):
+            chunk = data[w:w + write_size]
+            off = 0
+            while off < len(chunk):
+                n = min(len(chunk) - off, 32 * 1024)
+                produced, code, consumed = h.process(chunk[off:off + n], ob, Z_NO_FLUSH)
+                out.append(ob.raw[:produced])
+                lines.append(f"T {n} {produced} {code} {consumed}\n")
+                if code < 0:
+                    failed = True
+                    break
+                if consumed == 0:
+                    break
+                off += consumed
+            if failed:
+                break
+        while not failed:
+            produced, code, _ = h.process(b"", ob, Z_FINISH)
+            out.append(ob.raw[:produced])
+            lines.append(f"F 0 {produced} {code} 0\n")
+            if code < 0 or code == 1 or produced == 0:
+                break
+    finally:
+        h.end()
+    return "".join(lines), b"".join(out)
+
+
 def decompress(data, fmt="deflate-raw", write_size=4096):
     """Pipe ``data`` through a DecompressionStreamZlib in ``write_size`` writes."""
     ds = DecompressionStreamZlib(fmt)
