@@ -143,6 +143,8 @@ def main():
     ap.add_argument("--no-compress", action="store_true", help="skip the GPU deflate leg")
     ap.add_argument("--compress-level", type=int, default=6)
     ap.add_argument("--cpu-deflate-seconds", type=float, default=10.0)
+    ap.add_argument("--no-deflate64", action="store_true", help="skip the deflate64 suite leg (configs[3])")
+    ap.add_argument("--d64-reps", type=int, default=256, help="copies of the deflate64 fixture suite per batch")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json"),
                     help="PMC-derived HBM bytes per pipeline launch (null in the line when absent)")
     args = ap.parse_args()
@@ -244,6 +246,10 @@ def main():
         comp_leg = compress_leg(args, zstreams, shard, torch, np, dev, dist, raws, d_out, out_ptrs, nbytes,
                                 comp_total, host_threads, rank)
 
+    d64_leg = None
+    if not args.no_deflate64:
+        d64_leg = deflate64_leg(args, zstreams, torch, np, dev, rank)
+
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
         # interleave Zipf (first half) and lines (second half) streams
@@ -273,10 +279,106 @@ def main():
             "cpu_baseline": cpu,
             "path_stats": stats,
             "compress": comp_leg,
+            "deflate64": d64_leg,
         }
         print(json.dumps(line), flush=True)
     if dist:
         tdist.destroy_process_group()
+
+
+D64_FIXTURES = ("100k_lines", "10k_lines", "payload_63k", "payload_64k", "payload_65k", "rand_block_gap",
+                "repeat_63k", "repeat_64k", "repeat_65k", "zeros_100k")
+
+
+def deflate64_leg(args, zstreams, torch, np, dev, rank):
+    """configs[3]: the reference's deflate64 suite (test/run_deflate64_suite.sh:8-17 fixtures,
+    committed under tests/golden/ref-data) inflated at windowBits -16, as one device-resident
+    batch of `d64_reps` copies of the suite.  Every output is checked against the fixture
+    SHA-256 values of tests/golden/manifest.json; the oracle's C restatement (-16) is timed on
+    1 host thread beside it."""
+    import hashlib
+    gold = os.path.join(ROOT, "tests", "golden")
+    man = json.load(open(os.path.join(gold, "manifest.json")))["fixtures"]
+    suite = [open(os.path.join(gold, "ref-data", n + ".deflate64"), "rb").read() for n in D64_FIXTURES]
+    outs = [man[n]["len"] for n in D64_FIXTURES]
+    reps = max(1, args.d64_reps)
+    streams = suite * reps
+    offs, o = [], 0
+    for c in streams:
+        offs.append(o)
+        o += (len(c) + 255) & ~255
+    hbuf = np.zeros(o + 256, dtype=np.uint8)
+    for c, of in zip(streams, offs):
+        hbuf[of:of + len(c)] = np.frombuffer(c, dtype=np.uint8)
+    d_in = torch.from_numpy(hbuf).to(dev)
+    cap = (max(outs) + 4095) & ~4095
+    d_out = torch.empty(len(streams) * cap, dtype=torch.uint8, device=dev)
+    in_ptrs = [d_in.data_ptr() + of for of in offs]
+    in_lens = [len(c) for c in streams]
+    out_ptrs = [d_out.data_ptr() + k * cap for k in range(len(streams))]
+
+    def step():
+        return zstreams.inflate_batch_device(in_ptrs, in_lens, out_ptrs, [cap] * len(streams), -16)
+
+    for _ in range(max(1, args.warmup)):
+        res = step()
+    torch.cuda.synchronize()
+    host = d_out.cpu().numpy()
+    ok = all(r["ret"] == 1 and r["total_out"] == outs[k % len(suite)] for k, r in enumerate(res))
+    for k in range(len(streams)):
+        f = k % len(suite)
+        if k < len(suite) or k % 97 == 0:
+            ok = ok and hashlib.sha256(host[k * cap:k * cap + outs[f]].tobytes()).hexdigest() == man[D64_FIXTURES[f]]["sha256"]
+    del host
+    zstreams.profile(True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    t_el = (time.perf_counter() - t0) / args.steps
+    k_ms, b_ms, k_n = zstreams.profile_read()
+    zstreams.profile(False)
+    out_b = sum(outs) * reps
+    in_b = sum(in_lens)
+    k_s = k_ms / max(k_n, 1) / 1e3
+    leg = {"metric": "MiB/s decompressed, deflate64 (windowBits -16) fixture suite", "value": round(out_b / t_el / 2**20, 1),
+           "unit": "MiB/s", "ms_per_step": round(t_el * 1e3, 3),
+           "workload": f"{reps} copies of the {len(suite)}-fixture deflate64 suite ({len(streams)} streams, "
+                       f"{out_b / 2**20:.0f} MiB out), inputs resident in HBM, one batch per step",
+           "verified_sha256": bool(ok),
+           "roofline": {"bound": "hbm", "achieved": round((in_b + out_b) / k_s / 1e9, 2), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round((in_b + out_b) / k_s / 1e9 / HBM_PEAK_GBS, 6),
+                        "kernel": "zs_decode_kernel<true> (wave per stream)", "kernel_ms_avg": round(k_s * 1e3, 3),
+                        "alg_bytes_per_launch": in_b + out_b}}
+    if rank == 0 and not args.no_cpu_baseline:
+        L = ctypes.CDLL(os.path.join(ROOT, "oracle", "libzs_cpubase.so"))
+        L.zs_cpu_inflate.restype = ctypes.c_double
+        L.zs_cpu_inflate.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t),
+                                     ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_int)]
+        arrs = [np.frombuffer(c, dtype=np.uint8) for c in suite]
+        obufs = [np.empty(cap, dtype=np.uint8) for _ in suite]
+        n = len(suite)
+        cp = (ctypes.c_void_p * n)(*[a.ctypes.data for a in arrs])
+        cl = (ctypes.c_size_t * n)(*[len(a) for a in arrs])
+        op = (ctypes.c_void_p * n)(*[b.ctypes.data for b in obufs])
+        tt = bb = 0.0
+        passes = 0
+        bad = ctypes.c_int()
+        anybad = False
+        while tt < 3.0 or passes == 0:
+            tot = ctypes.c_uint64()
+            tt += L.zs_cpu_inflate(cp, cl, op, cap, n, 1, -16, 1, ctypes.byref(tot), ctypes.byref(bad))
+            anybad = anybad or bool(bad.value)
+            bb += tot.value
+            passes += 1
+        leg["cpu_baseline"] = {"value": round(bb / tt / 2**20, 1), "unit": "MiB/s", "cores": 1, "kind": "port",
+                               "impl": "oracle/zo_inflate.c at windowBits -16 (C restatement of the reference's "
+                                       "deflate64 inflate; the reference build is unbuildable here)",
+                               "sample": f"the {n}-fixture suite x {passes} passes, {tt:.1f} s on 1 thread",
+                               "verified": not anybad}
+    return leg
 
 
 def compress_leg(args, zstreams, shard, torch, np, dev, dist, raws, d_out, raw_ptrs, nbytes, zlib_raw_total,
