@@ -494,6 +494,200 @@ struct Inflater {
     return -1;
   }
 
+  // ---- wave-parallel symbol window ----------------------------------------
+  // The serial loop pays several dependent LDS round trips per symbol.  Here
+  // the 64 lanes decode a complete symbol (literal/length code, extra bits,
+  // distance code, extra bits) at EVERY bit offset of a 512-bit window, 8
+  // offsets per lane, all independent; the true symbol chain is then followed
+  // through register reads (readlane of packed lengths) and the chain's
+  // symbols are expanded 64 output bytes at a time, in-batch copy sources
+  // resolved by pointer jumping.  Only symbols with nothing exceptional are
+  // taken (complete inside the input, fitting the output, legal distance,
+  // not end-of-block / invalid): everything else stays on the exact serial
+  // path, so results and stop points are unchanged.
+  static constexpr uint32_t FW_OFFS = 8;
+  static constexpr uint32_t FW_BITS = FW_OFFS * WAVE;
+
+  __device__ __forceinline__ uint64_t bits_at(uint32_t q) const {
+    const uint32_t w = q >> 5, sh = q & 31u;
+    const uint32_t a = inring[w & (IN_RING_WORDS - 1)];
+    const uint32_t b = inring[(w + 1) & (IN_RING_WORDS - 1)];
+    const uint32_t c = inring[(w + 2) & (IN_RING_WORDS - 1)];
+    uint64_t h = ((((uint64_t)b) << 32) | a) >> sh;
+    if (sh) h |= (uint64_t)c << (64u - sh);
+    return h;
+  }
+  // words [.., w_end) resident in the LDS input ring
+  __device__ void ensure_words(uint32_t w_end) {
+    while (committed * PIECE_WORDS < w_end) {
+      __builtin_amdgcn_wave_barrier();
+      store_piece(committed, pending);
+      committed++;
+      pending = load_piece(committed);
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+  // bit reader at absolute bit `bit` (its word is in the ring)
+  __device__ void reseat(uint32_t bit) {
+    wi = bit >> 5;
+    hold = (uint64_t)inring[wi & (IN_RING_WORDS - 1)] >> (bit & 31u);
+    nbits = 32u - (bit & 31u);
+    wi++;
+  }
+  __device__ __forceinline__ static uint32_t scan_sum(uint32_t x) {  // inclusive, wave64
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);
+    return x;
+  }
+  __device__ __forceinline__ static uint32_t scan_max(uint32_t v) {  // inclusive, wave64
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));
+    return v;
+  }
+  __device__ __forceinline__ static uint32_t perm(uint32_t from_lane, uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(from_lane << 2), (int)v);
+  }
+
+  // Returns the symbols applied (0: the caller decodes the next one serially).
+  __device__ uint32_t fast_window(const uint32_t *lt, const uint32_t *dt, uint32_t lmask, uint32_t dmask) {
+    const uint32_t lane = lane_id();
+    const uint32_t P = bitpos();
+    if (P + FW_BITS + 64u > limit_bits || pos == cap) return 0;
+    ensure_words(((P + FW_BITS + 64u) >> 5) + 3u);
+    // 1. a complete symbol at every offset P + lane + 64 i
+    uint32_t nbp0 = 0, nbp1 = 0;  // total bits per slot, 8 bits each (0 = stop here)
+    uint32_t lv[FW_OFFS], dv[FW_OFFS];
+#pragma unroll
+    for (uint32_t i = 0; i < FW_OFFS; i++) {
+      const uint32_t q = P + lane + i * WAVE;
+      const uint64_t h = bits_at(q);
+      uint32_t e = lt[(uint32_t)h & lmask];
+      uint32_t op = e_op(e);
+      uint32_t used = e_bits(e);
+      if (op != 0 && (op & 0xf0u) == 0) {
+        const uint32_t e2 = lt[e_val(e) + (((uint32_t)(h >> used)) & ((1u << op) - 1))];
+        used += e_bits(e2);
+        e = e2;
+        op = e_op(e);
+      }
+      uint32_t nb = 0, l = 0, d = 0;
+      if (op == 0) {
+        nb = used;
+        l = 0x80000000u | e_val(e);
+      } else if ((op & 96u) == 0) {
+        const uint32_t xb = op & (D64 ? 31u : 15u);
+        l = e_val(e) + ((uint32_t)(h >> used) & ((1u << xb) - 1u));
+        const uint32_t s = used + xb;
+        const uint64_t hd = h >> s;
+        uint32_t de = dt[(uint32_t)hd & dmask];
+        uint32_t dop = e_op(de);
+        uint32_t dused = e_bits(de);
+        if ((dop & 0xf0u) == 0) {
+          const uint32_t d2 = dt[e_val(de) + (((uint32_t)(hd >> dused)) & ((1u << dop) - 1))];
+          dused += e_bits(d2);
+          de = d2;
+          dop = e_op(de);
+        }
+        if ((dop & 64u) == 0) {
+          const uint32_t dx = dop & 15u;
+          d = e_val(de) + ((uint32_t)(hd >> dused) & ((1u << dx) - 1u));
+          nb = s + dused + dx;
+        }
+      }
+      if (q + nb > limit_bits) nb = 0;
+      lv[i] = l;
+      dv[i] = d;
+      if (i < 4) nbp0 |= nb << (8u * i);
+      else nbp1 |= nb << (8u * (i - 4u));
+    }
+    // 2. the chain from P: up to 64 symbols that start inside the window
+    uint32_t cur = 0, cnt = 0, mypos = 0;
+    while (cnt < WAVE && cur < FW_BITS) {
+      const uint32_t slot = cur >> 6;
+      const uint32_t x = __builtin_amdgcn_readlane(slot < 4u ? nbp0 : nbp1, cur & 63u);
+      const uint32_t nb = (x >> ((slot & 3u) * 8u)) & 0xffu;
+      if (nb == 0) break;
+      if (lane == cnt) mypos = cur;
+      cur += nb;
+      cnt++;
+    }
+    if (cnt == 0) return 0;
+    // 3. symbol k -> lane k
+    const uint32_t src = mypos & 63u, sl = mypos >> 6;
+    uint32_t L = 0, D = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < FW_OFFS; i++) {
+      const uint32_t a = perm(src, lv[i]);
+      const uint32_t b = perm(src, dv[i]);
+      if (sl == i) {
+        L = a;
+        D = b;
+      }
+    }
+    const bool act = lane < cnt;
+    const bool lit = (L & 0x80000000u) != 0;
+    const uint32_t olen = act ? (lit ? 1u : L) : 0u;
+    const uint32_t incl = scan_sum(olen);
+    const uint32_t ost = incl - olen;
+    // admissible prefix: fits the output and the distance reaches written history
+    const bool ok = act && incl <= cap - pos && (lit || D <= pos + ost + whave);
+    const uint64_t badm = __ballot(!ok);
+    const uint32_t n = badm ? (uint32_t)__builtin_ctzll(badm) : WAVE;
+    if (n == 0) return 0;
+    const uint32_t T = __builtin_amdgcn_readlane(incl, n - 1);
+    const uint32_t endrel = n < cnt ? __builtin_amdgcn_readlane(mypos, n) : cur;
+    // 4. expand 64 output bytes per step
+    const uint32_t base = pos;
+    uint32_t carry = 0;
+    uint16_t *marks = sorted;  // table-build scratch, idle inside a block
+    for (uint32_t b0 = 0; b0 < T; b0 += WAVE) {
+      marks[lane] = 0;
+      __builtin_amdgcn_wave_barrier();
+      if (lane < n && ost >= b0 && ost < b0 + WAVE) marks[ost - b0] = (uint16_t)(lane + 1u);
+      __builtin_amdgcn_wave_barrier();
+      const uint32_t s = max(scan_max(marks[lane]), carry + 1u) - 1u;
+      carry = __builtin_amdgcn_readlane(s, WAVE - 1);
+      const uint32_t j = b0 + lane;
+      const uint32_t Ls = perm(s, L), Ds = perm(s, D);
+      uint32_t val = Ls & 0xffu, ptr = lane;
+      bool res = true;
+      if (!(Ls & 0x80000000u)) {
+        const int32_t sp = (int32_t)j - (int32_t)Ds;  // relative to `base`
+        if (sp < (int32_t)b0) {
+          val = ring[(base + (uint32_t)sp) & RMASK];
+        } else {
+          res = false;
+          ptr = (uint32_t)sp - b0;
+        }
+      }
+      while (__ballot(!res)) {  // pointer jumping, <= 6 rounds
+        const uint32_t pv = perm(ptr, val), pr = perm(ptr, res ? 1u : 0u), pp = perm(ptr, ptr);
+        if (!res) {
+          if (pr) {
+            val = pv;
+            res = true;
+          } else {
+            ptr = pp;
+          }
+        }
+      }
+      if (j < T) ring[(base + j) & RMASK] = (uint8_t)val;
+      __builtin_amdgcn_wave_barrier();
+      pos = base + min(T, b0 + WAVE);
+      maybe_flush();
+    }
+    reseat(P + endrel);
+    return n;
+  }
+
   // MATCH state (src/inflate.c:1142-1187): a decoded match, or the pending
   // rest of one in a resumed call; -1 = copied whole.  left == 0 is tested
   // before the distance, so a too-far distance met with a full output is
@@ -530,6 +724,7 @@ struct Inflater {
     r_mode = ZSM_SYMS;
     const uint32_t lmask = (1u << lbits) - 1, dmask = (1u << dbits) - 1;
     for (;;) {
+      if (fast_window(lt, dt, lmask, dmask)) continue;
       refill();
       r_bit = bitpos();
       uint32_t e = lt[(uint32_t)hold & lmask];
