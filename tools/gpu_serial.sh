@@ -5,4 +5,6 @@ echo "gpu tests rc=$rc"; tail -15 gpurun_out/ser/pytest_gpu.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 200 python -u tools/serial_probe.py > gpurun_out/ser/probe.log 2>&1; rc=$?
 echo "probe rc=$rc"; cat gpurun_out/ser/probe.log
-exit $rc
+
+ZS_LIB=$PWD/zlib-streams_amd/libzstreams_mi355x_prof.so timeout -k 10 120 python -u tools/serial_kprof.py > gpurun_out/ser/kprof.log 2>&1; rc=$?
+echo "kprof rc=$rc"; cat gpurun_out/ser/kprof.log

@@ -27,6 +27,18 @@
 #include "zs_device.h"
 #include "zs_check.h"
 
+#include "zs_kprof.h"
+
+#if KP_ON
+__device__ unsigned long long g_kprof_w[16];  // KP_W_* - 64
+#define KPW_ADD(i, v)                                                          \
+  do {                                                                         \
+    if (lane_id() == 0) atomicAdd(&g_kprof_w[(i) - 64], (unsigned long long)(v)); \
+  } while (0)
+#else
+#define KPW_ADD(i, v) ((void)0)
+#endif
+
 #define IN_RING_WORDS 1024   // 4 KiB compressed-input ring
 #define PIECE_WORDS 256      // 1 KiB per fill (64 lanes x 16 B)
 #define FLUSH_BYTES 1024     // output flush granule (64 lanes x 16 B)
@@ -507,6 +519,8 @@ struct Inflater {
   // path, so results and stop points are unchanged.
   static constexpr uint32_t FW_OFFS = 8;
   static constexpr uint32_t FW_BITS = FW_OFFS * WAVE;
+  static constexpr uint32_t FW_JN = FW_BITS + WAVE;  // jump-table entries (offsets past the window loop on themselves)
+  uint16_t *jmp;  // LDS: 2 x FW_JN jump tables, reused as 256 u32 expansion entries
 
   __device__ __forceinline__ uint64_t bits_at(uint32_t q) const {
     const uint32_t w = q >> 5, sh = q & 31u;
@@ -561,65 +575,124 @@ struct Inflater {
     const uint32_t lane = lane_id();
     const uint32_t P = bitpos();
     if (P + FW_BITS + 64u > limit_bits || pos == cap) return 0;
+    [[maybe_unused]] const uint64_t kt0 = KP_NOW();
     ensure_words(((P + FW_BITS + 64u) >> 5) + 3u);
-    // 1. a complete symbol at every offset P + lane + 64 i
+    // 1. a complete symbol at every offset P + lane + 64 i; straight-line
+    //    stages (input bits, root, sub-table, distance root, distance
+    //    sub-table) so each stage issues its 8 LDS loads back to back
     uint32_t nbp0 = 0, nbp1 = 0;  // total bits per slot, 8 bits each (0 = stop here)
     uint32_t lv[FW_OFFS], dv[FW_OFFS];
+    uint64_t hh[FW_OFFS];
+    uint32_t ee[FW_OFFS], e2[FW_OFFS], used[FW_OFFS];
+#pragma unroll
+    for (uint32_t i = 0; i < FW_OFFS; i++) hh[i] = bits_at(P + lane + i * WAVE);
+#pragma unroll
+    for (uint32_t i = 0; i < FW_OFFS; i++) ee[i] = lt[(uint32_t)hh[i] & lmask];
 #pragma unroll
     for (uint32_t i = 0; i < FW_OFFS; i++) {
-      const uint32_t q = P + lane + i * WAVE;
-      const uint64_t h = bits_at(q);
-      uint32_t e = lt[(uint32_t)h & lmask];
-      uint32_t op = e_op(e);
-      uint32_t used = e_bits(e);
-      if (op != 0 && (op & 0xf0u) == 0) {
-        const uint32_t e2 = lt[e_val(e) + (((uint32_t)(h >> used)) & ((1u << op) - 1))];
-        used += e_bits(e2);
-        e = e2;
-        op = e_op(e);
+      const uint32_t op = e_op(ee[i]);
+      used[i] = e_bits(ee[i]);
+      const bool sub = op != 0 && (op & 0xf0u) == 0;
+      e2[i] = lt[sub ? e_val(ee[i]) + (((uint32_t)(hh[i] >> used[i])) & ((1u << op) - 1)) : 0u];
+    }
+    uint64_t hd[FW_OFFS];
+    uint32_t sb[FW_OFFS], de[FW_OFFS];
+#pragma unroll
+    for (uint32_t i = 0; i < FW_OFFS; i++) {
+      const uint32_t op0 = e_op(ee[i]);
+      if (op0 != 0 && (op0 & 0xf0u) == 0) {
+        used[i] += e_bits(e2[i]);
+        ee[i] = e2[i];
       }
-      uint32_t nb = 0, l = 0, d = 0;
+      const uint32_t op = e_op(ee[i]);
+      const uint32_t xb = (op == 0 || (op & 96u)) ? 0u : op & (D64 ? 31u : 15u);
+      lv[i] = op == 0 ? (0x80000000u | e_val(ee[i])) : e_val(ee[i]) + ((uint32_t)(hh[i] >> used[i]) & ((1u << xb) - 1u));
+      sb[i] = used[i] + xb;
+      hd[i] = hh[i] >> sb[i];
+      de[i] = dt[(uint32_t)hd[i] & dmask];
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < FW_OFFS; i++) {
+      const uint32_t dop0 = e_op(de[i]);
+      const uint32_t du0 = e_bits(de[i]);
+      const bool dsub = (dop0 & 0xf0u) == 0;
+      e2[i] = dt[dsub ? e_val(de[i]) + (((uint32_t)(hd[i] >> du0)) & ((1u << dop0) - 1)) : 0u];
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < FW_OFFS; i++) {
+      const uint32_t op = e_op(ee[i]);
+      uint32_t d = de[i];
+      uint32_t dused = e_bits(d);
+      if ((e_op(d) & 0xf0u) == 0) {
+        dused += e_bits(e2[i]);
+        d = e2[i];
+      }
+      const uint32_t dop = e_op(d);
+      const uint32_t dx = dop & 15u;
+      uint32_t nb = 0;
       if (op == 0) {
-        nb = used;
-        l = 0x80000000u | e_val(e);
-      } else if ((op & 96u) == 0) {
-        const uint32_t xb = op & (D64 ? 31u : 15u);
-        l = e_val(e) + ((uint32_t)(h >> used) & ((1u << xb) - 1u));
-        const uint32_t s = used + xb;
-        const uint64_t hd = h >> s;
-        uint32_t de = dt[(uint32_t)hd & dmask];
-        uint32_t dop = e_op(de);
-        uint32_t dused = e_bits(de);
-        if ((dop & 0xf0u) == 0) {
-          const uint32_t d2 = dt[e_val(de) + (((uint32_t)(hd >> dused)) & ((1u << dop) - 1))];
-          dused += e_bits(d2);
-          de = d2;
-          dop = e_op(de);
-        }
-        if ((dop & 64u) == 0) {
-          const uint32_t dx = dop & 15u;
-          d = e_val(de) + ((uint32_t)(hd >> dused) & ((1u << dx) - 1u));
-          nb = s + dused + dx;
-        }
+        nb = used[i];
+      } else if ((op & 96u) == 0 && (dop & 64u) == 0) {
+        nb = sb[i] + dused + dx;
+        dv[i] = e_val(d) + ((uint32_t)(hd[i] >> dused) & ((1u << dx) - 1u));
       }
+      if (op == 0 || nb == 0) dv[i] = 0;
+      const uint32_t q = P + lane + i * WAVE;
       if (q + nb > limit_bits) nb = 0;
-      lv[i] = l;
-      dv[i] = d;
       if (i < 4) nbp0 |= nb << (8u * i);
       else nbp1 |= nb << (8u * (i - 4u));
     }
-    // 2. the chain from P: up to 64 symbols that start inside the window
-    uint32_t cur = 0, cnt = 0, mypos = 0;
-    while (cnt < WAVE && cur < FW_BITS) {
-      const uint32_t slot = cur >> 6;
-      const uint32_t x = __builtin_amdgcn_readlane(slot < 4u ? nbp0 : nbp1, cur & 63u);
-      const uint32_t nb = (x >> ((slot & 3u) * 8u)) & 0xffu;
-      if (nb == 0) break;
-      if (lane == cnt) mypos = cur;
-      cur += nb;
-      cnt++;
+    [[maybe_unused]] const uint64_t kt1 = KP_NOW();
+    // 2. the chain from P by pointer doubling: J0(q) = q + bits(q) (q itself
+    //    where no symbol may start, and past the window), J(k+1) = Jk o Jk;
+    //    lane m ends with s_m, the start of the chain's m-th symbol
+    //    (s_(2^k + i) = Jk(s_i)).
+    uint16_t *ja = jmp, *jb = jmp + FW_JN;
+#pragma unroll
+    for (uint32_t i = 0; i < FW_OFFS; i++) {
+      const uint32_t q = lane + i * WAVE;
+      const uint32_t nb = ((i < 4 ? nbp0 : nbp1) >> (8u * (i & 3u))) & 0xffu;
+      ja[q] = (uint16_t)(q + nb);
     }
-    if (cnt == 0) return 0;
+    ja[FW_BITS + lane] = (uint16_t)(FW_BITS + lane);
+    __builtin_amdgcn_wave_barrier();
+    uint32_t s = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 6; k++) {
+      const uint32_t half = 1u << k;
+      const uint32_t t = perm(lane >= half ? lane - half : 0u, s);
+      const uint32_t g = ja[t];
+      if (lane >= half && lane < 2u * half) s = g;
+      if (k < 5) {
+#pragma unroll
+        for (uint32_t i = 0; i < FW_OFFS + 1; i++) {
+          const uint32_t q = lane + i * WAVE;
+          jb[q] = ja[ja[q]];
+        }
+        __builtin_amdgcn_wave_barrier();
+        uint16_t *tmp = ja;
+        ja = jb;
+        jb = tmp;
+      }
+    }
+    // a chain symbol: inside the window and decodable (nbits != 0)
+    const uint32_t xs = s < FW_BITS ? s : 0u;
+    const uint32_t px0 = perm(xs & 63u, nbp0), px1 = perm(xs & 63u, nbp1);
+    const uint32_t nbs = (((xs >> 6) < 4u ? px0 : px1) >> (8u * ((xs >> 6) & 3u))) & 0xffu;
+    const uint64_t badc = __ballot(!(s < FW_BITS && nbs != 0));
+    const uint32_t cnt = badc ? (uint32_t)__builtin_ctzll(badc) : WAVE;
+    const uint32_t mypos = s;
+    const uint32_t s63 = __builtin_amdgcn_readlane(s, WAVE - 1);
+    const uint32_t nb63 = __builtin_amdgcn_readlane(nbs, WAVE - 1);
+    const uint32_t cur = cnt < WAVE ? 0u : s63 + nb63;  // chain end when all 64 are symbols
+    [[maybe_unused]] const uint64_t kt2 = KP_NOW();
+    KPW_ADD(KP_W_WINDOWS, 1);
+    KPW_ADD(KP_W_CYC_DECODE, kt1 - kt0);
+    KPW_ADD(KP_W_CYC_CHAIN, kt2 - kt1);
+    if (cnt == 0) {
+      KPW_ADD(KP_W_EMPTY, 1);
+      return 0;
+    }
     // 3. symbol k -> lane k
     const uint32_t src = mypos & 63u, sl = mypos >> 6;
     uint32_t L = 0, D = 0;
@@ -641,50 +714,90 @@ struct Inflater {
     const bool ok = act && incl <= cap - pos && (lit || D <= pos + ost + whave);
     const uint64_t badm = __ballot(!ok);
     const uint32_t n = badm ? (uint32_t)__builtin_ctzll(badm) : WAVE;
-    if (n == 0) return 0;
+    if (n == 0) {
+      KPW_ADD(KP_W_EMPTY, 1);
+      return 0;
+    }
     const uint32_t T = __builtin_amdgcn_readlane(incl, n - 1);
-    const uint32_t endrel = n < cnt ? __builtin_amdgcn_readlane(mypos, n) : cur;
-    // 4. expand 64 output bytes per step
+    const uint32_t endrel = n < WAVE ? __builtin_amdgcn_readlane(mypos, n) : cur;
+    // 4. expand 256 output bytes per step, 4 consecutive per lane: symbol of
+    //    each byte from start marks + a max-scan; copy sources before the step
+    //    read the ring (final), sources inside it resolve by pointer jumping
+    //    through an LDS entry array (0x100 | byte = resolved, else index << 16)
     const uint32_t base = pos;
     uint32_t carry = 0;
-    uint16_t *marks = sorted;  // table-build scratch, idle inside a block
-    for (uint32_t b0 = 0; b0 < T; b0 += WAVE) {
-      marks[lane] = 0;
+    uint16_t *marks = sorted;                            // table-build scratch, idle inside a block
+    uint32_t *ent = reinterpret_cast<uint32_t *>(jmp);   // the jump tables are done with
+    for (uint32_t b0 = 0; b0 < T; b0 += 4u * WAVE) {
+      reinterpret_cast<uint2 *>(marks)[lane] = make_uint2(0u, 0u);
       __builtin_amdgcn_wave_barrier();
-      if (lane < n && ost >= b0 && ost < b0 + WAVE) marks[ost - b0] = (uint16_t)(lane + 1u);
+      if (lane < n && ost >= b0 && ost < b0 + 4u * WAVE) marks[ost - b0] = (uint16_t)(lane + 1u);
       __builtin_amdgcn_wave_barrier();
-      const uint32_t s = max(scan_max(marks[lane]), carry + 1u) - 1u;
-      carry = __builtin_amdgcn_readlane(s, WAVE - 1);
-      const uint32_t j = b0 + lane;
-      const uint32_t Ls = perm(s, L), Ds = perm(s, D);
-      uint32_t val = Ls & 0xffu, ptr = lane;
-      bool res = true;
-      if (!(Ls & 0x80000000u)) {
-        const int32_t sp = (int32_t)j - (int32_t)Ds;  // relative to `base`
-        if (sp < (int32_t)b0) {
-          val = ring[(base + (uint32_t)sp) & RMASK];
-        } else {
-          res = false;
-          ptr = (uint32_t)sp - b0;
-        }
+      const uint2 mk = reinterpret_cast<const uint2 *>(marks)[lane];
+      uint32_t mm[4] = {mk.x & 0xffffu, mk.x >> 16, mk.y & 0xffffu, mk.y >> 16};
+      mm[1] = max(mm[1], mm[0]);
+      mm[2] = max(mm[2], mm[1]);
+      mm[3] = max(mm[3], mm[2]);
+      const uint32_t inc = scan_max(mm[3]);
+      uint32_t prev = perm(lane ? lane - 1u : 0u, inc);
+      prev = max(lane ? prev : 0u, carry + 1u);
+      uint32_t e[4], Ls[4], Ds[4], rv[4];
+      int32_t sp[4];
+      bool open = false;
+#pragma unroll
+      for (uint32_t r = 0; r < 4; r++) {
+        const uint32_t si = max(prev, mm[r]) - 1u;
+        if (r == 3) carry = __builtin_amdgcn_readlane(si, WAVE - 1);
+        Ls[r] = perm(si, L);
+        Ds[r] = perm(si, D);
       }
-      while (__ballot(!res)) {  // pointer jumping, <= 6 rounds
-        const uint32_t pv = perm(ptr, val), pr = perm(ptr, res ? 1u : 0u), pp = perm(ptr, ptr);
-        if (!res) {
-          if (pr) {
-            val = pv;
-            res = true;
-          } else {
-            ptr = pp;
+#pragma unroll
+      for (uint32_t r = 0; r < 4; r++) {
+        sp[r] = (int32_t)(b0 + 4u * lane + r) - (int32_t)Ds[r];  // relative to `base`
+        rv[r] = ring[(base + (uint32_t)sp[r]) & RMASK];
+      }
+#pragma unroll
+      for (uint32_t r = 0; r < 4; r++) {
+        const bool inb = sp[r] >= (int32_t)b0;
+        e[r] = (Ls[r] & 0x80000000u) ? (0x100u | (Ls[r] & 0xffu))
+                                     : (inb ? (((uint32_t)sp[r] - b0) << 16) : (0x100u | rv[r]));
+        open = open || !(e[r] & 0x100u);
+      }
+      if (__ballot(open)) {
+        reinterpret_cast<uint4 *>(ent)[lane] = make_uint4(e[0], e[1], e[2], e[3]);
+        __builtin_amdgcn_wave_barrier();
+        do {
+          KPW_ADD(KP_W_JUMPS, 1);
+          uint32_t g[4];
+#pragma unroll
+          for (uint32_t r = 0; r < 4; r++) g[r] = ent[(e[r] & 0x100u) ? 0u : (e[r] >> 16)];
+          open = false;
+#pragma unroll
+          for (uint32_t r = 0; r < 4; r++) {
+            if (!(e[r] & 0x100u)) e[r] = (g[r] & 0x100u) ? g[r] : (g[r] & 0xffff0000u);
+            open = open || !(e[r] & 0x100u);
           }
-        }
+          __builtin_amdgcn_wave_barrier();
+          reinterpret_cast<uint4 *>(ent)[lane] = make_uint4(e[0], e[1], e[2], e[3]);
+          __builtin_amdgcn_wave_barrier();
+        } while (__ballot(open));
       }
-      if (j < T) ring[(base + j) & RMASK] = (uint8_t)val;
+#pragma unroll
+      for (uint32_t r = 0; r < 4; r++) {
+        const uint32_t j = b0 + 4u * lane + r;
+        if (j < T) ring[(base + j) & RMASK] = (uint8_t)e[r];
+      }
       __builtin_amdgcn_wave_barrier();
-      pos = base + min(T, b0 + WAVE);
+      pos = base + min(T, b0 + 4u * WAVE);
       maybe_flush();
     }
     reseat(P + endrel);
+    [[maybe_unused]] const uint64_t kt3 = KP_NOW();
+    KPW_ADD(KP_W_CYC_EXPAND, kt3 - kt2);
+    KPW_ADD(KP_W_CYC_WINDOW, kt3 - kt0);
+    KPW_ADD(KP_W_SYMS, n);
+    KPW_ADD(KP_W_BYTES, T);
+    KPW_ADD(KP_W_BATCHES, (T + WAVE - 1) / WAVE);
     return n;
   }
 
@@ -725,6 +838,7 @@ struct Inflater {
     const uint32_t lmask = (1u << lbits) - 1, dmask = (1u << dbits) - 1;
     for (;;) {
       if (fast_window(lt, dt, lmask, dmask)) continue;
+      KPW_ADD(KP_W_SERIAL, 1);
       refill();
       r_bit = bitpos();
       uint32_t e = lt[(uint32_t)hold & lmask];
@@ -850,8 +964,9 @@ __global__ void __launch_bounds__(64) zs_decode_kernel(const ZsJobDev *__restric
   __shared__ uint32_t s_tab[TABLE_ENTRIES];
   __shared__ uint32_t s_ftab[544];
   __shared__ uint16_t s_lens[320];
-  __shared__ uint16_t s_sorted[320];
+  __shared__ __attribute__((aligned(16))) uint16_t s_sorted[320];
   __shared__ uint32_t s_scr[32];
+  __shared__ __attribute__((aligned(16))) uint16_t s_jmp[2 * Inflater<D64>::FW_JN];
 
   const uint32_t j = job_ids[blockIdx.x];
   const ZsJobDev jb = jobs[j];
@@ -873,6 +988,7 @@ __global__ void __launch_bounds__(64) zs_decode_kernel(const ZsJobDev *__restric
   f.lens = s_lens;
   f.sorted = s_sorted;
   f.scratch16 = s_scr;
+  f.jmp = s_jmp;
   const uintptr_t ip = reinterpret_cast<uintptr_t>(jb.in);
   const uint32_t mis = (uint32_t)(ip & 15u);
   f.abase = reinterpret_cast<const uint8_t *>(ip - mis);
@@ -887,7 +1003,10 @@ __global__ void __launch_bounds__(64) zs_decode_kernel(const ZsJobDev *__restric
   f.blast = false;
   f.seek((mis + (uint32_t)hd.start_byte) * 8u);
   f.stop_bits = 0;
+  [[maybe_unused]] const uint64_t kt0 = KP_NOW();
   const int packed = f.run(ZSM_TYPE);
+  KPW_ADD(KP_W_WAVES, 1);
+  KPW_ADD(KP_W_CYC_TOTAL, KP_NOW() - kt0);
   const int code = packed & 0xff;
   f.flush_tail();
   res.code = code;
@@ -918,8 +1037,9 @@ __global__ void __launch_bounds__(64) zs_stream_kernel(ZsStreamDev *__restrict__
   __shared__ uint32_t s_tab[TABLE_ENTRIES];
   __shared__ uint32_t s_ftab[544];
   __shared__ uint16_t s_lens[320];
-  __shared__ uint16_t s_sorted[320];
+  __shared__ __attribute__((aligned(16))) uint16_t s_sorted[320];
   __shared__ uint32_t s_scr[32];
+  __shared__ __attribute__((aligned(16))) uint16_t s_jmp[2 * Inflater<D64>::FW_JN];
 
   const uint32_t lane = lane_id();
   const ZsJobDev jb = *job;
@@ -964,6 +1084,7 @@ __global__ void __launch_bounds__(64) zs_stream_kernel(ZsStreamDev *__restrict__
     f.lens = s_lens;
     f.sorted = s_sorted;
     f.scratch16 = s_scr;
+    f.jmp = s_jmp;
     const uintptr_t ip = reinterpret_cast<uintptr_t>(jb.in);
     const uint32_t mis = (uint32_t)(ip & 15u);
     f.abase = reinterpret_cast<const uint8_t *>(ip - mis);
@@ -1293,4 +1414,20 @@ extern "C" void zs_launch_finish(const ZsJobDev *d_jobs, const ZsHeadDev *d_head
   hipLaunchKernelGGL(zs_check_kernel, dim3(njobs, pieces), dim3(CHECK_THREADS), 0, stream, d_jobs, d_heads, d_decs, d_checks);
   hipLaunchKernelGGL(zs_finalize_kernel, dim3((njobs + tb - 1) / tb), dim3(tb), 0, stream, d_jobs, d_heads, d_decs, d_checks,
                      d_res, njobs);
+}
+
+// serial-decoder counters of the profiling build (zs_kprof_read's 64..79)
+extern "C" int zs_kprof_read_w(uint64_t *out16, int reset) {
+#if KP_ON
+  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_kprof_w), 16 * sizeof(uint64_t)) != hipSuccess) return -1;
+  if (reset) {
+    static const unsigned long long z[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_kprof_w), z, sizeof z) != hipSuccess) return -1;
+  }
+  return 16;
+#else
+  (void)out16;
+  (void)reset;
+  return 0;
+#endif
 }

@@ -22,7 +22,11 @@ enum ZsKprof {
   // link (chunk_kernels.hip; its own counter array, copied into 48..63)
   KP_L_STREAMS = 48, KP_L_STEPS, KP_L_CYC_SUCC, KP_L_CYC_WALK, KP_L_CYC_WINWRITE, KP_L_CYC_RESOLVE,
   KP_L_CYC_BARRIER, KP_L_MARKERS, KP_L_CYC_TOTAL, KP_L_CYC_MAX,
-  KP_COUNT = 64
+  KP_COUNT = 64,
+  // serial wave decoder (inflate_kernels.hip; its own array, read into 64..79)
+  KP_W_WAVES = 64, KP_W_CYC_TOTAL, KP_W_WINDOWS, KP_W_EMPTY, KP_W_SYMS, KP_W_BYTES, KP_W_BATCHES, KP_W_JUMPS,
+  KP_W_CYC_DECODE, KP_W_CYC_CHAIN, KP_W_CYC_EXPAND, KP_W_SERIAL, KP_W_CYC_WINDOW,
+  KP_TOTAL = 80
 };
 
 #ifdef ZS_KPROF
