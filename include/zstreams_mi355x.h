@@ -74,8 +74,10 @@ typedef struct zs_job {
   void *out;           /* output buffer (host, or 16-byte aligned device memory) */
   uint64_t out_cap;    /* < 2^32 */
   int32_t window_bits; /* as inflateInit2: -8..-15 raw, -16 raw deflate64, 8..15 zlib, +16 gzip, +32 auto */
-  int32_t reserved;
+  int32_t mode;        /* ZS_JOB_INFLATE (0), or ZS_JOB_COPY: stored bytes (ZIP method 0), output = input */
 } zs_job;
+#define ZS_JOB_INFLATE 0
+#define ZS_JOB_COPY 1
 
 typedef struct zs_result {
   int32_t ret;         /* Z_STREAM_END, Z_DATA_ERROR, Z_BUF_ERROR, Z_NEED_DICT, Z_STREAM_ERROR */
@@ -88,8 +90,32 @@ typedef struct zs_result {
 } zs_result;
 
 #define ZS_F_DEVICE 1u /* job in/out pointers are device (HBM) pointers: no staging copies */
+#define ZS_F_CRC32 2u  /* raw and copy jobs: CRC-32 of the output in adler (ZIP entries; computed on the GPU) */
 
 #define ZS_ENODEV (-100)
+#define ZS_EFORMAT (-101) /* malformed container (zs_zip_scan) */
+#define ZS_EINVAL (-102)  /* bad arguments */
+
+/* ---- ZIP containers (new; generalises src/generator/create_deflate64.cpp:51-93,
+ *      which reads the payload of the first local header) ---- */
+typedef struct zs_zip_entry {
+  uint64_t local_off;   /* local file header */
+  uint64_t data_off;    /* compressed payload */
+  uint64_t comp_size;
+  uint64_t uncomp_size;
+  uint64_t name_off;    /* file name bytes (central directory, or local header) */
+  uint32_t name_len;
+  uint32_t crc32;
+  uint16_t method;      /* 0 stored, 8 deflate (windowBits -15), 9 deflate64 (-16) */
+  uint16_t flags;
+  uint32_t reserved;
+} zs_zip_entry;
+
+/* Lists the entries (central directory incl. ZIP64, else consecutive local
+ * headers).  *n_out = entries in the archive; the first min(cap, n) are written.
+ * Returns 0, ZS_EFORMAT or ZS_EINVAL.  Decode them with zs_inflate_batch
+ * (ZS_F_CRC32; ZS_JOB_COPY for method 0) and compare adler with crc32. */
+int zs_zip_scan(const void *zip, uint64_t len, zs_zip_entry *out, uint32_t cap, uint32_t *n_out);
 
 int zs_inflate_batch(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t flags);
 

@@ -1282,7 +1282,9 @@ __global__ void __launch_bounds__(CHECK_THREADS) zs_check_kernel(const ZsJobDev 
   const uint32_t t = threadIdx.x;
   const ZsHeadDev hd = heads[j];
   const ZsDecDev dc = decs[j];
-  if (hd.code != ZD_END || hd.is_gzip < 0 || dc.code == ZD_SKIP) return;
+  // raw streams are checked only on request (ZIP entries carry a CRC-32)
+  const int kind = hd.is_gzip >= 0 ? hd.is_gzip : ((jobs[j].flags & ZS_JF_CRC32) ? 1 : -1);
+  if (hd.code != ZD_END || kind < 0 || dc.code == ZD_SKIP) return;
   const uint8_t *p = jobs[j].out;
   const uint64_t n = dc.total_out;
   const uint64_t piece = max<uint64_t>(65536u, ((n + gridDim.y - 1) / gridDim.y + 1023u) & ~1023ull);
@@ -1291,7 +1293,7 @@ __global__ void __launch_bounds__(CHECK_THREADS) zs_check_kernel(const ZsJobDev 
   const uint64_t plen = min(piece, n - p0);
   const uint64_t per = ((plen + CHECK_THREADS - 1) / CHECK_THREADS + 3u) & ~3ull;
   const uint64_t lo = p0 + min(plen, per * t), hi = p0 + min(plen, per * (t + 1));
-  if (hd.is_gzip == 1) {
+  if (kind == 1) {
     zs_crc_tables(s_tab);
     const uint32_t v = zs_block_xor(zs_crc_piece(p, lo, hi, n, s_tab), reinterpret_cast<uint32_t *>(s_red));
     if (t == 0 && v) atomicXor(reinterpret_cast<unsigned long long *>(&checks[2 * j]), (unsigned long long)v);
@@ -1341,7 +1343,7 @@ __global__ void zs_finalize_kernel(const ZsJobDev *__restrict__ jobs, const ZsHe
   const ZsDecDev dc = decs[j];
   const bool raw = hd.is_gzip < 0;
   r.total_out = dc.total_out;
-  r.adler = raw ? 0u
+  r.adler = raw ? ((jb.flags & ZS_JF_CRC32) ? zs_crc_final((uint32_t)checks[2 * j], dc.total_out) : 0u)
                 : hd.is_gzip == 1 ? zs_crc_final((uint32_t)checks[2 * j], dc.total_out)
                                   : zs_adler_final(checks[2 * j], checks[2 * j + 1], dc.total_out);
   // (an if-chain, not a switch: hipcc 7.2 dropped the msg copy of the default

@@ -274,7 +274,9 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
   uint32_t nv = 0;
   for (uint32_t i = 0; i < n; i++) {
     ZsJobDev jd{};
-    bool ok = parse_wbits(jobs[i].window_bits, &jd) && jobs[i].in_len < (1ull << 29) &&
+    const bool copy = jobs[i].mode == ZS_JOB_COPY;
+    bool ok = (jobs[i].mode == ZS_JOB_INFLATE || copy) && parse_wbits(copy ? -15 : jobs[i].window_bits, &jd) &&
+              jobs[i].in_len < (1ull << 29) &&
               jobs[i].out_cap < (1ull << 32) && (jobs[i].in || jobs[i].in_len == 0) &&
               (jobs[i].out || jobs[i].out_cap == 0);
     if (dev && jobs[i].out && (reinterpret_cast<uintptr_t>(jobs[i].out) & 15u)) ok = false;
@@ -283,6 +285,7 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
       continue;
     }
     slot[i] = nv;
+    jd.flags = (copy ? ZS_JF_COPY | ZS_JF_CRC32 : 0) | ((flags & ZS_F_CRC32) && jd.wrap == ZW_RAW ? ZS_JF_CRC32 : 0);
     jd.in_len = jobs[i].in_len;
     jd.out_cap = jobs[i].out_cap;
     max_out = std::max<uint64_t>(max_out, jd.out_cap);
@@ -321,14 +324,19 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
   for (uint32_t k = 0; k < nv; k++) {
     const ZsJobDev &jd = g_ws.h_jobs[k];
     const double ratio = jd.in_len ? (double)jd.out_cap / (double)jd.in_len : 0.0;
-    const bool chunk = chunking_enabled() && !jd.d64 && jd.in_len >= 4ull * C && ratio <= 64.0;
+    const bool chunk = chunking_enabled() && !jd.d64 && !(jd.flags & ZS_JF_COPY) && jd.in_len >= 4ull * C && ratio <= 64.0;
     if (chunk) {
       cj_list.push_back(k);
       nseg += (jd.in_len + C - 1) / C;
     }
   }
+  std::vector<uint32_t> copies;  // ZIP stored entries: output = input
   for (uint32_t k = 0; k < nv; k++)
-    if (!g_ws.h_jobs[k].d64 && std::find(cj_list.begin(), cj_list.end(), k) == cj_list.end()) g_ws.h_ids[n_std++] = k;
+    if (g_ws.h_jobs[k].flags & ZS_JF_COPY) copies.push_back(k);
+  for (uint32_t k = 0; k < nv; k++)
+    if (!g_ws.h_jobs[k].d64 && !(g_ws.h_jobs[k].flags & ZS_JF_COPY) &&
+        std::find(cj_list.begin(), cj_list.end(), k) == cj_list.end())
+      g_ws.h_ids[n_std++] = k;
   for (uint32_t k = 0; k < nv; k++)
     if (g_ws.h_jobs[k].d64) g_ws.h_ids[n_std + n_d64++] = k;
   for (uint32_t k : cj_list) g_ws.h_ids[n_std + n_d64 + n_cj++] = k;
@@ -386,6 +394,14 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
   zs_launch_decode(0, g_ws.d_jobs, g_ws.d_heads, g_ws.d_ids, n_std, g_ws.d_decs, nullptr, st);
   zs_launch_decode(1, g_ws.d_jobs, g_ws.d_heads, g_ws.d_ids + n_std, n_d64, g_ws.d_decs, nullptr, st);
   if (n_cj) zs_launch_decode(0, g_ws.d_jobs, g_ws.d_heads, g_ws.d_ids + n_std + n_d64, n_cj, g_ws.d_decs, g_ws.d_fallback, st);
+  std::vector<ZsDecDev> copy_decs(copies.size());
+  for (size_t q = 0; q < copies.size(); q++) {
+    const ZsJobDev &jd = g_ws.h_jobs[copies[q]];
+    const uint64_t m = std::min<uint64_t>(jd.in_len, jd.out_cap);
+    if (m) HIP_OK(hipMemcpyAsync(jd.out, jd.in, m, hipMemcpyDeviceToDevice, st));
+    copy_decs[q] = ZsDecDev{m == jd.in_len ? (int32_t)ZD_END : (int32_t)ZD_FULL, ZM_NONE, m * 8u, m};
+    HIP_OK(hipMemcpyAsync(g_ws.d_decs + copies[q], &copy_decs[q], sizeof(ZsDecDev), hipMemcpyHostToDevice, st));
+  }
   if (ev) HIP_OK(hipEventRecord(ev[7], st));
   zs_launch_finish(g_ws.d_jobs, g_ws.d_heads, g_ws.d_decs, g_ws.d_checks, g_ws.d_res, nv, max_out, st);
   if (ev) HIP_OK(hipEventRecord(ev[8], st));

@@ -55,8 +55,10 @@ struct ZsJobDev {
   int32_t wrap;        // ZsWrap allowed by windowBits (0 raw, 1 zlib, 2 gzip, 3 auto)
   int32_t d64;         // 1 => raw deflate64 (windowBits == -16)
   int32_t wbits;       // window bits after the reset rules (8..16, or 0 = from header)
-  int32_t pad;
+  int32_t flags;       // ZS_JF_*
 };
+#define ZS_JF_CRC32 1  // raw stream: CRC-32 of the output into the result's adler (ZIP entries)
+#define ZS_JF_COPY 2   // stored bytes: output = input (ZIP method 0), checked like a raw stream
 
 // Decoder outcome codes (device -> finalize).
 enum ZsDecCode {

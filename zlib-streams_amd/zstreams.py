@@ -30,6 +30,8 @@ Z_OK, Z_STREAM_END, Z_NEED_DICT = 0, 1, 2
 Z_STREAM_ERROR, Z_DATA_ERROR, Z_MEM_ERROR, Z_BUF_ERROR = -2, -3, -4, -5
 Z_NO_FLUSH, Z_FINISH = 0, 4
 ZS_F_DEVICE = 1
+ZS_F_CRC32 = 2  # raw / copy jobs: CRC-32 of the output in "adler" (ZIP entries)
+ZS_JOB_INFLATE, ZS_JOB_COPY = 0, 1
 
 # windowBits per format, as the reference's init functions choose them
 # (src/wasm/inflate_stream_wasm.c:22-45, inflate9_stream_wasm.c:15-20)
@@ -72,7 +74,14 @@ class ZStreamsError(RuntimeError):
 
 class ZsJob(ctypes.Structure):
     _fields_ = [("in_", ctypes.c_void_p), ("in_len", ctypes.c_uint64), ("out", ctypes.c_void_p),
-                ("out_cap", ctypes.c_uint64), ("window_bits", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                ("out_cap", ctypes.c_uint64), ("window_bits", ctypes.c_int32), ("mode", ctypes.c_int32)]
+
+
+class ZipEntry(ctypes.Structure):
+    _fields_ = [("local_off", ctypes.c_uint64), ("data_off", ctypes.c_uint64), ("comp_size", ctypes.c_uint64),
+                ("uncomp_size", ctypes.c_uint64), ("name_off", ctypes.c_uint64), ("name_len", ctypes.c_uint32),
+                ("crc32", ctypes.c_uint32), ("method", ctypes.c_uint16), ("flags", ctypes.c_uint16),
+                ("reserved", ctypes.c_uint32)]
 
 
 class ZsDJob(ctypes.Structure):
@@ -104,6 +113,9 @@ def lib():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
+        L.zs_zip_scan.restype = ctypes.c_int
+        L.zs_zip_scan.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.POINTER(ZipEntry), ctypes.c_uint32,
+                                  ctypes.POINTER(ctypes.c_uint32)]
         L.zs_inflate_batch.restype = ctypes.c_int
         L.zs_inflate_batch.argtypes = [ctypes.POINTER(ZsJob), ctypes.c_uint32, ctypes.POINTER(ZsResult), ctypes.c_uint32]
         L.zs_deflate_batch.restype = ctypes.c_int
@@ -142,6 +154,90 @@ def inflate_batch(streams, window_bits=-15, out_caps=None):
         jobs[i].window_bits = wbs[i]
     _check(lib().zs_inflate_batch(jobs, n, res, 0))
     return [(outbufs[i].raw[:res[i].total_out], res[i].as_dict()) for i in range(n)]
+
+
+def zip_scan(data):
+    """Entries of a ZIP archive (zs_zip_scan: central directory incl. ZIP64, else
+    local headers as src/generator/create_deflate64.cpp:51-93 reads them).
+    Returns a list of dicts (name, method, offsets, sizes, crc32)."""
+    data = bytes(data)
+    n = ctypes.c_uint32()
+    rc = lib().zs_zip_scan(data, len(data), None, 0, ctypes.byref(n))
+    if rc != 0:
+        raise ZStreamsError(f"zs_zip_scan: malformed archive ({rc})")
+    arr = (ZipEntry * max(n.value, 1))()
+    _check(lib().zs_zip_scan(data, len(data), arr, n.value, ctypes.byref(n)))
+    out = []
+    for e in arr[:n.value]:
+        out.append({"name": data[e.name_off:e.name_off + e.name_len].decode("utf-8", "replace"),
+                    "method": e.method, "flags": e.flags, "local_off": e.local_off, "data_off": e.data_off,
+                    "comp_size": e.comp_size, "uncomp_size": e.uncomp_size, "crc32": e.crc32})
+    return out
+
+
+ZIP_METHOD_WBITS = {8: -15, 9: -16}
+
+
+def unzip(data):
+    """Extract every entry of a ZIP archive on the GPU: deflate (8) and deflate64
+    (9) payloads in ONE batch inflate, stored (0) entries as copy jobs, each
+    output's CRC-32 computed on the GPU and checked against the entry.
+    Returns {name: bytes}; raises ZStreamsError on any bad entry."""
+    data = bytes(data)
+    ents = zip_scan(data)
+    for e in ents:
+        if e["method"] not in (0, 8, 9):
+            raise ZStreamsError(f"{e['name']}: unsupported method {e['method']}")
+    n = len(ents)
+    jobs = (ZsJob * max(n, 1))()
+    res = (ZsResult * max(n, 1))()
+    ib = ctypes.create_string_buffer(data, max(len(data), 1))
+    base = ctypes.addressof(ib)
+    outs = []
+    for i, e in enumerate(ents):
+        ob = ctypes.create_string_buffer(max(e["uncomp_size"], 1))
+        outs.append(ob)
+        jobs[i].in_ = base + e["data_off"]
+        jobs[i].in_len = e["comp_size"]
+        jobs[i].out = ctypes.addressof(ob)
+        jobs[i].out_cap = e["uncomp_size"]
+        jobs[i].window_bits = ZIP_METHOD_WBITS.get(e["method"], -15)
+        jobs[i].mode = ZS_JOB_COPY if e["method"] == 0 else ZS_JOB_INFLATE
+    if n:
+        _check(lib().zs_inflate_batch(jobs, n, res, ZS_F_CRC32))
+    got = {}
+    for i, e in enumerate(ents):
+        r = res[i]
+        if r.ret != Z_STREAM_END or r.total_out != e["uncomp_size"]:
+            raise ZStreamsError(f"{e['name']}: inflate ret {r.ret} "
+                                f"({r.msg.decode() if r.msg else 'size mismatch'}), {r.total_out} of {e['uncomp_size']} bytes")
+        if r.adler != e["crc32"]:
+            raise ZStreamsError(f"{e['name']}: CRC-32 {r.adler:08x} != {e['crc32']:08x}")
+        got[e["name"]] = outs[i].raw[:r.total_out]
+    return got
+
+
+def gunzip_members(data, out_hint=None):
+    """Every member of a multi-member gzip file, each decoded on the GPU (the
+    reference stops after the first member's trailer).  Returns the list of
+    member outputs; a member that fails raises ZStreamsError."""
+    data = bytes(data)
+    outs, off = [], 0
+    while off < len(data):
+        if data[off:off + 2] != b"\x1f\x8b":
+            break  # trailing non-gzip bytes are ignored, as gzip -d does with zeros
+        cap = out_hint or max(1 << 16, 4 * (len(data) - off))
+        while True:
+            (o, r), = inflate_batch([data[off:]], 31, [cap])
+            if r["ret"] == Z_BUF_ERROR and r["total_out"] == cap and cap < (1 << 32) - 1:
+                cap = min(cap * 4, (1 << 32) - 1)
+                continue
+            break
+        if r["ret"] != Z_STREAM_END:
+            raise ZStreamsError(f"gzip member at {off}: ret {r['ret']} {r['msg']}")
+        outs.append(o)
+        off += r["total_in"]
+    return outs
 
 
 def inflate_batch_device(in_ptrs, in_lens, out_ptrs, out_caps, window_bits):
