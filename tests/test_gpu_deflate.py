@@ -95,7 +95,7 @@ def test_deflate_window_bits_and_levels(zs):
 
 def test_deflate_invalid_parameters(zs):
     data = b"hello hello hello"
-    bad = [(-8, 6), (24, 6), (7, 6), (16, 6), (32, 6), (-16, 6), (15, 10), (15, -2)]
+    bad = [(-8, 6), (24, 6), (7, 6), (16, 6), (32, 6), (-17, 6), (15, 10), (15, -2)]
     got = zs.deflate_batch([data] * len(bad), [b[0] for b in bad], [b[1] for b in bad], [64] * len(bad))
     for b, (comp, info) in zip(bad, got):
         assert info["ret"] == -2 and comp == b"", (b, info)

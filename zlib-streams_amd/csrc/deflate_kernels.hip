@@ -80,8 +80,16 @@ __device__ __forceinline__ uint32_t dz_hash(uint32_t v) { return (v * 2654435761
 
 // length 3..258 -> length code index 0..28 and its extra bits (inverse of the
 // lbase/lext tables of src/inftrees.c:59-64)
-__device__ __forceinline__ uint32_t dz_len_sym(uint32_t len, uint32_t *xb, uint32_t *xv) {
+// Deflate64 (inflate9 tables, src/inftrees.c:73-87): code 284 covers 227..258
+// (5 extra bits), code 285 is 3 + a 16-bit extra (lengths 3..65538; used here
+// for merged runs longer than 258).
+__device__ __forceinline__ uint32_t dz_len_sym(uint32_t len, uint32_t *xb, uint32_t *xv, bool d64 = false) {
   const uint32_t l = len - 3u;
+  if (d64 && len >= 258u) {
+    *xb = len == 258u ? 5u : 16u;
+    *xv = len == 258u ? 31u : l;
+    return len == 258u ? 27u : 28u;
+  }
   if (len == 258u) {
     *xb = 0;
     *xv = 0;
@@ -124,7 +132,6 @@ __device__ __forceinline__ uint32_t dz_dist_sym(uint32_t dist, uint32_t *xb, uin
 // last -- the table, and so the output, is deterministic.
 #define DZ_MT 512u
 #define DZ_HALF 32768u
-#define DZ_MWIN (DZ_WIN + DZ_HALF + 288u)  // window bytes: history, the half, matches running past it
 
 __device__ __forceinline__ uint32_t dz_lds32(const uint32_t *w, uint32_t a) {
   return __builtin_amdgcn_alignbyte(w[(a >> 2) + 1], w[a >> 2], a & 3u);
@@ -136,26 +143,35 @@ __device__ __forceinline__ uint4 dz_lds128(const uint32_t *w, uint32_t a) {
                     __builtin_amdgcn_alignbyte(x3, x2, b), __builtin_amdgcn_alignbyte(x4, x3, b));
 }
 
+// Deflate64 (window_bits -16): a 64 KiB window, so one workgroup per QUARTER
+// segment (16 KiB of positions after 64 KiB of history: 80 KiB + the table in
+// LDS); table entries are then positions mod 2^16 (a candidate is rel minus
+// the 16-bit difference; every candidate is verified byte by byte anyway).
+template <bool D64>
 __global__ void __launch_bounds__(DZ_MT) zs_dz_match_kernel(const ZsDJobDev *__restrict__ jobs,
                                                              const ZsDSegDev *__restrict__ segs,
                                                              uint16_t *__restrict__ dist16, uint8_t *__restrict__ len8) {
+  constexpr uint32_t SPAN = D64 ? DZ_HALF / 2u : DZ_HALF;   // positions per workgroup
+  constexpr uint32_t HIST = D64 ? 2u * DZ_WIN : DZ_WIN;     // history before them
+  constexpr uint32_t PARTS = DZ_SEG / SPAN;
   __shared__ uint16_t tab[DZ_HB][DZ_WAYS];
-  __shared__ __attribute__((aligned(16))) uint32_t win[DZ_MWIN / 4 + 8];
+  __shared__ __attribute__((aligned(16))) uint32_t win[(HIST + SPAN + 288u) / 4 + 8];
   const uint32_t tid = threadIdx.x;
-  const ZsDSegDev sg = segs[blockIdx.x >> 1];
-  const uint32_t half = blockIdx.x & 1u;
+  const ZsDSegDev sg = segs[blockIdx.x / PARTS];
+  const uint32_t half = blockIdx.x % PARTS;
   const ZsDJobDev jb = jobs[sg.job];
-  if (jb.level == 0 || half * DZ_HALF >= sg.len) return;  // stored blocks / no positions
+  if ((jb.wbits == 16u) != D64) return;  // the other variant's job
+  if (jb.level == 0 || half * SPAN >= sg.len) return;  // stored blocks / no positions
   gcu8 *in = (gcu8 *)jb.in;
   const uint64_t n = jb.in_len;
-  const uint64_t s = sg.start + half * DZ_HALF;
+  const uint64_t s = sg.start + half * SPAN;
   const uint64_t segend = sg.start + sg.len;  // matches stop at the segment end
-  const uint64_t e = min<uint64_t>(segend, s + DZ_HALF);
-  const uint64_t hs = s > DZ_WIN ? s - DZ_WIN : 0;
+  const uint64_t e = min<uint64_t>(segend, s + SPAN);
+  const uint64_t hs = s > HIST ? s - HIST : 0;
   const uint64_t we = min<uint64_t>(segend, e + 272u);
   // per position: length - 3 (4..258 -> 1..255; 0 = no match) and distance - 1
-  uint16_t *do16 = dist16 + sg.tok + half * DZ_HALF;
-  uint8_t *lo8 = len8 + sg.tok + half * DZ_HALF;
+  uint16_t *do16 = dist16 + sg.tok + half * SPAN;
+  uint8_t *lo8 = len8 + sg.tok + half * SPAN;
   for (uint32_t i = tid; i < DZ_HB * DZ_WAYS / 2; i += DZ_MT) reinterpret_cast<uint32_t *>(tab)[i] = 0u;
   {
     const uint32_t nb = (uint32_t)(we - hs), n16 = (nb + 15u) / 16u;
@@ -181,9 +197,10 @@ __global__ void __launch_bounds__(DZ_MT) zs_dz_match_kernel(const ZsDJobDev *__r
     const bool ok = p < s && p + 4 <= n;
     const uint32_t rel = (uint32_t)(p - hs);
     const uint32_t h = ok ? dz_hash(dz_lds32(win, rel)) : 0u;
-    if (ok && !odd) tab[h][way] = (uint16_t)(rel + 1u);
+    const uint16_t tv = (uint16_t)(D64 ? rel : rel + 1u);
+    if (ok && !odd) tab[h][way] = tv;
     __syncthreads();
-    if (ok && odd) tab[h][way] = (uint16_t)(rel + 1u);
+    if (ok && odd) tab[h][way] = tv;
     __syncthreads();
   }
   const uint32_t maxd = 1u << jb.wbits;
@@ -200,10 +217,17 @@ __global__ void __launch_bounds__(DZ_MT) zs_dz_match_kernel(const ZsDJobDev *__r
       const uint32_t c4[4] = {ent.x & 0xffffu, ent.x >> 16, ent.y & 0xffffu, ent.y >> 16};
 #pragma unroll
       for (uint32_t w = 0; w < DZ_WAYS; w++) {
-        if (!c4[w]) continue;
-        const uint32_t crel = c4[w] - 1u;
-        const uint32_t d = rel - crel;
-        if (crel >= rel || d > maxd) continue;
+        uint32_t crel, d;
+        if (D64) {
+          d = (rel - c4[w]) & 0xffffu;  // 0: empty, or exactly 2^16 back (skipped)
+          if (d == 0 || d > rel) continue;
+          crel = rel - d;
+        } else {
+          if (!c4[w]) continue;
+          crel = c4[w] - 1u;
+          d = rel - crel;
+          if (crel >= rel || d > maxd) continue;
+        }
         uint32_t L = dz_eq16(dz_lds128(win, crel), cur);
         if (L < 4u) continue;
         if (L == 16u) {
@@ -225,11 +249,12 @@ __global__ void __launch_bounds__(DZ_MT) zs_dz_match_kernel(const ZsDJobDev *__r
       lo8[p - s] = (uint8_t)(best >= 4u ? best - 3u : 0u);
       do16[p - s] = (uint16_t)(best >= 4u ? bd - 1u : 0u);
     }
-    const bool ins = ok && rel + 1u <= 0xffffu;
+    const bool ins = ok && (D64 || rel + 1u <= 0xffffu);
+    const uint16_t tv = (uint16_t)(D64 ? rel : rel + 1u);
     __syncthreads();  // every lookup of the step before its inserts
-    if (ins && !odd) tab[h][way] = (uint16_t)(rel + 1u);
+    if (ins && !odd) tab[h][way] = tv;
     __syncthreads();
-    if (ins && odd) tab[h][way] = (uint16_t)(rel + 1u);
+    if (ins && odd) tab[h][way] = tv;
     __syncthreads();
   }
 }
@@ -334,15 +359,86 @@ __global__ void __launch_bounds__(DZ_T) zs_dz_parse_kernel(const ZsDJobDev *__re
 // (S), match starts (a start whose successor position is not a start; the
 // segment end counts as a start), lengths, distances (loaded only for the
 // halves holding a match start) and literal bytes
+// ---------------------------------------------------------------------------
+// D2b (deflate64 only): long copies become ONE code-285 match (3 + a 16-bit
+// extra: lengths up to 65538; src/inftrees.c:73-87).  From every 258-long
+// match at p with distance d, the wave extends the copy while
+// in[p + k] == in[p + k - d] (64 bytes per compare), then absorbs the
+// following tokens that lie wholly inside the extension: their bytes are the
+// copy's bytes, so the output is unchanged.  Absorbed starts leave the start
+// bitmap and x16[p] holds the length beyond 258.  One wave per segment walks
+// its tokens in order from an LDS copy of the bitmap and lengths (a
+// test-vector path, not a hot one).
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(WAVE) zs_dz_merge_kernel(const ZsDJobDev *__restrict__ jobs,
+                                                            const ZsDSegDev *__restrict__ segs,
+                                                            const uint16_t *__restrict__ dist16,
+                                                            const uint8_t *__restrict__ len8, uint32_t *__restrict__ bm,
+                                                            uint16_t *__restrict__ lx16) {
+  __shared__ uint32_t sS[DZ_SEG / 32u];
+  __shared__ __attribute__((aligned(16))) uint8_t sL[DZ_SEG];
+  const uint32_t lane = threadIdx.x;
+  const ZsDSegDev sg = segs[blockIdx.x];
+  const ZsDJobDev jb = jobs[sg.job];
+  if (jb.wbits != 16u || jb.level == 0) return;
+  uint32_t *S = bm + (uint64_t)blockIdx.x * (DZ_SEG / 32u);
+  const uint16_t *d16 = dist16 + sg.tok;
+  uint16_t *x16 = lx16 + sg.tok;
+  const uint8_t *in = jb.in + sg.start;
+  const uint32_t len = sg.len;
+  for (uint32_t k = lane; k < DZ_SEG / 32u; k += WAVE) sS[k] = S[k];
+  for (uint32_t k = lane; k < (len + 15u) / 16u; k += WAVE)
+    reinterpret_cast<uint4 *>(sL)[k] = reinterpret_cast<const uint4 *>(len8 + sg.tok)[k];
+  __syncthreads();
+  auto start = [&](uint32_t q) -> bool { return q >= len || ((sS[q >> 5] >> (q & 31u)) & 1u); };
+  auto tlen = [&](uint32_t q) -> uint32_t { return (q + 1 < len && !start(q + 1)) ? sL[q] + 3u : 1u; };
+  uint32_t p = 0;
+  while (p < len) {  // p is a token start: tokens tile the segment
+    const uint32_t L = tlen(p);
+    if (L != 258u) {
+      p += L;
+      continue;
+    }
+    const uint32_t d = (uint32_t)d16[p] + 1u;
+    const uint32_t lim = min(65538u, len - p);
+    uint32_t M = 258u;
+    while (M < lim) {
+      const uint32_t k = M + lane;
+      const bool bad = k < lim && in[p + k] != in[(int64_t)p + k - d];
+      const uint64_t bm64 = __ballot(bad);
+      if (bm64) {
+        M += (uint32_t)__builtin_ctzll(bm64);
+        break;
+      }
+      M = min(lim, M + WAVE);
+    }
+    uint32_t q = p + 258u;
+    while (q < len) {
+      const uint32_t Lq = tlen(q);
+      if (q + Lq > p + M) break;
+      if (lane == 0) sS[q >> 5] &= ~(1u << (q & 31u));
+      __builtin_amdgcn_wave_barrier();
+      q += Lq;
+    }
+    if (lane == 0) x16[p] = (uint16_t)(q - p - 258u);
+    p = q;
+  }
+  __syncthreads();
+  for (uint32_t k = lane; k < DZ_SEG / 32u; k += WAVE) S[k] = sS[k];
+}
+
 struct DzTok16 {
   uint32_t s16, t16;
   uint4 l8, lit;
   uint4 d[2];
+  uint32_t q0;
+  const uint16_t *x16;  // deflate64: length beyond 258 of merged runs (zs_dz_merge_kernel), else null
 };
 __device__ __forceinline__ void dz_load_tok16(DzTok16 &k, gcu32 *bS, gcu8 *l8, const uint16_t *d16, gcu8 *in, uint32_t q0,
                                               uint32_t len) {
   k.s16 = 0;
   k.t16 = 0;
+  k.q0 = q0;
   if (q0 >= len) return;
   const uint32_t w = bS[q0 >> 5];
   const uint32_t sh = q0 & 16u;
@@ -369,13 +465,15 @@ __device__ __forceinline__ uint32_t dz_u4_byte(uint4 v, uint32_t i) {
   const uint32_t w = i < 4 ? v.x : i < 8 ? v.y : i < 12 ? v.z : v.w;
   return (w >> (8u * (i & 3u))) & 0xffu;
 }
-// the token word at position i: (length << 16) | (distance - 1), or the literal
+// the token word at position i: ((length - 2) << 16) | (distance - 1), or the literal
 __device__ __forceinline__ uint32_t dz_tok16_at(const DzTok16 &k, uint32_t i) {
   if ((k.t16 >> i) & 1u) {
     const uint4 dv = k.d[i >> 3];
     const uint32_t j = i & 7u;
     const uint32_t w = j < 2 ? dv.x : j < 4 ? dv.y : j < 6 ? dv.z : dv.w;
-    return ((dz_u4_byte(k.l8, i) + 3u) << 16) | ((w >> (16u * (j & 1u))) & 0xffffu);
+    uint32_t L = dz_u4_byte(k.l8, i) + 3u;
+    if (k.x16 && L == 258u) L += k.x16[k.q0 + i];
+    return ((L - 2u) << 16) | ((w >> (16u * (j & 1u))) & 0xffffu);
   }
   return dz_u4_byte(k.lit, i);
 }
@@ -397,10 +495,12 @@ __device__ __forceinline__ uint32_t dz_tok16_at(const DzTok16 &k, uint32_t i) {
 //                       is flushed to the segment's output after every chunk.
 // ---------------------------------------------------------------------------
 #define NL 286
-#define ND 30
+#define ND 32  // 30 deflate distance codes + deflate64's 30/31 (zero for deflate streams)
 #define NC 19
-#define DZ_HROWS 320u  // histogram rows per segment (SoA): lit/len 0..285, dist 286..315, extra bits 316, fixed bits 317
-#define DZ_CROW 320u   // code words per segment (AoS): lit/len 0..285, dist 286..315 (code | len << 16, code bit-reversed)
+#define DZ_HROWS 320u  // histogram rows per segment (SoA): lit/len 0..285, dist 286..317, extra bits 318, fixed bits 319
+#define DZ_ROW_XBITS (NL + ND)
+#define DZ_ROW_FIX (NL + ND + 1)
+#define DZ_CROW 320u   // code words per segment (AoS): lit/len 0..285, dist 286..317 (code | len << 16, code bit-reversed)
 #define DZ_HDRW 192u   // header words per segment (AoS); word 191 = header bit count
 #define DZ_SCR 2400u   // build scratch rows per segment (SoA)
 #define DZ_AUXW (DZ_HROWS + DZ_CROW + DZ_HDRW + DZ_SCR)  // aux words per segment
@@ -430,7 +530,7 @@ __device__ __forceinline__ uint32_t dz_scan_excl(uint32_t v, uint32_t *s_tmp, ui
 }
 
 __device__ __forceinline__ uint32_t dz_tok_bits(uint32_t tk, const uint32_t *cl, const uint32_t *cd, uint32_t *v0,
-                                                uint32_t *n0, uint32_t *v1, uint32_t *n1) {
+                                                uint32_t *n0, uint32_t *v1, uint32_t *n1, bool d64) {
   // returns total bits; emits as up to two (value, bits) pieces of <= 32 bits
   if ((tk >> 16) == 0) {
     const uint32_t c = cl[tk & 0xffu];
@@ -441,13 +541,13 @@ __device__ __forceinline__ uint32_t dz_tok_bits(uint32_t tk, const uint32_t *cl,
     return *n0;
   }
   uint32_t lx, lv, dx, dv;
-  const uint32_t ls = dz_len_sym(tk >> 16, &lx, &lv);
+  const uint32_t ls = dz_len_sym((tk >> 16) + 2u, &lx, &lv, d64);
   const uint32_t ds = dz_dist_sym((tk & 0xffffu) + 1u, &dx, &dv);
   const uint32_t c1 = cl[257 + ls], c2 = cd[ds];
   const uint32_t b1 = c1 >> 16, b2 = c2 >> 16;
-  *v0 = (c1 & 0xffffu) | (lv << b1);  // <= 15 + 5 bits
+  *v0 = (c1 & 0xffffu) | (lv << b1);  // <= 15 + 16 bits
   *n0 = b1 + lx;
-  *v1 = (c2 & 0xffffu) | (dv << b2);  // <= 15 + 13 bits
+  *v1 = (c2 & 0xffffu) | (dv << b2);  // <= 15 + 14 bits
   *n1 = b2 + dx;
   return *n0 + *n1;
 }
@@ -464,7 +564,7 @@ __device__ __forceinline__ void dz_put_ring(uint32_t *ring, uint32_t bit, uint32
 __global__ void __launch_bounds__(DZ_T) zs_dz_hist_kernel(const ZsDJobDev *__restrict__ jobs, const ZsDSegDev *__restrict__ segs,
                                                            uint32_t nseg, const uint16_t *__restrict__ dist16,
                                                            const uint8_t *__restrict__ len8, const uint32_t *__restrict__ bm,
-                                                           uint32_t *__restrict__ hist) {
+                                                           uint32_t *__restrict__ hist, const uint16_t *__restrict__ lx16) {
   __shared__ uint32_t fl[NL + 2], fd[ND + 2];
   __shared__ uint64_t s_red[16];
   const uint32_t t = threadIdx.x;
@@ -480,8 +580,11 @@ __global__ void __launch_bounds__(DZ_T) zs_dz_hist_kernel(const ZsDJobDev *__res
   if (t < ND + 2) fd[t] = 0;
   __syncthreads();
   uint32_t xbits = 0, fix = 0;  // length/distance extra bits; fixed-code cost
+  const bool d64 = jb.wbits == 16u;
+  const uint16_t *x16 = d64 ? lx16 + sg.tok : nullptr;
   for (uint32_t c = 0; c < nch; c++) {
     DzTok16 k;
+    k.x16 = x16;
     dz_load_tok16(k, bS, l8, d16, in, c * 4096u + 16u * t, sg.len);
 #pragma unroll
     for (uint32_t i = 0; i < 16; i++) {
@@ -492,7 +595,7 @@ __global__ void __launch_bounds__(DZ_T) zs_dz_hist_kernel(const ZsDJobDev *__res
         fix += x < 144u ? 8u : 9u;
       } else {
         uint32_t lx, lv, dx, dv;
-        const uint32_t ls = dz_len_sym(x >> 16, &lx, &lv);
+        const uint32_t ls = dz_len_sym((x >> 16) + 2u, &lx, &lv, d64);
         atomicAdd(&fl[257 + ls], 1u);
         atomicAdd(&fd[dz_dist_sym((x & 0xffffu) + 1u, &dx, &dv)], 1u);
         xbits += lx + dx;
@@ -506,8 +609,8 @@ __global__ void __launch_bounds__(DZ_T) zs_dz_hist_kernel(const ZsDJobDev *__res
   for (uint32_t i = t; i < NL; i += DZ_T) h[(uint64_t)i * nseg] = i == 256 ? 1u : fl[i];  // one end-of-block
   if (t < ND) h[(uint64_t)(NL + t) * nseg] = fd[t];
   if (t == 0) {
-    h[(uint64_t)316 * nseg] = (uint32_t)xs;
-    h[(uint64_t)317 * nseg] = (uint32_t)fs;
+    h[(uint64_t)DZ_ROW_XBITS * nseg] = (uint32_t)xs;
+    h[(uint64_t)DZ_ROW_FIX * nseg] = (uint32_t)fs;
   }
 }
 
@@ -521,8 +624,8 @@ struct DzRows {  // SoA rows of one segment
 #define DZS_TMP 288u
 #define DZS_W 576u
 #define DZS_P 1152u
-#define DZS_LEN 1728u  // lit/len 1728..2013, dist 2014..2043, code-length 2044..2062
-#define DZS_RLE 2064u  // header symbols: sym | extra << 8
+#define DZS_LEN 1728u  // lit/len 1728..2013, dist 2014..2045, code-length 2046..2064
+#define DZS_RLE 2068u  // header symbols: sym | extra << 8
 
 // Code lengths (1..maxbits, 0 = unused) of the n frequencies freq(i) into
 // scratch rows LEN0 .. LEN0 + n: at least two symbols used (trees.c:610-620),
@@ -725,10 +828,10 @@ __global__ void __launch_bounds__(WAVE) zs_dz_codes_kernel(const ZsDJobDev *__re
     const uint32_t sym = S[DZS_RLE + i] & 0xffu;
     hb += (cc[sym] >> 16) + (sym == 16 ? 2u : sym == 17 ? 3u : sym == 18 ? 7u : 0u);
   }
-  uint64_t dyn = (uint64_t)hb + H[316];
+  uint64_t dyn = (uint64_t)hb + H[DZ_ROW_XBITS];
   for (uint32_t i = 0; i < NL; i++) dyn += (uint64_t)H[i] * S[DZS_LEN + i];
   for (uint32_t i = 0; i < ND; i++) dyn += (uint64_t)H[NL + i] * S[DZS_LEN + NL + i];
-  const uint64_t fix = 3ull + H[317] + 7ull;
+  const uint64_t fix = 3ull + H[DZ_ROW_FIX] + 7ull;
   DzBitW bw{HB, 0, 0, 0};
   bw.put(sg.last ? 1u : 0u, 1);
   if (dyn < fix) {
@@ -766,7 +869,8 @@ __global__ void __launch_bounds__(WAVE) zs_dz_codes_kernel(const ZsDJobDev *__re
 __global__ void __launch_bounds__(DZ_T) zs_dz_emit_kernel(const ZsDJobDev *__restrict__ jobs, ZsDSegDev *__restrict__ segs,
                                                            uint32_t nseg, const uint16_t *__restrict__ dist16,
                                                            const uint8_t *__restrict__ len8, const uint32_t *__restrict__ bm,
-                                                           const uint32_t *__restrict__ aux, uint32_t *__restrict__ obuf) {
+                                                           const uint32_t *__restrict__ aux, uint32_t *__restrict__ obuf,
+                                                           const uint16_t *__restrict__ lx16) {
   __shared__ uint32_t ring[DZ_RING];
   __shared__ uint32_t s_cl[NL + 2], s_cd[ND + 2];
   __shared__ uint32_t s_scan[DZ_T / WAVE + 1];
@@ -808,15 +912,18 @@ __global__ void __launch_bounds__(DZ_T) zs_dz_emit_kernel(const ZsDJobDev *__res
   gcu32 *bS = (gcu32 *)(bm + (uint64_t)blockIdx.x * DZ_BMW);
   const uint32_t nch = (sg.len + 4095u) / 4096u;
   uint32_t base = hbits, flushed = 0;  // bits emitted; words written to gout
+  const bool d64 = jb.wbits == 16u;
+  const uint16_t *x16 = d64 ? lx16 + sg.tok : nullptr;
   for (uint32_t c = 0; c < nch; c++) {
     DzTok16 k;
+    k.x16 = x16;
     dz_load_tok16(k, bS, l8, d16, in, c * 4096u + 16u * t, sg.len);
     uint32_t nb = 0;
 #pragma unroll
     for (uint32_t i = 0; i < 16; i++) {
       if (!((k.s16 >> i) & 1u)) continue;
       uint32_t v0, n0, v1, n1;
-      nb += dz_tok_bits(dz_tok16_at(k, i), s_cl, s_cd, &v0, &n0, &v1, &n1);
+      nb += dz_tok_bits(dz_tok16_at(k, i), s_cl, s_cd, &v0, &n0, &v1, &n1, d64);
     }
     uint32_t all;
     uint32_t off = dz_scan_excl(nb, s_scan, &all) + base;
@@ -824,7 +931,7 @@ __global__ void __launch_bounds__(DZ_T) zs_dz_emit_kernel(const ZsDJobDev *__res
     for (uint32_t i = 0; i < 16; i++) {
       if (!((k.s16 >> i) & 1u)) continue;
       uint32_t v0, n0, v1, n1;
-      dz_tok_bits(dz_tok16_at(k, i), s_cl, s_cd, &v0, &n0, &v1, &n1);
+      dz_tok_bits(dz_tok16_at(k, i), s_cl, s_cd, &v0, &n0, &v1, &n1, d64);
       dz_put_ring(ring, off, v0, n0);
       dz_put_ring(ring, off + n0, v1, n1);
       off += n0 + n1;
@@ -994,18 +1101,24 @@ __global__ void zs_dz_trailer_kernel(const ZsDJobDev *__restrict__ jobs, uint32_
 // launcher
 // ---------------------------------------------------------------------------
 // per segment: d_dist16 / d_len8 DZ_SEG entries, d_bm DZ_BMW bitmap words, d_aux DZ_AUXW words
+// d_lx16: DZ_SEG u16 per segment when the batch has deflate64 jobs (has_d64), else unused
 extern "C" void zs_launch_deflate(ZsDJobDev *d_jobs, uint32_t njobs, ZsDSegDev *d_segs, uint32_t nseg, uint16_t *d_dist16,
                                   uint8_t *d_len8, uint32_t *d_bm, uint32_t *d_aux, uint32_t *d_obuf, uint8_t *d_stage,
-                                  hipStream_t st, hipEvent_t *ev) {
+                                  uint16_t *d_lx16, int has_std, int has_d64, hipStream_t st, hipEvent_t *ev) {
   if (ev) (void)hipEventRecord(ev[0], st);
-  hipLaunchKernelGGL(zs_dz_match_kernel, dim3(2 * nseg), dim3(DZ_MT), 0, st, d_jobs, d_segs, d_dist16, d_len8);
+  if (has_std)
+    hipLaunchKernelGGL(zs_dz_match_kernel<false>, dim3(2 * nseg), dim3(DZ_MT), 0, st, d_jobs, d_segs, d_dist16, d_len8);
+  if (has_d64)
+    hipLaunchKernelGGL(zs_dz_match_kernel<true>, dim3(4 * nseg), dim3(DZ_MT), 0, st, d_jobs, d_segs, d_dist16, d_len8);
   if (ev) (void)hipEventRecord(ev[1], st);
   hipLaunchKernelGGL(zs_dz_parse_kernel, dim3(nseg), dim3(DZ_T), 0, st, d_jobs, d_segs, d_len8, d_bm);
+  if (has_d64) hipLaunchKernelGGL(zs_dz_merge_kernel, dim3(nseg), dim3(64), 0, st, d_jobs, d_segs, d_dist16, d_len8, d_bm, d_lx16);
   if (ev) (void)hipEventRecord(ev[2], st);
-  hipLaunchKernelGGL(zs_dz_hist_kernel, dim3(nseg), dim3(DZ_T), 0, st, d_jobs, d_segs, nseg, d_dist16, d_len8, d_bm, d_aux);
+  hipLaunchKernelGGL(zs_dz_hist_kernel, dim3(nseg), dim3(DZ_T), 0, st, d_jobs, d_segs, nseg, d_dist16, d_len8, d_bm, d_aux,
+                     d_lx16);
   hipLaunchKernelGGL(zs_dz_codes_kernel, dim3((nseg + WAVE - 1) / WAVE), dim3(WAVE), 0, st, d_jobs, d_segs, nseg, d_aux);
   hipLaunchKernelGGL(zs_dz_emit_kernel, dim3(nseg), dim3(DZ_T), 0, st, d_jobs, d_segs, nseg, d_dist16, d_len8, d_bm, d_aux,
-                     d_obuf);
+                     d_obuf, d_lx16);
   hipLaunchKernelGGL(zs_dz_check_kernel, dim3(nseg), dim3(DZ_T), 0, st, d_jobs, d_segs);
   if (ev) (void)hipEventRecord(ev[3], st);
   hipLaunchKernelGGL(zs_dz_offsets_kernel, dim3(njobs), dim3(DZ_JT), 0, st, d_jobs, d_segs, d_stage);

@@ -34,7 +34,7 @@ extern "C" void zs_launch_fixed_tables(uint32_t *fixed, hipStream_t st);
 extern "C" void zs_launch_fixed_compact(uint32_t *fixed, hipStream_t st);
 extern "C" void zs_launch_deflate(ZsDJobDev *d_jobs, uint32_t njobs, ZsDSegDev *d_segs, uint32_t nseg, uint16_t *d_dist16,
                                   uint8_t *d_len8, uint32_t *d_bm, uint32_t *d_aux, uint32_t *d_obuf, uint8_t *d_stage,
-                                  hipStream_t st, hipEvent_t *ev);
+                                  uint16_t *d_lx16, int has_std, int has_d64, hipStream_t st, hipEvent_t *ev);
 extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, ZsSegDev *d_segs, uint32_t nseg,
                                   ZsCJobDev *d_cjobs, uint32_t ncjobs, ZsChunkDev *d_units, uint32_t nunit_slots,
                                   uint16_t *d_scratch, uint32_t *d_tokens, uint32_t *d_tables, const uint32_t *d_fixed,
@@ -727,7 +727,8 @@ struct DzWorkspace {
   uint16_t *d_tok = nullptr;  // distance - 1 per position
   uint32_t *d_obuf = nullptr, *d_bm = nullptr, *d_aux = nullptr;
   uint8_t *d_len8 = nullptr;
-  size_t cap_bm = 0, cap_len8 = 0, cap_aux = 0;
+  uint16_t *d_lx16 = nullptr;  // deflate64 merged-run lengths (batches with deflate64 jobs)
+  size_t cap_bm = 0, cap_len8 = 0, cap_aux = 0, cap_lx16 = 0;
   uint8_t *d_stage = nullptr, *d_in = nullptr;
   hipEvent_t ev[5] = {};
   double stage_ms[4] = {};
@@ -789,7 +790,11 @@ int deflate_batch_locked(const zs_djob *jobs, uint32_t n, zs_result *results, ui
     int wrap = 0;
     uint32_t w = 15;
     int level = jobs[i].level == Z_DEFAULT_COMPRESSION ? 6 : jobs[i].level;
-    const bool ok = parse_dz_wbits(jobs[i].window_bits, &wrap, &w) && level >= 0 && level <= 9 &&
+    // -16: raw deflate64 (64 KiB window, code 285 runs; a batch-API extension,
+    // the reference has no deflate64 compressor)
+    const bool d64 = jobs[i].window_bits == -16;
+    if (d64) w = 16;
+    const bool ok = (d64 || parse_dz_wbits(jobs[i].window_bits, &wrap, &w)) && level >= 0 && level <= 9 &&
                     jobs[i].in_len < (1ull << 32) && (jobs[i].in || jobs[i].in_len == 0) &&
                     (jobs[i].out || jobs[i].out_cap == 0);
     if (!ok) {
@@ -816,7 +821,10 @@ int deflate_batch_locked(const zs_djob *jobs, uint32_t n, zs_result *results, ui
     g_dz.h_jobs[nv++] = jd;
   }
   if (nv == 0) return 0;
+  int has_std = 0, has_d64 = 0;
+  for (uint32_t k = 0; k < nv; k++) (g_dz.h_jobs[k].wbits == 16 ? has_d64 : has_std) = 1;
   hipStream_t st = g_ws.stream;
+  if (has_d64 && (r = dz_grow(&g_dz.d_lx16, &g_dz.cap_lx16, nseg * DZ_SEG_HOST))) return r;
   if (nseg > g_dz.cap_segs) {
     const size_t c = std::max(nseg, g_dz.cap_segs + g_dz.cap_segs / 2);
     if ((r = grow_dev(&g_dz.d_segs, c)) || (r = grow_host(&g_dz.h_segs, c))) return r;
@@ -861,8 +869,8 @@ int deflate_batch_locked(const zs_djob *jobs, uint32_t n, zs_result *results, ui
       for (int i = 0; i < 5; i++) HIP_OK(hipEventCreate(&g_dz.ev[i]));
     ev = g_dz.ev;
   }
-  zs_launch_deflate(g_dz.d_jobs, nv, g_dz.d_segs, (uint32_t)nseg, g_dz.d_tok, g_dz.d_len8, g_dz.d_bm, g_dz.d_aux, g_dz.d_obuf, g_dz.d_stage, st,
-                    ev);
+  zs_launch_deflate(g_dz.d_jobs, nv, g_dz.d_segs, (uint32_t)nseg, g_dz.d_tok, g_dz.d_len8, g_dz.d_bm, g_dz.d_aux, g_dz.d_obuf,
+                    g_dz.d_stage, g_dz.d_lx16, has_std, has_d64, st, ev);
   {
     hipError_t le = hipGetLastError();
     if (le != hipSuccess) {

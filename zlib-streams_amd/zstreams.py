@@ -270,7 +270,7 @@ def deflate_batch(streams, window_bits=-15, level=-1, out_caps=None):
     wbs = window_bits if isinstance(window_bits, (list, tuple)) else [window_bits] * n
     lvs = level if isinstance(level, (list, tuple)) else [level] * n
     if out_caps is None:
-        out_caps = [deflate_bound(len(s), wbs[i]) if -15 <= wbs[i] <= 31 else 64 for i, s in enumerate(streams)]
+        out_caps = [deflate_bound(len(s), wbs[i]) if -16 <= wbs[i] <= 31 else 64 for i, s in enumerate(streams)]
     jobs = (ZsDJob * max(n, 1))()
     res = (ZsResult * max(n, 1))()
     inbufs, outbufs = [], []
