@@ -191,16 +191,29 @@ __global__ void __launch_bounds__(DZ_MT) zs_dz_match_kernel(const ZsDJobDev *__r
   __syncthreads();
   const uint32_t way = (tid >> 7) & 3u;
   const bool odd = (tid >> 6) & 1u;
-  // prime with the history
-  for (uint64_t P = hs; P < s; P += DZ_MT) {
-    const uint64_t p = P + tid;
-    const bool ok = p < s && p + 4 <= n;
-    const uint32_t rel = (uint32_t)(p - hs);
-    const uint32_t h = ok ? dz_hash(dz_lds32(win, rel)) : 0u;
-    const uint16_t tv = (uint16_t)(D64 ? rel : rel + 1u);
-    if (ok && !odd) tab[h][way] = tv;
+  // prime with the history: 4 consecutive positions per thread and step (a
+  // thread's stores land in order, the even wave of a pair before the odd)
+  for (uint64_t P = hs; P < s; P += 4u * DZ_MT) {
+    uint32_t hh[4];
+    uint16_t tv[4];
+    bool okk[4];
+#pragma unroll
+    for (uint32_t r = 0; r < 4; r++) {
+      const uint64_t p = P + 4u * tid + r;
+      okk[r] = p < s && p + 4 <= n;
+      const uint32_t rel = (uint32_t)(p - hs);
+      hh[r] = okk[r] ? dz_hash(dz_lds32(win, rel)) : 0u;
+      tv[r] = (uint16_t)(D64 ? rel : rel + 1u);
+    }
+    if (!odd)
+#pragma unroll
+      for (uint32_t r = 0; r < 4; r++)
+        if (okk[r]) tab[hh[r]][way] = tv[r];
     __syncthreads();
-    if (ok && odd) tab[h][way] = tv;
+    if (odd)
+#pragma unroll
+      for (uint32_t r = 0; r < 4; r++)
+        if (okk[r]) tab[hh[r]][way] = tv[r];
     __syncthreads();
   }
   const uint32_t maxd = 1u << jb.wbits;
@@ -228,6 +241,7 @@ __global__ void __launch_bounds__(DZ_MT) zs_dz_match_kernel(const ZsDJobDev *__r
           d = rel - crel;
           if (crel >= rel || d > maxd) continue;
         }
+        if (dz_lds32(win, crel) != cur.x) continue;  // 2 LDS words reject most candidates (hash collisions)
         uint32_t L = dz_eq16(dz_lds128(win, crel), cur);
         if (L < 4u) continue;
         if (L == 16u) {
