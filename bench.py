@@ -416,6 +416,7 @@ def compress_leg(args, zstreams, shard, torch, np, dev, dist, raws, d_out, raw_p
     # round trip: GPU inflate of the GPU gzip streams into the zeroed raw buffers
     d_out.zero_()
     back = zstreams.inflate_batch_device(cz_ptrs, sizes, raw_ptrs, [nbytes] * n, 31)
+    rt_stats = zstreams.last_stats()
     torch.cuda.synchronize()
     ok = ok and all(b["ret"] == 1 and b["total_out"] == nbytes and b["adler"] == r["adler"]
                     for b, r in zip(back, res))
@@ -434,7 +435,7 @@ def compress_leg(args, zstreams, shard, torch, np, dev, dist, raws, d_out, raw_p
            "workload": f"{n}x{nbytes >> 20}MiB gzip (windowBits 31) level {level} deflate, inputs resident in HBM",
            "compressed_bytes": comp_total, "ratio": round(n * nbytes / comp_total, 3),
            "zlib_l6_bytes": zlib_total, "size_vs_zlib_l6": round(comp_total / zlib_total, 4),
-           "roundtrip_verified": ok,
+           "roundtrip_verified": ok, "roundtrip_path_stats": rt_stats,
            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(achieved / HBM_PEAK_GBS, 5), "kernel": "deflate pipeline",
                         "kernel_ms_avg": round(k_avg_s * 1e3, 3), "alg_bytes_per_launch": alg,

@@ -231,3 +231,21 @@ def test_chunked_random_and_stored(zs):
     got = zs.inflate_batch(comps, -15, [len(raw)] * 3)
     for (out, info), comp in zip(got, comps):
         assert info["ret"] == 1 and info["total_in"] == len(comp) and out == raw
+
+
+def test_chunked_capacity_retry(zs):
+    """Blocks far more compressible than their stream (random bytes, then line
+    text): units outgrow 2 x span x ratio, the chain breaks, and the jobs get a
+    second chunked pass with 8x capacity instead of the serial decoder."""
+    import numpy as np
+    rng = np.random.default_rng(11)
+    raw = rng.integers(0, 256, 4 << 20, dtype=np.uint8).tobytes() + corpus.stream(41, 4 << 20)
+    streams, outs = [], []
+    for wb in (-15, 31):
+        c = zlib.compressobj(6, zlib.DEFLATED, wb)
+        streams.append(c.compress(raw) + c.flush())
+    got = zs.inflate_batch(streams, [-15, 31], [len(raw)] * 2)
+    st = zs.last_stats()
+    for (out, info), comp in zip(got, streams):
+        assert info["ret"] == 1 and info["total_in"] == len(comp) and out == raw
+    assert st["chunked_jobs"] == 2 and st["fallback_jobs"] == 0, st

@@ -371,7 +371,7 @@ __global__ void __launch_bounds__(PLAN_T) zs_plan_kernel(const ZsJobDev *__restr
         st = units[cj.unit0 + i].start_bit;
         sp = i + 1 < nunits ? units[cj.unit0 + i + 1].start_bit : ZS_NONE;
         const uint32_t span_bytes = ((sp == ZS_NONE ? end_bit : sp) - st + 7u) / 8u;
-        cap = ((uint64_t)(2.0 * span_bytes * ratio) + UNIT_SLACK + 7u) & ~7ull;
+        cap = ((uint64_t)((double)cj.cap_mul * span_bytes * ratio) + UNIT_SLACK + 7u) & ~7ull;
         if (cap > 0xfff00000ull) cap = 0xfff00000ull;
       }
       // exclusive u64 prefix of the capacities (thread 0 walks the tile)

@@ -319,7 +319,7 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
   // the wave-per-stream serial decoder.  Lists in h_ids: [serial std | d64 | chunked].
   const uint32_t C = chunk_bytes();
   uint32_t n_std = 0, n_d64 = 0, n_cj = 0;
-  size_t nseg = 0, nunit_slots = 0, scratch_need = 0;
+  size_t nseg = 0, nunit_slots = 0;
   std::vector<uint32_t> cj_list;
   for (uint32_t k = 0; k < nv; k++) {
     const ZsJobDev &jd = g_ws.h_jobs[k];
@@ -340,27 +340,35 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
   for (uint32_t k = 0; k < nv; k++)
     if (g_ws.h_jobs[k].d64) g_ws.h_ids[n_std + n_d64++] = k;
   for (uint32_t k : cj_list) g_ws.h_ids[n_std + n_d64 + n_cj++] = k;
-  if (n_cj) {
-    if ((r = ws_reserve_chunks(nseg, 0, 0))) return r;
-    size_t si = 0;
-    for (uint32_t q = 0; q < n_cj; q++) {
-      const uint32_t k = cj_list[q];
+  // Plan the chunked jobs of `list` (segments, unit slots, scratch ranges) and
+  // upload them.  cap_mul scales each unit's output capacity (cap_mul x span x
+  // ratio + slack, zs_plan_kernel).
+  size_t nunit_slots_max = 0;
+  auto plan_chunked = [&](const std::vector<uint32_t> &list, uint32_t cap_mul, size_t *nseg_out, size_t *nslots_out) -> int {
+    size_t ns_total = 0;
+    for (uint32_t k : list) ns_total += (g_ws.h_jobs[k].in_len + C - 1) / C;
+    int rr;
+    if ((rr = ws_reserve_chunks(ns_total, 0, 0))) return rr;
+    size_t si = 0, slots = 0, need = 0;
+    for (uint32_t q = 0; q < list.size(); q++) {
+      const uint32_t k = list[q];
       const ZsJobDev &jd = g_ws.h_jobs[k];
       const uint32_t ns = (uint32_t)((jd.in_len + C - 1) / C);
       const double ratio = std::max(1.0, (double)jd.out_cap / (double)jd.in_len);
       const uint32_t max_units = ns * SEG_SLOTS + 1;
-      // zs_plan_kernel gives each unit 2 x span x ratio + slack entries; spans
-      // of a job's units sum to at most its input (+1 byte of rounding each)
-      const size_t reserve = (size_t)(2.0 * ratio * ((double)jd.in_len + max_units)) +
+      // zs_plan_kernel gives each unit cap_mul x span x ratio + slack entries;
+      // spans of a job's units sum to at most its input (+1 byte of rounding each)
+      const size_t reserve = (size_t)(cap_mul * ratio * ((double)jd.in_len + max_units)) +
                              (size_t)max_units * ((size_t)UNIT_SLACK_HOST + 8) + 64;
       ZsCJobDev cj{};
       cj.job = k;
       cj.first_seg = (uint32_t)si;
       cj.nseg = ns;
-      cj.unit0 = (uint32_t)nunit_slots;
+      cj.unit0 = (uint32_t)slots;
       cj.max_units = max_units;
-      cj.scratch0 = scratch_need;
+      cj.scratch0 = need;
       cj.scratch_n = reserve;
+      cj.cap_mul = cap_mul;
       g_ws.h_cjobs[q] = cj;
       for (uint32_t o = 0; o < ns; o++, si++) {
         ZsSegDev sg{};
@@ -371,25 +379,48 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
         sg.final_ok = o + 2 >= ns;  // the final block lies within the last segments
         g_ws.h_segs[si] = sg;
       }
-      nunit_slots += max_units;
-      scratch_need += (reserve + 7) & ~size_t(7);
+      slots += max_units;
+      need += (reserve + 7) & ~size_t(7);
     }
-    if ((r = ws_reserve_chunks(nseg, nunit_slots, scratch_need))) return r;
-    HIP_OK(hipMemcpyAsync(g_ws.d_segs, g_ws.h_segs, nseg * sizeof(ZsSegDev), hipMemcpyHostToDevice, st));
-    HIP_OK(hipMemcpyAsync(g_ws.d_cjobs, g_ws.h_cjobs, n_cj * sizeof(ZsCJobDev), hipMemcpyHostToDevice, st));
-  }
+    if ((rr = ws_reserve_chunks(ns_total, slots, need))) return rr;
+    HIP_OK(hipMemcpyAsync(g_ws.d_segs, g_ws.h_segs, ns_total * sizeof(ZsSegDev), hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemcpyAsync(g_ws.d_cjobs, g_ws.h_cjobs, list.size() * sizeof(ZsCJobDev), hipMemcpyHostToDevice, st));
+    *nseg_out = ns_total;
+    *nslots_out = slots;
+    nunit_slots_max = std::max(nunit_slots_max, slots);
+    return 0;
+  };
+  if (n_cj && (r = plan_chunked(cj_list, 2, &nseg, &nunit_slots))) return r;
   HIP_OK(hipMemcpyAsync(g_ws.d_jobs, g_ws.h_jobs, nv * sizeof(ZsJobDev), hipMemcpyHostToDevice, st));
   HIP_OK(hipMemcpyAsync(g_ws.d_ids, g_ws.h_ids, nv * sizeof(uint32_t), hipMemcpyHostToDevice, st));
   hipEvent_t *ev = g_ws.prof ? g_ws.ev : nullptr;
   if (ev) HIP_OK(hipEventRecord(ev[0], st));
   zs_launch_header(g_ws.d_jobs, g_ws.d_heads, nv, st);
-  if (n_cj)
+  uint32_t n_retry = 0;
+  if (n_cj) {
     zs_launch_chunked(g_ws.d_jobs, g_ws.d_heads, g_ws.d_segs, (uint32_t)nseg, g_ws.d_cjobs, n_cj, g_ws.d_chunks,
                       (uint32_t)nunit_slots,
                       g_ws.d_scratch, g_ws.d_tokens, g_ws.d_tables, g_ws.d_fixed, g_ws.d_windows, g_ws.d_linkinfo,
                       g_ws.d_decs,
                       g_ws.d_fallback, st, ev ? ev + 1 : nullptr);
-  else if (ev)
+    // Jobs whose chain broke (most often a unit whose output outgrew cap_mul x
+    // its span x the job's ratio: blocks far more compressible than the
+    // stream) get one more chunked pass with 8x capacity before the serial
+    // decoder; finished jobs are final already (emitted, decs set).
+    std::vector<uint32_t> fb(nv), retry;
+    HIP_OK(hipMemcpyAsync(fb.data(), g_ws.d_fallback, nv * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    for (uint32_t k : cj_list)
+      if (fb[k]) retry.push_back(k);
+    if (!retry.empty()) {
+      size_t rseg = 0, rslots = 0;
+      if ((r = plan_chunked(retry, 8, &rseg, &rslots))) return r;
+      zs_launch_chunked(g_ws.d_jobs, g_ws.d_heads, g_ws.d_segs, (uint32_t)rseg, g_ws.d_cjobs, (uint32_t)retry.size(),
+                        g_ws.d_chunks, (uint32_t)rslots, g_ws.d_scratch, g_ws.d_tokens, g_ws.d_tables, g_ws.d_fixed,
+                        g_ws.d_windows, g_ws.d_linkinfo, g_ws.d_decs, g_ws.d_fallback, st, nullptr);
+      n_retry = (uint32_t)retry.size();
+    }
+  } else if (ev)
     for (int i = 1; i <= 6; i++) HIP_OK(hipEventRecord(ev[i], st));
   zs_launch_decode(0, g_ws.d_jobs, g_ws.d_heads, g_ws.d_ids, n_std, g_ws.d_decs, nullptr, st);
   zs_launch_decode(1, g_ws.d_jobs, g_ws.d_heads, g_ws.d_ids + n_std, n_d64, g_ws.d_decs, nullptr, st);
@@ -434,9 +465,9 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
   if (n_cj) {
     std::vector<uint32_t> fb(nv);
     HIP_OK(hipMemcpy(fb.data(), g_ws.d_fallback, nv * sizeof(uint32_t), hipMemcpyDeviceToHost));
-    HIP_OK(hipMemcpy(g_ws.h_cjobs, g_ws.d_cjobs, n_cj * sizeof(ZsCJobDev), hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(g_ws.h_cjobs, g_ws.d_cjobs, (n_retry ? n_retry : n_cj) * sizeof(ZsCJobDev), hipMemcpyDeviceToHost));
     for (uint32_t k : cj_list) g_ws.stats[2] += fb[k];
-    for (uint32_t q = 0; q < n_cj; q++) g_ws.stats[1] += g_ws.h_cjobs[q].nunits;
+    for (uint32_t q = 0; q < (n_retry ? n_retry : n_cj); q++) g_ws.stats[1] += g_ws.h_cjobs[q].nunits;
     if (std::getenv("ZS_DEBUG_CHUNKS")) {
       HIP_OK(hipMemcpy(g_ws.h_chunks, g_ws.d_chunks, nunit_slots * sizeof(ZsChunkDev), hipMemcpyDeviceToHost));
       size_t inch = 0, stopped = 0;

@@ -155,6 +155,8 @@ struct ZsCJobDev {     // a job on the chunked path
   uint32_t nunits;     // units planned (zs_plan_kernel)
   uint64_t scratch0;   // first scratch entry reserved for this job (host)
   uint64_t scratch_n;  // scratch entries reserved
+  uint32_t cap_mul;    // unit output capacity = cap_mul x span x ratio + slack
+  uint32_t pad;
 };
 
 // ---------------------------------------------------------------------------
