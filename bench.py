@@ -20,6 +20,7 @@ Prints ONE JSON line (rank 0) with the driver's contract fields plus
                   1 thread and on all threads, plus the oracle port on 1 thread.
 """
 import argparse
+import zlib
 import ctypes
 import hashlib
 import json
@@ -135,6 +136,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", choices=("c2", "c5"), default="c2",
+                    help="c2: 64 x 64 MiB raw deflate per GPU (BASELINE configs[1], the metric's workload); "
+                         "c5: configs[4], 4096 x 4 MiB mixed raw/gzip streams split across the ranks")
+    ap.add_argument("--c5-streams", type=int, default=4096)
     ap.add_argument("--streams", type=int, default=64)
     ap.add_argument("--stream-mib", type=int, default=64)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -168,13 +173,33 @@ def main():
     import shard
     import zstreams
 
-    nbytes = args.stream_mib << 20
-    first = rank * args.streams
     host_threads = min(16, os.cpu_count() or 1)
     t0 = time.time()
-    raws, comps = corpus.batch(first, args.streams, nbytes, level=6, wbits=-15, nthreads=host_threads)
+    if args.workload == "c5":
+        # configs[4]: the 4096 x 4 MiB mixed set, an equal contiguous share per rank
+        # (equal sizes: the LPT partition of shard.py is a count split), host zlib L6
+        nbytes = 4 << 20
+        lo = rank * args.c5_streams // world
+        hi = (rank + 1) * args.c5_streams // world
+        args.streams = hi - lo
+        from concurrent.futures import ThreadPoolExecutor
+        gen = [corpus.c5_stream(k, nbytes) for k in range(lo, hi)]
+        raws = [g[0] for g in gen]
+        wbits_list = [g[1] for g in gen]
+
+        def _deflate(k):
+            c = zlib.compressobj(6, zlib.DEFLATED, wbits_list[k], 8)
+            return np.frombuffer(c.compress(raws[k].tobytes()) + c.flush(), dtype=np.uint8)
+        with ThreadPoolExecutor(host_threads) as ex:
+            comps = list(ex.map(_deflate, range(len(raws))))
+        args.no_compress = args.no_deflate64 = True
+    else:
+        nbytes = args.stream_mib << 20
+        first = rank * args.streams
+        raws, comps = corpus.batch(first, args.streams, nbytes, level=6, wbits=-15, nthreads=host_threads)
+        wbits_list = [-15] * args.streams
     comp_total = sum(len(c) for c in comps)
-    log(f"[rank {rank}] generated+compressed {args.streams} x {args.stream_mib} MiB in {time.time() - t0:.1f}s "
+    log(f"[rank {rank}] generated+compressed {args.streams} x {nbytes >> 20} MiB in {time.time() - t0:.1f}s "
         f"(ratio {args.streams * nbytes / comp_total:.2f})")
 
     # device-resident inputs (16 B aligned) and outputs
@@ -200,7 +225,7 @@ def main():
     zstreams.set_stream(stream.cuda_stream)
 
     def step():
-        return zstreams.inflate_batch_device(in_ptrs, in_lens, out_ptrs, caps, -15)
+        return zstreams.inflate_batch_device(in_ptrs, in_lens, out_ptrs, caps, wbits_list)
 
     for _ in range(args.warmup):
         res = step()
@@ -255,6 +280,8 @@ def main():
         # interleave Zipf (first half) and lines (second half) streams
         half = args.streams // 2
         order = [x for k in range(half) for x in (k, k + half)] + list(range(2 * half, args.streams))
+        if args.workload == "c5":  # the raw (-15) half; host zlib's gzip inflate costs the same plus a CRC
+            order = [k for k in range(args.streams) if wbits_list[k] == -15]
         sample = order[:max(1, args.cpu_sample)]
         cpu = cpu_baseline(comps, raws, -15, sample, host_threads, args.cpu_seconds)
 
@@ -262,10 +289,15 @@ def main():
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "MiB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(t_el * 1e3 / args.steps, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-            "data": "synthetic: 32 Zipf-text + 32 line-text streams per GPU, host zlib L6 memLevel 8 raw (-15)",
-            "config": {"workload": f"{args.streams}x{args.stream_mib}MiB raw-deflate inflate (windowBits -15), "
-                                   "inputs resident in HBM", "streams_per_gpu": args.streams,
+            "scaling": "weak" if args.workload == "c2" else "strong", "vs_baseline": None, "dtype": "u8",
+            "data": ("synthetic: 32 Zipf-text + 32 line-text streams per GPU, host zlib L6 memLevel 8 raw (-15)"
+                     if args.workload == "c2" else
+                     "synthetic: Zipf / line text alternating in pairs, raw (-15) / gzip (31) alternating, host zlib L6"),
+            "config": {"workload": (f"{args.streams}x{args.stream_mib}MiB raw-deflate inflate (windowBits -15), "
+                                    "inputs resident in HBM" if args.workload == "c2" else
+                                    f"configs[4]: {args.c5_streams}x4MiB mixed raw/gzip inflate, "
+                                    f"{args.streams} streams on this rank, inputs resident in HBM"),
+                       "streams_per_gpu": args.streams,
                        "stream_bytes": nbytes, "compressed_bytes_per_gpu": comp_total,
                        "parallelism": f"stream-shard x{world}"},
             "verified_bit_exact": ok,

@@ -23,6 +23,8 @@ def lib():
             subprocess.run(["make", "-s", "-C", TOOLS], check=True)
         L = ctypes.CDLL(SO)
         L.zs_corpus_stream.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        L.zs_corpus_zipf.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64]
+        L.zs_corpus_lines.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64]
         L.zs_corpus_bound.restype = ctypes.c_size_t
         L.zs_corpus_bound.argtypes = [ctypes.c_size_t]
         L.zs_corpus_deflate.restype = ctypes.c_size_t
@@ -65,3 +67,15 @@ def zipf_text(nbytes, i=0):
 
 def lines_text(nbytes, i=32):
     return stream(32 + i % 32, nbytes)
+
+
+def c5_stream(k, nbytes):
+    """configs[4] stream k: Zipf text (seed 5000 + k) when
+    k % 4 < 2, else line text starting at record k << 20; raw deflate (-15)
+    when k is even, gzip (31) when odd.  Returns (raw ndarray, window_bits)."""
+    buf = np.empty(nbytes, dtype=np.uint8)
+    if k % 4 < 2:
+        lib().zs_corpus_zipf(buf.ctypes.data, nbytes, 5000 + k)
+    else:
+        lib().zs_corpus_lines(buf.ctypes.data, nbytes, k << 20)
+    return buf, (-15 if k % 2 == 0 else 31)

@@ -372,6 +372,10 @@ __global__ void __launch_bounds__(PLAN_T) zs_plan_kernel(const ZsJobDev *__restr
         sp = i + 1 < nunits ? units[cj.unit0 + i + 1].start_bit : ZS_NONE;
         const uint32_t span_bytes = ((sp == ZS_NONE ? end_bit : sp) - st + 7u) / 8u;
         cap = ((uint64_t)((double)cj.cap_mul * span_bytes * ratio) + UNIT_SLACK + 7u) & ~7ull;
+        // a false start shortly after a real one leaves a short span but a
+        // whole block to decode: such units get the job's output capacity
+        for (uint32_t b = 0; b < cj.n_boost && b < 4; b++)
+          if (cj.boost[b] == i) cap = max(cap, ((uint64_t)cj.boost_cap + UNIT_SLACK + 7u) & ~7ull);
         if (cap > 0xfff00000ull) cap = 0xfff00000ull;
       }
       // exclusive u64 prefix of the capacities (thread 0 walks the tile)

@@ -344,7 +344,9 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
   // upload them.  cap_mul scales each unit's output capacity (cap_mul x span x
   // ratio + slack, zs_plan_kernel).
   size_t nunit_slots_max = 0;
-  auto plan_chunked = [&](const std::vector<uint32_t> &list, uint32_t cap_mul, size_t *nseg_out, size_t *nslots_out) -> int {
+  auto plan_chunked = [&](const std::vector<uint32_t> &list, uint32_t cap_mul,
+                          const std::vector<std::vector<uint32_t>> *boosts, size_t *nseg_out,
+                          size_t *nslots_out) -> int {
     size_t ns_total = 0;
     for (uint32_t k : list) ns_total += (g_ws.h_jobs[k].in_len + C - 1) / C;
     int rr;
@@ -358,8 +360,11 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
       const uint32_t max_units = ns * SEG_SLOTS + 1;
       // zs_plan_kernel gives each unit cap_mul x span x ratio + slack entries;
       // spans of a job's units sum to at most its input (+1 byte of rounding each)
+      const uint32_t n_boost = boosts ? (uint32_t)std::min<size_t>((*boosts)[q].size(), 4) : 0;
+      const uint32_t boost_cap = (uint32_t)std::min<uint64_t>(jd.out_cap, 0xffe00000ull);
       const size_t reserve = (size_t)(cap_mul * ratio * ((double)jd.in_len + max_units)) +
-                             (size_t)max_units * ((size_t)UNIT_SLACK_HOST + 8) + 64;
+                             (size_t)max_units * ((size_t)UNIT_SLACK_HOST + 8) + 64 +
+                             (size_t)n_boost * ((size_t)boost_cap + (size_t)UNIT_SLACK_HOST + 8);
       ZsCJobDev cj{};
       cj.job = k;
       cj.first_seg = (uint32_t)si;
@@ -369,6 +374,9 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
       cj.scratch0 = need;
       cj.scratch_n = reserve;
       cj.cap_mul = cap_mul;
+      cj.n_boost = n_boost;
+      for (uint32_t b = 0; b < n_boost; b++) cj.boost[b] = (*boosts)[q][b];
+      cj.boost_cap = boost_cap;
       g_ws.h_cjobs[q] = cj;
       for (uint32_t o = 0; o < ns; o++, si++) {
         ZsSegDev sg{};
@@ -390,7 +398,7 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
     nunit_slots_max = std::max(nunit_slots_max, slots);
     return 0;
   };
-  if (n_cj && (r = plan_chunked(cj_list, 2, &nseg, &nunit_slots))) return r;
+  if (n_cj && (r = plan_chunked(cj_list, 2, nullptr, &nseg, &nunit_slots))) return r;
   HIP_OK(hipMemcpyAsync(g_ws.d_jobs, g_ws.h_jobs, nv * sizeof(ZsJobDev), hipMemcpyHostToDevice, st));
   HIP_OK(hipMemcpyAsync(g_ws.d_ids, g_ws.h_ids, nv * sizeof(uint32_t), hipMemcpyHostToDevice, st));
   hipEvent_t *ev = g_ws.prof ? g_ws.ev : nullptr;
@@ -405,16 +413,31 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
                       g_ws.d_fallback, st, ev ? ev + 1 : nullptr);
     // Jobs whose chain broke (most often a unit whose output outgrew cap_mul x
     // its span x the job's ratio: blocks far more compressible than the
-    // stream) get one more chunked pass with 8x capacity before the serial
-    // decoder; finished jobs are final already (emitted, decs set).
+    // stream, or a false start just after a real one cutting the span short)
+    // get one more chunked pass before the serial decoder: 8x capacity, and
+    // the job's whole output capacity for up to 4 units that ran out (the
+    // finder is deterministic, so unit i is the same unit in both passes).
+    // Finished jobs are final already (emitted, decs set).
     std::vector<uint32_t> fb(nv), retry;
+    std::vector<std::vector<uint32_t>> boosts;
     HIP_OK(hipMemcpyAsync(fb.data(), g_ws.d_fallback, nv * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
-    for (uint32_t k : cj_list)
-      if (fb[k]) retry.push_back(k);
+    for (uint32_t q = 0; q < n_cj; q++) {
+      if (!fb[cj_list[q]]) continue;
+      const ZsCJobDev &cj = g_ws.h_cjobs[q];
+      std::vector<ZsChunkDev> us(cj.max_units);
+      HIP_OK(hipMemcpyAsync(us.data(), g_ws.d_chunks + cj.unit0, cj.max_units * sizeof(ZsChunkDev),
+                            hipMemcpyDeviceToHost, st));
+      HIP_OK(hipStreamSynchronize(st));
+      std::vector<uint32_t> full;
+      for (uint32_t i = 0; i < cj.max_units; i++)
+        if (us[i].start_bit != ZS_NONE && (us[i].code & 0xff) == ZD_FULL) full.push_back(i);
+      retry.push_back(cj_list[q]);
+      boosts.push_back(full.size() <= 4 ? full : std::vector<uint32_t>());
+    }
     if (!retry.empty()) {
       size_t rseg = 0, rslots = 0;
-      if ((r = plan_chunked(retry, 8, &rseg, &rslots))) return r;
+      if ((r = plan_chunked(retry, 8, &boosts, &rseg, &rslots))) return r;
       zs_launch_chunked(g_ws.d_jobs, g_ws.d_heads, g_ws.d_segs, (uint32_t)rseg, g_ws.d_cjobs, (uint32_t)retry.size(),
                         g_ws.d_chunks, (uint32_t)rslots, g_ws.d_scratch, g_ws.d_tokens, g_ws.d_tables, g_ws.d_fixed,
                         g_ws.d_windows, g_ws.d_linkinfo, g_ws.d_decs, g_ws.d_fallback, st, nullptr);
@@ -477,7 +500,8 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
       }
       std::fprintf(stderr, "[zs] chunked jobs %u segments %zu units %u in_chain %zu stopped %zu fallback %u\n", n_cj, nseg,
                    g_ws.stats[1], inch, stopped, g_ws.stats[2]);
-      for (size_t i = 0; i < nunit_slots && i < 8; i++) {
+      const size_t show = std::getenv("ZS_DEBUG_CHUNKS")[0] == '2' ? nunit_slots : 8;
+      for (size_t i = 0; i < nunit_slots && i < show; i++) {
         const ZsChunkDev &c = g_ws.h_chunks[i];
         std::fprintf(stderr, "  unit %zu ord %u start %u stop %u end %u code %d n_out %u ntok %u cap %u chain %u\n", i, c.ord,
                      c.start_bit, c.stop_bit, c.end_bit, c.code, c.n_out, c.n_tok, c.cap, c.in_chain);

@@ -156,6 +156,9 @@ struct ZsCJobDev {     // a job on the chunked path
   uint64_t scratch0;   // first scratch entry reserved for this job (host)
   uint64_t scratch_n;  // scratch entries reserved
   uint32_t cap_mul;    // unit output capacity = cap_mul x span x ratio + slack
+  uint32_t n_boost;    // units (job-local index) given boost_cap entries at least:
+  uint32_t boost[4];   //   units that ran out of capacity in the previous pass
+  uint32_t boost_cap;
   uint32_t pad;
 };
 
