@@ -126,7 +126,7 @@ struct Workspace {
   uint32_t stats[4] = {0, 0, 0, 0};
 };
 
-// chunked-path tuning (env: ZS_CHUNK_KB, ZS_NO_CHUNK)
+// chunked-path tuning (env: ZS_CHUNK_KB, ZS_CAP_MUL, ZS_NO_CHUNK)
 uint32_t chunk_bytes() {
   static uint32_t v = [] {
     const char *e = std::getenv("ZS_CHUNK_KB");
@@ -134,6 +134,15 @@ uint32_t chunk_bytes() {
     if (kb < 4) kb = 4;
     if (kb > 65536) kb = 65536;
     return (uint32_t)(kb * 1024);
+  }();
+  return v;
+}
+// first-pass unit capacity multiplier (env: ZS_CAP_MUL, 1..8)
+uint32_t first_cap_mul() {
+  static uint32_t v = [] {
+    const char *e = std::getenv("ZS_CAP_MUL");
+    long m = e ? std::atol(e) : 2;
+    return (uint32_t)(m < 1 ? 1 : m > 8 ? 8 : m);
   }();
   return v;
 }
@@ -398,7 +407,7 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
     nunit_slots_max = std::max(nunit_slots_max, slots);
     return 0;
   };
-  if (n_cj && (r = plan_chunked(cj_list, 2, nullptr, &nseg, &nunit_slots))) return r;
+  if (n_cj && (r = plan_chunked(cj_list, first_cap_mul(), nullptr, &nseg, &nunit_slots))) return r;
   HIP_OK(hipMemcpyAsync(g_ws.d_jobs, g_ws.h_jobs, nv * sizeof(ZsJobDev), hipMemcpyHostToDevice, st));
   HIP_OK(hipMemcpyAsync(g_ws.d_ids, g_ws.h_ids, nv * sizeof(uint32_t), hipMemcpyHostToDevice, st));
   hipEvent_t *ev = g_ws.prof ? g_ws.ev : nullptr;
