@@ -1,32 +1,44 @@
 """bench.py -- BASELINE.json headline: MiB/s decompressed per node on the
 64 x 64 MiB raw-deflate batch (configs[1]), inflated on MI355X.
 
-One "step" = one zs_inflate_batch() over all of this rank's streams, inputs
-already resident in HBM, outputs written to HBM (ZS_F_DEVICE).  Weak scaling:
-every rank decodes its own 64 streams (stream ids rank*64 .. rank*64+63).
+One "step" = one zs_inflate_batch() over this rank's share of the batch,
+inputs already resident in HBM, outputs written to HBM (ZS_F_DEVICE).
+
+Scaling (streams are independent, no exchange step):
+  --scaling strong (default, the metric's definition): the node decodes THE
+      64 x 64 MiB batch; rank r decodes its LPT share of the 64 streams
+      (shard.bench_shard), so per-GPU work shrinks as N grows;
+  --scaling weak: every rank decodes its own 64 streams (ids 64r .. 64r+63).
+No collective touches the data: RCCL carries the contract's barrier and the
+reduction of the per-rank counters (max elapsed, summed bytes, all verified).
+
+`python bench.py --gpus N` with no WORLD_SIZE in the environment starts the N
+ranks itself (torch.distributed.run as a child process, before this process
+touches torch or the GPU) and exits with its status; under an external
+launcher (WORLD_SIZE set) it is one rank.
 
 The "(+ compressed)" half of the metric (configs[2]): after the inflate
-measurement the 64 decompressed streams, still in HBM, are gzip-compressed
+measurement this rank's decompressed streams, still in HBM, are gzip-compressed
 (level 6) by one zs_deflate_batch() per step; the line's "compress" object
-holds that rate (input MiB/s), the size against host zlib L6 on the same
-streams, the GPU inflate round trip check and a host zlib L6 deflate baseline.
+holds that rate, the size against host zlib L6, the GPU inflate round trip
+check and a host zlib L6 deflate baseline.
 
 Prints ONE JSON line (rank 0) with the driver's contract fields plus
-  roofline     -- decode kernel: algorithmic bytes (compressed in + decompressed
-                  out) per launch / average decode-kernel time measured with HIP
-                  events on the launch stream, vs 8 TB/s HBM peak;
-  cpu_baseline -- host zlib inflate on a bounded sample of the same streams
-                  (>= --cpu-seconds of 1-thread work), timed on this host on
-                  1 thread and on all threads, plus the oracle port on 1 thread.
+  roofline     -- rank 0's inflate pipeline: algorithmic bytes (compressed in +
+                  decompressed out) per launch / average pipeline time measured
+                  with HIP events on the launch stream, vs 8 TB/s HBM peak;
+  cpu_baseline -- host zlib inflate on a bounded sample of the same streams, on
+                  1 thread and on one thread per physical core of this host.
 """
 import argparse
-import zlib
 import ctypes
-import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
+import zlib
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "zlib-streams_amd"))
@@ -40,105 +52,16 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(comps, raws, wbits, sample, threads, min_seconds):
-    """Host zlib inflate of `sample` streams (whole-buffer Z_FINISH) on 1 thread,
-    repeated until `min_seconds` of CPU work, then on `threads` threads; plus
-    the oracle's C restatement (oracle/zo_inflate.c) on 1 thread over the first
-    8 sample streams.  Returns the cpu_baseline JSON object."""
-    import numpy as np
-
-    so = os.path.join(ROOT, "oracle", "libzs_cpubase.so")
-    L = ctypes.CDLL(so)
-    L.zs_cpu_inflate.restype = ctypes.c_double
-    L.zs_cpu_inflate.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t),
-                                 ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
-                                 ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_int)]
-    L.zs_cpu_zlib_version.restype = ctypes.c_char_p
-
-    def run(ids, nthreads, use_oracle, outs):
-        n = len(ids)
-        cp = (ctypes.c_void_p * n)(*[comps[i].ctypes.data for i in ids])
-        cl = (ctypes.c_size_t * n)(*[len(comps[i]) for i in ids])
-        op = (ctypes.c_void_p * n)(*[outs[i].ctypes.data for i in ids])
-        cap = max(len(raws[i]) for i in ids)
-        tot = ctypes.c_uint64()
-        bad = ctypes.c_int()
-        t = L.zs_cpu_inflate(cp, cl, op, cap, n, nthreads, wbits, use_oracle, ctypes.byref(tot), ctypes.byref(bad))
-        ok = not bad.value and all(np.array_equal(outs[i], raws[i]) for i in ids)
-        return t, tot.value, ok
-
-    outs = {i: np.empty(len(raws[i]), dtype=np.uint8) for i in sample}
-    t1 = b1 = 0
-    passes = 0
-    ok = True
-    while t1 < min_seconds or passes == 0:
-        t, b, k = run(sample, 1, 0, outs)
-        t1, b1, ok, passes = t1 + t, b1 + b, ok and k, passes + 1
-    tn = bn = 0
-    for _ in range(passes):
-        t, b, k = run(sample, threads, 0, outs)
-        tn, bn, ok = tn + t, bn + b, ok and k
-    psample = sample[:8]
-    tp, bp, kp = run(psample, 1, 1, outs)
-    return {"value": round(b1 / t1 / 2**20, 1), "unit": "MiB/s", "cores": 1, "kind": "reference",
-            "impl": f"host zlib {L.zs_cpu_zlib_version().decode()} inflate: upstream of the reference's src/inflate.c "
-                    "for windowBits -15 (the reference build needs its absent zlib submodule headers)",
-            "sample": f"{len(sample)} streams x {passes} pass(es), whole-buffer inflate(Z_FINISH), "
-                      f"{b1 / 2**20:.0f} MiB out, {t1:.1f} s on 1 thread",
-            "value_all_threads": round(bn / tn / 2**20, 1), "threads": threads,
-            "value_port_1t": round(bp / tp / 2**20, 1),
-            "port_sample": f"oracle/zo_inflate.c (C restatement) on {len(psample)} streams, 1 thread",
-            "verified": bool(ok and kp)}
-
-
-def cpu_deflate_baseline(raws, sample, threads, level, wbits, min_seconds):
-    """Host zlib deflate (the reference's deflate, byte-identical) of `sample`
-    streams on 1 thread (repeated to >= min_seconds) and on `threads` threads."""
-    import numpy as np
-
-    L = ctypes.CDLL(os.path.join(ROOT, "oracle", "libzs_cpubase.so"))
-    L.zs_cpu_deflate.restype = ctypes.c_double
-    L.zs_cpu_zlib_version.restype = ctypes.c_char_p
-    L.zs_cpu_deflate.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t),
-                                 ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t), ctypes.c_size_t,
-                                 ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                                 ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_int)]
-    cap = max(len(raws[i]) for i in sample) * 11 // 10 + 65536
-    bufs = {i: np.empty(cap, dtype=np.uint8) for i in sample}
-
-    def run(ids, nthreads):
-        n = len(ids)
-        rp = (ctypes.c_void_p * n)(*[raws[i].ctypes.data for i in ids])
-        rl = (ctypes.c_size_t * n)(*[len(raws[i]) for i in ids])
-        cp = (ctypes.c_void_p * n)(*[bufs[i].ctypes.data for i in ids])
-        cl = (ctypes.c_size_t * n)()
-        tot = ctypes.c_uint64()
-        bad = ctypes.c_int()
-        t = L.zs_cpu_deflate(rp, rl, cp, cl, cap, n, nthreads, level, wbits, ctypes.byref(tot), ctypes.byref(bad))
-        return t, tot.value, not bad.value, sum(cl)
-
-    t1 = b1 = c1 = passes = 0
-    ok = True
-    while t1 < min_seconds or passes == 0:
-        t, b, k, c = run(sample, 1)
-        t1, b1, c1, ok, passes = t1 + t, b1 + b, c1 + c, ok and k, passes + 1
-    tn, bn, kn, _ = run(sample * max(1, threads // len(sample)), threads)
-    return {"value": round(b1 / t1 / 2**20, 2), "unit": "MiB/s (input)", "cores": 1, "kind": "reference",
-            "impl": f"host zlib {L.zs_cpu_zlib_version().decode()} deflate level {level} memLevel 8 "
-                    "(byte-identical to the reference's deflate)",
-            "sample": f"{len(sample)} streams x {passes} pass(es), {b1 / 2**20:.0f} MiB in, {t1:.1f} s on 1 thread",
-            "ratio": round(b1 / c1, 3) if c1 else None,
-            "value_all_threads": round(bn / tn / 2**20, 1), "threads": threads, "verified": bool(ok and kn)}
-
-
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", choices=("c2", "c5"), default="c2",
-                    help="c2: 64 x 64 MiB raw deflate per GPU (BASELINE configs[1], the metric's workload); "
-                         "c5: configs[4], 4096 x 4 MiB mixed raw/gzip streams split across the ranks")
+                    help="c2: the 64 x 64 MiB raw-deflate batch (BASELINE configs[1], the metric's workload); "
+                         "c5: configs[4], 4096 x 4 MiB mixed raw/gzip streams")
+    ap.add_argument("--scaling", choices=("strong", "weak"), default="strong",
+                    help="strong: the node decodes one batch split across ranks; weak: a batch per rank")
     ap.add_argument("--c5-streams", type=int, default=4096)
     ap.add_argument("--streams", type=int, default=64)
     ap.add_argument("--stream-mib", type=int, default=64)
@@ -150,169 +73,382 @@ def main():
     ap.add_argument("--cpu-deflate-seconds", type=float, default=10.0)
     ap.add_argument("--no-deflate64", action="store_true", help="skip the deflate64 suite leg (configs[3])")
     ap.add_argument("--d64-reps", type=int, default=256, help="copies of the deflate64 fixture suite per batch")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json"),
                     help="PMC-derived HBM bytes per pipeline launch (null in the line when absent)")
-    args = ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU rehearsal of the multi-rank path (gloo, host zlib as the step, tiny streams); "
+                         "prints a line marked dry_run and measures nothing")
+    return ap.parse_args(argv)
 
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(args):
+    """Start `args.gpus` ranks of this script under torch.distributed.run as a
+    child process; nothing in this process has touched torch or the GPU."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "4"))
+    return subprocess.call(cmd, env=env)
+
+
+def host_cpu_info():
+    """Physical cores this process may run on (sysfs topology over the affinity
+    mask), the cgroup CPU quota if any, and the CPU model."""
+    aff = sorted(os.sched_getaffinity(0))
+    cores = set()
+    for c in aff:
+        try:
+            with open(f"/sys/devices/system/cpu/cpu{c}/topology/core_id") as f:
+                core = f.read().strip()
+            with open(f"/sys/devices/system/cpu/cpu{c}/topology/physical_package_id") as f:
+                pkg = f.read().strip()
+            cores.add((pkg, core))
+        except OSError:
+            cores.add(("?", c))
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            with open(path) as f:
+                q, per = f.read().split()[:2]
+            if q != "max":
+                quota = round(int(q) / int(per), 2)
+        except (OSError, ValueError):
+            pass
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"logical_cpus": len(aff), "physical_cores": len(cores), "cgroup_cpu_quota": quota, "model": model}
+
+
+def _cpulib():
+    L = ctypes.CDLL(os.path.join(ROOT, "oracle", "libzs_cpubase.so"))
+    P, S = ctypes.POINTER, ctypes.c_size_t
+    L.zs_cpu_inflate.restype = ctypes.c_double
+    L.zs_cpu_inflate.argtypes = [P(ctypes.c_void_p), P(S), P(ctypes.c_void_p), S, ctypes.c_int, ctypes.c_int,
+                                 ctypes.c_int, ctypes.c_int, P(ctypes.c_uint64), P(ctypes.c_int)]
+    L.zs_cpu_inflate_pt.restype = ctypes.c_double
+    L.zs_cpu_inflate_pt.argtypes = [P(ctypes.c_void_p), P(S), P(ctypes.c_void_p), S, ctypes.c_int, ctypes.c_int,
+                                    ctypes.c_int, P(ctypes.c_uint64), P(ctypes.c_int)]
+    for fn in ("zs_cpu_deflate", "zs_cpu_deflate_pt"):
+        f = getattr(L, fn)
+        f.restype = ctypes.c_double
+        f.argtypes = [P(ctypes.c_void_p), P(S), P(ctypes.c_void_p), P(S), S, ctypes.c_int, ctypes.c_int,
+                      ctypes.c_int, ctypes.c_int, P(ctypes.c_uint64), P(ctypes.c_int)]
+    L.zs_cpu_zlib_version.restype = ctypes.c_char_p
+    return L
+
+
+def cpu_baseline(comps, raws, wbits_list, sample, cpu, min_seconds):
+    """Host zlib inflate of `sample` streams (whole-buffer Z_FINISH): on 1 thread,
+    repeated until `min_seconds` of work; then one thread per physical core, the
+    sample repeated so that every thread decodes >= 2 streams; plus the oracle's C
+    restatement (oracle/zo_inflate.c) on 1 thread over the first 8 sample streams."""
     import numpy as np
-    import torch
+
+    L = _cpulib()
+    wbits = wbits_list[sample[0]]
+    sample = [i for i in sample if wbits_list[i] == wbits]
+
+    def arrs(ids):
+        n = len(ids)
+        return ((ctypes.c_void_p * n)(*[comps[i].ctypes.data for i in ids]),
+                (ctypes.c_size_t * n)(*[len(comps[i]) for i in ids]), n)
+
+    outs = {i: np.empty(len(raws[i]), dtype=np.uint8) for i in sample}
+    cap = max(len(raws[i]) for i in sample)
+
+    def run1(ids, use_oracle):
+        cp, cl, n = arrs(ids)
+        op = (ctypes.c_void_p * n)(*[outs[i].ctypes.data for i in ids])
+        tot, bad = ctypes.c_uint64(), ctypes.c_int()
+        t = L.zs_cpu_inflate(cp, cl, op, cap, n, 1, wbits, use_oracle, ctypes.byref(tot), ctypes.byref(bad))
+        ok = not bad.value and all(np.array_equal(outs[i], raws[i]) for i in ids)
+        return t, tot.value, ok
+
+    t1 = b1 = passes = 0
+    ok = True
+    while t1 < min_seconds or passes == 0:
+        t, b, k = run1(sample, 0)
+        t1, b1, ok, passes = t1 + t, b1 + b, ok and k, passes + 1
+    threads = max(1, cpu["physical_cores"])
+    ids = (sample * (2 * threads // len(sample) + 1))[:max(len(sample), 2 * threads)]
+    cp, cl, n = arrs(ids)
+    pt_outs = [np.empty(cap, dtype=np.uint8) for _ in range(threads)]
+    op = (ctypes.c_void_p * threads)(*[o.ctypes.data for o in pt_outs])
+    tot, bad = ctypes.c_uint64(), ctypes.c_int()
+    tn = L.zs_cpu_inflate_pt(cp, cl, op, cap, n, threads, wbits, ctypes.byref(tot), ctypes.byref(bad))
+    bn = tot.value
+    last = {k: ids[k + ((n - 1 - k) // threads) * threads] for k in range(min(threads, n))}
+    ok = ok and not bad.value and all(np.array_equal(pt_outs[k][:len(raws[i])], raws[i]) for k, i in last.items())
+    del pt_outs
+    tp, bp, kp = run1(sample[:8], 1)
+    v1 = b1 / t1 / 2**20
+    vn = bn / tn / 2**20
+    return {"value": round(v1, 1), "unit": "MiB/s", "cores": 1, "kind": "reference",
+            "impl": f"host zlib {L.zs_cpu_zlib_version().decode()} inflate: upstream of the reference's src/inflate.c "
+                    f"for windowBits {wbits} (the reference build needs its absent zlib submodule headers)",
+            "sample": f"{len(sample)} streams x {passes} pass(es), whole-buffer inflate(Z_FINISH), "
+                      f"{b1 / 2**20:.0f} MiB out, {t1:.1f} s on 1 thread",
+            "value_all_cores": round(vn, 1), "threads": threads,
+            "all_cores_sample": f"{n} stream decodes dealt round-robin to {threads} threads "
+                                f"(one per physical core), {bn / 2**20:.0f} MiB out, {tn:.1f} s",
+            "value_all_cores_linear": round(v1 * threads, 1),
+            "host": cpu,
+            "value_port_1t": round(bp / tp / 2**20, 1),
+            "port_sample": f"oracle/zo_inflate.c (C restatement) on {min(8, len(sample))} streams, 1 thread",
+            "verified": bool(ok and kp)}
+
+
+def cpu_deflate_baseline(raws, sample, cpu, level, wbits, min_seconds):
+    """Host zlib deflate (the reference's deflate, byte-identical) of `sample`
+    buffers on 1 thread (repeated to >= min_seconds) and on one thread per
+    physical core (every thread compressing >= 1 buffer)."""
+    import numpy as np
+
+    L = _cpulib()
+    cap = max(len(raws[i]) for i in sample) * 11 // 10 + 65536
+    bufs = {i: np.empty(cap, dtype=np.uint8) for i in sample}
+
+    def arrs(ids):
+        n = len(ids)
+        return ((ctypes.c_void_p * n)(*[raws[i].ctypes.data for i in ids]),
+                (ctypes.c_size_t * n)(*[len(raws[i]) for i in ids]), n)
+
+    t1 = b1 = c1 = passes = 0
+    ok = True
+    while t1 < min_seconds or passes == 0:
+        rp, rl, n = arrs(sample)
+        cp = (ctypes.c_void_p * n)(*[bufs[i].ctypes.data for i in sample])
+        cl = (ctypes.c_size_t * n)()
+        tot, bad = ctypes.c_uint64(), ctypes.c_int()
+        t = L.zs_cpu_deflate(rp, rl, cp, cl, cap, n, 1, level, wbits, ctypes.byref(tot), ctypes.byref(bad))
+        t1, b1, c1, ok, passes = t1 + t, b1 + tot.value, c1 + sum(cl), ok and not bad.value, passes + 1
+    threads = max(1, cpu["physical_cores"])
+    ids = (sample * (threads // len(sample) + 1))[:max(len(sample), threads)]
+    rp, rl, n = arrs(ids)
+    pt = [np.empty(cap, dtype=np.uint8) for _ in range(threads)]
+    cp = (ctypes.c_void_p * threads)(*[b.ctypes.data for b in pt])
+    cl = (ctypes.c_size_t * threads)()
+    tot, bad = ctypes.c_uint64(), ctypes.c_int()
+    tn = L.zs_cpu_deflate_pt(rp, rl, cp, cl, cap, n, threads, level, wbits, ctypes.byref(tot), ctypes.byref(bad))
+    del pt
+    v1 = b1 / t1 / 2**20
+    return {"value": round(v1, 2), "unit": "MiB/s (input)", "cores": 1, "kind": "reference",
+            "impl": f"host zlib {L.zs_cpu_zlib_version().decode()} deflate level {level} memLevel 8 "
+                    "(byte-identical to the reference's deflate)",
+            "sample": f"{len(sample)} streams x {passes} pass(es), {b1 / 2**20:.0f} MiB in, {t1:.1f} s on 1 thread",
+            "ratio": round(b1 / c1, 3) if c1 else None,
+            "value_all_cores": round(tot.value / tn / 2**20, 1), "threads": threads,
+            "value_all_cores_linear": round(v1 * threads, 1),
+            "verified": bool(ok and not bad.value)}
+
+
+def generate(ids, nbytes, kind, nthreads):
+    """Raw + host-zlib-compressed streams for `ids` (configs[1] or configs[4]);
+    generation and compression run in C threads (ctypes releases the GIL)."""
+    import numpy as np
+    from concurrent.futures import ThreadPoolExecutor
+
+    import corpus
+
+    def one(i):
+        if kind == "c2":
+            r, c = corpus.batch(i, 1, nbytes, level=6, wbits=-15, nthreads=1)
+            return r[0], c[0], -15
+        raw, wb = corpus.c5_stream(i, nbytes)
+        co = zlib.compressobj(6, zlib.DEFLATED, wb, 8)
+        return raw, np.frombuffer(co.compress(raw.tobytes()) + co.flush(), dtype=np.uint8), wb
+
+    with ThreadPoolExecutor(max(1, nthreads)) as ex:
+        out = list(ex.map(one, ids))
+    return [o[0] for o in out], [o[1] for o in out], [o[2] for o in out]
+
+
+def main():
+    args = parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
-    if dist:
-        import torch.distributed as tdist
-        torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", torch.cuda.current_device())
 
-    import corpus
+    import numpy as np
+    import torch
+
     import shard
-    import zstreams
 
-    host_threads = min(16, os.cpu_count() or 1)
+    if args.dry_run:
+        dev = torch.device("cpu")
+        if dist:
+            import torch.distributed as tdist
+            tdist.init_process_group("gloo")
+    else:
+        if dist:
+            import torch.distributed as tdist
+            torch.cuda.set_device(local)
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            torch.cuda.set_device(0)
+        dev = torch.device("cuda", torch.cuda.current_device())
+
+    cpu = host_cpu_info()
+    gen_threads = max(1, min(16, cpu["logical_cpus"] // max(1, world)))
     t0 = time.time()
     if args.workload == "c5":
-        # configs[4]: the 4096 x 4 MiB mixed set, an equal contiguous share per rank
-        # (equal sizes: the LPT partition of shard.py is a count split), host zlib L6
         nbytes = 4 << 20
-        lo = rank * args.c5_streams // world
-        hi = (rank + 1) * args.c5_streams // world
-        args.streams = hi - lo
-        from concurrent.futures import ThreadPoolExecutor
-        gen = [corpus.c5_stream(k, nbytes) for k in range(lo, hi)]
-        raws = [g[0] for g in gen]
-        wbits_list = [g[1] for g in gen]
-
-        def _deflate(k):
-            c = zlib.compressobj(6, zlib.DEFLATED, wbits_list[k], 8)
-            return np.frombuffer(c.compress(raws[k].tobytes()) + c.flush(), dtype=np.uint8)
-        with ThreadPoolExecutor(host_threads) as ex:
-            comps = list(ex.map(_deflate, range(len(raws))))
+        total_streams = args.c5_streams
+        ids = shard.bench_shard(args.c5_streams, rank, world, shard.c5_kind)
         args.no_compress = args.no_deflate64 = True
     else:
         nbytes = args.stream_mib << 20
-        first = rank * args.streams
-        raws, comps = corpus.batch(first, args.streams, nbytes, level=6, wbits=-15, nthreads=host_threads)
-        wbits_list = [-15] * args.streams
+        total_streams = args.streams if args.scaling == "strong" else args.streams * world
+        ids = (shard.bench_shard(args.streams, rank, world, shard.c2_kind) if args.scaling == "strong"
+               else list(range(rank * args.streams, (rank + 1) * args.streams)))
+    raws, comps, wbits_list = generate(ids, nbytes, args.workload, gen_threads)
+    nloc = len(ids)
     comp_total = sum(len(c) for c in comps)
-    log(f"[rank {rank}] generated+compressed {args.streams} x {nbytes >> 20} MiB in {time.time() - t0:.1f}s "
-        f"(ratio {args.streams * nbytes / comp_total:.2f})")
+    log(f"[rank {rank}] {nloc} of {total_streams} streams ({args.workload}, {args.scaling}) x {nbytes >> 20} MiB "
+        f"generated+compressed in {time.time() - t0:.1f}s (ratio {nloc * nbytes / max(1, comp_total):.2f})")
 
-    # device-resident inputs (16 B aligned) and outputs
-    offs = []
-    o = 0
-    for c in comps:
-        offs.append(o)
-        o += (len(c) + 255) & ~255
-    d_in = torch.empty(o + 256, dtype=torch.uint8, device=dev)
-    d_in_cpu = np.zeros(o + 256, dtype=np.uint8)
-    for c, of in zip(comps, offs):
-        d_in_cpu[of:of + len(c)] = c
-    d_in.copy_(torch.from_numpy(d_in_cpu))
-    del d_in_cpu
-    d_out = torch.empty(args.streams * nbytes, dtype=torch.uint8, device=dev)
-    in_ptrs = [d_in.data_ptr() + of for of in offs]
-    in_lens = [len(c) for c in comps]
-    out_ptrs = [d_out.data_ptr() + k * nbytes for k in range(args.streams)]
-    caps = [nbytes] * args.streams
-
-    torch.cuda.synchronize()
-    stream = torch.cuda.Stream(device=dev)  # a real (non-NULL) HIP stream shared with the library
-    zstreams.set_stream(stream.cuda_stream)
-
-    def step():
-        return zstreams.inflate_batch_device(in_ptrs, in_lens, out_ptrs, caps, wbits_list)
-
-    for _ in range(args.warmup):
+    if args.dry_run:
+        def step():
+            return [zlib.decompressobj(wb).decompress(c.tobytes()) for c, wb in zip(comps, wbits_list)]
         res = step()
-    # correctness of the measured configuration (bit-exact vs generator)
-    res = step()
-    ok = all(r["ret"] == 1 and r["total_out"] == nbytes and r["total_in"] == in_lens[k] for k, r in enumerate(res))
-    torch.cuda.synchronize()
-    out_host = d_out.cpu().numpy().reshape(args.streams, nbytes)
-    ok = ok and all(np.array_equal(out_host[k], raws[k]) for k in range(args.streams))
-    del out_host
-    log(f"[rank {rank}] verified bit-exact: {ok}")
+        ok = all(r == raw.tobytes() for r, raw in zip(res, raws))
+    else:
+        import zstreams
+        offs, o = [], 0
+        for c in comps:
+            offs.append(o)
+            o += (len(c) + 255) & ~255
+        hbuf = np.zeros(o + 256, dtype=np.uint8)
+        for c, of in zip(comps, offs):
+            hbuf[of:of + len(c)] = c
+        d_in = torch.from_numpy(hbuf).to(dev)
+        del hbuf
+        d_out = torch.empty(max(1, nloc) * nbytes, dtype=torch.uint8, device=dev)
+        in_ptrs = [d_in.data_ptr() + of for of in offs]
+        in_lens = [len(c) for c in comps]
+        out_ptrs = [d_out.data_ptr() + k * nbytes for k in range(nloc)]
+        caps = [nbytes] * nloc
+        torch.cuda.synchronize()
+        stream = torch.cuda.Stream(device=dev)  # a real (non-NULL) HIP stream shared with the library
+        zstreams.set_stream(stream.cuda_stream)
 
-    zstreams.profile(True)
+        def step():
+            return zstreams.inflate_batch_device(in_ptrs, in_lens, out_ptrs, caps, wbits_list) if nloc else []
+
+        for _ in range(args.warmup):
+            step()
+        res = step()  # correctness of the measured configuration (bit-exact vs generator)
+        ok = all(r["ret"] == 1 and r["total_out"] == nbytes and r["total_in"] == in_lens[k] for k, r in enumerate(res))
+        torch.cuda.synchronize()
+        if nloc:
+            out_host = d_out.cpu().numpy().reshape(nloc, nbytes)
+            ok = ok and all(np.array_equal(out_host[k], raws[k]) for k in range(nloc))
+            del out_host
+        log(f"[rank {rank}] verified bit-exact: {ok}")
+        zstreams.profile(True)
+
     if dist:
         tdist.barrier()
-    torch.cuda.synchronize()
+    if not args.dry_run:
+        torch.cuda.synchronize()
     t_start = time.perf_counter()
     for _ in range(args.steps):
         step()
-    torch.cuda.synchronize()
+    if not args.dry_run:
+        torch.cuda.synchronize()
     if dist:
         tdist.barrier()
     t_el = time.perf_counter() - t_start
-    k_ms, b_ms, k_n = zstreams.profile_read()
-    stage_ms = zstreams.profile_stages()
-    stats = zstreams.last_stats()
-    zstreams.profile(False)
-    # max elapsed over ranks, summed decompressed bytes, all ranks verified
-    t_el, out_bytes, ok = shard.reduce_counters(t_el, args.streams * nbytes * args.steps, ok, device=dev)
 
+    if args.dry_run:
+        k_ms, k_n, stage_ms, stats = 0.0, 0, {}, {}
+    else:
+        k_ms, b_ms, k_n = zstreams.profile_read()
+        stage_ms = zstreams.profile_stages()
+        stats = zstreams.last_stats()
+        zstreams.profile(False)
+    # max elapsed over ranks, summed decompressed bytes, all ranks verified
+    t_el, out_bytes, ok = shard.reduce_counters(t_el, nloc * nbytes * args.steps, ok, device=dev)
     value = out_bytes / t_el / 2**20
-    per_launch_alg = comp_total + args.streams * nbytes  # algorithmic bytes of one decode launch
+    per_launch_alg = comp_total + nloc * nbytes  # rank 0's algorithmic bytes of one decode launch
     k_avg_s = (k_ms / max(k_n, 1)) / 1e3
     achieved = per_launch_alg / k_avg_s / 1e9 if k_avg_s > 0 else 0.0
 
     traffic = None
-    if args.traffic_json and os.path.exists(args.traffic_json):
-        # HBM bytes per launch from rocprofv3 PMC passes (tools/pmc_traffic.py)
+    if args.traffic_json and os.path.exists(args.traffic_json) and world == 1 and args.workload == "c2":
+        # HBM bytes per pipeline launch from rocprofv3 PMC passes (tools/pmc_traffic.py), same workload
         traffic = json.load(open(args.traffic_json)).get("hbm_bytes_per_launch")
 
-    comp_leg = None
-    if not args.no_compress:
+    comp_leg = d64_leg = None
+    if not args.dry_run and not args.no_compress and nloc:
         comp_leg = compress_leg(args, zstreams, shard, torch, np, dev, dist, raws, d_out, out_ptrs, nbytes,
-                                comp_total, host_threads, rank)
-
-    d64_leg = None
-    if not args.no_deflate64:
+                                comp_total, cpu, rank, [shard.c2_kind(i) for i in ids])
+    if not args.dry_run and not args.no_deflate64:
         d64_leg = deflate64_leg(args, zstreams, torch, np, dev, rank)
 
-    cpu = None
-    if rank == 0 and not args.no_cpu_baseline:
-        # interleave Zipf (first half) and lines (second half) streams
-        half = args.streams // 2
-        order = [x for k in range(half) for x in (k, k + half)] + list(range(2 * half, args.streams))
-        if args.workload == "c5":  # the raw (-15) half; host zlib's gzip inflate costs the same plus a CRC
-            order = [k for k in range(args.streams) if wbits_list[k] == -15]
+    cpu_b = None
+    if rank == 0 and not args.no_cpu_baseline and not args.dry_run and nloc:
+        # interleave Zipf and line-text streams of this rank (the raw -15 ones for c5)
+        kinds = [shard.c2_kind(i) if args.workload == "c2" else shard.c5_kind(i) for i in ids]
+        z = [k for k in range(nloc) if kinds[k] == "zipf" and wbits_list[k] == -15]
+        li = [k for k in range(nloc) if kinds[k] == "lines" and wbits_list[k] == -15]
+        order = [x for pair in zip(z, li) for x in pair] + z[len(li):] + li[len(z):]
         sample = order[:max(1, args.cpu_sample)]
-        cpu = cpu_baseline(comps, raws, -15, sample, host_threads, args.cpu_seconds)
+        cpu_b = cpu_baseline(comps, raws, wbits_list, sample, cpu, args.cpu_seconds)
+        cpu_b["gpu_vs_1core"] = round(value / cpu_b["value"], 1)
+        cpu_b["gpu_vs_all_cores"] = round(value / cpu_b["value_all_cores"], 2)
+        cpu_b["gpu_vs_all_cores_linear"] = round(value / cpu_b["value_all_cores_linear"], 2)
 
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "MiB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(t_el * 1e3 / args.steps, 3), "higher_is_better": True,
-            "scaling": "weak" if args.workload == "c2" else "strong", "vs_baseline": None, "dtype": "u8",
-            "data": ("synthetic: 32 Zipf-text + 32 line-text streams per GPU, host zlib L6 memLevel 8 raw (-15)"
+            "scaling": args.scaling if args.workload == "c2" else "strong", "vs_baseline": None, "dtype": "u8",
+            "data": ("synthetic: Zipf-text (ids i%64<32) + line-text streams, host zlib L6 memLevel 8 raw (-15)"
                      if args.workload == "c2" else
                      "synthetic: Zipf / line text alternating in pairs, raw (-15) / gzip (31) alternating, host zlib L6"),
-            "config": {"workload": (f"{args.streams}x{args.stream_mib}MiB raw-deflate inflate (windowBits -15), "
+            "config": {"workload": (f"{total_streams}x{args.stream_mib}MiB raw-deflate inflate (windowBits -15), "
                                     "inputs resident in HBM" if args.workload == "c2" else
-                                    f"configs[4]: {args.c5_streams}x4MiB mixed raw/gzip inflate, "
-                                    f"{args.streams} streams on this rank, inputs resident in HBM"),
-                       "streams_per_gpu": args.streams,
-                       "stream_bytes": nbytes, "compressed_bytes_per_gpu": comp_total,
+                                    f"configs[4]: {total_streams}x4MiB mixed raw/gzip inflate, inputs resident in HBM"),
+                       "streams_total": total_streams, "streams_rank0": nloc, "stream_bytes": nbytes,
+                       "compressed_bytes_rank0": comp_total,
+                       "partition": "LPT over the node's streams (shard.bench_shard)" if (
+                           args.scaling == "strong" or args.workload == "c5") else "64 streams per rank",
                        "parallelism": f"stream-shard x{world}"},
             "verified_bit_exact": ok,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                         "kernel": "inflate pipeline (find+parse+expand+link+emit+serial decode)",
-                         "kernel_ms_avg": round(k_avg_s * 1e3, 3), "batch_ms_avg": round(b_ms / max(k_n, 1), 3),
+                         "kernel": "inflate pipeline (find+plan+parse+chain+expand+link+emit+serial decode), rank 0",
+                         "kernel_ms_avg": round(k_avg_s * 1e3, 3),
                          "alg_bytes_per_launch": per_launch_alg,
                          "stages_ms_avg": {k: round(v / max(k_n, 1), 3) for k, v in stage_ms.items()},
-                         "stage_kernels": zstreams.STAGE_KERNELS},
-            "cpu_baseline": cpu,
+                         "stage_kernels": None if args.dry_run else zstreams.STAGE_KERNELS},
+            "cpu_baseline": cpu_b,
             "path_stats": stats,
             "compress": comp_leg,
             "deflate64": d64_leg,
         }
+        if args.dry_run:
+            line["dry_run"] = True
+            line["rank_streams"] = ids
         print(json.dumps(line), flush=True)
     if dist:
         tdist.destroy_process_group()
@@ -384,11 +520,7 @@ def deflate64_leg(args, zstreams, torch, np, dev, rank):
                         "kernel": "zs_decode_kernel<true> (wave per stream)", "kernel_ms_avg": round(k_s * 1e3, 3),
                         "alg_bytes_per_launch": in_b + out_b}}
     if rank == 0 and not args.no_cpu_baseline:
-        L = ctypes.CDLL(os.path.join(ROOT, "oracle", "libzs_cpubase.so"))
-        L.zs_cpu_inflate.restype = ctypes.c_double
-        L.zs_cpu_inflate.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t),
-                                     ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
-                                     ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_int)]
+        L = _cpulib()
         arrs = [np.frombuffer(c, dtype=np.uint8) for c in suite]
         obufs = [np.empty(cap, dtype=np.uint8) for _ in suite]
         n = len(suite)
@@ -413,8 +545,8 @@ def deflate64_leg(args, zstreams, torch, np, dev, rank):
     return leg
 
 
-def compress_leg(args, zstreams, shard, torch, np, dev, dist, raws, d_out, raw_ptrs, nbytes, zlib_raw_total,
-                 host_threads, rank):
+def compress_leg(args, zstreams, shard, torch, np, dev, dist, raws, d_out, raw_ptrs, nbytes, zlib_raw_total, cpu, rank,
+                 kinds):
     """configs[2]: gzip (windowBits 31) level-L GPU deflate of the decompressed
     streams resident in HBM, then a GPU inflate round trip of its output."""
     n = len(raw_ptrs)
@@ -462,9 +594,10 @@ def compress_leg(args, zstreams, shard, torch, np, dev, dist, raws, d_out, raw_p
     k_avg_s = (k_ms / max(k_n, 1)) / 1e3
     alg = n * nbytes + comp_total
     achieved = alg / k_avg_s / 1e9 if k_avg_s > 0 else 0.0
+    value = in_bytes / t_el / 2**20
     leg = {"metric": "MiB/s compressed (input bytes), gzip level %d" % level,
-           "value": round(in_bytes / t_el / 2**20, 1), "unit": "MiB/s", "ms_per_step": round(t_el * 1e3 / args.steps, 3),
-           "workload": f"{n}x{nbytes >> 20}MiB gzip (windowBits 31) level {level} deflate, inputs resident in HBM",
+           "value": round(value, 1), "unit": "MiB/s", "ms_per_step": round(t_el * 1e3 / args.steps, 3),
+           "workload": f"{n}x{nbytes >> 20}MiB gzip (windowBits 31) level {level} deflate on rank 0, inputs resident in HBM",
            "compressed_bytes": comp_total, "ratio": round(n * nbytes / comp_total, 3),
            "zlib_l6_bytes": zlib_total, "size_vs_zlib_l6": round(comp_total / zlib_total, 4),
            "roundtrip_verified": ok, "roundtrip_path_stats": rt_stats,
@@ -474,9 +607,13 @@ def compress_leg(args, zstreams, shard, torch, np, dev, dist, raws, d_out, raw_p
                         "stages_ms_avg": {k: round(v / max(k_n, 1), 3) for k, v in stages.items()},
                         "stage_kernels": zstreams.DEFLATE_STAGE_KERNELS}}
     if rank == 0 and not args.no_cpu_baseline:
-        half = n // 2
-        sample = [0, half, 1, half + 1][:max(1, min(4, n))]
-        leg["cpu_baseline"] = cpu_deflate_baseline(raws, sample, host_threads, level, 31, args.cpu_deflate_seconds)
+        z = [k for k in range(n) if kinds[k] == "zipf"]
+        li = [k for k in range(n) if kinds[k] == "lines"]
+        sample = (z[:2] + li[:2]) or [0]
+        cb = cpu_deflate_baseline(raws, sample, cpu, level, 31, args.cpu_deflate_seconds)
+        cb["gpu_vs_1core"] = round(value / cb["value"], 1)
+        cb["gpu_vs_all_cores"] = round(value / cb["value_all_cores"], 2)
+        leg["cpu_baseline"] = cb
     del d_cz
     return leg
 

@@ -24,14 +24,16 @@ typedef struct {
   int n, nthreads, tid, wbits, use_oracle;
   uint64_t produced;
   int bad;
+  int per_thread_out; /* 1: out[tid] is this thread's buffer for all its streams */
 } task_t;
 
 static void *run(void *arg) {
   task_t *t = (task_t *)arg;
   for (int i = t->tid; i < t->n; i += t->nthreads) {
+    uint8_t *dst = t->per_thread_out ? t->out[t->tid] : t->out[i];
     if (t->use_oracle) {
       zo_result r;
-      zo_oneshot(t->comp[i], (uint32_t)t->comp_len[i], t->out[i], (uint32_t)t->out_cap, t->wbits, &r);
+      zo_oneshot(t->comp[i], (uint32_t)t->comp_len[i], dst, (uint32_t)t->out_cap, t->wbits, &r);
       t->produced += r.total_out;
       t->bad |= r.ret != 1;
     } else {
@@ -40,7 +42,7 @@ static void *run(void *arg) {
       inflateInit2(&z, t->wbits);
       z.next_in = (Bytef *)t->comp[i];
       z.avail_in = (uInt)t->comp_len[i];
-      z.next_out = t->out[i];
+      z.next_out = dst;
       z.avail_out = (uInt)t->out_cap;
       int r = inflate(&z, Z_FINISH);
       t->produced += z.total_out;
@@ -51,21 +53,21 @@ static void *run(void *arg) {
   return NULL;
 }
 
-double zs_cpu_inflate(const uint8_t *const *comp, const size_t *comp_len, uint8_t *const *out, size_t out_cap, int n,
-                      int nthreads, int wbits, int use_oracle, uint64_t *total_out, int *bad) {
+static double inflate_timed(const uint8_t *const *comp, const size_t *comp_len, uint8_t *const *out, size_t out_cap, int n,
+                            int nthreads, int wbits, int use_oracle, int per_thread_out, uint64_t *total_out, int *bad) {
   if (nthreads < 1) nthreads = 1;
-  if (nthreads > 512) nthreads = 512;
+  if (nthreads > 1024) nthreads = 1024;
   task_t *ts = (task_t *)calloc((size_t)nthreads, sizeof(task_t));
   pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
   /* warm any lazily built static tables before timing (single thread) */
   if (n > 0) {
-    task_t w = {comp, comp_len, out, out_cap, 1, 1, 0, wbits, use_oracle, 0, 0};
+    task_t w = {comp, comp_len, out, out_cap, 1, 1, 0, wbits, use_oracle, 0, 0, per_thread_out};
     run(&w);
   }
   struct timespec a, b;
   clock_gettime(CLOCK_MONOTONIC, &a);
   for (int k = 0; k < nthreads; k++) {
-    ts[k] = (task_t){comp, comp_len, out, out_cap, n, nthreads, k, wbits, use_oracle, 0, 0};
+    ts[k] = (task_t){comp, comp_len, out, out_cap, n, nthreads, k, wbits, use_oracle, 0, 0, per_thread_out};
     pthread_create(&th[k], NULL, run, &ts[k]);
   }
   uint64_t tot = 0;
@@ -81,6 +83,18 @@ double zs_cpu_inflate(const uint8_t *const *comp, const size_t *comp_len, uint8_
   *total_out = tot;
   *bad = anybad;
   return (double)(b.tv_sec - a.tv_sec) + 1e-9 * (double)(b.tv_nsec - a.tv_nsec);
+}
+
+double zs_cpu_inflate(const uint8_t *const *comp, const size_t *comp_len, uint8_t *const *out, size_t out_cap, int n,
+                      int nthreads, int wbits, int use_oracle, uint64_t *total_out, int *bad) {
+  return inflate_timed(comp, comp_len, out, out_cap, n, nthreads, wbits, use_oracle, 0, total_out, bad);
+}
+
+/* all-core variant: n streams (a stream may repeat) dealt round-robin to
+ * nthreads threads, thread k decoding every one of its streams into out[k] */
+double zs_cpu_inflate_pt(const uint8_t *const *comp, const size_t *comp_len, uint8_t *const *out, size_t out_cap, int n,
+                         int nthreads, int wbits, uint64_t *total_out, int *bad) {
+  return inflate_timed(comp, comp_len, out, out_cap, n, nthreads, wbits, 0, 1, total_out, bad);
 }
 
 const char *zs_cpu_zlib_version(void) { return zlibVersion(); }
@@ -99,6 +113,7 @@ typedef struct {
   int n, nthreads, tid, level, wbits;
   uint64_t consumed;
   int bad;
+  int per_thread_out; /* 1: comp[tid] / comp_len[tid] serve all of this thread's buffers */
 } dtask_t;
 
 static void *drun(void *arg) {
@@ -109,27 +124,29 @@ static void *drun(void *arg) {
     deflateInit2(&z, t->level, Z_DEFLATED, t->wbits, 8, Z_DEFAULT_STRATEGY);
     z.next_in = (Bytef *)t->raw[i];
     z.avail_in = (uInt)t->raw_len[i];
-    z.next_out = t->comp[i];
+    const int o = t->per_thread_out ? t->tid : i;
+    z.next_out = t->comp[o];
     z.avail_out = (uInt)t->comp_cap;
     int r = deflate(&z, Z_FINISH);
     t->consumed += z.total_in;
-    t->comp_len[i] = z.total_out;
+    t->comp_len[o] = z.total_out;
     t->bad |= r != Z_STREAM_END;
     deflateEnd(&z);
   }
   return NULL;
 }
 
-double zs_cpu_deflate(const uint8_t *const *raw, const size_t *raw_len, uint8_t *const *comp, size_t *comp_len,
-                      size_t comp_cap, int n, int nthreads, int level, int wbits, uint64_t *total_in, int *bad) {
+static double deflate_timed(const uint8_t *const *raw, const size_t *raw_len, uint8_t *const *comp, size_t *comp_len,
+                            size_t comp_cap, int n, int nthreads, int level, int wbits, int per_thread_out,
+                            uint64_t *total_in, int *bad) {
   if (nthreads < 1) nthreads = 1;
-  if (nthreads > 512) nthreads = 512;
+  if (nthreads > 1024) nthreads = 1024;
   dtask_t *ts = (dtask_t *)calloc((size_t)nthreads, sizeof(dtask_t));
   pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
   struct timespec a, b;
   clock_gettime(CLOCK_MONOTONIC, &a);
   for (int k = 0; k < nthreads; k++) {
-    ts[k] = (dtask_t){raw, raw_len, comp, comp_len, comp_cap, n, nthreads, k, level, wbits, 0, 0};
+    ts[k] = (dtask_t){raw, raw_len, comp, comp_len, comp_cap, n, nthreads, k, level, wbits, 0, 0, per_thread_out};
     pthread_create(&th[k], NULL, drun, &ts[k]);
   }
   uint64_t tot = 0;
@@ -145,4 +162,15 @@ double zs_cpu_deflate(const uint8_t *const *raw, const size_t *raw_len, uint8_t 
   *total_in = tot;
   *bad = anybad;
   return (double)(b.tv_sec - a.tv_sec) + 1e-9 * (double)(b.tv_nsec - a.tv_nsec);
+}
+
+double zs_cpu_deflate(const uint8_t *const *raw, const size_t *raw_len, uint8_t *const *comp, size_t *comp_len,
+                      size_t comp_cap, int n, int nthreads, int level, int wbits, uint64_t *total_in, int *bad) {
+  return deflate_timed(raw, raw_len, comp, comp_len, comp_cap, n, nthreads, level, wbits, 0, total_in, bad);
+}
+
+/* all-core variant: thread k compresses every one of its buffers into comp[k] */
+double zs_cpu_deflate_pt(const uint8_t *const *raw, const size_t *raw_len, uint8_t *const *comp, size_t *comp_len,
+                         size_t comp_cap, int n, int nthreads, int level, int wbits, uint64_t *total_in, int *bad) {
+  return deflate_timed(raw, raw_len, comp, comp_len, comp_cap, n, nthreads, level, wbits, 1, total_in, bad);
 }

@@ -233,14 +233,14 @@ def test_chunked_random_and_stored(zs):
         assert info["ret"] == 1 and info["total_in"] == len(comp) and out == raw
 
 
-def test_chunked_capacity_retry(zs):
+def test_chunked_no_capacity_guess(zs):
     """Blocks far more compressible than their stream (random bytes, then line
-    text): units outgrow 2 x span x ratio, the chain breaks, and the jobs get a
-    second chunked pass with 8x capacity instead of the serial decoder."""
+    text): unit storage is never sized from the stream's ratio (token pages,
+    exact entry placement), so the chain holds on the first and only pass."""
     import numpy as np
     rng = np.random.default_rng(11)
     raw = rng.integers(0, 256, 4 << 20, dtype=np.uint8).tobytes() + corpus.stream(41, 4 << 20)
-    streams, outs = [], []
+    streams = []
     for wb in (-15, 31):
         c = zlib.compressobj(6, zlib.DEFLATED, wb)
         streams.append(c.compress(raw) + c.flush())
@@ -249,3 +249,92 @@ def test_chunked_capacity_retry(zs):
     for (out, info), comp in zip(got, streams):
         assert info["ret"] == 1 and info["total_in"] == len(comp) and out == raw
     assert st["chunked_jobs"] == 2 and st["fallback_jobs"] == 0, st
+
+
+def test_chunked_overprovisioned_out_cap(zs):
+    """A caller that over-provisions out_cap (64x the output) still takes the
+    chunked path with no fallback: nothing on it depends on out_cap / in_len."""
+    raw = corpus.stream(7, 6 << 20)
+    c = zlib.compressobj(6, zlib.DEFLATED, -15)
+    comp = c.compress(raw) + c.flush()
+    got = zs.inflate_batch([comp], -15, [64 * len(raw)])
+    st = zs.last_stats()
+    assert got[0][0] == raw and got[0][1]["ret"] == 1 and got[0][1]["total_in"] == len(comp)
+    assert st["chunked_jobs"] == 1 and st["fallback_jobs"] == 0, st
+
+
+def test_chunked_fixed_strategy_16mib(zs):
+    """A 16 MiB Z_FIXED stream (fixed-Huffman blocks only, no header to search
+    for): zs_find_fixed_kernel records the block starts, the stream splits into
+    many units, and output + zlib fields match the oracle."""
+    raw = corpus.stream(12, 8 << 20) + corpus.stream(44, 8 << 20)
+    for wb in (-15, 31):
+        c = zlib.compressobj(6, zlib.DEFLATED, wb, 8, zlib.Z_FIXED)
+        comp = c.compress(raw) + c.flush()
+        got = zs.inflate_batch([comp], wb, [len(raw)])
+        st = zs.last_stats()
+        eo, ei = O.oneshot(comp, wb, len(raw))
+        assert got[0][0] == eo == raw and got[0][1] == ei, (got[0][1], ei)
+        assert st["chunked_jobs"] == 1 and st["fallback_jobs"] == 0, st
+        assert st["units"] >= 64, st  # ~16 K-symbol fixed blocks found, not one serial lane
+
+
+def test_chunked_high_ratio(zs):
+    """A ratio > 100 stream (long repeats with sparse changes, a few KiB of
+    input per 4 MiB block) takes the chunked path with no fallback."""
+    import numpy as np
+    rng = np.random.default_rng(3)
+    unit = rng.integers(0, 256, 1500, dtype=np.uint8)
+    reps = np.tile(unit, (24 << 20) // 1500 + 1)[:24 << 20].copy()
+    idx = rng.integers(0, len(reps), len(reps) // 4000)
+    reps[idx] = rng.integers(0, 256, len(idx), dtype=np.uint8)
+    raw = reps.tobytes()
+    c = zlib.compressobj(9, zlib.DEFLATED, -15)
+    comp = c.compress(raw) + c.flush()
+    assert len(raw) / len(comp) > 100
+    got = zs.inflate_batch([comp], -15, [len(raw)])
+    st = zs.last_stats()
+    eo, ei = O.oneshot(comp, -15, len(raw))
+    assert got[0][0] == eo == raw and got[0][1] == ei
+    assert st["chunked_jobs"] == 1 and st["fallback_jobs"] == 0 and st["units"] > 1, st
+
+
+def test_c2_full_size_vs_oracle(zs):
+    """configs[1] at full size: one Zipf and one line-text 64 MiB raw stream
+    (host zlib L6), output and (ret, msg, total_in, total_out) vs the oracle."""
+    raws, comps = corpus.batch(0, 1, 64 << 20, level=6, wbits=-15, nthreads=1)
+    r2, c2 = corpus.batch(32, 1, 64 << 20, level=6, wbits=-15, nthreads=1)
+    raws += r2
+    comps += c2
+    got = zs.inflate_batch([c.tobytes() for c in comps], -15, [64 << 20] * 2)
+    st = zs.last_stats()
+    for r, c, (out, info) in zip(raws, comps, got):
+        eo, ei = O.oneshot(c.tobytes(), -15, 64 << 20)
+        assert info == ei and info["ret"] == 1 and info["total_out"] == 64 << 20
+        assert out == eo and out == r.tobytes()
+    assert st["chunked_jobs"] == 2 and st["fallback_jobs"] == 0, st
+
+
+def test_c5_shape_vs_oracle(zs):
+    """configs[4] shape: 256 x 4 MiB, raw (-15) / gzip (31) alternating, Zipf /
+    line text alternating in pairs (corpus.c5_stream), host zlib L6; every job's
+    output and zlib fields vs the oracle, all on the chunked path."""
+    from concurrent.futures import ThreadPoolExecutor
+    n = 256
+
+    def make(k):
+        raw, wb = corpus.c5_stream(k, 4 << 20)
+        c = zlib.compressobj(6, zlib.DEFLATED, wb, 8)
+        return raw.tobytes(), c.compress(raw.tobytes()) + c.flush(), wb
+
+    with ThreadPoolExecutor(16) as ex:
+        cases = list(ex.map(make, range(n)))
+    got = zs.inflate_batch([c[1] for c in cases], [c[2] for c in cases], [4 << 20] * n)
+    st = zs.last_stats()
+    bad = []
+    for k, ((raw, comp, wb), (out, info)) in enumerate(zip(cases, got)):
+        eo, ei = O.oneshot(comp, wb, 4 << 20)
+        if out != eo or info != ei or out != raw:
+            bad.append((k, wb, info, ei))
+    assert not bad, bad[:4]
+    assert st["chunked_jobs"] == n and st["fallback_jobs"] == 0, st

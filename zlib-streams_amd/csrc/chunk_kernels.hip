@@ -299,14 +299,153 @@ __global__ void __launch_bounds__(64) zs_find_kernel(const ZsJobDev *__restrict_
 }
 
 // ---------------------------------------------------------------------------
+// Fixed-Huffman block finder (src/inflate.c:834-869, BTYPE = 1), for search
+// segments in which zs_find_kernel recorded no dynamic start (streams written
+// with Z_FIXED, or long runs of fixed blocks).  A fixed block has no header
+// to validate, so a candidate bit p must (a) follow a fixed-code end of block
+// (the 7-bit code 0000000 at p-7..p-1), (b) carry BTYPE = 01 (BFINAL = 0 unless
+// this is one of the stream's last segments), and (c) decode FIXED_CHECK
+// fixed-code symbols (or reach an end of block after at least FIXED_MIN of
+// them) without an invalid literal/length (286, 287) or distance (30, 31)
+// code.  The chain check of zs_chain_kernel keeps results exact whatever is
+// recorded; (c) only keeps false starts rare.
+// ---------------------------------------------------------------------------
+#define FIXED_CHECK 384
+#define FIXED_MIN 64
+
+__device__ bool fixed_plausible(const uint32_t *w, uint32_t end_byte, uint32_t bit) {
+  const uint32_t limit = end_byte * 8u;
+  uint32_t wi = bit >> 5;
+  uint64_t hold = (uint64_t)in_word(w, wi, end_byte) >> (bit & 31);
+  uint32_t n = 32 - (bit & 31);
+  wi++;
+  uint32_t pos = bit + 3;
+  hold >>= 3;
+  n -= 3;
+  for (uint32_t k = 0; k < FIXED_CHECK; k++) {
+    if (n <= 32) {
+      hold |= (uint64_t)in_word(w, wi, end_byte) << n;
+      n += 32;
+      wi++;
+    }
+    // literal/length: 7-bit codes 256..279, 8-bit 0..143 and 280..287, 9-bit 144..255
+    const uint32_t r9 = __builtin_bitreverse32((uint32_t)hold) >> 23;  // next 9 bits, first bit highest
+    const uint32_t c7 = r9 >> 2, c8 = r9 >> 1;
+    uint32_t sym, used;
+    if (c7 < 24u) {
+      sym = 256 + c7;
+      used = 7;
+    } else if (c8 < 0xc0u) {
+      sym = c8 - 0x30u;
+      used = 8;
+    } else if (c8 < 0xc8u) {
+      sym = 280 + (c8 - 0xc0u);
+      used = 8;
+    } else {
+      sym = 144 + (r9 - 0x190u);
+      used = 9;
+    }
+    hold >>= used;
+    n -= used;
+    pos += used;
+    if (sym == 256) return k >= FIXED_MIN;
+    if (sym > 285) return false;
+    if (sym > 256) {
+      const uint32_t ls = sym - 257;
+      const uint32_t xb = (ls >= 8 && ls < 28) ? (ls >> 2) - 1 : 0u;
+      hold >>= xb;
+      n -= xb;
+      pos += xb;
+      if (n <= 32) {
+        hold |= (uint64_t)in_word(w, wi, end_byte) << n;
+        n += 32;
+        wi++;
+      }
+      const uint32_t d = __builtin_bitreverse32((uint32_t)hold) >> 27;
+      if (d >= 30) return false;
+      const uint32_t dx = d < 4 ? 0u : (d >> 1) - 1;
+      hold >>= 5 + dx;
+      n -= 5 + dx;
+      pos += 5 + dx;
+    }
+    if (pos > limit) return false;
+  }
+  return true;
+}
+
+__global__ void __launch_bounds__(64) zs_find_fixed_kernel(const ZsJobDev *__restrict__ jobs, const ZsHeadDev *__restrict__ heads,
+                                                            ZsSegDev *__restrict__ segs) {
+  __shared__ uint32_t s_q[WAVE * 32];
+  const uint32_t lane = threadIdx.x;
+  const uint32_t sg = blockIdx.x;
+  const ZsSegDev seg = segs[sg];
+  if (seg.ncand != 0) return;
+  const ZsJobDev jb = jobs[seg.job];
+  const ZsHeadDev hd = heads[seg.job];
+  if (hd.code != ZD_END) return;
+  const uintptr_t ip = reinterpret_cast<uintptr_t>(jb.in);
+  const uint32_t mis = (uint32_t)(ip & 3u);
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(ip - mis);
+  const uint32_t end_byte = mis + (uint32_t)jb.in_len;
+  const uint32_t lo = max((mis + seg.s_byte) * 8u, (mis + (uint32_t)hd.start_byte) * 8u + 8u);
+  const uint32_t hi = (mis + seg.e_byte) * 8u;
+  uint32_t nfound = 0;
+  for (uint32_t base = lo & ~31u; base < hi && nfound < SEG_SLOTS; base += WAVE * 32u) {
+    const uint32_t b0 = base + lane * 32u;
+    uint32_t cand = 0;
+    if (b0 < hi) {
+      const uint32_t wi = b0 >> 5;
+      const uint32_t pw = wi ? in_word(w, wi - 1, end_byte) : 0u;
+      const uint64_t lw = (uint64_t)pw | ((uint64_t)in_word(w, wi, end_byte) << 32);
+      const uint64_t y = (lw >> 25) | ((uint64_t)in_word(w, wi + 1, end_byte) << 39);  // bit k = stream bit b0 - 7 + k
+      const uint64_t z = ~y;
+      const uint64_t eob = z & (z >> 1) & (z >> 2) & (z >> 3) & (z >> 4) & (z >> 5) & (z >> 6);
+      const uint64_t bt = (y >> 8) & ~(y >> 9);
+      cand = (uint32_t)(eob & bt & (seg.final_ok ? ~0ull : ~(y >> 7)));
+      if (b0 < lo) cand &= lo - b0 >= 32u ? 0u : ~0u << (lo - b0);
+      if (hi - b0 < 32u) cand &= (1u << (hi - b0)) - 1u;
+    }
+    uint32_t tot;
+    const uint32_t at = find_scan_excl((uint32_t)__builtin_popcount(cand), &tot);
+    for (uint32_t k = 0; cand; k++) {
+      s_q[at + k] = b0 + (uint32_t)__builtin_ctz(cand);
+      cand &= cand - 1u;
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t q0 = 0; q0 < tot && nfound < SEG_SLOTS; q0 += WAVE) {
+      const uint32_t take = min(tot - q0, (uint32_t)WAVE);
+      uint32_t cb = 0;
+      bool ok = false;
+      if (lane < take) {
+        cb = s_q[q0 + lane];
+        ok = fixed_plausible(w, end_byte, cb);
+      }
+      uint64_t m = __ballot(ok);
+      while (m && nfound < SEG_SLOTS) {
+        const uint32_t l = (uint32_t)__builtin_ctzll(m);
+        m &= m - 1;
+        const uint32_t f = __builtin_amdgcn_readlane(cb, l);
+        if (lane == 0) segs[sg].cand[nfound] = f;
+        nfound++;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (lane == 0) segs[sg].ncand = nfound;
+}
+
+// ---------------------------------------------------------------------------
 // Plan: one workgroup per chunked job.  Units = the stream's first block +
-// every recorded start, in order; each unit's stop is the next unit's start;
-// scratch/token capacity per unit = 2 x its compressed span x the job's
-// output/input ratio + slack, carved from the job's host-reserved range.
-// Unused unit slots of the job are marked inactive.
+// every recorded start, in order; each unit's stop is the next unit's start.
+// Each unit gets a primary token region sized from its own compressed span
+// (TOK_PER_BYTE tokens per span byte + TOK_SLACK), carved from the job's
+// host-reserved range; tokens beyond it go to pool pages taken on demand by
+// the parse pass (ZsTokPool), so a unit never fails for an underestimated
+// size.  Output entries are not reserved here at all: zs_chain_kernel places
+// every verified unit at its exact output offset.  Unused slots are marked
+// inactive.
 // ---------------------------------------------------------------------------
 #define PLAN_T 256
-#define UNIT_SLACK 8192u  // entries of slack per unit
 
 __device__ uint32_t plan_block_scan(uint32_t v, uint32_t *s_tmp, uint32_t *total) {  // exclusive, PLAN_T threads
   const uint32_t t = threadIdx.x, lane = t & (WAVE - 1), wv = t / WAVE;
@@ -327,7 +466,7 @@ __device__ uint32_t plan_block_scan(uint32_t v, uint32_t *s_tmp, uint32_t *total
 
 __global__ void __launch_bounds__(PLAN_T) zs_plan_kernel(const ZsJobDev *__restrict__ jobs, const ZsHeadDev *__restrict__ heads,
                                                           const ZsSegDev *__restrict__ segs, ZsCJobDev *__restrict__ cjobs,
-                                                          ZsChunkDev *__restrict__ units) {
+                                                          ZsChunkDev *__restrict__ units, ZsTokPool pool) {
   __shared__ uint32_t s_tmp[PLAN_T / WAVE];
   __shared__ uint64_t s_cap_base;
   __shared__ uint64_t s_c[PLAN_T];
@@ -337,7 +476,7 @@ __global__ void __launch_bounds__(PLAN_T) zs_plan_kernel(const ZsJobDev *__restr
   const ZsHeadDev hd = heads[cj.job];
   const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(jb.in) & 3u);
   const uint32_t end_bit = (mis + (uint32_t)jb.in_len) * 8u;
-  const double ratio = fmax(1.0, (double)jb.out_cap / fmax(1.0, (double)jb.in_len));
+  const uint32_t ecap = (uint32_t)min<uint64_t>(jb.out_cap, 0xfff00000ull);
   uint32_t nunits = 0;
   if (hd.code == ZD_END) {
     // unit index of each segment's first candidate (unit 0 = stream start)
@@ -362,7 +501,7 @@ __global__ void __launch_bounds__(PLAN_T) zs_plan_kernel(const ZsJobDev *__restr
       units[cj.unit0] = u;
     }
     __syncthreads();
-    // stops, spans, capacities (scanned in u64 through per-thread sums)
+    // stops, spans, primary token regions (scanned in u64 through per-thread sums)
     for (uint32_t u0 = 0; u0 < nunits; u0 += PLAN_T) {
       const uint32_t i = u0 + t;
       uint64_t cap = 0;
@@ -371,14 +510,9 @@ __global__ void __launch_bounds__(PLAN_T) zs_plan_kernel(const ZsJobDev *__restr
         st = units[cj.unit0 + i].start_bit;
         sp = i + 1 < nunits ? units[cj.unit0 + i + 1].start_bit : ZS_NONE;
         const uint32_t span_bytes = ((sp == ZS_NONE ? end_bit : sp) - st + 7u) / 8u;
-        cap = ((uint64_t)((double)cj.cap_mul * span_bytes * ratio) + UNIT_SLACK + 7u) & ~7ull;
-        // a false start shortly after a real one leaves a short span but a
-        // whole block to decode: such units get the job's output capacity
-        for (uint32_t b = 0; b < cj.n_boost && b < 4; b++)
-          if (cj.boost[b] == i) cap = max(cap, ((uint64_t)cj.boost_cap + UNIT_SLACK + 7u) & ~7ull);
-        if (cap > 0xfff00000ull) cap = 0xfff00000ull;
+        cap = ((uint64_t)span_bytes * ZS_TOK_PER_BYTE + ZS_TOK_SLACK + 7u) & ~7ull;
       }
-      // exclusive u64 prefix of the capacities (thread 0 walks the tile)
+      // exclusive u64 prefix of the regions (thread 0 walks the tile)
       s_c[t] = cap;
       __syncthreads();
       if (t == 0) {
@@ -402,13 +536,16 @@ __global__ void __launch_bounds__(PLAN_T) zs_plan_kernel(const ZsJobDev *__restr
         u.stop_bit = sp;
         u.end_bit = 0;
         u.code = ZD_SKIP;
-        u.cap = (uint32_t)cap;
+        u.cap = ecap;
         u.tcap = (uint32_t)cap;
-        u.scratch = cj.scratch0 + pre;
-        u.tok = cj.scratch0 + pre;
+        u.scratch = 0;
+        u.tok = cj.tok0 + pre;
         u.chain_next = ZS_NONE;
         u.in_chain = 0;
         units[cj.unit0 + i] = u;  // start_bit unchanged: neighbours' reads stay valid
+        uint4 *pt = reinterpret_cast<uint4 *>(pool.ptab + (size_t)(cj.unit0 + i) * ZS_TP_MAXPG);
+#pragma unroll
+        for (int k = 0; k < ZS_TP_MAXPG / 4; k++) pt[k] = make_uint4(0, 0, 0, 0);
       }
       __syncthreads();
     }
@@ -423,7 +560,11 @@ __global__ void __launch_bounds__(PLAN_T) zs_plan_kernel(const ZsJobDev *__restr
     u.chain_next = ZS_NONE;
     units[cj.unit0 + i] = u;
   }
-  if (t == 0) cjobs[blockIdx.x].nunits = nunits;
+  if (t == 0) {
+    cjobs[blockIdx.x].nunits = nunits;
+    cjobs[blockIdx.x].nchain = 0;
+    cjobs[blockIdx.x].ok = 0;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -447,16 +588,17 @@ __global__ void __launch_bounds__(64) zs_fixed_tables_kernel(uint32_t *__restric
 }
 
 // ---------------------------------------------------------------------------
-// Link (one 1024-thread workgroup per stream):
+// Chain (one 1024-thread workgroup per stream), between parse and expand:
 //   A. in parallel, every unit finds its successor: the first later unit whose
 //      start is its end bit (recorded starts that are not block boundaries
 //      are skipped; starts ascend, so the search stops early);
 //   B. thread 0 walks the successors (in LDS for up to LINK_MAXU units),
 //      assigning output offsets and writing the chain in order to `info`;
-//   C. the 32 KiB history windows are resolved in chain order from each
-//      unit's last HIST entries; the entries of the next chain member are
-//      loaded into registers while the current one resolves (one memory
-//      latency per step is hidden behind the LDS work).
+//      every chain member's u16 entries are placed at the job's entry base +
+//      its output offset, so entry space is exact (no per-unit estimate) and
+//      the expand pass runs only on chain members.
+// Any break (a unit that did not end at a block boundary, no successor, more
+// output than out_cap) sends the stream to the exact serial decoder.
 // ---------------------------------------------------------------------------
 #define LINK_THREADS 1024
 #define LINK_PER (HIST / LINK_THREADS)  // window entries per thread and chain step
@@ -468,36 +610,11 @@ struct ZsLinkInfo {
   uint32_t unit;  // unit index (ord 0 <=> first of the job)
 };
 
-// thread t owns window entries 4t + 4096 g + {0..3}, g < LINK_PER / 4; entry
-// pairs are packed in u32 (2 per word, 2 words per group)
-#define LINK_G (LINK_PER / 4)
-__device__ __forceinline__ void link_load(const uint16_t *__restrict__ scratch, const ZsLinkInfo &li, uint32_t t,
-                                          uint2 (&v)[LINK_G]) {
-  const uint32_t n = li.n_out;
-  const uint16_t *e = scratch + li.scratch;
-#pragma unroll
-  for (int g = 0; g < LINK_G; g++) {
-    const uint32_t i = (uint32_t)g * (LINK_THREADS * 4) + t * 4;
-    if (n >= HIST) {
-      __builtin_memcpy(&v[g], e + (n - HIST) + i, 8);
-    } else {  // short unit: entry i exists only for i >= HIST - n
-      uint16_t x[4];
-      for (int k = 0; k < 4; k++) x[k] = (i + k >= HIST - n) ? e[i + k - (HIST - n)] : (uint16_t)0;
-      __builtin_memcpy(&v[g], x, 8);
-    }
-  }
-}
-
-__global__ void __launch_bounds__(LINK_THREADS) zs_link_kernel(const ZsJobDev *__restrict__ jobs, const ZsHeadDev *__restrict__ heads,
-                                                               ZsChunkDev *__restrict__ chunks, const ZsCJobDev *__restrict__ cjobs,
-                                                               const uint16_t *__restrict__ scratch, uint8_t *__restrict__ windows,
-                                                               ZsLinkInfo *__restrict__ info, ZsDecDev *__restrict__ decs,
-                                                               uint32_t *__restrict__ fallback) {
-  __shared__ uint8_t s_win[2][HIST];
+__global__ void __launch_bounds__(LINK_THREADS) zs_chain_kernel(const ZsJobDev *__restrict__ jobs, const ZsHeadDev *__restrict__ heads,
+                                                                ZsChunkDev *__restrict__ chunks, ZsCJobDev *__restrict__ cjobs,
+                                                                ZsLinkInfo *__restrict__ info, ZsDecDev *__restrict__ decs,
+                                                                uint32_t *__restrict__ fallback) {
   __shared__ uint16_t s_succ[LINK_MAXU];  // successor - unit (0: none / end)
-  __shared__ uint32_t s_ok, s_len;
-  __shared__ uint32_t s_end_bit;
-  __shared__ uint64_t s_total;
   const uint32_t t = threadIdx.x;
   const ZsCJobDev cj = cjobs[blockIdx.x];
   const ZsJobDev jb = jobs[cj.job];
@@ -516,11 +633,6 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_link_kernel(const ZsJobDev *_
   }
   const uint32_t u0 = cj.unit0, nu = cj.nunits, last = u0 + nu;
   const bool small = nu <= LINK_MAXU;
-#if KP_ON
-  const uint64_t kt0 = KP_NOW();
-  uint64_t kt_ww = 0, kt_res = 0, kt_bar = 0;
-  uint32_t kmark = 0;
-#endif
   // A: successors
   for (uint32_t i = u0 + t; i < last; i += LINK_THREADS) {
     const ZsChunkDev ch = chunks[i];
@@ -540,29 +652,28 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_link_kernel(const ZsJobDev *_
     if (small) s_succ[i - u0] = (k == ZS_NONE || k - i > 0xffffu) ? (uint16_t)0 : (uint16_t)(k - i);
   }
   __syncthreads();
-#if KP_ON
-  const uint64_t kt1 = KP_NOW();
-#endif
   // B: walk the chain
   if (t == 0) {
     uint32_t c = u0, len = 0, ok = 1, end_bit = 0;
-    uint64_t total = 0;
+    uint64_t total = 0, spos = 0;  // output bytes; entries used (each member starts 8-entry aligned)
     for (;;) {
       const ZsChunkDev ch = chunks[c];
       const int code = ch.code & 0xff;
-      if (code != ZD_STOP && code != ZD_END) {
+      spos = (spos + 7u) & ~7ull;
+      if ((code != ZD_STOP && code != ZD_END) || spos + ch.n_out > cj.scratch_n) {
         ok = 0;
         break;
       }
       ZsLinkInfo li;
-      li.scratch = ch.scratch;
+      li.scratch = cj.scratch0 + spos;
       li.n_out = ch.n_out;
       li.unit = c;
       info[u0 + len] = li;
       len++;
       chunks[c].out_off = total;
-      chunks[c].in_chain = 1;
+      chunks[c].scratch = cj.scratch0 + spos;
       total += ch.n_out;
+      spos += ch.n_out;
       if (code == ZD_END) {
         end_bit = ch.end_bit;
         break;
@@ -581,21 +692,84 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_link_kernel(const ZsJobDev *_
       c = k;
     }
     if (total > jb.out_cap) ok = 0;
-    s_ok = ok;
-    s_total = total;
-    s_end_bit = end_bit;
-    s_len = len;
+    if (ok) {  // members are flagged only once the whole chain holds
+      for (uint32_t j = 0; j < len; j++) chunks[info[u0 + j].unit].in_chain = 1;
+      ZsDecDev d;
+      d.code = ZD_END;
+      d.msg = 0;
+      const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(jb.in) & 3u);
+      d.end_bits = end_bit - mis * 8u;
+      d.total_out = total;
+      decs[cj.job] = d;
+    }
+    fallback[cj.job] = ok ? 0u : 1u;
+    cjobs[blockIdx.x].nchain = ok ? len : 0u;
+    cjobs[blockIdx.x].ok = ok;
   }
-  __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// Link (one 1024-thread workgroup per verified stream), after expand: the
+// 32 KiB history windows are resolved in chain order from each unit's last
+// HIST entries; the entries of the next chain member are loaded into
+// registers while the current one resolves (one memory latency per step is
+// hidden behind the LDS work).
+// ---------------------------------------------------------------------------
+// thread t owns window entries 4t + 4096 g + {0..3}, g < LINK_PER / 4; entry
+// pairs are packed in u32 (2 per word, 2 words per group)
+#define LINK_G (LINK_PER / 4)
+__device__ __forceinline__ void link_load(const uint16_t *__restrict__ scratch, const ZsLinkInfo &li, uint32_t t,
+                                          uint2 (&v)[LINK_G]) {
+  const uint32_t n = li.n_out;
+  if (n >= HIST) {
+    // entries of a chain member start at any entry index: two aligned 8-byte
+    // loads and a funnel shift give the thread's 4 entries
+    const uint64_t b = li.scratch + n - HIST;
+    const uint32_t m = (uint32_t)(b & 3u);
+    const uint2 *al = reinterpret_cast<const uint2 *>(scratch + (b - m));
+#pragma unroll
+    for (int g = 0; g < LINK_G; g++) {
+      const uint32_t i = (uint32_t)g * (LINK_THREADS * 4) + t * 4;
+      const uint2 lo = al[i / 4];
+      if (m == 0) {
+        v[g] = lo;
+      } else {
+        const uint2 hi = al[i / 4 + 1];
+        const uint64_t a = (uint64_t)lo.x | ((uint64_t)lo.y << 32), c = (uint64_t)hi.x | ((uint64_t)hi.y << 32);
+        const uint64_t r = (a >> (16 * m)) | (c << (64 - 16 * m));
+        v[g] = make_uint2((uint32_t)r, (uint32_t)(r >> 32));
+      }
+    }
+  } else {  // short unit: entry i exists only for i >= HIST - n
+    const uint16_t *e = scratch + li.scratch;
+#pragma unroll
+    for (int g = 0; g < LINK_G; g++) {
+      const uint32_t i = (uint32_t)g * (LINK_THREADS * 4) + t * 4;
+      uint16_t x[4];
+      for (int k = 0; k < 4; k++) x[k] = (i + k + n >= HIST) ? e[i + k + n - HIST] : (uint16_t)0;
+      __builtin_memcpy(&v[g], x, 8);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(LINK_THREADS) zs_link_kernel(const ZsJobDev *__restrict__ jobs, ZsCJobDev *__restrict__ cjobs,
+                                                               const uint16_t *__restrict__ scratch, uint8_t *__restrict__ windows,
+                                                               const ZsLinkInfo *__restrict__ info, uint32_t *__restrict__ fallback) {
+  __shared__ uint8_t s_win[2][HIST];
+  __shared__ uint32_t s_bad;
+  const uint32_t t = threadIdx.x;
+  const ZsCJobDev cj = cjobs[blockIdx.x];
+  if (!cj.ok) return;
+  (void)jobs;
+  const uint32_t u0 = cj.unit0;
+  const uint32_t len = cj.nchain;
 #if KP_ON
-  const uint64_t kt2 = KP_NOW();
+  const uint64_t kt0 = KP_NOW();
+  uint64_t kt_ww = 0, kt_res = 0, kt_bar = 0;
+  uint32_t kmark = 0;
 #endif
-  if (!s_ok) {
-    if (t == 0) fallback[cj.job] = 1;
-    return;
-  }
-  // C: history windows in chain order: W holds the last HIST bytes before unit c
-  const uint32_t len = s_len;
+  if (t == 0) s_bad = 0;
+  // W holds the last HIST bytes before unit c
   uint32_t wv = 0;  // valid bytes of history
   int cur = 0;
   uint2 v[LINK_G], vn[LINK_G];
@@ -616,7 +790,7 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_link_kernel(const ZsJobDev *_
 #if KP_ON
     const uint64_t ka = KP_NOW();
 #endif
-    if (c != u0) {
+    if (j != 0) {
       uint8_t *g = windows + (size_t)c * HIST;
       for (uint32_t i = t * 16; i < HIST; i += LINK_THREADS * 16)
         *reinterpret_cast<uint4 *>(g + i) = *reinterpret_cast<const uint4 *>(W + i);
@@ -681,7 +855,7 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_link_kernel(const ZsJobDev *_
 #pragma unroll
     for (int g = 0; g < LINK_G; g++) v[g] = vn[g];
   }
-  if (bad) s_ok = 0;
+  if (bad) s_bad = 1;
   __syncthreads();
 #if KP_ON
   if ((t & 63) == 0) KPC_ADD(KP_L_MARKERS, kmark);  // lane 0 of each wave: a sample
@@ -689,8 +863,6 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_link_kernel(const ZsJobDev *_
     const uint64_t tot = KP_NOW() - kt0;
     KPC_ADD(KP_L_STREAMS, 1);
     KPC_ADD(KP_L_STEPS, len);
-    KPC_ADD(KP_L_CYC_SUCC, kt1 - kt0);
-    KPC_ADD(KP_L_CYC_WALK, kt2 - kt1);
     KPC_ADD(KP_L_CYC_WINWRITE, kt_ww);
     KPC_ADD(KP_L_CYC_RESOLVE, kt_res);
     KPC_ADD(KP_L_CYC_BARRIER, kt_bar);
@@ -698,19 +870,9 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_link_kernel(const ZsJobDev *_
     KPC_MAX(KP_L_CYC_MAX, tot);
   }
 #endif
-  if (t == 0) {
-    if (!s_ok) {
-      fallback[cj.job] = 1;
-    } else {
-      fallback[cj.job] = 0;
-      ZsDecDev d;
-      d.code = ZD_END;
-      d.msg = 0;
-      const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(jb.in) & 3u);
-      d.end_bits = s_end_bit - mis * 8u;
-      d.total_out = s_total;
-      decs[cj.job] = d;
-    }
+  if (t == 0 && s_bad) {  // a marker reached before the stream start: the serial decoder reports it
+    fallback[cj.job] = 1;
+    cjobs[blockIdx.x].ok = 0;
   }
 }
 
@@ -777,24 +939,33 @@ extern "C" void zs_launch_fixed_tables(uint32_t *fixed, hipStream_t st) {
   hipLaunchKernelGGL(zs_fixed_tables_kernel, dim3(1), dim3(64), 0, st, fixed);
 }
 
-extern "C" void zs_launch_lane(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, ZsChunkDev *d_chunks, uint32_t nchunks,
-                               uint16_t *d_scratch, uint32_t *d_tokens, uint32_t *d_tables, const uint32_t *d_fixed,
-                               hipStream_t st, hipEvent_t *ev);
+extern "C" void zs_launch_parse(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, ZsChunkDev *d_chunks, uint32_t nchunks,
+                                uint32_t *d_tokens, uint32_t *d_tables, const uint32_t *d_fixed, ZsTokPool pool,
+                                hipStream_t st);
+extern "C" void zs_launch_expand(const ZsJobDev *d_jobs, ZsChunkDev *d_chunks, uint32_t nchunks, uint16_t *d_scratch,
+                                 const uint32_t *d_tokens, ZsTokPool pool, hipStream_t st);
 
 extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, ZsSegDev *d_segs, uint32_t nseg,
                                   ZsCJobDev *d_cjobs, uint32_t ncjobs, ZsChunkDev *d_units, uint32_t nunit_slots,
-                                  uint16_t *d_scratch, uint32_t *d_tokens, uint32_t *d_tables, const uint32_t *d_fixed,
-                                  uint8_t *d_windows, void *d_linkinfo, ZsDecDev *d_decs, uint32_t *d_fallback,
-                                  hipStream_t st, hipEvent_t *ev) {
+                                  uint16_t *d_scratch, uint32_t *d_tokens, ZsTokPool pool, uint32_t *d_tables,
+                                  const uint32_t *d_fixed, uint8_t *d_windows, void *d_linkinfo, ZsDecDev *d_decs,
+                                  uint32_t *d_fallback, hipStream_t st, hipEvent_t *ev) {
   // ev (profiling, optional): [0] before find, [1] after find + plan, [2] after
-  // parse, [3] after expand, [4] after link, [5] after emit
+  // parse + chain, [3] after expand, [4] after link, [5] after emit
   if (ev) (void)hipEventRecord(ev[0], st);
   hipLaunchKernelGGL(zs_find_kernel, dim3(nseg), dim3(64), 0, st, d_jobs, d_heads, d_segs);
-  hipLaunchKernelGGL(zs_plan_kernel, dim3(ncjobs), dim3(PLAN_T), 0, st, d_jobs, d_heads, d_segs, d_cjobs, d_units);
+  hipLaunchKernelGGL(zs_find_fixed_kernel, dim3(nseg), dim3(64), 0, st, d_jobs, d_heads, d_segs);
+  hipLaunchKernelGGL(zs_plan_kernel, dim3(ncjobs), dim3(PLAN_T), 0, st, d_jobs, d_heads, d_segs, d_cjobs, d_units, pool);
   if (ev) (void)hipEventRecord(ev[1], st);
-  zs_launch_lane(d_jobs, d_heads, d_units, nunit_slots, d_scratch, d_tokens, d_tables, d_fixed, st, ev ? ev + 2 : nullptr);
-  hipLaunchKernelGGL(zs_link_kernel, dim3(ncjobs), dim3(LINK_THREADS), 0, st, d_jobs, d_heads, d_units, d_cjobs,
-                     d_scratch, d_windows, reinterpret_cast<ZsLinkInfo *>(d_linkinfo), d_decs, d_fallback);
+  ZsLinkInfo *info = reinterpret_cast<ZsLinkInfo *>(d_linkinfo);
+  zs_launch_parse(d_jobs, d_heads, d_units, nunit_slots, d_tokens, d_tables, d_fixed, pool, st);
+  hipLaunchKernelGGL(zs_chain_kernel, dim3(ncjobs), dim3(LINK_THREADS), 0, st, d_jobs, d_heads, d_units, d_cjobs, info,
+                     d_decs, d_fallback);
+  if (ev) (void)hipEventRecord(ev[2], st);
+  zs_launch_expand(d_jobs, d_units, nunit_slots, d_scratch, d_tokens, pool, st);
+  if (ev) (void)hipEventRecord(ev[3], st);
+  hipLaunchKernelGGL(zs_link_kernel, dim3(ncjobs), dim3(LINK_THREADS), 0, st, d_jobs, d_cjobs, d_scratch, d_windows, info,
+                     d_fallback);
   if (ev) (void)hipEventRecord(ev[4], st);
   hipLaunchKernelGGL(zs_emit_kernel, dim3(nunit_slots), dim3(EMIT_THREADS), 0, st, d_jobs, d_units, d_scratch, d_windows,
                      d_fallback);

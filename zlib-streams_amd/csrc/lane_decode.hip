@@ -117,6 +117,36 @@ __device__ __forceinline__ uint32_t in_word_g(gcu32 *w, uint32_t wi, uint32_t en
   return keep >= 4u ? v : __builtin_amdgcn_ubfe(v, 0, 8u * keep);
 }
 
+// Token storage (zs_common.h): token x of a unit lives in its primary
+// region (x < tcap) or in pool page ptab[(x - tcap) >> ZS_TP_LOG].  Only the
+// unit's writer calls tok_ensure (one lane at a time); pages are taken from
+// the pool with one atomic each.  Returns false when the pool (or the unit's
+// page table) is exhausted.
+__device__ __forceinline__ bool tok_ensure(const ZsTokPool &pool, uint32_t unit, uint32_t tcap, uint32_t x_end) {
+  if (x_end <= tcap) return true;
+  const uint32_t kl = (x_end - 1u - tcap) >> ZS_TP_LOG;
+  if (kl >= ZS_TP_MAXPG) return false;
+  uint32_t *pt = pool.ptab + (size_t)unit * ZS_TP_MAXPG;
+  for (uint32_t k = 0; k <= kl; k++) {
+    uint32_t pg = __hip_atomic_load(pt + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!pg) {
+      pg = atomicAdd(pool.next, 1u) + 1u;
+      if (pg > pool.npages) return false;
+      __hip_atomic_store(pt + k, pg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  return true;
+}
+// address of token x (pages already ensured); page ids are read from L2
+__device__ __forceinline__ uint32_t *tok_addr(const ZsTokPool &pool, uint32_t *tokens, uint32_t unit, uint64_t prim,
+                                              uint32_t tcap, uint32_t x) {
+  if (x < tcap) return tokens + prim + x;
+  const uint32_t r = x - tcap;
+  const uint32_t pg =
+      __hip_atomic_load(pool.ptab + (size_t)unit * ZS_TP_MAXPG + (r >> ZS_TP_LOG), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return tokens + pool.base + ((uint64_t)(pg - 1u) << ZS_TP_LOG) + (r & ((1u << ZS_TP_LOG) - 1u));
+}
+
 enum { LM_SYM = 0, LM_BLOCK = 1, LM_DONE = 2 };
 
 struct KpPhase {
@@ -130,8 +160,9 @@ struct LaneState {
   uint32_t rk;        // ring index of nw during a group
   uint32_t lastw;     // last word index holding input
   uint64_t hold;
-  gu32 *tok;          // token output (parse pass)
+  gu32 *tok;          // primary token region (parse pass); later tokens: pool pages
   uint32_t ntok, tcap;
+  uint32_t unit;      // unit slot (page table row)
   uint32_t gk;        // tokens of the current group (in LDS)
 #if KP_ON
   uint32_t kp_steps, kp_slow_l, kp_slow_d, kp_refills;
@@ -583,7 +614,8 @@ __device__ void install_roots(LaneLDS &L, uint32_t ln, const uint32_t *zl, uint3
 // Cooperative block-boundary processing for lane `ln` (all lanes call it with
 // the same ln): end/stop checks, stored blocks, fixed and dynamic headers
 // (src/inflate.c:834-1033); installs the lane's tables.
-__device__ void coop_block(LaneState &s, uint32_t ln, LaneLDS &L, uint32_t *lane_tab, const uint32_t *fixed) {
+__device__ void coop_block(LaneState &s, uint32_t ln, LaneLDS &L, uint32_t *lane_tab, const uint32_t *fixed,
+                           uint32_t *tokens, const ZsTokPool &pool) {
   const uint32_t lane = lane_id();
   const uint32_t *w = reinterpret_cast<const uint32_t *>(readlane_ptr((const void *)(uintptr_t)s.w, ln));
   uint32_t *tok = reinterpret_cast<uint32_t *>(readlane_ptr((const void *)(uintptr_t)s.tok, ln));
@@ -639,15 +671,33 @@ __device__ void coop_block(LaneState &s, uint32_t ln, LaneLDS &L, uint32_t *lane
         code = ZD_TRUNC;
         break;
       }
-      if (pos + n > cap || ntok + n > tcap) {
+      if (pos + n > cap) {
         code = ZD_FULL;
         break;
       }
       {  // stored bytes become literal tokens (coalesced: 64 per store)
         const uint32_t b0 = bit / 8;
-        for (uint32_t k = lane; k < n; k += WAVE) {
-          const uint32_t b = b0 + k;
-          tok[ntok + k] = (w[b >> 2] >> (8u * (b & 3u))) & 0xffu;
+        if (ntok + n <= tcap) {
+          for (uint32_t k = lane; k < n; k += WAVE) {
+            const uint32_t b = b0 + k;
+            tok[ntok + k] = (w[b >> 2] >> (8u * (b & 3u))) & 0xffu;
+          }
+        } else {  // past the primary region: pool pages (taken by lane 0, then visible to all)
+          const uint32_t unit = __builtin_amdgcn_readlane(s.unit, ln);
+          uint32_t okp = 1;
+          if (lane == 0) okp = tok_ensure(pool, unit, tcap, ntok + n) ? 1u : 0u;
+          okp = __builtin_amdgcn_readfirstlane(okp);
+          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+          if (!okp) {
+            code = ZD_FULL;
+            break;
+          }
+          const uint32_t *prim = reinterpret_cast<const uint32_t *>(readlane_ptr((const void *)(uintptr_t)s.tok, ln));
+          const uint64_t prim_off = (uint64_t)(prim - tokens);
+          for (uint32_t k = lane; k < n; k += WAVE) {
+            const uint32_t b = b0 + k;
+            *tok_addr(pool, tokens, unit, prim_off, tcap, ntok + k) = (w[b >> 2] >> (8u * (b & 3u))) & 0xffu;
+          }
         }
         ntok += n;
       }
@@ -700,7 +750,7 @@ __device__ void coop_block(LaneState &s, uint32_t ln, LaneLDS &L, uint32_t *lane
       s.dbits = dbits;
       s.cl = (gcu16 *)cl;
       s.cd = (gcu16 *)cd;
-      s.capx = min(cap, pos + (tcap - ntok));
+      s.capx = cap;
       lane_prime(s, bit);
     } else {
       s.code = code;
@@ -712,7 +762,8 @@ __device__ void coop_block(LaneState &s, uint32_t ln, LaneLDS &L, uint32_t *lane
 __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict__ jobs, const ZsHeadDev *__restrict__ heads,
                                                       ZsChunkDev *__restrict__ chunks, uint32_t nchunks,
                                                       uint32_t *__restrict__ tokens, uint32_t *__restrict__ tables,
-                                                      const uint32_t *__restrict__ fixed, const uint32_t *__restrict__ order) {
+                                                      const uint32_t *__restrict__ fixed, const uint32_t *__restrict__ order,
+                                                      ZsTokPool pool) {
   __shared__ LaneLDS L;
   const uint32_t lane = threadIdx.x;
   // units by decreasing span: a wave's lanes run similar lengths, the longest first
@@ -729,6 +780,7 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
   s.tok = nullptr;
   s.ntok = 0;
   s.tcap = 0;
+  s.unit = 0;
   s.end_byte = 0;
   s.limit = 0;
   s.cap = 0;
@@ -759,6 +811,7 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
       s.limit = s.end_byte * 8u;
       s.tok = (gu32 *)(tokens + ch.tok);
       s.tcap = ch.tcap;
+      s.unit = c;
       s.cap = ch.cap;
       s.whave = ch.ord == 0 ? 0u : HIST;
       s.bit = ch.start_bit;
@@ -790,7 +843,7 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
         s.dbits = db;
         s.cl = (gcu16 *)ctab;
         s.cd = (gcu16 *)(ctab + DIST_TABLE_OFF);
-        s.capx = min(s.cap, s.tcap);
+        s.capx = s.cap;
         lane_prime(s, s.bit);
       }
     }
@@ -814,7 +867,7 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
     while (need) {
       const uint32_t ln = (uint32_t)__builtin_ctzll(need);
       need &= need - 1;
-      coop_block(s, ln, L, lane_tab, fixed);
+      coop_block(s, ln, L, lane_tab, fixed, tokens, pool);
     }
 #if KP_ON
     const uint64_t kc1 = KP_NOW();
@@ -837,9 +890,17 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
     kp_wsteps += kp_wave_max(s.kp_steps - kp_st0);
 #endif
     const uint32_t g0 = s.ntok - s.gk;
+    if (s.ntok <= s.tcap) {
 #pragma unroll
-    for (uint32_t j = 0; j < GROUP; j++)
-      if (j < s.gk) s.tok[g0 + j] = L.g.tokbuf[j][lane];
+      for (uint32_t j = 0; j < GROUP; j++)
+        if (j < s.gk) s.tok[g0 + j] = L.g.tokbuf[j][lane];
+    } else if (tok_ensure(pool, s.unit, s.tcap, s.ntok)) {  // past the primary region: pool pages
+      const uint64_t prim_off = (uint64_t)((const uint32_t *)s.tok - tokens);
+      for (uint32_t j = 0; j < s.gk; j++) *tok_addr(pool, tokens, s.unit, prim_off, s.tcap, g0 + j) = L.g.tokbuf[j][lane];
+    } else {
+      s.code = ZD_FULL;
+      s.mode = LM_DONE;
+    }
     __builtin_amdgcn_wave_barrier();  // tokbuf area is reused by the next header build
 #if KP_ON
     kp_flush += KP_NOW() - kc2;
@@ -927,7 +988,7 @@ __global__ void __launch_bounds__(EXP_T) zs_expand_kernel(const ZsJobDev *__rest
                                                            const ZsChunkDev *__restrict__ chunks,
                                                            uint16_t *__restrict__ scratch,
                                                            const uint32_t *__restrict__ tokens,
-                                                           const uint32_t *__restrict__ order) {
+                                                           const uint32_t *__restrict__ order, ZsTokPool pool) {
   __shared__ __attribute__((aligned(16))) uint16_t ring[HIST];
   __shared__ __attribute__((aligned(16))) uint32_t s_mark[EXP_N];
   __shared__ uint32_t s_tval[EXP_T];
@@ -935,11 +996,17 @@ __global__ void __launch_bounds__(EXP_T) zs_expand_kernel(const ZsJobDev *__rest
   __shared__ __attribute__((aligned(16))) uint32_t s_j[2][EXP_N];
   __shared__ uint32_t s_jf[2][EXP_W];
   const uint32_t tid = threadIdx.x, lane = tid & (WAVE - 1), wv = tid / WAVE;
-  const ZsChunkDev ch = chunks[order[blockIdx.x]];  // units by decreasing output (longest first)
-  const int code = ch.code & 0xff;
-  if (!(code == ZD_STOP || code == ZD_END)) return;
+  const uint32_t unit = order[blockIdx.x];
+  const ZsChunkDev ch = chunks[unit];  // chain members by decreasing output (longest first)
+  if (!ch.in_chain) return;
   gcu32 *tk = (gcu32 *)(tokens + ch.tok);
-  const uint32_t ntok = ch.n_tok;
+  const uint32_t ntok = ch.n_tok, tcap = ch.tcap;
+  const uint32_t *ptab = pool.ptab + (size_t)unit * ZS_TP_MAXPG;
+  auto tread = [&](uint32_t x) -> uint32_t {
+    if (x < tcap) return tk[x];
+    const uint32_t r = x - tcap;
+    return tokens[pool.base + ((uint64_t)(ptab[r >> ZS_TP_LOG] - 1u) << ZS_TP_LOG) + (r & ((1u << ZS_TP_LOG) - 1u))];
+  };
   uint16_t *out = scratch + ch.scratch;
   (void)jobs;
 #if KP_ON
@@ -956,10 +1023,10 @@ __global__ void __launch_bounds__(EXP_T) zs_expand_kernel(const ZsJobDev *__rest
   const uint64_t kp_init = KP_NOW() - kp_t0;
 #endif
   uint32_t pos = 0, flushed = 0, stamp = 0;
-  uint32_t tnext = tid < ntok ? tk[tid] : 0u;
+  uint32_t tnext = tid < ntok ? tread(tid) : 0u;
   for (uint32_t tb = 0; tb < ntok; tb += EXP_T) {
     const uint32_t t = tnext;
-    if (tb + EXP_T + tid < ntok) tnext = tk[tb + EXP_T + tid];  // next batch, in flight during this one
+    if (tb + EXP_T + tid < ntok) tnext = tread(tb + EXP_T + tid);  // next batch, in flight during this one
     const bool valid = tb + tid < ntok;
     const uint32_t hi = t >> 16;
     const uint32_t len = valid ? (hi ? hi : 1u) : 0u;
@@ -1180,8 +1247,7 @@ __global__ void zs_unit_keys_kernel(const ZsJobDev *__restrict__ jobs, const ZsC
   uint32_t k = 0;
   if (ch.start_bit != ZS_NONE) {
     if (after_parse) {
-      const int code = ch.code & 0xff;
-      k = (code == ZD_STOP || code == ZD_END) ? ch.n_out : 0u;
+      k = ch.in_chain ? ch.n_out : 0u;
     } else {
       const uint64_t end = ch.stop_bit != ZS_NONE ? ch.stop_bit : (uint64_t)jobs[ch.job].in_len * 8u + 32u;
       k = (uint32_t)min<uint64_t>(end > ch.start_bit ? end - ch.start_bit : 1u, 0xffffffffu);
@@ -1227,20 +1293,25 @@ int sort_units(const ZsJobDev *d_jobs, const ZsChunkDev *d_chunks, uint32_t n, i
 }
 }  // namespace
 
-extern "C" void zs_launch_lane(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, ZsChunkDev *d_chunks, uint32_t nchunks,
-                               uint16_t *d_scratch, uint32_t *d_tokens, uint32_t *d_tables, const uint32_t *d_fixed,
-                               hipStream_t st, hipEvent_t *ev) {
-  // ev (profiling, optional): [0] after parse, [1] after expand
+extern "C" void zs_launch_parse(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, ZsChunkDev *d_chunks, uint32_t nchunks,
+                                uint32_t *d_tokens, uint32_t *d_tables, const uint32_t *d_fixed, ZsTokPool pool,
+                                hipStream_t st) {
   if (!nchunks) return;
   hipLaunchKernelGGL(zs_unit_header_kernel, dim3(nchunks), dim3(WAVE), 0, st, d_jobs, d_heads, d_chunks, d_tables);
   uint32_t *order = nullptr;
   if (sort_units(d_jobs, d_chunks, nchunks, 0, &order, st)) return;
   hipLaunchKernelGGL(zs_lane_kernel, dim3((nchunks + WAVE - 1) / WAVE), dim3(WAVE), 0, st, d_jobs, d_heads, d_chunks,
-                     nchunks, d_tokens, d_tables, d_fixed, order);
-  if (ev) (void)hipEventRecord(ev[0], st);
+                     nchunks, d_tokens, d_tables, d_fixed, order, pool);
+}
+
+// expand the verified chain members (after zs_chain_kernel), longest first
+extern "C" void zs_launch_expand(const ZsJobDev *d_jobs, ZsChunkDev *d_chunks, uint32_t nchunks, uint16_t *d_scratch,
+                                 const uint32_t *d_tokens, ZsTokPool pool, hipStream_t st) {
+  if (!nchunks) return;
+  uint32_t *order = nullptr;
   if (sort_units(d_jobs, d_chunks, nchunks, 1, &order, st)) return;
-  hipLaunchKernelGGL(zs_expand_kernel, dim3(nchunks), dim3(EXP_T), 0, st, d_jobs, d_chunks, d_scratch, d_tokens, order);
-  if (ev) (void)hipEventRecord(ev[1], st);
+  hipLaunchKernelGGL(zs_expand_kernel, dim3(nchunks), dim3(EXP_T), 0, st, d_jobs, d_chunks, d_scratch, d_tokens, order,
+                     pool);
 }
 
 extern "C" int zs_kprof_read_ck(uint64_t *out16, int reset);

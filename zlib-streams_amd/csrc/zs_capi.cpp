@@ -37,15 +37,15 @@ extern "C" void zs_launch_deflate(ZsDJobDev *d_jobs, uint32_t njobs, ZsDSegDev *
                                   uint16_t *d_lx16, int has_std, int has_d64, hipStream_t st, hipEvent_t *ev);
 extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, ZsSegDev *d_segs, uint32_t nseg,
                                   ZsCJobDev *d_cjobs, uint32_t ncjobs, ZsChunkDev *d_units, uint32_t nunit_slots,
-                                  uint16_t *d_scratch, uint32_t *d_tokens, uint32_t *d_tables, const uint32_t *d_fixed,
-                                  uint8_t *d_windows, void *d_linkinfo, ZsDecDev *d_decs, uint32_t *d_fallback,
-                                  hipStream_t st, hipEvent_t *ev);
+                                  uint16_t *d_scratch, uint32_t *d_tokens, ZsTokPool pool, uint32_t *d_tables,
+                                  const uint32_t *d_fixed, uint8_t *d_windows, void *d_linkinfo, ZsDecDev *d_decs,
+                                  uint32_t *d_fallback, hipStream_t st, hipEvent_t *ev);
 
 namespace {
 
 constexpr size_t TABLE_ENTRIES_HOST = 1448 + 724 + 176;  // must match TABLE_STRIDE (zs_device.h)
 constexpr size_t FIXED_WORDS_HOST = 544 + 272;      // must match FIXED_WORDS (zs_device.h)
-constexpr double UNIT_SLACK_HOST = 8192.0;          // must match UNIT_SLACK (chunk_kernels.hip)
+constexpr uint64_t MAX_RATIO = 1032;  // deflate's largest expansion: 258 bytes per 2 bits
 
 const char *const kMsgs[ZM_COUNT] = {
     nullptr,
@@ -109,9 +109,12 @@ struct Workspace {
   uint32_t *d_tables = nullptr;  // TABLE_STRIDE words per unit slot
   uint8_t *d_windows = nullptr;  // 32 KiB per unit slot
   uint64_t *d_linkinfo = nullptr;  // zs_link_kernel chain order: 16 B per unit slot
-  size_t cap_scratch = 0;        // u16 entries (and u32 parse tokens, same count)
+  size_t cap_scratch = 0;        // u16 entries (chain members at their output offsets)
   uint16_t *d_scratch = nullptr;
+  size_t cap_tokens = 0;         // u32 parse tokens: primary regions + pool pages
   uint32_t *d_tokens = nullptr;
+  uint32_t *d_ptab = nullptr;    // pool page table: ZS_TP_MAXPG per unit slot (cap_units)
+  uint32_t *d_pool_next = nullptr;
   uint32_t *d_fixed = nullptr;
   // timing (zs_profile): events on the launch stream
   bool prof = false;
@@ -122,11 +125,12 @@ struct Workspace {
   double prof_stage[ZS_PROF_STAGES] = {};
   double prof_ms = 0.0, prof_batch_ms = 0.0;
   uint64_t prof_launches = 0;
-  // last batch: chunked jobs, chunks, chunked jobs that fell back, serial jobs
+  // last batch: chunked jobs, decode units planned, chunked jobs that fell back
+  // to the serial decoder, serial jobs
   uint32_t stats[4] = {0, 0, 0, 0};
 };
 
-// chunked-path tuning (env: ZS_CHUNK_KB, ZS_CAP_MUL, ZS_NO_CHUNK)
+// chunked-path tuning (env: ZS_CHUNK_KB, ZS_NO_CHUNK, ZS_POOL_PER_KB)
 uint32_t chunk_bytes() {
   static uint32_t v = [] {
     const char *e = std::getenv("ZS_CHUNK_KB");
@@ -134,15 +138,6 @@ uint32_t chunk_bytes() {
     if (kb < 4) kb = 4;
     if (kb > 65536) kb = 65536;
     return (uint32_t)(kb * 1024);
-  }();
-  return v;
-}
-// first-pass unit capacity multiplier (env: ZS_CAP_MUL, 1..8)
-uint32_t first_cap_mul() {
-  static uint32_t v = [] {
-    const char *e = std::getenv("ZS_CAP_MUL");
-    long m = e ? std::atol(e) : 2;
-    return (uint32_t)(m < 1 ? 1 : m > 8 ? 8 : m);
   }();
   return v;
 }
@@ -189,6 +184,7 @@ int grow_host(T **p, size_t n) {
 int ws_reserve_jobs(size_t n) {
   if (n <= g_ws.cap_jobs) return 0;
   size_t c = std::max<size_t>(n, 2 * g_ws.cap_jobs);
+  g_ws.cap_jobs = 0;
   int r;
   if ((r = grow_dev(&g_ws.d_jobs, c)) || (r = grow_dev(&g_ws.d_heads, c)) || (r = grow_dev(&g_ws.d_decs, c)) ||
       (r = grow_dev(&g_ws.d_checks, 2 * c)) || (r = grow_dev(&g_ws.d_res, c)) || (r = grow_dev(&g_ws.d_ids, 3 * c)) ||
@@ -199,26 +195,38 @@ int ws_reserve_jobs(size_t n) {
   return 0;
 }
 
-int ws_reserve_chunks(size_t nseg, size_t nunits, size_t scratch_entries) {
+// A failed allocation leaves the buffer null AND its capacity 0, so the next
+// call allocates again instead of trusting a stale capacity.
+int ws_reserve_chunks(size_t nseg, size_t nunits, size_t scratch_entries, size_t tokens) {
   int r;
   if (nseg > g_ws.cap_segs) {
     size_t c = std::max(nseg, g_ws.cap_segs + g_ws.cap_segs / 2);
+    g_ws.cap_segs = 0;
     if ((r = grow_dev(&g_ws.d_segs, c)) || (r = grow_host(&g_ws.h_segs, c))) return r;
     g_ws.cap_segs = c;
   }
   if (nunits > g_ws.cap_units) {
     size_t c = std::max(nunits, g_ws.cap_units + g_ws.cap_units / 2);
+    g_ws.cap_units = 0;
     if ((r = grow_dev(&g_ws.d_chunks, c)) || (r = grow_host(&g_ws.h_chunks, c)) ||
         (r = grow_dev(&g_ws.d_tables, c * TABLE_ENTRIES_HOST)) || (r = grow_dev(&g_ws.d_windows, c * 32768)) ||
-        (r = grow_dev(&g_ws.d_linkinfo, c * 2)))
+        (r = grow_dev(&g_ws.d_linkinfo, c * 2)) || (r = grow_dev(&g_ws.d_ptab, c * ZS_TP_MAXPG)))
       return r;
     g_ws.cap_units = c;
   }
   if (scratch_entries > g_ws.cap_scratch) {
     size_t c = std::max(scratch_entries, g_ws.cap_scratch + g_ws.cap_scratch / 4);
-    if ((r = grow_dev(&g_ws.d_scratch, c)) || (r = grow_dev(&g_ws.d_tokens, c))) return r;
+    g_ws.cap_scratch = 0;
+    if ((r = grow_dev(&g_ws.d_scratch, c))) return r;
     g_ws.cap_scratch = c;
   }
+  if (tokens > g_ws.cap_tokens) {
+    size_t c = std::max(tokens, g_ws.cap_tokens + g_ws.cap_tokens / 4);
+    g_ws.cap_tokens = 0;
+    if ((r = grow_dev(&g_ws.d_tokens, c))) return r;
+    g_ws.cap_tokens = c;
+  }
+  if (!g_ws.d_pool_next && (r = grow_dev(&g_ws.d_pool_next, 4))) return r;
   if (!g_ws.d_fixed) {
     if ((r = grow_dev(&g_ws.d_fixed, FIXED_WORDS_HOST))) return r;
     zs_launch_fixed_tables(g_ws.d_fixed, g_ws.stream);
@@ -227,9 +235,21 @@ int ws_reserve_chunks(size_t nseg, size_t nunits, size_t scratch_entries) {
   return 0;
 }
 
+// pool tokens per KiB of chunked input (env ZS_POOL_PER_KB, default 1024: one
+// token per compressed byte on top of the primary regions)
+size_t pool_per_kb() {
+  static size_t v = [] {
+    const char *e = std::getenv("ZS_POOL_PER_KB");
+    long x = e ? std::atol(e) : 1024;
+    return (size_t)(x < 0 ? 0 : x);
+  }();
+  return v;
+}
+
 int ws_reserve_bytes(uint8_t **p, size_t *cap, size_t need) {
   if (need <= *cap) return 0;
   size_t c = std::max(need, *cap + *cap / 2);
+  *cap = 0;
   int r = grow_dev(p, c);
   if (r) return r;
   *cap = c;
@@ -323,69 +343,61 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
       if (jobs[i].in_len) HIP_OK(hipMemcpyAsync(g_ws.d_in + in_off[i], jobs[i].in, jobs[i].in_len, hipMemcpyHostToDevice, st));
     }
   }
-  // Route each job: large raw/zlib/gzip streams -> speculative chunked path
-  // (with the serial decoder as exact fallback); small ones and deflate64 ->
-  // the wave-per-stream serial decoder.  Lists in h_ids: [serial std | d64 | chunked].
+  // Route each job: raw/zlib/gzip streams with enough blocks -> speculative
+  // chunked path (with the serial decoder as exact fallback); small ones and
+  // deflate64 -> the wave-per-stream serial decoder.  Routing looks at the
+  // compressed size (>= 4 search segments), or at >= 1 segment when the caller
+  // allows >= 4 MiB of output (long-match streams); never at a ratio, since no
+  // capacity on the chunked path depends on one.  Lists in h_ids:
+  // [serial std | d64 | chunked].
   const uint32_t C = chunk_bytes();
   uint32_t n_std = 0, n_d64 = 0, n_cj = 0;
   size_t nseg = 0, nunit_slots = 0;
   std::vector<uint32_t> cj_list;
+  std::vector<uint8_t> is_cj(nv, 0);
   for (uint32_t k = 0; k < nv; k++) {
     const ZsJobDev &jd = g_ws.h_jobs[k];
-    const double ratio = jd.in_len ? (double)jd.out_cap / (double)jd.in_len : 0.0;
-    const bool chunk = chunking_enabled() && !jd.d64 && !(jd.flags & ZS_JF_COPY) && jd.in_len >= 4ull * C && ratio <= 64.0;
-    if (chunk) {
+    const bool big = jd.in_len >= 4ull * C || (jd.in_len >= C && jd.out_cap >= (4ull << 20));
+    if (chunking_enabled() && !jd.d64 && !(jd.flags & ZS_JF_COPY) && big && jd.in_len < (1ull << 29)) {
       cj_list.push_back(k);
-      nseg += (jd.in_len + C - 1) / C;
+      is_cj[k] = 1;
     }
   }
   std::vector<uint32_t> copies;  // ZIP stored entries: output = input
   for (uint32_t k = 0; k < nv; k++)
     if (g_ws.h_jobs[k].flags & ZS_JF_COPY) copies.push_back(k);
-  for (uint32_t k = 0; k < nv; k++)
-    if (!g_ws.h_jobs[k].d64 && !(g_ws.h_jobs[k].flags & ZS_JF_COPY) &&
-        std::find(cj_list.begin(), cj_list.end(), k) == cj_list.end())
-      g_ws.h_ids[n_std++] = k;
-  for (uint32_t k = 0; k < nv; k++)
-    if (g_ws.h_jobs[k].d64) g_ws.h_ids[n_std + n_d64++] = k;
-  for (uint32_t k : cj_list) g_ws.h_ids[n_std + n_d64 + n_cj++] = k;
-  // Plan the chunked jobs of `list` (segments, unit slots, scratch ranges) and
-  // upload them.  cap_mul scales each unit's output capacity (cap_mul x span x
-  // ratio + slack, zs_plan_kernel).
-  size_t nunit_slots_max = 0;
-  auto plan_chunked = [&](const std::vector<uint32_t> &list, uint32_t cap_mul,
-                          const std::vector<std::vector<uint32_t>> *boosts, size_t *nseg_out,
-                          size_t *nslots_out) -> int {
-    size_t ns_total = 0;
-    for (uint32_t k : list) ns_total += (g_ws.h_jobs[k].in_len + C - 1) / C;
-    int rr;
-    if ((rr = ws_reserve_chunks(ns_total, 0, 0))) return rr;
-    size_t si = 0, slots = 0, need = 0;
-    for (uint32_t q = 0; q < list.size(); q++) {
-      const uint32_t k = list[q];
+  // Plan the chunked jobs (segments, unit slots, token regions, entry ranges,
+  // token pool) and upload them.  Any allocation failure here only sends the
+  // jobs to the serial decoder.
+  ZsTokPool pool{};
+  if (!cj_list.empty()) {
+    size_t slots = 0, toks = 0, ents = 0, in_sum = 0;
+    nseg = 0;
+    for (uint32_t k : cj_list) nseg += (g_ws.h_jobs[k].in_len + C - 1) / C;
+    int rr = ws_reserve_chunks(nseg, 0, 0, 0);
+    size_t si = 0;
+    for (uint32_t q = 0; q < cj_list.size() && !rr; q++) {
+      const uint32_t k = cj_list[q];
       const ZsJobDev &jd = g_ws.h_jobs[k];
       const uint32_t ns = (uint32_t)((jd.in_len + C - 1) / C);
-      const double ratio = std::max(1.0, (double)jd.out_cap / (double)jd.in_len);
       const uint32_t max_units = ns * SEG_SLOTS + 1;
-      // zs_plan_kernel gives each unit cap_mul x span x ratio + slack entries;
-      // spans of a job's units sum to at most its input (+1 byte of rounding each)
-      const uint32_t n_boost = boosts ? (uint32_t)std::min<size_t>((*boosts)[q].size(), 4) : 0;
-      const uint32_t boost_cap = (uint32_t)std::min<uint64_t>(jd.out_cap, 0xffe00000ull);
-      const size_t reserve = (size_t)(cap_mul * ratio * ((double)jd.in_len + max_units)) +
-                             (size_t)max_units * ((size_t)UNIT_SLACK_HOST + 8) + 64 +
-                             (size_t)n_boost * ((size_t)boost_cap + (size_t)UNIT_SLACK_HOST + 8);
       ZsCJobDev cj{};
       cj.job = k;
       cj.first_seg = (uint32_t)si;
       cj.nseg = ns;
       cj.unit0 = (uint32_t)slots;
       cj.max_units = max_units;
-      cj.scratch0 = need;
-      cj.scratch_n = reserve;
-      cj.cap_mul = cap_mul;
-      cj.n_boost = n_boost;
-      for (uint32_t b = 0; b < n_boost; b++) cj.boost[b] = (*boosts)[q][b];
-      cj.boost_cap = boost_cap;
+      // primary token regions (zs_plan_kernel): per unit span x ZS_TOK_PER_BYTE
+      // + slack, spans summing to at most the input plus a byte per unit
+      cj.tok0 = toks;
+      toks += ((jd.in_len + max_units) * ZS_TOK_PER_BYTE + (size_t)max_units * (ZS_TOK_SLACK + 8) + 63) & ~size_t(63);
+      // entries: the verified chain's total never exceeds out_cap (else the
+      // serial decoder answers); every member starts 8-entry aligned
+      // (zs_chain_kernel), hence 8 entries of padding per possible unit
+      cj.scratch0 = ents;
+      cj.scratch_n = std::min<uint64_t>(jd.out_cap, MAX_RATIO * jd.in_len + 64) + 8ull * max_units;
+      ents += (cj.scratch_n + 16 + 15) & ~size_t(15);
+      in_sum += jd.in_len;
       g_ws.h_cjobs[q] = cj;
       for (uint32_t o = 0; o < ns; o++, si++) {
         ZsSegDev sg{};
@@ -397,61 +409,39 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
         g_ws.h_segs[si] = sg;
       }
       slots += max_units;
-      need += (reserve + 7) & ~size_t(7);
     }
-    if ((rr = ws_reserve_chunks(ns_total, slots, need))) return rr;
-    HIP_OK(hipMemcpyAsync(g_ws.d_segs, g_ws.h_segs, ns_total * sizeof(ZsSegDev), hipMemcpyHostToDevice, st));
-    HIP_OK(hipMemcpyAsync(g_ws.d_cjobs, g_ws.h_cjobs, list.size() * sizeof(ZsCJobDev), hipMemcpyHostToDevice, st));
-    *nseg_out = ns_total;
-    *nslots_out = slots;
-    nunit_slots_max = std::max(nunit_slots_max, slots);
-    return 0;
-  };
-  if (n_cj && (r = plan_chunked(cj_list, first_cap_mul(), nullptr, &nseg, &nunit_slots))) return r;
+    const size_t pool_pages = std::max<size_t>(16, (in_sum / 1024 * pool_per_kb() + ((size_t)1 << ZS_TP_LOG) - 1) >> ZS_TP_LOG);
+    if (!rr) rr = ws_reserve_chunks(nseg, slots, ents + 16, toks + (pool_pages << ZS_TP_LOG));
+    if (rr) {  // no room for the chunked path: every job decodes serially
+      cj_list.clear();
+      std::fill(is_cj.begin(), is_cj.end(), 0);
+      nseg = 0;
+    } else {
+      n_cj = (uint32_t)cj_list.size();
+      nunit_slots = slots;
+      pool.base = toks;
+      pool.npages = (uint32_t)pool_pages;
+      pool.next = g_ws.d_pool_next;
+      pool.ptab = g_ws.d_ptab;
+      HIP_OK(hipMemcpyAsync(g_ws.d_segs, g_ws.h_segs, nseg * sizeof(ZsSegDev), hipMemcpyHostToDevice, st));
+      HIP_OK(hipMemcpyAsync(g_ws.d_cjobs, g_ws.h_cjobs, n_cj * sizeof(ZsCJobDev), hipMemcpyHostToDevice, st));
+      HIP_OK(hipMemsetAsync(g_ws.d_pool_next, 0, sizeof(uint32_t), st));
+    }
+  }
+  for (uint32_t k = 0; k < nv; k++)
+    if (!g_ws.h_jobs[k].d64 && !(g_ws.h_jobs[k].flags & ZS_JF_COPY) && !is_cj[k]) g_ws.h_ids[n_std++] = k;
+  for (uint32_t k = 0; k < nv; k++)
+    if (g_ws.h_jobs[k].d64) g_ws.h_ids[n_std + n_d64++] = k;
+  for (uint32_t q = 0; q < n_cj; q++) g_ws.h_ids[n_std + n_d64 + q] = cj_list[q];
   HIP_OK(hipMemcpyAsync(g_ws.d_jobs, g_ws.h_jobs, nv * sizeof(ZsJobDev), hipMemcpyHostToDevice, st));
   HIP_OK(hipMemcpyAsync(g_ws.d_ids, g_ws.h_ids, nv * sizeof(uint32_t), hipMemcpyHostToDevice, st));
   hipEvent_t *ev = g_ws.prof ? g_ws.ev : nullptr;
   if (ev) HIP_OK(hipEventRecord(ev[0], st));
   zs_launch_header(g_ws.d_jobs, g_ws.d_heads, nv, st);
-  uint32_t n_retry = 0;
   if (n_cj) {
     zs_launch_chunked(g_ws.d_jobs, g_ws.d_heads, g_ws.d_segs, (uint32_t)nseg, g_ws.d_cjobs, n_cj, g_ws.d_chunks,
-                      (uint32_t)nunit_slots,
-                      g_ws.d_scratch, g_ws.d_tokens, g_ws.d_tables, g_ws.d_fixed, g_ws.d_windows, g_ws.d_linkinfo,
-                      g_ws.d_decs,
-                      g_ws.d_fallback, st, ev ? ev + 1 : nullptr);
-    // Jobs whose chain broke (most often a unit whose output outgrew cap_mul x
-    // its span x the job's ratio: blocks far more compressible than the
-    // stream, or a false start just after a real one cutting the span short)
-    // get one more chunked pass before the serial decoder: 8x capacity, and
-    // the job's whole output capacity for up to 4 units that ran out (the
-    // finder is deterministic, so unit i is the same unit in both passes).
-    // Finished jobs are final already (emitted, decs set).
-    std::vector<uint32_t> fb(nv), retry;
-    std::vector<std::vector<uint32_t>> boosts;
-    HIP_OK(hipMemcpyAsync(fb.data(), g_ws.d_fallback, nv * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
-    for (uint32_t q = 0; q < n_cj; q++) {
-      if (!fb[cj_list[q]]) continue;
-      const ZsCJobDev &cj = g_ws.h_cjobs[q];
-      std::vector<ZsChunkDev> us(cj.max_units);
-      HIP_OK(hipMemcpyAsync(us.data(), g_ws.d_chunks + cj.unit0, cj.max_units * sizeof(ZsChunkDev),
-                            hipMemcpyDeviceToHost, st));
-      HIP_OK(hipStreamSynchronize(st));
-      std::vector<uint32_t> full;
-      for (uint32_t i = 0; i < cj.max_units; i++)
-        if (us[i].start_bit != ZS_NONE && (us[i].code & 0xff) == ZD_FULL) full.push_back(i);
-      retry.push_back(cj_list[q]);
-      boosts.push_back(full.size() <= 4 ? full : std::vector<uint32_t>());
-    }
-    if (!retry.empty()) {
-      size_t rseg = 0, rslots = 0;
-      if ((r = plan_chunked(retry, 8, &boosts, &rseg, &rslots))) return r;
-      zs_launch_chunked(g_ws.d_jobs, g_ws.d_heads, g_ws.d_segs, (uint32_t)rseg, g_ws.d_cjobs, (uint32_t)retry.size(),
-                        g_ws.d_chunks, (uint32_t)rslots, g_ws.d_scratch, g_ws.d_tokens, g_ws.d_tables, g_ws.d_fixed,
-                        g_ws.d_windows, g_ws.d_linkinfo, g_ws.d_decs, g_ws.d_fallback, st, nullptr);
-      n_retry = (uint32_t)retry.size();
-    }
+                      (uint32_t)nunit_slots, g_ws.d_scratch, g_ws.d_tokens, pool, g_ws.d_tables, g_ws.d_fixed,
+                      g_ws.d_windows, g_ws.d_linkinfo, g_ws.d_decs, g_ws.d_fallback, st, ev ? ev + 1 : nullptr);
   } else if (ev)
     for (int i = 1; i <= 6; i++) HIP_OK(hipEventRecord(ev[i], st));
   zs_launch_decode(0, g_ws.d_jobs, g_ws.d_heads, g_ws.d_ids, n_std, g_ws.d_decs, nullptr, st);
@@ -497,23 +487,25 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
   if (n_cj) {
     std::vector<uint32_t> fb(nv);
     HIP_OK(hipMemcpy(fb.data(), g_ws.d_fallback, nv * sizeof(uint32_t), hipMemcpyDeviceToHost));
-    HIP_OK(hipMemcpy(g_ws.h_cjobs, g_ws.d_cjobs, (n_retry ? n_retry : n_cj) * sizeof(ZsCJobDev), hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(g_ws.h_cjobs, g_ws.d_cjobs, n_cj * sizeof(ZsCJobDev), hipMemcpyDeviceToHost));
     for (uint32_t k : cj_list) g_ws.stats[2] += fb[k];
-    for (uint32_t q = 0; q < (n_retry ? n_retry : n_cj); q++) g_ws.stats[1] += g_ws.h_cjobs[q].nunits;
+    for (uint32_t q = 0; q < n_cj; q++) g_ws.stats[1] += g_ws.h_cjobs[q].nunits;
     if (std::getenv("ZS_DEBUG_CHUNKS")) {
+      uint32_t used = 0;
+      HIP_OK(hipMemcpy(&used, g_ws.d_pool_next, sizeof used, hipMemcpyDeviceToHost));
       HIP_OK(hipMemcpy(g_ws.h_chunks, g_ws.d_chunks, nunit_slots * sizeof(ZsChunkDev), hipMemcpyDeviceToHost));
       size_t inch = 0, stopped = 0;
       for (size_t i = 0; i < nunit_slots; i++) {
         inch += g_ws.h_chunks[i].in_chain;
         stopped += (g_ws.h_chunks[i].code & 0xff) == ZD_STOP;
       }
-      std::fprintf(stderr, "[zs] chunked jobs %u segments %zu units %u in_chain %zu stopped %zu fallback %u\n", n_cj, nseg,
-                   g_ws.stats[1], inch, stopped, g_ws.stats[2]);
+      std::fprintf(stderr, "[zs] chunked jobs %u segments %zu units %u in_chain %zu stopped %zu fallback %u pool pages %u/%u\n",
+                   n_cj, nseg, g_ws.stats[1], inch, stopped, g_ws.stats[2], used, pool.npages);
       const size_t show = std::getenv("ZS_DEBUG_CHUNKS")[0] == '2' ? nunit_slots : 8;
       for (size_t i = 0; i < nunit_slots && i < show; i++) {
         const ZsChunkDev &c = g_ws.h_chunks[i];
-        std::fprintf(stderr, "  unit %zu ord %u start %u stop %u end %u code %d n_out %u ntok %u cap %u chain %u\n", i, c.ord,
-                     c.start_bit, c.stop_bit, c.end_bit, c.code, c.n_out, c.n_tok, c.cap, c.in_chain);
+        std::fprintf(stderr, "  unit %zu ord %u start %u stop %u end %u code %d n_out %u ntok %u tcap %u chain %u\n", i,
+                     c.ord, c.start_bit, c.stop_bit, c.end_bit, c.code, c.n_out, c.n_tok, c.tcap, c.in_chain);
       }
     }
   }

@@ -129,14 +129,14 @@ struct ZsChunkDev {    // one decode unit
   uint32_t end_bit;    // where decoding stopped
   int32_t code;        // ZD_* | (ZsMsg << 8)
   uint32_t n_out;      // u16 entries produced
-  uint32_t cap;        // scratch capacity (entries)
-  uint64_t scratch;    // entry offset of this unit's u16 scratch region
+  uint32_t cap;        // output entry limit (the job's out_cap, clamped)
+  uint64_t scratch;    // entry offset of this unit's u16 entries (zs_chain_kernel: job base + out_off)
   uint32_t chain_next; // next unit in the verified chain (ZS_NONE at the end)
   uint32_t in_chain;   // 1 = member of the verified chain of a non-fallback job
   uint64_t out_off;    // output byte offset (verified chain members)
   uint32_t n_tok;      // tokens produced by the parse pass
-  uint32_t tcap;       // token capacity
-  uint64_t tok;        // offset of this unit's token region (u32 units)
+  uint32_t tcap;       // tokens in the primary region; later tokens go to pool pages
+  uint64_t tok;        // offset of this unit's primary token region (u32 units)
   uint32_t hdr_bit;    // bit after the first block's header (when prebuilt)
   uint32_t hdr_info;   // bit 0: first header prebuilt by zs_unit_header_kernel;
                        // bit 1: its BFINAL; bits 8-11 / 12-15: lit/len and distance root bits
@@ -145,6 +145,22 @@ struct ZsChunkDev {    // one decode unit
 // Parse-pass tokens (u32), consumed by the expand pass:
 //   hi16 == 0          literal, byte in bits 0-7 (stored-block bytes included)
 //   hi16 in [3, 258]   match: length = hi16, distance = lo16 + 1
+// A unit's token i lives in its primary region (i < tcap) or in page
+// (i - tcap) >> ZS_TP_LOG of its page table, pages being taken on demand
+// from a pool shared by the batch (ZsTokPool).  No token count is ever
+// guessed from a compression ratio: a unit runs out of room only when the
+// pool does.
+#define ZS_TP_LOG 16                 // tokens per pool page: 64 Ki
+#define ZS_TP_MAXPG 16               // pool pages per unit
+#define ZS_TOK_PER_BYTE 1            // primary region: tokens per byte of the unit's compressed span
+#define ZS_TOK_SLACK 4096            // ... plus this many
+struct ZsTokPool {
+  uint64_t base;       // token offset of page 1 (page ids are 1-based; 0 = none)
+  uint32_t npages;     // pages in the pool
+  uint32_t pad;
+  uint32_t *next;      // device counter: pages taken
+  uint32_t *ptab;      // ZS_TP_MAXPG page ids per unit slot (zeroed by zs_plan_kernel)
+};
 
 struct ZsCJobDev {     // a job on the chunked path
   uint32_t job;        // job index
@@ -153,15 +169,12 @@ struct ZsCJobDev {     // a job on the chunked path
   uint32_t unit0;      // first unit slot reserved for this job (host)
   uint32_t max_units;  // unit slots reserved (nseg * SEG_SLOTS + 1)
   uint32_t nunits;     // units planned (zs_plan_kernel)
-  uint64_t scratch0;   // first scratch entry reserved for this job (host)
-  uint64_t scratch_n;  // scratch entries reserved
-  uint32_t cap_mul;    // unit output capacity = cap_mul x span x ratio + slack
-  uint32_t n_boost;    // units (job-local index) given boost_cap entries at least:
-  uint32_t boost[4];   //   units that ran out of capacity in the previous pass
-  uint32_t boost_cap;
-  uint32_t pad;
+  uint64_t tok0;       // first token of the job's primary regions (host)
+  uint64_t scratch0;   // first u16 entry of the job's entry range (host)
+  uint64_t scratch_n;  // entries reserved: min(out_cap, bound) -- the chain's total never exceeds it
+  uint32_t nchain;     // units in the verified chain (zs_chain_kernel)
+  uint32_t ok;         // chain verified (zs_chain_kernel); cleared again by zs_link_kernel on a bad window
 };
-
 // ---------------------------------------------------------------------------
 // GPU deflate (deflate_kernels.hip): one job = one whole stream compressed as
 // with deflateInit2(level, Z_DEFLATED, window_bits) + deflate(Z_FINISH).

@@ -29,6 +29,31 @@ def lpt_partition(costs, world):
     return [sorted(s) for s in shards]
 
 
+def corpus_costs(stream_ids, kind_of):
+    """Per-stream LPT costs for the bench corpora, known before any stream is
+    generated: a Zipf-text stream compresses to ~2x the bytes of a line-text
+    stream of the same size (ratio ~3-4 vs ~6-8 at zlib L6) and decodes in
+    ~2x the time, so it costs 2 and a line-text stream 1."""
+    return [2 if kind_of(i) == "zipf" else 1 for i in stream_ids]
+
+
+def c2_kind(i):
+    """configs[1] stream i: Zipf text for i % 64 < 32, line text otherwise (tests/corpus.py)."""
+    return "zipf" if i % 64 < 32 else "lines"
+
+
+def c5_kind(k):
+    """configs[4] stream k: Zipf text for k % 4 < 2, line text otherwise (tests/corpus.py:c5_stream)."""
+    return "zipf" if k % 4 < 2 else "lines"
+
+
+def bench_shard(nstreams, rank, world, kind_of):
+    """Stream ids of `rank` when `nstreams` bench streams are split across `world`
+    ranks (strong scaling: the node decodes the same batch whatever the world)."""
+    ids = list(range(nstreams))
+    return [ids[i] for i in lpt_partition(corpus_costs(ids, kind_of), world)[rank]]
+
+
 def my_shard(costs, rank, world):
     """Job indices of `rank` under lpt_partition(costs, world)."""
     return lpt_partition(costs, world)[rank]

@@ -338,7 +338,8 @@ def profile_read():
 
 
 PROFILE_STAGES = ("header", "find", "parse", "expand", "link", "emit", "serial_decode", "finalize")
-STAGE_KERNELS = {"header": "zs_header_kernel", "find": "zs_find_kernel", "parse": "zs_lane_kernel",
+STAGE_KERNELS = {"header": "zs_header_kernel", "find": "zs_find_kernel + zs_find_fixed_kernel + zs_plan_kernel",
+                 "parse": "zs_unit_header_kernel + zs_lane_kernel + zs_chain_kernel",
                  "expand": "zs_expand_kernel", "link": "zs_link_kernel", "emit": "zs_emit_kernel",
                  "serial_decode": "zs_decode_kernel", "finalize": "zs_check_kernel + zs_finalize_kernel"}
 
@@ -363,10 +364,12 @@ def kprof_read(reset=True):
 
 
 def last_stats():
-    """Last batch: chunked jobs, chunks, chunked jobs that fell back, serial jobs."""
+    """Last batch: jobs on the chunked path, decode units planned for them, chunked
+    jobs whose chain did not verify (decoded by the serial decoder instead), and
+    jobs routed to the serial decoder directly."""
     a = (ctypes.c_uint32 * 4)()
     _check(lib().zs_last_stats(a))
-    return {"chunked_jobs": a[0], "chunks": a[1], "fallback_jobs": a[2], "serial_jobs": a[3]}
+    return {"chunked_jobs": a[0], "units": a[1], "fallback_jobs": a[2], "serial_jobs": a[3]}
 
 
 def set_stream(hip_stream_handle):
