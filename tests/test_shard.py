@@ -85,3 +85,38 @@ def test_gloo_world2_shards_and_counters():
         assert t == 1.5  # max over ranks
         assert b == sum(costs)
         assert ok
+
+
+def test_bench_self_launch_dry_run():
+    """bench.py --gpus 2 with no launcher starts its own 2 ranks (gloo in the
+    dry run), each rank takes its LPT share of the 64-stream batch (strong
+    scaling), and rank 0 prints one line with the reduced counters."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--dry-run", "--gpus", "2", "--stream-mib", "1",
+                        "--steps", "1", "--warmup", "0"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["dry_run"] and d["n_gpus"] == 2 and d["verified_bit_exact"] and d["scaling"] == "strong"
+    assert d["config"]["streams_total"] == 64
+    assert d["rank_streams"] == shard.bench_shard(64, 0, 2, shard.c2_kind)
+    both = sorted(shard.bench_shard(64, 0, 2, shard.c2_kind) + shard.bench_shard(64, 1, 2, shard.c2_kind))
+    assert both == list(range(64))
+    # balanced: each rank gets half of the Zipf and half of the line-text streams
+    for rk in (0, 1):
+        ids = shard.bench_shard(64, rk, 2, shard.c2_kind)
+        assert sum(shard.c2_kind(i) == "zipf" for i in ids) == 16
+
+
+def test_bench_shards_cover_c5():
+    for world in (1, 2, 4, 8):
+        parts = [shard.bench_shard(4096, r, world, shard.c5_kind) for r in range(world)]
+        assert sorted(i for p in parts for i in p) == list(range(4096))
+        loads = [sum(2 if shard.c5_kind(i) == "zipf" else 1 for i in p) for p in parts]
+        assert max(loads) - min(loads) <= 2

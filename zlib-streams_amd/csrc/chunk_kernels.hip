@@ -310,76 +310,103 @@ __global__ void __launch_bounds__(64) zs_find_kernel(const ZsJobDev *__restrict_
 // code.  The chain check of zs_chain_kernel keeps results exact whatever is
 // recorded; (c) only keeps false starts rare.
 // ---------------------------------------------------------------------------
-#define FIXED_CHECK 384
+#define FIXED_CHECK 256
 #define FIXED_MIN 64
+#define FIXED_LOOKBACK 2048  // bits decoded before a candidate
 
-__device__ bool fixed_plausible(const uint32_t *w, uint32_t end_byte, uint32_t bit) {
+// One fixed-code symbol (literal/length + length extra + distance + extra)
+// from `hold`; returns its bit length, 0 for an invalid code; *eob on 256.
+__device__ __forceinline__ uint32_t fixed_symbol(uint64_t hold, bool *eob) {
+  const uint32_t r9 = __builtin_bitreverse32((uint32_t)hold) >> 23;  // next 9 bits, first bit highest
+  const uint32_t c7 = r9 >> 2, c8 = r9 >> 1;
+  uint32_t sym, used;
+  if (c7 < 24u) {
+    sym = 256 + c7;
+    used = 7;
+  } else if (c8 < 0xc0u) {
+    sym = c8 - 0x30u;
+    used = 8;
+  } else if (c8 < 0xc8u) {
+    sym = 280 + (c8 - 0xc0u);
+    used = 8;
+  } else {
+    sym = 144 + (r9 - 0x190u);
+    used = 9;
+  }
+  *eob = sym == 256;
+  if (sym > 285) return 0;
+  if (sym > 256) {
+    const uint32_t ls = sym - 257;
+    used += (ls >= 8 && ls < 28) ? (ls >> 2) - 1 : 0u;
+    const uint32_t d = __builtin_bitreverse32((uint32_t)(hold >> used)) >> 27;
+    if (d >= 30) return 0;
+    used += 5 + (d < 4 ? 0u : (d >> 1) - 1);
+  }
+  return used;  // <= 9 + 5 + 5 + 13 = 32
+}
+
+// Fixed-code decode from bit `from`: true when it reaches bit `to` exactly
+// on a symbol boundary with an end-of-block code ending there (mode 0), or
+// decodes FIXED_CHECK symbols from `from` (mode 1: `to` unused; an end of
+// block after FIXED_MIN symbols also passes).
+__device__ bool fixed_walk(const uint32_t *w, uint32_t end_byte, uint32_t from, uint32_t to, int mode) {
   const uint32_t limit = end_byte * 8u;
-  uint32_t wi = bit >> 5;
-  uint64_t hold = (uint64_t)in_word(w, wi, end_byte) >> (bit & 31);
-  uint32_t n = 32 - (bit & 31);
+  uint32_t wi = from >> 5;
+  uint64_t hold = (uint64_t)in_word(w, wi, end_byte) >> (from & 31);
+  uint32_t n = 32 - (from & 31);
   wi++;
-  uint32_t pos = bit + 3;
-  hold >>= 3;
-  n -= 3;
-  for (uint32_t k = 0; k < FIXED_CHECK; k++) {
-    if (n <= 32) {
+  uint32_t pos = from;
+  for (uint32_t k = 0; k < 4096; k++) {
+    while (n <= 32) {
       hold |= (uint64_t)in_word(w, wi, end_byte) << n;
       n += 32;
       wi++;
     }
-    // literal/length: 7-bit codes 256..279, 8-bit 0..143 and 280..287, 9-bit 144..255
-    const uint32_t r9 = __builtin_bitreverse32((uint32_t)hold) >> 23;  // next 9 bits, first bit highest
-    const uint32_t c7 = r9 >> 2, c8 = r9 >> 1;
-    uint32_t sym, used;
-    if (c7 < 24u) {
-      sym = 256 + c7;
-      used = 7;
-    } else if (c8 < 0xc0u) {
-      sym = c8 - 0x30u;
-      used = 8;
-    } else if (c8 < 0xc8u) {
-      sym = 280 + (c8 - 0xc0u);
-      used = 8;
+    bool eob;
+    uint32_t used = fixed_symbol(hold, &eob);
+    if (!used) return false;
+    if (mode == 0) {
+      if (eob && pos + 7 == to) return true;
+      if (pos + used > to) return false;  // ran over `to`: no symbol boundary there
+      if (eob) {  // an earlier block end: skip its successor's header (fixed blocks only)
+        used += 3;
+        if (((hold >> 7) & 6u) != 2u) return false;
+      }
     } else {
-      sym = 144 + (r9 - 0x190u);
-      used = 9;
+      if (eob) return k >= FIXED_MIN;
+      if (k + 1 >= FIXED_CHECK) return true;
     }
     hold >>= used;
     n -= used;
     pos += used;
-    if (sym == 256) return k >= FIXED_MIN;
-    if (sym > 285) return false;
-    if (sym > 256) {
-      const uint32_t ls = sym - 257;
-      const uint32_t xb = (ls >= 8 && ls < 28) ? (ls >> 2) - 1 : 0u;
-      hold >>= xb;
-      n -= xb;
-      pos += xb;
-      if (n <= 32) {
-        hold |= (uint64_t)in_word(w, wi, end_byte) << n;
-        n += 32;
-        wi++;
-      }
-      const uint32_t d = __builtin_bitreverse32((uint32_t)hold) >> 27;
-      if (d >= 30) return false;
-      const uint32_t dx = d < 4 ? 0u : (d >> 1) - 1;
-      hold >>= 5 + dx;
-      n -= 5 + dx;
-      pos += 5 + dx;
-    }
     if (pos > limit) return false;
   }
-  return true;
+  return false;
+}
+
+// Candidate fixed block start at bit p (header at p, data from `data_bit`):
+// a fixed-code decode from FIXED_LOOKBACK bits earlier must land exactly on an
+// end of block ending at p -- fixed codes resynchronise within a few symbols,
+// so a real boundary is met on a symbol boundary while a false candidate (7
+// zero bits inside other codes) is run over -- and the block must decode.
+__device__ bool fixed_plausible(const uint32_t *w, uint32_t end_byte, uint32_t data_bit, uint32_t p) {
+  const uint32_t from = p >= data_bit + 3u + FIXED_LOOKBACK ? p - FIXED_LOOKBACK : data_bit + 3u;
+  if (from + 7u > p) return false;
+  return fixed_walk(w, end_byte, from, p, 0) && fixed_walk(w, end_byte, p + 3u, 0, 1);
 }
 
 __global__ void __launch_bounds__(64) zs_find_fixed_kernel(const ZsJobDev *__restrict__ jobs, const ZsHeadDev *__restrict__ heads,
-                                                            ZsSegDev *__restrict__ segs) {
+                                                            ZsSegDev *__restrict__ segs, uint32_t nseg) {
   __shared__ uint32_t s_q[WAVE * 32];
   const uint32_t lane = threadIdx.x;
   const uint32_t sg = blockIdx.x;
   const ZsSegDev seg = segs[sg];
   if (seg.ncand != 0) return;
+  // a segment between segments with dynamic starts lies inside a long dynamic
+  // block: no fixed-block search there (the neighbours are this job's when
+  // their ordinals are adjacent)
+  if (seg.ord > 0 && segs[sg - 1].ncand != 0) return;
+  if (sg + 1 < nseg && segs[sg + 1].job == seg.job && segs[sg + 1].ncand != 0) return;
   const ZsJobDev jb = jobs[seg.job];
   const ZsHeadDev hd = heads[seg.job];
   if (hd.code != ZD_END) return;
@@ -418,7 +445,7 @@ __global__ void __launch_bounds__(64) zs_find_fixed_kernel(const ZsJobDev *__res
       bool ok = false;
       if (lane < take) {
         cb = s_q[q0 + lane];
-        ok = fixed_plausible(w, end_byte, cb);
+        ok = fixed_plausible(w, end_byte, (mis + (uint32_t)hd.start_byte) * 8u, cb);
       }
       uint64_t m = __ballot(ok);
       while (m && nfound < SEG_SLOTS) {
@@ -431,7 +458,7 @@ __global__ void __launch_bounds__(64) zs_find_fixed_kernel(const ZsJobDev *__res
     }
     __builtin_amdgcn_wave_barrier();
   }
-  if (lane == 0) segs[sg].ncand = nfound;
+  if (lane == 0) segs[sg].nfixed = nfound;
 }
 
 // ---------------------------------------------------------------------------
@@ -484,7 +511,8 @@ __global__ void __launch_bounds__(PLAN_T) zs_plan_kernel(const ZsJobDev *__restr
     if (t == 0) s_cap_base = 0;
     for (uint32_t s0 = 0; s0 < cj.nseg; s0 += PLAN_T) {
       const uint32_t sg = s0 + t;
-      const uint32_t c = sg < cj.nseg ? segs[cj.first_seg + sg].ncand : 0u;
+      const ZsSegDev *sgp = segs + cj.first_seg + sg;
+      const uint32_t c = sg < cj.nseg ? (sgp->ncand ? sgp->ncand : sgp->nfixed) : 0u;
       uint32_t tot;
       const uint32_t ex = plan_block_scan(c, s_tmp, &tot);
       for (uint32_t k = 0; k < c; k++) {
@@ -954,7 +982,7 @@ extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_hea
   // parse + chain, [3] after expand, [4] after link, [5] after emit
   if (ev) (void)hipEventRecord(ev[0], st);
   hipLaunchKernelGGL(zs_find_kernel, dim3(nseg), dim3(64), 0, st, d_jobs, d_heads, d_segs);
-  hipLaunchKernelGGL(zs_find_fixed_kernel, dim3(nseg), dim3(64), 0, st, d_jobs, d_heads, d_segs);
+  hipLaunchKernelGGL(zs_find_fixed_kernel, dim3(nseg), dim3(64), 0, st, d_jobs, d_heads, d_segs, nseg);
   hipLaunchKernelGGL(zs_plan_kernel, dim3(ncjobs), dim3(PLAN_T), 0, st, d_jobs, d_heads, d_segs, d_cjobs, d_units, pool);
   if (ev) (void)hipEventRecord(ev[1], st);
   ZsLinkInfo *info = reinterpret_cast<ZsLinkInfo *>(d_linkinfo);

@@ -118,20 +118,28 @@ __device__ __forceinline__ uint32_t in_word_g(gcu32 *w, uint32_t wi, uint32_t en
 }
 
 // Token storage (zs_common.h): token x of a unit lives in its primary
-// region (x < tcap) or in pool page ptab[(x - tcap) >> ZS_TP_LOG].  Only the
-// unit's writer calls tok_ensure (one lane at a time); pages are taken from
-// the pool with one atomic each.  Returns false when the pool (or the unit's
-// page table) is exhausted.
+// region (x < tcap) or in pool page k of its page table, page k holding
+// 2^k pool units of 2^ZS_TP_LOG tokens (geometric: 16 pages cover 4 Gi
+// tokens).  Only the unit's writer calls tok_ensure (one lane at a time);
+// each page is taken from the pool with one atomic.  Returns false when the
+// pool is exhausted.
+__device__ __forceinline__ uint32_t tok_page(uint32_t r, uint32_t *off) {  // r = x - tcap
+  const uint32_t q = (r >> ZS_TP_LOG) + 1u;
+  const uint32_t k = 31u - (uint32_t)__builtin_clz(q);
+  *off = r - (((1u << k) - 1u) << ZS_TP_LOG);
+  return k;
+}
 __device__ __forceinline__ bool tok_ensure(const ZsTokPool &pool, uint32_t unit, uint32_t tcap, uint32_t x_end) {
   if (x_end <= tcap) return true;
-  const uint32_t kl = (x_end - 1u - tcap) >> ZS_TP_LOG;
+  uint32_t off;
+  const uint32_t kl = tok_page(x_end - 1u - tcap, &off);
   if (kl >= ZS_TP_MAXPG) return false;
   uint32_t *pt = pool.ptab + (size_t)unit * ZS_TP_MAXPG;
   for (uint32_t k = 0; k <= kl; k++) {
     uint32_t pg = __hip_atomic_load(pt + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (!pg) {
-      pg = atomicAdd(pool.next, 1u) + 1u;
-      if (pg > pool.npages) return false;
+      pg = atomicAdd(pool.next, 1u << k) + 1u;
+      if (pg - 1u + (1u << k) > pool.npages) return false;
       __hip_atomic_store(pt + k, pg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
@@ -141,10 +149,11 @@ __device__ __forceinline__ bool tok_ensure(const ZsTokPool &pool, uint32_t unit,
 __device__ __forceinline__ uint32_t *tok_addr(const ZsTokPool &pool, uint32_t *tokens, uint32_t unit, uint64_t prim,
                                               uint32_t tcap, uint32_t x) {
   if (x < tcap) return tokens + prim + x;
-  const uint32_t r = x - tcap;
+  uint32_t off;
+  const uint32_t k = tok_page(x - tcap, &off);
   const uint32_t pg =
-      __hip_atomic_load(pool.ptab + (size_t)unit * ZS_TP_MAXPG + (r >> ZS_TP_LOG), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return tokens + pool.base + ((uint64_t)(pg - 1u) << ZS_TP_LOG) + (r & ((1u << ZS_TP_LOG) - 1u));
+      __hip_atomic_load(pool.ptab + (size_t)unit * ZS_TP_MAXPG + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return tokens + pool.base + ((uint64_t)(pg - 1u) << ZS_TP_LOG) + off;
 }
 
 enum { LM_SYM = 0, LM_BLOCK = 1, LM_DONE = 2 };
@@ -174,6 +183,7 @@ struct LaneState {
   uint32_t zlmask, zdmask;
   uint32_t lbits, dbits;    // root widths of the current block's zlib tables
   uint32_t stop, bit, whave;
+  uint32_t sidx, send;      // unit slot whose start is `stop`; end of the job's unit slots
   int mode, code, last;
 };
 
@@ -615,7 +625,7 @@ __device__ void install_roots(LaneLDS &L, uint32_t ln, const uint32_t *zl, uint3
 // the same ln): end/stop checks, stored blocks, fixed and dynamic headers
 // (src/inflate.c:834-1033); installs the lane's tables.
 __device__ void coop_block(LaneState &s, uint32_t ln, LaneLDS &L, uint32_t *lane_tab, const uint32_t *fixed,
-                           uint32_t *tokens, const ZsTokPool &pool) {
+                           uint32_t *tokens, const ZsTokPool &pool, const ZsChunkDev *units) {
   const uint32_t lane = lane_id();
   const uint32_t *w = reinterpret_cast<const uint32_t *>(readlane_ptr((const void *)(uintptr_t)s.w, ln));
   uint32_t *tok = reinterpret_cast<uint32_t *>(readlane_ptr((const void *)(uintptr_t)s.tok, ln));
@@ -626,7 +636,7 @@ __device__ void coop_block(LaneState &s, uint32_t ln, LaneLDS &L, uint32_t *lane
   const uint32_t tcap = __builtin_amdgcn_readlane(s.tcap, ln);
   const uint32_t end_byte = __builtin_amdgcn_readlane(s.end_byte, ln);
   const uint32_t limit = end_byte * 8u;
-  const uint32_t stop = __builtin_amdgcn_readlane(s.stop, ln);
+  uint32_t stop = __builtin_amdgcn_readlane(s.stop, ln);
   const uint32_t cap = __builtin_amdgcn_readlane(s.cap, ln);
   uint32_t bit = __builtin_amdgcn_readlane(s.bit, ln);
   uint32_t pos = __builtin_amdgcn_readlane(s.pos, ln);
@@ -640,8 +650,23 @@ __device__ void coop_block(LaneState &s, uint32_t ln, LaneLDS &L, uint32_t *lane
       break;
     }
     if (bit >= stop) {
-      code = ZD_STOP;
-      break;
+      // A unit stops only at a block boundary that is a recorded start (its
+      // successor's).  A block end past `stop` means `stop` was not a
+      // boundary of this decode (a false start, or one this decode ran
+      // over): move the stop to the next recorded start at or past `bit`
+      // and keep decoding, so false starts never break the chain.
+      uint32_t si = __builtin_amdgcn_readlane(s.sidx, ln);
+      const uint32_t se = __builtin_amdgcn_readlane(s.send, ln);
+      while (si < se && units[si].start_bit < bit) si++;
+      stop = si < se ? units[si].start_bit : ZS_NONE;
+      if (lane == ln) {
+        s.sidx = si;
+        s.stop = stop;
+      }
+      if (bit == stop) {
+        code = ZD_STOP;
+        break;
+      }
     }
     if (bit + 3 > limit) {
       code = ZD_TRUNC;
@@ -776,6 +801,7 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
   s.last = 0;
   s.bit = 0;
   s.stop = ZS_NONE;
+  s.sidx = s.send = 0;
   s.w = nullptr;
   s.tok = nullptr;
   s.ntok = 0;
@@ -816,6 +842,8 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
       s.whave = ch.ord == 0 ? 0u : HIST;
       s.bit = ch.start_bit;
       s.stop = ch.stop_bit;
+      s.sidx = c + 1;
+      s.send = ch.first + ch.nunits;
       s.mode = LM_BLOCK;
       s.code = 0;
       if (ch.hdr_info & 1u) {  // first header prebuilt by zs_unit_header_kernel: straight to symbols
@@ -867,7 +895,7 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
     while (need) {
       const uint32_t ln = (uint32_t)__builtin_ctzll(need);
       need &= need - 1;
-      coop_block(s, ln, L, lane_tab, fixed, tokens, pool);
+      coop_block(s, ln, L, lane_tab, fixed, tokens, pool, chunks);
     }
 #if KP_ON
     const uint64_t kc1 = KP_NOW();
@@ -1004,8 +1032,9 @@ __global__ void __launch_bounds__(EXP_T) zs_expand_kernel(const ZsJobDev *__rest
   const uint32_t *ptab = pool.ptab + (size_t)unit * ZS_TP_MAXPG;
   auto tread = [&](uint32_t x) -> uint32_t {
     if (x < tcap) return tk[x];
-    const uint32_t r = x - tcap;
-    return tokens[pool.base + ((uint64_t)(ptab[r >> ZS_TP_LOG] - 1u) << ZS_TP_LOG) + (r & ((1u << ZS_TP_LOG) - 1u))];
+    uint32_t off;
+    const uint32_t k = tok_page(x - tcap, &off);
+    return tokens[pool.base + ((uint64_t)(ptab[k] - 1u) << ZS_TP_LOG) + off];
   };
   uint16_t *out = scratch + ch.scratch;
   (void)jobs;

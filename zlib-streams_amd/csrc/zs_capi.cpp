@@ -235,12 +235,13 @@ int ws_reserve_chunks(size_t nseg, size_t nunits, size_t scratch_entries, size_t
   return 0;
 }
 
-// pool tokens per KiB of chunked input (env ZS_POOL_PER_KB, default 1024: one
-// token per compressed byte on top of the primary regions)
+// pool tokens per KiB of chunked input (env ZS_POOL_PER_KB, default 2048: two
+// tokens per compressed byte on top of the primary regions -- a stored-block
+// stretch needs one per byte, and geometric pages may overshoot 2x)
 size_t pool_per_kb() {
   static size_t v = [] {
     const char *e = std::getenv("ZS_POOL_PER_KB");
-    long x = e ? std::atol(e) : 1024;
+    long x = e ? std::atol(e) : 2048;
     return (size_t)(x < 0 ? 0 : x);
   }();
   return v;
@@ -410,7 +411,7 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
       }
       slots += max_units;
     }
-    const size_t pool_pages = std::max<size_t>(16, (in_sum / 1024 * pool_per_kb() + ((size_t)1 << ZS_TP_LOG) - 1) >> ZS_TP_LOG);
+    const size_t pool_pages = std::max<size_t>(64, (in_sum / 1024 * pool_per_kb() + ((size_t)1 << ZS_TP_LOG) - 1) >> ZS_TP_LOG);
     if (!rr) rr = ws_reserve_chunks(nseg, slots, ents + 16, toks + (pool_pages << ZS_TP_LOG));
     if (rr) {  // no room for the chunked path: every job decodes serially
       cj_list.clear();

@@ -116,7 +116,8 @@ struct ZsSegDev {
   uint32_t ncand;      // block starts found (<= SEG_SLOTS), ascending
   uint32_t cand[SEG_SLOTS];  // bit offsets from the 4-byte-aligned input base
   uint32_t final_ok;   // 1: BFINAL = 1 starts count too (the stream's last segments)
-  uint32_t pad[2];
+  uint32_t nfixed;     // fixed-block starts in cand[] (zs_find_fixed_kernel, only when ncand == 0)
+  uint32_t pad;
 };
 
 struct ZsChunkDev {    // one decode unit
@@ -145,18 +146,19 @@ struct ZsChunkDev {    // one decode unit
 // Parse-pass tokens (u32), consumed by the expand pass:
 //   hi16 == 0          literal, byte in bits 0-7 (stored-block bytes included)
 //   hi16 in [3, 258]   match: length = hi16, distance = lo16 + 1
-// A unit's token i lives in its primary region (i < tcap) or in page
-// (i - tcap) >> ZS_TP_LOG of its page table, pages being taken on demand
-// from a pool shared by the batch (ZsTokPool).  No token count is ever
-// guessed from a compression ratio: a unit runs out of room only when the
-// pool does.
-#define ZS_TP_LOG 16                 // tokens per pool page: 64 Ki
-#define ZS_TP_MAXPG 16               // pool pages per unit
+// A unit's token i lives in its primary region (i < tcap) or in page k of
+// its page table, page k holding 2^k pool units of 2^ZS_TP_LOG tokens
+// (geometric, so ZS_TP_MAXPG pages cover any unit), pages being taken on
+// demand from a pool shared by the batch (ZsTokPool).  No token count is
+// ever guessed from a compression ratio: a unit runs out of room only when
+// the pool does.
+#define ZS_TP_LOG 16                 // tokens per pool unit: 64 Ki
+#define ZS_TP_MAXPG 16               // pages per unit (page k = 2^k pool units)
 #define ZS_TOK_PER_BYTE 1            // primary region: tokens per byte of the unit's compressed span
 #define ZS_TOK_SLACK 4096            // ... plus this many
 struct ZsTokPool {
-  uint64_t base;       // token offset of page 1 (page ids are 1-based; 0 = none)
-  uint32_t npages;     // pages in the pool
+  uint64_t base;       // token offset of pool unit 1 (page ids = first pool unit, 1-based; 0 = none)
+  uint32_t npages;     // pool units (2^ZS_TP_LOG tokens each)
   uint32_t pad;
   uint32_t *next;      // device counter: pages taken
   uint32_t *ptab;      // ZS_TP_MAXPG page ids per unit slot (zeroed by zs_plan_kernel)
