@@ -131,14 +131,20 @@ typedef struct zs_djob {
 /* Each job = deflateInit2(level, Z_DEFLATED, window_bits, 8, Z_DEFAULT_STRATEGY)
    + one deflate(Z_FINISH) over the whole input: ret Z_STREAM_END (Z_OK when
    out_cap was too small: total_out = out_cap bytes of the stream), total_in,
-   total_out, adler (CRC-32 for gzip, Adler-32 for zlib, 1 for raw).  The
-   stream is valid deflate that any inflater decodes to the input; its bytes
-   are not zlib's. */
+   total_out, adler (CRC-32 for gzip, Adler-32 for zlib, 1 for raw).
+   Levels 4..9 write zlib's bytes: the same stream zlib 1.2.11's deflate_slow +
+   trees.c produce (the reference's deflate, src/wasm/deflate_stream_wasm.c:
+   31-49 and src/trees.c), byte for byte.  Levels 0..3, window_bits -16
+   (deflate64) and ZS_F_DEFLATE_FAST write valid deflate that any inflater
+   decodes to the input, with the GPU's own block structure (not zlib's bytes). */
+#define ZS_F_DEFLATE_FAST 4u /* levels 4..9: the throughput path instead of zlib's bytes */
 int zs_deflate_batch(const zs_djob *jobs, uint32_t n, zs_result *results, uint32_t flags);
 uint64_t zs_deflate_bound(uint64_t in_len, int32_t window_bits);
 /* accumulated deflate timing (zs_profile(1) enables): [0] whole pipeline ms,
    [1] match, [2] parse, [3] blocks + checks, [4] offsets + stitch + trailer,
-   [5] batches.  Returns the number of entries written. */
+   [5] batches.  zlib-identical jobs (levels 4..9): [1] chains + match search,
+   [2] parse + fix-up rounds, [3] trees + bits, [4] trailer.  Returns the
+   number of entries written. */
 int zs_profile_deflate(double *ms, uint32_t n);
 /* launch on this HIP stream (hipStream_t); NULL = the library's own stream */
 int zs_set_stream(void *hip_stream);
@@ -155,8 +161,9 @@ int zs_profile_stages(double *ms, uint32_t n);
    `make prof`); the product library returns 0 (no counters).  reset != 0
    zeroes them after the read.  Returns the number of counters written. */
 int zs_kprof_read(uint64_t *out, uint32_t n, int reset);
-/* last batch: [jobs on the chunked path, chunks, chunked jobs that fell back
-   to the serial decoder, jobs on the serial path] */
+/* last batch: [jobs on the chunked path, decode units planned for them,
+   chunked jobs whose chain did not verify (decoded by the serial decoder
+   instead), jobs routed to the serial decoder] */
 int zs_last_stats(uint32_t out[4]);
 const char *zs_version(void);
 const char *zs_last_error(void);

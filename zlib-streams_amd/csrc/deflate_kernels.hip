@@ -161,7 +161,7 @@ __global__ void __launch_bounds__(DZ_MT) zs_dz_match_kernel(const ZsDJobDev *__r
   const uint32_t half = blockIdx.x % PARTS;
   const ZsDJobDev jb = jobs[sg.job];
   if ((jb.wbits == 16u) != D64) return;  // the other variant's job
-  if (jb.level == 0 || half * SPAN >= sg.len) return;  // stored blocks / no positions
+  if (jb.level == 0 || jb.exact || half * SPAN >= sg.len) return;  // stored blocks / zlib-identical jobs / no positions
   gcu8 *in = (gcu8 *)jb.in;
   const uint64_t n = jb.in_len;
   const uint64_t s = sg.start + half * SPAN;
@@ -307,7 +307,7 @@ __global__ void __launch_bounds__(DZ_T) zs_dz_parse_kernel(const ZsDJobDev *__re
   const uint32_t t = threadIdx.x;
   const ZsDSegDev sg = segs[blockIdx.x];
   const ZsDJobDev jb = jobs[sg.job];
-  if (jb.level == 0) return;
+  if (jb.level == 0 || jb.exact) return;
   const uint32_t len = sg.len;
   {
     const uint4 *src = reinterpret_cast<const uint4 *>(len8 + sg.tok);
@@ -394,7 +394,7 @@ __global__ void __launch_bounds__(WAVE) zs_dz_merge_kernel(const ZsDJobDev *__re
   const uint32_t lane = threadIdx.x;
   const ZsDSegDev sg = segs[blockIdx.x];
   const ZsDJobDev jb = jobs[sg.job];
-  if (jb.wbits != 16u || jb.level == 0) return;
+  if (jb.wbits != 16u || jb.level == 0 || jb.exact) return;
   uint32_t *S = bm + (uint64_t)blockIdx.x * (DZ_SEG / 32u);
   const uint16_t *d16 = dist16 + sg.tok;
   uint16_t *x16 = lx16 + sg.tok;
@@ -584,7 +584,7 @@ __global__ void __launch_bounds__(DZ_T) zs_dz_hist_kernel(const ZsDJobDev *__res
   const uint32_t t = threadIdx.x;
   const ZsDSegDev sg = segs[blockIdx.x];
   const ZsDJobDev jb = jobs[sg.job];
-  if (jb.level == 0) return;
+  if (jb.level == 0 || jb.exact) return;
   gcu8 *l8 = (gcu8 *)(len8 + sg.tok);
   const uint16_t *d16 = dist16 + sg.tok;
   gcu8 *in = (gcu8 *)(jb.in + sg.start);
@@ -785,7 +785,7 @@ __global__ void __launch_bounds__(WAVE) zs_dz_codes_kernel(const ZsDJobDev *__re
   if (s >= nseg) return;
   const ZsDSegDev sg = segs[s];
   const ZsDJobDev jb = jobs[sg.job];
-  if (jb.level == 0) return;
+  if (jb.level == 0 || jb.exact) return;
   const uint32_t lane = threadIdx.x;
   gu32 *A = (gu32 *)aux;
   const DzRows H{A + s, nseg};                                              // histograms
@@ -891,6 +891,7 @@ __global__ void __launch_bounds__(DZ_T) zs_dz_emit_kernel(const ZsDJobDev *__res
   const uint32_t t = threadIdx.x;
   const ZsDSegDev sg = segs[blockIdx.x];
   const ZsDJobDev jb = jobs[sg.job];
+  if (jb.exact) return;  // zlib-identical jobs: deflate_zlib.hip
   uint32_t *gout = obuf + sg.obuf / 4;
   const uint32_t last = sg.last;
   if (jb.level == 0) {  // stored blocks of <= 65535 bytes, byte-aligned (every block is stored)
@@ -1007,6 +1008,7 @@ __global__ void __launch_bounds__(DZ_JT) zs_dz_offsets_kernel(ZsDJobDev *__restr
   __shared__ uint64_t s_sum[DZ_JT];
   const uint32_t t = threadIdx.x;
   ZsDJobDev jb = jobs[blockIdx.x];
+  if (jb.exact) return;  // zs_zd_layout_kernel
   const uint32_t hdr = jb.wrap == 2 ? 10u : (jb.wrap == 1 ? 2u : 0u);
   // segment k of the job: jb.seg0 + k; per-thread contiguous ranges
   const uint32_t ns = jb.nseg;
@@ -1062,7 +1064,7 @@ __global__ void __launch_bounds__(DZ_T) zs_dz_stitch_kernel(const ZsDJobDev *__r
   const ZsDSegDev sg = segs[blockIdx.x];
   const ZsDJobDev jb = jobs[sg.job];
   const uint32_t nbits = sg.nbits;
-  if (nbits == 0) return;
+  if (nbits == 0 || jb.exact) return;
   uint32_t *dst = reinterpret_cast<uint32_t *>(stage + jb.stage);  // 4 KiB aligned
   const uint32_t *src = obuf + sg.obuf / 4;
   const uint64_t off = sg.bitoff;
@@ -1085,10 +1087,12 @@ __global__ void __launch_bounds__(DZ_T) zs_dz_stitch_kernel(const ZsDJobDev *__r
 }
 
 // trailer (after all stitching): CRC-32 + ISIZE (gzip) or Adler-32 big-endian (zlib)
-__global__ void zs_dz_trailer_kernel(const ZsDJobDev *__restrict__ jobs, uint32_t njobs, uint8_t *__restrict__ stage) {
+__global__ void zs_dz_trailer_kernel(const ZsDJobDev *__restrict__ jobs, uint32_t njobs, uint8_t *__restrict__ stage,
+                                     uint32_t exact) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= njobs) return;
   const ZsDJobDev jb = jobs[j];
+  if (jb.exact != exact) return;
   uint8_t *o = stage + jb.stage;
   const uint64_t tr = jb.wrap == 2 ? 8u : (jb.wrap == 1 ? 4u : 0u);
   uint8_t *p = o + jb.total_out - tr;
@@ -1137,8 +1141,13 @@ extern "C" void zs_launch_deflate(ZsDJobDev *d_jobs, uint32_t njobs, ZsDSegDev *
   if (ev) (void)hipEventRecord(ev[3], st);
   hipLaunchKernelGGL(zs_dz_offsets_kernel, dim3(njobs), dim3(DZ_JT), 0, st, d_jobs, d_segs, d_stage);
   hipLaunchKernelGGL(zs_dz_stitch_kernel, dim3(nseg), dim3(DZ_T), 0, st, d_jobs, d_segs, d_obuf, d_stage);
-  hipLaunchKernelGGL(zs_dz_trailer_kernel, dim3((njobs + 63) / 64), dim3(64), 0, st, d_jobs, njobs, d_stage);
+  hipLaunchKernelGGL(zs_dz_trailer_kernel, dim3((njobs + 63) / 64), dim3(64), 0, st, d_jobs, njobs, d_stage, 0u);
   if (ev) (void)hipEventRecord(ev[4], st);
+}
+
+// trailers of the zlib-identical jobs, after their layout
+extern "C" void zs_launch_dz_trailer(ZsDJobDev *d_jobs, uint32_t njobs, uint8_t *d_stage, hipStream_t st) {
+  hipLaunchKernelGGL(zs_dz_trailer_kernel, dim3((njobs + 63) / 64), dim3(64), 0, st, d_jobs, njobs, d_stage, 1u);
 }
 
 // block-kernel counters of the profiling build (merged into zs_kprof_read's 26..37)

@@ -1,0 +1,1205 @@
+// deflate_zlib.hip -- GPU deflate that writes zlib's bytes (levels 4..9).
+//
+// Reference path: the deflate core of the zlib submodule (deflate.c
+// deflate_slow + longest_match, absent from /root/reference; pinned by host
+// zlib 1.2.11) called as deflateInit2(level, Z_DEFLATED,
+// -15|31, 8, Z_DEFAULT_STRATEGY) (src/wasm/deflate_stream_wasm.c:31-49), and
+// src/trees.c (_tr_tally 1029-1053, _tr_flush_block 931-1023, build_tree 561,
+// gen_bitlen 474, gen_codes 205, scan_tree / send_tree, build_bl_tree 734,
+// send_all_trees 767, compress_block 834-882, _tr_stored_block 794).
+//
+// deflate_slow inserts every position into its hash chains, so the chain of
+// position p is a function of the input alone: every earlier position q >= 1
+// whose 15-bit hash of in[q..q+2] equals p's.  That makes the search
+// data-parallel; the stages (their semantics pinned on the CPU by
+// tests/tools/dz_model.c against host zlib) are:
+//   zs_zd_prev_kernel   one wave per 128 Ki positions: previous same-hash
+//                       distance of every position (u16 head table in LDS,
+//                       64 positions per step, same-hash lanes found with 15
+//                       ballots; entries aged out every 16 Ki positions);
+//   zs_zd_match_kernel  one 1024-thread workgroup per 8 Ki positions (the
+//                       32 KiB window's bytes and chain links in LDS): the
+//                       longest match of every position under the level's
+//                       chain budget -- max_chain, and max_chain >> 2 (used when
+//                       prev_length >= good_length) -- as longest_match finds
+//                       it (first candidate reaching the best length, the
+//                       first reaching nice_length ending the walk); lanes
+//                       take a new position as soon as their walk ends;
+//   zs_zd_parse_kernel  one workgroup per 64 KiB region: deflate_slow's loop
+//                       replayed over those tables, 256-position pieces
+//                       walked speculatively and re-walked from their
+//                       predecessor's exit until the walks merge (a shared
+//                       position in the "just emitted a match" state);
+//                       zs_zd_fix_kernel does the same across regions;
+//   zs_zd_count / blocks / tree / layout / emit kernels: blocks of 16383
+//                       symbols, each flushed as _tr_flush_block does (stored /
+//                       static / dynamic by the same bit counts, trees built
+//                       with the same heap order and overflow repair), bit
+//                       offsets per job, then the bits.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "zs_check.h"
+#include "zs_common.h"
+#include "zs_device.h"
+
+#define ZD_MINM 3u
+#define ZD_MAXM 258u
+#define ZD_LOOK (ZD_MAXM + ZD_MINM + 1u)  // MIN_LOOKAHEAD
+#define ZD_TOO_FAR 4096u
+#define ZD_BLOCK 16383u                   // symbols per block: lit_bufsize - 1 (memLevel 8)
+#define ZD_S1 131072u                     // zs_zd_prev_kernel positions per wave
+#define ZD_SWEEP 16384u                   // head-table ageing period
+#define ZD_S2 8192u                       // zs_zd_match_kernel positions per workgroup
+#define ZD_MT 1024u
+#define ZD_REG 65536u                     // parse region (one ZsDSegDev segment)
+#define ZD_PT 256u                        // parse threads per region = pieces of 256 positions
+#define ZD_AUX 352u                       // per-block table words: 286 lit/len + 30 dist + 19 bit-length (+ pad)
+
+// zlib deflate.c configuration_table rows (good, lazy, nice, chain), levels 4..9
+__constant__ uint16_t zd_cfg[10][4] = {{0, 0, 0, 0},      {0, 0, 0, 0},        {0, 0, 0, 0},        {0, 0, 0, 0},
+                                       {4, 4, 16, 16},    {8, 16, 32, 32},     {8, 16, 128, 128},   {8, 32, 128, 256},
+                                       {32, 128, 258, 1024}, {32, 258, 258, 4096}};
+
+struct ZsZWorkDev {  // one K1 / K2 work item
+  uint32_t job;
+  uint32_t len;
+  uint64_t start;
+};
+
+__device__ __forceinline__ uint32_t zd_max_dist(const ZsDJobDev &jb) { return (1u << jb.wbits) - ZD_LOOK; }
+
+// ---------------------------------------------------------------------------
+// K1: previous same-hash distance (0: none within 32767, or position 0 = NIL)
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(WAVE) zs_zd_prev_kernel(const ZsDJobDev *__restrict__ jobs,
+                                                           const ZsZWorkDev *__restrict__ work, uint16_t *__restrict__ prevd) {
+  __shared__ uint16_t head[32768];
+  const uint32_t lane = threadIdx.x;
+  const ZsZWorkDev wk = work[blockIdx.x];
+  const ZsDJobDev jb = jobs[wk.job];
+  const uint8_t *in = jb.in;
+  const uint64_t L = jb.in_len;
+  const uint64_t start = wk.start, to = wk.start + wk.len;
+  const uint64_t from = start >= 32768u ? start - 32768u : 0u;
+  // entries hold position & 0xffff; an entry whose age could exceed 32767 is
+  // reset every ZD_SWEEP positions to a position 40000 back (age stays in
+  // 40000 .. 56384 < 65536 until the next sweep: decoded as "none")
+  auto sweep = [&](uint64_t t) {
+    const uint32_t sent = (uint32_t)((t - 40000u) & 0xffffu);
+    for (uint32_t i = lane * 8; i < 32768u; i += WAVE * 8) {
+      uint4 v = *reinterpret_cast<const uint4 *>(&head[i]);
+      uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        uint32_t lo = w[k] & 0xffffu, hi = w[k] >> 16;
+        if (((uint32_t)(t - lo) & 0xffffu) > 32768u) lo = sent;
+        if (((uint32_t)(t - hi) & 0xffffu) > 32768u) hi = sent;
+        w[k] = lo | (hi << 16);
+      }
+      *reinterpret_cast<uint4 *>(&head[i]) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+  };
+  {
+    const uint32_t sent = (uint32_t)((from - 40000u) & 0xffffu);
+    for (uint32_t i = lane; i < 32768u / 2; i += WAVE) reinterpret_cast<uint32_t *>(head)[i] = sent | (sent << 16);
+  }
+  __builtin_amdgcn_wave_barrier();
+  uint16_t *po = prevd + jb.pos0;
+  for (uint64_t base = from; base < to; base += WAVE) {
+    if (base != from && ((base - from) % ZD_SWEEP) == 0) {
+      sweep(base);
+      __builtin_amdgcn_wave_barrier();
+    }
+    const uint64_t p = base + lane;
+    const bool valid = p + 2 < L && p < to;
+    uint32_t h = 0;
+    if (valid) h = (((uint32_t)in[p] << 10) ^ ((uint32_t)in[p + 1] << 5) ^ in[p + 2]) & 0x7fffu;
+    // lanes with the same hash: 15 ballots
+    uint64_t m = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 15; b++) {
+      const uint64_t B = __ballot(valid && ((h >> b) & 1u));
+      m &= ((h >> b) & 1u) ? B : ~B;
+    }
+    const uint64_t below = m & ((1ull << lane) - 1ull);
+    const uint64_t above = lane == 63 ? 0ull : (m & ~((2ull << lane) - 1ull));
+    uint32_t d;
+    if (below) {
+      d = lane - (63u - (uint32_t)__builtin_clzll(below));
+    } else {
+      const uint32_t v = head[h];
+      d = (uint32_t)(p - v) & 0xffffu;
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (valid && !above) head[h] = (uint16_t)(p & 0xffffu);  // the group's latest position
+    __builtin_amdgcn_wave_barrier();
+    if (p >= start && p < to) po[p] = (valid && d < 32768u && p != d) ? (uint16_t)d : (uint16_t)0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K2: longest match per position, two chain budgets
+// ---------------------------------------------------------------------------
+#define ZD_WB (ZD_S2 + 32768u + 272u)  // window bytes in LDS
+
+__device__ __forceinline__ uint32_t zd_lw(const uint32_t *w, uint32_t a) {  // 4 bytes at byte a
+  const uint32_t lo = w[a >> 2], hi = w[(a >> 2) + 1];
+  return __builtin_amdgcn_alignbyte(hi, lo, a & 3u);
+}
+
+__global__ void __launch_bounds__(ZD_MT) zs_zd_match_kernel(const ZsDJobDev *__restrict__ jobs,
+                                                             const ZsZWorkDev *__restrict__ work,
+                                                             const uint16_t *__restrict__ prevd, uint32_t *__restrict__ ma,
+                                                             uint32_t *__restrict__ mb) {
+  __shared__ __attribute__((aligned(16))) uint32_t s_w[ZD_WB / 4 + 4];
+  __shared__ __attribute__((aligned(16))) uint16_t s_pd[ZD_S2 + 32768u];
+  const uint32_t t = threadIdx.x, lane = t & (WAVE - 1), wv = t / WAVE;
+  const ZsZWorkDev wk = work[blockIdx.x];
+  const ZsDJobDev jb = jobs[wk.job];
+  const uint64_t L = jb.in_len, s = wk.start;
+  const int64_t B = (int64_t)s - 32768;  // LDS index of position q: q - B
+  // stage window bytes [max(0, B), min(L, s + n + 272)) and chain links [max(0, B), s + n)
+  {
+    uint8_t *wb = reinterpret_cast<uint8_t *>(s_w);
+    const uint64_t lo = B < 0 ? 0u : (uint64_t)B;
+    const uint64_t hi_b = s + wk.len + 272u;
+    for (uint32_t i = t; i < ZD_WB / 4 + 4; i += ZD_MT) s_w[i] = 0;
+    __syncthreads();
+    for (uint64_t q = lo + t; q < hi_b && q < L; q += ZD_MT) wb[q - B] = jb.in[q];
+    const uint16_t *pd = prevd + jb.pos0;
+    for (uint64_t q = lo + t; q < s + wk.len; q += ZD_MT) s_pd[q - B] = pd[q];
+  }
+  __syncthreads();
+  const uint32_t level = (uint32_t)jb.level;
+  const uint32_t nice = zd_cfg[level][2], chain = zd_cfg[level][3], chain_b = chain >> 2;
+  const uint32_t max_dist = zd_max_dist(jb);
+  uint32_t *oa = ma + jb.pos0, *ob = mb + jb.pos0;
+  // each wave owns 512 consecutive positions; a lane takes the next one when its walk ends
+  const uint32_t per_w = ZD_S2 / (ZD_MT / WAVE);
+  const uint64_t q_beg = s + (uint64_t)wv * per_w;
+  const uint64_t q_end = min(s + wk.len, q_beg + per_w);
+  uint64_t nextp = q_beg + WAVE;
+  uint64_t p = q_beg + lane;
+  bool active = p < q_end, fresh = true, fin = false;
+  uint32_t c = 0, k = 0, best = 0, bdist = 0, bl = 0, bd = 0, cap = 0, nicep = 0, ow = 0;
+  for (;;) {
+    if (active && fresh) {
+      fresh = false;
+      best = bdist = bl = bd = 0;
+      k = 0;
+      const uint32_t d0 = s_pd[p - B];
+      if (p + ZD_MINM > L || d0 == 0 || d0 > max_dist) {
+        fin = true;
+      } else {
+        const uint64_t look = L - p;
+        cap = look < ZD_MAXM ? (uint32_t)look : ZD_MAXM;
+        nicep = look < nice ? (uint32_t)look : nice;
+        c = (uint32_t)(p - B) - d0;  // LDS byte index of the candidate
+      }
+    }
+    if (active && !fin) {
+      const uint32_t pi = (uint32_t)(p - B);
+      const uint32_t nd = s_pd[c];  // next link, in flight during the compare
+      bool full = true;
+      if (best >= 3) full = zd_lw(s_w, c + best - 3) == ow;
+      if (full) {
+        uint32_t n = 0;
+        for (;;) {
+          const uint32_t x = zd_lw(s_w, c + n) ^ zd_lw(s_w, pi + n);
+          if (x) {
+            n += (uint32_t)__builtin_ctz(x) >> 3;
+            break;
+          }
+          n += 4;
+          if (n >= cap) break;
+        }
+        n = min(n, cap);
+        if (n > best) {
+          best = n;
+          bdist = pi - c;
+          if (best >= 3) ow = zd_lw(s_w, pi + best - 3);
+        }
+      }
+      k++;
+      if (k == chain_b) {
+        bl = best;
+        bd = bdist;
+      }
+      // zlib: stop at nice, at the chain budget, at a missing link, or when the
+      // next candidate is not above strstart - MAX_DIST
+      if (best >= nicep || k >= chain || nd == 0 || (pi - (c - nd)) >= max_dist) {
+        fin = true;
+        if (k < chain_b) {
+          bl = best;
+          bd = bdist;
+        }
+      } else {
+        c -= nd;
+      }
+    }
+    const bool done = active && fin;
+    if (done) {
+      oa[p] = best | (bdist << 9);
+      ob[p] = bl | (bd << 9);
+    }
+    const uint64_t fm = __ballot(done);
+    if (fm) {
+      if (done) {
+        p = nextp + (uint64_t)__builtin_popcountll(fm & ((1ull << lane) - 1ull));
+        active = p < q_end;
+        fresh = true;
+        fin = false;
+      }
+      nextp += (uint64_t)__builtin_popcountll(fm);
+    }
+    if (!__ballot(active)) break;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K3: deflate_slow's loop over the match tables.
+// State at a loop top: avail (a literal is pending at p - 1), prev_length,
+// prev_match distance, and which table gave it (the V bit a match start
+// records).  Packed: bit 0 avail, 1-9 prev_len, 10 variant, 11-25 prev_dist.
+// State A (avail 0, prev_len 2) follows every match and starts the stream.
+// ---------------------------------------------------------------------------
+#define ZD_STATE_A (2u << 1)
+
+struct ZdTabs {
+  const uint32_t *ma, *mb;
+  const uint8_t *in;
+  uint64_t L;
+  uint32_t good, lazy;
+};
+
+// one loop iteration at p; returns the token emitted (start, kind) via out
+// params: tok = 0 none, 1 literal at p - 1, 2 match at p - 1 (variant in *var)
+__device__ __forceinline__ uint32_t zd_step(const ZdTabs &T, uint64_t &p, uint32_t &st, uint32_t *var) {
+  const uint32_t avail = st & 1u, pl = (st >> 1) & 511u;
+  uint32_t mlen = 2, mdist = 0, mvar = 0;
+  if (pl < T.lazy) {
+    mvar = pl >= T.good ? 1u : 0u;
+    const uint32_t m = (mvar ? T.mb : T.ma)[p];
+    const uint32_t ml = m & 511u;
+    if (ml > pl) {
+      mlen = ml;
+      mdist = m >> 9;
+    } else if (ml) {
+      mlen = pl;  // longest_match returns best_len = prev_length
+    }
+    if (mlen == ZD_MINM && mdist > ZD_TOO_FAR) mlen = 2;
+  }
+  if (pl >= ZD_MINM && mlen <= pl) {
+    *var = (st >> 10) & 1u;
+    p = p - 1 + pl;
+    st = ZD_STATE_A;
+    return 2;
+  }
+  const uint32_t tok = avail ? 1u : 0u;
+  *var = 0;
+  st = 1u | (mlen << 1) | (mvar << 10) | (mdist << 11);
+  p += 1;
+  return tok;
+}
+
+__device__ __forceinline__ void zd_setbit(uint32_t *w, uint64_t i) { w[i >> 5] |= 1u << (i & 31u); }
+__device__ __forceinline__ void zd_putbit(uint32_t *w, uint64_t i, bool v) {
+  if (v) w[i >> 5] |= 1u << (i & 31u);
+}
+__device__ __forceinline__ bool zd_getbit(const uint32_t *w, uint64_t i) { return (w[i >> 5] >> (i & 31u)) & 1u; }
+
+// bitmaps of a job: S (token starts), V (variant of match starts), M (state-A marks)
+struct ZdBm {
+  uint32_t *S, *V, *M;
+};
+__device__ __forceinline__ uint64_t zd_bm_words(uint64_t L) { return (L + 32u) / 32u + 1u; }
+__device__ __forceinline__ ZdBm zd_bm(uint32_t *bm, const ZsDJobDev &jb) {
+  const uint64_t words = zd_bm_words(jb.in_len);
+  ZdBm b;
+  b.S = bm + jb.bm0;
+  b.V = b.S + words;
+  b.M = b.V + words;
+  return b;
+}
+
+// Token bits of a walk over [lo, hi): every loop top q with a literal pending
+// (avail) makes q - 1 a token start -- a literal, or the match deflate_slow
+// emits there, whose table is the state's variant bit.  A walk records
+// pending positions from its second loop top on, and the one pending when it
+// leaves (then q == hi): so each walk writes only positions in [lo, hi).
+template <typename SetF>
+__device__ __forceinline__ void zd_walk_record(const ZdTabs &T, uint64_t &q, uint32_t &qs, uint64_t hi, SetF set,
+                                               uint32_t *marks, uint64_t mark0) {
+  uint32_t var;
+  bool first = true;
+  while (q < hi) {
+    if (marks && qs == ZD_STATE_A) zd_setbit(marks, q - mark0);
+    if ((qs & 1u) && !first) set(q - 1, (qs >> 10) & 1u);
+    first = false;
+    (void)zd_step(T, q, qs, &var);
+  }
+  if (qs & 1u) set(q - 1, (qs >> 10) & 1u);
+}
+
+__global__ void __launch_bounds__(ZD_PT) zs_zd_parse_kernel(const ZsDJobDev *__restrict__ jobs, ZsDSegDev *__restrict__ segs,
+                                                             const uint32_t *__restrict__ ma, const uint32_t *__restrict__ mb,
+                                                             uint32_t *__restrict__ bm) {
+  __shared__ uint32_t s_S[ZD_REG / 32], s_V[ZD_REG / 32], s_M[ZD_REG / 32];
+  __shared__ uint64_t s_xp[ZD_PT];
+  __shared__ uint32_t s_xs[ZD_PT];
+  const uint32_t t = threadIdx.x;
+  const ZsDSegDev sg = segs[blockIdx.x];
+  const ZsDJobDev jb = jobs[sg.job];
+  if (!jb.exact) return;
+  ZdTabs T;
+  T.ma = ma + jb.pos0;
+  T.mb = mb + jb.pos0;
+  T.in = jb.in;
+  T.L = jb.in_len;
+  T.good = zd_cfg[jb.level][0];
+  T.lazy = zd_cfg[jb.level][1];
+  const uint64_t r0 = sg.start, rend = sg.start + sg.len;
+  const uint64_t a = r0 + (uint64_t)t * 256u, b = min(rend, a + 256u);
+  const bool act = a < rend;
+  for (uint32_t i = t; i < ZD_REG / 32; i += ZD_PT) s_S[i] = s_V[i] = s_M[i] = 0;
+  __syncthreads();
+  uint32_t var;
+  // speculative walk of the piece from (a, A): marks its state-A positions
+  uint64_t p = a;
+  uint32_t st = ZD_STATE_A;
+  while (act && p < b) {
+    if (st == ZD_STATE_A) zd_setbit(s_M, p - r0);
+    (void)zd_step(T, p, st, &var);
+  }
+  const uint64_t spec_p = act ? p : a;
+  const uint32_t spec_s = act ? st : ZD_STATE_A;
+  s_xp[t] = spec_p;
+  s_xs[t] = spec_s;
+  __syncthreads();
+  for (;;) {  // re-walk from the predecessor's exit until meeting a marked state-A position
+    uint64_t q = t == 0 ? r0 : s_xp[t - 1];
+    uint32_t qs = t == 0 ? ZD_STATE_A : s_xs[t - 1];
+    uint64_t rp = s_xp[t];
+    uint32_t rs = s_xs[t];
+    if (act) {
+      bool merged = false;
+      while (q < b) {
+        if (qs == ZD_STATE_A && zd_getbit(s_M, q - r0)) {
+          merged = true;
+          break;
+        }
+        (void)zd_step(T, q, qs, &var);
+      }
+      rp = merged ? spec_p : q;
+      rs = merged ? spec_s : qs;
+    }
+    __syncthreads();
+    const bool changed = act && (rp != s_xp[t] || rs != s_xs[t]);
+    if (changed) {
+      s_xp[t] = rp;
+      s_xs[t] = rs;
+    }
+    if (!__syncthreads_or(changed)) break;
+  }
+  // final walk from the true entry: token starts, variants, state-A marks
+  for (uint32_t i = t * 8; i < t * 8 + 8; i++) s_M[i] = 0;  // own words (256 positions)
+  __syncthreads();
+  if (act) {
+    uint64_t q = t == 0 ? r0 : s_xp[t - 1];
+    uint32_t qs = t == 0 ? ZD_STATE_A : s_xs[t - 1];
+    zd_walk_record(
+        T, q, qs, b,
+        [&](uint64_t x, uint32_t v) {
+          zd_setbit(s_S, x - r0);
+          zd_putbit(s_V, x - r0, v != 0);
+        },
+        s_M, r0);
+  }
+  __syncthreads();
+  ZdBm Bm = zd_bm(bm, jb);
+  const uint64_t w0 = r0 / 32u;
+  const uint32_t nw = (uint32_t)((sg.len + 31u) / 32u);
+  for (uint32_t i = t; i < nw; i += ZD_PT) {
+    Bm.S[w0 + i] = s_S[i];
+    Bm.V[w0 + i] = s_V[i];
+    Bm.M[w0 + i] = s_M[i];
+  }
+  const uint32_t lastp = sg.len ? (uint32_t)((sg.len + 255u) / 256u) - 1u : 0u;
+  if (t == lastp) {
+    segs[blockIdx.x].zx0 = s_xp[t];
+    segs[blockIdx.x].zs0 = s_xs[t];
+    segs[blockIdx.x].zx[0] = segs[blockIdx.x].zx[1] = s_xp[t];
+    segs[blockIdx.x].zs[0] = segs[blockIdx.x].zs[1] = s_xs[t];
+    segs[blockIdx.x].zfix = r0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K3b: across regions.  Region r's true entry is region r-1's current exit;
+// when it differs from the assumed one (region start, state A) the region is
+// re-walked from it until the walk meets a state-A position of the region's
+// own parse (and reaches past earlier rewrites), its tokens before that point
+// rewritten.  One round per launch (exits double-buffered: read [cur], write
+// [cur ^ 1]); the host repeats rounds until no exit changes.
+// ---------------------------------------------------------------------------
+__global__ void zs_zd_fix_kernel(const ZsDJobDev *__restrict__ jobs, ZsDSegDev *__restrict__ segs, uint32_t nseg,
+                                 const uint32_t *__restrict__ ma, const uint32_t *__restrict__ mb, uint32_t *__restrict__ bm,
+                                 uint32_t cur, uint32_t *__restrict__ changed) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nseg) return;
+  const ZsDSegDev sg = segs[i];
+  const ZsDJobDev jb = jobs[sg.job];
+  if (!jb.exact) return;
+  const uint64_t r0 = sg.start, rend = sg.start + sg.len;
+  uint64_t ep = r0;
+  uint32_t es = ZD_STATE_A;
+  if (r0 != 0) {
+    ep = segs[i - 1].zx[cur];
+    es = segs[i - 1].zs[cur];
+  }
+  uint64_t xp = sg.zx0;
+  uint32_t xs = sg.zs0;
+  if (!(ep == r0 && es == ZD_STATE_A) || sg.zfix != r0) {
+    ZdTabs T;
+    T.ma = ma + jb.pos0;
+    T.mb = mb + jb.pos0;
+    T.in = jb.in;
+    T.L = jb.in_len;
+    T.good = zd_cfg[jb.level][0];
+    T.lazy = zd_cfg[jb.level][1];
+    ZdBm Bm = zd_bm(bm, jb);
+    // 1. where does the walk from the entry merge with the region's own parse?
+    uint64_t q = ep;
+    uint32_t qs = es, var;
+    bool merged = false;
+    while (q < rend) {
+      if (qs == ZD_STATE_A && q >= sg.zfix && zd_getbit(Bm.M, q)) {
+        merged = true;
+        break;
+      }
+      (void)zd_step(T, q, qs, &var);
+    }
+    const uint64_t conv = merged ? q : rend;
+    if (!merged) {
+      xp = q;
+      xs = qs;
+    }
+    // 2. rewrite the tokens of [r0, conv)
+    for (uint64_t x = r0; x < conv; x += 32u) {
+      const uint64_t w = x >> 5;
+      const uint32_t n = (uint32_t)min<uint64_t>(32u, conv - x);
+      const uint32_t keep = n == 32u ? 0u : ~0u << n;  // region words start 32-aligned
+      Bm.S[w] &= keep;
+      Bm.V[w] &= keep;
+    }
+    q = ep;
+    qs = es;
+    zd_walk_record(
+        T, q, qs, conv,
+        [&](uint64_t x, uint32_t v) {
+          Bm.S[x >> 5] |= 1u << (x & 31u);
+          if (v) Bm.V[x >> 5] |= 1u << (x & 31u);
+        },
+        (uint32_t *)nullptr, 0);
+    segs[i].zfix = conv;
+  }
+  segs[i].zx[cur ^ 1u] = xp;
+  segs[i].zs[cur ^ 1u] = xs;
+  if (xp != sg.zx[cur] || xs != sg.zs[cur]) atomicOr(changed, 1u);
+}
+
+// ---------------------------------------------------------------------------
+// K4: blocks.  Symbols per region, then per job a prefix over regions and
+// the block list: block k holds symbols [16383 k, 16383 k + 16383); the last
+// one the rest -- or none, when a symbol of deflate_slow's loop filled the
+// previous block exactly (its pending final literal is tallied without a
+// flush check, trees.c _tr_tally + deflate.c FLUSH_BLOCK(s, 1)).
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) zs_zd_count_kernel(const ZsDJobDev *__restrict__ jobs, ZsDSegDev *__restrict__ segs,
+                                                           const uint32_t *__restrict__ bm) {
+  __shared__ uint32_t s_red[4];
+  const uint32_t t = threadIdx.x;
+  const ZsDSegDev sg = segs[blockIdx.x];
+  const ZsDJobDev jb = jobs[sg.job];
+  if (!jb.exact) return;
+  const uint32_t *S = bm + jb.bm0;
+  const uint64_t w0 = sg.start / 32u;
+  const uint32_t nw = (uint32_t)((sg.len + 31u) / 32u);
+  uint32_t c = 0;
+  for (uint32_t k = t; k < nw; k += 256) c += (uint32_t)__builtin_popcount(S[w0 + k]);
+  for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o);
+  if ((t & 63) == 0) s_red[t / 64] = c;
+  __syncthreads();
+  if (t == 0) segs[blockIdx.x].nsym = s_red[0] + s_red[1] + s_red[2] + s_red[3];
+}
+
+// zlib's window slides at a loop top t when the lookahead is short of
+// MIN_LOOKAHEAD and strstart >= wsize + MAX_DIST (deflate.c fill_window):
+// the slides done by loop top t of an L-byte input
+__device__ __forceinline__ uint64_t zd_slides(uint64_t t, uint64_t L, uint64_t wsize, uint64_t max_dist) {
+  uint64_t k = 0;
+  for (;;) {
+    const uint64_t base = k * wsize;
+    const uint64_t wend = min(L, base + 2 * wsize);
+    if (t >= base && wend - min(wend, t) < ZD_LOOK && t - base >= wsize + max_dist) k++;
+    else return k;
+  }
+}
+
+// position of symbol number `sym` of a job (sym < its symbol count)
+__device__ uint64_t zd_sym_pos(const ZsDSegDev *segs, const ZsDJobDev &jb, const uint32_t *S, uint64_t sym) {
+  // region: last one whose sym0 <= sym (binary search over the job's regions)
+  uint32_t lo = 0, hi = jb.nseg - 1;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi + 1) / 2;
+    if (segs[jb.seg0 + mid].sym0 <= sym) lo = mid;
+    else hi = mid - 1;
+  }
+  const ZsDSegDev &sg = segs[jb.seg0 + lo];
+  uint64_t rem = sym - sg.sym0;
+  uint64_t w = sg.start / 32u;
+  for (;; w++) {
+    const uint32_t x = S[w];
+    const uint32_t c = (uint32_t)__builtin_popcount(x);
+    if (rem < c) {
+      uint32_t y = x;
+      for (uint64_t k = 0; k < rem; k++) y &= y - 1u;
+      return w * 32u + (uint32_t)__builtin_ctz(y);
+    }
+    rem -= c;
+  }
+}
+
+// one workgroup per job: symbol prefix over regions, block count
+__global__ void __launch_bounds__(1024) zs_zd_blocks_kernel(ZsDJobDev *__restrict__ jobs, ZsDSegDev *__restrict__ segs,
+                                                             const uint32_t *__restrict__ bm) {
+  __shared__ uint64_t s_sum[1024];
+  const uint32_t t = threadIdx.x;
+  const ZsDJobDev jb = jobs[blockIdx.x];
+  if (!jb.exact) return;
+  const uint32_t ns = jb.nseg, per = (ns + 1023) / 1024;
+  const uint32_t k0 = min(ns, per * t), k1 = min(ns, per * (t + 1));
+  uint64_t sum = 0;
+  for (uint32_t k = k0; k < k1; k++) sum += segs[jb.seg0 + k].nsym;
+  s_sum[t] = sum;
+  __syncthreads();
+  if (t == 0) {
+    uint64_t acc = 0;
+    for (uint32_t k = 0; k < 1024; k++) {
+      const uint64_t x = s_sum[k];
+      s_sum[k] = acc;
+      acc += x;
+    }
+    const uint32_t *S = bm + jb.bm0;
+    const uint64_t L = jb.in_len;
+    const bool end_lit = acc && zd_getbit(S, L - 1);
+    const uint64_t nfull = acc / ZD_BLOCK;
+    const bool empty_last = acc % ZD_BLOCK == 0 && !end_lit;
+    jobs[blockIdx.x].nzblk = (uint32_t)(empty_last ? nfull + 1 : (acc + ZD_BLOCK - 1) / ZD_BLOCK);
+    s_sum[1023] = s_sum[1023];  // keep the scan in LDS
+  }
+  __syncthreads();
+  uint64_t off = s_sum[t];
+  for (uint32_t k = k0; k < k1; k++) {
+    segs[jb.seg0 + k].sym0 = off;
+    off += segs[jb.seg0 + k].nsym;
+  }
+}
+
+// one thread per block slot: byte range, BFINAL, stored eligibility
+__global__ void zs_zd_blist_kernel(const ZsDJobDev *__restrict__ jobs, uint32_t njobs, const ZsDSegDev *__restrict__ segs,
+                                   const uint32_t *__restrict__ bm, ZsZBlkDev *__restrict__ blks, uint32_t nslots,
+                                   const uint32_t *__restrict__ slot_job) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nslots) return;
+  const uint32_t j = slot_job[i];
+  const ZsDJobDev jb = jobs[j];
+  const uint32_t k = i - jb.zblk0;
+  ZsZBlkDev b{};
+  b.job = j;
+  if (!jb.exact || k >= jb.nzblk) {
+    b.nsym = 0xffffffffu;  // unused slot
+    blks[i] = b;
+    return;
+  }
+  const uint32_t *S = bm + jb.bm0;
+  const uint64_t L = jb.in_len;
+  const ZsDSegDev &lastseg = segs[jb.seg0 + jb.nseg - 1];
+  const uint64_t ns = lastseg.sym0 + lastseg.nsym;
+  const uint64_t s0 = (uint64_t)k * ZD_BLOCK;
+  const uint64_t s1 = min(ns, s0 + ZD_BLOCK);
+  b.last = k + 1 == jb.nzblk;
+  b.nsym = (uint32_t)(s1 > s0 ? s1 - s0 : 0);
+  b.first = b.nsym ? zd_sym_pos(segs, jb, S, s0) : L;
+  b.end = s1 < ns ? zd_sym_pos(segs, jb, S, s1) : L;
+  // the flush runs in the iteration whose loop top followed the block's last
+  // symbol start; the final block flushes after the loop (top = L)
+  uint64_t top = L;
+  if (!b.last) {
+    uint64_t x = b.end - 1;
+    while (!zd_getbit(S, x)) x--;
+    top = x + 1;
+  }
+  const uint64_t wsize = 1ull << jb.wbits;
+  b.stored_ok = b.first >= zd_slides(top, L, wsize, wsize - ZD_LOOK) * wsize;
+  blks[i] = b;
+}
+
+// ---------------------------------------------------------------------------
+// K4c: one workgroup per block: symbol frequencies, then (thread 0) the trees
+// and the choice of _tr_flush_block, restated from trees.c:
+//   build_tree   -- leaves in a heap ordered by (freq, depth), two nodes
+//                   joined per step, a third parent numbered from `elems`;
+//   gen_bitlen   -- lengths from the root down, overflow past max_length
+//                   repaired by moving leaves as zlib does;
+//   gen_codes    -- canonical codes (bit-reversed here for LSB-first output);
+//   build_bl_tree / scan_tree -- the code-length code;
+// opt_len / static_len accumulate exactly as zlib's (including its forced
+// second leaf), so the stored / static / dynamic choice is zlib's.
+// ---------------------------------------------------------------------------
+#define ZD_HEAP 573
+#define ZD_TT 256
+
+__constant__ uint8_t zd_xl[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
+__constant__ uint8_t zd_xd[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
+__constant__ uint8_t zd_xb[19] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 2, 3, 7};
+__constant__ uint8_t zd_blord[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+__device__ __forceinline__ uint32_t zd_lcode(uint32_t len) {  // 3..258 -> 0..28
+  if (len == 258) return 28;
+  const uint32_t l = len - 3;
+  if (l < 8) return l;
+  const uint32_t e = 29u - (uint32_t)__builtin_clz(l);
+  return 4 * (e + 1) + ((l >> e) & 3u);
+}
+__device__ __forceinline__ uint32_t zd_lbase(uint32_t c) { return c == 28 ? 258u : c < 8 ? c + 3 : ((4u + (c & 3u)) << (c / 4 - 1)) + 3u; }
+__device__ __forceinline__ uint32_t zd_dcode(uint32_t d) {  // 1..32768 -> 0..29
+  const uint32_t x = d - 1;
+  if (x < 4) return x;
+  const uint32_t e = 30u - (uint32_t)__builtin_clz(x);
+  return 2 * (e + 1) + ((x >> e) & 1u);
+}
+__device__ __forceinline__ uint32_t zd_dbase(uint32_t c) { return c < 4 ? c + 1 : ((2u + (c & 1u)) << (c / 2 - 1)) + 1u; }
+__device__ __forceinline__ uint32_t zd_rev(uint32_t c, uint32_t n) { return __builtin_bitreverse32(c) >> (32u - n); }
+
+struct ZdTreeLDS {
+  uint32_t freq[ZD_HEAP];
+  uint16_t dl[ZD_HEAP];  // parent while building, then code length (zlib's Dad / Len union)
+  uint8_t depth[ZD_HEAP];
+  int16_t heap[ZD_HEAP];
+  uint16_t blc[16];
+};
+
+__device__ __forceinline__ bool zd_smaller(const ZdTreeLDS &w, int n, int m) {
+  return w.freq[n] < w.freq[m] || (w.freq[n] == w.freq[m] && w.depth[n] <= w.depth[m]);
+}
+__device__ void zd_sift(ZdTreeLDS &w, int hl, int k) {
+  const int v = w.heap[k];
+  for (int j = k << 1; j <= hl; j <<= 1) {
+    if (j < hl && zd_smaller(w, w.heap[j + 1], w.heap[j])) j++;
+    if (zd_smaller(w, v, w.heap[j])) break;
+    w.heap[k] = w.heap[j];
+    k = j;
+  }
+  w.heap[k] = (int16_t)v;
+}
+
+// freq[0..elems) in w.freq; lens out in len_out[0..elems), canonical LSB-first
+// codes in code_out; returns max_code.  stat: static lengths (nullptr: none).
+__device__ int zd_build(ZdTreeLDS &w, int elems, const uint8_t *stat, const uint8_t *xb, int xbase, int maxlen,
+                        uint64_t &opt_len, uint64_t &static_len, uint16_t *len_out, uint16_t *code_out) {
+  int max_code = -1, hl = 0, hmax = ZD_HEAP;
+  for (int n = 0; n < elems; n++) {
+    if (w.freq[n]) {
+      w.heap[++hl] = (int16_t)(max_code = n);
+      w.depth[n] = 0;
+    } else {
+      w.dl[n] = 0;
+    }
+  }
+  while (hl < 2) {
+    const int node = max_code < 2 ? ++max_code : 0;
+    w.heap[++hl] = (int16_t)node;
+    w.freq[node] = 1;
+    w.depth[node] = 0;
+    opt_len--;
+    if (stat) static_len -= stat[node];
+  }
+  for (int n = hl / 2; n >= 1; n--) zd_sift(w, hl, n);
+  int node = elems;
+  do {
+    const int n = w.heap[1];
+    w.heap[1] = w.heap[hl--];
+    zd_sift(w, hl, 1);
+    const int m = w.heap[1];
+    w.heap[--hmax] = (int16_t)n;
+    w.heap[--hmax] = (int16_t)m;
+    w.freq[node] = w.freq[n] + w.freq[m];
+    w.depth[node] = (uint8_t)((w.depth[n] >= w.depth[m] ? w.depth[n] : w.depth[m]) + 1);
+    w.dl[n] = w.dl[m] = (uint16_t)node;
+    w.heap[1] = (int16_t)node++;
+    zd_sift(w, hl, 1);
+  } while (hl >= 2);
+  w.heap[--hmax] = w.heap[1];
+  for (int b = 0; b < 16; b++) w.blc[b] = 0;
+  w.dl[w.heap[hmax]] = 0;
+  int overflow = 0, h;
+  for (h = hmax + 1; h < ZD_HEAP; h++) {
+    const int n = w.heap[h];
+    int bits = w.dl[w.dl[n]] + 1;
+    if (bits > maxlen) bits = maxlen, overflow++;
+    w.dl[n] = (uint16_t)bits;
+    if (n > max_code) continue;
+    w.blc[bits]++;
+    const int x = n >= xbase ? xb[n - xbase] : 0;
+    opt_len += (uint64_t)w.freq[n] * (uint64_t)(bits + x);
+    if (stat) static_len += (uint64_t)w.freq[n] * (uint64_t)(stat[n] + x);
+  }
+  if (overflow) {
+    do {
+      int bits = maxlen - 1;
+      while (w.blc[bits] == 0) bits--;
+      w.blc[bits]--;
+      w.blc[bits + 1] += 2;
+      w.blc[maxlen]--;
+      overflow -= 2;
+    } while (overflow > 0);
+    for (int bits = maxlen; bits != 0; bits--) {
+      int n = w.blc[bits];
+      while (n != 0) {
+        const int m = w.heap[--h];
+        if (m > max_code) continue;
+        if (w.dl[m] != bits) {
+          opt_len += ((uint64_t)bits - w.dl[m]) * w.freq[m];
+          w.dl[m] = (uint16_t)bits;
+        }
+        n--;
+      }
+    }
+  }
+  uint32_t next[16], code = 0;
+  for (int b = 1; b <= 15; b++) next[b] = code = (code + w.blc[b - 1]) << 1;
+  for (int n = 0; n < elems; n++) {
+    const uint32_t len = n <= max_code ? w.dl[n] : 0u;
+    len_out[n] = (uint16_t)len;
+    code_out[n] = len ? (uint16_t)zd_rev(next[len]++, len) : (uint16_t)0;
+  }
+  return max_code;
+}
+
+// run-length coding of a code-length array (scan_tree / send_tree): mode 0
+// counts into freq[], mode 1 returns the bits it would send with (bl_len, bl_code)
+template <typename Emit>
+__device__ void zd_rle(const uint16_t *lens, int max_code, Emit emit) {
+  int prevlen = -1, nextlen = lens[0], count = 0, max_count = 7, min_count = 4;
+  if (nextlen == 0) max_count = 138, min_count = 3;
+  for (int n = 0; n <= max_code; n++) {
+    const int curlen = nextlen;
+    nextlen = n + 1 <= max_code ? lens[n + 1] : 0xffff;
+    if (++count < max_count && curlen == nextlen) continue;
+    if (count < min_count) {
+      for (; count; count--) emit(curlen, 0u, 0u);
+    } else if (curlen != 0) {
+      if (curlen != prevlen) {
+        emit(curlen, 0u, 0u);
+        count--;
+      }
+      emit(16, (uint32_t)count - 3u, 2u);
+    } else if (count <= 10) {
+      emit(17, (uint32_t)count - 3u, 3u);
+    } else {
+      emit(18, (uint32_t)count - 11u, 7u);
+    }
+    count = 0;
+    prevlen = curlen;
+    if (nextlen == 0) max_count = 138, min_count = 3;
+    else if (curlen == nextlen) max_count = 6, min_count = 3;
+    else max_count = 7, min_count = 4;
+  }
+}
+
+// token at position q (S bit set): literal, or match (len, dist) from its table
+struct ZdTok {
+  uint32_t len;  // 0: literal
+  uint32_t dist;
+  uint32_t lit;
+};
+__device__ __forceinline__ ZdTok zd_tok(const ZdTabs &T, const ZdBm &B, uint64_t q) {
+  ZdTok k;
+  const bool lit = q + 1 >= T.L || zd_getbit(B.S, q + 1);
+  if (lit) {
+    k.len = 0;
+    k.dist = 0;
+    k.lit = T.in[q];
+  } else {
+    const uint32_t m = (zd_getbit(B.V, q) ? T.mb : T.ma)[q];
+    k.len = m & 511u;
+    k.dist = m >> 9;
+    k.lit = 0;
+  }
+  return k;
+}
+
+// per-block tables in global memory (ZD_AUX words): [0, 286) lit/len code |
+// len << 16, [286, 316) distance, [316, 335) bit-length code
+__global__ void __launch_bounds__(ZD_TT) zs_zd_tree_kernel(const ZsDJobDev *__restrict__ jobs, ZsZBlkDev *__restrict__ blks,
+                                                            const uint32_t *__restrict__ ma, const uint32_t *__restrict__ mb,
+                                                            uint32_t *__restrict__ bm, uint32_t *__restrict__ aux) {
+  __shared__ uint32_t s_lf[288], s_df[32];
+  __shared__ ZdTreeLDS W;
+  __shared__ uint16_t s_ll[288], s_lc[288], s_dlen[32], s_dc[32], s_bl[19], s_bc[19];
+  const uint32_t t = threadIdx.x;
+  const ZsZBlkDev bk = blks[blockIdx.x];
+  if (bk.nsym == 0xffffffffu) return;
+  const ZsDJobDev jb = jobs[bk.job];
+  ZdTabs T;
+  T.ma = ma + jb.pos0;
+  T.mb = mb + jb.pos0;
+  T.in = jb.in;
+  T.L = jb.in_len;
+  const ZdBm B = zd_bm(bm, jb);
+  for (uint32_t i = t; i < 288; i += ZD_TT) s_lf[i] = 0;
+  if (t < 32) s_df[t] = 0;
+  __syncthreads();
+  const uint64_t n = bk.end - bk.first, per = (n + ZD_TT - 1) / ZD_TT;
+  const uint64_t q0 = bk.first + min(n, per * t), q1 = bk.first + min(n, per * (t + 1));
+  for (uint64_t q = q0; q < q1; q++) {
+    if (!zd_getbit(B.S, q)) continue;
+    const ZdTok k = zd_tok(T, B, q);
+    if (!k.len) {
+      atomicAdd(&s_lf[k.lit], 1u);
+    } else {
+      atomicAdd(&s_lf[257 + zd_lcode(k.len)], 1u);
+      atomicAdd(&s_df[zd_dcode(k.dist)], 1u);
+    }
+  }
+  __syncthreads();
+  if (t != 0) return;
+  uint8_t stat_l[288], stat_d[30];
+  for (int i = 0; i < 288; i++) stat_l[i] = i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : 8;
+  for (int i = 0; i < 30; i++) stat_d[i] = 5;
+  uint64_t opt = 0, stat = 0;
+  for (int i = 0; i < ZD_HEAP; i++) W.freq[i] = i < 286 ? s_lf[i] : 0u;
+  W.freq[256] = 1;  // end of block
+  const int lmax = zd_build(W, 286, stat_l, zd_xl, 257, 15, opt, stat, s_ll, s_lc);
+  for (int i = 0; i < ZD_HEAP; i++) W.freq[i] = i < 30 ? s_df[i] : 0u;
+  const int dmax = zd_build(W, 30, stat_d, zd_xd, 0, 15, opt, stat, s_dlen, s_dc);
+  uint32_t blf[19];
+  for (int i = 0; i < 19; i++) blf[i] = 0;
+  auto count = [&](int sym, uint32_t, uint32_t) { blf[sym]++; };
+  zd_rle(s_ll, lmax, count);
+  zd_rle(s_dlen, dmax, count);
+  for (int i = 0; i < ZD_HEAP; i++) W.freq[i] = i < 19 ? blf[i] : 0u;
+  uint64_t dummy = 0;
+  (void)zd_build(W, 19, nullptr, zd_xb, 0, 7, opt, dummy, s_bl, s_bc);
+  int blmax = 18;
+  for (; blmax >= 3; blmax--)
+    if (s_bl[zd_blord[blmax]] != 0) break;
+  opt += 3 * ((uint64_t)blmax + 1) + 5 + 5 + 4;
+  uint64_t opt_b = (opt + 3 + 7) >> 3;
+  const uint64_t stat_b = (stat + 3 + 7) >> 3;
+  if (stat_b <= opt_b) opt_b = stat_b;
+  const uint64_t nbytes = bk.end - bk.first;
+  ZsZBlkDev o = bk;
+  o.lmax = (uint32_t)lmax;
+  o.dmax = (uint32_t)dmax;
+  o.blmax = (uint32_t)blmax;
+  o.hbits = 0;
+  // exact bits (zlib's opt_len counts its forced leaves; the stream does not)
+  uint64_t body_dyn = 0, body_fix = 0;
+  for (int i = 0; i < 286; i++) {
+    const uint64_t f = s_lf[i] + (i == 256 ? 1u : 0u);
+    const uint32_t x = i >= 257 ? zd_xl[i - 257] : 0u;
+    body_dyn += f * (s_ll[i] + x);
+    body_fix += f * (stat_l[i] + x);
+  }
+  for (int i = 0; i < 30; i++) {
+    body_dyn += (uint64_t)s_df[i] * (s_dlen[i] + zd_xd[i]);
+    body_fix += (uint64_t)s_df[i] * (5u + zd_xd[i]);
+  }
+  if (nbytes + 4 <= opt_b && bk.stored_ok) {
+    o.type = 0;
+    o.bits = 32 + 8 * nbytes;  // + alignment, known at layout
+  } else if (stat_b == opt_b) {
+    o.type = 1;
+    o.bits = body_fix;
+  } else {
+    o.type = 2;
+    uint32_t hb = 5 + 5 + 4 + 3 * ((uint32_t)blmax + 1);
+    auto bits = [&](int sym, uint32_t, uint32_t xn) { hb += s_bl[sym] + xn; };
+    zd_rle(s_ll, lmax, bits);
+    zd_rle(s_dlen, dmax, bits);
+    o.hbits = hb;
+    o.bits = hb + body_dyn;
+  }
+  blks[blockIdx.x] = o;
+  uint32_t *ax = aux + (size_t)blockIdx.x * ZD_AUX;
+  if (o.type == 1) {
+    for (int i = 0; i < 286; i++) {
+      const uint32_t L = stat_l[i];
+      uint32_t c;  // static code of symbol i (trees.c tr_static_init: canonical over 288 lengths)
+      if (i < 144) c = 0x30 + i;
+      else if (i < 256) c = 0x190 + (i - 144);
+      else if (i < 280) c = i - 256;
+      else c = 0xc0 + (i - 280);
+      ax[i] = zd_rev(c, L) | (L << 16);
+    }
+    for (int i = 0; i < 30; i++) ax[286 + i] = zd_rev((uint32_t)i, 5) | (5u << 16);
+  } else if (o.type == 2) {
+    for (int i = 0; i < 286; i++) ax[i] = s_lc[i] | ((uint32_t)s_ll[i] << 16);
+    for (int i = 0; i < 30; i++) ax[286 + i] = s_dc[i] | ((uint32_t)s_dlen[i] << 16);
+    for (int i = 0; i < 19; i++) ax[316 + i] = s_bc[i] | ((uint32_t)s_bl[i] << 16);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K4d: one workgroup per job: block bit offsets.  A block takes 3 type bits
+// plus its body; a stored block also aligns to a byte after the type bits
+// (trees.c _tr_stored_block: bi_windup), so with stored blocks the offsets
+// are summed in order by one thread.  Then the wrapper header and the check.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(1024) zs_zd_layout_kernel(ZsDJobDev *__restrict__ jobs, ZsZBlkDev *__restrict__ blks,
+                                                             uint8_t *__restrict__ stage) {
+  __shared__ uint64_t s_sum[1024];
+  __shared__ uint32_t s_stored;
+  const uint32_t t = threadIdx.x;
+  ZsDJobDev jb = jobs[blockIdx.x];
+  if (!jb.exact) return;
+  const uint32_t nb = jb.nzblk, per = (nb + 1023) / 1024;
+  const uint32_t k0 = min(nb, per * t), k1 = min(nb, per * (t + 1));
+  const uint32_t hdr = jb.wrap == 2 ? 10u : (jb.wrap == 1 ? 2u : 0u);
+  if (t == 0) s_stored = 0;
+  __syncthreads();
+  uint64_t sum = 0;
+  bool stored = false;
+  for (uint32_t k = k0; k < k1; k++) {
+    const ZsZBlkDev &b = blks[jb.zblk0 + k];
+    sum += 3 + b.bits;
+    stored |= b.type == 0;
+  }
+  if (stored) atomicOr(&s_stored, 1u);
+  s_sum[t] = sum;
+  __syncthreads();
+  uint64_t endbit = 0;
+  if (!s_stored) {
+    if (t == 0) {
+      uint64_t acc = 8ull * hdr;
+      for (uint32_t k = 0; k < 1024; k++) {
+        const uint64_t x = s_sum[k];
+        s_sum[k] = acc;
+        acc += x;
+      }
+      s_sum[0] = s_sum[0];
+      jobs[blockIdx.x].total_out = (acc + 7) / 8 + (jb.wrap == 2 ? 8u : (jb.wrap == 1 ? 4u : 0u));
+    }
+    __syncthreads();
+    uint64_t off = s_sum[t];
+    for (uint32_t k = k0; k < k1; k++) {
+      blks[jb.zblk0 + k].bitoff = off;
+      off += 3 + blks[jb.zblk0 + k].bits;
+    }
+  } else if (t == 0) {
+    uint64_t off = 8ull * hdr;
+    for (uint32_t k = 0; k < nb; k++) {
+      ZsZBlkDev &b = blks[jb.zblk0 + k];
+      b.bitoff = off;
+      off += 3;
+      if (b.type == 0) off = (off + 7) & ~7ull;
+      off += b.bits;
+    }
+    endbit = off;
+    jobs[blockIdx.x].total_out = (endbit + 7) / 8 + (jb.wrap == 2 ? 8u : (jb.wrap == 1 ? 4u : 0u));
+  }
+  if (t == 0) {
+    jobs[blockIdx.x].check = jb.wrap == 2   ? zs_crc_final((uint32_t)jb.ck_a, jb.in_len)
+                             : jb.wrap == 1 ? zs_adler_final(jb.ck_a, jb.ck_b, jb.in_len)
+                                            : 0u;
+    uint8_t *o = stage + jb.stage;
+    if (jb.wrap == 2) {  // gzip header as zlib writes it with no options (mtime 0, OS 3)
+      const uint8_t gz[10] = {0x1f, 0x8b, 8, 0, 0, 0, 0, 0, (uint8_t)(jb.level == 9 ? 2 : (jb.level < 2 ? 4 : 0)), 3};
+      for (int i = 0; i < 10; i++) o[i] = gz[i];
+    } else if (jb.wrap == 1) {  // CMF/FLG with FLEVEL as deflate.c sets it, FCHECK % 31
+      const uint32_t flevel = jb.level < 2 ? 0u : (jb.level < 6 ? 1u : (jb.level == 6 ? 2u : 3u));
+      uint32_t h = ((((jb.wbits - 8u) << 4) | 8u) << 8) | (flevel << 6);
+      h += 31u - (h % 31u);
+      o[0] = (uint8_t)(h >> 8);
+      o[1] = (uint8_t)h;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K5: one workgroup per block: the bits.  Threads own contiguous position
+// ranges; a count pass and a block scan give each its bit offset, then each
+// writes its bits -- whole words with plain stores, its first and last
+// partial words with atomicOr (the staging area is zeroed).
+// ---------------------------------------------------------------------------
+struct ZdBits {
+  uint32_t *w;   // staging words
+  uint64_t wi;   // current word
+  uint64_t acc;  // pending bits, LSB first
+  uint32_t n;    // pending bit count (first word: the bits before our start count as zeros)
+  bool first;
+  __device__ void init(uint32_t *base, uint64_t bit) {
+    w = base;
+    wi = bit >> 5;
+    acc = 0;
+    n = (uint32_t)(bit & 31u);
+    first = true;
+  }
+  __device__ __forceinline__ void put(uint32_t v, uint32_t nb) {
+    acc |= (uint64_t)v << n;
+    n += nb;
+    if (n >= 32) {
+      const uint32_t x = (uint32_t)acc;
+      if (first) atomicOr(&w[wi], x);
+      else w[wi] = x;
+      first = false;
+      wi++;
+      acc >>= 32;
+      n -= 32;
+    }
+  }
+  __device__ void done() {
+    if (n) atomicOr(&w[wi], (uint32_t)acc);
+  }
+};
+
+__global__ void __launch_bounds__(ZD_TT) zs_zd_emit_kernel(const ZsDJobDev *__restrict__ jobs, const ZsZBlkDev *__restrict__ blks,
+                                                            const uint32_t *__restrict__ ma, const uint32_t *__restrict__ mb,
+                                                            uint32_t *__restrict__ bm, const uint32_t *__restrict__ aux,
+                                                            uint8_t *__restrict__ stage) {
+  __shared__ uint32_t s_l[288], s_d[32];
+  __shared__ uint64_t s_off[ZD_TT];
+  const uint32_t t = threadIdx.x;
+  const ZsZBlkDev bk = blks[blockIdx.x];
+  if (bk.nsym == 0xffffffffu) return;
+  const ZsDJobDev jb = jobs[bk.job];
+  uint8_t *o8 = stage + jb.stage;  // 4 KiB aligned
+  uint32_t *o32 = reinterpret_cast<uint32_t *>(o8);
+  const uint64_t n = bk.end - bk.first;
+  if (bk.type == 0) {  // stored: 3 type bits, align, LEN, NLEN, the bytes
+    if (t == 0) {
+      const uint64_t b = bk.bitoff;
+      const uint64_t v = (uint64_t)bk.last << (b & 31u);
+      if (v) {
+        atomicOr(&o32[b >> 5], (uint32_t)v);
+        if (v >> 32) atomicOr(&o32[(b >> 5) + 1], (uint32_t)(v >> 32));
+      }
+    }
+    const uint64_t P = (bk.bitoff + 3 + 7) / 8;
+    const uint32_t len = (uint32_t)n;
+    if (t < 4) o8[P + t] = (uint8_t)((t < 2 ? len : ~len) >> (8 * (t & 1)));
+    for (uint64_t i = t; i < n; i += ZD_TT) o8[P + 4 + i] = jb.in[bk.first + i];
+    return;
+  }
+  const uint32_t *ax = aux + (size_t)blockIdx.x * ZD_AUX;
+  for (uint32_t i = t; i < 286; i += ZD_TT) s_l[i] = ax[i];
+  if (t < 30) s_d[t] = ax[286 + t];
+  __syncthreads();
+  ZdTabs T;
+  T.ma = ma + jb.pos0;
+  T.mb = mb + jb.pos0;
+  T.in = jb.in;
+  T.L = jb.in_len;
+  const ZdBm B = zd_bm(bm, jb);
+  const uint64_t per = (n + ZD_TT - 1) / ZD_TT;
+  const uint64_t q0 = bk.first + min(n, per * t), q1 = bk.first + min(n, per * (t + 1));
+  auto sym_bits = [&](const ZdTok &k) -> uint32_t {
+    if (!k.len) return s_l[k.lit] >> 16;
+    const uint32_t lc = zd_lcode(k.len), dc = zd_dcode(k.dist);
+    return (s_l[257 + lc] >> 16) + zd_xl[lc] + (s_d[dc] >> 16) + zd_xd[dc];
+  };
+  uint64_t mine = t == 0 ? 3u + bk.hbits : 0u;
+  for (uint64_t q = q0; q < q1; q++)
+    if (zd_getbit(B.S, q)) mine += sym_bits(zd_tok(T, B, q));
+  if (t == ZD_TT - 1) mine += s_l[256] >> 16;  // end of block
+  s_off[t] = mine;
+  __syncthreads();
+  if (t == 0) {
+    uint64_t acc = bk.bitoff;
+    for (uint32_t k = 0; k < ZD_TT; k++) {
+      const uint64_t x = s_off[k];
+      s_off[k] = acc;
+      acc += x;
+    }
+  }
+  __syncthreads();
+  ZdBits W;
+  W.init(o32, s_off[t]);
+  if (t == 0) {
+    W.put(bk.last | (bk.type << 1), 3);
+    if (bk.type == 2) {
+      W.put(bk.lmax + 1 - 257, 5);
+      W.put(bk.dmax + 1 - 1, 5);
+      W.put(bk.blmax + 1 - 4, 4);
+      const uint32_t *bl = ax + 316;
+      for (uint32_t r = 0; r <= bk.blmax; r++) W.put(bl[zd_blord[r]] >> 16, 3);
+      uint16_t lens[286];
+      auto send = [&](int sym, uint32_t xv, uint32_t xn) {
+        W.put(bl[sym] & 0xffffu, bl[sym] >> 16);
+        if (xn) W.put(xv, xn);
+      };
+      for (uint32_t i = 0; i <= bk.lmax; i++) lens[i] = (uint16_t)(s_l[i] >> 16);
+      zd_rle(lens, (int)bk.lmax, send);
+      for (uint32_t i = 0; i <= bk.dmax; i++) lens[i] = (uint16_t)(s_d[i] >> 16);
+      zd_rle(lens, (int)bk.dmax, send);
+    }
+  }
+  for (uint64_t q = q0; q < q1; q++) {
+    if (!zd_getbit(B.S, q)) continue;
+    const ZdTok k = zd_tok(T, B, q);
+    if (!k.len) {
+      W.put(s_l[k.lit] & 0xffffu, s_l[k.lit] >> 16);
+    } else {
+      const uint32_t lc = zd_lcode(k.len), dc = zd_dcode(k.dist);
+      W.put(s_l[257 + lc] & 0xffffu, s_l[257 + lc] >> 16);
+      if (zd_xl[lc]) W.put(k.len - zd_lbase(lc), zd_xl[lc]);
+      W.put(s_d[dc] & 0xffffu, s_d[dc] >> 16);
+      if (zd_xd[dc]) W.put(k.dist - zd_dbase(dc), zd_xd[dc]);
+    }
+  }
+  if (t == ZD_TT - 1) W.put(s_l[256] & 0xffffu, s_l[256] >> 16);
+  W.done();
+}
+
+// ---------------------------------------------------------------------------
+// host launch: everything up to the bits (the check and trailer kernels of
+// deflate_kernels.hip run beside it); returns after the fix-up rounds, which
+// need the host (a flag read per round)
+// ---------------------------------------------------------------------------
+extern "C" int zs_launch_zdeflate(ZsDJobDev *d_jobs, uint32_t njobs, ZsDSegDev *d_segs, uint32_t nseg,
+                                  const ZsZWorkDev *d_w1, uint32_t n1, const ZsZWorkDev *d_w2, uint32_t n2,
+                                  uint16_t *d_prevd, uint32_t *d_ma, uint32_t *d_mb, uint32_t *d_bm, ZsZBlkDev *d_blks,
+                                  uint32_t nblk_slots, const uint32_t *d_slot_job, uint32_t *d_aux, uint8_t *d_stage,
+                                  uint32_t *d_flag, hipStream_t st, hipEvent_t *ev) {
+  if (ev) (void)hipEventRecord(ev[0], st);
+  hipLaunchKernelGGL(zs_zd_prev_kernel, dim3(n1), dim3(WAVE), 0, st, d_jobs, d_w1, d_prevd);
+  hipLaunchKernelGGL(zs_zd_match_kernel, dim3(n2), dim3(ZD_MT), 0, st, d_jobs, d_w2, d_prevd, d_ma, d_mb);
+  if (ev) (void)hipEventRecord(ev[1], st);
+  hipLaunchKernelGGL(zs_zd_parse_kernel, dim3(nseg), dim3(ZD_PT), 0, st, d_jobs, d_segs, d_ma, d_mb, d_bm);
+  uint32_t cur = 0;
+  for (int round = 0; round < 4096; round++) {
+    uint32_t changed = 0;
+    if (hipMemsetAsync(d_flag, 0, sizeof(uint32_t), st) != hipSuccess) return -1;
+    hipLaunchKernelGGL(zs_zd_fix_kernel, dim3((nseg + 255) / 256), dim3(256), 0, st, d_jobs, d_segs, nseg, d_ma, d_mb, d_bm,
+                       cur, d_flag);
+    if (hipMemcpyAsync(&changed, d_flag, sizeof(uint32_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+      return -1;
+    cur ^= 1u;
+    if (!changed) break;
+  }
+  if (ev) (void)hipEventRecord(ev[2], st);
+  hipLaunchKernelGGL(zs_zd_count_kernel, dim3(nseg), dim3(256), 0, st, d_jobs, d_segs, d_bm);
+  hipLaunchKernelGGL(zs_zd_blocks_kernel, dim3(njobs), dim3(1024), 0, st, d_jobs, d_segs, d_bm);
+  hipLaunchKernelGGL(zs_zd_blist_kernel, dim3((nblk_slots + 255) / 256), dim3(256), 0, st, d_jobs, njobs, d_segs, d_bm,
+                     d_blks, nblk_slots, d_slot_job);
+  hipLaunchKernelGGL(zs_zd_tree_kernel, dim3(nblk_slots), dim3(ZD_TT), 0, st, d_jobs, d_blks, d_ma, d_mb, d_bm, d_aux);
+  hipLaunchKernelGGL(zs_zd_layout_kernel, dim3(njobs), dim3(1024), 0, st, d_jobs, d_blks, d_stage);
+  hipLaunchKernelGGL(zs_zd_emit_kernel, dim3(nblk_slots), dim3(ZD_TT), 0, st, d_jobs, d_blks, d_ma, d_mb, d_bm, d_aux,
+                     d_stage);
+  if (ev) (void)hipEventRecord(ev[3], st);
+  return 0;
+}

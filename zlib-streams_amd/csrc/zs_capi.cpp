@@ -35,6 +35,17 @@ extern "C" void zs_launch_fixed_compact(uint32_t *fixed, hipStream_t st);
 extern "C" void zs_launch_deflate(ZsDJobDev *d_jobs, uint32_t njobs, ZsDSegDev *d_segs, uint32_t nseg, uint16_t *d_dist16,
                                   uint8_t *d_len8, uint32_t *d_bm, uint32_t *d_aux, uint32_t *d_obuf, uint8_t *d_stage,
                                   uint16_t *d_lx16, int has_std, int has_d64, hipStream_t st, hipEvent_t *ev);
+struct ZsZWorkDev {  // must match deflate_zlib.hip
+  uint32_t job;
+  uint32_t len;
+  uint64_t start;
+};
+extern "C" int zs_launch_zdeflate(ZsDJobDev *d_jobs, uint32_t njobs, ZsDSegDev *d_segs, uint32_t nseg,
+                                  const ZsZWorkDev *d_w1, uint32_t n1, const ZsZWorkDev *d_w2, uint32_t n2,
+                                  uint16_t *d_prevd, uint32_t *d_ma, uint32_t *d_mb, uint32_t *d_bm, ZsZBlkDev *d_blks,
+                                  uint32_t nblk_slots, const uint32_t *d_slot_job, uint32_t *d_aux, uint8_t *d_stage,
+                                  uint32_t *d_flag, hipStream_t st, hipEvent_t *ev);
+extern "C" void zs_launch_dz_trailer(ZsDJobDev *d_jobs, uint32_t njobs, uint8_t *d_stage, hipStream_t st);
 extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, ZsSegDev *d_segs, uint32_t nseg,
                                   ZsCJobDev *d_cjobs, uint32_t ncjobs, ZsChunkDev *d_units, uint32_t nunit_slots,
                                   uint16_t *d_scratch, uint32_t *d_tokens, ZsTokPool pool, uint32_t *d_tables,
@@ -794,6 +805,20 @@ struct DzWorkspace {
 };
 DzWorkspace g_dz;
 
+// zlib-identical deflate (deflate_zlib.hip): per position, per bitmap word,
+// per work item, per block
+constexpr uint64_t ZD_S1_HOST = 131072, ZD_S2_HOST = 8192, ZD_BLOCK_HOST = 16383, ZD_AUX_HOST = 352;
+struct ZdWorkspace {
+  size_t cap_pos = 0, cap_bm = 0, cap_w1 = 0, cap_w2 = 0, cap_blk = 0;
+  uint16_t *d_prevd = nullptr;
+  uint32_t *d_ma = nullptr, *d_mb = nullptr, *d_bm = nullptr, *d_aux = nullptr, *d_slot_job = nullptr, *d_flag = nullptr;
+  ZsZWorkDev *d_w1 = nullptr, *d_w2 = nullptr;
+  ZsZBlkDev *d_blks = nullptr;
+  hipEvent_t ev[4] = {};
+};
+ZdWorkspace g_zd;
+uint64_t zd_bm_words(uint64_t L) { return (L + 32) / 32 + 1; }
+
 // deflateInit2 windowBits as zlib 1.2.11 deflate.c checks them: 9..15 zlib,
 // -9..-15 raw, 25..31 gzip; 8 only with the zlib wrapper, where it becomes 9
 bool parse_dz_wbits(int wb, int *wrap, uint32_t *w) {
@@ -824,6 +849,109 @@ int dz_grow(T **p, size_t *cap, size_t need) {
   int r = grow_dev(p, c);
   if (r) return r;
   *cap = c;
+  return 0;
+}
+
+// The zlib-identical jobs of the batch in g_dz.h_jobs[0..nv) (exact = 1): lay
+// out their position arrays, bitmaps, work items and block slots, then run
+// deflate_zlib.hip after the fast pipeline (whose check kernel computed their
+// CRC-32 / Adler-32 pieces).
+struct ZdPlan {
+  std::vector<ZsZWorkDev> w1, w2;
+  std::vector<uint32_t> slot_job;
+  size_t pos = 0, bmw = 0;
+  uint32_t nex = 0;
+} g_zdp;
+
+// before the jobs are uploaded: position arrays, bitmaps, block slots of the
+// zlib-identical jobs
+void zd_plan(uint32_t nv) {
+  ZdPlan &P = g_zdp;
+  P = ZdPlan();
+  for (uint32_t k = 0; k < nv; k++) {
+    ZsDJobDev &jd = g_dz.h_jobs[k];
+    if (!jd.exact) continue;
+    P.nex++;
+    const uint64_t L = jd.in_len;
+    jd.pos0 = P.pos;
+    P.pos += (L + 64) & ~uint64_t(63);
+    jd.bm0 = P.bmw;
+    P.bmw += 3 * zd_bm_words(L) + 4;
+    for (uint64_t a = 0; a < L; a += ZD_S1_HOST) P.w1.push_back({k, (uint32_t)std::min<uint64_t>(ZD_S1_HOST, L - a), a});
+    for (uint64_t a = 0; a < L; a += ZD_S2_HOST) P.w2.push_back({k, (uint32_t)std::min<uint64_t>(ZD_S2_HOST, L - a), a});
+    jd.zblk0 = (uint32_t)P.slot_job.size();
+    jd.zblk_cap = (uint32_t)((L + ZD_BLOCK_HOST - 1) / ZD_BLOCK_HOST + 1);
+    for (uint32_t b = 0; b < jd.zblk_cap; b++) P.slot_job.push_back(k);
+  }
+}
+
+int zd_run(uint32_t nv, size_t nseg, hipStream_t st) {
+  ZdPlan &P = g_zdp;
+  std::vector<ZsZWorkDev> &w1 = P.w1, &w2 = P.w2;
+  std::vector<uint32_t> &slot_job = P.slot_job;
+  const size_t pos = P.pos, bmw = P.bmw;
+  const uint32_t nex = P.nex;
+  if (!nex) return 0;
+  int r;
+  auto grow = [&](auto **p, size_t *cap, size_t need) -> int {
+    if (need <= *cap) return 0;
+    const size_t c = std::max(need, *cap + *cap / 4);
+    *cap = 0;
+    int rr = grow_dev(p, c);
+    if (!rr) *cap = c;
+    return rr;
+  };
+  size_t cpos = g_zd.cap_pos;
+  if (pos + 64 > g_zd.cap_pos) {
+    size_t dummy = 0;
+    g_zd.cap_pos = 0;
+    if ((r = grow(&g_zd.d_prevd, &dummy, pos + 64)) || (dummy = 0, r = grow(&g_zd.d_ma, &dummy, pos + 64)) ||
+        (dummy = 0, r = grow(&g_zd.d_mb, &dummy, pos + 64)))
+      return r;
+    g_zd.cap_pos = pos + 64;
+  }
+  (void)cpos;
+  if ((r = grow(&g_zd.d_bm, &g_zd.cap_bm, bmw + 16)) || (r = grow(&g_zd.d_w1, &g_zd.cap_w1, w1.size() + 1)) ||
+      (r = grow(&g_zd.d_w2, &g_zd.cap_w2, w2.size() + 1)))
+    return r;
+  if (slot_job.size() > g_zd.cap_blk) {
+    const size_t c = std::max(slot_job.size(), g_zd.cap_blk + g_zd.cap_blk / 4);
+    g_zd.cap_blk = 0;
+    if ((r = grow_dev(&g_zd.d_blks, c)) || (r = grow_dev(&g_zd.d_slot_job, c)) || (r = grow_dev(&g_zd.d_aux, c * ZD_AUX_HOST)))
+      return r;
+    g_zd.cap_blk = c;
+  }
+  if (!g_zd.d_flag && (r = grow_dev(&g_zd.d_flag, 4))) return r;
+  // bitmaps start zeroed (the parse writes whole region words; a region's
+  // tail word and the words past the input stay 0)
+  HIP_OK(hipMemsetAsync(g_zd.d_bm, 0, (bmw + 16) * sizeof(uint32_t), st));
+  if (!w1.empty()) HIP_OK(hipMemcpyAsync(g_zd.d_w1, w1.data(), w1.size() * sizeof(ZsZWorkDev), hipMemcpyHostToDevice, st));
+  if (!w2.empty()) HIP_OK(hipMemcpyAsync(g_zd.d_w2, w2.data(), w2.size() * sizeof(ZsZWorkDev), hipMemcpyHostToDevice, st));
+  HIP_OK(hipMemcpyAsync(g_zd.d_slot_job, slot_job.data(), slot_job.size() * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+  hipEvent_t *ev = nullptr;
+  if (g_ws.prof) {
+    if (!g_zd.ev[0])
+      for (int i = 0; i < 4; i++) HIP_OK(hipEventCreate(&g_zd.ev[i]));
+    ev = g_zd.ev;
+  }
+  if (zs_launch_zdeflate(g_dz.d_jobs, nv, g_dz.d_segs, (uint32_t)nseg, g_zd.d_w1, (uint32_t)w1.size(), g_zd.d_w2,
+                         (uint32_t)w2.size(), g_zd.d_prevd, g_zd.d_ma, g_zd.d_mb, g_zd.d_bm, g_zd.d_blks,
+                         (uint32_t)slot_job.size(), g_zd.d_slot_job, g_zd.d_aux, g_dz.d_stage, g_zd.d_flag, st, ev)) {
+    set_err("zlib-identical deflate: fix-up round failed");
+    return ZS_ENODEV;
+  }
+  zs_launch_dz_trailer(g_dz.d_jobs, nv, g_dz.d_stage, st);
+  if (ev) {
+    HIP_OK(hipStreamSynchronize(st));
+    float a = 0, b = 0, c = 0;
+    HIP_OK(hipEventElapsedTime(&a, ev[0], ev[1]));
+    HIP_OK(hipEventElapsedTime(&b, ev[1], ev[2]));
+    HIP_OK(hipEventElapsedTime(&c, ev[2], ev[3]));
+    g_dz.stage_ms[0] += a;
+    g_dz.stage_ms[1] += b;
+    g_dz.stage_ms[2] += c;
+    g_dz.ms += a + b + c;
+  }
   return 0;
 }
 
@@ -863,6 +991,7 @@ int deflate_batch_locked(const zs_djob *jobs, uint32_t n, zs_result *results, ui
     jd.wrap = wrap;
     jd.level = level;
     jd.wbits = w;
+    jd.exact = (!d64 && level >= 4 && !(flags & ZS_F_DEFLATE_FAST)) ? 1u : 0u;
     jd.seg0 = (uint32_t)nseg;
     jd.nseg = (uint32_t)std::max<uint64_t>(1, (jd.in_len + DZ_SEG_HOST - 1) / DZ_SEG_HOST);
     jd.stage = stage_total;
@@ -918,6 +1047,7 @@ int deflate_batch_locked(const zs_djob *jobs, uint32_t n, zs_result *results, ui
     }
   }
   HIP_OK(hipMemsetAsync(g_dz.d_stage, 0, stage_total, st));
+  zd_plan(nv);
   HIP_OK(hipMemcpyAsync(g_dz.d_jobs, g_dz.h_jobs, nv * sizeof(ZsDJobDev), hipMemcpyHostToDevice, st));
   HIP_OK(hipMemcpyAsync(g_dz.d_segs, g_dz.h_segs, nseg * sizeof(ZsDSegDev), hipMemcpyHostToDevice, st));
   hipEvent_t *ev = nullptr;
@@ -928,6 +1058,7 @@ int deflate_batch_locked(const zs_djob *jobs, uint32_t n, zs_result *results, ui
   }
   zs_launch_deflate(g_dz.d_jobs, nv, g_dz.d_segs, (uint32_t)nseg, g_dz.d_tok, g_dz.d_len8, g_dz.d_bm, g_dz.d_aux, g_dz.d_obuf,
                     g_dz.d_stage, g_dz.d_lx16, has_std, has_d64, st, ev);
+  if ((r = zd_run(nv, nseg, st))) return r;
   {
     hipError_t le = hipGetLastError();
     if (le != hipSuccess) {

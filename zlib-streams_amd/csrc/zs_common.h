@@ -194,6 +194,32 @@ struct ZsDJobDev {
   uint32_t wbits;      // window bits 9..15 (match distances <= 2^wbits; zlib CINFO = wbits - 8)
   uint64_t ck_a;       // check accumulators (zs_check.h): CRC XOR / Adler sum A (zeroed by the host)
   uint64_t ck_b;       // Adler weighted sum B
+  // zlib-identical mode (exact = 1; deflate_zlib.hip)
+  uint32_t exact;
+  uint32_t nzblk;      // blocks (zs_zd_blocks_kernel)
+  uint64_t pos0;       // first entry of the job's position arrays
+  uint64_t bm0;        // first word of the job's bitmaps
+  uint32_t zblk0;      // first block slot
+  uint32_t zblk_cap;   // block slots reserved: ceil(in_len / 16383) + 1
+};
+
+// zlib-identical mode (deflate_zlib.hip, levels 4..9): per job, position
+// arrays at pos0 (previous same-hash distance u16, the two longest-match
+// tables u32), bitmaps at bm0 (token starts S, match-table variant V, walk
+// state-A marks M; one u32 word per 32 positions each), and blocks of 16383
+// symbols at zblk0 (ZsZBlkDev), as zlib's deflate_slow + trees.c make them.
+struct ZsZBlkDev {
+  uint32_t job;
+  uint32_t last;       // BFINAL
+  uint64_t first;      // first input byte covered (== end for an empty block)
+  uint64_t end;        // one past the last byte covered
+  uint32_t nsym;       // symbols (<= 16383)
+  uint32_t type;       // 0 stored, 1 fixed, 2 dynamic (zs_zd_tree_kernel)
+  uint32_t stored_ok;  // the block's bytes still in zlib's window (_tr_flush_block's buf != NULL)
+  uint32_t hbits;      // dynamic: tree header bits after the 3 block-type bits
+  uint64_t bits;       // bits after the 3 block-type bits (stored: bytes * 8 + 32, alignment added at layout)
+  uint64_t bitoff;     // bit offset of the block in the job's stream (zs_zd_layout_kernel)
+  uint32_t lmax, dmax, blmax, pad;
 };
 
 struct ZsDSegDev {
@@ -208,7 +234,15 @@ struct ZsDSegDev {
   uint32_t nbits;      // block bits
   uint32_t ck_a;       // CRC-32 of the segment, or Adler sum a
   uint32_t ck_b;       // Adler weighted sum b (to the segment end)
-  uint32_t pad;
+  // zlib-identical mode: the segment is a 64 KiB parse region; its exit is
+  // the first loop top past it and deflate_slow's state there
+  uint32_t nsym;       // token starts in the region
+  uint32_t zs0;        // exit state of the region's own parse (entry = its start, state A)
+  uint64_t zx0;        // ... and its position
+  uint64_t zx[2];      // current exit (double-buffered across fix-up rounds)
+  uint32_t zs[2];
+  uint64_t zfix;       // tokens rewritten by fix-ups up to this position
+  uint64_t sym0;       // symbols before the region (zs_zd_blocks_kernel)
 };
 
 // ---------------------------------------------------------------------------
