@@ -399,8 +399,11 @@ def main():
 
     comp_leg = d64_leg = None
     if not args.dry_run and not args.no_compress and nloc:
+        kinds = [shard.c2_kind(i) for i in ids]
         comp_leg = compress_leg(args, zstreams, shard, torch, np, dev, dist, raws, d_out, out_ptrs, nbytes,
-                                comp_total, cpu, rank, [shard.c2_kind(i) for i in ids])
+                                comps, cpu, rank, kinds)
+        comp_leg["fast_mode"] = compress_leg(args, zstreams, shard, torch, np, dev, dist, raws, d_out, out_ptrs, nbytes,
+                                             comps, cpu, rank, kinds, fast=True)
     if not args.dry_run and not args.no_deflate64:
         d64_leg = deflate64_leg(args, zstreams, torch, np, dev, rank)
 
@@ -545,10 +548,13 @@ def deflate64_leg(args, zstreams, torch, np, dev, rank):
     return leg
 
 
-def compress_leg(args, zstreams, shard, torch, np, dev, dist, raws, d_out, raw_ptrs, nbytes, zlib_raw_total, cpu, rank,
-                 kinds):
+def compress_leg(args, zstreams, shard, torch, np, dev, dist, raws, d_out, raw_ptrs, nbytes, zlib_raws, cpu, rank,
+                 kinds, fast=False):
     """configs[2]: gzip (windowBits 31) level-L GPU deflate of the decompressed
-    streams resident in HBM, then a GPU inflate round trip of its output."""
+    streams resident in HBM, then a GPU inflate round trip of its output.
+    Default mode writes zlib's bytes (checked against the host-zlib raw streams
+    the bench inflated: the gzip body must equal them byte for byte); fast=True
+    is ZS_F_DEFLATE_FAST."""
     n = len(raw_ptrs)
     level = args.compress_level
     bound = zstreams.deflate_bound(nbytes, 31)
@@ -557,7 +563,7 @@ def compress_leg(args, zstreams, shard, torch, np, dev, dist, raws, d_out, raw_p
     cz_ptrs = [d_cz.data_ptr() + k * slot for k in range(n)]
 
     def step():
-        return zstreams.deflate_batch_device(raw_ptrs, [nbytes] * n, cz_ptrs, [bound] * n, 31, level)
+        return zstreams.deflate_batch_device(raw_ptrs, [nbytes] * n, cz_ptrs, [bound] * n, 31, level, fast=fast)
 
     for _ in range(args.warmup):
         res = step()
@@ -577,6 +583,12 @@ def compress_leg(args, zstreams, shard, torch, np, dev, dist, raws, d_out, raw_p
     zstreams.profile(False)
     sizes = [r["total_out"] for r in res]
     ok = all(r["ret"] == 1 and r["total_in"] == nbytes for r in res)
+    identical = None
+    if not fast and level == 6:
+        cz_host = d_cz.cpu().numpy()
+        identical = all(sizes[k] == len(zlib_raws[k]) + 18 and
+                        np.array_equal(cz_host[k * slot + 10:k * slot + sizes[k] - 8], zlib_raws[k]) for k in range(n))
+        del cz_host
     # round trip: GPU inflate of the GPU gzip streams into the zeroed raw buffers
     d_out.zero_()
     back = zstreams.inflate_batch_device(cz_ptrs, sizes, raw_ptrs, [nbytes] * n, 31)
@@ -587,26 +599,29 @@ def compress_leg(args, zstreams, shard, torch, np, dev, dist, raws, d_out, raw_p
     out_host = d_out.cpu().numpy().reshape(n, nbytes)
     ok = ok and all(np.array_equal(out_host[k], raws[k]) for k in range(n))
     del out_host
-    log(f"[rank {rank}] GPU gzip L{level}: {sum(sizes)} bytes, round trip ok: {ok}")
+    log(f"[rank {rank}] GPU gzip L{level} ({'fast' if fast else 'zlib bytes'}): {sum(sizes)} bytes, round trip ok: {ok}, "
+        f"identical to zlib: {identical}")
     t_el, in_bytes, ok = shard.reduce_counters(t_el, n * nbytes * args.steps, ok, device=dev)
     comp_total = sum(sizes)
-    zlib_total = zlib_raw_total + 18 * n  # host zlib L6 raw streams + gzip wrapper
+    zlib_total = sum(len(c) for c in zlib_raws) + 18 * n  # host zlib L6 raw streams + gzip wrapper
     k_avg_s = (k_ms / max(k_n, 1)) / 1e3
     alg = n * nbytes + comp_total
     achieved = alg / k_avg_s / 1e9 if k_avg_s > 0 else 0.0
     value = in_bytes / t_el / 2**20
     leg = {"metric": "MiB/s compressed (input bytes), gzip level %d" % level,
+           "mode": "fast (ZS_F_DEFLATE_FAST: GPU block structure)" if fast else "zlib bytes (deflate_slow + trees.c identical)",
            "value": round(value, 1), "unit": "MiB/s", "ms_per_step": round(t_el * 1e3 / args.steps, 3),
            "workload": f"{n}x{nbytes >> 20}MiB gzip (windowBits 31) level {level} deflate on rank 0, inputs resident in HBM",
            "compressed_bytes": comp_total, "ratio": round(n * nbytes / comp_total, 3),
            "zlib_l6_bytes": zlib_total, "size_vs_zlib_l6": round(comp_total / zlib_total, 4),
+           "bytes_identical_to_zlib": identical,
            "roundtrip_verified": ok, "roundtrip_path_stats": rt_stats,
            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(achieved / HBM_PEAK_GBS, 5), "kernel": "deflate pipeline",
                         "kernel_ms_avg": round(k_avg_s * 1e3, 3), "alg_bytes_per_launch": alg,
                         "stages_ms_avg": {k: round(v / max(k_n, 1), 3) for k, v in stages.items()},
-                        "stage_kernels": zstreams.DEFLATE_STAGE_KERNELS}}
-    if rank == 0 and not args.no_cpu_baseline:
+                        "stage_kernels": zstreams.DEFLATE_STAGE_KERNELS if fast else zstreams.ZDEFLATE_STAGE_KERNELS}}
+    if rank == 0 and not args.no_cpu_baseline and not fast:
         z = [k for k in range(n) if kinds[k] == "zipf"]
         li = [k for k in range(n) if kinds[k] == "lines"]
         sample = (z[:2] + li[:2]) or [0]

@@ -1,13 +1,17 @@
 """GPU deflate (LZ77 match-find + Huffman emission)
 through the C-ABI.
 
-Bar: every GPU stream is valid deflate that the
-CPU oracle (and, independently, host zlib 1.2.11) inflates to the input, with
-Z_STREAM_END, the whole stream consumed and the wrapper check value matching.
-The wrapper bytes (zlib CMF/FLG, gzip header) are pinned against host zlib's
-deflate, which is byte-identical to the reference's.  The
-compressed body is not zlib's bytes (no sequential hash chains): its size is
-reported against zlib at the same level, and bounded.
+Bar, levels 4..9 (the reference's deflate_slow levels; level 6 is
+Z_DEFAULT_COMPRESSION): the GPU writes zlib's bytes -- the exact stream host
+zlib 1.2.11 writes for deflateInit2(level, Z_DEFLATED, window_bits, 8,
+Z_DEFAULT_STRATEGY) + deflate(Z_FINISH), which SURVEY.md §8c pins as
+byte-identical to the reference's shipped deflate.  Every stream also
+inflates back through the CPU oracle and host zlib.
+
+Levels 0..3 and ZS_F_DEFLATE_FAST (the throughput path): every GPU stream is
+valid deflate that the oracle and host zlib inflate to the input, with
+Z_STREAM_END, the whole stream consumed, the wrapper bytes and check value as
+zlib writes them; its size is bounded against zlib at the same level.
 """
 import ctypes
 import random
@@ -37,8 +41,16 @@ def expected_check(data, wbits):
     return 1  # raw: strm->adler keeps adler32(0) (deflateResetKeep)
 
 
-def check_stream(data, wbits, level, comp, info):
+def zlib_bytes(data, wbits, level):
+    c = zlib.compressobj(level, zlib.DEFLATED, wbits, 8, zlib.Z_DEFAULT_STRATEGY)
+    return c.compress(data) + c.flush()
+
+
+def check_stream(data, wbits, level, comp, info, fast=False):
     assert info["ret"] == 1, info
+    if 4 <= level <= 9 and not fast:
+        ref = zlib_bytes(data, wbits, level)
+        assert comp == ref, ("not zlib's bytes", len(data), wbits, level, len(comp), len(ref))
     assert info["total_in"] == len(data) and info["total_out"] == len(comp), info
     assert info["adler"] == expected_check(data, wbits), info
     # zlib turns deflate windowBits 8 into 9 and writes CINFO 1, which an
@@ -108,12 +120,51 @@ def test_deflate_small_out_cap(zs):
     assert info["ret"] == 0 and info["total_out"] == 1000 and part == full[:1000]
 
 
+def test_deflate_zlib_bytes_levels_4_to_9(zs):
+    """Every deflate_slow level, every wrapper, the corpora and edge sizes:
+    byte-identical to host zlib (long matches, stored blocks, block ends at
+    16383 symbols, the empty final block, windows below 32 KiB)."""
+    rng = random.Random(11)
+    pats = _patterns(rng)
+    cases = []
+    for name, p in pats.items():
+        for n in (0, 1, 3, 300, 16383, 16384, 65536, 70000, 200000):
+            if n <= len(p):
+                for lv in (4, 5, 6, 7, 8, 9):
+                    cases.append((p[:n], rng.choice((-15, 15, 31)), lv))
+    # all-literal stretches whose symbol count ends exactly on a block boundary
+    for extra in (-2, -1, 0, 1, 2):
+        rnd = bytes(rng.getrandbits(8) for _ in range(2 * 16383 + extra))
+        cases.append((rnd, -15, 6))
+    for wb in (-9, -10, -13, 9, 12, 25, 29):
+        cases.append((pats["text"][:150000], wb, 6))
+    got = zs.deflate_batch([c[0] for c in cases], [c[1] for c in cases], [c[2] for c in cases])
+    bad = [(i, len(d), wb, lv) for i, ((d, wb, lv), (comp, info)) in enumerate(zip(cases, got))
+           if comp != zlib_bytes(d, wb, lv) or info["ret"] != 1]
+    assert not bad, bad[:8]
+
+
+def test_deflate_zlib_bytes_large_c3_shape(zs):
+    """configs[2] shape at 16 MiB per stream: gzip L6, one Zipf-text and one
+    line-text stream, byte-identical to host zlib (window slides, thousands of
+    blocks), and inflated back by the GPU."""
+    datas = [corpus.stream(0, 16 << 20), corpus.stream(32, 16 << 20)]
+    got = zs.deflate_batch(datas, 31, 6)
+    for d, (comp, info) in zip(datas, got):
+        assert info["ret"] == 1 and info["adler"] == zlib.crc32(d)
+        assert comp == zlib_bytes(d, 31, 6)
+    back = zs.inflate_batch([g[0] for g in got], 31, [len(d) for d in datas])
+    for d, (out, info) in zip(datas, back):
+        assert info["ret"] == 1 and out == d
+
+
 def test_deflate_large_corpus_ratio_and_gpu_roundtrip(zs):
-    """C3 shape at reduced size: gzip L6 GPU compress -> oracle + GPU inflate."""
+    """C3 shape at reduced size, fast mode (ZS_F_DEFLATE_FAST): gzip L6 GPU
+    compress -> oracle + GPU inflate, size within 25% of zlib L6."""
     raws, _ = corpus.batch(0, 4, 8 << 20, compress=False)
     raws += corpus.batch(32, 2, 8 << 20, compress=False)[0]
     datas = [r.tobytes() for r in raws]
-    got = zs.deflate_batch(datas, 31, 6)
+    got = zs.deflate_batch(datas, 31, 6, fast=True)
     comps = [g[0] for g in got]
     for d, (comp, info) in zip(datas, got):
         assert info["ret"] == 1 and info["adler"] == zlib.crc32(d)
@@ -129,8 +180,20 @@ def test_deflate_large_corpus_ratio_and_gpu_roundtrip(zs):
 
 def test_deflate_deterministic(zs):
     data = corpus.stream(9, 1 << 20)
-    a = zs.deflate_batch([data] * 3, -15, 6)
-    assert a[0][0] == a[1][0] == a[2][0]
+    for fast in (False, True):
+        a = zs.deflate_batch([data] * 3, -15, 6, fast=fast)
+        assert a[0][0] == a[1][0] == a[2][0]
+
+
+def test_deflate_fast_mode_all_levels(zs):
+    """ZS_F_DEFLATE_FAST at every level: valid streams (property bar)."""
+    rng = random.Random(5)
+    pats = _patterns(rng)
+    cases = [(p[:n], wb, lv) for p in pats.values() for n in (0, 5, 65537, 200000) if n <= len(p)
+             for wb in (-15, 31) for lv in (4, 6, 9)]
+    got = zs.deflate_batch([c[0] for c in cases], [c[1] for c in cases], [c[2] for c in cases], fast=True)
+    for (d, wb, lv), (comp, info) in zip(cases, got):
+        check_stream(d, wb, lv, comp, info, fast=True)
 
 
 def test_compression_stream_js_schedule(zs):

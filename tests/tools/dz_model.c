@@ -429,7 +429,8 @@ static uint32_t slides_at(uint32_t t, uint32_t L, uint32_t wsize, uint32_t max_d
   for (;;) {
     const uint64_t base = (uint64_t)k * wsize;
     const uint64_t wend = base + 2ull * wsize < L ? base + 2ull * wsize : L;
-    if (wend - t < LOOKAHEAD_MIN && t - base >= wsize + max_dist) k++;
+    const uint64_t look = wend > t ? wend - t : 0;
+    if (t >= base && look < LOOKAHEAD_MIN && t - base >= wsize + max_dist) k++;
     else return k;
   }
 }

@@ -1175,8 +1175,8 @@ extern "C" int zs_launch_zdeflate(ZsDJobDev *d_jobs, uint32_t njobs, ZsDSegDev *
                                   uint32_t nblk_slots, const uint32_t *d_slot_job, uint32_t *d_aux, uint8_t *d_stage,
                                   uint32_t *d_flag, hipStream_t st, hipEvent_t *ev) {
   if (ev) (void)hipEventRecord(ev[0], st);
-  hipLaunchKernelGGL(zs_zd_prev_kernel, dim3(n1), dim3(WAVE), 0, st, d_jobs, d_w1, d_prevd);
-  hipLaunchKernelGGL(zs_zd_match_kernel, dim3(n2), dim3(ZD_MT), 0, st, d_jobs, d_w2, d_prevd, d_ma, d_mb);
+  if (n1) hipLaunchKernelGGL(zs_zd_prev_kernel, dim3(n1), dim3(WAVE), 0, st, d_jobs, d_w1, d_prevd);
+  if (n2) hipLaunchKernelGGL(zs_zd_match_kernel, dim3(n2), dim3(ZD_MT), 0, st, d_jobs, d_w2, d_prevd, d_ma, d_mb);
   if (ev) (void)hipEventRecord(ev[1], st);
   hipLaunchKernelGGL(zs_zd_parse_kernel, dim3(nseg), dim3(ZD_PT), 0, st, d_jobs, d_segs, d_ma, d_mb, d_bm);
   uint32_t cur = 0;

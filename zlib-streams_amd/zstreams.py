@@ -31,6 +31,7 @@ Z_STREAM_ERROR, Z_DATA_ERROR, Z_MEM_ERROR, Z_BUF_ERROR = -2, -3, -4, -5
 Z_NO_FLUSH, Z_FINISH = 0, 4
 ZS_F_DEVICE = 1
 ZS_F_CRC32 = 2  # raw / copy jobs: CRC-32 of the output in "adler" (ZIP entries)
+ZS_F_DEFLATE_FAST = 4  # deflate levels 4..9: the throughput path instead of zlib's bytes
 ZS_JOB_INFLATE, ZS_JOB_COPY = 0, 1
 
 # windowBits per format, as the reference's init functions choose them
@@ -260,11 +261,13 @@ def deflate_bound(n, window_bits=-15):
     return int(lib().zs_deflate_bound(n, window_bits))
 
 
-def deflate_batch(streams, window_bits=-15, level=-1, out_caps=None):
+def deflate_batch(streams, window_bits=-15, level=-1, out_caps=None, fast=False):
     """Deflate many whole buffers on the GPU (host buffers).
 
     Each job behaves like deflateInit2(level, Z_DEFLATED, window_bits, 8,
-    Z_DEFAULT_STRATEGY) + one deflate(Z_FINISH).  Returns [(bytes, result_dict)].
+    Z_DEFAULT_STRATEGY) + one deflate(Z_FINISH).  Levels 4..9 write zlib's bytes
+    (unless fast=True: ZS_F_DEFLATE_FAST, the throughput path with its own block
+    structure).  Returns [(bytes, result_dict)].
     """
     n = len(streams)
     wbs = window_bits if isinstance(window_bits, (list, tuple)) else [window_bits] * n
@@ -285,11 +288,11 @@ def deflate_batch(streams, window_bits=-15, level=-1, out_caps=None):
         jobs[i].out_cap = out_caps[i]
         jobs[i].window_bits = wbs[i]
         jobs[i].level = lvs[i]
-    _check(lib().zs_deflate_batch(jobs, n, res, 0))
+    _check(lib().zs_deflate_batch(jobs, n, res, ZS_F_DEFLATE_FAST if fast else 0))
     return [(outbufs[i].raw[:res[i].total_out], res[i].as_dict()) for i in range(n)]
 
 
-def deflate_batch_device(in_ptrs, in_lens, out_ptrs, out_caps, window_bits, level=-1):
+def deflate_batch_device(in_ptrs, in_lens, out_ptrs, out_caps, window_bits, level=-1, fast=False):
     """Deflate buffers already resident in HBM (device pointers)."""
     n = len(in_ptrs)
     jobs = (ZsDJob * n)()
@@ -301,7 +304,7 @@ def deflate_batch_device(in_ptrs, in_lens, out_ptrs, out_caps, window_bits, leve
         jobs[i].out_cap = out_caps[i]
         jobs[i].window_bits = window_bits[i] if isinstance(window_bits, (list, tuple)) else window_bits
         jobs[i].level = level[i] if isinstance(level, (list, tuple)) else level
-    _check(lib().zs_deflate_batch(jobs, n, res, ZS_F_DEVICE))
+    _check(lib().zs_deflate_batch(jobs, n, res, ZS_F_DEVICE | (ZS_F_DEFLATE_FAST if fast else 0)))
     return [res[i].as_dict() for i in range(n)]
 
 
@@ -309,6 +312,10 @@ DEFLATE_STAGES = ("match", "parse", "blocks", "stitch")
 DEFLATE_STAGE_KERNELS = {"match": "zs_dz_match_kernel", "parse": "zs_dz_parse_kernel",
                          "blocks": "zs_dz_block_kernel + zs_dz_check_kernel",
                          "stitch": "zs_dz_offsets_kernel + zs_dz_stitch_kernel + zs_dz_trailer_kernel"}
+ZDEFLATE_STAGE_KERNELS = {"match": "zs_zd_prev_kernel + zs_zd_match_kernel",
+                          "parse": "zs_zd_parse_kernel + zs_zd_fix_kernel rounds",
+                          "blocks": "zs_zd_count/blocks/blist/tree/layout/emit kernels",
+                          "stitch": "zs_dz_trailer_kernel"}
 
 
 def profile_deflate():
