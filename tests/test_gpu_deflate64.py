@@ -69,3 +69,22 @@ def test_deflate64_reaches_64k_back(zs):
     assert len(c64) < 0.4 * len(c15), (len(c64), len(c15))
     out, oi = _inflate64(c64, len(data))
     assert oi["ret"] == 1 and out == data
+
+
+def test_deflate64_chunked_block_parallel(zs):
+    """Large deflate64 streams take the block-parallel path (64 KiB history
+    windows, 32 distance codes, code-285 copies split into tokens) with no
+    serial fallback, and match the oracle at windowBits -16 (the reference's
+    inflate9 semantics, src/inflate.c:1037-1193, inftrees.c:73-87)."""
+    import numpy as np
+    rng = np.random.default_rng(9)
+    blk = rng.integers(0, 256, 40000, dtype=np.uint8).tobytes()
+    datas = [corpus.stream(3, 24 << 20),
+             corpus.stream(35, 12 << 20) + bytes(3 << 20) + blk * 40 + corpus.stream(4, 2 << 20)]
+    comps = [c for c, _ in zs.deflate_batch(datas, -16, 6)]
+    got = zs.inflate_batch(comps, -16, [len(d) for d in datas])
+    st = zs.last_stats()
+    for d, c, (out, info) in zip(datas, comps, got):
+        eo, ei = O.oneshot(c, -16, len(d))
+        assert info == ei and info["ret"] == 1 and out == eo == d, (info, ei)
+    assert st["chunked_jobs"] == 2 and st["fallback_jobs"] == 0 and st["units"] > 100, st

@@ -41,6 +41,7 @@ __device__ unsigned long long g_kprof_ck[16];  // KP_L_* - 48
 // (complete code-length code, repeat rules, end-of-block present, literal and
 // distance codes complete or a single 1-bit code, empty distance code allowed).
 // ---------------------------------------------------------------------------
+template <bool D64>
 __device__ bool validate_header(const uint32_t *w, uint32_t end_byte, uint32_t bit, uint8_t *lut) {
   const uint32_t limit = end_byte * 8u;
   uint32_t wi = bit >> 5;
@@ -62,7 +63,7 @@ __device__ bool validate_header(const uint32_t *w, uint32_t end_byte, uint32_t b
   const uint32_t ncode = (uint32_t)((hold >> 10) & 15) + 4;
   hold >>= 14;
   n -= 14;
-  if (nlen > 286 || ndist > 30) return false;
+  if (nlen > 286 || ndist > (D64 ? 32u : 30u)) return false;
   uint8_t cl[19];
 #pragma unroll
   for (int i = 0; i < 19; i++) cl[i] = 0;
@@ -149,6 +150,7 @@ __device__ bool validate_header(const uint32_t *w, uint32_t end_byte, uint32_t b
   if (eob == 0) return false;
   if (lk > 32768u || (lk < 32768u && lmax != 1)) return false;
   if (dn && (dk > 32768u || (dk < 32768u && dmax != 1))) return false;
+  if (D64 && dn == 0) return false;  // deflate64 rejects an empty distance code (src/inftrees.c:131-132)
   return true;
 }
 
@@ -197,6 +199,7 @@ __device__ __forceinline__ bool cl_complete(const uint32_t *st, uint32_t base, u
   return kraft == 128u;
 }
 
+template <bool D64>
 __global__ void __launch_bounds__(64) zs_find_kernel(const ZsJobDev *__restrict__ jobs, const ZsHeadDev *__restrict__ heads,
                                                       ZsSegDev *__restrict__ segs) {
   __shared__ uint8_t s_lut[WAVE][128];
@@ -244,7 +247,8 @@ __global__ void __launch_bounds__(64) zs_find_kernel(const ZsJobDev *__restrict_
         // (not bits p+9..p+12 all set)
         const uint64_t bt = ~(x >> 1) & (x >> 2);
         const uint64_t hlit_bad = (x >> 4) & (x >> 5) & (x >> 6) & (x >> 7);
-        const uint64_t hdist_bad = (x >> 9) & (x >> 10) & (x >> 11) & (x >> 12);
+        // (deflate64 allows HDIST 30 and 31: 32 distance codes)
+        const uint64_t hdist_bad = D64 ? 0ull : (x >> 9) & (x >> 10) & (x >> 11) & (x >> 12);
         cand = (uint32_t)((seg.final_ok ? bt : (bt & ~x)) & ~hlit_bad & ~hdist_bad);
         if (b0 < lo) cand &= ~0u << (lo - b0);
         if (hi - b0 < 32u) cand &= (1u << (hi - b0)) - 1u;
@@ -279,7 +283,7 @@ __global__ void __launch_bounds__(64) zs_find_kernel(const ZsJobDev *__restrict_
         bool ok = false;
         if (lane < take) {
           cb = s_v[(vh + lane) & (FQ - 1)];
-          ok = validate_header(w, end_byte, cb, s_lut[lane]);
+          ok = validate_header<D64>(w, end_byte, cb, s_lut[lane]);
         }
         uint64_t m = __ballot(ok);
         while (m && nfound < SEG_SLOTS) {
@@ -598,7 +602,9 @@ __global__ void __launch_bounds__(PLAN_T) zs_plan_kernel(const ZsJobDev *__restr
 // ---------------------------------------------------------------------------
 // Fixed tables (src/inflate.c:260-298) built once into global memory.
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(64) zs_fixed_tables_kernel(uint32_t *__restrict__ fixed) {
+// (d64: the deflate64 set -- length code 285 = 3 + 16 extra bits, distance
+// codes 30 and 31 valid, src/inftrees.c:73-87)
+__global__ void __launch_bounds__(64) zs_fixed_tables_kernel(uint32_t *__restrict__ fixed, int d64) {
   __shared__ uint32_t s_tab[544];
   __shared__ uint16_t s_lens[320];
   __shared__ uint16_t s_sorted[320];
@@ -607,11 +613,11 @@ __global__ void __launch_bounds__(64) zs_fixed_tables_kernel(uint32_t *__restric
   for (uint32_t s = lane; s < 288; s += WAVE) s_lens[s] = s < 144 ? 8 : (s < 256 ? 9 : (s < 280 ? 7 : 8));
   __builtin_amdgcn_wave_barrier();
   uint32_t r = 9;
-  build_table(T_LENS, s_lens, 288, s_tab, &r, s_sorted, s_scr, 0);
+  build_table(T_LENS, s_lens, 288, s_tab, &r, s_sorted, s_scr, d64);
   for (uint32_t s = lane; s < 32; s += WAVE) s_lens[s] = 5;
   __builtin_amdgcn_wave_barrier();
   r = 5;
-  build_table(T_DISTS, s_lens, 32, s_tab + 512, &r, s_sorted, s_scr, 0);
+  build_table(T_DISTS, s_lens, 32, s_tab + 512, &r, s_sorted, s_scr, d64);
   for (uint32_t i = lane; i < 544; i += WAVE) fixed[i] = s_tab[i];
 }
 
@@ -693,13 +699,13 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_chain_kernel(const ZsJobDev *
         break;
       }
       ZsLinkInfo li;
-      li.scratch = cj.scratch0 + spos;
+      li.scratch = cj.scratch0 + (uint64_t)cj.esz * spos;
       li.n_out = ch.n_out;
       li.unit = c;
       info[u0 + len] = li;
       len++;
       chunks[c].out_off = total;
-      chunks[c].scratch = cj.scratch0 + spos;
+      chunks[c].scratch = li.scratch;
       total += ch.n_out;
       spos += ch.n_out;
       if (code == ZD_END) {
@@ -745,14 +751,15 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_chain_kernel(const ZsJobDev *
 // ---------------------------------------------------------------------------
 // thread t owns window entries 4t + 4096 g + {0..3}, g < LINK_PER / 4; entry
 // pairs are packed in u32 (2 per word, 2 words per group)
-#define LINK_G (LINK_PER / 4)
+template <uint32_t HN>
 __device__ __forceinline__ void link_load(const uint16_t *__restrict__ scratch, const ZsLinkInfo &li, uint32_t t,
-                                          uint2 (&v)[LINK_G]) {
+                                          uint2 (&v)[HN / LINK_THREADS / 4]) {
+  constexpr int LINK_G = HN / LINK_THREADS / 4;
   const uint32_t n = li.n_out;
-  if (n >= HIST) {
+  if (n >= HN) {
     // entries of a chain member start at any entry index: two aligned 8-byte
     // loads and a funnel shift give the thread's 4 entries
-    const uint64_t b = li.scratch + n - HIST;
+    const uint64_t b = li.scratch + n - HN;
     const uint32_t m = (uint32_t)(b & 3u);
     const uint2 *al = reinterpret_cast<const uint2 *>(scratch + (b - m));
 #pragma unroll
@@ -768,22 +775,25 @@ __device__ __forceinline__ void link_load(const uint16_t *__restrict__ scratch, 
         v[g] = make_uint2((uint32_t)r, (uint32_t)(r >> 32));
       }
     }
-  } else {  // short unit: entry i exists only for i >= HIST - n
+  } else {  // short unit: entry i exists only for i >= HN - n
     const uint16_t *e = scratch + li.scratch;
 #pragma unroll
     for (int g = 0; g < LINK_G; g++) {
       const uint32_t i = (uint32_t)g * (LINK_THREADS * 4) + t * 4;
       uint16_t x[4];
-      for (int k = 0; k < 4; k++) x[k] = (i + k + n >= HIST) ? e[i + k + n - HIST] : (uint16_t)0;
+      for (int k = 0; k < 4; k++) x[k] = (i + k + n >= HN) ? e[i + k + n - HN] : (uint16_t)0;
       __builtin_memcpy(&v[g], x, 8);
     }
   }
 }
 
+template <uint32_t HN>
 __global__ void __launch_bounds__(LINK_THREADS) zs_link_kernel(const ZsJobDev *__restrict__ jobs, ZsCJobDev *__restrict__ cjobs,
                                                                const uint16_t *__restrict__ scratch, uint8_t *__restrict__ windows,
                                                                const ZsLinkInfo *__restrict__ info, uint32_t *__restrict__ fallback) {
-  __shared__ uint8_t s_win[2][HIST];
+  constexpr int LINK_G = HN / LINK_THREADS / 4;
+  constexpr uint32_t MB = HN == 65536u ? 0u : MARK_BASE;  // marker of history byte w: MB + w (deflate64: w)
+  __shared__ uint8_t s_win[2][HN];
   __shared__ uint32_t s_bad;
   const uint32_t t = threadIdx.x;
   const ZsCJobDev cj = cjobs[blockIdx.x];
@@ -797,19 +807,19 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_link_kernel(const ZsJobDev *_
   uint32_t kmark = 0;
 #endif
   if (t == 0) s_bad = 0;
-  // W holds the last HIST bytes before unit c
+  // W holds the last HN bytes before unit c
   uint32_t wv = 0;  // valid bytes of history
   int cur = 0;
   uint2 v[LINK_G], vn[LINK_G];
   ZsLinkInfo li = info[u0];
-  link_load(scratch, li, t, v);
+  link_load<HN>(scratch, li, t, v);
   ZsLinkInfo lin = len > 1 ? info[u0 + 1] : li;
   bool bad = false;
   for (uint32_t j = 0; j < len; j++) {
     // next member's entries (and the one after's descriptor) in flight now
     ZsLinkInfo li2 = lin;
     if (j + 1 < len) {
-      link_load(scratch, lin, t, vn);
+      link_load<HN>(scratch, lin, t, vn);
       if (j + 2 < len) li2 = info[u0 + j + 2];
     }
     const uint32_t c = li.unit;
@@ -819,8 +829,8 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_link_kernel(const ZsJobDev *_
     const uint64_t ka = KP_NOW();
 #endif
     if (j != 0) {
-      uint8_t *g = windows + (size_t)c * HIST;
-      for (uint32_t i = t * 16; i < HIST; i += LINK_THREADS * 16)
+      uint8_t *g = windows + (size_t)c * HN;
+      for (uint32_t i = t * 16; i < HN; i += LINK_THREADS * 16)
         *reinterpret_cast<uint4 *>(g + i) = *reinterpret_cast<const uint4 *>(W + i);
     }
 #if KP_ON
@@ -828,8 +838,8 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_link_kernel(const ZsJobDev *_
     kt_ww += kb - ka;
 #endif
     const uint32_t n = li.n_out;
-    const uint32_t keep = n < HIST ? HIST - n : 0u;  // old history bytes still inside the new window
-    const uint32_t lowest = HIST - wv;                // first valid history index
+    const uint32_t keep = n < HN ? HN - n : 0u;  // old history bytes still inside the new window
+    const uint32_t lowest = HN - wv;                // first valid history index
     if (keep == 0 && lowest == 0) {
       // common case (full window, unit >= 32 KiB): branch-free gather, every
       // entry reads the window and selects literal or history byte
@@ -837,8 +847,8 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_link_kernel(const ZsJobDev *_
       for (int g = 0; g < LINK_G; g++) {
         const uint32_t i = (uint32_t)g * (LINK_THREADS * 4) + t * 4;
         const uint32_t x0 = v[g].x & 0xffffu, x1 = v[g].x >> 16, x2 = v[g].y & 0xffffu, x3 = v[g].y >> 16;
-        const uint32_t r0 = W[(x0 - MARK_BASE) & (HIST - 1)], r1 = W[(x1 - MARK_BASE) & (HIST - 1)];
-        const uint32_t r2 = W[(x2 - MARK_BASE) & (HIST - 1)], r3 = W[(x3 - MARK_BASE) & (HIST - 1)];
+        const uint32_t r0 = W[(x0 - MB) & (HN - 1)], r1 = W[(x1 - MB) & (HN - 1)];
+        const uint32_t r2 = W[(x2 - MB) & (HN - 1)], r3 = W[(x3 - MB) & (HN - 1)];
         const uint32_t b0 = x0 < MARK_BASE ? x0 : r0, b1 = x1 < MARK_BASE ? x1 : r1;
         const uint32_t b2 = x2 < MARK_BASE ? x2 : r2, b3 = x3 < MARK_BASE ? x3 : r3;
         *reinterpret_cast<uint32_t *>(W2 + i) = b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
@@ -860,15 +870,15 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_link_kernel(const ZsJobDev *_
           } else if (x < MARK_BASE) {
             b = x;
           } else {
-            const uint32_t wx = x - MARK_BASE;
+            const uint32_t wx = x - MB;
             bad |= wx < lowest;  // reaches before the stream start
-            b = W[wx & (HIST - 1)];
+            b = W[wx & (HN - 1)];
           }
           W2[i] = (uint8_t)b;
         }
       }
     }
-    wv = min(HIST, wv + n);
+    wv = min(HN, wv + n);
     cur ^= 1;
 #if KP_ON
     const uint64_t kc = KP_NOW();
@@ -908,17 +918,19 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_link_kernel(const ZsJobDev *_
 // Emit: u16 entries -> final bytes (one workgroup per chunk)
 // ---------------------------------------------------------------------------
 #define EMIT_THREADS 256
+template <uint32_t HN>
 __global__ void __launch_bounds__(EMIT_THREADS) zs_emit_kernel(const ZsJobDev *__restrict__ jobs, const ZsChunkDev *__restrict__ chunks,
                                                                const uint16_t *__restrict__ scratch, const uint8_t *__restrict__ windows,
                                                                const uint32_t *__restrict__ fallback) {
-  __shared__ uint8_t s_w[HIST];
+  constexpr uint32_t MB = HN == 65536u ? 0u : MARK_BASE;
+  __shared__ uint8_t s_w[HN];
   const uint32_t c = blockIdx.x;
   const uint32_t t = threadIdx.x;
   const ZsChunkDev ch = chunks[c];
   if (!ch.in_chain || fallback[ch.job]) return;
   if (ch.ord != 0) {
-    const uint8_t *g = windows + (size_t)c * HIST;
-    for (uint32_t i = t * 16; i < HIST; i += EMIT_THREADS * 16)
+    const uint8_t *g = windows + (size_t)c * HN;
+    for (uint32_t i = t * 16; i < HN; i += EMIT_THREADS * 16)
       *reinterpret_cast<uint4 *>(s_w + i) = *reinterpret_cast<const uint4 *>(g + i);
     __syncthreads();
   }
@@ -941,7 +953,7 @@ __global__ void __launch_bounds__(EMIT_THREADS) zs_emit_kernel(const ZsJobDev *_
 #pragma unroll
       for (int k = 0; k < 16; k++) {
         const uint32_t v = (w[k >> 1] >> (16 * (k & 1))) & 0xffffu;
-        b[k] = v < MARK_BASE ? v : s_w[v - MARK_BASE];
+        b[k] = v < MARK_BASE ? v : s_w[v - MB];
       }
       uint4 o;
       o.x = b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
@@ -954,49 +966,143 @@ __global__ void __launch_bounds__(EMIT_THREADS) zs_emit_kernel(const ZsJobDev *_
         const int32_t i = i0 + k;
         if (i < 0 || (uint32_t)i >= n) continue;
         const uint32_t v = e[i];
-        out[i] = (uint8_t)(v < MARK_BASE ? v : s_w[v - MARK_BASE]);
+        out[i] = (uint8_t)(v < MARK_BASE ? v : s_w[v - MB]);
       }
     }
   }
 }
 
 // ---------------------------------------------------------------------------
+// Deflate64 link and emit: 64 KiB windows, 17-bit entries stored as u32
+// (literal byte, or 256 + w for byte w of the unit's 64 KiB history).
+// ---------------------------------------------------------------------------
+#define H64 65536u
+__global__ void __launch_bounds__(LINK_THREADS) zs_link64_kernel(ZsCJobDev *__restrict__ cjobs, const uint16_t *__restrict__ scratch,
+                                                                 uint8_t *__restrict__ windows, const ZsLinkInfo *__restrict__ info,
+                                                                 uint32_t *__restrict__ fallback) {
+  __shared__ uint8_t s_win[2][H64];
+  __shared__ uint32_t s_bad;
+  const uint32_t t = threadIdx.x;
+  const ZsCJobDev cj = cjobs[blockIdx.x];
+  if (!cj.ok) return;
+  if (t == 0) s_bad = 0;
+  uint32_t wv = 0;
+  int cur = 0;
+  bool bad = false;
+  for (uint32_t j = 0; j < cj.nchain; j++) {
+    const ZsLinkInfo li = info[cj.unit0 + j];
+    const uint32_t *E = reinterpret_cast<const uint32_t *>(scratch + li.scratch);
+    const uint32_t n = li.n_out;
+    uint8_t *W = s_win[cur];
+    uint8_t *W2 = s_win[cur ^ 1];
+    if (j != 0) {
+      uint8_t *g = windows + (size_t)li.unit * H64;
+      for (uint32_t i = t * 16; i < H64; i += LINK_THREADS * 16)
+        *reinterpret_cast<uint4 *>(g + i) = *reinterpret_cast<const uint4 *>(W + i);
+    }
+    const uint32_t keep = n < H64 ? H64 - n : 0u;
+    const uint32_t lowest = H64 - wv;
+    for (uint32_t i = t; i < H64; i += LINK_THREADS) {
+      uint32_t b;
+      if (i < keep) {
+        b = W[i + n];
+      } else {
+        const uint32_t x = E[i + n - H64];
+        if (x < MARK_BASE) {
+          b = x;
+        } else {
+          const uint32_t wx = x - MARK_BASE;
+          bad |= wx < lowest;
+          b = W[wx & (H64 - 1)];
+        }
+      }
+      W2[i] = (uint8_t)b;
+    }
+    wv = min(H64, wv + n);
+    cur ^= 1;
+    __syncthreads();
+  }
+  if (bad) s_bad = 1;
+  __syncthreads();
+  if (t == 0 && s_bad) {
+    fallback[cj.job] = 1;
+    cjobs[blockIdx.x].ok = 0;
+  }
+}
+
+__global__ void __launch_bounds__(EMIT_THREADS) zs_emit64_kernel(const ZsJobDev *__restrict__ jobs, const ZsChunkDev *__restrict__ chunks,
+                                                                 const uint16_t *__restrict__ scratch, const uint8_t *__restrict__ windows,
+                                                                 const uint32_t *__restrict__ fallback) {
+  __shared__ uint8_t s_w[H64];
+  const uint32_t c = blockIdx.x;
+  const uint32_t t = threadIdx.x;
+  const ZsChunkDev ch = chunks[c];
+  if (!ch.in_chain || fallback[ch.job]) return;
+  if (ch.ord != 0) {
+    const uint8_t *g = windows + (size_t)c * H64;
+    for (uint32_t i = t * 16; i < H64; i += EMIT_THREADS * 16)
+      *reinterpret_cast<uint4 *>(s_w + i) = *reinterpret_cast<const uint4 *>(g + i);
+    __syncthreads();
+  }
+  uint8_t *out = jobs[ch.job].out + ch.out_off;
+  const uint32_t *e = reinterpret_cast<const uint32_t *>(scratch + ch.scratch);
+  const uint32_t n = ch.n_out;
+  for (uint32_t i = t; i < n; i += EMIT_THREADS) {
+    const uint32_t v = e[i];
+    out[i] = (uint8_t)(v < MARK_BASE ? v : s_w[(v - MARK_BASE) & (H64 - 1)]);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // host launch helpers
 // ---------------------------------------------------------------------------
-extern "C" void zs_launch_fixed_tables(uint32_t *fixed, hipStream_t st) {
-  hipLaunchKernelGGL(zs_fixed_tables_kernel, dim3(1), dim3(64), 0, st, fixed);
+extern "C" void zs_launch_fixed_tables(uint32_t *fixed, int d64, hipStream_t st) {
+  hipLaunchKernelGGL(zs_fixed_tables_kernel, dim3(1), dim3(64), 0, st, fixed, d64);
 }
 
 extern "C" void zs_launch_parse(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, ZsChunkDev *d_chunks, uint32_t nchunks,
-                                uint32_t *d_tokens, uint32_t *d_tables, const uint32_t *d_fixed, ZsTokPool pool,
+                                uint32_t *d_tokens, uint32_t *d_tables, const uint32_t *d_fixed, ZsTokPool pool, int d64,
                                 hipStream_t st);
 extern "C" void zs_launch_expand(const ZsJobDev *d_jobs, ZsChunkDev *d_chunks, uint32_t nchunks, uint16_t *d_scratch,
-                                 const uint32_t *d_tokens, ZsTokPool pool, hipStream_t st);
+                                 const uint32_t *d_tokens, ZsTokPool pool, uint32_t *d_fallback, int d64, hipStream_t st);
 
+// One group of chunked jobs, all raw/zlib/gzip (d64 = 0) or all deflate64
+// (d64 = 1: 64 KiB history, so 64 KiB windows per unit slot).
 extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, ZsSegDev *d_segs, uint32_t nseg,
                                   ZsCJobDev *d_cjobs, uint32_t ncjobs, ZsChunkDev *d_units, uint32_t nunit_slots,
                                   uint16_t *d_scratch, uint32_t *d_tokens, ZsTokPool pool, uint32_t *d_tables,
                                   const uint32_t *d_fixed, uint8_t *d_windows, void *d_linkinfo, ZsDecDev *d_decs,
-                                  uint32_t *d_fallback, hipStream_t st, hipEvent_t *ev) {
+                                  uint32_t *d_fallback, int d64, hipStream_t st, hipEvent_t *ev) {
   // ev (profiling, optional): [0] before find, [1] after find + plan, [2] after
   // parse + chain, [3] after expand, [4] after link, [5] after emit
   if (ev) (void)hipEventRecord(ev[0], st);
-  hipLaunchKernelGGL(zs_find_kernel, dim3(nseg), dim3(64), 0, st, d_jobs, d_heads, d_segs);
+  if (d64)
+    hipLaunchKernelGGL(zs_find_kernel<true>, dim3(nseg), dim3(64), 0, st, d_jobs, d_heads, d_segs);
+  else
+    hipLaunchKernelGGL(zs_find_kernel<false>, dim3(nseg), dim3(64), 0, st, d_jobs, d_heads, d_segs);
   hipLaunchKernelGGL(zs_find_fixed_kernel, dim3(nseg), dim3(64), 0, st, d_jobs, d_heads, d_segs, nseg);
   hipLaunchKernelGGL(zs_plan_kernel, dim3(ncjobs), dim3(PLAN_T), 0, st, d_jobs, d_heads, d_segs, d_cjobs, d_units, pool);
   if (ev) (void)hipEventRecord(ev[1], st);
   ZsLinkInfo *info = reinterpret_cast<ZsLinkInfo *>(d_linkinfo);
-  zs_launch_parse(d_jobs, d_heads, d_units, nunit_slots, d_tokens, d_tables, d_fixed, pool, st);
+  zs_launch_parse(d_jobs, d_heads, d_units, nunit_slots, d_tokens, d_tables, d_fixed, pool, d64, st);
   hipLaunchKernelGGL(zs_chain_kernel, dim3(ncjobs), dim3(LINK_THREADS), 0, st, d_jobs, d_heads, d_units, d_cjobs, info,
                      d_decs, d_fallback);
   if (ev) (void)hipEventRecord(ev[2], st);
-  zs_launch_expand(d_jobs, d_units, nunit_slots, d_scratch, d_tokens, pool, st);
+  zs_launch_expand(d_jobs, d_units, nunit_slots, d_scratch, d_tokens, pool, d_fallback, d64, st);
   if (ev) (void)hipEventRecord(ev[3], st);
-  hipLaunchKernelGGL(zs_link_kernel, dim3(ncjobs), dim3(LINK_THREADS), 0, st, d_jobs, d_cjobs, d_scratch, d_windows, info,
-                     d_fallback);
-  if (ev) (void)hipEventRecord(ev[4], st);
-  hipLaunchKernelGGL(zs_emit_kernel, dim3(nunit_slots), dim3(EMIT_THREADS), 0, st, d_jobs, d_units, d_scratch, d_windows,
-                     d_fallback);
+  if (d64) {
+    hipLaunchKernelGGL(zs_link64_kernel, dim3(ncjobs), dim3(LINK_THREADS), 0, st, d_cjobs, d_scratch, d_windows, info,
+                       d_fallback);
+    if (ev) (void)hipEventRecord(ev[4], st);
+    hipLaunchKernelGGL(zs_emit64_kernel, dim3(nunit_slots), dim3(EMIT_THREADS), 0, st, d_jobs, d_units, d_scratch,
+                       d_windows, d_fallback);
+  } else {
+    hipLaunchKernelGGL(zs_link_kernel<HIST>, dim3(ncjobs), dim3(LINK_THREADS), 0, st, d_jobs, d_cjobs, d_scratch, d_windows,
+                       info, d_fallback);
+    if (ev) (void)hipEventRecord(ev[4], st);
+    hipLaunchKernelGGL(zs_emit_kernel<HIST>, dim3(nunit_slots), dim3(EMIT_THREADS), 0, st, d_jobs, d_units, d_scratch,
+                       d_windows, d_fallback);
+  }
   if (ev) (void)hipEventRecord(ev[5], st);
 }
 

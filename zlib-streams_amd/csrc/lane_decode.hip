@@ -75,10 +75,11 @@ __device__ __forceinline__ uint16_t compact_len_entry(uint32_t z, uint32_t add_b
   if (op & 32) return (uint16_t)(CK_EOB | (bits << 2));  // 96 = end of block
   if (op & 64) return (uint16_t)CK_SLOW;                 // invalid code
   if ((op & 0xf0u) == 0) return (uint16_t)(CK_SLOW | (op << 2) | (val << 6));  // sub-table link
-  // length base -> code index k (lbase of src/inftrees.c:59-61)
+  // length base -> code index k (lbase of src/inftrees.c:59-61; deflate64's
+  // code 285 is op 144, base 3 + 16 extra bits, src/inftrees.c:73-77)
   const uint32_t e = op & 15u;
   uint32_t k;
-  if (val == 258) k = 28;
+  if (val == 258 || op == 144) k = 28;
   else if (e == 0) k = val - 3;
   else k = 4 * (e + 1) + ((val - 3) >> e) - 4;
   return (uint16_t)(CK_LEN | (bits << 2) | (k << 6));
@@ -297,6 +298,7 @@ __device__ __forceinline__ uint32_t dist_tail(const uint32_t *__restrict__ dtl, 
 #define KPT(i) ((void)0)
 #endif
 
+template <bool D64>
 __device__ __forceinline__ bool lane_step(LaneState &s, const uint16_t *__restrict__ lt, const uint16_t *__restrict__ dt,
                                           uint32_t *__restrict__ tb, const uint32_t *__restrict__ dtl,
                                           const uint32_t *__restrict__ rp, KpPhase &kp) {
@@ -346,6 +348,9 @@ __device__ __forceinline__ bool lane_step(LaneState &s, const uint16_t *__restri
     } else if (sym < 28) {
       xb = (sym >> 2) - 1;
       len = ((4u + (sym & 3u)) << xb) + 3u;
+    } else if (D64) {  // deflate64 code 285: 3 + 16 extra bits
+      xb = 16;
+      len = 3;
     } else {
       len = 258;
     }
@@ -404,7 +409,14 @@ __device__ __forceinline__ bool lane_step(LaneState &s, const uint16_t *__restri
     s.mode = LM_DONE;
     return true;
   }
-  tb[s.gk * WAVE] = kind == CK_SYM ? sym : ((len << 16) | (dist - 1u));
+  if (D64 && len > 0xffffu) {  // a deflate64 copy longer than a token holds: two copies, same distance
+    tb[s.gk * WAVE] = (0xffffu << 16) | (dist - 1u);
+    s.gk++;
+    s.ntok++;
+    tb[s.gk * WAVE] = ((len - 0xffffu) << 16) | (dist - 1u);
+  } else {
+    tb[s.gk * WAVE] = kind == CK_SYM ? sym : ((len << 16) | (dist - 1u));
+  }
   KPT(4);
   s.gk++;
   s.ntok++;
@@ -511,7 +523,7 @@ __device__ void build_dist_tail(const uint16_t *dl, uint32_t n, uint8_t *out) {
   uint32_t r = 0;
   for (int L = 7; L < 16; L++)
     for (uint32_t i = 0; i < n; i++)
-      if (dl[i] == (uint32_t)L && r < 30) out[27 + r++] = (uint8_t)i;
+      if (dl[i] == (uint32_t)L && r < 32) out[27 + r++] = (uint8_t)i;
 }
 
 // Dynamic block header after the 3 block-type bits (src/inflate.c:905-1033):
@@ -520,6 +532,7 @@ __device__ void build_dist_tail(const uint16_t *dl, uint32_t n, uint8_t *out) {
 // (zlib layout + compact copy) and the compact root images lroot_out (256 u16)
 // and droot_out (64 u16), which may be LDS or global.  Wave-cooperative: every
 // lane calls it with the same arguments.  Returns 0, or ZD_* | msg << 8.
+template <bool D64>
 __device__ int wave_dyn_header(BuildLDS &B, const uint32_t *w, uint32_t end_byte, uint32_t &bit, uint32_t *tabg,
                                uint16_t *ctab, uint32_t &lbits, uint32_t &dbits, uint16_t *lroot_out,
                                uint16_t *droot_out, uint8_t *dtail_out) {
@@ -533,7 +546,7 @@ __device__ int wave_dyn_header(BuildLDS &B, const uint32_t *w, uint32_t end_byte
   const uint32_t h = sb.peek(bit, 14);
   const uint32_t nlen = (h & 31) + 257, ndist = ((h >> 5) & 31) + 1, ncode = ((h >> 10) & 15) + 4;
   bit += 14;
-  if (nlen > 286 || ndist > 30) {
+  if (nlen > 286 || ndist > (D64 ? 32u : 30u)) {
     return ZD_ERROR | (ZM_TOO_MANY << 8);
   }
   if (bit + 3 * ncode > limit) {
@@ -588,7 +601,7 @@ __device__ int wave_dyn_header(BuildLDS &B, const uint32_t *w, uint32_t end_byte
   // literal/length table: build in LDS, keep the full zlib table in global
   // (slow path), compact root into the lane's LDS slot
   lbits = 9;
-  if (build_table(T_LENS, B.lens, nlen, B.tab, &lbits, B.sorted, B.scr, 0)) {
+  if (build_table(T_LENS, B.lens, nlen, B.tab, &lbits, B.sorted, B.scr, D64 ? 1 : 0)) {
     return ZD_ERROR | (ZM_LITLEN_SET << 8);
   }
   __builtin_amdgcn_wave_barrier();
@@ -599,11 +612,11 @@ __device__ int wave_dyn_header(BuildLDS &B, const uint32_t *w, uint32_t end_byte
   for (uint32_t i = lane; i < LROOT_N; i += WAVE) lroot_out[i] = lds_len_root(B.tab, lbits, i);
   __builtin_amdgcn_wave_barrier();
   dbits = 6;
-  if (build_table(T_DISTS, B.lens + nlen, ndist, B.tab, &dbits, B.sorted, B.scr, 0)) {
+  if (build_table(T_DISTS, B.lens + nlen, ndist, B.tab, &dbits, B.sorted, B.scr, D64 ? 1 : 0)) {
     return ZD_ERROR | (ZM_DIST_SET << 8);
   }
   __builtin_amdgcn_wave_barrier();
-  for (uint32_t i = lane; i < 592; i += WAVE) {
+  for (uint32_t i = lane; i < (D64 ? 594u : 592u); i += WAVE) {
     tabg[DIST_TABLE_OFF + i] = B.tab[i];
     ctab[DIST_TABLE_OFF + i] = compact_dist_entry(B.tab[i], i < (1u << dbits) ? 0u : dbits);
   }
@@ -624,6 +637,7 @@ __device__ void install_roots(LaneLDS &L, uint32_t ln, const uint32_t *zl, uint3
 // Cooperative block-boundary processing for lane `ln` (all lanes call it with
 // the same ln): end/stop checks, stored blocks, fixed and dynamic headers
 // (src/inflate.c:834-1033); installs the lane's tables.
+template <bool D64>
 __device__ void coop_block(LaneState &s, uint32_t ln, LaneLDS &L, uint32_t *lane_tab, const uint32_t *fixed,
                            uint32_t *tokens, const ZsTokPool &pool, const ZsChunkDev *units) {
   const uint32_t lane = lane_id();
@@ -746,7 +760,7 @@ __device__ void coop_block(LaneState &s, uint32_t ln, LaneLDS &L, uint32_t *lane
       break;
     }
     {
-      const int hc = wave_dyn_header(L.b, w, end_byte, bit, tabg, ctab, lbits, dbits, L.lroot[ln], L.droot[ln],
+      const int hc = wave_dyn_header<D64>(L.b, w, end_byte, bit, tabg, ctab, lbits, dbits, L.lroot[ln], L.droot[ln],
                                      reinterpret_cast<uint8_t *>(L.dtail[ln]));
       if (hc) {
         code = hc;
@@ -784,6 +798,7 @@ __device__ void coop_block(LaneState &s, uint32_t ln, LaneLDS &L, uint32_t *lane
 }
 
 // Parse pass: one lane per chunk, symbols -> tokens (no history reads at all).
+template <bool D64>
 __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict__ jobs, const ZsHeadDev *__restrict__ heads,
                                                       ZsChunkDev *__restrict__ chunks, uint32_t nchunks,
                                                       uint32_t *__restrict__ tokens, uint32_t *__restrict__ tables,
@@ -839,7 +854,7 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
       s.tcap = ch.tcap;
       s.unit = c;
       s.cap = ch.cap;
-      s.whave = ch.ord == 0 ? 0u : HIST;
+      s.whave = ch.ord == 0 ? 0u : (D64 ? 65536u : HIST);
       s.bit = ch.start_bit;
       s.stop = ch.stop_bit;
       s.sidx = c + 1;
@@ -895,7 +910,7 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
     while (need) {
       const uint32_t ln = (uint32_t)__builtin_ctzll(need);
       need &= need - 1;
-      coop_block(s, ln, L, lane_tab, fixed, tokens, pool, chunks);
+      coop_block<D64>(s, ln, L, lane_tab, fixed, tokens, pool, chunks);
     }
 #if KP_ON
     const uint64_t kc1 = KP_NOW();
@@ -906,9 +921,10 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
     s.gk = 0;
     if (s.mode == LM_SYM) {
       lane_fill_ring(s, rp);
-      // a step reads at most 2 more ring words
-      for (int it = 0; it < GROUP && s.rk + 2 < RING; it++)
-        if (lane_step(s, lt, dt, tb, dtl, rp, kph)) break;
+      // a step reads at most 2 more ring words and stores 1 token (2 for a
+      // deflate64 copy longer than 65535)
+      while (s.gk + (D64 ? 2u : 1u) <= GROUP && s.rk + 2 < RING)
+        if (lane_step<D64>(s, lt, dt, tb, dtl, rp, kph)) break;
     }
     __builtin_amdgcn_wave_barrier();
 #if KP_ON
@@ -1012,12 +1028,19 @@ __device__ __forceinline__ void exp_barrier() {
 #define TV_LIT 0x80000000u  // s_tval: literal byte | TV_LIT, else match distance
 #define JR 0x80000000u      // s_j: resolved value | JR, else index of the source in the round
 
+// Deflate64 (D64): a 64 Ki-entry ring and 64 KiB of history, so markers
+// 256 + w need 17 bits: the ring keeps the low 16 bits and a flag byte per 4
+// entries the 17th (entries go to HBM as u32).
+template <bool D64>
 __global__ void __launch_bounds__(EXP_T) zs_expand_kernel(const ZsJobDev *__restrict__ jobs,
                                                            const ZsChunkDev *__restrict__ chunks,
                                                            uint16_t *__restrict__ scratch,
                                                            const uint32_t *__restrict__ tokens,
-                                                           const uint32_t *__restrict__ order, ZsTokPool pool) {
-  __shared__ __attribute__((aligned(16))) uint16_t ring[HIST];
+                                                           const uint32_t *__restrict__ order, ZsTokPool pool,
+                                                           uint32_t *__restrict__ fallback) {
+  constexpr uint32_t HN = D64 ? 65536u : HIST;
+  __shared__ __attribute__((aligned(16))) uint16_t ring[HN];
+  __shared__ uint8_t qflag[D64 ? HN / 4 : 4];  // bit k of qflag[i >> 2]: bit 16 of entry 4 (i >> 2) + k
   __shared__ __attribute__((aligned(16))) uint32_t s_mark[EXP_N];
   __shared__ uint32_t s_tval[EXP_T];
   __shared__ uint32_t s_red[EXP_W], s_flag[EXP_W];
@@ -1037,15 +1060,22 @@ __global__ void __launch_bounds__(EXP_T) zs_expand_kernel(const ZsJobDev *__rest
     return tokens[pool.base + ((uint64_t)(ptab[k] - 1u) << ZS_TP_LOG) + off];
   };
   uint16_t *out = scratch + ch.scratch;
+  uint32_t *out32 = reinterpret_cast<uint32_t *>(scratch + ch.scratch);  // D64: u32 entries
+  auto rget = [&](uint32_t i) -> uint32_t {  // ring entry i (masked index)
+    if (!D64) return ring[i];
+    return ring[i] | (((uint32_t)(qflag[i >> 2] >> (i & 3u)) & 1u) << 16);
+  };
   (void)jobs;
 #if KP_ON
   const uint64_t kp_t0 = KP_NOW();
   uint64_t kp_jump = 0;
   uint32_t kp_rounds = 0, kp_jits = 0, kp_jrounds = 0, kp_batches = 0;
 #endif
-  if (ch.ord != 0) {  // history before the chunk: markers 256 + w for position w - HIST
+  if (ch.ord != 0) {  // history before the chunk: markers 256 + w for position w - HN
     uint32_t *r32 = reinterpret_cast<uint32_t *>(ring);
-    for (uint32_t i = tid; i < HIST / 2; i += EXP_T) r32[i] = (MARK_BASE + 2 * i) | ((MARK_BASE + 2 * i + 1) << 16);
+    for (uint32_t i = tid; i < HN / 2; i += EXP_T) r32[i] = ((MARK_BASE + 2 * i) & 0xffffu) | ((MARK_BASE + 2 * i + 1) << 16);
+    if (D64)
+      for (uint32_t i = tid; i < HN / 4; i += EXP_T) qflag[i] = i >= (HN - MARK_BASE) / 4 ? 0xfu : 0u;
   }
   for (uint32_t i = tid; i < EXP_N; i += EXP_T) s_mark[i] = 0;
 #if KP_ON
@@ -1085,8 +1115,17 @@ __global__ void __launch_bounds__(EXP_T) zs_expand_kernel(const ZsJobDev *__rest
       if (len && tstart >= R && tstart < R + EXP_N) s_mark[tstart - R] = (st << 9) | (tid + 1);
       exp_barrier();  // B1: marks, token values and the previous round's ring writes visible
       while (lo - flushed >= EXP_FLUSH) {
-        const uint4 v4 = *reinterpret_cast<const uint4 *>(&ring[(flushed + tid * 8) & (HIST - 1)]);
-        *reinterpret_cast<uint4 *>(out + flushed + tid * 8) = v4;
+        const uint32_t ri = (flushed + tid * 8) & (HN - 1);
+        if (D64) {
+          uint32_t x[8];
+#pragma unroll
+          for (int k = 0; k < 8; k++) x[k] = rget(ri + k);
+          *reinterpret_cast<uint4 *>(out32 + flushed + tid * 8) = make_uint4(x[0], x[1], x[2], x[3]);
+          *reinterpret_cast<uint4 *>(out32 + flushed + tid * 8 + 4) = make_uint4(x[4], x[5], x[6], x[7]);
+        } else {
+          const uint4 v4 = *reinterpret_cast<const uint4 *>(&ring[ri]);
+          *reinterpret_cast<uint4 *>(out + flushed + tid * 8) = v4;
+        }
         flushed += EXP_FLUSH;
       }
       // owner token of each of this thread's entries: running max of marks
@@ -1123,7 +1162,7 @@ __global__ void __launch_bounds__(EXP_T) zs_expand_kernel(const ZsJobDev *__rest
         if (e >= lo && e < pos + S && !(vj & TV_LIT)) {
           const int p = (int)e - (int)vj;
           if (p < (int)lo) {
-            v[k] = ring[(uint32_t)p & (HIST - 1)];
+            v[k] = rget((uint32_t)p & (HN - 1));
           } else {
             q[k] = (uint32_t)(p - (int)R);
             unres |= 1u << k;
@@ -1167,7 +1206,7 @@ __global__ void __launch_bounds__(EXP_T) zs_expand_kernel(const ZsJobDev *__rest
             if (unres & (1u << k)) {
               const uint32_t x = s_j[b][q[k]];
               if (x & JR) {
-                v[k] = x & 0xffffu;
+                v[k] = x & ~JR;
                 unres &= ~(1u << k);
               } else {
                 q[k] = x;
@@ -1181,13 +1220,20 @@ __global__ void __launch_bounds__(EXP_T) zs_expand_kernel(const ZsJobDev *__rest
 #endif
       if (e0 >= lo && e0 + EXP_E <= pos + S) {
         uint2 w2;
-        w2.x = v[0] | (v[1] << 16);
-        w2.y = v[2] | (v[3] << 16);
-        *reinterpret_cast<uint2 *>(&ring[e0 & (HIST - 1)]) = w2;
+        w2.x = (v[0] & 0xffffu) | (v[1] << 16);
+        w2.y = (v[2] & 0xffffu) | (v[3] << 16);
+        *reinterpret_cast<uint2 *>(&ring[e0 & (HN - 1)]) = w2;
+        if (D64)
+          qflag[(e0 & (HN - 1)) >> 2] =
+              (uint8_t)(((v[0] >> 16) & 1u) | ((v[1] >> 15) & 2u) | ((v[2] >> 14) & 4u) | ((v[3] >> 13) & 8u));
       } else {
 #pragma unroll
         for (int k = 0; k < EXP_E; k++)
-          if (e0 + k >= lo && e0 + k < pos + S) ring[(e0 + k) & (HIST - 1)] = (uint16_t)v[k];
+          if (e0 + k >= lo && e0 + k < pos + S) {
+            const uint32_t ri = (e0 + k) & (HN - 1);
+            ring[ri] = (uint16_t)v[k];
+            if (D64) qflag[ri >> 2] = (uint8_t)((qflag[ri >> 2] & ~(1u << (ri & 3u))) | (((v[k] >> 16) & 1u) << (ri & 3u)));
+          }
       }
     }
     pos += S;
@@ -1197,11 +1243,24 @@ __global__ void __launch_bounds__(EXP_T) zs_expand_kernel(const ZsJobDev *__rest
   }
   exp_barrier();
   while (pos - flushed >= EXP_FLUSH) {
-    const uint4 v4 = *reinterpret_cast<const uint4 *>(&ring[(flushed + tid * 8) & (HIST - 1)]);
-    *reinterpret_cast<uint4 *>(out + flushed + tid * 8) = v4;
+    const uint32_t ri = (flushed + tid * 8) & (HN - 1);
+    if (D64) {
+      uint32_t x[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) x[k] = rget(ri + k);
+      *reinterpret_cast<uint4 *>(out32 + flushed + tid * 8) = make_uint4(x[0], x[1], x[2], x[3]);
+      *reinterpret_cast<uint4 *>(out32 + flushed + tid * 8 + 4) = make_uint4(x[4], x[5], x[6], x[7]);
+    } else {
+      const uint4 v4 = *reinterpret_cast<const uint4 *>(&ring[ri]);
+      *reinterpret_cast<uint4 *>(out + flushed + tid * 8) = v4;
+    }
     flushed += EXP_FLUSH;
   }
-  for (uint32_t k = tid; k < pos - flushed; k += EXP_T) out[flushed + k] = ring[(flushed + k) & (HIST - 1)];
+  for (uint32_t k = tid; k < pos - flushed; k += EXP_T) {
+    if (D64) out32[flushed + k] = rget((flushed + k) & (HN - 1));
+    else out[flushed + k] = ring[(flushed + k) & (HN - 1)];
+  }
+  (void)fallback;
 #if KP_ON
   if (wv == 0) {
     const uint64_t tot = KP_NOW() - kp_t0;
@@ -1224,6 +1283,7 @@ __global__ void __launch_bounds__(EXP_T) zs_expand_kernel(const ZsJobDev *__rest
 // the compact root image next to them; the parse pass then starts each lane
 // directly in symbol mode.  A header that does not decode is left to the parse
 // pass, which redoes it cooperatively and reports exactly.
+template <bool D64>
 __global__ void __launch_bounds__(64) zs_unit_header_kernel(const ZsJobDev *__restrict__ jobs,
                                                              const ZsHeadDev *__restrict__ heads,
                                                              ZsChunkDev *__restrict__ units, uint32_t *__restrict__ tables) {
@@ -1247,7 +1307,7 @@ __global__ void __launch_bounds__(64) zs_unit_header_kernel(const ZsJobDev *__re
   uint16_t *ctab = reinterpret_cast<uint16_t *>(tabg + TABLE_ENTRIES);
   uint16_t *img = reinterpret_cast<uint16_t *>(tabg + TABLE_ENTRIES + TABLE_ENTRIES / 2);
   uint32_t lbits = 9, dbits = 6;
-  if (wave_dyn_header(B, w, end_byte, bit, tabg, ctab, lbits, dbits, img, img + LROOT_N,
+  if (wave_dyn_header<D64>(B, w, end_byte, bit, tabg, ctab, lbits, dbits, img, img + LROOT_N,
                       reinterpret_cast<uint8_t *>(img + LROOT_N + DROOT_N)))
     return;
   if (lane == 0) {
@@ -1323,24 +1383,35 @@ int sort_units(const ZsJobDev *d_jobs, const ZsChunkDev *d_chunks, uint32_t n, i
 }  // namespace
 
 extern "C" void zs_launch_parse(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, ZsChunkDev *d_chunks, uint32_t nchunks,
-                                uint32_t *d_tokens, uint32_t *d_tables, const uint32_t *d_fixed, ZsTokPool pool,
+                                uint32_t *d_tokens, uint32_t *d_tables, const uint32_t *d_fixed, ZsTokPool pool, int d64,
                                 hipStream_t st) {
   if (!nchunks) return;
-  hipLaunchKernelGGL(zs_unit_header_kernel, dim3(nchunks), dim3(WAVE), 0, st, d_jobs, d_heads, d_chunks, d_tables);
+  if (d64)
+    hipLaunchKernelGGL(zs_unit_header_kernel<true>, dim3(nchunks), dim3(WAVE), 0, st, d_jobs, d_heads, d_chunks, d_tables);
+  else
+    hipLaunchKernelGGL(zs_unit_header_kernel<false>, dim3(nchunks), dim3(WAVE), 0, st, d_jobs, d_heads, d_chunks, d_tables);
   uint32_t *order = nullptr;
   if (sort_units(d_jobs, d_chunks, nchunks, 0, &order, st)) return;
-  hipLaunchKernelGGL(zs_lane_kernel, dim3((nchunks + WAVE - 1) / WAVE), dim3(WAVE), 0, st, d_jobs, d_heads, d_chunks,
-                     nchunks, d_tokens, d_tables, d_fixed, order, pool);
+  if (d64)
+    hipLaunchKernelGGL(zs_lane_kernel<true>, dim3((nchunks + WAVE - 1) / WAVE), dim3(WAVE), 0, st, d_jobs, d_heads,
+                       d_chunks, nchunks, d_tokens, d_tables, d_fixed, order, pool);
+  else
+    hipLaunchKernelGGL(zs_lane_kernel<false>, dim3((nchunks + WAVE - 1) / WAVE), dim3(WAVE), 0, st, d_jobs, d_heads,
+                       d_chunks, nchunks, d_tokens, d_tables, d_fixed, order, pool);
 }
 
 // expand the verified chain members (after zs_chain_kernel), longest first
 extern "C" void zs_launch_expand(const ZsJobDev *d_jobs, ZsChunkDev *d_chunks, uint32_t nchunks, uint16_t *d_scratch,
-                                 const uint32_t *d_tokens, ZsTokPool pool, hipStream_t st) {
+                                 const uint32_t *d_tokens, ZsTokPool pool, uint32_t *d_fallback, int d64, hipStream_t st) {
   if (!nchunks) return;
   uint32_t *order = nullptr;
   if (sort_units(d_jobs, d_chunks, nchunks, 1, &order, st)) return;
-  hipLaunchKernelGGL(zs_expand_kernel, dim3(nchunks), dim3(EXP_T), 0, st, d_jobs, d_chunks, d_scratch, d_tokens, order,
-                     pool);
+  if (d64)
+    hipLaunchKernelGGL(zs_expand_kernel<true>, dim3(nchunks), dim3(EXP_T), 0, st, d_jobs, d_chunks, d_scratch, d_tokens,
+                       order, pool, d_fallback);
+  else
+    hipLaunchKernelGGL(zs_expand_kernel<false>, dim3(nchunks), dim3(EXP_T), 0, st, d_jobs, d_chunks, d_scratch, d_tokens,
+                       order, pool, d_fallback);
 }
 
 extern "C" int zs_kprof_read_ck(uint64_t *out16, int reset);

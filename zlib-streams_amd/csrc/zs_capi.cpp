@@ -30,7 +30,7 @@ extern "C" void zs_launch_finish(const ZsJobDev *d_jobs, const ZsHeadDev *d_head
                                  hipStream_t stream);
 extern "C" void zs_launch_stream(int d64, int run_header, ZsStreamDev *d_st, const ZsJobDev *d_job, ZsHeadDev *d_head,
                                  uint64_t out_cap, hipStream_t stream);
-extern "C" void zs_launch_fixed_tables(uint32_t *fixed, hipStream_t st);
+extern "C" void zs_launch_fixed_tables(uint32_t *fixed, int d64, hipStream_t st);
 extern "C" void zs_launch_fixed_compact(uint32_t *fixed, hipStream_t st);
 extern "C" void zs_launch_deflate(ZsDJobDev *d_jobs, uint32_t njobs, ZsDSegDev *d_segs, uint32_t nseg, uint16_t *d_dist16,
                                   uint8_t *d_len8, uint32_t *d_bm, uint32_t *d_aux, uint32_t *d_obuf, uint8_t *d_stage,
@@ -50,7 +50,7 @@ extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_hea
                                   ZsCJobDev *d_cjobs, uint32_t ncjobs, ZsChunkDev *d_units, uint32_t nunit_slots,
                                   uint16_t *d_scratch, uint32_t *d_tokens, ZsTokPool pool, uint32_t *d_tables,
                                   const uint32_t *d_fixed, uint8_t *d_windows, void *d_linkinfo, ZsDecDev *d_decs,
-                                  uint32_t *d_fallback, hipStream_t st, hipEvent_t *ev);
+                                  uint32_t *d_fallback, int d64, hipStream_t st, hipEvent_t *ev);
 
 namespace {
 
@@ -118,7 +118,8 @@ struct Workspace {
   ZsSegDev *d_segs = nullptr, *h_segs = nullptr;
   ZsChunkDev *d_chunks = nullptr, *h_chunks = nullptr;  // unit slots
   uint32_t *d_tables = nullptr;  // TABLE_STRIDE words per unit slot
-  uint8_t *d_windows = nullptr;  // 32 KiB per unit slot
+  uint8_t *d_windows = nullptr;  // 32 KiB per unit slot (64 KiB for deflate64 units)
+  size_t cap_windows = 0;
   uint64_t *d_linkinfo = nullptr;  // zs_link_kernel chain order: 16 B per unit slot
   size_t cap_scratch = 0;        // u16 entries (chain members at their output offsets)
   uint16_t *d_scratch = nullptr;
@@ -208,8 +209,14 @@ int ws_reserve_jobs(size_t n) {
 
 // A failed allocation leaves the buffer null AND its capacity 0, so the next
 // call allocates again instead of trusting a stale capacity.
-int ws_reserve_chunks(size_t nseg, size_t nunits, size_t scratch_entries, size_t tokens) {
+int ws_reserve_chunks(size_t nseg, size_t nunits, size_t scratch_entries, size_t tokens, size_t window_bytes) {
   int r;
+  if (window_bytes > g_ws.cap_windows) {
+    size_t c = std::max(window_bytes, g_ws.cap_windows + g_ws.cap_windows / 2);
+    g_ws.cap_windows = 0;
+    if ((r = grow_dev(&g_ws.d_windows, c))) return r;
+    g_ws.cap_windows = c;
+  }
   if (nseg > g_ws.cap_segs) {
     size_t c = std::max(nseg, g_ws.cap_segs + g_ws.cap_segs / 2);
     g_ws.cap_segs = 0;
@@ -220,7 +227,7 @@ int ws_reserve_chunks(size_t nseg, size_t nunits, size_t scratch_entries, size_t
     size_t c = std::max(nunits, g_ws.cap_units + g_ws.cap_units / 2);
     g_ws.cap_units = 0;
     if ((r = grow_dev(&g_ws.d_chunks, c)) || (r = grow_host(&g_ws.h_chunks, c)) ||
-        (r = grow_dev(&g_ws.d_tables, c * TABLE_ENTRIES_HOST)) || (r = grow_dev(&g_ws.d_windows, c * 32768)) ||
+        (r = grow_dev(&g_ws.d_tables, c * TABLE_ENTRIES_HOST)) ||
         (r = grow_dev(&g_ws.d_linkinfo, c * 2)) || (r = grow_dev(&g_ws.d_ptab, c * ZS_TP_MAXPG)))
       return r;
     g_ws.cap_units = c;
@@ -238,10 +245,12 @@ int ws_reserve_chunks(size_t nseg, size_t nunits, size_t scratch_entries, size_t
     g_ws.cap_tokens = c;
   }
   if (!g_ws.d_pool_next && (r = grow_dev(&g_ws.d_pool_next, 4))) return r;
-  if (!g_ws.d_fixed) {
-    if ((r = grow_dev(&g_ws.d_fixed, FIXED_WORDS_HOST))) return r;
-    zs_launch_fixed_tables(g_ws.d_fixed, g_ws.stream);
+  if (!g_ws.d_fixed) {  // fixed tables: the deflate set, then the deflate64 set
+    if ((r = grow_dev(&g_ws.d_fixed, 2 * FIXED_WORDS_HOST))) return r;
+    zs_launch_fixed_tables(g_ws.d_fixed, 0, g_ws.stream);
     zs_launch_fixed_compact(g_ws.d_fixed, g_ws.stream);
+    zs_launch_fixed_tables(g_ws.d_fixed + FIXED_WORDS_HOST, 1, g_ws.stream);
+    zs_launch_fixed_compact(g_ws.d_fixed + FIXED_WORDS_HOST, g_ws.stream);
   }
   return 0;
 }
@@ -363,41 +372,49 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
   // capacity on the chunked path depends on one.  Lists in h_ids:
   // [serial std | d64 | chunked].
   const uint32_t C = chunk_bytes();
-  uint32_t n_std = 0, n_d64 = 0, n_cj = 0;
+  uint32_t n_std = 0, n_d64 = 0, n_cj = 0, n_cj64 = 0;
   size_t nseg = 0, nunit_slots = 0;
-  std::vector<uint32_t> cj_list;
+  // chunked jobs: the raw/zlib/gzip group first, then the deflate64 group
+  std::vector<uint32_t> cj_list, cj64_list;
   std::vector<uint8_t> is_cj(nv, 0);
   for (uint32_t k = 0; k < nv; k++) {
     const ZsJobDev &jd = g_ws.h_jobs[k];
     const bool big = jd.in_len >= 4ull * C || (jd.in_len >= C && jd.out_cap >= (4ull << 20));
-    if (chunking_enabled() && !jd.d64 && !(jd.flags & ZS_JF_COPY) && big && jd.in_len < (1ull << 29)) {
-      cj_list.push_back(k);
+    if (chunking_enabled() && !(jd.flags & ZS_JF_COPY) && big && jd.in_len < (1ull << 29)) {
+      (jd.d64 ? cj64_list : cj_list).push_back(k);
       is_cj[k] = 1;
     }
   }
+  const uint32_t n_cj_std = (uint32_t)cj_list.size();
+  cj_list.insert(cj_list.end(), cj64_list.begin(), cj64_list.end());
   std::vector<uint32_t> copies;  // ZIP stored entries: output = input
   for (uint32_t k = 0; k < nv; k++)
     if (g_ws.h_jobs[k].flags & ZS_JF_COPY) copies.push_back(k);
   // Plan the chunked jobs (segments, unit slots, token regions, entry ranges,
-  // token pool) and upload them.  Any allocation failure here only sends the
-  // jobs to the serial decoder.
+  // token pool, history windows) and upload them.  Any allocation failure here
+  // only sends the jobs to the serial decoder.
   ZsTokPool pool{};
+  size_t seg_std = 0, slots_std = 0;
   if (!cj_list.empty()) {
-    size_t slots = 0, toks = 0, ents = 0, in_sum = 0;
+    size_t slots = 0, toks = 0, ents = 0, in_sum = 0, win = 0;
     nseg = 0;
     for (uint32_t k : cj_list) nseg += (g_ws.h_jobs[k].in_len + C - 1) / C;
-    int rr = ws_reserve_chunks(nseg, 0, 0, 0);
+    int rr = ws_reserve_chunks(nseg, 0, 0, 0, 0);
     size_t si = 0;
     for (uint32_t q = 0; q < cj_list.size() && !rr; q++) {
       const uint32_t k = cj_list[q];
       const ZsJobDev &jd = g_ws.h_jobs[k];
+      if (q == n_cj_std) {
+        seg_std = si;
+        slots_std = slots;
+      }
       const uint32_t ns = (uint32_t)((jd.in_len + C - 1) / C);
       const uint32_t max_units = ns * SEG_SLOTS + 1;
       ZsCJobDev cj{};
       cj.job = k;
-      cj.first_seg = (uint32_t)si;
+      cj.first_seg = (uint32_t)(si - (q >= n_cj_std ? seg_std : 0));  // group-relative
       cj.nseg = ns;
-      cj.unit0 = (uint32_t)slots;
+      cj.unit0 = (uint32_t)(slots - (q >= n_cj_std ? slots_std : 0));
       cj.max_units = max_units;
       // primary token regions (zs_plan_kernel): per unit span x ZS_TOK_PER_BYTE
       // + slack, spans summing to at most the input plus a byte per unit
@@ -408,8 +425,10 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
       // (zs_chain_kernel), hence 8 entries of padding per possible unit
       cj.scratch0 = ents;
       cj.scratch_n = std::min<uint64_t>(jd.out_cap, MAX_RATIO * jd.in_len + 64) + 8ull * max_units;
-      ents += (cj.scratch_n + 16 + 15) & ~size_t(15);
+      cj.esz = jd.d64 ? 2u : 1u;  // deflate64: 17-bit entries, stored as u32
+      ents += (cj.esz * (cj.scratch_n + 16) + 15) & ~size_t(15);
       in_sum += jd.in_len;
+      win += (size_t)max_units * (jd.d64 ? 65536u : 32768u);
       g_ws.h_cjobs[q] = cj;
       for (uint32_t o = 0; o < ns; o++, si++) {
         ZsSegDev sg{};
@@ -422,14 +441,19 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
       }
       slots += max_units;
     }
+    if (n_cj_std == cj_list.size()) {
+      seg_std = si;
+      slots_std = slots;
+    }
     const size_t pool_pages = std::max<size_t>(64, (in_sum / 1024 * pool_per_kb() + ((size_t)1 << ZS_TP_LOG) - 1) >> ZS_TP_LOG);
-    if (!rr) rr = ws_reserve_chunks(nseg, slots, ents + 16, toks + (pool_pages << ZS_TP_LOG));
+    if (!rr) rr = ws_reserve_chunks(nseg, slots, ents + 16, toks + (pool_pages << ZS_TP_LOG), win);
     if (rr) {  // no room for the chunked path: every job decodes serially
       cj_list.clear();
       std::fill(is_cj.begin(), is_cj.end(), 0);
       nseg = 0;
     } else {
       n_cj = (uint32_t)cj_list.size();
+      n_cj64 = n_cj - n_cj_std;
       nunit_slots = slots;
       pool.base = toks;
       pool.npages = (uint32_t)pool_pages;
@@ -440,25 +464,41 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
       HIP_OK(hipMemsetAsync(g_ws.d_pool_next, 0, sizeof(uint32_t), st));
     }
   }
+  // serial lists: [std | d64 | chunked std | chunked d64] in h_ids
   for (uint32_t k = 0; k < nv; k++)
     if (!g_ws.h_jobs[k].d64 && !(g_ws.h_jobs[k].flags & ZS_JF_COPY) && !is_cj[k]) g_ws.h_ids[n_std++] = k;
   for (uint32_t k = 0; k < nv; k++)
-    if (g_ws.h_jobs[k].d64) g_ws.h_ids[n_std + n_d64++] = k;
+    if (g_ws.h_jobs[k].d64 && !is_cj[k]) g_ws.h_ids[n_std + n_d64++] = k;
   for (uint32_t q = 0; q < n_cj; q++) g_ws.h_ids[n_std + n_d64 + q] = cj_list[q];
   HIP_OK(hipMemcpyAsync(g_ws.d_jobs, g_ws.h_jobs, nv * sizeof(ZsJobDev), hipMemcpyHostToDevice, st));
   HIP_OK(hipMemcpyAsync(g_ws.d_ids, g_ws.h_ids, nv * sizeof(uint32_t), hipMemcpyHostToDevice, st));
   hipEvent_t *ev = g_ws.prof ? g_ws.ev : nullptr;
   if (ev) HIP_OK(hipEventRecord(ev[0], st));
   zs_launch_header(g_ws.d_jobs, g_ws.d_heads, nv, st);
-  if (n_cj) {
-    zs_launch_chunked(g_ws.d_jobs, g_ws.d_heads, g_ws.d_segs, (uint32_t)nseg, g_ws.d_cjobs, n_cj, g_ws.d_chunks,
-                      (uint32_t)nunit_slots, g_ws.d_scratch, g_ws.d_tokens, pool, g_ws.d_tables, g_ws.d_fixed,
-                      g_ws.d_windows, g_ws.d_linkinfo, g_ws.d_decs, g_ws.d_fallback, st, ev ? ev + 1 : nullptr);
-  } else if (ev)
+  const uint32_t n_cjs = n_cj - n_cj64;
+  if (n_cjs) {
+    zs_launch_chunked(g_ws.d_jobs, g_ws.d_heads, g_ws.d_segs, (uint32_t)seg_std, g_ws.d_cjobs, n_cjs, g_ws.d_chunks,
+                      (uint32_t)slots_std, g_ws.d_scratch, g_ws.d_tokens, pool, g_ws.d_tables, g_ws.d_fixed,
+                      g_ws.d_windows, g_ws.d_linkinfo, g_ws.d_decs, g_ws.d_fallback, 0, st, ev ? ev + 1 : nullptr);
+  }
+  if (n_cj64) {  // the deflate64 group: its own slice of every per-unit array
+    ZsTokPool p64 = pool;
+    p64.ptab = pool.ptab + slots_std * ZS_TP_MAXPG;
+    zs_launch_chunked(g_ws.d_jobs, g_ws.d_heads, g_ws.d_segs + seg_std, (uint32_t)(nseg - seg_std),
+                      g_ws.d_cjobs + n_cjs, n_cj64, g_ws.d_chunks + slots_std, (uint32_t)(nunit_slots - slots_std),
+                      g_ws.d_scratch, g_ws.d_tokens, p64, g_ws.d_tables + slots_std * TABLE_ENTRIES_HOST,
+                      g_ws.d_fixed + FIXED_WORDS_HOST, g_ws.d_windows + slots_std * 32768, g_ws.d_linkinfo + slots_std * 2,
+                      g_ws.d_decs, g_ws.d_fallback, 1, st, (ev && !n_cjs) ? ev + 1 : nullptr);
+  }
+  if (!n_cj && ev)
     for (int i = 1; i <= 6; i++) HIP_OK(hipEventRecord(ev[i], st));
+  if (n_cj && ev && n_cjs && n_cj64)  // stage events cover the first group only
+    ;
   zs_launch_decode(0, g_ws.d_jobs, g_ws.d_heads, g_ws.d_ids, n_std, g_ws.d_decs, nullptr, st);
   zs_launch_decode(1, g_ws.d_jobs, g_ws.d_heads, g_ws.d_ids + n_std, n_d64, g_ws.d_decs, nullptr, st);
-  if (n_cj) zs_launch_decode(0, g_ws.d_jobs, g_ws.d_heads, g_ws.d_ids + n_std + n_d64, n_cj, g_ws.d_decs, g_ws.d_fallback, st);
+  if (n_cjs) zs_launch_decode(0, g_ws.d_jobs, g_ws.d_heads, g_ws.d_ids + n_std + n_d64, n_cjs, g_ws.d_decs, g_ws.d_fallback, st);
+  if (n_cj64)
+    zs_launch_decode(1, g_ws.d_jobs, g_ws.d_heads, g_ws.d_ids + n_std + n_d64 + n_cjs, n_cj64, g_ws.d_decs, g_ws.d_fallback, st);
   std::vector<ZsDecDev> copy_decs(copies.size());
   for (size_t q = 0; q < copies.size(); q++) {
     const ZsJobDev &jd = g_ws.h_jobs[copies[q]];

@@ -176,6 +176,8 @@ struct ZsCJobDev {     // a job on the chunked path
   uint64_t scratch_n;  // entries reserved: min(out_cap, bound) -- the chain's total never exceeds it
   uint32_t nchain;     // units in the verified chain (zs_chain_kernel)
   uint32_t ok;         // chain verified (zs_chain_kernel); cleared again by zs_link_kernel on a bad window
+  uint32_t esz;        // u16 slots per entry: 1, or 2 for deflate64 (17-bit entries stored as u32)
+  uint32_t pad;
 };
 // ---------------------------------------------------------------------------
 // GPU deflate (deflate_kernels.hip): one job = one whole stream compressed as
