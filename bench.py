@@ -73,6 +73,11 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-deflate-seconds", type=float, default=10.0)
     ap.add_argument("--no-deflate64", action="store_true", help="skip the deflate64 suite leg (configs[3])")
     ap.add_argument("--d64-reps", type=int, default=256, help="copies of the deflate64 fixture suite per batch")
+    ap.add_argument("--no-stream-leg", action="store_true", help="skip the handle-ABI stream leg")
+    ap.add_argument("--only-stream", action="store_true", help="run only the handle-ABI stream leg")
+    ap.add_argument("--stream-leg-mib", type=int, default=16, help="line-text stream of the one-handle run")
+    ap.add_argument("--stream-handles", type=int, default=64, help="concurrent handles of the aggregate run")
+    ap.add_argument("--stream-handle-mib", type=int, default=4, help="stream size per concurrent handle")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json"),
                     help="PMC-derived HBM bytes per pipeline launch (null in the line when absent)")
     ap.add_argument("--dry-run", action="store_true",
@@ -307,6 +312,10 @@ def main():
         dev = torch.device("cuda", torch.cuda.current_device())
 
     cpu = host_cpu_info()
+    if args.only_stream:
+        import zstreams
+        print(json.dumps({"stream": stream_leg(args, zstreams, np, cpu)}), flush=True)
+        return
     gen_threads = max(1, min(16, cpu["logical_cpus"] // max(1, world)))
     t0 = time.time()
     if args.workload == "c5":
@@ -406,6 +415,9 @@ def main():
                                              comps, cpu, rank, kinds, fast=True)
     if not args.dry_run and not args.no_deflate64:
         d64_leg = deflate64_leg(args, zstreams, torch, np, dev, rank)
+    stream_l = None
+    if not args.dry_run and not args.no_stream_leg and rank == 0 and world == 1:
+        stream_l = stream_leg(args, zstreams, np, cpu)
 
     cpu_b = None
     if rank == 0 and not args.no_cpu_baseline and not args.dry_run and nloc:
@@ -448,6 +460,7 @@ def main():
             "path_stats": stats,
             "compress": comp_leg,
             "deflate64": d64_leg,
+            "stream": stream_l,
         }
         if args.dry_run:
             line["dry_run"] = True
@@ -455,6 +468,137 @@ def main():
         print(json.dumps(line), flush=True)
     if dist:
         tdist.destroy_process_group()
+
+
+def _js_schedule_loop(L, h, comp, out, write_size):
+    """The reference's DecompressionStreamZlib call schedule (src/wasm/api/zlib-streams.js:64-136)
+    over inflate_process on one handle: writes of `write_size`, <= 32 KiB slices, a 64 KiB output
+    buffer per call, advance by last_consumed, stop a write on 0; then Z_FINISH drains.  Output is
+    written consecutively into `out` (a numpy array).  Returns (bytes produced, final code, calls)."""
+    base = comp.ctypes.data
+    n = len(comp)
+    put = 0
+    op = out.ctypes.data
+    code = 0
+    calls = 0
+    for w in range(0, n, write_size):
+        ln = min(write_size, n - w)
+        off = 0
+        while off < ln:
+            k = min(ln - off, 32768)
+            r = L.inflate_process(h, base + w + off, k, op + put, 65536, 0) & 0xffffffff
+            calls += 1
+            put += r & 0xffffff
+            code = (r >> 24) - 256 if r >> 31 else r >> 24
+            if code < 0:
+                return put, code, calls
+            c = L.inflate_last_consumed(h)
+            if c == 0:
+                break
+            off += c
+    while True:
+        r = L.inflate_process(h, 0, 0, op + put, 65536, 4) & 0xffffffff
+        calls += 1
+        got = r & 0xffffff
+        put += got
+        code = (r >> 24) - 256 if r >> 31 else r >> 24
+        if code < 0 or code == 1 or got == 0:
+            return put, code, calls
+
+
+def stream_leg(args, zstreams, np, cpu):
+    """The reference's product entry: DecompressionStreamZlib over the handle ABI
+    (inflate_new / inflate_init_raw / inflate_process / inflate_last_consumed), fed as
+    zlib-streams.js feeds WASM: 64 KiB writes, <= 32 KiB per process() call, 64 KiB out.
+    One handle on a line-text stream (per-stream MiB/s, the figure the shipped WASM's
+    493 MiB/s is quoted on), then `stream_handles` handles on their own
+    host threads at once (aggregate MiB/s).  Host zlib runs the same schedule beside it."""
+    import threading
+
+    import corpus
+
+    L = zstreams.lib()
+    ws = 65536
+    one_bytes = args.stream_leg_mib << 20
+    r1, c1 = corpus.batch(32, 1, one_bytes, level=6, wbits=-15, nthreads=1)
+    raw1, comp1 = r1[0], c1[0]
+    nh = args.stream_handles
+    each = args.stream_handle_mib << 20
+    rs, cs = corpus.batch(32, nh, each, level=6, wbits=-15, nthreads=min(16, cpu["logical_cpus"]))
+
+    def run_one(comp, raw, out, res, k):
+        h = L.inflate_new()
+        L.inflate_init_raw(h)
+        try:
+            res[k] = _js_schedule_loop(L, h, comp, out, ws)
+        finally:
+            L.inflate_end(h)
+
+    out1 = np.empty(one_bytes + 65536, dtype=np.uint8)
+    res = [None]
+    run_one(comp1, raw1, out1, res, 0)  # warm (device state, buffers)
+    t0 = time.perf_counter()
+    run_one(comp1, raw1, out1, res, 0)
+    t1 = time.perf_counter() - t0
+    ok1 = res[0][0] == one_bytes and res[0][1] == 1 and np.array_equal(out1[:one_bytes], raw1)
+    calls1 = res[0][2]
+
+    outs = [np.empty(each + 65536, dtype=np.uint8) for _ in range(nh)]
+    resm = [None] * nh
+    st0 = zstreams.stream_stats()
+    th = [threading.Thread(target=run_one, args=(cs[k], rs[k], outs[k], resm, k)) for k in range(nh)]
+    t0 = time.perf_counter()
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    tm = time.perf_counter() - t0
+    st1 = zstreams.stream_stats()
+    launches = st1["launches"] - st0["launches"]
+    calls_m = st1["calls"] - st0["calls"]
+    okm = all(resm[k] is not None and resm[k][0] == each and resm[k][1] == 1 and np.array_equal(outs[k][:each], rs[k])
+              for k in range(nh))
+
+    # host zlib, same schedule: the one stream on 1 thread; the handle set on all cores
+    C = _cpulib()
+    P, S = ctypes.POINTER, ctypes.c_size_t
+    C.zs_cpu_inflate_js.restype = ctypes.c_double
+    C.zs_cpu_inflate_js.argtypes = [P(ctypes.c_void_p), P(S), P(ctypes.c_void_p), S, ctypes.c_int, ctypes.c_int,
+                                    ctypes.c_int, S, P(ctypes.c_uint64), P(ctypes.c_int)]
+
+    def cpu_js(comps, nthreads, cap):
+        bufs = [np.empty(cap + 65536, dtype=np.uint8) for _ in range(nthreads)]
+        cp = (ctypes.c_void_p * len(comps))(*[c.ctypes.data for c in comps])
+        cl = (S * len(comps))(*[len(c) for c in comps])
+        op = (ctypes.c_void_p * nthreads)(*[b.ctypes.data for b in bufs])
+        tot, bad = ctypes.c_uint64(0), ctypes.c_int(0)
+        t = C.zs_cpu_inflate_js(cp, cl, op, cap + 65536, len(comps), nthreads, -15, ws, ctypes.byref(tot),
+                                ctypes.byref(bad))
+        return tot.value / t / 2**20, bool(not bad.value)
+
+    reps = max(1, int(2e9 // one_bytes))
+    c1v, c1ok = cpu_js([comp1] * reps, 1, one_bytes)
+    thr = max(1, min(cpu["physical_cores"], nh))
+    cmv, cmok = cpu_js(cs, thr, each)
+    mib1 = one_bytes / t1 / 2**20
+    mibm = nh * each / tm / 2**20
+    return {
+        "metric": "MiB/s decompressed through the handle ABI (inflate_process), reference JS call schedule",
+        "schedule": "64 KiB writes, <= 32 KiB per inflate_process, 64 KiB out, advance by inflate_last_consumed, "
+                    "Z_FINISH drain (src/wasm/api/zlib-streams.js:64-136)",
+        "one_handle": {"value": round(mib1, 1), "unit": "MiB/s", "stream": f"line text {args.stream_leg_mib} MiB, "
+                       "host zlib L6 raw (-15)", "calls": calls1, "us_per_call": round(t1 * 1e6 / calls1, 1),
+                       "verified": bool(ok1)},
+        "handles": {"value": round(mibm, 1), "unit": "MiB/s (aggregate)", "handles": nh,
+                    "stream": f"{nh} x {args.stream_handle_mib} MiB line text (ids 32..), one host thread per handle",
+                    "launches": launches, "calls_per_launch": round(calls_m / max(1, launches), 1),
+                    "verified": bool(okm)},
+        "wasm_reference_mibs": 493,
+        "cpu_baseline": {"one_handle": round(c1v, 1), "handles_all_cores": round(cmv, 1), "threads": thr,
+                         "unit": "MiB/s", "kind": "reference",
+                         "impl": "host zlib 1.2.11 inflate, same call schedule (the shipped WASM runs this loop)",
+                         "verified": bool(c1ok and cmok)},
+    }
 
 
 D64_FIXTURES = ("100k_lines", "10k_lines", "payload_63k", "payload_64k", "payload_65k", "rand_block_gap",

@@ -30,6 +30,10 @@
  *     buffer after inflateInit2(strm, window_bits) (src/inflate.c:186, 597):
  *     same ret, msg, total_in, total_out and adler.
  *
+ * Surfaces 1 and 2 are thread-safe across handles (a handle, like a z_stream,
+ * belongs to one thread at a time): concurrent calls of different handles are
+ * batched into shared GPU launches.
+ *
  * All decoding runs on the GPU (HIP, gfx950).  There is no CPU fallback: if no
  * HIP device is usable every entry point fails with Z_STREAM_ERROR /
  * ZS_ENODEV and zs_last_error() says why.
@@ -165,6 +169,10 @@ int zs_kprof_read(uint64_t *out, uint32_t n, int reset);
    chunked jobs whose chain did not verify (decoded by the serial decoder
    instead), jobs routed to the serial decoder] */
 int zs_last_stats(uint32_t out[4]);
+/* stream-call batching since load: [launch sequences, calls they ran].  Calls of
+   the handle / zlib ABIs made at the same time from different threads (one
+   handle per thread) share one launch, a workgroup per call. */
+int zs_stream_stats(uint64_t out[2]);
 const char *zs_version(void);
 const char *zs_last_error(void);
 

@@ -174,3 +174,90 @@ double zs_cpu_deflate_pt(const uint8_t *const *raw, const size_t *raw_len, uint8
                          size_t comp_cap, int n, int nthreads, int level, int wbits, uint64_t *total_in, int *bad) {
   return deflate_timed(raw, raw_len, comp, comp_len, comp_cap, n, nthreads, level, wbits, 1, total_in, bad);
 }
+
+/* The reference's stream call schedule on host zlib (src/wasm/api/zlib-streams.js:64-136 over
+ * wasm_stream_common.c:37-63): writes of `write_size` bytes, each fed in <= 32 KiB slices to
+ * inflate(Z_NO_FLUSH) with a 64 KiB output buffer, advancing by the bytes consumed and stopping
+ * a write on consumed == 0; then Z_FINISH drains.  Output lands consecutively in `out`.  Streams
+ * dealt round-robin to `nthreads` threads (out[k] per thread).  Returns wall seconds. */
+typedef struct {
+  const uint8_t *const *comp;
+  const size_t *comp_len;
+  uint8_t *const *out;
+  size_t out_cap, write_size;
+  int n, nthreads, tid, wbits;
+  uint64_t produced;
+  int bad;
+} stask_t;
+
+static void *srun(void *arg) {
+  stask_t *t = (stask_t *)arg;
+  for (int i = t->tid; i < t->n; i += t->nthreads) {
+    z_stream z;
+    memset(&z, 0, sizeof z);
+    inflateInit2(&z, t->wbits);
+    uint8_t *dst = t->out[t->tid];
+    size_t put = 0;
+    int r = Z_OK;
+    for (size_t w = 0; w < t->comp_len[i] && r >= 0 && r != Z_STREAM_END; w += t->write_size) {
+      const size_t len = t->comp_len[i] - w < t->write_size ? t->comp_len[i] - w : t->write_size;
+      size_t off = 0;
+      while (off < len) {
+        const size_t n = len - off < 32768 ? len - off : 32768;
+        size_t room = t->out_cap - put < 65536 ? t->out_cap - put : 65536;
+        z.next_in = (Bytef *)(t->comp[i] + w + off);
+        z.avail_in = (uInt)n;
+        z.next_out = dst + put;
+        z.avail_out = (uInt)room;
+        r = inflate(&z, Z_NO_FLUSH);
+        const size_t consumed = n - z.avail_in;
+        put += room - z.avail_out;
+        if (r < 0 && r != Z_BUF_ERROR) break;
+        if (consumed == 0) break;
+        off += consumed;
+      }
+    }
+    for (;;) {
+      size_t room = t->out_cap - put < 65536 ? t->out_cap - put : 65536;
+      z.next_in = NULL;
+      z.avail_in = 0;
+      z.next_out = dst + put;
+      z.avail_out = (uInt)room;
+      r = inflate(&z, Z_FINISH);
+      const size_t got = room - z.avail_out;
+      put += got;
+      if (r < 0 || r == Z_STREAM_END || got == 0) break;
+    }
+    t->produced += put;
+    t->bad |= r != Z_STREAM_END;
+    inflateEnd(&z);
+  }
+  return NULL;
+}
+
+double zs_cpu_inflate_js(const uint8_t *const *comp, const size_t *comp_len, uint8_t *const *out, size_t out_cap, int n,
+                         int nthreads, int wbits, size_t write_size, uint64_t *total_out, int *bad) {
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 1024) nthreads = 1024;
+  stask_t *ts = (stask_t *)calloc((size_t)nthreads, sizeof(stask_t));
+  pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
+  struct timespec a, b;
+  clock_gettime(CLOCK_MONOTONIC, &a);
+  for (int k = 0; k < nthreads; k++) {
+    ts[k] = (stask_t){comp, comp_len, out, out_cap, write_size, n, nthreads, k, wbits, 0, 0};
+    pthread_create(&th[k], NULL, srun, &ts[k]);
+  }
+  uint64_t tot = 0;
+  int anybad = 0;
+  for (int k = 0; k < nthreads; k++) {
+    pthread_join(th[k], NULL);
+    tot += ts[k].produced;
+    anybad |= ts[k].bad;
+  }
+  clock_gettime(CLOCK_MONOTONIC, &b);
+  free(ts);
+  free(th);
+  *total_out = tot;
+  *bad = anybad;
+  return (double)(b.tv_sec - a.tv_sec) + 1e-9 * (double)(b.tv_nsec - a.tv_nsec);
+}

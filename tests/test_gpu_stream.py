@@ -94,6 +94,28 @@ def test_js_schedule_traces_match_oracle(zs, write):
     assert not bad, bad[:3]
 
 
+def test_concurrent_handles_match_oracle(zs):
+    """Many handles driven at once from their own threads (the library batches
+    their calls into shared launches): every per-call trace and output still
+    equals the oracle's for that stream alone."""
+    from concurrent.futures import ThreadPoolExecutor
+    cases = _schedule_cases() * 2
+    writes = [4096 if i % 2 else 65536 for i in range(len(cases))]
+    before = zs.stream_stats()
+    with ThreadPoolExecutor(16) as ex:
+        got = list(ex.map(lambda a: zs.js_schedule(a[0][0], FMT[a[0][1]], a[1]), zip(cases, writes)))
+    after = zs.stream_stats()
+    bad = []
+    for i, ((data, wb), w, (tr, out)) in enumerate(zip(cases, writes, got)):
+        etr, eout = O.js_schedule(data, w, wb)
+        if tr != etr or out != eout:
+            bad.append((i, wb, w, tr[:200], etr[:200]))
+    assert not bad, bad[:3]
+    calls = after["calls"] - before["calls"]
+    launches = after["launches"] - before["launches"]
+    assert 0 < launches < calls  # some calls shared a launch
+
+
 def _gzip_header_all_fields(body_raw):
     """gzip member with FEXTRA, FNAME, FCOMMENT and FHCRC set."""
     hdr = bytearray(b"\x1f\x8b\x08\x1e") + struct.pack("<I", 12345) + b"\x00\x03"

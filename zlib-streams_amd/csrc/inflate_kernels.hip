@@ -1028,8 +1028,12 @@ template __global__ void zs_decode_kernel<true>(const ZsJobDev *, const ZsHeadDe
 // over from earlier calls + the new input) and the call's output buffer.
 // ---------------------------------------------------------------------------
 template <bool D64>
-__global__ void __launch_bounds__(64) zs_stream_kernel(ZsStreamDev *__restrict__ st, const ZsJobDev *__restrict__ job,
-                                                        const ZsHeadDev *__restrict__ head) {
+__global__ void __launch_bounds__(64) zs_stream_kernel(ZsStreamDev *const *__restrict__ sts, const ZsJobDev *__restrict__ jobs,
+                                                        const ZsHeadDev *__restrict__ heads) {
+  // one workgroup per call of the batch (calls of different handles; see zs_launch_stream)
+  ZsStreamDev *__restrict__ st = sts[blockIdx.x];
+  const ZsJobDev *__restrict__ job = jobs + blockIdx.x;
+  const ZsHeadDev *__restrict__ head = heads + blockIdx.x;
   constexpr uint32_t RING = D64 ? 65536u : 32768u;
   constexpr uint32_t WOFF = 65536u - RING;  // window bytes used: the newest RING
   __shared__ __attribute__((aligned(16))) uint8_t s_ring[RING];
@@ -1150,13 +1154,15 @@ __global__ void __launch_bounds__(64) zs_stream_kernel(ZsStreamDev *__restrict__
   }
 }
 
-template __global__ void zs_stream_kernel<false>(ZsStreamDev *, const ZsJobDev *, const ZsHeadDev *);
-template __global__ void zs_stream_kernel<true>(ZsStreamDev *, const ZsJobDev *, const ZsHeadDev *);
+template __global__ void zs_stream_kernel<false>(ZsStreamDev *const *, const ZsJobDev *, const ZsHeadDev *);
+template __global__ void zs_stream_kernel<true>(ZsStreamDev *const *, const ZsJobDev *, const ZsHeadDev *);
 
 // check contributions of the call's output (zs_check.h accumulators)
 #define SCHECK_THREADS 256
-__global__ void __launch_bounds__(SCHECK_THREADS) zs_stream_check_kernel(ZsStreamDev *__restrict__ st,
-                                                                         const ZsJobDev *__restrict__ job) {
+__global__ void __launch_bounds__(SCHECK_THREADS) zs_stream_check_kernel(ZsStreamDev *const *__restrict__ sts,
+                                                                         const ZsJobDev *__restrict__ jobs) {
+  ZsStreamDev *__restrict__ st = sts[blockIdx.y];
+  const ZsJobDev *__restrict__ job = jobs + blockIdx.y;
   __shared__ uint32_t s_tab[4][256];
   __shared__ uint64_t s_red[16];
   const uint32_t t = threadIdx.x;
@@ -1187,9 +1193,7 @@ __global__ void __launch_bounds__(SCHECK_THREADS) zs_stream_check_kernel(ZsStrea
 }
 
 // Running check, then the CHECK / LENGTH trailer states (src/inflate.c:1194-1232).
-__global__ void zs_stream_finish_kernel(ZsStreamDev *__restrict__ st, const ZsJobDev *__restrict__ job) {
-  if (threadIdx.x != 0) return;
-  ZsStreamDev &s = *st;
+__device__ void stream_finish(ZsStreamDev &s, const ZsJobDev *__restrict__ job) {
   if (s.mode == ZSM_HEAD || s.mode == ZSM_DICT || s.code == ZD_NEED_DICT) return;
   const int gz = s.is_gzip;
   const uint64_t n = s.produced;
@@ -1253,17 +1257,38 @@ __global__ void zs_stream_finish_kernel(ZsStreamDev *__restrict__ st, const ZsJo
   }
 }
 
-// One call: [wrapper header] -> resumable decode -> check -> trailers.
-extern "C" void zs_launch_stream(int d64, int run_header, ZsStreamDev *d_st, const ZsJobDev *d_job, ZsHeadDev *d_head,
-                                 uint64_t out_cap, hipStream_t stream) {
-  if (run_header) hipLaunchKernelGGL(zs_header_kernel, dim3(1), dim3(64), 0, stream, d_job, d_head, 1u);
+// The call's outcome, gathered for the host (one copy for the whole batch).
+__global__ void zs_stream_finish_kernel(ZsStreamDev *const *__restrict__ sts, const ZsJobDev *__restrict__ jobs,
+                                        ZsStreamRes *__restrict__ res) {
+  if (threadIdx.x != 0) return;
+  ZsStreamDev &s = *sts[blockIdx.x];
+  stream_finish(s, jobs + blockIdx.x);
+  ZsStreamRes r;
+  r.mode = s.mode;
+  r.rbit = s.rbit;
+  r.code = s.code;
+  r.msg = s.msg;
+  r.stop_bits = s.stop_bits;
+  r.produced = s.produced;
+  r.check = s.check;
+  r.is_gzip = s.is_gzip;
+  res[blockIdx.x] = r;
+}
+
+// One batch of calls, one per handle (the library funnels concurrent calls of
+// different handles into one launch): [wrapper headers] -> resumable decode
+// (a workgroup per call) -> checks -> trailers -> outcome gather.
+extern "C" void zs_launch_stream(int d64, int run_header, ZsStreamDev *const *d_sts, const ZsJobDev *d_jobs,
+                                 ZsHeadDev *d_heads, uint32_t n, uint64_t max_out_cap, ZsStreamRes *d_res,
+                                 hipStream_t stream) {
+  if (run_header) hipLaunchKernelGGL(zs_header_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, d_jobs, d_heads, n);
   if (d64)
-    hipLaunchKernelGGL(zs_stream_kernel<true>, dim3(1), dim3(64), 0, stream, d_st, d_job, d_head);
+    hipLaunchKernelGGL(zs_stream_kernel<true>, dim3(n), dim3(64), 0, stream, d_sts, d_jobs, d_heads);
   else
-    hipLaunchKernelGGL(zs_stream_kernel<false>, dim3(1), dim3(64), 0, stream, d_st, d_job, d_head);
-  const uint32_t pieces = (uint32_t)std::min<uint64_t>(1024, std::max<uint64_t>(1, (out_cap + 65535) / 65536));
-  hipLaunchKernelGGL(zs_stream_check_kernel, dim3(pieces), dim3(SCHECK_THREADS), 0, stream, d_st, d_job);
-  hipLaunchKernelGGL(zs_stream_finish_kernel, dim3(1), dim3(64), 0, stream, d_st, d_job);
+    hipLaunchKernelGGL(zs_stream_kernel<false>, dim3(n), dim3(64), 0, stream, d_sts, d_jobs, d_heads);
+  const uint32_t pieces = (uint32_t)std::min<uint64_t>(1024, std::max<uint64_t>(1, (max_out_cap + 65535) / 65536));
+  hipLaunchKernelGGL(zs_stream_check_kernel, dim3(pieces, n), dim3(SCHECK_THREADS), 0, stream, d_sts, d_jobs);
+  hipLaunchKernelGGL(zs_stream_finish_kernel, dim3(n), dim3(64), 0, stream, d_sts, d_jobs, d_res);
 }
 
 // ---------------------------------------------------------------------------

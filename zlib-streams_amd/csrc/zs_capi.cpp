@@ -12,6 +12,8 @@
 #include <zlib.h>
 
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -28,8 +30,9 @@ extern "C" void zs_launch_decode(int d64, const ZsJobDev *d_jobs, const ZsHeadDe
 extern "C" void zs_launch_finish(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, const ZsDecDev *d_decs,
                                  uint64_t *d_checks, ZsResultDev *d_res, uint32_t njobs, uint64_t max_out,
                                  hipStream_t stream);
-extern "C" void zs_launch_stream(int d64, int run_header, ZsStreamDev *d_st, const ZsJobDev *d_job, ZsHeadDev *d_head,
-                                 uint64_t out_cap, hipStream_t stream);
+extern "C" void zs_launch_stream(int d64, int run_header, ZsStreamDev *const *d_sts, const ZsJobDev *d_jobs,
+                                 ZsHeadDev *d_heads, uint32_t n, uint64_t max_out_cap, ZsStreamRes *d_res,
+                                 hipStream_t stream);
 extern "C" void zs_launch_fixed_tables(uint32_t *fixed, int d64, hipStream_t st);
 extern "C" void zs_launch_fixed_compact(uint32_t *fixed, hipStream_t st);
 extern "C" void zs_launch_deflate(ZsDJobDev *d_jobs, uint32_t njobs, ZsDSegDev *d_segs, uint32_t nseg, uint16_t *d_dist16,
@@ -605,7 +608,33 @@ struct StreamState {
   const char *msg = nullptr;
   uint32_t adler = 0;
   ZsStreamDev *d_st = nullptr;
+  // the handle's own call buffers and copy stream: calls of different handles
+  // (different host threads) copy concurrently and share batch launches
+  hipStream_t hs = nullptr;
+  uint8_t *d_in = nullptr, *d_out = nullptr;
+  size_t cap_in = 0, cap_out = 0;
+  uint8_t *h_in = nullptr, *h_out = nullptr;  // pinned staging (calls up to STAGE_MAX bytes)
+  size_t cap_hin = 0, cap_hout = 0;
 };
+
+constexpr size_t STAGE_MAX = 4u << 20;
+
+// pinned staging buffer of >= need bytes (need <= STAGE_MAX), else nullptr
+uint8_t *stage_buf(uint8_t **p, size_t *cap, size_t need) {
+  if (need > STAGE_MAX) return nullptr;
+  if (need > *cap) {
+    if (*p) (void)hipHostFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    const size_t c = std::max<size_t>(need, 128u << 10);
+    if (hipHostMalloc(reinterpret_cast<void **>(p), c, hipHostMallocDefault) != hipSuccess) {
+      *p = nullptr;
+      return nullptr;
+    }
+    *cap = c;
+  }
+  return *p;
+}
 
 size_t stream_fast_min() {
   static size_t v = [] {
@@ -615,23 +644,147 @@ size_t stream_fast_min() {
   return v;
 }
 
-struct StreamBufs {
-  ZsJobDev *d_job = nullptr;
-  ZsHeadDev *d_head = nullptr;
-  uint8_t *d_in = nullptr, *d_out = nullptr;
-  size_t cap_in = 0, cap_out = 0;
-} g_sb;
+// ---------------------------------------------------------------------------
+// Call batching.  A call's inputs are staged on its handle's stream, then the
+// call joins the pending queue; whichever caller finds no launch in flight
+// becomes the leader, takes every pending call (up to SQ_MAX) and runs them as
+// ONE launch sequence (zs_launch_stream: a workgroup per call), so concurrent
+// streams share the GPU instead of queueing behind a process-wide lock.  A
+// lone caller's batch is itself: no added latency.
+// ---------------------------------------------------------------------------
+constexpr size_t SQ_MAX = 2048;
+constexpr long SQ_GAP_US = 40;   // gathering: quiet gap that ends it
+constexpr long SQ_WAIT_US = 400; // gathering: longest wait
+
+struct StreamCall {
+  StreamState *s = nullptr;
+  ZsJobDev jb{};
+  int run_header = 0;
+  ZsStreamRes res{};
+  int err = 0;
+  std::string errmsg;
+  bool done = false;
+};
+
+struct StreamQueue {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::condition_variable arrive;  // a call joined the queue (a gathering leader waits on it)
+  std::vector<StreamCall *> pending;
+  bool busy = false;
+  size_t last_n = 0;  // calls in the previous launch
+  hipStream_t st = nullptr;
+  size_t cap = 0;
+  ZsJobDev *d_jobs = nullptr, *h_jobs = nullptr;
+  ZsHeadDev *d_heads = nullptr;
+  ZsStreamDev **d_sts = nullptr, **h_sts = nullptr;
+  ZsStreamRes *d_res = nullptr, *h_res = nullptr;
+  uint64_t launches = 0, calls = 0;  // zs_stream_stats
+} g_sq;
+
+// leader only (g_sq.busy): one launch sequence per decoder variant
+int sq_launch(std::vector<StreamCall *> &calls) {
+  if (!g_sq.st) HIP_OK(hipStreamCreateWithFlags(&g_sq.st, hipStreamNonBlocking));
+  const size_t n = calls.size();
+  if (n > g_sq.cap) {
+    const size_t c = std::max<size_t>(n, 64);
+    g_sq.cap = 0;
+    int r;
+    if ((r = grow_dev(&g_sq.d_jobs, c)) || (r = grow_host(&g_sq.h_jobs, c)) || (r = grow_dev(&g_sq.d_heads, c)) ||
+        (r = grow_dev(&g_sq.d_sts, c)) || (r = grow_host(&g_sq.h_sts, c)) || (r = grow_dev(&g_sq.d_res, c)) ||
+        (r = grow_host(&g_sq.h_res, c)))
+      return r;
+    g_sq.cap = c;
+  }
+  std::vector<size_t> order;
+  order.reserve(n);
+  size_t nstd = 0;
+  for (int d64 = 0; d64 < 2; d64++)
+    for (size_t i = 0; i < n; i++)
+      if ((calls[i]->s->cfg.d64 != 0) == (d64 != 0)) {
+        order.push_back(i);
+        nstd += d64 ? 0 : 1;
+      }
+  for (size_t k = 0; k < n; k++) {
+    g_sq.h_jobs[k] = calls[order[k]]->jb;
+    g_sq.h_sts[k] = calls[order[k]]->s->d_st;
+  }
+  const hipStream_t st = g_sq.st;
+  HIP_OK(hipMemcpyAsync(g_sq.d_jobs, g_sq.h_jobs, n * sizeof(ZsJobDev), hipMemcpyHostToDevice, st));
+  HIP_OK(hipMemcpyAsync(g_sq.d_sts, g_sq.h_sts, n * sizeof(ZsStreamDev *), hipMemcpyHostToDevice, st));
+  for (int d64 = 0; d64 < 2; d64++) {
+    const size_t k0 = d64 ? nstd : 0, k1 = d64 ? n : nstd;
+    if (k1 == k0) continue;
+    int run_header = 0;
+    uint64_t max_out = 0;
+    for (size_t k = k0; k < k1; k++) {
+      run_header |= calls[order[k]]->run_header;
+      max_out = std::max<uint64_t>(max_out, g_sq.h_jobs[k].out_cap);
+    }
+    zs_launch_stream(d64, run_header, g_sq.d_sts + k0, g_sq.d_jobs + k0, g_sq.d_heads + k0, (uint32_t)(k1 - k0),
+                     max_out, g_sq.d_res + k0, st);
+    HIP_OK(hipGetLastError());
+  }
+  HIP_OK(hipMemcpyAsync(g_sq.h_res, g_sq.d_res, n * sizeof(ZsStreamRes), hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  for (size_t k = 0; k < n; k++) calls[order[k]]->res = g_sq.h_res[k];
+  g_sq.launches++;
+  g_sq.calls += n;
+  return 0;
+}
+
+int sq_submit(StreamCall *c) {
+  std::unique_lock<std::mutex> lk(g_sq.mu);
+  g_sq.pending.push_back(c);
+  g_sq.arrive.notify_one();
+  while (!c->done) {
+    if (g_sq.busy) {
+      g_sq.cv.wait(lk);
+      continue;
+    }
+    g_sq.busy = true;
+    // Several streams were active in the previous launch: gather their next
+    // calls (callers stage inputs between launches) until none arrives for
+    // SQ_GAP or SQ_WAIT has passed; a lone stream launches at once.
+    if (g_sq.last_n > 1 && g_sq.pending.size() < g_sq.last_n) {
+      const auto t_end = std::chrono::steady_clock::now() + std::chrono::microseconds(SQ_WAIT_US);
+      for (;;) {
+        const size_t had = g_sq.pending.size();
+        const auto t = std::min(t_end, std::chrono::steady_clock::now() + std::chrono::microseconds(SQ_GAP_US));
+        g_sq.arrive.wait_until(lk, t, [&] { return g_sq.pending.size() > had; });
+        if (g_sq.pending.size() == had || g_sq.pending.size() >= g_sq.last_n ||
+            std::chrono::steady_clock::now() >= t_end)
+          break;
+      }
+    }
+    const size_t take = std::min(g_sq.pending.size(), SQ_MAX);
+    std::vector<StreamCall *> batch(g_sq.pending.begin(), g_sq.pending.begin() + take);
+    g_sq.pending.erase(g_sq.pending.begin(), g_sq.pending.begin() + take);
+    lk.unlock();
+    g_sq.last_n = std::max(batch.size(), g_sq.pending.size() + batch.size() / 2);
+    const int rc = sq_launch(batch);
+    const std::string msg = rc ? g_err : std::string();
+    lk.lock();
+    for (StreamCall *b : batch) {
+      b->err = rc;
+      b->errmsg = msg;
+      b->done = true;
+    }
+    g_sq.busy = false;
+    g_sq.cv.notify_all();
+  }
+  if (c->err) set_err(c->errmsg);
+  return c->err;
+}
 
 int stream_init(StreamState *s, int wbits) {
   ZsJobDev cfg{};
   if (!parse_wbits(wbits, &cfg)) return Z_STREAM_ERROR;
-  if (ws_init()) return Z_STREAM_ERROR;
-  if (!g_sb.d_job) {
-    if (hipMalloc(&g_sb.d_job, sizeof(ZsJobDev)) != hipSuccess || hipMalloc(&g_sb.d_head, sizeof(ZsHeadDev)) != hipSuccess) {
-      set_err("stream: device allocation failed");
-      return Z_MEM_ERROR;
-    }
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (ws_init()) return Z_STREAM_ERROR;
   }
+  if (!s->hs) HIP_OK(hipStreamCreateWithFlags(&s->hs, hipStreamNonBlocking));
   if (!s->d_st && hipMalloc(&s->d_st, sizeof(ZsStreamDev)) != hipSuccess) {
     s->d_st = nullptr;
     set_err("stream: device state allocation failed");
@@ -642,13 +795,20 @@ int stream_init(StreamState *s, int wbits) {
   h.mode = cfg.wrap == ZW_RAW ? ZSM_TYPE : ZSM_HEAD;
   h.wbits = (uint32_t)cfg.wbits;
   h.is_gzip = -1;
-  if (hipMemcpy(s->d_st, &h, offsetof(ZsStreamDev, lens), hipMemcpyHostToDevice) != hipSuccess) {
-    set_err("stream: state upload failed");
-    return Z_STREAM_ERROR;
-  }
-  ZsStreamDev *keep = s->d_st;
+  HIP_OK(hipMemcpyAsync(s->d_st, &h, offsetof(ZsStreamDev, lens), hipMemcpyHostToDevice, s->hs));
+  HIP_OK(hipStreamSynchronize(s->hs));
+  StreamState keep = std::move(*s);
   *s = StreamState();
-  s->d_st = keep;
+  s->d_st = keep.d_st;
+  s->hs = keep.hs;
+  s->d_in = keep.d_in;
+  s->d_out = keep.d_out;
+  s->cap_in = keep.cap_in;
+  s->cap_out = keep.cap_out;
+  s->h_in = keep.h_in;
+  s->h_out = keep.h_out;
+  s->cap_hin = keep.cap_hin;
+  s->cap_hout = keep.cap_hout;
   s->inited = 1;
   s->wbits = wbits;
   s->cfg = cfg;
@@ -658,8 +818,19 @@ int stream_init(StreamState *s, int wbits) {
 }
 
 void stream_free(StreamState *s) {
+  if (s->hs) (void)hipStreamSynchronize(s->hs);
   if (s->d_st) (void)hipFree(s->d_st);
+  if (s->d_in) (void)hipFree(s->d_in);
+  if (s->d_out) (void)hipFree(s->d_out);
+  if (s->h_in) (void)hipHostFree(s->h_in);
+  if (s->h_out) (void)hipHostFree(s->h_out);
+  if (s->hs) (void)hipStreamDestroy(s->hs);
+  s->h_in = s->h_out = nullptr;
+  s->cap_hin = s->cap_hout = 0;
   s->d_st = nullptr;
+  s->d_in = s->d_out = nullptr;
+  s->cap_in = s->cap_out = 0;
+  s->hs = nullptr;
 }
 
 // Whole-stream attempt through the batch pipeline; true when it settled the call.
@@ -672,7 +843,10 @@ bool stream_fast(StreamState *s, const uint8_t *in, unsigned in_len, uint8_t *ou
   j.out_cap = out_len;
   j.window_bits = s->wbits;
   zs_result r;
-  if (batch_locked(&j, 1, &r, 0) || (r.ret != Z_STREAM_END && r.ret != Z_DATA_ERROR)) return false;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (batch_locked(&j, 1, &r, 0) || (r.ret != Z_STREAM_END && r.ret != Z_DATA_ERROR)) return false;
+  }
   *consumed = (unsigned)r.total_in;
   *produced = (unsigned)r.total_out;
   *ret = r.ret;
@@ -699,33 +873,45 @@ int stream_call(StreamState *s, const uint8_t *in, unsigned in_len, uint8_t *out
     s->total_out += *produced;
     return fret;
   }
-  const hipStream_t st = g_ws.stream;
-  ZsStreamDev h;
+  const hipStream_t hs = s->hs;
+  ZsStreamRes h{};
   size_t off = 0;
   uint64_t cons = 0, prod = 0;
   for (;;) {
     const size_t take = std::min<size_t>(in_len - off, STREAM_SLICE);
     const size_t clen = s->carry.size();
     const size_t blen = clen + take;
-    if (ws_reserve_bytes(&g_sb.d_in, &g_sb.cap_in, std::max<size_t>(blen, 64)) ||
-        ws_reserve_bytes(&g_sb.d_out, &g_sb.cap_out, std::max<size_t>((size_t)out_len - prod, 64))) {
+    if (ws_reserve_bytes(&s->d_in, &s->cap_in, std::max<size_t>(blen, 64)) ||
+        ws_reserve_bytes(&s->d_out, &s->cap_out, std::max<size_t>((size_t)out_len - prod, 64))) {
       set_err("stream: device buffer allocation failed");
       return Z_MEM_ERROR;
     }
-    if (clen) HIP_OK(hipMemcpyAsync(g_sb.d_in, s->carry.data(), clen, hipMemcpyHostToDevice, st));
-    if (take) HIP_OK(hipMemcpyAsync(g_sb.d_in + clen, in + off, take, hipMemcpyHostToDevice, st));
-    ZsJobDev jb = s->cfg;
-    jb.in = g_sb.d_in;
-    jb.in_len = blen;
-    jb.out = g_sb.d_out;
-    jb.out_cap = (uint64_t)out_len - prod;
-    HIP_OK(hipMemcpyAsync(g_sb.d_job, &jb, sizeof jb, hipMemcpyHostToDevice, st));
-    HIP_OK(hipMemcpyAsync(&s->d_st->rbit, &s->carry_bit, sizeof(uint32_t), hipMemcpyHostToDevice, st));
-    zs_launch_stream(s->cfg.d64, s->mode == ZSM_HEAD, s->d_st, g_sb.d_job, g_sb.d_head, jb.out_cap, st);
-    HIP_OK(hipGetLastError());
-    HIP_OK(hipMemcpyAsync(&h, s->d_st, offsetof(ZsStreamDev, lens), hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
-    if (h.produced) HIP_OK(hipMemcpy(out + prod, g_sb.d_out, h.produced, hipMemcpyDeviceToHost));
+    if (uint8_t *hb = stage_buf(&s->h_in, &s->cap_hin, blen)) {  // one DMA from pinned staging
+      if (clen) std::memcpy(hb, s->carry.data(), clen);
+      if (take) std::memcpy(hb + clen, in + off, take);
+      if (blen) HIP_OK(hipMemcpyAsync(s->d_in, hb, blen, hipMemcpyHostToDevice, hs));
+    } else {
+      if (clen) HIP_OK(hipMemcpyAsync(s->d_in, s->carry.data(), clen, hipMemcpyHostToDevice, hs));
+      if (take) HIP_OK(hipMemcpyAsync(s->d_in + clen, in + off, take, hipMemcpyHostToDevice, hs));
+    }
+    HIP_OK(hipMemcpyAsync(&s->d_st->rbit, &s->carry_bit, sizeof(uint32_t), hipMemcpyHostToDevice, hs));
+    HIP_OK(hipStreamSynchronize(hs));
+    StreamCall c;
+    c.s = s;
+    c.jb = s->cfg;
+    c.jb.in = s->d_in;
+    c.jb.in_len = blen;
+    c.jb.out = s->d_out;
+    c.jb.out_cap = (uint64_t)out_len - prod;
+    c.run_header = s->mode == ZSM_HEAD;
+    if (int rc = sq_submit(&c)) return rc;
+    h = c.res;
+    if (h.produced) {
+      uint8_t *hb = stage_buf(&s->h_out, &s->cap_hout, h.produced);
+      HIP_OK(hipMemcpyAsync(hb ? hb : out + prod, s->d_out, h.produced, hipMemcpyDeviceToHost, hs));
+      HIP_OK(hipStreamSynchronize(hs));
+      if (hb) std::memcpy(out + prod, hb, h.produced);
+    }
     prod += h.produced;
     s->mode = h.mode;
     if (h.is_gzip >= 0) s->adler = h.check;
@@ -792,13 +978,11 @@ uintptr_t handle_new() {
 int handle_init(uintptr_t hp, int wbits) {
   Handle *h = reinterpret_cast<Handle *>(hp);
   if (!h) return Z_STREAM_ERROR;
-  std::lock_guard<std::mutex> lk(g_mu);
   return stream_init(&h->st, wbits);
 }
 int handle_process(uintptr_t hp, uintptr_t in_ptr, unsigned in_len, uintptr_t out_ptr, unsigned out_len, int flush) {
   Handle *h = reinterpret_cast<Handle *>(hp);
   if (!h || !h->st.inited) return (int)((unsigned)(Z_STREAM_ERROR & 0xff) << 24);
-  std::lock_guard<std::mutex> lk(g_mu);
   unsigned cons = 0, prod = 0;
   int ret = stream_call(&h->st, reinterpret_cast<const uint8_t *>(in_ptr), in_len, reinterpret_cast<uint8_t *>(out_ptr),
                         out_len, flush, &cons, &prod);
@@ -808,10 +992,7 @@ int handle_process(uintptr_t hp, uintptr_t in_ptr, unsigned in_len, uintptr_t ou
 int handle_end(uintptr_t hp) {
   Handle *h = reinterpret_cast<Handle *>(hp);
   if (!h) return Z_STREAM_ERROR;
-  {
-    std::lock_guard<std::mutex> lk(g_mu);
-    stream_free(&h->st);
-  }
+  stream_free(&h->st);
   delete h;
   return Z_OK;
 }
@@ -1276,6 +1457,13 @@ int zs_profile_stages(double *ms, uint32_t n) {
   return (int)k;
 }
 
+int zs_stream_stats(uint64_t out[2]) {
+  std::lock_guard<std::mutex> lk(g_sq.mu);
+  out[0] = g_sq.launches;
+  out[1] = g_sq.calls;
+  return 0;
+}
+
 int zs_last_stats(uint32_t out[4]) {
   std::lock_guard<std::mutex> lk(g_mu);
   for (int i = 0; i < 4; i++) out[i] = g_ws.stats[i];
@@ -1322,12 +1510,8 @@ int ZEXPORT inflateInit2_(z_streamp strm, int windowBits, const char *version, i
   if (!parse_wbits(windowBits, &probe)) return Z_STREAM_ERROR;
   StreamState *s = new (std::nothrow) StreamState();
   if (!s) return Z_MEM_ERROR;
-  int r;
-  {
-    std::lock_guard<std::mutex> lk(g_mu);
-    r = stream_init(s, windowBits);
-    if (r != Z_OK) stream_free(s);
-  }
+  const int r = stream_init(s, windowBits);
+  if (r != Z_OK) stream_free(s);
   if (r != Z_OK) {
     delete s;
     return r;
@@ -1347,7 +1531,6 @@ int ZEXPORT inflate(z_streamp strm, int flush) {
       (strm->next_in == Z_NULL && strm->avail_in != 0))
     return Z_STREAM_ERROR;
   StreamState *s = reinterpret_cast<StreamState *>(strm->state);
-  std::lock_guard<std::mutex> lk(g_mu);
   unsigned cons = 0, prod = 0;
   int ret = stream_call(s, strm->next_in, strm->avail_in, strm->next_out, strm->avail_out, flush, &cons, &prod);
   strm->next_in += cons;
@@ -1364,10 +1547,7 @@ int ZEXPORT inflate(z_streamp strm, int flush) {
 int ZEXPORT inflateEnd(z_streamp strm) {
   if (strm == Z_NULL || strm->state == Z_NULL) return Z_STREAM_ERROR;
   StreamState *s = reinterpret_cast<StreamState *>(strm->state);
-  {
-    std::lock_guard<std::mutex> lk(g_mu);
-    stream_free(s);
-  }
+  stream_free(s);
   delete s;
   strm->state = Z_NULL;
   return Z_OK;

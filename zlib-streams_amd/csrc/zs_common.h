@@ -293,6 +293,18 @@ struct ZsStreamDev {
   __attribute__((aligned(16))) uint8_t window[65536];  // last 64 KiB (32 KiB used unless deflate64) of output, oldest first
 };
 
+// Outcome of one stream call (device -> host, gathered per batch).
+struct ZsStreamRes {
+  int32_t mode;
+  uint32_t rbit;
+  int32_t code;
+  int32_t msg;
+  uint32_t stop_bits;
+  uint32_t produced;
+  uint32_t check;
+  int32_t is_gzip;
+};
+
 // Final per-job result (device -> host), zlib z_stream fields after the call.
 struct ZsResultDev {
   int32_t ret;

@@ -64,6 +64,7 @@ _SIGS = {
     "zs_profile_stages": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.c_uint32]),
     "zs_kprof_read": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32, ctypes.c_int]),
     "zs_last_stats": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint32)]),
+    "zs_stream_stats": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64)]),
     "zs_synchronize": (ctypes.c_int, []),
     "zs_version": (ctypes.c_char_p, []), "zs_last_error": (ctypes.c_char_p, []),
 }
@@ -377,6 +378,13 @@ def last_stats():
     a = (ctypes.c_uint32 * 4)()
     _check(lib().zs_last_stats(a))
     return {"chunked_jobs": a[0], "units": a[1], "fallback_jobs": a[2], "serial_jobs": a[3]}
+
+
+def stream_stats():
+    """Stream-call batching since load: launch sequences and the calls they ran."""
+    a = (ctypes.c_uint64 * 2)()
+    _check(lib().zs_stream_stats(a))
+    return {"launches": a[0], "calls": a[1]}
 
 
 def set_stream(hip_stream_handle):
