@@ -424,6 +424,115 @@ __device__ __forceinline__ bool lane_step(LaneState &s, const uint16_t *__restri
   return false;
 }
 
+// The common symbol, with few instructions and no divergent exits: literal /
+// length from the LDS root (codes longer than the root via the lane's compact
+// sub-tables in a wave-uniform side branch), length base / extra computed,
+// distance from the LDS root (the canonical tail in a side branch), one token.
+// Anything lane_step would treat differently -- end of block, invalid codes,
+// a full unit, a too-far distance, truncation, a deflate64 copy longer than a
+// token -- restores the lane's reader and runs lane_step itself, so results
+// are lane_step's by construction.  lane_step costs ~3x the instructions
+// (every divergent exit path is issued by the whole wave); at one wave per
+// SIMD the parse is issue- and latency-bound on exactly this loop.
+template <bool D64>
+__device__ __forceinline__ bool lane_step_fast(LaneState &s, const uint16_t *__restrict__ lt,
+                                               const uint16_t *__restrict__ dt, uint32_t *__restrict__ tb,
+                                               const uint32_t *__restrict__ dtl, const uint32_t *__restrict__ rp,
+                                               KpPhase &kp) {
+#if KP_ON
+  const uint64_t kq0 = KP_NOW();
+#endif
+  const uint64_t h0 = s.hold;
+  const uint32_t nb0 = s.nbits, wi0 = s.wi, rk0 = s.rk, nw0 = s.nw;
+  lane_refill(s, rp);
+  uint32_t e = lt[(uint32_t)s.hold & (LROOT_N - 1)];
+  uint32_t kind = e & 3u;
+  if (__builtin_expect(__ballot(kind == CK_SLOW) != 0, 0)) {
+#if KP_ON
+    const uint64_t kq = KP_NOW();
+#endif
+    if (kind == CK_SLOW) {  // as lane_step: zlib's 9-bit root / sub-table, compact, global
+      const uint32_t op = (e >> 2) & 15u;
+      uint32_t e2 = CK_SLOW;
+      if (op == OP_ROOT9) {
+        e2 = s.cl[(uint32_t)s.hold & 511u];
+        const uint32_t op2 = (e2 >> 2) & 15u;
+        if ((e2 & 3u) == CK_SLOW && op2) e2 = s.cl[(e2 >> 6) + (((uint32_t)s.hold >> 9) & ((1u << op2) - 1u))];
+      } else if (op) {
+        e2 = s.cl[(e >> 6) + (((uint32_t)s.hold >> s.lbits) & ((1u << op) - 1u))];
+      }
+      e = e2;
+      kind = e & 3u;
+    }
+#if KP_ON
+    kp.t[0] += KP_NOW() - kq;
+#endif
+  }
+  const uint32_t used = (e >> 2) & 15u, sym = e >> 6;
+  const bool isl = kind == CK_LEN;
+  // length code sym (0..28): base / extra of src/inftrees.c:59-64 (deflate64 285: 3 + 16 bits)
+  uint32_t xb = sym < 8u ? 0u : (sym < 28u ? (sym >> 2) - 1u : (D64 ? 16u : 0u));
+  xb = isl ? xb : 0u;
+  const uint32_t lbase = sym < 8u ? sym + 3u : (sym < 28u ? ((4u + (sym & 3u)) << xb) + 3u : (D64 ? 3u : 258u));
+  s.hold >>= used;
+  const uint32_t len = isl ? lbase + ((uint32_t)s.hold & ((1u << xb) - 1u)) : 1u;
+  s.hold >>= xb;
+  s.nbits -= used + xb;
+  lane_refill(s, rp);
+  uint32_t d = dt[(uint32_t)s.hold & (DROOT_N - 1)];
+  const bool dslow = isl && (d & 3u) == CK_SLOW;
+  if (__ballot(dslow)) {
+#if KP_ON
+    const uint64_t kq = KP_NOW();
+#endif
+    if (dslow) d = ((d >> 2) & 15u) ? dist_tail(dtl, (uint32_t)s.hold) : (uint32_t)CK_SLOW;
+#if KP_ON
+    kp.t[1] += KP_NOW() - kq;
+#endif
+  }
+  const uint32_t dused = (d >> 2) & 15u, dsym = d >> 6;
+  const uint32_t dx = dsym < 4u ? 0u : (dsym >> 1) - 1u;
+  const uint32_t dist = (dsym < 4u ? dsym + 1u : ((2u + (dsym & 1u)) << dx) + 1u) +
+                        ((uint32_t)(s.hold >> dused) & ((1u << dx) - 1u));
+  const uint32_t dcons = isl ? dused + dx : 0u;
+  s.hold >>= dcons;
+  s.nbits -= dcons;
+#if KP_ON
+  s.kp_steps++;
+#else
+  (void)kp;
+#endif
+  const bool exc = kind == CK_SLOW || kind == CK_EOB || (isl && (d & 3u) == CK_SLOW) || lane_pos(s) > s.limit ||
+                   s.pos + len > s.capx || (isl && dist > s.pos + s.whave) || (D64 && len > 0xffffu);
+  bool left = false;
+#if KP_ON
+  const uint64_t kq2 = KP_NOW();
+  const bool any_exc = __ballot(exc) != 0;
+#endif
+  if (exc) {
+    s.hold = h0;
+    s.nbits = nb0;
+    s.wi = wi0;
+    s.rk = rk0;
+    s.nw = nw0;
+#if KP_ON
+    s.kp_steps--;
+#endif
+    left = lane_step<D64>(s, lt, dt, tb, dtl, rp, kp);
+  } else {
+    tb[s.gk * WAVE] = isl ? ((len << 16) | (dist - 1u)) : sym;
+    s.gk++;
+    s.ntok++;
+    s.pos += len;
+  }
+#if KP_ON
+  const uint64_t kq3 = KP_NOW();
+  if (any_exc) kp.t[2] += kq3 - kq2;
+  kp.t[3] += kq3 - kq0;
+#endif
+  return left;
+}
+
 // Wave-uniform bit reader over the LDS-staged header bits.
 struct StageBits {
   const uint32_t *st;
@@ -920,11 +1029,18 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
     if (__ballot(s.mode == LM_SYM) == 0) break;
     s.gk = 0;
     if (s.mode == LM_SYM) {
+#if KP_ON
+      const uint64_t kf = KP_NOW();
+#endif
       lane_fill_ring(s, rp);
+#if KP_ON
+      __builtin_amdgcn_s_waitcnt(0);
+      kph.t[4] += KP_NOW() - kf;
+#endif
       // a step reads at most 2 more ring words and stores 1 token (2 for a
       // deflate64 copy longer than 65535)
       while (s.gk + (D64 ? 2u : 1u) <= GROUP && s.rk + 2 < RING)
-        if (lane_step<D64>(s, lt, dt, tb, dtl, rp, kph)) break;
+        if (lane_step_fast<D64>(s, lt, dt, tb, dtl, rp, kph)) break;
     }
     __builtin_amdgcn_wave_barrier();
 #if KP_ON
