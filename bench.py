@@ -689,7 +689,55 @@ def deflate64_leg(args, zstreams, torch, np, dev, rank):
                                        "deflate64 inflate; the reference build is unbuildable here)",
                                "sample": f"the {n}-fixture suite x {passes} passes, {tt:.1f} s on 1 thread",
                                "verified": not anybad}
+    leg["one_large_stream"] = deflate64_large(args, zstreams, torch, np, dev, rank)
     return leg
+
+
+def deflate64_large(args, zstreams, torch, np, dev, rank):
+    """One large deflate64 stream (a multi-GB ZIP entry in miniature): 64 MiB of line text
+    + Zipf text, compressed at windowBits -16 by the GPU deflate64 encoder (code-285 runs,
+    64 KiB window), then inflated alone on the block-parallel path and compared with the
+    input.  The oracle's C restatement (the reference's inflate9 semantics) decodes the same
+    stream on 1 host thread beside it, its output checked against the input too."""
+    import corpus
+    nb = 64 << 20
+    raw = corpus.stream(40, nb // 2) + corpus.stream(7, nb // 2)
+    comp, info = zstreams.deflate_batch([raw], -16, 6)[0]
+    ok = info["ret"] == 1
+    d_in = torch.from_numpy(np.frombuffer(comp, dtype=np.uint8).copy()).to(dev)
+    d_out = torch.empty(nb, dtype=torch.uint8, device=dev)
+
+    def step():
+        return zstreams.inflate_batch_device([d_in.data_ptr()], [len(comp)], [d_out.data_ptr()], [nb], -16)[0]
+
+    r = step()
+    torch.cuda.synchronize()
+    st = zstreams.last_stats()
+    ok = ok and r["ret"] == 1 and r["total_out"] == nb and bytes(d_out.cpu().numpy()) == raw
+    reps = max(3, args.steps)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        step()
+    torch.cuda.synchronize()
+    t_el = (time.perf_counter() - t0) / reps
+    out = {"value": round(nb / t_el / 2**20, 1), "unit": "MiB/s", "ms": round(t_el * 1e3, 3),
+           "stream": f"64 MiB (line text + Zipf), GPU deflate64 level 6 -> {len(comp)} bytes, "
+                     "verified by the oracle at -16", "path_stats": st, "verified": bool(ok)}
+    if rank == 0 and not args.no_cpu_baseline:
+        L = _cpulib()
+        a = np.frombuffer(comp, dtype=np.uint8)
+        ob = np.empty(nb, dtype=np.uint8)
+        cp = (ctypes.c_void_p * 1)(a.ctypes.data)
+        cl = (ctypes.c_size_t * 1)(len(a))
+        op = (ctypes.c_void_p * 1)(ob.ctypes.data)
+        tot, bad = ctypes.c_uint64(), ctypes.c_int()
+        tt = L.zs_cpu_inflate(cp, cl, op, nb, 1, 1, -16, 1, ctypes.byref(tot), ctypes.byref(bad))
+        port = tot.value / tt / 2**20
+        out["cpu_port_1t"] = round(port, 1)
+        out["oracle_verified"] = bool(not bad.value and tot.value == nb and bytes(ob) == raw)
+        out["gpu_vs_port_1t"] = round(out["value"] / port, 1)
+    return out
 
 
 def compress_leg(args, zstreams, shard, torch, np, dev, dist, raws, d_out, raw_ptrs, nbytes, zlib_raws, cpu, rank,

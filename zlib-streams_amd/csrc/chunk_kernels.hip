@@ -143,6 +143,9 @@ __device__ bool validate_header(const uint32_t *w, uint32_t end_byte, uint32_t b
       dn += nd;
       if (nd) dmax = max(dmax, v);
       if (have <= 256 && 256 < have + rep) eob = v;
+      // partial Kraft sums only grow: an over-subscribed code fails now rather
+      // than after all nlen + ndist lengths (most false candidates end here)
+      if (lk > 32768u || dk > 32768u) return false;
     }
     prev = v;
     have += rep;

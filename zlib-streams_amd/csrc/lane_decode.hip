@@ -220,9 +220,8 @@ __device__ __forceinline__ void lane_refill(LaneState &s, const uint32_t *__rest
     s.nw = rp[s.rk * WAVE];
   }
 }
-// group start: ring[0..RING) = input words wi .. wi + RING - 1 (masked)
-__device__ __forceinline__ void lane_fill_ring(LaneState &s, uint32_t *__restrict__ rp) {
-  uint32_t v[RING];
+// input words wi .. wi + RING - 1 (masked) into registers
+__device__ __forceinline__ void lane_load_ring(const LaneState &s, uint32_t (&v)[RING]) {
   if (s.wi + RING <= s.lastw) {  // all full words: 16-byte loads
     const uint32_t *src = (const uint32_t *)(s.w + s.wi);
 #pragma unroll
@@ -238,10 +237,18 @@ __device__ __forceinline__ void lane_fill_ring(LaneState &s, uint32_t *__restric
 #pragma unroll
     for (int q = 0; q < RING; q++) v[q] = in_word_g(s.w, s.wi + q, s.end_byte);
   }
+}
+__device__ __forceinline__ void lane_store_ring(LaneState &s, uint32_t *__restrict__ rp, const uint32_t (&v)[RING]) {
 #pragma unroll
   for (int q = 0; q < RING; q++) rp[q * WAVE] = v[q];
   s.nw = v[0];
   s.rk = 0;
+}
+// group start: ring[0..RING) = input words wi .. wi + RING - 1 (masked)
+__device__ __forceinline__ void lane_fill_ring(LaneState &s, uint32_t *__restrict__ rp) {
+  uint32_t v[RING];
+  lane_load_ring(s, v);
+  lane_store_ring(s, rp, v);
 }
 // bit position of the next unconsumed bit (wi = index of the prefetched word)
 __device__ __forceinline__ uint32_t lane_pos(const LaneState &s) { return s.wi * 32u - s.nbits; }
@@ -1007,6 +1014,8 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
   uint32_t *rp = &L.g.ring[0][lane];
   const uint32_t *dtl = L.dtail[lane];
   KpPhase kph = {{0, 0, 0, 0, 0}};
+  uint32_t pre[RING];
+  uint32_t pre_wi = ~0u;  // input word the prefetched group words start at
 #if KP_ON
   kp_init = KP_NOW() - kp_t0;
 #endif
@@ -1032,7 +1041,8 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
 #if KP_ON
       const uint64_t kf = KP_NOW();
 #endif
-      lane_fill_ring(s, rp);
+      if (s.wi == pre_wi) lane_store_ring(s, rp, pre);  // words loaded during the last flush
+      else lane_fill_ring(s, rp);
 #if KP_ON
       __builtin_amdgcn_s_waitcnt(0);
       kph.t[4] += KP_NOW() - kf;
@@ -1049,6 +1059,10 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
     kp_groups++;
     kp_wsteps += kp_wave_max(s.kp_steps - kp_st0);
 #endif
+    // the next group's input words, loaded while this group's tokens leave
+    // (the loads precede the stores, so waiting for them never waits for a store)
+    pre_wi = s.mode == LM_SYM ? s.wi : ~0u;
+    if (s.mode == LM_SYM) lane_load_ring(s, pre);
     const uint32_t g0 = s.ntok - s.gk;
     if (s.ntok <= s.tcap) {
 #pragma unroll
