@@ -71,7 +71,8 @@ def test_deflate64_reaches_64k_back(zs):
     assert oi["ret"] == 1 and out == data
 
 
-def test_deflate64_chunked_block_parallel(zs):
+@pytest.mark.parametrize("parse", ["lane", "wave"])
+def test_deflate64_chunked_block_parallel(zs, parse):
     """Large deflate64 streams take the block-parallel path (64 KiB history
     windows, 32 distance codes, code-285 copies split into tokens) with no
     serial fallback, and match the oracle at windowBits -16 (the reference's
@@ -82,7 +83,7 @@ def test_deflate64_chunked_block_parallel(zs):
     datas = [corpus.stream(3, 24 << 20),
              corpus.stream(35, 12 << 20) + bytes(3 << 20) + blk * 40 + corpus.stream(4, 2 << 20)]
     comps = [c for c, _ in zs.deflate_batch(datas, -16, 6)]
-    got = zs.inflate_batch(comps, -16, [len(d) for d in datas])
+    got = zs.inflate_batch(comps, -16, [len(d) for d in datas], parse=parse)
     st = zs.last_stats()
     for d, c, (out, info) in zip(datas, comps, got):
         eo, ei = O.oneshot(c, -16, len(d))

@@ -29,12 +29,12 @@ def zs():
     return zstreams
 
 
-def run_and_compare(zs, cases):
+def run_and_compare(zs, cases, parse=None):
     """cases: list of (data, wbits, cap).  One GPU batch; every job vs the oracle."""
     streams = [c[0] for c in cases]
     wbs = [c[1] for c in cases]
     caps = [c[2] for c in cases]
-    got = zs.inflate_batch(streams, wbs, caps)
+    got = zs.inflate_batch(streams, wbs, caps, parse=parse)
     bad = []
     for i, (c, (out, info)) in enumerate(zip(cases, got)):
         eo, ei = O.oneshot(c[0], c[1], c[2])
@@ -193,9 +193,12 @@ def _big_cases(rng, n, lo=1 << 20, hi=6 << 20):
     return cases
 
 
-def test_chunked_path_exact_and_taken(zs):
+@pytest.mark.parametrize("parse", ["lane", "wave"])
+def test_chunked_path_exact_and_taken(zs, parse):
+    """Both parse modes of the block-parallel path (a lane per decode unit, a
+    wave per unit) take every stream and give the same exact results."""
     cases = _big_cases(random.Random(5), 8)
-    got = zs.inflate_batch([c[1] for c in cases], [c[2] for c in cases], [len(c[0]) for c in cases])
+    got = zs.inflate_batch([c[1] for c in cases], [c[2] for c in cases], [len(c[0]) for c in cases], parse=parse)
     st = zs.last_stats()
     assert st["chunked_jobs"] == len(cases), st
     for (raw, comp, wb), (out, info) in zip(cases, got):
@@ -204,7 +207,8 @@ def test_chunked_path_exact_and_taken(zs):
     assert st["fallback_jobs"] == 0, st
 
 
-def test_chunked_path_errors_match_oracle(zs):
+@pytest.mark.parametrize("parse", ["lane", "wave"])
+def test_chunked_path_errors_match_oracle(zs, parse):
     rng = random.Random(6)
     base = _big_cases(rng, 6, 600 << 10, 2 << 20)
     cases = []
@@ -218,7 +222,7 @@ def test_chunked_path_errors_match_oracle(zs):
             b = b[:rng.randrange(len(b) // 2, len(b))]
         cap = len(raw) if rng.random() < 0.7 else rng.randint(len(raw) // 2, len(raw))
         cases.append((bytes(b), wb, cap))
-    run_and_compare(zs, cases)
+    run_and_compare(zs, cases, parse)
 
 
 def test_chunked_random_and_stored(zs):

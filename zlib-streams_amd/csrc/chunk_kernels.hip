@@ -980,6 +980,30 @@ __global__ void __launch_bounds__(EMIT_THREADS) zs_emit_kernel(const ZsJobDev *_
 // (literal byte, or 256 + w for byte w of the unit's 64 KiB history).
 // ---------------------------------------------------------------------------
 #define H64 65536u
+// Thread t owns window entries 4t + 4096 g + {0..3}, g < 16: its 64 entries
+// of a chain member are loaded together (16 x 16 B, issued back to back) so a
+// step pays one memory latency, not one per entry.
+#define L64_G (H64 / LINK_THREADS / 4)
+__device__ __forceinline__ void link64_load(const uint16_t *__restrict__ scratch, const ZsLinkInfo &li, uint32_t t,
+                                            uint4 (&v)[L64_G]) {
+  const uint32_t *E = reinterpret_cast<const uint32_t *>(scratch + li.scratch);
+  const uint32_t n = li.n_out;
+  if (n >= H64) {
+    const uint32_t *b = E + (n - H64);  // 4-byte aligned
+#pragma unroll
+    for (int g = 0; g < L64_G; g++) __builtin_memcpy(&v[g], b + (uint32_t)g * (LINK_THREADS * 4) + t * 4, 16);
+  } else {  // short unit: entry i exists only for i >= H64 - n
+#pragma unroll
+    for (int g = 0; g < L64_G; g++) {
+      const uint32_t i = (uint32_t)g * (LINK_THREADS * 4) + t * 4;
+      uint32_t x[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) x[k] = (i + k + n >= H64) ? E[i + k + n - H64] : 0u;
+      v[g] = make_uint4(x[0], x[1], x[2], x[3]);
+    }
+  }
+}
+
 __global__ void __launch_bounds__(LINK_THREADS) zs_link64_kernel(ZsCJobDev *__restrict__ cjobs, const uint16_t *__restrict__ scratch,
                                                                  uint8_t *__restrict__ windows, const ZsLinkInfo *__restrict__ info,
                                                                  uint32_t *__restrict__ fallback) {
@@ -992,9 +1016,11 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_link64_kernel(ZsCJobDev *__re
   uint32_t wv = 0;
   int cur = 0;
   bool bad = false;
+  uint4 v[L64_G];
+  ZsLinkInfo li = info[cj.unit0];
   for (uint32_t j = 0; j < cj.nchain; j++) {
-    const ZsLinkInfo li = info[cj.unit0 + j];
-    const uint32_t *E = reinterpret_cast<const uint32_t *>(scratch + li.scratch);
+    link64_load(scratch, li, t, v);
+    const ZsLinkInfo lin = j + 1 < cj.nchain ? info[cj.unit0 + j + 1] : li;
     const uint32_t n = li.n_out;
     uint8_t *W = s_win[cur];
     uint8_t *W2 = s_win[cur ^ 1];
@@ -1005,24 +1031,29 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_link64_kernel(ZsCJobDev *__re
     }
     const uint32_t keep = n < H64 ? H64 - n : 0u;
     const uint32_t lowest = H64 - wv;
-    for (uint32_t i = t; i < H64; i += LINK_THREADS) {
-      uint32_t b;
-      if (i < keep) {
-        b = W[i + n];
-      } else {
-        const uint32_t x = E[i + n - H64];
-        if (x < MARK_BASE) {
-          b = x;
+#pragma unroll
+    for (int g = 0; g < L64_G; g++) {
+      const uint32_t i0 = (uint32_t)g * (LINK_THREADS * 4) + t * 4;
+      const uint32_t xs[4] = {v[g].x, v[g].y, v[g].z, v[g].w};
+      uint32_t b[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const uint32_t i = i0 + k, x = xs[k];
+        if (i < keep) {
+          b[k] = W[i + n];
+        } else if (x < MARK_BASE) {
+          b[k] = x;
         } else {
           const uint32_t wx = x - MARK_BASE;
           bad |= wx < lowest;
-          b = W[wx & (H64 - 1)];
+          b[k] = W[wx & (H64 - 1)];
         }
       }
-      W2[i] = (uint8_t)b;
+      *reinterpret_cast<uint32_t *>(W2 + i0) = b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
     }
     wv = min(H64, wv + n);
     cur ^= 1;
+    li = lin;
     __syncthreads();
   }
   if (bad) s_bad = 1;
@@ -1065,7 +1096,7 @@ extern "C" void zs_launch_fixed_tables(uint32_t *fixed, int d64, hipStream_t st)
 
 extern "C" void zs_launch_parse(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, ZsChunkDev *d_chunks, uint32_t nchunks,
                                 uint32_t *d_tokens, uint32_t *d_tables, const uint32_t *d_fixed, ZsTokPool pool, int d64,
-                                hipStream_t st);
+                                int wave_units, hipStream_t st);
 extern "C" void zs_launch_expand(const ZsJobDev *d_jobs, ZsChunkDev *d_chunks, uint32_t nchunks, uint16_t *d_scratch,
                                  const uint32_t *d_tokens, ZsTokPool pool, uint32_t *d_fallback, int d64, hipStream_t st);
 
@@ -1075,7 +1106,7 @@ extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_hea
                                   ZsCJobDev *d_cjobs, uint32_t ncjobs, ZsChunkDev *d_units, uint32_t nunit_slots,
                                   uint16_t *d_scratch, uint32_t *d_tokens, ZsTokPool pool, uint32_t *d_tables,
                                   const uint32_t *d_fixed, uint8_t *d_windows, void *d_linkinfo, ZsDecDev *d_decs,
-                                  uint32_t *d_fallback, int d64, hipStream_t st, hipEvent_t *ev) {
+                                  uint32_t *d_fallback, int d64, int wave_units, hipStream_t st, hipEvent_t *ev) {
   // ev (profiling, optional): [0] before find, [1] after find + plan, [2] after
   // parse + chain, [3] after expand, [4] after link, [5] after emit
   if (ev) (void)hipEventRecord(ev[0], st);
@@ -1087,7 +1118,7 @@ extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_hea
   hipLaunchKernelGGL(zs_plan_kernel, dim3(ncjobs), dim3(PLAN_T), 0, st, d_jobs, d_heads, d_segs, d_cjobs, d_units, pool);
   if (ev) (void)hipEventRecord(ev[1], st);
   ZsLinkInfo *info = reinterpret_cast<ZsLinkInfo *>(d_linkinfo);
-  zs_launch_parse(d_jobs, d_heads, d_units, nunit_slots, d_tokens, d_tables, d_fixed, pool, d64, st);
+  zs_launch_parse(d_jobs, d_heads, d_units, nunit_slots, d_tokens, d_tables, d_fixed, pool, d64, wave_units, st);
   hipLaunchKernelGGL(zs_chain_kernel, dim3(ncjobs), dim3(LINK_THREADS), 0, st, d_jobs, d_heads, d_units, d_cjobs, info,
                      d_decs, d_fallback);
   if (ev) (void)hipEventRecord(ev[2], st);

@@ -743,10 +743,11 @@ __device__ int wave_dyn_header(BuildLDS &B, const uint32_t *w, uint32_t end_byte
 }
 
 // Install compact roots for lane ln from zlib tables zl (root bits lb) and zd (db).
-__device__ void install_roots(LaneLDS &L, uint32_t ln, const uint32_t *zl, uint32_t lb, const uint32_t *zd, uint32_t db) {
+__device__ void install_roots(uint16_t *lroot, uint16_t *droot, const uint32_t *zl, uint32_t lb, const uint32_t *zd,
+                              uint32_t db) {
   const uint32_t lane = lane_id();
-  for (uint32_t i = lane; i < LROOT_N; i += WAVE) L.lroot[ln][i] = lds_len_root(zl, lb, i);
-  L.droot[ln][lane] = compact_dist_entry(zd[lane & ((1u << db) - 1u)]);
+  for (uint32_t i = lane; i < LROOT_N; i += WAVE) lroot[i] = lds_len_root(zl, lb, i);
+  droot[lane] = compact_dist_entry(zd[lane & ((1u << db) - 1u)]);
   __builtin_amdgcn_wave_barrier();
 }
 
@@ -754,7 +755,8 @@ __device__ void install_roots(LaneLDS &L, uint32_t ln, const uint32_t *zl, uint3
 // the same ln): end/stop checks, stored blocks, fixed and dynamic headers
 // (src/inflate.c:834-1033); installs the lane's tables.
 template <bool D64>
-__device__ void coop_block(LaneState &s, uint32_t ln, LaneLDS &L, uint32_t *lane_tab, const uint32_t *fixed,
+__device__ void coop_block(LaneState &s, uint32_t ln, BuildLDS &LB, uint16_t *lroot_ln, uint16_t *droot_ln,
+                           uint32_t *dtail_ln, uint32_t *lane_tab, const uint32_t *fixed,
                            uint32_t *tokens, const ZsTokPool &pool, const ZsChunkDev *units) {
   const uint32_t lane = lane_id();
   const uint32_t *w = reinterpret_cast<const uint32_t *>(readlane_ptr((const void *)(uintptr_t)s.w, ln));
@@ -803,7 +805,7 @@ __device__ void coop_block(LaneState &s, uint32_t ln, LaneLDS &L, uint32_t *lane
       break;
     }
     StageBits sb;
-    stage_bits(L.b, w, end_byte, bit, sb);
+    stage_bits(LB, w, end_byte, bit, sb);
     const uint32_t hdr = sb.peek(bit, 3);
     last = hdr & 1;
     const uint32_t type = hdr >> 1;
@@ -814,7 +816,7 @@ __device__ void coop_block(LaneState &s, uint32_t ln, LaneLDS &L, uint32_t *lane
         code = ZD_TRUNC;
         break;
       }
-      stage_bits(L.b, w, end_byte, bit, sb);
+      stage_bits(LB, w, end_byte, bit, sb);
       const uint32_t v = sb.peek(bit, 32);
       if ((v & 0xffffu) != ((v >> 16) ^ 0xffffu)) {
         code = ZD_ERROR | (ZM_STORED_LEN << 8);
@@ -867,7 +869,7 @@ __device__ void coop_block(LaneState &s, uint32_t ln, LaneLDS &L, uint32_t *lane
       cd = cl + 512;
       lbits = 9;
       dbits = 5;
-      install_roots(L, ln, zl, lbits, zd, dbits);
+      install_roots(lroot_ln, droot_ln, zl, lbits, zd, dbits);
       mode = LM_SYM;
       break;
     }
@@ -876,8 +878,8 @@ __device__ void coop_block(LaneState &s, uint32_t ln, LaneLDS &L, uint32_t *lane
       break;
     }
     {
-      const int hc = wave_dyn_header<D64>(L.b, w, end_byte, bit, tabg, ctab, lbits, dbits, L.lroot[ln], L.droot[ln],
-                                     reinterpret_cast<uint8_t *>(L.dtail[ln]));
+      const int hc = wave_dyn_header<D64>(LB, w, end_byte, bit, tabg, ctab, lbits, dbits, lroot_ln, droot_ln,
+                                     reinterpret_cast<uint8_t *>(dtail_ln));
       if (hc) {
         code = hc;
         break;
@@ -1028,7 +1030,7 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
     while (need) {
       const uint32_t ln = (uint32_t)__builtin_ctzll(need);
       need &= need - 1;
-      coop_block<D64>(s, ln, L, lane_tab, fixed, tokens, pool, chunks);
+      coop_block<D64>(s, ln, L.b, L.lroot[ln], L.droot[ln], L.dtail[ln], lane_tab, fixed, tokens, pool, chunks);
     }
 #if KP_ON
     const uint64_t kc1 = KP_NOW();
@@ -1108,6 +1110,335 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
     ch->end_bit = (s.code == ZD_END || s.code == ZD_STOP) ? s.bit : 0u;
     ch->n_out = s.pos;
     ch->n_tok = s.ntok;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Parse pass, wave per unit (zs_unitw_kernel): for batches with few units
+// (one large stream, a handful of files) a lane per unit leaves the GPU idle
+// and every unit pays the lane decoder's serial latency.  Here a whole wave
+// decodes ONE unit: each window, lane j decodes the complete symbol starting
+// at bit P + j (zlib's two-level tables in LDS, shared by the wave), and a
+// uniform walk from P follows the true symbol boundaries through the window,
+// admitting symbols until the window ends or a symbol needs lane_step's
+// exceptional handling (end of block, invalid code, truncation, a full unit,
+// a too-far distance), which it applies exactly as lane_step decides it.
+// Block headers, stored blocks and unit stops go through coop_block, so the
+// unit's tokens, end bit, code, n_out and n_tok equal the lane decoder's.
+// ---------------------------------------------------------------------------
+#define UW_STG 64
+#define UW_SETS 1  // symbol offsets per lane per window (2: measured 28% slower, the walk dominates)
+struct UnitWLDS {
+  BuildLDS b;
+  uint16_t lroot[LROOT_N];  // coop_block's compact roots (not used by this decoder)
+  uint16_t droot[DROOT_N];
+  uint32_t dtail[DTAIL_BYTES / 4];
+  uint32_t lt[ZBUILD];  // current block: zlib literal/length table
+  uint32_t dt[594];     // ... and distance table
+  uint32_t stg[UW_STG + 8];  // staged input words (one global load per ~30 windows)
+};
+
+enum { UW_SYM = 0, UW_EOB = 1, UW_INVL = 2, UW_INVD = 3 };
+
+struct UwSym {
+  uint32_t kind, endr, len, dist, tok, dend;  // endr / dend: bits past the window start
+};
+
+// field f of offset set j at lane ql, wave-uniform
+__device__ __forceinline__ uint32_t uw_rl(const UwSym (&y)[UW_SETS], uint32_t UwSym::*f, uint32_t j, uint32_t ql) {
+  uint32_t v = __builtin_amdgcn_readlane(y[0].*f, ql);
+#pragma unroll
+  for (int k = 1; k < UW_SETS; k++)
+    if (j == (uint32_t)k) v = __builtin_amdgcn_readlane(y[k].*f, ql);
+  return v;
+}
+
+// the complete symbol in `hold` (its first bit at window bit rel)
+template <bool D64>
+__device__ __forceinline__ UwSym uw_decode(const uint32_t *lt, const uint32_t *dt, uint32_t lmask, uint32_t dmask,
+                                           uint64_t hold, uint32_t rel) {
+  UwSym r;
+  uint32_t e = lt[(uint32_t)hold & lmask];
+  uint32_t used = e_bits(e), op = e_op(e);
+  if (op != 0 && (op & 0xf0u) == 0) {
+    e = lt[e_val(e) + (((uint32_t)(hold >> used)) & ((1u << op) - 1u))];
+    used += e_bits(e);
+    op = e_op(e);
+  }
+  r.kind = UW_SYM;
+  r.endr = rel + used;
+  r.len = 1;
+  r.dist = 0;
+  r.tok = e_val(e);
+  r.dend = 0;
+  if (op & 32) {  // end of block (zlib's op 96 carries the invalid bit too)
+    r.kind = UW_EOB;
+  } else if (op & 64) {
+    r.kind = UW_INVL;
+  } else if (op != 0) {  // length: base + extra, then the distance
+    const uint32_t xb = op & (D64 ? 31u : 15u);
+    const uint64_t h1 = hold >> used;
+    r.len = e_val(e) + ((uint32_t)h1 & ((1u << xb) - 1u));
+    const uint64_t h2 = h1 >> xb;
+    uint32_t d = dt[(uint32_t)h2 & dmask];
+    uint32_t dused = e_bits(d), dop = e_op(d);
+    if ((dop & 0xf0u) == 0) {
+      d = dt[e_val(d) + (((uint32_t)(h2 >> dused)) & ((1u << dop) - 1u))];
+      dused += e_bits(d);
+      dop = e_op(d);
+    }
+    r.dend = rel + used + xb + dused;
+    if (dop & 64) {
+      r.kind = UW_INVD;
+    } else {
+      const uint32_t dx = dop & 15u;
+      r.dist = e_val(d) + ((uint32_t)(h2 >> dused) & ((1u << dx) - 1u));
+      r.endr = r.dend + dx;
+      r.tok = (r.len << 16) | (r.dist - 1u);
+    }
+  }
+  return r;
+}
+
+__device__ __forceinline__ uint32_t uni32(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+template <bool D64>
+__global__ void __launch_bounds__(64) zs_unitw_kernel(const ZsJobDev *__restrict__ jobs, const ZsHeadDev *__restrict__ heads,
+                                                       ZsChunkDev *__restrict__ chunks, uint32_t nchunks,
+                                                       uint32_t *__restrict__ tokens, uint32_t *__restrict__ tables,
+                                                       const uint32_t *__restrict__ fixed, const uint32_t *__restrict__ order,
+                                                       ZsTokPool pool) {
+  __shared__ UnitWLDS L;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t c = order[blockIdx.x];  // units by decreasing span
+  if (c >= nchunks) return;
+  const ZsChunkDev ch = chunks[c];
+  if (ch.start_bit == ZS_NONE || heads[ch.job].code != ZD_END) {
+    if (lane == 0) {
+      chunks[c].code = ZD_SKIP;
+      chunks[c].end_bit = 0;
+      chunks[c].n_out = 0;
+      chunks[c].n_tok = 0;
+    }
+    return;
+  }
+  const ZsJobDev jb = jobs[ch.job];
+  LaneState s;
+  const uintptr_t ip = reinterpret_cast<uintptr_t>(jb.in);
+  const uint32_t mis = (uint32_t)(ip & 3u);
+  s.w = (gcu32 *)(ip - mis);
+  s.end_byte = mis + (uint32_t)jb.in_len;
+  s.limit = s.end_byte * 8u;
+  s.tok = (gu32 *)(tokens + ch.tok);
+  s.tcap = ch.tcap;
+  s.unit = c;
+  s.cap = ch.cap;
+  s.capx = ch.cap;
+  s.whave = ch.ord == 0 ? 0u : (D64 ? 65536u : HIST);
+  s.bit = ch.start_bit;
+  s.stop = ch.stop_bit;
+  s.sidx = c + 1;
+  s.send = ch.first + ch.nunits;
+  s.mode = LM_BLOCK;
+  s.code = 0;
+  s.pos = 0;
+  s.ntok = 0;
+  s.last = 0;
+  s.gk = s.rk = 0;
+  s.wi = s.nw = s.nkeep = s.nbits = s.lastw = 0;
+  s.hold = 0;
+#if KP_ON
+  s.kp_steps = s.kp_slow_l = s.kp_slow_d = s.kp_refills = 0;
+#endif
+  uint32_t *lane_tab = tables + (size_t)c * TABLE_STRIDE;
+  s.zl = fixed;
+  s.zd = fixed + 512;
+  s.cl = s.cd = (gcu16 *)(lane_tab + TABLE_ENTRIES);
+  s.zlmask = s.zdmask = 0;
+  s.lbits = 9;
+  s.dbits = 5;
+  if (ch.hdr_info & 1u) {  // first header prebuilt by zs_unit_header_kernel
+    s.mode = LM_SYM;
+    s.last = (ch.hdr_info >> 1) & 1u;
+    s.bit = ch.hdr_bit;
+    s.zl = lane_tab;
+    s.zd = lane_tab + DIST_TABLE_OFF;
+    s.lbits = (ch.hdr_info >> 8) & 15u;
+    s.dbits = (ch.hdr_info >> 12) & 15u;
+  }
+  const uint64_t prim = ch.tok;
+  for (;;) {
+    if (s.mode == LM_BLOCK) {
+      coop_block<D64>(s, 0, L.b, L.lroot, L.droot, L.dtail, lane_tab, fixed, tokens, pool, chunks);
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // the header's global tables, read below
+      // coop_block left the outcome in lane 0: every lane takes it
+      s.pos = uni32(s.pos);
+      s.ntok = uni32(s.ntok);
+      s.last = (int)uni32((uint32_t)s.last);
+      s.bit = uni32(s.bit);
+      s.mode = (int)uni32((uint32_t)s.mode);
+      s.code = (int)uni32((uint32_t)s.code);
+      s.sidx = uni32(s.sidx);
+      s.stop = uni32(s.stop);
+      s.lbits = uni32(s.lbits);
+      s.dbits = uni32(s.dbits);
+      s.zl = reinterpret_cast<const uint32_t *>(readlane_ptr(s.zl, 0));
+      s.zd = reinterpret_cast<const uint32_t *>(readlane_ptr(s.zd, 0));
+    }
+    if (s.mode != LM_SYM) break;
+    // the block's tables into LDS
+    const bool fx = s.zl == fixed;
+    const uint32_t nl = fx ? 512u : ZBUILD, nd = fx ? 32u : (D64 ? 594u : 592u);
+    for (uint32_t i = lane; i < nl; i += WAVE) L.lt[i] = s.zl[i];
+    for (uint32_t i = lane; i < nd; i += WAVE) L.dt[i] = s.zd[i];
+    __syncthreads();
+    const uint32_t lmask = (1u << s.lbits) - 1u, dmask = (1u << s.dbits) - 1u;
+    uint32_t sbase = 0;
+    bool staged = false;
+    for (;;) {
+      const uint32_t P = s.bit;
+      // a window reads words P/32 .. P/32 + 2 UW_SETS + 3 (a symbol ends <= 64 UW_SETS - 1 + 60 bits past P)
+      if (!staged || (P >> 5) + 2 * UW_SETS + 4 > sbase + UW_STG + 8) {
+        __syncthreads();
+        sbase = P >> 5;
+        L.stg[lane] = in_word_g(s.w, sbase + lane, s.end_byte);
+        if (lane < 8) L.stg[UW_STG + lane] = in_word_g(s.w, sbase + UW_STG + lane, s.end_byte);
+        staged = true;
+        __syncthreads();
+      }
+      // each lane decodes the complete symbol(s) starting at bit P + lane
+      // (+ 64 j) (src/inffast.c:107-166 on zlib's tables)
+      const uint32_t base = (P & 31u) + 32u * ((P >> 5) - sbase);
+      UwSym y[UW_SETS];
+#pragma unroll
+      for (int j = 0; j < UW_SETS; j++) {
+        const uint32_t rel = lane + 64u * (uint32_t)j;
+        const uint32_t off = base + rel, k = off >> 5, sh = off & 31u;
+        const uint64_t ab = (uint64_t)L.stg[k] | ((uint64_t)L.stg[k + 1] << 32);
+        const uint64_t hold = sh ? ((ab >> sh) | ((uint64_t)L.stg[k + 2] << (64u - sh))) : ab;
+        y[j] = uw_decode<D64>(L.lt, L.dt, lmask, dmask, hold, rel);
+      }
+      // walk the true boundaries through the window: every value is
+      // wave-uniform (readlane), so the walk runs on the scalar unit
+      uint64_t chosen[UW_SETS] = {}, dbl[UW_SETS] = {};
+      uint32_t q = 0, pos = uni32(s.pos);
+      const uint32_t limit = uni32(s.limit), capx = uni32(s.capx), whave = uni32(s.whave);
+      bool exc = false;
+      // symbols that need lane_step's exceptional handling, per offset
+      uint64_t xm[UW_SETS];
+      uint32_t pk[UW_SETS];
+#pragma unroll
+      for (int j = 0; j < UW_SETS; j++) {
+        xm[j] = __ballot(y[j].kind != UW_SYM || P + y[j].endr > limit);
+        pk[j] = y[j].endr | (y[j].len << 8);  // endr < 256, len <= 65538
+      }
+      while (q < UW_SETS * WAVE) {
+        const uint32_t j = UW_SETS > 1 ? q >> 6 : 0u, ql = q & 63u;
+        uint64_t xj = xm[0];
+        uint32_t w, dq;
+        if (UW_SETS > 1) {
+#pragma unroll
+          for (int k = 1; k < UW_SETS; k++)
+            if (j == (uint32_t)k) xj = xm[k];
+        }
+        if ((xj >> ql) & 1u) {  // exactly as lane_step orders its checks
+          const uint32_t kq = uw_rl(y, &UwSym::kind, j, ql);
+          const uint32_t eq = uw_rl(y, &UwSym::endr, j, ql);
+          if (kq == UW_INVL) {  // invalid literal/length code: truncated or invalid by zlib's code length
+            s.code = P + eq > limit ? ZD_TRUNC : (ZD_ERROR | (ZM_LITLEN_CODE << 8));
+            s.mode = LM_DONE;
+          } else if (kq == UW_INVD) {
+            const uint32_t de = uw_rl(y, &UwSym::dend, j, ql);
+            s.code = P + de > limit ? ZD_TRUNC : (ZD_ERROR | (ZM_DIST_CODE << 8));
+            s.mode = LM_DONE;
+          } else if (P + eq > limit) {
+            s.code = ZD_TRUNC;
+            s.mode = LM_DONE;
+          } else {  // end of block
+            s.bit = P + eq;
+            s.mode = LM_BLOCK;
+          }
+          exc = true;
+          break;
+        }
+        {
+          uint32_t pv = __builtin_amdgcn_readlane(pk[0], ql), dv = __builtin_amdgcn_readlane(y[0].dist, ql);
+#pragma unroll
+          for (int k = 1; k < UW_SETS; k++)
+            if (j == (uint32_t)k) {
+              pv = __builtin_amdgcn_readlane(pk[k], ql);
+              dv = __builtin_amdgcn_readlane(y[k].dist, ql);
+            }
+          w = pv;
+          dq = dv;
+        }
+        const uint32_t lq = w >> 8, eq = w & 0xffu;
+        if (pos + lq > capx) {
+          s.code = ZD_FULL;
+          s.mode = LM_DONE;
+          exc = true;
+          break;
+        }
+        if (dq > pos + whave) {
+          s.code = ZD_ERROR | (ZM_TOO_FAR << 8);
+          s.mode = LM_DONE;
+          exc = true;
+          break;
+        }
+        chosen[j] |= 1ull << ql;
+        if (D64 && lq > 0xffffu) dbl[j] |= 1ull << ql;  // two tokens, same distance
+        pos = uni32(pos + lq);
+        q = uni32(eq);
+      }
+      // the admitted symbols' tokens, in window order
+      uint32_t nb[UW_SETS], nt = 0;
+#pragma unroll
+      for (int j = 0; j < UW_SETS; j++) {
+        nb[j] = nt;
+        nt += (uint32_t)__builtin_popcountll(chosen[j]) + (uint32_t)__builtin_popcountll(dbl[j]);
+      }
+      if (nt) {
+        const uint32_t ntok = uni32(s.ntok), tcap = uni32(s.tcap);
+        uint32_t okp = 1;
+        if (ntok + nt > tcap) {
+          if (lane == 0) okp = tok_ensure(pool, s.unit, tcap, ntok + nt) ? 1u : 0u;
+          okp = uni32(okp);
+          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+        }
+        if (!okp) {
+          s.code = ZD_FULL;
+          s.mode = LM_DONE;
+          break;
+        }
+        const uint64_t below = (1ull << lane) - 1ull;
+#pragma unroll
+        for (int j = 0; j < UW_SETS; j++) {
+          if ((chosen[j] >> lane) & 1u) {
+            const uint32_t x = ntok + nb[j] + (uint32_t)__builtin_popcountll(chosen[j] & below) +
+                               (uint32_t)__builtin_popcountll(dbl[j] & below);
+            if (D64 && ((dbl[j] >> lane) & 1u)) {
+              *tok_addr(pool, tokens, s.unit, prim, tcap, x) = (0xffffu << 16) | (y[j].dist - 1u);
+              *tok_addr(pool, tokens, s.unit, prim, tcap, x + 1) = ((y[j].len - 0xffffu) << 16) | (y[j].dist - 1u);
+            } else {
+              *tok_addr(pool, tokens, s.unit, prim, tcap, x) = y[j].tok;
+            }
+          }
+        }
+        s.ntok = ntok + nt;
+      }
+      s.pos = pos;
+      if (exc) break;
+      s.bit = P + q;
+    }
+    if (s.mode != LM_BLOCK) break;
+    __syncthreads();
+  }
+  if (lane == 0) {
+    ZsChunkDev *o = &chunks[c];
+    o->code = s.code;
+    o->end_bit = (s.code == ZD_END || s.code == ZD_STOP) ? s.bit : 0u;
+    o->n_out = s.pos;
+    o->n_tok = s.ntok;
   }
 }
 
@@ -1512,9 +1843,11 @@ int sort_units(const ZsJobDev *d_jobs, const ZsChunkDev *d_chunks, uint32_t n, i
 }
 }  // namespace
 
+// wave_units: decode with a wave per unit (zs_unitw_kernel) instead of a lane
+// per unit -- the host picks it when a batch has few units for the GPU.
 extern "C" void zs_launch_parse(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, ZsChunkDev *d_chunks, uint32_t nchunks,
                                 uint32_t *d_tokens, uint32_t *d_tables, const uint32_t *d_fixed, ZsTokPool pool, int d64,
-                                hipStream_t st) {
+                                int wave_units, hipStream_t st) {
   if (!nchunks) return;
   if (d64)
     hipLaunchKernelGGL(zs_unit_header_kernel<true>, dim3(nchunks), dim3(WAVE), 0, st, d_jobs, d_heads, d_chunks, d_tables);
@@ -1522,6 +1855,15 @@ extern "C" void zs_launch_parse(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads
     hipLaunchKernelGGL(zs_unit_header_kernel<false>, dim3(nchunks), dim3(WAVE), 0, st, d_jobs, d_heads, d_chunks, d_tables);
   uint32_t *order = nullptr;
   if (sort_units(d_jobs, d_chunks, nchunks, 0, &order, st)) return;
+  if (wave_units) {
+    if (d64)
+      hipLaunchKernelGGL(zs_unitw_kernel<true>, dim3(nchunks), dim3(WAVE), 0, st, d_jobs, d_heads, d_chunks, nchunks,
+                         d_tokens, d_tables, d_fixed, order, pool);
+    else
+      hipLaunchKernelGGL(zs_unitw_kernel<false>, dim3(nchunks), dim3(WAVE), 0, st, d_jobs, d_heads, d_chunks, nchunks,
+                         d_tokens, d_tables, d_fixed, order, pool);
+    return;
+  }
   if (d64)
     hipLaunchKernelGGL(zs_lane_kernel<true>, dim3((nchunks + WAVE - 1) / WAVE), dim3(WAVE), 0, st, d_jobs, d_heads,
                        d_chunks, nchunks, d_tokens, d_tables, d_fixed, order, pool);

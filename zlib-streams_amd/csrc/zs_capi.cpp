@@ -53,7 +53,7 @@ extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_hea
                                   ZsCJobDev *d_cjobs, uint32_t ncjobs, ZsChunkDev *d_units, uint32_t nunit_slots,
                                   uint16_t *d_scratch, uint32_t *d_tokens, ZsTokPool pool, uint32_t *d_tables,
                                   const uint32_t *d_fixed, uint8_t *d_windows, void *d_linkinfo, ZsDecDev *d_decs,
-                                  uint32_t *d_fallback, int d64, hipStream_t st, hipEvent_t *ev);
+                                  uint32_t *d_fallback, int d64, int wave_units, hipStream_t st, hipEvent_t *ev);
 
 namespace {
 
@@ -155,6 +155,23 @@ uint32_t chunk_bytes() {
     return (uint32_t)(kb * 1024);
   }();
   return v;
+}
+// Parse mode of a chunked group: a wave per unit when the group has few units
+// for the GPU (about one per search segment), a lane per unit otherwise
+// (env ZS_PARSE = lane | wave forces one; ZS_WAVE_SEGS moves the threshold).
+int wave_units(size_t nseg, uint32_t flags) {
+  if (flags & ZS_F_PARSE_LANE) return 0;
+  if (flags & ZS_F_PARSE_WAVE) return 1;
+  static const int force = [] {
+    const char *e = std::getenv("ZS_PARSE");
+    return e ? (std::strcmp(e, "wave") == 0 ? 1 : (std::strcmp(e, "lane") == 0 ? 0 : -1)) : -1;
+  }();
+  static const size_t lim = [] {
+    const char *e = std::getenv("ZS_WAVE_SEGS");
+    return (size_t)(e ? std::atoll(e) : 8192);
+  }();
+  if (force >= 0) return force;
+  return nseg <= lim ? 1 : 0;
 }
 bool chunking_enabled() {
   static bool v = [] {
@@ -482,7 +499,8 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
   if (n_cjs) {
     zs_launch_chunked(g_ws.d_jobs, g_ws.d_heads, g_ws.d_segs, (uint32_t)seg_std, g_ws.d_cjobs, n_cjs, g_ws.d_chunks,
                       (uint32_t)slots_std, g_ws.d_scratch, g_ws.d_tokens, pool, g_ws.d_tables, g_ws.d_fixed,
-                      g_ws.d_windows, g_ws.d_linkinfo, g_ws.d_decs, g_ws.d_fallback, 0, st, ev ? ev + 1 : nullptr);
+                      g_ws.d_windows, g_ws.d_linkinfo, g_ws.d_decs, g_ws.d_fallback, 0, wave_units(seg_std, flags), st,
+                      ev ? ev + 1 : nullptr);
   }
   if (n_cj64) {  // the deflate64 group: its own slice of every per-unit array
     ZsTokPool p64 = pool;
@@ -491,7 +509,7 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
                       g_ws.d_cjobs + n_cjs, n_cj64, g_ws.d_chunks + slots_std, (uint32_t)(nunit_slots - slots_std),
                       g_ws.d_scratch, g_ws.d_tokens, p64, g_ws.d_tables + slots_std * TABLE_ENTRIES_HOST,
                       g_ws.d_fixed + FIXED_WORDS_HOST, g_ws.d_windows + slots_std * 32768, g_ws.d_linkinfo + slots_std * 2,
-                      g_ws.d_decs, g_ws.d_fallback, 1, st, (ev && !n_cjs) ? ev + 1 : nullptr);
+                      g_ws.d_decs, g_ws.d_fallback, 1, wave_units(nseg - seg_std, flags), st, (ev && !n_cjs) ? ev + 1 : nullptr);
   }
   if (!n_cj && ev)
     for (int i = 1; i <= 6; i++) HIP_OK(hipEventRecord(ev[i], st));

@@ -131,11 +131,15 @@ def _check(rc):
         raise ZStreamsError(f"libzstreams_mi355x error {rc}: {lib().zs_last_error().decode()}")
 
 
-def inflate_batch(streams, window_bits=-15, out_caps=None):
+PARSE_FLAGS = {None: 0, "lane": 8, "wave": 16}  # ZS_F_PARSE_LANE / ZS_F_PARSE_WAVE
+
+
+def inflate_batch(streams, window_bits=-15, out_caps=None, parse=None):
     """Inflate many whole streams on the GPU (host buffers).
 
     Each stream behaves like inflateInit2(window_bits) + one inflate(Z_FINISH)
-    into an out_cap-byte buffer.  Returns [(bytes, result_dict)].
+    into an out_cap-byte buffer.  Returns [(bytes, result_dict)].  parse =
+    "lane" / "wave" forces the block-parallel path's parse mode (same results).
     """
     n = len(streams)
     if out_caps is None:
@@ -154,7 +158,7 @@ def inflate_batch(streams, window_bits=-15, out_caps=None):
         jobs[i].out = ctypes.cast(ob, ctypes.c_void_p).value
         jobs[i].out_cap = out_caps[i]
         jobs[i].window_bits = wbs[i]
-    _check(lib().zs_inflate_batch(jobs, n, res, 0))
+    _check(lib().zs_inflate_batch(jobs, n, res, PARSE_FLAGS[parse]))
     return [(outbufs[i].raw[:res[i].total_out], res[i].as_dict()) for i in range(n)]
 
 
