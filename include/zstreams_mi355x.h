@@ -96,7 +96,7 @@ typedef struct zs_result {
 #define ZS_F_DEVICE 1u /* job in/out pointers are device (HBM) pointers: no staging copies */
 #define ZS_F_CRC32 2u  /* raw and copy jobs: CRC-32 of the output in adler (ZIP entries; computed on the GPU) */
 /* Parse mode of the block-parallel path (results are identical; speed differs).
-   By default a batch with few decode units (<= 8192 search segments of 32 KiB
+   By default a batch with few decode units (<= 12288 search segments of 32 KiB
    compressed, env ZS_WAVE_SEGS) decodes each unit with a whole wave, a larger
    one each unit with one lane.  These force one mode (testing, tuning). */
 #define ZS_F_PARSE_LANE 8u

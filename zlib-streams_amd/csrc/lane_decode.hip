@@ -1126,7 +1126,10 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
 // Block headers, stored blocks and unit stops go through coop_block, so the
 // unit's tokens, end bit, code, n_out and n_tok equal the lane decoder's.
 // ---------------------------------------------------------------------------
-#define UW_STG 64
+#define UW_STG 128
+#define UF_OFFS 8                    // fast window: symbol offsets per lane
+#define UF_BITS (UF_OFFS * WAVE)     // ... bits per window
+#define UF_JN (UF_BITS + WAVE)       // jump-table entries (offsets past the window loop on themselves)
 #define UW_SETS 1  // symbol offsets per lane per window (2: measured 28% slower, the walk dominates)
 struct UnitWLDS {
   BuildLDS b;
@@ -1135,7 +1138,8 @@ struct UnitWLDS {
   uint32_t dtail[DTAIL_BYTES / 4];
   uint32_t lt[ZBUILD];  // current block: zlib literal/length table
   uint32_t dt[594];     // ... and distance table
-  uint32_t stg[UW_STG + 8];  // staged input words (one global load per ~30 windows)
+  uint32_t stg[UW_STG + 8];  // staged input words (one global load per ~3 fast windows)
+  uint16_t jmp[2][UF_JN];    // fast window: pointer-doubling tables
 };
 
 enum { UW_SYM = 0, UW_EOB = 1, UW_INVL = 2, UW_INVD = 3 };
@@ -1143,6 +1147,168 @@ enum { UW_SYM = 0, UW_EOB = 1, UW_INVL = 2, UW_INVD = 3 };
 struct UwSym {
   uint32_t kind, endr, len, dist, tok, dend;  // endr / dend: bits past the window start
 };
+
+// Fast window: the stages of Inflater::fast_window (inflate_kernels.hip) in
+// token mode.  A complete symbol at every offset P + lane + 64 i of a 512-bit
+// window (8 per lane, each stage's LDS loads issued back to back), the chain
+// from P by pointer doubling (lane m ends with the start of the m-th symbol),
+// then the longest prefix of plain symbols: complete inside the input, fitting
+// the unit, distance within written history, no end of block / invalid code
+// (and, for deflate64, no copy longer than one token).  Lane k < n returns
+// symbol k's (L, D) (L: 0x80000000 | literal, or length); *T the output
+// bytes, *endrel the bits consumed.  Anything else is left to the exact step.
+template <bool D64>
+__device__ uint32_t uw_fast(UnitWLDS &L, uint32_t P, uint32_t sbase, uint32_t lmask, uint32_t dmask, uint32_t limit,
+                            uint32_t pos, uint32_t capx, uint32_t whave, uint32_t *T, uint32_t *endrel, uint32_t *Lo,
+                            uint32_t *Do, bool *stopped) {
+  const uint32_t lane = lane_id();
+  auto bits_at = [&](uint32_t q) -> uint64_t {
+    const uint32_t w = (q >> 5) - sbase, sh = q & 31u;
+    uint64_t h = (((uint64_t)L.stg[w + 1]) << 32 | L.stg[w]) >> sh;
+    if (sh) h |= (uint64_t)L.stg[w + 2] << (64u - sh);
+    return h;
+  };
+  auto perm = [](uint32_t from_lane, uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(from_lane << 2), (int)v);
+  };
+  uint32_t nbp0 = 0, nbp1 = 0;  // total bits per slot, 8 bits each (0 = not a plain symbol)
+  uint32_t lv[UF_OFFS], dv[UF_OFFS];
+  uint64_t hh[UF_OFFS];
+  uint32_t ee[UF_OFFS], e2[UF_OFFS], used[UF_OFFS];
+#pragma unroll
+  for (uint32_t i = 0; i < UF_OFFS; i++) hh[i] = bits_at(P + lane + i * WAVE);
+#pragma unroll
+  for (uint32_t i = 0; i < UF_OFFS; i++) ee[i] = L.lt[(uint32_t)hh[i] & lmask];
+#pragma unroll
+  for (uint32_t i = 0; i < UF_OFFS; i++) {
+    const uint32_t op = e_op(ee[i]);
+    used[i] = e_bits(ee[i]);
+    const bool sub = op != 0 && (op & 0xf0u) == 0;
+    e2[i] = L.lt[sub ? e_val(ee[i]) + (((uint32_t)(hh[i] >> used[i])) & ((1u << op) - 1)) : 0u];
+  }
+  uint64_t hd[UF_OFFS];
+  uint32_t sb[UF_OFFS], de[UF_OFFS];
+#pragma unroll
+  for (uint32_t i = 0; i < UF_OFFS; i++) {
+    const uint32_t op0 = e_op(ee[i]);
+    if (op0 != 0 && (op0 & 0xf0u) == 0) {
+      used[i] += e_bits(e2[i]);
+      ee[i] = e2[i];
+    }
+    const uint32_t op = e_op(ee[i]);
+    const uint32_t xb = (op == 0 || (op & 96u)) ? 0u : op & (D64 ? 31u : 15u);
+    lv[i] = op == 0 ? (0x80000000u | e_val(ee[i])) : e_val(ee[i]) + ((uint32_t)(hh[i] >> used[i]) & ((1u << xb) - 1u));
+    sb[i] = used[i] + xb;
+    hd[i] = hh[i] >> sb[i];
+    de[i] = L.dt[(uint32_t)hd[i] & dmask];
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < UF_OFFS; i++) {
+    const uint32_t dop0 = e_op(de[i]);
+    const uint32_t du0 = e_bits(de[i]);
+    const bool dsub = (dop0 & 0xf0u) == 0;
+    e2[i] = L.dt[dsub ? e_val(de[i]) + (((uint32_t)(hd[i] >> du0)) & ((1u << dop0) - 1)) : 0u];
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < UF_OFFS; i++) {
+    const uint32_t op = e_op(ee[i]);
+    uint32_t d = de[i];
+    uint32_t dused = e_bits(d);
+    if ((e_op(d) & 0xf0u) == 0) {
+      dused += e_bits(e2[i]);
+      d = e2[i];
+    }
+    const uint32_t dop = e_op(d);
+    const uint32_t dx = dop & 15u;
+    uint32_t nb = 0;
+    dv[i] = 0;
+    if (op == 0) {
+      nb = used[i];
+    } else if ((op & 96u) == 0 && (dop & 64u) == 0 && !(D64 && lv[i] > 0xffffu)) {
+      nb = sb[i] + dused + dx;
+      dv[i] = e_val(d) + ((uint32_t)(hd[i] >> dused) & ((1u << dx) - 1u));
+    }
+    if (P + lane + i * WAVE + nb > limit) nb = 0;
+    if (i < 4) nbp0 |= nb << (8u * i);
+    else nbp1 |= nb << (8u * (i - 4u));
+  }
+  // the chain from P by pointer doubling
+  uint16_t *ja = L.jmp[0], *jb = L.jmp[1];
+#pragma unroll
+  for (uint32_t i = 0; i < UF_OFFS; i++) {
+    const uint32_t q = lane + i * WAVE;
+    const uint32_t nb = ((i < 4 ? nbp0 : nbp1) >> (8u * (i & 3u))) & 0xffu;
+    ja[q] = (uint16_t)(q + nb);
+  }
+  ja[UF_BITS + lane] = (uint16_t)(UF_BITS + lane);
+  __builtin_amdgcn_wave_barrier();
+  uint32_t sp = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 6; k++) {
+    const uint32_t half = 1u << k;
+    const uint32_t t = perm(lane >= half ? lane - half : 0u, sp);
+    const uint32_t g = ja[t];
+    if (lane >= half && lane < 2u * half) sp = g;
+    if (k < 5) {
+#pragma unroll
+      for (uint32_t i = 0; i < UF_OFFS + 1; i++) {
+        const uint32_t q = lane + i * WAVE;
+        jb[q] = ja[ja[q]];
+      }
+      __builtin_amdgcn_wave_barrier();
+      uint16_t *tmp = ja;
+      ja = jb;
+      jb = tmp;
+    }
+  }
+  const uint32_t xs = sp < UF_BITS ? sp : 0u;
+  const uint32_t px0 = perm(xs & 63u, nbp0), px1 = perm(xs & 63u, nbp1);
+  const uint32_t nbs = (((xs >> 6) < 4u ? px0 : px1) >> (8u * ((xs >> 6) & 3u))) & 0xffu;
+  const uint64_t badc = __ballot(!(sp < UF_BITS && nbs != 0));
+  const uint32_t cnt = badc ? (uint32_t)__builtin_ctzll(badc) : WAVE;
+  const uint32_t s63 = __builtin_amdgcn_readlane(sp, WAVE - 1);
+  const uint32_t nb63 = __builtin_amdgcn_readlane(nbs, WAVE - 1);
+  const uint32_t cur = cnt < WAVE ? 0u : s63 + nb63;
+  __builtin_amdgcn_wave_barrier();  // the jump tables are rewritten by the next window
+  // a symbol that is not plain stopped the chain inside the window (the exact
+  // step takes it); otherwise the chain only left the window
+  const bool inner_stop = cnt < WAVE && __builtin_amdgcn_readlane(sp, cnt) < UF_BITS;
+  *stopped = true;
+  if (cnt == 0) return 0;
+  // symbol k -> lane k, then the admissible prefix (lane_step's FULL / too-far order)
+  const uint32_t src = sp & 63u, sl = sp >> 6;
+  uint32_t Ls = 0, Ds = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < UF_OFFS; i++) {
+    const uint32_t a = perm(src, lv[i]);
+    const uint32_t b = perm(src, dv[i]);
+    if (sl == i) {
+      Ls = a;
+      Ds = b;
+    }
+  }
+  const bool act = lane < cnt;
+  const bool lit = (Ls & 0x80000000u) != 0;
+  const uint32_t olen = act ? (lit ? 1u : Ls) : 0u;
+  uint32_t incl = olen;
+  incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x111, 0xf, 0xf, false);
+  incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x112, 0xf, 0xf, false);
+  incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x114, 0xf, 0xf, false);
+  incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x118, 0xf, 0xf, false);
+  incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x142, 0xa, 0xf, false);
+  incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x143, 0xc, 0xf, false);
+  const uint32_t ost = incl - olen;
+  const bool ok = act && pos + incl <= capx && (lit || Ds <= pos + ost + whave);
+  const uint64_t badm = __ballot(!ok);
+  const uint32_t n = badm ? (uint32_t)__builtin_ctzll(badm) : WAVE;
+  if (n == 0) return 0;
+  *stopped = n < cnt || inner_stop;
+  *T = __builtin_amdgcn_readlane(incl, n - 1);
+  *endrel = n < WAVE ? __builtin_amdgcn_readlane(sp, n) : cur;
+  *Lo = Ls;
+  *Do = Ds;
+  return n;
+}
 
 // field f of offset set j at lane ql, wave-uniform
 __device__ __forceinline__ uint32_t uw_rl(const UwSym (&y)[UW_SETS], uint32_t UwSym::*f, uint32_t j, uint32_t ql) {
@@ -1294,18 +1460,49 @@ __global__ void __launch_bounds__(64) zs_unitw_kernel(const ZsJobDev *__restrict
     __syncthreads();
     const uint32_t lmask = (1u << s.lbits) - 1u, dmask = (1u << s.dbits) - 1u;
     uint32_t sbase = 0;
-    bool staged = false;
+    bool staged = false, exact_next = false;
     for (;;) {
       const uint32_t P = s.bit;
-      // a window reads words P/32 .. P/32 + 2 UW_SETS + 3 (a symbol ends <= 64 UW_SETS - 1 + 60 bits past P)
-      if (!staged || (P >> 5) + 2 * UW_SETS + 4 > sbase + UW_STG + 8) {
+      // a fast window reads words P/32 .. P/32 + 20 (a symbol ends <= 511 + 60
+      // bits past P), the exact step P/32 .. P/32 + 5
+      if (!staged || (P >> 5) + 22 > sbase + UW_STG + 8) {
         __syncthreads();
         sbase = P >> 5;
         L.stg[lane] = in_word_g(s.w, sbase + lane, s.end_byte);
+        L.stg[WAVE + lane] = in_word_g(s.w, sbase + WAVE + lane, s.end_byte);
         if (lane < 8) L.stg[UW_STG + lane] = in_word_g(s.w, sbase + UW_STG + lane, s.end_byte);
         staged = true;
         __syncthreads();
       }
+      if (!exact_next && P + UF_BITS + 64u <= uni32(s.limit)) {
+        uint32_t T = 0, er = 0, Ls = 0, Ds = 0;
+        bool stopped = true;
+        const uint32_t n = uw_fast<D64>(L, P, sbase, lmask, dmask, uni32(s.limit), uni32(s.pos), uni32(s.capx),
+                                        uni32(s.whave), &T, &er, &Ls, &Ds, &stopped);
+        if (n) {
+          const uint32_t ntok = uni32(s.ntok), tcap = uni32(s.tcap);
+          uint32_t okp = 1;
+          if (ntok + n > tcap) {
+            if (lane == 0) okp = tok_ensure(pool, s.unit, tcap, ntok + n) ? 1u : 0u;
+            okp = uni32(okp);
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+          }
+          if (!okp) {
+            s.code = ZD_FULL;
+            s.mode = LM_DONE;
+            break;
+          }
+          if (lane < n)
+            *tok_addr(pool, tokens, s.unit, prim, tcap, ntok + lane) =
+                (Ls & 0x80000000u) ? (Ls & 0xffu) : ((Ls << 16) | (Ds - 1u));
+          s.ntok = ntok + n;
+          s.pos = uni32(s.pos) + T;
+          s.bit = P + er;
+          exact_next = stopped;  // the symbol that stopped the prefix needs the exact step
+          continue;
+        }
+      }
+      exact_next = false;
       // each lane decodes the complete symbol(s) starting at bit P + lane
       // (+ 64 j) (src/inffast.c:107-166 on zlib's tables)
       const uint32_t base = (P & 31u) + 32u * ((P >> 5) - sbase);

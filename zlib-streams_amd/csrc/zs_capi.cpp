@@ -168,7 +168,7 @@ int wave_units(size_t nseg, uint32_t flags) {
   }();
   static const size_t lim = [] {
     const char *e = std::getenv("ZS_WAVE_SEGS");
-    return (size_t)(e ? std::atoll(e) : 8192);
+    return (size_t)(e ? std::atoll(e) : 12288);
   }();
   if (force >= 0) return force;
   return nseg <= lim ? 1 : 0;
