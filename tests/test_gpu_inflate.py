@@ -342,3 +342,33 @@ def test_c5_shape_vs_oracle(zs):
             bad.append((k, wb, info, ei))
     assert not bad, bad[:4]
     assert st["chunked_jobs"] == n and st["fallback_jobs"] == 0, st
+
+
+def _too_far_after_start():
+    """Raw deflate whose SECOND block (a decode unit of its own) copies from a
+    preset dictionary, i.e. reaches before the stream start while the output is
+    still shorter than the window: inflate without the dictionary must report
+    "invalid distance too far back" where zlib does (detected at the window
+    link / emit on the block-parallel path, then decoded exactly)."""
+    rng = random.Random(12)
+    dictionary = bytes(rng.getrandbits(8) for _ in range(32768))
+    co = zlib.compressobj(6, zlib.DEFLATED, -15, 8, zlib.Z_DEFAULT_STRATEGY, dictionary)
+    head = bytes(rng.getrandbits(8) for _ in range(3000))
+    tail = corpus.stream(3, 900 << 10)
+    out = co.compress(head) + co.flush(zlib.Z_SYNC_FLUSH)
+    out += co.compress(dictionary[5000:9000] + tail) + co.flush()
+    return out, len(head) + 4000 + len(tail)
+
+
+@pytest.mark.parametrize("copies", [1, 6])
+def test_chunked_too_far_back_across_units(zs, copies):
+    """A too-far distance in a later unit, with one stream per batch (windows by
+    the parallel-prefix link) and six (the per-stream serial link)."""
+    comp, n = _too_far_after_start()
+    got = zs.inflate_batch([comp] * copies, -15, [n] * copies)
+    st = zs.last_stats()
+    eo, ei = O.oneshot(comp, -15, n)
+    assert ei["ret"] == -3 and ei["msg"] == "invalid distance too far back", ei
+    for out, info in got:
+        assert info == ei and out == eo, (info, ei)
+    assert st["chunked_jobs"] == copies and st["fallback_jobs"] == copies, st

@@ -924,7 +924,7 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_link_kernel(const ZsJobDev *_
 template <uint32_t HN>
 __global__ void __launch_bounds__(EMIT_THREADS) zs_emit_kernel(const ZsJobDev *__restrict__ jobs, const ZsChunkDev *__restrict__ chunks,
                                                                const uint16_t *__restrict__ scratch, const uint8_t *__restrict__ windows,
-                                                               const uint32_t *__restrict__ fallback) {
+                                                               uint32_t *__restrict__ fallback) {
   constexpr uint32_t MB = HN == 65536u ? 0u : MARK_BASE;
   __shared__ uint8_t s_w[HN];
   const uint32_t c = blockIdx.x;
@@ -940,6 +940,10 @@ __global__ void __launch_bounds__(EMIT_THREADS) zs_emit_kernel(const ZsJobDev *_
   uint8_t *out = jobs[ch.job].out + ch.out_off;
   const uint16_t *e = scratch + ch.scratch;
   const uint32_t n = ch.n_out;
+  // window bytes below `lowest` lie before the stream start: a marker into
+  // them is a too-far distance (the parallel-prefix link leaves that check here)
+  const uint32_t lowest = HN - (uint32_t)min<uint64_t>(HN, ch.out_off);
+  bool bad = false;
   // 16-byte output groups aligned in memory; group g covers unit bytes
   // [16 g - mis, 16 g - mis + 16).  Groups straddling the unit's ends are
   // written bytewise (neighbouring units own the other bytes).
@@ -957,6 +961,7 @@ __global__ void __launch_bounds__(EMIT_THREADS) zs_emit_kernel(const ZsJobDev *_
       for (int k = 0; k < 16; k++) {
         const uint32_t v = (w[k >> 1] >> (16 * (k & 1))) & 0xffffu;
         b[k] = v < MARK_BASE ? v : s_w[v - MB];
+        bad |= v >= MARK_BASE && v - MB < lowest;
       }
       uint4 o;
       o.x = b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
@@ -970,9 +975,11 @@ __global__ void __launch_bounds__(EMIT_THREADS) zs_emit_kernel(const ZsJobDev *_
         if (i < 0 || (uint32_t)i >= n) continue;
         const uint32_t v = e[i];
         out[i] = (uint8_t)(v < MARK_BASE ? v : s_w[v - MB]);
+        bad |= v >= MARK_BASE && v - MB < lowest;
       }
     }
   }
+  if (__syncthreads_or(bad) && t == 0) fallback[ch.job] = 1;
 }
 
 // ---------------------------------------------------------------------------
@@ -1066,7 +1073,7 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_link64_kernel(ZsCJobDev *__re
 
 __global__ void __launch_bounds__(EMIT_THREADS) zs_emit64_kernel(const ZsJobDev *__restrict__ jobs, const ZsChunkDev *__restrict__ chunks,
                                                                  const uint16_t *__restrict__ scratch, const uint8_t *__restrict__ windows,
-                                                                 const uint32_t *__restrict__ fallback) {
+                                                                 uint32_t *__restrict__ fallback) {
   __shared__ uint8_t s_w[H64];
   const uint32_t c = blockIdx.x;
   const uint32_t t = threadIdx.x;
@@ -1081,9 +1088,111 @@ __global__ void __launch_bounds__(EMIT_THREADS) zs_emit64_kernel(const ZsJobDev 
   uint8_t *out = jobs[ch.job].out + ch.out_off;
   const uint32_t *e = reinterpret_cast<const uint32_t *>(scratch + ch.scratch);
   const uint32_t n = ch.n_out;
+  const uint32_t lowest = H64 - (uint32_t)min<uint64_t>(H64, ch.out_off);
+  bool bad = false;
   for (uint32_t i = t; i < n; i += EMIT_THREADS) {
     const uint32_t v = e[i];
     out[i] = (uint8_t)(v < MARK_BASE ? v : s_w[(v - MARK_BASE) & (H64 - 1)]);
+    bad |= v >= MARK_BASE && v - MARK_BASE < lowest;
+  }
+  if (__syncthreads_or(bad) && t == 0) fallback[ch.job] = 1;
+}
+
+// ---------------------------------------------------------------------------
+// Link by parallel prefix, for batches of few long streams (one large file):
+// the serial link resolves a stream's windows one chain member at a time,
+// which for one stream of 1024 units is 1024 dependent steps.  Here each
+// window W_j (the HN bytes before chain member j) is first a MAP over
+// W_{j-1}: entry i is a literal byte, or MARK_BASE + w for byte w of W_{j-1}
+//   M_j[i] = i < keep ? ref(i + n) : E_{j-1}[i + n - HN],
+// n = member j-1's output, keep = HN - n (src/inffast.c window semantics, as
+// zs_link_kernel).  Maps compose (A o B: literals stay, ref w -> B[w]), so
+// a Hillis-Steele scan over the chain (ceil(log2 nchain) launches, each
+// composing every map with the one 2^d members earlier) leaves every W_j in
+// terms of the stream start: literals, or refs before it (never read by a
+// valid stream; zs_emit_kernel reports any marker into them).  Entries are u16
+// (std, markers < 256 + 32768) or u32 (deflate64).
+// ---------------------------------------------------------------------------
+#define PL_T 256
+#define PL_E 16                      // entries per thread
+#define PL_BLK (PL_T * PL_E)         // entries per workgroup
+
+// chain member (job q, index j) of unit slot u of the group; false if unused
+__device__ __forceinline__ bool pl_member(const ZsCJobDev *__restrict__ cjobs, uint32_t ncj, uint32_t u, uint32_t *q,
+                                          uint32_t *j) {
+  for (uint32_t k = 0; k < ncj; k++) {
+    const ZsCJobDev &cj = cjobs[k];
+    if (u >= cj.unit0 && u < cj.unit0 + cj.max_units) {
+      *q = k;
+      *j = u - cj.unit0;
+      return cj.ok && *j < cj.nchain;
+    }
+  }
+  return false;
+}
+
+template <uint32_t HN, typename T>
+__global__ void __launch_bounds__(PL_T) zs_plink_init_kernel(const ZsCJobDev *__restrict__ cjobs, uint32_t ncj,
+                                                             const uint16_t *__restrict__ scratch,
+                                                             const ZsLinkInfo *__restrict__ info, T *__restrict__ A) {
+  const uint32_t u = blockIdx.y;
+  uint32_t q, j;
+  if (!pl_member(cjobs, ncj, u, &q, &j) || j == 0) return;
+  const ZsLinkInfo prev = info[cjobs[q].unit0 + j - 1];
+  const T *E = reinterpret_cast<const T *>(scratch + prev.scratch);
+  const uint32_t n = prev.n_out, keep = n < HN ? HN - n : 0u;
+  T *out = A + (size_t)u * HN;
+  const uint32_t i0 = blockIdx.x * PL_BLK + threadIdx.x;
+#pragma unroll
+  for (uint32_t k = 0; k < PL_E; k++) {
+    const uint32_t i = i0 + k * PL_T;
+    out[i] = i < keep ? (T)(MARK_BASE + i + n) : E[i + n - HN];
+  }
+}
+
+template <uint32_t HN, typename T>
+__global__ void __launch_bounds__(PL_T) zs_plink_step_kernel(const ZsCJobDev *__restrict__ cjobs, uint32_t ncj,
+                                                             const T *__restrict__ A, T *__restrict__ B, uint32_t stride) {
+  const uint32_t u = blockIdx.y;
+  uint32_t q, j;
+  if (!pl_member(cjobs, ncj, u, &q, &j) || j == 0) return;
+  const T *a = A + (size_t)u * HN;
+  T *b = B + (size_t)u * HN;
+  const uint32_t i0 = blockIdx.x * PL_BLK + threadIdx.x;
+  if (j <= stride) {  // already in terms of the stream start
+#pragma unroll
+    for (uint32_t k = 0; k < PL_E; k++) b[i0 + k * PL_T] = a[i0 + k * PL_T];
+    return;
+  }
+  const T *e = A + (size_t)(u - stride) * HN;  // member j - stride
+  T v[PL_E];
+#pragma unroll
+  for (uint32_t k = 0; k < PL_E; k++) v[k] = a[i0 + k * PL_T];
+#pragma unroll
+  for (uint32_t k = 0; k < PL_E; k++) {
+    const uint32_t x = v[k];
+    if (x >= MARK_BASE) v[k] = e[(x - MARK_BASE) & (HN - 1)];
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < PL_E; k++) b[i0 + k * PL_T] = v[k];
+}
+
+// windows[unit slot of member j] = W_j as bytes (refs before the stream start: 0)
+template <uint32_t HN, typename T>
+__global__ void __launch_bounds__(PL_T) zs_plink_out_kernel(const ZsCJobDev *__restrict__ cjobs, uint32_t ncj,
+                                                            const ZsLinkInfo *__restrict__ info, const T *__restrict__ A,
+                                                            uint8_t *__restrict__ windows) {
+  const uint32_t u = blockIdx.y;
+  uint32_t q, j;
+  if (!pl_member(cjobs, ncj, u, &q, &j) || j == 0) return;
+  const uint32_t c = info[cjobs[q].unit0 + j].unit;
+  const T *a = A + (size_t)u * HN;
+  uint8_t *w = windows + (size_t)c * HN;
+  const uint32_t i0 = blockIdx.x * PL_BLK + threadIdx.x;
+#pragma unroll
+  for (uint32_t k = 0; k < PL_E; k++) {
+    const uint32_t x = a[i0 + k * PL_T];
+    w[i0 + k * PL_T] = x < MARK_BASE ? (uint8_t)x : (uint8_t)0;
   }
 }
 
@@ -1106,7 +1215,8 @@ extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_hea
                                   ZsCJobDev *d_cjobs, uint32_t ncjobs, ZsChunkDev *d_units, uint32_t nunit_slots,
                                   uint16_t *d_scratch, uint32_t *d_tokens, ZsTokPool pool, uint32_t *d_tables,
                                   const uint32_t *d_fixed, uint8_t *d_windows, void *d_linkinfo, ZsDecDev *d_decs,
-                                  uint32_t *d_fallback, int d64, int wave_units, hipStream_t st, hipEvent_t *ev) {
+                                  uint32_t *d_fallback, int d64, int wave_units, void *d_plink, uint32_t plink_levels,
+                                  hipStream_t st, hipEvent_t *ev) {
   // ev (profiling, optional): [0] before find, [1] after find + plan, [2] after
   // parse + chain, [3] after expand, [4] after link, [5] after emit
   if (ev) (void)hipEventRecord(ev[0], st);
@@ -1124,7 +1234,41 @@ extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_hea
   if (ev) (void)hipEventRecord(ev[2], st);
   zs_launch_expand(d_jobs, d_units, nunit_slots, d_scratch, d_tokens, pool, d_fallback, d64, st);
   if (ev) (void)hipEventRecord(ev[3], st);
-  if (d64) {
+  if (d_plink) {  // few long streams: windows by parallel prefix over each chain
+    const dim3 grid((d64 ? 65536u : HIST) / PL_BLK, nunit_slots);
+    if (d64) {
+      uint32_t *A = static_cast<uint32_t *>(d_plink), *B = A + (size_t)nunit_slots * 65536u;
+      hipLaunchKernelGGL((zs_plink_init_kernel<65536u, uint32_t>), grid, dim3(PL_T), 0, st, d_cjobs, ncjobs, d_scratch,
+                         info, A);
+      for (uint32_t d = 0; d < plink_levels; d++) {
+        hipLaunchKernelGGL((zs_plink_step_kernel<65536u, uint32_t>), grid, dim3(PL_T), 0, st, d_cjobs, ncjobs, A, B, 1u << d);
+        uint32_t *t = A;
+        A = B;
+        B = t;
+      }
+      hipLaunchKernelGGL((zs_plink_out_kernel<65536u, uint32_t>), grid, dim3(PL_T), 0, st, d_cjobs, ncjobs, info, A,
+                         d_windows);
+    } else {
+      uint16_t *A = static_cast<uint16_t *>(d_plink), *B = A + (size_t)nunit_slots * HIST;
+      hipLaunchKernelGGL((zs_plink_init_kernel<HIST, uint16_t>), grid, dim3(PL_T), 0, st, d_cjobs, ncjobs, d_scratch,
+                         info, A);
+      for (uint32_t d = 0; d < plink_levels; d++) {
+        hipLaunchKernelGGL((zs_plink_step_kernel<HIST, uint16_t>), grid, dim3(PL_T), 0, st, d_cjobs, ncjobs, A, B, 1u << d);
+        uint16_t *t = A;
+        A = B;
+        B = t;
+      }
+      hipLaunchKernelGGL((zs_plink_out_kernel<HIST, uint16_t>), grid, dim3(PL_T), 0, st, d_cjobs, ncjobs, info, A,
+                         d_windows);
+    }
+    if (ev) (void)hipEventRecord(ev[4], st);
+    if (d64)
+      hipLaunchKernelGGL(zs_emit64_kernel, dim3(nunit_slots), dim3(EMIT_THREADS), 0, st, d_jobs, d_units, d_scratch,
+                         d_windows, d_fallback);
+    else
+      hipLaunchKernelGGL(zs_emit_kernel<HIST>, dim3(nunit_slots), dim3(EMIT_THREADS), 0, st, d_jobs, d_units, d_scratch,
+                         d_windows, d_fallback);
+  } else if (d64) {
     hipLaunchKernelGGL(zs_link64_kernel, dim3(ncjobs), dim3(LINK_THREADS), 0, st, d_cjobs, d_scratch, d_windows, info,
                        d_fallback);
     if (ev) (void)hipEventRecord(ev[4], st);

@@ -53,7 +53,8 @@ extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_hea
                                   ZsCJobDev *d_cjobs, uint32_t ncjobs, ZsChunkDev *d_units, uint32_t nunit_slots,
                                   uint16_t *d_scratch, uint32_t *d_tokens, ZsTokPool pool, uint32_t *d_tables,
                                   const uint32_t *d_fixed, uint8_t *d_windows, void *d_linkinfo, ZsDecDev *d_decs,
-                                  uint32_t *d_fallback, int d64, int wave_units, hipStream_t st, hipEvent_t *ev);
+                                  uint32_t *d_fallback, int d64, int wave_units, void *d_plink, uint32_t plink_levels,
+                                  hipStream_t st, hipEvent_t *ev);
 
 namespace {
 
@@ -124,6 +125,8 @@ struct Workspace {
   uint8_t *d_windows = nullptr;  // 32 KiB per unit slot (64 KiB for deflate64 units)
   size_t cap_windows = 0;
   uint64_t *d_linkinfo = nullptr;  // zs_link_kernel chain order: 16 B per unit slot
+  uint8_t *d_plink = nullptr;      // parallel-prefix link maps (few long streams): 2 x slots x window entries
+  size_t cap_plink = 0;
   size_t cap_scratch = 0;        // u16 entries (chain members at their output offsets)
   uint16_t *d_scratch = nullptr;
   size_t cap_tokens = 0;         // u32 parse tokens: primary regions + pool pages
@@ -159,6 +162,20 @@ uint32_t chunk_bytes() {
 // Parse mode of a chunked group: a wave per unit when the group has few units
 // for the GPU (about one per search segment), a lane per unit otherwise
 // (env ZS_PARSE = lane | wave forces one; ZS_WAVE_SEGS moves the threshold).
+// Link mode of a chunked group: the parallel-prefix link for a group of at
+// most PLINK_JOBS streams with long chains (env ZS_PLINK = 0 disables it);
+// returns the scan levels (0 = the serial per-stream link).
+constexpr uint32_t PLINK_JOBS = 4;
+uint32_t plink_levels(uint32_t njobs, uint32_t max_units) {
+  static const bool off = [] {
+    const char *e = std::getenv("ZS_PLINK");
+    return e && e[0] == '0';
+  }();
+  if (off || njobs == 0 || njobs > PLINK_JOBS || max_units < 64) return 0;
+  uint32_t lv = 0;
+  while ((1u << lv) < max_units) lv++;
+  return lv;
+}
 int wave_units(size_t nseg, uint32_t flags) {
   if (flags & ZS_F_PARSE_LANE) return 0;
   if (flags & ZS_F_PARSE_WAVE) return 1;
@@ -496,11 +513,22 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
   if (ev) HIP_OK(hipEventRecord(ev[0], st));
   zs_launch_header(g_ws.d_jobs, g_ws.d_heads, nv, st);
   const uint32_t n_cjs = n_cj - n_cj64;
+  // parallel-prefix link buffers (groups of few long streams)
+  uint32_t pl_std = 0, pl_d64 = 0;
+  {
+    uint32_t mu_std = 0, mu_d64 = 0;
+    for (uint32_t q = 0; q < n_cj; q++) (q < n_cjs ? mu_std : mu_d64) = std::max((q < n_cjs ? mu_std : mu_d64), g_ws.h_cjobs[q].max_units);
+    pl_std = n_cjs ? plink_levels(n_cjs, mu_std) : 0;
+    pl_d64 = n_cj64 ? plink_levels(n_cj64, mu_d64) : 0;
+    const size_t need = std::max<size_t>(pl_std ? 2 * slots_std * 32768u * 2u : 0,
+                                         pl_d64 ? 2 * (nunit_slots - slots_std) * 65536u * 4u : 0);
+    if (need && ws_reserve_bytes(&g_ws.d_plink, &g_ws.cap_plink, need)) pl_std = pl_d64 = 0;  // serial link instead
+  }
   if (n_cjs) {
     zs_launch_chunked(g_ws.d_jobs, g_ws.d_heads, g_ws.d_segs, (uint32_t)seg_std, g_ws.d_cjobs, n_cjs, g_ws.d_chunks,
                       (uint32_t)slots_std, g_ws.d_scratch, g_ws.d_tokens, pool, g_ws.d_tables, g_ws.d_fixed,
-                      g_ws.d_windows, g_ws.d_linkinfo, g_ws.d_decs, g_ws.d_fallback, 0, wave_units(seg_std, flags), st,
-                      ev ? ev + 1 : nullptr);
+                      g_ws.d_windows, g_ws.d_linkinfo, g_ws.d_decs, g_ws.d_fallback, 0, wave_units(seg_std, flags),
+                      pl_std ? g_ws.d_plink : nullptr, pl_std, st, ev ? ev + 1 : nullptr);
   }
   if (n_cj64) {  // the deflate64 group: its own slice of every per-unit array
     ZsTokPool p64 = pool;
@@ -509,7 +537,8 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
                       g_ws.d_cjobs + n_cjs, n_cj64, g_ws.d_chunks + slots_std, (uint32_t)(nunit_slots - slots_std),
                       g_ws.d_scratch, g_ws.d_tokens, p64, g_ws.d_tables + slots_std * TABLE_ENTRIES_HOST,
                       g_ws.d_fixed + FIXED_WORDS_HOST, g_ws.d_windows + slots_std * 32768, g_ws.d_linkinfo + slots_std * 2,
-                      g_ws.d_decs, g_ws.d_fallback, 1, wave_units(nseg - seg_std, flags), st, (ev && !n_cjs) ? ev + 1 : nullptr);
+                      g_ws.d_decs, g_ws.d_fallback, 1, wave_units(nseg - seg_std, flags), pl_d64 ? g_ws.d_plink : nullptr,
+                      pl_d64, st, (ev && !n_cjs) ? ev + 1 : nullptr);
   }
   if (!n_cj && ev)
     for (int i = 1; i <= 6; i++) HIP_OK(hipEventRecord(ev[i], st));
