@@ -74,9 +74,11 @@ unsigned inflate9_last_consumed(uintptr_t h);
 /* ---- 3. batch API ---- */
 typedef struct zs_job {
   const void *in;      /* compressed bytes (host, or device with ZS_F_DEVICE) */
-  uint64_t in_len;     /* < 2^29 */
+  uint64_t in_len;     /* any length: a stream past 2^29 - 4096 compressed bytes or 0xfff00000 of
+                          out_cap decodes in 256 MiB pieces resumed at block boundaries (one deflate
+                          block must fit one piece's limits, else Z_STREAM_ERROR) */
   void *out;           /* output buffer (host, or 16-byte aligned device memory) */
-  uint64_t out_cap;    /* < 2^32 */
+  uint64_t out_cap;    /* any size */
   int32_t window_bits; /* as inflateInit2: -8..-15 raw, -16 raw deflate64, 8..15 zlib, +16 gzip, +32 auto */
   int32_t mode;        /* ZS_JOB_INFLATE (0), or ZS_JOB_COPY: stored bytes (ZIP method 0), output = input */
 } zs_job;

@@ -221,7 +221,7 @@ __global__ void __launch_bounds__(64) zs_find_kernel(const ZsJobDev *__restrict_
     const uint32_t *w = reinterpret_cast<const uint32_t *>(ip - mis);
     const uint32_t end_byte = mis + (uint32_t)jb.in_len;
     // strictly after the stream's first block (that start is unit 0)
-    const uint32_t lo = max((mis + seg.s_byte) * 8u, (mis + (uint32_t)hd.start_byte) * 8u + 1u);
+    const uint32_t lo = max((mis + seg.s_byte) * 8u, (mis + (uint32_t)hd.start_byte) * 8u + jb.sbit + 1u);
     const uint32_t hi = (mis + seg.e_byte) * 8u;
     uint32_t vh = 0, vt = 0;
     // input words of a step: lane word (base/32 + lane), the next one, and 8
@@ -421,7 +421,7 @@ __global__ void __launch_bounds__(64) zs_find_fixed_kernel(const ZsJobDev *__res
   const uint32_t mis = (uint32_t)(ip & 3u);
   const uint32_t *w = reinterpret_cast<const uint32_t *>(ip - mis);
   const uint32_t end_byte = mis + (uint32_t)jb.in_len;
-  const uint32_t lo = max((mis + seg.s_byte) * 8u, (mis + (uint32_t)hd.start_byte) * 8u + 8u);
+  const uint32_t lo = max((mis + seg.s_byte) * 8u, (mis + (uint32_t)hd.start_byte) * 8u + jb.sbit + 8u);
   const uint32_t hi = (mis + seg.e_byte) * 8u;
   uint32_t nfound = 0;
   for (uint32_t base = lo & ~31u; base < hi && nfound < SEG_SLOTS; base += WAVE * 32u) {
@@ -452,7 +452,7 @@ __global__ void __launch_bounds__(64) zs_find_fixed_kernel(const ZsJobDev *__res
       bool ok = false;
       if (lane < take) {
         cb = s_q[q0 + lane];
-        ok = fixed_plausible(w, end_byte, (mis + (uint32_t)hd.start_byte) * 8u, cb);
+        ok = fixed_plausible(w, end_byte, (mis + (uint32_t)hd.start_byte) * 8u + jb.sbit, cb);
       }
       uint64_t m = __ballot(ok);
       while (m && nfound < SEG_SLOTS) {
@@ -532,7 +532,7 @@ __global__ void __launch_bounds__(PLAN_T) zs_plan_kernel(const ZsJobDev *__restr
     nunits = run;
     if (t == 0) {
       ZsChunkDev u{};
-      u.start_bit = (mis + (uint32_t)hd.start_byte) * 8u;
+      u.start_bit = (mis + (uint32_t)hd.start_byte) * 8u + jb.sbit;
       units[cj.unit0] = u;
     }
     __syncthreads();
@@ -689,16 +689,27 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_chain_kernel(const ZsJobDev *
     if (small) s_succ[i - u0] = (k == ZS_NONE || k - i > 0xffffu) ? (uint16_t)0 : (uint16_t)(k - i);
   }
   __syncthreads();
-  // B: walk the chain
+  // B: walk the chain.  A piece of a longer stream (ZS_JF_PART) ends its
+  // chain at the last verified block boundary instead of failing: before a
+  // member that did not stop at a block boundary (the unit cut off by the
+  // piece's end) or that would pass the piece's output budget, or after a
+  // member with no successor; the next piece resumes there (ZD_STOP).
   if (t == 0) {
-    uint32_t c = u0, len = 0, ok = 1, end_bit = 0;
+    const bool part = (jb.flags & ZS_JF_PART) != 0;
+    uint32_t c = u0, len = 0, ok = 1, end_bit = 0, cut = 0, last_end = 0;
     uint64_t total = 0, spos = 0;  // output bytes; entries used (each member starts 8-entry aligned)
     for (;;) {
       const ZsChunkDev ch = chunks[c];
       const int code = ch.code & 0xff;
       spos = (spos + 7u) & ~7ull;
-      if ((code != ZD_STOP && code != ZD_END) || spos + ch.n_out > cj.scratch_n) {
-        ok = 0;
+      if ((code != ZD_STOP && code != ZD_END) || spos + ch.n_out > cj.scratch_n ||
+          (part && total + ch.n_out > ZS_PART_OUT)) {
+        if (part && len) {
+          cut = 1;
+          end_bit = last_end;
+        } else {
+          ok = 0;
+        }
         break;
       }
       ZsLinkInfo li;
@@ -711,6 +722,7 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_chain_kernel(const ZsJobDev *
       chunks[c].scratch = li.scratch;
       total += ch.n_out;
       spos += ch.n_out;
+      last_end = ch.end_bit;
       if (code == ZD_END) {
         end_bit = ch.end_bit;
         break;
@@ -723,7 +735,12 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_chain_kernel(const ZsJobDev *
         k = ch.chain_next;
       }
       if (k == ZS_NONE) {
-        ok = 0;
+        if (part) {
+          cut = 1;
+          end_bit = last_end;
+        } else {
+          ok = 0;
+        }
         break;
       }
       c = k;
@@ -732,7 +749,7 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_chain_kernel(const ZsJobDev *
     if (ok) {  // members are flagged only once the whole chain holds
       for (uint32_t j = 0; j < len; j++) chunks[info[u0 + j].unit].in_chain = 1;
       ZsDecDev d;
-      d.code = ZD_END;
+      d.code = cut ? ZD_STOP : ZD_END;
       d.msg = 0;
       const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(jb.in) & 3u);
       d.end_bits = end_bit - mis * 8u;
@@ -801,7 +818,6 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_link_kernel(const ZsJobDev *_
   const uint32_t t = threadIdx.x;
   const ZsCJobDev cj = cjobs[blockIdx.x];
   if (!cj.ok) return;
-  (void)jobs;
   const uint32_t u0 = cj.unit0;
   const uint32_t len = cj.nchain;
 #if KP_ON
@@ -810,8 +826,14 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_link_kernel(const ZsJobDev *_
   uint32_t kmark = 0;
 #endif
   if (t == 0) s_bad = 0;
-  // W holds the last HN bytes before unit c
-  uint32_t wv = 0;  // valid bytes of history
+  // W holds the last HN bytes before unit c; a later piece of a long stream
+  // (ZS_JF_CONT) starts with the earlier pieces' output before its own
+  const ZsJobDev jb = jobs[cj.job];
+  const bool cont = (jb.flags & ZS_JF_CONT) != 0;
+  uint32_t wv = cont ? min(jb.hist, HN) : 0u;  // valid bytes of history
+  if (cont)
+    for (uint32_t i = HN - wv + t; i < HN; i += LINK_THREADS) s_win[0][i] = jb.out[(int64_t)i - (int64_t)HN];
+  __syncthreads();
   int cur = 0;
   uint2 v[LINK_G], vn[LINK_G];
   ZsLinkInfo li = info[u0];
@@ -831,7 +853,7 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_link_kernel(const ZsJobDev *_
 #if KP_ON
     const uint64_t ka = KP_NOW();
 #endif
-    if (j != 0) {
+    if (j != 0 || cont) {
       uint8_t *g = windows + (size_t)c * HN;
       for (uint32_t i = t * 16; i < HN; i += LINK_THREADS * 16)
         *reinterpret_cast<uint4 *>(g + i) = *reinterpret_cast<const uint4 *>(W + i);
@@ -931,18 +953,20 @@ __global__ void __launch_bounds__(EMIT_THREADS) zs_emit_kernel(const ZsJobDev *_
   const uint32_t t = threadIdx.x;
   const ZsChunkDev ch = chunks[c];
   if (!ch.in_chain || fallback[ch.job]) return;
-  if (ch.ord != 0) {
+  const ZsJobDev jb = jobs[ch.job];
+  const uint64_t hist = (jb.flags & ZS_JF_CONT) ? jb.hist : 0u;  // output before the piece
+  if (ch.ord != 0 || hist) {
     const uint8_t *g = windows + (size_t)c * HN;
     for (uint32_t i = t * 16; i < HN; i += EMIT_THREADS * 16)
       *reinterpret_cast<uint4 *>(s_w + i) = *reinterpret_cast<const uint4 *>(g + i);
     __syncthreads();
   }
-  uint8_t *out = jobs[ch.job].out + ch.out_off;
+  uint8_t *out = jb.out + ch.out_off;
   const uint16_t *e = scratch + ch.scratch;
   const uint32_t n = ch.n_out;
   // window bytes below `lowest` lie before the stream start: a marker into
   // them is a too-far distance (the parallel-prefix link leaves that check here)
-  const uint32_t lowest = HN - (uint32_t)min<uint64_t>(HN, ch.out_off);
+  const uint32_t lowest = HN - (uint32_t)min<uint64_t>(HN, ch.out_off + hist);
   bool bad = false;
   // 16-byte output groups aligned in memory; group g covers unit bytes
   // [16 g - mis, 16 g - mis + 16).  Groups straddling the unit's ends are
@@ -1011,7 +1035,8 @@ __device__ __forceinline__ void link64_load(const uint16_t *__restrict__ scratch
   }
 }
 
-__global__ void __launch_bounds__(LINK_THREADS) zs_link64_kernel(ZsCJobDev *__restrict__ cjobs, const uint16_t *__restrict__ scratch,
+__global__ void __launch_bounds__(LINK_THREADS) zs_link64_kernel(const ZsJobDev *__restrict__ jobs, ZsCJobDev *__restrict__ cjobs,
+                                                                 const uint16_t *__restrict__ scratch,
                                                                  uint8_t *__restrict__ windows, const ZsLinkInfo *__restrict__ info,
                                                                  uint32_t *__restrict__ fallback) {
   __shared__ uint8_t s_win[2][H64];
@@ -1020,7 +1045,12 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_link64_kernel(ZsCJobDev *__re
   const ZsCJobDev cj = cjobs[blockIdx.x];
   if (!cj.ok) return;
   if (t == 0) s_bad = 0;
-  uint32_t wv = 0;
+  const ZsJobDev jb = jobs[cj.job];
+  const bool cont = (jb.flags & ZS_JF_CONT) != 0;  // as zs_link_kernel
+  uint32_t wv = cont ? min(jb.hist, H64) : 0u;
+  if (cont)
+    for (uint32_t i = H64 - wv + t; i < H64; i += LINK_THREADS) s_win[0][i] = jb.out[(int64_t)i - (int64_t)H64];
+  __syncthreads();
   int cur = 0;
   bool bad = false;
   uint4 v[L64_G];
@@ -1031,7 +1061,7 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_link64_kernel(ZsCJobDev *__re
     const uint32_t n = li.n_out;
     uint8_t *W = s_win[cur];
     uint8_t *W2 = s_win[cur ^ 1];
-    if (j != 0) {
+    if (j != 0 || cont) {
       uint8_t *g = windows + (size_t)li.unit * H64;
       for (uint32_t i = t * 16; i < H64; i += LINK_THREADS * 16)
         *reinterpret_cast<uint4 *>(g + i) = *reinterpret_cast<const uint4 *>(W + i);
@@ -1079,16 +1109,18 @@ __global__ void __launch_bounds__(EMIT_THREADS) zs_emit64_kernel(const ZsJobDev 
   const uint32_t t = threadIdx.x;
   const ZsChunkDev ch = chunks[c];
   if (!ch.in_chain || fallback[ch.job]) return;
-  if (ch.ord != 0) {
+  const ZsJobDev jb = jobs[ch.job];
+  const uint64_t hist = (jb.flags & ZS_JF_CONT) ? jb.hist : 0u;
+  if (ch.ord != 0 || hist) {
     const uint8_t *g = windows + (size_t)c * H64;
     for (uint32_t i = t * 16; i < H64; i += EMIT_THREADS * 16)
       *reinterpret_cast<uint4 *>(s_w + i) = *reinterpret_cast<const uint4 *>(g + i);
     __syncthreads();
   }
-  uint8_t *out = jobs[ch.job].out + ch.out_off;
+  uint8_t *out = jb.out + ch.out_off;
   const uint32_t *e = reinterpret_cast<const uint32_t *>(scratch + ch.scratch);
   const uint32_t n = ch.n_out;
-  const uint32_t lowest = H64 - (uint32_t)min<uint64_t>(H64, ch.out_off);
+  const uint32_t lowest = H64 - (uint32_t)min<uint64_t>(H64, ch.out_off + hist);
   bool bad = false;
   for (uint32_t i = t; i < n; i += EMIT_THREADS) {
     const uint32_t v = e[i];
@@ -1177,22 +1209,36 @@ __global__ void __launch_bounds__(PL_T) zs_plink_step_kernel(const ZsCJobDev *__
   for (uint32_t k = 0; k < PL_E; k++) b[i0 + k * PL_T] = v[k];
 }
 
-// windows[unit slot of member j] = W_j as bytes (refs before the stream start: 0)
+// windows[unit slot of member j] = W_j as bytes.  Refs before the stream
+// start: 0 -- or, in a later piece of a long stream (ZS_JF_CONT), the earlier
+// pieces' output before the piece, W_0 (member 0's map is the identity).
 template <uint32_t HN, typename T>
-__global__ void __launch_bounds__(PL_T) zs_plink_out_kernel(const ZsCJobDev *__restrict__ cjobs, uint32_t ncj,
+__global__ void __launch_bounds__(PL_T) zs_plink_out_kernel(const ZsJobDev *__restrict__ jobs,
+                                                            const ZsCJobDev *__restrict__ cjobs, uint32_t ncj,
                                                             const ZsLinkInfo *__restrict__ info, const T *__restrict__ A,
                                                             uint8_t *__restrict__ windows) {
   const uint32_t u = blockIdx.y;
   uint32_t q, j;
-  if (!pl_member(cjobs, ncj, u, &q, &j) || j == 0) return;
+  if (!pl_member(cjobs, ncj, u, &q, &j)) return;
+  const ZsJobDev jb = jobs[cjobs[q].job];
+  const uint32_t hist = (jb.flags & ZS_JF_CONT) ? min(jb.hist, HN) : 0u;
+  if (j == 0 && !hist) return;
   const uint32_t c = info[cjobs[q].unit0 + j].unit;
   const T *a = A + (size_t)u * HN;
   uint8_t *w = windows + (size_t)c * HN;
   const uint32_t i0 = blockIdx.x * PL_BLK + threadIdx.x;
 #pragma unroll
   for (uint32_t k = 0; k < PL_E; k++) {
-    const uint32_t x = a[i0 + k * PL_T];
-    w[i0 + k * PL_T] = x < MARK_BASE ? (uint8_t)x : (uint8_t)0;
+    const uint32_t i = i0 + k * PL_T;
+    const uint32_t x = j ? (uint32_t)a[i] : MARK_BASE + i;
+    uint8_t b = 0;
+    if (x < MARK_BASE) {
+      b = (uint8_t)x;
+    } else {
+      const uint32_t wx = (x - MARK_BASE) & (HN - 1);
+      if (wx >= HN - hist) b = jb.out[(int64_t)wx - (int64_t)HN];
+    }
+    w[i] = b;
   }
 }
 
@@ -1246,8 +1292,8 @@ extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_hea
         A = B;
         B = t;
       }
-      hipLaunchKernelGGL((zs_plink_out_kernel<65536u, uint32_t>), grid, dim3(PL_T), 0, st, d_cjobs, ncjobs, info, A,
-                         d_windows);
+      hipLaunchKernelGGL((zs_plink_out_kernel<65536u, uint32_t>), grid, dim3(PL_T), 0, st, d_jobs, d_cjobs, ncjobs, info,
+                         A, d_windows);
     } else {
       uint16_t *A = static_cast<uint16_t *>(d_plink), *B = A + (size_t)nunit_slots * HIST;
       hipLaunchKernelGGL((zs_plink_init_kernel<HIST, uint16_t>), grid, dim3(PL_T), 0, st, d_cjobs, ncjobs, d_scratch,
@@ -1258,7 +1304,7 @@ extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_hea
         A = B;
         B = t;
       }
-      hipLaunchKernelGGL((zs_plink_out_kernel<HIST, uint16_t>), grid, dim3(PL_T), 0, st, d_cjobs, ncjobs, info, A,
+      hipLaunchKernelGGL((zs_plink_out_kernel<HIST, uint16_t>), grid, dim3(PL_T), 0, st, d_jobs, d_cjobs, ncjobs, info, A,
                          d_windows);
     }
     if (ev) (void)hipEventRecord(ev[4], st);
@@ -1269,8 +1315,8 @@ extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_hea
       hipLaunchKernelGGL(zs_emit_kernel<HIST>, dim3(nunit_slots), dim3(EMIT_THREADS), 0, st, d_jobs, d_units, d_scratch,
                          d_windows, d_fallback);
   } else if (d64) {
-    hipLaunchKernelGGL(zs_link64_kernel, dim3(ncjobs), dim3(LINK_THREADS), 0, st, d_cjobs, d_scratch, d_windows, info,
-                       d_fallback);
+    hipLaunchKernelGGL(zs_link64_kernel, dim3(ncjobs), dim3(LINK_THREADS), 0, st, d_jobs, d_cjobs, d_scratch, d_windows,
+                       info, d_fallback);
     if (ev) (void)hipEventRecord(ev[4], st);
     hipLaunchKernelGGL(zs_emit64_kernel, dim3(nunit_slots), dim3(EMIT_THREADS), 0, st, d_jobs, d_units, d_scratch,
                        d_windows, d_fallback);

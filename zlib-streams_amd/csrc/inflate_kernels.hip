@@ -263,7 +263,13 @@ struct Inflater {
   __device__ void flush_piece() {
     uint32_t lane = lane_id();
     uint4 v = *reinterpret_cast<const uint4 *>(&ring[(flushed + lane * 16) & RMASK]);
-    *reinterpret_cast<uint4 *>(out + flushed + lane * 16) = v;
+    if (__builtin_expect((reinterpret_cast<uintptr_t>(out) & 15u) == 0, 1)) {
+      *reinterpret_cast<uint4 *>(out + flushed + lane * 16) = v;
+    } else {  // a later piece of a long stream starts at any output byte
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int k = 0; k < 16; k++) out[flushed + lane * 16 + k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+    }
     flushed += FLUSH_BYTES;
   }
   __device__ __forceinline__ void maybe_flush() {
@@ -358,6 +364,9 @@ struct Inflater {
   // the same bits and output).
   uint32_t r_mode, r_bit, r_len, r_dist, r_btype, r_nlen, r_ndist;
   bool blast;  // BFINAL of the current block
+  // ZS_JF_PART (a piece of a longer stream): stop with ZD_STOP at the first
+  // block boundary at or past bit stop_after or output byte out_stop
+  uint32_t stop_after = 0xffffffffu, out_stop = 0xffffffffu;
 
   // stored bytes [src, src + slen) (src/inflate.c:885-904 COPY); -1 = complete
   __device__ int stored_copy(uint32_t src, uint32_t slen) {
@@ -932,13 +941,17 @@ struct Inflater {
       }
       in_block = true;
     }
-    for (;;) {
+    for (bool first = true;; first = false) {
       if (!in_block) {
         if (blast) {
           stop_bits = bitpos();
           r_mode = ZSM_CHECK;
           r_bit = (stop_bits + 7u) & ~7u;
           return ZD_END;
+        }
+        if (!first && (bitpos() >= stop_after || pos >= out_stop)) {
+          stop_bits = bitpos();
+          return ZD_STOP;
         }
         rc = block_header(&lt, &dt, &lbits, &dbits);
         if (rc == -2) continue;
@@ -999,9 +1012,19 @@ __global__ void __launch_bounds__(64) zs_decode_kernel(const ZsJobDev *__restric
   f.pos = 0;
   f.flushed = 0;
   f.whave = 0;
+  if (jb.flags & ZS_JF_CONT) {  // a later piece: the output before `out` is its history
+    const uint32_t hv = min(jb.hist, RING);
+    for (uint32_t i = threadIdx.x; i < hv; i += WAVE) s_ring[RING - hv + i] = jb.out[(int64_t)i - (int64_t)hv];
+    __syncthreads();
+    f.whave = hv;
+  }
+  if (jb.flags & ZS_JF_PART) {
+    f.stop_after = mis * 8u + jb.stop_after;
+    f.out_stop = (uint32_t)ZS_PART_OUT;
+  }
   f.fixed_ready = false;
   f.blast = false;
-  f.seek((mis + (uint32_t)hd.start_byte) * 8u);
+  f.seek((mis + (uint32_t)hd.start_byte) * 8u + jb.sbit);
   f.stop_bits = 0;
   [[maybe_unused]] const uint64_t kt0 = KP_NOW();
   const int packed = f.run(ZSM_TYPE);

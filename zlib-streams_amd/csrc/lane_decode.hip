@@ -972,7 +972,8 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
       s.tcap = ch.tcap;
       s.unit = c;
       s.cap = ch.cap;
-      s.whave = ch.ord == 0 ? 0u : (D64 ? 65536u : HIST);
+      s.whave = ch.ord == 0 ? ((jb.flags & ZS_JF_CONT) ? min(jb.hist, D64 ? 65536u : HIST) : 0u)  // a later piece's unit 0: history
+                            : (D64 ? 65536u : HIST);
       s.bit = ch.start_bit;
       s.stop = ch.stop_bit;
       s.sidx = c + 1;
@@ -1400,7 +1401,8 @@ __global__ void __launch_bounds__(64) zs_unitw_kernel(const ZsJobDev *__restrict
   s.unit = c;
   s.cap = ch.cap;
   s.capx = ch.cap;
-  s.whave = ch.ord == 0 ? 0u : (D64 ? 65536u : HIST);
+  s.whave = ch.ord == 0 ? ((jb.flags & ZS_JF_CONT) ? min(jb.hist, D64 ? 65536u : HIST) : 0u)  // a later piece's unit 0: history
+                        : (D64 ? 65536u : HIST);
   s.bit = ch.start_bit;
   s.stop = ch.stop_bit;
   s.sidx = c + 1;
@@ -1723,13 +1725,14 @@ __global__ void __launch_bounds__(EXP_T) zs_expand_kernel(const ZsJobDev *__rest
     if (!D64) return ring[i];
     return ring[i] | (((uint32_t)(qflag[i >> 2] >> (i & 3u)) & 1u) << 16);
   };
-  (void)jobs;
 #if KP_ON
   const uint64_t kp_t0 = KP_NOW();
   uint64_t kp_jump = 0;
   uint32_t kp_rounds = 0, kp_jits = 0, kp_jrounds = 0, kp_batches = 0;
 #endif
-  if (ch.ord != 0) {  // history before the chunk: markers 256 + w for position w - HN
+  // history before the chunk (every unit after the first, and the first of a
+  // later piece of a long stream): markers 256 + w for position w - HN
+  if (ch.ord != 0 || (jobs[ch.job].flags & ZS_JF_CONT)) {
     uint32_t *r32 = reinterpret_cast<uint32_t *>(ring);
     for (uint32_t i = tid; i < HN / 2; i += EXP_T) r32[i] = ((MARK_BASE + 2 * i) & 0xffffu) | ((MARK_BASE + 2 * i + 1) << 16);
     if (D64)

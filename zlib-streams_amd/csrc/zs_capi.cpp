@@ -345,6 +345,22 @@ void fill_result(zs_result *r, int ret, const ZsResultDev *d) {
   }
 }
 
+// Limits of one launch (u32 bit and output positions inside the kernels); a
+// stream past them decodes in pieces (run_pieces).
+constexpr uint64_t ONE_IN_MAX = (1ull << 29) - 4096;
+constexpr uint64_t ONE_OUT_MAX = 0xfff00000ull;
+// compressed bytes per piece (env ZS_PIECE_KB, read per batch: tests set it
+// to split small streams; a stream longer than it then decodes in pieces too)
+uint64_t piece_bytes(bool *forced) {
+  const char *e = std::getenv("ZS_PIECE_KB");
+  const long kb = e ? std::atol(e) : 0;
+  *forced = kb > 0;
+  return kb > 0 ? std::max<uint64_t>(64, (uint64_t)kb) * 1024u : (256ull << 20);
+}
+
+int run_jobs(uint32_t nv, uint64_t max_out, uint32_t flags, ZsDecDev *dec_out, ZsHeadDev *head_out);
+int run_pieces(const ZsJobDev &full, uint64_t piece, uint32_t flags, ZsResultDev *res, uint32_t stats[4]);
+
 int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t flags) {
   int r = ws_init();
   if (r) {
@@ -353,9 +369,15 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
   }
   if ((r = ws_reserve_jobs(n))) return r;
   const bool dev = (flags & ZS_F_DEVICE) != 0;
-  // validate + lay out the staging arenas
+  bool forced = false;
+  const uint64_t piece = piece_bytes(&forced);
+  // validate + lay out the staging arenas; streams past one launch's limits
+  // (or, with ZS_PIECE_KB, longer than a piece) are decoded in pieces after
+  // the batch
+  constexpr uint32_t LONG = UINT32_MAX - 1;
   std::vector<uint32_t> slot(n, UINT32_MAX);
   std::vector<size_t> in_off(n, 0), out_off(n, 0);
+  std::vector<ZsJobDev> longs(n);
   size_t in_total = 0, out_total = 0;
   uint64_t max_out = 0;
   uint32_t nv = 0;
@@ -363,19 +385,17 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
     ZsJobDev jd{};
     const bool copy = jobs[i].mode == ZS_JOB_COPY;
     bool ok = (jobs[i].mode == ZS_JOB_INFLATE || copy) && parse_wbits(copy ? -15 : jobs[i].window_bits, &jd) &&
-              jobs[i].in_len < (1ull << 29) &&
-              jobs[i].out_cap < (1ull << 32) && (jobs[i].in || jobs[i].in_len == 0) &&
-              (jobs[i].out || jobs[i].out_cap == 0);
+              (jobs[i].in || jobs[i].in_len == 0) && (jobs[i].out || jobs[i].out_cap == 0);
     if (dev && jobs[i].out && (reinterpret_cast<uintptr_t>(jobs[i].out) & 15u)) ok = false;
     if (!ok) {
       fill_result(&results[i], Z_STREAM_ERROR, nullptr);
       continue;
     }
-    slot[i] = nv;
+    const bool is_long = !copy && (jobs[i].in_len > ONE_IN_MAX || jobs[i].out_cap > ONE_OUT_MAX ||
+                                   (forced && jobs[i].in_len > piece));
     jd.flags = (copy ? ZS_JF_COPY | ZS_JF_CRC32 : 0) | ((flags & ZS_F_CRC32) && jd.wrap == ZW_RAW ? ZS_JF_CRC32 : 0);
     jd.in_len = jobs[i].in_len;
     jd.out_cap = jobs[i].out_cap;
-    max_out = std::max<uint64_t>(max_out, jd.out_cap);
     if (dev) {
       jd.in = static_cast<const uint8_t *>(jobs[i].in);
       jd.out = static_cast<uint8_t *>(jobs[i].out);
@@ -385,22 +405,59 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
       out_off[i] = out_total;
       out_total += (jobs[i].out_cap + 255) & ~size_t(255);
     }
+    if (is_long) {
+      slot[i] = LONG;
+      longs[i] = jd;
+      continue;
+    }
+    slot[i] = nv;
+    max_out = std::max<uint64_t>(max_out, jd.out_cap);
     g_ws.h_jobs[nv] = jd;
     nv++;
   }
-  if (nv == 0) return 0;
   hipStream_t st = g_ws.stream;
   if (!dev) {
     if ((r = ws_reserve_bytes(&g_ws.d_in, &g_ws.cap_in, in_total + 64))) return r;
     if ((r = ws_reserve_bytes(&g_ws.d_out, &g_ws.cap_out, out_total + 256))) return r;
     for (uint32_t i = 0; i < n; i++) {
       if (slot[i] == UINT32_MAX) continue;
-      ZsJobDev &jd = g_ws.h_jobs[slot[i]];
+      ZsJobDev &jd = slot[i] == LONG ? longs[i] : g_ws.h_jobs[slot[i]];
       jd.in = g_ws.d_in + in_off[i];
       jd.out = g_ws.d_out + out_off[i];
       if (jobs[i].in_len) HIP_OK(hipMemcpyAsync(g_ws.d_in + in_off[i], jobs[i].in, jobs[i].in_len, hipMemcpyHostToDevice, st));
     }
   }
+  uint32_t stats[4] = {0, 0, 0, 0};
+  if (nv) {
+    if ((r = run_jobs(nv, max_out, flags, nullptr, nullptr))) return r;
+    for (int k = 0; k < 4; k++) stats[k] += g_ws.stats[k];
+    for (uint32_t i = 0; i < n; i++) {
+      if (slot[i] == UINT32_MAX || slot[i] == LONG) continue;
+      const ZsResultDev &d = g_ws.h_res[slot[i]];
+      fill_result(&results[i], d.ret, &d);
+      if (!dev && d.total_out)
+        HIP_OK(hipMemcpyAsync(jobs[i].out, g_ws.d_out + out_off[i], d.total_out, hipMemcpyDeviceToHost, st));
+    }
+  }
+  for (uint32_t i = 0; i < n; i++) {
+    if (slot[i] != LONG) continue;
+    ZsResultDev d{};
+    if ((r = run_pieces(longs[i], piece, flags, &d, stats))) return r;
+    fill_result(&results[i], d.ret, &d);
+    if (!dev && d.total_out)
+      HIP_OK(hipMemcpyAsync(jobs[i].out, g_ws.d_out + out_off[i], d.total_out, hipMemcpyDeviceToHost, st));
+  }
+  for (int k = 0; k < 4; k++) g_ws.stats[k] = stats[k];
+  if (!dev) HIP_OK(hipStreamSynchronize(st));
+  return 0;
+}
+
+// One launch over the prepared jobs g_ws.h_jobs[0, nv): routing, the chunked
+// pipeline, the serial decoders, then (dec_out == nullptr) the checks and
+// results into g_ws.h_res, or (pieces) each job's header and decode outcome
+// into head_out / dec_out.
+int run_jobs(uint32_t nv, uint64_t max_out, uint32_t flags, ZsDecDev *dec_out, ZsHeadDev *head_out) {
+  hipStream_t st = g_ws.stream;
   // Route each job: raw/zlib/gzip streams with enough blocks -> speculative
   // chunked path (with the serial decoder as exact fallback); small ones and
   // deflate64 -> the wave-per-stream serial decoder.  Routing looks at the
@@ -417,7 +474,7 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
   for (uint32_t k = 0; k < nv; k++) {
     const ZsJobDev &jd = g_ws.h_jobs[k];
     const bool big = jd.in_len >= 4ull * C || (jd.in_len >= C && jd.out_cap >= (4ull << 20));
-    if (chunking_enabled() && !(jd.flags & ZS_JF_COPY) && big && jd.in_len < (1ull << 29)) {
+    if (chunking_enabled() && !(jd.flags & ZS_JF_COPY) && big) {
       (jd.d64 ? cj64_list : cj_list).push_back(k);
       is_cj[k] = 1;
     }
@@ -461,7 +518,10 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
       // serial decoder answers); every member starts 8-entry aligned
       // (zs_chain_kernel), hence 8 entries of padding per possible unit
       cj.scratch0 = ents;
-      cj.scratch_n = std::min<uint64_t>(jd.out_cap, MAX_RATIO * jd.in_len + 64) + 8ull * max_units;
+      // (a piece of a long stream cuts its chain at ZS_PART_OUT bytes)
+      cj.scratch_n = std::min<uint64_t>(std::min<uint64_t>(jd.out_cap, MAX_RATIO * jd.in_len + 64),
+                                        (jd.flags & ZS_JF_PART) ? ZS_PART_OUT : ~0ull) +
+                     8ull * max_units;
       cj.esz = jd.d64 ? 2u : 1u;  // deflate64: 17-bit entries, stored as u32
       ents += (cj.esz * (cj.scratch_n + 16) + 15) & ~size_t(15);
       in_sum += jd.in_len;
@@ -558,7 +618,7 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
     HIP_OK(hipMemcpyAsync(g_ws.d_decs + copies[q], &copy_decs[q], sizeof(ZsDecDev), hipMemcpyHostToDevice, st));
   }
   if (ev) HIP_OK(hipEventRecord(ev[7], st));
-  zs_launch_finish(g_ws.d_jobs, g_ws.d_heads, g_ws.d_decs, g_ws.d_checks, g_ws.d_res, nv, max_out, st);
+  if (!dec_out) zs_launch_finish(g_ws.d_jobs, g_ws.d_heads, g_ws.d_decs, g_ws.d_checks, g_ws.d_res, nv, max_out, st);
   if (ev) HIP_OK(hipEventRecord(ev[8], st));
   {
     hipError_t le = hipGetLastError();
@@ -567,7 +627,12 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
       return ZS_ENODEV;
     }
   }
-  HIP_OK(hipMemcpyAsync(g_ws.h_res, g_ws.d_res, nv * sizeof(ZsResultDev), hipMemcpyDeviceToHost, st));
+  if (dec_out) {
+    HIP_OK(hipMemcpyAsync(dec_out, g_ws.d_decs, nv * sizeof(ZsDecDev), hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(head_out, g_ws.d_heads, nv * sizeof(ZsHeadDev), hipMemcpyDeviceToHost, st));
+  } else {
+    HIP_OK(hipMemcpyAsync(g_ws.h_res, g_ws.d_res, nv * sizeof(ZsResultDev), hipMemcpyDeviceToHost, st));
+  }
   HIP_OK(hipStreamSynchronize(st));
   if (ev) {
     float ms = 0.f, bms = 0.f;
@@ -611,14 +676,99 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
       }
     }
   }
-  for (uint32_t i = 0; i < n; i++) {
-    if (slot[i] == UINT32_MAX) continue;
-    const ZsResultDev &d = g_ws.h_res[slot[i]];
-    fill_result(&results[i], d.ret, &d);
-    if (!dev && d.total_out)
-      HIP_OK(hipMemcpyAsync(jobs[i].out, g_ws.d_out + out_off[i], d.total_out, hipMemcpyDeviceToHost, st));
+  return 0;
+}
+
+// A stream past one launch's limits, in pieces of `piece` compressed bytes:
+// piece k is a one-job launch over the input from the bit where piece k-1
+// stopped (ZS_JF_CONT: raw deflate at that block boundary, the output so far
+// as history right before its own output), which stops at the last block
+// boundary it verifies (ZS_JF_PART -> ZD_STOP, at most ZS_PART_OUT bytes) --
+// the chunked path's cut chain, or the serial decoder's first boundary past a
+// margin before the piece's end.  The last piece (the rest of the input)
+// decodes to the end of the stream or to its error; the checks and the
+// result then cover the whole stream (zs_finalize_kernel on the full job,
+// with piece 0's header).  A piece that cannot reach a boundary (one deflate
+// block longer than the piece) is retried twice as long.
+int run_pieces(const ZsJobDev &full, uint64_t piece, uint32_t flags, ZsResultDev *res, uint32_t stats[4]) {
+  hipStream_t st = g_ws.stream;
+  const uint32_t HN = full.d64 ? 65536u : 32768u;
+  ZsHeadDev head0{};
+  ZsDecDev fin{};
+  uint64_t bit = 0, total = 0;
+  bool first = true;
+  for (;;) {
+    const uint64_t byte0 = bit >> 3, rem = full.in_len - byte0, ocap = full.out_cap - total;
+    piece = std::min(piece, ONE_IN_MAX);
+    const bool last = rem <= piece;
+    ZsJobDev p = full;
+    p.in = full.in + byte0;
+    p.in_len = last ? rem : piece;
+    p.out = full.out + total;
+    p.out_cap = std::min(ocap, ONE_OUT_MAX);
+    p.flags = 0;
+    p.sbit = (uint32_t)(bit & 7u);
+    if (!first) {
+      p.wrap = ZW_RAW;
+      p.flags |= ZS_JF_CONT;
+      p.hist = (uint32_t)std::min<uint64_t>(total, HN);
+    }
+    const bool part = !last || ocap > ONE_OUT_MAX;
+    if (part) {
+      p.flags |= ZS_JF_PART;
+      p.stop_after = (uint32_t)((p.in_len - std::min<uint64_t>(p.in_len / 2, 1u << 20)) * 8u);
+    }
+    g_ws.h_jobs[0] = p;
+    ZsDecDev dec{};
+    ZsHeadDev hd{};
+    int r = run_jobs(1, p.out_cap, flags, &dec, &hd);
+    if (r) return r;
+    for (int k = 0; k < 4; k++) stats[k] += g_ws.stats[k];
+    if (first) {
+      head0 = hd;
+      if (hd.code != ZD_END) {  // header error / need dictionary: answered by the header alone
+        fin.code = ZD_SKIP;
+        break;
+      }
+    }
+    first = false;
+    // no boundary within one launch's limits (a deflate block of > 512 MiB in
+    // or > 4 GiB out): Z_STREAM_ERROR rather than a guess
+    const bool stuck = (dec.code == ZD_STOP && dec.end_bits <= p.sbit) ||
+                       (part && !last && dec.code == ZD_TRUNC && piece >= ONE_IN_MAX) ||
+                       (part && dec.code == ZD_FULL && ocap > ONE_OUT_MAX);
+    if (stuck) {
+      set_err("a deflate block longer than one launch's limits (512 MiB in, 4 GiB out)");
+      fin.code = ZD_SKIP;
+      head0.code = ZD_SKIP;
+      head0.ret = ZS_STREAM_ERROR;
+      head0.total_in = byte0;
+      head0.msg = ZM_NONE;
+      break;
+    }
+    if (dec.code == ZD_STOP) {
+      bit = byte0 * 8u + dec.end_bits;
+      total += dec.total_out;
+      continue;
+    }
+    if (part && !last && dec.code == ZD_TRUNC) {  // a block longer than the piece: retry it longer
+      piece *= 2;
+      continue;
+    }
+    fin = dec;
+    fin.end_bits = byte0 * 8u + (dec.code == ZD_TRUNC ? p.in_len * 8u : dec.end_bits);
+    fin.total_out = total + dec.total_out;
+    break;
   }
-  if (!dev) HIP_OK(hipStreamSynchronize(st));
+  // the result of the whole stream
+  ZsJobDev j = full;
+  g_ws.h_jobs[0] = j;
+  HIP_OK(hipMemcpyAsync(g_ws.d_jobs, g_ws.h_jobs, sizeof(ZsJobDev), hipMemcpyHostToDevice, st));
+  HIP_OK(hipMemcpyAsync(g_ws.d_heads, &head0, sizeof head0, hipMemcpyHostToDevice, st));
+  HIP_OK(hipMemcpyAsync(g_ws.d_decs, &fin, sizeof fin, hipMemcpyHostToDevice, st));
+  zs_launch_finish(g_ws.d_jobs, g_ws.d_heads, g_ws.d_decs, g_ws.d_checks, g_ws.d_res, 1, std::max<uint64_t>(fin.total_out, 1), st);
+  HIP_OK(hipMemcpyAsync(res, g_ws.d_res, sizeof(ZsResultDev), hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
   return 0;
 }
 

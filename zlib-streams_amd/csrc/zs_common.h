@@ -56,9 +56,19 @@ struct ZsJobDev {
   int32_t d64;         // 1 => raw deflate64 (windowBits == -16)
   int32_t wbits;       // window bits after the reset rules (8..16, or 0 = from header)
   int32_t flags;       // ZS_JF_*
+  // pieces of a stream too long for one launch (zs_capi.cpp run_pieces):
+  uint32_t sbit;       // ZS_JF_CONT: bits of input byte 0 already consumed (0..7)
+  uint32_t hist;       // ZS_JF_CONT: output bytes before `out` that are history (the earlier pieces')
+  uint32_t stop_after; // ZS_JF_PART, serial decoder: stop at the first block boundary at or past this bit
+  uint32_t pad_;
 };
 #define ZS_JF_CRC32 1  // raw stream: CRC-32 of the output into the result's adler (ZIP entries)
 #define ZS_JF_COPY 2   // stored bytes: output = input (ZIP method 0), checked like a raw stream
+#define ZS_JF_CONT 4   // raw deflate resuming at a block boundary (bit sbit), with hist bytes of history
+#define ZS_JF_PART 8   // the input is a piece of a longer stream: stop at a block boundary (ZD_STOP)
+// ZS_JF_PART output budget: the chunked path cuts its chain, the serial
+// decoder stops at a block boundary, once a piece has produced this much
+#define ZS_PART_OUT (1ull << 30)
 
 // Decoder outcome codes (device -> finalize).
 enum ZsDecCode {
