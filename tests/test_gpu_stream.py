@@ -219,8 +219,8 @@ def test_zlib_abi_one_shot_fast_path(zs):
     L.inflate.argtypes = [ctypes.POINTER(libz_ref.ZStream), ctypes.c_int]
     L.inflateEnd.argtypes = [ctypes.POINTER(libz_ref.ZStream)]
     raw = corpus.stream(9, 6 << 20)
-    for wb in (-15, 15, 31):
-        data = _comp(raw, wb)
+    for wb in (-15, 15, 31, -16):  # -16: deflate64 (inflate9_process), block-parallel too
+        data = _comp(raw, wb) if wb != -16 else zs.deflate_batch([raw], -16, 6)[0][0]
         for out_len, fl in ((len(raw) + 10, 4), (len(raw), 0), (len(raw) // 2, 0), (len(raw) // 2, 4)):
             g, o = _GpuZ(L, wb), O.Stream(wb)
             rg, ro = g.call(data, out_len, fl), o.call(data, out_len, fl)

@@ -1064,7 +1064,7 @@ int stream_call(StreamState *s, const uint8_t *in, unsigned in_len, uint8_t *out
   if (s->mode == ZSM_BAD) return Z_DATA_ERROR;
   if (s->mode == ZSM_DICT) return Z_NEED_DICT;
   int fret;
-  if (s->total_in == 0 && s->total_out == 0 && s->carry.empty() && !s->cfg.d64 && in_len >= stream_fast_min() &&
+  if (s->total_in == 0 && s->total_out == 0 && s->carry.empty() && in_len >= stream_fast_min() &&
       stream_fast(s, in, in_len, out, out_len, consumed, produced, &fret)) {
     s->total_in += *consumed;
     s->total_out += *produced;
