@@ -977,11 +977,28 @@ __global__ void __launch_bounds__(DZ_T) zs_dz_emit_kernel(const ZsDJobDev *__res
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(DZ_T) zs_dz_check_kernel(ZsDJobDev *__restrict__ jobs, const ZsDSegDev *__restrict__ segs) {
   __shared__ uint32_t s_tab[4][256];
+  __shared__ ZsCkTabs s_ck;
   __shared__ uint64_t s_red[16];
   const uint32_t t = threadIdx.x;
   const ZsDSegDev sg = segs[blockIdx.x];
   const ZsDJobDev jb = jobs[sg.job];
   if (jb.wrap == 0 || sg.len == 0) return;
+  if ((reinterpret_cast<uintptr_t>(jb.in + sg.start) & 15u) == 0) {  // coalesced 4 KiB steps (zs_check.h)
+    static_assert(DZ_T == ZS_CK_T, "zs_check.h block checks run 256 threads");
+    zs_ck_tables(s_ck);
+    if (jb.wrap == 2) {
+      const uint32_t v = zs_crc_block(jb.in, sg.start, sg.start + sg.len, jb.in_len, s_ck, reinterpret_cast<uint32_t *>(s_red));
+      if (t == 0 && v) atomicXor(reinterpret_cast<unsigned long long *>(&jobs[sg.job].ck_a), (unsigned long long)v);
+    } else {
+      uint64_t sa, sb;
+      zs_adler_block(jb.in, sg.start, sg.start + sg.len, jb.in_len, s_red, &sa, &sb);
+      if (t == 0) {
+        atomicAdd(reinterpret_cast<unsigned long long *>(&jobs[sg.job].ck_a), (unsigned long long)sa);
+        atomicAdd(reinterpret_cast<unsigned long long *>(&jobs[sg.job].ck_b), (unsigned long long)sb);
+      }
+    }
+    return;
+  }
   const uint32_t per = ((sg.len + DZ_T - 1) / DZ_T + 3u) & ~3u;
   const uint64_t lo = sg.start + min(sg.len, per * t), hi = sg.start + min(sg.len, per * (t + 1));
   if (jb.wrap == 2) {

@@ -1325,6 +1325,7 @@ extern "C" void zs_launch_stream(int d64, int run_header, ZsStreamDev *const *d_
 __global__ void __launch_bounds__(CHECK_THREADS) zs_check_kernel(const ZsJobDev *__restrict__ jobs, const ZsHeadDev *__restrict__ heads,
                                                                  const ZsDecDev *__restrict__ decs, uint64_t *__restrict__ checks) {
   __shared__ uint32_t s_tab[4][256];
+  __shared__ ZsCkTabs s_ck;
   __shared__ uint64_t s_red[16];
   const uint32_t j = blockIdx.x;
   const uint32_t t = threadIdx.x;
@@ -1335,10 +1336,25 @@ __global__ void __launch_bounds__(CHECK_THREADS) zs_check_kernel(const ZsJobDev 
   if (hd.code != ZD_END || kind < 0 || dc.code == ZD_SKIP) return;
   const uint8_t *p = jobs[j].out;
   const uint64_t n = dc.total_out;
-  const uint64_t piece = max<uint64_t>(65536u, ((n + gridDim.y - 1) / gridDim.y + 1023u) & ~1023ull);
+  const uint64_t piece = max<uint64_t>(65536u, ((n + gridDim.y - 1) / gridDim.y + ZS_CK_STEP - 1) & ~(uint64_t)(ZS_CK_STEP - 1));
   const uint64_t p0 = (uint64_t)blockIdx.y * piece;
   if (p0 >= n) return;
   const uint64_t plen = min(piece, n - p0);
+  if ((reinterpret_cast<uintptr_t>(p) & 15u) == 0) {  // coalesced 4 KiB steps (zs_check.h)
+    zs_ck_tables(s_ck);
+    if (kind == 1) {
+      const uint32_t v = zs_crc_block(p, p0, p0 + plen, n, s_ck, reinterpret_cast<uint32_t *>(s_red));
+      if (t == 0 && v) atomicXor(reinterpret_cast<unsigned long long *>(&checks[2 * j]), (unsigned long long)v);
+    } else {
+      uint64_t sa, sb;
+      zs_adler_block(p, p0, p0 + plen, n, s_red, &sa, &sb);
+      if (t == 0) {
+        atomicAdd(reinterpret_cast<unsigned long long *>(&checks[2 * j]), (unsigned long long)sa);
+        atomicAdd(reinterpret_cast<unsigned long long *>(&checks[2 * j + 1]), (unsigned long long)sb);
+      }
+    }
+    return;
+  }
   const uint64_t per = ((plen + CHECK_THREADS - 1) / CHECK_THREADS + 3u) & ~3ull;
   const uint64_t lo = p0 + min(plen, per * t), hi = p0 + min(plen, per * (t + 1));
   if (kind == 1) {
