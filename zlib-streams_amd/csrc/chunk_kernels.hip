@@ -90,7 +90,10 @@ __device__ bool validate_header(const uint32_t *w, uint32_t end_byte, uint32_t b
     code = (code + (L > 1 ? cnt[L - 1] : 0)) << (L > 1 ? 1 : 0);
     nxt[L] = code;
   }
-  for (int i = 0; i < 128; i++) lut[i] = 0;
+  // a complete code-length code (src/inftrees.c:137-140 rejects any other for
+  // CODES) fills all 128 LUT entries: no clearing needed
+  if ((cnt[1] << 6) + (cnt[2] << 5) + (cnt[3] << 4) + (cnt[4] << 3) + (cnt[5] << 2) + (cnt[6] << 1) + cnt[7] != 128u)
+    return false;
 #pragma unroll
   for (int s = 0; s < 19; s++) {
     uint32_t L = cl[s];
@@ -184,24 +187,23 @@ __device__ __forceinline__ uint32_t find_scan_excl(uint32_t v, uint32_t *total) 
 
 // code-length-code completeness (Kraft sum == 2^7) of the candidate header at
 // bit p (p - base < 2048): HCLEN at p+13, 3-bit lengths from p+17; the bits
-// come from the step's LDS stage st (words of the input from bit base)
-__device__ __forceinline__ bool cl_complete(const uint32_t *st, uint32_t base, uint32_t p) {
+// come from the step's LDS stage st (words of the input from bit base).  The
+// lengths past HCLEN + 4 are masked off, then the sum goes three lengths at a
+// time through k9 (k9[x] = the Kraft weights 2^(7-L) of the three 3-bit
+// lengths of x, 0 for L = 0): 7 independent LDS reads instead of 19 serial
+// extract/shift/select/add steps.
+__device__ __forceinline__ bool cl_complete(const uint32_t *st, uint32_t base, uint32_t p, const uint16_t *k9) {
   const uint32_t r = p - base, wi = r >> 5, sh = r & 31u;
   const uint64_t a = (uint64_t)st[wi] | ((uint64_t)st[wi + 1] << 32);
   const uint64_t b = (uint64_t)st[wi + 2] | ((uint64_t)st[wi + 3] << 32);
-  const uint64_t h = sh ? ((a >> sh) | (b << (64 - sh))) : a;  // bits p .. p+63 (74 needed: 17 + 57)
-  const uint64_t h2 = sh ? ((b >> sh) | ((uint64_t)st[wi + 4] << (64 - sh))) : b;  // p+64 ..
+  const uint64_t h = sh ? ((a >> sh) | (b << (64 - sh))) : a;
+  const uint64_t h2 = sh ? ((b >> sh) | ((uint64_t)st[wi + 4] << (64 - sh))) : b;
   const uint32_t ncode = (uint32_t)((h >> 13) & 15) + 4;
-  const uint64_t clb = (h >> 17) | (h2 << 47);  // lengths: 57 bits from p+17
-  uint32_t kraft = 0;
-#pragma unroll
-  for (int i = 0; i < 19; i++) {
-    const uint32_t L = (uint32_t)(clb >> (3 * i)) & 7u;
-    if ((uint32_t)i < ncode && L) kraft += 128u >> L;
-  }
+  const uint64_t clb = ((h >> 17) | (h2 << 47)) & (~0ull >> (64 - 3 * ncode));
+  const uint32_t kraft = k9[clb & 511u] + k9[(clb >> 9) & 511u] + k9[(clb >> 18) & 511u] + k9[(clb >> 27) & 511u] +
+                         k9[(clb >> 36) & 511u] + k9[(clb >> 45) & 511u] + k9[(clb >> 54) & 511u];
   return kraft == 128u;
 }
-
 template <bool D64>
 __global__ void __launch_bounds__(64) zs_find_kernel(const ZsJobDev *__restrict__ jobs, const ZsHeadDev *__restrict__ heads,
                                                       ZsSegDev *__restrict__ segs) {
@@ -209,7 +211,17 @@ __global__ void __launch_bounds__(64) zs_find_kernel(const ZsJobDev *__restrict_
   __shared__ uint32_t s_st[WAVE + 8];  // this step's input words (2048 bits + overlap)
   __shared__ uint32_t s_q[WAVE * 12]; // this step's candidates passing the bit-parallel filters
   __shared__ uint32_t s_v[FQ];        // ... and the code-length-code completeness check
+  __shared__ uint16_t s_k9[512];      // Kraft weights of 3 code-length-code lengths (cl_complete)
   const uint32_t lane = threadIdx.x;
+  for (uint32_t x = lane; x < 512; x += WAVE) {
+    uint32_t k = 0;
+    for (int f = 0; f < 3; f++) {
+      const uint32_t L = (x >> (3 * f)) & 7u;
+      k += L ? 128u >> L : 0u;
+    }
+    s_k9[x] = (uint16_t)k;
+  }
+  __builtin_amdgcn_wave_barrier();
   const uint32_t sg = blockIdx.x;
   const ZsSegDev seg = segs[sg];
   const ZsJobDev jb = jobs[seg.job];
@@ -271,7 +283,7 @@ __global__ void __launch_bounds__(64) zs_find_kernel(const ZsJobDev *__restrict_
         bool ok = false;
         if (lane < take) {
           cb = s_q[q0 + lane];
-          ok = cl_complete(s_st, base, cb);
+          ok = cl_complete(s_st, base, cb, s_k9);
         }
         uint32_t vtot;
         const uint32_t vat = find_scan_excl(ok ? 1u : 0u, &vtot);
