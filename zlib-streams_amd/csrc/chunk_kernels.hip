@@ -171,7 +171,7 @@ __device__ bool validate_header(const uint32_t *w, uint32_t end_byte, uint32_t b
 //      through the full header validation, so the expensive check runs
 //      SIMD-parallel instead of stalling the wave lane by lane.
 // ---------------------------------------------------------------------------
-#define FQ 512  // validation queue (ring) per wave
+#define FQ 256  // validation queue (ring) per wave; a step's surplus past it is dropped (hints only)
 
 __device__ __forceinline__ uint32_t find_scan_excl(uint32_t v, uint32_t *total) {
   uint32_t x = v;
@@ -192,7 +192,7 @@ __device__ __forceinline__ uint32_t find_scan_excl(uint32_t v, uint32_t *total) 
 // time through k9 (k9[x] = the Kraft weights 2^(7-L) of the three 3-bit
 // lengths of x, 0 for L = 0): 7 independent LDS reads instead of 19 serial
 // extract/shift/select/add steps.
-__device__ __forceinline__ bool cl_complete(const uint32_t *st, uint32_t base, uint32_t p, const uint16_t *k9) {
+__device__ __forceinline__ bool cl_complete(const uint32_t *st, uint32_t base, uint32_t p, const uint8_t *k9) {
   const uint32_t r = p - base, wi = r >> 5, sh = r & 31u;
   const uint64_t a = (uint64_t)st[wi] | ((uint64_t)st[wi + 1] << 32);
   const uint64_t b = (uint64_t)st[wi + 2] | ((uint64_t)st[wi + 3] << 32);
@@ -207,11 +207,23 @@ __device__ __forceinline__ bool cl_complete(const uint32_t *st, uint32_t base, u
 template <bool D64>
 __global__ void __launch_bounds__(64) zs_find_kernel(const ZsJobDev *__restrict__ jobs, const ZsHeadDev *__restrict__ heads,
                                                       ZsSegDev *__restrict__ segs) {
-  __shared__ uint8_t s_lut[WAVE][128];
   __shared__ uint32_t s_st[WAVE + 8];  // this step's input words (2048 bits + overlap)
-  __shared__ uint32_t s_q[WAVE * 12]; // this step's candidates passing the bit-parallel filters
+  // this step's candidates passing the bit-parallel filters: ~11% of random
+  // bits; past FQC (adversarial bit patterns) the rest of the step is dropped
+  // -- starts are hints, the chain check keeps results exact
+  constexpr uint32_t FQC = WAVE * 12;
+  // full validations run FV lanes at a time: their LUTs then fit the queue's
+  // space, and the smaller LDS footprint raises occupancy
+  constexpr uint32_t FV = 32;
+  // the full validation's per-lane code-length LUTs reuse this space: they are
+  // built after the step's candidates have left it
+  __shared__ union {
+    uint32_t q[FQC];
+    uint8_t lut[FV][128];
+  } s_u;
+  uint32_t *const s_q = s_u.q;
   __shared__ uint32_t s_v[FQ];        // ... and the code-length-code completeness check
-  __shared__ uint16_t s_k9[512];      // Kraft weights of 3 code-length-code lengths (cl_complete)
+  __shared__ uint8_t s_k9[512];       // Kraft weights of 3 code-length-code lengths (cl_complete), <= 192
   const uint32_t lane = threadIdx.x;
   for (uint32_t x = lane; x < 512; x += WAVE) {
     uint32_t k = 0;
@@ -219,7 +231,7 @@ __global__ void __launch_bounds__(64) zs_find_kernel(const ZsJobDev *__restrict_
       const uint32_t L = (x >> (3 * f)) & 7u;
       k += L ? 128u >> L : 0u;
     }
-    s_k9[x] = (uint16_t)k;
+    s_k9[x] = (uint8_t)k;
   }
   __builtin_amdgcn_wave_barrier();
   const uint32_t sg = blockIdx.x;
@@ -270,10 +282,11 @@ __global__ void __launch_bounds__(64) zs_find_kernel(const ZsJobDev *__restrict_
       }
       uint32_t tot;
       const uint32_t at = find_scan_excl((uint32_t)__builtin_popcount(cand), &tot);
-      for (uint32_t k = 0; cand; k++) {
+      for (uint32_t k = 0; cand && at + k < FQC; k++) {
         s_q[at + k] = b0 + (uint32_t)__builtin_ctz(cand);
         cand &= cand - 1u;
       }
+      tot = min(tot, FQC);
       __builtin_amdgcn_wave_barrier();
       // completeness check on this step's candidates, one per lane; survivors
       // keep their order in the validation queue
@@ -287,18 +300,18 @@ __global__ void __launch_bounds__(64) zs_find_kernel(const ZsJobDev *__restrict_
         }
         uint32_t vtot;
         const uint32_t vat = find_scan_excl(ok ? 1u : 0u, &vtot);
-        if (ok) s_v[(vt + vat) & (FQ - 1)] = cb;
-        vt += vtot;
+        if (ok && vt + vat - vh < FQ) s_v[(vt + vat) & (FQ - 1)] = cb;
+        vt = min(vt + vtot, vh + FQ);
       }
       __builtin_amdgcn_wave_barrier();
       // full header validation, one candidate per lane
-      while (vt - vh >= WAVE || (!more && vt != vh)) {
-        const uint32_t take = min(vt - vh, (uint32_t)WAVE);
+      while (vt - vh >= FV || (!more && vt != vh)) {
+        const uint32_t take = min(vt - vh, FV);
         uint32_t cb = 0;
         bool ok = false;
         if (lane < take) {
           cb = s_v[(vh + lane) & (FQ - 1)];
-          ok = validate_header<D64>(w, end_byte, cb, s_lut[lane]);
+          ok = validate_header<D64>(w, end_byte, cb, s_u.lut[lane]);
         }
         uint64_t m = __ballot(ok);
         while (m && nfound < SEG_SLOTS) {
