@@ -204,14 +204,32 @@ __global__ void __launch_bounds__(ZD_MT) zs_zd_match_kernel(const ZsDJobDev *__r
       bool full = true;
       if (best >= 3) full = zd_lw(s_w, c + best - 3) == ow;
       if (full) {
+        // 16 bytes of both strings per iteration: 10 independent LDS dword
+        // reads, one round trip (a 4-byte step paid one per 4 bytes)
         uint32_t n = 0;
         for (;;) {
-          const uint32_t x = zd_lw(s_w, c + n) ^ zd_lw(s_w, pi + n);
+          const uint32_t a = c + n, b = pi + n;
+          const uint32_t wa = a >> 2, wb = b >> 2, sa = a & 3u, sb = b & 3u;
+          uint32_t ua[5], ub[5];
+#pragma unroll
+          for (int k = 0; k < 5; k++) {
+            ua[k] = s_w[wa + k];
+            ub[k] = s_w[wb + k];
+          }
+          uint32_t x = 0, k = 0;
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            const uint32_t d = __builtin_amdgcn_alignbyte(ua[j + 1], ua[j], sa) ^ __builtin_amdgcn_alignbyte(ub[j + 1], ub[j], sb);
+            if (x == 0) {
+              x = d;
+              k = (uint32_t)j;
+            }
+          }
           if (x) {
-            n += (uint32_t)__builtin_ctz(x) >> 3;
+            n += 4 * k + ((uint32_t)__builtin_ctz(x) >> 3);
             break;
           }
-          n += 4;
+          n += 16;
           if (n >= cap) break;
         }
         n = min(n, cap);
