@@ -150,6 +150,9 @@ typedef struct zs_djob {
    (deflate64) and ZS_F_DEFLATE_FAST write valid deflate that any inflater
    decodes to the input, with the GPU's own block structure (not zlib's bytes). */
 #define ZS_F_DEFLATE_FAST 4u /* levels 4..9: the throughput path instead of zlib's bytes */
+#define ZS_F_DEFLATE_SYNC 64u /* end each job as deflate(Z_SYNC_FLUSH) does at the end of its input: blocks
+                                 not final, then an empty stored block (00 00 FF FF), no trailer; res.adler
+                                 still holds the input's check (zlib/gzip) */
 int zs_deflate_batch(const zs_djob *jobs, uint32_t n, zs_result *results, uint32_t flags);
 uint64_t zs_deflate_bound(uint64_t in_len, int32_t window_bits);
 /* accumulated deflate timing (zs_profile(1) enables): [0] whole pipeline ms,

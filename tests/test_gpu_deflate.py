@@ -262,3 +262,113 @@ def test_deflate_device_pointers(zs):
     dst = torch.zeros(cap, dtype=torch.uint8, device="cuda")
     info = zs.deflate_batch_device([src.data_ptr()], [len(data)], [dst.data_ptr()], [cap], -15, 6)[0]
     assert info["ret"] == 1 and dst[:info["total_out"]].cpu().numpy().tobytes() == ref
+
+
+class _GpuDeflate:
+    """deflateInit2_ / deflate / deflateEnd through the library's zlib ABI."""
+
+    def __init__(self, zs, level, wb):
+        import libz_ref
+        self.Z = libz_ref.ZStream
+        L = self.L = ctypes.CDLL(zs.LIB_PATH)
+        L.deflateInit2_.argtypes = [ctypes.POINTER(self.Z), ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                    ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+        L.deflate.argtypes = [ctypes.POINTER(self.Z), ctypes.c_int]
+        L.deflateEnd.argtypes = [ctypes.POINTER(self.Z)]
+        self.s = self.Z()
+        assert L.deflateInit2_(ctypes.byref(self.s), level, 8, wb, 8, 0, b"1.2.11", ctypes.sizeof(self.Z)) == 0
+        self.ob = ctypes.create_string_buffer(5000)
+
+    def call(self, data, flush):
+        """One deflate() with `data`, then the same flush again while the output
+        buffer comes back full (zlib's calling convention); returns (bytes, last ret)."""
+        ib = ctypes.create_string_buffer(data, max(len(data), 1))
+        s = self.s
+        s.next_in = ctypes.cast(ib, ctypes.c_void_p)
+        s.avail_in = len(data)
+        out = bytearray()
+        while True:
+            s.next_out = ctypes.cast(self.ob, ctypes.c_void_p)
+            s.avail_out = len(self.ob)
+            ret = self.L.deflate(ctypes.byref(s), flush)
+            out += self.ob.raw[:len(self.ob) - s.avail_out]
+            if ret != 0 or s.avail_out != 0:
+                return bytes(out), ret
+
+    def end(self):
+        return self.L.deflateEnd(ctypes.byref(self.s))
+
+
+def test_deflate_flush_points(zs):
+    """Z_SYNC_FLUSH / Z_FULL_FLUSH / Z_PARTIAL_FLUSH / Z_BLOCK mid-stream: after
+    every flush the output so far decodes (host zlib, streaming) to exactly the
+    input so far; the finished stream decodes to the input with its trailer
+    checked (the oracle and host zlib).  zlib.h: deflate() flush semantics."""
+    rng = random.Random(7)
+    data = corpus.stream(14, 1500000)
+    for wb in (-15, 15, 31):
+        for level in (1, 6, 9):
+            g = _GpuDeflate(zs, level, wb)
+            d = zlib.decompressobj(wb)
+            out, got, off = bytearray(), bytearray(), 0
+            while off < len(data):
+                n = rng.choice([1, 100, 5000, 70000, 300000])
+                chunk = data[off:off + n]
+                off += len(chunk)
+                fl = rng.choice([0, 0, 2, 3, 1, 5])  # NO_FLUSH, SYNC, FULL, PARTIAL, BLOCK
+                o, ret = g.call(chunk, fl)
+                assert ret == 0, (wb, level, fl, ret)
+                out += o
+                got += d.decompress(o)
+                if fl:
+                    assert bytes(got) == data[:off], (wb, level, fl, off, len(got))
+            o, ret = g.call(b"", 4)
+            assert ret == 1
+            out += o
+            assert g.s.adler == expected_check(data, wb) and g.s.total_in == len(data) and g.s.total_out == len(out)
+            assert g.end() == 0
+            eo, ei = O.oneshot(bytes(out), wb, len(data) + 64)
+            assert ei["ret"] == 1 and eo == data and ei["total_in"] == len(out), (wb, level, ei)
+            assert zlib.decompress(bytes(out), wb) == data
+
+
+def test_deflate_sync_flush_is_zlibs(zs):
+    """NO_FLUSH ... Z_SYNC_FLUSH, then Z_FINISH: zlib's exact bytes (levels 4..9:
+    the sync flush ends the last block with BFINAL = 0 and no empty block, then
+    the empty stored block; deflate.c deflate_slow / deflate()); a repeated
+    flush with no input makes no progress (Z_BUF_ERROR)."""
+    data = corpus.stream(15, 700000)
+    for wb in (-15, 15, 31):
+        for level in (6, 9):
+            c = zlib.compressobj(level, zlib.DEFLATED, wb, 8, zlib.Z_DEFAULT_STRATEGY)
+            ref_sync = c.compress(data) + c.flush(zlib.Z_SYNC_FLUSH)
+            ref_end = c.flush(zlib.Z_FINISH)
+            g = _GpuDeflate(zs, level, wb)
+            o1, r1 = g.call(data, 2)
+            assert r1 == 0 and o1 == ref_sync, (wb, level, len(o1), len(ref_sync))
+            o2, r2 = g.call(b"", 2)
+            assert r2 == -5 and o2 == b""  # Z_BUF_ERROR
+            o3, r3 = g.call(b"", 4)
+            assert r3 == 1 and o3 == ref_end, (wb, level, o3.hex(), ref_end.hex())
+            assert g.end() == 0
+
+
+def test_deflate_stream_buffer_bound(zs, monkeypatch):
+    """Past ZS_DSTREAM_MAX_KB of accumulated input a stream emits a segment
+    (sync-flush ending) without waiting for a flush: output arrives while the
+    input does, and the stream still decodes to the input."""
+    monkeypatch.setenv("ZS_DSTREAM_MAX_KB", "256")
+    data = corpus.stream(16, 2 << 20)
+    for wb in (-15, 31):
+        g = _GpuDeflate(zs, 6, wb)
+        out, early = bytearray(), 0
+        for off in range(0, len(data), 65536):
+            o, ret = g.call(data[off:off + 65536], 0)
+            assert ret == 0
+            out += o
+            early += len(o)
+        o, ret = g.call(b"", 4)
+        assert ret == 1
+        out += o
+        assert early > 0 and g.end() == 0
+        assert zlib.decompress(bytes(out), wb) == data

@@ -1042,8 +1042,9 @@ __global__ void __launch_bounds__(DZ_JT) zs_dz_offsets_kernel(ZsDJobDev *__restr
       s_sum[k] = acc;
       acc += x;
     }
-    const uint64_t body_bytes = (acc + 7) / 8;
-    const uint32_t tr = jb.wrap == 2 ? 8u : (jb.wrap == 1 ? 4u : 0u);
+    // (sync: 3 header bits of the empty stored block, padding, 00 00 FF FF)
+    const uint64_t body_bytes = (acc + (jb.sync ? 3u : 0u) + 7) / 8;
+    const uint32_t tr = jb.sync ? 4u : (jb.wrap == 2 ? 8u : (jb.wrap == 1 ? 4u : 0u));
     jobs[blockIdx.x].total_out = body_bytes + tr;
   }
   __syncthreads();
@@ -1111,6 +1112,14 @@ __global__ void zs_dz_trailer_kernel(const ZsDJobDev *__restrict__ jobs, uint32_
   const ZsDJobDev jb = jobs[j];
   if (jb.exact != exact) return;
   uint8_t *o = stage + jb.stage;
+  if (jb.sync) {  // the empty stored block's LEN / NLEN (its header bits and padding are zero)
+    uint8_t *p = o + jb.total_out - 4;
+    p[0] = 0;
+    p[1] = 0;
+    p[2] = 0xff;
+    p[3] = 0xff;
+    return;
+  }
   const uint64_t tr = jb.wrap == 2 ? 8u : (jb.wrap == 1 ? 4u : 0u);
   uint8_t *p = o + jb.total_out - tr;
   if (jb.wrap == 2) {

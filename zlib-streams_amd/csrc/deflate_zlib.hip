@@ -614,7 +614,9 @@ __global__ void __launch_bounds__(1024) zs_zd_blocks_kernel(ZsDJobDev *__restric
     const bool end_lit = acc && zd_getbit(S, L - 1);
     const uint64_t nfull = acc / ZD_BLOCK;
     const bool empty_last = acc % ZD_BLOCK == 0 && !end_lit;
-    jobs[blockIdx.x].nzblk = (uint32_t)(empty_last ? nfull + 1 : (acc + ZD_BLOCK - 1) / ZD_BLOCK);
+    // Z_FINISH flushes an empty last block; Z_SYNC_FLUSH only a non-empty one
+    // (deflate.c deflate_slow: `if (s->sym_next) FLUSH_BLOCK(s, 0)`)
+    jobs[blockIdx.x].nzblk = (uint32_t)(empty_last ? nfull + (jb.sync ? 0u : 1u) : (acc + ZD_BLOCK - 1) / ZD_BLOCK);
     s_sum[1023] = s_sum[1023];  // keep the scan in LDS
   }
   __syncthreads();
@@ -647,14 +649,15 @@ __global__ void zs_zd_blist_kernel(const ZsDJobDev *__restrict__ jobs, uint32_t 
   const uint64_t ns = lastseg.sym0 + lastseg.nsym;
   const uint64_t s0 = (uint64_t)k * ZD_BLOCK;
   const uint64_t s1 = min(ns, s0 + ZD_BLOCK);
-  b.last = k + 1 == jb.nzblk;
+  const bool final_blk = k + 1 == jb.nzblk;
+  b.last = final_blk && !jb.sync;
   b.nsym = (uint32_t)(s1 > s0 ? s1 - s0 : 0);
   b.first = b.nsym ? zd_sym_pos(segs, jb, S, s0) : L;
   b.end = s1 < ns ? zd_sym_pos(segs, jb, S, s1) : L;
   // the flush runs in the iteration whose loop top followed the block's last
   // symbol start; the final block flushes after the loop (top = L)
   uint64_t top = L;
-  if (!b.last) {
+  if (!final_blk) {
     uint64_t x = b.end - 1;
     while (!zd_getbit(S, x)) x--;
     top = x + 1;
@@ -1009,7 +1012,7 @@ __global__ void __launch_bounds__(1024) zs_zd_layout_kernel(ZsDJobDev *__restric
         acc += x;
       }
       s_sum[0] = s_sum[0];
-      jobs[blockIdx.x].total_out = (acc + 7) / 8 + (jb.wrap == 2 ? 8u : (jb.wrap == 1 ? 4u : 0u));
+      jobs[blockIdx.x].total_out = jb.sync ? (acc + 3 + 7) / 8 + 4u : (acc + 7) / 8 + (jb.wrap == 2 ? 8u : (jb.wrap == 1 ? 4u : 0u));
     }
     __syncthreads();
     uint64_t off = s_sum[t];
@@ -1027,7 +1030,8 @@ __global__ void __launch_bounds__(1024) zs_zd_layout_kernel(ZsDJobDev *__restric
       off += b.bits;
     }
     endbit = off;
-    jobs[blockIdx.x].total_out = (endbit + 7) / 8 + (jb.wrap == 2 ? 8u : (jb.wrap == 1 ? 4u : 0u));
+    jobs[blockIdx.x].total_out =
+        jb.sync ? (endbit + 3 + 7) / 8 + 4u : (endbit + 7) / 8 + (jb.wrap == 2 ? 8u : (jb.wrap == 1 ? 4u : 0u));
   }
   if (t == 0) {
     jobs[blockIdx.x].check = jb.wrap == 2   ? zs_crc_final((uint32_t)jb.ck_a, jb.in_len)

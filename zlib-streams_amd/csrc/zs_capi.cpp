@@ -11,6 +11,8 @@
 #include <hip/hip_runtime.h>
 #include <zlib.h>
 
+#include "zs_check.h"
+
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
@@ -1410,6 +1412,7 @@ int deflate_batch_locked(const zs_djob *jobs, uint32_t n, zs_result *results, ui
     jd.level = level;
     jd.wbits = w;
     jd.exact = (!d64 && level >= 4 && !(flags & ZS_F_DEFLATE_FAST)) ? 1u : 0u;
+    jd.sync = (flags & ZS_F_DEFLATE_SYNC) ? 1u : 0u;
     jd.seg0 = (uint32_t)nseg;
     jd.nseg = (uint32_t)std::max<uint64_t>(1, (jd.in_len + DZ_SEG_HOST - 1) / DZ_SEG_HOST);
     jd.stage = stage_total;
@@ -1456,7 +1459,7 @@ int deflate_batch_locked(const zs_djob *jobs, uint32_t n, zs_result *results, ui
     for (uint32_t o = 0; o < jd.nseg; o++, si++) {
       ZsDSegDev sg{};
       sg.job = k;
-      sg.last = o + 1 == jd.nseg;
+      sg.last = o + 1 == jd.nseg && !jd.sync;
       sg.start = (uint64_t)o * DZ_SEG_HOST;
       sg.len = (uint32_t)std::min<uint64_t>(DZ_SEG_HOST, jd.in_len - std::min<uint64_t>(jd.in_len, sg.start));
       sg.tok = (uint64_t)si * DZ_SEG_HOST;
@@ -1517,48 +1520,137 @@ int deflate_batch_locked(const zs_djob *jobs, uint32_t n, zs_result *results, ui
 }
 
 // stream surface for deflate: accept all input, compress at Z_FINISH, serve
+// Deflate stream state.  Input accumulates and compresses as ONE GPU job at
+// Z_FINISH -- zlib's exact bytes for levels 4..9.  A flush (Z_SYNC_FLUSH,
+// Z_FULL_FLUSH, Z_PARTIAL_FLUSH, Z_BLOCK) compresses what has accumulated as
+// a segment ending as deflate(Z_SYNC_FLUSH) does (blocks not final, then the
+// empty stored block 00 00 FF FF: everything so far decodes from the output so
+// far); so does an accumulation past dstream_max() bytes, which bounds host
+// buffering.  Segments after the first carry no header and no history (they
+// restart the window: valid deflate, zlib's bytes only up to the first flush),
+// and the last one ends with the trailer of the whole input (its CRC-32 /
+// Adler-32 combined from the segments' checks).
 struct DStreamState {
   int inited = 0;
   int wbits = 15, level = 6;
-  std::vector<uint8_t> acc;
-  std::vector<uint8_t> out;
+  std::vector<uint8_t> acc;  // input since the last segment
+  std::vector<uint8_t> out;  // output not yet served (from `served` on)
   bool done = false;
   size_t served = 0;
-  uint32_t adler = 1;
+  uint32_t adler = 1;        // strm->adler: check of the input in emitted segments
+  uint32_t nseg = 0;         // segments emitted
+  uint64_t total = 0;        // input bytes in emitted segments
+  bool flushed = false;      // the last segment was a user flush and no input came since
 };
+
+size_t dstream_max() {  // env ZS_DSTREAM_MAX_KB (default 1 GiB)
+  const char *e = std::getenv("ZS_DSTREAM_MAX_KB");
+  const long long kb = e ? std::atoll(e) : (1ll << 20);
+  return (size_t)std::max<long long>(64, kb) << 10;
+}
+
+// checks of A || B from those of A and B (|B| = n2): CRC-32 by x^(8 n2) mod P
+// (reflected), Adler-32 by a = a1 + a2 - 1, b = b1 + b2 + n2 (a1 - 1) mod 65521
+uint32_t crc32_join(uint32_t c1, uint32_t c2, uint64_t n2) {
+  uint32_t sq = 1u << 23, p = 1u << 31;  // x^8, and x^0
+  for (uint64_t k = n2; k; k >>= 1) {
+    if (k & 1) p = zs_gf2_mul(sq, p);
+    sq = zs_gf2_mul(sq, sq);
+  }
+  return (c1 ? zs_gf2_mul(p, c1) : 0u) ^ c2;
+}
+uint32_t adler32_join(uint32_t x1, uint32_t x2, uint64_t n2) {
+  const uint64_t M = 65521, a1 = x1 & 0xffffu, b1 = x1 >> 16, a2 = x2 & 0xffffu, b2 = x2 >> 16;
+  const uint64_t a = (a1 + a2 + M - 1) % M;
+  const uint64_t b = (b1 + b2 + (n2 % M) * ((a1 + M - 1) % M)) % M;
+  return (uint32_t)(a | (b << 16));
+}
+
+// one segment of the stream from s->acc; final: the stream's end
+int dstream_segment(DStreamState *s, bool final) {
+  int wrap = 0;
+  uint32_t w = 15;
+  parse_dz_wbits(s->wbits, &wrap, &w);
+  const size_t hdr = wrap == 2 ? 10u : (wrap == 1 ? 2u : 0u), tr = wrap == 2 ? 8u : (wrap == 1 ? 4u : 0u);
+  std::vector<uint8_t> seg;
+  uint32_t chk = wrap == 2 ? 0u : 1u;  // check of the empty input
+  if (!final && s->acc.empty() && s->nseg > 0) {
+    seg = {0x00, 0x00, 0x00, 0xff, 0xff};  // empty stored block at a byte boundary
+  } else {
+    seg.resize(dz_bound(s->acc.size(), wrap) + 8);
+    zs_djob j{};
+    j.in = s->acc.data();
+    j.in_len = s->acc.size();
+    j.out = seg.data();
+    j.out_cap = seg.size();
+    j.window_bits = s->wbits;
+    j.level = s->level;
+    zs_result res;
+    if (deflate_batch_locked(&j, 1, &res, final ? 0u : ZS_F_DEFLATE_SYNC) || res.ret != Z_STREAM_END)
+      return Z_STREAM_ERROR;
+    seg.resize(res.total_out);
+    chk = res.adler;
+    if (s->nseg > 0) seg.erase(seg.begin(), seg.begin() + (ptrdiff_t)std::min(hdr, seg.size()));  // header once
+  }
+  const uint64_t n = s->acc.size();
+  if (wrap) s->adler = s->nseg == 0 ? chk : (wrap == 2 ? crc32_join(s->adler, chk, n) : adler32_join(s->adler, chk, n));
+  s->total += n;
+  if (final && s->nseg > 0 && tr) {  // the whole input's trailer in place of the last segment's own
+    seg.resize(seg.size() - std::min(tr, seg.size()));
+    const uint32_t c = s->adler, isz = (uint32_t)s->total;
+    if (wrap == 2) {
+      const uint8_t t8[8] = {(uint8_t)c, (uint8_t)(c >> 8), (uint8_t)(c >> 16), (uint8_t)(c >> 24),
+                             (uint8_t)isz, (uint8_t)(isz >> 8), (uint8_t)(isz >> 16), (uint8_t)(isz >> 24)};
+      seg.insert(seg.end(), t8, t8 + 8);
+    } else {
+      const uint8_t t4[4] = {(uint8_t)(c >> 24), (uint8_t)(c >> 16), (uint8_t)(c >> 8), (uint8_t)c};
+      seg.insert(seg.end(), t4, t4 + 4);
+    }
+  }
+  s->nseg++;
+  s->acc.clear();
+  if (s->served == s->out.size()) {
+    s->out.clear();
+    s->served = 0;
+  }
+  s->out.insert(s->out.end(), seg.begin(), seg.end());
+  return Z_OK;
+}
 
 int dstream_call(DStreamState *s, const uint8_t *in, unsigned in_len, uint8_t *out, unsigned out_len, int flush,
                  unsigned *consumed, unsigned *produced) {
   *consumed = 0;
   *produced = 0;
+  bool progress = false;
   if (!s->done) {
-    s->acc.insert(s->acc.end(), in, in + in_len);
-    *consumed = in_len;
-    if (flush != Z_FINISH) return in_len ? Z_OK : Z_BUF_ERROR;
-    int wrap = 0;
-    uint32_t w = 15;
-    parse_dz_wbits(s->wbits, &wrap, &w);
-    s->out.resize(dz_bound(s->acc.size(), wrap));
-    zs_djob j{};
-    j.in = s->acc.data();
-    j.in_len = s->acc.size();
-    j.out = s->out.data();
-    j.out_cap = s->out.size();
-    j.window_bits = s->wbits;
-    j.level = s->level;
-    zs_result res;
-    if (deflate_batch_locked(&j, 1, &res, 0) || res.ret != Z_STREAM_END) return Z_STREAM_ERROR;
-    s->out.resize(res.total_out);
-    s->adler = res.adler;
-    s->done = true;
+    if (in_len) {
+      s->acc.insert(s->acc.end(), in, in + in_len);
+      *consumed = in_len;
+      s->flushed = false;
+      progress = true;
+    }
+    if (flush == Z_FINISH) {
+      if (dstream_segment(s, true)) return Z_STREAM_ERROR;
+      s->done = true;
+      progress = true;
+    } else if (flush != Z_NO_FLUSH) {
+      if (!s->acc.empty() || !s->flushed) {  // a repeated flush with no new input: no progress (Z_BUF_ERROR)
+        if (dstream_segment(s, false)) return Z_STREAM_ERROR;
+        s->flushed = true;
+        progress = true;
+      }
+    } else if (s->acc.size() >= dstream_max()) {
+      if (dstream_segment(s, false)) return Z_STREAM_ERROR;
+    }
   }
   const size_t rem = s->out.size() - s->served;
   const size_t k = std::min<size_t>(rem, out_len);
   if (k) std::memcpy(out, s->out.data() + s->served, k);
   s->served += k;
   *produced = (unsigned)k;
-  if (s->served < s->out.size()) return Z_OK;
-  return Z_STREAM_END;
+  if (k) progress = true;
+  if (s->done && s->served == s->out.size()) return Z_STREAM_END;
+  return progress ? Z_OK : Z_BUF_ERROR;
 }
 
 struct DHandle {
@@ -1832,7 +1924,7 @@ int ZEXPORT deflate(z_streamp strm, int flush) {
   strm->next_out += prod;
   strm->avail_out -= prod;
   strm->total_out += prod;
-  if (s->done) strm->adler = s->adler;
+  if (s->nseg) strm->adler = s->adler;
   return ret;
 }
 int ZEXPORT deflateEnd(z_streamp strm) {

@@ -213,6 +213,11 @@ struct ZsDJobDev {
   uint64_t bm0;        // first word of the job's bitmaps
   uint32_t zblk0;      // first block slot
   uint32_t zblk_cap;   // block slots reserved: ceil(in_len / 16383) + 1
+  // ZS_F_DEFLATE_SYNC: end as zlib's deflate(Z_SYNC_FLUSH) at the end of the
+  // input does -- last block BFINAL = 0 (no empty last block), then an empty
+  // stored block (000, pad, 00 00 FF FF) in place of the trailer
+  uint32_t sync;
+  uint32_t pad_;
 };
 
 // zlib-identical mode (deflate_zlib.hip, levels 4..9): per job, position
