@@ -181,81 +181,80 @@ __global__ void __launch_bounds__(ZD_MT) zs_zd_match_kernel(const ZsDJobDev *__r
   const uint64_t q_end = min(s + wk.len, q_beg + per_w);
   uint64_t nextp = q_beg + WAVE;
   uint64_t p = q_beg + lane;
-  bool active = p < q_end, fresh = true, fin = false;
-  uint32_t c = 0, k = 0, best = 0, bdist = 0, bl = 0, bd = 0, cap = 0, nicep = 0, ow = 0;
+  bool active = p < q_end, fin = false;
+  uint32_t c = 0, k = 0, best = 0, bdist = 0, bl = 0, bd = 0, cap = 0, nicep = 0, ow = 0, pi = 0;
+  // a walk starts at position p: its first candidate, or done at once
+  auto start = [&]() {
+    best = bdist = bl = bd = 0;
+    k = 0;
+    fin = true;
+    if (!active) return;
+    pi = (uint32_t)(p - B);
+    const uint32_t d0 = s_pd[pi];
+    if (p + ZD_MINM <= L && d0 != 0 && d0 <= max_dist) {
+      const uint64_t look = L - p;
+      cap = look < ZD_MAXM ? (uint32_t)look : ZD_MAXM;
+      nicep = look < nice ? (uint32_t)look : nice;
+      c = pi - d0;  // LDS byte index of the candidate
+      fin = false;
+    }
+  };
+  start();
+  // One chain step per iteration for every walking lane, written with selects
+  // (the per-step exec-mask bookkeeping of nested branches cost as many scalar
+  // instructions as the step's vector work); only the full compare branches.
   for (;;) {
-    if (active && fresh) {
-      fresh = false;
-      best = bdist = bl = bd = 0;
-      k = 0;
-      const uint32_t d0 = s_pd[p - B];
-      if (p + ZD_MINM > L || d0 == 0 || d0 > max_dist) {
-        fin = true;
-      } else {
-        const uint64_t look = L - p;
-        cap = look < ZD_MAXM ? (uint32_t)look : ZD_MAXM;
-        nicep = look < nice ? (uint32_t)look : nice;
-        c = (uint32_t)(p - B) - d0;  // LDS byte index of the candidate
+    const bool walking = active && !fin;
+    const uint32_t cc = walking ? c : 0u;
+    const uint32_t nd = s_pd[cc];  // next link, in flight during the compare
+    const uint32_t se = zd_lw(s_w, cc + (best >= 3 ? best - 3 : 0u));
+    if (walking && (best < 3 || se == ow)) {
+      // 16 bytes of both strings per iteration: 10 independent LDS dword
+      // reads, one round trip (a 4-byte step paid one per 4 bytes)
+      uint32_t n = 0;
+      for (;;) {
+        const uint32_t a = c + n, b = pi + n;
+        const uint32_t wa = a >> 2, wb = b >> 2, sa = a & 3u, sb = b & 3u;
+        uint32_t ua[5], ub[5];
+#pragma unroll
+        for (int q = 0; q < 5; q++) {
+          ua[q] = s_w[wa + q];
+          ub[q] = s_w[wb + q];
+        }
+        uint32_t x = 0, g = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const uint32_t d = __builtin_amdgcn_alignbyte(ua[q + 1], ua[q], sa) ^ __builtin_amdgcn_alignbyte(ub[q + 1], ub[q], sb);
+          if (x == 0) {
+            x = d;
+            g = (uint32_t)q;
+          }
+        }
+        if (x) {
+          n += 4 * g + ((uint32_t)__builtin_ctz(x) >> 3);
+          break;
+        }
+        n += 16;
+        if (n >= cap) break;
+      }
+      n = min(n, cap);
+      if (n > best) {
+        best = n;
+        bdist = pi - c;
+        if (best >= 3) ow = zd_lw(s_w, pi + best - 3);
       }
     }
-    if (active && !fin) {
-      const uint32_t pi = (uint32_t)(p - B);
-      const uint32_t nd = s_pd[c];  // next link, in flight during the compare
-      bool full = true;
-      if (best >= 3) full = zd_lw(s_w, c + best - 3) == ow;
-      if (full) {
-        // 16 bytes of both strings per iteration: 10 independent LDS dword
-        // reads, one round trip (a 4-byte step paid one per 4 bytes)
-        uint32_t n = 0;
-        for (;;) {
-          const uint32_t a = c + n, b = pi + n;
-          const uint32_t wa = a >> 2, wb = b >> 2, sa = a & 3u, sb = b & 3u;
-          uint32_t ua[5], ub[5];
-#pragma unroll
-          for (int k = 0; k < 5; k++) {
-            ua[k] = s_w[wa + k];
-            ub[k] = s_w[wb + k];
-          }
-          uint32_t x = 0, k = 0;
-#pragma unroll
-          for (int j = 0; j < 4; j++) {
-            const uint32_t d = __builtin_amdgcn_alignbyte(ua[j + 1], ua[j], sa) ^ __builtin_amdgcn_alignbyte(ub[j + 1], ub[j], sb);
-            if (x == 0) {
-              x = d;
-              k = (uint32_t)j;
-            }
-          }
-          if (x) {
-            n += 4 * k + ((uint32_t)__builtin_ctz(x) >> 3);
-            break;
-          }
-          n += 16;
-          if (n >= cap) break;
-        }
-        n = min(n, cap);
-        if (n > best) {
-          best = n;
-          bdist = pi - c;
-          if (best >= 3) ow = zd_lw(s_w, pi + best - 3);
-        }
-      }
-      k++;
-      if (k == chain_b) {
-        bl = best;
-        bd = bdist;
-      }
-      // zlib: stop at nice, at the chain budget, at a missing link, or when the
-      // next candidate is not above strstart - MAX_DIST
-      if (best >= nicep || k >= chain || nd == 0 || (pi - (c - nd)) >= max_dist) {
-        fin = true;
-        if (k < chain_b) {
-          bl = best;
-          bd = bdist;
-        }
-      } else {
-        c -= nd;
-      }
-    }
+    k += walking ? 1u : 0u;
+    // the chain_b budget's result: at its last candidate, or at an earlier stop
+    // zlib: stop at nice, at the chain budget, at a missing link, or when the
+    // next candidate is not above strstart - MAX_DIST
+    const uint32_t cn = c - nd;
+    const bool stop = walking && (best >= nicep || k >= chain || nd == 0 || (pi - cn) >= max_dist);
+    const bool snap = walking && (k == chain_b || (stop && k < chain_b));
+    bl = snap ? best : bl;
+    bd = snap ? bdist : bd;
+    c = walking && !stop ? cn : c;
+    fin = fin || stop;
     const bool done = active && fin;
     if (done) {
       oa[p] = best | (bdist << 9);
@@ -266,8 +265,7 @@ __global__ void __launch_bounds__(ZD_MT) zs_zd_match_kernel(const ZsDJobDev *__r
       if (done) {
         p = nextp + (uint64_t)__builtin_popcountll(fm & ((1ull << lane) - 1ull));
         active = p < q_end;
-        fresh = true;
-        fin = false;
+        start();
       }
       nextp += (uint64_t)__builtin_popcountll(fm);
     }
