@@ -203,7 +203,7 @@ __global__ void __launch_bounds__(ZD_MT) zs_zd_match_kernel(const ZsDJobDev *__r
   // One chain step per iteration for every walking lane, written with selects
   // (the per-step exec-mask bookkeeping of nested branches cost as many scalar
   // instructions as the step's vector work); only the full compare branches.
-  for (;;) {
+  auto step = [&]() {
     const bool walking = active && !fin;
     const uint32_t cc = walking ? c : 0u;
     const uint32_t nd = s_pd[cc];  // next link, in flight during the compare
@@ -255,6 +255,12 @@ __global__ void __launch_bounds__(ZD_MT) zs_zd_match_kernel(const ZsDJobDev *__r
     bd = snap ? bdist : bd;
     c = walking && !stop ? cn : c;
     fin = fin || stop;
+  };
+  for (;;) {
+    // two steps between refills: the ballot / refill bookkeeping is paid every
+    // other step (a lane that stops after the first idles one step)
+    step();
+    step();
     const bool done = active && fin;
     if (done) {
       oa[p] = best | (bdist << 9);
