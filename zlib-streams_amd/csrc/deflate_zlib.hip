@@ -257,8 +257,10 @@ __global__ void __launch_bounds__(ZD_MT) zs_zd_match_kernel(const ZsDJobDev *__r
     fin = fin || stop;
   };
   for (;;) {
-    // two steps between refills: the ballot / refill bookkeeping is paid every
-    // other step (a lane that stops after the first idles one step)
+    // four steps between refills: the ballot / refill bookkeeping is paid every
+    // fourth step (a lane that stops early idles the rest)
+    step();
+    step();
     step();
     step();
     const bool done = active && fin;
