@@ -257,12 +257,10 @@ __global__ void __launch_bounds__(ZD_MT) zs_zd_match_kernel(const ZsDJobDev *__r
     fin = fin || stop;
   };
   for (;;) {
-    // four steps between refills: the ballot / refill bookkeeping is paid every
-    // fourth step (a lane that stops early idles the rest)
-    step();
-    step();
-    step();
-    step();
+    // eight steps between refills: the ballot / refill bookkeeping is paid
+    // every eighth step (a lane that stops early idles the rest)
+#pragma unroll
+    for (int r = 0; r < 8; r++) step();
     const bool done = active && fin;
     if (done) {
       oa[p] = best | (bdist << 9);
