@@ -260,7 +260,7 @@ __global__ void __launch_bounds__(ZD_MT) zs_zd_match_kernel(const ZsDJobDev *__r
     // eight steps between refills: the ballot / refill bookkeeping is paid
     // every eighth step (a lane that stops early idles the rest)
 #pragma unroll
-    for (int r = 0; r < 8; r++) step();
+    for (int r = 0; r < 16; r++) step();
     const bool done = active && fin;
     if (done) {
       oa[p] = best | (bdist << 9);
