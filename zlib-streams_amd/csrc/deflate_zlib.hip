@@ -13,7 +13,7 @@
 // whose 15-bit hash of in[q..q+2] equals p's.  That makes the search
 // data-parallel; the stages (their semantics pinned on the CPU by
 // tests/tools/dz_model.c against host zlib) are:
-//   zs_zd_prev_kernel   one wave per 128 Ki positions: previous same-hash
+//   zs_zd_prev_kernel   four waves per 128 Ki positions: previous same-hash
 //                       distance of every position (u16 head table in LDS,
 //                       64 positions per step, same-hash lanes found with 15
 //                       ballots; entries aged out every 16 Ki positions);
@@ -72,10 +72,17 @@ __device__ __forceinline__ uint32_t zd_max_dist(const ZsDJobDev &jb) { return (1
 // ---------------------------------------------------------------------------
 // K1: previous same-hash distance (0: none within 32767, or position 0 = NIL)
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(WAVE) zs_zd_prev_kernel(const ZsDJobDev *__restrict__ jobs,
-                                                           const ZsZWorkDev *__restrict__ work, uint16_t *__restrict__ prevd) {
+// Four waves per work item, 256 positions per step: each wave finds, for its
+// 64 positions, the earlier same-hash lanes of its own wave (15 ballots: the
+// bulk of the work, in parallel across the waves); then, in wave order, the
+// lanes with none read the head table and each hash group's last lane writes
+// it (four short phases between barriers).  Occupancy: 2 work items (8 waves)
+// per CU instead of 2 waves.
+#define ZD_PT1 256u
+__global__ void __launch_bounds__(ZD_PT1) zs_zd_prev_kernel(const ZsDJobDev *__restrict__ jobs,
+                                                             const ZsZWorkDev *__restrict__ work, uint16_t *__restrict__ prevd) {
   __shared__ uint16_t head[32768];
-  const uint32_t lane = threadIdx.x;
+  const uint32_t t = threadIdx.x, lane = t & (WAVE - 1), wv = t / WAVE;
   const ZsZWorkDev wk = work[blockIdx.x];
   const ZsDJobDev jb = jobs[wk.job];
   const uint8_t *in = jb.in;
@@ -85,16 +92,16 @@ __global__ void __launch_bounds__(WAVE) zs_zd_prev_kernel(const ZsDJobDev *__res
   // entries hold position & 0xffff; an entry whose age could exceed 32767 is
   // reset every ZD_SWEEP positions to a position 40000 back (age stays in
   // 40000 .. 56384 < 65536 until the next sweep: decoded as "none")
-  auto sweep = [&](uint64_t t) {
-    const uint32_t sent = (uint32_t)((t - 40000u) & 0xffffu);
-    for (uint32_t i = lane * 8; i < 32768u; i += WAVE * 8) {
+  auto sweep = [&](uint64_t b) {
+    const uint32_t sent = (uint32_t)((b - 40000u) & 0xffffu);
+    for (uint32_t i = t * 8; i < 32768u; i += ZD_PT1 * 8) {
       uint4 v = *reinterpret_cast<const uint4 *>(&head[i]);
       uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
       for (int k = 0; k < 4; k++) {
         uint32_t lo = w[k] & 0xffffu, hi = w[k] >> 16;
-        if (((uint32_t)(t - lo) & 0xffffu) > 32768u) lo = sent;
-        if (((uint32_t)(t - hi) & 0xffffu) > 32768u) hi = sent;
+        if (((uint32_t)(b - lo) & 0xffffu) > 32768u) lo = sent;
+        if (((uint32_t)(b - hi) & 0xffffu) > 32768u) hi = sent;
         w[k] = lo | (hi << 16);
       }
       *reinterpret_cast<uint4 *>(&head[i]) = make_uint4(w[0], w[1], w[2], w[3]);
@@ -102,20 +109,21 @@ __global__ void __launch_bounds__(WAVE) zs_zd_prev_kernel(const ZsDJobDev *__res
   };
   {
     const uint32_t sent = (uint32_t)((from - 40000u) & 0xffffu);
-    for (uint32_t i = lane; i < 32768u / 2; i += WAVE) reinterpret_cast<uint32_t *>(head)[i] = sent | (sent << 16);
+    for (uint32_t i = t; i < 32768u / 2; i += ZD_PT1) reinterpret_cast<uint32_t *>(head)[i] = sent | (sent << 16);
   }
-  __builtin_amdgcn_wave_barrier();
+  __syncthreads();
   uint16_t *po = prevd + jb.pos0;
-  for (uint64_t base = from; base < to; base += WAVE) {
+  static_assert(ZD_SWEEP % ZD_PT1 == 0, "sweeps fall on step boundaries");
+  for (uint64_t base = from; base < to; base += ZD_PT1) {
     if (base != from && ((base - from) % ZD_SWEEP) == 0) {
       sweep(base);
-      __builtin_amdgcn_wave_barrier();
+      __syncthreads();
     }
-    const uint64_t p = base + lane;
+    const uint64_t p = base + (uint64_t)wv * WAVE + lane;
     const bool valid = p + 2 < L && p < to;
     uint32_t h = 0;
     if (valid) h = (((uint32_t)in[p] << 10) ^ ((uint32_t)in[p + 1] << 5) ^ in[p + 2]) & 0x7fffu;
-    // lanes with the same hash: 15 ballots
+    // lanes of this wave with the same hash: 15 ballots
     uint64_t m = __ballot(valid);
 #pragma unroll
     for (int b = 0; b < 15; b++) {
@@ -124,16 +132,17 @@ __global__ void __launch_bounds__(WAVE) zs_zd_prev_kernel(const ZsDJobDev *__res
     }
     const uint64_t below = m & ((1ull << lane) - 1ull);
     const uint64_t above = lane == 63 ? 0ull : (m & ~((2ull << lane) - 1ull));
-    uint32_t d;
-    if (below) {
-      d = lane - (63u - (uint32_t)__builtin_clzll(below));
-    } else {
-      const uint32_t v = head[h];
-      d = (uint32_t)(p - v) & 0xffffu;
+    uint32_t d = below ? lane - (63u - (uint32_t)__builtin_clzll(below)) : 0u;
+    // head table in wave order: earlier waves' positions of this step first
+#pragma unroll
+    for (uint32_t ph = 0; ph < ZD_PT1 / WAVE; ph++) {
+      if (wv == ph) {
+        if (!below) d = (uint32_t)(p - head[h]) & 0xffffu;
+        __builtin_amdgcn_wave_barrier();
+        if (valid && !above) head[h] = (uint16_t)(p & 0xffffu);  // the group's latest position
+      }
+      __syncthreads();
     }
-    __builtin_amdgcn_wave_barrier();
-    if (valid && !above) head[h] = (uint16_t)(p & 0xffffu);  // the group's latest position
-    __builtin_amdgcn_wave_barrier();
     if (p >= start && p < to) po[p] = (valid && d < 32768u && p != d) ? (uint16_t)d : (uint16_t)0;
   }
 }
@@ -1202,7 +1211,7 @@ extern "C" int zs_launch_zdeflate(ZsDJobDev *d_jobs, uint32_t njobs, ZsDSegDev *
                                   uint32_t nblk_slots, const uint32_t *d_slot_job, uint32_t *d_aux, uint8_t *d_stage,
                                   uint32_t *d_flag, hipStream_t st, hipEvent_t *ev) {
   if (ev) (void)hipEventRecord(ev[0], st);
-  if (n1) hipLaunchKernelGGL(zs_zd_prev_kernel, dim3(n1), dim3(WAVE), 0, st, d_jobs, d_w1, d_prevd);
+  if (n1) hipLaunchKernelGGL(zs_zd_prev_kernel, dim3(n1), dim3(ZD_PT1), 0, st, d_jobs, d_w1, d_prevd);
   if (n2) hipLaunchKernelGGL(zs_zd_match_kernel, dim3(n2), dim3(ZD_MT), 0, st, d_jobs, d_w2, d_prevd, d_ma, d_mb);
   if (ev) (void)hipEventRecord(ev[1], st);
   hipLaunchKernelGGL(zs_zd_parse_kernel, dim3(nseg), dim3(ZD_PT), 0, st, d_jobs, d_segs, d_ma, d_mb, d_bm);
