@@ -876,6 +876,38 @@ __device__ __forceinline__ ZdTok zd_tok(const ZdTabs &T, const ZdBm &B, uint64_t
   return k;
 }
 
+// f(token) for every token start in [q0, q1), in order: the start bitmap is
+// read a word at a time and walked by its set bits (a per-position test read
+// a bitmap word per input byte)
+template <typename F>
+__device__ __forceinline__ void zd_for_tokens(const ZdTabs &T, const ZdBm &B, uint64_t q0, uint64_t q1, F f) {
+  for (uint64_t wq = q0 & ~31ull; wq < q1; wq += 32) {
+    uint32_t sw = B.S[wq >> 5];
+    if (wq < q0) sw &= ~0u << (q0 - wq);
+    if (q1 - wq < 32) sw &= (1u << (q1 - wq)) - 1u;
+    if (!sw) continue;
+    const uint32_t s_all = B.S[wq >> 5], s_next = B.S[(wq >> 5) + 1], vw = B.V[wq >> 5];
+    while (sw) {
+      const uint32_t b = (uint32_t)__builtin_ctz(sw);
+      sw &= sw - 1u;
+      const uint64_t q = wq + b;
+      const bool next_start = b < 31 ? ((s_all >> (b + 1)) & 1u) : (s_next & 1u);
+      ZdTok k;
+      if (q + 1 >= T.L || next_start) {  // as zd_tok
+        k.len = 0;
+        k.dist = 0;
+        k.lit = T.in[q];
+      } else {
+        const uint32_t m = ((vw >> b) & 1u ? T.mb : T.ma)[q];
+        k.len = m & 511u;
+        k.dist = m >> 9;
+        k.lit = 0;
+      }
+      f(k);
+    }
+  }
+}
+
 // per-block tables in global memory (ZD_AUX words): [0, 286) lit/len code |
 // len << 16, [286, 316) distance, [316, 335) bit-length code
 __global__ void __launch_bounds__(ZD_TT) zs_zd_tree_kernel(const ZsDJobDev *__restrict__ jobs, ZsZBlkDev *__restrict__ blks,
@@ -899,16 +931,14 @@ __global__ void __launch_bounds__(ZD_TT) zs_zd_tree_kernel(const ZsDJobDev *__re
   __syncthreads();
   const uint64_t n = bk.end - bk.first, per = (n + ZD_TT - 1) / ZD_TT;
   const uint64_t q0 = bk.first + min(n, per * t), q1 = bk.first + min(n, per * (t + 1));
-  for (uint64_t q = q0; q < q1; q++) {
-    if (!zd_getbit(B.S, q)) continue;
-    const ZdTok k = zd_tok(T, B, q);
+  zd_for_tokens(T, B, q0, q1, [&](const ZdTok &k) {
     if (!k.len) {
       atomicAdd(&s_lf[k.lit], 1u);
     } else {
       atomicAdd(&s_lf[257 + zd_lcode(k.len)], 1u);
       atomicAdd(&s_df[zd_dcode(k.dist)], 1u);
     }
-  }
+  });
   __syncthreads();
   if (t != 0) return;
   uint8_t stat_l[288], stat_d[30];
@@ -1148,8 +1178,7 @@ __global__ void __launch_bounds__(ZD_TT) zs_zd_emit_kernel(const ZsDJobDev *__re
     return (s_l[257 + lc] >> 16) + zd_xl[lc] + (s_d[dc] >> 16) + zd_xd[dc];
   };
   uint64_t mine = t == 0 ? 3u + bk.hbits : 0u;
-  for (uint64_t q = q0; q < q1; q++)
-    if (zd_getbit(B.S, q)) mine += sym_bits(zd_tok(T, B, q));
+  zd_for_tokens(T, B, q0, q1, [&](const ZdTok &k) { mine += sym_bits(k); });
   if (t == ZD_TT - 1) mine += s_l[256] >> 16;  // end of block
   s_off[t] = mine;
   __syncthreads();
@@ -1183,9 +1212,7 @@ __global__ void __launch_bounds__(ZD_TT) zs_zd_emit_kernel(const ZsDJobDev *__re
       zd_rle(lens, (int)bk.dmax, send);
     }
   }
-  for (uint64_t q = q0; q < q1; q++) {
-    if (!zd_getbit(B.S, q)) continue;
-    const ZdTok k = zd_tok(T, B, q);
+  zd_for_tokens(T, B, q0, q1, [&](const ZdTok &k) {
     if (!k.len) {
       W.put(s_l[k.lit] & 0xffffu, s_l[k.lit] >> 16);
     } else {
@@ -1195,7 +1222,7 @@ __global__ void __launch_bounds__(ZD_TT) zs_zd_emit_kernel(const ZsDJobDev *__re
       W.put(s_d[dc] & 0xffffu, s_d[dc] >> 16);
       if (zd_xd[dc]) W.put(k.dist - zd_dbase(dc), zd_xd[dc]);
     }
-  }
+  });
   if (t == ZD_TT - 1) W.put(s_l[256] & 0xffffu, s_l[256] >> 16);
   W.done();
 }
