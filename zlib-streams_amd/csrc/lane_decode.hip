@@ -1940,6 +1940,200 @@ __global__ void __launch_bounds__(EXP_T) zs_expand_kernel(const ZsJobDev *__rest
 #endif
 }
 
+// ---------------------------------------------------------------------------
+// Expand, 32 KiB window (zs_expand2_kernel): rounds of 2048 entries, 8
+// consecutive entries per thread, decoupled from the token batches (1024
+// tokens, 4 per thread, loaded whenever the next round reaches past the last
+// loaded token), so every round but the unit's last is full.
+//  - Marks: each token writes key (start - R + 1) << 20 | payload at its start
+//    entry (payload: the literal byte, or distance + 256); a running max over
+//    the round (thread, wave DPP scan, per-wave totals) gives every entry its
+//    token's payload directly -- the max-key mark, or the carry of the last
+//    token started before the round (key 0).  Readers zero their marks.
+//  - The ring holds HIST + 2048 entries, so a round's writes never land on a
+//    slot any entry of the round may still read (its sources reach back at
+//    most HIST): every entry is written in the same phase that computes it --
+//    the literal, the ring value of a source before the round, or PTR | the
+//    in-round index of its source.
+//  - After one barrier, entries holding a pointer follow it through the ring
+//    and write back what they found (a value, or the target's own pointer:
+//    pointer jumping without barriers; every pointer points strictly back, so
+//    each lane terminates on its own).
+// Three barriers per round (+1 per token batch); ~15 VALU per entry.
+// ---------------------------------------------------------------------------
+#define EX2_T 256
+#define EX2_W (EX2_T / WAVE)
+#define EX2_E 8
+#define EX2_N (EX2_T * EX2_E)   // entries per round
+#define EX2_RS (HIST + EX2_N)   // ring slots
+#define EX2_TPT 4               // tokens per thread per batch
+#define EX2_TB (EX2_T * EX2_TPT)
+#define EX2_PTR 0xF800u         // ring value >= PTR: pointer to in-round entry (value & 0x7ff)
+static_assert(EX2_RS % EX2_N == 0 && EX2_N <= 2048 && MARK_BASE + HIST <= EX2_PTR, "expand2 layout");
+
+__global__ void __launch_bounds__(EX2_T) zs_expand2_kernel(const ZsJobDev *__restrict__ jobs,
+                                                            const ZsChunkDev *__restrict__ chunks,
+                                                            uint16_t *__restrict__ scratch,
+                                                            const uint32_t *__restrict__ tokens,
+                                                            const uint32_t *__restrict__ order, ZsTokPool pool) {
+  __shared__ __attribute__((aligned(16))) uint16_t ring[EX2_RS];
+  __shared__ __attribute__((aligned(16))) uint32_t s_mark[EX2_N];
+  __shared__ uint32_t s_red[EX2_W];
+  __shared__ uint32_t s_bs[2][EX2_W];
+  const uint32_t tid = threadIdx.x, lane = tid & (WAVE - 1), wv = tid / WAVE;
+  const uint32_t unit = order[blockIdx.x];
+  const ZsChunkDev ch = chunks[unit];
+  if (!ch.in_chain) return;
+  gcu32 *tk = (gcu32 *)(tokens + ch.tok);
+  const uint32_t ntok = ch.n_tok, tcap = ch.tcap, total = ch.n_out;
+  const uint32_t *ptab = pool.ptab + (size_t)unit * ZS_TP_MAXPG;
+  auto tread = [&](uint32_t x) -> uint32_t {
+    if (x < tcap) return tk[x];
+    uint32_t off;
+    const uint32_t k = tok_page(x - tcap, &off);
+    return tokens[pool.base + ((uint64_t)(ptab[k] - 1u) << ZS_TP_LOG) + off];
+  };
+  uint16_t *out = scratch + ch.scratch;
+  // history before the unit: position p in [-HIST, 0) sits at slot p + RS
+  if (ch.ord != 0 || (jobs[ch.job].flags & ZS_JF_CONT)) {
+    uint32_t *r32 = reinterpret_cast<uint32_t *>(ring + EX2_N);
+    for (uint32_t i = tid; i < HIST / 2; i += EX2_T) r32[i] = (MARK_BASE + 2 * i) | ((MARK_BASE + 2 * i + 1) << 16);
+  }
+  for (uint32_t i = tid; i < EX2_N; i += EX2_T) s_mark[i] = 0;
+  // token batches: thread tid holds tokens tb + 4 tid + j (payload, start entry)
+  uint32_t nxt[EX2_TPT], pay[EX2_TPT], ts[EX2_TPT];
+  uint32_t tb = 0, bend = 0, par = 0;
+#pragma unroll
+  for (int j = 0; j < EX2_TPT; j++) {
+    const uint32_t x = tid * EX2_TPT + j;
+    nxt[j] = x < ntok ? tread(x) : 0u;
+  }
+  auto load_batch = [&]() {
+    uint32_t lsum = 0, ex[EX2_TPT];
+#pragma unroll
+    for (int j = 0; j < EX2_TPT; j++) {
+      const uint32_t t = nxt[j], hi = t >> 16;
+      const uint32_t len = tb + tid * EX2_TPT + j < ntok ? (hi ? hi : 1u) : 0u;
+      ex[j] = lsum;
+      lsum += len;
+      pay[j] = hi ? (t & 0xffffu) + 1u + MARK_BASE : (t & 0xffu);
+      ts[j] = len ? 0u : 0xffffffffu;
+    }
+#pragma unroll
+    for (int j = 0; j < EX2_TPT; j++) {  // next batch, in flight while this one is used
+      const uint32_t x = tb + EX2_TB + tid * EX2_TPT + j;
+      nxt[j] = x < ntok ? tread(x) : 0u;
+    }
+    const uint32_t incl = wave_scan_add(lsum);
+    if (lane == WAVE - 1) s_bs[par][wv] = incl;
+    exp_barrier();
+    uint32_t before = 0, S = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < EX2_W; w++) {
+      const uint32_t x = s_bs[par][w];
+      before += w < wv ? x : 0u;
+      S += x;
+    }
+    par ^= 1u;
+    const uint32_t b0 = bend + before + incl - lsum;
+#pragma unroll
+    for (int j = 0; j < EX2_TPT; j++) ts[j] = ts[j] ? ts[j] : b0 + ex[j];
+    bend += S;
+    tb += EX2_TB;
+  };
+  if (ntok) load_batch();
+  uint32_t R = 0, Rs = 0, carry = 0, flushed = 0, Fs = 0;
+  const uint32_t toff = tid * EX2_E;
+  while (R < total) {
+    auto place = [&]() {
+#pragma unroll
+      for (int j = 0; j < EX2_TPT; j++) {
+        const uint32_t rel = ts[j] - R;
+        if (rel < EX2_N) s_mark[rel] = ((rel + 1u) << 20) | pay[j];
+      }
+    };
+    place();
+    while (bend < R + EX2_N && tb < ntok) {
+      load_batch();
+      place();
+    }
+    exp_barrier();  // B1: marks visible; the previous round's entries final
+    while (R - flushed >= EX2_N) {
+      const uint4 v4 = *reinterpret_cast<const uint4 *>(&ring[Fs + toff]);
+      *reinterpret_cast<uint4 *>(out + flushed + toff) = v4;
+      flushed += EX2_N;
+      Fs = Fs + EX2_N == EX2_RS ? 0u : Fs + EX2_N;
+    }
+    uint32_t mk[EX2_E];
+    {
+      uint4 *mp = reinterpret_cast<uint4 *>(&s_mark[toff]);
+      const uint4 a = mp[0], b = mp[1];
+      mk[0] = a.x, mk[1] = a.y, mk[2] = a.z, mk[3] = a.w, mk[4] = b.x, mk[5] = b.y, mk[6] = b.z, mk[7] = b.w;
+      mp[0] = make_uint4(0, 0, 0, 0);
+      mp[1] = make_uint4(0, 0, 0, 0);
+    }
+    const uint32_t tmax = max(max(max(mk[0], mk[1]), max(mk[2], mk[3])), max(max(mk[4], mk[5]), max(mk[6], mk[7])));
+    const uint32_t winc = wave_scan_max(tmax);
+    const uint32_t wexc = __shfl_up(winc, 1);
+    if (lane == WAVE - 1) s_red[wv] = winc;
+    exp_barrier();  // B2
+    uint32_t run = max(carry, lane ? wexc : 0u), all = carry;
+#pragma unroll
+    for (uint32_t w = 0; w < EX2_W; w++) {
+      const uint32_t x = s_red[w];
+      run = w < wv ? max(run, x) : run;
+      all = max(all, x);
+    }
+    carry = all & 0xfffffu;
+    const uint32_t s0 = Rs + toff;
+    uint32_t v[EX2_E], unres = 0;
+#pragma unroll
+    for (int k = 0; k < EX2_E; k++) {
+      run = max(run, mk[k]);
+      const uint32_t pl = run & 0xfffffu;
+      const uint32_t x = s0 + (uint32_t)k + MARK_BASE - pl;  // source slot (wrapped below)
+      const uint32_t xs = min(x, x + EX2_RS);
+      const uint32_t rv = ring[xs < EX2_RS ? xs : 0u];
+      const bool lit = pl < MARK_BASE;
+      const bool in = pl <= toff + (uint32_t)k + MARK_BASE;  // distance <= e - R: source inside the round
+      v[k] = lit ? pl : (in ? EX2_PTR + xs - Rs : rv);
+      unres |= (!lit && in) ? 1u << k : 0u;
+    }
+    {
+      uint4 w4;
+      w4.x = v[0] | (v[1] << 16);
+      w4.y = v[2] | (v[3] << 16);
+      w4.z = v[4] | (v[5] << 16);
+      w4.w = v[6] | (v[7] << 16);
+      *reinterpret_cast<uint4 *>(&ring[s0]) = w4;
+    }
+    exp_barrier();  // B3: every entry holds a value or a pointer
+    while (unres) {
+      // other lanes write the ring meanwhile: no load may be reused across passes
+      __asm__ volatile("" ::: "memory");
+#pragma unroll
+      for (int k = 0; k < EX2_E; k++) {
+        if (unres & (1u << k)) {
+          const uint32_t r = ring[Rs + (v[k] & 0x7ffu)];
+          if (r < EX2_PTR) unres &= ~(1u << k);
+          v[k] = r;
+          ring[s0 + k] = (uint16_t)r;
+        }
+      }
+    }
+    R += EX2_N;
+    Rs = Rs + EX2_N == EX2_RS ? 0u : Rs + EX2_N;
+  }
+  exp_barrier();
+  while (total - flushed >= EX2_N) {
+    const uint4 v4 = *reinterpret_cast<const uint4 *>(&ring[Fs + toff]);
+    *reinterpret_cast<uint4 *>(out + flushed + toff) = v4;
+    flushed += EX2_N;
+    Fs = Fs + EX2_N == EX2_RS ? 0u : Fs + EX2_N;
+  }
+  for (uint32_t k = tid; k < total - flushed; k += EX2_T) out[flushed + k] = ring[Fs + k];
+}
+
 // First dynamic header of every unit after the stream's first (the finder
 // only records BFINAL = 0, BTYPE = 2 starts whose header validated), one wave
 // per unit across the whole GPU: tables go to the unit's global table area and
@@ -2090,6 +2284,15 @@ extern "C" void zs_launch_parse(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads
                        d_chunks, nchunks, d_tokens, d_tables, d_fixed, order, pool, lane_map);
 }
 
+// ZS_EXPAND=1: the round-per-batch expand kernel for 32 KiB windows too (A/B)
+static bool expand_v1() {
+  static const bool v = [] {
+    const char *e = getenv("ZS_EXPAND");
+    return e && atoi(e) == 1;
+  }();
+  return v;
+}
+
 // expand the verified chain members (after zs_chain_kernel), longest first
 extern "C" void zs_launch_expand(const ZsJobDev *d_jobs, ZsChunkDev *d_chunks, uint32_t nchunks, uint16_t *d_scratch,
                                  const uint32_t *d_tokens, ZsTokPool pool, uint32_t *d_fallback, int d64, hipStream_t st) {
@@ -2099,9 +2302,12 @@ extern "C" void zs_launch_expand(const ZsJobDev *d_jobs, ZsChunkDev *d_chunks, u
   if (d64)
     hipLaunchKernelGGL(zs_expand_kernel<true>, dim3(nchunks), dim3(EXP_T), 0, st, d_jobs, d_chunks, d_scratch, d_tokens,
                        order, pool, d_fallback);
-  else
+  else if (expand_v1())
     hipLaunchKernelGGL(zs_expand_kernel<false>, dim3(nchunks), dim3(EXP_T), 0, st, d_jobs, d_chunks, d_scratch, d_tokens,
                        order, pool, d_fallback);
+  else
+    hipLaunchKernelGGL(zs_expand2_kernel, dim3(nchunks), dim3(EX2_T), 0, st, d_jobs, d_chunks, d_scratch, d_tokens,
+                       order, pool);
 }
 
 extern "C" int zs_kprof_read_ck(uint64_t *out16, int reset);
