@@ -1945,7 +1945,7 @@ __global__ void __launch_bounds__(EXP_T) zs_expand_kernel(const ZsJobDev *__rest
 // consecutive entries per thread, decoupled from the token batches (1024
 // tokens, 4 per thread, loaded whenever the next round reaches past the last
 // loaded token), so every round but the unit's last is full.
-//  - Marks: each token writes key (start - R + 1) << 20 | payload at its start
+//  - Marks: each token writes key (start - R + 1) << 16 | payload at its start
 //    entry (payload: the literal byte, or distance + 256); a running max over
 //    the round (thread, wave DPP scan, per-wave totals) gives every entry its
 //    token's payload directly -- the max-key mark, or the carry of the last
@@ -1961,15 +1961,28 @@ __global__ void __launch_bounds__(EXP_T) zs_expand_kernel(const ZsJobDev *__rest
 //    each lane terminates on its own).
 // Three barriers per round (+1 per token batch); ~15 VALU per entry.
 // ---------------------------------------------------------------------------
-#define EX2_T 256
+#ifndef EX2_T
+#define EX2_T 512  // measured (C2 expand): 256 x 8 entries 8.5 ms, 512 x 4 7.2, 1024 x 4 10.2, 1024 x 2 12.9
+#endif
 #define EX2_W (EX2_T / WAVE)
-#define EX2_E 8
+#ifndef EX2_E
+#define EX2_E 4                 // consecutive entries per thread per round
+#endif
 #define EX2_N (EX2_T * EX2_E)   // entries per round
 #define EX2_RS (HIST + EX2_N)   // ring slots
-#define EX2_TPT 4               // tokens per thread per batch
+#ifndef EX2_TPT
+#define EX2_TPT 2               // tokens per thread per batch
+#endif
 #define EX2_TB (EX2_T * EX2_TPT)
-#define EX2_PTR 0xF800u         // ring value >= PTR: pointer to in-round entry (value & 0x7ff)
-static_assert(EX2_RS % EX2_N == 0 && EX2_N <= 2048 && MARK_BASE + HIST <= EX2_PTR, "expand2 layout");
+#define EX2_PTR (0x10000u - EX2_N)  // ring value >= PTR: pointer to in-round entry (value & (N - 1))
+static_assert(EX2_RS % EX2_N == 0 && (EX2_E == 2 || EX2_E % 4 == 0) && MARK_BASE + HIST <= EX2_PTR, "expand2 layout");
+// E entries (2E bytes) at u16 index i of a 16-byte-aligned LDS / global array
+__device__ __forceinline__ void ex2_copy(uint16_t *dst, const uint16_t *src) {
+#pragma unroll
+  for (int c = 0; c < EX2_E / 8; c++) reinterpret_cast<uint4 *>(dst)[c] = reinterpret_cast<const uint4 *>(src)[c];
+  if (EX2_E == 4) *reinterpret_cast<uint2 *>(dst) = *reinterpret_cast<const uint2 *>(src);
+  if (EX2_E == 2) *reinterpret_cast<uint32_t *>(dst) = *reinterpret_cast<const uint32_t *>(src);
+}
 
 __global__ void __launch_bounds__(EX2_T) zs_expand2_kernel(const ZsJobDev *__restrict__ jobs,
                                                             const ZsChunkDev *__restrict__ chunks,
@@ -1987,11 +2000,15 @@ __global__ void __launch_bounds__(EX2_T) zs_expand2_kernel(const ZsJobDev *__res
   gcu32 *tk = (gcu32 *)(tokens + ch.tok);
   const uint32_t ntok = ch.n_tok, tcap = ch.tcap, total = ch.n_out;
   const uint32_t *ptab = pool.ptab + (size_t)unit * ZS_TP_MAXPG;
-  auto tread = [&](uint32_t x) -> uint32_t {
-    if (x < tcap) return tk[x];
+  // address of token x (x >= ntok: any valid word, its length is masked):
+  // one load per token whatever the path, so the prefetch registers are not
+  // copied (and waited for) where the paths merge
+  auto taddr = [&](uint32_t x) -> gcu32 * {
+    if (x >= ntok) return (gcu32 *)tokens;
+    if (x < tcap) return tk + x;
     uint32_t off;
     const uint32_t k = tok_page(x - tcap, &off);
-    return tokens[pool.base + ((uint64_t)(ptab[k] - 1u) << ZS_TP_LOG) + off];
+    return (gcu32 *)(tokens + pool.base + ((uint64_t)(ptab[k] - 1u) << ZS_TP_LOG) + off);
   };
   uint16_t *out = scratch + ch.scratch;
   // history before the unit: position p in [-HIST, 0) sits at slot p + RS
@@ -2005,8 +2022,7 @@ __global__ void __launch_bounds__(EX2_T) zs_expand2_kernel(const ZsJobDev *__res
   uint32_t tb = 0, bend = 0, par = 0;
 #pragma unroll
   for (int j = 0; j < EX2_TPT; j++) {
-    const uint32_t x = tid * EX2_TPT + j;
-    nxt[j] = x < ntok ? tread(x) : 0u;
+    nxt[j] = *taddr(tid * EX2_TPT + j);
   }
   auto load_batch = [&]() {
     uint32_t lsum = 0, ex[EX2_TPT];
@@ -2019,14 +2035,17 @@ __global__ void __launch_bounds__(EX2_T) zs_expand2_kernel(const ZsJobDev *__res
       pay[j] = hi ? (t & 0xffffu) + 1u + MARK_BASE : (t & 0xffu);
       ts[j] = len ? 0u : 0xffffffffu;
     }
-#pragma unroll
-    for (int j = 0; j < EX2_TPT; j++) {  // next batch, in flight while this one is used
-      const uint32_t x = tb + EX2_TB + tid * EX2_TPT + j;
-      nxt[j] = x < ntok ? tread(x) : 0u;
-    }
     const uint32_t incl = wave_scan_add(lsum);
     if (lane == WAVE - 1) s_bs[par][wv] = incl;
+#pragma unroll
+    for (int j = 0; j < EX2_TPT; j++) __asm__ volatile("" : "+v"(pay[j]));  // done with nxt before it reloads
     exp_barrier();
+    // next batch, in flight while this one is used (issued after the barrier,
+    // so that no wait for it lands before the next batch)
+#pragma unroll
+    for (int j = 0; j < EX2_TPT; j++) {
+      nxt[j] = *taddr(tb + EX2_TB + tid * EX2_TPT + j);
+    }
     uint32_t before = 0, S = 0;
 #pragma unroll
     for (uint32_t w = 0; w < EX2_W; w++) {
@@ -2041,38 +2060,51 @@ __global__ void __launch_bounds__(EX2_T) zs_expand2_kernel(const ZsJobDev *__res
     bend += S;
     tb += EX2_TB;
   };
-  if (ntok) load_batch();
   uint32_t R = 0, Rs = 0, carry = 0, flushed = 0, Fs = 0;
   const uint32_t toff = tid * EX2_E;
-  while (R < total) {
-    auto place = [&]() {
+  auto place = [&]() {  // marks of the loaded batch's tokens that start in round R
 #pragma unroll
-      for (int j = 0; j < EX2_TPT; j++) {
-        const uint32_t rel = ts[j] - R;
-        if (rel < EX2_N) s_mark[rel] = ((rel + 1u) << 20) | pay[j];
-      }
-    };
-    place();
-    while (bend < R + EX2_N && tb < ntok) {
+    for (int j = 0; j < EX2_TPT; j++) {
+      const uint32_t rel = ts[j] - R;
+      if (rel < EX2_N) s_mark[rel] = ((rel + 1u) << 16) | pay[j];
+    }
+  };
+  // one loop for batches and rounds: the prefetched tokens stay in one set of
+  // registers (a second loop made the compiler copy them at its back edge,
+  // waiting for the loads every round)
+  for (;;) {
+    if (bend < R + EX2_N && tb < ntok) {  // round R reaches past the loaded tokens
       load_batch();
       place();
+      continue;
     }
+    if (R >= total) break;
     exp_barrier();  // B1: marks visible; the previous round's entries final
     while (R - flushed >= EX2_N) {
-      const uint4 v4 = *reinterpret_cast<const uint4 *>(&ring[Fs + toff]);
-      *reinterpret_cast<uint4 *>(out + flushed + toff) = v4;
+      ex2_copy(out + flushed + toff, &ring[Fs + toff]);
       flushed += EX2_N;
       Fs = Fs + EX2_N == EX2_RS ? 0u : Fs + EX2_N;
     }
     uint32_t mk[EX2_E];
     {
       uint4 *mp = reinterpret_cast<uint4 *>(&s_mark[toff]);
-      const uint4 a = mp[0], b = mp[1];
-      mk[0] = a.x, mk[1] = a.y, mk[2] = a.z, mk[3] = a.w, mk[4] = b.x, mk[5] = b.y, mk[6] = b.z, mk[7] = b.w;
-      mp[0] = make_uint4(0, 0, 0, 0);
-      mp[1] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+      for (int c = 0; c < EX2_E / 4; c++) {
+        const uint4 a = mp[c];
+        mk[4 * c] = a.x, mk[4 * c + 1] = a.y, mk[4 * c + 2] = a.z, mk[4 * c + 3] = a.w;
+      }
+#pragma unroll
+      for (int c = 0; c < EX2_E / 4; c++) mp[c] = make_uint4(0, 0, 0, 0);
+      if (EX2_E == 2) {
+        uint2 *m2 = reinterpret_cast<uint2 *>(&s_mark[toff]);
+        const uint2 a = *m2;
+        mk[0] = a.x, mk[1 % EX2_E] = a.y;
+        *m2 = make_uint2(0, 0);
+      }
     }
-    const uint32_t tmax = max(max(max(mk[0], mk[1]), max(mk[2], mk[3])), max(max(mk[4], mk[5]), max(mk[6], mk[7])));
+    uint32_t tmax = 0;
+#pragma unroll
+    for (int k = 0; k < EX2_E; k++) tmax = max(tmax, mk[k]);
     const uint32_t winc = wave_scan_max(tmax);
     const uint32_t wexc = __shfl_up(winc, 1);
     if (lane == WAVE - 1) s_red[wv] = winc;
@@ -2084,13 +2116,13 @@ __global__ void __launch_bounds__(EX2_T) zs_expand2_kernel(const ZsJobDev *__res
       run = w < wv ? max(run, x) : run;
       all = max(all, x);
     }
-    carry = all & 0xfffffu;
+    carry = all & 0xffffu;
     const uint32_t s0 = Rs + toff;
     uint32_t v[EX2_E], unres = 0;
 #pragma unroll
     for (int k = 0; k < EX2_E; k++) {
       run = max(run, mk[k]);
-      const uint32_t pl = run & 0xfffffu;
+      const uint32_t pl = run & 0xffffu;
       const uint32_t x = s0 + (uint32_t)k + MARK_BASE - pl;  // source slot (wrapped below)
       const uint32_t xs = min(x, x + EX2_RS);
       const uint32_t rv = ring[xs < EX2_RS ? xs : 0u];
@@ -2099,35 +2131,53 @@ __global__ void __launch_bounds__(EX2_T) zs_expand2_kernel(const ZsJobDev *__res
       v[k] = lit ? pl : (in ? EX2_PTR + xs - Rs : rv);
       unres |= (!lit && in) ? 1u << k : 0u;
     }
-    {
+#pragma unroll
+    for (int c = 0; c < EX2_E / 8; c++) {
       uint4 w4;
-      w4.x = v[0] | (v[1] << 16);
-      w4.y = v[2] | (v[3] << 16);
-      w4.z = v[4] | (v[5] << 16);
-      w4.w = v[6] | (v[7] << 16);
-      *reinterpret_cast<uint4 *>(&ring[s0]) = w4;
+      w4.x = v[8 * c] | (v[8 * c + 1] << 16);
+      w4.y = v[8 * c + 2] | (v[8 * c + 3] << 16);
+      w4.z = v[8 * c + 4] | (v[8 * c + 5] << 16);
+      w4.w = v[8 * c + 6] | (v[8 * c + 7] << 16);
+      *reinterpret_cast<uint4 *>(&ring[s0 + 8 * c]) = w4;
     }
+    if (EX2_E == 4)
+      *reinterpret_cast<uint2 *>(&ring[s0]) = make_uint2(v[0] | (v[1] << 16), v[2 % EX2_E] | (v[3 % EX2_E] << 16));
+    if (EX2_E == 2) *reinterpret_cast<uint32_t *>(&ring[s0]) = v[0] | (v[1 % EX2_E] << 16);
     exp_barrier();  // B3: every entry holds a value or a pointer
     while (unres) {
       // other lanes write the ring meanwhile: no load may be reused across passes
       __asm__ volatile("" ::: "memory");
+#ifndef EX2_SPIN_SEQ
+      uint32_t r[EX2_E];
+#pragma unroll
+      for (int k = 0; k < EX2_E; k++) r[k] = ring[Rs + ((unres >> k) & 1u ? (v[k] & (EX2_N - 1u)) : 0u)];
 #pragma unroll
       for (int k = 0; k < EX2_E; k++) {
         if (unres & (1u << k)) {
-          const uint32_t r = ring[Rs + (v[k] & 0x7ffu)];
+          if (r[k] < EX2_PTR) unres &= ~(1u << k);
+          v[k] = r[k];
+          ring[s0 + k] = (uint16_t)r[k];
+        }
+      }
+#else
+#pragma unroll
+      for (int k = 0; k < EX2_E; k++) {
+        if (unres & (1u << k)) {
+          const uint32_t r = ring[Rs + (v[k] & (EX2_N - 1u))];
           if (r < EX2_PTR) unres &= ~(1u << k);
           v[k] = r;
           ring[s0 + k] = (uint16_t)r;
         }
       }
+#endif
     }
     R += EX2_N;
     Rs = Rs + EX2_N == EX2_RS ? 0u : Rs + EX2_N;
+    place();
   }
   exp_barrier();
   while (total - flushed >= EX2_N) {
-    const uint4 v4 = *reinterpret_cast<const uint4 *>(&ring[Fs + toff]);
-    *reinterpret_cast<uint4 *>(out + flushed + toff) = v4;
+    ex2_copy(out + flushed + toff, &ring[Fs + toff]);
     flushed += EX2_N;
     Fs = Fs + EX2_N == EX2_RS ? 0u : Fs + EX2_N;
   }
