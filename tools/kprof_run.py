@@ -14,7 +14,7 @@ NAMES = {0: "p_waves", 1: "p_cyc_total", 2: "p_cyc_coop", 3: "p_cyc_steps", 4: "
          6: "p_coop_calls", 7: "p_lane_steps", 8: "p_wave_steps", 9: "p_slow_lit", 10: "p_slow_dist",
          11: "p_cyc_max", 12: "p_cyc_init", 13: "p_refills",
          16: "e_blocks", 17: "e_cyc_total", 18: "e_rounds", 19: "e_jump_iters", 20: "e_cyc_jump", 21: "e_batches",
-         22: "e_cyc_max", 23: "e_cyc_init", 24: "e_jump_rounds",
+         22: "e_cyc_max", 23: "e_cyc_init", 24: "e_jump_rounds", 25: "e_cyc_pre",
          40: "s_refill1", 41: "s_lit", 42: "s_refill2", 43: "s_dist", 44: "s_tail",
          26: "d_blocks", 27: "d_cyc_total", 28: "d_cyc_hist", 29: "d_cyc_build", 30: "d_cyc_hdr", 31: "d_cyc_emit",
          32: "d_cyc_out", 33: "d_chunks",
@@ -66,6 +66,12 @@ def main():
         "expand_jump_rounds_frac": d["e_jump_rounds"] / max(d["e_rounds"], 1),
         "expand_jump_iters_per_jround": d["e_jump_iters"] / max(d["e_jump_rounds"], 1),
         "expand_frac_init": d["e_cyc_init"] / max(d["e_cyc_total"], 1),
+        # zs_expand2_kernel (32 KiB windows): counters per wave; init = token batches, pre = B1..B3
+        "expand2_frac_batch": d["e_cyc_init"] / max(d["e_cyc_total"], 1),
+        "expand2_frac_pre_spin": d["e_cyc_pre"] / max(d["e_cyc_total"], 1),
+        "expand2_frac_spin": d["e_cyc_jump"] / max(d["e_cyc_total"], 1),
+        "expand2_spin_rounds_frac": d["e_jump_rounds"] / max(d["e_rounds"], 1),
+        "expand2_passes_per_round_max_lane": d["e_jump_iters"] / max(d["e_rounds"], 1),
         "link_cycles_per_step": {k: d[k] / max(d["l_steps"], 1) for k in
                                  ("l_cyc_succ", "l_cyc_walk", "l_cyc_winwrite", "l_cyc_resolve", "l_cyc_barrier",
                                   "l_cyc_total")},

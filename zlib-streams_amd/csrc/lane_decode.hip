@@ -2024,7 +2024,16 @@ __global__ void __launch_bounds__(EX2_T) zs_expand2_kernel(const ZsJobDev *__res
   for (int j = 0; j < EX2_TPT; j++) {
     nxt[j] = *taddr(tid * EX2_TPT + j);
   }
+#if KP_ON
+  const uint64_t kp_t0 = KP_NOW();
+  uint64_t kp_batch = 0, kp_pre = 0, kp_spin = 0;
+  uint32_t kp_rounds = 0, kp_passes = 0, kp_srounds = 0, kp_batches = 0;
+#endif
   auto load_batch = [&]() {
+#if KP_ON
+    const uint64_t kb0 = KP_NOW();
+    kp_batches++;
+#endif
     uint32_t lsum = 0, ex[EX2_TPT];
 #pragma unroll
     for (int j = 0; j < EX2_TPT; j++) {
@@ -2059,6 +2068,9 @@ __global__ void __launch_bounds__(EX2_T) zs_expand2_kernel(const ZsJobDev *__res
     for (int j = 0; j < EX2_TPT; j++) ts[j] = ts[j] ? ts[j] : b0 + ex[j];
     bend += S;
     tb += EX2_TB;
+#if KP_ON
+    kp_batch += KP_NOW() - kb0;
+#endif
   };
   uint32_t R = 0, Rs = 0, carry = 0, flushed = 0, Fs = 0;
   const uint32_t toff = tid * EX2_E;
@@ -2079,6 +2091,10 @@ __global__ void __launch_bounds__(EX2_T) zs_expand2_kernel(const ZsJobDev *__res
       continue;
     }
     if (R >= total) break;
+#if KP_ON
+    const uint64_t kr0 = KP_NOW();
+    kp_rounds++;
+#endif
     exp_barrier();  // B1: marks visible; the previous round's entries final
     while (R - flushed >= EX2_N) {
       ex2_copy(out + flushed + toff, &ring[Fs + toff]);
@@ -2144,7 +2160,15 @@ __global__ void __launch_bounds__(EX2_T) zs_expand2_kernel(const ZsJobDev *__res
       *reinterpret_cast<uint2 *>(&ring[s0]) = make_uint2(v[0] | (v[1] << 16), v[2 % EX2_E] | (v[3 % EX2_E] << 16));
     if (EX2_E == 2) *reinterpret_cast<uint32_t *>(&ring[s0]) = v[0] | (v[1 % EX2_E] << 16);
     exp_barrier();  // B3: every entry holds a value or a pointer
+#if KP_ON
+    const uint64_t kr1 = KP_NOW();
+    kp_pre += kr1 - kr0;
+    kp_srounds += __ballot(unres != 0) ? 1u : 0u;
+#endif
     while (unres) {
+#if KP_ON
+      kp_passes++;
+#endif
       // other lanes write the ring meanwhile: no load may be reused across passes
       __asm__ volatile("" ::: "memory");
 #ifndef EX2_SPIN_SEQ
@@ -2171,6 +2195,9 @@ __global__ void __launch_bounds__(EX2_T) zs_expand2_kernel(const ZsJobDev *__res
       }
 #endif
     }
+#if KP_ON
+    kp_spin += KP_NOW() - kr1;
+#endif
     R += EX2_N;
     Rs = Rs + EX2_N == EX2_RS ? 0u : Rs + EX2_N;
     place();
@@ -2182,6 +2209,22 @@ __global__ void __launch_bounds__(EX2_T) zs_expand2_kernel(const ZsJobDev *__res
     Fs = Fs + EX2_N == EX2_RS ? 0u : Fs + EX2_N;
   }
   for (uint32_t k = tid; k < total - flushed; k += EX2_T) out[flushed + k] = ring[Fs + k];
+#if KP_ON  // per wave: E_BLOCKS waves, JUMP_ITERS spin passes (max over lanes), JUMP_ROUNDS rounds with a spin,
+           // CYC_INIT token-batch cycles, CYC_JUMP spin cycles, slot 25 B1..B3 cycles
+  {
+    const uint64_t tot = KP_NOW() - kp_t0;
+    KP_ADD(KP_E_BLOCKS, 1);
+    KP_ADD(KP_E_CYC_TOTAL, tot);
+    KP_MAX(KP_E_CYC_MAX, tot);
+    KP_ADD(KP_E_CYC_INIT, kp_batch);
+    KP_ADD(KP_E_ROUNDS, kp_rounds);
+    KP_ADD(KP_E_JUMP_ITERS, kp_wave_max(kp_passes));
+    KP_ADD(KP_E_JUMP_ROUNDS, kp_srounds);
+    KP_ADD(KP_E_CYC_JUMP, kp_spin);
+    KP_ADD(KP_E_BATCHES, kp_batches);
+    KP_ADD(KP_E_JUMP_ROUNDS + 1, kp_pre);
+  }
+#endif
 }
 
 // First dynamic header of every unit after the stream's first (the finder
