@@ -798,38 +798,37 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_chain_kernel(const ZsJobDev *
 // pairs are packed in u32 (2 per word, 2 words per group)
 template <uint32_t HN>
 __device__ __forceinline__ void link_load(const uint16_t *__restrict__ scratch, const ZsLinkInfo &li, uint32_t t,
-                                          uint2 (&v)[HN / LINK_THREADS / 4]) {
+                                          uint2 (&lo)[HN / LINK_THREADS / 4], uint2 (&hi)[HN / LINK_THREADS / 4]) {
+  // window entry i is the unit's entry n - HN + i (0 before the unit: a short
+  // unit).  Two aligned 8-byte loads per 4 entries whatever the unit, and the
+  // funnel shift left to link_take: the same loads every step and no use of
+  // them before the next step lets the compiler wait for exactly the loads it
+  // needs (vmcnt is in order; a branchy, immediately consumed load sequence
+  // made it wait for everything, the prefetch included)
   constexpr int LINK_G = HN / LINK_THREADS / 4;
-  const uint32_t n = li.n_out;
-  if (n >= HN) {
-    // entries of a chain member start at any entry index: two aligned 8-byte
-    // loads and a funnel shift give the thread's 4 entries
-    const uint64_t b = li.scratch + n - HN;
-    const uint32_t m = (uint32_t)(b & 3u);
-    const uint2 *al = reinterpret_cast<const uint2 *>(scratch + (b - m));
+  const int64_t b0 = (int64_t)li.scratch + (int64_t)li.n_out - (int64_t)HN;  // entry index of window entry 0
+  const uint32_t m = (uint32_t)((uint64_t)b0 & 3u);
 #pragma unroll
-    for (int g = 0; g < LINK_G; g++) {
-      const uint32_t i = (uint32_t)g * (LINK_THREADS * 4) + t * 4;
-      const uint2 lo = al[i / 4];
-      if (m == 0) {
-        v[g] = lo;
-      } else {
-        const uint2 hi = al[i / 4 + 1];
-        const uint64_t a = (uint64_t)lo.x | ((uint64_t)lo.y << 32), c = (uint64_t)hi.x | ((uint64_t)hi.y << 32);
-        const uint64_t r = (a >> (16 * m)) | (c << (64 - 16 * m));
-        v[g] = make_uint2((uint32_t)r, (uint32_t)(r >> 32));
-      }
-    }
-  } else {  // short unit: entry i exists only for i >= HN - n
-    const uint16_t *e = scratch + li.scratch;
-#pragma unroll
-    for (int g = 0; g < LINK_G; g++) {
-      const uint32_t i = (uint32_t)g * (LINK_THREADS * 4) + t * 4;
-      uint16_t x[4];
-      for (int k = 0; k < 4; k++) x[k] = (i + k + n >= HN) ? e[i + k + n - HN] : (uint16_t)0;
-      __builtin_memcpy(&v[g], x, 8);
-    }
+  for (int g = 0; g < LINK_G; g++) {
+    const int64_t e = b0 + (int64_t)((uint32_t)g * (LINK_THREADS * 4) + t * 4);
+    const uint2 *al = reinterpret_cast<const uint2 *>(scratch + (e < 0 ? 0u : (uint64_t)(e - (int64_t)m)));
+    lo[g] = al[0];
+    hi[g] = al[1];
   }
+}
+template <uint32_t HN>
+__device__ __forceinline__ uint2 link_take(const ZsLinkInfo &li, uint32_t t, int g, uint2 lo, uint2 hi) {
+  const int64_t b0 = (int64_t)li.scratch + (int64_t)li.n_out - (int64_t)HN;
+  const uint32_t m = (uint32_t)((uint64_t)b0 & 3u);
+  const uint64_t x = (uint64_t)lo.x | ((uint64_t)lo.y << 32), c = (uint64_t)hi.x | ((uint64_t)hi.y << 32);
+  uint64_t r = (x >> (16 * m)) | ((c << 1) << (63 - 16 * m));  // m = 0: c contributes nothing
+  if (li.n_out < HN) {  // short unit: entries before it read as 0 (the keep rule replaces them)
+    const int64_t e = b0 + (int64_t)((uint32_t)g * (LINK_THREADS * 4) + t * 4);
+    const int64_t first = (int64_t)li.scratch - e;  // entries of this group before the unit
+    if (first >= 4) r = 0;
+    else if (first > 0) r &= ~0ull << (16 * first);
+  }
+  return make_uint2((uint32_t)r, (uint32_t)(r >> 32));
 }
 
 template <uint32_t HN>
@@ -860,32 +859,25 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_link_kernel(const ZsJobDev *_
     for (uint32_t i = HN - wv + t; i < HN; i += LINK_THREADS) s_win[0][i] = jb.out[(int64_t)i - (int64_t)HN];
   __syncthreads();
   int cur = 0;
-  uint2 v[LINK_G], vn[LINK_G];
-  ZsLinkInfo li = info[u0];
-  link_load<HN>(scratch, li, t, v);
-  ZsLinkInfo lin = len > 1 ? info[u0 + 1] : li;
+  uint2 la[LINK_G], ha[LINK_G], lb[LINK_G], hb[LINK_G];
   bool bad = false;
-  for (uint32_t j = 0; j < len; j++) {
-    // next member's entries (and the one after's descriptor) in flight now
-    ZsLinkInfo li2 = lin;
-    if (j + 1 < len) {
-      link_load<HN>(scratch, lin, t, vn);
-      if (j + 2 < len) li2 = info[u0 + j + 2];
-    }
+  // member j's entries were loaded one step earlier; each step first issues
+  // the next member's loads, then resolves, then stores the window (two
+  // register sets, swapped by unrolling by two: no copies of loaded registers)
+  link_load<HN>(scratch, info[u0], t, la, ha);
+  auto step = [&](uint32_t j, const uint2 (&vl)[LINK_G], const uint2 (&vh)[LINK_G], uint2 (&nl)[LINK_G],
+                  uint2 (&nh)[LINK_G]) {
+    const ZsLinkInfo li = info[u0 + j];
+    link_load<HN>(scratch, info[u0 + min(j + 1, len - 1)], t, nl, nh);
+    __builtin_amdgcn_sched_barrier(0);  // nothing that uses this step's entries moves above the next loads
+    uint2 v[LINK_G];
+#pragma unroll
+    for (int g = 0; g < LINK_G; g++) v[g] = link_take<HN>(li, t, g, vl[g], vh[g]);
     const uint32_t c = li.unit;
     uint8_t *W = s_win[cur];
     uint8_t *W2 = s_win[cur ^ 1];
 #if KP_ON
-    const uint64_t ka = KP_NOW();
-#endif
-    if (j != 0 || cont) {
-      uint8_t *g = windows + (size_t)c * HN;
-      for (uint32_t i = t * 16; i < HN; i += LINK_THREADS * 16)
-        *reinterpret_cast<uint4 *>(g + i) = *reinterpret_cast<const uint4 *>(W + i);
-    }
-#if KP_ON
     const uint64_t kb = KP_NOW();
-    kt_ww += kb - ka;
 #endif
     const uint32_t n = li.n_out;
     const uint32_t keep = n < HN ? HN - n : 0u;  // old history bytes still inside the new window
@@ -928,20 +920,31 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_link_kernel(const ZsJobDev *_
         }
       }
     }
-    wv = min(HN, wv + n);
-    cur ^= 1;
+#if KP_ON
+    const uint64_t ka = KP_NOW();
+    kt_res += ka - kb;
+#endif
+    // the window before unit c (for the first unit of a stream it is unused)
+    {
+      uint8_t *g = windows + (size_t)c * HN;
+#pragma unroll
+      for (uint32_t i = t * 16; i < HN; i += LINK_THREADS * 16)
+        *reinterpret_cast<uint4 *>(g + i) = *reinterpret_cast<const uint4 *>(W + i);
+    }
 #if KP_ON
     const uint64_t kc = KP_NOW();
-    kt_res += kc - kb;
+    kt_ww += kc - ka;
 #endif
+    wv = min(HN, wv + n);
+    cur ^= 1;
     __syncthreads();
 #if KP_ON
     kt_bar += KP_NOW() - kc;
 #endif
-    li = lin;
-    lin = li2;
-#pragma unroll
-    for (int g = 0; g < LINK_G; g++) v[g] = vn[g];
+  };
+  for (uint32_t j = 0; j < len; j += 2) {
+    step(j, la, ha, lb, hb);
+    if (j + 1 < len) step(j + 1, lb, hb, la, ha);
   }
   if (bad) s_bad = 1;
   __syncthreads();
