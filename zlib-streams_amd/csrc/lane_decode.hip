@@ -431,34 +431,43 @@ __device__ __forceinline__ bool lane_step(LaneState &s, const uint16_t *__restri
   return false;
 }
 
-// The common symbol, with few instructions and no divergent exits: literal /
-// length from the LDS root (codes longer than the root via the lane's compact
-// sub-tables in a wave-uniform side branch), length base / extra computed,
-// distance from the LDS root (the canonical tail in a side branch), one token.
-// Anything lane_step would treat differently -- end of block, invalid codes,
-// a full unit, a too-far distance, truncation, a deflate64 copy longer than a
-// token -- restores the lane's reader and runs lane_step itself, so results
-// are lane_step's by construction.  lane_step costs ~3x the instructions
-// (every divergent exit path is issued by the whole wave); at one wave per
-// SIMD the parse is issue- and latency-bound on exactly this loop.
+// refill without a branch: the ring word after nw is read every time (same word
+// when no refill happens), the hold / counters advance by selects
+__device__ __forceinline__ void lane_refill_bf(LaneState &s, const uint32_t *__restrict__ rp) {
+  const uint32_t r = s.nbits < 32u;
+  const uint64_t add = (uint64_t)s.nw << (s.nbits & 31u);
+  s.hold |= r ? add : 0ull;
+  s.nbits += r << 5;
+  s.wi += r;
+  s.rk += r;
+  s.nw = rp[s.rk * WAVE];
+}
+
+// The common symbol, straight-line: literal / length from the LDS root (codes
+// longer than the root via the lane's compact sub-tables in a wave-uniform side
+// branch), length / distance bases by shifts and selects (no sym < 8 / sym < 28
+// branches), refills by selects, distance from the LDS root (the canonical tail
+// in a side branch), the exception test as one bitwise OR and the token stored
+// unconditionally (a slot past gk is never read).  Anything lane_step would
+// treat differently -- end of block, invalid codes, a full unit, a too-far
+// distance, truncation, a deflate64 copy longer than a token -- restores the
+// lane's reader and runs lane_step itself, so results are lane_step's by
+// construction.  At one wave per SIMD the parse is issue-bound on this loop:
+// the short-circuit form (branchy length bases, `||` exception chain,
+// conditional refills) compiled to nested exec-mask branches; written this
+// way C2's parse went 18.0 -> 15.0 ms.
 template <bool D64>
 __device__ __forceinline__ bool lane_step_fast(LaneState &s, const uint16_t *__restrict__ lt,
                                                const uint16_t *__restrict__ dt, uint32_t *__restrict__ tb,
                                                const uint32_t *__restrict__ dtl, const uint32_t *__restrict__ rp,
                                                KpPhase &kp) {
-#if KP_ON
-  const uint64_t kq0 = KP_NOW();
-#endif
   const uint64_t h0 = s.hold;
   const uint32_t nb0 = s.nbits, wi0 = s.wi, rk0 = s.rk, nw0 = s.nw;
-  lane_refill(s, rp);
+  lane_refill_bf(s, rp);
   uint32_t e = lt[(uint32_t)s.hold & (LROOT_N - 1)];
   uint32_t kind = e & 3u;
   if (__builtin_expect(__ballot(kind == CK_SLOW) != 0, 0)) {
-#if KP_ON
-    const uint64_t kq = KP_NOW();
-#endif
-    if (kind == CK_SLOW) {  // as lane_step: zlib's 9-bit root / sub-table, compact, global
+    if (kind == CK_SLOW) {
       const uint32_t op = (e >> 2) & 15u;
       uint32_t e2 = CK_SLOW;
       if (op == OP_ROOT9) {
@@ -471,35 +480,33 @@ __device__ __forceinline__ bool lane_step_fast(LaneState &s, const uint16_t *__r
       e = e2;
       kind = e & 3u;
     }
-#if KP_ON
-    kp.t[0] += KP_NOW() - kq;
-#endif
   }
   const uint32_t used = (e >> 2) & 15u, sym = e >> 6;
-  const bool isl = kind == CK_LEN;
-  // length code sym (0..28): base / extra of src/inftrees.c:59-64 (deflate64 285: 3 + 16 bits)
-  uint32_t xb = sym < 8u ? 0u : (sym < 28u ? (sym >> 2) - 1u : (D64 ? 16u : 0u));
+  const uint32_t isl = kind == CK_LEN;
+  // length code sym (0..28), src/inftrees.c:59-64: extra = max(sym/4 - 1, 0),
+  // base = ((4 + sym%4) << extra) + 3, minus 4 for sym < 4; code 28 is 258
+  // (deflate64 285: 3 + 16 extra bits)
+  const uint32_t top = sym >= 28u;
+  uint32_t xb = (uint32_t)max((int)(sym >> 2) - 1, 0);
+  xb = top ? (D64 ? 16u : 0u) : xb;
   xb = isl ? xb : 0u;
-  const uint32_t lbase = sym < 8u ? sym + 3u : (sym < 28u ? ((4u + (sym & 3u)) << xb) + 3u : (D64 ? 3u : 258u));
+  uint32_t lbase = ((4u + (sym & 3u)) << (xb & 15u)) + 3u - (sym < 4u ? 4u : 0u);
+  lbase = top ? (D64 ? 3u : 258u) : lbase;
   s.hold >>= used;
   const uint32_t len = isl ? lbase + ((uint32_t)s.hold & ((1u << xb) - 1u)) : 1u;
   s.hold >>= xb;
   s.nbits -= used + xb;
-  lane_refill(s, rp);
+  lane_refill_bf(s, rp);
   uint32_t d = dt[(uint32_t)s.hold & (DROOT_N - 1)];
   const bool dslow = isl && (d & 3u) == CK_SLOW;
   if (__ballot(dslow)) {
-#if KP_ON
-    const uint64_t kq = KP_NOW();
-#endif
     if (dslow) d = ((d >> 2) & 15u) ? dist_tail(dtl, (uint32_t)s.hold) : (uint32_t)CK_SLOW;
-#if KP_ON
-    kp.t[1] += KP_NOW() - kq;
-#endif
   }
-  const uint32_t dused = (d >> 2) & 15u, dsym = d >> 6;
-  const uint32_t dx = dsym < 4u ? 0u : (dsym >> 1) - 1u;
-  const uint32_t dist = (dsym < 4u ? dsym + 1u : ((2u + (dsym & 1u)) << dx) + 1u) +
+  // distance code dsym (0..31), src/inftrees.c:65-72: extra = max(dsym/2 - 1, 0),
+  // base = ((2 + dsym%2) << extra) + 1, minus 2 for dsym < 2
+  const uint32_t dused = (d >> 2) & 15u, dsym = (d >> 6) & 31u;
+  const uint32_t dx = min((uint32_t)max((int)(dsym >> 1) - 1, 0), 14u);
+  const uint32_t dist = ((2u + (dsym & 1u)) << dx) + 1u - (dsym < 2u ? 2u : 0u) +
                         ((uint32_t)(s.hold >> dused) & ((1u << dx) - 1u));
   const uint32_t dcons = isl ? dused + dx : 0u;
   s.hold >>= dcons;
@@ -509,13 +516,10 @@ __device__ __forceinline__ bool lane_step_fast(LaneState &s, const uint16_t *__r
 #else
   (void)kp;
 #endif
-  const bool exc = kind == CK_SLOW || kind == CK_EOB || (isl && (d & 3u) == CK_SLOW) || lane_pos(s) > s.limit ||
-                   s.pos + len > s.capx || (isl && dist > s.pos + s.whave) || (D64 && len > 0xffffu);
-  bool left = false;
-#if KP_ON
-  const uint64_t kq2 = KP_NOW();
-  const bool any_exc = __ballot(exc) != 0;
-#endif
+  const uint32_t exc = (uint32_t)(kind >= CK_EOB) | (isl & (uint32_t)((d & 3u) == CK_SLOW)) |
+                       (uint32_t)(lane_pos(s) > s.limit) | (uint32_t)(s.pos + len > s.capx) |
+                       (isl & (uint32_t)(dist > s.pos + s.whave)) | (uint32_t)(D64 && len > 0xffffu);
+  tb[s.gk * WAVE] = isl ? ((len << 16) | (dist - 1u)) : sym;
   if (exc) {
     s.hold = h0;
     s.nbits = nb0;
@@ -525,19 +529,12 @@ __device__ __forceinline__ bool lane_step_fast(LaneState &s, const uint16_t *__r
 #if KP_ON
     s.kp_steps--;
 #endif
-    left = lane_step<D64>(s, lt, dt, tb, dtl, rp, kp);
-  } else {
-    tb[s.gk * WAVE] = isl ? ((len << 16) | (dist - 1u)) : sym;
-    s.gk++;
-    s.ntok++;
-    s.pos += len;
+    return lane_step<D64>(s, lt, dt, tb, dtl, rp, kp);
   }
-#if KP_ON
-  const uint64_t kq3 = KP_NOW();
-  if (any_exc) kp.t[2] += kq3 - kq2;
-  kp.t[3] += kq3 - kq0;
-#endif
-  return left;
+  s.gk++;
+  s.ntok++;
+  s.pos += len;
+  return false;
 }
 
 // Wave-uniform bit reader over the LDS-staged header bits.
@@ -1046,8 +1043,29 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
 #if KP_ON
       const uint64_t kf = KP_NOW();
 #endif
+#ifdef ZS_TPF
+    }
+    {  // words loaded transposed during the last flush: lane (q, m) holds quad q of source 16 r + m
+      const uint32_t q = lane >> 4;
+#pragma unroll
+      for (uint32_t r = 0; r < 4; r++) {
+        const uint32_t src = 16u * r + (lane & 15u);
+#pragma unroll
+        for (uint32_t i = 0; i < 4; i++) L.g.ring[4 * q + i][src] = pre[4 * r + i];
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (s.mode == LM_SYM) {
+      if (s.wi == pre_wi) {
+        s.nw = rp[0];
+        s.rk = 0;
+      } else {
+        lane_fill_ring(s, rp);
+      }
+#else
       if (s.wi == pre_wi) lane_store_ring(s, rp, pre);  // words loaded during the last flush
       else lane_fill_ring(s, rp);
+#endif
 #if KP_ON
       __builtin_amdgcn_s_waitcnt(0);
       kph.t[4] += KP_NOW() - kf;
@@ -1067,13 +1085,98 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
     // the next group's input words, loaded while this group's tokens leave
     // (the loads precede the stores, so waiting for them never waits for a store)
     pre_wi = s.mode == LM_SYM ? s.wi : ~0u;
-    if (s.mode == LM_SYM) lane_load_ring(s, pre);
-    const uint32_t g0 = s.ntok - s.gk;
-    if (s.ntok <= s.tcap) {
+#ifdef ZS_TPF
+    {  // the next group's words, transposed: in round r, lane (q, m) loads words
+       // 4q..4q+3 of source lane 16 r + m (the four lanes of a source read its
+       // 64 contiguous bytes together)
+      const uint32_t q = lane >> 4;
+      const uintptr_t wp = (uintptr_t)s.w;
 #pragma unroll
-      for (uint32_t j = 0; j < GROUP; j++)
-        if (j < s.gk) s.tok[g0 + j] = L.g.tokbuf[j][lane];
-    } else if (tok_ensure(pool, s.unit, s.tcap, s.ntok)) {  // past the primary region: pool pages
+      for (uint32_t r = 0; r < 4; r++) {
+        const uint32_t src = 16u * r + (lane & 15u);
+        const uint32_t wi_s = (uint32_t)__shfl((int)(s.mode == LM_SYM ? s.wi : 0u), (int)src);
+        const uint32_t eb_s = (uint32_t)__shfl((int)s.end_byte, (int)src);
+        const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)wp, (int)src);
+        const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)((uint64_t)wp >> 32), (int)src);
+        gcu32 *w_s = reinterpret_cast<gcu32 *>((uint64_t)hi << 32 | lo);
+        const uint32_t x = wi_s + 4u * q;
+        if (eb_s != 0u && x + 4u <= ((eb_s - 1u) >> 2)) {
+          typedef uint32_t u32x4a4l __attribute__((ext_vector_type(4), aligned(4)));
+          const u32x4a4l v = *reinterpret_cast<const __attribute__((address_space(1))) u32x4a4l *>(w_s + x);
+          pre[4 * r] = v.x;
+          pre[4 * r + 1] = v.y;
+          pre[4 * r + 2] = v.z;
+          pre[4 * r + 3] = v.w;
+        } else if (eb_s != 0u) {
+#pragma unroll
+          for (uint32_t i = 0; i < 4; i++) pre[4 * r + i] = in_word_g(w_s, x + i, eb_s);
+        } else {
+#pragma unroll
+          for (uint32_t i = 0; i < 4; i++) pre[4 * r + i] = 0u;
+        }
+      }
+    }
+#else
+    if (s.mode == LM_SYM) lane_load_ring(s, pre);
+#endif
+    const uint32_t g0 = s.ntok - s.gk;
+#ifdef ZS_TFL
+    // full token quads written transposed: in round r, lane (q = lane / 16,
+    // m = lane % 16) stores quad q of source lane 16 r + m, so the four lanes of
+    // a source write its run's 64 contiguous bytes together (16 sources per
+    // store instruction instead of 64 scattered ones)
+    {
+      typedef uint32_t u32x4a4t __attribute__((ext_vector_type(4), aligned(4)));
+      const uint32_t q = lane >> 4;
+      const uint32_t nq = s.ntok <= s.tcap ? (s.gk >> 2) : 0u;
+      const uintptr_t dst = (uintptr_t)(s.tok + g0);
+#pragma unroll
+      for (uint32_t r = 0; r < 4; r++) {
+        const uint32_t src = 16u * r + (lane & 15u);
+        const uint32_t nq_s = (uint32_t)__shfl((int)nq, (int)src);
+        const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)dst, (int)src);
+        const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)((uint64_t)dst >> 32), (int)src);
+        if (q < nq_s) {
+          u32x4a4t v;
+          v.x = L.g.tokbuf[4 * q][src];
+          v.y = L.g.tokbuf[4 * q + 1][src];
+          v.z = L.g.tokbuf[4 * q + 2][src];
+          v.w = L.g.tokbuf[4 * q + 3][src];
+          *reinterpret_cast<__attribute__((address_space(1))) u32x4a4t *>(((uint64_t)hi << 32 | lo) + 16u * q) = v;
+        }
+      }
+    }
+    if (s.ntok <= s.tcap) {
+      const uint32_t t0 = s.gk & ~3u;
+#pragma unroll
+      for (uint32_t j = 0; j < 3; j++)
+        if (t0 + j < s.gk) s.tok[g0 + t0 + j] = L.g.tokbuf[t0 + j][lane];
+    } else if
+#else
+    if (s.ntok <= s.tcap) {
+      // 16-byte stores (dword-aligned: the target is the lane's own run), the
+      // last gk % 4 tokens singly: 4 + 3 store instructions per group, not 16.
+      // Every lane writes its own unit's region, so each store instruction
+      // touches ~64 cache lines: the count of instructions is what costs
+      // (C2 parse 15.0 -> 11.6 ms from the 16 dword stores)
+      typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+#pragma unroll
+      for (uint32_t q = 0; q < GROUP / 4; q++)
+        if (4 * q + 4 <= s.gk) {
+          u32x4a4 v;
+          v.x = L.g.tokbuf[4 * q][lane];
+          v.y = L.g.tokbuf[4 * q + 1][lane];
+          v.z = L.g.tokbuf[4 * q + 2][lane];
+          v.w = L.g.tokbuf[4 * q + 3][lane];
+          *reinterpret_cast<__attribute__((address_space(1))) u32x4a4 *>(s.tok + g0 + 4 * q) = v;
+        }
+      const uint32_t t0 = s.gk & ~3u;
+#pragma unroll
+      for (uint32_t j = 0; j < 3; j++)
+        if (t0 + j < s.gk) s.tok[g0 + t0 + j] = L.g.tokbuf[t0 + j][lane];
+    } else if
+#endif
+        (tok_ensure(pool, s.unit, s.tcap, s.ntok)) {  // past the primary region: pool pages
       const uint64_t prim_off = (uint64_t)((const uint32_t *)s.tok - tokens);
       for (uint32_t j = 0; j < s.gk; j++) *tok_addr(pool, tokens, s.unit, prim_off, s.tcap, g0 + j) = L.g.tokbuf[j][lane];
     } else {
