@@ -1043,29 +1043,8 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
 #if KP_ON
       const uint64_t kf = KP_NOW();
 #endif
-#ifdef ZS_TPF
-    }
-    {  // words loaded transposed during the last flush: lane (q, m) holds quad q of source 16 r + m
-      const uint32_t q = lane >> 4;
-#pragma unroll
-      for (uint32_t r = 0; r < 4; r++) {
-        const uint32_t src = 16u * r + (lane & 15u);
-#pragma unroll
-        for (uint32_t i = 0; i < 4; i++) L.g.ring[4 * q + i][src] = pre[4 * r + i];
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
-    if (s.mode == LM_SYM) {
-      if (s.wi == pre_wi) {
-        s.nw = rp[0];
-        s.rk = 0;
-      } else {
-        lane_fill_ring(s, rp);
-      }
-#else
       if (s.wi == pre_wi) lane_store_ring(s, rp, pre);  // words loaded during the last flush
       else lane_fill_ring(s, rp);
-#endif
 #if KP_ON
       __builtin_amdgcn_s_waitcnt(0);
       kph.t[4] += KP_NOW() - kf;
@@ -1085,46 +1064,17 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
     // the next group's input words, loaded while this group's tokens leave
     // (the loads precede the stores, so waiting for them never waits for a store)
     pre_wi = s.mode == LM_SYM ? s.wi : ~0u;
-#ifdef ZS_TPF
-    {  // the next group's words, transposed: in round r, lane (q, m) loads words
-       // 4q..4q+3 of source lane 16 r + m (the four lanes of a source read its
-       // 64 contiguous bytes together)
-      const uint32_t q = lane >> 4;
-      const uintptr_t wp = (uintptr_t)s.w;
-#pragma unroll
-      for (uint32_t r = 0; r < 4; r++) {
-        const uint32_t src = 16u * r + (lane & 15u);
-        const uint32_t wi_s = (uint32_t)__shfl((int)(s.mode == LM_SYM ? s.wi : 0u), (int)src);
-        const uint32_t eb_s = (uint32_t)__shfl((int)s.end_byte, (int)src);
-        const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)wp, (int)src);
-        const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)((uint64_t)wp >> 32), (int)src);
-        gcu32 *w_s = reinterpret_cast<gcu32 *>((uint64_t)hi << 32 | lo);
-        const uint32_t x = wi_s + 4u * q;
-        if (eb_s != 0u && x + 4u <= ((eb_s - 1u) >> 2)) {
-          typedef uint32_t u32x4a4l __attribute__((ext_vector_type(4), aligned(4)));
-          const u32x4a4l v = *reinterpret_cast<const __attribute__((address_space(1))) u32x4a4l *>(w_s + x);
-          pre[4 * r] = v.x;
-          pre[4 * r + 1] = v.y;
-          pre[4 * r + 2] = v.z;
-          pre[4 * r + 3] = v.w;
-        } else if (eb_s != 0u) {
-#pragma unroll
-          for (uint32_t i = 0; i < 4; i++) pre[4 * r + i] = in_word_g(w_s, x + i, eb_s);
-        } else {
-#pragma unroll
-          for (uint32_t i = 0; i < 4; i++) pre[4 * r + i] = 0u;
-        }
-      }
-    }
-#else
     if (s.mode == LM_SYM) lane_load_ring(s, pre);
-#endif
     const uint32_t g0 = s.ntok - s.gk;
-#ifdef ZS_TFL
-    // full token quads written transposed: in round r, lane (q = lane / 16,
-    // m = lane % 16) stores quad q of source lane 16 r + m, so the four lanes of
-    // a source write its run's 64 contiguous bytes together (16 sources per
-    // store instruction instead of 64 scattered ones)
+    // Every lane writes its own unit's region, so a store instruction of the
+    // wave touches ~64 cache lines and the count of store instructions is what
+    // costs: full token quads go as 16-byte stores, written transposed -- in
+    // round r, lane (q = lane / 16, m = lane % 16) stores quad q of source lane
+    // 16 r + m, so a source's four lanes write its 64 contiguous bytes together
+    // -- and the last gk % 4 tokens singly.  C2 parse: 16 dword stores per
+    // group 15.0 ms, 4 per-lane 16-byte stores + 3 singles 11.6 ms, transposed
+    // 11.4 ms.  Measured and dropped: the input prefetch transposed the same way
+    // (12.5 ms: its 4 loads were not the cost, the 20 extra lane shuffles were).
     {
       typedef uint32_t u32x4a4t __attribute__((ext_vector_type(4), aligned(4)));
       const uint32_t q = lane >> 4;
@@ -1151,32 +1101,7 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
 #pragma unroll
       for (uint32_t j = 0; j < 3; j++)
         if (t0 + j < s.gk) s.tok[g0 + t0 + j] = L.g.tokbuf[t0 + j][lane];
-    } else if
-#else
-    if (s.ntok <= s.tcap) {
-      // 16-byte stores (dword-aligned: the target is the lane's own run), the
-      // last gk % 4 tokens singly: 4 + 3 store instructions per group, not 16.
-      // Every lane writes its own unit's region, so each store instruction
-      // touches ~64 cache lines: the count of instructions is what costs
-      // (C2 parse 15.0 -> 11.6 ms from the 16 dword stores)
-      typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
-#pragma unroll
-      for (uint32_t q = 0; q < GROUP / 4; q++)
-        if (4 * q + 4 <= s.gk) {
-          u32x4a4 v;
-          v.x = L.g.tokbuf[4 * q][lane];
-          v.y = L.g.tokbuf[4 * q + 1][lane];
-          v.z = L.g.tokbuf[4 * q + 2][lane];
-          v.w = L.g.tokbuf[4 * q + 3][lane];
-          *reinterpret_cast<__attribute__((address_space(1))) u32x4a4 *>(s.tok + g0 + 4 * q) = v;
-        }
-      const uint32_t t0 = s.gk & ~3u;
-#pragma unroll
-      for (uint32_t j = 0; j < 3; j++)
-        if (t0 + j < s.gk) s.tok[g0 + t0 + j] = L.g.tokbuf[t0 + j][lane];
-    } else if
-#endif
-        (tok_ensure(pool, s.unit, s.tcap, s.ntok)) {  // past the primary region: pool pages
+    } else if (tok_ensure(pool, s.unit, s.tcap, s.ntok)) {  // past the primary region: pool pages
       const uint64_t prim_off = (uint64_t)((const uint32_t *)s.tok - tokens);
       for (uint32_t j = 0; j < s.gk; j++) *tok_addr(pool, tokens, s.unit, prim_off, s.tcap, g0 + j) = L.g.tokbuf[j][lane];
     } else {
