@@ -177,6 +177,7 @@ struct LaneState {
 #if KP_ON
   uint32_t kp_steps, kp_slow_l, kp_slow_d, kp_refills;
 #endif
+  uint4 dta, dtb;     // the lane's distance tail header (lim / offs), loaded at group start
   uint32_t pos, cap;  // entries the tokens expand to / entry capacity
   uint32_t capx;      // min(cap, pos + tcap - ntok) at block start: one check covers both
   gcu16 *cl, *cd;     // compact sub-tables (global) of the current block
@@ -281,6 +282,33 @@ __device__ __forceinline__ uint32_t dist_tail(const uint32_t *__restrict__ dtl, 
   for (int k = 1; k < 9; k++) {
     const uint32_t lim = (lw[k >> 1] >> (16 * (k & 1))) & 0xffffu;
     // offs[k] lives at byte 18 + k: word 4 + (2 + k) / 4 of the 32 bytes read
+    const uint32_t ob = 18 + k;
+    const uint32_t ow = ob < 20 ? b.x : (ob < 24 ? b.y : b.z);
+    const uint32_t ofk = (ow >> (8 * (ob & 3))) & 0xffu;
+    const bool ge = rev >= lim;
+    L += ge ? 1u : 0u;
+    fl = ge ? lim : fl;
+    of = ge ? ofk : of;
+  }
+  const uint32_t idx = of + ((rev - fl) >> (15u - L));
+  const uint32_t sym = reinterpret_cast<const uint8_t *>(dtl)[27 + min(idx, 29u)];
+  return CK_SYM | (L << 2) | (sym << 6);
+}
+
+// dist_tail with the 32-byte tail header already in registers (loaded at group
+// start): the canonical search is VALU only and its one LDS read (the symbol)
+// is issued next to the distance root's.  lane_step_fast computes it on every
+// step, no branch: with 64 lanes some lane needs a long distance code on most
+// wave-steps, and the branch paid two dependent LDS round trips (C2 parse
+// 11.4 -> 10.8 ms)
+__device__ __forceinline__ uint32_t dist_tail_r(const uint4 a, const uint4 b, const uint32_t *__restrict__ dtl,
+                                                uint32_t hold) {
+  const uint32_t rev = __builtin_bitreverse32(hold) >> 17;
+  const uint32_t lw[5] = {a.x, a.y, a.z, a.w, b.x};
+  uint32_t L = 7, fl = lw[0] & 0xffffu, of = (b.x >> 16) & 0xffu;
+#pragma unroll
+  for (int k = 1; k < 9; k++) {
+    const uint32_t lim = (lw[k >> 1] >> (16 * (k & 1))) & 0xffffu;
     const uint32_t ob = 18 + k;
     const uint32_t ow = ob < 20 ? b.x : (ob < 24 ? b.y : b.z);
     const uint32_t ofk = (ow >> (8 * (ob & 3))) & 0xffu;
@@ -498,10 +526,9 @@ __device__ __forceinline__ bool lane_step_fast(LaneState &s, const uint16_t *__r
   s.nbits -= used + xb;
   lane_refill_bf(s, rp);
   uint32_t d = dt[(uint32_t)s.hold & (DROOT_N - 1)];
+  const uint32_t dtr = dist_tail_r(s.dta, s.dtb, dtl, (uint32_t)s.hold);
   const bool dslow = isl && (d & 3u) == CK_SLOW;
-  if (__ballot(dslow)) {
-    if (dslow) d = ((d >> 2) & 15u) ? dist_tail(dtl, (uint32_t)s.hold) : (uint32_t)CK_SLOW;
-  }
+  d = dslow ? (((d >> 2) & 15u) ? dtr : (uint32_t)CK_SLOW) : d;
   // distance code dsym (0..31), src/inftrees.c:65-72: extra = max(dsym/2 - 1, 0),
   // base = ((2 + dsym%2) << extra) + 1, minus 2 for dsym < 2
   const uint32_t dused = (d >> 2) & 15u, dsym = (d >> 6) & 31u;
@@ -1045,6 +1072,8 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
 #endif
       if (s.wi == pre_wi) lane_store_ring(s, rp, pre);  // words loaded during the last flush
       else lane_fill_ring(s, rp);
+      s.dta = *reinterpret_cast<const uint4 *>(dtl);
+      s.dtb = *reinterpret_cast<const uint4 *>(dtl + 4);
 #if KP_ON
       __builtin_amdgcn_s_waitcnt(0);
       kph.t[4] += KP_NOW() - kf;
