@@ -295,12 +295,15 @@ __device__ __forceinline__ uint32_t dist_tail(const uint32_t *__restrict__ dtl, 
   return CK_SYM | (L << 2) | (sym << 6);
 }
 
+
 // dist_tail with the 32-byte tail header already in registers (loaded at group
 // start): the canonical search is VALU only and its one LDS read (the symbol)
 // is issued next to the distance root's.  lane_step_fast computes it on every
 // step, no branch: with 64 lanes some lane needs a long distance code on most
 // wave-steps, and the branch paid two dependent LDS round trips (C2 parse
-// 11.4 -> 10.8 ms)
+// 11.4 -> 10.8 ms).  Measured and dropped: the header unpacked at group start
+// into lim << 8 | offs words, one select per length (11.7 ms: one serial
+// select chain instead of three independent ones, at one wave per SIMD)
 __device__ __forceinline__ uint32_t dist_tail_r(const uint4 a, const uint4 b, const uint32_t *__restrict__ dtl,
                                                 uint32_t hold) {
   const uint32_t rev = __builtin_bitreverse32(hold) >> 17;
