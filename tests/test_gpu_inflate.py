@@ -303,6 +303,29 @@ def test_chunked_high_ratio(zs):
     assert st["chunked_jobs"] == 1 and st["fallback_jobs"] == 0 and st["units"] > 1, st
 
 
+@pytest.mark.parametrize("parse", ["lane", "wave"])
+def test_chunked_token_pool_pages(zs, parse):
+    """Streams with several symbols per compressed byte (Huffman-only and RLE
+    over a 3-letter alphabet: 1-2 bit literal codes) outgrow the primary token
+    regions (1 token per compressed byte + slack), so every unit's tokens spill
+    into pool pages -- the lane parse's flush (16-byte stores of full token
+    quads) and its page path, under both parse modes; output and zlib fields
+    match the oracle, nothing falls back."""
+    import numpy as np
+    rng = np.random.default_rng(11)
+    raw = rng.choice(np.frombuffer(b"abc", np.uint8), 12 << 20, p=[0.6, 0.3, 0.1]).tobytes()
+    for strategy, wb in ((zlib.Z_HUFFMAN_ONLY, -15), (zlib.Z_RLE, 31)):
+        c = zlib.compressobj(6, zlib.DEFLATED, wb, 8, strategy)
+        comp = c.compress(raw) + c.flush()
+        assert len(raw) / len(comp) > 4
+        got = zs.inflate_batch([comp, comp], wb, [len(raw)] * 2, parse=parse)
+        st = zs.last_stats()
+        eo, ei = O.oneshot(comp, wb, len(raw))
+        for out, info in got:
+            assert out == eo == raw and info == ei, (info, ei)
+        assert st["chunked_jobs"] == 2 and st["fallback_jobs"] == 0 and st["units"] > 2, st
+
+
 def test_c2_full_size_vs_oracle(zs):
     """configs[1] at full size: one Zipf and one line-text 64 MiB raw stream
     (host zlib L6), output and (ret, msg, total_in, total_out) vs the oracle."""

@@ -294,16 +294,28 @@ int ws_reserve_chunks(size_t nseg, size_t nunits, size_t scratch_entries, size_t
   return 0;
 }
 
-// pool tokens per KiB of chunked input (env ZS_POOL_PER_KB, default 2048: two
-// tokens per compressed byte on top of the primary regions -- a stored-block
-// stretch needs one per byte, and geometric pages may overshoot 2x)
+// pool tokens per KiB of chunked input (env ZS_POOL_PER_KB; 0 = default)
 size_t pool_per_kb() {
   static size_t v = [] {
     const char *e = std::getenv("ZS_POOL_PER_KB");
-    long x = e ? std::atol(e) : 2048;
+    long x = e ? std::atol(e) : 0;
     return (size_t)(x < 0 ? 0 : x);
   }();
   return v;
+}
+// Pool tokens for a batch of in_sum compressed bytes.  Default: 32 per byte on
+// top of the primary regions.  A symbol takes at least one bit, so a unit has at
+// most 8 tokens per compressed byte; a spilling unit takes whole pages (the
+// first one 64 Ki tokens), which for the shortest units (one block of 16 383
+// one-bit symbols: 2 KiB) is 32 per byte.  So no stream outgrows it, however
+// dense its symbols (Huffman-only or RLE over a small alphabet: ~5 per byte).
+// Batches where that passes 4 Gi tokens (16 GiB, > 128 MiB compressed) get
+// max(4 Gi, 2 per byte): there the pool is shared by many streams, and text
+// averages < 0.4 tokens per byte past its primary region.
+size_t pool_tokens(size_t in_sum) {
+  if (pool_per_kb()) return in_sum / 1024 * pool_per_kb();
+  const size_t dense = in_sum * 32, base = in_sum * 2, cap = (size_t)1 << 32;
+  return std::max(base, std::min(dense, cap));
 }
 
 int ws_reserve_bytes(uint8_t **p, size_t *cap, size_t need) {
@@ -544,7 +556,7 @@ int run_jobs(uint32_t nv, uint64_t max_out, uint32_t flags, ZsDecDev *dec_out, Z
       seg_std = si;
       slots_std = slots;
     }
-    const size_t pool_pages = std::max<size_t>(64, (in_sum / 1024 * pool_per_kb() + ((size_t)1 << ZS_TP_LOG) - 1) >> ZS_TP_LOG);
+    const size_t pool_pages = std::max<size_t>(64, (pool_tokens(in_sum) + ((size_t)1 << ZS_TP_LOG) - 1) >> ZS_TP_LOG);
     if (!rr) rr = ws_reserve_chunks(nseg, slots, ents + 16, toks + (pool_pages << ZS_TP_LOG), win);
     if (rr) {  // no room for the chunked path: every job decodes serially
       cj_list.clear();
