@@ -498,6 +498,10 @@ __device__ __forceinline__ bool lane_step_fast(LaneState &s, const uint16_t *__r
   uint32_t e = lt[(uint32_t)s.hold & (LROOT_N - 1)];
   uint32_t kind = e & 3u;
   if (__builtin_expect(__ballot(kind == CK_SLOW) != 0, 0)) {
+#if KP_ON
+    const uint64_t kq = KP_NOW();
+    s.kp_slow_l++;  // every lane of a wave taking the side branch: sum / lane steps = its wave-step share
+#endif
     if (kind == CK_SLOW) {
       const uint32_t op = (e >> 2) & 15u;
       uint32_t e2 = CK_SLOW;
@@ -511,6 +515,9 @@ __device__ __forceinline__ bool lane_step_fast(LaneState &s, const uint16_t *__r
       e = e2;
       kind = e & 3u;
     }
+#if KP_ON
+    kp.t[0] += KP_NOW() - kq;
+#endif
   }
   const uint32_t used = (e >> 2) & 15u, sym = e >> 6;
   const uint32_t isl = kind == CK_LEN;
