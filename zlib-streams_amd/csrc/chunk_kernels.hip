@@ -295,9 +295,13 @@ __global__ void __launch_bounds__(64) zs_find_kernel(const ZsJobDev *__restrict_
       }
       uint32_t tot;
       const uint32_t at = find_scan_excl((uint32_t)__builtin_popcount(cand), &tot);
-      for (uint32_t k = 0; cand && at + k < FQC; k++) {
+      // two candidates per iteration (the loop runs for the wave's largest
+      // count, ~9 of a lane's 32 offsets): find 5.12 -> 4.98 ms on C2
+      for (uint32_t k = 0; cand && at + k < FQC; k += 2) {
+        const uint32_t c1 = cand & (cand - 1u);
         s_q[at + k] = b0 + (uint32_t)__builtin_ctz(cand);
-        cand &= cand - 1u;
+        if (c1 && at + k + 1 < FQC) s_q[at + k + 1] = b0 + (uint32_t)__builtin_ctz(c1);
+        cand = c1 & (c1 - 1u);
       }
       tot = min(tot, FQC);
       __builtin_amdgcn_wave_barrier();
