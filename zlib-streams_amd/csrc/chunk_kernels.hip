@@ -48,18 +48,6 @@ __device__ bool validate_header(const uint32_t *w, uint32_t end_byte, uint32_t b
   uint64_t hold = (uint64_t)in_word(w, wi, end_byte) >> (bit & 31);
   uint32_t n = 32 - (bit & 31);
   wi++;
-#ifdef ZS_FPF
-  // word wi loaded one refill ahead: a refill never waits on its own load
-  uint32_t nw = in_word(w, wi, end_byte);
-  auto refill = [&]() {
-    while (n <= 32) {
-      hold |= (uint64_t)nw << n;
-      n += 32;
-      wi++;
-      nw = in_word(w, wi, end_byte);
-    }
-  };
-#else
   auto refill = [&]() {
     while (n <= 32) {
       hold |= (uint64_t)in_word(w, wi, end_byte) << n;
@@ -67,7 +55,6 @@ __device__ bool validate_header(const uint32_t *w, uint32_t end_byte, uint32_t b
       wi++;
     }
   };
-#endif
   auto pos = [&]() { return wi * 32u - n; };
   refill();
   hold >>= 3;
