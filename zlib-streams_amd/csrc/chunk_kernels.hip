@@ -212,9 +212,16 @@ __global__ void __launch_bounds__(64) zs_find_kernel(const ZsJobDev *__restrict_
   // bits; past FQC (adversarial bit patterns) the rest of the step is dropped
   // -- starts are hints, the chain check keeps results exact
   constexpr uint32_t FQC = WAVE * 12;
-  // full validations run FV lanes at a time: their LUTs then fit the queue's
-  // space, and the smaller LDS footprint raises occupancy
-  constexpr uint32_t FV = 32;
+  // full validations run FV lanes at a time, their LUTs in the queue's space.
+  // Measured on C2 (find): FV 16 6.5 ms, 32 5.0 ms (7 waves/SIMD), 64 4.7 ms
+  // (8 KiB of LUTs, 4 waves/SIMD): each batch's cost is set by its slowest
+  // lane (the per-symbol LUT fill loops, the code-length walk), so half as many
+  // batches beat the lost occupancy
+#ifndef ZS_FV
+  constexpr uint32_t FV = 64;
+#else
+  constexpr uint32_t FV = ZS_FV;
+#endif
   // the full validation's per-lane code-length LUTs reuse this space: they are
   // built after the step's candidates have left it
   __shared__ union {
