@@ -401,23 +401,30 @@ def main():
     k_avg_s = (k_ms / max(k_n, 1)) / 1e3
     achieved = per_launch_alg / k_avg_s / 1e9 if k_avg_s > 0 else 0.0
 
-    traffic = None
+    traffic = traffic_src = None
     if args.traffic_json and os.path.exists(args.traffic_json) and world == 1 and args.workload == "c2":
-        # HBM bytes per pipeline launch from rocprofv3 PMC passes (tools/pmc_traffic.py), same workload
-        traffic = json.load(open(args.traffic_json)).get("hbm_bytes_per_launch")
+        # HBM bytes per pipeline launch from separate rocprofv3 --pmc passes over this same workload
+        # (tools/pmc_traffic.sh -> tools/pmc_traffic.py); PMC cannot be read from inside the timed run
+        tj = json.load(open(args.traffic_json))
+        traffic = tj.get("hbm_bytes_per_launch")
+        import hashlib
+        so_sha = hashlib.sha256(open(os.path.join(ROOT, "zlib-streams_amd", "libzstreams_mi355x.so"), "rb").read()).hexdigest()
+        traffic_src = {"file": os.path.relpath(args.traffic_json, ROOT), "checkpoint": tj.get("checkpoint"),
+                       "same_library_build": tj.get("library_sha256") == so_sha if tj.get("library_sha256") else None,
+                       "how": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, gfx950-corrected, every pipeline kernel"}
 
     comp_leg = d64_leg = None
     if not args.dry_run and not args.no_compress and nloc:
         kinds = [shard.c2_kind(i) for i in ids]
-        comp_leg = compress_leg(args, zstreams, shard, torch, np, dev, dist, raws, d_out, out_ptrs, nbytes,
-                                comps, cpu, rank, kinds)
-        comp_leg["fast_mode"] = compress_leg(args, zstreams, shard, torch, np, dev, dist, raws, d_out, out_ptrs, nbytes,
-                                             comps, cpu, rank, kinds, fast=True)
+        comp_leg = guarded("compress", compress_leg, args, zstreams, shard, torch, np, dev, dist, raws, d_out,
+                           out_ptrs, nbytes, comps, cpu, rank, kinds)
+        comp_leg["fast_mode"] = guarded("compress.fast_mode", compress_leg, args, zstreams, shard, torch, np, dev,
+                                        dist, raws, d_out, out_ptrs, nbytes, comps, cpu, rank, kinds, fast=True)
     if not args.dry_run and not args.no_deflate64:
-        d64_leg = deflate64_leg(args, zstreams, torch, np, dev, rank)
+        d64_leg = guarded("deflate64", deflate64_leg, args, zstreams, torch, np, dev, rank)
     stream_l = None
     if not args.dry_run and not args.no_stream_leg and rank == 0 and world == 1:
-        stream_l = stream_leg(args, zstreams, np, cpu)
+        stream_l = guarded("stream", stream_leg, args, zstreams, np, cpu)
 
     cpu_b = None
     if rank == 0 and not args.no_cpu_baseline and not args.dry_run and nloc:
@@ -427,10 +434,11 @@ def main():
         li = [k for k in range(nloc) if kinds[k] == "lines" and wbits_list[k] == -15]
         order = [x for pair in zip(z, li) for x in pair] + z[len(li):] + li[len(z):]
         sample = order[:max(1, args.cpu_sample)]
-        cpu_b = cpu_baseline(comps, raws, wbits_list, sample, cpu, args.cpu_seconds)
-        cpu_b["gpu_vs_1core"] = round(value / cpu_b["value"], 1)
-        cpu_b["gpu_vs_all_cores"] = round(value / cpu_b["value_all_cores"], 2)
-        cpu_b["gpu_vs_all_cores_linear"] = round(value / cpu_b["value_all_cores_linear"], 2)
+        cpu_b = guarded("cpu_baseline", cpu_baseline, comps, raws, wbits_list, sample, cpu, args.cpu_seconds)
+        if "error" not in cpu_b:
+            cpu_b["gpu_vs_1core"] = round(value / cpu_b["value"], 1)
+            cpu_b["gpu_vs_all_cores"] = round(value / cpu_b["value_all_cores"], 2)
+            cpu_b["gpu_vs_all_cores_linear"] = round(value / cpu_b["value_all_cores_linear"], 2)
 
     if rank == 0:
         line = {
@@ -451,6 +459,7 @@ def main():
             "verified_bit_exact": ok,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "kernel": "inflate pipeline (find+plan+parse+chain+expand+link+emit+serial decode), rank 0",
                          "kernel_ms_avg": round(k_avg_s * 1e3, 3),
                          "alg_bytes_per_launch": per_launch_alg,
@@ -468,6 +477,16 @@ def main():
         print(json.dumps(line), flush=True)
     if dist:
         tdist.destroy_process_group()
+
+
+def guarded(name, fn, *a, **kw):
+    """Run an optional bench leg; a failure is recorded in the line instead of losing the headline."""
+    import traceback
+    try:
+        return fn(*a, **kw)
+    except Exception as e:  # noqa: BLE001 -- any leg failure must not drop the headline line
+        log(f"[bench] leg {name} failed:\n{traceback.format_exc()}")
+        return {"error": f"{type(e).__name__}: {e}"}
 
 
 def _js_schedule_loop(L, h, comp, out, write_size):

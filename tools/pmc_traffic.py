@@ -9,9 +9,11 @@ streaming reads, so it is doubled.  Our kernels also issue narrower accesses
 figure is an estimate of bytes crossing the L2's memory side (Infinity Cache
 hits included), per launch of each pipeline kernel, averaged over dispatches.
 
-usage: pmc_traffic.py FETCH_CSV WRITE_CSV OUT_JSON
+usage: pmc_traffic.py FETCH_CSV WRITE_CSV OUT_JSON [CHECKPOINT_TAG]
+The output records the sha256 of the library the passes ran, so bench.py can
+say whether the traffic figure belongs to the build it is timing.
 """
-import csv, json, sys
+import csv, hashlib, json, os, sys
 from collections import defaultdict
 
 PIPELINE = ("zs_header_kernel", "zs_find_kernel", "zs_find_fixed_kernel", "zs_plan_kernel", "zs_unit_header_kernel",
@@ -46,7 +48,10 @@ def main():
         kernels[k] = {"read_bytes": round(rd), "write_bytes": round(wr),
                       "dispatches": max(fetch.get(k, (0, 0))[1], write.get(k, (0, 0))[1])}
         total += rd + wr
+    so = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "zlib-streams_amd", "libzstreams_mi355x.so")
     out = {"hbm_bytes_per_launch": round(total), "kernels": kernels,
+           "checkpoint": sys.argv[4] if len(sys.argv) > 4 else None,
+           "library_sha256": hashlib.sha256(open(so, "rb").read()).hexdigest(),
            "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes); bytes = 2*FETCH_SIZE*1024 "
                      "+ WRITE_SIZE*1024 per dispatch, averaged over dispatches, summed over pipeline kernels"}
     json.dump(out, open(sys.argv[3], "w"), indent=1)

@@ -11,5 +11,5 @@ B="$R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-compress --no-deflate
 timeout -k 10 400 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o fetch -- python3 $B > $OUT/fetch.log 2>&1 && \
 timeout -k 10 400 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $OUT/write -o write -- python3 $B > $OUT/write.log 2>&1 && \
 python3 $R/tools/pmc_traffic.py $(find $OUT/fetch -name "*counter_collection.csv" | head -1) \
-  $(find $OUT/write -name "*counter_collection.csv" | head -1) $OUT/pmc_traffic.json
+  $(find $OUT/write -name "*counter_collection.csv" | head -1) $OUT/pmc_traffic.json ${PMC_TAG:-}
 echo "pmc rc=$?"
