@@ -103,6 +103,11 @@ typedef struct zs_result {
    one each unit with one lane.  These force one mode (testing, tuning). */
 #define ZS_F_PARSE_LANE 8u
 #define ZS_F_PARSE_WAVE 16u
+/* Link mode of the block-parallel path (results are identical): groups of at
+   most 4 long streams use the parallel-prefix window link by default, larger
+   groups the per-stream serial link (zs_link_kernel).  This forces the serial
+   link (testing, tuning). */
+#define ZS_F_LINK_SERIAL 32u
 
 #define ZS_ENODEV (-100)
 #define ZS_EFORMAT (-101) /* malformed container (zs_zip_scan) */
@@ -180,6 +185,14 @@ int zs_kprof_read(uint64_t *out, uint32_t n, int reset);
    chunked jobs whose chain did not verify (decoded by the serial decoder
    instead), jobs routed to the serial decoder] */
 int zs_last_stats(uint32_t out[4]);
+/* The same four counters, then the path the last batch's block-parallel groups
+   took: [4] raw/zlib/gzip group parse mode (0 lane per unit, 1 wave per unit,
+   UINT32_MAX no such group), [5] its link (0 serial, else parallel-prefix scan
+   levels), [6] / [7] the same for the deflate64 group, [8] lane-parse waves
+   resident at once (units dealt in groups of 64 x this), [9] decode units of the
+   raw/zlib/gzip group, [10] of the deflate64 group.  Writes min(n, 11) entries
+   and returns that count. */
+int zs_last_stats_ex(uint32_t *out, uint32_t n);
 /* stream-call batching since load: [launch sequences, calls they ran].  Calls of
    the handle / zlib ABIs made at the same time from different threads (one
    handle per thread) share one launch, a workgroup per call. */

@@ -372,3 +372,32 @@ def test_deflate_stream_buffer_bound(zs, monkeypatch):
         out += o
         assert early > 0 and g.end() == 0
         assert zlib.decompress(bytes(out), wb) == data
+
+
+def test_deflate_fixup_in_order_pass(zs, monkeypatch):
+    """ZS_ZD_ROUNDS=0 skips the parallel cross-region fix-up rounds, so every
+    job's regions are settled by the in-order pass (zs_zd_fix_seq_kernel):
+    zlib's bytes at every deflate_slow level on text, periodic runs (whose
+    parse offsets never line up across 64 KiB regions) and mixed inputs."""
+    monkeypatch.setenv("ZS_ZD_ROUNDS", "0")
+    rng = random.Random(21)
+    pats = _patterns(rng)
+    per = bytes(rng.getrandbits(8) for _ in range(1000)) * 1200  # period 1000, 1.2 MB
+    cases = [(d, wb, lv) for d in (pats["text"], pats["mixed"], bytes(1 << 20), per, b"ab" * 400000)
+             for wb, lv in ((-15, 4), (31, 6), (15, 9))]
+    got = zs.deflate_batch([c[0] for c in cases], [c[1] for c in cases], [c[2] for c in cases])
+    bad = [(i, len(d), wb, lv) for i, ((d, wb, lv), (comp, info)) in enumerate(zip(cases, got))
+           if comp != zlib_bytes(d, wb, lv) or info["ret"] != 1]
+    assert not bad, bad
+
+
+def test_deflate_long_zero_run_is_zlibs(zs):
+    """300 MiB of zeros (> 4096 regions of 64 KiB: the cascade a bounded number
+    of parallel rounds cannot settle) and a 300 MiB periodic run, levels 4 and 9:
+    zlib's bytes."""
+    zeros = bytes(300 << 20)
+    per = (bytes(random.Random(5).getrandbits(8) for _ in range(777)) * ((300 << 20) // 777 + 1))[:300 << 20]
+    for data in (zeros, per):
+        for wb, lv in ((-15, 4), (31, 9)):
+            (comp, info), = zs.deflate_batch([data], wb, lv)
+            assert info["ret"] == 1 and comp == zlib_bytes(data, wb, lv), (len(data), wb, lv, len(comp))

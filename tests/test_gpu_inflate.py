@@ -395,3 +395,67 @@ def test_chunked_too_far_back_across_units(zs, copies):
     for out, info in got:
         assert info == ei and out == eo, (info, ei)
     assert st["chunked_jobs"] == copies and st["fallback_jobs"] == copies, st
+
+
+# ---------------------------------------------------------------------------
+# the headline's own kernel path at headline scale: lane-per-unit parse (the
+# mode a batch of > ZS_WAVE_SEGS search segments takes) with the multi-group
+# dealing of lane_decode.hip (units past 64 x the resident waves), and the
+# per-stream serial window link (zs_link_kernel) on the C2 pair
+# ---------------------------------------------------------------------------
+def _c5_cases(n, nthreads=16):
+    from concurrent.futures import ThreadPoolExecutor
+
+    def make(k):
+        raw, wb = corpus.c5_stream(k, 4 << 20)
+        c = zlib.compressobj(6, zlib.DEFLATED, wb, 8)
+        return raw, c.compress(raw) + c.flush(), wb
+
+    with ThreadPoolExecutor(nthreads) as ex:
+        return list(ex.map(make, range(n)))
+
+
+def _compare_all_with_oracle(cases, got, cap, nthreads=16):
+    """Every job's output and (ret, msg, total_in, total_out, adler) vs the
+    oracle, the oracle's output vs the generator; oracle calls run on threads
+    (ctypes releases the GIL)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    def check(k):
+        raw, comp, wb = cases[k]
+        out, info = got[k]
+        eo, ei = O.oneshot(comp, wb, cap)
+        ok = out == eo and info == ei and len(eo) == len(raw) and eo == raw.tobytes()
+        return None if ok else (k, wb, info, ei)
+
+    with ThreadPoolExecutor(nthreads) as ex:
+        bad = [b for b in ex.map(check, range(len(cases))) if b]
+    assert not bad, f"{len(bad)} mismatches, first: {bad[:4]}"
+
+
+def test_c5_lane_parse_multigroup_vs_oracle(zs):
+    """configs[4] shape at a scale where the lane parse deals its sorted units
+    over more than one group of resident waves: 1 280 x 4 MiB streams (raw / gzip
+    alternating, Zipf / line text), lane mode forced, every job vs the oracle."""
+    n = 1280
+    cases = _c5_cases(n)
+    got = zs.inflate_batch([c[1] for c in cases], [c[2] for c in cases], [4 << 20] * n, parse="lane")
+    st = zs.last_stats()
+    assert st["parse"] == "lane" and st["link"] == "serial", st
+    assert st["lane_resident_waves"] > 0 and st["units_std"] > 64 * st["lane_resident_waves"], st
+    assert st["chunked_jobs"] == n and st["fallback_jobs"] == 0, st
+    _compare_all_with_oracle(cases, got, 4 << 20)
+
+
+def test_c2_pair_lane_parse_serial_link_vs_oracle(zs):
+    """configs[1] streams at full size (one Zipf, one line text, 64 MiB each)
+    through the lane parse and the serial per-stream link -- the kernels the C2
+    headline runs -- vs the oracle."""
+    raws, comps = corpus.batch(0, 1, 64 << 20, level=6, wbits=-15, nthreads=1)
+    r2, c2 = corpus.batch(32, 1, 64 << 20, level=6, wbits=-15, nthreads=1)
+    cases = [(r, c.tobytes(), -15) for r, c in zip(raws + r2, comps + c2)]
+    got = zs.inflate_batch([c[1] for c in cases], -15, [64 << 20] * 2, parse="lane", link="serial")
+    st = zs.last_stats()
+    assert st["parse"] == "lane" and st["link"] == "serial", st
+    assert st["chunked_jobs"] == 2 and st["fallback_jobs"] == 0, st
+    _compare_all_with_oracle(cases, got, 64 << 20, nthreads=2)

@@ -61,3 +61,17 @@ def test_gpu_code_object_is_gfx950():
     _ensure_built()
     blob = open(SO, "rb").read()
     assert b"amdgcn-amd-amdhsa--gfx950" in blob
+
+
+ZLIB_ABI = {"inflateInit_", "inflateInit2_", "inflate", "inflateEnd",
+            "deflateInit_", "deflateInit2_", "deflate", "deflateEnd", "deflateBound"}
+
+
+def test_library_exports_only_the_public_abi():
+    """The dynamic symbol table is exactly the header's functions plus the zlib
+    ABI (csrc/exports.map): no kernel launchers or helpers leak into a host
+    application's namespace."""
+    _ensure_built()
+    out = subprocess.run(["nm", "-D", "--defined-only", SO], capture_output=True, text=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if ln.strip()}
+    assert exported == set(declared_functions()) | ZLIB_ABI, sorted(exported ^ (set(declared_functions()) | ZLIB_ABI))

@@ -38,6 +38,7 @@
 //                       offsets per job, then the bits.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "zs_check.h"
 #include "zs_common.h"
@@ -472,9 +473,69 @@ __global__ void __launch_bounds__(ZD_PT) zs_zd_parse_kernel(const ZsDJobDev *__r
 // when it differs from the assumed one (region start, state A) the region is
 // re-walked from it until the walk meets a state-A position of the region's
 // own parse (and reaches past earlier rewrites), its tokens before that point
-// rewritten.  One round per launch (exits double-buffered: read [cur], write
-// [cur ^ 1]); the host repeats rounds until no exit changes.
+// rewritten.  zs_zd_fix_kernel: one round, every region at once (exits
+// double-buffered: read [cur], write [cur ^ 1]); the host repeats rounds while
+// exits change, up to a bound.  A correction moves one region per round, so a
+// long periodic run (zeros, a repeated pattern: the true parse and each
+// region's own parse step in 258s from offsets that never line up) would need
+// a round per region; past the bound zs_zd_fix_seq_kernel finishes the job in
+// ONE pass, a thread per job walking its regions in order, each region's
+// entry being the exit its predecessor just got.
 // ---------------------------------------------------------------------------
+// region i from entry (ep, es): rewrites its tokens where they change, returns
+// its exit in (xp, xs)
+__device__ void zd_fix_region(const ZsDJobDev &jb, ZsDSegDev *__restrict__ segs, uint32_t i,
+                              const uint32_t *__restrict__ ma, const uint32_t *__restrict__ mb, uint32_t *__restrict__ bm,
+                              uint64_t ep, uint32_t es, uint64_t &xp, uint32_t &xs) {
+  const ZsDSegDev sg = segs[i];
+  const uint64_t r0 = sg.start, rend = sg.start + sg.len;
+  xp = sg.zx0;
+  xs = sg.zs0;
+  if (ep == r0 && es == ZD_STATE_A && sg.zfix == r0) return;  // its own parse stands
+  ZdTabs T;
+  T.ma = ma + jb.pos0;
+  T.mb = mb + jb.pos0;
+  T.in = jb.in;
+  T.L = jb.in_len;
+  T.good = zd_cfg[jb.level][0];
+  T.lazy = zd_cfg[jb.level][1];
+  ZdBm Bm = zd_bm(bm, jb);
+  // 1. where does the walk from the entry merge with the region's own parse?
+  uint64_t q = ep;
+  uint32_t qs = es, var;
+  bool merged = false;
+  while (q < rend) {
+    if (qs == ZD_STATE_A && q >= sg.zfix && zd_getbit(Bm.M, q)) {
+      merged = true;
+      break;
+    }
+    (void)zd_step(T, q, qs, &var);
+  }
+  const uint64_t conv = merged ? q : rend;
+  if (!merged) {
+    xp = q;
+    xs = qs;
+  }
+  // 2. rewrite the tokens of [r0, conv)
+  for (uint64_t x = r0; x < conv; x += 32u) {
+    const uint64_t w = x >> 5;
+    const uint32_t n = (uint32_t)min<uint64_t>(32u, conv - x);
+    const uint32_t keep = n == 32u ? 0u : ~0u << n;  // region words start 32-aligned
+    Bm.S[w] &= keep;
+    Bm.V[w] &= keep;
+  }
+  q = ep;
+  qs = es;
+  zd_walk_record(
+      T, q, qs, conv,
+      [&](uint64_t x, uint32_t v) {
+        Bm.S[x >> 5] |= 1u << (x & 31u);
+        if (v) Bm.V[x >> 5] |= 1u << (x & 31u);
+      },
+      (uint32_t *)nullptr, 0);
+  segs[i].zfix = conv;
+}
+
 __global__ void zs_zd_fix_kernel(const ZsDJobDev *__restrict__ jobs, ZsDSegDev *__restrict__ segs, uint32_t nseg,
                                  const uint32_t *__restrict__ ma, const uint32_t *__restrict__ mb, uint32_t *__restrict__ bm,
                                  uint32_t cur, uint32_t *__restrict__ changed) {
@@ -483,62 +544,44 @@ __global__ void zs_zd_fix_kernel(const ZsDJobDev *__restrict__ jobs, ZsDSegDev *
   const ZsDSegDev sg = segs[i];
   const ZsDJobDev jb = jobs[sg.job];
   if (!jb.exact) return;
-  const uint64_t r0 = sg.start, rend = sg.start + sg.len;
-  uint64_t ep = r0;
+  uint64_t ep = sg.start;
   uint32_t es = ZD_STATE_A;
-  if (r0 != 0) {
+  if (sg.start != 0) {
     ep = segs[i - 1].zx[cur];
     es = segs[i - 1].zs[cur];
   }
-  uint64_t xp = sg.zx0;
-  uint32_t xs = sg.zs0;
-  if (!(ep == r0 && es == ZD_STATE_A) || sg.zfix != r0) {
-    ZdTabs T;
-    T.ma = ma + jb.pos0;
-    T.mb = mb + jb.pos0;
-    T.in = jb.in;
-    T.L = jb.in_len;
-    T.good = zd_cfg[jb.level][0];
-    T.lazy = zd_cfg[jb.level][1];
-    ZdBm Bm = zd_bm(bm, jb);
-    // 1. where does the walk from the entry merge with the region's own parse?
-    uint64_t q = ep;
-    uint32_t qs = es, var;
-    bool merged = false;
-    while (q < rend) {
-      if (qs == ZD_STATE_A && q >= sg.zfix && zd_getbit(Bm.M, q)) {
-        merged = true;
-        break;
-      }
-      (void)zd_step(T, q, qs, &var);
-    }
-    const uint64_t conv = merged ? q : rend;
-    if (!merged) {
-      xp = q;
-      xs = qs;
-    }
-    // 2. rewrite the tokens of [r0, conv)
-    for (uint64_t x = r0; x < conv; x += 32u) {
-      const uint64_t w = x >> 5;
-      const uint32_t n = (uint32_t)min<uint64_t>(32u, conv - x);
-      const uint32_t keep = n == 32u ? 0u : ~0u << n;  // region words start 32-aligned
-      Bm.S[w] &= keep;
-      Bm.V[w] &= keep;
-    }
-    q = ep;
-    qs = es;
-    zd_walk_record(
-        T, q, qs, conv,
-        [&](uint64_t x, uint32_t v) {
-          Bm.S[x >> 5] |= 1u << (x & 31u);
-          if (v) Bm.V[x >> 5] |= 1u << (x & 31u);
-        },
-        (uint32_t *)nullptr, 0);
-    segs[i].zfix = conv;
-  }
+  uint64_t xp;
+  uint32_t xs;
+  zd_fix_region(jb, segs, i, ma, mb, bm, ep, es, xp, xs);
   segs[i].zx[cur ^ 1u] = xp;
   segs[i].zs[cur ^ 1u] = xs;
   if (xp != sg.zx[cur] || xs != sg.zs[cur]) atomicOr(changed, 1u);
+}
+
+// one thread per job: its regions in order from the job's start, so every
+// entry is final when its region is walked (no rounds)
+__global__ void zs_zd_fix_seq_kernel(const ZsDJobDev *__restrict__ jobs, uint32_t njobs, ZsDSegDev *__restrict__ segs,
+                                     const uint32_t *__restrict__ ma, const uint32_t *__restrict__ mb,
+                                     uint32_t *__restrict__ bm) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= njobs) return;
+  const ZsDJobDev jb = jobs[j];
+  if (!jb.exact) return;
+  uint64_t ep = 0;
+  uint32_t es = ZD_STATE_A;
+  for (uint32_t i = jb.seg0; i < jb.seg0 + jb.nseg; i++) {
+    if (segs[i].start == 0) {
+      ep = 0;
+      es = ZD_STATE_A;
+    }
+    uint64_t xp;
+    uint32_t xs;
+    zd_fix_region(jb, segs, i, ma, mb, bm, ep, es, xp, xs);
+    segs[i].zx[0] = segs[i].zx[1] = xp;
+    segs[i].zs[0] = segs[i].zs[1] = xs;
+    ep = xp;
+    es = xs;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1232,6 +1275,14 @@ __global__ void __launch_bounds__(ZD_TT) zs_zd_emit_kernel(const ZsDJobDev *__re
 // deflate_kernels.hip run beside it); returns after the fix-up rounds, which
 // need the host (a flag read per round)
 // ---------------------------------------------------------------------------
+// parallel fix-up rounds before the in-order pass (env ZS_ZD_ROUNDS, read per
+// batch so tests can force the in-order pass on small inputs)
+static int zd_fix_rounds() {
+  const char *e = getenv("ZS_ZD_ROUNDS");
+  const int v = e ? atoi(e) : 8;
+  return v < 0 ? 0 : v;
+}
+
 extern "C" int zs_launch_zdeflate(ZsDJobDev *d_jobs, uint32_t njobs, ZsDSegDev *d_segs, uint32_t nseg,
                                   const ZsZWorkDev *d_w1, uint32_t n1, const ZsZWorkDev *d_w2, uint32_t n2,
                                   uint16_t *d_prevd, uint32_t *d_ma, uint32_t *d_mb, uint32_t *d_bm, ZsZBlkDev *d_blks,
@@ -1242,8 +1293,12 @@ extern "C" int zs_launch_zdeflate(ZsDJobDev *d_jobs, uint32_t njobs, ZsDSegDev *
   if (n2) hipLaunchKernelGGL(zs_zd_match_kernel, dim3(n2), dim3(ZD_MT), 0, st, d_jobs, d_w2, d_prevd, d_ma, d_mb);
   if (ev) (void)hipEventRecord(ev[1], st);
   hipLaunchKernelGGL(zs_zd_parse_kernel, dim3(nseg), dim3(ZD_PT), 0, st, d_jobs, d_segs, d_ma, d_mb, d_bm);
+  // parallel fix-up rounds while exits change (nearly every input settles in
+  // one or two), then, if a cascade is still moving, the in-order pass
+  const int max_rounds = zd_fix_rounds();
   uint32_t cur = 0;
-  for (int round = 0; round < 4096; round++) {
+  bool settled = false;
+  for (int round = 0; round < max_rounds; round++) {
     uint32_t changed = 0;
     if (hipMemsetAsync(d_flag, 0, sizeof(uint32_t), st) != hipSuccess) return -1;
     hipLaunchKernelGGL(zs_zd_fix_kernel, dim3((nseg + 255) / 256), dim3(256), 0, st, d_jobs, d_segs, nseg, d_ma, d_mb, d_bm,
@@ -1252,7 +1307,14 @@ extern "C" int zs_launch_zdeflate(ZsDJobDev *d_jobs, uint32_t njobs, ZsDSegDev *
         hipStreamSynchronize(st) != hipSuccess)
       return -1;
     cur ^= 1u;
-    if (!changed) break;
+    if (!changed) {
+      settled = true;
+      break;
+    }
+  }
+  if (!settled) {
+    hipLaunchKernelGGL(zs_zd_fix_seq_kernel, dim3((njobs + 63) / 64), dim3(64), 0, st, d_jobs, njobs, d_segs, d_ma, d_mb,
+                       d_bm);
   }
   if (ev) (void)hipEventRecord(ev[2], st);
   hipLaunchKernelGGL(zs_zd_count_kernel, dim3(nseg), dim3(256), 0, st, d_jobs, d_segs, d_bm);

@@ -2399,6 +2399,23 @@ int sort_units(const ZsJobDev *d_jobs, const ZsChunkDev *d_chunks, uint32_t n, i
 }
 }  // namespace
 
+// Lane-parse waves resident at once (CUs x waves per CU by LDS); the lane
+// kernel deals the sorted units over groups of this many waves.
+extern "C" uint32_t zs_lane_resident_waves(void) {
+  static const uint32_t v = [] {
+    const char *e = std::getenv("ZS_LANE_MAP");
+    if (e) return (uint32_t)std::atoi(e);
+    int dev = 0, cus = 0, lds = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess || cus <= 0 ||
+        lds <= 0)
+      return 0u;
+    return (uint32_t)cus * std::max<uint32_t>(1u, (uint32_t)lds / (uint32_t)sizeof(LaneLDS));
+  }();
+  return v;
+}
+
 // wave_units: decode with a wave per unit (zs_unitw_kernel) instead of a lane
 // per unit -- the host picks it when a batch has few units for the GPU.
 extern "C" void zs_launch_parse(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, ZsChunkDev *d_chunks, uint32_t nchunks,
@@ -2425,17 +2442,7 @@ extern "C" void zs_launch_parse(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads
   // group: every resident wave gets a share of the long units (C2 parse 18.7 ->
   // 17.8 ms, C5 73.8 -> 69.0 ms; spreading over more waves than fit made the
   // last ones wait a round, 28.6 ms).  Env ZS_LANE_MAP: group size, 0 = blocked.
-  static const uint32_t lane_map = [] {
-    const char *e = std::getenv("ZS_LANE_MAP");
-    if (e) return (uint32_t)std::atoi(e);
-    int dev = 0, cus = 0, lds = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess || cus <= 0 ||
-        lds <= 0)
-      return 0u;
-    return (uint32_t)cus * std::max<uint32_t>(1u, (uint32_t)lds / (uint32_t)sizeof(LaneLDS));
-  }();
+  const uint32_t lane_map = zs_lane_resident_waves();
   if (d64)
     hipLaunchKernelGGL(zs_lane_kernel<true>, dim3((nchunks + WAVE - 1) / WAVE), dim3(WAVE), 0, st, d_jobs, d_heads,
                        d_chunks, nchunks, d_tokens, d_tables, d_fixed, order, pool, lane_map);

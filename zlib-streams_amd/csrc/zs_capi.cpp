@@ -35,6 +35,7 @@ extern "C" void zs_launch_finish(const ZsJobDev *d_jobs, const ZsHeadDev *d_head
 extern "C" void zs_launch_stream(int d64, int run_header, ZsStreamDev *const *d_sts, const ZsJobDev *d_jobs,
                                  ZsHeadDev *d_heads, uint32_t n, uint64_t max_out_cap, ZsStreamRes *d_res,
                                  hipStream_t stream);
+extern "C" uint32_t zs_lane_resident_waves(void);
 extern "C" void zs_launch_fixed_tables(uint32_t *fixed, int d64, hipStream_t st);
 extern "C" void zs_launch_fixed_compact(uint32_t *fixed, hipStream_t st);
 extern "C" void zs_launch_deflate(ZsDJobDev *d_jobs, uint32_t njobs, ZsDSegDev *d_segs, uint32_t nseg, uint16_t *d_dist16,
@@ -63,6 +64,9 @@ namespace {
 constexpr size_t TABLE_ENTRIES_HOST = 1448 + 724 + 176;  // must match TABLE_STRIDE (zs_device.h)
 constexpr size_t FIXED_WORDS_HOST = 544 + 272;      // must match FIXED_WORDS (zs_device.h)
 constexpr uint64_t MAX_RATIO = 1032;  // deflate's largest expansion: 258 bytes per 2 bits
+// deflate64: code 285 carries 16 extra bits for up to 65538 bytes, so one 1-bit
+// length code + 16 extra bits + a 1-bit distance code (18 bits) yield 65538 bytes
+constexpr uint64_t MAX_RATIO_D64 = 65538ull * 8 / 18 + 1;
 
 const char *const kMsgs[ZM_COUNT] = {
     nullptr,
@@ -148,6 +152,9 @@ struct Workspace {
   // last batch: chunked jobs, decode units planned, chunked jobs that fell back
   // to the serial decoder, serial jobs
   uint32_t stats[4] = {0, 0, 0, 0};
+  // last launch's block-parallel path: parse mode / link levels of the std and
+  // deflate64 groups, lane-parse resident waves, units per group (zs_last_stats_ex)
+  uint32_t path[7] = {UINT32_MAX, 0, UINT32_MAX, 0, 0, 0, 0};
 };
 
 // chunked-path tuning (env: ZS_CHUNK_KB, ZS_NO_CHUNK, ZS_POOL_PER_KB)
@@ -168,12 +175,12 @@ uint32_t chunk_bytes() {
 // most PLINK_JOBS streams with long chains (env ZS_PLINK = 0 disables it);
 // returns the scan levels (0 = the serial per-stream link).
 constexpr uint32_t PLINK_JOBS = 4;
-uint32_t plink_levels(uint32_t njobs, uint32_t max_units) {
+uint32_t plink_levels(uint32_t njobs, uint32_t max_units, uint32_t flags) {
   static const bool off = [] {
     const char *e = std::getenv("ZS_PLINK");
     return e && e[0] == '0';
   }();
-  if (off || njobs == 0 || njobs > PLINK_JOBS || max_units < 64) return 0;
+  if (off || (flags & ZS_F_LINK_SERIAL) || njobs == 0 || njobs > PLINK_JOBS || max_units < 64) return 0;
   uint32_t lv = 0;
   while ((1u << lv) < max_units) lv++;
   return lv;
@@ -533,7 +540,7 @@ int run_jobs(uint32_t nv, uint64_t max_out, uint32_t flags, ZsDecDev *dec_out, Z
       // (zs_chain_kernel), hence 8 entries of padding per possible unit
       cj.scratch0 = ents;
       // (a piece of a long stream cuts its chain at ZS_PART_OUT bytes)
-      cj.scratch_n = std::min<uint64_t>(std::min<uint64_t>(jd.out_cap, MAX_RATIO * jd.in_len + 64),
+      cj.scratch_n = std::min<uint64_t>(std::min<uint64_t>(jd.out_cap, (jd.d64 ? MAX_RATIO_D64 : MAX_RATIO) * jd.in_len + 64),
                                         (jd.flags & ZS_JF_PART) ? ZS_PART_OUT : ~0ull) +
                      8ull * max_units;
       cj.esz = jd.d64 ? 2u : 1u;  // deflate64: 17-bit entries, stored as u32
@@ -559,6 +566,8 @@ int run_jobs(uint32_t nv, uint64_t max_out, uint32_t flags, ZsDecDev *dec_out, Z
     const size_t pool_pages = std::max<size_t>(64, (pool_tokens(in_sum) + ((size_t)1 << ZS_TP_LOG) - 1) >> ZS_TP_LOG);
     if (!rr) rr = ws_reserve_chunks(nseg, slots, ents + 16, toks + (pool_pages << ZS_TP_LOG), win);
     if (rr) {  // no room for the chunked path: every job decodes serially
+      (void)hipGetLastError();  // the failed hipMalloc is tolerated: clear HIP's last error and ours
+      g_err.clear();
       cj_list.clear();
       std::fill(is_cj.begin(), is_cj.end(), 0);
       nseg = 0;
@@ -592,16 +601,26 @@ int run_jobs(uint32_t nv, uint64_t max_out, uint32_t flags, ZsDecDev *dec_out, Z
   {
     uint32_t mu_std = 0, mu_d64 = 0;
     for (uint32_t q = 0; q < n_cj; q++) (q < n_cjs ? mu_std : mu_d64) = std::max((q < n_cjs ? mu_std : mu_d64), g_ws.h_cjobs[q].max_units);
-    pl_std = n_cjs ? plink_levels(n_cjs, mu_std) : 0;
-    pl_d64 = n_cj64 ? plink_levels(n_cj64, mu_d64) : 0;
+    pl_std = n_cjs ? plink_levels(n_cjs, mu_std, flags) : 0;
+    pl_d64 = n_cj64 ? plink_levels(n_cj64, mu_d64, flags) : 0;
     const size_t need = std::max<size_t>(pl_std ? 2 * slots_std * 32768u * 2u : 0,
                                          pl_d64 ? 2 * (nunit_slots - slots_std) * 65536u * 4u : 0);
-    if (need && ws_reserve_bytes(&g_ws.d_plink, &g_ws.cap_plink, need)) pl_std = pl_d64 = 0;  // serial link instead
+    if (need && ws_reserve_bytes(&g_ws.d_plink, &g_ws.cap_plink, need)) {
+      pl_std = pl_d64 = 0;  // serial link instead; the failed hipMalloc must not fail the batch
+      (void)hipGetLastError();
+      g_err.clear();
+    }
   }
+  const uint32_t wu_std = n_cjs ? (uint32_t)wave_units(seg_std, flags) : UINT32_MAX;
+  const uint32_t wu_d64 = n_cj64 ? (uint32_t)wave_units(nseg - seg_std, flags) : UINT32_MAX;
+  g_ws.path[0] = wu_std;
+  g_ws.path[1] = pl_std;
+  g_ws.path[2] = wu_d64;
+  g_ws.path[3] = pl_d64;
   if (n_cjs) {
     zs_launch_chunked(g_ws.d_jobs, g_ws.d_heads, g_ws.d_segs, (uint32_t)seg_std, g_ws.d_cjobs, n_cjs, g_ws.d_chunks,
                       (uint32_t)slots_std, g_ws.d_scratch, g_ws.d_tokens, pool, g_ws.d_tables, g_ws.d_fixed,
-                      g_ws.d_windows, g_ws.d_linkinfo, g_ws.d_decs, g_ws.d_fallback, 0, wave_units(seg_std, flags),
+                      g_ws.d_windows, g_ws.d_linkinfo, g_ws.d_decs, g_ws.d_fallback, 0, (int)wu_std,
                       pl_std ? g_ws.d_plink : nullptr, pl_std, st, ev ? ev + 1 : nullptr);
   }
   if (n_cj64) {  // the deflate64 group: its own slice of every per-unit array
@@ -611,13 +630,11 @@ int run_jobs(uint32_t nv, uint64_t max_out, uint32_t flags, ZsDecDev *dec_out, Z
                       g_ws.d_cjobs + n_cjs, n_cj64, g_ws.d_chunks + slots_std, (uint32_t)(nunit_slots - slots_std),
                       g_ws.d_scratch, g_ws.d_tokens, p64, g_ws.d_tables + slots_std * TABLE_ENTRIES_HOST,
                       g_ws.d_fixed + FIXED_WORDS_HOST, g_ws.d_windows + slots_std * 32768, g_ws.d_linkinfo + slots_std * 2,
-                      g_ws.d_decs, g_ws.d_fallback, 1, wave_units(nseg - seg_std, flags), pl_d64 ? g_ws.d_plink : nullptr,
+                      g_ws.d_decs, g_ws.d_fallback, 1, (int)wu_d64, pl_d64 ? g_ws.d_plink : nullptr,
                       pl_d64, st, (ev && !n_cjs) ? ev + 1 : nullptr);
   }
   if (!n_cj && ev)
     for (int i = 1; i <= 6; i++) HIP_OK(hipEventRecord(ev[i], st));
-  if (n_cj && ev && n_cjs && n_cj64)  // stage events cover the first group only
-    ;
   zs_launch_decode(0, g_ws.d_jobs, g_ws.d_heads, g_ws.d_ids, n_std, g_ws.d_decs, nullptr, st);
   zs_launch_decode(1, g_ws.d_jobs, g_ws.d_heads, g_ws.d_ids + n_std, n_d64, g_ws.d_decs, nullptr, st);
   if (n_cjs) zs_launch_decode(0, g_ws.d_jobs, g_ws.d_heads, g_ws.d_ids + n_std + n_d64, n_cjs, g_ws.d_decs, g_ws.d_fallback, st);
@@ -661,6 +678,8 @@ int run_jobs(uint32_t nv, uint64_t max_out, uint32_t flags, ZsDecDev *dec_out, Z
     g_ws.prof_batch_ms += bms;
     g_ws.prof_launches++;
   }
+  g_ws.path[4] = zs_lane_resident_waves();
+  g_ws.path[5] = g_ws.path[6] = 0;
   g_ws.stats[0] = n_cj;
   g_ws.stats[1] = 0;
   g_ws.stats[2] = 0;
@@ -671,6 +690,7 @@ int run_jobs(uint32_t nv, uint64_t max_out, uint32_t flags, ZsDecDev *dec_out, Z
     HIP_OK(hipMemcpy(g_ws.h_cjobs, g_ws.d_cjobs, n_cj * sizeof(ZsCJobDev), hipMemcpyDeviceToHost));
     for (uint32_t k : cj_list) g_ws.stats[2] += fb[k];
     for (uint32_t q = 0; q < n_cj; q++) g_ws.stats[1] += g_ws.h_cjobs[q].nunits;
+    for (uint32_t q = 0; q < n_cj; q++) g_ws.path[q < n_cjs ? 5 : 6] += g_ws.h_cjobs[q].nunits;
     if (std::getenv("ZS_DEBUG_CHUNKS")) {
       uint32_t used = 0;
       HIP_OK(hipMemcpy(&used, g_ws.d_pool_next, sizeof used, hipMemcpyDeviceToHost));
@@ -971,8 +991,8 @@ int sq_submit(StreamCall *c) {
     const size_t take = std::min(g_sq.pending.size(), SQ_MAX);
     std::vector<StreamCall *> batch(g_sq.pending.begin(), g_sq.pending.begin() + take);
     g_sq.pending.erase(g_sq.pending.begin(), g_sq.pending.begin() + take);
+    g_sq.last_n = std::max(batch.size(), g_sq.pending.size() + batch.size() / 2);  // under the mutex
     lk.unlock();
-    g_sq.last_n = std::max(batch.size(), g_sq.pending.size() + batch.size() / 2);
     const int rc = sq_launch(batch);
     const std::string msg = rc ? g_err : std::string();
     lk.lock();
@@ -1769,6 +1789,16 @@ int zs_last_stats(uint32_t out[4]) {
   std::lock_guard<std::mutex> lk(g_mu);
   for (int i = 0; i < 4; i++) out[i] = g_ws.stats[i];
   return 0;
+}
+
+int zs_last_stats_ex(uint32_t *out, uint32_t n) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  uint32_t v[11];
+  for (int i = 0; i < 4; i++) v[i] = g_ws.stats[i];
+  for (int i = 0; i < 7; i++) v[4 + i] = g_ws.path[i];
+  const uint32_t k = n < 11 ? n : 11;
+  for (uint32_t i = 0; i < k; i++) out[i] = v[i];
+  return (int)k;
 }
 
 int zs_synchronize(void) {

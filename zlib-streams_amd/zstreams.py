@@ -64,6 +64,7 @@ _SIGS = {
     "zs_profile_stages": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.c_uint32]),
     "zs_kprof_read": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32, ctypes.c_int]),
     "zs_last_stats": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint32)]),
+    "zs_last_stats_ex": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32]),
     "zs_stream_stats": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64)]),
     "zs_synchronize": (ctypes.c_int, []),
     "zs_version": (ctypes.c_char_p, []), "zs_last_error": (ctypes.c_char_p, []),
@@ -132,14 +133,16 @@ def _check(rc):
 
 
 PARSE_FLAGS = {None: 0, "lane": 8, "wave": 16}  # ZS_F_PARSE_LANE / ZS_F_PARSE_WAVE
+LINK_FLAGS = {None: 0, "serial": 32}  # ZS_F_LINK_SERIAL
 
 
-def inflate_batch(streams, window_bits=-15, out_caps=None, parse=None):
+def inflate_batch(streams, window_bits=-15, out_caps=None, parse=None, link=None):
     """Inflate many whole streams on the GPU (host buffers).
 
     Each stream behaves like inflateInit2(window_bits) + one inflate(Z_FINISH)
     into an out_cap-byte buffer.  Returns [(bytes, result_dict)].  parse =
-    "lane" / "wave" forces the block-parallel path's parse mode (same results).
+    "lane" / "wave" forces the block-parallel path's parse mode, link = "serial"
+    its per-stream window link (same results).
     """
     n = len(streams)
     if out_caps is None:
@@ -158,7 +161,7 @@ def inflate_batch(streams, window_bits=-15, out_caps=None, parse=None):
         jobs[i].out = ctypes.cast(ob, ctypes.c_void_p).value
         jobs[i].out_cap = out_caps[i]
         jobs[i].window_bits = wbs[i]
-    _check(lib().zs_inflate_batch(jobs, n, res, PARSE_FLAGS[parse]))
+    _check(lib().zs_inflate_batch(jobs, n, res, PARSE_FLAGS[parse] | LINK_FLAGS[link]))
     return [(outbufs[i].raw[:res[i].total_out], res[i].as_dict()) for i in range(n)]
 
 
@@ -379,9 +382,15 @@ def last_stats():
     """Last batch: jobs on the chunked path, decode units planned for them, chunked
     jobs whose chain did not verify (decoded by the serial decoder instead), and
     jobs routed to the serial decoder directly."""
-    a = (ctypes.c_uint32 * 4)()
-    _check(lib().zs_last_stats(a))
-    return {"chunked_jobs": a[0], "units": a[1], "fallback_jobs": a[2], "serial_jobs": a[3]}
+    a = (ctypes.c_uint32 * 11)()
+    k = lib().zs_last_stats_ex(a, 11)
+    if k < 0:
+        _check(k)
+    mode = {0: "lane", 1: "wave"}
+    return {"chunked_jobs": a[0], "units": a[1], "fallback_jobs": a[2], "serial_jobs": a[3],
+            "parse": mode.get(a[4]), "link": None if a[4] > 1 else ("serial" if a[5] == 0 else "prefix"),
+            "parse_d64": mode.get(a[6]), "link_d64": None if a[6] > 1 else ("serial" if a[7] == 0 else "prefix"),
+            "lane_resident_waves": a[8], "units_std": a[9], "units_d64": a[10]}
 
 
 def stream_stats():
