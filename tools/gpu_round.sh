@@ -17,6 +17,6 @@ t1=$SECONDS
 echo "bench rc=$rc wall_s=$((t1 - t0))" | tee $O/bench_wall.txt; cat $O/bench.json
 [ $rc -eq 0 ] || exit $rc
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $O/bench_rocprof.json 2> $O/bench_rocprof.err; rc=$?
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $O/bench_rocprof.json 2> $O/bench_rocprof.err; rc=$?
 echo "rocprof rc=$rc"
 exit $rc
