@@ -55,3 +55,34 @@ def oneshot(data, wbits, cap=None):
             "total_out": s.total_out, "adler": s.adler & 0xffffffff}
     z.inflateEnd(ctypes.byref(s))
     return ob.raw[:info["total_out"]], info
+
+
+class Deflater:
+    """Host zlib deflate driven call by call: deflateInit2_(level, 8, wbits, 8, 0),
+    then deflate(strm, flush) with a given input and output space -- zlib's own
+    per-call (ret, consumed, produced) for the reference's deflate (SURVEY §8c
+    pins host zlib's bytes to the shipped deflate)."""
+
+    def __init__(self, level, wbits):
+        z = self.z = libz()
+        z.deflateInit2_.argtypes = [ctypes.POINTER(ZStream), ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                    ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+        z.deflate.argtypes = [ctypes.POINTER(ZStream), ctypes.c_int]
+        z.deflateEnd.argtypes = [ctypes.POINTER(ZStream)]
+        self.s = ZStream()
+        self.rc = z.deflateInit2_(ctypes.byref(self.s), level, 8, wbits, 8, 0, z.zlibVersion(), ctypes.sizeof(ZStream))
+
+    def call(self, data, out_len, flush):
+        ib = ctypes.create_string_buffer(bytes(data), max(len(data), 1))
+        ob = ctypes.create_string_buffer(max(out_len, 1))
+        s = self.s
+        s.next_in = ctypes.cast(ib, ctypes.c_void_p) if data else None
+        s.avail_in = len(data)
+        s.next_out = ctypes.cast(ob, ctypes.c_void_p)
+        s.avail_out = out_len
+        r = self.z.deflate(ctypes.byref(s), flush)
+        prod = out_len - s.avail_out
+        return r, len(data) - s.avail_in, ob.raw[:prod]
+
+    def end(self):
+        return self.z.deflateEnd(ctypes.byref(self.s))

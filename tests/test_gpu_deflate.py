@@ -295,6 +295,18 @@ class _GpuDeflate:
             if ret != 0 or s.avail_out != 0:
                 return bytes(out), ret
 
+    def call1(self, data, out_len, flush):
+        """Exactly one deflate() call: (ret, consumed, produced bytes)."""
+        ib = ctypes.create_string_buffer(data, max(len(data), 1))
+        ob = ctypes.create_string_buffer(max(out_len, 1))
+        s = self.s
+        s.next_in = ctypes.cast(ib, ctypes.c_void_p) if data else None
+        s.avail_in = len(data)
+        s.next_out = ctypes.cast(ob, ctypes.c_void_p)
+        s.avail_out = out_len
+        ret = self.L.deflate(ctypes.byref(s), flush)
+        return ret, len(data) - s.avail_in, ob.raw[:out_len - s.avail_out]
+
     def end(self):
         return self.L.deflateEnd(ctypes.byref(self.s))
 
@@ -353,14 +365,15 @@ def test_deflate_sync_flush_is_zlibs(zs):
             assert g.end() == 0
 
 
-def test_deflate_stream_buffer_bound(zs, monkeypatch):
-    """Past ZS_DSTREAM_MAX_KB of accumulated input a stream emits a segment
-    (sync-flush ending) without waiting for a flush: output arrives while the
-    input does, and the stream still decodes to the input."""
+def test_deflate_stream_buffer_bound_fast_levels(zs, monkeypatch):
+    """Levels 0..3 (the GPU throughput encoder): past ZS_DSTREAM_MAX_KB of
+    gathered input a stream sends its blocks without waiting for a flush (a
+    non-final block end, no injected flush marker), and still decodes to the
+    input."""
     monkeypatch.setenv("ZS_DSTREAM_MAX_KB", "256")
     data = corpus.stream(16, 2 << 20)
     for wb in (-15, 31):
-        g = _GpuDeflate(zs, 6, wb)
+        g = _GpuDeflate(zs, 1, wb)
         out, early = bytearray(), 0
         for off in range(0, len(data), 65536):
             o, ret = g.call(data[off:off + 65536], 0)
@@ -374,30 +387,134 @@ def test_deflate_stream_buffer_bound(zs, monkeypatch):
         assert zlib.decompress(bytes(out), wb) == data
 
 
-def test_deflate_fixup_in_order_pass(zs, monkeypatch):
-    """ZS_ZD_ROUNDS=0 skips the parallel cross-region fix-up rounds, so every
-    job's regions are settled by the in-order pass (zs_zd_fix_seq_kernel):
-    zlib's bytes at every deflate_slow level on text, periodic runs (whose
-    parse offsets never line up across 64 KiB regions) and mixed inputs."""
-    monkeypatch.setenv("ZS_ZD_ROUNDS", "0")
-    rng = random.Random(21)
-    pats = _patterns(rng)
-    per = bytes(rng.getrandbits(8) for _ in range(1000)) * 1200  # period 1000, 1.2 MB
-    cases = [(d, wb, lv) for d in (pats["text"], pats["mixed"], bytes(1 << 20), per, b"ab" * 400000)
-             for wb, lv in ((-15, 4), (31, 6), (15, 9))]
-    got = zs.deflate_batch([c[0] for c in cases], [c[1] for c in cases], [c[2] for c in cases])
-    bad = [(i, len(d), wb, lv) for i, ((d, wb, lv), (comp, info)) in enumerate(zip(cases, got))
-           if comp != zlib_bytes(d, wb, lv) or info["ret"] != 1]
-    assert not bad, bad
+def _stream_data(rng, n):
+    """Text, line text, random bytes and zero runs, mixed."""
+    parts, k = [], 0
+    while sum(len(p) for p in parts) < n:
+        kind = rng.random()
+        m = rng.choice([3000, 40000, 200000])
+        if kind < 0.4:
+            parts.append(corpus.stream(rng.randrange(64), m))
+        elif kind < 0.6:
+            parts.append(bytes(rng.getrandbits(8) for _ in range(min(m, 20000))))
+        elif kind < 0.8:
+            parts.append(bytes(m))
+        else:
+            parts.append(corpus.stream(32 + k % 32, m))
+        k += 1
+    return b"".join(parts)[:n]
 
 
-def test_deflate_long_zero_run_is_zlibs(zs):
-    """300 MiB of zeros (> 4096 regions of 64 KiB: the cascade a bounded number
-    of parallel rounds cannot settle) and a 300 MiB periodic run, levels 4 and 9:
-    zlib's bytes."""
-    zeros = bytes(300 << 20)
-    per = (bytes(random.Random(5).getrandbits(8) for _ in range(777)) * ((300 << 20) // 777 + 1))[:300 << 20]
-    for data in (zeros, per):
-        for wb, lv in ((-15, 4), (31, 9)):
-            (comp, info), = zs.deflate_batch([data], wb, lv)
-            assert info["ret"] == 1 and comp == zlib_bytes(data, wb, lv), (len(data), wb, lv, len(comp))
+def _compare_calls(zs, level, wb, calls, out_len):
+    """Drive the library's deflate() and host zlib's with the same calls;
+    every call's (ret, consumed, produced bytes) must be equal."""
+    import libz_ref
+    g = _GpuDeflate(zs, level, wb)
+    h = libz_ref.Deflater(level, wb)
+    assert h.rc == 0
+    total = bytearray()
+    for i, (chunk, fl) in enumerate(calls):
+        a = g.call1(chunk, out_len, fl)
+        b = h.call(chunk, out_len, fl)
+        assert a == b, (level, wb, i, fl, len(chunk), a[:2], b[:2], len(a[2]), len(b[2]))
+        total += a[2]
+    assert g.s.adler == h.s.adler & 0xffffffff
+    assert g.end() == h.end()
+    return bytes(total)
+
+
+@pytest.mark.parametrize("level", [4, 5, 6, 7, 8, 9])
+def test_deflate_stream_calls_are_zlibs(zs, level):
+    """zlib's deflate() call by call (reference: src/wasm/deflate_stream_wasm.c:51-55
+    runs one deflate per process call): random input sizes and every flush value
+    -- Z_NO_FLUSH (blocks sent as zlib completes them, nothing injected),
+    Z_PARTIAL_FLUSH, Z_SYNC_FLUSH, Z_FULL_FLUSH, Z_BLOCK (the window carried
+    across all but Z_FULL_FLUSH, bits continuing across unaligned ends) -- then
+    Z_FINISH and its drain: each call's ret, consumed and produced bytes equal
+    host zlib's, for raw, zlib and gzip streams."""
+    rng = random.Random(100 + level)
+    for wb in (-15, 15, 31):
+        data = _stream_data(rng, 1_500_000)
+        calls, off = [], 0
+        while off < len(data):
+            n = rng.choice([1, 700, 5000, 33000, 70000, 250000])
+            fl = rng.choice([0, 0, 0, 0, 1, 2, 3, 5])
+            calls.append((data[off:off + n], fl))
+            off += n
+        calls.append((b"", rng.choice([0, 2])))  # nothing to do: Z_BUF_ERROR
+        calls += [(b"", 4)] * 3
+        out = _compare_calls(zs, level, wb, calls, 1 << 21)
+        assert zlib.decompress(out, wb) == data
+
+
+def test_deflate_stream_long_no_flush_is_zlibs(zs):
+    """A 64 MiB stream fed in 1 MiB Z_NO_FLUSH calls, then Z_FINISH drained in
+    64 KiB pieces: every call equals host zlib's (blocks sent as they complete,
+    never a flush the caller did not ask for)."""
+    data = corpus.stream(3, 32 << 20) + corpus.stream(40, 32 << 20)
+    calls = [(data[o:o + (1 << 20)], 0) for o in range(0, len(data), 1 << 20)]
+    calls += [(b"", 4)] * 400
+    for level, wb in ((6, 31), (9, -15)):
+        out = _compare_calls(zs, level, wb, calls, 1 << 22)
+        assert zlib.decompress(out, wb) == data
+
+
+def test_compression_stream_js_schedule_calls_are_zlibs(zs):
+    """The reference's CompressionStreamZlib schedule (zlib-streams.js:64-156: 64 KiB
+    writes, <= 32 KiB per deflate_process, 64 KiB out, Z_FINISH drain) through the
+    handle ABI: every call's packed return and last_consumed equal what host
+    zlib's deflate returns for the same call."""
+    import libz_ref
+    L = zs.lib()
+    data = corpus.stream(41, 1_200_000) + bytes(100000) + corpus.stream(5, 300000)
+    for fmt, wb, init in (("deflate-raw", -15, L.deflate_init_raw), ("gzip", 31, L.deflate_init_gzip),
+                          ("deflate", 15, L.deflate_init)):
+        for level in (4, 6, 9):
+            h = L.deflate_new()
+            assert init(h, level) == 0
+            ref = libz_ref.Deflater(level, wb)
+            ob = ctypes.create_string_buffer(65536)
+            got, exp = bytearray(), bytearray()
+            for w in range(0, len(data), 65536):
+                chunk = data[w:w + 65536]
+                off = 0
+                while off < len(chunk):
+                    piece = chunk[off:off + 32768]
+                    ib = ctypes.create_string_buffer(piece, len(piece))
+                    r = L.deflate_process(h, ctypes.addressof(ib), len(piece), ctypes.addressof(ob), 65536, 0)
+                    rr, cons, prod = ref.call(piece, 65536, 0)
+                    assert (r >> 24, r & 0xffffff, L.deflate_last_consumed(h)) == (rr & 0xff, len(prod), cons), (fmt, level, w)
+                    got += ob.raw[:r & 0xffffff]
+                    exp += prod
+                    if cons == 0:
+                        break
+                    off += cons
+            while True:
+                r = L.deflate_process(h, 0, 0, ctypes.addressof(ob), 65536, 4)
+                rr, cons, prod = ref.call(b"", 65536, 4)
+                assert (r >> 24, r & 0xffffff) == (rr & 0xff, len(prod)), (fmt, level)
+                got += ob.raw[:r & 0xffffff]
+                exp += prod
+                if (r >> 24) == 1 or (r & 0xffffff) == 0:
+                    break
+            assert got == exp and zlib.decompress(bytes(got), wb) == data
+            assert L.deflate_end(h) == ref.end() == 0
+
+
+def test_deflate_init_rejects_unimplemented_parameters(zs):
+    """memLevel != 8 and strategies other than Z_DEFAULT_STRATEGY would change
+    zlib's bytes: deflateInit2_ refuses them (Z_STREAM_ERROR) instead of
+    silently writing default-parameter bytes; an unfinished stream ends with
+    Z_DATA_ERROR as zlib's deflateEnd says."""
+    import libz_ref
+    Z = libz_ref.ZStream
+    L = ctypes.CDLL(zs.LIB_PATH)
+    L.deflateInit2_.argtypes = [ctypes.POINTER(Z), ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+    L.deflateEnd.argtypes = [ctypes.POINTER(Z)]
+    for mem, strat in ((9, 0), (1, 0), (8, 1), (8, 2), (8, 3), (8, 4)):
+        s = Z()
+        assert L.deflateInit2_(ctypes.byref(s), 6, 8, 15, mem, strat, b"1.2.11", ctypes.sizeof(Z)) == -2, (mem, strat)
+    g = _GpuDeflate(zs, 6, 31)
+    g.call1(b"abc" * 1000, 1 << 16, 0)
+    assert g.end() == -3  # Z_DATA_ERROR: stream freed before Z_FINISH

@@ -982,16 +982,22 @@ __global__ void __launch_bounds__(DZ_T) zs_dz_check_kernel(ZsDJobDev *__restrict
   const uint32_t t = threadIdx.x;
   const ZsDSegDev sg = segs[blockIdx.x];
   const ZsDJobDev jb = jobs[sg.job];
-  if (jb.wrap == 0 || sg.len == 0) return;
-  if ((reinterpret_cast<uintptr_t>(jb.in + sg.start) & 15u) == 0) {  // coalesced 4 KiB steps (zs_check.h)
+  // the check covers in[ck0, in_len): the bytes before ck0 are history the
+  // check of an earlier segment of the stream already took
+  const uint8_t *in = jb.in + jb.ck0;
+  const uint64_t n = jb.in_len - jb.ck0;
+  const uint64_t s_lo = max(sg.start, jb.ck0) - jb.ck0, s_hi = sg.start + sg.len;
+  if (jb.wrap == 0 || s_hi <= jb.ck0) return;
+  const uint64_t s_len = s_hi - jb.ck0 - s_lo;
+  if ((reinterpret_cast<uintptr_t>(in + s_lo) & 15u) == 0) {  // coalesced 4 KiB steps (zs_check.h)
     static_assert(DZ_T == ZS_CK_T, "zs_check.h block checks run 256 threads");
     zs_ck_tables(s_ck);
     if (jb.wrap == 2) {
-      const uint32_t v = zs_crc_block(jb.in, sg.start, sg.start + sg.len, jb.in_len, s_ck, reinterpret_cast<uint32_t *>(s_red));
+      const uint32_t v = zs_crc_block(in, s_lo, s_lo + s_len, n, s_ck, reinterpret_cast<uint32_t *>(s_red));
       if (t == 0 && v) atomicXor(reinterpret_cast<unsigned long long *>(&jobs[sg.job].ck_a), (unsigned long long)v);
     } else {
       uint64_t sa, sb;
-      zs_adler_block(jb.in, sg.start, sg.start + sg.len, jb.in_len, s_red, &sa, &sb);
+      zs_adler_block(in, s_lo, s_lo + s_len, n, s_red, &sa, &sb);
       if (t == 0) {
         atomicAdd(reinterpret_cast<unsigned long long *>(&jobs[sg.job].ck_a), (unsigned long long)sa);
         atomicAdd(reinterpret_cast<unsigned long long *>(&jobs[sg.job].ck_b), (unsigned long long)sb);
@@ -999,15 +1005,15 @@ __global__ void __launch_bounds__(DZ_T) zs_dz_check_kernel(ZsDJobDev *__restrict
     }
     return;
   }
-  const uint32_t per = ((sg.len + DZ_T - 1) / DZ_T + 3u) & ~3u;
-  const uint64_t lo = sg.start + min(sg.len, per * t), hi = sg.start + min(sg.len, per * (t + 1));
+  const uint64_t per = ((s_len + DZ_T - 1) / DZ_T + 3u) & ~3ull;
+  const uint64_t lo = s_lo + min(s_len, per * t), hi = s_lo + min(s_len, per * (t + 1));
   if (jb.wrap == 2) {
     zs_crc_tables(s_tab);
-    const uint32_t v = zs_block_xor(zs_crc_piece(jb.in, lo, hi, jb.in_len, s_tab), reinterpret_cast<uint32_t *>(s_red));
+    const uint32_t v = zs_block_xor(zs_crc_piece(in, lo, hi, n, s_tab), reinterpret_cast<uint32_t *>(s_red));
     if (t == 0 && v) atomicXor(reinterpret_cast<unsigned long long *>(&jobs[sg.job].ck_a), (unsigned long long)v);
   } else {
     uint32_t A = 0, B = 0;
-    if (hi > lo) zs_adler_piece(jb.in, lo, hi, jb.in_len, &A, &B);
+    if (hi > lo) zs_adler_piece(in, lo, hi, n, &A, &B);
     const uint64_t sa = zs_block_sum(A, s_red);
     const uint64_t sb = zs_block_sum(B, s_red);
     if (t == 0) {
@@ -1026,7 +1032,7 @@ __global__ void __launch_bounds__(DZ_JT) zs_dz_offsets_kernel(ZsDJobDev *__restr
   const uint32_t t = threadIdx.x;
   ZsDJobDev jb = jobs[blockIdx.x];
   if (jb.exact) return;  // zs_zd_layout_kernel
-  const uint32_t hdr = jb.wrap == 2 ? 10u : (jb.wrap == 1 ? 2u : 0u);
+  const uint32_t hdr = !jb.hdr ? 0u : jb.wrap == 2 ? 10u : (jb.wrap == 1 ? 2u : 0u);
   // segment k of the job: jb.seg0 + k; per-thread contiguous ranges
   const uint32_t ns = jb.nseg;
   const uint32_t per = (ns + DZ_JT - 1) / DZ_JT;
@@ -1036,16 +1042,14 @@ __global__ void __launch_bounds__(DZ_JT) zs_dz_offsets_kernel(ZsDJobDev *__restr
   s_sum[t] = sum;
   __syncthreads();
   if (t == 0) {  // small serial exclusive scan over 1024 partial sums
-    uint64_t acc = 8ull * hdr;
+    uint64_t acc = jb.bit0 + 8ull * hdr;
     for (uint32_t k = 0; k < DZ_JT; k++) {
       const uint64_t x = s_sum[k];
       s_sum[k] = acc;
       acc += x;
     }
-    // (sync: 3 header bits of the empty stored block, padding, 00 00 FF FF)
-    const uint64_t body_bytes = (acc + (jb.sync ? 3u : 0u) + 7) / 8;
-    const uint32_t tr = jb.sync ? 4u : (jb.wrap == 2 ? 8u : (jb.wrap == 1 ? 4u : 0u));
-    jobs[blockIdx.x].total_out = body_bytes + tr;
+    jobs[blockIdx.x].endbit = acc;
+    jobs[blockIdx.x].total_out = zs_dz_total_bytes(jb, acc);
   }
   __syncthreads();
   uint64_t off = s_sum[t];
@@ -1054,10 +1058,10 @@ __global__ void __launch_bounds__(DZ_JT) zs_dz_offsets_kernel(ZsDJobDev *__restr
     off += segs[jb.seg0 + k].nbits;
   }
   if (t == 0)
-    jobs[blockIdx.x].check = jb.wrap == 2   ? zs_crc_final((uint32_t)jb.ck_a, jb.in_len)
-                             : jb.wrap == 1 ? zs_adler_final(jb.ck_a, jb.ck_b, jb.in_len)
+    jobs[blockIdx.x].check = jb.wrap == 2   ? zs_crc_final((uint32_t)jb.ck_a, jb.in_len - jb.ck0)
+                             : jb.wrap == 1 ? zs_adler_final(jb.ck_a, jb.ck_b, jb.in_len - jb.ck0)
                                             : 0u;
-  if (t == 0) {
+  if (t == 0 && hdr) {
     uint8_t *o = stage + jb.stage;
     if (jb.wrap == 2) {  // gzip header as zlib writes it with no options (mtime 0, OS 3)
       const uint8_t gz[10] = {0x1f, 0x8b, 8, 0, 0, 0, 0, 0, (uint8_t)(jb.level == 9 ? 2 : (jb.level < 2 ? 4 : 0)), 3};
@@ -1112,7 +1116,7 @@ __global__ void zs_dz_trailer_kernel(const ZsDJobDev *__restrict__ jobs, uint32_
   const ZsDJobDev jb = jobs[j];
   if (jb.exact != exact) return;
   uint8_t *o = stage + jb.stage;
-  if (jb.sync) {  // the empty stored block's LEN / NLEN (its header bits and padding are zero)
+  if (jb.term == ZS_DT_SYNC) {  // the empty stored block's LEN / NLEN (its header bits and padding are zero)
     uint8_t *p = o + jb.total_out - 4;
     p[0] = 0;
     p[1] = 0;
@@ -1120,10 +1124,16 @@ __global__ void zs_dz_trailer_kernel(const ZsDJobDev *__restrict__ jobs, uint32_
     p[3] = 0xff;
     return;
   }
+  if (jb.term == ZS_DT_PARTIAL) {  // trees.c _tr_align: BFINAL 0, BTYPE 01, static END_BLOCK (7 zero bits)
+    const uint64_t b = jb.endbit + 1;
+    o[b >> 3] |= (uint8_t)(1u << (b & 7u));
+    return;
+  }
+  if (jb.term != ZS_DT_FINAL || !jb.trl) return;
   const uint64_t tr = jb.wrap == 2 ? 8u : (jb.wrap == 1 ? 4u : 0u);
   uint8_t *p = o + jb.total_out - tr;
   if (jb.wrap == 2) {
-    const uint32_t c = jb.check, n = (uint32_t)jb.in_len;
+    const uint32_t c = jb.check, n = (uint32_t)(jb.in_len - jb.ck0);
     p[0] = (uint8_t)c;
     p[1] = (uint8_t)(c >> 8);
     p[2] = (uint8_t)(c >> 16);

@@ -361,11 +361,13 @@ __device__ __forceinline__ ZdBm zd_bm(uint32_t *bm, const ZsDJobDev &jb) {
 // emits there, whose table is the state's variant bit.  A walk records
 // pending positions from its second loop top on, and the one pending when it
 // leaves (then q == hi): so each walk writes only positions in [lo, hi).
+// (rec_first: also the literal pending at the first loop top -- a job's parse
+// entry, whose pending literal no earlier walk of the job records)
 template <typename SetF>
 __device__ __forceinline__ void zd_walk_record(const ZdTabs &T, uint64_t &q, uint32_t &qs, uint64_t hi, SetF set,
-                                               uint32_t *marks, uint64_t mark0) {
+                                               uint32_t *marks, uint64_t mark0, bool rec_first = false) {
   uint32_t var;
-  bool first = true;
+  bool first = !rec_first;
   while (q < hi) {
     if (marks && qs == ZD_STATE_A) zd_setbit(marks, q - mark0);
     if ((qs & 1u) && !first) set(q - 1, (qs >> 10) & 1u);
@@ -394,13 +396,20 @@ __global__ void __launch_bounds__(ZD_PT) zs_zd_parse_kernel(const ZsDJobDev *__r
   T.lazy = zd_cfg[jb.level][1];
   const uint64_t r0 = sg.start, rend = sg.start + sg.len;
   const uint64_t a = r0 + (uint64_t)t * 256u, b = min(rend, a + 256u);
-  const bool act = a < rend;
+  // the job's parse entry (pstart, pstate) lies in its first region (the
+  // history before it is at most one window); pieces before it hold no tokens
+  // and the piece holding it starts there, in that state
+  const bool has_ent = r0 == 0 && jb.pstart < rend;
+  const uint32_t ent_t = has_ent ? (uint32_t)(jb.pstart / 256u) : 0u;
+  const uint64_t ent_p = has_ent ? jb.pstart : r0;
+  const uint32_t ent_s = has_ent ? jb.pstate : ZD_STATE_A;
+  const bool act = a < rend && t >= ent_t && (r0 != 0 || jb.pstart < rend);
   for (uint32_t i = t; i < ZD_REG / 32; i += ZD_PT) s_S[i] = s_V[i] = s_M[i] = 0;
   __syncthreads();
   uint32_t var;
   // speculative walk of the piece from (a, A): marks its state-A positions
-  uint64_t p = a;
-  uint32_t st = ZD_STATE_A;
+  uint64_t p = t == ent_t ? ent_p : a;
+  uint32_t st = t == ent_t ? ent_s : ZD_STATE_A;
   while (act && p < b) {
     if (st == ZD_STATE_A) zd_setbit(s_M, p - r0);
     (void)zd_step(T, p, st, &var);
@@ -411,8 +420,8 @@ __global__ void __launch_bounds__(ZD_PT) zs_zd_parse_kernel(const ZsDJobDev *__r
   s_xs[t] = spec_s;
   __syncthreads();
   for (;;) {  // re-walk from the predecessor's exit until meeting a marked state-A position
-    uint64_t q = t == 0 ? r0 : s_xp[t - 1];
-    uint32_t qs = t == 0 ? ZD_STATE_A : s_xs[t - 1];
+    uint64_t q = t == ent_t ? ent_p : s_xp[t - 1];
+    uint32_t qs = t == ent_t ? ent_s : s_xs[t - 1];
     uint64_t rp = s_xp[t];
     uint32_t rs = s_xs[t];
     if (act) {
@@ -439,15 +448,15 @@ __global__ void __launch_bounds__(ZD_PT) zs_zd_parse_kernel(const ZsDJobDev *__r
   for (uint32_t i = t * 8; i < t * 8 + 8; i++) s_M[i] = 0;  // own words (256 positions)
   __syncthreads();
   if (act) {
-    uint64_t q = t == 0 ? r0 : s_xp[t - 1];
-    uint32_t qs = t == 0 ? ZD_STATE_A : s_xs[t - 1];
+    uint64_t q = t == ent_t ? ent_p : s_xp[t - 1];
+    uint32_t qs = t == ent_t ? ent_s : s_xs[t - 1];
     zd_walk_record(
         T, q, qs, b,
         [&](uint64_t x, uint32_t v) {
           zd_setbit(s_S, x - r0);
           zd_putbit(s_V, x - r0, v != 0);
         },
-        s_M, r0);
+        s_M, r0, has_ent && t == ent_t);
   }
   __syncthreads();
   ZdBm Bm = zd_bm(bm, jb);
@@ -668,12 +677,14 @@ __global__ void __launch_bounds__(1024) zs_zd_blocks_kernel(ZsDJobDev *__restric
     }
     const uint32_t *S = bm + jb.bm0;
     const uint64_t L = jb.in_len;
-    const bool end_lit = acc && zd_getbit(S, L - 1);
-    const uint64_t nfull = acc / ZD_BLOCK;
-    const bool empty_last = acc % ZD_BLOCK == 0 && !end_lit;
-    // Z_FINISH flushes an empty last block; Z_SYNC_FLUSH only a non-empty one
-    // (deflate.c deflate_slow: `if (s->sym_next) FLUSH_BLOCK(s, 0)`)
-    jobs[blockIdx.x].nzblk = (uint32_t)(empty_last ? nfull + (jb.sync ? 0u : 1u) : (acc + ZD_BLOCK - 1) / ZD_BLOCK);
+    const uint64_t eff = acc - min(acc, jb.skip);  // symbols of this job's blocks
+    const bool end_lit = eff && zd_getbit(S, L - 1);
+    const uint64_t nfull = eff / ZD_BLOCK;
+    const bool empty_last = eff % ZD_BLOCK == 0 && !end_lit;
+    // Z_FINISH flushes an empty last block; a flush mid-stream only a
+    // non-empty one (deflate.c deflate_slow: `if (s->sym_next) FLUSH_BLOCK(s, 0)`)
+    jobs[blockIdx.x].nzblk =
+        (uint32_t)(empty_last ? nfull + (jb.term == ZS_DT_FINAL ? 1u : 0u) : (eff + ZD_BLOCK - 1) / ZD_BLOCK);
     s_sum[1023] = s_sum[1023];  // keep the scan in LDS
   }
   __syncthreads();
@@ -704,24 +715,85 @@ __global__ void zs_zd_blist_kernel(const ZsDJobDev *__restrict__ jobs, uint32_t 
   const uint64_t L = jb.in_len;
   const ZsDSegDev &lastseg = segs[jb.seg0 + jb.nseg - 1];
   const uint64_t ns = lastseg.sym0 + lastseg.nsym;
-  const uint64_t s0 = (uint64_t)k * ZD_BLOCK;
+  const uint64_t s0 = jb.skip + (uint64_t)k * ZD_BLOCK;
   const uint64_t s1 = min(ns, s0 + ZD_BLOCK);
   const bool final_blk = k + 1 == jb.nzblk;
-  b.last = final_blk && !jb.sync;
+  b.last = final_blk && jb.term == ZS_DT_FINAL;
   b.nsym = (uint32_t)(s1 > s0 ? s1 - s0 : 0);
   b.first = b.nsym ? zd_sym_pos(segs, jb, S, s0) : L;
   b.end = s1 < ns ? zd_sym_pos(segs, jb, S, s1) : L;
   // the flush runs in the iteration whose loop top followed the block's last
-  // symbol start; the final block flushes after the loop (top = L)
+  // symbol start; the last block of a flushed job flushes after the loop (top = L)
   uint64_t top = L;
-  if (!final_blk) {
+  if (b.nsym && (!final_blk || jb.term == ZS_DT_CUT)) {
     uint64_t x = b.end - 1;
     while (!zd_getbit(S, x)) x--;
     top = x + 1;
   }
+  b.top = top;
+  // window slides counted in stream positions since zlib's window last restarted
   const uint64_t wsize = 1ull << jb.wbits;
-  b.stored_ok = b.first >= zd_slides(top, L, wsize, wsize - ZD_LOOK) * wsize;
+  b.stored_ok = jb.abs0 + b.first >= zd_slides(jb.abs0 + top, jb.abs0 + L, wsize, wsize - ZD_LOOK) * wsize;
   blks[i] = b;
+}
+
+// symbols whose start lies in [0, y) (regions' symbol prefix, then the start
+// bitmap of y's region)
+__device__ uint64_t zd_syms_before(const ZsDSegDev *segs, const ZsDJobDev &jb, const uint32_t *S, uint64_t y) {
+  if (y >= jb.in_len) {
+    const ZsDSegDev &l = segs[jb.seg0 + jb.nseg - 1];
+    return l.sym0 + l.nsym;
+  }
+  const ZsDSegDev &sg = segs[jb.seg0 + (uint32_t)(y / ZD_REG)];
+  uint64_t c = sg.sym0;
+  uint64_t w = sg.start / 32u;
+  for (; (w + 1) * 32u <= y; w++) c += (uint64_t)__builtin_popcount(S[w]);
+  if (y & 31u) c += (uint64_t)__builtin_popcount(S[w] & ((1u << (y & 31u)) - 1u));
+  return c;
+}
+
+// ZS_DT_CUT jobs (Z_NO_FLUSH calls of a stream), one thread per job: zlib
+// processes loop tops t while the lookahead in_len - t >= MIN_LOOKAHEAD, so
+// the blocks it completes are the leading full blocks whose flush loop top
+// is <= in_len - 262; only those are emitted.  The next segment restarts at
+// the last region exit at or before the first unsent symbol whose walk saw
+// full lookahead (an exact loop top and state, from the fix-up), with the
+// symbols from there to the first unsent one as its skip; with none, at this
+// job's own entry.
+__global__ void zs_zd_cut_kernel(ZsDJobDev *__restrict__ jobs, uint32_t njobs, const ZsDSegDev *__restrict__ segs,
+                                 const uint32_t *__restrict__ bm, ZsZBlkDev *__restrict__ blks) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= njobs) return;
+  const ZsDJobDev jb = jobs[j];
+  if (!jb.exact || jb.term != ZS_DT_CUT) return;
+  const uint32_t *S = bm + jb.bm0;
+  const uint64_t L = jb.in_len;
+  uint32_t K = 0;
+  while (K < jb.nzblk && blks[jb.zblk0 + K].nsym == ZD_BLOCK && blks[jb.zblk0 + K].top + ZD_LOOK <= L) K++;
+  uint64_t T = jb.pstart, sT = jb.pstate, skip = jb.skip + (uint64_t)K * ZD_BLOCK;
+  if (K < jb.nzblk) {
+    const uint64_t P0 = blks[jb.zblk0 + K].first;
+    for (int32_t r = (int32_t)min<uint64_t>(jb.nseg - 1, P0 / ZD_REG); r >= 0; r--) {
+      const ZsDSegDev &sg = segs[jb.seg0 + r];
+      const uint64_t x = sg.zx[0];
+      const uint32_t xs = sg.zs[0];
+      if (sg.start + sg.len + ZD_LOOK + ZD_MAXM <= L && x - (xs & 1u) <= P0 && x >= jb.pstart) {
+        T = x;
+        sT = xs;
+        skip = jb.skip + (uint64_t)K * ZD_BLOCK - zd_syms_before(segs, jb, S, x - (xs & 1u));
+        break;
+      }
+    }
+  }
+  // symbols zlib has tallied by its last loop top (a token at x is tallied at x + 1)
+  const uint64_t done = L >= ZD_LOOK ? zd_syms_before(segs, jb, S, L - ZD_LOOK) : 0;
+  const uint64_t sent = jb.skip + (uint64_t)K * ZD_BLOCK;
+  for (uint32_t k = K; k < jb.nzblk; k++) blks[jb.zblk0 + k].nsym = 0xffffffffu;  // not sent by this call
+  jobs[j].cut_open = done > sent ? done - sent : 0;
+  jobs[j].nzblk = K;
+  jobs[j].cut_pos = T;
+  jobs[j].cut_state = (uint32_t)sT;
+  jobs[j].cut_skip = skip;
 }
 
 // ---------------------------------------------------------------------------
@@ -1076,7 +1148,7 @@ __global__ void __launch_bounds__(1024) zs_zd_layout_kernel(ZsDJobDev *__restric
   if (!jb.exact) return;
   const uint32_t nb = jb.nzblk, per = (nb + 1023) / 1024;
   const uint32_t k0 = min(nb, per * t), k1 = min(nb, per * (t + 1));
-  const uint32_t hdr = jb.wrap == 2 ? 10u : (jb.wrap == 1 ? 2u : 0u);
+  const uint32_t hdr = !jb.hdr ? 0u : jb.wrap == 2 ? 10u : (jb.wrap == 1 ? 2u : 0u);
   if (t == 0) s_stored = 0;
   __syncthreads();
   uint64_t sum = 0;
@@ -1092,14 +1164,14 @@ __global__ void __launch_bounds__(1024) zs_zd_layout_kernel(ZsDJobDev *__restric
   uint64_t endbit = 0;
   if (!s_stored) {
     if (t == 0) {
-      uint64_t acc = 8ull * hdr;
+      uint64_t acc = jb.bit0 + 8ull * hdr;
       for (uint32_t k = 0; k < 1024; k++) {
         const uint64_t x = s_sum[k];
         s_sum[k] = acc;
         acc += x;
       }
-      s_sum[0] = s_sum[0];
-      jobs[blockIdx.x].total_out = jb.sync ? (acc + 3 + 7) / 8 + 4u : (acc + 7) / 8 + (jb.wrap == 2 ? 8u : (jb.wrap == 1 ? 4u : 0u));
+      jobs[blockIdx.x].endbit = acc;
+      jobs[blockIdx.x].total_out = zs_dz_total_bytes(jb, acc);
     }
     __syncthreads();
     uint64_t off = s_sum[t];
@@ -1108,7 +1180,7 @@ __global__ void __launch_bounds__(1024) zs_zd_layout_kernel(ZsDJobDev *__restric
       off += 3 + blks[jb.zblk0 + k].bits;
     }
   } else if (t == 0) {
-    uint64_t off = 8ull * hdr;
+    uint64_t off = jb.bit0 + 8ull * hdr;
     for (uint32_t k = 0; k < nb; k++) {
       ZsZBlkDev &b = blks[jb.zblk0 + k];
       b.bitoff = off;
@@ -1117,13 +1189,15 @@ __global__ void __launch_bounds__(1024) zs_zd_layout_kernel(ZsDJobDev *__restric
       off += b.bits;
     }
     endbit = off;
-    jobs[blockIdx.x].total_out =
-        jb.sync ? (endbit + 3 + 7) / 8 + 4u : (endbit + 7) / 8 + (jb.wrap == 2 ? 8u : (jb.wrap == 1 ? 4u : 0u));
+    jobs[blockIdx.x].endbit = endbit;
+    jobs[blockIdx.x].total_out = zs_dz_total_bytes(jb, endbit);
   }
   if (t == 0) {
-    jobs[blockIdx.x].check = jb.wrap == 2   ? zs_crc_final((uint32_t)jb.ck_a, jb.in_len)
-                             : jb.wrap == 1 ? zs_adler_final(jb.ck_a, jb.ck_b, jb.in_len)
+    jobs[blockIdx.x].check = jb.wrap == 2   ? zs_crc_final((uint32_t)jb.ck_a, jb.in_len - jb.ck0)
+                             : jb.wrap == 1 ? zs_adler_final(jb.ck_a, jb.ck_b, jb.in_len - jb.ck0)
                                             : 0u;
+  }
+  if (t == 0 && hdr) {
     uint8_t *o = stage + jb.stage;
     if (jb.wrap == 2) {  // gzip header as zlib writes it with no options (mtime 0, OS 3)
       const uint8_t gz[10] = {0x1f, 0x8b, 8, 0, 0, 0, 0, 0, (uint8_t)(jb.level == 9 ? 2 : (jb.level < 2 ? 4 : 0)), 3};
@@ -1321,6 +1395,7 @@ extern "C" int zs_launch_zdeflate(ZsDJobDev *d_jobs, uint32_t njobs, ZsDSegDev *
   hipLaunchKernelGGL(zs_zd_blocks_kernel, dim3(njobs), dim3(1024), 0, st, d_jobs, d_segs, d_bm);
   hipLaunchKernelGGL(zs_zd_blist_kernel, dim3((nblk_slots + 255) / 256), dim3(256), 0, st, d_jobs, njobs, d_segs, d_bm,
                      d_blks, nblk_slots, d_slot_job);
+  hipLaunchKernelGGL(zs_zd_cut_kernel, dim3((njobs + 63) / 64), dim3(64), 0, st, d_jobs, njobs, d_segs, d_bm, d_blks);
   hipLaunchKernelGGL(zs_zd_tree_kernel, dim3(nblk_slots), dim3(ZD_TT), 0, st, d_jobs, d_blks, d_ma, d_mb, d_bm, d_aux);
   hipLaunchKernelGGL(zs_zd_layout_kernel, dim3(njobs), dim3(1024), 0, st, d_jobs, d_blks, d_stage);
   hipLaunchKernelGGL(zs_zd_emit_kernel, dim3(nblk_slots), dim3(ZD_TT), 0, st, d_jobs, d_blks, d_ma, d_mb, d_bm, d_aux,

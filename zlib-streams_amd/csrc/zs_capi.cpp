@@ -1260,6 +1260,7 @@ DzWorkspace g_dz;
 // zlib-identical deflate (deflate_zlib.hip): per position, per bitmap word,
 // per work item, per block
 constexpr uint64_t ZD_S1_HOST = 131072, ZD_S2_HOST = 8192, ZD_BLOCK_HOST = 16383, ZD_AUX_HOST = 352;
+constexpr uint32_t ZD_STATE_A_HOST = 2u << 1;  // deflate_slow state A (deflate_zlib.hip ZD_STATE_A)
 struct ZdWorkspace {
   size_t cap_pos = 0, cap_bm = 0, cap_w1 = 0, cap_w2 = 0, cap_blk = 0;
   uint16_t *d_prevd = nullptr;
@@ -1407,13 +1408,29 @@ int zd_run(uint32_t nv, size_t nseg, hipStream_t st) {
   return 0;
 }
 
-int deflate_batch_locked(const zs_djob *jobs, uint32_t n, zs_result *results, uint32_t flags) {
+// One deflate job as the kernels see it (the batch API's zs_djob + flags, or a
+// segment of a stream surface).
+struct DzSpec {
+  const void *in = nullptr;
+  uint64_t in_len = 0;
+  void *out = nullptr;     // nullptr: keep the bytes in the staging area (stream segments copy them out)
+  uint64_t out_cap = 0;
+  int32_t window_bits = -15;
+  int32_t level = 6;
+  bool fast = false;       // ZS_F_DEFLATE_FAST
+  uint32_t term = ZS_DT_FINAL, hdr = 1, trl = 1, bit0 = 0, pstate = ZD_STATE_A_HOST;
+  uint64_t pstart = 0, skip = 0, abs0 = 0, ck0 = 0;
+  // results
+  int ret = Z_STREAM_ERROR;
+  uint64_t total_out = 0, endbit = 0, stage = 0;
+  uint32_t check = 0;
+  uint64_t cut_pos = 0, cut_skip = 0, cut_open = 0;
+  uint32_t cut_state = 0;
+};
+
+int dz_run(DzSpec *sp, uint32_t n, bool dev) {
   int r = ws_init();
-  if (r) {
-    for (uint32_t i = 0; i < n; i++) fill_result(&results[i], Z_STREAM_ERROR, nullptr);
-    return r;
-  }
-  const bool dev = (flags & ZS_F_DEVICE) != 0;
+  if (r) return r;
   if (n > g_dz.cap_jobs) {
     const size_t c = std::max<size_t>(n, 2 * g_dz.cap_jobs);
     if ((r = grow_dev(&g_dz.d_jobs, c)) || (r = grow_host(&g_dz.h_jobs, c))) return r;
@@ -1424,37 +1441,49 @@ int deflate_batch_locked(const zs_djob *jobs, uint32_t n, zs_result *results, ui
   size_t nseg = 0, stage_total = 0, in_total = 0;
   uint32_t nv = 0;
   for (uint32_t i = 0; i < n; i++) {
+    DzSpec &s = sp[i];
     int wrap = 0;
     uint32_t w = 15;
-    int level = jobs[i].level == Z_DEFAULT_COMPRESSION ? 6 : jobs[i].level;
+    const int level = s.level == Z_DEFAULT_COMPRESSION ? 6 : s.level;
     // -16: raw deflate64 (64 KiB window, code 285 runs; a batch-API extension,
     // the reference has no deflate64 compressor)
-    const bool d64 = jobs[i].window_bits == -16;
+    const bool d64 = s.window_bits == -16;
     if (d64) w = 16;
-    const bool ok = (d64 || parse_dz_wbits(jobs[i].window_bits, &wrap, &w)) && level >= 0 && level <= 9 &&
-                    jobs[i].in_len < (1ull << 32) && (jobs[i].in || jobs[i].in_len == 0) &&
-                    (jobs[i].out || jobs[i].out_cap == 0);
+    const bool exact = !d64 && level >= 4 && !s.fast;
+    bool ok = (d64 || parse_dz_wbits(s.window_bits, &wrap, &w)) && level >= 0 && level <= 9 &&
+              s.in_len < (1ull << 32) && (s.in || s.in_len == 0) && s.term <= ZS_DT_CUT && s.bit0 < 8 &&
+              s.pstart <= s.in_len && s.ck0 <= s.in_len && (s.out || s.out_cap == 0);
+    // history, a parse entry and a cut need the zlib-identical parse
+    if (!exact && (s.pstart || s.skip || s.term == ZS_DT_CUT)) ok = false;
     if (!ok) {
-      fill_result(&results[i], Z_STREAM_ERROR, nullptr);
+      s.ret = Z_STREAM_ERROR;
       continue;
     }
     ZsDJobDev jd{};
-    jd.in_len = jobs[i].in_len;
+    jd.in_len = s.in_len;
     jd.wrap = wrap;
     jd.level = level;
     jd.wbits = w;
-    jd.exact = (!d64 && level >= 4 && !(flags & ZS_F_DEFLATE_FAST)) ? 1u : 0u;
-    jd.sync = (flags & ZS_F_DEFLATE_SYNC) ? 1u : 0u;
+    jd.exact = exact ? 1u : 0u;
+    jd.term = s.term;
+    jd.hdr = s.hdr;
+    jd.trl = s.trl;
+    jd.bit0 = s.bit0;
+    jd.pstart = s.pstart;
+    jd.pstate = s.pstate;
+    jd.skip = s.skip;
+    jd.abs0 = s.abs0;
+    jd.ck0 = s.ck0;
     jd.seg0 = (uint32_t)nseg;
     jd.nseg = (uint32_t)std::max<uint64_t>(1, (jd.in_len + DZ_SEG_HOST - 1) / DZ_SEG_HOST);
     jd.stage = stage_total;
     stage_total += (dz_bound(jd.in_len, wrap) + 4095) & ~size_t(4095);
     nseg += jd.nseg;
     if (dev) {
-      jd.in = static_cast<const uint8_t *>(jobs[i].in);
+      jd.in = static_cast<const uint8_t *>(s.in);
     } else {
       in_off[i] = in_total;
-      in_total += (jobs[i].in_len + 15) & ~size_t(15);
+      in_total += (s.in_len + 15) & ~size_t(15);
     }
     slot[i] = nv;
     g_dz.h_jobs[nv++] = jd;
@@ -1481,8 +1510,8 @@ int deflate_batch_locked(const zs_djob *jobs, uint32_t n, zs_result *results, ui
     for (uint32_t i = 0; i < n; i++) {
       if (slot[i] == UINT32_MAX) continue;
       g_dz.h_jobs[slot[i]].in = g_dz.d_in + in_off[i];
-      if (jobs[i].in_len)
-        HIP_OK(hipMemcpyAsync(g_dz.d_in + in_off[i], jobs[i].in, jobs[i].in_len, hipMemcpyHostToDevice, st));
+      if (sp[i].in_len)
+        HIP_OK(hipMemcpyAsync(g_dz.d_in + in_off[i], sp[i].in, sp[i].in_len, hipMemcpyHostToDevice, st));
     }
   }
   size_t si = 0;
@@ -1491,7 +1520,7 @@ int deflate_batch_locked(const zs_djob *jobs, uint32_t n, zs_result *results, ui
     for (uint32_t o = 0; o < jd.nseg; o++, si++) {
       ZsDSegDev sg{};
       sg.job = k;
-      sg.last = o + 1 == jd.nseg && !jd.sync;
+      sg.last = o + 1 == jd.nseg && jd.term == ZS_DT_FINAL;
       sg.start = (uint64_t)o * DZ_SEG_HOST;
       sg.len = (uint32_t)std::min<uint64_t>(DZ_SEG_HOST, jd.in_len - std::min<uint64_t>(jd.in_len, sg.start));
       sg.tok = (uint64_t)si * DZ_SEG_HOST;
@@ -1534,51 +1563,114 @@ int deflate_batch_locked(const zs_djob *jobs, uint32_t n, zs_result *results, ui
   for (uint32_t i = 0; i < n; i++) {
     if (slot[i] == UINT32_MAX) continue;
     const ZsDJobDev &jd = g_dz.h_jobs[slot[i]];
-    const uint64_t tot = jd.total_out;
-    const uint64_t give = std::min<uint64_t>(tot, jobs[i].out_cap);
+    DzSpec &s = sp[i];
+    s.total_out = jd.total_out;
+    s.endbit = jd.endbit;
+    s.stage = jd.stage;
+    s.check = jd.check;
+    s.cut_pos = jd.cut_pos;
+    s.cut_state = jd.cut_state;
+    s.cut_skip = jd.cut_skip;
+    s.cut_open = jd.cut_open;
+    const uint64_t give = std::min<uint64_t>(jd.total_out, s.out_cap);
     if (give)
-      HIP_OK(hipMemcpyAsync(jobs[i].out, g_dz.d_stage + jd.stage, give,
-                            dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, st));
-    zs_result &res = results[i];
-    std::memset(&res, 0, sizeof res);
-    res.ret = give == tot ? Z_STREAM_END : Z_OK;  // Z_OK: output space ran out (deflate(Z_FINISH) semantics)
-    res.total_in = jd.in_len;
-    res.total_out = give;
-    res.adler = jd.wrap ? jd.check : 1u;  // deflateResetKeep: adler32(0) for raw/zlib, crc32(0) for gzip
-    res.msg = nullptr;
+      HIP_OK(hipMemcpyAsync(s.out, g_dz.d_stage + jd.stage, give, dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, st));
+    s.ret = give == jd.total_out ? Z_STREAM_END : Z_OK;  // Z_OK: output space ran out (deflate(Z_FINISH) semantics)
+    s.total_out = give;
   }
   HIP_OK(hipStreamSynchronize(st));
   return 0;
 }
 
-// stream surface for deflate: accept all input, compress at Z_FINISH, serve
-// Deflate stream state.  Input accumulates and compresses as ONE GPU job at
-// Z_FINISH -- zlib's exact bytes for levels 4..9.  A flush (Z_SYNC_FLUSH,
-// Z_FULL_FLUSH, Z_PARTIAL_FLUSH, Z_BLOCK) compresses what has accumulated as
-// a segment ending as deflate(Z_SYNC_FLUSH) does (blocks not final, then the
-// empty stored block 00 00 FF FF: everything so far decodes from the output so
-// far); so does an accumulation past dstream_max() bytes, which bounds host
-// buffering.  Segments after the first carry no header and no history (they
-// restart the window: valid deflate, zlib's bytes only up to the first flush),
-// and the last one ends with the trailer of the whole input (its CRC-32 /
-// Adler-32 combined from the segments' checks).
+int deflate_batch_locked(const zs_djob *jobs, uint32_t n, zs_result *results, uint32_t flags) {
+  std::vector<DzSpec> sp(n);
+  for (uint32_t i = 0; i < n; i++) {
+    DzSpec &s = sp[i];
+    s.in = jobs[i].in;
+    s.in_len = jobs[i].in_len;
+    s.out = jobs[i].out;
+    s.out_cap = jobs[i].out_cap;
+    s.window_bits = jobs[i].window_bits;
+    s.level = jobs[i].level;
+    s.fast = (flags & ZS_F_DEFLATE_FAST) != 0;
+    s.term = (flags & ZS_F_DEFLATE_SYNC) ? ZS_DT_SYNC : ZS_DT_FINAL;
+    s.trl = s.term == ZS_DT_FINAL;
+  }
+  const int r = dz_run(sp.data(), n, (flags & ZS_F_DEVICE) != 0);
+  if (r) {
+    for (uint32_t i = 0; i < n; i++) fill_result(&results[i], Z_STREAM_ERROR, nullptr);
+    return r;
+  }
+  for (uint32_t i = 0; i < n; i++) {
+    zs_result &res = results[i];
+    std::memset(&res, 0, sizeof res);
+    res.ret = sp[i].ret;
+    if (res.ret == Z_STREAM_ERROR) continue;
+    int wrap = 0;
+    uint32_t w;
+    parse_dz_wbits(jobs[i].window_bits, &wrap, &w);
+    res.total_in = jobs[i].in_len;
+    res.total_out = sp[i].total_out;
+    res.adler = wrap ? sp[i].check : 1u;  // deflateResetKeep: adler32(0) for raw/zlib, crc32(0) for gzip
+  }
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Deflate stream surfaces (deflate_process, zlib deflate()): every call is
+// zlib's deflate(strm, flush) -- the same bytes, produced by the same call.
+//
+// zlib's deflate_slow processes a loop top t only while the lookahead (input
+// available past t) is >= MIN_LOOKAHEAD (262) unless the call flushes, and
+// writes a block out as soon as its 16 383rd symbol is tallied.  A stream
+// here is a sequence of GPU jobs over [history | unparsed input]: the last
+// window of input before the parse position as history (zlib's window: its
+// hash chains and match sources), the parse resuming in deflate_slow's exact
+// state there, the symbols already sent skipped:
+//   * Z_NO_FLUSH: a ZS_DT_CUT job sends exactly the blocks zlib completes with
+//     the input so far, and names the next job's entry (an exact loop top and
+//     state from the fix-up) -- no flush is ever injected;
+//   * Z_SYNC_FLUSH / Z_FULL_FLUSH / Z_PARTIAL_FLUSH / Z_BLOCK: the job parses
+//     to the end of the input as zlib does for a flush, ends its last block
+//     non-final and writes the flush's terminator (empty stored block, empty
+//     static block, nothing); the window carries over (Z_FULL_FLUSH restarts
+//     it, as deflate.c's CLEAR_HASH + strstart = 0);
+//   * Z_FINISH: the final block, then the trailer of the whole input (CRC-32 /
+//     Adler-32 joined from the jobs' GPU checks).
+// Bits past the last whole byte of a job wait for the next one (zlib keeps
+// them in bi_buf).  The wrapper header is zlib's constant header, sent by the
+// first call.  Levels 0..3 (the GPU throughput encoder, not zlib's bytes)
+// restart the window at each job.  Concurrent handles' jobs share launches.
+// ---------------------------------------------------------------------------
+constexpr uint32_t ZD_BLOCK_SYMS = 16383, ZD_LOOK_HOST = 262;
+
 struct DStreamState {
   int inited = 0;
-  int wbits = 15, level = 6;
-  std::vector<uint8_t> acc;  // input since the last segment
-  std::vector<uint8_t> out;  // output not yet served (from `served` on)
-  bool done = false;
+  int wbits = 15, level = 6, wrap = 0;
+  uint32_t w = 15;             // window bits (zlib's wsize = 1 << w)
+  bool exact = true;           // levels 4..9: zlib's bytes
+  int status = 0;              // 0 no call yet, 1 busy, 2 finished (deflate.c INIT/BUSY/FINISH_STATE)
+  int last_flush = -2;         // deflate.c s->last_flush (deflateResetKeep: -2)
+  std::vector<uint8_t> buf;    // [history | unparsed input]
+  size_t hist = 0;             // parse position in buf (bytes before it: history)
+  uint64_t abs = 0;            // stream offset of buf[0] since the window last restarted
+  uint32_t state = ZD_STATE_A_HOST;  // deflate_slow state at buf[hist]
+  uint64_t skip = 0;           // symbols from buf[hist] already sent
+  size_t ck_from = 0;          // buf[ck_from..) not yet in the running check
+  size_t need = 16383 + 262;   // Z_NO_FLUSH: new bytes before a call can complete a block
+  size_t fresh = 0;            // bytes added since the last job
+  std::vector<uint8_t> out;    // output not yet served (from `served` on)
   size_t served = 0;
-  uint32_t adler = 1;        // strm->adler: check of the input in emitted segments
-  uint32_t nseg = 0;         // segments emitted
-  uint64_t total = 0;        // input bytes in emitted segments
-  bool flushed = false;      // the last segment was a user flush and no input came since
+  uint8_t pend_byte = 0;       // bits of an unfinished last byte (zlib's bi_buf)
+  uint32_t pend_bits = 0;
+  uint32_t adler = 1;          // strm->adler: check of the input the jobs have covered
+  uint64_t checked = 0;        // bytes in `adler`
+  uint64_t total_in = 0;
 };
 
-size_t dstream_max() {  // env ZS_DSTREAM_MAX_KB (default 1 GiB)
-  const char *e = std::getenv("ZS_DSTREAM_MAX_KB");
-  const long long kb = e ? std::atoll(e) : (1ll << 20);
-  return (size_t)std::max<long long>(64, kb) << 10;
+size_t dstream_run_min() {  // env ZS_DSTREAM_RUN_KB: Z_NO_FLUSH input gathered per job (default 0: every call)
+  const char *e = std::getenv("ZS_DSTREAM_RUN_KB");
+  return e ? (size_t)std::max<long long>(0, std::atoll(e)) << 10 : 0;
 }
 
 // checks of A || B from those of A and B (|B| = n2): CRC-32 by x^(8 n2) mod P
@@ -1598,91 +1690,262 @@ uint32_t adler32_join(uint32_t x1, uint32_t x2, uint64_t n2) {
   return (uint32_t)(a | (b << 16));
 }
 
-// one segment of the stream from s->acc; final: the stream's end
-int dstream_segment(DStreamState *s, bool final) {
-  int wrap = 0;
-  uint32_t w = 15;
-  parse_dz_wbits(s->wbits, &wrap, &w);
-  const size_t hdr = wrap == 2 ? 10u : (wrap == 1 ? 2u : 0u), tr = wrap == 2 ? 8u : (wrap == 1 ? 4u : 0u);
-  std::vector<uint8_t> seg;
-  uint32_t chk = wrap == 2 ? 0u : 1u;  // check of the empty input
-  if (!final && s->acc.empty() && s->nseg > 0) {
-    seg = {0x00, 0x00, 0x00, 0xff, 0xff};  // empty stored block at a byte boundary
-  } else {
-    seg.resize(dz_bound(s->acc.size(), wrap) + 8);
-    zs_djob j{};
-    j.in = s->acc.data();
-    j.in_len = s->acc.size();
-    j.out = seg.data();
-    j.out_cap = seg.size();
-    j.window_bits = s->wbits;
-    j.level = s->level;
-    zs_result res;
-    if (deflate_batch_locked(&j, 1, &res, final ? 0u : ZS_F_DEFLATE_SYNC) || res.ret != Z_STREAM_END)
-      return Z_STREAM_ERROR;
-    seg.resize(res.total_out);
-    chk = res.adler;
-    if (s->nseg > 0) seg.erase(seg.begin(), seg.begin() + (ptrdiff_t)std::min(hdr, seg.size()));  // header once
-  }
-  const uint64_t n = s->acc.size();
-  if (wrap) s->adler = s->nseg == 0 ? chk : (wrap == 2 ? crc32_join(s->adler, chk, n) : adler32_join(s->adler, chk, n));
-  s->total += n;
-  if (final && s->nseg > 0 && tr) {  // the whole input's trailer in place of the last segment's own
-    seg.resize(seg.size() - std::min(tr, seg.size()));
-    const uint32_t c = s->adler, isz = (uint32_t)s->total;
-    if (wrap == 2) {
-      const uint8_t t8[8] = {(uint8_t)c, (uint8_t)(c >> 8), (uint8_t)(c >> 16), (uint8_t)(c >> 24),
-                             (uint8_t)isz, (uint8_t)(isz >> 8), (uint8_t)(isz >> 16), (uint8_t)(isz >> 24)};
-      seg.insert(seg.end(), t8, t8 + 8);
-    } else {
-      const uint8_t t4[4] = {(uint8_t)(c >> 24), (uint8_t)(c >> 16), (uint8_t)(c >> 8), (uint8_t)c};
-      seg.insert(seg.end(), t4, t4 + 4);
-    }
-  }
-  s->nseg++;
-  s->acc.clear();
+void ds_put(DStreamState *s, const uint8_t *p, size_t n) {
   if (s->served == s->out.size()) {
     s->out.clear();
     s->served = 0;
   }
-  s->out.insert(s->out.end(), seg.begin(), seg.end());
+  s->out.insert(s->out.end(), p, p + n);
+}
+
+// zlib's wrapper header for (wrap, level), deflate.c (status INIT / GZIP)
+void ds_header(DStreamState *s) {
+  if (s->wrap == 2) {
+    const uint8_t gz[10] = {0x1f, 0x8b, 8, 0, 0, 0, 0, 0, (uint8_t)(s->level == 9 ? 2 : (s->level < 2 ? 4 : 0)), 3};
+    ds_put(s, gz, 10);
+  } else if (s->wrap == 1) {
+    const uint32_t flevel = s->level < 2 ? 0u : (s->level < 6 ? 1u : (s->level == 6 ? 2u : 3u));
+    uint32_t h = ((((s->w - 8u) << 4) | 8u) << 8) | (flevel << 6);
+    h += 31u - (h % 31u);
+    const uint8_t z[2] = {(uint8_t)(h >> 8), (uint8_t)h};
+    ds_put(s, z, 2);
+  }
+}
+
+// the job for the stream's next step: term as the call's flush asks
+DzSpec ds_spec(const DStreamState *s, uint32_t term) {
+  DzSpec j;
+  j.in = s->buf.data();
+  j.in_len = s->buf.size();
+  j.window_bits = s->wbits;
+  j.level = s->level;
+  j.term = term;
+  j.hdr = 0;
+  j.trl = 0;
+  j.bit0 = s->pend_bits;
+  j.pstart = s->exact ? s->hist : 0;
+  j.pstate = s->state;
+  j.skip = s->skip;
+  j.abs0 = s->abs;
+  j.ck0 = s->ck_from;
+  return j;
+}
+
+// a finished job: its bytes into the output (the pending partial byte merged
+// into its first byte, its own partial last byte kept back), the running
+// check, and the next parse position (Z_FULL_FLUSH: full = true)
+void ds_after(DStreamState *s, const DzSpec &j, const uint8_t *bytes, bool full) {
+  const uint32_t term = j.term;
+  uint64_t bits = j.endbit;  // blocks (and the pending bits) end here
+  if (term == ZS_DT_PARTIAL) bits += 10;
+  size_t nb = (size_t)j.total_out;
+  std::vector<uint8_t> o(bytes, bytes + nb);
+  if (s->pend_bits && !o.empty()) o[0] |= s->pend_byte;
+  if (term == ZS_DT_PARTIAL || term == ZS_DT_BLOCK || term == ZS_DT_CUT) {
+    const size_t whole = (size_t)(bits / 8);
+    s->pend_bits = (uint32_t)(bits & 7u);
+    s->pend_byte = s->pend_bits ? o[whole] : 0;
+    o.resize(whole);
+  } else {
+    s->pend_bits = 0;
+    s->pend_byte = 0;
+  }
+  const uint64_t n = s->buf.size() - s->ck_from;
+  if (s->wrap && n) {
+    s->adler = s->checked == 0 ? j.check
+                               : (s->wrap == 2 ? crc32_join(s->adler, j.check, n) : adler32_join(s->adler, j.check, n));
+  }
+  s->checked += n;
+  if (term == ZS_DT_FINAL && s->wrap) {  // the whole input's trailer
+    const uint32_t c = s->adler, isz = (uint32_t)s->total_in;
+    if (s->wrap == 2) {
+      const uint8_t t8[8] = {(uint8_t)c, (uint8_t)(c >> 8), (uint8_t)(c >> 16), (uint8_t)(c >> 24),
+                             (uint8_t)isz, (uint8_t)(isz >> 8), (uint8_t)(isz >> 16), (uint8_t)(isz >> 24)};
+      o.insert(o.end(), t8, t8 + 8);
+    } else {
+      const uint8_t t4[4] = {(uint8_t)(c >> 24), (uint8_t)(c >> 16), (uint8_t)(c >> 8), (uint8_t)c};
+      o.insert(o.end(), t4, t4 + 4);
+    }
+  }
+  ds_put(s, o.data(), o.size());
+  // next parse position
+  const size_t wsize = (size_t)1 << s->w;
+  size_t T;
+  if (term == ZS_DT_CUT) {
+    T = (size_t)j.cut_pos;
+    s->state = j.cut_state;
+    s->skip = j.cut_skip;
+    // new bytes before a call can complete the open block: each symbol it
+    // still lacks starts at a distinct position past the last loop top zlib
+    // processed, and needs the lookahead past it
+    s->need = (size_t)(ZD_BLOCK_SYMS - std::min<uint64_t>(ZD_BLOCK_SYMS, j.cut_open));
+  } else {
+    T = s->buf.size();
+    s->state = ZD_STATE_A_HOST;
+    s->skip = 0;
+    s->need = ZD_BLOCK_SYMS + ZD_LOOK_HOST;
+  }
+  s->fresh = 0;
+  if (full || !s->exact) {  // the window restarts (Z_FULL_FLUSH; levels 0..3 always)
+    s->buf.erase(s->buf.begin(), s->buf.begin() + (ptrdiff_t)T);
+    s->hist = 0;
+    s->abs = full ? 0 : s->abs + T;
+  } else {
+    const size_t h = std::min(T, wsize);
+    s->buf.erase(s->buf.begin(), s->buf.begin() + (ptrdiff_t)(T - h));
+    s->hist = h;
+    s->abs += T - h;
+  }
+  s->ck_from = s->buf.size();  // every byte in buf is in the check now
+}
+
+// ---------------------------------------------------------------------------
+// Deflate-call batching: a stream's job joins a queue; whichever caller finds
+// no launch in flight runs every pending job (any handles, any flush) as ONE
+// dz_run, so concurrent streams share launches (the pattern of sq_submit).
+// ---------------------------------------------------------------------------
+struct DzCall {
+  DzSpec *spec = nullptr;
+  int err = 0;
+  std::string errmsg;
+  bool done = false;
+};
+struct DzQueue {
+  std::mutex mu;
+  std::condition_variable cv, arrive;
+  std::vector<DzCall *> pending;
+  bool busy = false;
+  size_t last_n = 0;
+  uint64_t launches = 0, calls = 0;
+} g_dq;
+
+int dq_submit(DzCall *c) {
+  std::unique_lock<std::mutex> lk(g_dq.mu);
+  g_dq.pending.push_back(c);
+  g_dq.arrive.notify_one();
+  while (!c->done) {
+    if (g_dq.busy) {
+      g_dq.cv.wait(lk);
+      continue;
+    }
+    g_dq.busy = true;
+    if (g_dq.last_n > 1 && g_dq.pending.size() < g_dq.last_n) {  // gather the other active streams' next jobs
+      const auto t_end = std::chrono::steady_clock::now() + std::chrono::microseconds(SQ_WAIT_US);
+      for (;;) {
+        const size_t had = g_dq.pending.size();
+        const auto t = std::min(t_end, std::chrono::steady_clock::now() + std::chrono::microseconds(SQ_GAP_US));
+        g_dq.arrive.wait_until(lk, t, [&] { return g_dq.pending.size() > had; });
+        if (g_dq.pending.size() == had || g_dq.pending.size() >= g_dq.last_n || std::chrono::steady_clock::now() >= t_end)
+          break;
+      }
+    }
+    std::vector<DzCall *> batch(g_dq.pending.begin(), g_dq.pending.end());
+    g_dq.pending.clear();
+    g_dq.last_n = batch.size();
+    lk.unlock();
+    std::vector<DzSpec> specs(batch.size());
+    for (size_t k = 0; k < batch.size(); k++) specs[k] = *batch[k]->spec;
+    int rc;
+    std::string msg;
+    {
+      std::lock_guard<std::mutex> g(g_mu);
+      rc = dz_run(specs.data(), (uint32_t)specs.size(), false);
+      if (rc) msg = g_err;
+    }
+    lk.lock();
+    for (size_t k = 0; k < batch.size(); k++) {
+      *batch[k]->spec = specs[k];
+      batch[k]->err = rc;
+      batch[k]->errmsg = msg;
+      batch[k]->done = true;
+    }
+    g_dq.launches++;
+    g_dq.calls += batch.size();
+    g_dq.busy = false;
+    g_dq.cv.notify_all();
+  }
+  if (c->err) set_err(c->errmsg);
+  return c->err;
+}
+
+// run the stream's next job (term) on the GPU and take its output
+int ds_job(DStreamState *s, uint32_t term, bool full) {
+  DzSpec j = ds_spec(s, term);
+  std::vector<uint8_t> bytes((size_t)dz_bound(s->buf.size(), s->wrap) + 64);
+  j.out = bytes.data();
+  j.out_cap = bytes.size();
+  DzCall c;
+  c.spec = &j;
+  if (dq_submit(&c) || j.ret != Z_STREAM_END) return Z_STREAM_ERROR;
+  ds_after(s, j, bytes.data(), full);
   return Z_OK;
 }
 
+size_t dstream_fast_max() {  // levels 0..3: input gathered per job (env ZS_DSTREAM_MAX_KB, default 64 MiB)
+  const char *e = std::getenv("ZS_DSTREAM_MAX_KB");
+  const long long kb = e ? std::atoll(e) : (64ll << 10);
+  return (size_t)std::max<long long>(64, kb) << 10;
+}
+
+// One zlib deflate(strm, flush) call (deflate.c deflate(): argument checks,
+// pending output first, Z_BUF_ERROR for a call that cannot progress -- the
+// last_flush ranks --, the header at the first call, all input consumed).
 int dstream_call(DStreamState *s, const uint8_t *in, unsigned in_len, uint8_t *out, unsigned out_len, int flush,
                  unsigned *consumed, unsigned *produced) {
   *consumed = 0;
   *produced = 0;
-  bool progress = false;
-  if (!s->done) {
-    if (in_len) {
-      s->acc.insert(s->acc.end(), in, in + in_len);
-      *consumed = in_len;
-      s->flushed = false;
-      progress = true;
+  if (flush < 0 || flush > Z_BLOCK || (s->status == 2 && flush != Z_FINISH)) return Z_STREAM_ERROR;
+  if (out_len == 0) return Z_BUF_ERROR;
+  auto rank = [](int f) { return f * 2 - (f > 4 ? 9 : 0); };
+  auto serve = [&]() {
+    const size_t k = std::min<size_t>(s->out.size() - s->served, out_len - *produced);
+    if (k) std::memcpy(out + *produced, s->out.data() + s->served, k);
+    s->served += k;
+    *produced += (unsigned)k;
+    return *produced == out_len;  // output space used up
+  };
+  const int old_flush = s->last_flush;
+  s->last_flush = flush;
+  if (s->served < s->out.size()) {
+    if (serve()) {
+      s->last_flush = -1;
+      return Z_OK;
     }
-    if (flush == Z_FINISH) {
-      if (dstream_segment(s, true)) return Z_STREAM_ERROR;
-      s->done = true;
-      progress = true;
-    } else if (flush != Z_NO_FLUSH) {
-      if (!s->acc.empty() || !s->flushed) {  // a repeated flush with no new input: no progress (Z_BUF_ERROR)
-        if (dstream_segment(s, false)) return Z_STREAM_ERROR;
-        s->flushed = true;
-        progress = true;
-      }
-    } else if (s->acc.size() >= dstream_max()) {
-      if (dstream_segment(s, false)) return Z_STREAM_ERROR;
-    }
+  } else if (in_len == 0 && rank(flush) <= rank(old_flush) && flush != Z_FINISH) {
+    return Z_BUF_ERROR;
   }
-  const size_t rem = s->out.size() - s->served;
-  const size_t k = std::min<size_t>(rem, out_len);
-  if (k) std::memcpy(out, s->out.data() + s->served, k);
-  s->served += k;
-  *produced = (unsigned)k;
-  if (k) progress = true;
-  if (s->done && s->served == s->out.size()) return Z_STREAM_END;
-  return progress ? Z_OK : Z_BUF_ERROR;
+  if (s->status == 2 && in_len != 0) return Z_BUF_ERROR;
+  if (s->status == 0) {
+    ds_header(s);
+    s->status = 1;
+  }
+  if (in_len || (flush != Z_NO_FLUSH && s->status != 2)) {
+    if (in_len) {
+      s->buf.insert(s->buf.end(), in, in + in_len);
+      s->total_in += in_len;
+      s->fresh += in_len;
+      *consumed = in_len;
+    }
+    int r = Z_OK;
+    if (flush == Z_FINISH) {
+      r = ds_job(s, ZS_DT_FINAL, false);
+      s->status = 2;
+    } else if (flush != Z_NO_FLUSH) {
+      r = ds_job(s, flush == Z_PARTIAL_FLUSH ? ZS_DT_PARTIAL : (flush == Z_BLOCK ? ZS_DT_BLOCK : ZS_DT_SYNC),
+                 flush == Z_FULL_FLUSH);
+    } else if (s->exact) {
+      if (s->fresh >= std::max(s->need, dstream_run_min())) r = ds_job(s, ZS_DT_CUT, false);
+    } else if (s->buf.size() >= dstream_fast_max()) {
+      r = ds_job(s, ZS_DT_BLOCK, false);
+    }
+    if (r) return Z_STREAM_ERROR;
+  }
+  if (serve()) {
+    s->last_flush = -1;
+    return (s->status == 2 && s->served == s->out.size()) ? Z_STREAM_END : Z_OK;
+  }
+  if (flush != Z_FINISH) return Z_OK;
+  return s->served == s->out.size() ? Z_STREAM_END : Z_OK;
 }
 
 struct DHandle {
@@ -1697,32 +1960,44 @@ uintptr_t dhandle_new() {
   std::memset(&h->strm, 0, sizeof h->strm);
   return reinterpret_cast<uintptr_t>(h);
 }
+// deflateInit2(level, Z_DEFLATED, wbits, 8, Z_DEFAULT_STRATEGY) state
+int dstream_init(DStreamState *s, int level, int wbits) {
+  int wrap;
+  uint32_t w;
+  if (level == Z_DEFAULT_COMPRESSION) level = 6;
+  if (level < 0 || level > 9 || !parse_dz_wbits(wbits, &wrap, &w)) return Z_STREAM_ERROR;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (ws_init()) return Z_STREAM_ERROR;
+  }
+  *s = DStreamState();
+  s->inited = 1;
+  s->level = level;
+  s->wbits = wbits;
+  s->wrap = wrap;
+  s->w = w;
+  s->exact = level >= 4;
+  s->adler = wrap == 2 ? 0u : 1u;
+  return Z_OK;
+}
 // src/wasm/deflate_stream_wasm.c:22-49: level < 0 -> Z_DEFAULT_COMPRESSION
 int dhandle_init(uintptr_t hp, int level, int wbits) {
   DHandle *h = reinterpret_cast<DHandle *>(hp);
   if (!h) return Z_STREAM_ERROR;
-  int wrap;
-  uint32_t w;
-  if (level < 0) level = 6;
-  if (level > 9 || !parse_dz_wbits(wbits, &wrap, &w)) return Z_STREAM_ERROR;
-  std::lock_guard<std::mutex> lk(g_mu);
-  if (ws_init()) return Z_STREAM_ERROR;
-  h->st = DStreamState();
-  h->st.inited = 1;
-  h->st.level = level;
-  h->st.wbits = wbits;
-  return Z_OK;
+  return dstream_init(&h->st, level < 0 ? Z_DEFAULT_COMPRESSION : level, wbits);
 }
 int dhandle_process(uintptr_t hp, uintptr_t in_ptr, unsigned in_len, uintptr_t out_ptr, unsigned out_len, int flush) {
   DHandle *h = reinterpret_cast<DHandle *>(hp);
-  if (!h || !h->st.inited) return (int)((unsigned)(Z_STREAM_ERROR & 0xff) << 24);
-  std::lock_guard<std::mutex> lk(g_mu);
+  if (!h) return Z_STREAM_ERROR;  // wasm_stream_common.c:41-43
+  if (!h->st.inited) return (int)((unsigned)(Z_STREAM_ERROR & 0xff) << 24);
   unsigned cons = 0, prod = 0;
   const int ret = dstream_call(&h->st, reinterpret_cast<const uint8_t *>(in_ptr), in_len,
                                reinterpret_cast<uint8_t *>(out_ptr), out_len, flush, &cons, &prod);
   h->last_consumed = cons;
   return (int)((prod & 0x00ffffffu) | ((unsigned)(ret & 0xff) << 24));
 }
+// deflateEnd: Z_DATA_ERROR when the stream was left unfinished (deflate.c)
+int dstream_end_code(const DStreamState *s) { return s->inited && s->status == 1 ? Z_DATA_ERROR : Z_OK; }
 }  // namespace
 
 // ===========================================================================
@@ -1914,8 +2189,9 @@ int deflate_process(uintptr_t h, uintptr_t in_ptr, unsigned in_len, uintptr_t ou
 int deflate_end(uintptr_t h) {
   DHandle *d = reinterpret_cast<DHandle *>(h);
   if (!d) return Z_STREAM_ERROR;
+  const int r = dstream_end_code(&d->st);
   delete d;
-  return Z_OK;
+  return r;
 }
 unsigned deflate_last_consumed(uintptr_t h) {
   DHandle *d = reinterpret_cast<DHandle *>(h);
@@ -1934,15 +2210,21 @@ int ZEXPORT deflateInit2_(z_streamp strm, int level, int method, int windowBits,
   if (method != Z_DEFLATED || memLevel < 1 || memLevel > 9 || level < 0 || level > 9 || strategy < 0 ||
       strategy > Z_FIXED || !parse_dz_wbits(windowBits, &wrap, &w))
     return Z_STREAM_ERROR;
-  {
-    std::lock_guard<std::mutex> lk(g_mu);
-    if (ws_init()) return Z_STREAM_ERROR;
+  // memLevel (hash bits, lit_bufsize) and the strategies change zlib's bytes;
+  // the GPU encoder implements memLevel 8 / Z_DEFAULT_STRATEGY -- the only
+  // parameters the reference passes (src/wasm/deflate_stream_wasm.c:31-49) --
+  // and refuses the rest rather than silently writing other bytes
+  if (memLevel != 8 || strategy != Z_DEFAULT_STRATEGY) {
+    set_err("deflateInit2_: only memLevel 8 and Z_DEFAULT_STRATEGY are implemented on the GPU");
+    return Z_STREAM_ERROR;
   }
   DStreamState *s = new (std::nothrow) DStreamState();
   if (!s) return Z_MEM_ERROR;
-  s->inited = 1;
-  s->level = level;
-  s->wbits = windowBits;
+  const int r = dstream_init(s, level, windowBits);
+  if (r != Z_OK) {
+    delete s;
+    return r;
+  }
   strm->state = reinterpret_cast<struct internal_state *>(s);
   strm->total_in = strm->total_out = 0;
   strm->adler = wrap == 2 ? 0u : 1u;
@@ -1957,7 +2239,6 @@ int ZEXPORT deflate(z_streamp strm, int flush) {
     return Z_STREAM_ERROR;
   if (strm->avail_out == 0) return Z_BUF_ERROR;
   DStreamState *s = reinterpret_cast<DStreamState *>(strm->state);
-  std::lock_guard<std::mutex> lk(g_mu);
   unsigned cons = 0, prod = 0;
   const int ret = dstream_call(s, strm->next_in, strm->avail_in, strm->next_out, strm->avail_out, flush, &cons, &prod);
   strm->next_in += cons;
@@ -1966,14 +2247,16 @@ int ZEXPORT deflate(z_streamp strm, int flush) {
   strm->next_out += prod;
   strm->avail_out -= prod;
   strm->total_out += prod;
-  if (s->nseg) strm->adler = s->adler;
+  if (s->checked) strm->adler = s->adler;  // the input the GPU jobs have checked so far
   return ret;
 }
 int ZEXPORT deflateEnd(z_streamp strm) {
   if (strm == Z_NULL || strm->state == Z_NULL) return Z_STREAM_ERROR;
-  delete reinterpret_cast<DStreamState *>(strm->state);
+  DStreamState *s = reinterpret_cast<DStreamState *>(strm->state);
+  const int r = dstream_end_code(s);
+  delete s;
   strm->state = Z_NULL;
-  return Z_OK;
+  return r;
 }
 uLong ZEXPORT deflateBound(z_streamp strm, uLong sourceLen) {
   int wrap = 1;

@@ -213,12 +213,47 @@ struct ZsDJobDev {
   uint64_t bm0;        // first word of the job's bitmaps
   uint32_t zblk0;      // first block slot
   uint32_t zblk_cap;   // block slots reserved: ceil(in_len / 16383) + 1
-  // ZS_F_DEFLATE_SYNC: end as zlib's deflate(Z_SYNC_FLUSH) at the end of the
-  // input does -- last block BFINAL = 0 (no empty last block), then an empty
-  // stored block (000, pad, 00 00 FF FF) in place of the trailer
-  uint32_t sync;
-  uint32_t pad_;
+  // How the job's bits end (ZS_DT_*) and what else it writes.  A one-shot
+  // job is hdr = 1, trl = 1, ZS_DT_FINAL from pstart = 0 in state A.  A stream
+  // segment (deflate() of the stream surfaces) starts where the previous one
+  // stopped: bit0 bits already pending in its first byte, bytes before pstart
+  // as history (zlib's window), deflate_slow's state pstate at pstart, the
+  // first `skip` symbols from pstart already sent in earlier blocks.
+  uint32_t term;       // ZS_DT_FINAL / _SYNC / _PARTIAL / _BLOCK / _CUT
+  uint32_t hdr;        // write the wrapper header first
+  uint32_t trl;        // ZS_DT_FINAL: write the trailer (check of in[ck0, in_len))
+  uint32_t bit0;       // 0..7 bits of the first byte belong to earlier output
+  uint32_t pstate;     // deflate_slow state at pstart (deflate_zlib.hip encoding)
+  uint32_t cut_state;  // ZS_DT_CUT (out): state at cut_pos
+  uint64_t pstart;     // first loop top of the parse (zlib-identical jobs)
+  uint64_t skip;       // symbols from pstart that earlier jobs already emitted
+  uint64_t abs0;       // stream offset of in[0] since zlib's window last restarted (window slides)
+  uint64_t ck0;        // the check covers in[ck0, in_len)
+  uint64_t endbit;     // (out) bits of the job's blocks, bit0 and header included, before the terminator
+  uint64_t cut_pos;    // ZS_DT_CUT (out): where the next segment's parse starts (job offset)
+  uint64_t cut_skip;   // ZS_DT_CUT (out): ... and the symbols from there already emitted
+  uint64_t cut_open;   // ZS_DT_CUT (out): symbols of the unsent block zlib has already tallied
 };
+// ZsDJobDev::term -- the end of a job's bits, as zlib's deflate() ends a call:
+#define ZS_DT_FINAL 0u    // Z_FINISH: last block BFINAL = 1 (an empty one if needed), trailer
+#define ZS_DT_SYNC 1u     // Z_SYNC_FLUSH / Z_FULL_FLUSH: blocks not final, empty stored block 00 00 FF FF
+#define ZS_DT_PARTIAL 2u  // Z_PARTIAL_FLUSH: blocks not final, then an empty static block (_tr_align, 10 bits)
+#define ZS_DT_BLOCK 3u    // Z_BLOCK: blocks not final, nothing after (not byte aligned)
+#define ZS_DT_CUT 4u      // Z_NO_FLUSH: only the blocks zlib completes with this input (the stream goes on)
+#ifdef __HIP__
+// bytes of a job whose blocks end at bit `endbit`: the terminator, then the
+// trailer (a ZS_DT_PARTIAL / _BLOCK / _CUT job's last byte is partial: the
+// next segment of the stream continues it)
+__device__ __forceinline__ uint64_t zs_dz_total_bytes(const ZsDJobDev &jb, uint64_t endbit) {
+  switch (jb.term) {
+    case ZS_DT_SYNC: return (endbit + 3 + 7) / 8 + 4;  // 000, pad, 00 00 FF FF
+    case ZS_DT_PARTIAL: return (endbit + 10 + 7) / 8;
+    case ZS_DT_BLOCK:
+    case ZS_DT_CUT: return (endbit + 7) / 8;
+    default: return (endbit + 7) / 8 + (jb.trl ? (jb.wrap == 2 ? 8u : (jb.wrap == 1 ? 4u : 0u)) : 0u);
+  }
+}
+#endif
 
 // zlib-identical mode (deflate_zlib.hip, levels 4..9): per job, position
 // arrays at pos0 (previous same-hash distance u16, the two longest-match
@@ -236,6 +271,7 @@ struct ZsZBlkDev {
   uint32_t hbits;      // dynamic: tree header bits after the 3 block-type bits
   uint64_t bits;       // bits after the 3 block-type bits (stored: bytes * 8 + 32, alignment added at layout)
   uint64_t bitoff;     // bit offset of the block in the job's stream (zs_zd_layout_kernel)
+  uint64_t top;        // loop top of the deflate_slow iteration that flushes it
   uint32_t lmax, dmax, blmax, pad;
 };
 
