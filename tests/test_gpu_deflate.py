@@ -459,6 +459,44 @@ def test_deflate_stream_long_no_flush_is_zlibs(zs):
         assert zlib.decompress(out, wb) == data
 
 
+def test_deflate_small_buffer_flush_loops_are_zlibs(zs):
+    """zlib's calling convention with little output space: each segment's
+    deflate(flush) is repeated with the unconsumed input while it returns with
+    avail_out == 0.  The concatenated output equals host zlib's driven the same
+    way -- including the repeated flush markers zlib writes when a flush call
+    runs out of space right at its marker (zlib.h, deflate())."""
+    import libz_ref
+    rng = random.Random(77)
+    data = _stream_data(rng, 900_000)
+    for level, wb in ((6, -15), (9, 31), (4, 15)):
+        segs, off = [], 0
+        while off < len(data):
+            n = rng.choice([5000, 40000, 120000])
+            segs.append((data[off:off + n], rng.choice([0, 1, 2, 3, 5])))
+            off += n
+        segs.append((b"", 4))
+        outs = []
+        for drv in ("gpu", "zlib"):
+            d = _GpuDeflate(zs, level, wb) if drv == "gpu" else libz_ref.Deflater(level, wb)
+            call = d.call1 if drv == "gpu" else d.call
+            out = bytearray()
+            for chunk, fl in segs:
+                rest = chunk
+                k = 0
+                while True:
+                    space = (5, 7, 3000)[min(k, 2)] if fl else 3000
+                    ret, cons, prod = call(rest, space, fl)
+                    out += prod
+                    rest = rest[cons:]
+                    k += 1
+                    if ret == 1 or ret < 0 or (len(prod) < space and not rest):
+                        break
+            assert d.end() == 0
+            outs.append(bytes(out))
+        assert outs[0] == outs[1], (level, wb, len(outs[0]), len(outs[1]))
+        assert zlib.decompress(outs[0], wb) == data
+
+
 def test_compression_stream_js_schedule_calls_are_zlibs(zs):
     """The reference's CompressionStreamZlib schedule (zlib-streams.js:64-156: 64 KiB
     writes, <= 32 KiB per deflate_process, 64 KiB out, Z_FINISH drain) through the

@@ -1661,6 +1661,13 @@ struct DStreamState {
   size_t fresh = 0;            // bytes added since the last job
   std::vector<uint8_t> out;    // output not yet served (from `served` on)
   size_t served = 0;
+  uint64_t out_base = 0;       // stream offset of out[0]
+  // the last flush job's terminator starts at stream offset `mark`: zlib
+  // appends it in the call whose output reaches that byte, and a call with
+  // the same flush after it ran out of space writes another (zlib.h: "avail_out
+  // greater than six to avoid repeated flush markers")
+  bool mark_valid = false;
+  uint64_t mark = 0;
   uint8_t pend_byte = 0;       // bits of an unfinished last byte (zlib's bi_buf)
   uint32_t pend_bits = 0;
   uint32_t adler = 1;          // strm->adler: check of the input the jobs have covered
@@ -1692,6 +1699,7 @@ uint32_t adler32_join(uint32_t x1, uint32_t x2, uint64_t n2) {
 
 void ds_put(DStreamState *s, const uint8_t *p, size_t n) {
   if (s->served == s->out.size()) {
+    s->out_base += s->out.size();
     s->out.clear();
     s->served = 0;
   }
@@ -1767,6 +1775,9 @@ void ds_after(DStreamState *s, const DzSpec &j, const uint8_t *bytes, bool full)
       o.insert(o.end(), t4, t4 + 4);
     }
   }
+  ds_put(s, nullptr, 0);
+  s->mark_valid = term == ZS_DT_SYNC || term == ZS_DT_PARTIAL || term == ZS_DT_BLOCK;
+  s->mark = s->out_base + s->out.size() + (size_t)(j.endbit / 8);  // the terminator's first byte
   ds_put(s, o.data(), o.size());
   // next parse position
   const size_t wsize = (size_t)1 << s->w;
@@ -1906,7 +1917,9 @@ int dstream_call(DStreamState *s, const uint8_t *in, unsigned in_len, uint8_t *o
   };
   const int old_flush = s->last_flush;
   s->last_flush = flush;
-  if (s->served < s->out.size()) {
+  const uint64_t served_start = s->out_base + s->served;
+  const bool had_pending = s->served < s->out.size();
+  if (had_pending) {
     if (serve()) {
       s->last_flush = -1;
       return Z_OK;
@@ -1919,7 +1932,10 @@ int dstream_call(DStreamState *s, const uint8_t *in, unsigned in_len, uint8_t *o
     ds_header(s);
     s->status = 1;
   }
-  if (in_len || (flush != Z_NO_FLUSH && s->status != 2)) {
+  // a call that only delivers the rest of a flush whose terminator zlib
+  // writes in this very call has nothing more to do
+  const bool term_here = had_pending && !in_len && s->mark_valid && served_start <= s->mark;
+  if (in_len || (flush != Z_NO_FLUSH && s->status != 2 && !term_here)) {
     if (in_len) {
       s->buf.insert(s->buf.end(), in, in + in_len);
       s->total_in += in_len;
