@@ -80,6 +80,10 @@ def parse_args(argv=None):
     ap.add_argument("--stream-handle-mib", type=int, default=4, help="stream size per concurrent handle")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json"),
                     help="PMC-derived HBM bytes per pipeline launch (null in the line when absent)")
+    ap.add_argument("--sim-world", type=int, default=0,
+                    help="one-GPU rehearsal of a strong split: decode only rank --sim-rank's LPT share of the "
+                         "node batch as it would be at --sim-world ranks (scaling prediction; not the headline)")
+    ap.add_argument("--sim-rank", type=int, default=0)
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU rehearsal of the multi-rank path (gloo, host zlib as the step, tiny streams); "
                          "prints a line marked dry_run and measures nothing")
@@ -328,6 +332,9 @@ def main():
         total_streams = args.streams if args.scaling == "strong" else args.streams * world
         ids = (shard.bench_shard(args.streams, rank, world, shard.c2_kind) if args.scaling == "strong"
                else list(range(rank * args.streams, (rank + 1) * args.streams)))
+    if args.sim_world > 1:  # this process plays rank sim_rank of sim_world
+        kind = shard.c5_kind if args.workload == "c5" else shard.c2_kind
+        ids = shard.bench_shard(total_streams, args.sim_rank, args.sim_world, kind)
     raws, comps, wbits_list = generate(ids, nbytes, args.workload, gen_threads)
     nloc = len(ids)
     comp_total = sum(len(c) for c in comps)
@@ -471,6 +478,10 @@ def main():
             "deflate64": d64_leg,
             "stream": stream_l,
         }
+        if args.sim_world > 1:
+            line["simulated_rank"] = {"rank": args.sim_rank, "world": args.sim_world, "streams": ids,
+                                      "note": "one GPU decoding one rank's strong-split share; value is that "
+                                              "rank's rate, not the node's"}
         if args.dry_run:
             line["dry_run"] = True
             line["rank_streams"] = ids
