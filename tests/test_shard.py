@@ -89,20 +89,29 @@ def test_gloo_world2_shards_and_counters():
 
 def test_bench_self_launch_dry_run():
     """bench.py --gpus 2 with no launcher starts its own 2 ranks (gloo in the
-    dry run), each rank takes its LPT share of the 64-stream batch (strong
-    scaling), and rank 0 prints one line with the reduced counters."""
+    dry run); by default (weak scaling) each rank decodes its own 64-stream
+    batch, with --scaling strong its LPT share of one batch; rank 0 prints one
+    line with the reduced counters."""
     import json
     import subprocess
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
-    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--dry-run", "--gpus", "2", "--stream-mib", "1",
-                        "--steps", "1", "--warmup", "0"], capture_output=True, text=True, timeout=300, env=env)
-    assert r.returncode == 0, r.stderr[-2000:]
-    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, r.stdout
-    d = json.loads(lines[0])
+
+    def run(*extra):
+        r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--dry-run", "--gpus", "2", "--stream-mib",
+                            "1", "--steps", "1", "--warmup", "0", *extra], capture_output=True, text=True, timeout=300,
+                           env=env)
+        assert r.returncode == 0, r.stderr[-2000:]
+        lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+        assert len(lines) == 1, r.stdout
+        return json.loads(lines[0])
+
+    d = run()
+    assert d["dry_run"] and d["n_gpus"] == 2 and d["verified_bit_exact"] and d["scaling"] == "weak"
+    assert d["config"]["streams_total"] == 128 and d["rank_streams"] == list(range(64))
+    d = run("--scaling", "strong")
     assert d["dry_run"] and d["n_gpus"] == 2 and d["verified_bit_exact"] and d["scaling"] == "strong"
     assert d["config"]["streams_total"] == 64
     assert d["rank_streams"] == shard.bench_shard(64, 0, 2, shard.c2_kind)
