@@ -166,7 +166,297 @@ __global__ void zs_header_kernel(const ZsJobDev *__restrict__ jobs, ZsHeadDev *_
 // ---------------------------------------------------------------------------
 // The wave-uniform deflate decoder.
 // ---------------------------------------------------------------------------
+// ---------------------------------------------------------------------------
+// Workgroup-wide symbol window (the stream kernel: one handle call per
+// 1 024-thread workgroup).  A call of the handle ABI decodes one slice (<= 32
+// KiB in, <= 64 KiB out): one or two blocks, so there is no block parallelism
+// to use, and one wave's fast_window (512 bits, <= 64 symbols) left the call
+// at one wave's serial pace.  Here all 16 waves decode one window of up to
+// WW_BITS = 8 192 bits (~900 symbols): every thread decodes a complete symbol
+// at 8 bit offsets; pointer doubling over the jump table q -> q + bits(q)
+// (10 rounds, workgroup barriers) gives the chain's first 1 024 symbol
+// starts; symbol k's data moves to thread k through an on-chain mark; a
+// workgroup scan of the output lengths admits the longest prefix that is
+// plain (complete in the input, fits the output, distance within the history,
+// not end-of-block / invalid -- as fast_window); the bytes expand 4 096 per
+// step into the history ring (sources before the step read the ring, sources
+// inside it resolve by pointer jumping).  Wave 0 runs the exact state machine
+// (Inflater) and posts a window to the other waves, which wait at a barrier
+// in between; everything a window does not take stays on the exact serial
+// path, so results and stop points are the serial decoder's.
+// ---------------------------------------------------------------------------
+#define WW_T 1024u                 // threads of the stream kernel
+#define WW_OFFS 8u                 // bit offsets per thread
+#define WW_BITS (WW_T * WW_OFFS)   // 8 192-bit window
+#define WW_JN (WW_BITS + 64u)      // jump-table entries (a symbol is <= 48 bits)
+#define WW_STEP (4u * WW_T)        // bytes expanded per step
+#define WW_TCAP 16384u             // bytes per window (the ring keeps the unflushed tail)
+#define WW_RUN 1u
+#define WW_EXIT 2u
+
+struct WideLDS {
+  // command (wave 0 -> all waves)
+  uint32_t op, P, W, limit_bits, pos, cap, whave, lmask, dmask;
+  const uint32_t *lt, *dt;
+  uint8_t *ring;               // wave 0's history ring and input ring (LDS)
+  const uint32_t *inring;
+  // results and reductions
+  uint32_t n, T, endrel, cnt_min, n_min, carry, open;
+  uint32_t wtot[WW_T / 64];
+  uint32_t S[WW_T];            // chain: start bit (window-relative) of symbol k
+  uint32_t symL[WW_T], symD[WW_T];
+  uint8_t nb[WW_JN];           // symbol bits at each offset (0: no plain symbol starts there)
+  __attribute__((aligned(16))) uint16_t ja[WW_JN];
+  __attribute__((aligned(16))) uint16_t jb[WW_JN];  // + ja: marks / expansion entries later
+};
+static_assert(sizeof(uint16_t) * WW_JN * 2 >= WW_STEP * 6, "expansion marks + entries alias the jump tables");
+
+__device__ __forceinline__ uint32_t ww_scan_sum(uint32_t x) {  // inclusive, wave64
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);
+  return x;
+}
+__device__ __forceinline__ uint32_t ww_scan_max(uint32_t v) {  // inclusive, wave64
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));
+  return v;
+}
+// workgroup inclusive scan (sum or max) of one value per thread
+template <bool MAX>
+__device__ __forceinline__ uint32_t ww_scan(WideLDS &w, uint32_t v) {
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  const uint32_t inc = MAX ? ww_scan_max(v) : ww_scan_sum(v);
+  if (lane == 63) w.wtot[wv] = inc;
+  __syncthreads();
+  uint32_t pre = 0;
+  for (uint32_t k = 0; k < wv; k++) pre = MAX ? max(pre, w.wtot[k]) : pre + w.wtot[k];
+  __syncthreads();  // wtot is reused by the next scan
+  return MAX ? max(pre, inc) : pre + inc;
+}
+
+__device__ __forceinline__ uint64_t ww_bits_at(const uint32_t *inring, uint32_t q) {
+  const uint32_t wq = q >> 5, sh = q & 31u;
+  const uint32_t a = inring[wq & (IN_RING_WORDS - 1)];
+  const uint32_t b = inring[(wq + 1) & (IN_RING_WORDS - 1)];
+  const uint32_t c = inring[(wq + 2) & (IN_RING_WORDS - 1)];
+  uint64_t h = ((((uint64_t)b) << 32) | a) >> sh;
+  if (sh) h |= (uint64_t)c << (64u - sh);
+  return h;
+}
+
+// One complete symbol at bit q (as fast_window's stage 1): returns its bits
+// (0: not a plain symbol), the length (0x80000000 | literal for a literal)
+// and the distance.
 template <bool D64>
+__device__ __forceinline__ uint32_t ww_decode(const WideLDS &w, const uint32_t *inring, uint32_t q, uint32_t &lv,
+                                              uint32_t &dv) {
+  const uint32_t *lt = w.lt, *dt = w.dt;
+  const uint64_t hh = ww_bits_at(inring, q);
+  uint32_t e = lt[(uint32_t)hh & w.lmask];
+  uint32_t used = e_bits(e);
+  {
+    const uint32_t op0 = e_op(e);
+    if (op0 != 0 && (op0 & 0xf0u) == 0) {
+      const uint32_t e2 = lt[e_val(e) + (((uint32_t)(hh >> used)) & ((1u << op0) - 1))];
+      used += e_bits(e2);
+      e = e2;
+    }
+  }
+  const uint32_t op = e_op(e);
+  dv = 0;
+  if (op == 0) {
+    lv = 0x80000000u | e_val(e);
+    return q + used > w.limit_bits ? 0u : used;
+  }
+  if (op & 96u) {  // end of block / invalid code: not plain
+    lv = 0;
+    return 0;
+  }
+  const uint32_t xb = op & (D64 ? 31u : 15u);
+  lv = e_val(e) + ((uint32_t)(hh >> used) & ((1u << xb) - 1u));
+  const uint32_t sb = used + xb;
+  const uint64_t hd = hh >> sb;
+  uint32_t d = dt[(uint32_t)hd & w.dmask];
+  uint32_t dused = e_bits(d);
+  {
+    const uint32_t dop0 = e_op(d);
+    if ((dop0 & 0xf0u) == 0) {
+      const uint32_t d2 = dt[e_val(d) + (((uint32_t)(hd >> dused)) & ((1u << dop0) - 1))];
+      dused += e_bits(d2);
+      d = d2;
+    }
+  }
+  const uint32_t dop = e_op(d);
+  if (dop & 64u) return 0;  // invalid distance code
+  const uint32_t dx = dop & 15u;
+  dv = e_val(d) + ((uint32_t)(hd >> dused) & ((1u << dx) - 1u));
+  const uint32_t nb = sb + dused + dx;
+  return q + nb > w.limit_bits || nb > 63u ? 0u : nb;
+}
+
+// the window, run by all WW_T threads (wave 0 posted the command)
+template <bool D64>
+__device__ void ww_run(WideLDS &w) {
+  constexpr uint32_t RMASK = (D64 ? 65536u : 32768u) - 1u;
+  uint8_t *ring = w.ring;
+  const uint32_t *inring = w.inring;
+  const uint32_t t = threadIdx.x;
+  const uint32_t P = w.P, W = w.W;
+  // 1. a complete symbol at every offset of the window
+  uint32_t lv[WW_OFFS], dv[WW_OFFS];
+#pragma unroll
+  for (uint32_t i = 0; i < WW_OFFS; i++) {
+    const uint32_t q = t + i * WW_T;
+    uint32_t nb = 0;
+    lv[i] = dv[i] = 0;
+    if (q < W) nb = ww_decode<D64>(w, inring, P + q, lv[i], dv[i]);
+    w.nb[q] = (uint8_t)nb;
+    w.ja[q] = (uint16_t)(q + nb);
+  }
+  if (t < WW_JN - WW_BITS) {
+    w.nb[WW_BITS + t] = 0;
+    w.ja[WW_BITS + t] = (uint16_t)(WW_BITS + t);
+  }
+  if (t == 0) {
+    w.S[0] = 0;
+    w.cnt_min = WW_T;
+    w.n_min = WW_T;
+  }
+  // 2. pointer doubling: S[k] = start of the chain's k-th symbol
+  uint16_t *ja = w.ja, *jb = w.jb;
+#pragma unroll 1
+  for (uint32_t k = 0; k < 10; k++) {
+    __syncthreads();
+    const uint32_t half = 1u << k;
+    if (t >= half && t < 2u * half) w.S[t] = ja[w.S[t - half]];
+    if (k < 9) {
+#pragma unroll
+      for (uint32_t i = 0; i < WW_OFFS; i++) {
+        const uint32_t q = t + i * WW_T;
+        jb[q] = ja[ja[q]];
+      }
+      if (t < WW_JN - WW_BITS) jb[WW_BITS + t] = (uint16_t)(WW_BITS + t);
+      uint16_t *x = ja;
+      ja = jb;
+      jb = x;
+    }
+  }
+  __syncthreads();
+  // 3. the chain's symbols: inside the window and plain
+  const uint32_t s = w.S[t];
+  const uint32_t snb = s < WW_BITS ? w.nb[s] : 0u;
+  if (!(s < W && snb != 0)) atomicMin(&w.cnt_min, t);
+  uint16_t *mark = w.jb;  // the jump tables are done with
+#pragma unroll
+  for (uint32_t i = 0; i < WW_OFFS; i++) mark[t + i * WW_T] = 0;
+  __syncthreads();
+  const uint32_t cnt = w.cnt_min;
+  if (t < cnt) mark[s] = (uint16_t)(t + 1u);
+  __syncthreads();
+#pragma unroll
+  for (uint32_t i = 0; i < WW_OFFS; i++) {
+    const uint32_t m = mark[t + i * WW_T];
+    if (m) {
+      w.symL[m - 1u] = lv[i];
+      w.symD[m - 1u] = dv[i];
+    }
+  }
+  __syncthreads();
+  // 4. admissible prefix: fits the output (and WW_TCAP), distance within history
+  const bool act = t < cnt;
+  const uint32_t L = act ? w.symL[t] : 0u, D = act ? w.symD[t] : 0u;
+  const bool lit = (L & 0x80000000u) != 0;
+  const uint32_t olen = act ? (lit ? 1u : L) : 0u;
+  const uint32_t incl = ww_scan<false>(w, olen);
+  const uint32_t ost = incl - olen;
+  const uint32_t room = min(w.cap - w.pos, WW_TCAP);
+  const bool ok = act && incl <= room && (lit || D <= w.pos + ost + w.whave);
+  if (!ok) atomicMin(&w.n_min, t);
+  __syncthreads();
+  const uint32_t n = w.n_min;
+  if (n > 0 && t == n - 1u) w.T = incl;
+  if (n == 0 && t == 0) w.T = 0;
+  if (t == (n < WW_T ? n : WW_T - 1u)) w.endrel = n < WW_T ? s : s + snb;
+  if (t == 0) w.carry = 0;
+  __syncthreads();
+  const uint32_t T = w.T;
+  // 5. expansion, WW_STEP bytes per step, 4 consecutive per thread
+  const uint32_t base = w.pos;
+  uint16_t *marks = w.ja;                                   // WW_STEP u16
+  uint32_t *ent = reinterpret_cast<uint32_t *>(w.ja + WW_STEP);  // WW_STEP u32 (ja tail + jb)
+  for (uint32_t b0 = 0; b0 < T; b0 += WW_STEP) {
+    reinterpret_cast<uint2 *>(marks)[t] = make_uint2(0u, 0u);
+    __syncthreads();
+    if (t < n && ost >= b0 && ost < b0 + WW_STEP) marks[ost - b0] = (uint16_t)(t + 1u);
+    __syncthreads();
+    const uint2 mk = reinterpret_cast<const uint2 *>(marks)[t];
+    uint32_t mm[4] = {mk.x & 0xffffu, mk.x >> 16, mk.y & 0xffffu, mk.y >> 16};
+    mm[1] = max(mm[1], mm[0]);
+    mm[2] = max(mm[2], mm[1]);
+    mm[3] = max(mm[3], mm[2]);
+    const uint32_t carry = w.carry;
+    // symbol of each byte: the last mark at or before it (an inclusive max
+    // scan; the thread's bytes before its own first mark continue the symbol
+    // open at the end of thread t - 1, or of the previous step)
+    const uint32_t inc = ww_scan<true>(w, mm[3]);
+    w.S[t] = inc;  // the chain starts are in registers now
+    __syncthreads();
+    const uint32_t pv = max(t ? w.S[t - 1u] : 0u, carry + 1u);
+    __syncthreads();
+    uint32_t e[4];
+    bool open = false;
+#pragma unroll
+    for (uint32_t r = 0; r < 4; r++) {
+      const uint32_t si = max(pv, mm[r]) - 1u;
+      if (r == 3 && t == WW_T - 1u) w.carry = si;
+      const uint32_t Ls = w.symL[si], Ds = w.symD[si];
+      const uint32_t j = b0 + 4u * t + r;
+      const int32_t sp = (int32_t)j - (int32_t)Ds;  // relative to `base`
+      const uint32_t rv = ring[(base + (uint32_t)sp) & RMASK];
+      e[r] = (Ls & 0x80000000u) ? (0x100u | (Ls & 0xffu))
+                                : (sp >= (int32_t)b0 ? (((uint32_t)sp - b0) << 16) : (0x100u | rv));
+      open = open || (j < T && !(e[r] & 0x100u));
+    }
+    reinterpret_cast<uint4 *>(ent)[t] = make_uint4(e[0], e[1], e[2], e[3]);
+    if (t == 0) w.open = 0;
+    __syncthreads();
+    if (open) atomicOr(&w.open, 1u);
+    __syncthreads();
+    while (w.open) {
+      uint32_t g[4];
+#pragma unroll
+      for (uint32_t r = 0; r < 4; r++) g[r] = ent[(e[r] & 0x100u) ? 0u : (e[r] >> 16)];
+      open = false;
+#pragma unroll
+      for (uint32_t r = 0; r < 4; r++) {
+        if (!(e[r] & 0x100u)) e[r] = (g[r] & 0x100u) ? g[r] : (g[r] & 0xffff0000u);
+        open = open || (b0 + 4u * t + r < T && !(e[r] & 0x100u));
+      }
+      __syncthreads();
+      reinterpret_cast<uint4 *>(ent)[t] = make_uint4(e[0], e[1], e[2], e[3]);
+      if (t == 0) w.open = 0;
+      __syncthreads();
+      if (open) atomicOr(&w.open, 1u);
+      __syncthreads();
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < 4; r++) {
+      const uint32_t j = b0 + 4u * t + r;
+      if (j < T) ring[(base + j) & RMASK] = (uint8_t)e[r];
+    }
+    __syncthreads();
+  }
+}
+
+template <bool D64, bool WIDE = false>
 struct Inflater {
   static constexpr uint32_t RING = D64 ? 65536u : 32768u;
   static constexpr uint32_t RMASK = RING - 1;
@@ -810,6 +1100,46 @@ struct Inflater {
     return n;
   }
 
+  // The workgroup-wide window (WIDE: the stream kernel, this wave is wave 0
+  // of WW_T threads): post the window, take part in it, apply its prefix.
+  WideLDS *wide = nullptr;
+  __device__ uint32_t wide_window(const uint32_t *lt, const uint32_t *dt, uint32_t lmask, uint32_t dmask) {
+    const uint32_t P = bitpos();
+    if (pos == cap || P + 64u + 1024u > limit_bits) return 0;
+    const uint32_t W = min(WW_BITS, ((limit_bits - P - 64u) / 1024u) * 1024u);
+    ensure_words(((P + W + 64u) >> 5) + 3u);
+    WideLDS &w = *wide;
+    if (lane_id() == 0) {
+      w.op = WW_RUN;
+      w.P = P;
+      w.W = W;
+      w.limit_bits = limit_bits;
+      w.pos = pos;
+      w.cap = cap;
+      w.whave = whave;
+      w.lmask = lmask;
+      w.dmask = dmask;
+      w.lt = lt;
+      w.dt = dt;
+      w.ring = ring;
+      w.inring = inring;
+    }
+    __syncthreads();  // the other waves wait here for a window
+    ww_run<D64>(w);
+    const uint32_t n = w.n_min, T = w.T, endrel = w.endrel;
+    KPW_ADD(KP_W_WINDOWS, 1);
+    if (n == 0) {
+      KPW_ADD(KP_W_EMPTY, 1);
+      return 0;
+    }
+    pos += T;
+    maybe_flush();
+    reseat(P + endrel);
+    KPW_ADD(KP_W_SYMS, n);
+    KPW_ADD(KP_W_BYTES, T);
+    return n;
+  }
+
   // MATCH state (src/inflate.c:1142-1187): a decoded match, or the pending
   // rest of one in a resumed call; -1 = copied whole.  left == 0 is tested
   // before the distance, so a too-far distance met with a full output is
@@ -846,7 +1176,11 @@ struct Inflater {
     r_mode = ZSM_SYMS;
     const uint32_t lmask = (1u << lbits) - 1, dmask = (1u << dbits) - 1;
     for (;;) {
-      if (fast_window(lt, dt, lmask, dmask)) continue;
+      if constexpr (WIDE) {
+        if (wide_window(lt, dt, lmask, dmask)) continue;
+      } else {
+        if (fast_window(lt, dt, lmask, dmask)) continue;
+      }
       KPW_ADD(KP_W_SERIAL, 1);
       refill();
       r_bit = bitpos();
@@ -1050,10 +1384,10 @@ template __global__ void zs_decode_kernel<true>(const ZsJobDev *, const ZsHeadDe
 // the handle's device state.  The job holds the call buffer (bytes carried
 // over from earlier calls + the new input) and the call's output buffer.
 // ---------------------------------------------------------------------------
+// wave 0 of zs_stream_kernel: one call
 template <bool D64>
-__global__ void __launch_bounds__(64) zs_stream_kernel(ZsStreamDev *const *__restrict__ sts, const ZsJobDev *__restrict__ jobs,
-                                                        const ZsHeadDev *__restrict__ heads) {
-  // one workgroup per call of the batch (calls of different handles; see zs_launch_stream)
+__device__ __forceinline__ void zs_stream_call(ZsStreamDev *const *__restrict__ sts, const ZsJobDev *__restrict__ jobs,
+                                               const ZsHeadDev *__restrict__ heads, WideLDS &s_wide) {
   ZsStreamDev *__restrict__ st = sts[blockIdx.x];
   const ZsJobDev *__restrict__ job = jobs + blockIdx.x;
   const ZsHeadDev *__restrict__ head = heads + blockIdx.x;
@@ -1066,7 +1400,6 @@ __global__ void __launch_bounds__(64) zs_stream_kernel(ZsStreamDev *const *__res
   __shared__ uint16_t s_lens[320];
   __shared__ __attribute__((aligned(16))) uint16_t s_sorted[320];
   __shared__ uint32_t s_scr[32];
-  __shared__ __attribute__((aligned(16))) uint16_t s_jmp[2 * Inflater<D64>::FW_JN];
 
   const uint32_t lane = lane_id();
   const ZsJobDev jb = *job;
@@ -1101,9 +1434,10 @@ __global__ void __launch_bounds__(64) zs_stream_kernel(ZsStreamDev *const *__res
       }
     }
   }
-  __syncthreads();
+  __builtin_amdgcn_wave_barrier();
   if (mode >= ZSM_TYPE && mode <= ZSM_STORED) {
-    Inflater<D64> f;
+    Inflater<D64, true> f;
+    f.wide = &s_wide;
     f.ring = s_ring;
     f.inring = s_in;
     f.tab = s_tab;
@@ -1111,7 +1445,6 @@ __global__ void __launch_bounds__(64) zs_stream_kernel(ZsStreamDev *const *__res
     f.lens = s_lens;
     f.sorted = s_sorted;
     f.scratch16 = s_scr;
-    f.jmp = s_jmp;
     const uintptr_t ip = reinterpret_cast<uintptr_t>(jb.in);
     const uint32_t mis = (uint32_t)(ip & 15u);
     f.abase = reinterpret_cast<const uint8_t *>(ip - mis);
@@ -1139,12 +1472,12 @@ __global__ void __launch_bounds__(64) zs_stream_kernel(ZsStreamDev *const *__res
     f.blast = st->last != 0;
     if (mode != ZSM_TYPE && mode != ZSM_STORED && f.r_btype == 2)
       for (uint32_t k = lane; k < f.r_nlen + f.r_ndist; k += WAVE) s_lens[k] = st->lens[k];
-    __syncthreads();
+    __builtin_amdgcn_wave_barrier();
     f.seek(mis * 8u + rbit);
     f.stop_bits = 0;
     const int packed = f.run((uint32_t)mode);
     f.flush_tail();
-    __syncthreads();
+    __builtin_amdgcn_wave_barrier();
     code = packed & 0xff;
     msg = packed >> 8;
     mode = code == ZD_ERROR ? (int32_t)ZSM_BAD : (int32_t)f.r_mode;
@@ -1175,6 +1508,26 @@ __global__ void __launch_bounds__(64) zs_stream_kernel(ZsStreamDev *const *__res
     st->acc_a = 0;
     st->acc_b = 0;
   }
+}
+
+template <bool D64>
+__global__ void __launch_bounds__(WW_T) zs_stream_kernel(ZsStreamDev *const *__restrict__ sts, const ZsJobDev *__restrict__ jobs,
+                                                          const ZsHeadDev *__restrict__ heads) {
+  // one workgroup per call of the batch (calls of different handles; see
+  // zs_launch_stream): wave 0 runs the call's exact state machine, the other
+  // waves join its workgroup-wide symbol windows (WideLDS)
+  __shared__ WideLDS s_wide;
+  if (threadIdx.x >= WAVE) {
+    for (;;) {
+      __syncthreads();  // a window posted by wave 0, or the end of the call
+      if (s_wide.op == WW_EXIT) break;
+      ww_run<D64>(s_wide);
+    }
+    return;
+  }
+  zs_stream_call<D64>(sts, jobs, heads, s_wide);
+  if (threadIdx.x == 0) s_wide.op = WW_EXIT;
+  __syncthreads();
 }
 
 template __global__ void zs_stream_kernel<false>(ZsStreamDev *const *, const ZsJobDev *, const ZsHeadDev *);
@@ -1306,9 +1659,9 @@ extern "C" void zs_launch_stream(int d64, int run_header, ZsStreamDev *const *d_
                                  hipStream_t stream) {
   if (run_header) hipLaunchKernelGGL(zs_header_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, d_jobs, d_heads, n);
   if (d64)
-    hipLaunchKernelGGL(zs_stream_kernel<true>, dim3(n), dim3(64), 0, stream, d_sts, d_jobs, d_heads);
+    hipLaunchKernelGGL(zs_stream_kernel<true>, dim3(n), dim3(WW_T), 0, stream, d_sts, d_jobs, d_heads);
   else
-    hipLaunchKernelGGL(zs_stream_kernel<false>, dim3(n), dim3(64), 0, stream, d_sts, d_jobs, d_heads);
+    hipLaunchKernelGGL(zs_stream_kernel<false>, dim3(n), dim3(WW_T), 0, stream, d_sts, d_jobs, d_heads);
   const uint32_t pieces = (uint32_t)std::min<uint64_t>(1024, std::max<uint64_t>(1, (max_out_cap + 65535) / 65536));
   hipLaunchKernelGGL(zs_stream_check_kernel, dim3(pieces, n), dim3(SCHECK_THREADS), 0, stream, d_sts, d_jobs);
   hipLaunchKernelGGL(zs_stream_finish_kernel, dim3(n), dim3(64), 0, stream, d_sts, d_jobs, d_res);
