@@ -197,11 +197,10 @@ __global__ void zs_header_kernel(const ZsJobDev *__restrict__ jobs, ZsHeadDev *_
 struct WideLDS {
   // command (wave 0 -> all waves)
   uint32_t op, P, W, limit_bits, pos, cap, whave, lmask, dmask;
-  const uint32_t *lt, *dt;
-  uint8_t *ring;               // wave 0's history ring and input ring (LDS)
-  const uint32_t *inring;
+  uint32_t lt_off, dt_off;     // the code tables: byte offsets in the kernel's StreamLDS
   // results and reductions
   uint32_t n, T, endrel, cnt_min, n_min, carry, open;
+  uint32_t save, save_pos;     // end of the call: the history ring goes to the handle's state
   uint32_t wtot[WW_T / 64];
   uint32_t S[WW_T];            // chain: start bit (window-relative) of symbol k
   uint32_t symL[WW_T], symD[WW_T];
@@ -210,6 +209,21 @@ struct WideLDS {
   __attribute__((aligned(16))) uint16_t jb[WW_JN];  // + ja: marks / expansion entries later
 };
 static_assert(sizeof(uint16_t) * WW_JN * 2 >= WW_STEP * 6, "expansion marks + entries alias the jump tables");
+
+// All LDS of one stream-kernel workgroup in one object, so every wave reaches
+// it through the same LDS addresses (ds_* instructions, not flat ones)
+template <bool D64>
+struct StreamLDS {
+  static constexpr uint32_t RING = D64 ? 65536u : 32768u;
+  __attribute__((aligned(16))) uint8_t ring[RING];
+  __attribute__((aligned(16))) uint32_t in[IN_RING_WORDS];
+  uint32_t tab[TABLE_ENTRIES];
+  uint32_t ftab[544];
+  uint16_t lens[320];
+  __attribute__((aligned(16))) uint16_t sorted[320];
+  uint32_t scr[32];
+  WideLDS wide;
+};
 
 __device__ __forceinline__ uint32_t ww_scan_sum(uint32_t x) {  // inclusive, wave64
   x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);
@@ -256,9 +270,8 @@ __device__ __forceinline__ uint64_t ww_bits_at(const uint32_t *inring, uint32_t 
 // (0: not a plain symbol), the length (0x80000000 | literal for a literal)
 // and the distance.
 template <bool D64>
-__device__ __forceinline__ uint32_t ww_decode(const WideLDS &w, const uint32_t *inring, uint32_t q, uint32_t &lv,
-                                              uint32_t &dv) {
-  const uint32_t *lt = w.lt, *dt = w.dt;
+__device__ __forceinline__ uint32_t ww_decode(const WideLDS &w, const uint32_t *lt, const uint32_t *dt,
+                                              const uint32_t *inring, uint32_t q, uint32_t &lv, uint32_t &dv) {
   const uint64_t hh = ww_bits_at(inring, q);
   uint32_t e = lt[(uint32_t)hh & w.lmask];
   uint32_t used = e_bits(e);
@@ -304,10 +317,13 @@ __device__ __forceinline__ uint32_t ww_decode(const WideLDS &w, const uint32_t *
 
 // the window, run by all WW_T threads (wave 0 posted the command)
 template <bool D64>
-__device__ void ww_run(WideLDS &w) {
+__device__ void ww_run(StreamLDS<D64> &Ls) {
   constexpr uint32_t RMASK = (D64 ? 65536u : 32768u) - 1u;
-  uint8_t *ring = w.ring;
-  const uint32_t *inring = w.inring;
+  WideLDS &w = Ls.wide;
+  uint8_t *ring = Ls.ring;
+  const uint32_t *inring = Ls.in;
+  const uint32_t *lt = reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(&Ls) + w.lt_off);
+  const uint32_t *dt = reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(&Ls) + w.dt_off);
   const uint32_t t = threadIdx.x;
   const uint32_t P = w.P, W = w.W;
   // 1. a complete symbol at every offset of the window
@@ -317,7 +333,7 @@ __device__ void ww_run(WideLDS &w) {
     const uint32_t q = t + i * WW_T;
     uint32_t nb = 0;
     lv[i] = dv[i] = 0;
-    if (q < W) nb = ww_decode<D64>(w, inring, P + q, lv[i], dv[i]);
+    if (q < W) nb = ww_decode<D64>(w, lt, dt, inring, P + q, lv[i], dv[i]);
     w.nb[q] = (uint8_t)nb;
     w.ja[q] = (uint16_t)(q + nb);
   }
@@ -1102,13 +1118,14 @@ struct Inflater {
 
   // The workgroup-wide window (WIDE: the stream kernel, this wave is wave 0
   // of WW_T threads): post the window, take part in it, apply its prefix.
-  WideLDS *wide = nullptr;
+  StreamLDS<D64> *wide = nullptr;  // the workgroup's LDS (WIDE)
   __device__ uint32_t wide_window(const uint32_t *lt, const uint32_t *dt, uint32_t lmask, uint32_t dmask) {
     const uint32_t P = bitpos();
     if (pos == cap || P + 64u + 1024u > limit_bits) return 0;
     const uint32_t W = min(WW_BITS, ((limit_bits - P - 64u) / 1024u) * 1024u);
     ensure_words(((P + W + 64u) >> 5) + 3u);
-    WideLDS &w = *wide;
+    WideLDS &w = wide->wide;
+    const uint8_t *lb = reinterpret_cast<const uint8_t *>(wide);
     if (lane_id() == 0) {
       w.op = WW_RUN;
       w.P = P;
@@ -1119,13 +1136,11 @@ struct Inflater {
       w.whave = whave;
       w.lmask = lmask;
       w.dmask = dmask;
-      w.lt = lt;
-      w.dt = dt;
-      w.ring = ring;
-      w.inring = inring;
+      w.lt_off = (uint32_t)(reinterpret_cast<const uint8_t *>(lt) - lb);
+      w.dt_off = (uint32_t)(reinterpret_cast<const uint8_t *>(dt) - lb);
     }
     __syncthreads();  // the other waves wait here for a window
-    ww_run<D64>(w);
+    ww_run<D64>(*wide);
     const uint32_t n = w.n_min, T = w.T, endrel = w.endrel;
     KPW_ADD(KP_W_WINDOWS, 1);
     if (n == 0) {
@@ -1387,19 +1402,19 @@ template __global__ void zs_decode_kernel<true>(const ZsJobDev *, const ZsHeadDe
 // wave 0 of zs_stream_kernel: one call
 template <bool D64>
 __device__ __forceinline__ void zs_stream_call(ZsStreamDev *const *__restrict__ sts, const ZsJobDev *__restrict__ jobs,
-                                               const ZsHeadDev *__restrict__ heads, WideLDS &s_wide) {
+                                               const ZsHeadDev *__restrict__ heads, StreamLDS<D64> &L) {
   ZsStreamDev *__restrict__ st = sts[blockIdx.x];
   const ZsJobDev *__restrict__ job = jobs + blockIdx.x;
   const ZsHeadDev *__restrict__ head = heads + blockIdx.x;
   constexpr uint32_t RING = D64 ? 65536u : 32768u;
-  constexpr uint32_t WOFF = 65536u - RING;  // window bytes used: the newest RING
-  __shared__ __attribute__((aligned(16))) uint8_t s_ring[RING];
-  __shared__ __attribute__((aligned(16))) uint32_t s_in[IN_RING_WORDS];
-  __shared__ uint32_t s_tab[TABLE_ENTRIES];
-  __shared__ uint32_t s_ftab[544];
-  __shared__ uint16_t s_lens[320];
-  __shared__ __attribute__((aligned(16))) uint16_t s_sorted[320];
-  __shared__ uint32_t s_scr[32];
+  uint8_t *s_ring = L.ring;
+  uint32_t *s_in = L.in;
+  uint32_t *s_tab = L.tab;
+  uint32_t *s_ftab = L.ftab;
+  uint16_t *s_lens = L.lens;
+  uint16_t *s_sorted = L.sorted;
+  uint32_t *s_scr = L.scr;
+  L.wide.save = 0;
 
   const uint32_t lane = lane_id();
   const ZsJobDev jb = *job;
@@ -1437,7 +1452,7 @@ __device__ __forceinline__ void zs_stream_call(ZsStreamDev *const *__restrict__ 
   __builtin_amdgcn_wave_barrier();
   if (mode >= ZSM_TYPE && mode <= ZSM_STORED) {
     Inflater<D64, true> f;
-    f.wide = &s_wide;
+    f.wide = &L;
     f.ring = s_ring;
     f.inring = s_in;
     f.tab = s_tab;
@@ -1457,10 +1472,8 @@ __device__ __forceinline__ void zs_stream_call(ZsStreamDev *const *__restrict__ 
     const uint64_t total = st->total_out;
     const uint32_t wbits = st->wbits ? st->wbits : 15u;
     f.whave = (uint32_t)min<uint64_t>(total, 1ull << wbits);
-    if (total) {  // history: window[WOFF + k] is ring position k - RING
-      for (uint32_t k = lane * 16u; k < RING; k += WAVE * 16u)
-        *reinterpret_cast<uint4 *>(&s_ring[k]) = *reinterpret_cast<const uint4 *>(&st->window[WOFF + k]);
-    }
+    // history (window[WOFF + k] is ring position k - RING): loaded by the whole
+    // workgroup before the call (zs_stream_kernel)
     f.fixed_ready = false;
     f.r_mode = (uint32_t)mode;
     f.r_bit = mis * 8u + rbit;
@@ -1484,8 +1497,12 @@ __device__ __forceinline__ void zs_stream_call(ZsStreamDev *const *__restrict__ 
     stop = code == ZD_TRUNC ? (uint32_t)jb.in_len * 8u : f.stop_bits - mis * 8u;
     rbit = f.r_bit - mis * 8u;
     produced = f.pos;
-    // window for the next call: the newest RING bytes, oldest first
-    for (uint32_t k = lane; k < RING; k += WAVE) st->window[WOFF + k] = s_ring[(f.pos + k) & (RING - 1u)];
+    // window for the next call (the newest RING bytes, oldest first): saved
+    // by the whole workgroup after the call (zs_stream_kernel)
+    if (lane == 0) {
+      L.wide.save = 1;
+      L.wide.save_pos = f.pos;
+    }
     const bool dyn = (mode == ZSM_SYMS || mode == ZSM_LIT || mode == ZSM_MATCH) && f.r_btype == 2;
     if (dyn)
       for (uint32_t k = lane; k < f.r_nlen + f.r_ndist; k += WAVE) st->lens[k] = (uint8_t)s_lens[k];
@@ -1516,18 +1533,38 @@ __global__ void __launch_bounds__(WW_T) zs_stream_kernel(ZsStreamDev *const *__r
   // one workgroup per call of the batch (calls of different handles; see
   // zs_launch_stream): wave 0 runs the call's exact state machine, the other
   // waves join its workgroup-wide symbol windows (WideLDS)
-  __shared__ WideLDS s_wide;
-  if (threadIdx.x >= WAVE) {
+  __shared__ StreamLDS<D64> L;
+  constexpr uint32_t RING = StreamLDS<D64>::RING;
+  constexpr uint32_t WOFF = 65536u - RING;
+  const uint32_t t = threadIdx.x;
+  ZsStreamDev *__restrict__ st = sts[blockIdx.x];
+  {  // the handle's history window into the ring, by every wave (a resumed call)
+    const int32_t mode0 = st->mode;
+    if (mode0 >= ZSM_TYPE && mode0 <= ZSM_STORED && st->total_out)
+      for (uint32_t k = t * 16u; k < RING; k += WW_T * 16u)
+        *reinterpret_cast<uint4 *>(&L.ring[k]) = *reinterpret_cast<const uint4 *>(&st->window[WOFF + k]);
+  }
+  __syncthreads();
+  if (t >= WAVE) {
     for (;;) {
       __syncthreads();  // a window posted by wave 0, or the end of the call
-      if (s_wide.op == WW_EXIT) break;
-      ww_run<D64>(s_wide);
+      if (L.wide.op == WW_EXIT) break;
+      ww_run<D64>(L);
     }
-    return;
+  } else {
+    zs_stream_call<D64>(sts, jobs, heads, L);
+    if (t == 0) L.wide.op = WW_EXIT;
+    __syncthreads();
   }
-  zs_stream_call<D64>(sts, jobs, heads, s_wide);
-  if (threadIdx.x == 0) s_wide.op = WW_EXIT;
-  __syncthreads();
+  if (L.wide.save) {  // the newest RING bytes, oldest first, for the next call
+    const uint32_t p0 = L.wide.save_pos;
+    for (uint32_t k = 4u * t; k < RING; k += 4u * WW_T) {
+      const uint32_t v = (uint32_t)L.ring[(p0 + k) & (RING - 1u)] | ((uint32_t)L.ring[(p0 + k + 1u) & (RING - 1u)] << 8) |
+                         ((uint32_t)L.ring[(p0 + k + 2u) & (RING - 1u)] << 16) |
+                         ((uint32_t)L.ring[(p0 + k + 3u) & (RING - 1u)] << 24);
+      *reinterpret_cast<uint32_t *>(&st->window[WOFF + k]) = v;
+    }
+  }
 }
 
 template __global__ void zs_stream_kernel<false>(ZsStreamDev *const *, const ZsJobDev *, const ZsHeadDev *);
