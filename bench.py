@@ -546,7 +546,6 @@ def stream_leg(args, zstreams, np, cpu):
     One handle on a line-text stream (per-stream MiB/s, the figure the shipped WASM's
     493 MiB/s is quoted on), then `stream_handles` handles on their own
     host threads at once (aggregate MiB/s).  Host zlib runs the same schedule beside it."""
-    import threading
 
     import corpus
 
@@ -577,20 +576,26 @@ def stream_leg(args, zstreams, np, cpu):
     calls1 = res[0][2]
 
     outs = [np.empty(each + 65536, dtype=np.uint8) for _ in range(nh)]
-    resm = [None] * nh
+    # the handle set on native host threads (tools/js_driver.c: the same loop, no GIL
+    # between calls -- the caller a native or WASM host is)
+    J = ctypes.CDLL(os.path.join(ROOT, "tools", "libzs_jsdrive.so"))
+    P, S = ctypes.POINTER, ctypes.c_size_t
+    J.zs_js_drive.restype = ctypes.c_double
+    J.zs_js_drive.argtypes = [ctypes.c_char_p, P(ctypes.c_void_p), P(S), P(ctypes.c_void_p), P(S), ctypes.c_int, S,
+                              P(ctypes.c_uint64), P(ctypes.c_int), P(ctypes.c_uint64)]
+    cp = (ctypes.c_void_p * nh)(*[c.ctypes.data for c in cs])
+    cl = (S * nh)(*[len(c) for c in cs])
+    op = (ctypes.c_void_p * nh)(*[o.ctypes.data for o in outs])
+    oc = (S * nh)(*[len(o) for o in outs])
+    prod, codes, ncalls = (ctypes.c_uint64 * nh)(), (ctypes.c_int * nh)(), ctypes.c_uint64(0)
     st0 = zstreams.stream_stats()
-    th = [threading.Thread(target=run_one, args=(cs[k], rs[k], outs[k], resm, k)) for k in range(nh)]
-    t0 = time.perf_counter()
-    for t in th:
-        t.start()
-    for t in th:
-        t.join()
-    tm = time.perf_counter() - t0
+    tm = J.zs_js_drive(zstreams.LIB_PATH.encode(), cp, cl, op, oc, nh, ws, prod, codes, ctypes.byref(ncalls))
+    if tm <= 0:
+        raise RuntimeError(f"zs_js_drive failed ({tm})")
     st1 = zstreams.stream_stats()
     launches = st1["launches"] - st0["launches"]
     calls_m = st1["calls"] - st0["calls"]
-    okm = all(resm[k] is not None and resm[k][0] == each and resm[k][1] == 1 and np.array_equal(outs[k][:each], rs[k])
-              for k in range(nh))
+    okm = all(prod[k] == each and codes[k] == 1 and np.array_equal(outs[k][:each], rs[k]) for k in range(nh))
 
     # host zlib, same schedule: the one stream on 1 thread; the handle set on all cores
     C = _cpulib()
@@ -623,7 +628,8 @@ def stream_leg(args, zstreams, np, cpu):
                        "host zlib L6 raw (-15)", "calls": calls1, "us_per_call": round(t1 * 1e6 / calls1, 1),
                        "verified": bool(ok1)},
         "handles": {"value": round(mibm, 1), "unit": "MiB/s (aggregate)", "handles": nh,
-                    "stream": f"{nh} x {args.stream_handle_mib} MiB line text (ids 32..), one host thread per handle",
+                    "stream": f"{nh} x {args.stream_handle_mib} MiB line text (ids 32..), one native host thread per "
+                              "handle (tools/js_driver.c)",
                     "launches": launches, "calls_per_launch": round(calls_m / max(1, launches), 1),
                     "verified": bool(okm)},
         "wasm_reference_mibs": 493,

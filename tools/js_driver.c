@@ -1,0 +1,127 @@
+/* js_driver.c -- native host threads driving the handle ABI with the reference
+ * JS call schedule (src/wasm/api/zlib-streams.js:64-136), for bench.py's
+ * aggregate stream leg: 64 KiB writes, <= 32 KiB per inflate_process, a 64 KiB
+ * output buffer per call, advance by inflate_last_consumed, stop a write on 0,
+ * then Z_FINISH drains.  The library is dlopen'ed by path (the product .so), so
+ * the same loop shape as oracle/cpu_baseline.c's host-zlib driver runs on
+ * native threads instead of Python threads holding the GIL between calls.
+ *
+ * Bench tooling only: not part of the product library. */
+#include <dlfcn.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+typedef uintptr_t (*new_fn)(void);
+typedef int (*init_fn)(uintptr_t);
+typedef int (*proc_fn)(uintptr_t, uintptr_t, unsigned, uintptr_t, unsigned, int);
+typedef int (*end_fn)(uintptr_t);
+typedef unsigned (*cons_fn)(uintptr_t);
+
+typedef struct {
+  new_fn f_new;
+  init_fn f_init;
+  proc_fn f_proc;
+  end_fn f_end;
+  cons_fn f_cons;
+} api_t;
+
+typedef struct {
+  const api_t *api;
+  const uint8_t *comp;
+  size_t comp_len, write_size, out_cap;
+  uint8_t *out;
+  uint64_t produced, calls;
+  int code;
+} job_t;
+
+static int unpack(uint32_t r, uint32_t *got) {
+  *got = r & 0xffffffu;
+  return (r >> 31) ? (int)(r >> 24) - 256 : (int)(r >> 24);
+}
+
+static void *run_job(void *arg) {
+  job_t *j = (job_t *)arg;
+  const api_t *a = j->api;
+  const uintptr_t h = a->f_new();
+  a->f_init(h);
+  size_t put = 0;
+  int code = 0;
+  uint64_t calls = 0;
+  for (size_t w = 0; w < j->comp_len && code >= 0; w += j->write_size) {
+    const size_t ln = j->comp_len - w < j->write_size ? j->comp_len - w : j->write_size;
+    size_t off = 0;
+    while (off < ln) {
+      const size_t k = ln - off < 32768 ? ln - off : 32768;
+      uint32_t got;
+      const size_t room = j->out_cap - put < 65536 ? j->out_cap - put : 65536;
+      code = unpack((uint32_t)a->f_proc(h, (uintptr_t)(j->comp + w + off), (unsigned)k, (uintptr_t)(j->out + put),
+                                        (unsigned)room, 0),
+                    &got);
+      calls++;
+      put += got;
+      if (code < 0) break;
+      const unsigned c = a->f_cons(h);
+      if (c == 0) break;
+      off += c;
+    }
+  }
+  while (code >= 0) {
+    uint32_t got;
+    const size_t room = j->out_cap - put < 65536 ? j->out_cap - put : 65536;
+    code = unpack((uint32_t)a->f_proc(h, 0, 0, (uintptr_t)(j->out + put), (unsigned)room, 4), &got);
+    calls++;
+    put += got;
+    if (code == 1 || got == 0) break;
+  }
+  a->f_end(h);
+  j->produced = put;
+  j->calls = calls;
+  j->code = code;
+  return NULL;
+}
+
+/* n streams, one native thread each; produced[k] / codes[k] per stream.
+ * Returns wall seconds, or a negative value (-1: library/symbols, -2: threads). */
+double zs_js_drive(const char *lib_path, const uint8_t *const *comp, const size_t *comp_len, uint8_t *const *out,
+                   const size_t *out_cap, int n, size_t write_size, uint64_t *produced, int *codes,
+                   uint64_t *total_calls) {
+  void *lib = dlopen(lib_path, RTLD_NOW | RTLD_LOCAL);
+  if (!lib) return -1.0;
+  api_t a;
+  a.f_new = (new_fn)dlsym(lib, "inflate_new");
+  a.f_init = (init_fn)dlsym(lib, "inflate_init_raw");
+  a.f_proc = (proc_fn)dlsym(lib, "inflate_process");
+  a.f_end = (end_fn)dlsym(lib, "inflate_end");
+  a.f_cons = (cons_fn)dlsym(lib, "inflate_last_consumed");
+  if (!a.f_new || !a.f_init || !a.f_proc || !a.f_end || !a.f_cons) return -1.0;
+  job_t *js = (job_t *)calloc((size_t)n, sizeof(job_t));
+  pthread_t *th = (pthread_t *)calloc((size_t)n, sizeof(pthread_t));
+  if (!js || !th) {
+    free(js);
+    free(th);
+    return -2.0;
+  }
+  struct timespec t0, t1;
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  int started = 0;
+  for (int k = 0; k < n; k++) {
+    js[k] = (job_t){&a, comp[k], comp_len[k], write_size, out_cap[k], out[k], 0, 0, 0};
+    if (pthread_create(&th[k], NULL, run_job, &js[k]) != 0) break;
+    started++;
+  }
+  uint64_t calls = 0;
+  for (int k = 0; k < started; k++) {
+    pthread_join(th[k], NULL);
+    produced[k] = js[k].produced;
+    codes[k] = js[k].code;
+    calls += js[k].calls;
+  }
+  clock_gettime(CLOCK_MONOTONIC, &t1);
+  *total_calls = calls;
+  free(js);
+  free(th);
+  return started < n ? -2.0 : (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}

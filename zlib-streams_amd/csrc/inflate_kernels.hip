@@ -30,13 +30,18 @@
 #include "zs_kprof.h"
 
 #if KP_ON
-__device__ unsigned long long g_kprof_w[16];  // KP_W_* - 64
+__device__ unsigned long long g_kprof_w[32];  // KP_W_* - 64
 #define KPW_ADD(i, v)                                                          \
   do {                                                                         \
     if (lane_id() == 0) atomicAdd(&g_kprof_w[(i) - 64], (unsigned long long)(v)); \
   } while (0)
+#define KPW0_ADD(i, v)                                                          \
+  do {                                                                          \
+    if (threadIdx.x == 0) atomicAdd(&g_kprof_w[(i) - 64], (unsigned long long)(v)); \
+  } while (0)
 #else
 #define KPW_ADD(i, v) ((void)0)
+#define KPW0_ADD(i, v) ((void)0)
 #endif
 
 #define IN_RING_WORDS 1024   // 4 KiB compressed-input ring
@@ -189,8 +194,11 @@ __global__ void zs_header_kernel(const ZsJobDev *__restrict__ jobs, ZsHeadDev *_
 #define WW_OFFS 8u                 // bit offsets per thread
 #define WW_BITS (WW_T * WW_OFFS)   // 8 192-bit window
 #define WW_JN (WW_BITS + 64u)      // jump-table entries (a symbol is <= 48 bits)
-#define WW_STEP (4u * WW_T)        // bytes expanded per step
+#define WW_SKIP 32u                // J5: 32-symbol jumps
+#define WW_EB 8u                   // bytes expanded per thread and step
+#define WW_STEP (WW_EB * WW_T)     // bytes expanded per step
 #define WW_TCAP 16384u             // bytes per window (the ring keeps the unflushed tail)
+#define WW_MIN_ROOM 512u           // output room below which the serial loop runs
 #define WW_RUN 1u
 #define WW_EXIT 2u
 
@@ -201,14 +209,18 @@ struct WideLDS {
   // results and reductions
   uint32_t n, T, endrel, cnt_min, n_min, carry, open;
   uint32_t save, save_pos;     // end of the call: the history ring goes to the handle's state
+  uint32_t tab_in, tab_out;    // cached dynamic tables (ZsStreamDev::tab_bits) loaded / to save
   uint32_t wtot[WW_T / 64];
-  uint32_t S[WW_T];            // chain: start bit (window-relative) of symbol k
+  uint32_t sk[WW_T / WW_SKIP];   // chain start of symbols 32 m
   uint32_t symL[WW_T], symD[WW_T];
   uint8_t nb[WW_JN];           // symbol bits at each offset (0: no plain symbol starts there)
-  __attribute__((aligned(16))) uint16_t ja[WW_JN];
-  __attribute__((aligned(16))) uint16_t jb[WW_JN];  // + ja: marks / expansion entries later
+  __attribute__((aligned(16))) uint16_t ja[WW_JN];  // J0 (one symbol) -- kept
+  __attribute__((aligned(16))) uint16_t jb[WW_JN];  // J1 .. J5, ping-pong with jc
+  __attribute__((aligned(16))) uint16_t jc[WW_JN];
 };
-static_assert(sizeof(uint16_t) * WW_JN * 2 >= WW_STEP * 6, "expansion marks + entries alias the jump tables");
+// expansion marks (u16) + entries (u32) of one step alias the three jump tables
+static_assert(sizeof(uint16_t) * WW_JN * 3 >= WW_STEP * 6, "expansion marks + entries alias the jump tables");
+static_assert(ZS_STREAM_TAB_WORDS == TABLE_ENTRIES, "ZsStreamDev::tab holds one table set");
 
 // All LDS of one stream-kernel workgroup in one object, so every wave reaches
 // it through the same LDS addresses (ds_* instructions, not flat ones)
@@ -243,17 +255,28 @@ __device__ __forceinline__ uint32_t ww_scan_max(uint32_t v) {  // inclusive, wav
   v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));
   return v;
 }
-// workgroup inclusive scan (sum or max) of one value per thread
+// workgroup scan (sum or max) of one value per thread: inclusive, and the
+// exclusive value (the inclusive one of thread t - 1; 0 for thread 0)
 template <bool MAX>
-__device__ __forceinline__ uint32_t ww_scan(WideLDS &w, uint32_t v) {
+__device__ __forceinline__ uint32_t ww_scan(WideLDS &w, uint32_t v, uint32_t *excl) {
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
   const uint32_t inc = MAX ? ww_scan_max(v) : ww_scan_sum(v);
+  const uint32_t up = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane ? lane - 1u : 0u) << 2), (int)inc);
   if (lane == 63) w.wtot[wv] = inc;
   __syncthreads();
   uint32_t pre = 0;
   for (uint32_t k = 0; k < wv; k++) pre = MAX ? max(pre, w.wtot[k]) : pre + w.wtot[k];
   __syncthreads();  // wtot is reused by the next scan
+  const uint32_t own = lane ? up : 0u;
+  *excl = MAX ? max(pre, own) : pre + own;
   return MAX ? max(pre, inc) : pre + inc;
+}
+
+// index of the first thread whose flag is set (WW_T if none) into *dst (a
+// word set to WW_T beforehand): one LDS atomic per wave
+__device__ __forceinline__ void ww_first(uint32_t *dst, bool flag) {
+  const uint64_t m = __ballot(flag);
+  if (m && (threadIdx.x & 63u) == 0) atomicMin(dst, (threadIdx.x & ~63u) + (uint32_t)__builtin_ctzll(m));
 }
 
 __device__ __forceinline__ uint64_t ww_bits_at(const uint32_t *inring, uint32_t q) {
@@ -326,6 +349,7 @@ __device__ void ww_run(StreamLDS<D64> &Ls) {
   const uint32_t *dt = reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(&Ls) + w.dt_off);
   const uint32_t t = threadIdx.x;
   const uint32_t P = w.P, W = w.W;
+  [[maybe_unused]] const uint64_t kt0 = KP_NOW();
   // 1. a complete symbol at every offset of the window
   uint32_t lv[WW_OFFS], dv[WW_OFFS];
 #pragma unroll
@@ -342,34 +366,45 @@ __device__ void ww_run(StreamLDS<D64> &Ls) {
     w.ja[WW_BITS + t] = (uint16_t)(WW_BITS + t);
   }
   if (t == 0) {
-    w.S[0] = 0;
     w.cnt_min = WW_T;
     w.n_min = WW_T;
   }
-  // 2. pointer doubling: S[k] = start of the chain's k-th symbol
-  uint16_t *ja = w.ja, *jb = w.jb;
+  // 2. the chain from the window start: J5 = 32 symbols per jump (five
+  //    compositions of J0), a serial walk of J5 for every 32nd symbol, then
+  //    each thread walks J0 from its group's start (<= 31 steps)
+  [[maybe_unused]] const uint64_t kt1 = KP_NOW();
+  {
+    const uint16_t *src = w.ja;
+    uint16_t *dst = w.jb;
 #pragma unroll 1
-  for (uint32_t k = 0; k < 10; k++) {
-    __syncthreads();
-    const uint32_t half = 1u << k;
-    if (t >= half && t < 2u * half) w.S[t] = ja[w.S[t - half]];
-    if (k < 9) {
+    for (uint32_t k = 0; k < 5; k++) {
+      __syncthreads();
 #pragma unroll
       for (uint32_t i = 0; i < WW_OFFS; i++) {
         const uint32_t q = t + i * WW_T;
-        jb[q] = ja[ja[q]];
+        dst[q] = src[src[q]];
       }
-      if (t < WW_JN - WW_BITS) jb[WW_BITS + t] = (uint16_t)(WW_BITS + t);
-      uint16_t *x = ja;
-      ja = jb;
-      jb = x;
+      if (t < WW_JN - WW_BITS) dst[WW_BITS + t] = (uint16_t)(WW_BITS + t);
+      src = dst;
+      dst = dst == w.jb ? w.jc : w.jb;
     }
+    __syncthreads();
+    KPW0_ADD(KP_W_CYC_COMPOSE, KP_NOW() - kt1);
+    if (t == 0) {
+      uint32_t x = 0;
+      for (uint32_t m = 0; m < WW_T / WW_SKIP; m++) {
+        w.sk[m] = x;
+        x = src[x];
+      }
+    }
+    __syncthreads();
   }
-  __syncthreads();
+  uint32_t s = w.sk[t / WW_SKIP];
+  for (uint32_t r = t % WW_SKIP; r; r--) s = w.ja[s];
+  KPW0_ADD(KP_W_CYC_WALK, KP_NOW() - kt1);  // compose + walks (thread 0 walks the J5 chain)
   // 3. the chain's symbols: inside the window and plain
-  const uint32_t s = w.S[t];
   const uint32_t snb = s < WW_BITS ? w.nb[s] : 0u;
-  if (!(s < W && snb != 0)) atomicMin(&w.cnt_min, t);
+  ww_first(&w.cnt_min, !(s < W && snb != 0));
   uint16_t *mark = w.jb;  // the jump tables are done with
 #pragma unroll
   for (uint32_t i = 0; i < WW_OFFS; i++) mark[t + i * WW_T] = 0;
@@ -391,11 +426,10 @@ __device__ void ww_run(StreamLDS<D64> &Ls) {
   const uint32_t L = act ? w.symL[t] : 0u, D = act ? w.symD[t] : 0u;
   const bool lit = (L & 0x80000000u) != 0;
   const uint32_t olen = act ? (lit ? 1u : L) : 0u;
-  const uint32_t incl = ww_scan<false>(w, olen);
-  const uint32_t ost = incl - olen;
+  uint32_t ost;
+  const uint32_t incl = ww_scan<false>(w, olen, &ost);
   const uint32_t room = min(w.cap - w.pos, WW_TCAP);
-  const bool ok = act && incl <= room && (lit || D <= w.pos + ost + w.whave);
-  if (!ok) atomicMin(&w.n_min, t);
+  ww_first(&w.n_min, !(act && incl <= room && (lit || D <= w.pos + ost + w.whave)));
   __syncthreads();
   const uint32_t n = w.n_min;
   if (n > 0 && t == n - 1u) w.T = incl;
@@ -404,72 +438,78 @@ __device__ void ww_run(StreamLDS<D64> &Ls) {
   if (t == 0) w.carry = 0;
   __syncthreads();
   const uint32_t T = w.T;
-  // 5. expansion, WW_STEP bytes per step, 4 consecutive per thread
+  [[maybe_unused]] const uint64_t kt2 = KP_NOW();
+  KPW0_ADD(KP_W_CYC_DECODE, kt1 - kt0);
+  KPW0_ADD(KP_W_CYC_CHAIN, kt2 - kt1);
+  // 5. expansion, WW_STEP bytes per step, WW_EB consecutive per thread
   const uint32_t base = w.pos;
-  uint16_t *marks = w.ja;                                   // WW_STEP u16
-  uint32_t *ent = reinterpret_cast<uint32_t *>(w.ja + WW_STEP);  // WW_STEP u32 (ja tail + jb)
+  uint16_t *marks = w.ja;                                        // WW_STEP u16
+  uint32_t *ent = reinterpret_cast<uint32_t *>(w.ja + WW_STEP);  // WW_STEP u32 (into jb / jc)
   for (uint32_t b0 = 0; b0 < T; b0 += WW_STEP) {
-    reinterpret_cast<uint2 *>(marks)[t] = make_uint2(0u, 0u);
+    reinterpret_cast<uint4 *>(marks)[t] = make_uint4(0u, 0u, 0u, 0u);
     __syncthreads();
     if (t < n && ost >= b0 && ost < b0 + WW_STEP) marks[ost - b0] = (uint16_t)(t + 1u);
     __syncthreads();
-    const uint2 mk = reinterpret_cast<const uint2 *>(marks)[t];
-    uint32_t mm[4] = {mk.x & 0xffffu, mk.x >> 16, mk.y & 0xffffu, mk.y >> 16};
-    mm[1] = max(mm[1], mm[0]);
-    mm[2] = max(mm[2], mm[1]);
-    mm[3] = max(mm[3], mm[2]);
+    const uint4 mk = reinterpret_cast<const uint4 *>(marks)[t];
+    uint32_t mm[WW_EB] = {mk.x & 0xffffu, mk.x >> 16, mk.y & 0xffffu, mk.y >> 16,
+                          mk.z & 0xffffu, mk.z >> 16, mk.w & 0xffffu, mk.w >> 16};
+#pragma unroll
+    for (uint32_t r = 1; r < WW_EB; r++) mm[r] = max(mm[r], mm[r - 1]);
     const uint32_t carry = w.carry;
-    // symbol of each byte: the last mark at or before it (an inclusive max
-    // scan; the thread's bytes before its own first mark continue the symbol
-    // open at the end of thread t - 1, or of the previous step)
-    const uint32_t inc = ww_scan<true>(w, mm[3]);
-    w.S[t] = inc;  // the chain starts are in registers now
-    __syncthreads();
-    const uint32_t pv = max(t ? w.S[t - 1u] : 0u, carry + 1u);
-    __syncthreads();
-    uint32_t e[4];
+    // symbol of each byte: the last mark at or before it; the thread's bytes
+    // before its own first mark continue the symbol open at the end of thread
+    // t - 1, or of the previous step
+    uint32_t pin;
+    (void)ww_scan<true>(w, mm[WW_EB - 1], &pin);
+    const uint32_t pv = max(pin, carry + 1u);
+    uint32_t e[WW_EB];
     bool open = false;
 #pragma unroll
-    for (uint32_t r = 0; r < 4; r++) {
+    for (uint32_t r = 0; r < WW_EB; r++) {
       const uint32_t si = max(pv, mm[r]) - 1u;
-      if (r == 3 && t == WW_T - 1u) w.carry = si;
+      if (r == WW_EB - 1 && t == WW_T - 1u) w.carry = si;
       const uint32_t Ls = w.symL[si], Ds = w.symD[si];
-      const uint32_t j = b0 + 4u * t + r;
+      const uint32_t j = b0 + WW_EB * t + r;
       const int32_t sp = (int32_t)j - (int32_t)Ds;  // relative to `base`
       const uint32_t rv = ring[(base + (uint32_t)sp) & RMASK];
       e[r] = (Ls & 0x80000000u) ? (0x100u | (Ls & 0xffu))
                                 : (sp >= (int32_t)b0 ? (((uint32_t)sp - b0) << 16) : (0x100u | rv));
       open = open || (j < T && !(e[r] & 0x100u));
     }
-    reinterpret_cast<uint4 *>(ent)[t] = make_uint4(e[0], e[1], e[2], e[3]);
+    reinterpret_cast<uint4 *>(ent)[2u * t] = make_uint4(e[0], e[1], e[2], e[3]);
+    reinterpret_cast<uint4 *>(ent)[2u * t + 1u] = make_uint4(e[4], e[5], e[6], e[7]);
     if (t == 0) w.open = 0;
     __syncthreads();
-    if (open) atomicOr(&w.open, 1u);
+    if (__ballot(open) && (t & 63u) == 0) atomicOr(&w.open, 1u);
     __syncthreads();
     while (w.open) {
-      uint32_t g[4];
+      KPW0_ADD(KP_W_JUMPS, 1);
+      uint32_t g[WW_EB];
 #pragma unroll
-      for (uint32_t r = 0; r < 4; r++) g[r] = ent[(e[r] & 0x100u) ? 0u : (e[r] >> 16)];
+      for (uint32_t r = 0; r < WW_EB; r++) g[r] = ent[(e[r] & 0x100u) ? 0u : (e[r] >> 16)];
       open = false;
 #pragma unroll
-      for (uint32_t r = 0; r < 4; r++) {
+      for (uint32_t r = 0; r < WW_EB; r++) {
         if (!(e[r] & 0x100u)) e[r] = (g[r] & 0x100u) ? g[r] : (g[r] & 0xffff0000u);
-        open = open || (b0 + 4u * t + r < T && !(e[r] & 0x100u));
+        open = open || (b0 + WW_EB * t + r < T && !(e[r] & 0x100u));
       }
       __syncthreads();
-      reinterpret_cast<uint4 *>(ent)[t] = make_uint4(e[0], e[1], e[2], e[3]);
+      reinterpret_cast<uint4 *>(ent)[2u * t] = make_uint4(e[0], e[1], e[2], e[3]);
+      reinterpret_cast<uint4 *>(ent)[2u * t + 1u] = make_uint4(e[4], e[5], e[6], e[7]);
       if (t == 0) w.open = 0;
       __syncthreads();
-      if (open) atomicOr(&w.open, 1u);
+      if (__ballot(open) && (t & 63u) == 0) atomicOr(&w.open, 1u);
       __syncthreads();
     }
 #pragma unroll
-    for (uint32_t r = 0; r < 4; r++) {
-      const uint32_t j = b0 + 4u * t + r;
+    for (uint32_t r = 0; r < WW_EB; r++) {
+      const uint32_t j = b0 + WW_EB * t + r;
       if (j < T) ring[(base + j) & RMASK] = (uint8_t)e[r];
     }
     __syncthreads();
   }
+  KPW0_ADD(KP_W_BATCHES, (T + WW_STEP - 1) / WW_STEP);
+  KPW0_ADD(KP_W_CYC_EXPAND, KP_NOW() - kt2);
 }
 
 template <bool D64, bool WIDE = false>
@@ -480,6 +520,7 @@ struct Inflater {
   uint8_t *ring;       // LDS history ring
   uint32_t *inring;    // LDS compressed-input ring
   uint32_t *tab;       // LDS dynamic tables
+  uint32_t tab_bits = 0;  // tab holds built dynamic tables: lbits | dbits << 8 | 1 << 16
   uint32_t *ftab;      // LDS fixed tables (built on first use)
   uint16_t *lens;      // LDS code lengths
   uint16_t *sorted;    // LDS sort scratch
@@ -704,6 +745,7 @@ struct Inflater {
       return ZD_ERROR | (ZM_DIST_SET << 8);
     *lt = tab;
     *dt = tab + 852;
+    tab_bits = *lbits | (*dbits << 8) | (1u << 16);
     return -1;
   }
 
@@ -1120,8 +1162,18 @@ struct Inflater {
   // of WW_T threads): post the window, take part in it, apply its prefix.
   StreamLDS<D64> *wide = nullptr;  // the workgroup's LDS (WIDE)
   __device__ uint32_t wide_window(const uint32_t *lt, const uint32_t *dt, uint32_t lmask, uint32_t dmask) {
+    [[maybe_unused]] const uint64_t kq0 = KP_NOW();
     const uint32_t P = bitpos();
-    if (pos == cap || P + 64u + 1024u > limit_bits) return 0;
+    // not worth a window: little output room, little input, or the next
+    // symbol is not plain (end of block) -- the serial loop takes these
+    if (cap - pos < WW_MIN_ROOM || P + 64u + 1024u > limit_bits) return 0;
+    refill();
+    {
+      uint32_t e = lt[(uint32_t)hold & lmask];
+      uint32_t op = e_op(e);
+      if (op != 0 && (op & 0xf0u) == 0) op = e_op(lt[e_val(e) + (((uint32_t)(hold >> e_bits(e))) & ((1u << op) - 1))]);
+      if (op & 96u) return 0;
+    }
     const uint32_t W = min(WW_BITS, ((limit_bits - P - 64u) / 1024u) * 1024u);
     ensure_words(((P + W + 64u) >> 5) + 3u);
     WideLDS &w = wide->wide;
@@ -1139,9 +1191,13 @@ struct Inflater {
       w.lt_off = (uint32_t)(reinterpret_cast<const uint8_t *>(lt) - lb);
       w.dt_off = (uint32_t)(reinterpret_cast<const uint8_t *>(dt) - lb);
     }
+    [[maybe_unused]] const uint64_t kw0 = KP_NOW();
+    KPW_ADD(KP_W_CYC_PRE, kw0 - kq0);
     __syncthreads();  // the other waves wait here for a window
     ww_run<D64>(*wide);
     const uint32_t n = w.n_min, T = w.T, endrel = w.endrel;
+    [[maybe_unused]] const uint64_t kw1 = KP_NOW();
+    KPW_ADD(KP_W_CYC_WINDOW, kw1 - kw0);
     KPW_ADD(KP_W_WINDOWS, 1);
     if (n == 0) {
       KPW_ADD(KP_W_EMPTY, 1);
@@ -1150,6 +1206,7 @@ struct Inflater {
     pos += T;
     maybe_flush();
     reseat(P + endrel);
+    KPW_ADD(KP_W_CYC_POST, KP_NOW() - kw1);
     KPW_ADD(KP_W_SYMS, n);
     KPW_ADD(KP_W_BYTES, T);
     return n;
@@ -1276,7 +1333,14 @@ struct Inflater {
       if (r_btype == 1) {
         if (!fixed_ready) build_fixed();
       } else {
-        dyn_tables(r_nlen, r_ndist, &lt, &dt, &lbits, &dbits);  // built once already: cannot fail
+        if (tab_bits >> 16) {  // the tables a previous call built (zs_stream_kernel loaded them)
+          lt = tab;
+          dt = tab + 852;
+          lbits = tab_bits & 0xffu;
+          dbits = (tab_bits >> 8) & 0xffu;
+        } else {
+          dyn_tables(r_nlen, r_ndist, &lt, &dt, &lbits, &dbits);  // built once already: cannot fail
+        }
       }
       if (mode == ZSM_LIT) {
         if (pos == cap) {
@@ -1302,7 +1366,9 @@ struct Inflater {
           stop_bits = bitpos();
           return ZD_STOP;
         }
+        [[maybe_unused]] const uint64_t kh0 = KP_NOW();
         rc = block_header(&lt, &dt, &lbits, &dbits);
+        KPW_ADD(KP_W_CYC_TABLES, KP_NOW() - kh0);
         if (rc == -2) continue;
         if (rc >= 0) return rc;
       }
@@ -1406,7 +1472,6 @@ __device__ __forceinline__ void zs_stream_call(ZsStreamDev *const *__restrict__ 
   ZsStreamDev *__restrict__ st = sts[blockIdx.x];
   const ZsJobDev *__restrict__ job = jobs + blockIdx.x;
   const ZsHeadDev *__restrict__ head = heads + blockIdx.x;
-  constexpr uint32_t RING = D64 ? 65536u : 32768u;
   uint8_t *s_ring = L.ring;
   uint32_t *s_in = L.in;
   uint32_t *s_tab = L.tab;
@@ -1483,13 +1548,17 @@ __device__ __forceinline__ void zs_stream_call(ZsStreamDev *const *__restrict__ 
     f.r_nlen = st->nlen;
     f.r_ndist = st->ndist;
     f.blast = st->last != 0;
+    f.tab_bits = L.wide.tab_in;  // tables loaded by the workgroup (zs_stream_kernel), or 0
     if (mode != ZSM_TYPE && mode != ZSM_STORED && f.r_btype == 2)
       for (uint32_t k = lane; k < f.r_nlen + f.r_ndist; k += WAVE) s_lens[k] = st->lens[k];
     __builtin_amdgcn_wave_barrier();
     f.seek(mis * 8u + rbit);
     f.stop_bits = 0;
+    [[maybe_unused]] const uint64_t kc0 = KP_NOW();
     const int packed = f.run((uint32_t)mode);
     f.flush_tail();
+    KPW_ADD(KP_W_WAVES, 1);
+    KPW_ADD(KP_W_CYC_TOTAL, KP_NOW() - kc0);
     __builtin_amdgcn_wave_barrier();
     code = packed & 0xff;
     msg = packed >> 8;
@@ -1504,6 +1573,7 @@ __device__ __forceinline__ void zs_stream_call(ZsStreamDev *const *__restrict__ 
       L.wide.save_pos = f.pos;
     }
     const bool dyn = (mode == ZSM_SYMS || mode == ZSM_LIT || mode == ZSM_MATCH) && f.r_btype == 2;
+    if (lane == 0) L.wide.tab_out = dyn ? f.tab_bits : 0u;  // saved with the window after the call
     if (dyn)
       for (uint32_t k = lane; k < f.r_nlen + f.r_ndist; k += WAVE) st->lens[k] = (uint8_t)s_lens[k];
     if (lane == 0) {
@@ -1543,6 +1613,14 @@ __global__ void __launch_bounds__(WW_T) zs_stream_kernel(ZsStreamDev *const *__r
     if (mode0 >= ZSM_TYPE && mode0 <= ZSM_STORED && st->total_out)
       for (uint32_t k = t * 16u; k < RING; k += WW_T * 16u)
         *reinterpret_cast<uint4 *>(&L.ring[k]) = *reinterpret_cast<const uint4 *>(&st->window[WOFF + k]);
+    // and the tables of a dynamic block in progress (built by an earlier call)
+    const uint32_t tb = ((mode0 == ZSM_SYMS || mode0 == ZSM_LIT || mode0 == ZSM_MATCH) && st->btype == 2) ? st->tab_bits : 0u;
+    if (tb >> 16)
+      for (uint32_t k = t; k < TABLE_ENTRIES; k += WW_T) L.tab[k] = st->tab[k];
+    if (t == 0) {
+      L.wide.tab_in = tb;
+      L.wide.tab_out = 0;
+    }
   }
   __syncthreads();
   if (t >= WAVE) {
@@ -1565,15 +1643,40 @@ __global__ void __launch_bounds__(WW_T) zs_stream_kernel(ZsStreamDev *const *__r
       *reinterpret_cast<uint32_t *>(&st->window[WOFF + k]) = v;
     }
   }
+  {  // the current dynamic block's tables for the next call
+    const uint32_t tb = L.wide.tab_out;
+    if (tb >> 16)
+      for (uint32_t k = t; k < TABLE_ENTRIES; k += WW_T) st->tab[k] = L.tab[k];
+    if (t == 0) st->tab_bits = tb;
+  }
 }
 
 template __global__ void zs_stream_kernel<false>(ZsStreamDev *const *, const ZsJobDev *, const ZsHeadDev *);
 template __global__ void zs_stream_kernel<true>(ZsStreamDev *const *, const ZsJobDev *, const ZsHeadDev *);
 
-// check contributions of the call's output (zs_check.h accumulators)
+// The calls' inputs from host-mapped staging into their device buffers, and
+// the carried restart bit (a workgroup column per call; before the decode).
+#define SIO_THREADS 256
+__global__ void __launch_bounds__(SIO_THREADS) zs_stream_in_kernel(ZsStreamDev *const *__restrict__ sts,
+                                                                   const ZsJobDev *__restrict__ jobs,
+                                                                   const ZsStreamIo *__restrict__ io) {
+  const ZsStreamIo c = io[blockIdx.y];
+  if (blockIdx.x == 0 && threadIdx.x == 0) sts[blockIdx.y]->rbit = c.rbit;
+  if (!c.hin) return;
+  const uint64_t n = jobs[blockIdx.y].in_len;
+  uint8_t *dst = const_cast<uint8_t *>(jobs[blockIdx.y].in);
+  const uint64_t nw = n / 16u;
+  for (uint64_t k = (uint64_t)blockIdx.x * SIO_THREADS + threadIdx.x; k < nw; k += (uint64_t)gridDim.x * SIO_THREADS)
+    reinterpret_cast<uint4 *>(dst)[k] = reinterpret_cast<const uint4 *>(c.hin)[k];
+  if (blockIdx.x == 0 && threadIdx.x < (n & 15u)) dst[nw * 16u + threadIdx.x] = c.hin[nw * 16u + threadIdx.x];
+}
+
+// The call's output to its host-mapped staging, and its check contributions
+// (zs_check.h accumulators); a workgroup per (piece, call).
 #define SCHECK_THREADS 256
 __global__ void __launch_bounds__(SCHECK_THREADS) zs_stream_check_kernel(ZsStreamDev *const *__restrict__ sts,
-                                                                         const ZsJobDev *__restrict__ jobs) {
+                                                                         const ZsJobDev *__restrict__ jobs,
+                                                                         const ZsStreamIo *__restrict__ io) {
   ZsStreamDev *__restrict__ st = sts[blockIdx.y];
   const ZsJobDev *__restrict__ job = jobs + blockIdx.y;
   __shared__ uint32_t s_tab[4][256];
@@ -1581,12 +1684,19 @@ __global__ void __launch_bounds__(SCHECK_THREADS) zs_stream_check_kernel(ZsStrea
   const uint32_t t = threadIdx.x;
   const int gz = st->is_gzip;
   const uint64_t n = st->produced;
-  if (gz < 0 || n == 0 || st->mode == ZSM_HEAD) return;
+  if (n == 0 || st->mode == ZSM_HEAD) return;
   const uint8_t *p = job->out;
   const uint64_t piece = max<uint64_t>(4096u, ((n + gridDim.x - 1) / gridDim.x + 1023u) & ~1023ull);
   const uint64_t p0 = (uint64_t)blockIdx.x * piece;
   if (p0 >= n) return;
   const uint64_t plen = min(piece, n - p0);
+  if (uint8_t *h = io[blockIdx.y].hout) {  // p0 is a multiple of 1024: 16-byte words
+    const uint64_t nw = plen / 16u;
+    for (uint64_t k = t; k < nw; k += SCHECK_THREADS)
+      reinterpret_cast<uint4 *>(h + p0)[k] = reinterpret_cast<const uint4 *>(p + p0)[k];
+    if (t < (plen & 15u)) h[p0 + nw * 16u + t] = p[p0 + nw * 16u + t];
+  }
+  if (gz < 0) return;
   const uint64_t per = ((plen + SCHECK_THREADS - 1) / SCHECK_THREADS + 3u) & ~3ull;
   const uint64_t lo = p0 + min(plen, per * t), hi = p0 + min(plen, per * (t + 1));
   if (gz == 1) {
@@ -1692,15 +1802,17 @@ __global__ void zs_stream_finish_kernel(ZsStreamDev *const *__restrict__ sts, co
 // different handles into one launch): [wrapper headers] -> resumable decode
 // (a workgroup per call) -> checks -> trailers -> outcome gather.
 extern "C" void zs_launch_stream(int d64, int run_header, ZsStreamDev *const *d_sts, const ZsJobDev *d_jobs,
-                                 ZsHeadDev *d_heads, uint32_t n, uint64_t max_out_cap, ZsStreamRes *d_res,
-                                 hipStream_t stream) {
+                                 ZsHeadDev *d_heads, const ZsStreamIo *io, uint32_t n, uint64_t max_in_len,
+                                 uint64_t max_out_cap, ZsStreamRes *d_res, hipStream_t stream) {
+  const uint32_t in_pieces = (uint32_t)std::min<uint64_t>(256, std::max<uint64_t>(1, (max_in_len + 16383) / 16384));
+  hipLaunchKernelGGL(zs_stream_in_kernel, dim3(in_pieces, n), dim3(SIO_THREADS), 0, stream, d_sts, d_jobs, io);
   if (run_header) hipLaunchKernelGGL(zs_header_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, d_jobs, d_heads, n);
   if (d64)
     hipLaunchKernelGGL(zs_stream_kernel<true>, dim3(n), dim3(WW_T), 0, stream, d_sts, d_jobs, d_heads);
   else
     hipLaunchKernelGGL(zs_stream_kernel<false>, dim3(n), dim3(WW_T), 0, stream, d_sts, d_jobs, d_heads);
-  const uint32_t pieces = (uint32_t)std::min<uint64_t>(1024, std::max<uint64_t>(1, (max_out_cap + 65535) / 65536));
-  hipLaunchKernelGGL(zs_stream_check_kernel, dim3(pieces, n), dim3(SCHECK_THREADS), 0, stream, d_sts, d_jobs);
+  const uint32_t pieces = (uint32_t)std::min<uint64_t>(1024, std::max<uint64_t>(1, (max_out_cap + 16383) / 16384));
+  hipLaunchKernelGGL(zs_stream_check_kernel, dim3(pieces, n), dim3(SCHECK_THREADS), 0, stream, d_sts, d_jobs, io);
   hipLaunchKernelGGL(zs_stream_finish_kernel, dim3(n), dim3(64), 0, stream, d_sts, d_jobs, d_res);
 }
 
@@ -1872,17 +1984,17 @@ extern "C" void zs_launch_finish(const ZsJobDev *d_jobs, const ZsHeadDev *d_head
                      d_res, njobs);
 }
 
-// serial-decoder counters of the profiling build (zs_kprof_read's 64..79)
-extern "C" int zs_kprof_read_w(uint64_t *out16, int reset) {
+// serial-decoder counters of the profiling build (zs_kprof_read's 64..95)
+extern "C" int zs_kprof_read_w(uint64_t *out32, int reset) {
 #if KP_ON
-  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_kprof_w), 16 * sizeof(uint64_t)) != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_kprof_w), 32 * sizeof(uint64_t)) != hipSuccess) return -1;
   if (reset) {
-    static const unsigned long long z[16] = {};
+    static const unsigned long long z[32] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_kprof_w), z, sizeof z) != hipSuccess) return -1;
   }
-  return 16;
+  return 32;
 #else
-  (void)out16;
+  (void)out32;
   (void)reset;
   return 0;
 #endif

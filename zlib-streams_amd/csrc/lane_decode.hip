@@ -2480,16 +2480,16 @@ extern "C" void zs_launch_expand(const ZsJobDev *d_jobs, ZsChunkDev *d_chunks, u
 extern "C" int zs_kprof_read_ck(uint64_t *out16, int reset);
 extern "C" int zs_kprof_read_dz(uint64_t *out12, int reset);
 // Counter readback (profiling builds only; product builds report 0 counters).
-extern "C" int zs_kprof_read_w(uint64_t *out16, int reset);
+extern "C" int zs_kprof_read_w(uint64_t *out32, int reset);
 extern "C" int zs_kprof_read(uint64_t *out, uint32_t n, int reset) {
 #if KP_ON
   const uint32_t k = n < KP_TOTAL ? n : KP_TOTAL;
   if (hipDeviceSynchronize() != hipSuccess) return -1;
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_kprof), (k < KP_COUNT ? k : KP_COUNT) * sizeof(uint64_t)) != hipSuccess) return -1;
   if (k >= KP_TOTAL) {
-    uint64_t w[16];
-    if (zs_kprof_read_w(w, reset) == 16)
-      for (int i = 0; i < 16; i++) out[64 + i] = w[i];
+    uint64_t w[32];
+    if (zs_kprof_read_w(w, reset) == 32)
+      for (int i = 0; i < 32; i++) out[64 + i] = w[i];
   }
   if (k >= 64) {
     uint64_t ck[16];

@@ -33,8 +33,8 @@ extern "C" void zs_launch_finish(const ZsJobDev *d_jobs, const ZsHeadDev *d_head
                                  uint64_t *d_checks, ZsResultDev *d_res, uint32_t njobs, uint64_t max_out,
                                  hipStream_t stream);
 extern "C" void zs_launch_stream(int d64, int run_header, ZsStreamDev *const *d_sts, const ZsJobDev *d_jobs,
-                                 ZsHeadDev *d_heads, uint32_t n, uint64_t max_out_cap, ZsStreamRes *d_res,
-                                 hipStream_t stream);
+                                 ZsHeadDev *d_heads, const ZsStreamIo *io, uint32_t n, uint64_t max_in_len,
+                                 uint64_t max_out_cap, ZsStreamRes *d_res, hipStream_t stream);
 extern "C" uint32_t zs_lane_resident_waves(void);
 extern "C" void zs_launch_fixed_tables(uint32_t *fixed, int d64, hipStream_t st);
 extern "C" void zs_launch_fixed_compact(uint32_t *fixed, hipStream_t st);
@@ -845,6 +845,7 @@ struct StreamState {
   uint8_t *d_in = nullptr, *d_out = nullptr;
   size_t cap_in = 0, cap_out = 0;
   uint8_t *h_in = nullptr, *h_out = nullptr;  // pinned staging (calls up to STAGE_MAX bytes)
+  uint8_t *dh_in = nullptr, *dh_out = nullptr;  // their device views (host-mapped)
   size_t cap_hin = 0, cap_hout = 0;
 };
 
@@ -865,6 +866,33 @@ uint8_t *stage_buf(uint8_t **p, size_t *cap, size_t need) {
     *cap = c;
   }
   return *p;
+}
+
+// stage_buf plus the buffer's device view (kernels read / write it over the bus)
+uint8_t *stage_mapped(uint8_t **p, size_t *cap, uint8_t **dp, size_t need) {
+  const uint8_t *old = *p;
+  uint8_t *h = stage_buf(p, cap, need);
+  if (!h) return nullptr;
+  if (h != old || !*dp) {
+    void *d = nullptr;
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+      (void)hipGetLastError();
+      *dp = nullptr;
+      return nullptr;
+    }
+    *dp = static_cast<uint8_t *>(d);
+  }
+  return *dp ? h : nullptr;
+}
+
+template <typename T>
+T *host_view(T *h) {  // device view of a pinned host array (nullptr if none)
+  void *d = nullptr;
+  if (!h || hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return static_cast<T *>(d);
 }
 
 size_t stream_fast_min() {
@@ -890,6 +918,7 @@ constexpr long SQ_WAIT_US = 400; // gathering: longest wait
 struct StreamCall {
   StreamState *s = nullptr;
   ZsJobDev jb{};
+  ZsStreamIo io{};  // host-mapped staging of the call (or DMA: null), carried restart bit
   int run_header = 0;
   ZsStreamRes res{};
   int err = 0;
@@ -910,6 +939,13 @@ struct StreamQueue {
   ZsHeadDev *d_heads = nullptr;
   ZsStreamDev **d_sts = nullptr, **h_sts = nullptr;
   ZsStreamRes *d_res = nullptr, *h_res = nullptr;
+  ZsStreamIo *h_io = nullptr;
+  // device views of the pinned arrays: the kernels read the batch's jobs and
+  // write its outcomes over the bus, no copies of their own
+  ZsJobDev *v_jobs = nullptr;
+  ZsStreamDev **v_sts = nullptr;
+  ZsStreamIo *v_io = nullptr;
+  ZsStreamRes *v_res = nullptr;
   uint64_t launches = 0, calls = 0;  // zs_stream_stats
 } g_sq;
 
@@ -923,8 +959,16 @@ int sq_launch(std::vector<StreamCall *> &calls) {
     int r;
     if ((r = grow_dev(&g_sq.d_jobs, c)) || (r = grow_host(&g_sq.h_jobs, c)) || (r = grow_dev(&g_sq.d_heads, c)) ||
         (r = grow_dev(&g_sq.d_sts, c)) || (r = grow_host(&g_sq.h_sts, c)) || (r = grow_dev(&g_sq.d_res, c)) ||
-        (r = grow_host(&g_sq.h_res, c)))
+        (r = grow_host(&g_sq.h_res, c)) || (r = grow_host(&g_sq.h_io, c)))
       return r;
+    g_sq.v_jobs = host_view(g_sq.h_jobs);
+    g_sq.v_sts = host_view(g_sq.h_sts);
+    g_sq.v_io = host_view(g_sq.h_io);
+    g_sq.v_res = host_view(g_sq.h_res);
+    if (!g_sq.v_io) {
+      set_err("stream: pinned call array has no device view");
+      return ZS_ENODEV;
+    }
     g_sq.cap = c;
   }
   std::vector<size_t> order;
@@ -939,24 +983,34 @@ int sq_launch(std::vector<StreamCall *> &calls) {
   for (size_t k = 0; k < n; k++) {
     g_sq.h_jobs[k] = calls[order[k]]->jb;
     g_sq.h_sts[k] = calls[order[k]]->s->d_st;
+    g_sq.h_io[k] = calls[order[k]]->io;
   }
   const hipStream_t st = g_sq.st;
-  HIP_OK(hipMemcpyAsync(g_sq.d_jobs, g_sq.h_jobs, n * sizeof(ZsJobDev), hipMemcpyHostToDevice, st));
-  HIP_OK(hipMemcpyAsync(g_sq.d_sts, g_sq.h_sts, n * sizeof(ZsStreamDev *), hipMemcpyHostToDevice, st));
+  // jobs / states / outcomes: read and written by the kernels through the
+  // pinned arrays' device views when the runtime gives them, else copied
+  const bool views = g_sq.v_jobs && g_sq.v_sts && g_sq.v_res;
+  ZsJobDev *jobs = views ? g_sq.v_jobs : g_sq.d_jobs;
+  ZsStreamDev **sts = views ? g_sq.v_sts : g_sq.d_sts;
+  ZsStreamRes *res = views ? g_sq.v_res : g_sq.d_res;
+  if (!views) {
+    HIP_OK(hipMemcpyAsync(g_sq.d_jobs, g_sq.h_jobs, n * sizeof(ZsJobDev), hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemcpyAsync(g_sq.d_sts, g_sq.h_sts, n * sizeof(ZsStreamDev *), hipMemcpyHostToDevice, st));
+  }
   for (int d64 = 0; d64 < 2; d64++) {
     const size_t k0 = d64 ? nstd : 0, k1 = d64 ? n : nstd;
     if (k1 == k0) continue;
     int run_header = 0;
-    uint64_t max_out = 0;
+    uint64_t max_out = 0, max_in = 0;
     for (size_t k = k0; k < k1; k++) {
       run_header |= calls[order[k]]->run_header;
       max_out = std::max<uint64_t>(max_out, g_sq.h_jobs[k].out_cap);
+      if (g_sq.h_io[k].hin) max_in = std::max<uint64_t>(max_in, g_sq.h_jobs[k].in_len);
     }
-    zs_launch_stream(d64, run_header, g_sq.d_sts + k0, g_sq.d_jobs + k0, g_sq.d_heads + k0, (uint32_t)(k1 - k0),
-                     max_out, g_sq.d_res + k0, st);
+    zs_launch_stream(d64, run_header, sts + k0, jobs + k0, g_sq.d_heads + k0, g_sq.v_io + k0, (uint32_t)(k1 - k0),
+                     max_in, max_out, res + k0, st);
     HIP_OK(hipGetLastError());
   }
-  HIP_OK(hipMemcpyAsync(g_sq.h_res, g_sq.d_res, n * sizeof(ZsStreamRes), hipMemcpyDeviceToHost, st));
+  if (!views) HIP_OK(hipMemcpyAsync(g_sq.h_res, g_sq.d_res, n * sizeof(ZsStreamRes), hipMemcpyDeviceToHost, st));
   HIP_OK(hipStreamSynchronize(st));
   for (size_t k = 0; k < n; k++) calls[order[k]]->res = g_sq.h_res[k];
   g_sq.launches++;
@@ -1040,6 +1094,8 @@ int stream_init(StreamState *s, int wbits) {
   s->h_out = keep.h_out;
   s->cap_hin = keep.cap_hin;
   s->cap_hout = keep.cap_hout;
+  s->dh_in = keep.dh_in;
+  s->dh_out = keep.dh_out;
   s->inited = 1;
   s->wbits = wbits;
   s->cfg = cfg;
@@ -1057,6 +1113,7 @@ void stream_free(StreamState *s) {
   if (s->h_out) (void)hipHostFree(s->h_out);
   if (s->hs) (void)hipStreamDestroy(s->hs);
   s->h_in = s->h_out = nullptr;
+  s->dh_in = s->dh_out = nullptr;
   s->cap_hin = s->cap_hout = 0;
   s->d_st = nullptr;
   s->d_in = s->d_out = nullptr;
@@ -1117,17 +1174,30 @@ int stream_call(StreamState *s, const uint8_t *in, unsigned in_len, uint8_t *out
       set_err("stream: device buffer allocation failed");
       return Z_MEM_ERROR;
     }
-    if (uint8_t *hb = stage_buf(&s->h_in, &s->cap_hin, blen)) {  // one DMA from pinned staging
-      if (clen) std::memcpy(hb, s->carry.data(), clen);
-      if (take) std::memcpy(hb + clen, in + off, take);
-      if (blen) HIP_OK(hipMemcpyAsync(s->d_in, hb, blen, hipMemcpyHostToDevice, hs));
+    // host-mapped staging both ways (the batch's kernels pull the input and
+    // push the output: no copy or sync of the call's own), else DMA
+    const size_t ocap = (size_t)out_len - prod;
+    uint8_t *hmi = stage_mapped(&s->h_in, &s->cap_hin, &s->dh_in, std::max<size_t>(blen, 1));
+    uint8_t *hmo = hmi ? stage_mapped(&s->h_out, &s->cap_hout, &s->dh_out, std::max<size_t>(ocap, 1)) : nullptr;
+    const bool mapped = hmi && hmo;
+    if (mapped) {
+      if (clen) std::memcpy(hmi, s->carry.data(), clen);
+      if (take) std::memcpy(hmi + clen, in + off, take);
     } else {
-      if (clen) HIP_OK(hipMemcpyAsync(s->d_in, s->carry.data(), clen, hipMemcpyHostToDevice, hs));
-      if (take) HIP_OK(hipMemcpyAsync(s->d_in + clen, in + off, take, hipMemcpyHostToDevice, hs));
+      if (uint8_t *hb = stage_buf(&s->h_in, &s->cap_hin, blen)) {  // one DMA from pinned staging
+        if (clen) std::memcpy(hb, s->carry.data(), clen);
+        if (take) std::memcpy(hb + clen, in + off, take);
+        if (blen) HIP_OK(hipMemcpyAsync(s->d_in, hb, blen, hipMemcpyHostToDevice, hs));
+      } else {
+        if (clen) HIP_OK(hipMemcpyAsync(s->d_in, s->carry.data(), clen, hipMemcpyHostToDevice, hs));
+        if (take) HIP_OK(hipMemcpyAsync(s->d_in + clen, in + off, take, hipMemcpyHostToDevice, hs));
+      }
+      HIP_OK(hipStreamSynchronize(hs));
     }
-    HIP_OK(hipMemcpyAsync(&s->d_st->rbit, &s->carry_bit, sizeof(uint32_t), hipMemcpyHostToDevice, hs));
-    HIP_OK(hipStreamSynchronize(hs));
     StreamCall c;
+    c.io.hin = mapped ? s->dh_in : nullptr;
+    c.io.hout = mapped ? s->dh_out : nullptr;
+    c.io.rbit = s->carry_bit;
     c.s = s;
     c.jb = s->cfg;
     c.jb.in = s->d_in;
@@ -1137,7 +1207,9 @@ int stream_call(StreamState *s, const uint8_t *in, unsigned in_len, uint8_t *out
     c.run_header = s->mode == ZSM_HEAD;
     if (int rc = sq_submit(&c)) return rc;
     h = c.res;
-    if (h.produced) {
+    if (h.produced && mapped) {
+      std::memcpy(out + prod, hmo, h.produced);
+    } else if (h.produced) {
       uint8_t *hb = stage_buf(&s->h_out, &s->cap_hout, h.produced);
       HIP_OK(hipMemcpyAsync(hb ? hb : out + prod, s->d_out, h.produced, hipMemcpyDeviceToHost, hs));
       HIP_OK(hipStreamSynchronize(hs));

@@ -319,6 +319,7 @@ enum ZsStreamMode {
   ZSM_DICT = 10    // zlib FDICT: Z_NEED_DICT on every call
 };
 
+#define ZS_STREAM_TAB_WORDS 1448u  // TABLE_ENTRIES (zs_device.h)
 struct ZsStreamDev {
   // resume point, in and out of every call; bit offsets relative to the
   // call buffer (the host rebases them onto the bytes it carries over)
@@ -338,10 +339,22 @@ struct ZsStreamDev {
   uint32_t stop_bits;  // bits pulled (FULL / END / ERROR / trailer): zlib total_in = ceil(/8)
   uint32_t produced;   // bytes written this call
   uint32_t check;      // strm->adler after the call
-  uint32_t pad;
+  uint32_t tab_bits;   // tab holds the current dynamic block's tables: lbits | dbits << 8 | 1 << 16 (0: rebuild)
   uint64_t acc_a, acc_b;  // check accumulators of this call's output
   uint8_t lens[320];   // code lengths of the current dynamic block
   __attribute__((aligned(16))) uint8_t window[65536];  // last 64 KiB (32 KiB used unless deflate64) of output, oldest first
+  __attribute__((aligned(16))) uint32_t tab[ZS_STREAM_TAB_WORDS];  // built tables (TABLE_ENTRIES), see tab_bits
+};
+
+// Host side of one stream call (zs_capi.cpp sq_launch): with host-mapped
+// pinned staging the call needs no copy of its own -- the batch's first kernel
+// pulls every input into its device buffer and the check kernel pushes every
+// output out.  Null pointers: the host copied by DMA (calls above the staging size).
+struct ZsStreamIo {
+  const uint8_t *hin;  // host-mapped input, in_len bytes -> the job's in
+  uint8_t *hout;       // host-mapped output: the call's produced bytes <- the job's out
+  uint32_t rbit;       // restart bit within input byte 0 (the carried partial byte)
+  uint32_t pad;
 };
 
 // Outcome of one stream call (device -> host, gathered per batch).

@@ -171,43 +171,80 @@ static __device__ __attribute__((noinline)) int build_table(int type, const uint
   // incomplete single 1-bit code: slot 1 is an invalid marker
   if (room > 0 && lane == 0) table[1] = mk_entry(64, 1, 0);
 
-  // long codes: serial over codes (uniform), lane-parallel replication
-  uint32_t next = 0, cur_size = 1u << root, open_low = 0xffffffffu, curr = root;
+  // long codes, 64 at a time across the lanes.  In sorted order the codes of
+  // one sub-table (same root bits `low`) are consecutive; a sub-table's size
+  // depends only on the counts of its first code's length and longer ones
+  // (src/inftrees.c:258-274, `count[len]` less the codes of that length
+  // already placed), so every group start sizes its own sub-table and a scan
+  // of the sizes gives zlib's allocation offsets (`next`).
+  uint32_t c_low = 0xffffffffu, c_next = 0, c_size = 0, c_sum = 1u << root;
   const uint32_t rmask = (1u << root) - 1;
-  for (uint32_t i = nshort; i < ncodes; i++) {
-    uint32_t s = uni(sorted[i]);
-    uint32_t L = uni(lens[s]);
-    uint32_t st = uni(scratch16[16 + L]);
-    uint32_t code = 0;
+  for (uint32_t g0 = nshort; g0 < ncodes; g0 += WAVE) {
+    const uint32_t i = g0 + lane;
+    const bool act = i < ncodes;
+    uint32_t s = 0, L = root + 1, rev = 0, low = 0xfffffffeu;
+    if (act) {
+      s = sorted[i];
+      L = lens[s];
+      const uint32_t st = scratch16[16 + L];
+      uint32_t code = 0;
 #pragma unroll
-    for (int x = 1; x <= 15; x++)
-      if ((uint32_t)x == L) code = first[x];
-    code += i - st;
-    uint32_t rev = __builtin_bitreverse32(code) >> (32 - L);
-    uint32_t low = rev & rmask;
-    if (low != open_low) {
-      next += cur_size;
+      for (int x = 1; x <= 15; x++)
+        if ((uint32_t)x == L) code = first[x];
+      code += i - st;
+      rev = __builtin_bitreverse32(code) >> (32 - L);
+      low = rev & rmask;
+    }
+    uint32_t prev_low = (uint32_t)__shfl_up((int)low, 1);
+    if (lane == 0) prev_low = c_low;
+    const bool start = act && low != prev_low;
+    uint32_t curr = 0, size = 0;
+    if (start) {
+      const uint32_t st = scratch16[16 + L];
       curr = L - root;
       int left = 1 << curr;
       while (curr + root < maxlen) {
-        uint32_t x = curr + root;
-        uint32_t remain = uni(scratch16[x]) - ((x == L) ? (i - st) : 0u);
+        const uint32_t x = curr + root;
+        const uint32_t remain = scratch16[x] - ((x == L) ? (i - st) : 0u);
         left -= (int)remain;
         if (left <= 0) break;
         curr++;
         left <<= 1;
       }
-      cur_size = 1u << curr;
-      used += cur_size;
-      if (used > lim) return 1;
-      open_low = low;
-      if (lane == 0) table[low] = mk_entry(curr, root, next);
+      size = 1u << curr;
     }
-    uint32_t e = sym_entry(s, L - root);
-    uint32_t step = 1u << (L - root);
-    uint32_t reps = cur_size >> (L - root);
-    uint32_t idx0 = next + (rev >> root);
-    for (uint32_t j = lane; j < reps; j += WAVE) table[idx0 + j * step] = e;
+    // inclusive sum of sizes and the latest group start at or before each lane
+    uint32_t incl = size;
+    int sl = start ? (int)lane : -1;
+#pragma unroll
+    for (uint32_t d = 1; d < WAVE; d <<= 1) {
+      const uint32_t v = (uint32_t)__shfl_up((int)incl, d);
+      const int m = __shfl_up(sl, d);
+      if (lane >= d) {
+        incl += v;
+        sl = max(sl, m);
+      }
+    }
+    const uint32_t gnext_own = c_sum + incl - size;
+    const uint32_t gnext_sl = (uint32_t)__shfl((int)gnext_own, sl < 0 ? 0 : sl);
+    const uint32_t gsize_sl = (uint32_t)__shfl((int)size, sl < 0 ? 0 : sl);
+    const uint32_t gnext = sl < 0 ? c_next : gnext_sl;
+    const uint32_t gsize = sl < 0 ? c_size : gsize_sl;
+    const uint32_t total = uni((uint32_t)__shfl((int)incl, WAVE - 1));
+    if (c_sum + total > lim) return 1;  // zlib stops at the first sub-table past the bound: same result
+    if (start) table[low] = mk_entry(curr, root, gnext);
+    if (act) {
+      const uint32_t e = sym_entry(s, L - root);
+      const uint32_t step = 1u << (L - root);
+      const uint32_t reps = gsize >> (L - root);
+      const uint32_t idx0 = gnext + (rev >> root);
+      for (uint32_t j = 0; j < reps; j++) table[idx0 + j * step] = e;
+    }
+    const uint32_t last = min(ncodes - g0, (uint32_t)WAVE) - 1u;
+    c_low = uni((uint32_t)__shfl((int)low, last));
+    c_next = uni((uint32_t)__shfl((int)gnext, last));
+    c_size = uni((uint32_t)__shfl((int)gsize, last));
+    c_sum += total;
   }
   __builtin_amdgcn_wave_barrier();
   *root_io = root;

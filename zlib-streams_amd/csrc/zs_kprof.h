@@ -26,7 +26,10 @@ enum ZsKprof {
   // serial wave decoder (inflate_kernels.hip; its own array, read into 64..79)
   KP_W_WAVES = 64, KP_W_CYC_TOTAL, KP_W_WINDOWS, KP_W_EMPTY, KP_W_SYMS, KP_W_BYTES, KP_W_BATCHES, KP_W_JUMPS,
   KP_W_CYC_DECODE, KP_W_CYC_CHAIN, KP_W_CYC_EXPAND, KP_W_SERIAL, KP_W_CYC_WINDOW,
-  KP_TOTAL = 80
+  // stream window sub-phases: jump-table compositions, chain walks, wave 0
+  // before (post + refill) and after (flush + reseat) a window, table builds
+  KP_W_CYC_COMPOSE, KP_W_CYC_WALK, KP_W_CYC_PRE, KP_W_CYC_POST, KP_W_CYC_TABLES,
+  KP_TOTAL = 96
 };
 
 #ifdef ZS_KPROF

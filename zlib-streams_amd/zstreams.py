@@ -371,8 +371,8 @@ def profile_stages():
 def kprof_read(reset=True):
     """In-kernel counters of the profiling build (ZS_LIB=.../libzstreams_mi355x_prof.so);
     an empty list with the product library."""
-    a = (ctypes.c_uint64 * 80)()
-    k = lib().zs_kprof_read(a, 80, 1 if reset else 0)
+    a = (ctypes.c_uint64 * 96)()
+    k = lib().zs_kprof_read(a, 96, 1 if reset else 0)
     if k < 0:
         raise ZStreamsError("zs_kprof_read failed")
     return list(a[:k])
