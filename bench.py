@@ -588,6 +588,10 @@ def stream_leg(args, zstreams, np, cpu):
     op = (ctypes.c_void_p * nh)(*[o.ctypes.data for o in outs])
     oc = (S * nh)(*[len(o) for o in outs])
     prod, codes, ncalls = (ctypes.c_uint64 * nh)(), (ctypes.c_int * nh)(), ctypes.c_uint64(0)
+    # warm run (as the one-handle leg's): the library's per-stream device and pinned
+    # buffers come from its pool afterwards, as in a process that keeps serving streams
+    if J.zs_js_drive(zstreams.LIB_PATH.encode(), cp, cl, op, oc, nh, ws, prod, codes, ctypes.byref(ncalls)) <= 0:
+        raise RuntimeError("zs_js_drive failed (warm run)")
     st0 = zstreams.stream_stats()
     tm = J.zs_js_drive(zstreams.LIB_PATH.encode(), cp, cl, op, oc, nh, ws, prod, codes, ctypes.byref(ncalls))
     if tm <= 0:

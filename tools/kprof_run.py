@@ -12,7 +12,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 NAMES = {0: "p_waves", 1: "p_cyc_total", 2: "p_cyc_coop", 3: "p_cyc_steps", 4: "p_cyc_flush", 5: "p_groups",
          6: "p_coop_calls", 7: "p_lane_steps", 8: "p_wave_steps", 9: "p_slow_lit", 10: "p_slow_dist",
-         11: "p_cyc_max", 12: "p_cyc_init", 13: "p_refills",
+         11: "p_cyc_max", 12: "p_cyc_init", 13: "p_refills", 14: "p_busy_waves", 15: "p_cyc_busy",
          16: "e_blocks", 17: "e_cyc_total", 18: "e_rounds", 19: "e_jump_iters", 20: "e_cyc_jump", 21: "e_batches",
          22: "e_cyc_max", 23: "e_cyc_init", 24: "e_jump_rounds", 25: "e_cyc_pre",
          40: "s_refill1", 41: "s_lit", 42: "s_refill2", 43: "s_dist", 44: "s_tail",
@@ -51,6 +51,9 @@ def main():
     derived = {
         "ok": ok,
         "parse_cycles_per_wave": d["p_cyc_total"] / w, "parse_cycles_max": d["p_cyc_max"],
+        "parse_cycles_per_busy_wave": d["p_cyc_busy"] / max(d["p_busy_waves"], 1),
+        "parse_tail_ratio_all_waves": d["p_cyc_max"] / max(d["p_cyc_total"] / w, 1),
+        "parse_tail_ratio_busy_waves": d["p_cyc_max"] / max(d["p_cyc_busy"] / max(d["p_busy_waves"], 1), 1),
         "parse_frac_coop": d["p_cyc_coop"] / max(d["p_cyc_total"], 1),
         "parse_frac_steps": d["p_cyc_steps"] / max(d["p_cyc_total"], 1),
         "parse_frac_flush": d["p_cyc_flush"] / max(d["p_cyc_total"], 1),

@@ -23,7 +23,7 @@ r, c = corpus.batch(sid, 1, mib << 20, level=6, wbits=-15, nthreads=1)
 raw, comp = r[0], c[0]
 out = np.empty((mib << 20) + 65536, dtype=np.uint8)
 names = ["waves", "cyc_total", "windows", "empty", "syms", "bytes", "batches", "jumps", "cyc_decode", "cyc_chain",
-         "cyc_expand", "serial", "cyc_window", "cyc_compose", "cyc_walk", "cyc_pre", "cyc_post", "cyc_tables"]
+         "cyc_expand", "serial", "cyc_window", "cyc_compose", "cyc_walk", "cyc_pre", "cyc_post", "cyc_tables", "steps", "redos"]
 for rep in range(2):
     zstreams.kprof_read(reset=True)
     h = L.inflate_new()
@@ -47,4 +47,5 @@ for rep in range(2):
                   flush=True)
             nw = max(1, w["windows"])
             print(f"  per window: compose {w['cyc_compose'] / nw:.0f} compose+walk {w['cyc_walk'] / nw:.0f} pre {w['cyc_pre'] / nw:.0f} "
-                  f"post {w['cyc_post'] / nw:.0f}; per call: tables {w['cyc_tables'] / w['waves']:.0f}", flush=True)
+                  f"post {w['cyc_post'] / nw:.0f}; per call: tables {w['cyc_tables'] / w['waves']:.0f}; wave-0 walk steps "
+                  f"{w['steps'] / nw:.1f}, redos {w['redos'] / nw:.2f} per window", flush=True)

@@ -1158,6 +1158,10 @@ __global__ void __launch_bounds__(64) zs_lane_kernel(const ZsJobDev *__restrict_
     KP_ADD(KP_P_WAVES, 1);
     KP_ADD(KP_P_CYC_TOTAL, tot);
     KP_MAX(KP_P_CYC_MAX, tot);
+    if (kp_groups) {
+      KP_ADD(KP_P_BUSY, 1);
+      KP_ADD(KP_P_CYC_BUSY, tot);
+    }
     KP_ADD(KP_P_CYC_INIT, kp_init);
     KP_ADD(KP_P_CYC_COOP, kp_coop);
     KP_ADD(KP_P_CYC_STEPS, kp_steps_c);

@@ -904,16 +904,21 @@ size_t stream_fast_min() {
 }
 
 // ---------------------------------------------------------------------------
-// Call batching.  A call's inputs are staged on its handle's stream, then the
-// call joins the pending queue; whichever caller finds no launch in flight
-// becomes the leader, takes every pending call (up to SQ_MAX) and runs them as
-// ONE launch sequence (zs_launch_stream: a workgroup per call), so concurrent
-// streams share the GPU instead of queueing behind a process-wide lock.  A
-// lone caller's batch is itself: no added latency.
+// Call batching.  A call's input is staged (host-mapped, or copied on its
+// handle's stream), then the call joins the pending queue.  A caller that
+// finds a free launch slot becomes that slot's leader: it takes every pending
+// call (up to SQ_MAX) and runs them as ONE launch sequence on the slot's
+// stream (zs_launch_stream: a workgroup per call), then waits for it outside
+// the lock.  Up to SQ_SLOTS batches run at once (one per hardware queue).
+// While a batch runs, a new one starts only once it holds a 1/SQ_SLOTS share
+// of the active calls (pending + running): the calls that return from a
+// batch gather into the next instead of each taking a slot alone.  A lone
+// caller's batch is itself: no added latency.
 // ---------------------------------------------------------------------------
 constexpr size_t SQ_MAX = 2048;
-constexpr long SQ_GAP_US = 40;   // gathering: quiet gap that ends it
-constexpr long SQ_WAIT_US = 400; // gathering: longest wait
+constexpr int SQ_SLOTS = 4;
+constexpr long SQ_GAP_US = 40;   // deflate job gathering (DzQueue): quiet gap that ends it
+constexpr long SQ_WAIT_US = 400; // deflate job gathering: longest wait
 
 struct StreamCall {
   StreamState *s = nullptr;
@@ -923,16 +928,11 @@ struct StreamCall {
   ZsStreamRes res{};
   int err = 0;
   std::string errmsg;
+  bool taken = false;  // in a batch (its leader completes it)
   bool done = false;
 };
 
-struct StreamQueue {
-  std::mutex mu;
-  std::condition_variable cv;
-  std::condition_variable arrive;  // a call joined the queue (a gathering leader waits on it)
-  std::vector<StreamCall *> pending;
-  bool busy = false;
-  size_t last_n = 0;  // calls in the previous launch
+struct SqSlot {  // one launch slot: its stream and the batch's call arrays
   hipStream_t st = nullptr;
   size_t cap = 0;
   ZsJobDev *d_jobs = nullptr, *h_jobs = nullptr;
@@ -946,30 +946,39 @@ struct StreamQueue {
   ZsStreamDev **v_sts = nullptr;
   ZsStreamIo *v_io = nullptr;
   ZsStreamRes *v_res = nullptr;
+};
+
+struct StreamQueue {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<StreamCall *> pending;
+  SqSlot slot[SQ_SLOTS];
+  bool busy[SQ_SLOTS] = {};
+  size_t running = 0;  // calls in batches in flight
   uint64_t launches = 0, calls = 0;  // zs_stream_stats
 } g_sq;
 
-// leader only (g_sq.busy): one launch sequence per decoder variant
-int sq_launch(std::vector<StreamCall *> &calls) {
-  if (!g_sq.st) HIP_OK(hipStreamCreateWithFlags(&g_sq.st, hipStreamNonBlocking));
+// a slot's leader only (busy[slot] set): one launch sequence per decoder variant
+int sq_launch(SqSlot &q, std::vector<StreamCall *> &calls) {
+  if (!q.st) HIP_OK(hipStreamCreateWithFlags(&q.st, hipStreamNonBlocking));
   const size_t n = calls.size();
-  if (n > g_sq.cap) {
+  if (n > q.cap) {
     const size_t c = std::max<size_t>(n, 64);
-    g_sq.cap = 0;
+    q.cap = 0;
     int r;
-    if ((r = grow_dev(&g_sq.d_jobs, c)) || (r = grow_host(&g_sq.h_jobs, c)) || (r = grow_dev(&g_sq.d_heads, c)) ||
-        (r = grow_dev(&g_sq.d_sts, c)) || (r = grow_host(&g_sq.h_sts, c)) || (r = grow_dev(&g_sq.d_res, c)) ||
-        (r = grow_host(&g_sq.h_res, c)) || (r = grow_host(&g_sq.h_io, c)))
+    if ((r = grow_dev(&q.d_jobs, c)) || (r = grow_host(&q.h_jobs, c)) || (r = grow_dev(&q.d_heads, c)) ||
+        (r = grow_dev(&q.d_sts, c)) || (r = grow_host(&q.h_sts, c)) || (r = grow_dev(&q.d_res, c)) ||
+        (r = grow_host(&q.h_res, c)) || (r = grow_host(&q.h_io, c)))
       return r;
-    g_sq.v_jobs = host_view(g_sq.h_jobs);
-    g_sq.v_sts = host_view(g_sq.h_sts);
-    g_sq.v_io = host_view(g_sq.h_io);
-    g_sq.v_res = host_view(g_sq.h_res);
-    if (!g_sq.v_io) {
+    q.v_jobs = host_view(q.h_jobs);
+    q.v_sts = host_view(q.h_sts);
+    q.v_io = host_view(q.h_io);
+    q.v_res = host_view(q.h_res);
+    if (!q.v_io) {
       set_err("stream: pinned call array has no device view");
       return ZS_ENODEV;
     }
-    g_sq.cap = c;
+    q.cap = c;
   }
   std::vector<size_t> order;
   order.reserve(n);
@@ -981,20 +990,20 @@ int sq_launch(std::vector<StreamCall *> &calls) {
         nstd += d64 ? 0 : 1;
       }
   for (size_t k = 0; k < n; k++) {
-    g_sq.h_jobs[k] = calls[order[k]]->jb;
-    g_sq.h_sts[k] = calls[order[k]]->s->d_st;
-    g_sq.h_io[k] = calls[order[k]]->io;
+    q.h_jobs[k] = calls[order[k]]->jb;
+    q.h_sts[k] = calls[order[k]]->s->d_st;
+    q.h_io[k] = calls[order[k]]->io;
   }
-  const hipStream_t st = g_sq.st;
+  const hipStream_t st = q.st;
   // jobs / states / outcomes: read and written by the kernels through the
   // pinned arrays' device views when the runtime gives them, else copied
-  const bool views = g_sq.v_jobs && g_sq.v_sts && g_sq.v_res;
-  ZsJobDev *jobs = views ? g_sq.v_jobs : g_sq.d_jobs;
-  ZsStreamDev **sts = views ? g_sq.v_sts : g_sq.d_sts;
-  ZsStreamRes *res = views ? g_sq.v_res : g_sq.d_res;
+  const bool views = q.v_jobs && q.v_sts && q.v_res;
+  ZsJobDev *jobs = views ? q.v_jobs : q.d_jobs;
+  ZsStreamDev **sts = views ? q.v_sts : q.d_sts;
+  ZsStreamRes *res = views ? q.v_res : q.d_res;
   if (!views) {
-    HIP_OK(hipMemcpyAsync(g_sq.d_jobs, g_sq.h_jobs, n * sizeof(ZsJobDev), hipMemcpyHostToDevice, st));
-    HIP_OK(hipMemcpyAsync(g_sq.d_sts, g_sq.h_sts, n * sizeof(ZsStreamDev *), hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemcpyAsync(q.d_jobs, q.h_jobs, n * sizeof(ZsJobDev), hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemcpyAsync(q.d_sts, q.h_sts, n * sizeof(ZsStreamDev *), hipMemcpyHostToDevice, st));
   }
   for (int d64 = 0; d64 < 2; d64++) {
     const size_t k0 = d64 ? nstd : 0, k1 = d64 ? n : nstd;
@@ -1003,68 +1012,124 @@ int sq_launch(std::vector<StreamCall *> &calls) {
     uint64_t max_out = 0, max_in = 0;
     for (size_t k = k0; k < k1; k++) {
       run_header |= calls[order[k]]->run_header;
-      max_out = std::max<uint64_t>(max_out, g_sq.h_jobs[k].out_cap);
-      if (g_sq.h_io[k].hin) max_in = std::max<uint64_t>(max_in, g_sq.h_jobs[k].in_len);
+      max_out = std::max<uint64_t>(max_out, q.h_jobs[k].out_cap);
+      if (q.h_io[k].hin) max_in = std::max<uint64_t>(max_in, q.h_jobs[k].in_len);
     }
-    zs_launch_stream(d64, run_header, sts + k0, jobs + k0, g_sq.d_heads + k0, g_sq.v_io + k0, (uint32_t)(k1 - k0),
-                     max_in, max_out, res + k0, st);
+    zs_launch_stream(d64, run_header, sts + k0, jobs + k0, q.d_heads + k0, q.v_io + k0, (uint32_t)(k1 - k0), max_in,
+                     max_out, res + k0, st);
     HIP_OK(hipGetLastError());
   }
-  if (!views) HIP_OK(hipMemcpyAsync(g_sq.h_res, g_sq.d_res, n * sizeof(ZsStreamRes), hipMemcpyDeviceToHost, st));
+  if (!views) HIP_OK(hipMemcpyAsync(q.h_res, q.d_res, n * sizeof(ZsStreamRes), hipMemcpyDeviceToHost, st));
   HIP_OK(hipStreamSynchronize(st));
-  for (size_t k = 0; k < n; k++) calls[order[k]]->res = g_sq.h_res[k];
-  g_sq.launches++;
-  g_sq.calls += n;
+  for (size_t k = 0; k < n; k++) calls[order[k]]->res = q.h_res[k];
   return 0;
 }
 
+int sq_slots() {  // env ZS_STREAM_SLOTS (1..SQ_SLOTS)
+  static const int v = [] {
+    const char *e = std::getenv("ZS_STREAM_SLOTS");
+    const int k = e ? std::atoi(e) : SQ_SLOTS;
+    return std::max(1, std::min(SQ_SLOTS, k));
+  }();
+  return v;
+}
+
 int sq_submit(StreamCall *c) {
+  const int slots = sq_slots();
   std::unique_lock<std::mutex> lk(g_sq.mu);
   g_sq.pending.push_back(c);
-  g_sq.arrive.notify_one();
-  while (!c->done) {
-    if (g_sq.busy) {
+  for (;;) {
+    if (c->done) break;
+    int k = -1, nbusy = 0;
+    for (int i = 0; i < slots; i++) nbusy += g_sq.busy[i] ? 1 : 0;
+    const size_t share = (g_sq.pending.size() + g_sq.running + slots - 1) / slots;
+    if (!c->taken && (nbusy == 0 || g_sq.pending.size() >= share))
+      for (int i = 0; i < slots && k < 0; i++)
+        if (!g_sq.busy[i]) k = i;
+    if (k < 0) {  // our batch runs, or every slot does: wait for a completion
       g_sq.cv.wait(lk);
       continue;
     }
-    g_sq.busy = true;
-    // Several streams were active in the previous launch: gather their next
-    // calls (callers stage inputs between launches) until none arrives for
-    // SQ_GAP or SQ_WAIT has passed; a lone stream launches at once.
-    if (g_sq.last_n > 1 && g_sq.pending.size() < g_sq.last_n) {
-      const auto t_end = std::chrono::steady_clock::now() + std::chrono::microseconds(SQ_WAIT_US);
-      for (;;) {
-        const size_t had = g_sq.pending.size();
-        const auto t = std::min(t_end, std::chrono::steady_clock::now() + std::chrono::microseconds(SQ_GAP_US));
-        g_sq.arrive.wait_until(lk, t, [&] { return g_sq.pending.size() > had; });
-        if (g_sq.pending.size() == had || g_sq.pending.size() >= g_sq.last_n ||
-            std::chrono::steady_clock::now() >= t_end)
-          break;
-      }
-    }
+    g_sq.busy[k] = true;
     const size_t take = std::min(g_sq.pending.size(), SQ_MAX);
     std::vector<StreamCall *> batch(g_sq.pending.begin(), g_sq.pending.begin() + take);
     g_sq.pending.erase(g_sq.pending.begin(), g_sq.pending.begin() + take);
-    g_sq.last_n = std::max(batch.size(), g_sq.pending.size() + batch.size() / 2);  // under the mutex
+    for (StreamCall *b : batch) b->taken = true;
+    g_sq.running += batch.size();
     lk.unlock();
-    const int rc = sq_launch(batch);
+    const int rc = sq_launch(g_sq.slot[k], batch);
     const std::string msg = rc ? g_err : std::string();
+    if (rc) (void)hipGetLastError();
     lk.lock();
     for (StreamCall *b : batch) {
       b->err = rc;
       b->errmsg = msg;
       b->done = true;
     }
-    g_sq.busy = false;
+    g_sq.busy[k] = false;
+    g_sq.running -= batch.size();
+    g_sq.launches++;
+    g_sq.calls += batch.size();
     g_sq.cv.notify_all();
   }
   if (c->err) set_err(c->errmsg);
   return c->err;
 }
 
+// Device / pinned resources of ended streams, kept for the next ones:
+// hipMalloc, hipHostMalloc and stream creation cost up to milliseconds and
+// serialise concurrent callers, and hipFree synchronises the device, so a
+// server that opens and closes many streams reuses them instead.
+struct StreamRes {
+  ZsStreamDev *d_st;
+  hipStream_t hs;
+  uint8_t *d_in, *d_out, *h_in, *h_out, *dh_in, *dh_out;
+  size_t cap_in, cap_out, cap_hin, cap_hout;
+};
+constexpr size_t STREAM_POOL_MAX = 1024;
+constexpr size_t STREAM_POOL_BYTES = 64u << 20;  // larger buffers are freed, not kept
+std::mutex g_pool_mu;
+std::vector<StreamRes> g_pool;
+
+void res_take(StreamState *s) {
+  if (s->d_st) return;
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  if (g_pool.empty()) return;
+  const StreamRes r = g_pool.back();
+  g_pool.pop_back();
+  s->d_st = r.d_st;
+  s->hs = r.hs;
+  s->d_in = r.d_in;
+  s->d_out = r.d_out;
+  s->h_in = r.h_in;
+  s->h_out = r.h_out;
+  s->dh_in = r.dh_in;
+  s->dh_out = r.dh_out;
+  s->cap_in = r.cap_in;
+  s->cap_out = r.cap_out;
+  s->cap_hin = r.cap_hin;
+  s->cap_hout = r.cap_hout;
+}
+
+bool res_give(StreamState *s) {  // true: s's resources went to the pool
+  if (!s->d_st || !s->hs || s->cap_in + s->cap_out + s->cap_hin + s->cap_hout > STREAM_POOL_BYTES) return false;
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    if (g_pool.size() >= STREAM_POOL_MAX) return false;
+    g_pool.push_back({s->d_st, s->hs, s->d_in, s->d_out, s->h_in, s->h_out, s->dh_in, s->dh_out, s->cap_in, s->cap_out,
+                      s->cap_hin, s->cap_hout});
+  }
+  s->d_st = nullptr;
+  s->hs = nullptr;
+  s->d_in = s->d_out = s->h_in = s->h_out = s->dh_in = s->dh_out = nullptr;
+  s->cap_in = s->cap_out = s->cap_hin = s->cap_hout = 0;
+  return true;
+}
+
 int stream_init(StreamState *s, int wbits) {
   ZsJobDev cfg{};
   if (!parse_wbits(wbits, &cfg)) return Z_STREAM_ERROR;
+  res_take(s);
   {
     std::lock_guard<std::mutex> lk(g_mu);
     if (ws_init()) return Z_STREAM_ERROR;
@@ -1106,6 +1171,7 @@ int stream_init(StreamState *s, int wbits) {
 
 void stream_free(StreamState *s) {
   if (s->hs) (void)hipStreamSynchronize(s->hs);
+  if (res_give(s)) return;
   if (s->d_st) (void)hipFree(s->d_st);
   if (s->d_in) (void)hipFree(s->d_in);
   if (s->d_out) (void)hipFree(s->d_out);

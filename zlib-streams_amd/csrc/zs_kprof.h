@@ -9,6 +9,7 @@ enum ZsKprof {
   // parse pass (zs_lane_kernel), per wave
   KP_P_WAVES = 0, KP_P_CYC_TOTAL, KP_P_CYC_COOP, KP_P_CYC_STEPS, KP_P_CYC_FLUSH, KP_P_GROUPS, KP_P_COOP,
   KP_P_LANE_STEPS, KP_P_WAVE_STEPS, KP_P_SLOW_LIT, KP_P_SLOW_DIST, KP_P_CYC_MAX, KP_P_CYC_INIT, KP_P_REFILLS,
+  KP_P_BUSY, KP_P_CYC_BUSY,  // waves that decoded at least one group, and their cycles
   // expand pass (zs_expand_kernel), per workgroup (wave 0)
   KP_E_BLOCKS = 16, KP_E_CYC_TOTAL, KP_E_ROUNDS, KP_E_JUMP_ITERS, KP_E_CYC_JUMP, KP_E_BATCHES, KP_E_CYC_MAX,
   KP_E_CYC_INIT, KP_E_JUMP_ROUNDS,
@@ -28,7 +29,7 @@ enum ZsKprof {
   KP_W_CYC_DECODE, KP_W_CYC_CHAIN, KP_W_CYC_EXPAND, KP_W_SERIAL, KP_W_CYC_WINDOW,
   // stream window sub-phases: jump-table compositions, chain walks, wave 0
   // before (post + refill) and after (flush + reseat) a window, table builds
-  KP_W_CYC_COMPOSE, KP_W_CYC_WALK, KP_W_CYC_PRE, KP_W_CYC_POST, KP_W_CYC_TABLES,
+  KP_W_CYC_COMPOSE, KP_W_CYC_WALK, KP_W_CYC_PRE, KP_W_CYC_POST, KP_W_CYC_TABLES, KP_W_STEPS, KP_W_REDOS,
   KP_TOTAL = 96
 };
 
