@@ -8,7 +8,9 @@ Z_DEFAULT_STRATEGY) + deflate(Z_FINISH), which SURVEY.md §8c pins as
 byte-identical to the reference's shipped deflate.  Every stream also
 inflates back through the CPU oracle and host zlib.
 
-Levels 0..3 and ZS_F_DEFLATE_FAST (the throughput path): every GPU stream is
+Level 0 (deflate_stored): zlib's bytes too, with or without ZS_F_DEFLATE_FAST.
+
+Levels 1..3 and ZS_F_DEFLATE_FAST (the throughput path): every GPU stream is
 valid deflate that the oracle and host zlib inflate to the input, with
 Z_STREAM_END, the whole stream consumed, the wrapper bytes and check value as
 zlib writes them; its size is bounded against zlib at the same level.
@@ -21,6 +23,7 @@ import numpy as np
 import pytest
 
 import corpus
+import libz_ref
 import oracle_lib as O
 
 pytestmark = pytest.mark.gpu
@@ -42,13 +45,24 @@ def expected_check(data, wbits):
 
 
 def zlib_bytes(data, wbits, level):
+    """Host zlib's bytes for one deflate(Z_FINISH) with room for the whole output
+    (the batch API's call).  Level 0 needs exactly that call: deflate_stored
+    sizes its blocks by the output space each deflate() call offers (Python's
+    compressobj grows its buffer call by call, giving other block lengths);
+    levels 1..9 write the same bytes under any output schedule."""
+    if level == 0:
+        d = libz_ref.Deflater(0, wbits)
+        r, used, out = d.call(data, len(data) + 5 * (len(data) // 65535 + 1) + 64, 4)
+        d.end()
+        assert r == 1 and used == len(data), (r, used, len(data))
+        return out
     c = zlib.compressobj(level, zlib.DEFLATED, wbits, 8, zlib.Z_DEFAULT_STRATEGY)
     return c.compress(data) + c.flush()
 
 
 def check_stream(data, wbits, level, comp, info, fast=False):
     assert info["ret"] == 1, info
-    if 4 <= level <= 9 and not fast:
+    if level == 0 or (4 <= level <= 9 and not fast):
         ref = zlib_bytes(data, wbits, level)
         assert comp == ref, ("not zlib's bytes", len(data), wbits, level, len(comp), len(ref))
     assert info["total_in"] == len(data) and info["total_out"] == len(comp), info
@@ -142,6 +156,22 @@ def test_deflate_zlib_bytes_levels_4_to_9(zs):
     bad = [(i, len(d), wb, lv) for i, ((d, wb, lv), (comp, info)) in enumerate(zip(cases, got))
            if comp != zlib_bytes(d, wb, lv) or info["ret"] != 1]
     assert not bad, bad[:8]
+
+
+def test_deflate_level0_is_zlibs(zs):
+    """Level 0: zlib's deflate_stored blocks of 65535 bytes from the stream start,
+    across the 64 KiB segment grid (the final block starting one segment early
+    at 2 x 65535), every wrapper, with and without ZS_F_DEFLATE_FAST."""
+    rng = random.Random(12)
+    data = bytes(rng.getrandbits(8) for _ in range(5 * 65536 + 11))
+    sizes = [0, 1, 65534, 65535, 65536, 65537, 2 * 65535, 2 * 65535 + 1, 2 * 65536, 3 * 65535 + 7,
+             4 * 65536 - 3, 5 * 65535, 5 * 65536 + 11]
+    cases = [(data[:n], wb) for n in sizes for wb in (-15, 15, 31)]
+    for fast in (False, True):
+        got = zs.deflate_batch([c[0] for c in cases], [c[1] for c in cases], 0, fast=fast)
+        for (d, wb), (comp, info) in zip(cases, got):
+            assert comp == zlib_bytes(d, wb, 0), (len(d), wb, fast, len(comp))
+            check_stream(d, wb, 0, comp, info)
 
 
 def test_deflate_zlib_bytes_large_c3_shape(zs):

@@ -893,25 +893,37 @@ __global__ void __launch_bounds__(DZ_T) zs_dz_emit_kernel(const ZsDJobDev *__res
   const ZsDJobDev jb = jobs[sg.job];
   if (jb.exact) return;  // zlib-identical jobs: deflate_zlib.hip
   uint32_t *gout = obuf + sg.obuf / 4;
-  const uint32_t last = sg.last;
-  if (jb.level == 0) {  // stored blocks of <= 65535 bytes, byte-aligned (every block is stored)
-    const uint8_t *in = jb.in + sg.start;
-    uint8_t *ob = reinterpret_cast<uint8_t *>(gout);
+  if (jb.level == 0) {
+    // zlib's deflate_stored for one deflate(Z_FINISH) with room for the whole
+    // output: stored blocks of MAX_STORED = 65535 bytes from the stream's
+    // start (the last one shorter; an empty stream is one empty block), each
+    // a byte-aligned 5-byte header + its bytes.  Blocks do not align with the
+    // 64 KiB segments: a segment writes the tail of the block open at its start,
+    // then a header + bytes for each block that starts inside it.
+    const uint64_t S = sg.start, N = jb.in_len;
     const uint32_t n = sg.len;
-    const uint32_t nblk = n ? (n + 65534u) / 65535u : 1u;
-    for (uint32_t b = 0; b < nblk; b++) {
-      const uint32_t off = b * 65535u, bl = min(65535u, n - off);
-      uint8_t *hp = ob + off + 5u * b;
+    const uint8_t *in = jb.in + S;
+    uint8_t *ob = reinterpret_cast<uint8_t *>(gout);
+    const uint64_t k0 = (S + 65534u) / 65535u;  // first block starting at or after S
+    const uint64_t kend = N ? (S + n + 65534u) / 65535u : 1u;  // blocks starting before S + n (an empty stream: block 0)
+    const uint32_t nst = (uint32_t)(kend > k0 ? kend - k0 : 0u);
+    const uint32_t lead = (uint32_t)min<uint64_t>(n, k0 * 65535u - S);  // tail of the block open at S
+    for (uint32_t i = t; i < lead; i += DZ_T) ob[i] = in[i];
+    for (uint32_t j = 0; j < nst; j++) {
+      const uint64_t bs = (k0 + j) * 65535u;  // block start (stream position)
+      const uint32_t bl = (uint32_t)min<uint64_t>(65535u, N - bs);
+      const uint32_t seg_bl = (uint32_t)min<uint64_t>(bl, S + n - bs);  // its bytes inside this segment
+      uint8_t *hp = ob + (bs - S) + 5u * j;
       if (t == 0) {
-        hp[0] = (uint8_t)((last && b + 1 == nblk) ? 1u : 0u);
+        hp[0] = (uint8_t)((jb.term == ZS_DT_FINAL && bs + bl == N) ? 1u : 0u);  // the final block may start a segment early
         hp[1] = (uint8_t)bl;
         hp[2] = (uint8_t)(bl >> 8);
         hp[3] = (uint8_t)~bl;
         hp[4] = (uint8_t)(~bl >> 8);
       }
-      for (uint32_t i = t; i < bl; i += DZ_T) hp[5 + i] = in[off + i];
+      for (uint32_t i = t; i < seg_bl; i += DZ_T) hp[5 + i] = in[bs - S + i];
     }
-    if (t == 0) segs[blockIdx.x].nbits = 8u * (n + 5u * nblk);
+    if (t == 0) segs[blockIdx.x].nbits = 8u * (n + 5u * nst);
     return;
   }
   const uint32_t *C = aux + (uint64_t)DZ_HROWS * nseg + (uint64_t)blockIdx.x * DZ_CROW;

@@ -273,7 +273,7 @@ def deflate_batch(streams, window_bits=-15, level=-1, out_caps=None, fast=False)
     """Deflate many whole buffers on the GPU (host buffers).
 
     Each job behaves like deflateInit2(level, Z_DEFLATED, window_bits, 8,
-    Z_DEFAULT_STRATEGY) + one deflate(Z_FINISH).  Levels 4..9 write zlib's bytes
+    Z_DEFAULT_STRATEGY) + one deflate(Z_FINISH).  Levels 0 and 4..9 write zlib's bytes
     (unless fast=True: ZS_F_DEFLATE_FAST, the throughput path with its own block
     structure).  Returns [(bytes, result_dict)].
     """
