@@ -149,12 +149,15 @@ typedef struct zs_djob {
    + one deflate(Z_FINISH) over the whole input: ret Z_STREAM_END (Z_OK when
    out_cap was too small: total_out = out_cap bytes of the stream), total_in,
    total_out, adler (CRC-32 for gzip, Adler-32 for zlib, 1 for raw).
-   Levels 4..9 write zlib's bytes: the same stream zlib 1.2.11's deflate_slow +
-   trees.c produce (the reference's deflate, src/wasm/deflate_stream_wasm.c:
-   31-49 and src/trees.c), byte for byte.  Levels 0..3, window_bits -16
-   (deflate64) and ZS_F_DEFLATE_FAST write valid deflate that any inflater
-   decodes to the input, with the GPU's own block structure (not zlib's bytes). */
-#define ZS_F_DEFLATE_FAST 4u /* levels 4..9: the throughput path instead of zlib's bytes */
+   Every level writes zlib's bytes: the same stream zlib 1.2.11 produces
+   (the reference's deflate, src/wasm/deflate_stream_wasm.c:22-49 passes the
+   level through; src/trees.c), byte for byte -- level 0 deflate_stored's
+   65535-byte blocks, levels 1..3 deflate_fast (serial per stream: one wave
+   per job, ~4-18 MiB/s per stream), levels 4..9 deflate_slow (data-parallel).
+   window_bits -16 (deflate64) and ZS_F_DEFLATE_FAST write valid deflate that
+   any inflater decodes to the input, with the GPU's own block structure (not
+   zlib's bytes). */
+#define ZS_F_DEFLATE_FAST 4u /* levels 1..9: the throughput path instead of zlib's bytes */
 #define ZS_F_DEFLATE_SYNC 64u /* end each job as deflate(Z_SYNC_FLUSH) does at the end of its input: blocks
                                  not final, then an empty stored block (00 00 FF FF), no trailer; res.adler
                                  still holds the input's check (zlib/gzip) */
@@ -162,8 +165,9 @@ int zs_deflate_batch(const zs_djob *jobs, uint32_t n, zs_result *results, uint32
 uint64_t zs_deflate_bound(uint64_t in_len, int32_t window_bits);
 /* accumulated deflate timing (zs_profile(1) enables): [0] whole pipeline ms,
    [1] match, [2] parse, [3] blocks + checks, [4] offsets + stitch + trailer,
-   [5] batches.  zlib-identical jobs (levels 4..9): [1] chains + match search,
-   [2] parse + fix-up rounds, [3] trees + bits, [4] trailer.  Returns the
+   [5] batches.  zlib-identical jobs (levels 1..9): [1] chains + match search
+   (levels 4..9), [2] parse + fix-up rounds (levels 1..3: the whole serial
+   deflate_fast), [3] trees + bits, [4] trailer.  Returns the
    number of entries written. */
 int zs_profile_deflate(double *ms, uint32_t n);
 /* launch on this HIP stream (hipStream_t); NULL = the library's own stream */

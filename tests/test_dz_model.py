@@ -38,13 +38,14 @@ def zlib_raw(data, level, wbits=15):
 
 
 def test_model_small_and_edges():
+    """deflate_fast (1..3, serial) and deflate_slow (4..9, stage model)."""
     rng = random.Random(1)
     cases = [b"", b"a", b"ab", b"abc", b"abcabcabc", b"hello hello hello world", bytes(100000),
              bytes(rng.getrandbits(8) for _ in range(70000))]
     for extra in (-1, 0, 1):  # all-literal input ending on a block boundary
         cases.append(bytes(rng.getrandbits(8) for _ in range(16383 + extra)))
     for d in cases:
-        for lv in (4, 5, 6, 7, 8, 9):
+        for lv in range(1, 10):
             assert model(d, lv) == zlib_raw(d, lv), (len(d), lv)
 
 
@@ -54,7 +55,8 @@ def test_model_corpora_and_windows():
     lines = corpus.stream(33, 1 << 20)
     mixed = bytes(rng.getrandbits(8) for _ in range(40000)) + corpus.stream(2, 300000)
     for d in (zipf, lines, mixed):
-        for lv in (4, 6, 7):
+        for lv in (1, 3, 4, 6, 7):
             assert model(d, lv) == zlib_raw(d, lv)
     for wb in (9, 12, 14):
         assert model(mixed, 6, wb) == zlib_raw(mixed, 6, wb)
+        assert model(mixed, 2, wb) == zlib_raw(mixed, 2, wb)

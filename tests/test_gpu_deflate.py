@@ -1,7 +1,7 @@
 """GPU deflate (LZ77 match-find + Huffman emission)
 through the C-ABI.
 
-Bar, levels 4..9 (the reference's deflate_slow levels; level 6 is
+Bar, levels 1..9 (deflate_fast 1..3, deflate_slow 4..9; level 6 is
 Z_DEFAULT_COMPRESSION): the GPU writes zlib's bytes -- the exact stream host
 zlib 1.2.11 writes for deflateInit2(level, Z_DEFLATED, window_bits, 8,
 Z_DEFAULT_STRATEGY) + deflate(Z_FINISH), which SURVEY.md §8c pins as
@@ -10,7 +10,7 @@ inflates back through the CPU oracle and host zlib.
 
 Level 0 (deflate_stored): zlib's bytes too, with or without ZS_F_DEFLATE_FAST.
 
-Levels 1..3 and ZS_F_DEFLATE_FAST (the throughput path): every GPU stream is
+ZS_F_DEFLATE_FAST (the throughput path, any level): every GPU stream is
 valid deflate that the oracle and host zlib inflate to the input, with
 Z_STREAM_END, the whole stream consumed, the wrapper bytes and check value as
 zlib writes them; its size is bounded against zlib at the same level.
@@ -62,7 +62,7 @@ def zlib_bytes(data, wbits, level):
 
 def check_stream(data, wbits, level, comp, info, fast=False):
     assert info["ret"] == 1, info
-    if level == 0 or (4 <= level <= 9 and not fast):
+    if level == 0 or (1 <= level <= 9 and not fast):
         ref = zlib_bytes(data, wbits, level)
         assert comp == ref, ("not zlib's bytes", len(data), wbits, level, len(comp), len(ref))
     assert info["total_in"] == len(data) and info["total_out"] == len(comp), info
@@ -134,24 +134,28 @@ def test_deflate_small_out_cap(zs):
     assert info["ret"] == 0 and info["total_out"] == 1000 and part == full[:1000]
 
 
-def test_deflate_zlib_bytes_levels_4_to_9(zs):
-    """Every deflate_slow level, every wrapper, the corpora and edge sizes:
-    byte-identical to host zlib (long matches, stored blocks, block ends at
-    16383 symbols, the empty final block, windows below 32 KiB)."""
+def test_deflate_zlib_bytes_levels_1_to_9(zs):
+    """Every deflate_fast (1..3) and deflate_slow (4..9) level, every wrapper,
+    the corpora and edge sizes: byte-identical to host zlib (long matches,
+    stored blocks, block ends at 16383 symbols, the empty final block, windows
+    below 32 KiB; zero runs and short periods, where deflate_fast's skipped
+    insertions shape every later chain)."""
     rng = random.Random(11)
     pats = _patterns(rng)
     cases = []
     for name, p in pats.items():
         for n in (0, 1, 3, 300, 16383, 16384, 65536, 70000, 200000):
             if n <= len(p):
-                for lv in (4, 5, 6, 7, 8, 9):
+                for lv in range(1, 10):
                     cases.append((p[:n], rng.choice((-15, 15, 31)), lv))
     # all-literal stretches whose symbol count ends exactly on a block boundary
     for extra in (-2, -1, 0, 1, 2):
         rnd = bytes(rng.getrandbits(8) for _ in range(2 * 16383 + extra))
         cases.append((rnd, -15, 6))
+        cases.append((rnd, 15, 1))
     for wb in (-9, -10, -13, 9, 12, 25, 29):
         cases.append((pats["text"][:150000], wb, 6))
+        cases.append((pats["lines"][:150000], wb, 2))
     got = zs.deflate_batch([c[0] for c in cases], [c[1] for c in cases], [c[2] for c in cases])
     bad = [(i, len(d), wb, lv) for i, ((d, wb, lv), (comp, info)) in enumerate(zip(cases, got))
            if comp != zlib_bytes(d, wb, lv) or info["ret"] != 1]
@@ -220,7 +224,7 @@ def test_deflate_fast_mode_all_levels(zs):
     rng = random.Random(5)
     pats = _patterns(rng)
     cases = [(p[:n], wb, lv) for p in pats.values() for n in (0, 5, 65537, 200000) if n <= len(p)
-             for wb in (-15, 31) for lv in (4, 6, 9)]
+             for wb in (-15, 31) for lv in (1, 3, 4, 6, 9)]
     got = zs.deflate_batch([c[0] for c in cases], [c[1] for c in cases], [c[2] for c in cases], fast=True)
     for (d, wb, lv), (comp, info) in zip(cases, got):
         check_stream(d, wb, lv, comp, info, fast=True)
@@ -381,7 +385,7 @@ def test_deflate_sync_flush_is_zlibs(zs):
     flush with no input makes no progress (Z_BUF_ERROR)."""
     data = corpus.stream(15, 700000)
     for wb in (-15, 15, 31):
-        for level in (6, 9):
+        for level in (1, 6, 9):
             c = zlib.compressobj(level, zlib.DEFLATED, wb, 8, zlib.Z_DEFAULT_STRATEGY)
             ref_sync = c.compress(data) + c.flush(zlib.Z_SYNC_FLUSH)
             ref_end = c.flush(zlib.Z_FINISH)
@@ -396,14 +400,14 @@ def test_deflate_sync_flush_is_zlibs(zs):
 
 
 def test_deflate_stream_buffer_bound_fast_levels(zs, monkeypatch):
-    """Levels 0..3 (the GPU throughput encoder): past ZS_DSTREAM_MAX_KB of
-    gathered input a stream sends its blocks without waiting for a flush (a
-    non-final block end, no injected flush marker), and still decodes to the
-    input."""
+    """Level 0 in a stream (the throughput encoder's stored blocks): past
+    ZS_DSTREAM_MAX_KB of gathered input a stream sends its blocks without
+    waiting for a flush (a non-final block end, no injected flush marker), and
+    still decodes to the input."""
     monkeypatch.setenv("ZS_DSTREAM_MAX_KB", "256")
     data = corpus.stream(16, 2 << 20)
     for wb in (-15, 31):
-        g = _GpuDeflate(zs, 1, wb)
+        g = _GpuDeflate(zs, 0, wb)
         out, early = bytearray(), 0
         for off in range(0, len(data), 65536):
             o, ret = g.call(data[off:off + 65536], 0)
@@ -453,7 +457,7 @@ def _compare_calls(zs, level, wb, calls, out_len):
     return bytes(total)
 
 
-@pytest.mark.parametrize("level", [4, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("level", [1, 2, 3, 4, 5, 6, 7, 8, 9])
 def test_deflate_stream_calls_are_zlibs(zs, level):
     """zlib's deflate() call by call (reference: src/wasm/deflate_stream_wasm.c:51-55
     runs one deflate per process call): random input sizes and every flush value
@@ -498,7 +502,7 @@ def test_deflate_small_buffer_flush_loops_are_zlibs(zs):
     import libz_ref
     rng = random.Random(77)
     data = _stream_data(rng, 900_000)
-    for level, wb in ((6, -15), (9, 31), (4, 15)):
+    for level, wb in ((6, -15), (9, 31), (4, 15), (1, -15), (3, 31)):
         segs, off = [], 0
         while off < len(data):
             n = rng.choice([5000, 40000, 120000])
@@ -537,7 +541,7 @@ def test_compression_stream_js_schedule_calls_are_zlibs(zs):
     data = corpus.stream(41, 1_200_000) + bytes(100000) + corpus.stream(5, 300000)
     for fmt, wb, init in (("deflate-raw", -15, L.deflate_init_raw), ("gzip", 31, L.deflate_init_gzip),
                           ("deflate", 15, L.deflate_init)):
-        for level in (4, 6, 9):
+        for level in (1, 4, 6, 9):
             h = L.deflate_new()
             assert init(h, level) == 0
             ref = libz_ref.Deflater(level, wb)

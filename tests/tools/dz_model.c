@@ -1,5 +1,5 @@
 /*
- * dz_model.c -- CPU model of the GPU's zlib-identical deflate (levels 4..9),
+ * dz_model.c -- CPU model of the GPU's zlib-identical deflate (levels 1..9),
  * test infrastructure only: it states the stage decomposition the HIP kernels
  * use and is checked byte-for-byte against host zlib (tests/test_dz_model.py),
  * so every stage's semantics are pinned before they run on the GPU.
@@ -435,11 +435,63 @@ static uint32_t slides_at(uint32_t t, uint32_t L, uint32_t wsize, uint32_t max_d
   }
 }
 
-/* Raw deflate of in[0..L) at `level` (4..9), window bits wbits (9..15):
+/* ---- levels 1..3: deflate_fast ------------------------------------------
+ * zlib deflate.c configuration_table rows 1..3 (good, lazy = max_insert_length,
+ * nice, chain).  deflate_fast searches at every loop top (prev_length stays
+ * MIN_MATCH - 1, so the full chain budget always applies), takes any match of
+ * >= MIN_MATCH (no TOO_FAR rule), and inserts a match's inner positions into
+ * the hash chains only when its length is <= max_insert_length and >= 3 bytes
+ * follow it.  So the chain of a position holds only the INSERTED earlier
+ * positions of its hash: the search depends on every earlier parse decision,
+ * and the model runs the loop serially, as the GPU kernel does (one wave per
+ * stream, zs_zd_fast_kernel).  Iterating "matches under an assumed insertion
+ * set -> parse -> the set it implies" to a fixed point is exact (the fixed
+ * point is unique) but, measured on line text, fixes only ~1 K positions per
+ * round: a wrong insertion history changes the parse for good
+ * (tools/fast_resync_probe.c). */
+static const uint16_t CFGF[4][4] = {{0, 0, 0, 0}, {4, 4, 8, 4}, {4, 5, 16, 8}, {4, 6, 32, 32}};
+
+/* longest match at p over inserted positions only (ins: 1 per position) */
+static void longest_ins(const uint8_t *in, uint32_t L, const uint32_t *prevd, const uint8_t *ins, uint32_t p,
+                        uint32_t max_dist, uint32_t chain, uint32_t nice, dz_match *out) {
+  out->len = 0;
+  out->dist = 0;
+  if (p + MINM > L) return;
+  /* hash_head: the latest inserted same-hash position before p */
+  uint32_t c = prevd[p] ? p - prevd[p] : 0;
+  while (c && !ins[c] && p - c <= max_dist) c = prevd[c] ? c - prevd[c] : 0;
+  if (!c || p - c > max_dist) return;
+  const uint32_t look = L - p;
+  const uint32_t cap = look < MAXM ? look : MAXM;
+  const uint32_t nice_p = nice < look ? nice : look;
+  uint32_t best = 0;
+  for (uint32_t k = 0;;) {
+    uint32_t n = 0;
+    while (n < cap && in[c + n] == in[p + n]) n++;
+    if (n > best) {
+      best = n;
+      out->len = (uint16_t)n;
+      out->dist = (uint16_t)(p - c);
+      if (n >= nice_p) break;
+    }
+    if (++k >= chain) break;
+    uint32_t nc = prevd[c] ? c - prevd[c] : 0;
+    while (nc && !ins[nc] && p - nc < max_dist) nc = prevd[nc] ? nc - prevd[nc] : 0;
+    if (!nc || p - nc >= max_dist) break;
+    c = nc;
+  }
+}
+
+static size_t dz_blocks_out(const uint8_t *in, uint32_t L, int fast, uint32_t wbits, const dz_sym *syms, uint32_t ns,
+                            int end_lit, uint8_t *out, size_t cap);
+size_t dz_model_fast_serial(const uint8_t *in, uint32_t L, int level, int wbits, uint8_t *out, size_t cap);
+
+/* Raw deflate of in[0..L) at `level` (1..9), window bits wbits (9..15):
  * returns the compressed size (bytes written up to cap). */
 size_t dz_model_deflate(const uint8_t *in, uint32_t L, int level, int wbits, uint8_t *out, size_t cap) {
   stat_init();
-  if (level < 4 || level > 9) return 0;
+  if (level < 1 || level > 9) return 0;
+  if (level <= 3) return dz_model_fast_serial(in, L, level, wbits, out, cap);
   const uint32_t wsize = 1u << wbits, max_dist = wsize - LOOKAHEAD_MIN;
   uint32_t *prevd = (uint32_t *)calloc(L + 1, sizeof(uint32_t));
   dz_match *ma = (dz_match *)calloc(L + 1, sizeof(dz_match)), *mb = (dz_match *)calloc(L + 1, sizeof(dz_match));
@@ -452,6 +504,17 @@ size_t dz_model_deflate(const uint8_t *in, uint32_t L, int level, int wbits, uin
   }
   int end_lit = 0;
   const uint32_t ns = stage_parse(in, L, level, ma, mb, syms, &end_lit);
+  const size_t r = dz_blocks_out(in, L, 0, (uint32_t)wbits, syms, ns, end_lit, out, cap);
+  free(prevd);
+  free(ma);
+  free(mb);
+  free(syms);
+  return r;
+}
+
+static size_t dz_blocks_out(const uint8_t *in, uint32_t L, int fast, uint32_t wbits, const dz_sym *syms, uint32_t ns,
+                            int end_lit, uint8_t *out, size_t cap) {
+  const uint32_t wsize = 1u << wbits, max_dist = wsize - LOOKAHEAD_MIN;
   dz_bits b = {out, cap, 0, 0, 0};
   /* blocks of BLOCK_SYMS symbols; the last one holds the rest -- or is empty
    * when a symbol of the main loop filled the previous block exactly */
@@ -465,16 +528,46 @@ size_t dz_model_deflate(const uint8_t *in, uint32_t L, int level, int wbits, uin
     const dz_sym *e = cnt ? &syms[s0 + cnt - 1] : NULL;
     const uint32_t first = cnt ? syms[s0].pos : L;
     const uint32_t end = cnt ? e->pos + (e->dist ? e->lit_or_len : 1) : L;
-    /* the flush runs in the iteration whose loop top followed the block's
-     * last symbol's start (a literal at strstart-1, a match found at
-     * strstart-1); the final block flushes after the loop (top = L) */
-    const uint32_t top = last ? L : e->pos + 1;
+    /* deflate_slow flushes in the iteration whose loop top followed the
+     * block's last symbol's start (a literal at strstart-1, a match found at
+     * strstart-1); deflate_fast in the symbol's own iteration; the final
+     * block flushes after the loop (top = L) */
+    const uint32_t top = last ? L : e->pos + (fast ? 0 : 1);
     const int stored_ok = (uint64_t)first >= (uint64_t)slides_at(top, L, wsize, max_dist) * wsize;
     flush_block(&b, in, syms + s0, cnt, first, end - first, stored_ok, last);
   }
-  free(prevd);
-  free(ma);
-  free(mb);
-  free(syms);
   return b.n;
+}
+
+/* the serial deflate_fast (a hash chain walk per loop top, the insertion set
+ * built as it goes), to pin the iterated form: returns the compressed size */
+size_t dz_model_fast_serial(const uint8_t *in, uint32_t L, int level, int wbits, uint8_t *out, size_t cap) {
+  stat_init();
+  if (level < 1 || level > 3) return 0;
+  const uint32_t wsize = 1u << wbits, max_dist = wsize - LOOKAHEAD_MIN;
+  uint32_t *prevd = (uint32_t *)calloc(L + 1, sizeof(uint32_t));
+  uint8_t *ins = (uint8_t *)calloc(L + 1, 1);
+  dz_sym *syms = (dz_sym *)malloc(((size_t)L + 1) * sizeof(dz_sym));
+  stage_prev(in, L, prevd);
+  const uint32_t max_ins = CFGF[level][1], nice = CFGF[level][2], chain = CFGF[level][3];
+  uint32_t n = 0, p = 0;
+  while (p < L) {
+    dz_match m;
+    longest_ins(in, L, prevd, ins, p, max_dist, chain, nice, &m);
+    if (p + MINM <= L) ins[p] = 1;
+    if (m.len >= MINM) {
+      syms[n++] = (dz_sym){m.len, m.dist, p};
+      if (m.len <= max_ins && L - (p + m.len) >= MINM)
+        for (uint32_t q = p + 1; q < p + m.len; q++) ins[q] = 1;
+      p += m.len;
+    } else {
+      syms[n++] = (dz_sym){in[p], 0, p};
+      p++;
+    }
+  }
+  const size_t r = dz_blocks_out(in, L, 1, (uint32_t)wbits, syms, n, 0, out, cap);
+  free(prevd);
+  free(ins);
+  free(syms);
+  return r;
 }

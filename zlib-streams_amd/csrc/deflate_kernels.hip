@@ -1126,7 +1126,7 @@ __global__ void zs_dz_trailer_kernel(const ZsDJobDev *__restrict__ jobs, uint32_
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= njobs) return;
   const ZsDJobDev jb = jobs[j];
-  if (jb.exact != exact) return;
+  if ((jb.exact != 0) != (exact != 0)) return;
   uint8_t *o = stage + jb.stage;
   if (jb.term == ZS_DT_SYNC) {  // the empty stored block's LEN / NLEN (its header bits and padding are zero)
     uint8_t *p = o + jb.total_out - 4;

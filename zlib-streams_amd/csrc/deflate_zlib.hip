@@ -342,9 +342,10 @@ __device__ __forceinline__ void zd_putbit(uint32_t *w, uint64_t i, bool v) {
 }
 __device__ __forceinline__ bool zd_getbit(const uint32_t *w, uint64_t i) { return (w[i >> 5] >> (i & 31u)) & 1u; }
 
-// bitmaps of a job: S (token starts), V (variant of match starts), M (state-A marks)
+// bitmaps of a job: S (token starts), V (variant of match starts), M (state-A
+// marks), I (deflate_fast: positions inserted into the hash chains)
 struct ZdBm {
-  uint32_t *S, *V, *M;
+  uint32_t *S, *V, *M, *I;
 };
 __device__ __forceinline__ uint64_t zd_bm_words(uint64_t L) { return (L + 32u) / 32u + 1u; }
 __device__ __forceinline__ ZdBm zd_bm(uint32_t *bm, const ZsDJobDev &jb) {
@@ -353,6 +354,7 @@ __device__ __forceinline__ ZdBm zd_bm(uint32_t *bm, const ZsDJobDev &jb) {
   b.S = bm + jb.bm0;
   b.V = b.S + words;
   b.M = b.V + words;
+  b.I = b.M + words;
   return b;
 }
 
@@ -386,7 +388,7 @@ __global__ void __launch_bounds__(ZD_PT) zs_zd_parse_kernel(const ZsDJobDev *__r
   const uint32_t t = threadIdx.x;
   const ZsDSegDev sg = segs[blockIdx.x];
   const ZsDJobDev jb = jobs[sg.job];
-  if (!jb.exact) return;
+  if (jb.exact != ZD_SLOW) return;
   ZdTabs T;
   T.ma = ma + jb.pos0;
   T.mb = mb + jb.pos0;
@@ -552,7 +554,7 @@ __global__ void zs_zd_fix_kernel(const ZsDJobDev *__restrict__ jobs, ZsDSegDev *
   if (i >= nseg) return;
   const ZsDSegDev sg = segs[i];
   const ZsDJobDev jb = jobs[sg.job];
-  if (!jb.exact) return;
+  if (jb.exact != ZD_SLOW) return;
   uint64_t ep = sg.start;
   uint32_t es = ZD_STATE_A;
   if (sg.start != 0) {
@@ -575,7 +577,7 @@ __global__ void zs_zd_fix_seq_kernel(const ZsDJobDev *__restrict__ jobs, uint32_
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= njobs) return;
   const ZsDJobDev jb = jobs[j];
-  if (!jb.exact) return;
+  if (jb.exact != ZD_SLOW) return;
   uint64_t ep = 0;
   uint32_t es = ZD_STATE_A;
   for (uint32_t i = jb.seg0; i < jb.seg0 + jb.nseg; i++) {
@@ -591,6 +593,263 @@ __global__ void zs_zd_fix_seq_kernel(const ZsDJobDev *__restrict__ jobs, uint32_
     ep = xp;
     es = xs;
   }
+}
+
+// ---------------------------------------------------------------------------
+// K3c: levels 1..3, deflate_fast (zlib deflate.c, configuration_table rows
+// 1..3).  deflate_fast inserts a match's inner positions into the hash chains
+// only when the match is at most max_insert_length (= max_lazy) long, so the
+// chain a search walks depends on every earlier parse decision -- and on
+// periodic text that dependence never dies out: started mid-stream from a
+// different insertion history, the parse of `line-%08d` text still differs
+// 4 MiB later (13% of decisions; tools/fast_resync_probe.c), so no
+// speculative split of a stream can be verified locally.  The parse is
+// therefore serial per stream, and the parallelism is inside one step: one
+// wave per job, zlib's head / prev tables in LDS, and 64 consecutive positions
+// searched at once against the tables as they stand before those positions.
+// A position's search is the one zlib makes there unless an earlier position
+// of the same 64 with the same hash gets inserted first (its chain would then
+// start there): the wave walks the loop tops in order, commits searches until
+// the first such one, inserts what it committed, and starts the next step at
+// that position.  Positions are kept as (absolute & 0xffff), entries older
+// than a window reset every 16 Ki positions (as zs_zd_prev_kernel), so a
+// stored position decodes as `q - ((q - e) & 0xffff)` without aliasing.
+// Output: token starts (S), match length | distance << 9 at each match start
+// (ma), the insertion bits (I) -- the format of the deflate_slow parse, read by
+// the same block kernels.
+// ---------------------------------------------------------------------------
+// zlib deflate.c configuration_table rows 1..3: good, lazy (max_insert_length), nice, chain
+__constant__ uint16_t zd_cfgf[4][4] = {{0, 0, 0, 0}, {4, 4, 8, 4}, {4, 5, 16, 8}, {4, 6, 32, 32}};
+#define ZF_SWEEP 16384u
+
+// the job's input read as aligned words (unaligned caller buffers; word
+// indices clamped to the buffer's own words)
+struct ZfIn {
+  const uint32_t *w;
+  uint32_t sh;
+  uint64_t nw;
+  __device__ void init(const uint8_t *in, uint64_t L) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(in);
+    w = reinterpret_cast<const uint32_t *>(a & ~uintptr_t(3));
+    sh = (uint32_t)(a & 3u);
+    nw = (sh + L + 3) / 4;
+    if (nw == 0) nw = 1;
+  }
+  __device__ __forceinline__ uint32_t ld4(uint64_t pos) const {  // bytes pos..pos+3 (past the end: unspecified)
+    const uint64_t a = pos + sh, k = a >> 2;
+    const uint32_t lo = w[min(k, nw - 1)], hi = w[min(k + 1, nw - 1)];
+    return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(a & 3u));
+  }
+};
+
+__device__ __forceinline__ uint32_t zf_hash(const ZfIn &X, uint64_t q) {
+  const uint32_t v = X.ld4(q);
+  return (((v & 0xffu) << 10) ^ (((v >> 8) & 0xffu) << 5) ^ ((v >> 16) & 0xffu)) & 0x7fffu;
+}
+
+// age out entries more than a window old (see zs_zd_prev_kernel's sweep)
+__device__ void zf_sweep(uint16_t *tab, uint64_t b, uint32_t lane) {
+  const uint32_t sent = (uint32_t)((b - 40000u) & 0xffffu);
+  for (uint32_t i = lane * 8; i < 65536u; i += WAVE * 8) {
+    uint4 v = *reinterpret_cast<const uint4 *>(&tab[i]);
+    uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      uint32_t lo = wv[k] & 0xffffu, hi = wv[k] >> 16;
+      if (((uint32_t)(b - lo) & 0xffffu) > 32768u) lo = sent;
+      if (((uint32_t)(b - hi) & 0xffffu) > 32768u) hi = sent;
+      wv[k] = lo | (hi << 16);
+    }
+    *reinterpret_cast<uint4 *>(&tab[i]) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+  }
+}
+
+// lanes of the wave with the same 15-bit hash (among `on` lanes)
+__device__ __forceinline__ uint64_t zf_same(uint32_t h, bool on) {
+  uint64_t m = __ballot(on);
+#pragma unroll
+  for (int b = 0; b < 15; b++) {
+    const uint64_t B = __ballot(on && ((h >> b) & 1u));
+    m &= ((h >> b) & 1u) ? B : ~B;
+  }
+  return on ? m : 0ull;
+}
+
+// INSERT_STRING for every lane with `ins` set, in lane (position) order:
+// prev[q] = the latest earlier inserted position of its hash (an earlier lane
+// of this step, else the head), head = the group's last inserted lane
+__device__ __forceinline__ void zf_insert(uint16_t *head, uint16_t *prev, uint64_t q, uint32_t h, bool ins,
+                                          uint64_t same, uint32_t lane) {
+  const uint64_t insm = __ballot(ins);
+  const uint64_t below = same & insm & ((1ull << lane) - 1ull);
+  const uint64_t above = lane == 63 ? 0ull : (same & insm & ~((2ull << lane) - 1ull));
+  uint32_t pv = 0;
+  if (ins) pv = below ? (uint32_t)((q - lane + (63u - (uint32_t)__builtin_clzll(below))) & 0xffffu) : head[h];
+  __builtin_amdgcn_wave_barrier();
+  if (ins) {
+    prev[q & 0x7fffu] = (uint16_t)pv;
+    if (!above) head[h] = (uint16_t)(q & 0xffffu);
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
+// longest_match at q (prev_length = MIN_MATCH - 1, the full chain budget):
+// candidates from head entry e0, best length and the distance of the first
+// candidate reaching it
+__device__ __forceinline__ void zf_search(const ZfIn &X, const uint16_t *prev, uint64_t q, uint64_t L, uint32_t e0,
+                                          uint32_t max_dist, uint32_t nice, uint32_t chain, uint32_t &olen,
+                                          uint32_t &odist) {
+  olen = 0;
+  odist = 0;
+  uint32_t age = (uint32_t)(q - e0) & 0xffffu;
+  if (age > max_dist || age == 0 || q == age) return;  // NIL, out of range, or position 0 (zlib's NIL)
+  const uint64_t look = L - q;
+  const uint32_t cap = look < ZD_MAXM ? (uint32_t)look : ZD_MAXM;
+  const uint32_t nicep = look < nice ? (uint32_t)look : nice;
+  uint32_t best = ZD_MINM - 1, bdist = 0;
+  for (uint32_t k = 0;;) {
+    const uint64_t c = q - age;
+    uint32_t n = 0;
+    for (;;) {  // 16 bytes of both strings per step
+      uint32_t x = 0, g = 0;
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const uint32_t d = X.ld4(c + n + 4 * i) ^ X.ld4(q + n + 4 * i);
+        if (x == 0) {
+          x = d;
+          g = (uint32_t)i;
+        }
+      }
+      if (x) {
+        n += 4 * g + ((uint32_t)__builtin_ctz(x) >> 3);
+        break;
+      }
+      n += 16;
+      if (n >= cap) break;
+    }
+    n = min(n, cap);
+    if (n > best) {
+      best = n;
+      bdist = age;
+      if (n >= nicep) break;
+    }
+    if (++k >= chain) break;
+    const uint32_t e = prev[c & 0x7fffu];
+    age = (uint32_t)(q - e) & 0xffffu;
+    if (age >= max_dist || q == age) break;  // cur_match <= strstart - MAX_DIST, or NIL
+  }
+  if (best >= ZD_MINM) {
+    olen = best;
+    odist = bdist;
+  }
+}
+
+__global__ void __launch_bounds__(WAVE) zs_zd_fast_kernel(ZsDJobDev *__restrict__ jobs, uint32_t *__restrict__ bm,
+                                                           uint32_t *__restrict__ ma) {
+  __shared__ __attribute__((aligned(16))) uint16_t s_tab[65536];  // head[32768] | prev[32768]
+  uint16_t *s_head = s_tab, *s_prev = s_tab + 32768;
+  const uint32_t lane = threadIdx.x;
+  const ZsDJobDev jb = jobs[blockIdx.x];
+  if (jb.exact != ZD_FAST) return;
+  const uint64_t L = jb.in_len;
+  ZfIn X;
+  X.init(jb.in, L);
+  const ZdBm B = zd_bm(bm, jb);
+  uint32_t *om = ma + jb.pos0;
+  const uint32_t level = (uint32_t)jb.level;
+  const uint32_t max_ins = zd_cfgf[level][1], nice = zd_cfgf[level][2], chain = zd_cfgf[level][3];
+  const uint32_t max_dist = zd_max_dist(jb);
+  const bool cut = jb.term == ZS_DT_CUT;
+  {
+    const uint32_t sent = (uint32_t)((0u - 40000u) & 0xffffu);
+    for (uint32_t i = lane; i < 32768u / 2; i += WAVE) {
+      reinterpret_cast<uint32_t *>(s_head)[i] = sent | (sent << 16);
+      reinterpret_cast<uint32_t *>(s_prev)[i] = sent | (sent << 16);
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  uint64_t next_sweep = ZF_SWEEP;
+  auto sweep_to = [&](uint64_t p) {
+    if (p < next_sweep) return;
+    __builtin_amdgcn_wave_barrier();
+    zf_sweep(s_tab, p, lane);
+    __builtin_amdgcn_wave_barrier();
+    next_sweep = p + ZF_SWEEP;
+  };
+  // the history before the parse entry: its inserted positions, in order
+  // (a stream segment's window; the bits come from the previous segment)
+  for (uint64_t p = 0; p < jb.pstart; p += WAVE) {
+    sweep_to(p);
+    const uint64_t q = p + lane;
+    const bool on = q < jb.pstart && q + ZD_MINM <= L && zd_getbit(B.I, q);
+    const uint32_t h = q + ZD_MINM <= L ? zf_hash(X, q) : 0u;
+    zf_insert(s_head, s_prev, q, h, on, zf_same(h, on), lane);
+  }
+  uint64_t p = jb.pstart;
+  bool stop = false;
+  while (p < L && !stop) {
+    sweep_to(p);
+    const uint64_t q = p + lane;
+    const bool insq = q + ZD_MINM <= L;  // zlib inserts and searches only with lookahead >= MIN_MATCH
+    const uint32_t h = insq ? zf_hash(X, q) : 0u;
+    const uint64_t same = zf_same(h, insq);
+    const uint64_t below = same & ((1ull << lane) - 1ull);
+    uint32_t mlen = 0, mdist = 0;
+    if (insq) zf_search(X, s_prev, q, L, s_head[h], max_dist, nice, chain, mlen, mdist);
+    // commit loop tops in order (wave-uniform): stop at the end, at a cut
+    // job's first short lookahead, or at the first search an earlier inserted
+    // position of this step invalidates
+    uint32_t t = 0;
+    uint64_t insm = 0, tokm = 0;
+    while (t < WAVE) {
+      const uint64_t qt = p + t;
+      if (qt >= L) break;
+      if (cut && L - qt < ZD_LOOK) {
+        stop = true;
+        break;
+      }
+      const uint64_t bt = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(below >> 32), t) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane((uint32_t)below, t);
+      if (bt & insm) break;
+      const uint32_t lt = __builtin_amdgcn_readlane(mlen, t);
+      const bool it = qt + ZD_MINM <= L;
+      if (lt >= ZD_MINM) {
+        const bool shrt = lt <= max_ins && L - (qt + lt) >= ZD_MINM;
+        if (shrt && t + lt > WAVE) break;  // its inner inserts would pass this step
+        tokm |= 1ull << t;
+        if (shrt) insm |= (lt == 64 ? ~0ull : ((1ull << lt) - 1ull)) << t;
+        else if (it) insm |= 1ull << t;
+        t += lt;
+      } else {
+        tokm |= 1ull << t;
+        if (it) insm |= 1ull << t;
+        t += 1;
+      }
+    }
+    const bool tok = (tokm >> lane) & 1ull, ins = (insm >> lane) & 1ull;
+    if (tok && mlen >= ZD_MINM) om[q] = mlen | (mdist << 9);
+    if (lane < 3) {  // token starts and insertion bits of [p, p + 64): three words
+      const uint32_t sh = (uint32_t)(p & 31u);
+      const uint64_t w0 = p >> 5;
+      const uint32_t k = lane;
+      uint32_t vs, vi;
+      if (k == 0) {
+        vs = (uint32_t)(tokm << sh);
+        vi = (uint32_t)(insm << sh);
+      } else if (k == 1) {
+        vs = (uint32_t)(sh ? (tokm >> (32 - sh)) : (tokm >> 32));
+        vi = (uint32_t)(sh ? (insm >> (32 - sh)) : (insm >> 32));
+      } else {
+        vs = sh ? (uint32_t)(tokm >> (64 - sh)) : 0u;
+        vi = sh ? (uint32_t)(insm >> (64 - sh)) : 0u;
+      }
+      if (vs) atomicOr(&B.S[w0 + k], vs);
+      if (vi) atomicOr(&B.I[w0 + k], vi);
+    }
+    zf_insert(s_head, s_prev, q, h, ins, same, lane);
+    p += t;
+  }
+  if (lane == 0) jobs[blockIdx.x].cut_pos = p;  // where the parse stopped (zs_zd_cut_kernel)
 }
 
 // ---------------------------------------------------------------------------
@@ -678,7 +937,9 @@ __global__ void __launch_bounds__(1024) zs_zd_blocks_kernel(ZsDJobDev *__restric
     const uint32_t *S = bm + jb.bm0;
     const uint64_t L = jb.in_len;
     const uint64_t eff = acc - min(acc, jb.skip);  // symbols of this job's blocks
-    const bool end_lit = eff && zd_getbit(S, L - 1);
+    // deflate_slow tallies its pending last literal after the loop without a
+    // flush check; deflate_fast tallies every symbol inside it
+    const bool end_lit = jb.exact == ZD_SLOW && eff && zd_getbit(S, L - 1);
     const uint64_t nfull = eff / ZD_BLOCK;
     const bool empty_last = eff % ZD_BLOCK == 0 && !end_lit;
     // Z_FINISH flushes an empty last block; a flush mid-stream only a
@@ -722,13 +983,14 @@ __global__ void zs_zd_blist_kernel(const ZsDJobDev *__restrict__ jobs, uint32_t 
   b.nsym = (uint32_t)(s1 > s0 ? s1 - s0 : 0);
   b.first = b.nsym ? zd_sym_pos(segs, jb, S, s0) : L;
   b.end = s1 < ns ? zd_sym_pos(segs, jb, S, s1) : L;
-  // the flush runs in the iteration whose loop top followed the block's last
-  // symbol start; the last block of a flushed job flushes after the loop (top = L)
+  // deflate_slow flushes in the iteration whose loop top followed the block's
+  // last symbol start, deflate_fast in that symbol's own iteration; the last
+  // block of a flushed job flushes after the loop (top = L)
   uint64_t top = L;
   if (b.nsym && (!final_blk || jb.term == ZS_DT_CUT)) {
     uint64_t x = b.end - 1;
     while (!zd_getbit(S, x)) x--;
-    top = x + 1;
+    top = jb.exact == ZD_FAST ? x : x + 1;
   }
   b.top = top;
   // window slides counted in stream positions since zlib's window last restarted
@@ -768,6 +1030,24 @@ __global__ void zs_zd_cut_kernel(ZsDJobDev *__restrict__ jobs, uint32_t njobs, c
   if (!jb.exact || jb.term != ZS_DT_CUT) return;
   const uint32_t *S = bm + jb.bm0;
   const uint64_t L = jb.in_len;
+  if (jb.exact == ZD_FAST) {
+    // deflate_fast stopped at its first loop top with a short lookahead
+    // (jb.cut_pos, zs_zd_fast_kernel): every symbol before it is tallied and
+    // its full blocks are sent.  Every token start is a loop top, so the next
+    // segment restarts at the first unsent symbol with nothing to skip (its
+    // hash chains rebuilt from the insertion bits before it).
+    uint32_t K = 0;
+    while (K < jb.nzblk && blks[jb.zblk0 + K].nsym == ZD_BLOCK) K++;
+    const ZsDSegDev &ls = segs[jb.seg0 + jb.nseg - 1];
+    const uint64_t done = ls.sym0 + ls.nsym;
+    for (uint32_t k = K; k < jb.nzblk; k++) blks[jb.zblk0 + k].nsym = 0xffffffffu;
+    jobs[j].cut_open = done - (uint64_t)K * ZD_BLOCK;
+    jobs[j].cut_pos = K < jb.nzblk ? blks[jb.zblk0 + K].first : jb.cut_pos;
+    jobs[j].nzblk = K;
+    jobs[j].cut_state = ZD_STATE_A;
+    jobs[j].cut_skip = 0;
+    return;
+  }
   uint32_t K = 0;
   while (K < jb.nzblk && blks[jb.zblk0 + K].nsym == ZD_BLOCK && blks[jb.zblk0 + K].top + ZD_LOOK <= L) K++;
   uint64_t T = jb.pstart, sT = jb.pstate, skip = jb.skip + (uint64_t)K * ZD_BLOCK;
@@ -1361,17 +1641,18 @@ extern "C" int zs_launch_zdeflate(ZsDJobDev *d_jobs, uint32_t njobs, ZsDSegDev *
                                   const ZsZWorkDev *d_w1, uint32_t n1, const ZsZWorkDev *d_w2, uint32_t n2,
                                   uint16_t *d_prevd, uint32_t *d_ma, uint32_t *d_mb, uint32_t *d_bm, ZsZBlkDev *d_blks,
                                   uint32_t nblk_slots, const uint32_t *d_slot_job, uint32_t *d_aux, uint8_t *d_stage,
-                                  uint32_t *d_flag, hipStream_t st, hipEvent_t *ev) {
+                                  uint32_t *d_flag, int has_slow, int has_fast, hipStream_t st, hipEvent_t *ev) {
   if (ev) (void)hipEventRecord(ev[0], st);
   if (n1) hipLaunchKernelGGL(zs_zd_prev_kernel, dim3(n1), dim3(ZD_PT1), 0, st, d_jobs, d_w1, d_prevd);
   if (n2) hipLaunchKernelGGL(zs_zd_match_kernel, dim3(n2), dim3(ZD_MT), 0, st, d_jobs, d_w2, d_prevd, d_ma, d_mb);
   if (ev) (void)hipEventRecord(ev[1], st);
-  hipLaunchKernelGGL(zs_zd_parse_kernel, dim3(nseg), dim3(ZD_PT), 0, st, d_jobs, d_segs, d_ma, d_mb, d_bm);
+  if (has_fast) hipLaunchKernelGGL(zs_zd_fast_kernel, dim3(njobs), dim3(WAVE), 0, st, d_jobs, d_bm, d_ma);
+  if (has_slow) hipLaunchKernelGGL(zs_zd_parse_kernel, dim3(nseg), dim3(ZD_PT), 0, st, d_jobs, d_segs, d_ma, d_mb, d_bm);
   // parallel fix-up rounds while exits change (nearly every input settles in
   // one or two), then, if a cascade is still moving, the in-order pass
-  const int max_rounds = zd_fix_rounds();
+  const int max_rounds = has_slow ? zd_fix_rounds() : 0;
   uint32_t cur = 0;
-  bool settled = false;
+  bool settled = !has_slow;
   for (int round = 0; round < max_rounds; round++) {
     uint32_t changed = 0;
     if (hipMemsetAsync(d_flag, 0, sizeof(uint32_t), st) != hipSuccess) return -1;

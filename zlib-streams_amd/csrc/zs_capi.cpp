@@ -50,7 +50,7 @@ extern "C" int zs_launch_zdeflate(ZsDJobDev *d_jobs, uint32_t njobs, ZsDSegDev *
                                   const ZsZWorkDev *d_w1, uint32_t n1, const ZsZWorkDev *d_w2, uint32_t n2,
                                   uint16_t *d_prevd, uint32_t *d_ma, uint32_t *d_mb, uint32_t *d_bm, ZsZBlkDev *d_blks,
                                   uint32_t nblk_slots, const uint32_t *d_slot_job, uint32_t *d_aux, uint8_t *d_stage,
-                                  uint32_t *d_flag, hipStream_t st, hipEvent_t *ev);
+                                  uint32_t *d_flag, int has_slow, int has_fast, hipStream_t st, hipEvent_t *ev);
 extern "C" void zs_launch_dz_trailer(ZsDJobDev *d_jobs, uint32_t njobs, uint8_t *d_stage, hipStream_t st);
 extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, ZsSegDev *d_segs, uint32_t nseg,
                                   ZsCJobDev *d_cjobs, uint32_t ncjobs, ZsChunkDev *d_units, uint32_t nunit_slots,
@@ -1447,11 +1447,17 @@ int dz_grow(T **p, size_t *cap, size_t need) {
 // out their position arrays, bitmaps, work items and block slots, then run
 // deflate_zlib.hip after the fast pipeline (whose check kernel computed their
 // CRC-32 / Adler-32 pieces).
+struct ZdHist {  // a deflate_fast job's insertion bits for its history [0, pstart)
+  uint64_t word0;  // first word of the job's I bitmap
+  const uint32_t *bits;
+  size_t nwords;
+};
 struct ZdPlan {
   std::vector<ZsZWorkDev> w1, w2;
   std::vector<uint32_t> slot_job;
+  std::vector<ZdHist> hist;
   size_t pos = 0, bmw = 0;
-  uint32_t nex = 0;
+  uint32_t nex = 0, nslow = 0, nfast = 0;
 } g_zdp;
 
 // before the jobs are uploaded: position arrays, bitmaps, block slots of the
@@ -1467,9 +1473,14 @@ void zd_plan(uint32_t nv) {
     jd.pos0 = P.pos;
     P.pos += (L + 64) & ~uint64_t(63);
     jd.bm0 = P.bmw;
-    P.bmw += 3 * zd_bm_words(L) + 4;
-    for (uint64_t a = 0; a < L; a += ZD_S1_HOST) P.w1.push_back({k, (uint32_t)std::min<uint64_t>(ZD_S1_HOST, L - a), a});
-    for (uint64_t a = 0; a < L; a += ZD_S2_HOST) P.w2.push_back({k, (uint32_t)std::min<uint64_t>(ZD_S2_HOST, L - a), a});
+    P.bmw += 4 * zd_bm_words(L) + 4;  // S, V, M, I
+    if (jd.exact == ZD_FAST) {  // deflate_fast searches inside its own kernel
+      P.nfast++;
+    } else {
+      P.nslow++;
+      for (uint64_t a = 0; a < L; a += ZD_S1_HOST) P.w1.push_back({k, (uint32_t)std::min<uint64_t>(ZD_S1_HOST, L - a), a});
+      for (uint64_t a = 0; a < L; a += ZD_S2_HOST) P.w2.push_back({k, (uint32_t)std::min<uint64_t>(ZD_S2_HOST, L - a), a});
+    }
     jd.zblk0 = (uint32_t)P.slot_job.size();
     jd.zblk_cap = (uint32_t)((L + ZD_BLOCK_HOST - 1) / ZD_BLOCK_HOST + 1);
     for (uint32_t b = 0; b < jd.zblk_cap; b++) P.slot_job.push_back(k);
@@ -1516,6 +1527,9 @@ int zd_run(uint32_t nv, size_t nseg, hipStream_t st) {
   // bitmaps start zeroed (the parse writes whole region words; a region's
   // tail word and the words past the input stay 0)
   HIP_OK(hipMemsetAsync(g_zd.d_bm, 0, (bmw + 16) * sizeof(uint32_t), st));
+  for (const ZdHist &h : P.hist)
+    if (h.nwords)
+      HIP_OK(hipMemcpyAsync(g_zd.d_bm + h.word0, h.bits, h.nwords * sizeof(uint32_t), hipMemcpyHostToDevice, st));
   if (!w1.empty()) HIP_OK(hipMemcpyAsync(g_zd.d_w1, w1.data(), w1.size() * sizeof(ZsZWorkDev), hipMemcpyHostToDevice, st));
   if (!w2.empty()) HIP_OK(hipMemcpyAsync(g_zd.d_w2, w2.data(), w2.size() * sizeof(ZsZWorkDev), hipMemcpyHostToDevice, st));
   HIP_OK(hipMemcpyAsync(g_zd.d_slot_job, slot_job.data(), slot_job.size() * sizeof(uint32_t), hipMemcpyHostToDevice, st));
@@ -1527,7 +1541,8 @@ int zd_run(uint32_t nv, size_t nseg, hipStream_t st) {
   }
   if (zs_launch_zdeflate(g_dz.d_jobs, nv, g_dz.d_segs, (uint32_t)nseg, g_zd.d_w1, (uint32_t)w1.size(), g_zd.d_w2,
                          (uint32_t)w2.size(), g_zd.d_prevd, g_zd.d_ma, g_zd.d_mb, g_zd.d_bm, g_zd.d_blks,
-                         (uint32_t)slot_job.size(), g_zd.d_slot_job, g_zd.d_aux, g_dz.d_stage, g_zd.d_flag, st, ev)) {
+                         (uint32_t)slot_job.size(), g_zd.d_slot_job, g_zd.d_aux, g_dz.d_stage, g_zd.d_flag, P.nslow != 0,
+                         P.nfast != 0, st, ev)) {
     set_err("zlib-identical deflate: fix-up round failed");
     return ZS_ENODEV;
   }
@@ -1558,6 +1573,14 @@ struct DzSpec {
   bool fast = false;       // ZS_F_DEFLATE_FAST
   uint32_t term = ZS_DT_FINAL, hdr = 1, trl = 1, bit0 = 0, pstate = ZD_STATE_A_HOST;
   uint64_t pstart = 0, skip = 0, abs0 = 0, ck0 = 0;
+  // levels 1..3 (deflate_fast): which history positions [0, pstart) zlib had
+  // inserted into its hash chains (bit q of word q / 32), and whether to
+  // return the bits of the window before the next segment's entry
+  const uint32_t *ins = nullptr;
+  size_t ins_words = 0;
+  bool want_ins = false;
+  std::vector<uint32_t> ins_out;  // words [ins_w0, ...) of the job's insertion bits
+  uint64_t ins_w0 = 0;
   // results
   int ret = Z_STREAM_ERROR;
   uint64_t total_out = 0, endbit = 0, stage = 0;
@@ -1587,7 +1610,9 @@ int dz_run(DzSpec *sp, uint32_t n, bool dev) {
     // the reference has no deflate64 compressor)
     const bool d64 = s.window_bits == -16;
     if (d64) w = 16;
-    const bool exact = !d64 && level >= 4 && !s.fast;
+    // zlib's bytes: deflate_slow (levels 4..9) or deflate_fast (1..3); level 0
+    // is deflate_stored's block grid on the throughput path
+    const uint32_t exact = d64 || s.fast || level == 0 ? 0u : (level >= 4 ? ZD_SLOW : ZD_FAST);
     bool ok = (d64 || parse_dz_wbits(s.window_bits, &wrap, &w)) && level >= 0 && level <= 9 &&
               s.in_len < (1ull << 32) && (s.in || s.in_len == 0) && s.term <= ZS_DT_CUT && s.bit0 < 8 &&
               s.pstart <= s.in_len && s.ck0 <= s.in_len && (s.out || s.out_cap == 0);
@@ -1602,7 +1627,7 @@ int dz_run(DzSpec *sp, uint32_t n, bool dev) {
     jd.wrap = wrap;
     jd.level = level;
     jd.wbits = w;
-    jd.exact = exact ? 1u : 0u;
+    jd.exact = exact;
     jd.term = s.term;
     jd.hdr = s.hdr;
     jd.trl = s.trl;
@@ -1668,6 +1693,13 @@ int dz_run(DzSpec *sp, uint32_t n, bool dev) {
   }
   HIP_OK(hipMemsetAsync(g_dz.d_stage, 0, stage_total, st));
   zd_plan(nv);
+  for (uint32_t i = 0; i < n; i++) {
+    if (slot[i] == UINT32_MAX) continue;
+    const ZsDJobDev &jd = g_dz.h_jobs[slot[i]];
+    if (jd.exact == ZD_FAST && jd.pstart && sp[i].ins)
+      g_zdp.hist.push_back({jd.bm0 + 3 * zd_bm_words(jd.in_len), sp[i].ins,
+                            std::min<size_t>(sp[i].ins_words, (size_t)((jd.pstart + 31) / 32))});
+  }
   HIP_OK(hipMemcpyAsync(g_dz.d_jobs, g_dz.h_jobs, nv * sizeof(ZsDJobDev), hipMemcpyHostToDevice, st));
   HIP_OK(hipMemcpyAsync(g_dz.d_segs, g_dz.h_segs, nseg * sizeof(ZsDSegDev), hipMemcpyHostToDevice, st));
   hipEvent_t *ev = nullptr;
@@ -1715,6 +1747,15 @@ int dz_run(DzSpec *sp, uint32_t n, bool dev) {
       HIP_OK(hipMemcpyAsync(s.out, g_dz.d_stage + jd.stage, give, dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, st));
     s.ret = give == jd.total_out ? Z_STREAM_END : Z_OK;  // Z_OK: output space ran out (deflate(Z_FINISH) semantics)
     s.total_out = give;
+    if (s.want_ins && jd.exact == ZD_FAST) {  // the insertion bits of the window before the next entry
+      const uint64_t T = jd.term == ZS_DT_CUT ? jd.cut_pos : jd.in_len;
+      const uint64_t a = T - std::min<uint64_t>(T, (uint64_t)1 << jd.wbits), w0 = a / 32, w1 = (T + 31) / 32;
+      s.ins_w0 = w0;
+      s.ins_out.assign((size_t)(w1 - w0), 0u);
+      if (w1 > w0)
+        HIP_OK(hipMemcpyAsync(s.ins_out.data(), g_zd.d_bm + jd.bm0 + 3 * zd_bm_words(jd.in_len) + w0,
+                              (size_t)(w1 - w0) * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    }
   }
   HIP_OK(hipStreamSynchronize(st));
   return 0;
@@ -1786,7 +1827,8 @@ struct DStreamState {
   int inited = 0;
   int wbits = 15, level = 6, wrap = 0;
   uint32_t w = 15;             // window bits (zlib's wsize = 1 << w)
-  bool exact = true;           // levels 4..9: zlib's bytes
+  bool exact = true;           // levels 1..9: zlib's bytes (deflate_fast 1..3, deflate_slow 4..9)
+  std::vector<uint32_t> ins;   // levels 1..3: insertion bits of buf[0, hist) (zlib's hash chains)
   int status = 0;              // 0 no call yet, 1 busy, 2 finished (deflate.c INIT/BUSY/FINISH_STATE)
   int last_flush = -2;         // deflate.c s->last_flush (deflateResetKeep: -2)
   std::vector<uint8_t> buf;    // [history | unparsed input]
@@ -1874,6 +1916,11 @@ DzSpec ds_spec(const DStreamState *s, uint32_t term) {
   j.skip = s->skip;
   j.abs0 = s->abs;
   j.ck0 = s->ck_from;
+  if (s->exact && s->level <= 3) {
+    j.ins = s->ins.data();
+    j.ins_words = s->ins.size();
+    j.want_ins = true;
+  }
   return j;
 }
 
@@ -1935,12 +1982,24 @@ void ds_after(DStreamState *s, const DzSpec &j, const uint8_t *bytes, bool full)
     s->need = ZD_BLOCK_SYMS + ZD_LOOK_HOST;
   }
   s->fresh = 0;
-  if (full || !s->exact) {  // the window restarts (Z_FULL_FLUSH; levels 0..3 always)
+  s->ins.clear();
+  if (full || !s->exact) {  // the window restarts (Z_FULL_FLUSH; level 0 always)
     s->buf.erase(s->buf.begin(), s->buf.begin() + (ptrdiff_t)T);
     s->hist = 0;
     s->abs = full ? 0 : s->abs + T;
   } else {
     const size_t h = std::min(T, wsize);
+    if (s->level <= 3) {  // deflate_fast: which window positions are in the hash chains
+      s->ins.assign((h + 31) / 32, 0u);
+      for (size_t i = 0; i < h; i++) {
+        const uint64_t q = T - h + i, wi = q / 32 - j.ins_w0;
+        if (wi < j.ins_out.size() && ((j.ins_out[(size_t)wi] >> (q & 31u)) & 1u)) s->ins[i / 32] |= 1u << (i & 31u);
+      }
+      // a flush leaves the last MIN_MATCH - 1 positions to the next fill_window
+      // (deflate.c s->insert), which inserts them before any later search
+      if (term != ZS_DT_CUT)
+        for (size_t i = h - std::min<size_t>(h, 2); i < h; i++) s->ins[i / 32] |= 1u << (i & 31u);
+    }
     s->buf.erase(s->buf.begin(), s->buf.begin() + (ptrdiff_t)(T - h));
     s->hist = h;
     s->abs += T - h;
@@ -2130,7 +2189,7 @@ int dstream_init(DStreamState *s, int level, int wbits) {
   s->wbits = wbits;
   s->wrap = wrap;
   s->w = w;
-  s->exact = level >= 4;
+  s->exact = level >= 1;
   s->adler = wrap == 2 ? 0u : 1u;
   return Z_OK;
 }

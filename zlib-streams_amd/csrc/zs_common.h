@@ -206,7 +206,8 @@ struct ZsDJobDev {
   uint32_t wbits;      // window bits 9..15 (match distances <= 2^wbits; zlib CINFO = wbits - 8)
   uint64_t ck_a;       // check accumulators (zs_check.h): CRC XOR / Adler sum A (zeroed by the host)
   uint64_t ck_b;       // Adler weighted sum B
-  // zlib-identical mode (exact = 1; deflate_zlib.hip)
+  // zlib-identical mode (deflate_zlib.hip): exact = ZD_SLOW (levels 4..9,
+  // deflate_slow) or ZD_FAST (levels 1..3, deflate_fast); 0: the throughput path
   uint32_t exact;
   uint32_t nzblk;      // blocks (zs_zd_blocks_kernel)
   uint64_t pos0;       // first entry of the job's position arrays
@@ -234,6 +235,8 @@ struct ZsDJobDev {
   uint64_t cut_skip;   // ZS_DT_CUT (out): ... and the symbols from there already emitted
   uint64_t cut_open;   // ZS_DT_CUT (out): symbols of the unsent block zlib has already tallied
 };
+#define ZD_SLOW 1u
+#define ZD_FAST 2u
 // ZsDJobDev::term -- the end of a job's bits, as zlib's deflate() ends a call:
 #define ZS_DT_FINAL 0u    // Z_FINISH: last block BFINAL = 1 (an empty one if needed), trailer
 #define ZS_DT_SYNC 1u     // Z_SYNC_FLUSH / Z_FULL_FLUSH: blocks not final, empty stored block 00 00 FF FF

@@ -31,7 +31,7 @@ Z_STREAM_ERROR, Z_DATA_ERROR, Z_MEM_ERROR, Z_BUF_ERROR = -2, -3, -4, -5
 Z_NO_FLUSH, Z_FINISH = 0, 4
 ZS_F_DEVICE = 1
 ZS_F_CRC32 = 2  # raw / copy jobs: CRC-32 of the output in "adler" (ZIP entries)
-ZS_F_DEFLATE_FAST = 4  # deflate levels 4..9: the throughput path instead of zlib's bytes
+ZS_F_DEFLATE_FAST = 4  # deflate levels 1..9: the throughput path instead of zlib's bytes
 ZS_JOB_INFLATE, ZS_JOB_COPY = 0, 1
 
 # windowBits per format, as the reference's init functions choose them
@@ -273,7 +273,7 @@ def deflate_batch(streams, window_bits=-15, level=-1, out_caps=None, fast=False)
     """Deflate many whole buffers on the GPU (host buffers).
 
     Each job behaves like deflateInit2(level, Z_DEFLATED, window_bits, 8,
-    Z_DEFAULT_STRATEGY) + one deflate(Z_FINISH).  Levels 0 and 4..9 write zlib's bytes
+    Z_DEFAULT_STRATEGY) + one deflate(Z_FINISH).  Every level writes zlib's bytes
     (unless fast=True: ZS_F_DEFLATE_FAST, the throughput path with its own block
     structure).  Returns [(bytes, result_dict)].
     """
