@@ -468,7 +468,8 @@ def test_deflate_stream_calls_are_zlibs(zs, level):
     host zlib's, for raw, zlib and gzip streams."""
     rng = random.Random(100 + level)
     for wb in (-15, 15, 31):
-        data = _stream_data(rng, 1_500_000)
+        # deflate_fast (1..3) is serial per stream on the GPU: a smaller stream
+        data = _stream_data(rng, 1_500_000 if level >= 4 else 400_000)
         calls, off = [], 0
         while off < len(data):
             n = rng.choice([1, 700, 5000, 33000, 70000, 250000])
