@@ -193,6 +193,38 @@ __global__ void __launch_bounds__(ZD_MT) zs_zd_match_kernel(const ZsDJobDev *__r
   uint64_t p = q_beg + lane;
   bool active = p < q_end, fin = false;
   uint32_t c = 0, k = 0, best = 0, bdist = 0, bl = 0, bd = 0, cap = 0, nicep = 0, ow = 0, pi = 0;
+  // the common prefix of the strings at LDS bytes a and pi, capped at cap:
+  // 16 bytes of both per iteration (10 independent LDS dword reads, one round
+  // trip; a 4-byte step paid one per 4 bytes)
+  auto cmp_len = [&](uint32_t a0) -> uint32_t {
+    uint32_t n = 0;
+    for (;;) {
+      const uint32_t a = a0 + n, b = pi + n;
+      const uint32_t wa = a >> 2, wb = b >> 2, sa = a & 3u, sb = b & 3u;
+      uint32_t ua[5], ub[5];
+#pragma unroll
+      for (int q = 0; q < 5; q++) {
+        ua[q] = s_w[wa + q];
+        ub[q] = s_w[wb + q];
+      }
+      uint32_t x = 0, g = 0;
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const uint32_t d = __builtin_amdgcn_alignbyte(ua[q + 1], ua[q], sa) ^ __builtin_amdgcn_alignbyte(ub[q + 1], ub[q], sb);
+        if (x == 0) {
+          x = d;
+          g = (uint32_t)q;
+        }
+      }
+      if (x) {
+        n += 4 * g + ((uint32_t)__builtin_ctz(x) >> 3);
+        break;
+      }
+      n += 16;
+      if (n >= cap) break;
+    }
+    return min(n, cap);
+  };
   // a walk starts at position p: its first candidate, or done at once
   auto start = [&]() {
     best = bdist = bl = bd = 0;
@@ -219,35 +251,7 @@ __global__ void __launch_bounds__(ZD_MT) zs_zd_match_kernel(const ZsDJobDev *__r
     const uint32_t nd = s_pd[cc];  // next link, in flight during the compare
     const uint32_t se = zd_lw(s_w, cc + (best >= 3 ? best - 3 : 0u));
     if (walking && (best < 3 || se == ow)) {
-      // 16 bytes of both strings per iteration: 10 independent LDS dword
-      // reads, one round trip (a 4-byte step paid one per 4 bytes)
-      uint32_t n = 0;
-      for (;;) {
-        const uint32_t a = c + n, b = pi + n;
-        const uint32_t wa = a >> 2, wb = b >> 2, sa = a & 3u, sb = b & 3u;
-        uint32_t ua[5], ub[5];
-#pragma unroll
-        for (int q = 0; q < 5; q++) {
-          ua[q] = s_w[wa + q];
-          ub[q] = s_w[wb + q];
-        }
-        uint32_t x = 0, g = 0;
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-          const uint32_t d = __builtin_amdgcn_alignbyte(ua[q + 1], ua[q], sa) ^ __builtin_amdgcn_alignbyte(ub[q + 1], ub[q], sb);
-          if (x == 0) {
-            x = d;
-            g = (uint32_t)q;
-          }
-        }
-        if (x) {
-          n += 4 * g + ((uint32_t)__builtin_ctz(x) >> 3);
-          break;
-        }
-        n += 16;
-        if (n >= cap) break;
-      }
-      n = min(n, cap);
+      const uint32_t n = cmp_len(c);
       if (n > best) {
         best = n;
         bdist = pi - c;
