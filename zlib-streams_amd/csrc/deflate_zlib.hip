@@ -625,6 +625,9 @@ __global__ void zs_zd_fix_seq_kernel(const ZsDJobDev *__restrict__ jobs, uint32_
 // zlib deflate.c configuration_table rows 1..3: good, lazy (max_insert_length), nice, chain
 __constant__ uint16_t zd_cfgf[4][4] = {{0, 0, 0, 0}, {4, 4, 8, 4}, {4, 5, 16, 8}, {4, 6, 32, 32}};
 #define ZF_SWEEP 16384u
+#ifndef ZF_PROF
+#define ZF_PROF 0  // per-step phase clocks, printed per job (tools/build_variant.sh ... -DZF_PROF=1)
+#endif
 
 // the job's input read as aligned words (unaligned caller buffers; word
 // indices clamped to the buffer's own words)
@@ -791,15 +794,29 @@ __global__ void __launch_bounds__(WAVE) zs_zd_fast_kernel(ZsDJobDev *__restrict_
   }
   uint64_t p = jb.pstart;
   bool stop = false;
+#if ZF_PROF
+  uint64_t zt[6] = {0, 0, 0, 0, 0, 0}, zsteps = 0, zt0 = __builtin_amdgcn_s_memtime();
+#define ZF_T(i)                                         \
+  do {                                                  \
+    const uint64_t n_ = __builtin_amdgcn_s_memtime();   \
+    zt[i] += n_ - zt0;                                  \
+    zt0 = n_;                                           \
+  } while (0)
+#else
+#define ZF_T(i) ((void)0)
+#endif
   while (p < L && !stop) {
     sweep_to(p);
+    ZF_T(0);
     const uint64_t q = p + lane;
     const bool insq = q + ZD_MINM <= L;  // zlib inserts and searches only with lookahead >= MIN_MATCH
     const uint32_t h = insq ? zf_hash(X, q) : 0u;
     const uint64_t same = zf_same(h, insq);
     const uint64_t below = same & ((1ull << lane) - 1ull);
     uint32_t mlen = 0, mdist = 0;
+    ZF_T(1);
     if (insq) zf_search(X, s_prev, q, L, s_head[h], max_dist, nice, chain, mlen, mdist);
+    ZF_T(2);
     // commit loop tops in order (wave-uniform): stop at the end, at a cut
     // job's first short lookahead, or at the first search an earlier inserted
     // position of this step invalidates
@@ -830,6 +847,7 @@ __global__ void __launch_bounds__(WAVE) zs_zd_fast_kernel(ZsDJobDev *__restrict_
         t += 1;
       }
     }
+    ZF_T(3);
     const bool tok = (tokm >> lane) & 1ull, ins = (insm >> lane) & 1ull;
     if (tok && mlen >= ZD_MINM) om[q] = mlen | (mdist << 9);
     if (lane < 3) {  // token starts and insertion bits of [p, p + 64): three words
@@ -851,8 +869,20 @@ __global__ void __launch_bounds__(WAVE) zs_zd_fast_kernel(ZsDJobDev *__restrict_
       if (vi) atomicOr(&B.I[w0 + k], vi);
     }
     zf_insert(s_head, s_prev, q, h, ins, same, lane);
+    ZF_T(4);
+#if ZF_PROF
+    zsteps++;
+#endif
     p += t;
   }
+#if ZF_PROF
+  if (lane == 0)
+    printf("zf job %u L=%lu steps %lu pos/step %.1f clk/step: sweep %lu hash+same %lu search %lu commit %lu out+ins %lu\n",
+           blockIdx.x, (unsigned long)L, (unsigned long)zsteps, (double)(p - jb.pstart) / (double)(zsteps ? zsteps : 1),
+           (unsigned long)(zt[0] / (zsteps ? zsteps : 1)), (unsigned long)(zt[1] / (zsteps ? zsteps : 1)),
+           (unsigned long)(zt[2] / (zsteps ? zsteps : 1)), (unsigned long)(zt[3] / (zsteps ? zsteps : 1)),
+           (unsigned long)(zt[4] / (zsteps ? zsteps : 1)));
+#endif
   if (lane == 0) jobs[blockIdx.x].cut_pos = p;  // where the parse stopped (zs_zd_cut_kernel)
 }
 
