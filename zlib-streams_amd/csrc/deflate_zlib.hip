@@ -649,9 +649,52 @@ struct ZfIn {
   }
 };
 
-__device__ __forceinline__ uint32_t zf_hash(const ZfIn &X, uint64_t q) {
-  const uint32_t v = X.ld4(q);
+__device__ __forceinline__ uint32_t zf_hash3(uint32_t v) {
   return (((v & 0xffu) << 10) ^ (((v >> 8) & 0xffu) << 5) ^ ((v >> 16) & 0xffu)) & 0x7fffu;
+}
+__device__ __forceinline__ uint32_t zf_hash(const ZfIn &X, uint64_t q) { return zf_hash3(X.ld4(q)); }
+
+// The window in LDS: a 32 KiB ring of input words (slot = position mod
+// 32768) holding [fend - 32768, fend).  A step at p reads positions < p + 340
+// and advances <= 321, so the ring is refilled ZF_FILL bytes at a time (loads
+// issued before the step's searches, stored after them) while fend - p <
+// 661 + ZF_FILL; a candidate older than the ring's start (the oldest ~2 K
+// positions of the window) is compared from global memory instead.
+#define ZF_RING_WORDS 8192u
+#define ZF_FILL 1024u
+struct ZfWin {
+  const uint32_t *r;
+  uint64_t lo;  // first position held
+  __device__ __forceinline__ uint32_t rd4(uint64_t pos) const {
+    const uint32_t a = (uint32_t)pos, w = (a >> 2) & (ZF_RING_WORDS - 1u);
+    return __builtin_amdgcn_alignbyte(r[(w + 1u) & (ZF_RING_WORDS - 1u)], r[w], a & 3u);
+  }
+};
+
+// common prefix of the strings at c and q, capped (16 bytes of both per step);
+// RING: the candidate's bytes from the LDS ring, else from global memory
+template <bool RING>
+__device__ __forceinline__ uint32_t zf_cmp(const ZfWin &Wn, const ZfIn &X, uint64_t c, uint64_t q, uint32_t cap) {
+  uint32_t n = 0;
+  for (;;) {
+    uint32_t x = 0, g = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const uint64_t cp = c + n + 4 * i;
+      const uint32_t d = (RING ? Wn.rd4(cp) : X.ld4(cp)) ^ Wn.rd4(q + n + 4 * i);
+      if (x == 0) {
+        x = d;
+        g = (uint32_t)i;
+      }
+    }
+    if (x) {
+      n += 4 * g + ((uint32_t)__builtin_ctz(x) >> 3);
+      break;
+    }
+    n += 16;
+    if (n >= cap) break;
+  }
+  return min(n, cap);
 }
 
 // age out entries more than a window old (see zs_zd_prev_kernel's sweep)
@@ -703,7 +746,8 @@ __device__ __forceinline__ void zf_insert(uint16_t *head, uint16_t *prev, uint64
 // longest_match at q (prev_length = MIN_MATCH - 1, the full chain budget):
 // candidates from head entry e0, best length and the distance of the first
 // candidate reaching it
-__device__ __forceinline__ void zf_search(const ZfIn &X, const uint16_t *prev, uint64_t q, uint64_t L, uint32_t e0,
+__device__ __forceinline__ void zf_search(const ZfWin &Wn, const ZfIn &X, const uint16_t *prev, uint64_t q, uint64_t L,
+                                          uint32_t e0,
                                           uint32_t max_dist, uint32_t nice, uint32_t chain, uint32_t &olen,
                                           uint32_t &odist) {
   olen = 0;
@@ -716,25 +760,7 @@ __device__ __forceinline__ void zf_search(const ZfIn &X, const uint16_t *prev, u
   uint32_t best = ZD_MINM - 1, bdist = 0;
   for (uint32_t k = 0;;) {
     const uint64_t c = q - age;
-    uint32_t n = 0;
-    for (;;) {  // 16 bytes of both strings per step
-      uint32_t x = 0, g = 0;
-#pragma unroll
-      for (int i = 0; i < 4; i++) {
-        const uint32_t d = X.ld4(c + n + 4 * i) ^ X.ld4(q + n + 4 * i);
-        if (x == 0) {
-          x = d;
-          g = (uint32_t)i;
-        }
-      }
-      if (x) {
-        n += 4 * g + ((uint32_t)__builtin_ctz(x) >> 3);
-        break;
-      }
-      n += 16;
-      if (n >= cap) break;
-    }
-    n = min(n, cap);
+    const uint32_t n = c >= Wn.lo ? zf_cmp<true>(Wn, X, c, q, cap) : zf_cmp<false>(Wn, X, c, q, cap);
     if (n > best) {
       best = n;
       bdist = age;
@@ -754,6 +780,7 @@ __device__ __forceinline__ void zf_search(const ZfIn &X, const uint16_t *prev, u
 __global__ void __launch_bounds__(WAVE) zs_zd_fast_kernel(ZsDJobDev *__restrict__ jobs, uint32_t *__restrict__ bm,
                                                            uint32_t *__restrict__ ma) {
   __shared__ __attribute__((aligned(16))) uint16_t s_tab[65536];  // head[32768] | prev[32768]
+  __shared__ __attribute__((aligned(16))) uint32_t s_ring[ZF_RING_WORDS];
   uint16_t *s_head = s_tab, *s_prev = s_tab + 32768;
   const uint32_t lane = threadIdx.x;
   const ZsDJobDev jb = jobs[blockIdx.x];
@@ -805,47 +832,82 @@ __global__ void __launch_bounds__(WAVE) zs_zd_fast_kernel(ZsDJobDev *__restrict_
 #else
 #define ZF_T(i) ((void)0)
 #endif
+  ZfWin Wn;
+  Wn.r = s_ring;
+  uint64_t fend = (p + 661u + ZF_FILL + 3u) & ~3ull;
+  for (uint32_t i = lane; i < ZF_RING_WORDS; i += WAVE) {
+    const bool neg = fend < 32768u && 4ull * i < 32768u - fend;  // before the input: never read
+    const uint64_t pos = fend + 4ull * i - 32768u;
+    s_ring[(uint32_t)(pos >> 2) & (ZF_RING_WORDS - 1u)] = neg ? 0u : X.ld4(pos);
+  }
+  __builtin_amdgcn_wave_barrier();
   while (p < L && !stop) {
     sweep_to(p);
     ZF_T(0);
+    Wn.lo = fend < 32768u ? 0u : fend - 32768u;
+    const bool refill = fend - p < 661u + ZF_FILL;
+    uint32_t fw[ZF_FILL / 4 / WAVE];
+    if (refill) {
+#pragma unroll
+      for (uint32_t i = 0; i < ZF_FILL / 4 / WAVE; i++) fw[i] = X.ld4(fend + 4ull * (lane + WAVE * i));
+    }
     const uint64_t q = p + lane;
     const bool insq = q + ZD_MINM <= L;  // zlib inserts and searches only with lookahead >= MIN_MATCH
-    const uint32_t h = insq ? zf_hash(X, q) : 0u;
+    const uint32_t h = insq ? zf_hash3(Wn.rd4(q)) : 0u;
     const uint64_t same = zf_same(h, insq);
     const uint64_t below = same & ((1ull << lane) - 1ull);
     uint32_t mlen = 0, mdist = 0;
     ZF_T(1);
-    if (insq) zf_search(X, s_prev, q, L, s_head[h], max_dist, nice, chain, mlen, mdist);
+    if (insq) zf_search(Wn, X, s_prev, q, L, s_head[h], max_dist, nice, chain, mlen, mdist);
     ZF_T(2);
     // commit loop tops in order (wave-uniform): stop at the end, at a cut
     // job's first short lookahead, or at the first search an earlier inserted
-    // position of this step invalidates
+    // position of this step invalidates.  The walk goes match to match: the
+    // literal run before the next match start is committed at once (every
+    // position of it is a loop top), its stops found by one ballot.
+    const bool valid = q < L, cutq = cut && valid && L - q < ZD_LOOK;
+    const bool ism = valid && mlen >= ZD_MINM;
+    const bool shrtq = ism && mlen <= max_ins && L - (q + mlen) >= ZD_MINM;
+    const uint64_t Mm = __ballot(ism), Im = __ballot(insq), Sm = __ballot(shrtq);
+    const uint64_t lt_me = (1ull << lane) - 1ull;
+    auto below_from = [](uint32_t a) -> uint64_t { return a >= 64u ? ~0ull : ((1ull << a) - 1ull); };
     uint32_t t = 0;
     uint64_t insm = 0, tokm = 0;
     while (t < WAVE) {
-      const uint64_t qt = p + t;
-      if (qt >= L) break;
-      if (cut && L - qt < ZD_LOOK) {
-        stop = true;
+      const uint64_t from_t = ~below_from(t);
+      const uint64_t mt = Mm & from_t;
+      const uint32_t m = mt ? (uint32_t)__builtin_ctzll(mt) : WAVE;  // next match start (WAVE: none)
+      // loop tops t .. m (m included when < WAVE): any stop among them?
+      const uint64_t run = from_t & below_from(m + 1u);
+      const bool inrun = (run >> lane) & 1ull;
+      const bool conf = (below & (insm | (Im & run & lt_me))) != 0ull;
+      const uint64_t stops = __ballot(inrun && (!valid || cutq || conf));
+      const uint64_t lits = from_t & below_from(m);  // the literal loop tops t .. m - 1
+      if (stops) {
+        const uint32_t x = (uint32_t)__builtin_ctzll(stops);
+        const uint64_t done = lits & below_from(x);
+        tokm |= done;
+        insm |= Im & done;
+        stop = stop || (((__ballot(cutq) >> x) & 1ull) && p + x < L);
+        t = x;
         break;
       }
-      const uint64_t bt = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(below >> 32), t) << 32) |
-                          (uint32_t)__builtin_amdgcn_readlane((uint32_t)below, t);
-      if (bt & insm) break;
-      const uint32_t lt = __builtin_amdgcn_readlane(mlen, t);
-      const bool it = qt + ZD_MINM <= L;
-      if (lt >= ZD_MINM) {
-        const bool shrt = lt <= max_ins && L - (qt + lt) >= ZD_MINM;
-        if (shrt && t + lt > WAVE) break;  // its inner inserts would pass this step
-        tokm |= 1ull << t;
-        if (shrt) insm |= (lt == 64 ? ~0ull : ((1ull << lt) - 1ull)) << t;
-        else if (it) insm |= 1ull << t;
-        t += lt;
-      } else {
-        tokm |= 1ull << t;
-        if (it) insm |= 1ull << t;
-        t += 1;
+      tokm |= lits;
+      insm |= Im & lits;
+      if (m >= WAVE) {
+        t = WAVE;
+        break;
       }
+      const uint32_t lm = __builtin_amdgcn_readlane(mlen, m);
+      const bool shrt = (Sm >> m) & 1ull;
+      if (shrt && m + lm > WAVE) {  // its inner inserts would pass this step
+        t = m;
+        break;
+      }
+      tokm |= 1ull << m;
+      if (shrt) insm |= below_from(lm) << m;
+      else insm |= Im & (1ull << m);
+      t = m + lm;
     }
     ZF_T(3);
     const bool tok = (tokm >> lane) & 1ull, ins = (insm >> lane) & 1ull;
@@ -869,6 +931,13 @@ __global__ void __launch_bounds__(WAVE) zs_zd_fast_kernel(ZsDJobDev *__restrict_
       if (vi) atomicOr(&B.I[w0 + k], vi);
     }
     zf_insert(s_head, s_prev, q, h, ins, same, lane);
+    if (refill) {
+#pragma unroll
+      for (uint32_t i = 0; i < ZF_FILL / 4 / WAVE; i++)
+        s_ring[(uint32_t)((fend >> 2) + lane + WAVE * i) & (ZF_RING_WORDS - 1u)] = fw[i];
+      fend += ZF_FILL;
+      __builtin_amdgcn_wave_barrier();
+    }
     ZF_T(4);
 #if ZF_PROF
     zsteps++;
