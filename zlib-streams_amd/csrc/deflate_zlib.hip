@@ -148,6 +148,65 @@ __global__ void __launch_bounds__(ZD_PT1) zs_zd_prev_kernel(const ZsDJobDev *__r
   }
 }
 
+// The same table for small jobs (a stream segment: a window of history and the
+// call's new input) in short work items: the window before an item enters the
+// head table in one parallel pass (the latest position of each hash by LDS
+// atomicMax, u32 entries relative to the window start), instead of the 32 Ki
+// ordered steps the long items spend on it, so an item costs its own length.
+// Work items of at most ZD_S1S positions (the relative positions stay below
+// 2^16 + 1 with no ageing).
+#define ZD_S1S 8192u
+__global__ void __launch_bounds__(ZD_PT1) zs_zd_prev_small_kernel(const ZsDJobDev *__restrict__ jobs,
+                                                                   const ZsZWorkDev *__restrict__ work,
+                                                                   uint16_t *__restrict__ prevd) {
+  __shared__ uint32_t head[32768];  // relative position + 1 of the latest occurrence (0: none)
+  const uint32_t t = threadIdx.x, lane = t & (WAVE - 1), wv = t / WAVE;
+  const ZsZWorkDev wk = work[blockIdx.x];
+  const ZsDJobDev jb = jobs[wk.job];
+  const uint8_t *in = jb.in;
+  const uint64_t L = jb.in_len;
+  const uint64_t start = wk.start, to = wk.start + wk.len;
+  const uint64_t from = start >= 32768u ? start - 32768u : 0u;
+  for (uint32_t i = t; i < 32768u; i += ZD_PT1) head[i] = 0;
+  __syncthreads();
+  for (uint64_t r = from + t; r < start; r += ZD_PT1) {
+    if (r + 2 < L) {
+      const uint32_t h = (((uint32_t)in[r] << 10) ^ ((uint32_t)in[r + 1] << 5) ^ in[r + 2]) & 0x7fffu;
+      atomicMax(&head[h], (uint32_t)(r - from + 1u));
+    }
+  }
+  __syncthreads();
+  uint16_t *po = prevd + jb.pos0;
+  for (uint64_t base = start; base < to; base += ZD_PT1) {
+    const uint64_t p = base + (uint64_t)wv * WAVE + lane;
+    const bool valid = p + 2 < L && p < to;
+    uint32_t h = 0;
+    if (valid) h = (((uint32_t)in[p] << 10) ^ ((uint32_t)in[p + 1] << 5) ^ in[p + 2]) & 0x7fffu;
+    uint64_t m = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 15; b++) {
+      const uint64_t B = __ballot(valid && ((h >> b) & 1u));
+      m &= ((h >> b) & 1u) ? B : ~B;
+    }
+    const uint64_t below = m & ((1ull << lane) - 1ull);
+    const uint64_t above = lane == 63 ? 0ull : (m & ~((2ull << lane) - 1ull));
+    uint32_t d = below ? lane - (63u - (uint32_t)__builtin_clzll(below)) : 0u;
+#pragma unroll
+    for (uint32_t ph = 0; ph < ZD_PT1 / WAVE; ph++) {
+      if (wv == ph) {
+        if (!below) {
+          const uint32_t e = head[h];
+          d = e ? (uint32_t)(p - from - (e - 1u)) : 0xffffffffu;
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (valid && !above) head[h] = (uint32_t)(p - from + 1u);
+      }
+      __syncthreads();
+    }
+    if (p < to) po[p] = (valid && d < 32768u && p != d) ? (uint16_t)d : (uint16_t)0;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // K2: longest match per position, two chain budgets
 // ---------------------------------------------------------------------------
@@ -1005,6 +1064,23 @@ __device__ uint64_t zd_sym_pos(const ZsDSegDev *segs, const ZsDJobDev &jb, const
   const ZsDSegDev &sg = segs[jb.seg0 + lo];
   uint64_t rem = sym - sg.sym0;
   uint64_t w = sg.start / 32u;
+  // 64 words (2 K positions) per iteration while the symbol lies past them:
+  // 16 independent 16-byte loads in flight (a word at a time paid a memory
+  // round trip per 32 positions -- the latency of a stream segment's blocks);
+  // region words start 4-aligned and the bitmaps are padded past the input
+  for (;;) {
+    const uint4 *v = reinterpret_cast<const uint4 *>(S + w);
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      const uint4 x = v[i];
+      c += (uint32_t)(__builtin_popcount(x.x) + __builtin_popcount(x.y) + __builtin_popcount(x.z) +
+                      __builtin_popcount(x.w));
+    }
+    if (rem < c) break;
+    rem -= c;
+    w += 64;
+  }
   for (;; w++) {
     const uint32_t x = S[w];
     const uint32_t c = (uint32_t)__builtin_popcount(x);
@@ -1112,6 +1188,14 @@ __device__ uint64_t zd_syms_before(const ZsDSegDev *segs, const ZsDJobDev &jb, c
   const ZsDSegDev &sg = segs[jb.seg0 + (uint32_t)(y / ZD_REG)];
   uint64_t c = sg.sym0;
   uint64_t w = sg.start / 32u;
+  for (; (w + 64) * 32u <= y; w += 64) {  // 64 words per iteration (see zd_sym_pos)
+    const uint4 *v = reinterpret_cast<const uint4 *>(S + w);
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      const uint4 x = v[i];
+      c += (uint64_t)(__builtin_popcount(x.x) + __builtin_popcount(x.y) + __builtin_popcount(x.z) + __builtin_popcount(x.w));
+    }
+  }
   for (; (w + 1) * 32u <= y; w++) c += (uint64_t)__builtin_popcount(S[w]);
   if (y & 31u) c += (uint64_t)__builtin_popcount(S[w] & ((1u << (y & 31u)) - 1u));
   return c;
@@ -1741,21 +1825,26 @@ static int zd_fix_rounds() {
 }
 
 extern "C" int zs_launch_zdeflate(ZsDJobDev *d_jobs, uint32_t njobs, ZsDSegDev *d_segs, uint32_t nseg,
-                                  const ZsZWorkDev *d_w1, uint32_t n1, const ZsZWorkDev *d_w2, uint32_t n2,
+                                  const ZsZWorkDev *d_w1, uint32_t n1, const ZsZWorkDev *d_w1s, uint32_t n1s,
+                                  const ZsZWorkDev *d_w2, uint32_t n2,
                                   uint16_t *d_prevd, uint32_t *d_ma, uint32_t *d_mb, uint32_t *d_bm, ZsZBlkDev *d_blks,
                                   uint32_t nblk_slots, const uint32_t *d_slot_job, uint32_t *d_aux, uint8_t *d_stage,
-                                  uint32_t *d_flag, int has_slow, int has_fast, hipStream_t st, hipEvent_t *ev) {
+                                  uint32_t *d_flag, int has_slow, int has_fast, uint32_t max_regions, hipStream_t st,
+                                  hipEvent_t *ev) {
   if (ev) (void)hipEventRecord(ev[0], st);
   if (n1) hipLaunchKernelGGL(zs_zd_prev_kernel, dim3(n1), dim3(ZD_PT1), 0, st, d_jobs, d_w1, d_prevd);
+  if (n1s) hipLaunchKernelGGL(zs_zd_prev_small_kernel, dim3(n1s), dim3(ZD_PT1), 0, st, d_jobs, d_w1s, d_prevd);
   if (n2) hipLaunchKernelGGL(zs_zd_match_kernel, dim3(n2), dim3(ZD_MT), 0, st, d_jobs, d_w2, d_prevd, d_ma, d_mb);
   if (ev) (void)hipEventRecord(ev[1], st);
   if (has_fast) hipLaunchKernelGGL(zs_zd_fast_kernel, dim3(njobs), dim3(WAVE), 0, st, d_jobs, d_bm, d_ma);
   if (has_slow) hipLaunchKernelGGL(zs_zd_parse_kernel, dim3(nseg), dim3(ZD_PT), 0, st, d_jobs, d_segs, d_ma, d_mb, d_bm);
   // parallel fix-up rounds while exits change (nearly every input settles in
   // one or two), then, if a cascade is still moving, the in-order pass
-  const int max_rounds = has_slow ? zd_fix_rounds() : 0;
+  // (jobs of a few regions -- stream segments -- go straight to the in-order
+  // pass: no host round trip per round)
+  const int max_rounds = has_slow && max_regions > 4 ? zd_fix_rounds() : 0;
   uint32_t cur = 0;
-  bool settled = !has_slow;
+  bool settled = !has_slow;  // (max_rounds 0 with slow jobs: the in-order pass below)
   for (int round = 0; round < max_rounds; round++) {
     uint32_t changed = 0;
     if (hipMemsetAsync(d_flag, 0, sizeof(uint32_t), st) != hipSuccess) return -1;

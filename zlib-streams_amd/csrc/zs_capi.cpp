@@ -47,10 +47,12 @@ struct ZsZWorkDev {  // must match deflate_zlib.hip
   uint64_t start;
 };
 extern "C" int zs_launch_zdeflate(ZsDJobDev *d_jobs, uint32_t njobs, ZsDSegDev *d_segs, uint32_t nseg,
-                                  const ZsZWorkDev *d_w1, uint32_t n1, const ZsZWorkDev *d_w2, uint32_t n2,
+                                  const ZsZWorkDev *d_w1, uint32_t n1, const ZsZWorkDev *d_w1s, uint32_t n1s,
+                                  const ZsZWorkDev *d_w2, uint32_t n2,
                                   uint16_t *d_prevd, uint32_t *d_ma, uint32_t *d_mb, uint32_t *d_bm, ZsZBlkDev *d_blks,
                                   uint32_t nblk_slots, const uint32_t *d_slot_job, uint32_t *d_aux, uint8_t *d_stage,
-                                  uint32_t *d_flag, int has_slow, int has_fast, hipStream_t st, hipEvent_t *ev);
+                                  uint32_t *d_flag, int has_slow, int has_fast, uint32_t max_regions, hipStream_t st,
+                                  hipEvent_t *ev);
 extern "C" void zs_launch_dz_trailer(ZsDJobDev *d_jobs, uint32_t njobs, uint8_t *d_stage, hipStream_t st);
 extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, ZsSegDev *d_segs, uint32_t nseg,
                                   ZsCJobDev *d_cjobs, uint32_t ncjobs, ZsChunkDev *d_units, uint32_t nunit_slots,
@@ -1398,12 +1400,14 @@ DzWorkspace g_dz;
 // zlib-identical deflate (deflate_zlib.hip): per position, per bitmap word,
 // per work item, per block
 constexpr uint64_t ZD_S1_HOST = 131072, ZD_S2_HOST = 8192, ZD_BLOCK_HOST = 16383, ZD_AUX_HOST = 352;
+// jobs up to this size (stream segments, small buffers) take short prev items
+constexpr uint64_t ZD_S1S_HOST = 8192, ZD_SMALL_JOB_HOST = 4ull << 20;
 constexpr uint32_t ZD_STATE_A_HOST = 2u << 1;  // deflate_slow state A (deflate_zlib.hip ZD_STATE_A)
 struct ZdWorkspace {
-  size_t cap_pos = 0, cap_bm = 0, cap_w1 = 0, cap_w2 = 0, cap_blk = 0;
+  size_t cap_pos = 0, cap_bm = 0, cap_w1 = 0, cap_w1s = 0, cap_w2 = 0, cap_blk = 0;
   uint16_t *d_prevd = nullptr;
   uint32_t *d_ma = nullptr, *d_mb = nullptr, *d_bm = nullptr, *d_aux = nullptr, *d_slot_job = nullptr, *d_flag = nullptr;
-  ZsZWorkDev *d_w1 = nullptr, *d_w2 = nullptr;
+  ZsZWorkDev *d_w1 = nullptr, *d_w1s = nullptr, *d_w2 = nullptr;
   ZsZBlkDev *d_blks = nullptr;
   hipEvent_t ev[4] = {};
 };
@@ -1453,11 +1457,11 @@ struct ZdHist {  // a deflate_fast job's insertion bits for its history [0, psta
   size_t nwords;
 };
 struct ZdPlan {
-  std::vector<ZsZWorkDev> w1, w2;
+  std::vector<ZsZWorkDev> w1, w1s, w2;  // w1s: short prev items of small jobs (zs_zd_prev_small_kernel)
   std::vector<uint32_t> slot_job;
   std::vector<ZdHist> hist;
   size_t pos = 0, bmw = 0;
-  uint32_t nex = 0, nslow = 0, nfast = 0;
+  uint32_t nex = 0, nslow = 0, nfast = 0, max_regions = 0;  // max_regions: over the deflate_slow jobs
 } g_zdp;
 
 // before the jobs are uploaded: position arrays, bitmaps, block slots of the
@@ -1478,7 +1482,11 @@ void zd_plan(uint32_t nv) {
       P.nfast++;
     } else {
       P.nslow++;
-      for (uint64_t a = 0; a < L; a += ZD_S1_HOST) P.w1.push_back({k, (uint32_t)std::min<uint64_t>(ZD_S1_HOST, L - a), a});
+      P.max_regions = std::max(P.max_regions, jd.nseg);
+      if (L <= ZD_SMALL_JOB_HOST)
+        for (uint64_t a = 0; a < L; a += ZD_S1S_HOST) P.w1s.push_back({k, (uint32_t)std::min<uint64_t>(ZD_S1S_HOST, L - a), a});
+      else
+        for (uint64_t a = 0; a < L; a += ZD_S1_HOST) P.w1.push_back({k, (uint32_t)std::min<uint64_t>(ZD_S1_HOST, L - a), a});
       for (uint64_t a = 0; a < L; a += ZD_S2_HOST) P.w2.push_back({k, (uint32_t)std::min<uint64_t>(ZD_S2_HOST, L - a), a});
     }
     jd.zblk0 = (uint32_t)P.slot_job.size();
@@ -1489,7 +1497,7 @@ void zd_plan(uint32_t nv) {
 
 int zd_run(uint32_t nv, size_t nseg, hipStream_t st) {
   ZdPlan &P = g_zdp;
-  std::vector<ZsZWorkDev> &w1 = P.w1, &w2 = P.w2;
+  std::vector<ZsZWorkDev> &w1 = P.w1, &w1s = P.w1s, &w2 = P.w2;
   std::vector<uint32_t> &slot_job = P.slot_job;
   const size_t pos = P.pos, bmw = P.bmw;
   const uint32_t nex = P.nex;
@@ -1514,6 +1522,7 @@ int zd_run(uint32_t nv, size_t nseg, hipStream_t st) {
   }
   (void)cpos;
   if ((r = grow(&g_zd.d_bm, &g_zd.cap_bm, bmw + 16)) || (r = grow(&g_zd.d_w1, &g_zd.cap_w1, w1.size() + 1)) ||
+      (r = grow(&g_zd.d_w1s, &g_zd.cap_w1s, w1s.size() + 1)) ||
       (r = grow(&g_zd.d_w2, &g_zd.cap_w2, w2.size() + 1)))
     return r;
   if (slot_job.size() > g_zd.cap_blk) {
@@ -1531,6 +1540,8 @@ int zd_run(uint32_t nv, size_t nseg, hipStream_t st) {
     if (h.nwords)
       HIP_OK(hipMemcpyAsync(g_zd.d_bm + h.word0, h.bits, h.nwords * sizeof(uint32_t), hipMemcpyHostToDevice, st));
   if (!w1.empty()) HIP_OK(hipMemcpyAsync(g_zd.d_w1, w1.data(), w1.size() * sizeof(ZsZWorkDev), hipMemcpyHostToDevice, st));
+  if (!w1s.empty())
+    HIP_OK(hipMemcpyAsync(g_zd.d_w1s, w1s.data(), w1s.size() * sizeof(ZsZWorkDev), hipMemcpyHostToDevice, st));
   if (!w2.empty()) HIP_OK(hipMemcpyAsync(g_zd.d_w2, w2.data(), w2.size() * sizeof(ZsZWorkDev), hipMemcpyHostToDevice, st));
   HIP_OK(hipMemcpyAsync(g_zd.d_slot_job, slot_job.data(), slot_job.size() * sizeof(uint32_t), hipMemcpyHostToDevice, st));
   hipEvent_t *ev = nullptr;
@@ -1539,10 +1550,11 @@ int zd_run(uint32_t nv, size_t nseg, hipStream_t st) {
       for (int i = 0; i < 4; i++) HIP_OK(hipEventCreate(&g_zd.ev[i]));
     ev = g_zd.ev;
   }
-  if (zs_launch_zdeflate(g_dz.d_jobs, nv, g_dz.d_segs, (uint32_t)nseg, g_zd.d_w1, (uint32_t)w1.size(), g_zd.d_w2,
+  if (zs_launch_zdeflate(g_dz.d_jobs, nv, g_dz.d_segs, (uint32_t)nseg, g_zd.d_w1, (uint32_t)w1.size(), g_zd.d_w1s,
+                         (uint32_t)w1s.size(), g_zd.d_w2,
                          (uint32_t)w2.size(), g_zd.d_prevd, g_zd.d_ma, g_zd.d_mb, g_zd.d_bm, g_zd.d_blks,
                          (uint32_t)slot_job.size(), g_zd.d_slot_job, g_zd.d_aux, g_dz.d_stage, g_zd.d_flag, P.nslow != 0,
-                         P.nfast != 0, st, ev)) {
+                         P.nfast != 0, P.max_regions, st, ev)) {
     set_err("zlib-identical deflate: fix-up round failed");
     return ZS_ENODEV;
   }
