@@ -244,8 +244,10 @@ __global__ void __launch_bounds__(ZD_MT) zs_zd_match_kernel(const ZsDJobDev *__r
   const uint32_t nice = zd_cfg[level][2], chain = zd_cfg[level][3], chain_b = chain >> 2;
   const uint32_t max_dist = zd_max_dist(jb);
   uint32_t *oa = ma + jb.pos0, *ob = mb + jb.pos0;
-  // each wave owns 512 consecutive positions; a lane takes the next one when its walk ends
-  const uint32_t per_w = ZD_S2 / (ZD_MT / WAVE);
+  // each wave owns a 16th of the item (512 positions of a full one; short
+  // items -- small jobs, for latency -- at least 64); a lane takes the next
+  // position when its walk ends
+  const uint32_t per_w = max(64u, ((wk.len + ZD_MT / WAVE - 1) / (ZD_MT / WAVE) + 63u) & ~63u);
   const uint64_t q_beg = s + (uint64_t)wv * per_w;
   const uint64_t q_end = min(s + wk.len, q_beg + per_w);
   uint64_t nextp = q_beg + WAVE;

@@ -1401,7 +1401,7 @@ DzWorkspace g_dz;
 // per work item, per block
 constexpr uint64_t ZD_S1_HOST = 131072, ZD_S2_HOST = 8192, ZD_BLOCK_HOST = 16383, ZD_AUX_HOST = 352;
 // jobs up to this size (stream segments, small buffers) take short prev items
-constexpr uint64_t ZD_S1S_HOST = 8192, ZD_SMALL_JOB_HOST = 4ull << 20;
+constexpr uint64_t ZD_S1S_HOST = 8192, ZD_S2S_HOST = 2048, ZD_SMALL_JOB_HOST = 4ull << 20;
 constexpr uint32_t ZD_STATE_A_HOST = 2u << 1;  // deflate_slow state A (deflate_zlib.hip ZD_STATE_A)
 struct ZdWorkspace {
   size_t cap_pos = 0, cap_bm = 0, cap_w1 = 0, cap_w1s = 0, cap_w2 = 0, cap_blk = 0;
@@ -1483,11 +1483,13 @@ void zd_plan(uint32_t nv) {
     } else {
       P.nslow++;
       P.max_regions = std::max(P.max_regions, jd.nseg);
-      if (L <= ZD_SMALL_JOB_HOST)
+      const bool small = L <= ZD_SMALL_JOB_HOST;
+      if (small)
         for (uint64_t a = 0; a < L; a += ZD_S1S_HOST) P.w1s.push_back({k, (uint32_t)std::min<uint64_t>(ZD_S1S_HOST, L - a), a});
       else
         for (uint64_t a = 0; a < L; a += ZD_S1_HOST) P.w1.push_back({k, (uint32_t)std::min<uint64_t>(ZD_S1_HOST, L - a), a});
-      for (uint64_t a = 0; a < L; a += ZD_S2_HOST) P.w2.push_back({k, (uint32_t)std::min<uint64_t>(ZD_S2_HOST, L - a), a});
+      const uint64_t s2 = small ? ZD_S2S_HOST : ZD_S2_HOST;  // shorter match items: the job's latency
+      for (uint64_t a = 0; a < L; a += s2) P.w2.push_back({k, (uint32_t)std::min<uint64_t>(s2, L - a), a});
     }
     jd.zblk0 = (uint32_t)P.slot_job.size();
     jd.zblk_cap = (uint32_t)((L + ZD_BLOCK_HOST - 1) / ZD_BLOCK_HOST + 1);
