@@ -618,6 +618,20 @@ def stream_leg(args, zstreams, np, cpu):
                                 ctypes.byref(bad))
         return tot.value / t / 2**20, bool(not bad.value)
 
+    # the compress side of the surface: CompressionStreamZlib (deflate_process per
+    # <= 32 KiB, Z_NO_FLUSH, then the Z_FINISH drain) at the default level, one
+    # handle; bytes checked against host zlib driven with the same calls
+    import zlib as _zlib
+    dbytes = raw1[: min(len(raw1), 8 << 20)].tobytes()
+    zstreams.compress(dbytes[: 1 << 20], "deflate-raw", 6, ws)  # warm
+    t0 = time.perf_counter()
+    dcomp = zstreams.compress(dbytes, "deflate-raw", 6, ws)
+    tdz = time.perf_counter() - t0
+    zc = _zlib.compressobj(6, _zlib.DEFLATED, -15, 8, 0)
+    t0 = time.perf_counter()
+    zref = b"".join(zc.compress(dbytes[o:o + 32768]) for o in range(0, len(dbytes), 32768)) + zc.flush()
+    tzl = time.perf_counter() - t0
+
     reps = max(1, int(2e9 // one_bytes))
     c1v, c1ok = cpu_js([comp1] * reps, 1, one_bytes)
     thr = max(1, min(cpu["physical_cores"], nh))
@@ -637,6 +651,12 @@ def stream_leg(args, zstreams, np, cpu):
                     "launches": launches, "calls_per_launch": round(calls_m / max(1, launches), 1),
                     "verified": bool(okm)},
         "wasm_reference_mibs": 493,
+        "compress_one_handle": {"value": round(len(dbytes) / tdz / 2**20, 1), "unit": "MiB/s (input)",
+                                "api": "CompressionStreamZlib deflate-raw level 6 (deflate_process per <= 32 KiB, "
+                                       "Z_NO_FLUSH, Z_FINISH drain)",
+                                "stream": f"line text {len(dbytes) >> 20} MiB",
+                                "bytes_identical_to_zlib": dcomp == zref,
+                                "cpu_zlib_same_calls": round(len(dbytes) / tzl / 2**20, 1)},
         "cpu_baseline": {"one_handle": round(c1v, 1), "handles_all_cores": round(cmv, 1), "threads": thr,
                          "unit": "MiB/s", "kind": "reference",
                          "impl": "host zlib 1.2.11 inflate, same call schedule (the shipped WASM runs this loop)",

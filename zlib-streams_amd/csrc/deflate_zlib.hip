@@ -1306,22 +1306,33 @@ struct ZdTreeLDS {
   uint32_t freq[ZD_HEAP];
   uint16_t dl[ZD_HEAP];  // parent while building, then code length (zlib's Dad / Len union)
   uint8_t depth[ZD_HEAP];
-  int16_t heap[ZD_HEAP];
+  int16_t heap[ZD_HEAP];  // the nodes in extraction order (heap[heap_max..])
+  uint64_t hk[ZD_HEAP];   // the live heap: (freq << 8 | depth) << 10 | node
   uint16_t blc[16];
 };
 
-__device__ __forceinline__ bool zd_smaller(const ZdTreeLDS &w, int n, int m) {
-  return w.freq[n] < w.freq[m] || (w.freq[n] == w.freq[m] && w.depth[n] <= w.depth[m]);
+// zlib's smaller(): freq, then depth, as one key -- the heap holds its
+// entries' keys, so a sift level is one LDS round trip (two children), not
+// two (the children, then their freq and depth)
+__device__ __forceinline__ uint64_t zd_key(const ZdTreeLDS &w, int n) {
+  return ((uint64_t)((w.freq[n] << 8) | w.depth[n]) << 10) | (uint64_t)n;
 }
 __device__ void zd_sift(ZdTreeLDS &w, int hl, int k) {
-  const int v = w.heap[k];
+  const uint64_t v = w.hk[k];
   for (int j = k << 1; j <= hl; j <<= 1) {
-    if (j < hl && zd_smaller(w, w.heap[j + 1], w.heap[j])) j++;
-    if (zd_smaller(w, v, w.heap[j])) break;
-    w.heap[k] = w.heap[j];
+    uint64_t a = w.hk[j];
+    if (j < hl) {
+      const uint64_t b = w.hk[j + 1];
+      if ((b >> 10) <= (a >> 10)) {
+        j++;
+        a = b;
+      }
+    }
+    if ((v >> 10) <= (a >> 10)) break;
+    w.hk[k] = a;
     k = j;
   }
-  w.heap[k] = (int16_t)v;
+  w.hk[k] = v;
 }
 
 // freq[0..elems) in w.freq; lens out in len_out[0..elems), canonical LSB-first
@@ -1331,36 +1342,37 @@ __device__ int zd_build(ZdTreeLDS &w, int elems, const uint8_t *stat, const uint
   int max_code = -1, hl = 0, hmax = ZD_HEAP;
   for (int n = 0; n < elems; n++) {
     if (w.freq[n]) {
-      w.heap[++hl] = (int16_t)(max_code = n);
+      max_code = n;
       w.depth[n] = 0;
+      w.hk[++hl] = zd_key(w, n);
     } else {
       w.dl[n] = 0;
     }
   }
   while (hl < 2) {
     const int node = max_code < 2 ? ++max_code : 0;
-    w.heap[++hl] = (int16_t)node;
     w.freq[node] = 1;
     w.depth[node] = 0;
+    w.hk[++hl] = zd_key(w, node);
     opt_len--;
     if (stat) static_len -= stat[node];
   }
   for (int n = hl / 2; n >= 1; n--) zd_sift(w, hl, n);
   int node = elems;
   do {
-    const int n = w.heap[1];
-    w.heap[1] = w.heap[hl--];
+    const int n = (int)(w.hk[1] & 1023u);
+    w.hk[1] = w.hk[hl--];
     zd_sift(w, hl, 1);
-    const int m = w.heap[1];
+    const int m = (int)(w.hk[1] & 1023u);
     w.heap[--hmax] = (int16_t)n;
     w.heap[--hmax] = (int16_t)m;
     w.freq[node] = w.freq[n] + w.freq[m];
     w.depth[node] = (uint8_t)((w.depth[n] >= w.depth[m] ? w.depth[n] : w.depth[m]) + 1);
     w.dl[n] = w.dl[m] = (uint16_t)node;
-    w.heap[1] = (int16_t)node++;
+    w.hk[1] = zd_key(w, node++);
     zd_sift(w, hl, 1);
   } while (hl >= 2);
-  w.heap[--hmax] = w.heap[1];
+  w.heap[--hmax] = (int16_t)(w.hk[1] & 1023u);
   for (int b = 0; b < 16; b++) w.blc[b] = 0;
   w.dl[w.heap[hmax]] = 0;
   int overflow = 0, h;
