@@ -70,6 +70,29 @@ struct ZsZWorkDev {  // one K1 / K2 work item
 
 __device__ __forceinline__ uint32_t zd_max_dist(const ZsDJobDev &jb) { return (1u << jb.wbits) - ZD_LOOK; }
 
+// deflate_slow state A (avail 0, prev_len 2): after every match, and the stream start (K3)
+#define ZD_STATE_A (2u << 1)
+
+// bitmaps of a job: S (token starts), V (variant of match starts), M (state-A
+// marks), I (deflate_fast: positions inserted into the hash chains), A / B
+// (deflate_slow: positions whose match under max_chain / max_chain >> 2 the
+// search kernel wrote)
+struct ZdBm {
+  uint32_t *S, *V, *M, *I, *A, *B;
+};
+__device__ __forceinline__ uint64_t zd_bm_words(uint64_t L) { return (L + 32u) / 32u + 1u; }
+__device__ __forceinline__ ZdBm zd_bm(uint32_t *bm, const ZsDJobDev &jb) {
+  const uint64_t words = zd_bm_words(jb.in_len);
+  ZdBm b;
+  b.S = bm + jb.bm0;
+  b.V = b.S + words;
+  b.M = b.V + words;
+  b.I = b.M + words;
+  b.A = b.I + words;
+  b.B = b.A + words;
+  return b;
+}
+
 // ---------------------------------------------------------------------------
 // K1: previous same-hash distance (0: none within 32767, or position 0 = NIL)
 // ---------------------------------------------------------------------------
@@ -220,7 +243,7 @@ __device__ __forceinline__ uint32_t zd_lw(const uint32_t *w, uint32_t a) {  // 4
 __global__ void __launch_bounds__(ZD_MT) zs_zd_match_kernel(const ZsDJobDev *__restrict__ jobs,
                                                              const ZsZWorkDev *__restrict__ work,
                                                              const uint16_t *__restrict__ prevd, uint32_t *__restrict__ ma,
-                                                             uint32_t *__restrict__ mb) {
+                                                             uint32_t *__restrict__ mb, uint32_t *__restrict__ bm) {
   __shared__ __attribute__((aligned(16))) uint32_t s_w[ZD_WB / 4 + 4];
   __shared__ __attribute__((aligned(16))) uint16_t s_pd[ZD_S2 + 32768u];
   const uint32_t t = threadIdx.x, lane = t & (WAVE - 1), wv = t / WAVE;
@@ -353,6 +376,227 @@ __global__ void __launch_bounds__(ZD_MT) zs_zd_match_kernel(const ZsDJobDev *__r
     }
     if (!__ballot(active)) break;
   }
+  // every position of the item has both results (items start 32-aligned)
+  const ZdBm Bm = zd_bm(bm, jb);
+  for (uint32_t i = t; i < (wk.len + 31u) / 32u; i += ZD_MT) Bm.A[s / 32u + i] = Bm.B[s / 32u + i] = ~0u;
+}
+
+// ---------------------------------------------------------------------------
+// K2 (default): longest matches only where deflate_slow's parse looks for them.
+// The parse searches at a loop top only while prev_length < max_lazy, never
+// inside the matches it emits: ~0.2-0.3 searches per byte of text, and the
+// positions it skips are the expensive ones (inside repeats, the full chain
+// budget runs): tools/zd_search_probe.c, C2 text at L6, zs_zd_match_kernel
+// walks 43 (Zipf) / 98 (lines) chain candidates per byte, the true parse 4.8 /
+// 3.3.  Which loop tops the parse reaches depends on the matches, so the
+// kernel walks the parse itself: one workgroup per 16 KiB item (window bytes
+// and chain links in LDS, as zs_zd_match_kernel), a walk starting in state A
+// at every 16th position (and at the job's parse entry), each lane taking the
+// next start when its walk ends.  A walk stops at a state-A loop top another
+// walk already claimed (both would continue identically) or at the item's
+// end, so every path from a start is walked once up to the item end -- the
+// paths the parse kernel's pieces (state A at every 256th position) and
+// re-walks follow.  A search runs the budget the state asks for, as
+// longest_match does; its result goes to ma / mb and its bit to the job's A / B
+// bitmap.  Searches the walks did not make (a parse path entering an item from
+// the previous one, until it meets a walked path) run on demand in the parse
+// (zd_lookup).  Probe: 0.41 (Zipf) / 0.49 (lines) searches per byte, 8.9 /
+// 20.8 candidates, lanes busy 42 / 59% of the workgroup's time.
+// ---------------------------------------------------------------------------
+#define ZD_S3 16384u                     // positions per workgroup
+#define ZD_MT3 512u                      // threads per workgroup
+#define ZD_PL3 16u                       // a walk starts at every 16th position
+#define ZD_WB3 (ZD_S3 + 32768u + 272u)  // window bytes in LDS
+
+__global__ void __launch_bounds__(ZD_MT3) zs_zd_msearch_kernel(const ZsDJobDev *__restrict__ jobs,
+                                                                const ZsZWorkDev *__restrict__ work,
+                                                                const uint16_t *__restrict__ prevd,
+                                                                uint32_t *__restrict__ ma, uint32_t *__restrict__ mb,
+                                                                uint32_t *__restrict__ bm) {
+  __shared__ __attribute__((aligned(16))) uint32_t s_w[ZD_WB3 / 4 + 4];
+  __shared__ __attribute__((aligned(16))) uint16_t s_pd[ZD_S3 + 32768u];
+  __shared__ uint32_t s_claim[ZD_S3 / 32], s_sa[ZD_S3 / 32], s_sb[ZD_S3 / 32];
+  __shared__ uint32_t s_next;
+  const uint32_t t = threadIdx.x;
+  const ZsZWorkDev wk = work[blockIdx.x];
+  const ZsDJobDev jb = jobs[wk.job];
+  const uint64_t L = jb.in_len, s = wk.start;
+  const uint32_t len = wk.len;
+  if (jb.pstart >= s + len) return;  // history only: the parse never searches here
+  const int64_t B = (int64_t)s - 32768;  // LDS index of position q: q - B
+  {
+    uint8_t *wb = reinterpret_cast<uint8_t *>(s_w);
+    const uint64_t lo = B < 0 ? 0u : (uint64_t)B;
+    const uint64_t hi_b = s + len + 272u;
+    for (uint32_t i = t; i < ZD_WB3 / 4 + 4; i += ZD_MT3) s_w[i] = 0;
+    for (uint32_t i = t; i < ZD_S3 / 32; i += ZD_MT3) s_claim[i] = s_sa[i] = s_sb[i] = 0;
+    if (t == 0) s_next = 0;
+    __syncthreads();
+    for (uint64_t q = lo + t; q < hi_b && q < L; q += ZD_MT3) wb[q - B] = jb.in[q];
+    const uint16_t *pd = prevd + jb.pos0;
+    for (uint64_t q = lo + t; q < s + len; q += ZD_MT3) s_pd[q - B] = pd[q];
+  }
+  __syncthreads();
+  const uint32_t level = (uint32_t)jb.level;
+  const uint32_t good = zd_cfg[level][0], lazy = zd_cfg[level][1], nice = zd_cfg[level][2], chain = zd_cfg[level][3];
+  const uint32_t max_dist = zd_max_dist(jb);
+  uint32_t *oa = ma + jb.pos0 + s, *ob = mb + jb.pos0 + s;
+  // starts: the job's parse entry when it lies in this item, then every 16th
+  // position after it
+  const bool ent = jb.pstart >= s;
+  const uint32_t k0 = ent ? (uint32_t)((jb.pstart - s) / ZD_PL3) + 1u : 0u;
+  const uint32_t npl = (len + ZD_PL3 - 1u) / ZD_PL3;
+  const uint32_t nst = (ent ? 1u : 0u) + (npl > k0 ? npl - k0 : 0u);
+  // walk: loop top iq (item offset) in state st; search: at iq, budget svar
+  uint32_t iq = 0, st = 0, svar = 0;
+  bool walking = false, idle = false, srch = false, have = false;
+  uint32_t c = 0, k = 0, best = 0, bdist = 0, cap = 0, nicep = 0, ow = 0, pi = 0, clim = 0;
+  auto cmp_len = [&](uint32_t a0) -> uint32_t {  // as zs_zd_match_kernel
+    uint32_t n = 0;
+    for (;;) {
+      const uint32_t a = a0 + n, b = pi + n;
+      const uint32_t wa = a >> 2, wb = b >> 2, sa = a & 3u, sb = b & 3u;
+      uint32_t ua[5], ub[5];
+#pragma unroll
+      for (int q = 0; q < 5; q++) {
+        ua[q] = s_w[wa + q];
+        ub[q] = s_w[wb + q];
+      }
+      uint32_t x = 0, g = 0;
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const uint32_t d = __builtin_amdgcn_alignbyte(ua[q + 1], ua[q], sa) ^ __builtin_amdgcn_alignbyte(ub[q + 1], ub[q], sb);
+        if (x == 0) {
+          x = d;
+          g = (uint32_t)q;
+        }
+      }
+      if (x) {
+        n += 4 * g + ((uint32_t)__builtin_ctz(x) >> 3);
+        break;
+      }
+      n += 16;
+      if (n >= cap) break;
+    }
+    return min(n, cap);
+  };
+  // one chain step of a searching lane (zs_zd_match_kernel's step, one budget)
+  auto cstep = [&]() {
+    const uint32_t cc = srch ? c : 0u;
+    const uint32_t nd = s_pd[cc];
+    const uint32_t se = zd_lw(s_w, cc + (best >= 3 ? best - 3 : 0u));
+    if (srch && (best < 3 || se == ow)) {
+      const uint32_t n = cmp_len(c);
+      if (n > best) {
+        best = n;
+        bdist = pi - c;
+        if (best >= 3) ow = zd_lw(s_w, pi + best - 3);
+      }
+    }
+    k += srch ? 1u : 0u;
+    const uint32_t cn = c - nd;
+    const bool stop = srch && (best >= nicep || k >= clim || nd == 0 || (pi - cn) >= max_dist);
+    c = srch && !stop ? cn : c;
+    have = have || stop;
+    srch = srch && !stop;
+  };
+  // deflate_slow's iteration at iq with match m (zd_step)
+  auto advance = [&](uint32_t m) {
+    const uint32_t pl = (st >> 1) & 511u;
+    uint32_t mlen = 2, mdist = 0, mvar = 0;
+    if (pl < lazy) {
+      mvar = pl >= good ? 1u : 0u;
+      const uint32_t ml = m & 511u;
+      if (ml > pl) {
+        mlen = ml;
+        mdist = m >> 9;
+      } else if (ml) {
+        mlen = pl;
+      }
+      if (mlen == ZD_MINM && mdist > ZD_TOO_FAR) mlen = 2;
+    }
+    if (pl >= ZD_MINM && mlen <= pl) {
+      iq = iq - 1u + pl;
+      st = ZD_STATE_A;
+    } else {
+      st = 1u | (mlen << 1) | (mvar << 10) | (mdist << 11);
+      iq += 1u;
+    }
+  };
+  auto record = [&](uint32_t m) {
+    (svar ? ob : oa)[iq] = m;
+    atomicOr(&(svar ? s_sb : s_sa)[iq >> 5], 1u << (iq & 31u));
+  };
+  for (;;) {
+    if (!idle && !srch) {
+      if (have) {  // the search at iq ended
+        const uint32_t m = best | (bdist << 9);
+        record(m);
+        advance(m);
+        have = false;
+      }
+      // step the walk to its next search, taking new starts as walks end
+      for (;;) {
+        if (!walking) {
+          const uint32_t i = atomicAdd(&s_next, 1u);
+          if (i >= nst) {
+            idle = true;
+            break;
+          }
+          if (ent && i == 0) {
+            iq = (uint32_t)(jb.pstart - s);
+            st = jb.pstate;
+          } else {
+            iq = (k0 + i - (ent ? 1u : 0u)) * ZD_PL3;
+            st = ZD_STATE_A;
+          }
+          walking = true;
+        }
+        if (iq >= len) {  // the item's exit: the next item's walks go on from there
+          walking = false;
+          continue;
+        }
+        if (st == ZD_STATE_A) {
+          const uint32_t bit = 1u << (iq & 31u);
+          if (atomicOr(&s_claim[iq >> 5], bit) & bit) {  // another walk goes on from here
+            walking = false;
+            continue;
+          }
+        }
+        const uint32_t pl = (st >> 1) & 511u;
+        if (pl >= lazy) {  // no search: the pending match is emitted
+          advance(0);
+          continue;
+        }
+        svar = pl >= good ? 1u : 0u;
+        pi = iq + 32768u;
+        best = bdist = k = 0;
+        clim = svar ? chain >> 2 : chain;
+        const uint32_t d0 = s_pd[pi];
+        const uint64_t look = L - s - iq;
+        if (look < ZD_MINM || d0 == 0 || d0 > max_dist) {  // no candidate
+          record(0);
+          advance(0);
+          continue;
+        }
+        cap = look < ZD_MAXM ? (uint32_t)look : ZD_MAXM;
+        nicep = look < nice ? (uint32_t)look : nice;
+        c = pi - d0;
+        srch = true;
+        break;
+      }
+    }
+    if (!__ballot(!idle)) break;
+    // sixteen chain steps between walk updates (zs_zd_match_kernel's refill rhythm)
+#pragma unroll
+    for (int r = 0; r < 16; r++) cstep();
+  }
+  __syncthreads();
+  const ZdBm Bm = zd_bm(bm, jb);
+  for (uint32_t i = t; i < (len + 31u) / 32u; i += ZD_MT3) {
+    Bm.A[s / 32u + i] = s_sa[i];
+    Bm.B[s / 32u + i] = s_sb[i];
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -362,14 +606,64 @@ __global__ void __launch_bounds__(ZD_MT) zs_zd_match_kernel(const ZsDJobDev *__r
 // records).  Packed: bit 0 avail, 1-9 prev_len, 10 variant, 11-25 prev_dist.
 // State A (avail 0, prev_len 2) follows every match and starts the stream.
 // ---------------------------------------------------------------------------
-#define ZD_STATE_A (2u << 1)
 
 struct ZdTabs {
   const uint32_t *ma, *mb;
   const uint8_t *in;
   uint64_t L;
   uint32_t good, lazy;
+  // the parse walks (zd_step): which (position, budget) zs_zd_msearch_kernel
+  // searched (bitmaps A / B), and what an on-demand search needs
+  const uint32_t *sa, *sb;
+  uint32_t *wa, *wb;  // ma / mb, written by on-demand searches
+  const uint16_t *pd;
+  uint32_t nice, chain, max_dist;
 };
+
+// longest_match at p under one chain budget (var 1: max_chain >> 2), from
+// global memory: the parse's searches zs_zd_msearch_kernel did not make (a
+// walk entering an item from its predecessor, until it meets a searched path).
+// Same rules and result as the kernel's LDS walk: candidates along the same-hash
+// chain while the chain budget lasts, the link exists and the candidate is
+// within max_dist; strictly longer matches only; nice_length ends the walk.
+__device__ __noinline__ uint32_t zd_search_g(const ZdTabs &T, uint64_t p, uint32_t var) {
+  const uint32_t d0 = T.pd[p];
+  if (p + ZD_MINM > T.L || d0 == 0 || d0 > T.max_dist) return 0;
+  const uint64_t look = T.L - p;
+  const uint32_t cap = look < ZD_MAXM ? (uint32_t)look : ZD_MAXM;
+  const uint32_t nicep = look < T.nice ? (uint32_t)look : T.nice;
+  const uint32_t clim = var ? T.chain >> 2 : T.chain;
+  const uint8_t *in = T.in;
+  uint64_t c = p - d0;
+  uint32_t best = 0, bdist = 0;
+  for (uint32_t k = 0;;) {
+    if (best < 3 || (in[c + best] == in[p + best] && in[c + best - 1] == in[p + best - 1])) {
+      uint32_t n = 0;
+      while (n < cap && in[c + n] == in[p + n]) n++;
+      if (n > best) {
+        best = n;
+        bdist = (uint32_t)(p - c);
+      }
+    }
+    k++;
+    const uint32_t nd = T.pd[c];
+    if (best >= nicep || k >= clim || nd == 0) break;
+    const uint64_t cn = c - nd;
+    if (p - cn >= T.max_dist) break;
+    c = cn;
+  }
+  return best | (bdist << 9);
+}
+
+// the match table entry the parse reads at p (budget var): searched by
+// zs_zd_msearch_kernel, or searched here and stored for the token kernels
+__device__ __forceinline__ uint32_t zd_lookup(const ZdTabs &T, uint64_t p, uint32_t var) {
+  const uint32_t m = (var ? T.mb : T.ma)[p];
+  if (((var ? T.sb : T.sa)[p >> 5] >> (p & 31u)) & 1u) return m;
+  const uint32_t x = zd_search_g(T, p, var);
+  (var ? T.wb : T.wa)[p] = x;
+  return x;
+}
 
 // one loop iteration at p; returns the token emitted (start, kind) via out
 // params: tok = 0 none, 1 literal at p - 1, 2 match at p - 1 (variant in *var)
@@ -378,7 +672,7 @@ __device__ __forceinline__ uint32_t zd_step(const ZdTabs &T, uint64_t &p, uint32
   uint32_t mlen = 2, mdist = 0, mvar = 0;
   if (pl < T.lazy) {
     mvar = pl >= T.good ? 1u : 0u;
-    const uint32_t m = (mvar ? T.mb : T.ma)[p];
+    const uint32_t m = zd_lookup(T, p, mvar);
     const uint32_t ml = m & 511u;
     if (ml > pl) {
       mlen = ml;
@@ -407,20 +701,25 @@ __device__ __forceinline__ void zd_putbit(uint32_t *w, uint64_t i, bool v) {
 }
 __device__ __forceinline__ bool zd_getbit(const uint32_t *w, uint64_t i) { return (w[i >> 5] >> (i & 31u)) & 1u; }
 
-// bitmaps of a job: S (token starts), V (variant of match starts), M (state-A
-// marks), I (deflate_fast: positions inserted into the hash chains)
-struct ZdBm {
-  uint32_t *S, *V, *M, *I;
-};
-__device__ __forceinline__ uint64_t zd_bm_words(uint64_t L) { return (L + 32u) / 32u + 1u; }
-__device__ __forceinline__ ZdBm zd_bm(uint32_t *bm, const ZsDJobDev &jb) {
-  const uint64_t words = zd_bm_words(jb.in_len);
-  ZdBm b;
-  b.S = bm + jb.bm0;
-  b.V = b.S + words;
-  b.M = b.V + words;
-  b.I = b.M + words;
-  return b;
+// the tables a parse walk reads (zd_step): match tables, searched bitmaps and
+// what an on-demand search needs
+__device__ __forceinline__ ZdTabs zd_tabs(const ZsDJobDev &jb, uint32_t *ma, uint32_t *mb, const uint16_t *prevd,
+                                          uint32_t *bm) {
+  ZdTabs T;
+  T.ma = T.wa = ma + jb.pos0;
+  T.mb = T.wb = mb + jb.pos0;
+  T.in = jb.in;
+  T.L = jb.in_len;
+  T.good = zd_cfg[jb.level][0];
+  T.lazy = zd_cfg[jb.level][1];
+  T.nice = zd_cfg[jb.level][2];
+  T.chain = zd_cfg[jb.level][3];
+  T.max_dist = zd_max_dist(jb);
+  T.pd = prevd + jb.pos0;
+  const ZdBm b = zd_bm(bm, jb);
+  T.sa = b.A;
+  T.sb = b.B;
+  return T;
 }
 
 // Token bits of a walk over [lo, hi): every loop top q with a literal pending
@@ -445,8 +744,8 @@ __device__ __forceinline__ void zd_walk_record(const ZdTabs &T, uint64_t &q, uin
 }
 
 __global__ void __launch_bounds__(ZD_PT) zs_zd_parse_kernel(const ZsDJobDev *__restrict__ jobs, ZsDSegDev *__restrict__ segs,
-                                                             const uint32_t *__restrict__ ma, const uint32_t *__restrict__ mb,
-                                                             uint32_t *__restrict__ bm) {
+                                                             uint32_t *__restrict__ ma, uint32_t *__restrict__ mb,
+                                                             const uint16_t *__restrict__ prevd, uint32_t *__restrict__ bm) {
   __shared__ uint32_t s_S[ZD_REG / 32], s_V[ZD_REG / 32], s_M[ZD_REG / 32];
   __shared__ uint64_t s_xp[ZD_PT];
   __shared__ uint32_t s_xs[ZD_PT];
@@ -454,13 +753,7 @@ __global__ void __launch_bounds__(ZD_PT) zs_zd_parse_kernel(const ZsDJobDev *__r
   const ZsDSegDev sg = segs[blockIdx.x];
   const ZsDJobDev jb = jobs[sg.job];
   if (jb.exact != ZD_SLOW) return;
-  ZdTabs T;
-  T.ma = ma + jb.pos0;
-  T.mb = mb + jb.pos0;
-  T.in = jb.in;
-  T.L = jb.in_len;
-  T.good = zd_cfg[jb.level][0];
-  T.lazy = zd_cfg[jb.level][1];
+  const ZdTabs T = zd_tabs(jb, ma, mb, prevd, bm);
   const uint64_t r0 = sg.start, rend = sg.start + sg.len;
   const uint64_t a = r0 + (uint64_t)t * 256u, b = min(rend, a + 256u);
   // the job's parse entry (pstart, pstate) lies in its first region (the
@@ -560,21 +853,15 @@ __global__ void __launch_bounds__(ZD_PT) zs_zd_parse_kernel(const ZsDJobDev *__r
 // ---------------------------------------------------------------------------
 // region i from entry (ep, es): rewrites its tokens where they change, returns
 // its exit in (xp, xs)
-__device__ void zd_fix_region(const ZsDJobDev &jb, ZsDSegDev *__restrict__ segs, uint32_t i,
-                              const uint32_t *__restrict__ ma, const uint32_t *__restrict__ mb, uint32_t *__restrict__ bm,
+__device__ void zd_fix_region(const ZsDJobDev &jb, ZsDSegDev *__restrict__ segs, uint32_t i, uint32_t *__restrict__ ma,
+                              uint32_t *__restrict__ mb, const uint16_t *__restrict__ prevd, uint32_t *__restrict__ bm,
                               uint64_t ep, uint32_t es, uint64_t &xp, uint32_t &xs) {
   const ZsDSegDev sg = segs[i];
   const uint64_t r0 = sg.start, rend = sg.start + sg.len;
   xp = sg.zx0;
   xs = sg.zs0;
   if (ep == r0 && es == ZD_STATE_A && sg.zfix == r0) return;  // its own parse stands
-  ZdTabs T;
-  T.ma = ma + jb.pos0;
-  T.mb = mb + jb.pos0;
-  T.in = jb.in;
-  T.L = jb.in_len;
-  T.good = zd_cfg[jb.level][0];
-  T.lazy = zd_cfg[jb.level][1];
+  const ZdTabs T = zd_tabs(jb, ma, mb, prevd, bm);
   ZdBm Bm = zd_bm(bm, jb);
   // 1. where does the walk from the entry merge with the region's own parse?
   uint64_t q = ep;
@@ -613,8 +900,8 @@ __device__ void zd_fix_region(const ZsDJobDev &jb, ZsDSegDev *__restrict__ segs,
 }
 
 __global__ void zs_zd_fix_kernel(const ZsDJobDev *__restrict__ jobs, ZsDSegDev *__restrict__ segs, uint32_t nseg,
-                                 const uint32_t *__restrict__ ma, const uint32_t *__restrict__ mb, uint32_t *__restrict__ bm,
-                                 uint32_t cur, uint32_t *__restrict__ changed) {
+                                 uint32_t *__restrict__ ma, uint32_t *__restrict__ mb, const uint16_t *__restrict__ prevd,
+                                 uint32_t *__restrict__ bm, uint32_t cur, uint32_t *__restrict__ changed) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nseg) return;
   const ZsDSegDev sg = segs[i];
@@ -628,7 +915,7 @@ __global__ void zs_zd_fix_kernel(const ZsDJobDev *__restrict__ jobs, ZsDSegDev *
   }
   uint64_t xp;
   uint32_t xs;
-  zd_fix_region(jb, segs, i, ma, mb, bm, ep, es, xp, xs);
+  zd_fix_region(jb, segs, i, ma, mb, prevd, bm, ep, es, xp, xs);
   segs[i].zx[cur ^ 1u] = xp;
   segs[i].zs[cur ^ 1u] = xs;
   if (xp != sg.zx[cur] || xs != sg.zs[cur]) atomicOr(changed, 1u);
@@ -637,8 +924,8 @@ __global__ void zs_zd_fix_kernel(const ZsDJobDev *__restrict__ jobs, ZsDSegDev *
 // one thread per job: its regions in order from the job's start, so every
 // entry is final when its region is walked (no rounds)
 __global__ void zs_zd_fix_seq_kernel(const ZsDJobDev *__restrict__ jobs, uint32_t njobs, ZsDSegDev *__restrict__ segs,
-                                     const uint32_t *__restrict__ ma, const uint32_t *__restrict__ mb,
-                                     uint32_t *__restrict__ bm) {
+                                     uint32_t *__restrict__ ma, uint32_t *__restrict__ mb,
+                                     const uint16_t *__restrict__ prevd, uint32_t *__restrict__ bm) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= njobs) return;
   const ZsDJobDev jb = jobs[j];
@@ -652,7 +939,7 @@ __global__ void zs_zd_fix_seq_kernel(const ZsDJobDev *__restrict__ jobs, uint32_
     }
     uint64_t xp;
     uint32_t xs;
-    zd_fix_region(jb, segs, i, ma, mb, bm, ep, es, xp, xs);
+    zd_fix_region(jb, segs, i, ma, mb, prevd, bm, ep, es, xp, xs);
     segs[i].zx[0] = segs[i].zx[1] = xp;
     segs[i].zs[0] = segs[i].zs[1] = xs;
     ep = xp;
@@ -1843,15 +2130,18 @@ extern "C" int zs_launch_zdeflate(ZsDJobDev *d_jobs, uint32_t njobs, ZsDSegDev *
                                   const ZsZWorkDev *d_w2, uint32_t n2,
                                   uint16_t *d_prevd, uint32_t *d_ma, uint32_t *d_mb, uint32_t *d_bm, ZsZBlkDev *d_blks,
                                   uint32_t nblk_slots, const uint32_t *d_slot_job, uint32_t *d_aux, uint8_t *d_stage,
-                                  uint32_t *d_flag, int has_slow, int has_fast, uint32_t max_regions, hipStream_t st,
-                                  hipEvent_t *ev) {
+                                  uint32_t *d_flag, int has_slow, int has_fast, uint32_t max_regions, int allpos,
+                                  hipStream_t st, hipEvent_t *ev) {
   if (ev) (void)hipEventRecord(ev[0], st);
   if (n1) hipLaunchKernelGGL(zs_zd_prev_kernel, dim3(n1), dim3(ZD_PT1), 0, st, d_jobs, d_w1, d_prevd);
   if (n1s) hipLaunchKernelGGL(zs_zd_prev_small_kernel, dim3(n1s), dim3(ZD_PT1), 0, st, d_jobs, d_w1s, d_prevd);
-  if (n2) hipLaunchKernelGGL(zs_zd_match_kernel, dim3(n2), dim3(ZD_MT), 0, st, d_jobs, d_w2, d_prevd, d_ma, d_mb);
+  if (n2 && allpos) hipLaunchKernelGGL(zs_zd_match_kernel, dim3(n2), dim3(ZD_MT), 0, st, d_jobs, d_w2, d_prevd, d_ma, d_mb, d_bm);
+  if (n2 && !allpos)
+    hipLaunchKernelGGL(zs_zd_msearch_kernel, dim3(n2), dim3(ZD_MT3), 0, st, d_jobs, d_w2, d_prevd, d_ma, d_mb, d_bm);
   if (ev) (void)hipEventRecord(ev[1], st);
   if (has_fast) hipLaunchKernelGGL(zs_zd_fast_kernel, dim3(njobs), dim3(WAVE), 0, st, d_jobs, d_bm, d_ma);
-  if (has_slow) hipLaunchKernelGGL(zs_zd_parse_kernel, dim3(nseg), dim3(ZD_PT), 0, st, d_jobs, d_segs, d_ma, d_mb, d_bm);
+  if (has_slow)
+    hipLaunchKernelGGL(zs_zd_parse_kernel, dim3(nseg), dim3(ZD_PT), 0, st, d_jobs, d_segs, d_ma, d_mb, d_prevd, d_bm);
   // parallel fix-up rounds while exits change (nearly every input settles in
   // one or two), then, if a cascade is still moving, the in-order pass
   // (jobs of a few regions -- stream segments -- go straight to the in-order
@@ -1862,7 +2152,7 @@ extern "C" int zs_launch_zdeflate(ZsDJobDev *d_jobs, uint32_t njobs, ZsDSegDev *
   for (int round = 0; round < max_rounds; round++) {
     uint32_t changed = 0;
     if (hipMemsetAsync(d_flag, 0, sizeof(uint32_t), st) != hipSuccess) return -1;
-    hipLaunchKernelGGL(zs_zd_fix_kernel, dim3((nseg + 255) / 256), dim3(256), 0, st, d_jobs, d_segs, nseg, d_ma, d_mb, d_bm,
+    hipLaunchKernelGGL(zs_zd_fix_kernel, dim3((nseg + 255) / 256), dim3(256), 0, st, d_jobs, d_segs, nseg, d_ma, d_mb, d_prevd, d_bm,
                        cur, d_flag);
     if (hipMemcpyAsync(&changed, d_flag, sizeof(uint32_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipStreamSynchronize(st) != hipSuccess)
@@ -1874,7 +2164,7 @@ extern "C" int zs_launch_zdeflate(ZsDJobDev *d_jobs, uint32_t njobs, ZsDSegDev *
     }
   }
   if (!settled) {
-    hipLaunchKernelGGL(zs_zd_fix_seq_kernel, dim3((njobs + 63) / 64), dim3(64), 0, st, d_jobs, njobs, d_segs, d_ma, d_mb,
+    hipLaunchKernelGGL(zs_zd_fix_seq_kernel, dim3((njobs + 63) / 64), dim3(64), 0, st, d_jobs, njobs, d_segs, d_ma, d_mb, d_prevd,
                        d_bm);
   }
   if (ev) (void)hipEventRecord(ev[2], st);

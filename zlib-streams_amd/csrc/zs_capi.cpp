@@ -51,8 +51,8 @@ extern "C" int zs_launch_zdeflate(ZsDJobDev *d_jobs, uint32_t njobs, ZsDSegDev *
                                   const ZsZWorkDev *d_w2, uint32_t n2,
                                   uint16_t *d_prevd, uint32_t *d_ma, uint32_t *d_mb, uint32_t *d_bm, ZsZBlkDev *d_blks,
                                   uint32_t nblk_slots, const uint32_t *d_slot_job, uint32_t *d_aux, uint8_t *d_stage,
-                                  uint32_t *d_flag, int has_slow, int has_fast, uint32_t max_regions, hipStream_t st,
-                                  hipEvent_t *ev);
+                                  uint32_t *d_flag, int has_slow, int has_fast, uint32_t max_regions, int allpos,
+                                  hipStream_t st, hipEvent_t *ev);
 extern "C" void zs_launch_dz_trailer(ZsDJobDev *d_jobs, uint32_t njobs, uint8_t *d_stage, hipStream_t st);
 extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, ZsSegDev *d_segs, uint32_t nseg,
                                   ZsCJobDev *d_cjobs, uint32_t ncjobs, ZsChunkDev *d_units, uint32_t nunit_slots,
@@ -1402,6 +1402,13 @@ DzWorkspace g_dz;
 constexpr uint64_t ZD_S1_HOST = 131072, ZD_S2_HOST = 8192, ZD_BLOCK_HOST = 16383, ZD_AUX_HOST = 352;
 // jobs up to this size (stream segments, small buffers) take short prev items
 constexpr uint64_t ZD_S1S_HOST = 8192, ZD_S2S_HOST = 2048, ZD_SMALL_JOB_HOST = 4ull << 20;
+// search items of zs_zd_msearch_kernel (the default); ZS_ZD_MATCH=all selects
+// zs_zd_match_kernel (every position, both budgets: the round-2 search)
+constexpr uint64_t ZD_S3_HOST = 16384;
+static bool zd_allpos() {
+  const char *e = getenv("ZS_ZD_MATCH");
+  return e && !strcmp(e, "all");
+}
 constexpr uint32_t ZD_STATE_A_HOST = 2u << 1;  // deflate_slow state A (deflate_zlib.hip ZD_STATE_A)
 struct ZdWorkspace {
   size_t cap_pos = 0, cap_bm = 0, cap_w1 = 0, cap_w1s = 0, cap_w2 = 0, cap_blk = 0;
@@ -1462,6 +1469,7 @@ struct ZdPlan {
   std::vector<ZdHist> hist;
   size_t pos = 0, bmw = 0;
   uint32_t nex = 0, nslow = 0, nfast = 0, max_regions = 0;  // max_regions: over the deflate_slow jobs
+  bool allpos = false;
 } g_zdp;
 
 // before the jobs are uploaded: position arrays, bitmaps, block slots of the
@@ -1469,6 +1477,7 @@ struct ZdPlan {
 void zd_plan(uint32_t nv) {
   ZdPlan &P = g_zdp;
   P = ZdPlan();
+  P.allpos = zd_allpos();
   for (uint32_t k = 0; k < nv; k++) {
     ZsDJobDev &jd = g_dz.h_jobs[k];
     if (!jd.exact) continue;
@@ -1477,7 +1486,7 @@ void zd_plan(uint32_t nv) {
     jd.pos0 = P.pos;
     P.pos += (L + 64) & ~uint64_t(63);
     jd.bm0 = P.bmw;
-    P.bmw += 4 * zd_bm_words(L) + 4;  // S, V, M, I
+    P.bmw += 6 * zd_bm_words(L) + 4;  // S, V, M, I, A, B
     if (jd.exact == ZD_FAST) {  // deflate_fast searches inside its own kernel
       P.nfast++;
     } else {
@@ -1488,7 +1497,7 @@ void zd_plan(uint32_t nv) {
         for (uint64_t a = 0; a < L; a += ZD_S1S_HOST) P.w1s.push_back({k, (uint32_t)std::min<uint64_t>(ZD_S1S_HOST, L - a), a});
       else
         for (uint64_t a = 0; a < L; a += ZD_S1_HOST) P.w1.push_back({k, (uint32_t)std::min<uint64_t>(ZD_S1_HOST, L - a), a});
-      const uint64_t s2 = small ? ZD_S2S_HOST : ZD_S2_HOST;  // shorter match items: the job's latency
+      const uint64_t s2 = !P.allpos ? ZD_S3_HOST : small ? ZD_S2S_HOST : ZD_S2_HOST;  // shorter match items: the job's latency
       for (uint64_t a = 0; a < L; a += s2) P.w2.push_back({k, (uint32_t)std::min<uint64_t>(s2, L - a), a});
     }
     jd.zblk0 = (uint32_t)P.slot_job.size();
@@ -1556,7 +1565,7 @@ int zd_run(uint32_t nv, size_t nseg, hipStream_t st) {
                          (uint32_t)w1s.size(), g_zd.d_w2,
                          (uint32_t)w2.size(), g_zd.d_prevd, g_zd.d_ma, g_zd.d_mb, g_zd.d_bm, g_zd.d_blks,
                          (uint32_t)slot_job.size(), g_zd.d_slot_job, g_zd.d_aux, g_dz.d_stage, g_zd.d_flag, P.nslow != 0,
-                         P.nfast != 0, P.max_regions, st, ev)) {
+                         P.nfast != 0, P.max_regions, P.allpos ? 1 : 0, st, ev)) {
     set_err("zlib-identical deflate: fix-up round failed");
     return ZS_ENODEV;
   }
