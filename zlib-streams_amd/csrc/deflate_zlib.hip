@@ -401,11 +401,27 @@ __global__ void __launch_bounds__(ZD_MT) zs_zd_match_kernel(const ZsDJobDev *__r
 // bitmap.  Searches the walks did not make (a parse path entering an item from
 // the previous one, until it meets a walked path) run on demand in the parse
 // (zd_lookup).  Probe: 0.41 (Zipf) / 0.49 (lines) searches per byte, 8.9 /
-// 20.8 candidates, lanes busy 42 / 59% of the workgroup's time.
+// 20.8 candidates; with one start per lane a workgroup lasts as long as its
+// longest walk (~1 K chain steps against ~300 on average: lanes busy 25 / 37%
+// of its time).  Measured on 16 x 64 MiB L6 (tools/gpu_msearch.sh): search
+// 118 ms (zs_zd_match_kernel) -> 66 ms; 512 threads 80.7 ms (half the waves
+// to cover the LDS latency of a chain step), a start every 8th position
+// (more starts per lane, 14% more searches) 109 / 85 ms, 8 chain steps per
+// walk update 103 ms.  Measured in the probe and not built: an LDS ring that
+// streams a span through one workgroup (the slowest walk holds the ring: lanes
+// busy 26-47% at 1024 threads), cheap-budget prefixes for the walks that start
+// off the parse kernel's piece grid (fewer searches, the same tail).
 // ---------------------------------------------------------------------------
-#define ZD_S3 16384u                     // positions per workgroup
-#define ZD_MT3 512u                      // threads per workgroup
-#define ZD_PL3 16u                       // a walk starts at every 16th position
+#define ZD_S3 16384u  // positions per workgroup (zs_capi.cpp ZD_S3_HOST)
+#ifndef ZD_MT3
+#define ZD_MT3 1024u  // threads per workgroup (512: 80.7 ms, 1024: 66 ms per 16 x 64 MiB L6)
+#endif
+#ifndef ZD_PL3
+#define ZD_PL3 16u  // a walk starts at every 16th position
+#endif
+#ifndef ZD_MSU
+#define ZD_MSU 16  // chain steps between walk updates
+#endif
 #define ZD_WB3 (ZD_S3 + 32768u + 272u)  // window bytes in LDS
 
 __global__ void __launch_bounds__(ZD_MT3) zs_zd_msearch_kernel(const ZsDJobDev *__restrict__ jobs,
@@ -589,7 +605,7 @@ __global__ void __launch_bounds__(ZD_MT3) zs_zd_msearch_kernel(const ZsDJobDev *
     if (!__ballot(!idle)) break;
     // sixteen chain steps between walk updates (zs_zd_match_kernel's refill rhythm)
 #pragma unroll
-    for (int r = 0; r < 16; r++) cstep();
+    for (int r = 0; r < ZD_MSU; r++) cstep();
   }
   __syncthreads();
   const ZdBm Bm = zd_bm(bm, jb);
