@@ -320,7 +320,7 @@ DEFLATE_STAGES = ("match", "parse", "blocks", "stitch")
 DEFLATE_STAGE_KERNELS = {"match": "zs_dz_match_kernel", "parse": "zs_dz_parse_kernel",
                          "blocks": "zs_dz_block_kernel + zs_dz_check_kernel",
                          "stitch": "zs_dz_offsets_kernel + zs_dz_stitch_kernel + zs_dz_trailer_kernel"}
-ZDEFLATE_STAGE_KERNELS = {"match": "zs_zd_prev_kernel + zs_zd_match_kernel",
+ZDEFLATE_STAGE_KERNELS = {"match": "zs_zd_prev_kernel + zs_zd_msearch_kernel (ZS_ZD_MATCH=all: zs_zd_match_kernel)",
                           "parse": "zs_zd_parse_kernel + zs_zd_fix_kernel rounds",
                           "blocks": "zs_zd_count/blocks/blist/tree/layout/emit kernels",
                           "stitch": "zs_dz_trailer_kernel"}
