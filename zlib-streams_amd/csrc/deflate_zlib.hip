@@ -422,7 +422,10 @@ __global__ void __launch_bounds__(ZD_MT) zs_zd_match_kernel(const ZsDJobDev *__r
 #ifndef ZD_MSU
 #define ZD_MSU 16  // chain steps between walk updates
 #endif
-#define ZD_WB3 (ZD_S3 + 32768u + 272u)  // window bytes in LDS
+#ifndef ZD_XT3
+#define ZD_XT3 512u  // walks go on this far past the item's end (parse paths entering the next item)
+#endif
+#define ZD_WB3 (ZD_S3 + ZD_XT3 + 32768u + 272u)  // window bytes in LDS
 
 __global__ void __launch_bounds__(ZD_MT3) zs_zd_msearch_kernel(const ZsDJobDev *__restrict__ jobs,
                                                                 const ZsZWorkDev *__restrict__ work,
@@ -430,8 +433,8 @@ __global__ void __launch_bounds__(ZD_MT3) zs_zd_msearch_kernel(const ZsDJobDev *
                                                                 uint32_t *__restrict__ ma, uint32_t *__restrict__ mb,
                                                                 uint32_t *__restrict__ bm) {
   __shared__ __attribute__((aligned(16))) uint32_t s_w[ZD_WB3 / 4 + 4];
-  __shared__ __attribute__((aligned(16))) uint16_t s_pd[ZD_S3 + 32768u];
-  __shared__ uint32_t s_claim[ZD_S3 / 32], s_sa[ZD_S3 / 32], s_sb[ZD_S3 / 32];
+  __shared__ __attribute__((aligned(16))) uint16_t s_pd[ZD_S3 + ZD_XT3 + 32768u];
+  __shared__ uint32_t s_claim[(ZD_S3 + ZD_XT3) / 32], s_sa[(ZD_S3 + ZD_XT3) / 32], s_sb[(ZD_S3 + ZD_XT3) / 32];
   __shared__ uint32_t s_next;
   const uint32_t t = threadIdx.x;
   const ZsZWorkDev wk = work[blockIdx.x];
@@ -439,18 +442,42 @@ __global__ void __launch_bounds__(ZD_MT3) zs_zd_msearch_kernel(const ZsDJobDev *
   const uint64_t L = jb.in_len, s = wk.start;
   const uint32_t len = wk.len;
   if (jb.pstart >= s + len) return;  // history only: the parse never searches here
+  // walks continue ZD_XT3 positions into the next item, with starts there as
+  // well: the paths the parse kernel's pieces and the region fix-ups follow
+  // across the item's end are searched here until they meet one of those
+  // starts' paths (= the next item's own walks).  Measured on 16 x 64 MiB L6:
+  // without the extension the parse made on-demand searches (parse 10.8 ->
+  // 16.5 ms); with it but no starts in it, a path crossing the end was one
+  // lane's serial 512-position walk, the workgroup's new tail (search 66 ->
+  // 167 ms); with both: search 66 ms, parse 10.85 ms, 9 915 MiB/s.
+  const uint32_t lenx = (uint32_t)min<uint64_t>(len + ZD_XT3, L - s);
   const int64_t B = (int64_t)s - 32768;  // LDS index of position q: q - B
   {
     uint8_t *wb = reinterpret_cast<uint8_t *>(s_w);
     const uint64_t lo = B < 0 ? 0u : (uint64_t)B;
-    const uint64_t hi_b = s + len + 272u;
+    const uint64_t hi_b = s + lenx + 272u;
     for (uint32_t i = t; i < ZD_WB3 / 4 + 4; i += ZD_MT3) s_w[i] = 0;
-    for (uint32_t i = t; i < ZD_S3 / 32; i += ZD_MT3) s_claim[i] = s_sa[i] = s_sb[i] = 0;
+    for (uint32_t i = t; i < (ZD_S3 + ZD_XT3) / 32; i += ZD_MT3) s_claim[i] = s_sa[i] = s_sb[i] = 0;
     if (t == 0) s_next = 0;
     __syncthreads();
-    for (uint64_t q = lo + t; q < hi_b && q < L; q += ZD_MT3) wb[q - B] = jb.in[q];
+    // 16-byte loads (lo and its LDS index are multiples of 16; the job's link
+    // array starts 64-position aligned); byte loads for an unaligned input
+    const uint64_t hb = min(hi_b, L);
+    uint64_t q16 = lo;
+    if ((reinterpret_cast<uintptr_t>(jb.in) & 15u) == 0) {
+      const uint64_t nq = (hb - lo) / 16u;
+      const uint4 *src = reinterpret_cast<const uint4 *>(jb.in + lo);
+      uint4 *dst = reinterpret_cast<uint4 *>(wb + (lo - B));
+      for (uint64_t i = t; i < nq; i += ZD_MT3) dst[i] = src[i];
+      q16 = lo + nq * 16u;
+    }
+    for (uint64_t q = q16 + t; q < hb; q += ZD_MT3) wb[q - B] = jb.in[q];
     const uint16_t *pd = prevd + jb.pos0;
-    for (uint64_t q = lo + t; q < s + len; q += ZD_MT3) s_pd[q - B] = pd[q];
+    const uint64_t he = s + lenx, nl = (he - lo) / 8u;
+    const uint4 *ps = reinterpret_cast<const uint4 *>(pd + lo);
+    uint4 *pdst = reinterpret_cast<uint4 *>(s_pd + (lo - B));
+    for (uint64_t i = t; i < nl; i += ZD_MT3) pdst[i] = ps[i];
+    for (uint64_t q = lo + nl * 8u + t; q < he; q += ZD_MT3) s_pd[q - B] = pd[q];
   }
   __syncthreads();
   const uint32_t level = (uint32_t)jb.level;
@@ -461,7 +488,7 @@ __global__ void __launch_bounds__(ZD_MT3) zs_zd_msearch_kernel(const ZsDJobDev *
   // position after it
   const bool ent = jb.pstart >= s;
   const uint32_t k0 = ent ? (uint32_t)((jb.pstart - s) / ZD_PL3) + 1u : 0u;
-  const uint32_t npl = (len + ZD_PL3 - 1u) / ZD_PL3;
+  const uint32_t npl = (lenx + ZD_PL3 - 1u) / ZD_PL3;  // (starts in the extension too: a crossing path meets one within ~64 positions)
   const uint32_t nst = (ent ? 1u : 0u) + (npl > k0 ? npl - k0 : 0u);
   // walk: loop top iq (item offset) in state st; search: at iq, budget svar
   uint32_t iq = 0, st = 0, svar = 0;
@@ -568,7 +595,7 @@ __global__ void __launch_bounds__(ZD_MT3) zs_zd_msearch_kernel(const ZsDJobDev *
           }
           walking = true;
         }
-        if (iq >= len) {  // the item's exit: the next item's walks go on from there
+        if (iq >= lenx) {  // ZD_XT3 past the item's end: the next item's walks cover what follows
           walking = false;
           continue;
         }
@@ -609,9 +636,16 @@ __global__ void __launch_bounds__(ZD_MT3) zs_zd_msearch_kernel(const ZsDJobDev *
   }
   __syncthreads();
   const ZdBm Bm = zd_bm(bm, jb);
-  for (uint32_t i = t; i < (len + 31u) / 32u; i += ZD_MT3) {
-    Bm.A[s / 32u + i] = s_sa[i];
-    Bm.B[s / 32u + i] = s_sb[i];
+  // words the previous item's walks may also set ([0, ZD_XT3)) and the ones
+  // past this item's end are OR-ed in; the rest belong to this item alone
+  for (uint32_t i = t; i < (lenx + 31u) / 32u; i += ZD_MT3) {
+    if (i < ZD_XT3 / 32u || i >= len / 32u) {
+      if (s_sa[i]) atomicOr(&Bm.A[s / 32u + i], s_sa[i]);
+      if (s_sb[i]) atomicOr(&Bm.B[s / 32u + i], s_sb[i]);
+    } else {
+      Bm.A[s / 32u + i] = s_sa[i];
+      Bm.B[s / 32u + i] = s_sb[i];
+    }
   }
 }
 
