@@ -103,9 +103,11 @@ __device__ __forceinline__ ZdBm zd_bm(uint32_t *bm, const ZsDJobDev &jb) {
 // it (four short phases between barriers).  Occupancy: 2 work items (8 waves)
 // per CU instead of 2 waves.
 #define ZD_PT1 256u
+#define ZD_HB (ZD_PT1 * 16u)  // positions whose hashes are computed together
 __global__ void __launch_bounds__(ZD_PT1) zs_zd_prev_kernel(const ZsDJobDev *__restrict__ jobs,
                                                              const ZsZWorkDev *__restrict__ work, uint16_t *__restrict__ prevd) {
   __shared__ uint16_t head[32768];
+  __shared__ __attribute__((aligned(16))) uint16_t s_h[ZD_HB];
   const uint32_t t = threadIdx.x, lane = t & (WAVE - 1), wv = t / WAVE;
   const ZsZWorkDev wk = work[blockIdx.x];
   const ZsDJobDev jb = jobs[wk.job];
@@ -138,15 +140,51 @@ __global__ void __launch_bounds__(ZD_PT1) zs_zd_prev_kernel(const ZsDJobDev *__r
   __syncthreads();
   uint16_t *po = prevd + jb.pos0;
   static_assert(ZD_SWEEP % ZD_PT1 == 0, "sweeps fall on step boundaries");
+  static_assert(ZD_SWEEP % ZD_HB == 0, "hash blocks fall on sweep boundaries");
   for (uint64_t base = from; base < to; base += ZD_PT1) {
-    if (base != from && ((base - from) % ZD_SWEEP) == 0) {
-      sweep(base);
+    if (((base - from) % ZD_HB) == 0) {
+      // the next ZD_HB positions' hashes into LDS, 16 per thread from 20 input
+      // bytes (one batch of loads per 16 steps instead of three byte loads in
+      // every step, each waiting on memory)
+      __syncthreads();
+      const uint64_t q0 = base + (uint64_t)t * 16u;
+      uint8_t b[20];
+      const uintptr_t a = reinterpret_cast<uintptr_t>(in + q0);
+      if (q0 + 24u <= L && q0 >= 4u) {  // six aligned words cover the 20 bytes
+        const uint32_t *w = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
+        const uint32_t sh = (uint32_t)(a & 3u);
+        uint32_t x[6];
+#pragma unroll
+        for (int k = 0; k < 6; k++) x[k] = w[k];
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+          const uint32_t v = __builtin_amdgcn_alignbyte(x[k + 1], x[k], sh);
+          b[4 * k] = (uint8_t)v;
+          b[4 * k + 1] = (uint8_t)(v >> 8);
+          b[4 * k + 2] = (uint8_t)(v >> 16);
+          b[4 * k + 3] = (uint8_t)(v >> 24);
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 20; k++) b[k] = q0 + k < L ? in[q0 + k] : 0;
+      }
+      uint32_t hv[8];
+#pragma unroll
+      for (int k = 0; k < 16; k += 2) {
+        const uint32_t h0 = (((uint32_t)b[k] << 10) ^ ((uint32_t)b[k + 1] << 5) ^ b[k + 2]) & 0x7fffu;
+        const uint32_t h1 = (((uint32_t)b[k + 1] << 10) ^ ((uint32_t)b[k + 2] << 5) ^ b[k + 3]) & 0x7fffu;
+        hv[k / 2] = h0 | (h1 << 16);
+      }
+      uint4 *hd = reinterpret_cast<uint4 *>(s_h + t * 16u);
+      hd[0] = make_uint4(hv[0], hv[1], hv[2], hv[3]);
+      hd[1] = make_uint4(hv[4], hv[5], hv[6], hv[7]);
+      if (base != from && ((base - from) % ZD_SWEEP) == 0) sweep(base);
       __syncthreads();
     }
     const uint64_t p = base + (uint64_t)wv * WAVE + lane;
     const bool valid = p + 2 < L && p < to;
     uint32_t h = 0;
-    if (valid) h = (((uint32_t)in[p] << 10) ^ ((uint32_t)in[p + 1] << 5) ^ in[p + 2]) & 0x7fffu;
+    if (valid) h = s_h[(uint32_t)((base - from) % ZD_HB) + wv * WAVE + lane];
     // lanes of this wave with the same hash: 15 ballots
     uint64_t m = __ballot(valid);
 #pragma unroll
