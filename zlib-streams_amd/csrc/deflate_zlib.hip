@@ -54,7 +54,10 @@
 #define ZD_S2 8192u                       // zs_zd_match_kernel positions per workgroup
 #define ZD_MT 1024u
 #define ZD_REG 65536u                     // parse region (one ZsDSegDev segment)
-#define ZD_PT 256u                        // parse threads per region = pieces of 256 positions
+#ifndef ZD_PT
+#define ZD_PT 256u  // parse threads per region
+#endif
+#define ZD_PIECE (ZD_REG / ZD_PT)  // positions per parse piece (a multiple of zs_zd_msearch_kernel's start spacing)
 #define ZD_AUX 352u                       // per-block table words: 286 lit/len + 30 dist + 19 bit-length (+ pad)
 
 // zlib deflate.c configuration_table rows (good, lazy, nice, chain), levels 4..9
@@ -460,6 +463,12 @@ __global__ void __launch_bounds__(ZD_MT) zs_zd_match_kernel(const ZsDJobDev *__r
 #ifndef ZD_MSU
 #define ZD_MSU 16  // chain steps between walk updates
 #endif
+#ifndef ZD_MS_STEP
+#define ZD_MS_STEP 1  // 2: fixed-sequence chain step (one compare block per step)
+#endif
+#ifndef ZD_MS_PROF
+#define ZD_MS_PROF 0  // per-workgroup timeline printed for a few items (tools/build_variant.sh ... -DZD_MS_PROF=1)
+#endif
 #ifndef ZD_XT3
 #define ZD_XT3 512u  // walks go on this far past the item's end (parse paths entering the next item)
 #endif
@@ -474,6 +483,11 @@ __global__ void __launch_bounds__(ZD_MT3) zs_zd_msearch_kernel(const ZsDJobDev *
   __shared__ __attribute__((aligned(16))) uint16_t s_pd[ZD_S3 + ZD_XT3 + 32768u];
   __shared__ uint32_t s_claim[(ZD_S3 + ZD_XT3) / 32], s_sa[(ZD_S3 + ZD_XT3) / 32], s_sb[(ZD_S3 + ZD_XT3) / 32];
   __shared__ uint32_t s_next;
+#if ZD_MS_PROF
+  __shared__ uint32_t pf_iters, pf_lanes, pf_titers, pf_tlanes, pf_tail_at, pf_end, pf_stage;
+  const uint64_t pf_t0 = clock64();
+  if (threadIdx.x == 0) pf_iters = pf_lanes = pf_titers = pf_tlanes = pf_tail_at = pf_end = pf_stage = 0;
+#endif
   const uint32_t t = threadIdx.x;
   const ZsZWorkDev wk = work[blockIdx.x];
   const ZsDJobDev jb = jobs[wk.job];
@@ -518,6 +532,9 @@ __global__ void __launch_bounds__(ZD_MT3) zs_zd_msearch_kernel(const ZsDJobDev *
     for (uint64_t q = lo + nl * 8u + t; q < he; q += ZD_MT3) s_pd[q - B] = pd[q];
   }
   __syncthreads();
+#if ZD_MS_PROF
+  if (t == 0) pf_stage = (uint32_t)(clock64() - pf_t0);
+#endif
   const uint32_t level = (uint32_t)jb.level;
   const uint32_t good = zd_cfg[level][0], lazy = zd_cfg[level][1], nice = zd_cfg[level][2], chain = zd_cfg[level][3];
   const uint32_t max_dist = zd_max_dist(jb);
@@ -530,8 +547,8 @@ __global__ void __launch_bounds__(ZD_MT3) zs_zd_msearch_kernel(const ZsDJobDev *
   const uint32_t nst = (ent ? 1u : 0u) + (npl > k0 ? npl - k0 : 0u);
   // walk: loop top iq (item offset) in state st; search: at iq, budget svar
   uint32_t iq = 0, st = 0, svar = 0;
-  bool walking = false, idle = false, srch = false, have = false;
-  uint32_t c = 0, k = 0, best = 0, bdist = 0, cap = 0, nicep = 0, ow = 0, pi = 0, clim = 0;
+  bool walking = false, idle = false, srch = false, have = false, cmpm = false;
+  uint32_t c = 0, k = 0, best = 0, bdist = 0, cap = 0, nicep = 0, ow = 0, pi = 0, clim = 0, cn_off = 0;
   auto cmp_len = [&](uint32_t a0) -> uint32_t {  // as zs_zd_match_kernel
     uint32_t n = 0;
     for (;;) {
@@ -562,6 +579,61 @@ __global__ void __launch_bounds__(ZD_MT3) zs_zd_msearch_kernel(const ZsDJobDev *
     return min(n, cap);
   };
   // one chain step of a searching lane (zs_zd_match_kernel's step, one budget)
+#if ZD_MS_STEP == 2
+  // A chain step as a fixed instruction sequence: the scan-end filter for lanes
+  // starting on a candidate, then ONE 16-byte compare block for every lane
+  // comparing (a long common prefix takes a block per step instead of a
+  // divergent loop), then the candidate's result and the chain advance.  Same
+  // candidates, same results as the loop form.
+  auto cstep = [&]() {
+    const uint32_t cc = srch ? c : 0u;
+    const uint32_t nd = s_pd[cc];
+    const bool fl = srch && !cmpm;  // a fresh candidate: the filter
+    const uint32_t se = zd_lw(s_w, cc + (best >= 3 ? best - 3 : 0u));
+    const bool pass = fl && (best < 3 || se == ow);
+    cn_off = pass ? 0u : cn_off;
+    cmpm = cmpm || pass;
+    bool fin = fl && !pass;  // rejected by the filter: the candidate is done
+    if (__ballot(srch && cmpm)) {
+      const bool on = srch && cmpm;
+      const uint32_t a = (on ? c : 0u) + cn_off, b = (on ? pi : 0u) + cn_off;
+      const uint32_t wa = a >> 2, wb = b >> 2, sa = a & 3u, sb = b & 3u;
+      uint32_t ua[5], ub[5];
+#pragma unroll
+      for (int q = 0; q < 5; q++) {
+        ua[q] = s_w[wa + q];
+        ub[q] = s_w[wb + q];
+      }
+      uint32_t x = 0, g = 4;
+#pragma unroll
+      for (int q = 3; q >= 0; q--) {
+        const uint32_t d = __builtin_amdgcn_alignbyte(ua[q + 1], ua[q], sa) ^ __builtin_amdgcn_alignbyte(ub[q + 1], ub[q], sb);
+        g = d ? (uint32_t)q : g;
+        x = d ? d : x;
+      }
+      const uint32_t m16 = g < 4 ? 4u * g + ((uint32_t)__builtin_ctz(x) >> 3) : 16u;
+      const uint32_t nn = cn_off + m16;
+      const bool done = on && (m16 < 16u || nn >= cap);
+      cn_off = on ? nn : cn_off;
+      if (done) {
+        const uint32_t n = min(nn, cap);
+        if (n > best) {
+          best = n;
+          bdist = pi - c;
+          if (best >= 3) ow = zd_lw(s_w, pi + best - 3);
+        }
+      }
+      cmpm = cmpm && !done;
+      fin = fin || done;
+    }
+    k += fin ? 1u : 0u;
+    const uint32_t cn = c - nd;
+    const bool stop = fin && (best >= nicep || k >= clim || nd == 0 || (pi - cn) >= max_dist);
+    c = fin && !stop ? cn : c;
+    have = have || stop;
+    srch = srch && !stop;
+  };
+#else
   auto cstep = [&]() {
     const uint32_t cc = srch ? c : 0u;
     const uint32_t nd = s_pd[cc];
@@ -581,6 +653,7 @@ __global__ void __launch_bounds__(ZD_MT3) zs_zd_msearch_kernel(const ZsDJobDev *
     have = have || stop;
     srch = srch && !stop;
   };
+#endif
   // deflate_slow's iteration at iq with match m (zd_step)
   auto advance = [&](uint32_t m) {
     const uint32_t pl = (st >> 1) & 511u;
@@ -664,15 +737,39 @@ __global__ void __launch_bounds__(ZD_MT3) zs_zd_msearch_kernel(const ZsDJobDev *
         nicep = look < nice ? (uint32_t)look : nice;
         c = pi - d0;
         srch = true;
+        cmpm = false;
         break;
       }
     }
     if (!__ballot(!idle)) break;
+#if ZD_MS_PROF
+    {
+      const uint64_t am = __ballot(srch);
+      if ((t & 63u) == 0) {
+        atomicAdd(&pf_iters, 1u);
+        atomicAdd(&pf_lanes, (uint32_t)__builtin_popcountll(am));
+        if (s_next >= nst && pf_tail_at == 0) atomicMax(&pf_tail_at, (uint32_t)(clock64() - pf_t0));
+        if (s_next >= nst) {
+          atomicAdd(&pf_titers, 1u);
+          atomicAdd(&pf_tlanes, (uint32_t)__builtin_popcountll(am));
+        }
+      }
+    }
+#endif
     // sixteen chain steps between walk updates (zs_zd_match_kernel's refill rhythm)
 #pragma unroll
     for (int r = 0; r < ZD_MSU; r++) cstep();
   }
+#if ZD_MS_PROF
+  if ((t & 63u) == 0) atomicMax(&pf_end, (uint32_t)(clock64() - pf_t0));
+#endif
   __syncthreads();
+#if ZD_MS_PROF
+  if (t == 0 && (blockIdx.x % 512u) == 7u)
+    printf("msprof blk %u len %u nst %u: stage %u cyc, walks %u cyc (tail from %u), wave-iters %u (tail %u), active lanes/iter %.1f (tail %.1f)\n",
+           blockIdx.x, len, nst, pf_stage, pf_end, pf_tail_at, pf_iters, pf_titers, (double)pf_lanes / max(pf_iters, 1u),
+           (double)pf_tlanes / max(pf_titers, 1u));
+#endif
   const ZdBm Bm = zd_bm(bm, jb);
   // words the previous item's walks may also set ([0, ZD_XT3)) and the ones
   // past this item's end are OR-ed in; the rest belong to this item alone
@@ -843,12 +940,12 @@ __global__ void __launch_bounds__(ZD_PT) zs_zd_parse_kernel(const ZsDJobDev *__r
   if (jb.exact != ZD_SLOW) return;
   const ZdTabs T = zd_tabs(jb, ma, mb, prevd, bm);
   const uint64_t r0 = sg.start, rend = sg.start + sg.len;
-  const uint64_t a = r0 + (uint64_t)t * 256u, b = min(rend, a + 256u);
+  const uint64_t a = r0 + (uint64_t)t * ZD_PIECE, b = min(rend, a + ZD_PIECE);
   // the job's parse entry (pstart, pstate) lies in its first region (the
   // history before it is at most one window); pieces before it hold no tokens
   // and the piece holding it starts there, in that state
   const bool has_ent = r0 == 0 && jb.pstart < rend;
-  const uint32_t ent_t = has_ent ? (uint32_t)(jb.pstart / 256u) : 0u;
+  const uint32_t ent_t = has_ent ? (uint32_t)(jb.pstart / ZD_PIECE) : 0u;
   const uint64_t ent_p = has_ent ? jb.pstart : r0;
   const uint32_t ent_s = has_ent ? jb.pstate : ZD_STATE_A;
   const bool act = a < rend && t >= ent_t && (r0 != 0 || jb.pstart < rend);
@@ -893,7 +990,7 @@ __global__ void __launch_bounds__(ZD_PT) zs_zd_parse_kernel(const ZsDJobDev *__r
     if (!__syncthreads_or(changed)) break;
   }
   // final walk from the true entry: token starts, variants, state-A marks
-  for (uint32_t i = t * 8; i < t * 8 + 8; i++) s_M[i] = 0;  // own words (256 positions)
+  for (uint32_t i = t * (ZD_PIECE / 32); i < (t + 1) * (ZD_PIECE / 32); i++) s_M[i] = 0;  // own words
   __syncthreads();
   if (act) {
     uint64_t q = t == ent_t ? ent_p : s_xp[t - 1];
@@ -915,7 +1012,7 @@ __global__ void __launch_bounds__(ZD_PT) zs_zd_parse_kernel(const ZsDJobDev *__r
     Bm.V[w0 + i] = s_V[i];
     Bm.M[w0 + i] = s_M[i];
   }
-  const uint32_t lastp = sg.len ? (uint32_t)((sg.len + 255u) / 256u) - 1u : 0u;
+  const uint32_t lastp = sg.len ? (uint32_t)((sg.len + ZD_PIECE - 1u) / ZD_PIECE) - 1u : 0u;
   if (t == lastp) {
     segs[blockIdx.x].zx0 = s_xp[t];
     segs[blockIdx.x].zs0 = s_xs[t];
