@@ -451,7 +451,13 @@ __global__ void __launch_bounds__(ZD_MT) zs_zd_match_kernel(const ZsDJobDev *__r
 // walk update 103 ms.  Measured in the probe and not built: an LDS ring that
 // streams a span through one workgroup (the slowest walk holds the ring: lanes
 // busy 26-47% at 1024 threads), cheap-budget prefixes for the walks that start
-// off the parse kernel's piece grid (fewer searches, the same tail).
+// off the parse kernel's piece grid (fewer searches, the same tail).  In-kernel
+// timeline (ZD_MS_PROF=1, 16 x 64 MiB L6): every start is handed out within
+// the first ~18% of a workgroup's time, 28 of 64 lanes search per wave-step on
+// average, a chain step costs ~1 250 cycles per wave (issue-bound: ~120
+// instructions, 4 waves per SIMD).  Measured and dropped: the step as a fixed
+// sequence (filter, then one 16-byte compare block per step for every
+// comparing lane, no divergent compare loop): 66 -> 78 ms.
 // ---------------------------------------------------------------------------
 #define ZD_S3 16384u  // positions per workgroup (zs_capi.cpp ZD_S3_HOST)
 #ifndef ZD_MT3
@@ -462,9 +468,6 @@ __global__ void __launch_bounds__(ZD_MT) zs_zd_match_kernel(const ZsDJobDev *__r
 #endif
 #ifndef ZD_MSU
 #define ZD_MSU 16  // chain steps between walk updates
-#endif
-#ifndef ZD_MS_STEP
-#define ZD_MS_STEP 1  // 2: fixed-sequence chain step (one compare block per step)
 #endif
 #ifndef ZD_MS_PROF
 #define ZD_MS_PROF 0  // per-workgroup timeline printed for a few items (tools/build_variant.sh ... -DZD_MS_PROF=1)
@@ -547,8 +550,8 @@ __global__ void __launch_bounds__(ZD_MT3) zs_zd_msearch_kernel(const ZsDJobDev *
   const uint32_t nst = (ent ? 1u : 0u) + (npl > k0 ? npl - k0 : 0u);
   // walk: loop top iq (item offset) in state st; search: at iq, budget svar
   uint32_t iq = 0, st = 0, svar = 0;
-  bool walking = false, idle = false, srch = false, have = false, cmpm = false;
-  uint32_t c = 0, k = 0, best = 0, bdist = 0, cap = 0, nicep = 0, ow = 0, pi = 0, clim = 0, cn_off = 0;
+  bool walking = false, idle = false, srch = false, have = false;
+  uint32_t c = 0, k = 0, best = 0, bdist = 0, cap = 0, nicep = 0, ow = 0, pi = 0, clim = 0;
   auto cmp_len = [&](uint32_t a0) -> uint32_t {  // as zs_zd_match_kernel
     uint32_t n = 0;
     for (;;) {
@@ -579,61 +582,6 @@ __global__ void __launch_bounds__(ZD_MT3) zs_zd_msearch_kernel(const ZsDJobDev *
     return min(n, cap);
   };
   // one chain step of a searching lane (zs_zd_match_kernel's step, one budget)
-#if ZD_MS_STEP == 2
-  // A chain step as a fixed instruction sequence: the scan-end filter for lanes
-  // starting on a candidate, then ONE 16-byte compare block for every lane
-  // comparing (a long common prefix takes a block per step instead of a
-  // divergent loop), then the candidate's result and the chain advance.  Same
-  // candidates, same results as the loop form.
-  auto cstep = [&]() {
-    const uint32_t cc = srch ? c : 0u;
-    const uint32_t nd = s_pd[cc];
-    const bool fl = srch && !cmpm;  // a fresh candidate: the filter
-    const uint32_t se = zd_lw(s_w, cc + (best >= 3 ? best - 3 : 0u));
-    const bool pass = fl && (best < 3 || se == ow);
-    cn_off = pass ? 0u : cn_off;
-    cmpm = cmpm || pass;
-    bool fin = fl && !pass;  // rejected by the filter: the candidate is done
-    if (__ballot(srch && cmpm)) {
-      const bool on = srch && cmpm;
-      const uint32_t a = (on ? c : 0u) + cn_off, b = (on ? pi : 0u) + cn_off;
-      const uint32_t wa = a >> 2, wb = b >> 2, sa = a & 3u, sb = b & 3u;
-      uint32_t ua[5], ub[5];
-#pragma unroll
-      for (int q = 0; q < 5; q++) {
-        ua[q] = s_w[wa + q];
-        ub[q] = s_w[wb + q];
-      }
-      uint32_t x = 0, g = 4;
-#pragma unroll
-      for (int q = 3; q >= 0; q--) {
-        const uint32_t d = __builtin_amdgcn_alignbyte(ua[q + 1], ua[q], sa) ^ __builtin_amdgcn_alignbyte(ub[q + 1], ub[q], sb);
-        g = d ? (uint32_t)q : g;
-        x = d ? d : x;
-      }
-      const uint32_t m16 = g < 4 ? 4u * g + ((uint32_t)__builtin_ctz(x) >> 3) : 16u;
-      const uint32_t nn = cn_off + m16;
-      const bool done = on && (m16 < 16u || nn >= cap);
-      cn_off = on ? nn : cn_off;
-      if (done) {
-        const uint32_t n = min(nn, cap);
-        if (n > best) {
-          best = n;
-          bdist = pi - c;
-          if (best >= 3) ow = zd_lw(s_w, pi + best - 3);
-        }
-      }
-      cmpm = cmpm && !done;
-      fin = fin || done;
-    }
-    k += fin ? 1u : 0u;
-    const uint32_t cn = c - nd;
-    const bool stop = fin && (best >= nicep || k >= clim || nd == 0 || (pi - cn) >= max_dist);
-    c = fin && !stop ? cn : c;
-    have = have || stop;
-    srch = srch && !stop;
-  };
-#else
   auto cstep = [&]() {
     const uint32_t cc = srch ? c : 0u;
     const uint32_t nd = s_pd[cc];
@@ -653,7 +601,6 @@ __global__ void __launch_bounds__(ZD_MT3) zs_zd_msearch_kernel(const ZsDJobDev *
     have = have || stop;
     srch = srch && !stop;
   };
-#endif
   // deflate_slow's iteration at iq with match m (zd_step)
   auto advance = [&](uint32_t m) {
     const uint32_t pl = (st >> 1) & 511u;
@@ -737,7 +684,6 @@ __global__ void __launch_bounds__(ZD_MT3) zs_zd_msearch_kernel(const ZsDJobDev *
         nicep = look < nice ? (uint32_t)look : nice;
         c = pi - d0;
         srch = true;
-        cmpm = false;
         break;
       }
     }
