@@ -2258,17 +2258,16 @@ static int zd_fix_rounds() {
 
 extern "C" int zs_launch_zdeflate(ZsDJobDev *d_jobs, uint32_t njobs, ZsDSegDev *d_segs, uint32_t nseg,
                                   const ZsZWorkDev *d_w1, uint32_t n1, const ZsZWorkDev *d_w1s, uint32_t n1s,
-                                  const ZsZWorkDev *d_w2, uint32_t n2,
+                                  const ZsZWorkDev *d_w2, uint32_t n2, const ZsZWorkDev *d_w3, uint32_t n3,
                                   uint16_t *d_prevd, uint32_t *d_ma, uint32_t *d_mb, uint32_t *d_bm, ZsZBlkDev *d_blks,
                                   uint32_t nblk_slots, const uint32_t *d_slot_job, uint32_t *d_aux, uint8_t *d_stage,
-                                  uint32_t *d_flag, int has_slow, int has_fast, uint32_t max_regions, int allpos,
-                                  hipStream_t st, hipEvent_t *ev) {
+                                  uint32_t *d_flag, int has_slow, int has_fast, uint32_t max_regions, hipStream_t st,
+                                  hipEvent_t *ev) {
   if (ev) (void)hipEventRecord(ev[0], st);
   if (n1) hipLaunchKernelGGL(zs_zd_prev_kernel, dim3(n1), dim3(ZD_PT1), 0, st, d_jobs, d_w1, d_prevd);
   if (n1s) hipLaunchKernelGGL(zs_zd_prev_small_kernel, dim3(n1s), dim3(ZD_PT1), 0, st, d_jobs, d_w1s, d_prevd);
-  if (n2 && allpos) hipLaunchKernelGGL(zs_zd_match_kernel, dim3(n2), dim3(ZD_MT), 0, st, d_jobs, d_w2, d_prevd, d_ma, d_mb, d_bm);
-  if (n2 && !allpos)
-    hipLaunchKernelGGL(zs_zd_msearch_kernel, dim3(n2), dim3(ZD_MT3), 0, st, d_jobs, d_w2, d_prevd, d_ma, d_mb, d_bm);
+  if (n2) hipLaunchKernelGGL(zs_zd_match_kernel, dim3(n2), dim3(ZD_MT), 0, st, d_jobs, d_w2, d_prevd, d_ma, d_mb, d_bm);
+  if (n3) hipLaunchKernelGGL(zs_zd_msearch_kernel, dim3(n3), dim3(ZD_MT3), 0, st, d_jobs, d_w3, d_prevd, d_ma, d_mb, d_bm);
   if (ev) (void)hipEventRecord(ev[1], st);
   if (has_fast) hipLaunchKernelGGL(zs_zd_fast_kernel, dim3(njobs), dim3(WAVE), 0, st, d_jobs, d_bm, d_ma);
   if (has_slow)

@@ -48,11 +48,11 @@ struct ZsZWorkDev {  // must match deflate_zlib.hip
 };
 extern "C" int zs_launch_zdeflate(ZsDJobDev *d_jobs, uint32_t njobs, ZsDSegDev *d_segs, uint32_t nseg,
                                   const ZsZWorkDev *d_w1, uint32_t n1, const ZsZWorkDev *d_w1s, uint32_t n1s,
-                                  const ZsZWorkDev *d_w2, uint32_t n2,
+                                  const ZsZWorkDev *d_w2, uint32_t n2, const ZsZWorkDev *d_w3, uint32_t n3,
                                   uint16_t *d_prevd, uint32_t *d_ma, uint32_t *d_mb, uint32_t *d_bm, ZsZBlkDev *d_blks,
                                   uint32_t nblk_slots, const uint32_t *d_slot_job, uint32_t *d_aux, uint8_t *d_stage,
-                                  uint32_t *d_flag, int has_slow, int has_fast, uint32_t max_regions, int allpos,
-                                  hipStream_t st, hipEvent_t *ev);
+                                  uint32_t *d_flag, int has_slow, int has_fast, uint32_t max_regions, hipStream_t st,
+                                  hipEvent_t *ev);
 extern "C" void zs_launch_dz_trailer(ZsDJobDev *d_jobs, uint32_t njobs, uint8_t *d_stage, hipStream_t st);
 extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, ZsSegDev *d_segs, uint32_t nseg,
                                   ZsCJobDev *d_cjobs, uint32_t ncjobs, ZsChunkDev *d_units, uint32_t nunit_slots,
@@ -1411,10 +1411,10 @@ static bool zd_allpos() {
 }
 constexpr uint32_t ZD_STATE_A_HOST = 2u << 1;  // deflate_slow state A (deflate_zlib.hip ZD_STATE_A)
 struct ZdWorkspace {
-  size_t cap_pos = 0, cap_bm = 0, cap_w1 = 0, cap_w1s = 0, cap_w2 = 0, cap_blk = 0;
+  size_t cap_pos = 0, cap_bm = 0, cap_w1 = 0, cap_w1s = 0, cap_w2 = 0, cap_w3 = 0, cap_blk = 0;
   uint16_t *d_prevd = nullptr;
   uint32_t *d_ma = nullptr, *d_mb = nullptr, *d_bm = nullptr, *d_aux = nullptr, *d_slot_job = nullptr, *d_flag = nullptr;
-  ZsZWorkDev *d_w1 = nullptr, *d_w1s = nullptr, *d_w2 = nullptr;
+  ZsZWorkDev *d_w1 = nullptr, *d_w1s = nullptr, *d_w2 = nullptr, *d_w3 = nullptr;
   ZsZBlkDev *d_blks = nullptr;
   hipEvent_t ev[4] = {};
 };
@@ -1464,7 +1464,7 @@ struct ZdHist {  // a deflate_fast job's insertion bits for its history [0, psta
   size_t nwords;
 };
 struct ZdPlan {
-  std::vector<ZsZWorkDev> w1, w1s, w2;  // w1s: short prev items of small jobs (zs_zd_prev_small_kernel)
+  std::vector<ZsZWorkDev> w1, w1s, w2, w3;  // w1s: short prev items of small jobs (zs_zd_prev_small_kernel); w2 / w3: zs_zd_match_kernel / zs_zd_msearch_kernel items
   std::vector<uint32_t> slot_job;
   std::vector<ZdHist> hist;
   size_t pos = 0, bmw = 0;
@@ -1497,8 +1497,16 @@ void zd_plan(uint32_t nv) {
         for (uint64_t a = 0; a < L; a += ZD_S1S_HOST) P.w1s.push_back({k, (uint32_t)std::min<uint64_t>(ZD_S1S_HOST, L - a), a});
       else
         for (uint64_t a = 0; a < L; a += ZD_S1_HOST) P.w1.push_back({k, (uint32_t)std::min<uint64_t>(ZD_S1_HOST, L - a), a});
-      const uint64_t s2 = !P.allpos ? ZD_S3_HOST : small ? ZD_S2S_HOST : ZD_S2_HOST;  // shorter match items: the job's latency
-      for (uint64_t a = 0; a < L; a += s2) P.w2.push_back({k, (uint32_t)std::min<uint64_t>(s2, L - a), a});
+      // large jobs: the demand-driven search (zs_zd_msearch_kernel); small
+      // jobs (stream segments, where one call's latency is the rate) and
+      // ZS_ZD_MATCH=all: every position in short items (zs_zd_match_kernel),
+      // which spreads a small job over many workgroups
+      if (P.allpos || small) {
+        const uint64_t s2 = small ? ZD_S2S_HOST : ZD_S2_HOST;
+        for (uint64_t a = 0; a < L; a += s2) P.w2.push_back({k, (uint32_t)std::min<uint64_t>(s2, L - a), a});
+      } else {
+        for (uint64_t a = 0; a < L; a += ZD_S3_HOST) P.w3.push_back({k, (uint32_t)std::min<uint64_t>(ZD_S3_HOST, L - a), a});
+      }
     }
     jd.zblk0 = (uint32_t)P.slot_job.size();
     jd.zblk_cap = (uint32_t)((L + ZD_BLOCK_HOST - 1) / ZD_BLOCK_HOST + 1);
@@ -1508,7 +1516,7 @@ void zd_plan(uint32_t nv) {
 
 int zd_run(uint32_t nv, size_t nseg, hipStream_t st) {
   ZdPlan &P = g_zdp;
-  std::vector<ZsZWorkDev> &w1 = P.w1, &w1s = P.w1s, &w2 = P.w2;
+  std::vector<ZsZWorkDev> &w1 = P.w1, &w1s = P.w1s, &w2 = P.w2, &w3 = P.w3;
   std::vector<uint32_t> &slot_job = P.slot_job;
   const size_t pos = P.pos, bmw = P.bmw;
   const uint32_t nex = P.nex;
@@ -1534,7 +1542,7 @@ int zd_run(uint32_t nv, size_t nseg, hipStream_t st) {
   (void)cpos;
   if ((r = grow(&g_zd.d_bm, &g_zd.cap_bm, bmw + 16)) || (r = grow(&g_zd.d_w1, &g_zd.cap_w1, w1.size() + 1)) ||
       (r = grow(&g_zd.d_w1s, &g_zd.cap_w1s, w1s.size() + 1)) ||
-      (r = grow(&g_zd.d_w2, &g_zd.cap_w2, w2.size() + 1)))
+      (r = grow(&g_zd.d_w2, &g_zd.cap_w2, w2.size() + 1)) || (r = grow(&g_zd.d_w3, &g_zd.cap_w3, w3.size() + 1)))
     return r;
   if (slot_job.size() > g_zd.cap_blk) {
     const size_t c = std::max(slot_job.size(), g_zd.cap_blk + g_zd.cap_blk / 4);
@@ -1554,6 +1562,7 @@ int zd_run(uint32_t nv, size_t nseg, hipStream_t st) {
   if (!w1s.empty())
     HIP_OK(hipMemcpyAsync(g_zd.d_w1s, w1s.data(), w1s.size() * sizeof(ZsZWorkDev), hipMemcpyHostToDevice, st));
   if (!w2.empty()) HIP_OK(hipMemcpyAsync(g_zd.d_w2, w2.data(), w2.size() * sizeof(ZsZWorkDev), hipMemcpyHostToDevice, st));
+  if (!w3.empty()) HIP_OK(hipMemcpyAsync(g_zd.d_w3, w3.data(), w3.size() * sizeof(ZsZWorkDev), hipMemcpyHostToDevice, st));
   HIP_OK(hipMemcpyAsync(g_zd.d_slot_job, slot_job.data(), slot_job.size() * sizeof(uint32_t), hipMemcpyHostToDevice, st));
   hipEvent_t *ev = nullptr;
   if (g_ws.prof) {
@@ -1563,9 +1572,9 @@ int zd_run(uint32_t nv, size_t nseg, hipStream_t st) {
   }
   if (zs_launch_zdeflate(g_dz.d_jobs, nv, g_dz.d_segs, (uint32_t)nseg, g_zd.d_w1, (uint32_t)w1.size(), g_zd.d_w1s,
                          (uint32_t)w1s.size(), g_zd.d_w2,
-                         (uint32_t)w2.size(), g_zd.d_prevd, g_zd.d_ma, g_zd.d_mb, g_zd.d_bm, g_zd.d_blks,
+                         (uint32_t)w2.size(), g_zd.d_w3, (uint32_t)w3.size(), g_zd.d_prevd, g_zd.d_ma, g_zd.d_mb, g_zd.d_bm, g_zd.d_blks,
                          (uint32_t)slot_job.size(), g_zd.d_slot_job, g_zd.d_aux, g_dz.d_stage, g_zd.d_flag, P.nslow != 0,
-                         P.nfast != 0, P.max_regions, P.allpos ? 1 : 0, st, ev)) {
+                         P.nfast != 0, P.max_regions, st, ev)) {
     set_err("zlib-identical deflate: fix-up round failed");
     return ZS_ENODEV;
   }
