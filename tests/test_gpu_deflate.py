@@ -162,6 +162,41 @@ def test_deflate_zlib_bytes_levels_1_to_9(zs):
     assert not bad, bad[:8]
 
 
+@pytest.mark.parametrize("mode", ["demand", "none", "all"])
+def test_deflate_slow_search_modes_are_zlibs(zs, monkeypatch, mode):
+    """deflate_slow (levels 4..9) under each search kernel, forced on inputs of
+    every size (ZS_ZD_MATCH): "demand" = zs_zd_msearch_kernel (walks of the
+    parse from every 16th position, searches only where a walk asks; large
+    jobs take it by default), "none" = no search kernel (every longest_match
+    runs on demand in the parse from global memory: zd_search_g, the path a
+    parse takes where the walks did not search), "all" = zs_zd_match_kernel
+    (every position, both budgets).  Byte-identical to host zlib: the
+    patterns and sizes around the 16 Ki search items and their 512-position
+    extension, every level 4..9 (each chain budget, good / lazy / nice), the
+    three wrappers, windowBits below 15 (a shorter MAX_DIST)."""
+    monkeypatch.setenv("ZS_ZD_MATCH", mode)
+    rng = random.Random(23)
+    pats = _patterns(rng)
+    # (every search of "none" is one thread's serial chain walk in global
+    # memory: short inputs, the short-budget levels)
+    sizes = (1, 300, 4000, 16384 + 513) if mode == "none" else \
+        (1, 300, 16383, 16384 + 511, 16384 + 513, 3 * 16384 + 5, 200000)
+    levels = (4, 5, 6) if mode == "none" else range(4, 10)
+    cases = []
+    for name, p in pats.items():
+        for n in sizes:
+            if n <= len(p):
+                for lv in levels:
+                    cases.append((p[:n], rng.choice((-15, 15, 31)), lv))
+    for wb in (-9, -12, 13):
+        cases.append((pats["text"][:20000 if mode == "none" else 100000], wb, 6))
+        cases.append((pats["lines"][:20000 if mode == "none" else 100000], wb, 4 if mode == "none" else 9))
+    got = zs.deflate_batch([c[0] for c in cases], [c[1] for c in cases], [c[2] for c in cases])
+    bad = [(i, len(d), wb, lv) for i, ((d, wb, lv), (comp, info)) in enumerate(zip(cases, got))
+           if comp != zlib_bytes(d, wb, lv) or info["ret"] != 1]
+    assert not bad, bad[:8]
+
+
 def test_deflate_level0_is_zlibs(zs):
     """Level 0: zlib's deflate_stored blocks of 65535 bytes from the stream start,
     across the 64 KiB segment grid (the final block starting one segment early

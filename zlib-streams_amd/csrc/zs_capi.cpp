@@ -1402,12 +1402,18 @@ DzWorkspace g_dz;
 constexpr uint64_t ZD_S1_HOST = 131072, ZD_S2_HOST = 8192, ZD_BLOCK_HOST = 16383, ZD_AUX_HOST = 352;
 // jobs up to this size (stream segments, small buffers) take short prev items
 constexpr uint64_t ZD_S1S_HOST = 8192, ZD_S2S_HOST = 2048, ZD_SMALL_JOB_HOST = 4ull << 20;
-// search items of zs_zd_msearch_kernel (the default); ZS_ZD_MATCH=all selects
-// zs_zd_match_kernel (every position, both budgets: the round-2 search)
+// search items of zs_zd_msearch_kernel.  ZS_ZD_MATCH (read per batch, for
+// tests and A/B): unset = small jobs zs_zd_match_kernel, large ones
+// zs_zd_msearch_kernel; "all" = every job zs_zd_match_kernel (every position,
+// both budgets: the round-2 search); "demand" = every job
+// zs_zd_msearch_kernel; "none" = no search kernel (every search on demand in
+// the parse: zd_search_g, the fallback path)
 constexpr uint64_t ZD_S3_HOST = 16384;
-static bool zd_allpos() {
+enum { ZD_M_AUTO = 0, ZD_M_ALL = 1, ZD_M_DEMAND = 2, ZD_M_NONE = 3 };
+static int zd_match_mode() {
   const char *e = getenv("ZS_ZD_MATCH");
-  return e && !strcmp(e, "all");
+  if (!e) return ZD_M_AUTO;
+  return !strcmp(e, "all") ? ZD_M_ALL : !strcmp(e, "demand") ? ZD_M_DEMAND : !strcmp(e, "none") ? ZD_M_NONE : ZD_M_AUTO;
 }
 constexpr uint32_t ZD_STATE_A_HOST = 2u << 1;  // deflate_slow state A (deflate_zlib.hip ZD_STATE_A)
 struct ZdWorkspace {
@@ -1469,7 +1475,7 @@ struct ZdPlan {
   std::vector<ZdHist> hist;
   size_t pos = 0, bmw = 0;
   uint32_t nex = 0, nslow = 0, nfast = 0, max_regions = 0;  // max_regions: over the deflate_slow jobs
-  bool allpos = false;
+  int mmode = ZD_M_AUTO;
 } g_zdp;
 
 // before the jobs are uploaded: position arrays, bitmaps, block slots of the
@@ -1477,7 +1483,7 @@ struct ZdPlan {
 void zd_plan(uint32_t nv) {
   ZdPlan &P = g_zdp;
   P = ZdPlan();
-  P.allpos = zd_allpos();
+  P.mmode = zd_match_mode();
   for (uint32_t k = 0; k < nv; k++) {
     ZsDJobDev &jd = g_dz.h_jobs[k];
     if (!jd.exact) continue;
@@ -1501,7 +1507,9 @@ void zd_plan(uint32_t nv) {
       // jobs (stream segments, where one call's latency is the rate) and
       // ZS_ZD_MATCH=all: every position in short items (zs_zd_match_kernel),
       // which spreads a small job over many workgroups
-      if (P.allpos || small) {
+      if (P.mmode == ZD_M_NONE) {
+        // no search items: the A / B bitmaps stay 0
+      } else if (P.mmode == ZD_M_ALL || (small && P.mmode != ZD_M_DEMAND)) {
         const uint64_t s2 = small ? ZD_S2S_HOST : ZD_S2_HOST;
         for (uint64_t a = 0; a < L; a += s2) P.w2.push_back({k, (uint32_t)std::min<uint64_t>(s2, L - a), a});
       } else {
