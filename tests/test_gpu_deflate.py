@@ -517,6 +517,29 @@ def test_deflate_stream_calls_are_zlibs(zs, level):
         assert zlib.decompress(out, wb) == data
 
 
+@pytest.mark.parametrize("mode", ["demand", "none"])
+def test_deflate_stream_calls_search_modes_are_zlibs(zs, monkeypatch, mode):
+    """The stream segments' searches under the demand-driven kernel and the
+    on-demand global search (ZS_ZD_MATCH; by default segments take the
+    all-positions kernel): a segment's parse starts at its entry (a loop top
+    past the carried window, in deflate_slow's state there), where the
+    walks start too.  Every call's ret, consumed and produced bytes equal host
+    zlib's, levels 4 and 6, every flush value, raw and gzip."""
+    monkeypatch.setenv("ZS_ZD_MATCH", mode)
+    rng = random.Random(300 + (mode == "none"))
+    for level, wb in ((4, -15), (6, 31)):
+        data = _stream_data(rng, 600_000 if mode == "demand" else 120_000)
+        calls, off = [], 0
+        while off < len(data):
+            n = rng.choice([1, 700, 5000, 33000, 70000])
+            fl = rng.choice([0, 0, 0, 1, 2, 3, 5])
+            calls.append((data[off:off + n], fl))
+            off += n
+        calls += [(b"", 4)] * 2
+        out = _compare_calls(zs, level, wb, calls, 1 << 21)
+        assert zlib.decompress(out, wb) == data
+
+
 def test_deflate_stream_long_no_flush_is_zlibs(zs):
     """A 64 MiB stream fed in 1 MiB Z_NO_FLUSH calls, then Z_FINISH drained in
     64 KiB pieces: every call equals host zlib's (blocks sent as they complete,
