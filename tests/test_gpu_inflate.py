@@ -459,3 +459,25 @@ def test_c2_pair_lane_parse_serial_link_vs_oracle(zs):
     assert st["parse"] == "lane" and st["link"] == "serial", st
     assert st["chunked_jobs"] == 2 and st["fallback_jobs"] == 0, st
     _compare_all_with_oracle(cases, got, 64 << 20, nthreads=2)
+
+
+def test_segmented_link_vs_oracle(zs):
+    """The segmented link (zs_linkseg_kernel: a group of 5..64 streams cuts each
+    chain into segments linked at once as u16 window maps, joined per stream,
+    resolved by the emit) on 24 C5-shape streams of 2 MiB -- 8 segments of ~3
+    members each -- every result field vs the oracle; the same batch through
+    the per-stream serial link for contrast."""
+    cases = []
+    for k in range(24):
+        raw, wb = corpus.c5_stream(k, 2 << 20)
+        c = zlib.compressobj(6, zlib.DEFLATED, wb, 8)
+        cases.append((raw, c.compress(raw) + c.flush(), wb))
+    caps = [2 << 20] * len(cases)
+    got = zs.inflate_batch([c[1] for c in cases], [c[2] for c in cases], caps)
+    st = zs.last_stats()
+    assert st["link"] == "segmented" and st["chunked_jobs"] == 24 and st["fallback_jobs"] == 0, st
+    _compare_all_with_oracle(cases, got, 2 << 20)
+    got2 = zs.inflate_batch([c[1] for c in cases], [c[2] for c in cases], caps, link="serial")
+    assert zs.last_stats()["link"] == "serial"
+    assert [g[0] for g in got2] == [g[0] for g in got] and [g[1] for g in got2] == [g[1] for g in got]
+

@@ -842,19 +842,28 @@ __device__ __forceinline__ uint2 link_take(const ZsLinkInfo &li, uint32_t t, int
   return make_uint2((uint32_t)r, (uint32_t)(r >> 32));
 }
 
+#define LS_SEGS_MAX 8u  // segments per chain at most (segmented link)
 template <uint32_t HN>
 __global__ void __launch_bounds__(LINK_THREADS) zs_link_kernel(const ZsJobDev *__restrict__ jobs, ZsCJobDev *__restrict__ cjobs,
                                                                const uint16_t *__restrict__ scratch, uint8_t *__restrict__ windows,
-                                                               const ZsLinkInfo *__restrict__ info, uint32_t *__restrict__ fallback) {
+                                                               const ZsLinkInfo *__restrict__ info, uint32_t *__restrict__ fallback,
+                                                               uint32_t nseg_per = 1, const uint16_t *__restrict__ sstart = nullptr,
+                                                               const ZsChunkDev *__restrict__ chunks = nullptr) {
   constexpr int LINK_G = HN / LINK_THREADS / 4;
   constexpr uint32_t MB = HN == 65536u ? 0u : MARK_BASE;  // marker of history byte w: MB + w (deflate64: w)
   __shared__ uint8_t s_win[2][HN];
   __shared__ uint32_t s_bad;
   const uint32_t t = threadIdx.x;
-  const ZsCJobDev cj = cjobs[blockIdx.x];
+  // segments (pass 2 of the segmented link): workgroup (chain b, segment k)
+  // links members [m0, m1) from the segment's start window (zs_linkseg_join_kernel)
+  const uint32_t b = blockIdx.x / nseg_per, k = blockIdx.x % nseg_per;
+  const ZsCJobDev cj = cjobs[b];
   if (!cj.ok) return;
-  const uint32_t u0 = cj.unit0;
-  const uint32_t len = cj.nchain;
+  const uint32_t m0 = (uint32_t)((uint64_t)k * cj.nchain / nseg_per);
+  const uint32_t m1 = (uint32_t)((uint64_t)(k + 1) * cj.nchain / nseg_per);
+  if (m0 >= m1) return;
+  const uint32_t u0 = cj.unit0 + m0;
+  const uint32_t len = m1 - m0;
 #if KP_ON
   const uint64_t kt0 = KP_NOW();
   uint64_t kt_ww = 0, kt_res = 0, kt_bar = 0;
@@ -866,8 +875,13 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_link_kernel(const ZsJobDev *_
   const ZsJobDev jb = jobs[cj.job];
   const bool cont = (jb.flags & ZS_JF_CONT) != 0;
   uint32_t wv = cont ? min(jb.hist, HN) : 0u;  // valid bytes of history
-  if (cont)
+  if (k > 0) {  // a later segment: its start window, valid as far as output precedes it
+    const uint16_t *S = sstart + ((size_t)cj.job * LS_SEGS_MAX + (k - 1u)) * HN;
+    wv = (uint32_t)min<uint64_t>(HN, chunks[info[u0].unit].out_off + (cont ? jb.hist : 0u));
+    for (uint32_t i = t; i < HN; i += LINK_THREADS) s_win[0][i] = (uint8_t)S[i];
+  } else if (cont) {
     for (uint32_t i = HN - wv + t; i < HN; i += LINK_THREADS) s_win[0][i] = jb.out[(int64_t)i - (int64_t)HN];
+  }
   __syncthreads();
   int cur = 0;
   uint2 la[LINK_G], ha[LINK_G], lb[LINK_G], hb[LINK_G];
@@ -974,7 +988,119 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_link_kernel(const ZsJobDev *_
 #endif
   if (t == 0 && s_bad) {  // a marker reached before the stream start: the serial decoder reports it
     fallback[cj.job] = 1;
-    cjobs[blockIdx.x].ok = 0;
+    cjobs[b].ok = 0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Segmented link (5..64 streams; zs_link_kernel alone links one chain per
+// workgroup, a serial chain of ~3.5 us steps per member while most CUs idle):
+// each chain is cut into S segments.  Pass 1 (zs_linkseg_kernel) links every
+// segment at once from an unknown start window, as MAPS: u16 windows whose
+// entries are a byte or MARK_BASE + w, "byte w of the segment's start window"
+// (segment 0 starts from the stream's real history, so its map is bytes); only
+// the map after a segment's last member is kept (M_end[k]).
+// zs_linkseg_join_kernel resolves the segments' start windows in order (S - 1
+// map applications per stream).  Pass 2 (zs_link_kernel with segments) links
+// every segment again from its real start window, writing the members' byte
+// windows as the serial link does, and the emit is unchanged.  Bytes before
+// the stream start stay unresolved (0), as in zs_link_kernel: the emit's
+// `lowest` check reports any marker into them.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(LINK_THREADS) zs_linkseg_kernel(const ZsJobDev *__restrict__ jobs,
+                                                                  const ZsCJobDev *__restrict__ cjobs, uint32_t nseg_per,
+                                                                  const uint16_t *__restrict__ scratch,
+                                                                  uint16_t *__restrict__ mend,
+                                                                  const ZsLinkInfo *__restrict__ info) {
+  constexpr uint32_t HN = HIST;
+  constexpr int LINK_G = HN / LINK_THREADS / 4;
+  __shared__ __attribute__((aligned(16))) uint16_t s_map[2][HN];
+  const uint32_t t = threadIdx.x;
+  const uint32_t b = blockIdx.x / nseg_per, k = blockIdx.x % nseg_per;
+  const ZsCJobDev cj = cjobs[b];
+  if (!cj.ok) return;
+  const uint32_t u0 = cj.unit0, len = cj.nchain;
+  const uint32_t m0 = (uint32_t)((uint64_t)k * len / nseg_per), m1 = (uint32_t)((uint64_t)(k + 1) * len / nseg_per);
+  const ZsJobDev jb = jobs[cj.job];
+  // start map: segment 0 the stream's history (a later piece's earlier output),
+  // else the identity (entry i = byte i of the start window)
+  if (k == 0) {
+    const bool cont = (jb.flags & ZS_JF_CONT) != 0;
+    const uint32_t wv = cont ? min(jb.hist, HN) : 0u;
+    for (uint32_t i = t; i < HN; i += LINK_THREADS)
+      s_map[0][i] = i >= HN - wv ? (uint16_t)jb.out[(int64_t)i - (int64_t)HN] : (uint16_t)0;
+  } else {
+    for (uint32_t i = t; i < HN; i += LINK_THREADS) s_map[0][i] = (uint16_t)(MARK_BASE + i);
+  }
+  __syncthreads();
+  int cur = 0;
+  uint2 la[LINK_G], ha[LINK_G], lb[LINK_G], hb[LINK_G];
+  if (m0 < m1) link_load<HN>(scratch, info[u0 + m0], t, la, ha);
+  auto step = [&](uint32_t j, const uint2 (&vl)[LINK_G], const uint2 (&vh)[LINK_G], uint2 (&nl)[LINK_G],
+                  uint2 (&nh)[LINK_G]) {
+    const ZsLinkInfo li = info[u0 + j];
+    link_load<HN>(scratch, info[u0 + min(j + 1, m1 - 1)], t, nl, nh);
+    __builtin_amdgcn_sched_barrier(0);
+    const uint16_t *W = s_map[cur];
+    uint16_t *W2 = s_map[cur ^ 1];
+    const uint32_t n = li.n_out;
+    const uint32_t keep = n < HN ? HN - n : 0u;
+#pragma unroll
+    for (int g = 0; g < LINK_G; g++) {
+      const uint2 v = link_take<HN>(li, t, g, vl[g], vh[g]);
+      const uint32_t xs[4] = {v.x & 0xffffu, v.x >> 16, v.y & 0xffffu, v.y >> 16};
+      uint32_t o[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const uint32_t i = (uint32_t)g * (LINK_THREADS * 4) + t * 4 + q;
+        const uint32_t x = xs[q];
+        o[q] = i < keep ? W[i + n] : (x < MARK_BASE ? x : W[(x - MARK_BASE) & (HN - 1)]);
+      }
+      *reinterpret_cast<uint2 *>(W2 + (uint32_t)g * (LINK_THREADS * 4) + t * 4) =
+          make_uint2(o[0] | (o[1] << 16), o[2] | (o[3] << 16));
+    }
+    cur ^= 1;
+    __syncthreads();
+  };
+  for (uint32_t j = m0; j < m1; j += 2) {
+    step(j, la, ha, lb, hb);
+    if (j + 1 < m1) step(j + 1, lb, hb, la, ha);
+  }
+  // the map after the segment's last member (the next segment's start window)
+  uint16_t *g = mend + ((size_t)cj.job * LS_SEGS_MAX + k) * HN;
+  for (uint32_t i = t * 8; i < HN; i += LINK_THREADS * 8)
+    *reinterpret_cast<uint4 *>(g + i) = *reinterpret_cast<const uint4 *>(&s_map[cur][i]);
+}
+
+// start windows of every segment: S(0) unused (segment 0's maps are bytes),
+// S(1) = M_end(0), S(k) = M_end(k - 1) applied to S(k - 1); written over the
+// job's M_end slots (M_end(k - 1) -> S(k)), one workgroup per chain
+__global__ void __launch_bounds__(LINK_THREADS) zs_linkseg_join_kernel(const ZsCJobDev *__restrict__ cjobs, uint32_t nseg_per,
+                                                                       uint16_t *__restrict__ mend) {
+  constexpr uint32_t HN = HIST;
+  __shared__ __attribute__((aligned(16))) uint16_t s_prev[HN];
+  const uint32_t t = threadIdx.x;
+  const ZsCJobDev cj = cjobs[blockIdx.x];
+  if (!cj.ok) return;
+  uint16_t *base = mend + (size_t)cj.job * LS_SEGS_MAX * HN;
+  // S(1) = M_end(0): bytes already
+  for (uint32_t i = t; i < HN; i += LINK_THREADS) s_prev[i] = base[i];
+  __syncthreads();
+  for (uint32_t k = 1; k + 1 < nseg_per; k++) {
+    uint16_t *m = base + (size_t)k * HN;  // M_end(k) -> S(k + 1)
+    uint16_t r[HN / LINK_THREADS];
+#pragma unroll
+    for (uint32_t q = 0; q < HN / LINK_THREADS; q++) {
+      const uint32_t v = m[t + q * LINK_THREADS];
+      r[q] = v < MARK_BASE ? (uint16_t)v : s_prev[(v - MARK_BASE) & (HN - 1)];
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t q = 0; q < HN / LINK_THREADS; q++) {
+      m[t + q * LINK_THREADS] = r[q];
+      s_prev[t + q * LINK_THREADS] = r[q];
+    }
+    __syncthreads();
   }
 }
 
@@ -1301,7 +1427,7 @@ extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_hea
                                   uint16_t *d_scratch, uint32_t *d_tokens, ZsTokPool pool, uint32_t *d_tables,
                                   const uint32_t *d_fixed, uint8_t *d_windows, void *d_linkinfo, ZsDecDev *d_decs,
                                   uint32_t *d_fallback, int d64, int wave_units, void *d_plink, uint32_t plink_levels,
-                                  hipStream_t st, hipEvent_t *ev) {
+                                  uint16_t *d_lmaps, uint32_t lsegs, hipStream_t st, hipEvent_t *ev) {
   // ev (profiling, optional): [0] before find, [1] after find + plan, [2] after
   // parse + chain, [3] after expand, [4] after link, [5] after emit
   if (ev) (void)hipEventRecord(ev[0], st);
@@ -1358,6 +1484,15 @@ extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_hea
                        info, d_fallback);
     if (ev) (void)hipEventRecord(ev[4], st);
     hipLaunchKernelGGL(zs_emit64_kernel, dim3(nunit_slots), dim3(EMIT_THREADS), 0, st, d_jobs, d_units, d_scratch,
+                       d_windows, d_fallback);
+  } else if (d_lmaps && lsegs > 1) {  // segmented link: segment maps, joined, then the segments' byte windows
+    hipLaunchKernelGGL(zs_linkseg_kernel, dim3(ncjobs * lsegs), dim3(LINK_THREADS), 0, st, d_jobs, d_cjobs, lsegs, d_scratch,
+                       d_lmaps, info);
+    hipLaunchKernelGGL(zs_linkseg_join_kernel, dim3(ncjobs), dim3(LINK_THREADS), 0, st, d_cjobs, lsegs, d_lmaps);
+    hipLaunchKernelGGL(zs_link_kernel<HIST>, dim3(ncjobs * lsegs), dim3(LINK_THREADS), 0, st, d_jobs, d_cjobs, d_scratch,
+                       d_windows, info, d_fallback, lsegs, (const uint16_t *)d_lmaps, (const ZsChunkDev *)d_units);
+    if (ev) (void)hipEventRecord(ev[4], st);
+    hipLaunchKernelGGL(zs_emit_kernel<HIST>, dim3(nunit_slots), dim3(EMIT_THREADS), 0, st, d_jobs, d_units, d_scratch,
                        d_windows, d_fallback);
   } else {
     hipLaunchKernelGGL(zs_link_kernel<HIST>, dim3(ncjobs), dim3(LINK_THREADS), 0, st, d_jobs, d_cjobs, d_scratch, d_windows,

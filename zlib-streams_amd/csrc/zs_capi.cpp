@@ -59,7 +59,7 @@ extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_hea
                                   uint16_t *d_scratch, uint32_t *d_tokens, ZsTokPool pool, uint32_t *d_tables,
                                   const uint32_t *d_fixed, uint8_t *d_windows, void *d_linkinfo, ZsDecDev *d_decs,
                                   uint32_t *d_fallback, int d64, int wave_units, void *d_plink, uint32_t plink_levels,
-                                  hipStream_t st, hipEvent_t *ev);
+                                  uint16_t *d_lmaps, uint32_t lsegs, hipStream_t st, hipEvent_t *ev);
 
 namespace {
 
@@ -132,6 +132,8 @@ struct Workspace {
   uint32_t *d_tables = nullptr;  // TABLE_STRIDE words per unit slot
   uint8_t *d_windows = nullptr;  // 32 KiB per unit slot (64 KiB for deflate64 units)
   size_t cap_windows = 0;
+  uint8_t *d_lmaps = nullptr;  // segmented link: per job LS_SEGS_MAX segment-end / start window maps (u16)
+  size_t cap_lmaps = 0;
   uint64_t *d_linkinfo = nullptr;  // zs_link_kernel chain order: 16 B per unit slot
   uint8_t *d_plink = nullptr;      // parallel-prefix link maps (few long streams): 2 x slots x window entries
   size_t cap_plink = 0;
@@ -186,6 +188,20 @@ uint32_t plink_levels(uint32_t njobs, uint32_t max_units, uint32_t flags) {
   uint32_t lv = 0;
   while ((1u << lv) < max_units) lv++;
   return lv;
+}
+// Segmented link (zs_linkseg_kernel): a group of at most 64 streams on the
+// serial link cuts each chain into segments so that about one workgroup per CU
+// links; env ZS_LINKSEG = 0 (or ZS_F_LINK_SERIAL) keeps zs_link_kernel.
+constexpr uint32_t LS_SEGS_MAX_HOST = 8, LS_TARGET_WG = 256;
+uint32_t link_segments(uint32_t njobs, uint32_t max_units, uint32_t flags) {
+  // env ZS_LINKSEG: 0 = off, N = N segments per chain (at most LS_SEGS_MAX), unset = auto
+  static const int force = [] {
+    const char *e = std::getenv("ZS_LINKSEG");
+    return (e && *e) ? atoi(e) : -1;
+  }();
+  if (force == 0 || (flags & ZS_F_LINK_SERIAL) || njobs == 0 || njobs > 64 || max_units < 64) return 1;
+  if (force > 0) return std::min<uint32_t>(LS_SEGS_MAX_HOST, (uint32_t)force);
+  return std::min(LS_SEGS_MAX_HOST, std::max(1u, LS_TARGET_WG / njobs));
 }
 int wave_units(size_t nseg, uint32_t flags) {
   if (flags & ZS_F_PARSE_LANE) return 0;
@@ -599,11 +615,12 @@ int run_jobs(uint32_t nv, uint64_t max_out, uint32_t flags, ZsDecDev *dec_out, Z
   zs_launch_header(g_ws.d_jobs, g_ws.d_heads, nv, st);
   const uint32_t n_cjs = n_cj - n_cj64;
   // parallel-prefix link buffers (groups of few long streams)
-  uint32_t pl_std = 0, pl_d64 = 0;
+  uint32_t pl_std = 0, pl_d64 = 0, ls_std = 1;
   {
     uint32_t mu_std = 0, mu_d64 = 0;
     for (uint32_t q = 0; q < n_cj; q++) (q < n_cjs ? mu_std : mu_d64) = std::max((q < n_cjs ? mu_std : mu_d64), g_ws.h_cjobs[q].max_units);
     pl_std = n_cjs ? plink_levels(n_cjs, mu_std, flags) : 0;
+    ls_std = n_cjs && !pl_std ? link_segments(n_cjs, mu_std, flags) : 1;
     pl_d64 = n_cj64 ? plink_levels(n_cj64, mu_d64, flags) : 0;
     const size_t need = std::max<size_t>(pl_std ? 2 * slots_std * 32768u * 2u : 0,
                                          pl_d64 ? 2 * (nunit_slots - slots_std) * 65536u * 4u : 0);
@@ -612,18 +629,27 @@ int run_jobs(uint32_t nv, uint64_t max_out, uint32_t flags, ZsDecDev *dec_out, Z
       (void)hipGetLastError();
       g_err.clear();
     }
+    // segmented link: LS_SEGS_MAX segment-end maps (u16 per window byte) per job
+    const size_t lneed = ls_std > 1 ? (size_t)nv * LS_SEGS_MAX_HOST * 32768u * 2u : 0;
+    if (lneed && ws_reserve_bytes(&g_ws.d_lmaps, &g_ws.cap_lmaps, lneed)) {
+      ls_std = 1;  // serial link instead
+      (void)hipGetLastError();
+      g_err.clear();
+    }
   }
   const uint32_t wu_std = n_cjs ? (uint32_t)wave_units(seg_std, flags) : UINT32_MAX;
   const uint32_t wu_d64 = n_cj64 ? (uint32_t)wave_units(nseg - seg_std, flags) : UINT32_MAX;
   g_ws.path[0] = wu_std;
-  g_ws.path[1] = pl_std;
+  g_ws.path[1] = pl_std ? pl_std : (ls_std > 1 ? 0x80000000u | ls_std : 0u);
   g_ws.path[2] = wu_d64;
   g_ws.path[3] = pl_d64;
   if (n_cjs) {
     zs_launch_chunked(g_ws.d_jobs, g_ws.d_heads, g_ws.d_segs, (uint32_t)seg_std, g_ws.d_cjobs, n_cjs, g_ws.d_chunks,
                       (uint32_t)slots_std, g_ws.d_scratch, g_ws.d_tokens, pool, g_ws.d_tables, g_ws.d_fixed,
                       g_ws.d_windows, g_ws.d_linkinfo, g_ws.d_decs, g_ws.d_fallback, 0, (int)wu_std,
-                      pl_std ? g_ws.d_plink : nullptr, pl_std, st, ev ? ev + 1 : nullptr);
+                      pl_std ? g_ws.d_plink : nullptr, pl_std,
+                      ls_std > 1 ? reinterpret_cast<uint16_t *>(g_ws.d_lmaps) : nullptr, ls_std, st,
+                      ev ? ev + 1 : nullptr);
   }
   if (n_cj64) {  // the deflate64 group: its own slice of every per-unit array
     ZsTokPool p64 = pool;
@@ -633,7 +659,7 @@ int run_jobs(uint32_t nv, uint64_t max_out, uint32_t flags, ZsDecDev *dec_out, Z
                       g_ws.d_scratch, g_ws.d_tokens, p64, g_ws.d_tables + slots_std * TABLE_ENTRIES_HOST,
                       g_ws.d_fixed + FIXED_WORDS_HOST, g_ws.d_windows + slots_std * 32768, g_ws.d_linkinfo + slots_std * 2,
                       g_ws.d_decs, g_ws.d_fallback, 1, (int)wu_d64, pl_d64 ? g_ws.d_plink : nullptr,
-                      pl_d64, st, (ev && !n_cjs) ? ev + 1 : nullptr);
+                      pl_d64, nullptr, 1, st, (ev && !n_cjs) ? ev + 1 : nullptr);
   }
   if (!n_cj && ev)
     for (int i = 1; i <= 6; i++) HIP_OK(hipEventRecord(ev[i], st));

@@ -388,7 +388,8 @@ def last_stats():
         _check(k)
     mode = {0: "lane", 1: "wave"}
     return {"chunked_jobs": a[0], "units": a[1], "fallback_jobs": a[2], "serial_jobs": a[3],
-            "parse": mode.get(a[4]), "link": None if a[4] > 1 else ("serial" if a[5] == 0 else "prefix"),
+            "parse": mode.get(a[4]), "link": None if a[4] > 1 else ("serial" if a[5] == 0 else
+                                                                    "segmented" if a[5] & 0x80000000 else "prefix"),
             "parse_d64": mode.get(a[6]), "link_d64": None if a[6] > 1 else ("serial" if a[7] == 0 else "prefix"),
             "lane_resident_waves": a[8], "units_std": a[9], "units_d64": a[10]}
 
