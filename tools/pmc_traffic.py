@@ -18,7 +18,7 @@ from collections import defaultdict
 
 PIPELINE = ("zs_header_kernel", "zs_find_kernel", "zs_find_fixed_kernel", "zs_plan_kernel", "zs_unit_header_kernel",
             "zs_unit_keys_kernel", "zs_lane_kernel", "zs_unitw_kernel", "zs_chain_kernel", "zs_expand_kernel", "zs_expand2_kernel",
-            "zs_link_kernel", "zs_link64_kernel", "zs_plink_init_kernel", "zs_plink_step_kernel", "zs_plink_out_kernel",
+            "zs_link_kernel", "zs_linkseg_kernel", "zs_linkseg_join_kernel", "zs_link64_kernel", "zs_plink_init_kernel", "zs_plink_step_kernel", "zs_plink_out_kernel",
             "zs_emit_kernel", "zs_emit64_kernel", "zs_decode_kernel", "zs_check_kernel", "zs_finalize_kernel")
 
 
