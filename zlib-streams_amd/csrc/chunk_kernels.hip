@@ -876,7 +876,7 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_link_kernel(const ZsJobDev *_
   const bool cont = (jb.flags & ZS_JF_CONT) != 0;
   uint32_t wv = cont ? min(jb.hist, HN) : 0u;  // valid bytes of history
   if (k > 0) {  // a later segment: its start window, valid as far as output precedes it
-    const uint16_t *S = sstart + ((size_t)cj.job * LS_SEGS_MAX + (k - 1u)) * HN;
+    const uint16_t *S = sstart + ((size_t)b * LS_SEGS_MAX + (k - 1u)) * HN;
     wv = (uint32_t)min<uint64_t>(HN, chunks[info[u0].unit].out_off + (cont ? jb.hist : 0u));
     for (uint32_t i = t; i < HN; i += LINK_THREADS) s_win[0][i] = (uint8_t)S[i];
   } else if (cont) {
@@ -1067,14 +1067,15 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_linkseg_kernel(const ZsJobDev
     if (j + 1 < m1) step(j + 1, lb, hb, la, ha);
   }
   // the map after the segment's last member (the next segment's start window)
-  uint16_t *g = mend + ((size_t)cj.job * LS_SEGS_MAX + k) * HN;
+  uint16_t *g = mend + ((size_t)b * LS_SEGS_MAX + k) * HN;
   for (uint32_t i = t * 8; i < HN; i += LINK_THREADS * 8)
     *reinterpret_cast<uint4 *>(g + i) = *reinterpret_cast<const uint4 *>(&s_map[cur][i]);
 }
 
 // start windows of every segment: S(0) unused (segment 0's maps are bytes),
 // S(1) = M_end(0), S(k) = M_end(k - 1) applied to S(k - 1); written over the
-// job's M_end slots (M_end(k - 1) -> S(k)), one workgroup per chain
+// chain's M_end slots (M_end(k - 1) -> S(k)), one workgroup per chain (slots
+// indexed by the chain's place in the group)
 __global__ void __launch_bounds__(LINK_THREADS) zs_linkseg_join_kernel(const ZsCJobDev *__restrict__ cjobs, uint32_t nseg_per,
                                                                        uint16_t *__restrict__ mend) {
   constexpr uint32_t HN = HIST;
@@ -1082,7 +1083,7 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_linkseg_join_kernel(const ZsC
   const uint32_t t = threadIdx.x;
   const ZsCJobDev cj = cjobs[blockIdx.x];
   if (!cj.ok) return;
-  uint16_t *base = mend + (size_t)cj.job * LS_SEGS_MAX * HN;
+  uint16_t *base = mend + (size_t)blockIdx.x * LS_SEGS_MAX * HN;
   // S(1) = M_end(0): bytes already
   for (uint32_t i = t; i < HN; i += LINK_THREADS) s_prev[i] = base[i];
   __syncthreads();

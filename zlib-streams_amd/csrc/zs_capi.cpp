@@ -132,7 +132,7 @@ struct Workspace {
   uint32_t *d_tables = nullptr;  // TABLE_STRIDE words per unit slot
   uint8_t *d_windows = nullptr;  // 32 KiB per unit slot (64 KiB for deflate64 units)
   size_t cap_windows = 0;
-  uint8_t *d_lmaps = nullptr;  // segmented link: per job LS_SEGS_MAX segment-end / start window maps (u16)
+  uint8_t *d_lmaps = nullptr;  // segmented link: per chain LS_SEGS_MAX segment-end / start window maps (u16)
   size_t cap_lmaps = 0;
   uint64_t *d_linkinfo = nullptr;  // zs_link_kernel chain order: 16 B per unit slot
   uint8_t *d_plink = nullptr;      // parallel-prefix link maps (few long streams): 2 x slots x window entries
@@ -629,8 +629,8 @@ int run_jobs(uint32_t nv, uint64_t max_out, uint32_t flags, ZsDecDev *dec_out, Z
       (void)hipGetLastError();
       g_err.clear();
     }
-    // segmented link: LS_SEGS_MAX segment-end maps (u16 per window byte) per job
-    const size_t lneed = ls_std > 1 ? (size_t)nv * LS_SEGS_MAX_HOST * 32768u * 2u : 0;
+    // segmented link: LS_SEGS_MAX segment-end maps (u16 per window byte) per chain of the group
+    const size_t lneed = ls_std > 1 ? (size_t)n_cjs * LS_SEGS_MAX_HOST * 32768u * 2u : 0;
     if (lneed && ws_reserve_bytes(&g_ws.d_lmaps, &g_ws.cap_lmaps, lneed)) {
       ls_std = 1;  // serial link instead
       (void)hipGetLastError();
