@@ -898,13 +898,16 @@ __global__ void __launch_bounds__(ZD_PT) zs_zd_parse_kernel(const ZsDJobDev *__r
   for (uint32_t i = t; i < ZD_REG / 32; i += ZD_PT) s_S[i] = s_V[i] = s_M[i] = 0;
   __syncthreads();
   uint32_t var;
-  // speculative walk of the piece from (a, A): marks its state-A positions
+  // speculative walk of the piece from (a, A), recording as the final walk
+  // would: its state-A positions, token starts and variants (kept from the
+  // point where the true parse meets it, below)
+  auto rec = [&](uint64_t x, uint32_t v) {
+    zd_setbit(s_S, x - r0);
+    zd_putbit(s_V, x - r0, v != 0);
+  };
   uint64_t p = t == ent_t ? ent_p : a;
   uint32_t st = t == ent_t ? ent_s : ZD_STATE_A;
-  while (act && p < b) {
-    if (st == ZD_STATE_A) zd_setbit(s_M, p - r0);
-    (void)zd_step(T, p, st, &var);
-  }
+  if (act) zd_walk_record(T, p, st, b, rec, s_M, r0, has_ent && t == ent_t);
   const uint64_t spec_p = act ? p : a;
   const uint32_t spec_s = act ? st : ZD_STATE_A;
   s_xp[t] = spec_p;
@@ -935,19 +938,26 @@ __global__ void __launch_bounds__(ZD_PT) zs_zd_parse_kernel(const ZsDJobDev *__r
     }
     if (!__syncthreads_or(changed)) break;
   }
-  // final walk from the true entry: token starts, variants, state-A marks
-  for (uint32_t i = t * (ZD_PIECE / 32); i < (t + 1) * (ZD_PIECE / 32); i++) s_M[i] = 0;  // own words
-  __syncthreads();
+  // final walk from the true entry, only up to where it meets the speculative
+  // walk (a marked state-A loop top: from there both walk the same path, whose
+  // tokens and marks the speculative walk recorded); the piece's bits below
+  // that point are cleared and rewritten (each piece owns its 32-aligned words)
   if (act) {
     uint64_t q = t == ent_t ? ent_p : s_xp[t - 1];
     uint32_t qs = t == ent_t ? ent_s : s_xs[t - 1];
-    zd_walk_record(
-        T, q, qs, b,
-        [&](uint64_t x, uint32_t v) {
-          zd_setbit(s_S, x - r0);
-          zd_putbit(s_V, x - r0, v != 0);
-        },
-        s_M, r0, has_ent && t == ent_t);
+    uint64_t mq = q;
+    uint32_t mqs = qs;
+    while (mq < b && !(mqs == ZD_STATE_A && zd_getbit(s_M, mq - r0))) (void)zd_step(T, mq, mqs, &var);
+    const uint64_t mp = min(mq, b);
+    for (uint64_t x = a; x < mp; x += 32u) {
+      const uint32_t wi = (uint32_t)((x - r0) >> 5);
+      const uint32_t n = (uint32_t)min<uint64_t>(32u, mp - x);
+      const uint32_t keep = n == 32u ? 0u : ~0u << n;
+      s_S[wi] &= keep;
+      s_V[wi] &= keep;
+      s_M[wi] &= keep;
+    }
+    zd_walk_record(T, q, qs, mp, rec, s_M, r0, has_ent && t == ent_t);
   }
   __syncthreads();
   ZdBm Bm = zd_bm(bm, jb);
