@@ -481,3 +481,27 @@ def test_segmented_link_vs_oracle(zs):
     assert zs.last_stats()["link"] == "serial"
     assert [g[0] for g in got2] == [g[0] for g in got] and [g[1] for g in got2] == [g[1] for g in got]
 
+
+
+def test_c5_rank_share_world8_vs_oracle(zs):
+    """configs[4] split over 8 ranks: the last rank's share of the 4 096 x 4 MiB
+    mixed raw / gzip streams (shard.bench_shard, the partition bench.py's ranks
+    derive), decoded on this GPU in the parse / link modes a 512-stream batch
+    takes by default, every job vs the oracle."""
+    import shard
+    from concurrent.futures import ThreadPoolExecutor
+
+    ids = shard.bench_shard(4096, 7, 8, shard.c5_kind)
+    assert len(ids) == 512
+
+    def make(k):
+        raw, wb = corpus.c5_stream(k, 4 << 20)
+        c = zlib.compressobj(6, zlib.DEFLATED, wb, 8)
+        return raw, c.compress(raw) + c.flush(), wb
+
+    with ThreadPoolExecutor(16) as ex:
+        cases = list(ex.map(make, ids))
+    got = zs.inflate_batch([c[1] for c in cases], [c[2] for c in cases], [4 << 20] * len(cases))
+    st = zs.last_stats()
+    assert st["chunked_jobs"] == len(cases) and st["fallback_jobs"] == 0, st
+    _compare_all_with_oracle(cases, got, 4 << 20)
