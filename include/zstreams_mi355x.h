@@ -108,6 +108,12 @@ typedef struct zs_result {
    groups the per-stream serial link (zs_link_kernel).  This forces the serial
    link (testing, tuning). */
 #define ZS_F_LINK_SERIAL 32u
+/* Force the segmented window link with n segments per chain (1 <= n <= 8; 1 is
+   the serial link) for the raw/zlib/gzip group, whatever its size (testing,
+   tuning; results are identical).  By default a group of 5..64 streams with
+   chains of >= 64 units cuts each chain into min(8, 256 / streams) segments. */
+#define ZS_F_LINKSEG(n) (((uint32_t)(n) & 15u) << 8)
+#define ZS_F_LINKSEG_GET(flags) (((flags) >> 8) & 15u)
 
 #define ZS_ENODEV (-100)
 #define ZS_EFORMAT (-101) /* malformed container (zs_zip_scan) */
@@ -191,8 +197,10 @@ int zs_kprof_read(uint64_t *out, uint32_t n, int reset);
 int zs_last_stats(uint32_t out[4]);
 /* The same four counters, then the path the last batch's block-parallel groups
    took: [4] raw/zlib/gzip group parse mode (0 lane per unit, 1 wave per unit,
-   UINT32_MAX no such group), [5] its link (0 serial, else parallel-prefix scan
-   levels), [6] / [7] the same for the deflate64 group, [8] lane-parse waves
+   UINT32_MAX no such group), [5] its link: 0 serial, 0x80000000 | S the
+   segmented link with S segments per chain, else the parallel-prefix link's
+   scan levels (< 32), [6] / [7] the same for the deflate64 group (which has no
+   segmented link), [8] lane-parse waves
    resident at once (units dealt in groups of 64 x this), [9] decode units of the
    raw/zlib/gzip group, [10] of the deflate64 group.  Writes min(n, 11) entries
    and returns that count. */

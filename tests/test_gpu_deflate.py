@@ -649,3 +649,36 @@ def test_deflate_init_rejects_unimplemented_parameters(zs):
     g = _GpuDeflate(zs, 6, 31)
     g.call1(b"abc" * 1000, 1 << 16, 0)
     assert g.end() == -3  # Z_DATA_ERROR: stream freed before Z_FINISH
+
+
+def test_deflate_fixup_in_order_pass(zs, monkeypatch):
+    """ZS_ZD_ROUNDS=0 skips the parallel cross-region fix-up rounds, so every
+    job's regions are settled by the in-order pass (zs_zd_fix_seq_kernel):
+    zlib's bytes at every deflate_slow level (4..9) on text, periodic runs (whose
+    parse offsets never line up across 64 KiB regions), zeros and mixed inputs,
+    under the demand-driven search the final build runs."""
+    monkeypatch.setenv("ZS_ZD_ROUNDS", "0")
+    rng = random.Random(21)
+    pats = _patterns(rng)
+    per = bytes(rng.getrandbits(8) for _ in range(1000)) * 1200  # period 1000, 1.2 MB
+    datas = (pats["text"], pats["mixed"], bytes(1 << 20), per, b"ab" * 400000)
+    cases = [(d, wb, lv) for d in datas for wb, lv in ((-15, 4), (31, 5), (15, 6), (-15, 7), (31, 8), (15, 9))]
+    got = zs.deflate_batch([c[0] for c in cases], [c[1] for c in cases], [c[2] for c in cases])
+    bad = [(i, len(d), wb, lv) for i, ((d, wb, lv), (comp, info)) in enumerate(zip(cases, got))
+           if comp != zlib_bytes(d, wb, lv) or info["ret"] != 1]
+    assert not bad, bad
+
+
+def test_deflate_long_zero_run_is_zlibs(zs):
+    """300 MiB of zeros (> 4 096 regions of 64 KiB: the cascade a bounded number
+    of parallel fix-up rounds cannot settle) and a 300 MiB period-777 run, at
+    level 4 raw and level 9 gzip: zlib's bytes (deflate.c deflate_slow; trees.c
+    block flushes), with the demand-driven search of the final build."""
+    zeros = bytes(300 << 20)
+    unit = bytes(random.Random(5).getrandbits(8) for _ in range(777))
+    per = (unit * ((300 << 20) // 777 + 1))[:300 << 20]
+    for data in (zeros, per):
+        for wb, lv in ((-15, 4), (31, 9)):
+            (comp, info), = zs.deflate_batch([data], wb, lv)
+            ref = zlib_bytes(data, wb, lv)
+            assert info["ret"] == 1 and comp == ref, (len(data), wb, lv, len(comp), len(ref))

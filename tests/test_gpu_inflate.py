@@ -505,3 +505,78 @@ def test_c5_rank_share_world8_vs_oracle(zs):
     st = zs.last_stats()
     assert st["chunked_jobs"] == len(cases) and st["fallback_jobs"] == 0, st
     _compare_all_with_oracle(cases, got, 4 << 20)
+
+
+# ---------------------------------------------------------------------------
+# the segmented window link at the configurations the final build runs it
+# (zs_capi.cpp link_segments: S = min(8, 256 / streams) segments per chain)
+# ---------------------------------------------------------------------------
+def test_c2_headline_batch_segmented_link_vs_oracle(zs):
+    """configs[1] exactly as the headline bench runs it: 64 x 64 MiB raw-deflate
+    streams (Zipf text 0..31, line text 32..63, host zlib L6) in ONE batch with
+    default flags -- lane parse, segmented link with 4 segments per chain of
+    ~720 members -- every job's output and (ret, msg, total_in, total_out,
+    adler) vs the oracle and the generator."""
+    raws, comps = corpus.batch(0, 64, 64 << 20, level=6, wbits=-15, nthreads=16)
+    cases = [(r, c.tobytes(), -15) for r, c in zip(raws, comps)]
+    del comps
+    got = zs.inflate_batch([c[1] for c in cases], -15, [64 << 20] * 64)
+    st = zs.last_stats()
+    assert st["parse"] == "lane" and st["link"] == "segmented" and st["link_segments"] == 4, st
+    assert st["chunked_jobs"] == 64 and st["fallback_jobs"] == 0, st
+    assert st["units_std"] >= 64 * 400, st  # chains of >= 400 members on average
+    _compare_all_with_oracle(cases, got, 64 << 20)
+
+
+def test_c2_strong_split_share_world8_vs_oracle(zs):
+    """The share one rank of 8 decodes when the 64 x 64 MiB C2 batch is split
+    across 8 GPUs (shard.bench_shard, bench.py --scaling strong / --sim-world 8):
+    8 streams -> wave-per-unit parse and the segmented link with 8 segments per
+    chain; every job vs the oracle."""
+    import shard
+    ids = shard.bench_shard(64, 7, 8, shard.c2_kind)
+    assert len(ids) == 8
+    cases = []
+    for i in ids:
+        r, c = corpus.batch(i, 1, 64 << 20, level=6, wbits=-15, nthreads=1)
+        cases.append((r[0], c[0].tobytes(), -15))
+    got = zs.inflate_batch([c[1] for c in cases], -15, [64 << 20] * len(cases))
+    st = zs.last_stats()
+    assert st["parse"] == "wave" and st["link"] == "segmented" and st["link_segments"] == 8, st
+    assert st["chunked_jobs"] == 8 and st["fallback_jobs"] == 0, st
+    _compare_all_with_oracle(cases, got, 64 << 20, nthreads=8)
+
+
+@pytest.mark.parametrize("parse", ["lane", "wave"])
+def test_c2_pair_forced_link_segments_vs_oracle(zs, parse):
+    """ZS_F_LINKSEG(n), n = 2 / 4 / 8, on the C2 pair (one Zipf, one line-text
+    64 MiB stream: chains of ~900 / ~500 members) under both parse modes: the
+    segmented link at every segment count gives the oracle's results; and on
+    short chains (2 MiB streams, fewer members than segments in some chains)
+    with n = 8."""
+    raws, comps = corpus.batch(0, 1, 64 << 20, level=6, wbits=-15, nthreads=1)
+    r2, c2 = corpus.batch(32, 1, 64 << 20, level=6, wbits=-15, nthreads=1)
+    cases = [(r, c.tobytes(), -15) for r, c in zip(raws + r2, comps + c2)]
+    ref = None
+    for n in (2, 4, 8):
+        got = zs.inflate_batch([c[1] for c in cases], -15, [64 << 20] * 2, parse=parse, link=("segmented", n))
+        st = zs.last_stats()
+        assert st["parse"] == parse and st["link"] == "segmented" and st["link_segments"] == n, st
+        assert st["chunked_jobs"] == 2 and st["fallback_jobs"] == 0, st
+        if ref is None:
+            _compare_all_with_oracle(cases, got, 64 << 20, nthreads=2)
+            ref = got
+        else:
+            assert [g[1] for g in got] == [g[1] for g in ref]
+            assert all(a[0] == b[0] for a, b in zip(got, ref))
+    small = []
+    for k in range(6):
+        raw, wb = corpus.c5_stream(k, (k + 1) << 18)
+        c = zlib.compressobj(6, zlib.DEFLATED, wb, 8)
+        small.append((raw, c.compress(raw.tobytes()) + c.flush(), wb))
+    cap = 6 << 18
+    got = zs.inflate_batch([c[1] for c in small], [c[2] for c in small], [cap] * len(small), parse=parse,
+                           link=("segmented", 8))
+    st = zs.last_stats()
+    assert st["link"] == "segmented" and st["link_segments"] == 8, st
+    _compare_all_with_oracle(small, got, cap)

@@ -230,3 +230,39 @@ def test_zlib_abi_one_shot_fast_path(zs):
                 assert rg == ro
             g.end()
             o.end()
+
+
+def test_handle_output_space_small_large_small(zs):
+    """One inflate handle whose calls offer small, then > 4 MiB, then small output
+    space: the large call's output goes back through a pinned staging buffer
+    that grows (reallocates) past the mapped one, and the next small call must
+    use the new buffer's device view (a stale view would write freed memory).
+    Every call's (produced, ret, last_consumed) and bytes equal the oracle's."""
+    raw = corpus.stream(9, 12 << 20)
+    comp = _comp(raw, -15)
+    L = zs.lib()
+    h = L.inflate_new()
+    assert L.inflate_init_raw(h) == 0
+    ref = O.Stream(-15)
+    ib = ctypes.create_string_buffer(comp, len(comp))
+    off, got, exp = 0, bytearray(), bytearray()
+    plan = [(4096, 65536), (4096, 65536), (600 << 10, 8 << 20), (4096, 65536), (4096, 65536),
+            (900 << 10, 6 << 20), (2048, 1000), (65536, 65536)]
+    k = 0
+    while True:
+        n_in, n_out = plan[k % len(plan)]
+        k += 1
+        n_in = min(n_in, len(comp) - off)
+        ob = ctypes.create_string_buffer(max(n_out, 1))
+        r = L.inflate_process(h, ctypes.addressof(ib) + off, n_in, ctypes.addressof(ob), n_out, 0)
+        prod, code, cons = r & 0xffffff, ((r >> 24) & 0xff), L.inflate_last_consumed(h)
+        code = code - 256 if code & 0x80 else code
+        e = ref.call(comp[off:off + n_in], n_out, 0)
+        assert (prod, code, cons) == (len(e["out"]), e["ret"], e["consumed"]), (k, n_in, n_out, e["ret"])
+        got += ob.raw[:prod]
+        exp += e["out"]
+        off += cons
+        if code != 0:
+            break
+    assert code == 1 and bytes(got) == bytes(exp) == raw
+    assert L.inflate_end(h) == 0

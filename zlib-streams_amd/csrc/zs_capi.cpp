@@ -184,7 +184,9 @@ uint32_t plink_levels(uint32_t njobs, uint32_t max_units, uint32_t flags) {
     const char *e = std::getenv("ZS_PLINK");
     return e && e[0] == '0';
   }();
-  if (off || (flags & ZS_F_LINK_SERIAL) || njobs == 0 || njobs > PLINK_JOBS || max_units < 64) return 0;
+  if (off || (flags & ZS_F_LINK_SERIAL) || ZS_F_LINKSEG_GET(flags) || njobs == 0 || njobs > PLINK_JOBS ||
+      max_units < 64)
+    return 0;
   uint32_t lv = 0;
   while ((1u << lv) < max_units) lv++;
   return lv;
@@ -199,7 +201,10 @@ uint32_t link_segments(uint32_t njobs, uint32_t max_units, uint32_t flags) {
     const char *e = std::getenv("ZS_LINKSEG");
     return (e && *e) ? atoi(e) : -1;
   }();
-  if (force == 0 || (flags & ZS_F_LINK_SERIAL) || njobs == 0 || njobs > 64 || max_units < 64) return 1;
+  if ((flags & ZS_F_LINK_SERIAL) || njobs == 0) return 1;
+  const uint32_t fseg = ZS_F_LINKSEG_GET(flags);  // per call: forced segments (tests), any chain length
+  if (fseg) return std::min<uint32_t>(LS_SEGS_MAX_HOST, fseg);
+  if (force == 0 || njobs > 64 || max_units < 64) return 1;
   if (force > 0) return std::min<uint32_t>(LS_SEGS_MAX_HOST, (uint32_t)force);
   return std::min(LS_SEGS_MAX_HOST, std::max(1u, LS_TARGET_WG / njobs));
 }
@@ -879,12 +884,15 @@ struct StreamState {
 
 constexpr size_t STAGE_MAX = 4u << 20;
 
-// pinned staging buffer of >= need bytes (need <= STAGE_MAX), else nullptr
-uint8_t *stage_buf(uint8_t **p, size_t *cap, size_t need) {
+// pinned staging buffer of >= need bytes (need <= STAGE_MAX), else nullptr.
+// dp: the buffer's cached device view, dropped whenever the buffer is
+// reallocated (a stale view would let a later mapped call write freed memory)
+uint8_t *stage_buf(uint8_t **p, size_t *cap, size_t need, uint8_t **dp) {
   if (need > STAGE_MAX) return nullptr;
   if (need > *cap) {
     if (*p) (void)hipHostFree(*p);
     *p = nullptr;
+    *dp = nullptr;
     *cap = 0;
     const size_t c = std::max<size_t>(need, 128u << 10);
     if (hipHostMalloc(reinterpret_cast<void **>(p), c, hipHostMallocDefault) != hipSuccess) {
@@ -898,10 +906,9 @@ uint8_t *stage_buf(uint8_t **p, size_t *cap, size_t need) {
 
 // stage_buf plus the buffer's device view (kernels read / write it over the bus)
 uint8_t *stage_mapped(uint8_t **p, size_t *cap, uint8_t **dp, size_t need) {
-  const uint8_t *old = *p;
-  uint8_t *h = stage_buf(p, cap, need);
+  uint8_t *h = stage_buf(p, cap, need, dp);
   if (!h) return nullptr;
-  if (h != old || !*dp) {
+  if (!*dp) {
     void *d = nullptr;
     if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
       (void)hipGetLastError();
@@ -1278,7 +1285,7 @@ int stream_call(StreamState *s, const uint8_t *in, unsigned in_len, uint8_t *out
       if (clen) std::memcpy(hmi, s->carry.data(), clen);
       if (take) std::memcpy(hmi + clen, in + off, take);
     } else {
-      if (uint8_t *hb = stage_buf(&s->h_in, &s->cap_hin, blen)) {  // one DMA from pinned staging
+      if (uint8_t *hb = stage_buf(&s->h_in, &s->cap_hin, blen, &s->dh_in)) {  // one DMA from pinned staging
         if (clen) std::memcpy(hb, s->carry.data(), clen);
         if (take) std::memcpy(hb + clen, in + off, take);
         if (blen) HIP_OK(hipMemcpyAsync(s->d_in, hb, blen, hipMemcpyHostToDevice, hs));
@@ -1304,7 +1311,7 @@ int stream_call(StreamState *s, const uint8_t *in, unsigned in_len, uint8_t *out
     if (h.produced && mapped) {
       std::memcpy(out + prod, hmo, h.produced);
     } else if (h.produced) {
-      uint8_t *hb = stage_buf(&s->h_out, &s->cap_hout, h.produced);
+      uint8_t *hb = stage_buf(&s->h_out, &s->cap_hout, h.produced, &s->dh_out);
       HIP_OK(hipMemcpyAsync(hb ? hb : out + prod, s->d_out, h.produced, hipMemcpyDeviceToHost, hs));
       HIP_OK(hipStreamSynchronize(hs));
       if (hb) std::memcpy(out + prod, hb, h.produced);

@@ -136,13 +136,22 @@ PARSE_FLAGS = {None: 0, "lane": 8, "wave": 16}  # ZS_F_PARSE_LANE / ZS_F_PARSE_W
 LINK_FLAGS = {None: 0, "serial": 32}  # ZS_F_LINK_SERIAL
 
 
+def _link_flags(link):
+    """link: None (auto), "serial", or ("segmented", n): ZS_F_LINKSEG(n)."""
+    if isinstance(link, tuple):
+        assert link[0] == "segmented" and 1 <= link[1] <= 8, link
+        return link[1] << 8
+    return LINK_FLAGS[link]
+
+
 def inflate_batch(streams, window_bits=-15, out_caps=None, parse=None, link=None):
     """Inflate many whole streams on the GPU (host buffers).
 
     Each stream behaves like inflateInit2(window_bits) + one inflate(Z_FINISH)
     into an out_cap-byte buffer.  Returns [(bytes, result_dict)].  parse =
     "lane" / "wave" forces the block-parallel path's parse mode, link = "serial"
-    its per-stream window link (same results).
+    its per-stream window link, link = ("segmented", n) the segmented link
+    with n segments per chain (same results).
     """
     n = len(streams)
     if out_caps is None:
@@ -161,7 +170,7 @@ def inflate_batch(streams, window_bits=-15, out_caps=None, parse=None, link=None
         jobs[i].out = ctypes.cast(ob, ctypes.c_void_p).value
         jobs[i].out_cap = out_caps[i]
         jobs[i].window_bits = wbs[i]
-    _check(lib().zs_inflate_batch(jobs, n, res, PARSE_FLAGS[parse] | LINK_FLAGS[link]))
+    _check(lib().zs_inflate_batch(jobs, n, res, PARSE_FLAGS[parse] | _link_flags(link)))
     return [(outbufs[i].raw[:res[i].total_out], res[i].as_dict()) for i in range(n)]
 
 
@@ -391,6 +400,7 @@ def last_stats():
             "parse": mode.get(a[4]), "link": None if a[4] > 1 else ("serial" if a[5] == 0 else
                                                                     "segmented" if a[5] & 0x80000000 else "prefix"),
             "parse_d64": mode.get(a[6]), "link_d64": None if a[6] > 1 else ("serial" if a[7] == 0 else "prefix"),
+            "link_segments": (a[5] & 0x7fffffff) if a[4] <= 1 and a[5] & 0x80000000 else None,
             "lane_resident_waves": a[8], "units_std": a[9], "units_d64": a[10]}
 
 
