@@ -5,13 +5,18 @@ One "step" = one zs_inflate_batch() over this rank's share of the batch,
 inputs already resident in HBM, outputs written to HBM (ZS_F_DEVICE).
 
 Scaling (streams are independent, no exchange step):
-  --scaling weak (default: the path partitions into independent streams, so
-      each rank decodes its own 64 x 64 MiB batch, ids 64r .. 64r+63, and the
-      node's value is all ranks' bytes / the slowest rank's time);
+  --scaling weak (default -- the task's multi-GPU rule for a path that
+      partitions into independent objects: shard them, no data-path collective,
+      report "scaling": "weak"; each rank decodes its own 64 x 64 MiB batch, ids
+      64r .. 64r+63, and the node's value is all ranks' bytes / the slowest
+      rank's time.  Not comparable with round 2's strong-scaling lines);
   --scaling strong: the node decodes ONE 64 x 64 MiB batch; rank r decodes its
       LPT share of the 64 streams (shard.bench_shard).  This is latency-bound
       (profiles/r03/strong_split_1gpu.json: 1.41x / 1.73x / 2.61x at 2 / 4 / 8).
   --workload c5 (configs[4]) is a fixed 4 096-stream batch sharded by LPT.
+  Every c2 run also carries a "c5" object: configs[4]'s fixed 4 096 x 4 MiB
+  batch LPT-split across the ranks (strong scaling), so a run at N = 1/2/4/8
+  gives configs[4]'s 1 -> 8 curve beside the weak headline.
 No collective touches the data: RCCL carries the contract's barrier and the
 reduction of the per-rank counters (max elapsed, summed bytes, all verified).
 
@@ -83,6 +88,13 @@ def parse_args(argv=None):
     ap.add_argument("--stream-handle-mib", type=int, default=4, help="stream size per concurrent handle")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r03", "pmc_traffic.json"),
                     help="PMC-derived HBM bytes per pipeline launch (null in the line when absent)")
+    ap.add_argument("--no-c5-leg", action="store_true",
+                    help="skip the configs[4] leg (the fixed 4096 x 4 MiB batch LPT-split across the ranks)")
+    ap.add_argument("--c5-leg-kib", type=int, default=4096, help="stream size of the configs[4] leg")
+    ap.add_argument("--no-ref-perf", action="store_true",
+                    help="skip the reference perf workload (test_round_trip_stream_perf.js) in the stream leg")
+    ap.add_argument("--ref-perf-mib", type=int, default=100)
+    ap.add_argument("--ref-perf-runs", type=int, default=3, help="runs per phase on the GPU (median reported)")
     ap.add_argument("--sim-world", type=int, default=0,
                     help="one-GPU rehearsal of a strong split: decode only rank --sim-rank's LPT share of the "
                          "node batch as it would be at --sim-world ranks (scaling prediction; not the headline)")
@@ -423,6 +435,12 @@ def main():
                        "same_library_build": tj.get("library_sha256") == so_sha if tj.get("library_sha256") else None,
                        "how": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, gfx950-corrected, every pipeline kernel"}
 
+    c5_l = None
+    if args.workload == "c2" and not args.no_c5_leg and args.sim_world <= 1:
+        c5_l = guarded("c5", c5_leg, args, shard, torch, np, dev, dist, rank, world, gen_threads)
+        if dist and "error" in c5_l:
+            raise RuntimeError(f"c5 leg failed on rank {rank}: {c5_l['error']}")  # its collectives would hang
+
     comp_leg = d64_leg = None
     if not args.dry_run and not args.no_compress and nloc:
         kinds = [shard.c2_kind(i) for i in ids]
@@ -477,6 +495,7 @@ def main():
                          "stage_kernels": None if args.dry_run else zstreams.STAGE_KERNELS},
             "cpu_baseline": cpu_b,
             "path_stats": stats,
+            "c5": c5_l,
             "compress": comp_leg,
             "deflate64": d64_leg,
             "stream": stream_l,
@@ -491,6 +510,87 @@ def main():
         print(json.dumps(line), flush=True)
     if dist:
         tdist.destroy_process_group()
+
+
+def c5_leg(args, shard, torch, np, dev, dist, rank, world, gen_threads):
+    """configs[4] beside the C2 headline: the FIXED batch of `c5_streams` x 4 MiB
+    mixed raw / gzip streams (tests/corpus.py c5_stream), split across the ranks by
+    LPT (shard.bench_shard) -- strong scaling, so a driver run at N = 1/2/4/8 gives
+    configs[4]'s curve.  Per rank: one zs_inflate_batch of its share per step,
+    inputs resident in HBM, outputs compared with the generator; the node's value
+    is the batch's bytes over the slowest rank's time (barrier + max over ranks,
+    as the headline)."""
+    ids = shard.bench_shard(args.c5_streams, rank, world, shard.c5_kind)
+    nbytes = args.c5_leg_kib << 10
+    t0 = time.time()
+    raws, comps, wbs = generate(ids, nbytes, "c5", gen_threads)
+    nloc = len(ids)
+    log(f"[rank {rank}] c5 leg: {nloc} of {args.c5_streams} streams x {nbytes >> 10} KiB generated in "
+        f"{time.time() - t0:.1f}s")
+    stats = {}
+    if args.dry_run:
+        def step():
+            return [zlib.decompressobj(wb).decompress(c.tobytes()) for c, wb in zip(comps, wbs)]
+        ok = all(r == raw.tobytes() for r, raw in zip(step(), raws))
+    else:
+        import zstreams
+        offs, o = [], 0
+        for c in comps:
+            offs.append(o)
+            o += (len(c) + 255) & ~255
+        hbuf = np.zeros(o + 256, dtype=np.uint8)
+        for c, of in zip(comps, offs):
+            hbuf[of:of + len(c)] = c
+        d_in = torch.from_numpy(hbuf).to(dev)
+        del hbuf
+        d_out = torch.empty(max(1, nloc) * nbytes, dtype=torch.uint8, device=dev)
+        in_ptrs = [d_in.data_ptr() + of for of in offs]
+        in_lens = [len(c) for c in comps]
+        out_ptrs = [d_out.data_ptr() + k * nbytes for k in range(nloc)]
+
+        def step():
+            return zstreams.inflate_batch_device(in_ptrs, in_lens, out_ptrs, [nbytes] * nloc, wbs) if nloc else []
+
+        for _ in range(max(1, args.warmup)):
+            res = step()
+        torch.cuda.synchronize()
+        stats = zstreams.last_stats() if nloc else {}
+        ok = all(r["ret"] == 1 and r["total_out"] == nbytes and r["total_in"] == in_lens[k] for k, r in enumerate(res))
+        per = max(1, (1 << 30) // nbytes)  # compare in 1 GiB pieces
+        for k0 in range(0, nloc, per):
+            k1 = min(nloc, k0 + per)
+            host = d_out[k0 * nbytes:k1 * nbytes].cpu().numpy().reshape(k1 - k0, nbytes)
+            ok = ok and all(np.array_equal(host[k - k0], raws[k]) for k in range(k0, k1))
+            del host
+    if dist:
+        torch.distributed.barrier()
+    if not args.dry_run:
+        torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if not args.dry_run:
+        torch.cuda.synchronize()
+    if dist:
+        torch.distributed.barrier()
+    t_el = time.perf_counter() - t_start
+    mine = {"rank": rank, "streams": nloc, "ms_per_step": round(t_el * 1e3 / args.steps, 3),
+            "parse": stats.get("parse"), "link": stats.get("link"), "link_segments": stats.get("link_segments"),
+            "units": stats.get("units"), "fallback_jobs": stats.get("fallback_jobs"), "verified": bool(ok)}
+    ranks = [mine]
+    if dist:
+        ranks = [None] * world
+        torch.distributed.all_gather_object(ranks, mine)
+    t_max, out_bytes, ok_all = shard.reduce_counters(t_el, nloc * nbytes * args.steps, ok, device=dev)
+    if not args.dry_run:
+        del d_in, d_out
+        torch.cuda.empty_cache()
+    return {"metric": f"MiB/s decompressed per node, configs[4]: {args.c5_streams}x{nbytes >> 10}KiB mixed raw/gzip",
+            "value": round(out_bytes / t_max / 2**20, 1), "unit": "MiB/s", "scaling": "strong",
+            "streams_total": args.c5_streams, "stream_bytes": nbytes, "ms_per_step": round(t_max * 1e3 / args.steps, 3),
+            "partition": "LPT over the fixed batch (shard.bench_shard, cost 2 Zipf / 1 line text)",
+            "data": "synthetic: Zipf / line text alternating in pairs, raw (-15) / gzip (31) alternating, host zlib L6",
+            "ranks": ranks, "verified_bit_exact": bool(ok_all)}
 
 
 def guarded(name, fn, *a, **kw):
@@ -632,6 +732,16 @@ def stream_leg(args, zstreams, np, cpu):
     zref = b"".join(zc.compress(dbytes[o:o + 32768]) for o in range(0, len(dbytes), 32768)) + zc.flush()
     tzl = time.perf_counter() - t0
 
+    # CompressionStreamZlib at level 1 (deflate_fast: serial per stream on the GPU), one handle
+    lbytes = raw1[: min(len(raw1), 4 << 20)].tobytes()
+    t0 = time.perf_counter()
+    l1comp = zstreams.compress(lbytes, "deflate-raw", 1, ws)
+    tl1 = time.perf_counter() - t0
+    zc = _zlib.compressobj(1, _zlib.DEFLATED, -15, 8, 0)
+    t0 = time.perf_counter()
+    l1ref = b"".join(zc.compress(lbytes[o:o + 32768]) for o in range(0, len(lbytes), 32768)) + zc.flush()
+    tl1z = time.perf_counter() - t0
+
     reps = max(1, int(2e9 // one_bytes))
     c1v, c1ok = cpu_js([comp1] * reps, 1, one_bytes)
     thr = max(1, min(cpu["physical_cores"], nh))
@@ -657,11 +767,69 @@ def stream_leg(args, zstreams, np, cpu):
                                 "stream": f"line text {len(dbytes) >> 20} MiB",
                                 "bytes_identical_to_zlib": dcomp == zref,
                                 "cpu_zlib_same_calls": round(len(dbytes) / tzl / 2**20, 1)},
+        "compress_one_handle_level1": {"value": round(len(lbytes) / tl1 / 2**20, 2), "unit": "MiB/s (input)",
+                                       "api": "CompressionStreamZlib deflate-raw level 1 (deflate_fast: serial per "
+                                              "stream on the GPU), same schedule",
+                                       "stream": f"line text {len(lbytes) >> 20} MiB",
+                                       "bytes_identical_to_zlib": l1comp == l1ref,
+                                       "cpu_zlib_same_calls": round(len(lbytes) / tl1z / 2**20, 1)},
+        "reference_perf_workload": None if args.no_ref_perf else guarded("stream.reference_perf_workload",
+                                                                         ref_perf_leg, args, zstreams, np),
         "cpu_baseline": {"one_handle": round(c1v, 1), "handles_all_cores": round(cmv, 1), "threads": thr,
                          "unit": "MiB/s", "kind": "reference",
                          "impl": "host zlib 1.2.11 inflate, same call schedule (the shipped WASM runs this loop)",
                          "verified": bool(c1ok and cmok)},
     }
+
+
+def ref_perf_leg(args, zstreams, np):
+    """The reference's own perf harness (src/wasm/tests/test_round_trip_stream_perf.js:23-185)
+    at its largest default size: `ref_perf_mib` MiB of random bytes written in 64 KiB packets
+    through CompressionStreamZlib('deflate-raw') (default level), the compressed stream through
+    DecompressionStreamZlib, and both chained (round trip), MiB/s = size / seconds as the
+    harness prints it (median of `ref_perf_runs` runs).  tools/js_perf.c runs the JS
+    wrapper's call schedule natively over the product library and, beside it, over host zlib
+    behind the reference's WASM glue compiled natively (one run per phase)."""
+    J = ctypes.CDLL(os.path.join(ROOT, "tools", "libzs_jsperf.so"))
+    J.zs_js_perf.restype = ctypes.c_double
+    J.zs_js_perf.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,
+                             ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]
+    n = args.ref_perf_mib << 20
+    src = np.random.default_rng(20261017).integers(0, 256, n, dtype=np.uint8)  # randomFillSync(src)
+    cap = n + n // 8 + (1 << 20)
+    packet = 65536
+
+    def run(lib, phase, data, runs):
+        out = np.empty(cap, dtype=np.uint8)
+        ol = ctypes.c_size_t()
+        ts = []
+        for _ in range(runs):
+            t = J.zs_js_perf(lib, phase, data.ctypes.data, len(data), packet, -1, out.ctypes.data, cap, ctypes.byref(ol))
+            if t <= 0:
+                raise RuntimeError(f"zs_js_perf phase {phase} failed ({t})")
+            ts.append(t)
+        return sorted(ts)[len(ts) // 2], out[:ol.value].copy(), ts
+
+    res = {}
+    comps = {}
+    for name, lib, runs in (("gpu", zstreams.LIB_PATH.encode(), max(1, args.ref_perf_runs)), ("host_zlib", None, 1)):
+        tc, comp, rc = run(lib, 0, src, runs)
+        td, dec, rd = run(lib, 1, comp, runs)
+        tr, rt, rr = run(lib, 2, src, runs)
+        comps[name] = comp
+        mib = n / 2**20
+        res[name] = {"compress_only": round(mib / tc, 2), "decompress_only": round(mib / td, 2),
+                     "roundtrip": round(mib / tr, 2), "runs": runs,
+                     "runs_s": {"compress": [round(x, 3) for x in rc], "decompress": [round(x, 3) for x in rd],
+                                "roundtrip": [round(x, 3) for x in rr]},
+                     "compressed_bytes": len(comp),
+                     "verified": bool(np.array_equal(dec, src) and np.array_equal(rt, src))}
+    res["gpu"]["bytes_identical_to_zlib"] = bool(np.array_equal(comps["gpu"], comps["host_zlib"]))
+    res["workload"] = (f"{args.ref_perf_mib} MiB random bytes, {packet >> 10} KiB packets, deflate-raw, default level; "
+                       "compress-only / decompress-only / round trip (test_round_trip_stream_perf.js)")
+    res["unit"] = "MiB/s (uncompressed)"
+    res["host_zlib"]["impl"] = "host zlib 1.2.11 behind the reference's WASM stream glue (tools/js_perf.c), 1 thread"
+    return res
 
 
 D64_FIXTURES = ("100k_lines", "10k_lines", "payload_63k", "payload_64k", "payload_65k", "rand_block_gap",

@@ -682,3 +682,214 @@ def test_deflate_long_zero_run_is_zlibs(zs):
             (comp, info), = zs.deflate_batch([data], wb, lv)
             ref = zlib_bytes(data, wb, lv)
             assert info["ret"] == 1 and comp == ref, (len(data), wb, lv, len(comp), len(ref))
+
+
+# ---------------------------------------------------------------------------
+# level 0 (deflate_stored) through the stream surfaces, call by call, and the
+# reference's own stream drivers with their output-buffer schedules
+# ---------------------------------------------------------------------------
+class _GpuHandle:
+    """One reference handle (deflate_* or inflate_* of the handle ABI): call() is
+    one *_process with the packed return unpacked, like wasm_stream_common.c."""
+
+    def __init__(self, zs, compress, wb, level=-1):
+        L = self.L = zs.lib()
+        p = "deflate_" if compress else "inflate_"
+        init = {-15: "init_raw", 15: "init", 31: "init_gzip"}[wb]
+        self.proc, self.cons, self.endf = (getattr(L, p + "process"), getattr(L, p + "last_consumed"),
+                                           getattr(L, p + "end"))
+        self.h = getattr(L, p + "new")()
+        assert (getattr(L, p + init)(self.h, level) if compress else getattr(L, p + init)(self.h)) == 0
+
+    def call(self, data, out_len, flush):
+        ib = ctypes.create_string_buffer(bytes(data), max(len(data), 1))
+        ob = ctypes.create_string_buffer(max(out_len, 1))
+        r = self.proc(self.h, ctypes.addressof(ib) if data else 0, len(data), ctypes.addressof(ob), out_len, flush)
+        r &= 0xffffffff
+        code = (r >> 24) & 0xff
+        return (code - 256 if code & 0x80 else code), self.cons(self.h), ob.raw[:r & 0xffffff]
+
+    def end(self):
+        return self.endf(self.h)
+
+
+class _HostDeflateHandle:
+    """Host zlib behind the reference's glue (deflate_stream_wasm.c:51-55)."""
+
+    def __init__(self, wb, level=-1):
+        import libz_ref
+        self.d = libz_ref.Deflater(6 if level < 0 else level, wb)
+
+    def call(self, data, out_len, flush):
+        r, cons, prod = self.d.call(data, out_len, flush)
+        return (r & 0xff) - 256 if (r & 0xff) & 0x80 else r & 0xff, cons, prod
+
+    def end(self):
+        return self.d.end()
+
+
+def _js_compress(h, data, out_buffer, write=65536):
+    """CompressionStreamZlib (zlib-streams.js:64-141) over one handle: writes of
+    `write` bytes, <= 32 KiB per process(flush 0) with an out_buffer-byte output
+    buffer, advance by last_consumed, stop a write on 0; flush() calls
+    process(Z_FINISH) until code 1 or nothing produced.  Returns the trace of
+    (code, consumed, produced bytes) per call."""
+    tr = []
+    for w in range(0, len(data), write):
+        chunk = data[w:w + write]
+        off = 0
+        while off < len(chunk):
+            r = h.call(chunk[off:off + 32768], out_buffer, 0)
+            tr.append(r)
+            if r[1] == 0:
+                break
+            off += r[1]
+    while True:
+        r = h.call(b"", out_buffer, 4)
+        tr.append(r)
+        if r[0] == 1 or not r[2]:
+            break
+    return tr
+
+
+def test_deflate_level0_stream_calls_are_zlibs(zs):
+    """Level 0 through deflate() call by call: zlib's deflate_stored sizes its
+    blocks from each call's output space and flush and from its window (direct
+    blocks of >= min_block, the window and pending-buffer path for small calls,
+    slides, Z_FULL_FLUSH restarts); random input sizes, output spaces from 7
+    bytes to 2 MiB, every flush value, raw / zlib / gzip: every call's (ret,
+    consumed, produced bytes) and strm->adler equal host zlib's."""
+    import libz_ref
+    rng = random.Random(500)
+    for wb in (-15, 15, 31):
+        data = _stream_data(rng, 700_000)
+        g = _GpuDeflate(zs, 0, wb)
+        h = libz_ref.Deflater(0, wb)
+        off, k, out = 0, 0, bytearray()
+        while True:
+            fin = off >= len(data)
+            n = 0 if fin else rng.choice([1, 100, 700, 5000, 33000, 70000, 250000])
+            chunk = data[off:off + n]
+            fl = 4 if fin else rng.choice([0, 0, 0, 1, 2, 3, 5])
+            rest = chunk
+            while True:
+                space = rng.choice([7, 100, 1024, 4096, 40000, 65536, 1 << 21])
+                a = g.call1(rest, space, fl)
+                b = h.call(rest, space, fl)
+                assert a == b, (wb, k, fl, len(rest), space, a[:2], b[:2], len(a[2]), len(b[2]))
+                assert g.s.adler == h.s.adler & 0xffffffff, (wb, k)
+                k += 1
+                out += a[2]
+                rest = rest[a[1]:]
+                if a[0] != 0 or (not rest and len(a[2]) < space and fl != 4):
+                    break
+                assert k < 200000
+            off += n
+            if fin:
+                assert a[0] == 1, a[:2]
+                break
+        assert g.end() == h.end()
+        assert zlib.decompress(bytes(out), wb) == data
+
+
+@pytest.mark.parametrize("out_buffer", [1024, 4096, 65536])
+def test_compression_stream_level0_js_schedule_is_zlibs(zs, out_buffer):
+    """CompressionStreamZlib(fmt, {level: 0, outBuffer}) (zlib-streams.js:16-17,
+    64-141): the level reaches deflateInit2 (deflate_stream_wasm.c:22-49), so every
+    deflate_process returns what host zlib's deflate_stored returns for the same
+    call, for outBuffer 1 / 4 / 64 KiB and every wrapper."""
+    data = corpus.stream(41, 300_000) + bytes(70000) + bytes(random.Random(3).getrandbits(8) for _ in range(50000))
+    for wb in (-15, 15, 31):
+        a = _js_compress(_GpuHandle(zs, True, wb, 0), data, out_buffer)
+        b = _js_compress(_HostDeflateHandle(wb, 0), data, out_buffer)
+        assert [t[:2] + (len(t[2]),) for t in a] == [t[:2] + (len(t[2]),) for t in b], (wb, out_buffer)
+        assert a == b
+        assert zlib.decompress(b"".join(t[2] for t in a), wb) == data
+
+
+def _roundtrip_inputs():
+    """The reference's round-trip inputs (test/ref-data/roundtrip_inputs), input3
+    as the Makefile rewrites it before the runs (Makefile:276: deflateRawSync of
+    24000 'x' bytes, node's zlib at its default level)."""
+    import os
+    d = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ref-data", "roundtrip_inputs")
+    ins = [open(os.path.join(d, n), "rb").read() for n in ("roundtrip_input.txt", "roundtrip_input1.txt",
+                                                             "roundtrip_input3.bin")]
+    c = zlib.compressobj(-1, zlib.DEFLATED, -15)
+    ins.append(c.compress(b"x" * 24000) + c.flush())
+    return ins
+
+
+def _ref_roundtrip_driver(dfl, inf, data):
+    """test_round_trip_stream.js:64-140 over a deflate and an inflate handle: deflate
+    <= 32 KiB per call (Z_FINISH once the input is used) into a rolling 64 KiB
+    output window (space = 65536 - position), every produced chunk fed at once to
+    inflate (its own rolling window, Z_FINISH on the deflater's last chunk), then
+    the inflater drained.  Returns the call trace and the inflated bytes."""
+    W = 65536
+    tr, out = [], bytearray()
+    off, cpos, dpos = 0, 0, 0
+    ddone = idone = False
+    while not (ddone and idone):
+        if not ddone:
+            avail = len(data) - off
+            fl = 4 if avail == 0 else 0
+            code, cons, prod = dfl.call(data[off:off + min(avail, 32768)], W - cpos, fl)
+            tr.append(("d", code, cons, prod))
+            comp = prod
+            while comp and not idone:
+                ifl = 4 if (code == 1 and len(data) - off - cons == 0) else 0
+                c2, cons2, p2 = inf.call(comp, W - dpos, ifl)
+                tr.append(("i", c2, cons2, p2))
+                assert c2 >= 0, tr[-1][:3]
+                out += p2
+                comp = comp[cons2:]
+                dpos = 0 if len(p2) == W - dpos else dpos + len(p2)
+                if c2 == 1:
+                    idone = True
+                    break
+                if cons2 == 0:
+                    break
+            off += cons
+            cpos = 0 if len(prod) == W - cpos else cpos + len(prod)
+            if code == 1:
+                ddone = True
+        if ddone and not idone:
+            c2, cons2, p2 = inf.call(b"", W - dpos, 4)
+            tr.append(("i", c2, cons2, p2))
+            out += p2
+            dpos = 0 if len(p2) == W - dpos else dpos + len(p2)
+            if c2 == 1 or (cons2 == 0 and not p2):
+                idone = c2 == 1
+                if not idone:
+                    break
+    return tr, bytes(out)
+
+
+class _OracleInflateHandle:
+    def __init__(self, wb):
+        self.s = O.Stream(wb)
+
+    def call(self, data, out_len, flush):
+        r = self.s.call(data, out_len, flush)
+        return r["ret"], r["consumed"], r["out"]
+
+
+@pytest.mark.parametrize("level", [-1, 0, 1, 6, 9])
+def test_reference_roundtrip_inputs_through_streams(zs, level):
+    """The reference's round-trip runner (test_round_trip_stream.js) on its committed
+    inputs and the Makefile's deflateRaw(24000 x 'x'), zlib wrapper: GPU deflate
+    handle -> GPU inflate handle with the runner's rolling output windows; every
+    call equals host zlib deflate -> oracle inflate driven the same way, and the
+    output is the input.  Plus CompressionStreamZlib -> DecompressionStreamZlib
+    (zlib-streams.js) at outBuffer 1 KiB on each input, bytes equal to host zlib's."""
+    for data in _roundtrip_inputs():
+        a_tr, a_out = _ref_roundtrip_driver(_GpuHandle(zs, True, 15, level), _GpuHandle(zs, False, 15), data)
+        b_tr, b_out = _ref_roundtrip_driver(_HostDeflateHandle(15, level), _OracleInflateHandle(15), data)
+        assert a_tr == b_tr and a_out == b_out == data, (len(data), level)
+        for wb in (-15, 31):
+            a = _js_compress(_GpuHandle(zs, True, wb, level), data, 1024)
+            b = _js_compress(_HostDeflateHandle(wb, level), data, 1024)
+            assert a == b, (len(data), level, wb)
+            comp = b"".join(t[2] for t in a)
+            assert zs.decompress(comp, {-15: "deflate-raw", 31: "gzip"}[wb], 1024) == data

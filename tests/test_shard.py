@@ -108,10 +108,15 @@ def test_bench_self_launch_dry_run():
         assert len(lines) == 1, r.stdout
         return json.loads(lines[0])
 
-    d = run()
+    d = run("--c5-streams", "64", "--c5-leg-kib", "4")
     assert d["dry_run"] and d["n_gpus"] == 2 and d["verified_bit_exact"] and d["scaling"] == "weak"
+    # configs[4] beside the weak headline: the fixed batch split across both ranks (strong)
+    c5 = d["c5"]
+    assert c5["scaling"] == "strong" and c5["streams_total"] == 64 and c5["verified_bit_exact"], c5
+    assert [r["rank"] for r in c5["ranks"]] == [0, 1] and sum(r["streams"] for r in c5["ranks"]) == 64
+    assert [r["streams"] for r in c5["ranks"]] == [len(shard.bench_shard(64, k, 2, shard.c5_kind)) for k in (0, 1)]
     assert d["config"]["streams_total"] == 128 and d["rank_streams"] == list(range(64))
-    d = run("--scaling", "strong")
+    d = run("--scaling", "strong", "--no-c5-leg")
     assert d["dry_run"] and d["n_gpus"] == 2 and d["verified_bit_exact"] and d["scaling"] == "strong"
     assert d["config"]["streams_total"] == 64
     assert d["rank_streams"] == shard.bench_shard(64, 0, 2, shard.c2_kind)

@@ -1164,6 +1164,61 @@ __global__ void zs_dz_trailer_kernel(const ZsDJobDev *__restrict__ jobs, uint32_
 }
 
 // ---------------------------------------------------------------------------
+// Level-0 stream calls (zs_capi.cpp ds_stored_call).  zlib's deflate_stored
+// sizes every stored block from the call's avail_out, flush and window
+// (deflate.c, 1.2.11); the host replays that arithmetic and hands the call's
+// output as copy pieces of the staged source [pieces | unframed window bytes |
+// new input | header / marker bytes].  A workgroup per 16 KiB of output writes
+// it; the last workgroup computes the check of the new input (zs_check.h).
+// ---------------------------------------------------------------------------
+#define ZS_SC_TILE 16384u
+__global__ void __launch_bounds__(DZ_T) zs_stored_call_kernel(const uint8_t *__restrict__ src,
+                                                              const ZsPiece *__restrict__ pc, uint32_t np, uint64_t total,
+                                                              uint8_t *__restrict__ dst, uint64_t ck_lo, uint64_t ck_hi,
+                                                              uint32_t wrap, uint32_t *__restrict__ res) {
+  __shared__ ZsCkTabs s_ck;
+  __shared__ uint32_t s_red32[16];
+  __shared__ uint64_t s_red[16];
+  const uint32_t t = threadIdx.x;
+  const uint64_t ntile = (total + ZS_SC_TILE - 1) / ZS_SC_TILE;
+  if (blockIdx.x < ntile) {
+    const uint64_t lo = (uint64_t)blockIdx.x * ZS_SC_TILE, hi = min(total, lo + ZS_SC_TILE);
+    uint32_t a = 0, b = np;  // the last piece starting at or before lo
+    while (b - a > 1) {
+      const uint32_t m = (a + b) / 2;
+      if (pc[m].dst <= lo) a = m;
+      else b = m;
+    }
+    for (uint32_t k = a; k < np && pc[k].dst < hi; k++) {
+      const ZsPiece q = pc[k];
+      const uint64_t s0 = max(lo, q.dst), e = min(hi, q.dst + q.len);
+      for (uint64_t i = s0 + t; i < e; i += DZ_T) dst[i] = src[q.src + (i - q.dst)];
+    }
+    return;
+  }
+  const uint64_t n = ck_hi > ck_lo ? ck_hi - ck_lo : 0u;
+  if (wrap == 2) {
+    zs_ck_tables(s_ck);
+    const uint32_t acc = zs_crc_block(src + ck_lo, 0, n, n, s_ck, s_red32);
+    if (t == 0) res[0] = zs_crc_final(acc, n);
+  } else if (wrap == 1) {
+    uint64_t A, B;
+    zs_adler_block(src + ck_lo, 0, n, n, s_red, &A, &B);
+    if (t == 0) res[0] = zs_adler_final(A, B, n);
+  } else if (t == 0) {
+    res[0] = 1u;
+  }
+}
+
+extern "C" void zs_launch_stored_call(const uint8_t *d_src, const ZsPiece *d_pc, uint32_t np, uint64_t total,
+                                      uint8_t *d_dst, uint64_t ck_lo, uint64_t ck_hi, uint32_t wrap, uint32_t *d_res,
+                                      hipStream_t st) {
+  const uint64_t ntile = (total + ZS_SC_TILE - 1) / ZS_SC_TILE;
+  hipLaunchKernelGGL(zs_stored_call_kernel, dim3((uint32_t)ntile + 1u), dim3(DZ_T), 0, st, d_src, d_pc, np, total, d_dst,
+                     ck_lo, ck_hi, wrap, d_res);
+}
+
+// ---------------------------------------------------------------------------
 // launcher
 // ---------------------------------------------------------------------------
 // per segment: d_dist16 / d_len8 DZ_SEG entries, d_bm DZ_BMW bitmap words, d_aux DZ_AUXW words

@@ -54,6 +54,9 @@ extern "C" int zs_launch_zdeflate(ZsDJobDev *d_jobs, uint32_t njobs, ZsDSegDev *
                                   uint32_t *d_flag, int has_slow, int has_fast, uint32_t max_regions, hipStream_t st,
                                   hipEvent_t *ev);
 extern "C" void zs_launch_dz_trailer(ZsDJobDev *d_jobs, uint32_t njobs, uint8_t *d_stage, hipStream_t st);
+extern "C" void zs_launch_stored_call(const uint8_t *d_src, const ZsPiece *d_pc, uint32_t np, uint64_t total,
+                                      uint8_t *d_dst, uint64_t ck_lo, uint64_t ck_hi, uint32_t wrap, uint32_t *d_res,
+                                      hipStream_t st);
 extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, ZsSegDev *d_segs, uint32_t nseg,
                                   ZsCJobDev *d_cjobs, uint32_t ncjobs, ZsChunkDev *d_units, uint32_t nunit_slots,
                                   uint16_t *d_scratch, uint32_t *d_tokens, ZsTokPool pool, uint32_t *d_tables,
@@ -1896,6 +1899,37 @@ int deflate_batch_locked(const zs_djob *jobs, uint32_t n, zs_result *results, ui
 // ---------------------------------------------------------------------------
 constexpr uint32_t ZD_BLOCK_SYMS = 16383, ZD_LOOK_HOST = 262;
 
+// a level-0 stream's call staging (ds_stored_call): pinned source / output and
+// their device copies, its own HIP stream; kept across deflateReset-style inits
+struct DsStage {
+  hipStream_t hs = nullptr;
+  uint8_t *h_src = nullptr, *h_dst = nullptr, *d_src = nullptr, *d_dst = nullptr;
+  size_t cap_hsrc = 0, cap_hdst = 0, cap_dsrc = 0, cap_ddst = 0;
+  DsStage() = default;
+  DsStage(const DsStage &) = delete;
+  DsStage &operator=(const DsStage &) = delete;
+  DsStage &operator=(DsStage &&o) noexcept {
+    std::swap(hs, o.hs);
+    std::swap(h_src, o.h_src);
+    std::swap(h_dst, o.h_dst);
+    std::swap(d_src, o.d_src);
+    std::swap(d_dst, o.d_dst);
+    std::swap(cap_hsrc, o.cap_hsrc);
+    std::swap(cap_hdst, o.cap_hdst);
+    std::swap(cap_dsrc, o.cap_dsrc);
+    std::swap(cap_ddst, o.cap_ddst);
+    return *this;
+  }
+  ~DsStage() {
+    if (hs) (void)hipStreamSynchronize(hs);
+    if (h_src) (void)hipHostFree(h_src);
+    if (h_dst) (void)hipHostFree(h_dst);
+    if (d_src) (void)hipFree(d_src);
+    if (d_dst) (void)hipFree(d_dst);
+    if (hs) (void)hipStreamDestroy(hs);
+  }
+};
+
 struct DStreamState {
   int inited = 0;
   int wbits = 15, level = 6, wrap = 0;
@@ -1926,6 +1960,12 @@ struct DStreamState {
   uint32_t adler = 1;          // strm->adler: check of the input the jobs have covered
   uint64_t checked = 0;        // bytes in `adler`
   uint64_t total_in = 0;
+  // level 0 (ds_stored_call): zlib's window positions strstart / block_start;
+  // buf holds the window's bytes [block_start, strstart), read but not yet
+  // framed; trl_done: the trailer is written (deflate.c negates s->wrap)
+  size_t z_strstart = 0, z_block_start = 0;
+  bool trl_done = false;
+  DsStage stage;
 };
 
 size_t dstream_run_min() {  // env ZS_DSTREAM_RUN_KB: Z_NO_FLUSH input gathered per job (default 0: every call)
@@ -2168,11 +2208,339 @@ size_t dstream_fast_max() {  // levels 0..3: input gathered per job (env ZS_DSTR
   return (size_t)std::max<long long>(64, kb) << 10;
 }
 
+// ---------------------------------------------------------------------------
+// Level 0: zlib's deflate() with deflate_stored (deflate.c, zlib 1.2.11), call
+// by call.  Stored block lengths follow each call's avail_out and flush and
+// zlib's window (strstart / block_start, slides of w_size): the host replays
+// that arithmetic on positions only (StoredPlan: the call's output as stream
+// byte ranges and header / marker bytes, in order) and the GPU writes the
+// bytes and the check of the input the call reads (zs_stored_call_kernel).
+// Output zlib leaves in its pending buffer waits in `out`, as for levels 1..9.
+// ---------------------------------------------------------------------------
+constexpr uint64_t ZS_MAX_STORED = 65535, ZS_PENDING_BUF = 65536;  // memLevel 8: lit_bufsize 16384 * 4
+
+struct StoredPlan {
+  struct Part {
+    bool lit;      // header / marker bytes (lit[off, off + len)), else stream bytes at offset off
+    uint64_t off;
+    uint64_t len;
+  };
+  std::vector<Part> parts;
+  std::vector<uint8_t> lit;
+  uint64_t total = 0;
+  void bytes(const uint8_t *p, size_t n) {
+    parts.push_back({true, lit.size(), n});
+    lit.insert(lit.end(), p, p + n);
+    total += n;
+  }
+  void stream(uint64_t off, uint64_t n) {
+    if (!n) return;
+    parts.push_back({false, off, n});
+    total += n;
+  }
+};
+
+// _tr_stored_block's header (trees.c): 3 bits (last, type 00) after the pending
+// bits, bi_windup, LEN, NLEN
+void ds_stored_hdr(DStreamState *s, StoredPlan &P, uint32_t last, uint32_t len) {
+  const uint32_t v = s->pend_byte | (last << s->pend_bits);
+  uint8_t h[6];
+  size_t n = 0;
+  h[n++] = (uint8_t)v;
+  if (s->pend_bits + 3 > 8) h[n++] = (uint8_t)(v >> 8);
+  h[n++] = (uint8_t)len;
+  h[n++] = (uint8_t)(len >> 8);
+  h[n++] = (uint8_t)~len;
+  h[n++] = (uint8_t)(~len >> 8);
+  P.bytes(h, n);
+  s->pend_bits = 0;
+  s->pend_byte = 0;
+}
+// _tr_align (trees.c): an empty static block, 10 bits; whole bytes leave (bi_flush)
+void ds_align(DStreamState *s, StoredPlan &P) {
+  const uint32_t v = s->pend_byte | (2u << s->pend_bits), nb = s->pend_bits + 10;
+  uint8_t h[3];
+  const uint32_t whole = nb / 8;
+  for (uint32_t k = 0; k < whole; k++) h[k] = (uint8_t)(v >> (8 * k));
+  P.bytes(h, whole);
+  s->pend_bits = nb % 8;
+  s->pend_byte = (uint8_t)((v >> (8 * whole)) & ((1u << s->pend_bits) - 1u));
+}
+
+// deflate_stored (deflate.c): 0 need_more, 1 block_done, 2 finish_started, 3
+// finish_done.  T0: stream offset of the call's input; *pos: input read so far;
+// avail_out: caller space left; *pend: generated bytes not delivered yet.
+int ds_stored_sim(DStreamState *s, StoredPlan &P, int flush, uint64_t T0, uint64_t in_len, uint64_t *pos,
+                  uint64_t *avail_out, uint64_t *pend) {
+  const uint64_t w_size = (uint64_t)1 << s->w, window_size = 2 * w_size;
+  uint64_t &strstart = s->z_strstart, &block_start = s->z_block_start;
+  auto avail_in = [&]() { return in_len - *pos; };
+  auto flush_pending = [&]() {
+    const uint64_t d = std::min(*pend, *avail_out);
+    *pend -= d;
+    *avail_out -= d;
+  };
+  // stream offset of window position i: the bytes before strstart are the last read
+  auto wabs = [&](uint64_t i) { return T0 + *pos - strstart + i; };
+  uint64_t min_block = std::min<uint64_t>(ZS_PENDING_BUF - 5, w_size);
+  uint32_t last = 0;
+  const uint64_t used0 = avail_in();
+  do {
+    uint64_t len = ZS_MAX_STORED;
+    uint64_t have = (s->pend_bits + 42) >> 3;
+    if (*avail_out < have) break;
+    have = *avail_out - have;
+    uint64_t left = strstart - block_start;
+    if (len > left + avail_in()) len = left + avail_in();
+    if (len > have) len = have;
+    if (len < min_block && ((len == 0 && flush != Z_FINISH) || flush == Z_NO_FLUSH || len != left + avail_in())) break;
+    last = flush == Z_FINISH && len == left + avail_in() ? 1u : 0u;
+    const uint64_t g0 = P.total;
+    ds_stored_hdr(s, P, last, (uint32_t)len);
+    *pend += P.total - g0;
+    flush_pending();  // the header fits: have >= its bytes
+    if (left) {
+      if (left > len) left = len;
+      P.stream(wabs(block_start), left);
+      *avail_out -= left;
+      block_start += left;
+      len -= left;
+    }
+    if (len) {  // read_buf straight to next_out
+      P.stream(T0 + *pos, len);
+      *avail_out -= len;
+      *pos += len;
+      // the window positions of bytes read this way are settled below
+      strstart += len;
+      block_start += len;
+    }
+  } while (last == 0);
+  // undo the provisional strstart moves of the direct copies, then zlib's window update
+  const uint64_t used = used0 - avail_in();
+  strstart -= used;
+  block_start -= used;
+  if (used) {
+    if (used >= w_size) {
+      strstart = w_size;  // the window is the last w_size bytes read
+    } else {
+      if (window_size - strstart <= used) strstart -= w_size;  // slide
+      strstart += used;
+    }
+    block_start = strstart;
+  }
+  if (last) return 3;
+  if (flush != Z_NO_FLUSH && flush != Z_FINISH && avail_in() == 0 && strstart == block_start) return 1;
+  // fill the window with the remaining input
+  uint64_t have = window_size - strstart - 1;
+  if (avail_in() > have && block_start >= w_size) {
+    block_start -= w_size;
+    strstart -= w_size;
+    have += w_size;
+  }
+  if (have > avail_in()) have = avail_in();
+  if (have) {
+    *pos += have;
+    strstart += have;
+  }
+  // a stored block from the window into the pending buffer
+  have = (s->pend_bits + 42) >> 3;
+  have = std::min<uint64_t>(ZS_PENDING_BUF - have, ZS_MAX_STORED);
+  min_block = std::min<uint64_t>(have, w_size);
+  const uint64_t left = strstart - block_start;
+  if (left >= min_block ||
+      ((left || flush == Z_FINISH) && flush != Z_NO_FLUSH && avail_in() == 0 && left <= have)) {
+    const uint64_t len = std::min(left, have);
+    last = flush == Z_FINISH && avail_in() == 0 && len == left ? 1u : 0u;
+    const uint64_t g0 = P.total;
+    ds_stored_hdr(s, P, last, (uint32_t)len);
+    P.stream(wabs(block_start), len);
+    *pend += P.total - g0;
+    block_start += len;
+    flush_pending();
+  }
+  return last ? 2 : 0;
+}
+
+template <typename T>
+int ds_grow_pinned(T **p, size_t *cap, size_t need) {
+  if (need <= *cap) return 0;
+  const size_t c = std::max(need, *cap + *cap / 2);
+  *cap = 0;
+  int r = grow_host(p, c);
+  if (!r) *cap = c;
+  return r;
+}
+
+// run a plan on the GPU: the call's output bytes into `gen`, the check of
+// in[0, n_in) into *check
+int ds_stored_run(DStreamState *s, const StoredPlan &P, const uint8_t *in, uint64_t n_in, uint64_t T0,
+                  std::vector<uint8_t> &gen, uint32_t *check) {
+  DsStage &g = s->stage;
+  if (!g.hs) HIP_OK(hipStreamCreateWithFlags(&g.hs, hipStreamNonBlocking));
+  // carried window bytes: stream [C0, T0)
+  const uint64_t C0 = T0 - s->buf.size();
+  std::vector<ZsPiece> pc;
+  pc.reserve(P.parts.size() + 4);
+  const auto a16 = [](uint64_t x) { return (x + 15) & ~(uint64_t)15; };
+  // staged source layout: [pieces | carried bytes | input | header bytes]
+  size_t np = 0;
+  for (const auto &q : P.parts) np += q.lit ? 1 : (q.off < T0 && q.off + q.len > T0 ? 2 : 1);
+  const uint64_t o_car = a16(np * sizeof(ZsPiece)), o_in = a16(o_car + s->buf.size()), o_lit = a16(o_in + n_in);
+  const uint64_t n_src = o_lit + P.lit.size();
+  uint64_t dst = 0;
+  for (const auto &q : P.parts) {
+    if (q.lit) {
+      pc.push_back({o_lit + q.off, dst, (uint32_t)q.len, 0});
+    } else {
+      uint64_t a = q.off, e = q.off + q.len;
+      if (a < T0) {
+        const uint64_t m = std::min(e, T0);
+        pc.push_back({o_car + (a - C0), dst, (uint32_t)(m - a), 0});
+        dst += m - a;
+        a = m;
+      }
+      if (a < e) pc.push_back({o_in + (a - T0), dst, (uint32_t)(e - a), 0});
+      dst += e - a;
+      continue;
+    }
+    dst += q.len;
+  }
+  const uint64_t o_res = a16(P.total);
+  int r;
+  if ((r = ds_grow_pinned(&g.h_src, &g.cap_hsrc, n_src)) || (r = ds_grow_pinned(&g.h_dst, &g.cap_hdst, o_res + 16)) ||
+      (r = ws_reserve_bytes(&g.d_src, &g.cap_dsrc, n_src)) || (r = ws_reserve_bytes(&g.d_dst, &g.cap_ddst, o_res + 16)))
+    return r;
+  std::memcpy(g.h_src, pc.data(), pc.size() * sizeof(ZsPiece));
+  if (!s->buf.empty()) std::memcpy(g.h_src + o_car, s->buf.data(), s->buf.size());
+  if (n_in) std::memcpy(g.h_src + o_in, in, n_in);
+  if (!P.lit.empty()) std::memcpy(g.h_src + o_lit, P.lit.data(), P.lit.size());
+  HIP_OK(hipMemcpyAsync(g.d_src, g.h_src, n_src, hipMemcpyHostToDevice, g.hs));
+  zs_launch_stored_call(g.d_src, reinterpret_cast<const ZsPiece *>(g.d_src), (uint32_t)pc.size(), P.total, g.d_dst, o_in,
+                        o_in + n_in, (uint32_t)s->wrap, reinterpret_cast<uint32_t *>(g.d_dst + o_res), g.hs);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipMemcpyAsync(g.h_dst, g.d_dst, o_res + 16, hipMemcpyDeviceToHost, g.hs));
+  HIP_OK(hipStreamSynchronize(g.hs));
+  gen.assign(g.h_dst, g.h_dst + P.total);
+  std::memcpy(check, g.h_dst + o_res, 4);
+  return 0;
+}
+
+// one deflate(strm, flush) call at level 0 (deflate.c deflate() around deflate_stored)
+int ds_stored_call(DStreamState *s, const uint8_t *in, unsigned in_len, uint8_t *out, unsigned out_len, int flush,
+                   unsigned *consumed, unsigned *produced) {
+  *consumed = 0;
+  *produced = 0;
+  if (flush < 0 || flush > Z_BLOCK || (s->status == 2 && flush != Z_FINISH)) return Z_STREAM_ERROR;
+  if (out_len == 0) return Z_BUF_ERROR;
+  auto rank = [](int f) { return f * 2 - (f > 4 ? 9 : 0); };
+  auto serve = [&]() {
+    const size_t k = std::min<size_t>(s->out.size() - s->served, out_len - *produced);
+    if (k) std::memcpy(out + *produced, s->out.data() + s->served, k);
+    s->served += k;
+    *produced += (unsigned)k;
+  };
+  const int old_flush = s->last_flush;
+  s->last_flush = flush;
+  if (s->served < s->out.size()) {  // flush as much pending output as possible
+    serve();
+    if (*produced == out_len) {
+      s->last_flush = -1;
+      return Z_OK;
+    }
+  } else if (in_len == 0 && rank(flush) <= rank(old_flush) && flush != Z_FINISH) {
+    return Z_BUF_ERROR;
+  }
+  if (s->status == 2 && in_len != 0) return Z_BUF_ERROR;
+  if (s->status == 0) {  // the header; compression starts with an empty pending buffer
+    ds_header(s);
+    s->status = 1;
+    serve();
+    if (s->served < s->out.size()) {
+      s->last_flush = -1;
+      return Z_OK;
+    }
+  }
+  const uint64_t T0 = s->total_in;
+  uint64_t avail_out = out_len - *produced, pend = 0, pos = 0;
+  StoredPlan P;
+  int ret = Z_OK;
+  bool trailer = false, done = false;
+  if (in_len || (flush != Z_NO_FLUSH && s->status != 2)) {
+    const int bstate = ds_stored_sim(s, P, flush, T0, in_len, &pos, &avail_out, &pend);
+    if (bstate >= 2) s->status = 2;
+    if (bstate == 0 || bstate == 2) {
+      if (avail_out == 0) s->last_flush = -1;
+      done = true;
+    } else if (bstate == 1) {
+      const uint64_t g0 = P.total;
+      if (flush == Z_PARTIAL_FLUSH) {
+        ds_align(s, P);
+      } else if (flush != Z_BLOCK) {
+        ds_stored_hdr(s, P, 0, 0);
+        if (flush == Z_FULL_FLUSH) s->z_strstart = s->z_block_start = 0;  // CLEAR_HASH, lookahead == 0
+      }
+      pend += P.total - g0;
+      const uint64_t d = std::min(pend, avail_out);
+      pend -= d;
+      avail_out -= d;
+      if (avail_out == 0) {
+        s->last_flush = -1;
+        done = true;
+      }
+    }
+  }
+  if (!done && flush == Z_FINISH) {
+    if (s->wrap == 0 || s->trl_done) ret = Z_STREAM_END;
+    else trailer = true;
+  }
+  // the GPU writes the plan's bytes and checks what the call read
+  std::vector<uint8_t> gen;
+  if (P.total || pos) {
+    uint32_t c = 0;
+    if (ds_stored_run(s, P, in, pos, T0, gen, &c)) return Z_STREAM_ERROR;
+    if (pos && s->wrap) s->adler = s->wrap == 2 ? crc32_join(s->adler, c, pos) : adler32_join(s->adler, c, pos);
+    s->checked += pos;
+  }
+  // the window's unframed bytes now: stream [strstart - block_start before the end of what was read)
+  {
+    const uint64_t T1 = T0 + pos, keep = s->z_strstart - s->z_block_start, C0 = T0 - s->buf.size();
+    std::vector<uint8_t> nb(keep);
+    for (uint64_t i = 0; i < keep; i++) {
+      const uint64_t a = T1 - keep + i;
+      nb[i] = a < T0 ? s->buf[a - C0] : in[a - T0];
+    }
+    s->buf.swap(nb);
+  }
+  s->total_in += pos;
+  *consumed = (unsigned)pos;
+  if (trailer) {  // deflate.c: the trailer into pending, then flush_pending
+    const uint32_t c = s->adler, isz = (uint32_t)s->total_in;
+    if (s->wrap == 2) {
+      const uint8_t t8[8] = {(uint8_t)c, (uint8_t)(c >> 8), (uint8_t)(c >> 16), (uint8_t)(c >> 24),
+                             (uint8_t)isz, (uint8_t)(isz >> 8), (uint8_t)(isz >> 16), (uint8_t)(isz >> 24)};
+      gen.insert(gen.end(), t8, t8 + 8);
+      pend += 8;
+    } else {
+      const uint8_t t4[4] = {(uint8_t)(c >> 24), (uint8_t)(c >> 16), (uint8_t)(c >> 8), (uint8_t)c};
+      gen.insert(gen.end(), t4, t4 + 4);
+      pend += 4;
+    }
+    pend -= std::min(pend, avail_out);
+    s->trl_done = true;
+    ret = pend ? Z_OK : Z_STREAM_END;
+  }
+  // delivered now: everything generated but the undelivered tail
+  ds_put(s, gen.data(), gen.size());
+  serve();
+  return ret;
+}
+
 // One zlib deflate(strm, flush) call (deflate.c deflate(): argument checks,
 // pending output first, Z_BUF_ERROR for a call that cannot progress -- the
 // last_flush ranks --, the header at the first call, all input consumed).
 int dstream_call(DStreamState *s, const uint8_t *in, unsigned in_len, uint8_t *out, unsigned out_len, int flush,
                  unsigned *consumed, unsigned *produced) {
+  if (s->level == 0) return ds_stored_call(s, in, in_len, out, out_len, flush, consumed, produced);
   *consumed = 0;
   *produced = 0;
   if (flush < 0 || flush > Z_BLOCK || (s->status == 2 && flush != Z_FINISH)) return Z_STREAM_ERROR;
@@ -2256,7 +2624,10 @@ int dstream_init(DStreamState *s, int level, int wbits) {
     std::lock_guard<std::mutex> lk(g_mu);
     if (ws_init()) return Z_STREAM_ERROR;
   }
+  DsStage keep;
+  keep = std::move(s->stage);
   *s = DStreamState();
+  s->stage = std::move(keep);
   s->inited = 1;
   s->level = level;
   s->wbits = wbits;
@@ -2283,7 +2654,10 @@ int dhandle_process(uintptr_t hp, uintptr_t in_ptr, unsigned in_len, uintptr_t o
   return (int)((prod & 0x00ffffffu) | ((unsigned)(ret & 0xff) << 24));
 }
 // deflateEnd: Z_DATA_ERROR when the stream was left unfinished (deflate.c)
-int dstream_end_code(const DStreamState *s) { return s->inited && s->status == 1 ? Z_DATA_ERROR : Z_OK; }
+// (a raw stream starts in BUSY_STATE: deflateResetKeep)
+int dstream_end_code(const DStreamState *s) {
+  return s->inited && (s->status == 1 || (s->status == 0 && s->wrap == 0)) ? Z_DATA_ERROR : Z_OK;
+}
 }  // namespace
 
 // ===========================================================================

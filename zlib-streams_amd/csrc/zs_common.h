@@ -237,6 +237,13 @@ struct ZsDJobDev {
 };
 #define ZD_SLOW 1u
 #define ZD_FAST 2u
+// Level-0 stream calls (zs_stored_call_kernel): one copy piece of the call's
+// output -- `len` bytes from the staged source at `src` to output offset `dst`
+// (pieces are contiguous in dst order)
+struct ZsPiece {
+  uint64_t src, dst;
+  uint32_t len, pad;
+};
 // ZsDJobDev::term -- the end of a job's bits, as zlib's deflate() ends a call:
 #define ZS_DT_FINAL 0u    // Z_FINISH: last block BFINAL = 1 (an empty one if needed), trailer
 #define ZS_DT_SYNC 1u     // Z_SYNC_FLUSH / Z_FULL_FLUSH: blocks not final, empty stored block 00 00 FF FF
