@@ -486,6 +486,8 @@ def _compare_calls(zs, level, wb, calls, out_len):
         a = g.call1(chunk, out_len, fl)
         b = h.call(chunk, out_len, fl)
         assert a == b, (level, wb, i, fl, len(chunk), a[:2], b[:2], len(a[2]), len(b[2]))
+        # strm->adler after every call: zlib's read_buf checks each byte it reads
+        assert g.s.adler == h.s.adler & 0xffffffff, (level, wb, i, g.s.adler, h.s.adler)
         total += a[2]
     assert g.s.adler == h.s.adler & 0xffffffff
     assert g.end() == h.end()
@@ -893,3 +895,20 @@ def test_reference_roundtrip_inputs_through_streams(zs, level):
             assert a == b, (len(data), level, wb)
             comp = b"".join(t[2] for t in a)
             assert zs.decompress(comp, {-15: "deflate-raw", 31: "gzip"}[wb], 1024) == data
+
+
+@pytest.mark.parametrize("out_buffer", [1024, 4096])
+def test_compression_stream_small_out_buffer_calls_are_zlibs(zs, out_buffer):
+    """CompressionStreamZlib with outBuffer 1 / 4 KiB (zlib-streams.js:17, passed to
+    every deflate_process, :83 / :122): blocks larger than the output space leave
+    zlib's pending output for later calls, a call that only drains it consumes
+    nothing (and the wrapper's write loop stops on 0), Z_FINISH drains in
+    outBuffer pieces; every call's (code, consumed, produced bytes) equals host
+    zlib's, levels 1 / 4 / 6 / 9, raw / zlib / gzip."""
+    data = corpus.stream(42, 500_000) + bytes(random.Random(4).getrandbits(8) for _ in range(60000))
+    for level in (1, 4, 6, 9):
+        for wb in (-15, 15, 31):
+            a = _js_compress(_GpuHandle(zs, True, wb, level), data, out_buffer)
+            b = _js_compress(_HostDeflateHandle(wb, level), data, out_buffer)
+            assert [t[:2] + (len(t[2]),) for t in a] == [t[:2] + (len(t[2]),) for t in b], (level, wb, out_buffer)
+            assert a == b

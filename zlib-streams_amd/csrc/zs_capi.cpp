@@ -2425,6 +2425,37 @@ int ds_stored_run(DStreamState *s, const StoredPlan &P, const uint8_t *in, uint6
   return 0;
 }
 
+// strm->adler after a zlib-ABI deflate() call: zlib's read_buf updates it with
+// every byte it reads, so the input this call appended but no GPU job has
+// checked yet (buf[ck_from, end)) gets its check now (a check-only launch)
+int ds_check_rest(DStreamState *s) {
+  const uint64_t n = s->buf.size() - s->ck_from;
+  if (!n || !s->wrap) {
+    s->checked += n;
+    s->ck_from = s->buf.size();
+    return 0;
+  }
+  DsStage &g = s->stage;
+  if (!g.hs) HIP_OK(hipStreamCreateWithFlags(&g.hs, hipStreamNonBlocking));
+  int r;
+  if ((r = ds_grow_pinned(&g.h_src, &g.cap_hsrc, n)) || (r = ds_grow_pinned(&g.h_dst, &g.cap_hdst, 16)) ||
+      (r = ws_reserve_bytes(&g.d_src, &g.cap_dsrc, n)) || (r = ws_reserve_bytes(&g.d_dst, &g.cap_ddst, 16)))
+    return r;
+  std::memcpy(g.h_src, s->buf.data() + s->ck_from, n);
+  HIP_OK(hipMemcpyAsync(g.d_src, g.h_src, n, hipMemcpyHostToDevice, g.hs));
+  zs_launch_stored_call(g.d_src, nullptr, 0, 0, g.d_dst, 0, n, (uint32_t)s->wrap, reinterpret_cast<uint32_t *>(g.d_dst),
+                        g.hs);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipMemcpyAsync(g.h_dst, g.d_dst, 4, hipMemcpyDeviceToHost, g.hs));
+  HIP_OK(hipStreamSynchronize(g.hs));
+  uint32_t c;
+  std::memcpy(&c, g.h_dst, 4);
+  s->adler = s->wrap == 2 ? crc32_join(s->adler, c, n) : adler32_join(s->adler, c, n);
+  s->checked += n;
+  s->ck_from = s->buf.size();
+  return 0;
+}
+
 // one deflate(strm, flush) call at level 0 (deflate.c deflate() around deflate_stored)
 int ds_stored_call(DStreamState *s, const uint8_t *in, unsigned in_len, uint8_t *out, unsigned out_len, int flush,
                    unsigned *consumed, unsigned *produced) {
@@ -2900,14 +2931,15 @@ int ZEXPORT deflate(z_streamp strm, int flush) {
   if (strm->avail_out == 0) return Z_BUF_ERROR;
   DStreamState *s = reinterpret_cast<DStreamState *>(strm->state);
   unsigned cons = 0, prod = 0;
-  const int ret = dstream_call(s, strm->next_in, strm->avail_in, strm->next_out, strm->avail_out, flush, &cons, &prod);
+  int ret = dstream_call(s, strm->next_in, strm->avail_in, strm->next_out, strm->avail_out, flush, &cons, &prod);
+  if (ret >= Z_OK && s->level > 0 && ds_check_rest(s)) ret = Z_STREAM_ERROR;  // strm->adler covers every byte read
   strm->next_in += cons;
   strm->avail_in -= cons;
   strm->total_in += cons;
   strm->next_out += prod;
   strm->avail_out -= prod;
   strm->total_out += prod;
-  if (s->checked) strm->adler = s->adler;  // the input the GPU jobs have checked so far
+  if (s->checked) strm->adler = s->adler;  // the check of all input read so far (GPU)
   return ret;
 }
 int ZEXPORT deflateEnd(z_streamp strm) {
