@@ -912,3 +912,48 @@ def test_compression_stream_small_out_buffer_calls_are_zlibs(zs, out_buffer):
             b = _js_compress(_HostDeflateHandle(wb, level), data, out_buffer)
             assert [t[:2] + (len(t[2]),) for t in a] == [t[:2] + (len(t[2]),) for t in b], (level, wb, out_buffer)
             assert a == b
+
+
+@pytest.mark.parametrize("level", [1, 3, 4, 6, 9])
+def test_deflate_output_full_consumed_is_zlibs(zs, level):
+    """zlib's pull-on-demand: deflate() returns right after the block flush that
+    fills avail_out, having read only what fill_window had read by then
+    (deflate.c deflate_slow / deflate_fast, FLUSH_BLOCK, fill_window).  Calls
+    with large inputs (100 KB .. 1.2 MB) and small output spaces (1 .. 40 KB),
+    the caller passing the unconsumed rest again (zlib's calling convention),
+    every flush value, raw / zlib / gzip; plus a header that does not fit (out
+    1 byte): every call's (ret, consumed, produced bytes) and strm->adler equal
+    host zlib's."""
+    import libz_ref
+    rng = random.Random(700 + level)
+    for wb in (-15, 15, 31):
+        data = _stream_data(rng, 2_500_000 if level >= 4 else 900_000)
+        g = _GpuDeflate(zs, level, wb)
+        h = libz_ref.Deflater(level, wb)
+        off, k, out = 0, 0, bytearray()
+        first = True
+        while True:
+            fin = off >= len(data)
+            n = 0 if fin else rng.choice([100_000, 300_000, 1_200_000])
+            chunk = data[off:off + n]
+            fl = 4 if fin else rng.choice([0, 0, 0, 2, 1, 5, 3])
+            rest = chunk
+            while True:
+                space = 1 if first else rng.choice([1000, 5000, 17000, 40000])
+                first = False
+                a = g.call1(rest, space, fl)
+                b = h.call(rest, space, fl)
+                assert a == b, (wb, k, fl, len(rest), space, a[:2], b[:2], len(a[2]), len(b[2]))
+                assert g.s.adler == h.s.adler & 0xffffffff, (wb, k)
+                k += 1
+                out += a[2]
+                rest = rest[a[1]:]
+                if a[0] != 0 or (not rest and len(a[2]) < space and fl != 4):
+                    break
+                assert k < 100000
+            off += n
+            if fin:
+                assert a[0] == 1, a[:2]
+                break
+        assert g.end() == h.end()
+        assert zlib.decompress(bytes(out), wb) == data

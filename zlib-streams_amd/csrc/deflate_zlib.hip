@@ -1639,12 +1639,50 @@ __device__ uint64_t zd_syms_before(const ZsDSegDev *segs, const ZsDJobDev &jb, c
 // full lookahead (an exact loop top and state, from the fix-up), with the
 // symbols from there to the first unsent one as its skip; with none, at this
 // job's own entry.
+// where the next segment of a stream resumes when the first K blocks of job
+// jb (nb of them parsed) are sent: a loop top T in state sT with `skip`
+// symbols from T already sent (deflate_slow: the last region exit at or before
+// the first unsent symbol whose walk saw full lookahead, from the fix-up; with
+// none, the job's own entry)
+__device__ void zd_cut_at(const ZsDJobDev &jb, uint32_t nb, uint32_t K, const ZsDSegDev *__restrict__ segs,
+                          const uint32_t *__restrict__ S, const ZsZBlkDev *__restrict__ blks, uint64_t *T_out,
+                          uint32_t *sT_out, uint64_t *skip_out) {
+  const uint64_t L = jb.in_len;
+  if (jb.exact == ZD_FAST) {  // every token start is a loop top: restart at the first unsent symbol
+    *T_out = K < nb ? blks[jb.zblk0 + K].first : jb.fstop;
+    *sT_out = ZD_STATE_A;
+    *skip_out = 0;
+    return;
+  }
+  uint64_t T = jb.pstart, sT = jb.pstate, skip = jb.skip + (uint64_t)K * ZD_BLOCK;
+  if (K < nb) {
+    const uint64_t P0 = blks[jb.zblk0 + K].first;
+    for (int32_t r = (int32_t)min<uint64_t>(jb.nseg - 1, P0 / ZD_REG); r >= 0; r--) {
+      const ZsDSegDev &sg = segs[jb.seg0 + r];
+      const uint64_t x = sg.zx[0];
+      const uint32_t xs = sg.zs[0];
+      if (sg.start + sg.len + ZD_LOOK + ZD_MAXM <= L && x - (xs & 1u) <= P0 && x >= jb.pstart) {
+        T = x;
+        sT = xs;
+        skip = jb.skip + (uint64_t)K * ZD_BLOCK - zd_syms_before(segs, jb, S, x - (xs & 1u));
+        break;
+      }
+    }
+  }
+  *T_out = T;
+  *sT_out = (uint32_t)sT;
+  *skip_out = skip;
+}
+
 __global__ void zs_zd_cut_kernel(ZsDJobDev *__restrict__ jobs, uint32_t njobs, const ZsDSegDev *__restrict__ segs,
                                  const uint32_t *__restrict__ bm, ZsZBlkDev *__restrict__ blks) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= njobs) return;
   const ZsDJobDev jb = jobs[j];
-  if (!jb.exact || jb.term != ZS_DT_CUT) return;
+  if (!jb.exact) return;
+  jobs[j].nzblk0 = jb.nzblk;
+  if (jb.exact == ZD_FAST) jobs[j].fstop = jb.cut_pos;
+  if (jb.term != ZS_DT_CUT) return;
   const uint32_t *S = bm + jb.bm0;
   const uint64_t L = jb.in_len;
   if (jb.exact == ZD_FAST) {
@@ -1691,6 +1729,118 @@ __global__ void zs_zd_cut_kernel(ZsDJobDev *__restrict__ jobs, uint32_t njobs, c
   jobs[j].cut_pos = T;
   jobs[j].cut_state = (uint32_t)sT;
   jobs[j].cut_skip = skip;
+}
+
+// first loop top at or after y of the job's parse (L if none).  deflate_slow
+// (zlib deflate.c): a literal or match starting at s is tallied in the
+// iteration at s + 1 and an emitted match moves the loop to its end, so the
+// loop tops are {y : y - 1 or y is a token start}.  deflate_fast: the token
+// starts (its CUT jobs know them up to fstop, their stop).
+__device__ uint64_t zd_looptop_ge(const ZsDJobDev &jb, const uint32_t *__restrict__ S, uint64_t y) {
+  const uint64_t L = jb.in_len;
+  const bool fast = jb.exact == ZD_FAST;
+  const uint64_t lim = fast && jb.term == ZS_DT_CUT ? min(L, jb.fstop) : L;
+  if (y >= lim) return fast ? max(y, lim) : L;
+  if (!fast && y > 0 && zd_getbit(S, y - 1)) return y;
+  uint64_t w = y >> 5;
+  uint32_t m = S[w] & (~0u << (y & 31u));
+  while (!m) {
+    if (++w * 32u >= lim) return lim;
+    m = S[w];
+  }
+  return min(lim, w * 32u + (uint64_t)__builtin_ctz(m));
+}
+
+// zlib's reading during one deflate() call up to loop top t_lim (fill_window at
+// every loop top whose lookahead is < MIN_LOOKAHEAD: slide by w_size once
+// strstart - window start >= w_size + MAX_DIST, then read up to window_size);
+// returns the read end (job offset) and moves *zb (stream offset).  A call that
+// runs out of input stops at its first loop top with a short lookahead (NO_FLUSH,
+// zs_zd_cut_kernel's rule) or processes every loop top to the end (a flush),
+// attempting the fill (so the slide) at each.
+__device__ uint64_t zd_read_model(const ZsDJobDev &jb, const uint32_t *__restrict__ S, uint64_t t_lim, bool early,
+                                  uint64_t *zb_io) {
+  const uint64_t L = jb.in_len, W = 1ull << jb.wbits, TH = 2 * W - ZD_LOOK, a0 = jb.abs0;
+  uint64_t zb = *zb_io, rd = jb.rd0, lo = 0;
+  if (jb.rtop == ~0ull) {
+    rd = min(L, zb + 2 * W - a0);  // the fill at the call's first loop top (its slide already decided)
+  } else {
+    lo = jb.rtop;
+    if (rd - min(rd, jb.rtop) < ZD_LOOK && jb.rtop <= t_lim) {
+      if (a0 + jb.rtop >= zb + TH) zb += W;
+      rd = min(L, zb + 2 * W - a0);
+    }
+  }
+  for (int guard = 0; guard < (1 << 20); guard++) {
+    const uint64_t y = max(lo, rd >= ZD_LOOK - 1 ? rd - (ZD_LOOK - 1) : 0ull);
+    const uint64_t t = zd_looptop_ge(jb, S, y);
+    if (t > t_lim) break;
+    if (rd < L) {
+      if (a0 + t >= zb + TH) zb += W;
+      rd = min(L, zb + 2 * W - a0);
+      lo = t + 1;
+      continue;
+    }
+    // no input left: fill attempts (slide checks) at every loop top from t on
+    const uint64_t tc = early ? t_lim : (jb.term == ZS_DT_CUT ? t : L);
+    if (a0 + tc >= zb + TH) zb += W;
+    break;
+  }
+  *zb_io = zb;
+  return rd;
+}
+
+// zlib's pull-on-demand (after the layout: block bit ends are known): the
+// first block whose flush leaves at least lim_bytes of the job's output makes
+// deflate() return right there -- blocks flushed inside the loop (all of a
+// CUT job's, all but the last of a flushing job's).  The job then ends as a
+// CUT after that block (no terminator, no trailer), resuming where the next
+// loop top is, and the read model gives what zlib had read.
+__global__ void zs_zd_limit_kernel(ZsDJobDev *__restrict__ jobs, uint32_t njobs, const ZsDSegDev *__restrict__ segs,
+                                   const uint32_t *__restrict__ bm, const ZsZBlkDev *__restrict__ blks) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= njobs) return;
+  const ZsDJobDev jb = jobs[j];
+  if (!jb.exact || jb.rd0 == ~0ull) return;  // not a stream segment (the batch API)
+  const uint32_t *S = bm + jb.bm0;
+  const uint32_t nb = jb.nzblk;
+  uint32_t stop = 0xffffffffu;
+  if (jb.lim_bytes != ~0ull) {
+    const uint32_t ncand = jb.term == ZS_DT_CUT ? nb : (nb ? nb - 1u : 0u);
+    for (uint32_t i = 0; i < ncand; i++) {
+      const uint64_t e = i + 1 < nb ? blks[jb.zblk0 + i + 1].bitoff : jb.endbit;
+      if (e / 8u >= jb.lim_bytes) {
+        stop = i;
+        break;
+      }
+    }
+  }
+  uint64_t zb = jb.zb;
+  if (stop == 0xffffffffu) {
+    jobs[j].early = 0;
+    jobs[j].rd_out = zd_read_model(jb, S, jb.in_len, false, &zb);
+    jobs[j].zb = zb;
+    return;
+  }
+  const ZsZBlkDev &b = blks[jb.zblk0 + stop];
+  const uint64_t t_i = b.top;
+  jobs[j].early = 1;
+  jobs[j].early_k = stop + 1;
+  jobs[j].rd_out = zd_read_model(jb, S, t_i, true, &zb);
+  jobs[j].zb = zb;
+  jobs[j].next_top = zd_looptop_ge(jb, S, t_i + 1);
+  jobs[j].endbit = stop + 1 < nb ? blks[jb.zblk0 + stop + 1].bitoff : jb.endbit;
+  jobs[j].term = ZS_DT_CUT;
+  jobs[j].trl = 0;
+  jobs[j].total_out = (jobs[j].endbit + 7u) / 8u;
+  uint64_t T, skip;
+  uint32_t sT;
+  zd_cut_at(jb, jb.nzblk0, stop + 1, segs, S, blks, &T, &sT, &skip);
+  jobs[j].cut_pos = T;
+  jobs[j].cut_state = sT;
+  jobs[j].cut_skip = skip;
+  jobs[j].cut_open = 0;
+  jobs[j].nzblk = stop + 1;
 }
 
 // ---------------------------------------------------------------------------
@@ -2317,6 +2467,7 @@ extern "C" int zs_launch_zdeflate(ZsDJobDev *d_jobs, uint32_t njobs, ZsDSegDev *
   hipLaunchKernelGGL(zs_zd_layout_kernel, dim3(njobs), dim3(1024), 0, st, d_jobs, d_blks, d_stage);
   hipLaunchKernelGGL(zs_zd_emit_kernel, dim3(nblk_slots), dim3(ZD_TT), 0, st, d_jobs, d_blks, d_ma, d_mb, d_bm, d_aux,
                      d_stage);
+  hipLaunchKernelGGL(zs_zd_limit_kernel, dim3((njobs + 63) / 64), dim3(64), 0, st, d_jobs, njobs, d_segs, d_bm, d_blks);
   if (ev) (void)hipEventRecord(ev[3], st);
   return 0;
 }

@@ -1649,6 +1649,8 @@ struct DzSpec {
   bool fast = false;       // ZS_F_DEFLATE_FAST
   uint32_t term = ZS_DT_FINAL, hdr = 1, trl = 1, bit0 = 0, pstate = ZD_STATE_A_HOST;
   uint64_t pstart = 0, skip = 0, abs0 = 0, ck0 = 0;
+  // stream segments: zlib's pull-on-demand (ZsDJobDev lim_bytes / zb / rd0 / rtop)
+  uint64_t lim_bytes = ~0ull, zb = 0, rd0 = ~0ull, rtop = ~0ull;
   // levels 1..3 (deflate_fast): which history positions [0, pstart) zlib had
   // inserted into its hash chains (bit q of word q / 32), and whether to
   // return the bits of the window before the next segment's entry
@@ -1663,6 +1665,8 @@ struct DzSpec {
   uint32_t check = 0;
   uint64_t cut_pos = 0, cut_skip = 0, cut_open = 0;
   uint32_t cut_state = 0;
+  bool early = false;  // deflate() returned after a block flush filled the output (the job ends as a cut)
+  uint64_t rd_out = 0, zb_out = 0, next_top = 0;
 };
 
 int dz_run(DzSpec *sp, uint32_t n, bool dev) {
@@ -1713,6 +1717,10 @@ int dz_run(DzSpec *sp, uint32_t n, bool dev) {
     jd.skip = s.skip;
     jd.abs0 = s.abs0;
     jd.ck0 = s.ck0;
+    jd.lim_bytes = s.lim_bytes;
+    jd.zb = s.zb;
+    jd.rd0 = s.rd0;
+    jd.rtop = s.rtop;
     jd.seg0 = (uint32_t)nseg;
     jd.nseg = (uint32_t)std::max<uint64_t>(1, (jd.in_len + DZ_SEG_HOST - 1) / DZ_SEG_HOST);
     jd.stage = stage_total;
@@ -1818,6 +1826,10 @@ int dz_run(DzSpec *sp, uint32_t n, bool dev) {
     s.cut_state = jd.cut_state;
     s.cut_skip = jd.cut_skip;
     s.cut_open = jd.cut_open;
+    s.early = jd.early != 0;
+    s.rd_out = jd.rd_out;
+    s.zb_out = jd.zb;
+    s.next_top = jd.next_top;
     const uint64_t give = std::min<uint64_t>(jd.total_out, s.out_cap);
     if (give)
       HIP_OK(hipMemcpyAsync(s.out, g_dz.d_stage + jd.stage, give, dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, st));
@@ -1965,6 +1977,11 @@ struct DStreamState {
   // framed; trl_done: the trailer is written (deflate.c negates s->wrap)
   size_t z_strstart = 0, z_block_start = 0;
   bool trl_done = false;
+  // levels 1..9, zlib's reading (fill_window): its window start zb (stream
+  // offset since the window restart) and, after a call that returned on a
+  // full output, the loop top the next call resumes at (stream offset; NONE:
+  // the next call fills at once)
+  uint64_t zb = 0, rtop = UINT64_MAX;
   DsStage stage;
 };
 
@@ -2029,6 +2046,8 @@ DzSpec ds_spec(const DStreamState *s, uint32_t term) {
   j.skip = s->skip;
   j.abs0 = s->abs;
   j.ck0 = s->ck_from;
+  j.zb = s->zb;
+  j.rtop = s->rtop == UINT64_MAX ? ~0ull : s->rtop - s->abs;
   if (s->exact && s->level <= 3) {
     j.ins = s->ins.data();
     j.ins_words = s->ins.size();
@@ -2050,18 +2069,23 @@ void ds_after(DStreamState *s, const DzSpec &j, const uint8_t *bytes, bool full)
   if (term == ZS_DT_PARTIAL || term == ZS_DT_BLOCK || term == ZS_DT_CUT) {
     const size_t whole = (size_t)(bits / 8);
     s->pend_bits = (uint32_t)(bits & 7u);
-    s->pend_byte = s->pend_bits ? o[whole] : 0;
+    s->pend_byte = s->pend_bits ? (uint8_t)(o[whole] & ((1u << s->pend_bits) - 1u)) : 0;
     o.resize(whole);
   } else {
     s->pend_bits = 0;
     s->pend_byte = 0;
   }
   const uint64_t n = s->buf.size() - s->ck_from;
-  if (s->wrap && n) {
+  if (j.early) {
+    // (ds_job checked what zlib read and cut buf there)
+  } else if (s->wrap && n) {
     s->adler = s->checked == 0 ? j.check
                                : (s->wrap == 2 ? crc32_join(s->adler, j.check, n) : adler32_join(s->adler, j.check, n));
   }
-  s->checked += n;
+  if (!j.early) s->checked += n;
+  // zlib's reading: its window start after the call, and where it resumes
+  s->zb = j.zb_out;
+  s->rtop = j.early ? s->abs + j.next_top : UINT64_MAX;
   if (term == ZS_DT_FINAL && s->wrap) {  // the whole input's trailer
     const uint32_t c = s->adler, isz = (uint32_t)s->total_in;
     if (s->wrap == 2) {
@@ -2086,8 +2110,9 @@ void ds_after(DStreamState *s, const DzSpec &j, const uint8_t *bytes, bool full)
     s->skip = j.cut_skip;
     // new bytes before a call can complete the open block: each symbol it
     // still lacks starts at a distinct position past the last loop top zlib
-    // processed, and needs the lookahead past it
-    s->need = (size_t)(ZD_BLOCK_SYMS - std::min<uint64_t>(ZD_BLOCK_SYMS, j.cut_open));
+    // processed, and needs the lookahead past it (after a call that returned on
+    // a full output, zlib has read input it has not parsed: always a job)
+    s->need = j.early ? 0 : (size_t)(ZD_BLOCK_SYMS - std::min<uint64_t>(ZD_BLOCK_SYMS, j.cut_open));
   } else {
     T = s->buf.size();
     s->state = ZD_STATE_A_HOST;
@@ -2100,6 +2125,10 @@ void ds_after(DStreamState *s, const DzSpec &j, const uint8_t *bytes, bool full)
     s->buf.erase(s->buf.begin(), s->buf.begin() + (ptrdiff_t)T);
     s->hist = 0;
     s->abs = full ? 0 : s->abs + T;
+    if (full) {  // deflate.c CLEAR_HASH, strstart = 0: the window starts over here
+      s->zb = 0;
+      s->rtop = UINT64_MAX;
+    }
   } else {
     const size_t h = std::min(T, wsize);
     if (s->level <= 3) {  // deflate_fast: which window positions are in the hash chains
@@ -2189,17 +2218,70 @@ int dq_submit(DzCall *c) {
   return c->err;
 }
 
-// run the stream's next job (term) on the GPU and take its output
-int ds_job(DStreamState *s, uint32_t term, bool full) {
+int ds_check_range(DStreamState *s, uint64_t lo, uint64_t hi);
+
+// run the stream's next job (term) on the GPU and take its output.  rd0: buf
+// offset where this call's input starts; room: output bytes of the job the
+// call's output space takes.  When zlib's deflate() would have returned after
+// a block flush filled that space (the job's `early`), it had read only up to
+// rd_out: the rest of the call's input is given back (*dropped bytes).
+int ds_job(DStreamState *s, uint32_t term, bool full, uint64_t rd0, uint64_t room, uint64_t *dropped) {
+  *dropped = 0;
   DzSpec j = ds_spec(s, term);
+  j.rd0 = rd0;
+  j.lim_bytes = room;
   std::vector<uint8_t> bytes((size_t)dz_bound(s->buf.size(), s->wrap) + 64);
   j.out = bytes.data();
   j.out_cap = bytes.size();
   DzCall c;
   c.spec = &j;
   if (dq_submit(&c) || j.ret != Z_STREAM_END) return Z_STREAM_ERROR;
+  if (j.early) {
+    const uint64_t rd = std::min<uint64_t>(j.rd_out, s->buf.size());
+    if (rd < s->ck_from || ds_check_range(s, s->ck_from, rd)) return Z_STREAM_ERROR;
+    *dropped = s->buf.size() - rd;
+    s->buf.resize((size_t)rd);
+    s->total_in -= *dropped;
+    s->fresh -= std::min<size_t>(s->fresh, *dropped);
+    s->ck_from = (size_t)rd;
+    j.term = ZS_DT_CUT;  // the job ends after its last flushed block
+    full = false;
+  }
   ds_after(s, j, bytes.data(), full);
   return Z_OK;
+}
+
+// zlib's reading during a Z_NO_FLUSH call that completes no block (no job):
+// fill_window at the call's first loop top, then whenever the parse passes
+// the read end - MIN_LOOKAHEAD, and a last attempt where the parse stops.
+// Each slide is decided by where that loop top falls, known here only to
+// within the longest gap between loop tops (258): false when that decides it
+// either way (the call then runs a job, whose read model knows the loop tops).
+bool ds_model_nojob(DStreamState *s, uint64_t rd, uint64_t end) {
+  const uint64_t W = (uint64_t)1 << s->w, TH = 2 * W - ZD_LOOK_HOST;
+  uint64_t zb = s->zb, lo = 0;
+  auto decide = [&](uint64_t y) -> int { return y >= zb + TH ? 1 : (y + 258 < zb + TH ? 0 : -1); };
+  if (s->rtop == UINT64_MAX) {
+    rd = std::min(end, zb + 2 * W);
+  } else {
+    lo = s->rtop;
+    if (rd - std::min(rd, s->rtop) < ZD_LOOK_HOST) {
+      if (s->rtop >= zb + TH) zb += W;
+      rd = std::min(end, zb + 2 * W);
+    }
+  }
+  for (int guard = 0; guard < (1 << 20); guard++) {
+    const uint64_t y = std::max(lo, rd >= ZD_LOOK_HOST - 1 ? rd - (ZD_LOOK_HOST - 1) : 0);
+    const int d = decide(y);
+    if (d < 0) return false;
+    if (d) zb += W;
+    if (rd >= end) break;
+    rd = std::min(end, zb + 2 * W);
+    lo = y + 1;
+  }
+  s->zb = zb;
+  s->rtop = UINT64_MAX;
+  return true;
 }
 
 size_t dstream_fast_max() {  // levels 0..3: input gathered per job (env ZS_DSTREAM_MAX_KB, default 64 MiB)
@@ -2428,11 +2510,10 @@ int ds_stored_run(DStreamState *s, const StoredPlan &P, const uint8_t *in, uint6
 // strm->adler after a zlib-ABI deflate() call: zlib's read_buf updates it with
 // every byte it reads, so the input this call appended but no GPU job has
 // checked yet (buf[ck_from, end)) gets its check now (a check-only launch)
-int ds_check_rest(DStreamState *s) {
-  const uint64_t n = s->buf.size() - s->ck_from;
+int ds_check_range(DStreamState *s, uint64_t lo, uint64_t hi) {
+  const uint64_t n = hi - lo;
   if (!n || !s->wrap) {
     s->checked += n;
-    s->ck_from = s->buf.size();
     return 0;
   }
   DsStage &g = s->stage;
@@ -2441,7 +2522,7 @@ int ds_check_rest(DStreamState *s) {
   if ((r = ds_grow_pinned(&g.h_src, &g.cap_hsrc, n)) || (r = ds_grow_pinned(&g.h_dst, &g.cap_hdst, 16)) ||
       (r = ws_reserve_bytes(&g.d_src, &g.cap_dsrc, n)) || (r = ws_reserve_bytes(&g.d_dst, &g.cap_ddst, 16)))
     return r;
-  std::memcpy(g.h_src, s->buf.data() + s->ck_from, n);
+  std::memcpy(g.h_src, s->buf.data() + lo, n);
   HIP_OK(hipMemcpyAsync(g.d_src, g.h_src, n, hipMemcpyHostToDevice, g.hs));
   zs_launch_stored_call(g.d_src, nullptr, 0, 0, g.d_dst, 0, n, (uint32_t)s->wrap, reinterpret_cast<uint32_t *>(g.d_dst),
                         g.hs);
@@ -2452,8 +2533,12 @@ int ds_check_rest(DStreamState *s) {
   std::memcpy(&c, g.h_dst, 4);
   s->adler = s->wrap == 2 ? crc32_join(s->adler, c, n) : adler32_join(s->adler, c, n);
   s->checked += n;
-  s->ck_from = s->buf.size();
   return 0;
+}
+int ds_check_rest(DStreamState *s) {
+  const int r = ds_check_range(s, s->ck_from, s->buf.size());
+  if (!r) s->ck_from = s->buf.size();
+  return r;
 }
 
 // one deflate(strm, flush) call at level 0 (deflate.c deflate() around deflate_stored)
@@ -2597,33 +2682,45 @@ int dstream_call(DStreamState *s, const uint8_t *in, unsigned in_len, uint8_t *o
     return Z_BUF_ERROR;
   }
   if (s->status == 2 && in_len != 0) return Z_BUF_ERROR;
-  if (s->status == 0) {
+  if (s->status == 0) {  // the header; compression starts with an empty pending buffer (deflate.c)
     ds_header(s);
     s->status = 1;
+    serve();
+    if (s->served < s->out.size()) {
+      s->last_flush = -1;
+      return Z_OK;
+    }
   }
   // a call that only delivers the rest of a flush whose terminator zlib
   // writes in this very call has nothing more to do
   const bool term_here = had_pending && !in_len && s->mark_valid && served_start <= s->mark;
   if (in_len || (flush != Z_NO_FLUSH && s->status != 2 && !term_here)) {
+    const uint64_t rd0 = s->buf.size();  // zlib has read everything before this call's input
     if (in_len) {
       s->buf.insert(s->buf.end(), in, in + in_len);
       s->total_in += in_len;
       s->fresh += in_len;
       *consumed = in_len;
     }
+    // output space left for the job's bytes (after the pending output and header)
+    const uint64_t room = (uint64_t)(out_len - *produced) - (s->out.size() - s->served);
     int r = Z_OK;
+    uint64_t dropped = 0;
     if (flush == Z_FINISH) {
-      r = ds_job(s, ZS_DT_FINAL, false);
-      s->status = 2;
+      r = ds_job(s, ZS_DT_FINAL, false, rd0, room, &dropped);
+      if (!r && s->rtop == UINT64_MAX) s->status = 2;  // else deflate_slow returned need_more: not finished
     } else if (flush != Z_NO_FLUSH) {
       r = ds_job(s, flush == Z_PARTIAL_FLUSH ? ZS_DT_PARTIAL : (flush == Z_BLOCK ? ZS_DT_BLOCK : ZS_DT_SYNC),
-                 flush == Z_FULL_FLUSH);
+                 flush == Z_FULL_FLUSH, rd0, room, &dropped);
     } else if (s->exact) {
-      if (s->fresh >= std::max(s->need, dstream_run_min())) r = ds_job(s, ZS_DT_CUT, false);
+      if (s->fresh >= std::max(s->need, dstream_run_min()) ||
+          !ds_model_nojob(s, s->abs + rd0, s->abs + rd0 + in_len))
+        r = ds_job(s, ZS_DT_CUT, false, rd0, room, &dropped);
     } else if (s->buf.size() >= dstream_fast_max()) {
-      r = ds_job(s, ZS_DT_BLOCK, false);
+      r = ds_job(s, ZS_DT_BLOCK, false, rd0, room, &dropped);
     }
     if (r) return Z_STREAM_ERROR;
+    *consumed = (unsigned)(in_len - dropped);
   }
   if (serve()) {
     s->last_flush = -1;

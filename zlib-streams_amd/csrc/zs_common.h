@@ -234,6 +234,23 @@ struct ZsDJobDev {
   uint64_t cut_pos;    // ZS_DT_CUT (out): where the next segment's parse starts (job offset)
   uint64_t cut_skip;   // ZS_DT_CUT (out): ... and the symbols from there already emitted
   uint64_t cut_open;   // ZS_DT_CUT (out): symbols of the unsent block zlib has already tallied
+  // zlib's pull-on-demand (zs_zd_limit_kernel): deflate() returns right after
+  // the block flush that fills the caller's output space, having read only
+  // what fill_window had read by then (deflate.c deflate_slow / deflate_fast,
+  // FLUSH_BLOCK; fill_window reads to window_size after sliding by w_size once
+  // strstart >= w_size + MAX_DIST)
+  uint64_t lim_bytes;  // (in) job output bytes the call's output space takes (UINT64_MAX: no limit)
+  uint64_t zb;         // (in / out) stream offset (since the window restart) of zlib's window start
+  uint64_t rd0;        // (in) job offset up to which zlib has read before this call
+  uint64_t rtop;       // (in) the call's first loop top when zlib may fill there (job offset), else UINT64_MAX:
+                       //      it resumes where its last fill attempt already took place, and reads at once
+  uint64_t rd_out;     // (out) job offset up to which zlib has read when the call returns
+  uint64_t next_top;   // (out, early) the loop top the next call resumes at (job offset)
+  uint64_t fstop;      // (deflate_fast CUT jobs) the loop top zs_zd_fast_kernel stopped at
+  uint32_t early;      // (out) 1: the call returns after block early_k - 1, its output space full
+  uint32_t early_k;
+  uint32_t nzblk0;     // blocks before the cut (zs_zd_cut_kernel)
+  uint32_t pad2;
 };
 #define ZD_SLOW 1u
 #define ZD_FAST 2u
