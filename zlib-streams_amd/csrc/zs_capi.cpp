@@ -1906,8 +1906,11 @@ int deflate_batch_locked(const zs_djob *jobs, uint32_t n, zs_result *results, ui
 //     Adler-32 joined from the jobs' GPU checks).
 // Bits past the last whole byte of a job wait for the next one (zlib keeps
 // them in bi_buf).  The wrapper header is zlib's constant header, sent by the
-// first call.  Levels 0..3 (the GPU throughput encoder, not zlib's bytes)
-// restart the window at each job.  Concurrent handles' jobs share launches.
+// first call.  When a block flush fills the caller's output space, deflate()
+// returns right there, having read only what fill_window had read (the GPU's
+// read model, zs_zd_limit_kernel): the rest of the input is not consumed.
+// Level 0 is zlib's deflate_stored call by call (ds_stored_call, below).
+// Concurrent handles' jobs share launches.
 // ---------------------------------------------------------------------------
 constexpr uint32_t ZD_BLOCK_SYMS = 16383, ZD_LOOK_HOST = 262;
 
