@@ -957,3 +957,28 @@ def test_deflate_output_full_consumed_is_zlibs(zs, level):
                 break
         assert g.end() == h.end()
         assert zlib.decompress(bytes(out), wb) == data
+
+
+@pytest.mark.parametrize("level", [1, 2, 3])
+def test_deflate_fast_flush_then_tiny_calls_are_zlibs(zs, level):
+    """deflate_fast after a flush leaves its last MIN_MATCH - 1 positions to the
+    next fill_window (deflate.c s->insert), which inserts them only while
+    lookahead + insert >= MIN_MATCH: a sync / partial / full flush, then 1- and
+    2-byte calls (Z_NO_FLUSH and flushing), then more input, several times over;
+    every call's (ret, consumed, produced bytes) and strm->adler equal host
+    zlib's, raw / zlib / gzip."""
+    rng = random.Random(900 + level)
+    text = corpus.stream(33, 400_000)
+    for wb in (-15, 15, 31):
+        calls, off = [], 0
+        while off < len(text):
+            n = rng.choice([3000, 20000, 70000])
+            calls.append((text[off:off + n], rng.choice([2, 1, 3])))
+            off += n
+            for _ in range(rng.randint(1, 3)):
+                m = rng.choice([1, 2])
+                calls.append((text[off:off + m], rng.choice([0, 0, 2, 1])))
+                off += m
+        calls += [(b"", 4)] * 2
+        out = _compare_calls(zs, level, wb, calls, 1 << 20)
+        assert zlib.decompress(out, wb) == text
