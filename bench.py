@@ -86,7 +86,7 @@ def parse_args(argv=None):
     ap.add_argument("--stream-leg-mib", type=int, default=16, help="line-text stream of the one-handle run")
     ap.add_argument("--stream-handles", type=int, default=64, help="concurrent handles of the aggregate run")
     ap.add_argument("--stream-handle-mib", type=int, default=4, help="stream size per concurrent handle")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r03", "pmc_traffic.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r04", "pmc_traffic.json"),
                     help="PMC-derived HBM bytes per pipeline launch (null in the line when absent)")
     ap.add_argument("--no-c5-leg", action="store_true",
                     help="skip the configs[4] leg (the fixed 4096 x 4 MiB batch LPT-split across the ranks)")
@@ -426,14 +426,20 @@ def main():
     traffic = traffic_src = None
     if args.traffic_json and os.path.exists(args.traffic_json) and world == 1 and args.workload == "c2":
         # HBM bytes per pipeline launch from separate rocprofv3 --pmc passes over this same workload
-        # (tools/pmc_traffic.sh -> tools/pmc_traffic.py); PMC cannot be read from inside the timed run
+        # (tools/pmc_traffic.sh -> tools/pmc_traffic.py); PMC cannot be read from inside the timed run.
+        # Reported only when those passes ran the library this run loaded (SHA-256 match).
         tj = json.load(open(args.traffic_json))
-        traffic = tj.get("hbm_bytes_per_launch")
         import hashlib
-        so_sha = hashlib.sha256(open(os.path.join(ROOT, "zlib-streams_amd", "libzstreams_mi355x.so"), "rb").read()).hexdigest()
+        so_path = os.environ.get("ZS_LIB") or os.path.join(ROOT, "zlib-streams_amd", "libzstreams_mi355x.so")
+        so_sha = hashlib.sha256(open(so_path, "rb").read()).hexdigest()
+        same = tj.get("library_sha256") == so_sha
+        traffic = tj.get("hbm_bytes_per_launch") if same else None
         traffic_src = {"file": os.path.relpath(args.traffic_json, ROOT), "checkpoint": tj.get("checkpoint"),
-                       "same_library_build": tj.get("library_sha256") == so_sha if tj.get("library_sha256") else None,
+                       "same_library_build": same, "library_sha256": so_sha,
                        "how": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, gfx950-corrected, every pipeline kernel"}
+        if not same:
+            traffic_src["reason_null"] = (f"the PMC passes in {traffic_src['file']} measured library "
+                                          f"{str(tj.get('library_sha256'))[:16]}, not this build")
 
     c5_l = None
     if args.workload == "c2" and not args.no_c5_leg and args.sim_world <= 1:
