@@ -476,13 +476,6 @@ __global__ void __launch_bounds__(ZD_MT) zs_zd_match_kernel(const ZsDJobDev *__r
 #define ZD_XT3 512u  // walks go on this far past the item's end (parse paths entering the next item)
 #endif
 #define ZD_WB3 (ZD_S3 + ZD_XT3 + 32768u + 272u)  // window bytes in LDS
-#ifndef ZD_MSQ
-#define ZD_MSQ 1  // walks hand their continuation to a workgroup queue every ZD_MSQ_SPLIT positions
-#endif
-#ifndef ZD_MSQ_SPLIT
-#define ZD_MSQ_SPLIT 48u
-#endif
-#define ZD_MSQ_N 448u  // continuation slots per item (u64 each; the LDS left over by the window and links)
 
 __global__ void __launch_bounds__(ZD_MT3) zs_zd_msearch_kernel(const ZsDJobDev *__restrict__ jobs,
                                                                 const ZsZWorkDev *__restrict__ work,
@@ -493,20 +486,6 @@ __global__ void __launch_bounds__(ZD_MT3) zs_zd_msearch_kernel(const ZsDJobDev *
   __shared__ __attribute__((aligned(16))) uint16_t s_pd[ZD_S3 + ZD_XT3 + 32768u];
   __shared__ uint32_t s_claim[(ZD_S3 + ZD_XT3) / 32], s_sa[(ZD_S3 + ZD_XT3) / 32], s_sb[(ZD_S3 + ZD_XT3) / 32];
   __shared__ uint32_t s_next;
-#if ZD_MSQ
-  // Work queue (load balance): a walk that has gone ZD_MSQ_SPLIT positions
-  // since its task began hands its next loop top and state on as a task and
-  // takes the next start (or task).  The same walks run -- a walk is a serial
-  // chain of searches however it is split -- but no lane holds a long walk
-  // while others idle: all starts are handed out early (~18% of an item's time)
-  // and lanes used to drain with 28 of 64 busy per wave-step.  s_qt reserves
-  // slots, an entry is published by a nonzero write, s_qh takes them in order;
-  // s_busy counts the lanes holding a task (taken before a take is attempted),
-  // so an item ends when no lane is busy, every start is out and the queue is
-  // empty.
-  __shared__ unsigned long long s_q[ZD_MSQ_N];
-  __shared__ uint32_t s_qh, s_qt, s_busy;
-#endif
 #if ZD_MS_PROF
   __shared__ uint32_t pf_iters, pf_lanes, pf_titers, pf_tlanes, pf_tail_at, pf_end, pf_stage;
   const uint64_t pf_t0 = clock64();
@@ -535,10 +514,6 @@ __global__ void __launch_bounds__(ZD_MT3) zs_zd_msearch_kernel(const ZsDJobDev *
     for (uint32_t i = t; i < ZD_WB3 / 4 + 4; i += ZD_MT3) s_w[i] = 0;
     for (uint32_t i = t; i < (ZD_S3 + ZD_XT3) / 32; i += ZD_MT3) s_claim[i] = s_sa[i] = s_sb[i] = 0;
     if (t == 0) s_next = 0;
-#if ZD_MSQ
-    for (uint32_t i = t; i < ZD_MSQ_N; i += ZD_MT3) s_q[i] = 0;
-    if (t == 0) s_qh = s_qt = s_busy = 0;
-#endif
     __syncthreads();
     // 16-byte loads (lo and its LDS index are multiples of 16; the job's link
     // array starts 64-position aligned); byte loads for an unaligned input
@@ -576,9 +551,6 @@ __global__ void __launch_bounds__(ZD_MT3) zs_zd_msearch_kernel(const ZsDJobDev *
   // walk: loop top iq (item offset) in state st; search: at iq, budget svar
   uint32_t iq = 0, st = 0, svar = 0;
   bool walking = false, idle = false, srch = false, have = false;
-#if ZD_MSQ
-  uint32_t iq0 = 0;  // loop top the lane's current task began at
-#endif
   uint32_t c = 0, k = 0, best = 0, bdist = 0, cap = 0, nicep = 0, ow = 0, pi = 0, clim = 0;
   auto cmp_len = [&](uint32_t a0) -> uint32_t {  // as zs_zd_match_kernel
     uint32_t n = 0;
@@ -657,9 +629,6 @@ __global__ void __launch_bounds__(ZD_MT3) zs_zd_msearch_kernel(const ZsDJobDev *
     atomicOr(&(svar ? s_sb : s_sa)[iq >> 5], 1u << (iq & 31u));
   };
   for (;;) {
-#if ZD_MSQ
-    idle = false;  // an idle lane looks for queued work again
-#endif
     if (!idle && !srch) {
       if (have) {  // the search at iq ended
         const uint32_t m = best | (bdist << 9);
@@ -670,50 +639,6 @@ __global__ void __launch_bounds__(ZD_MT3) zs_zd_msearch_kernel(const ZsDJobDev *
       // step the walk to its next search, taking new starts as walks end
       for (;;) {
         if (!walking) {
-#if ZD_MSQ
-          // a start, else a queued continuation (busy taken before either is
-          // tried; plain loads first, so idle lanes poll without atomics)
-          if (__hip_atomic_load(&s_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= nst &&
-              __hip_atomic_load(&s_qh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >=
-                  min(__hip_atomic_load(&s_qt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP), ZD_MSQ_N)) {
-            idle = true;
-            break;
-          }
-          atomicAdd(&s_busy, 1u);
-          const uint32_t i = s_next < nst ? atomicAdd(&s_next, 1u) : nst;
-          if (i < nst) {
-            if (ent && i == 0) {
-              iq = (uint32_t)(jb.pstart - s);
-              st = jb.pstate;
-            } else {
-              iq = (k0 + i - (ent ? 1u : 0u)) * ZD_PL3;
-              st = ZD_STATE_A;
-            }
-          } else {
-            bool got = false;
-            for (;;) {
-              const uint32_t h = __hip_atomic_load(&s_qh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-              const uint32_t tq = __hip_atomic_load(&s_qt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-              if (h >= min(tq, ZD_MSQ_N)) break;
-              if (atomicCAS(&s_qh, h, h + 1u) == h) {
-                unsigned long long e;
-                do {
-                  e = __hip_atomic_load(&s_q[h], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                } while (e == 0ull);
-                iq = (uint32_t)(e >> 32) & 0x7fffu;
-                st = (uint32_t)e;
-                got = true;
-                break;
-              }
-            }
-            if (!got) {
-              atomicSub(&s_busy, 1u);
-              idle = true;
-              break;
-            }
-          }
-          iq0 = iq;
-#else
           const uint32_t i = atomicAdd(&s_next, 1u);
           if (i >= nst) {
             idle = true;
@@ -726,37 +651,16 @@ __global__ void __launch_bounds__(ZD_MT3) zs_zd_msearch_kernel(const ZsDJobDev *
             iq = (k0 + i - (ent ? 1u : 0u)) * ZD_PL3;
             st = ZD_STATE_A;
           }
-#endif
           walking = true;
         }
         if (iq >= lenx) {  // ZD_XT3 past the item's end: the next item's walks cover what follows
           walking = false;
-#if ZD_MSQ
-          atomicSub(&s_busy, 1u);
-#endif
           continue;
         }
-#if ZD_MSQ
-        if (iq - iq0 >= ZD_MSQ_SPLIT &&
-            __hip_atomic_load(&s_qt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < ZD_MSQ_N) {
-          const uint32_t slot = atomicAdd(&s_qt, 1u);
-          if (slot < ZD_MSQ_N) {  // hand the walk on from here (bit 47 keeps the entry nonzero)
-            __hip_atomic_store(&s_q[slot], (1ull << 47) | ((unsigned long long)iq << 32) | st, __ATOMIC_RELEASE,
-                               __HIP_MEMORY_SCOPE_WORKGROUP);
-            walking = false;
-            atomicSub(&s_busy, 1u);
-            continue;
-          }
-          iq0 = iq;  // the queue is full: this walk goes on
-        }
-#endif
         if (st == ZD_STATE_A) {
           const uint32_t bit = 1u << (iq & 31u);
           if (atomicOr(&s_claim[iq >> 5], bit) & bit) {  // another walk goes on from here
             walking = false;
-#if ZD_MSQ
-            atomicSub(&s_busy, 1u);
-#endif
             continue;
           }
         }
@@ -783,21 +687,7 @@ __global__ void __launch_bounds__(ZD_MT3) zs_zd_msearch_kernel(const ZsDJobDev *
         break;
       }
     }
-#if ZD_MSQ
-    if (!__ballot(!idle)) {
-      // no lane of this wave holds a task: done when no lane anywhere does and
-      // nothing is left to take, else look again (a busy walk may queue more)
-      if (__hip_atomic_load(&s_busy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0 &&
-          __hip_atomic_load(&s_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= nst &&
-          __hip_atomic_load(&s_qh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >=
-              min(__hip_atomic_load(&s_qt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP), ZD_MSQ_N))
-        break;
-      __builtin_amdgcn_s_sleep(2);
-      continue;
-    }
-#else
     if (!__ballot(!idle)) break;
-#endif
 #if ZD_MS_PROF
     {
       const uint64_t am = __ballot(srch);

@@ -95,30 +95,14 @@ __device__ __forceinline__ uint16_t compact_dist_entry(uint32_t z, uint32_t add_
 
 #define OP_ROOT9 15u
 
-// ZS_LXB (raw / zlib / gzip units): a length entry of the 8-bit LDS root
-// carries code bits + extra bits in [5:2] (<= 8 + 5), so the lane parse issues
-// the distance-root read as soon as the root entry arrives, instead of after
-// the length's extra-bit arithmetic (lane_step_fast)
-#ifndef ZS_LXB
-#define ZS_LXB 1
-#endif
-// extra bits of length code k (0..28) of standard deflate, src/inftrees.c:59-64
-__device__ __forceinline__ uint32_t len_xbits(uint32_t k) { return k < 8u ? 0u : (k < 28u ? (k >> 2) - 1u : 0u); }
-
 // LDS root entry for 8-bit prefix i from a zlib literal/length table with
-// lbits-bit root (lbits <= 9); xb: length entries with their extra bits added
-__device__ __forceinline__ uint16_t lds_len_root(const uint32_t *zt, uint32_t lbits, uint32_t i, bool xb) {
-  uint16_t e;
-  if (lbits <= 8) {
-    e = compact_len_entry(zt[i & ((1u << lbits) - 1u)]);
-  } else {
-    const uint32_t z0 = zt[i], z1 = zt[i | 256u];
-    const bool link = e_op(z0) != 0 && (e_op(z0) & 0xf0u) == 0;
-    if (!(z0 == z1 && !link)) return (uint16_t)(CK_SLOW | (OP_ROOT9 << 2));
-    e = compact_len_entry(z0);  // code of <= 8 bits (or invalid both ways)
-  }
-  if (xb && (e & 3u) == CK_LEN) e = (uint16_t)(e + (len_xbits((uint32_t)e >> 6) << 2));
-  return e;
+// lbits-bit root (lbits <= 9)
+__device__ __forceinline__ uint16_t lds_len_root(const uint32_t *zt, uint32_t lbits, uint32_t i) {
+  if (lbits <= 8) return compact_len_entry(zt[i & ((1u << lbits) - 1u)]);
+  const uint32_t z0 = zt[i], z1 = zt[i | 256u];
+  const bool link = e_op(z0) != 0 && (e_op(z0) & 0xf0u) == 0;
+  if (z0 == z1 && !link) return compact_len_entry(z0);  // code of <= 8 bits (or invalid both ways)
+  return (uint16_t)(CK_SLOW | (OP_ROOT9 << 2));
 }
 
 typedef __attribute__((address_space(1))) const uint32_t gcu32;
@@ -367,8 +351,6 @@ __device__ __forceinline__ bool lane_step(LaneState &s, const uint16_t *__restri
 #if KP_ON
   s.kp_steps++;
 #endif
-  // a root length entry's [5:2] counts its extra bits too (ZS_LXB)
-  if (ZS_LXB && !D64 && (e & 3u) == CK_LEN) e -= len_xbits(e >> 6) << 2;
   if ((e & 3u) == CK_SLOW) {
 #if KP_ON
     s.kp_slow_l++;
@@ -509,102 +491,7 @@ template <bool D64>
 __device__ __forceinline__ bool lane_step_fast(LaneState &s, const uint16_t *__restrict__ lt,
                                                const uint16_t *__restrict__ dt, uint32_t *__restrict__ tb,
                                                const uint32_t *__restrict__ dtl, const uint32_t *__restrict__ rp,
-                                               KpPhase &kp);
-
-// lane_step_fast with root length entries carrying their extra bits (ZS_LXB,
-// raw / zlib / gzip): the distance root is read from the bits past the length
-// code and its extra bits right after the root entry arrives; the length value,
-// the refill and the distance tail's VALU search overlap that read.  (A step
-// starts with >= 32 bits; a root length code and its extra bits take <= 13, so
-// the 6 distance-root bits are present before the refill, which adds bits above.)
-__device__ __forceinline__ bool lane_step_fast_xb(LaneState &s, const uint16_t *__restrict__ lt,
-                                                  const uint16_t *__restrict__ dt, uint32_t *__restrict__ tb,
-                                                  const uint32_t *__restrict__ dtl, const uint32_t *__restrict__ rp,
-                                                  KpPhase &kp) {
-  const uint64_t h0 = s.hold;
-  const uint32_t nb0 = s.nbits, wi0 = s.wi, rk0 = s.rk, nw0 = s.nw;
-  lane_refill_bf(s, rp);
-  uint32_t e = lt[(uint32_t)s.hold & (LROOT_N - 1)];
-  uint32_t kind = e & 3u;
-  uint32_t tot = (e >> 2) & 15u;  // code bits (+ extra bits: root length entries)
-  if (__builtin_expect(__ballot(kind == CK_SLOW) != 0, 0)) {
-#if KP_ON
-    const uint64_t kq = KP_NOW();
-    s.kp_slow_l++;
-#endif
-    if (kind == CK_SLOW) {  // compact sub-table entries carry code bits only
-      const uint32_t op = (e >> 2) & 15u;
-      uint32_t e2 = CK_SLOW;
-      if (op == OP_ROOT9) {
-        e2 = s.cl[(uint32_t)s.hold & 511u];
-        const uint32_t op2 = (e2 >> 2) & 15u;
-        if ((e2 & 3u) == CK_SLOW && op2) e2 = s.cl[(e2 >> 6) + (((uint32_t)s.hold >> 9) & ((1u << op2) - 1u))];
-      } else if (op) {
-        e2 = s.cl[(e >> 6) + (((uint32_t)s.hold >> s.lbits) & ((1u << op) - 1u))];
-      }
-      e = e2;
-      kind = e & 3u;
-      tot = ((e >> 2) & 15u) + (kind == CK_LEN ? len_xbits(e >> 6) : 0u);
-    }
-#if KP_ON
-    kp.t[0] += KP_NOW() - kq;
-#endif
-  }
-  const uint32_t isl = kind == CK_LEN;
-  const uint64_t h1 = s.hold >> tot;  // the bits past the length (or literal) code
-  uint32_t d = dt[(uint32_t)h1 & (DROOT_N - 1)];
-  const uint32_t sym = e >> 6;
-  const uint32_t top = sym >= 28u;
-  uint32_t xb = isl ? len_xbits(sym) : 0u;
-  uint32_t lbase = ((4u + (sym & 3u)) << (xb & 15u)) + 3u - (sym < 4u ? 4u : 0u);
-  lbase = top ? 258u : lbase;
-  const uint32_t used = tot - xb;
-  const uint32_t len = isl ? lbase + ((uint32_t)(s.hold >> used) & ((1u << xb) - 1u)) : 1u;
-  s.hold = h1;
-  s.nbits -= tot;
-  lane_refill_bf(s, rp);
-  const uint32_t dtr = dist_tail_r(s.dta, s.dtb, dtl, (uint32_t)s.hold);
-  const bool dslow = isl && (d & 3u) == CK_SLOW;
-  d = dslow ? (((d >> 2) & 15u) ? dtr : (uint32_t)CK_SLOW) : d;
-  const uint32_t dused = (d >> 2) & 15u, dsym = (d >> 6) & 31u;
-  const uint32_t dx = min((uint32_t)max((int)(dsym >> 1) - 1, 0), 14u);
-  const uint32_t dist = ((2u + (dsym & 1u)) << dx) + 1u - (dsym < 2u ? 2u : 0u) +
-                        ((uint32_t)(s.hold >> dused) & ((1u << dx) - 1u));
-  const uint32_t dcons = isl ? dused + dx : 0u;
-  s.hold >>= dcons;
-  s.nbits -= dcons;
-#if KP_ON
-  s.kp_steps++;
-#else
-  (void)kp;
-#endif
-  const uint32_t exc = (uint32_t)(kind >= CK_EOB) | (isl & (uint32_t)((d & 3u) == CK_SLOW)) |
-                       (uint32_t)(lane_pos(s) > s.limit) | (uint32_t)(s.pos + len > s.capx) |
-                       (isl & (uint32_t)(dist > s.pos + s.whave));
-  tb[s.gk * WAVE] = isl ? ((len << 16) | (dist - 1u)) : sym;
-  if (exc) {
-    s.hold = h0;
-    s.nbits = nb0;
-    s.wi = wi0;
-    s.rk = rk0;
-    s.nw = nw0;
-#if KP_ON
-    s.kp_steps--;
-#endif
-    return lane_step<false>(s, lt, dt, tb, dtl, rp, kp);
-  }
-  s.gk++;
-  s.ntok++;
-  s.pos += len;
-  return false;
-}
-
-template <bool D64>
-__device__ __forceinline__ bool lane_step_fast(LaneState &s, const uint16_t *__restrict__ lt,
-                                               const uint16_t *__restrict__ dt, uint32_t *__restrict__ tb,
-                                               const uint32_t *__restrict__ dtl, const uint32_t *__restrict__ rp,
                                                KpPhase &kp) {
-  if constexpr (ZS_LXB && !D64) return lane_step_fast_xb(s, lt, dt, tb, dtl, rp, kp);
   const uint64_t h0 = s.hold;
   const uint32_t nb0 = s.nbits, wi0 = s.wi, rk0 = s.rk, nw0 = s.nw;
   lane_refill_bf(s, rp);
@@ -872,7 +759,7 @@ __device__ int wave_dyn_header(BuildLDS &B, const uint32_t *w, uint32_t end_byte
     tabg[i] = B.tab[i];
     ctab[i] = compact_len_entry(B.tab[i], i < (1u << lbits) ? 0u : lbits);
   }
-  for (uint32_t i = lane; i < LROOT_N; i += WAVE) lroot_out[i] = lds_len_root(B.tab, lbits, i, ZS_LXB && !D64);
+  for (uint32_t i = lane; i < LROOT_N; i += WAVE) lroot_out[i] = lds_len_root(B.tab, lbits, i);
   __builtin_amdgcn_wave_barrier();
   dbits = 6;
   if (build_table(T_DISTS, B.lens + nlen, ndist, B.tab, &dbits, B.sorted, B.scr, D64 ? 1 : 0)) {
@@ -891,9 +778,9 @@ __device__ int wave_dyn_header(BuildLDS &B, const uint32_t *w, uint32_t end_byte
 
 // Install compact roots for lane ln from zlib tables zl (root bits lb) and zd (db).
 __device__ void install_roots(uint16_t *lroot, uint16_t *droot, const uint32_t *zl, uint32_t lb, const uint32_t *zd,
-                              uint32_t db, bool xb) {
+                              uint32_t db) {
   const uint32_t lane = lane_id();
-  for (uint32_t i = lane; i < LROOT_N; i += WAVE) lroot[i] = lds_len_root(zl, lb, i, xb);
+  for (uint32_t i = lane; i < LROOT_N; i += WAVE) lroot[i] = lds_len_root(zl, lb, i);
   droot[lane] = compact_dist_entry(zd[lane & ((1u << db) - 1u)]);
   __builtin_amdgcn_wave_barrier();
 }
@@ -1016,7 +903,7 @@ __device__ void coop_block(LaneState &s, uint32_t ln, BuildLDS &LB, uint16_t *lr
       cd = cl + 512;
       lbits = 9;
       dbits = 5;
-      install_roots(lroot_ln, droot_ln, zl, lbits, zd, dbits, ZS_LXB && !D64);
+      install_roots(lroot_ln, droot_ln, zl, lbits, zd, dbits);
       mode = LM_SYM;
       break;
     }
