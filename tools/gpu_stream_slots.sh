@@ -1,0 +1,12 @@
+#!/bin/bash
+# handle-ABI aggregate A/B: the bench stream leg (one handle, 64 handles on
+# native threads) under ZS_STREAM_SLOTS = 1 / 2 / 4 launch slots
+TAG=${1:-slots}
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/$TAG
+mkdir -p $O
+cd $R
+for S in ${SLOTS:-4 2 1}; do
+  ZS_STREAM_SLOTS=$S timeout -k 10 300 python3 -u bench.py --only-stream --no-ref-perf > $O/stream_s$S.json 2> $O/stream_s$S.err || exit $?
+  echo "slots=$S $(python3 -c "import json;d=json.load(open('$O/stream_s$S.json'))['stream'];print('one',d['one_handle']['value'],'agg',d['handles']['value'],'cpl',d['handles']['calls_per_launch'])")"
+done
