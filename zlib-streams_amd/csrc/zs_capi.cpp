@@ -988,8 +988,9 @@ struct SqSlot {  // one launch slot: its stream and the batch's call arrays
 
 struct StreamQueue {
   std::mutex mu;
-  std::condition_variable cv;
+  std::condition_variable cv, arrive;
   std::vector<StreamCall *> pending;
+  size_t last_n = 0;  // calls in the last batch
   SqSlot slot[SQ_SLOTS];
   bool busy[SQ_SLOTS] = {};
   size_t running = 0;  // calls in batches in flight
@@ -1072,10 +1073,21 @@ int sq_slots() {  // env ZS_STREAM_SLOTS (1..SQ_SLOTS)
   return v;
 }
 
+// env ZS_STREAM_GATHER_US: a new leader waits up to this long (while calls keep
+// arriving, gaps below SQ_GAP_US) for as many calls as the last batch held
+long sq_gather_us() {
+  static const long v = [] {
+    const char *e = std::getenv("ZS_STREAM_GATHER_US");
+    return e ? std::max(0L, std::atol(e)) : 0L;
+  }();
+  return v;
+}
+
 int sq_submit(StreamCall *c) {
   const int slots = sq_slots();
   std::unique_lock<std::mutex> lk(g_sq.mu);
   g_sq.pending.push_back(c);
+  g_sq.arrive.notify_one();
   for (;;) {
     if (c->done) break;
     int k = -1, nbusy = 0;
@@ -1089,7 +1101,17 @@ int sq_submit(StreamCall *c) {
       continue;
     }
     g_sq.busy[k] = true;
+    if (const long gw = sq_gather_us(); gw > 0 && g_sq.pending.size() < g_sq.last_n) {
+      const auto t_end = std::chrono::steady_clock::now() + std::chrono::microseconds(gw);
+      while (g_sq.pending.size() < g_sq.last_n) {
+        const size_t had = g_sq.pending.size();
+        const auto t = std::min(t_end, std::chrono::steady_clock::now() + std::chrono::microseconds(SQ_GAP_US));
+        g_sq.arrive.wait_until(lk, t, [&] { return g_sq.pending.size() > had; });
+        if (g_sq.pending.size() == had || std::chrono::steady_clock::now() >= t_end) break;
+      }
+    }
     const size_t take = std::min(g_sq.pending.size(), SQ_MAX);
+    g_sq.last_n = take;
     std::vector<StreamCall *> batch(g_sq.pending.begin(), g_sq.pending.begin() + take);
     g_sq.pending.erase(g_sq.pending.begin(), g_sq.pending.begin() + take);
     for (StreamCall *b : batch) b->taken = true;
