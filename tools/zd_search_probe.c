@@ -235,7 +235,7 @@ int main(int argc, char **argv) {
     nocache = 1;
     static const uint32_t CF2[][3] = {{16384, 1024, 16}, {16384, 1024, 8}, {16384, 512, 16}};
     for (int ci = 0; ci < 1; ci++) {
-      classes = 1;
+      classes = getenv("CLASSES") ? atoi(getenv("CLASSES")) : 1;
       helpers = ci >= 3;
       const uint32_t ITEM = CF2[ci % 3][0], NL = CF2[ci % 3][1], PL = CF2[ci % 3][2];
       (void)CF;
@@ -348,7 +348,7 @@ int main(int argc, char **argv) {
     // (32 KiB window + ACT active); a start is taken only below the loaded
     // front, a walk waits while it would read past the front (q + 278), the
     // front moves by CH when every walk is at >= front - ACT + CH
-    {
+    if (!getenv("NORING")) {
       static const uint32_t RC[][4] = {{1024, 16, 16384, 4096}, {1024, 16, 16384, 2048}, {1024, 16, 8192, 2048}, {512, 16, 16384, 4096}};
       for (int ri = 0; ri < 4; ri++) {
         const uint32_t NL = RC[ri][0], PL = RC[ri][1], ACT = RC[ri][2], CH = RC[ri][3], SPAN = 1u << 20;
