@@ -710,6 +710,7 @@ def stream_leg(args, zstreams, np, cpu):
     st1 = zstreams.stream_stats()
     launches = st1["launches"] - st0["launches"]
     calls_m = st1["calls"] - st0["calls"]
+    dl = {k: st1[k] - st0[k] for k in ("launch_ns", "gather_ns", "kernel_ns")}
     okm = all(prod[k] == each and codes[k] == 1 and np.array_equal(outs[k][:each], rs[k]) for k in range(nh))
 
     # host zlib, same schedule: the one stream on 1 thread; the handle set on all cores
@@ -770,6 +771,10 @@ def stream_leg(args, zstreams, np, cpu):
                     "stream": f"{nh} x {args.stream_handle_mib} MiB line text (ids 32..), one native host thread per "
                               "handle (tools/js_driver.c)",
                     "launches": launches, "calls_per_launch": round(calls_m / max(1, launches), 1),
+                    "launch_us_avg": round(dl["launch_ns"] / 1e3 / max(1, launches), 1),
+                    "kernel_us_avg": round(dl["kernel_ns"] / 1e3 / max(1, launches), 1),
+                    "gather_us_avg": round(dl["gather_ns"] / 1e3 / max(1, launches), 1),
+                    "slots_busy": round(dl["launch_ns"] / 1e9 / tm, 2),
                     "verified": bool(okm)},
         "wasm_reference_mibs": 493,
         "compress_one_handle": {"value": round(len(dbytes) / tdz / 2**20, 1), "unit": "MiB/s (input)",

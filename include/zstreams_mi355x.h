@@ -209,6 +209,11 @@ int zs_last_stats_ex(uint32_t *out, uint32_t n);
    the handle / zlib ABIs made at the same time from different threads (one
    handle per thread) share one launch, a workgroup per call. */
 int zs_stream_stats(uint64_t out[2]);
+/* zs_stream_stats plus timing (ns, cumulative): out[0] launches, out[1] calls,
+ * out[2] wall time of the launch sequences (submit to synchronised, summed over
+ * slots), out[3] time leaders waited to gather calls (ZS_STREAM_GATHER_US),
+ * out[4] the batches' kernel time (HIP events around each launch sequence). */
+int zs_stream_stats_ex(uint64_t out[5]);
 const char *zs_version(void);
 const char *zs_last_error(void);
 

@@ -972,6 +972,8 @@ struct StreamCall {
 
 struct SqSlot {  // one launch slot: its stream and the batch's call arrays
   hipStream_t st = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;  // around the batch's kernels (zs_stream_stats_ex)
+  uint64_t last_kernel_ns = 0;
   size_t cap = 0;
   ZsJobDev *d_jobs = nullptr, *h_jobs = nullptr;
   ZsHeadDev *d_heads = nullptr;
@@ -995,11 +997,16 @@ struct StreamQueue {
   bool busy[SQ_SLOTS] = {};
   size_t running = 0;  // calls in batches in flight
   uint64_t launches = 0, calls = 0;  // zs_stream_stats
+  // zs_stream_stats_ex: launch sequences' wall time (sum over slots), the
+  // leaders' gather waits, and the kernels' time (HIP events around the launch)
+  uint64_t launch_ns = 0, gather_ns = 0, kernel_ns = 0;
 } g_sq;
 
 // a slot's leader only (busy[slot] set): one launch sequence per decoder variant
 int sq_launch(SqSlot &q, std::vector<StreamCall *> &calls) {
   if (!q.st) HIP_OK(hipStreamCreateWithFlags(&q.st, hipStreamNonBlocking));
+  if (!q.ev0) HIP_OK(hipEventCreate(&q.ev0));
+  if (!q.ev1) HIP_OK(hipEventCreate(&q.ev1));
   const size_t n = calls.size();
   if (n > q.cap) {
     const size_t c = std::max<size_t>(n, 64);
@@ -1044,6 +1051,7 @@ int sq_launch(SqSlot &q, std::vector<StreamCall *> &calls) {
     HIP_OK(hipMemcpyAsync(q.d_jobs, q.h_jobs, n * sizeof(ZsJobDev), hipMemcpyHostToDevice, st));
     HIP_OK(hipMemcpyAsync(q.d_sts, q.h_sts, n * sizeof(ZsStreamDev *), hipMemcpyHostToDevice, st));
   }
+  HIP_OK(hipEventRecord(q.ev0, st));
   for (int d64 = 0; d64 < 2; d64++) {
     const size_t k0 = d64 ? nstd : 0, k1 = d64 ? n : nstd;
     if (k1 == k0) continue;
@@ -1058,8 +1066,13 @@ int sq_launch(SqSlot &q, std::vector<StreamCall *> &calls) {
                      max_out, res + k0, st);
     HIP_OK(hipGetLastError());
   }
+  HIP_OK(hipEventRecord(q.ev1, st));
   if (!views) HIP_OK(hipMemcpyAsync(q.h_res, q.d_res, n * sizeof(ZsStreamRes), hipMemcpyDeviceToHost, st));
   HIP_OK(hipStreamSynchronize(st));
+  {
+    float ms = 0.f;
+    q.last_kernel_ns = hipEventElapsedTime(&ms, q.ev0, q.ev1) == hipSuccess ? (uint64_t)(ms * 1e6f) : 0u;
+  }
   for (size_t k = 0; k < n; k++) calls[order[k]]->res = q.h_res[k];
   return 0;
 }
@@ -1102,13 +1115,15 @@ int sq_submit(StreamCall *c) {
     }
     g_sq.busy[k] = true;
     if (const long gw = sq_gather_us(); gw > 0 && g_sq.pending.size() < g_sq.last_n) {
-      const auto t_end = std::chrono::steady_clock::now() + std::chrono::microseconds(gw);
+      const auto g0 = std::chrono::steady_clock::now();
+      const auto t_end = g0 + std::chrono::microseconds(gw);
       while (g_sq.pending.size() < g_sq.last_n) {
         const size_t had = g_sq.pending.size();
         const auto t = std::min(t_end, std::chrono::steady_clock::now() + std::chrono::microseconds(SQ_GAP_US));
         g_sq.arrive.wait_until(lk, t, [&] { return g_sq.pending.size() > had; });
         if (g_sq.pending.size() == had || std::chrono::steady_clock::now() >= t_end) break;
       }
+      g_sq.gather_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - g0).count();
     }
     const size_t take = std::min(g_sq.pending.size(), SQ_MAX);
     g_sq.last_n = take;
@@ -1117,7 +1132,9 @@ int sq_submit(StreamCall *c) {
     for (StreamCall *b : batch) b->taken = true;
     g_sq.running += batch.size();
     lk.unlock();
+    const auto l0 = std::chrono::steady_clock::now();
     const int rc = sq_launch(g_sq.slot[k], batch);
+    const uint64_t lns = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - l0).count();
     const std::string msg = rc ? g_err : std::string();
     if (rc) (void)hipGetLastError();
     lk.lock();
@@ -1130,6 +1147,8 @@ int sq_submit(StreamCall *c) {
     g_sq.running -= batch.size();
     g_sq.launches++;
     g_sq.calls += batch.size();
+    g_sq.launch_ns += lns;
+    g_sq.kernel_ns += g_sq.slot[k].last_kernel_ns;
     g_sq.cv.notify_all();
   }
   if (c->err) set_err(c->errmsg);
@@ -2870,6 +2889,16 @@ int zs_stream_stats(uint64_t out[2]) {
   std::lock_guard<std::mutex> lk(g_sq.mu);
   out[0] = g_sq.launches;
   out[1] = g_sq.calls;
+  return 0;
+}
+
+int zs_stream_stats_ex(uint64_t out[5]) {
+  std::lock_guard<std::mutex> lk(g_sq.mu);
+  out[0] = g_sq.launches;
+  out[1] = g_sq.calls;
+  out[2] = g_sq.launch_ns;
+  out[3] = g_sq.gather_ns;
+  out[4] = g_sq.kernel_ns;
   return 0;
 }
 

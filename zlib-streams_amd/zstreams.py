@@ -66,6 +66,7 @@ _SIGS = {
     "zs_last_stats": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint32)]),
     "zs_last_stats_ex": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32]),
     "zs_stream_stats": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64)]),
+    "zs_stream_stats_ex": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64)]),
     "zs_synchronize": (ctypes.c_int, []),
     "zs_version": (ctypes.c_char_p, []), "zs_last_error": (ctypes.c_char_p, []),
 }
@@ -406,9 +407,9 @@ def last_stats():
 
 def stream_stats():
     """Stream-call batching since load: launch sequences and the calls they ran."""
-    a = (ctypes.c_uint64 * 2)()
-    _check(lib().zs_stream_stats(a))
-    return {"launches": a[0], "calls": a[1]}
+    a = (ctypes.c_uint64 * 5)()
+    _check(lib().zs_stream_stats_ex(a))
+    return {"launches": a[0], "calls": a[1], "launch_ns": a[2], "gather_ns": a[3], "kernel_ns": a[4]}
 
 
 def set_stream(hip_stream_handle):
