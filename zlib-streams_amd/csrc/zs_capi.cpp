@@ -954,7 +954,7 @@ size_t stream_fast_min() {
 // caller's batch is itself: no added latency.
 // ---------------------------------------------------------------------------
 constexpr size_t SQ_MAX = 2048;
-constexpr int SQ_SLOTS = 4;
+constexpr int SQ_SLOTS = 32;  // most slots (ZS_STREAM_SLOTS); the default follows the process's hardware queues
 constexpr long SQ_GAP_US = 40;   // deflate job gathering (DzQueue): quiet gap that ends it
 constexpr long SQ_WAIT_US = 400; // deflate job gathering: longest wait
 
@@ -1043,7 +1043,11 @@ int sq_launch(SqSlot &q, std::vector<StreamCall *> &calls) {
   const hipStream_t st = q.st;
   // jobs / states / outcomes: read and written by the kernels through the
   // pinned arrays' device views when the runtime gives them, else copied
-  const bool views = q.v_jobs && q.v_sts && q.v_res;
+  static const bool use_views = [] {  // env ZS_STREAM_VIEWS=0: copy the arrays instead (A/B)
+    const char *e = std::getenv("ZS_STREAM_VIEWS");
+    return !(e && e[0] == '0');
+  }();
+  const bool views = use_views && q.v_jobs && q.v_sts && q.v_res;
   ZsJobDev *jobs = views ? q.v_jobs : q.d_jobs;
   ZsStreamDev **sts = views ? q.v_sts : q.d_sts;
   ZsStreamRes *res = views ? q.v_res : q.d_res;
@@ -1077,10 +1081,11 @@ int sq_launch(SqSlot &q, std::vector<StreamCall *> &calls) {
   return 0;
 }
 
-int sq_slots() {  // env ZS_STREAM_SLOTS (1..SQ_SLOTS)
+int sq_slots() {  // env ZS_STREAM_SLOTS (1..SQ_SLOTS), else one per hardware queue (GPU_MAX_HW_QUEUES, HIP's default 4)
   static const int v = [] {
     const char *e = std::getenv("ZS_STREAM_SLOTS");
-    const int k = e ? std::atoi(e) : SQ_SLOTS;
+    const char *q = std::getenv("GPU_MAX_HW_QUEUES");
+    const int k = e ? std::atoi(e) : (q ? std::atoi(q) : 4);
     return std::max(1, std::min(SQ_SLOTS, k));
   }();
   return v;
