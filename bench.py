@@ -680,9 +680,12 @@ def stream_leg(args, zstreams, np, cpu):
     out1 = np.empty(one_bytes + 65536, dtype=np.uint8)
     res = [None]
     run_one(comp1, raw1, out1, res, 0)  # warm (device state, buffers)
+    so0 = zstreams.stream_stats()
     t0 = time.perf_counter()
     run_one(comp1, raw1, out1, res, 0)
     t1 = time.perf_counter() - t0
+    so1 = zstreams.stream_stats()
+    pk1 = max(1, so1["pk_calls"] - so0["pk_calls"])
     ok1 = res[0][0] == one_bytes and res[0][1] == 1 and np.array_equal(out1[:one_bytes], raw1)
     calls1 = res[0][2]
 
@@ -710,7 +713,8 @@ def stream_leg(args, zstreams, np, cpu):
     st1 = zstreams.stream_stats()
     launches = st1["launches"] - st0["launches"]
     calls_m = st1["calls"] - st0["calls"]
-    dl = {k: st1[k] - st0[k] for k in ("launch_ns", "gather_ns", "kernel_ns")}
+    dl = {k: st1[k] - st0[k] for k in ("launch_ns", "gather_ns", "kernel_ns", "pk_launches", "pk_calls", "pk_busy_ns",
+                                       "pk_wait_ns")}
     okm = all(prod[k] == each and codes[k] == 1 and np.array_equal(outs[k][:each], rs[k]) for k in range(nh))
 
     # host zlib, same schedule: the one stream on 1 thread; the handle set on all cores
@@ -766,6 +770,9 @@ def stream_leg(args, zstreams, np, cpu):
                     "Z_FINISH drain (src/wasm/api/zlib-streams.js:64-136)",
         "one_handle": {"value": round(mib1, 1), "unit": "MiB/s", "stream": f"line text {args.stream_leg_mib} MiB, "
                        "host zlib L6 raw (-15)", "calls": calls1, "us_per_call": round(t1 * 1e6 / calls1, 1),
+                       "persistent_calls": so1["pk_calls"] - so0["pk_calls"],
+                       "persistent_call_us_avg": round((so1["pk_busy_ns"] - so0["pk_busy_ns"]) / 1e3 / pk1, 1),
+                       "persistent_wait_us_avg": round((so1["pk_wait_ns"] - so0["pk_wait_ns"]) / 1e3 / pk1, 1),
                        "verified": bool(ok1)},
         "handles": {"value": round(mibm, 1), "unit": "MiB/s (aggregate)", "handles": nh,
                     "stream": f"{nh} x {args.stream_handle_mib} MiB line text (ids 32..), one native host thread per "
@@ -775,6 +782,9 @@ def stream_leg(args, zstreams, np, cpu):
                     "kernel_us_avg": round(dl["kernel_ns"] / 1e3 / max(1, launches), 1),
                     "gather_us_avg": round(dl["gather_ns"] / 1e3 / max(1, launches), 1),
                     "slots_busy": round(dl["launch_ns"] / 1e9 / tm, 2),
+                    "persistent_calls": dl["pk_calls"], "persistent_launches": dl["pk_launches"],
+                    "persistent_call_us_avg": round(dl["pk_busy_ns"] / 1e3 / max(1, dl["pk_calls"]), 1),
+                    "persistent_wait_us_avg": round(dl["pk_wait_ns"] / 1e3 / max(1, dl["pk_calls"]), 1),
                     "verified": bool(okm)},
         "wasm_reference_mibs": 493,
         "compress_one_handle": {"value": round(len(dbytes) / tdz / 2**20, 1), "unit": "MiB/s (input)",

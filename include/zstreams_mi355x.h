@@ -209,11 +209,20 @@ int zs_last_stats_ex(uint32_t *out, uint32_t n);
    the handle / zlib ABIs made at the same time from different threads (one
    handle per thread) share one launch, a workgroup per call. */
 int zs_stream_stats(uint64_t out[2]);
-/* zs_stream_stats plus timing (ns, cumulative): out[0] launches, out[1] calls,
- * out[2] wall time of the launch sequences (submit to synchronised, summed over
- * slots), out[3] time leaders waited to gather calls (ZS_STREAM_GATHER_US),
- * out[4] the batches' kernel time (HIP events around each launch sequence). */
-int zs_stream_stats_ex(uint64_t out[5]);
+/* zs_stream_stats plus timing (ns, cumulative): out[0] launches, out[1] calls
+ * (batch path), out[2] wall time of the launch sequences (submit to
+ * synchronised, summed over slots), out[3] time leaders waited to gather calls
+ * (ZS_STREAM_GATHER_US), out[4] the batches' kernel time (HIP events around
+ * each launch sequence); the persistent worker: out[5] its launches, out[6] the
+ * calls it ran, out[7] their workgroup time (pickup to done), out[8] their
+ * host wait (post to seen done). */
+int zs_stream_stats_ex(uint64_t out[9]);
+
+/* Persistent stream worker on (1) / off (0) for later calls; -1 only reads.
+ * Returns the previous setting.  Default: on (env ZS_STREAM_PK=0: off).  With
+ * it on, a handle's mapped calls after the wrapper header run on a long-lived
+ * workgroup of their own and return as soon as that call is done. */
+int zs_stream_persist(int on);
 const char *zs_version(void);
 const char *zs_last_error(void);
 

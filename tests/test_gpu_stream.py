@@ -94,17 +94,23 @@ def test_js_schedule_traces_match_oracle(zs, write):
     assert not bad, bad[:3]
 
 
-def test_concurrent_handles_match_oracle(zs):
-    """Many handles driven at once from their own threads (the library batches
-    their calls into shared launches): every per-call trace and output still
-    equals the oracle's for that stream alone."""
+@pytest.mark.parametrize("persist", [True, False], ids=["persistent", "batched"])
+def test_concurrent_handles_match_oracle(zs, persist):
+    """Many handles driven at once from their own threads -- on the persistent
+    worker (a workgroup per handle, each call returned on its own) or batched
+    into shared launches: every per-call trace and output still equals the
+    oracle's for that stream alone."""
     from concurrent.futures import ThreadPoolExecutor
     cases = _schedule_cases() * 2
     writes = [4096 if i % 2 else 65536 for i in range(len(cases))]
-    before = zs.stream_stats()
-    with ThreadPoolExecutor(16) as ex:
-        got = list(ex.map(lambda a: zs.js_schedule(a[0][0], FMT[a[0][1]], a[1]), zip(cases, writes)))
-    after = zs.stream_stats()
+    prev = zs.stream_persist(persist)
+    try:
+        before = zs.stream_stats()
+        with ThreadPoolExecutor(16) as ex:
+            got = list(ex.map(lambda a: zs.js_schedule(a[0][0], FMT[a[0][1]], a[1]), zip(cases, writes)))
+        after = zs.stream_stats()
+    finally:
+        zs.stream_persist(prev)
     bad = []
     for i, ((data, wb), w, (tr, out)) in enumerate(zip(cases, writes, got)):
         etr, eout = O.js_schedule(data, w, wb)
@@ -113,7 +119,11 @@ def test_concurrent_handles_match_oracle(zs):
     assert not bad, bad[:3]
     calls = after["calls"] - before["calls"]
     launches = after["launches"] - before["launches"]
-    assert 0 < launches < calls  # some calls shared a launch
+    if persist:  # the wrapper headers take the batch path, every later call the worker
+        assert after["pk_calls"] - before["pk_calls"] > calls
+    else:
+        assert after["pk_calls"] == before["pk_calls"]
+        assert 0 < launches < calls  # some calls shared a launch
 
 
 def _gzip_header_all_fields(body_raw):
@@ -266,3 +276,52 @@ def test_handle_output_space_small_large_small(zs):
             break
     assert code == 1 and bytes(got) == bytes(exp) == raw
     assert L.inflate_end(h) == 0
+
+
+def test_persistent_worker_relaunch_and_reset(zs):
+    """The persistent worker leaves after ZS_PK_IDLE_US (2 ms) without posts and
+    the next call relaunches it: calls spaced 20 ms apart each find the launch
+    gone.  inflateReset between two streams on the same handle (its device state
+    set up again by the next call, on the worker's workgroup) and a gzip stream
+    (header call on the batch path, the rest on the worker) keep every call
+    equal to the oracle's."""
+    import time
+    L = zs.lib()
+    prev = zs.stream_persist(True)
+    try:
+        raw = corpus.stream(33, 600000)
+        for wb in (-15, 31):
+            comp = _comp(raw, wb)
+            h = L.inflate_new()
+            assert (L.inflate_init_raw if wb < 0 else L.inflate_init_gzip)(h) == 0
+            for rep in range(2):  # the second pass after a reset (init again on the same handle)
+                if rep:
+                    assert (L.inflate_init_raw if wb < 0 else L.inflate_init_gzip)(h) == 0
+                ref = O.Stream(wb)
+                st0 = zs.stream_stats()
+                ib = ctypes.create_string_buffer(comp, len(comp))
+                off, got, k, naps = 0, bytearray(), 0, 0
+                while True:
+                    if k % 3 == 2:
+                        time.sleep(0.02)
+                        naps += 1
+                    k += 1
+                    n_in = min(32768, len(comp) - off)
+                    ob = ctypes.create_string_buffer(65536)
+                    r = L.inflate_process(h, ctypes.addressof(ib) + off, n_in, ctypes.addressof(ob), 65536, 0)
+                    prod, code, cons = r & 0xffffff, ((r >> 24) & 0xff), L.inflate_last_consumed(h)
+                    code = code - 256 if code & 0x80 else code
+                    e = ref.call(comp[off:off + n_in], 65536, 0)
+                    assert (prod, code, cons) == (len(e["out"]), e["ret"], e["consumed"]), (wb, rep, k)
+                    assert ob.raw[:prod] == e["out"]
+                    got += ob.raw[:prod]
+                    off += cons
+                    if code != 0:
+                        break
+                assert code == 1 and bytes(got) == raw
+                st1 = zs.stream_stats()
+                assert st1["pk_calls"] - st0["pk_calls"] >= k - 1
+                assert st1["pk_launches"] - st0["pk_launches"] >= naps
+            assert L.inflate_end(h) == 0
+    finally:
+        zs.stream_persist(prev)

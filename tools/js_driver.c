@@ -8,6 +8,7 @@
  *
  * Bench tooling only: not part of the product library. */
 #include <dlfcn.h>
+#include <stdio.h>
 #include <pthread.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -35,7 +36,14 @@ typedef struct {
   uint8_t *out;
   uint64_t produced, calls;
   int code;
+  double t_total, t_proc, t_init, t_end;  /* env ZS_JS_DRIVE_PROF: per-thread split (stderr) */
 } job_t;
+
+static double now_s(void) {
+  struct timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
+}
 
 static int unpack(uint32_t r, uint32_t *got) {
   *got = r & 0xffffffu;
@@ -45,8 +53,11 @@ static int unpack(uint32_t r, uint32_t *got) {
 static void *run_job(void *arg) {
   job_t *j = (job_t *)arg;
   const api_t *a = j->api;
+  const double ts = now_s();
   const uintptr_t h = a->f_new();
   a->f_init(h);
+  const double ti = now_s();
+  double tp = 0;
   size_t put = 0;
   int code = 0;
   uint64_t calls = 0;
@@ -57,9 +68,11 @@ static void *run_job(void *arg) {
       const size_t k = ln - off < 32768 ? ln - off : 32768;
       uint32_t got;
       const size_t room = j->out_cap - put < 65536 ? j->out_cap - put : 65536;
+      const double tq = now_s();
       code = unpack((uint32_t)a->f_proc(h, (uintptr_t)(j->comp + w + off), (unsigned)k, (uintptr_t)(j->out + put),
                                         (unsigned)room, 0),
                     &got);
+      tp += now_s() - tq;
       calls++;
       put += got;
       if (code < 0) break;
@@ -76,7 +89,13 @@ static void *run_job(void *arg) {
     put += got;
     if (code == 1 || got == 0) break;
   }
+  const double te0 = now_s();
   a->f_end(h);
+  const double te1 = now_s();
+  j->t_total = te1 - ts;
+  j->t_proc = tp;
+  j->t_init = ti - ts;
+  j->t_end = te1 - te0;
   j->produced = put;
   j->calls = calls;
   j->code = code;
@@ -121,6 +140,19 @@ double zs_js_drive(const char *lib_path, const uint8_t *const *comp, const size_
   }
   clock_gettime(CLOCK_MONOTONIC, &t1);
   *total_calls = calls;
+  if (getenv("ZS_JS_DRIVE_PROF") && started) {
+    double tt = 0, tp = 0, ti = 0, te = 0, tmax = 0;
+    for (int k = 0; k < started; k++) {
+      tt += js[k].t_total;
+      tp += js[k].t_proc;
+      ti += js[k].t_init;
+      te += js[k].t_end;
+      tmax = js[k].t_total > tmax ? js[k].t_total : tmax;
+    }
+    fprintf(stderr, "js_drive %d threads: per thread avg total %.2f ms (max %.2f), in process() %.2f ms, init %.3f ms, end %.3f ms; %.1f us per call in process()\n",
+            started, 1e3 * tt / started, 1e3 * tmax, 1e3 * tp / started, 1e3 * ti / started, 1e3 * te / started,
+            1e6 * tp / (double)(calls ? calls : 1));
+  }
   free(js);
   free(th);
   return started < n ? -2.0 : (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);

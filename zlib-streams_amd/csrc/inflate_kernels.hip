@@ -1467,11 +1467,8 @@ template __global__ void zs_decode_kernel<true>(const ZsJobDev *, const ZsHeadDe
 // ---------------------------------------------------------------------------
 // wave 0 of zs_stream_kernel: one call
 template <bool D64>
-__device__ __forceinline__ void zs_stream_call(ZsStreamDev *const *__restrict__ sts, const ZsJobDev *__restrict__ jobs,
-                                               const ZsHeadDev *__restrict__ heads, StreamLDS<D64> &L) {
-  ZsStreamDev *__restrict__ st = sts[blockIdx.x];
-  const ZsJobDev *__restrict__ job = jobs + blockIdx.x;
-  const ZsHeadDev *__restrict__ head = heads + blockIdx.x;
+__device__ __forceinline__ void zs_stream_call(ZsStreamDev *__restrict__ st, const ZsJobDev *__restrict__ job,
+                                               const ZsHeadDev *__restrict__ head, StreamLDS<D64> &L) {
   uint8_t *s_ring = L.ring;
   uint32_t *s_in = L.in;
   uint32_t *s_tab = L.tab;
@@ -1597,17 +1594,15 @@ __device__ __forceinline__ void zs_stream_call(ZsStreamDev *const *__restrict__ 
   }
 }
 
+// One call by the whole workgroup (head: the wrapper header parse, read only
+// in HEAD mode): wave 0 runs the call's exact state machine, the other waves
+// join its workgroup-wide symbol windows (WideLDS)
 template <bool D64>
-__global__ void __launch_bounds__(WW_T) zs_stream_kernel(ZsStreamDev *const *__restrict__ sts, const ZsJobDev *__restrict__ jobs,
-                                                          const ZsHeadDev *__restrict__ heads) {
-  // one workgroup per call of the batch (calls of different handles; see
-  // zs_launch_stream): wave 0 runs the call's exact state machine, the other
-  // waves join its workgroup-wide symbol windows (WideLDS)
-  __shared__ StreamLDS<D64> L;
+__device__ __forceinline__ void zs_stream_wg(ZsStreamDev *__restrict__ st, const ZsJobDev *__restrict__ job,
+                                             const ZsHeadDev *__restrict__ head, StreamLDS<D64> &L) {
   constexpr uint32_t RING = StreamLDS<D64>::RING;
   constexpr uint32_t WOFF = 65536u - RING;
   const uint32_t t = threadIdx.x;
-  ZsStreamDev *__restrict__ st = sts[blockIdx.x];
   {  // the handle's history window into the ring, by every wave (a resumed call)
     const int32_t mode0 = st->mode;
     if (mode0 >= ZSM_TYPE && mode0 <= ZSM_STORED && st->total_out)
@@ -1630,7 +1625,7 @@ __global__ void __launch_bounds__(WW_T) zs_stream_kernel(ZsStreamDev *const *__r
       ww_run<D64>(L);
     }
   } else {
-    zs_stream_call<D64>(sts, jobs, heads, L);
+    zs_stream_call<D64>(st, job, head, L);
     if (t == 0) L.wide.op = WW_EXIT;
     __syncthreads();
   }
@@ -1651,8 +1646,31 @@ __global__ void __launch_bounds__(WW_T) zs_stream_kernel(ZsStreamDev *const *__r
   }
 }
 
+template <bool D64>
+__global__ void __launch_bounds__(WW_T) zs_stream_kernel(ZsStreamDev *const *__restrict__ sts, const ZsJobDev *__restrict__ jobs,
+                                                          const ZsHeadDev *__restrict__ heads) {
+  // one workgroup per call of the batch (calls of different handles; see zs_launch_stream)
+  __shared__ StreamLDS<D64> L;
+  zs_stream_wg<D64>(sts[blockIdx.x], jobs + blockIdx.x, heads + blockIdx.x, L);
+}
+
 template __global__ void zs_stream_kernel<false>(ZsStreamDev *const *, const ZsJobDev *, const ZsHeadDev *);
 template __global__ void zs_stream_kernel<true>(ZsStreamDev *const *, const ZsJobDev *, const ZsHeadDev *);
+
+// A handle's device state after inflateInit / inflateReset (its first call sets
+// it up: no copy or synchronisation of its own at init): zlib's mode for the
+// wrapper, the window bits, everything else zero.
+__device__ void stream_state_init(ZsStreamDev *st, const ZsJobDev &jb) {
+  st->mode = jb.wrap == ZW_RAW ? ZSM_TYPE : ZSM_HEAD;
+  st->rbit = st->last = st->btype = st->nlen = st->ndist = st->len = st->dist = 0;
+  st->wbits = (uint32_t)jb.wbits;
+  st->is_gzip = -1;
+  st->total_out = 0;
+  st->ck_a = st->ck_b = 0;
+  st->code = st->msg = 0;
+  st->stop_bits = st->produced = st->check = st->tab_bits = 0;
+  st->acc_a = st->acc_b = 0;
+}
 
 // The calls' inputs from host-mapped staging into their device buffers, and
 // the carried restart bit (a workgroup column per call; before the decode).
@@ -1661,7 +1679,10 @@ __global__ void __launch_bounds__(SIO_THREADS) zs_stream_in_kernel(ZsStreamDev *
                                                                    const ZsJobDev *__restrict__ jobs,
                                                                    const ZsStreamIo *__restrict__ io) {
   const ZsStreamIo c = io[blockIdx.y];
-  if (blockIdx.x == 0 && threadIdx.x == 0) sts[blockIdx.y]->rbit = c.rbit;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (c.fresh) stream_state_init(sts[blockIdx.y], jobs[blockIdx.y]);
+    sts[blockIdx.y]->rbit = c.rbit;
+  }
   if (!c.hin) return;
   const uint64_t n = jobs[blockIdx.y].in_len;
   uint8_t *dst = const_cast<uint8_t *>(jobs[blockIdx.y].in);
@@ -1814,6 +1835,150 @@ extern "C" void zs_launch_stream(int d64, int run_header, ZsStreamDev *const *d_
   const uint32_t pieces = (uint32_t)std::min<uint64_t>(1024, std::max<uint64_t>(1, (max_out_cap + 16383) / 16384));
   hipLaunchKernelGGL(zs_stream_check_kernel, dim3(pieces, n), dim3(SCHECK_THREADS), 0, stream, d_sts, d_jobs, io);
   hipLaunchKernelGGL(zs_stream_finish_kernel, dim3(n), dim3(64), 0, stream, d_sts, d_jobs, d_res);
+}
+
+// ---------------------------------------------------------------------------
+// Persistent stream worker: a workgroup per mailbox (ZsMbox, host-coherent
+// pinned memory) takes its handle's calls one at a time and completes each on
+// its own -- input pull, the call (zs_stream_wg), output push and check, the
+// trailer states, the outcome -- so a call returns when ITS workgroup is done,
+// not when the slowest call of a launch is (the batch path: ~2x the mean call
+// at 64 handles).  Wave 0 polls its mailbox with vector loads at system scope
+// (never the scalar cache), sleeping between polls.  Every workgroup leaves
+// when no call was posted to any mailbox for idle_t ticks (s_memrealtime,
+// 100 MHz), when the host sets ctl[0], or, between calls, once the launch is
+// older than life_t: the grid always drains; the host relaunches on demand.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t pk_ld(const uint32_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void pk_st(uint32_t *p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+template <bool D64>
+__global__ void __launch_bounds__(WW_T) zs_stream_pk_kernel(ZsMbox *__restrict__ mbs, const uint32_t *__restrict__ ctl,
+                                                             uint32_t zero, uint64_t idle_t, uint64_t life_t) {
+  __shared__ StreamLDS<D64> L;
+  __shared__ __attribute__((aligned(16))) uint32_t s_mb[ZS_MBOX_CALL_WORDS];
+  __shared__ uint32_t s_cmd, s_n, s_mode;
+  __shared__ int32_t s_gz;
+  __shared__ uint32_t s_tab[4][256];
+  __shared__ uint64_t s_red[16];
+  const uint32_t t = threadIdx.x, lane = t & 63u;
+  // lane-dependent addresses (zero == 0): vector memory, never the scalar cache
+  uint32_t *mbw = reinterpret_cast<uint32_t *>(mbs + blockIdx.x) + zero * t;
+  const uint32_t *ctw = ctl + zero * t;
+  uint32_t done = pk_ld(mbw + 1);  // seq_out: the last call of this mailbox already finished
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    if (t < WAVE) {
+      uint64_t last = __builtin_amdgcn_s_memrealtime();
+      uint32_t post = pk_ld(ctw + 1), cmd = 0, nap = 1;
+      for (;;) {
+        const uint32_t q = pk_ld(mbw);
+        if (q != done) {
+          cmd = q;
+          break;
+        }
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        const uint32_t p2 = pk_ld(ctw + 1);
+        if (p2 != post) {
+          post = p2;
+          last = now;
+        }
+        if (pk_ld(ctw) != 0u || now - last > idle_t || now - t0 > life_t) break;
+        for (uint32_t k = 0; k < nap; k++) __builtin_amdgcn_s_sleep(32);
+        nap = min(nap * 2u, 8u);
+      }
+      if (cmd) {  // the call's fields after its seq_in (system-scope acquire)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        for (uint32_t k = lane; k < ZS_MBOX_CALL_WORDS; k += WAVE) s_mb[k] = pk_ld(mbw + 4u + k);
+      }
+      if (lane == 0) s_cmd = cmd;
+    }
+    __syncthreads();
+    const uint32_t cmd = s_cmd;
+    if (cmd == 0) break;
+    const uint64_t tc0 = __builtin_amdgcn_s_memrealtime();
+    ZsStreamDev *st = *reinterpret_cast<ZsStreamDev *const *>(&s_mb[0]);
+    const ZsStreamIo io = *reinterpret_cast<const ZsStreamIo *>(&s_mb[4]);
+    const ZsJobDev *job = reinterpret_cast<const ZsJobDev *>(&s_mb[12]);
+    {  // input: host-mapped staging -> the job's device buffer; the carried restart bit
+      const uint64_t n = job->in_len;
+      uint8_t *dst = const_cast<uint8_t *>(job->in);
+      if (io.hin) {
+        const uint64_t nw = n / 16u;
+        for (uint64_t k = t; k < nw; k += WW_T) reinterpret_cast<uint4 *>(dst)[k] = reinterpret_cast<const uint4 *>(io.hin)[k];
+        if (t < (n & 15u)) dst[nw * 16u + t] = io.hin[nw * 16u + t];
+      }
+      if (t == 0) {
+        if (io.fresh) stream_state_init(st, *job);
+        st->rbit = io.rbit;
+      }
+    }
+    // the copies and the handle's state (last written by any workgroup, any
+    // launch) before the call reads them
+    __threadfence();
+    __syncthreads();
+    __threadfence();
+    zs_stream_wg<D64>(st, job, nullptr, L);
+    __threadfence();
+    __syncthreads();
+    __threadfence();
+    if (t == 0) {
+      s_n = st->produced;
+      s_mode = (uint32_t)st->mode;
+      s_gz = st->is_gzip;
+    }
+    __syncthreads();
+    const uint64_t n = s_n;
+    if (n && s_mode != (uint32_t)ZSM_HEAD) {  // zs_stream_check_kernel for one call, one piece
+      const uint8_t *p = job->out;
+      if (uint8_t *h = io.hout) {
+        const uint64_t nw = n / 16u;
+        for (uint64_t k = t; k < nw; k += WW_T) reinterpret_cast<uint4 *>(h)[k] = reinterpret_cast<const uint4 *>(p)[k];
+        if (t < (n & 15u)) h[nw * 16u + t] = p[nw * 16u + t];
+      }
+      const int gz = s_gz;
+      const uint64_t per = ((n + WW_T - 1) / WW_T + 3u) & ~3ull;
+      const uint64_t lo = min(n, per * t), hi = min(n, per * (t + 1));
+      if (gz == 1) {
+        zs_crc_tables(s_tab);
+        const uint32_t v = zs_block_xor(zs_crc_piece(p, lo, hi, n, s_tab), reinterpret_cast<uint32_t *>(s_red));
+        if (t == 0) st->acc_a = v;
+      } else if (gz == 0) {
+        uint32_t A = 0, B = 0;
+        if (hi > lo) zs_adler_piece(p, lo, hi, n, &A, &B);
+        const uint64_t sa = zs_block_sum(A, s_red);
+        const uint64_t sb = zs_block_sum(B, s_red);
+        if (t == 0) {
+          st->acc_a = sa;
+          st->acc_b = sb;
+        }
+      }
+    }
+    if (t == 0) {  // the trailer states and the outcome (zs_stream_finish_kernel)
+      stream_finish(*st, job);
+      const uint32_t r[8] = {(uint32_t)st->mode, st->rbit, (uint32_t)st->code, (uint32_t)st->msg,
+                             st->stop_bits, (uint32_t)st->produced, st->check, (uint32_t)st->is_gzip};
+#pragma unroll
+      for (int k = 0; k < 8; k++) pk_st(mbw + 32u + k, r[k]);
+      pk_st(mbw + 40u, (uint32_t)(__builtin_amdgcn_s_memrealtime() - tc0));
+    }
+    // this workgroup's output words and state before seq_out (system-scope release)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    __syncthreads();
+    if (t == 0) pk_st(mbw + 1, cmd);
+    done = cmd;
+  }
+}
+
+template __global__ void zs_stream_pk_kernel<false>(ZsMbox *, const uint32_t *, uint32_t, uint64_t, uint64_t);
+
+extern "C" void zs_launch_stream_pk(ZsMbox *d_mb, uint32_t nw, const uint32_t *d_ctl, uint64_t idle_t, uint64_t life_t,
+                                    hipStream_t stream) {
+  hipLaunchKernelGGL(zs_stream_pk_kernel<false>, dim3(nw), dim3(WW_T), 0, stream, d_mb, d_ctl, 0u, idle_t, life_t);
 }
 
 // ---------------------------------------------------------------------------

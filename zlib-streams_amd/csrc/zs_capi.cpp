@@ -14,6 +14,7 @@
 #include "zs_check.h"
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
@@ -21,6 +22,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/zstreams_mi355x.h"
@@ -35,6 +37,8 @@ extern "C" void zs_launch_finish(const ZsJobDev *d_jobs, const ZsHeadDev *d_head
 extern "C" void zs_launch_stream(int d64, int run_header, ZsStreamDev *const *d_sts, const ZsJobDev *d_jobs,
                                  ZsHeadDev *d_heads, const ZsStreamIo *io, uint32_t n, uint64_t max_in_len,
                                  uint64_t max_out_cap, ZsStreamRes *d_res, hipStream_t stream);
+extern "C" void zs_launch_stream_pk(ZsMbox *d_mb, uint32_t nw, const uint32_t *d_ctl, uint64_t idle_t, uint64_t life_t,
+                                    hipStream_t stream);
 extern "C" uint32_t zs_lane_resident_waves(void);
 extern "C" void zs_launch_fixed_tables(uint32_t *fixed, int d64, hipStream_t st);
 extern "C" void zs_launch_fixed_compact(uint32_t *fixed, hipStream_t st);
@@ -883,6 +887,9 @@ struct StreamState {
   uint8_t *h_in = nullptr, *h_out = nullptr;  // pinned staging (calls up to STAGE_MAX bytes)
   uint8_t *dh_in = nullptr, *dh_out = nullptr;  // their device views (host-mapped)
   size_t cap_hin = 0, cap_hout = 0;
+  int fresh = 0;  // the device state is set up by the next call (ZsStreamIo::fresh)
+  int pk_w = -1;  // the persistent worker's mailbox this handle holds (-1: none)
+  uint64_t pk_last_ns = 0;  // its last call's host wait (the next wait sleeps most of it)
 };
 
 constexpr size_t STAGE_MAX = 4u << 20;
@@ -1160,6 +1167,180 @@ int sq_submit(StreamCall *c) {
   return c->err;
 }
 
+// ---------------------------------------------------------------------------
+// Persistent stream worker (zs_stream_pk_kernel): one launch of PK_WGS
+// workgroups, a mailbox each in host-coherent pinned memory.  A handle holds a
+// mailbox from its first mapped, header-less call until it ends; each of its
+// calls is posted there and returns when that workgroup finished it -- no
+// launch, no batch, no wait for other handles' calls.  The launch leaves by
+// itself after PK_IDLE_US without posts (or PK_LIFE_MS, between calls), and
+// the next post relaunches it: a waiter that finds the launch ended with its
+// call undone relaunches (only ever one launch; the call stays posted).
+// Calls that need the wrapper header, DMA staging or deflate64, and handles
+// beyond the mailboxes, take the batch path.  env ZS_STREAM_PK=0 disables it.
+// ---------------------------------------------------------------------------
+constexpr int PK_MAX = 256;
+struct PkState {
+  std::mutex mu;
+  ZsMbox *h_mb = nullptr, *d_mb = nullptr;
+  uint32_t *h_ctl = nullptr, *d_ctl = nullptr;
+  hipStream_t st = nullptr;
+  hipEvent_t ev = nullptr;  // end of the current launch
+  bool launched = false, broken = false;
+  int nw = 0;
+  std::vector<int> free_w;
+  uint32_t seq[PK_MAX] = {};
+  uint64_t launches = 0;
+  std::atomic<uint64_t> calls{0}, busy_ns{0}, wait_ns{0};  // the calls' workgroup time; post to seen-done on the host
+  std::atomic<int64_t> last_post{0};  // steady_clock ns of the last post (the launch outlives it by >= PK_IDLE)
+} g_pk;
+std::atomic<int> g_pk_on{-1};  // -1: from env ZS_STREAM_PK (default on)
+
+bool pk_enabled() {
+  int v = g_pk_on.load();
+  if (v < 0) {
+    const char *e = std::getenv("ZS_STREAM_PK");
+    v = (e && e[0] == '0') ? 0 : 1;
+    g_pk_on.store(v);
+  }
+  return v != 0;
+}
+
+void pk_atexit() {  // let the launch leave before the runtime tears down
+  if (!g_pk.h_ctl) return;
+  __atomic_store_n(&g_pk.h_ctl[0], 1u, __ATOMIC_SEQ_CST);
+  if (g_pk.launched && g_pk.ev) (void)hipEventSynchronize(g_pk.ev);
+}
+
+int pk_init_locked() {
+  if (g_pk.h_mb) return 0;
+  if (g_pk.broken) return ZS_ENODEV;
+  const char *e = std::getenv("ZS_PK_WGS");
+  const int nw = std::max(1, std::min(PK_MAX, e ? std::atoi(e) : 64));
+  void *h = nullptr;
+  const size_t bytes = sizeof(ZsMbox) * (size_t)nw + ZS_PK_CTL_WORDS * sizeof(uint32_t);
+  if (hipHostMalloc(&h, bytes, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
+    (void)hipGetLastError();
+    g_pk.broken = true;
+    return ZS_ENODEV;
+  }
+  std::memset(h, 0, bytes);
+  void *d = nullptr;
+  if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess || hipStreamCreateWithFlags(&g_pk.st, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&g_pk.ev, hipEventDisableTiming) != hipSuccess) {
+    (void)hipGetLastError();
+    (void)hipHostFree(h);
+    g_pk.broken = true;
+    return ZS_ENODEV;
+  }
+  g_pk.h_mb = static_cast<ZsMbox *>(h);
+  g_pk.d_mb = static_cast<ZsMbox *>(d);
+  g_pk.h_ctl = reinterpret_cast<uint32_t *>(g_pk.h_mb + nw);
+  g_pk.d_ctl = reinterpret_cast<uint32_t *>(g_pk.d_mb + nw);
+  g_pk.nw = nw;
+  for (int w = nw - 1; w >= 0; w--) g_pk.free_w.push_back(w);
+  std::atexit(pk_atexit);
+  return 0;
+}
+
+bool pk_running_locked() {
+  if (!g_pk.launched) return false;
+  const hipError_t q = hipEventQuery(g_pk.ev);
+  if (q == hipErrorNotReady) return true;
+  (void)hipGetLastError();
+  g_pk.launched = false;
+  return false;
+}
+
+int64_t pk_idle_us() {
+  static const int64_t v = [] {
+    const char *e = std::getenv("ZS_PK_IDLE_US");
+    return (int64_t)std::max(100LL, e ? std::atoll(e) : 2000LL);
+  }();
+  return v;
+}
+
+int64_t pk_now_ns() {
+  return (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+int pk_launch_locked() {
+  const uint64_t idle_t = (uint64_t)pk_idle_us() * 100u;  // s_memrealtime ticks (100 MHz)
+  static const uint64_t life_t = [] {
+    const char *e = std::getenv("ZS_PK_LIFE_MS");
+    return (uint64_t)(e ? std::atoll(e) : 500) * 100000u;
+  }();
+  zs_launch_stream_pk(g_pk.d_mb, (uint32_t)g_pk.nw, g_pk.d_ctl, idle_t, life_t, g_pk.st);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipEventRecord(g_pk.ev, g_pk.st));
+  g_pk.launched = true;
+  g_pk.launches++;
+  return 0;
+}
+
+// the handle's mailbox (taken on first use), or -1: the batch path
+int pk_attach(StreamState *s) {
+  if (s->pk_w >= 0) return s->pk_w;
+  std::lock_guard<std::mutex> lk(g_pk.mu);
+  if (pk_init_locked() || g_pk.free_w.empty()) return -1;
+  s->pk_w = g_pk.free_w.back();
+  g_pk.free_w.pop_back();
+  return s->pk_w;
+}
+
+void pk_detach(StreamState *s) {  // the handle's calls are all finished
+  if (s->pk_w < 0) return;
+  std::lock_guard<std::mutex> lk(g_pk.mu);
+  g_pk.free_w.push_back(s->pk_w);
+  s->pk_w = -1;
+}
+
+int pk_submit(StreamCall *c, int w) {
+  ZsMbox *m = g_pk.h_mb + w;
+  m->st = c->s->d_st;
+  m->io = c->io;
+  m->job = c->jb;
+  const uint32_t seq = ++g_pk.seq[w] ? g_pk.seq[w] : ++g_pk.seq[w];  // never 0 (the worker's "no call")
+  __atomic_thread_fence(__ATOMIC_SEQ_CST);  // the call's fields before seq_in (also for write-combined mappings)
+  __atomic_store_n(&m->seq_in, seq, __ATOMIC_SEQ_CST);
+  __atomic_fetch_add(&g_pk.h_ctl[1], 1u, __ATOMIC_SEQ_CST);
+  const int64_t t0 = pk_now_ns();
+  // a post within half the idle time of the previous one finds the launch alive
+  // (its workgroups saw that post and wait PK_IDLE after it); else look
+  if (t0 - g_pk.last_post.exchange(t0) > pk_idle_us() * 500) {
+    std::lock_guard<std::mutex> lk(g_pk.mu);
+    if (!pk_running_locked())
+      if (int rc = pk_launch_locked()) return rc;
+  }
+  // sleep through most of the expected call (the last one's wait), then poll
+  const int64_t expect = (int64_t)c->s->pk_last_ns;
+  if (expect > 150000) std::this_thread::sleep_for(std::chrono::nanoseconds(expect - 100000));
+  int64_t next_look = t0 + 2000000;  // the launch may have left (PK_LIFE) before it saw the call
+  for (;;) {
+    if (__atomic_load_n(&m->seq_out, __ATOMIC_ACQUIRE) == seq) break;
+    const int64_t now = pk_now_ns();
+    if (now > next_look) {
+      next_look = now + 1000000;
+      std::lock_guard<std::mutex> lk(g_pk.mu);
+      if (!pk_running_locked()) {
+        if (__atomic_load_n(&m->seq_out, __ATOMIC_ACQUIRE) == seq) break;
+        if (int rc = pk_launch_locked()) return rc;
+      }
+    }
+    if (now - t0 < 3 * std::max<int64_t>(expect, 100000)) std::this_thread::yield();
+    else std::this_thread::sleep_for(std::chrono::microseconds(10));
+  }
+  const uint64_t waited = (uint64_t)(pk_now_ns() - t0);
+  c->s->pk_last_ns = waited;
+  ZsStreamRes r;
+  std::memcpy(&r, (const void *)&m->res, sizeof(r));
+  c->res = r;
+  g_pk.calls.fetch_add(1);
+  g_pk.busy_ns.fetch_add((uint64_t)__atomic_load_n(&m->busy, __ATOMIC_RELAXED) * 10u);
+  g_pk.wait_ns.fetch_add(waited);
+  return 0;
+}
+
 // Device / pinned resources of ended streams, kept for the next ones:
 // hipMalloc, hipHostMalloc and stream creation cost up to milliseconds and
 // serialise concurrent callers, and hipFree synchronises the device, so a
@@ -1224,13 +1405,9 @@ int stream_init(StreamState *s, int wbits) {
     set_err("stream: device state allocation failed");
     return Z_MEM_ERROR;
   }
-  ZsStreamDev h;
-  std::memset(&h, 0, offsetof(ZsStreamDev, lens));
-  h.mode = cfg.wrap == ZW_RAW ? ZSM_TYPE : ZSM_HEAD;
-  h.wbits = (uint32_t)cfg.wbits;
-  h.is_gzip = -1;
-  HIP_OK(hipMemcpyAsync(s->d_st, &h, offsetof(ZsStreamDev, lens), hipMemcpyHostToDevice, s->hs));
-  HIP_OK(hipStreamSynchronize(s->hs));
+  // the device state is set up by the first call (stream_state_init): no
+  // copy or synchronisation here, which many handles opened at once serialise on
+  const int mode0 = cfg.wrap == ZW_RAW ? ZSM_TYPE : ZSM_HEAD;
   StreamState keep = std::move(*s);
   *s = StreamState();
   s->d_st = keep.d_st;
@@ -1245,15 +1422,18 @@ int stream_init(StreamState *s, int wbits) {
   s->cap_hout = keep.cap_hout;
   s->dh_in = keep.dh_in;
   s->dh_out = keep.dh_out;
+  s->pk_w = keep.pk_w;
   s->inited = 1;
+  s->fresh = 1;
   s->wbits = wbits;
   s->cfg = cfg;
-  s->mode = h.mode;
+  s->mode = mode0;
   s->adler = (uint32_t)(cfg.wrap == ZW_RAW ? 0 : (cfg.wrap & 1));  // inflateResetKeep: strm->adler = wrap & 1
   return Z_OK;
 }
 
 void stream_free(StreamState *s) {
+  pk_detach(s);
   if (s->hs) (void)hipStreamSynchronize(s->hs);
   if (res_give(s)) return;
   if (s->d_st) (void)hipFree(s->d_st);
@@ -1348,6 +1528,7 @@ int stream_call(StreamState *s, const uint8_t *in, unsigned in_len, uint8_t *out
     c.io.hin = mapped ? s->dh_in : nullptr;
     c.io.hout = mapped ? s->dh_out : nullptr;
     c.io.rbit = s->carry_bit;
+    c.io.fresh = (uint32_t)s->fresh;
     c.s = s;
     c.jb = s->cfg;
     c.jb.in = s->d_in;
@@ -1355,7 +1536,9 @@ int stream_call(StreamState *s, const uint8_t *in, unsigned in_len, uint8_t *out
     c.jb.out = s->d_out;
     c.jb.out_cap = (uint64_t)out_len - prod;
     c.run_header = s->mode == ZSM_HEAD;
-    if (int rc = sq_submit(&c)) return rc;
+    const int pw = (mapped && !c.run_header && !s->cfg.d64 && pk_enabled()) ? pk_attach(s) : -1;
+    if (int rc = pw >= 0 ? pk_submit(&c, pw) : sq_submit(&c)) return rc;
+    s->fresh = 0;
     h = c.res;
     if (h.produced && mapped) {
       std::memcpy(out + prod, hmo, h.produced);
@@ -2897,14 +3080,27 @@ int zs_stream_stats(uint64_t out[2]) {
   return 0;
 }
 
-int zs_stream_stats_ex(uint64_t out[5]) {
-  std::lock_guard<std::mutex> lk(g_sq.mu);
-  out[0] = g_sq.launches;
-  out[1] = g_sq.calls;
-  out[2] = g_sq.launch_ns;
-  out[3] = g_sq.gather_ns;
-  out[4] = g_sq.kernel_ns;
+int zs_stream_stats_ex(uint64_t out[9]) {
+  {
+    std::lock_guard<std::mutex> lk(g_sq.mu);
+    out[0] = g_sq.launches;
+    out[1] = g_sq.calls;
+    out[2] = g_sq.launch_ns;
+    out[3] = g_sq.gather_ns;
+    out[4] = g_sq.kernel_ns;
+  }
+  std::lock_guard<std::mutex> lk(g_pk.mu);
+  out[5] = g_pk.launches;
+  out[6] = g_pk.calls.load();
+  out[7] = g_pk.busy_ns.load();
+  out[8] = g_pk.wait_ns.load();
   return 0;
+}
+
+int zs_stream_persist(int on) {
+  const int prev = pk_enabled() ? 1 : 0;
+  if (on >= 0) g_pk_on.store(on ? 1 : 0);
+  return prev;
 }
 
 int zs_last_stats(uint32_t out[4]) {

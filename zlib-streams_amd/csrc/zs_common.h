@@ -5,6 +5,7 @@
 // into an out_cap-byte buffer (reference: src/inflate.c:597-1275 driven as in
 // test/payload_decompress.c:148-178 with the whole payload in one buffer).
 #pragma once
+#include <stddef.h>
 #include <stdint.h>
 
 // zlib return codes (zlib.h; reference callers decode them in
@@ -381,7 +382,7 @@ struct ZsStreamIo {
   const uint8_t *hin;  // host-mapped input, in_len bytes -> the job's in
   uint8_t *hout;       // host-mapped output: the call's produced bytes <- the job's out
   uint32_t rbit;       // restart bit within input byte 0 (the carried partial byte)
-  uint32_t pad;
+  uint32_t fresh;      // 1: the handle's first call since init / reset -- the device state is set up first
 };
 
 // Outcome of one stream call (device -> host, gathered per batch).
@@ -395,6 +396,28 @@ struct ZsStreamRes {
   uint32_t check;
   int32_t is_gzip;
 };
+
+// Mailbox of one workgroup of the persistent stream worker (zs_stream_pk_kernel),
+// in host-coherent pinned memory: the host writes the call (st, io, job), then
+// seq_in; the workgroup runs it and writes res, then seq_out = seq_in.
+struct ZsMbox {
+  uint32_t seq_in;   // host -> device, written last
+  uint32_t seq_out;  // device -> host, written last
+  uint32_t pad0[2];
+  ZsStreamDev *st;   // words 4..5: the call (ZS_MBOX_CALL_WORDS from word 4)
+  uint64_t pad1;
+  ZsStreamIo io;     // words 8..13
+  uint64_t pad2;
+  ZsJobDev job;      // words 16..31
+  ZsStreamRes res;   // words 32..39
+  uint32_t busy;     // word 40: the call's s_memrealtime ticks (100 MHz) from pickup to done
+  uint32_t pad3[23];
+};
+#define ZS_MBOX_CALL_WORDS 28u  // st .. job (words 4..31)
+static_assert(sizeof(ZsMbox) == 256, "one mailbox per 256 bytes");
+static_assert(offsetof(ZsMbox, io) == 32 && offsetof(ZsMbox, job) == 64 && offsetof(ZsMbox, res) == 128, "mailbox layout");
+// persistent worker control words (host-coherent): [0] stop, [1] posts (any mailbox)
+#define ZS_PK_CTL_WORDS 16u
 
 // Final per-job result (device -> host), zlib z_stream fields after the call.
 struct ZsResultDev {

@@ -67,6 +67,7 @@ _SIGS = {
     "zs_last_stats_ex": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32]),
     "zs_stream_stats": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64)]),
     "zs_stream_stats_ex": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64)]),
+    "zs_stream_persist": (ctypes.c_int, [ctypes.c_int]),
     "zs_synchronize": (ctypes.c_int, []),
     "zs_version": (ctypes.c_char_p, []), "zs_last_error": (ctypes.c_char_p, []),
 }
@@ -407,9 +408,15 @@ def last_stats():
 
 def stream_stats():
     """Stream-call batching since load: launch sequences and the calls they ran."""
-    a = (ctypes.c_uint64 * 5)()
+    a = (ctypes.c_uint64 * 9)()
     _check(lib().zs_stream_stats_ex(a))
-    return {"launches": a[0], "calls": a[1], "launch_ns": a[2], "gather_ns": a[3], "kernel_ns": a[4]}
+    return {"launches": a[0], "calls": a[1], "launch_ns": a[2], "gather_ns": a[3], "kernel_ns": a[4],
+            "pk_launches": a[5], "pk_calls": a[6], "pk_busy_ns": a[7], "pk_wait_ns": a[8]}
+
+
+def stream_persist(on=None):
+    """Persistent stream worker on / off (None: only read); returns the previous setting."""
+    return bool(lib().zs_stream_persist(-1 if on is None else int(bool(on))))
 
 
 def set_stream(hip_stream_handle):
