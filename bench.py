@@ -714,7 +714,7 @@ def stream_leg(args, zstreams, np, cpu):
     launches = st1["launches"] - st0["launches"]
     calls_m = st1["calls"] - st0["calls"]
     dl = {k: st1[k] - st0[k] for k in ("launch_ns", "gather_ns", "kernel_ns", "pk_launches", "pk_calls", "pk_busy_ns",
-                                       "pk_wait_ns")}
+                                       "pk_wait_ns", "pk_idle_ns")}
     okm = all(prod[k] == each and codes[k] == 1 and np.array_equal(outs[k][:each], rs[k]) for k in range(nh))
 
     # host zlib, same schedule: the one stream on 1 thread; the handle set on all cores
@@ -785,6 +785,7 @@ def stream_leg(args, zstreams, np, cpu):
                     "persistent_calls": dl["pk_calls"], "persistent_launches": dl["pk_launches"],
                     "persistent_call_us_avg": round(dl["pk_busy_ns"] / 1e3 / max(1, dl["pk_calls"]), 1),
                     "persistent_wait_us_avg": round(dl["pk_wait_ns"] / 1e3 / max(1, dl["pk_calls"]), 1),
+                    "persistent_idle_us_avg": round(dl["pk_idle_ns"] / 1e3 / max(1, dl["pk_calls"]), 1),
                     "verified": bool(okm)},
         "wasm_reference_mibs": 493,
         "compress_one_handle": {"value": round(len(dbytes) / tdz / 2**20, 1), "unit": "MiB/s (input)",

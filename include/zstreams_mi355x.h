@@ -215,8 +215,9 @@ int zs_stream_stats(uint64_t out[2]);
  * (ZS_STREAM_GATHER_US), out[4] the batches' kernel time (HIP events around
  * each launch sequence); the persistent worker: out[5] its launches, out[6] the
  * calls it ran, out[7] their workgroup time (pickup to done), out[8] their
- * host wait (post to seen done). */
-int zs_stream_stats_ex(uint64_t out[9]);
+ * host wait (post to seen done), out[9] the workgroups' idle time before each
+ * call (since their previous one). */
+int zs_stream_stats_ex(uint64_t out[10]);
 
 /* Persistent stream worker on (1) / off (0) for later calls; -1 only reads.
  * Returns the previous setting.  Default: on (env ZS_STREAM_PK=0: off).  With

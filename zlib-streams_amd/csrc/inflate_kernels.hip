@@ -1871,6 +1871,7 @@ __global__ void __launch_bounds__(WW_T) zs_stream_pk_kernel(ZsMbox *__restrict__
   const uint32_t *ctw = ctl + zero * t;
   uint32_t done = pk_ld(mbw + 1);  // seq_out: the last call of this mailbox already finished
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  uint64_t tdone = t0;
   for (;;) {
     if (t < WAVE) {
       uint64_t last = __builtin_amdgcn_s_memrealtime();
@@ -1964,12 +1965,17 @@ __global__ void __launch_bounds__(WW_T) zs_stream_pk_kernel(ZsMbox *__restrict__
                              st->stop_bits, (uint32_t)st->produced, st->check, (uint32_t)st->is_gzip};
 #pragma unroll
       for (int k = 0; k < 8; k++) pk_st(mbw + 32u + k, r[k]);
-      pk_st(mbw + 40u, (uint32_t)(__builtin_amdgcn_s_memrealtime() - tc0));
+      pk_st(mbw + 41u, (uint32_t)(tc0 - tdone));  // idle since the last call of this mailbox
     }
     // this workgroup's output words and state before seq_out (system-scope release)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     __syncthreads();
-    if (t == 0) pk_st(mbw + 1, cmd);
+    if (t == 0) {
+      tdone = __builtin_amdgcn_s_memrealtime();
+      pk_st(mbw + 40u, (uint32_t)(tdone - tc0));
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      pk_st(mbw + 1, cmd);
+    }
     done = cmd;
   }
 }

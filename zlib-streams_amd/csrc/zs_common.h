@@ -411,7 +411,8 @@ struct ZsMbox {
   ZsJobDev job;      // words 16..31
   ZsStreamRes res;   // words 32..39
   uint32_t busy;     // word 40: the call's s_memrealtime ticks (100 MHz) from pickup to done
-  uint32_t pad3[23];
+  uint32_t idle;     // word 41: ticks the workgroup waited for this call since its previous one
+  uint32_t pad3[22];
 };
 #define ZS_MBOX_CALL_WORDS 28u  // st .. job (words 4..31)
 static_assert(sizeof(ZsMbox) == 256, "one mailbox per 256 bytes");

@@ -408,10 +408,10 @@ def last_stats():
 
 def stream_stats():
     """Stream-call batching since load: launch sequences and the calls they ran."""
-    a = (ctypes.c_uint64 * 9)()
+    a = (ctypes.c_uint64 * 10)()
     _check(lib().zs_stream_stats_ex(a))
     return {"launches": a[0], "calls": a[1], "launch_ns": a[2], "gather_ns": a[3], "kernel_ns": a[4],
-            "pk_launches": a[5], "pk_calls": a[6], "pk_busy_ns": a[7], "pk_wait_ns": a[8]}
+            "pk_launches": a[5], "pk_calls": a[6], "pk_busy_ns": a[7], "pk_wait_ns": a[8], "pk_idle_ns": a[9]}
 
 
 def stream_persist(on=None):
