@@ -8,8 +8,12 @@ sys.path.insert(0, os.path.join(ROOT, "zlib-streams_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 import corpus, zstreams
 n = (int(sys.argv[1]) if len(sys.argv) > 1 else 16) << 20
-for name, sid in (("zipf", 0), ("lines", 33)):
-    d = corpus.stream(sid, n)
+import numpy as np
+kinds = os.environ.get("KINDS", "zipf,lines").split(",")
+for name, sid in (("zipf", 0), ("lines", 33), ("random", -1)):
+    if name not in kinds:
+        continue
+    d = corpus.stream(sid, n) if sid >= 0 else np.random.default_rng(7).integers(0, 256, n, dtype=np.uint8).tobytes()
     for lv in [int(x) for x in os.environ.get("LEVELS", "6,1").split(",")]:
         zstreams.compress(d[:1 << 20], "deflate-raw", lv, 65536)  # warm
         t0 = time.perf_counter()

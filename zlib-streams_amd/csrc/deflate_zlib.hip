@@ -826,6 +826,15 @@ __device__ __forceinline__ uint32_t zd_step(const ZdTabs &T, uint64_t &p, uint32
   return tok;
 }
 
+// A loop-top state with no match pending (prev_length 2: state A, or a literal
+// pending after a search that found nothing) walks on exactly as state A: the
+// next iteration reads only prev_length, and avail / the variant / a too-far
+// distance only decide the token at p - 1.  Walks that meet in such states at the
+// same position walk the same path from there (merge points of the parse,
+// re-walks and region fix-ups; on text with literal runs they meet far sooner
+// than at state A, and on incompressible data -- no state A at all -- at once).
+__device__ __forceinline__ bool zd_free(uint32_t st) { return ((st >> 1) & 511u) == 2u; }
+
 __device__ __forceinline__ void zd_setbit(uint32_t *w, uint64_t i) { w[i >> 5] |= 1u << (i & 31u); }
 __device__ __forceinline__ void zd_putbit(uint32_t *w, uint64_t i, bool v) {
   if (v) w[i >> 5] |= 1u << (i & 31u);
@@ -866,7 +875,7 @@ __device__ __forceinline__ void zd_walk_record(const ZdTabs &T, uint64_t &q, uin
   uint32_t var;
   bool first = !rec_first;
   while (q < hi) {
-    if (marks && qs == ZD_STATE_A) zd_setbit(marks, q - mark0);
+    if (marks && zd_free(qs)) zd_setbit(marks, q - mark0);
     if ((qs & 1u) && !first) set(q - 1, (qs >> 10) & 1u);
     first = false;
     (void)zd_step(T, q, qs, &var);
@@ -921,7 +930,7 @@ __global__ void __launch_bounds__(ZD_PT) zs_zd_parse_kernel(const ZsDJobDev *__r
     if (act) {
       bool merged = false;
       while (q < b) {
-        if (qs == ZD_STATE_A && zd_getbit(s_M, q - r0)) {
+        if (zd_free(qs) && zd_getbit(s_M, q - r0)) {
           merged = true;
           break;
         }
@@ -947,7 +956,7 @@ __global__ void __launch_bounds__(ZD_PT) zs_zd_parse_kernel(const ZsDJobDev *__r
     uint32_t qs = t == ent_t ? ent_s : s_xs[t - 1];
     uint64_t mq = q;
     uint32_t mqs = qs;
-    while (mq < b && !(mqs == ZD_STATE_A && zd_getbit(s_M, mq - r0))) (void)zd_step(T, mq, mqs, &var);
+    while (mq < b && !(zd_free(mqs) && zd_getbit(s_M, mq - r0))) (void)zd_step(T, mq, mqs, &var);
     const uint64_t mp = min(mq, b);
     for (uint64_t x = a; x < mp; x += 32u) {
       const uint32_t wi = (uint32_t)((x - r0) >> 5);
@@ -1001,7 +1010,7 @@ __device__ void zd_fix_region(const ZsDJobDev &jb, ZsDSegDev *__restrict__ segs,
   const uint64_t r0 = sg.start, rend = sg.start + sg.len;
   xp = sg.zx0;
   xs = sg.zs0;
-  if (ep == r0 && es == ZD_STATE_A && sg.zfix == r0) return;  // its own parse stands
+  if (ep == r0 && zd_free(es) && sg.zfix == r0) return;  // its own parse stands (a pending literal at r0 - 1 is the predecessor's)
   const ZdTabs T = zd_tabs(jb, ma, mb, prevd, bm);
   ZdBm Bm = zd_bm(bm, jb);
   // 1. where does the walk from the entry merge with the region's own parse?
@@ -1009,7 +1018,7 @@ __device__ void zd_fix_region(const ZsDJobDev &jb, ZsDSegDev *__restrict__ segs,
   uint32_t qs = es, var;
   bool merged = false;
   while (q < rend) {
-    if (qs == ZD_STATE_A && q >= sg.zfix && zd_getbit(Bm.M, q)) {
+    if (zd_free(qs) && q >= sg.zfix && zd_getbit(Bm.M, q)) {
       merged = true;
       break;
     }
@@ -1301,6 +1310,9 @@ __global__ void __launch_bounds__(WAVE) zs_zd_fast_kernel(ZsDJobDev *__restrict_
   };
   // the history before the parse entry: its inserted positions, in order
   // (a stream segment's window; the bits come from the previous segment)
+#if ZF_PROF
+  const uint64_t zh0 = __builtin_amdgcn_s_memtime();
+#endif
   for (uint64_t p = 0; p < jb.pstart; p += WAVE) {
     sweep_to(p);
     const uint64_t q = p + lane;
@@ -1311,6 +1323,7 @@ __global__ void __launch_bounds__(WAVE) zs_zd_fast_kernel(ZsDJobDev *__restrict_
   uint64_t p = jb.pstart;
   bool stop = false;
 #if ZF_PROF
+  const uint64_t zhist = __builtin_amdgcn_s_memtime() - zh0;
   uint64_t zt[6] = {0, 0, 0, 0, 0, 0}, zsteps = 0, zt0 = __builtin_amdgcn_s_memtime();
 #define ZF_T(i)                                         \
   do {                                                  \
@@ -1435,8 +1448,9 @@ __global__ void __launch_bounds__(WAVE) zs_zd_fast_kernel(ZsDJobDev *__restrict_
   }
 #if ZF_PROF
   if (lane == 0)
-    printf("zf job %u L=%lu steps %lu pos/step %.1f clk/step: sweep %lu hash+same %lu search %lu commit %lu out+ins %lu\n",
-           blockIdx.x, (unsigned long)L, (unsigned long)zsteps, (double)(p - jb.pstart) / (double)(zsteps ? zsteps : 1),
+    printf("zf job %u L=%lu pstart %lu history clk %lu steps %lu pos/step %.1f clk/step: sweep %lu hash+same %lu search %lu commit %lu out+ins %lu\n",
+           blockIdx.x, (unsigned long)L, (unsigned long)jb.pstart, (unsigned long)zhist, (unsigned long)zsteps,
+           (double)(p - jb.pstart) / (double)(zsteps ? zsteps : 1),
            (unsigned long)(zt[0] / (zsteps ? zsteps : 1)), (unsigned long)(zt[1] / (zsteps ? zsteps : 1)),
            (unsigned long)(zt[2] / (zsteps ? zsteps : 1)), (unsigned long)(zt[3] / (zsteps ? zsteps : 1)),
            (unsigned long)(zt[4] / (zsteps ? zsteps : 1)));
