@@ -2114,6 +2114,12 @@ __global__ void __launch_bounds__(ZD_TT) zs_zd_tree_kernel(const ZsDJobDev *__re
   T.in = jb.in;
   T.L = jb.in_len;
   const ZdBm B = zd_bm(bm, jb);
+#ifndef ZD_TREE_PROF
+#define ZD_TREE_PROF 0  // per-block phase clocks, printed for a few blocks (tools/build_variant.sh ... -DZD_TREE_PROF=1)
+#endif
+#if ZD_TREE_PROF
+  const uint64_t tp0 = clock64();
+#endif
   for (uint32_t i = t; i < 288; i += ZD_TT) s_lf[i] = 0;
   if (t < 32) s_df[t] = 0;
   __syncthreads();
@@ -2129,6 +2135,9 @@ __global__ void __launch_bounds__(ZD_TT) zs_zd_tree_kernel(const ZsDJobDev *__re
   });
   __syncthreads();
   if (t != 0) return;
+#if ZD_TREE_PROF
+  const uint64_t tp1 = clock64();
+#endif
   uint8_t stat_l[288], stat_d[30];
   for (int i = 0; i < 288; i++) stat_l[i] = i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : 8;
   for (int i = 0; i < 30; i++) stat_d[i] = 5;
@@ -2187,6 +2196,11 @@ __global__ void __launch_bounds__(ZD_TT) zs_zd_tree_kernel(const ZsDJobDev *__re
     o.bits = hb + body_dyn;
   }
   blks[blockIdx.x] = o;
+#if ZD_TREE_PROF
+  if (blockIdx.x < 4)
+    printf("zd_tree blk %u syms %lu type %u: count %lu cyc, build %lu cyc (lmax %d)\n", blockIdx.x, (unsigned long)n, o.type,
+           (unsigned long)(tp1 - tp0), (unsigned long)(clock64() - tp1), lmax);
+#endif
   uint32_t *ax = aux + (size_t)blockIdx.x * ZD_AUX;
   if (o.type == 1) {
     for (int i = 0; i < 286; i++) {
