@@ -1918,15 +1918,15 @@ __global__ void __launch_bounds__(WW_T) zs_stream_pk_kernel(ZsMbox *__restrict__
         st->rbit = io.rbit;
       }
     }
-    // the copies and the handle's state (last written by any workgroup, any
-    // launch) before the call reads them
-    __threadfence();
+    // the copies (stores complete at the barrier) before the call reads them:
+    // an agent-scope acquire drops stale L1 lines (the handle's state from any
+    // other workgroup, launch or batch kernel came in with the system-scope
+    // acquire after seq_in, which also invalidates L2)
     __syncthreads();
-    __threadfence();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     zs_stream_wg<D64>(st, job, nullptr, L);
-    __threadfence();
     __syncthreads();
-    __threadfence();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     if (t == 0) {
       s_n = st->produced;
       s_mode = (uint32_t)st->mode;
@@ -1967,8 +1967,8 @@ __global__ void __launch_bounds__(WW_T) zs_stream_pk_kernel(ZsMbox *__restrict__
       for (int k = 0; k < 8; k++) pk_st(mbw + 32u + k, r[k]);
       pk_st(mbw + 41u, (uint32_t)(tc0 - tdone));  // idle since the last call of this mailbox
     }
-    // this workgroup's output words and state before seq_out (system-scope release)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    // every wave's output words and state stores complete at the barrier; one
+    // system-scope release writes the L2 back before seq_out
     __syncthreads();
     if (t == 0) {
       tdone = __builtin_amdgcn_s_memrealtime();
