@@ -1901,7 +1901,16 @@ struct ZdTreeLDS {
   int16_t heap[ZD_HEAP];  // the nodes in extraction order (heap[heap_max..])
   uint64_t hk[ZD_HEAP];   // the live heap: (freq << 8 | depth) << 10 | node
   uint16_t blc[16];
+  uint32_t next[16];      // gen_codes' next code per length
+  uint32_t blf[19];       // bit-length code frequencies (scan_tree)
 };
+
+// trees.c tr_static_init's static code lengths: literal/length (kind 1) 8 / 9 /
+// 7 / 8 by symbol range, distance (kind 2) 5 -- computed, not a private array
+// (dynamically indexed private arrays live in scratch memory)
+__device__ __forceinline__ uint32_t zd_stat_len(int kind, int n) {
+  return kind == 2 ? 5u : (n < 144 ? 8u : n < 256 ? 9u : n < 280 ? 7u : 8u);
+}
 
 // zlib's smaller(): freq, then depth, as one key -- the heap holds its
 // entries' keys, so a sift level is one LDS round trip (two children), not
@@ -1929,7 +1938,7 @@ __device__ void zd_sift(ZdTreeLDS &w, int hl, int k) {
 
 // freq[0..elems) in w.freq; lens out in len_out[0..elems), canonical LSB-first
 // codes in code_out; returns max_code.  stat: static lengths (nullptr: none).
-__device__ int zd_build(ZdTreeLDS &w, int elems, const uint8_t *stat, const uint8_t *xb, int xbase, int maxlen,
+__device__ int zd_build(ZdTreeLDS &w, int elems, int stat, const uint8_t *xb, int xbase, int maxlen,
                         uint64_t &opt_len, uint64_t &static_len, uint16_t *len_out, uint16_t *code_out) {
   int max_code = -1, hl = 0, hmax = ZD_HEAP;
   for (int n = 0; n < elems; n++) {
@@ -1947,7 +1956,7 @@ __device__ int zd_build(ZdTreeLDS &w, int elems, const uint8_t *stat, const uint
     w.depth[node] = 0;
     w.hk[++hl] = zd_key(w, node);
     opt_len--;
-    if (stat) static_len -= stat[node];
+    if (stat) static_len -= zd_stat_len(stat, node);
   }
   for (int n = hl / 2; n >= 1; n--) zd_sift(w, hl, n);
   int node = elems;
@@ -1977,7 +1986,7 @@ __device__ int zd_build(ZdTreeLDS &w, int elems, const uint8_t *stat, const uint
     w.blc[bits]++;
     const int x = n >= xbase ? xb[n - xbase] : 0;
     opt_len += (uint64_t)w.freq[n] * (uint64_t)(bits + x);
-    if (stat) static_len += (uint64_t)w.freq[n] * (uint64_t)(stat[n] + x);
+    if (stat) static_len += (uint64_t)w.freq[n] * (uint64_t)(zd_stat_len(stat, n) + x);
   }
   if (overflow) {
     do {
@@ -2001,12 +2010,12 @@ __device__ int zd_build(ZdTreeLDS &w, int elems, const uint8_t *stat, const uint
       }
     }
   }
-  uint32_t next[16], code = 0;
-  for (int b = 1; b <= 15; b++) next[b] = code = (code + w.blc[b - 1]) << 1;
+  uint32_t code = 0;
+  for (int b = 1; b <= 15; b++) w.next[b] = code = (code + w.blc[b - 1]) << 1;
   for (int n = 0; n < elems; n++) {
     const uint32_t len = n <= max_code ? w.dl[n] : 0u;
     len_out[n] = (uint16_t)len;
-    code_out[n] = len ? (uint16_t)zd_rev(next[len]++, len) : (uint16_t)0;
+    code_out[n] = len ? (uint16_t)zd_rev(w.next[len]++, len) : (uint16_t)0;
   }
   return max_code;
 }
@@ -2138,23 +2147,19 @@ __global__ void __launch_bounds__(ZD_TT) zs_zd_tree_kernel(const ZsDJobDev *__re
 #if ZD_TREE_PROF
   const uint64_t tp1 = clock64();
 #endif
-  uint8_t stat_l[288], stat_d[30];
-  for (int i = 0; i < 288; i++) stat_l[i] = i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : 8;
-  for (int i = 0; i < 30; i++) stat_d[i] = 5;
   uint64_t opt = 0, stat = 0;
   for (int i = 0; i < ZD_HEAP; i++) W.freq[i] = i < 286 ? s_lf[i] : 0u;
   W.freq[256] = 1;  // end of block
-  const int lmax = zd_build(W, 286, stat_l, zd_xl, 257, 15, opt, stat, s_ll, s_lc);
+  const int lmax = zd_build(W, 286, 1, zd_xl, 257, 15, opt, stat, s_ll, s_lc);
   for (int i = 0; i < ZD_HEAP; i++) W.freq[i] = i < 30 ? s_df[i] : 0u;
-  const int dmax = zd_build(W, 30, stat_d, zd_xd, 0, 15, opt, stat, s_dlen, s_dc);
-  uint32_t blf[19];
-  for (int i = 0; i < 19; i++) blf[i] = 0;
-  auto count = [&](int sym, uint32_t, uint32_t) { blf[sym]++; };
+  const int dmax = zd_build(W, 30, 2, zd_xd, 0, 15, opt, stat, s_dlen, s_dc);
+  for (int i = 0; i < 19; i++) W.blf[i] = 0;
+  auto count = [&](int sym, uint32_t, uint32_t) { W.blf[sym]++; };
   zd_rle(s_ll, lmax, count);
   zd_rle(s_dlen, dmax, count);
-  for (int i = 0; i < ZD_HEAP; i++) W.freq[i] = i < 19 ? blf[i] : 0u;
+  for (int i = 0; i < ZD_HEAP; i++) W.freq[i] = i < 19 ? W.blf[i] : 0u;
   uint64_t dummy = 0;
-  (void)zd_build(W, 19, nullptr, zd_xb, 0, 7, opt, dummy, s_bl, s_bc);
+  (void)zd_build(W, 19, 0, zd_xb, 0, 7, opt, dummy, s_bl, s_bc);
   int blmax = 18;
   for (; blmax >= 3; blmax--)
     if (s_bl[zd_blord[blmax]] != 0) break;
@@ -2174,7 +2179,7 @@ __global__ void __launch_bounds__(ZD_TT) zs_zd_tree_kernel(const ZsDJobDev *__re
     const uint64_t f = s_lf[i] + (i == 256 ? 1u : 0u);
     const uint32_t x = i >= 257 ? zd_xl[i - 257] : 0u;
     body_dyn += f * (s_ll[i] + x);
-    body_fix += f * (stat_l[i] + x);
+    body_fix += f * (zd_stat_len(1, i) + x);
   }
   for (int i = 0; i < 30; i++) {
     body_dyn += (uint64_t)s_df[i] * (s_dlen[i] + zd_xd[i]);
@@ -2204,7 +2209,7 @@ __global__ void __launch_bounds__(ZD_TT) zs_zd_tree_kernel(const ZsDJobDev *__re
   uint32_t *ax = aux + (size_t)blockIdx.x * ZD_AUX;
   if (o.type == 1) {
     for (int i = 0; i < 286; i++) {
-      const uint32_t L = stat_l[i];
+      const uint32_t L = zd_stat_len(1, i);
       uint32_t c;  // static code of symbol i (trees.c tr_static_init: canonical over 288 lengths)
       if (i < 144) c = 0x30 + i;
       else if (i < 256) c = 0x190 + (i - 144);

@@ -213,7 +213,7 @@ struct WideLDS {
   uint32_t wtot[WW_T / 64];
   uint32_t sk[WW_T / WW_SKIP];   // chain start of symbols 32 m
   uint32_t symL[WW_T], symD[WW_T];
-  uint8_t nb[WW_JN];           // symbol bits at each offset (0: no plain symbol starts there)
+  __attribute__((aligned(16))) uint8_t nb[WW_JN];  // symbol bits at each offset (0: no plain symbol starts there)
   __attribute__((aligned(16))) uint16_t ja[WW_JN];  // J0 (one symbol) -- kept
   __attribute__((aligned(16))) uint16_t jb[WW_JN];  // J1 .. J5, ping-pong with jc
   __attribute__((aligned(16))) uint16_t jc[WW_JN];
@@ -293,9 +293,8 @@ __device__ __forceinline__ uint64_t ww_bits_at(const uint32_t *inring, uint32_t 
 // (0: not a plain symbol), the length (0x80000000 | literal for a literal)
 // and the distance.
 template <bool D64>
-__device__ __forceinline__ uint32_t ww_decode(const WideLDS &w, const uint32_t *lt, const uint32_t *dt,
-                                              const uint32_t *inring, uint32_t q, uint32_t &lv, uint32_t &dv) {
-  const uint64_t hh = ww_bits_at(inring, q);
+__device__ __forceinline__ uint32_t ww_decode_bits(const WideLDS &w, const uint32_t *lt, const uint32_t *dt,
+                                                   const uint64_t hh, uint32_t q, uint32_t &lv, uint32_t &dv) {
   uint32_t e = lt[(uint32_t)hh & w.lmask];
   uint32_t used = e_bits(e);
   {
@@ -350,16 +349,28 @@ __device__ void ww_run(StreamLDS<D64> &Ls) {
   const uint32_t t = threadIdx.x;
   const uint32_t P = w.P, W = w.W;
   [[maybe_unused]] const uint64_t kt0 = KP_NOW();
-  // 1. a complete symbol at every offset of the window
+  // 1. a complete symbol at every offset of the window: thread t the 8
+  //    consecutive offsets 8t .. 8t + 7, whose bits one 128-bit read covers
   uint32_t lv[WW_OFFS], dv[WW_OFFS];
+  static_assert(WW_OFFS == 8, "8 consecutive offsets per thread");
+  {
+    const uint32_t q0 = WW_OFFS * t, b0 = P + q0, wq = b0 >> 5, sh = b0 & 31u;
+    const uint32_t a = inring[wq & (IN_RING_WORDS - 1)], b = inring[(wq + 1) & (IN_RING_WORDS - 1)];
+    const uint32_t c = inring[(wq + 2) & (IN_RING_WORDS - 1)], d = inring[(wq + 3) & (IN_RING_WORDS - 1)];
+    const uint64_t lo = ((uint64_t)b << 32) | a, hi = ((uint64_t)d << 32) | c;
+    uint32_t nbw[2] = {0, 0}, jw[4] = {0, 0, 0, 0};
 #pragma unroll
-  for (uint32_t i = 0; i < WW_OFFS; i++) {
-    const uint32_t q = t + i * WW_T;
-    uint32_t nb = 0;
-    lv[i] = dv[i] = 0;
-    if (q < W) nb = ww_decode<D64>(w, lt, dt, inring, P + q, lv[i], dv[i]);
-    w.nb[q] = (uint8_t)nb;
-    w.ja[q] = (uint16_t)(q + nb);
+    for (uint32_t i = 0; i < WW_OFFS; i++) {
+      const uint32_t q = q0 + i, x = sh + i;  // x <= 38
+      const uint64_t hh = (lo >> x) | (x ? hi << (64u - x) : 0ull);
+      uint32_t nb = 0;
+      lv[i] = dv[i] = 0;
+      if (q < W) nb = ww_decode_bits<D64>(w, lt, dt, hh, P + q, lv[i], dv[i]);
+      nbw[i >> 2] |= nb << (8u * (i & 3u));
+      jw[i >> 1] |= (q + nb) << (16u * (i & 1u));
+    }
+    *reinterpret_cast<uint2 *>(&w.nb[q0]) = make_uint2(nbw[0], nbw[1]);
+    *reinterpret_cast<uint4 *>(&w.ja[q0]) = make_uint4(jw[0], jw[1], jw[2], jw[3]);
   }
   if (t < WW_JN - WW_BITS) {
     w.nb[WW_BITS + t] = 0;
@@ -374,10 +385,14 @@ __device__ void ww_run(StreamLDS<D64> &Ls) {
   //    each thread walks J0 from its group's start (<= 31 steps)
   [[maybe_unused]] const uint64_t kt1 = KP_NOW();
   {
+    // J1 .. J4 ping-pong jb / jc (J3 ends in jb, J4 in jc); J5 is composed in
+    // place over J4 (all reads, a barrier, then the writes), so J3 survives:
+    // each thread then reaches its symbol from its 32-group's start in <= 3
+    // J3 hops and <= 7 J0 hops instead of <= 31 J0 hops
     const uint16_t *src = w.ja;
     uint16_t *dst = w.jb;
 #pragma unroll 1
-    for (uint32_t k = 0; k < 5; k++) {
+    for (uint32_t k = 0; k < 4; k++) {
       __syncthreads();
 #pragma unroll
       for (uint32_t i = 0; i < WW_OFFS; i++) {
@@ -389,35 +404,49 @@ __device__ void ww_run(StreamLDS<D64> &Ls) {
       dst = dst == w.jb ? w.jc : w.jb;
     }
     __syncthreads();
+    {
+      uint16_t j5[WW_OFFS];
+#pragma unroll
+      for (uint32_t i = 0; i < WW_OFFS; i++) j5[i] = w.jc[w.jc[t + i * WW_T]];
+      __syncthreads();
+#pragma unroll
+      for (uint32_t i = 0; i < WW_OFFS; i++) w.jc[t + i * WW_T] = j5[i];
+    }
+    __syncthreads();
     KPW0_ADD(KP_W_CYC_COMPOSE, KP_NOW() - kt1);
     if (t == 0) {
       uint32_t x = 0;
       for (uint32_t m = 0; m < WW_T / WW_SKIP; m++) {
         w.sk[m] = x;
-        x = src[x];
+        x = w.jc[x];
       }
     }
     __syncthreads();
   }
   uint32_t s = w.sk[t / WW_SKIP];
-  for (uint32_t r = t % WW_SKIP; r; r--) s = w.ja[s];
+  for (uint32_t r = (t % WW_SKIP) >> 3; r; r--) s = w.jb[s];
+  for (uint32_t r = t & 7u; r; r--) s = w.ja[s];
   KPW0_ADD(KP_W_CYC_WALK, KP_NOW() - kt1);  // compose + walks (thread 0 walks the J5 chain)
   // 3. the chain's symbols: inside the window and plain
   const uint32_t snb = s < WW_BITS ? w.nb[s] : 0u;
   ww_first(&w.cnt_min, !(s < W && snb != 0));
-  uint16_t *mark = w.jb;  // the jump tables are done with
+  uint16_t *mark = w.jc;  // J5 is done with (J3 in jb may still be read by other threads' walks)
 #pragma unroll
   for (uint32_t i = 0; i < WW_OFFS; i++) mark[t + i * WW_T] = 0;
   __syncthreads();
   const uint32_t cnt = w.cnt_min;
   if (t < cnt) mark[s] = (uint16_t)(t + 1u);
   __syncthreads();
+  {
+    const uint4 mk = *reinterpret_cast<const uint4 *>(&mark[WW_OFFS * t]);
+    const uint32_t mw[4] = {mk.x, mk.y, mk.z, mk.w};
 #pragma unroll
-  for (uint32_t i = 0; i < WW_OFFS; i++) {
-    const uint32_t m = mark[t + i * WW_T];
-    if (m) {
-      w.symL[m - 1u] = lv[i];
-      w.symD[m - 1u] = dv[i];
+    for (uint32_t i = 0; i < WW_OFFS; i++) {
+      const uint32_t m = (mw[i >> 1] >> (16u * (i & 1u))) & 0xffffu;
+      if (m) {
+        w.symL[m - 1u] = lv[i];
+        w.symD[m - 1u] = dv[i];
+      }
     }
   }
   __syncthreads();
