@@ -1875,8 +1875,9 @@ extern "C" void zs_launch_stream(int d64, int run_header, ZsStreamDev *const *d_
 // at 64 handles).  Wave 0 polls its mailbox with vector loads at system scope
 // (never the scalar cache), sleeping between polls.  Every workgroup leaves
 // when no call was posted to any mailbox for idle_t ticks (s_memrealtime,
-// 100 MHz), when the host sets ctl[0], or, between calls, once the launch is
-// older than life_t: the grid always drains; the host relaunches on demand.
+// 100 MHz), when the host sets ctl[0], or after its current call once the
+// launch is older than life_t: the grid always drains; the host relaunches on
+// demand.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t pk_ld(const uint32_t *p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1906,18 +1907,22 @@ __global__ void __launch_bounds__(WW_T) zs_stream_pk_kernel(ZsMbox *__restrict__
       uint64_t last = __builtin_amdgcn_s_memrealtime();
       uint32_t post = pk_ld(ctw + 1), cmd = 0, nap = 1;
       for (;;) {
+        // past its life (or told to stop) the launch leaves even with calls
+        // posted -- they stay posted for the relaunch -- so every workgroup
+        // goes within one call and no handle waits on the others' streams
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        if (now - t0 > life_t || pk_ld(ctw) != 0u) break;
         const uint32_t q = pk_ld(mbw);
         if (q != done) {
           cmd = q;
           break;
         }
-        const uint64_t now = __builtin_amdgcn_s_memrealtime();
         const uint32_t p2 = pk_ld(ctw + 1);
         if (p2 != post) {
           post = p2;
           last = now;
         }
-        if (pk_ld(ctw) != 0u || now - last > idle_t || now - t0 > life_t) break;
+        if (now - last > idle_t) break;
         for (uint32_t k = 0; k < nap; k++) __builtin_amdgcn_s_sleep(32);
         nap = min(nap * 2u, 8u);
       }

@@ -1174,7 +1174,7 @@ int sq_submit(StreamCall *c) {
 // mailbox from its first mapped, header-less call until it ends; each of its
 // calls is posted there and returns when that workgroup finished it -- no
 // launch, no batch, no wait for other handles' calls.  The launch leaves by
-// itself after PK_IDLE_US without posts (or PK_LIFE_MS, between calls), and
+// itself after PK_IDLE_US without posts (or after its current call once PK_LIFE_MS old), and
 // the next post relaunches it: a waiter that finds the launch ended with its
 // call undone relaunches (only ever one launch; the call stays posted).
 // Calls that need the wrapper header, DMA staging or deflate64, and handles
@@ -1270,7 +1270,7 @@ int pk_launch_locked() {
   const uint64_t idle_t = (uint64_t)pk_idle_us() * 100u;  // s_memrealtime ticks (100 MHz)
   static const uint64_t life_t = [] {
     const char *e = std::getenv("ZS_PK_LIFE_MS");
-    return (uint64_t)(e ? std::atoll(e) : 500) * 100000u;
+    return (uint64_t)(e ? std::atoll(e) : 4000) * 100000u;
   }();
   zs_launch_stream_pk(g_pk.d_mb, (uint32_t)g_pk.nw, g_pk.d_ctl, idle_t, life_t, g_pk.st);
   HIP_OK(hipGetLastError());
