@@ -325,3 +325,36 @@ def test_persistent_worker_relaunch_and_reset(zs):
             assert L.inflate_end(h) == 0
     finally:
         zs.stream_persist(prev)
+
+
+def test_more_handles_than_worker_mailboxes(zs):
+    """80 handles at once on 80 threads -- more than the persistent worker's 64
+    mailboxes (ZS_PK_WGS), plus deflate64 handles, which it never takes: the
+    handles that get a mailbox run on the worker, the rest on batch launches,
+    concurrently.  Every trace and output equals the oracle's."""
+    from concurrent.futures import ThreadPoolExecutor
+    rng = random.Random(21)
+    cases = []
+    for k in range(72):
+        data = corpus.stream(40 + k % 8, 120000 + 997 * k)
+        wb = (-15, 15, 31)[k % 3]
+        cases.append((_comp(data, wb, 1 + k % 9), wb))
+    for name in ("100k_lines", "zeros_100k", "payload_64k", "rand_block_gap"):
+        cases += [(fixture(name), -16)] * 2
+    rng.shuffle(cases)
+    prev = zs.stream_persist(True)
+    try:
+        before = zs.stream_stats()
+        with ThreadPoolExecutor(len(cases)) as ex:
+            got = list(ex.map(lambda c: zs.js_schedule(c[0], FMT[c[1]], 32768), cases))
+        after = zs.stream_stats()
+    finally:
+        zs.stream_persist(prev)
+    bad = []
+    for i, ((data, wb), (tr, out)) in enumerate(zip(cases, got)):
+        etr, eout = O.js_schedule(data, 32768, wb)
+        if tr != etr or out != eout:
+            bad.append((i, wb, tr[:200], etr[:200]))
+    assert not bad, bad[:3]
+    assert after["pk_calls"] > before["pk_calls"]  # the worker took calls
+    assert after["calls"] > before["calls"]        # and so did batch launches (headers, deflate64, extra handles)
