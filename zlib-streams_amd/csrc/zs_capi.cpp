@@ -1270,7 +1270,7 @@ int pk_launch_locked() {
   const uint64_t idle_t = (uint64_t)pk_idle_us() * 100u;  // s_memrealtime ticks (100 MHz)
   static const uint64_t life_t = [] {
     const char *e = std::getenv("ZS_PK_LIFE_MS");
-    return (uint64_t)(e ? std::atoll(e) : 4000) * 100000u;
+    return (uint64_t)(e ? std::atoll(e) : 250) * 100000u;
   }();
   zs_launch_stream_pk(g_pk.d_mb, (uint32_t)g_pk.nw, g_pk.d_ctl, idle_t, life_t, g_pk.st);
   HIP_OK(hipGetLastError());
@@ -1322,12 +1322,14 @@ int pk_submit(StreamCall *c, int w) {
   (void)slack;
   const int64_t expect = (int64_t)c->s->pk_last_ns;
   if (expect > 80000) std::this_thread::sleep_for(std::chrono::nanoseconds(expect * 5 / 8));  // calls vary +-30%
-  int64_t next_look = t0 + 2000000;  // the launch may have left (PK_LIFE) before it saw the call
+  // the launch may have left (its life ended) before it saw the call: look
+  // after three expected calls, then every 500 us
+  int64_t next_look = t0 + std::max<int64_t>(3 * expect, 500000);
   for (;;) {
     if (__atomic_load_n(&m->seq_out, __ATOMIC_ACQUIRE) == seq) break;
     const int64_t now = pk_now_ns();
     if (now > next_look) {
-      next_look = now + 1000000;
+      next_look = now + 500000;
       std::lock_guard<std::mutex> lk(g_pk.mu);
       if (!pk_running_locked()) {
         if (__atomic_load_n(&m->seq_out, __ATOMIC_ACQUIRE) == seq) break;
