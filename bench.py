@@ -777,15 +777,18 @@ def stream_leg(args, zstreams, np, cpu):
         "handles": {"value": round(mibm, 1), "unit": "MiB/s (aggregate)", "handles": nh,
                     "stream": f"{nh} x {args.stream_handle_mib} MiB line text (ids 32..), one native host thread per "
                               "handle (tools/js_driver.c)",
-                    "launches": launches, "calls_per_launch": round(calls_m / max(1, launches), 1),
-                    "launch_us_avg": round(dl["launch_ns"] / 1e3 / max(1, launches), 1),
-                    "kernel_us_avg": round(dl["kernel_ns"] / 1e3 / max(1, launches), 1),
-                    "gather_us_avg": round(dl["gather_ns"] / 1e3 / max(1, launches), 1),
-                    "slots_busy": round(dl["launch_ns"] / 1e9 / tm, 2),
+                    # calls on the persistent stream worker (a workgroup per handle):
+                    # workgroup time per call, host wait per call (post to seen done)
                     "persistent_calls": dl["pk_calls"], "persistent_launches": dl["pk_launches"],
                     "persistent_call_us_avg": round(dl["pk_busy_ns"] / 1e3 / max(1, dl["pk_calls"]), 1),
                     "persistent_wait_us_avg": round(dl["pk_wait_ns"] / 1e3 / max(1, dl["pk_calls"]), 1),
-                    "persistent_idle_us_avg": round(dl["pk_idle_ns"] / 1e3 / max(1, dl["pk_calls"]), 1),
+                    # calls on batch launches (ZS_STREAM_PK=0, or handles beyond the worker's mailboxes)
+                    "batch": None if launches == 0 else {
+                        "calls": calls_m, "launches": launches, "calls_per_launch": round(calls_m / launches, 1),
+                        "launch_us_avg": round(dl["launch_ns"] / 1e3 / launches, 1),
+                        "kernel_us_avg": round(dl["kernel_ns"] / 1e3 / launches, 1),
+                        "gather_us_avg": round(dl["gather_ns"] / 1e3 / launches, 1),
+                        "slots_busy": round(dl["launch_ns"] / 1e9 / tm, 2)},
                     "verified": bool(okm)},
         "wasm_reference_mibs": 493,
         "compress_one_handle": {"value": round(len(dbytes) / tdz / 2**20, 1), "unit": "MiB/s (input)",
