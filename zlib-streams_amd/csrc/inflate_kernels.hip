@@ -235,6 +235,10 @@ struct StreamLDS {
   __attribute__((aligned(16))) uint16_t sorted[320];
   uint32_t scr[32];
   WideLDS wide;
+  // the symbol decoded at each window offset (standard deflate: 1 | literal << 1,
+  // or length << 1 | distance << 10), so the chain's k-th symbol moves to thread k
+  // with one read (deflate64's lengths and distances do not fit: marks there)
+  __attribute__((aligned(16))) uint32_t osym[D64 ? 4u : WW_BITS];
 };
 
 __device__ __forceinline__ uint32_t ww_scan_sum(uint32_t x) {  // inclusive, wave64
@@ -371,6 +375,14 @@ __device__ void ww_run(StreamLDS<D64> &Ls) {
     }
     *reinterpret_cast<uint2 *>(&w.nb[q0]) = make_uint2(nbw[0], nbw[1]);
     *reinterpret_cast<uint4 *>(&w.ja[q0]) = make_uint4(jw[0], jw[1], jw[2], jw[3]);
+    if constexpr (!D64) {
+      uint32_t o[WW_OFFS];
+#pragma unroll
+      for (uint32_t i = 0; i < WW_OFFS; i++)
+        o[i] = (lv[i] & 0x80000000u) ? (1u | ((lv[i] & 0xffu) << 1)) : ((lv[i] << 1) | (dv[i] << 10));
+      *reinterpret_cast<uint4 *>(&Ls.osym[q0]) = make_uint4(o[0], o[1], o[2], o[3]);
+      *reinterpret_cast<uint4 *>(&Ls.osym[q0 + 4]) = make_uint4(o[4], o[5], o[6], o[7]);
+    }
   }
   if (t < WW_JN - WW_BITS) {
     w.nb[WW_BITS + t] = 0;
@@ -430,29 +442,49 @@ __device__ void ww_run(StreamLDS<D64> &Ls) {
   // 3. the chain's symbols: inside the window and plain
   const uint32_t snb = s < WW_BITS ? w.nb[s] : 0u;
   ww_first(&w.cnt_min, !(s < W && snb != 0));
-  uint16_t *mark = w.jc;  // J5 is done with (J3 in jb may still be read by other threads' walks)
+  uint32_t cnt, L = 0, D = 0;
+  if constexpr (!D64) {  // thread t reads its symbol (offset s) directly
+    if (s < W && snb != 0) {
+      const uint32_t o = Ls.osym[s];
+      L = (o & 1u) ? (0x80000000u | (o >> 1)) : ((o >> 1) & 511u);
+      D = (o & 1u) ? 0u : (o >> 10);
+    }
+    __syncthreads();
+    cnt = w.cnt_min;
+    if (t < cnt) {
+      w.symL[t] = L;
+      w.symD[t] = D;
+    } else {
+      L = D = 0;
+    }
+  } else {  // symbol k's data moves to thread k through an on-chain mark
+    uint16_t *mark = w.jc;  // J5 is done with (J3 in jb may still be read by other threads' walks)
 #pragma unroll
-  for (uint32_t i = 0; i < WW_OFFS; i++) mark[t + i * WW_T] = 0;
-  __syncthreads();
-  const uint32_t cnt = w.cnt_min;
-  if (t < cnt) mark[s] = (uint16_t)(t + 1u);
-  __syncthreads();
-  {
-    const uint4 mk = *reinterpret_cast<const uint4 *>(&mark[WW_OFFS * t]);
-    const uint32_t mw[4] = {mk.x, mk.y, mk.z, mk.w};
+    for (uint32_t i = 0; i < WW_OFFS; i++) mark[t + i * WW_T] = 0;
+    __syncthreads();
+    cnt = w.cnt_min;
+    if (t < cnt) mark[s] = (uint16_t)(t + 1u);
+    __syncthreads();
+    {
+      const uint4 mk = *reinterpret_cast<const uint4 *>(&mark[WW_OFFS * t]);
+      const uint32_t mw[4] = {mk.x, mk.y, mk.z, mk.w};
 #pragma unroll
-    for (uint32_t i = 0; i < WW_OFFS; i++) {
-      const uint32_t m = (mw[i >> 1] >> (16u * (i & 1u))) & 0xffffu;
-      if (m) {
-        w.symL[m - 1u] = lv[i];
-        w.symD[m - 1u] = dv[i];
+      for (uint32_t i = 0; i < WW_OFFS; i++) {
+        const uint32_t m = (mw[i >> 1] >> (16u * (i & 1u))) & 0xffffu;
+        if (m) {
+          w.symL[m - 1u] = lv[i];
+          w.symD[m - 1u] = dv[i];
+        }
       }
     }
+    __syncthreads();
+    if (t < cnt) {
+      L = w.symL[t];
+      D = w.symD[t];
+    }
   }
-  __syncthreads();
   // 4. admissible prefix: fits the output (and WW_TCAP), distance within history
   const bool act = t < cnt;
-  const uint32_t L = act ? w.symL[t] : 0u, D = act ? w.symD[t] : 0u;
   const bool lit = (L & 0x80000000u) != 0;
   const uint32_t olen = act ? (lit ? 1u : L) : 0u;
   uint32_t ost;
