@@ -1,13 +1,11 @@
-# round 4: stream windows (J3 walks, 8 consecutive offsets per thread) + tree build without scratch arrays
+# round 4: stream leg (default worker life, then a long life) -- relaunch feedback check
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/r4y
 mkdir -p $O
 cd $R
-bash tools/gpu_r4x.sh || exit $?
-timeout -k 10 900 python -u -m pytest tests/test_gpu_deflate.py -x -q --timeout 300 --timeout-method thread > $O/deflate_tests.log 2>&1; rc=$?
-echo "deflate tests rc=$rc"; tail -2 $O/deflate_tests.log
-[ $rc -eq 0 ] || exit $rc
-for K in random lines; do
-  LEVELS=6 KINDS=$K timeout -k 10 200 python3 -u tools/dstream_probe.py 4 2>&1 | grep GPU || exit 1
-done
-timeout -k 10 300 python3 tools/zd_probe.py 2>&1 | grep "zlib-bytes"
+show() { python3 -c "
+import json;d=json.load(open('$1'))['stream'];print(d['one_handle']);print(d['handles'])"; }
+timeout -k 10 300 python3 -u bench.py --only-stream --no-ref-perf > $O/stream.json 2> $O/stream.err || exit $?
+show $O/stream.json
+ZS_PK_LIFE_MS=5000 timeout -k 10 300 python3 -u bench.py --only-stream --no-ref-perf > $O/stream_life.json 2> $O/stream_life.err || exit $?
+show $O/stream_life.json

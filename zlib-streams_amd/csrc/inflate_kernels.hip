@@ -207,7 +207,10 @@ struct WideLDS {
   uint32_t op, P, W, limit_bits, pos, cap, whave, lmask, dmask;
   uint32_t lt_off, dt_off;     // the code tables: byte offsets in the kernel's StreamLDS
   // results and reductions
-  uint32_t n, T, endrel, cnt_min, n_min, carry, open;
+  uint32_t n, cnt_min, carry, open;
+  // admitted prefix: first inadmissible thread n << 32 | its chain offset << 16 |
+  // its output start (= the bytes admitted), by one 64-bit LDS min
+  __attribute__((aligned(8))) unsigned long long nkey;
   uint32_t save, save_pos;     // end of the call: the history ring goes to the handle's state
   uint32_t tab_in, tab_out;    // cached dynamic tables (ZsStreamDev::tab_bits) loaded / to save
   uint32_t wtot[WW_T / 64];
@@ -270,7 +273,7 @@ __device__ __forceinline__ uint32_t ww_scan(WideLDS &w, uint32_t v, uint32_t *ex
   __syncthreads();
   uint32_t pre = 0;
   for (uint32_t k = 0; k < wv; k++) pre = MAX ? max(pre, w.wtot[k]) : pre + w.wtot[k];
-  __syncthreads();  // wtot is reused by the next scan
+  // no trailing barrier: every caller passes one before its next scan writes wtot
   const uint32_t own = lane ? up : 0u;
   *excl = MAX ? max(pre, own) : pre + own;
   return MAX ? max(pre, inc) : pre + inc;
@@ -390,7 +393,7 @@ __device__ void ww_run(StreamLDS<D64> &Ls) {
   }
   if (t == 0) {
     w.cnt_min = WW_T;
-    w.n_min = WW_T;
+    w.nkey = ~0ull;
   }
   // 2. the chain from the window start: J5 = 32 symbols per jump (five
   //    compositions of J0), a serial walk of J5 for every 32nd symbol, then
@@ -490,15 +493,29 @@ __device__ void ww_run(StreamLDS<D64> &Ls) {
   uint32_t ost;
   const uint32_t incl = ww_scan<false>(w, olen, &ost);
   const uint32_t room = min(w.cap - w.pos, WW_TCAP);
-  ww_first(&w.n_min, !(act && incl <= room && (lit || D <= w.pos + ost + w.whave)));
-  __syncthreads();
-  const uint32_t n = w.n_min;
-  if (n > 0 && t == n - 1u) w.T = incl;
-  if (n == 0 && t == 0) w.T = 0;
-  if (t == (n < WW_T ? n : WW_T - 1u)) w.endrel = n < WW_T ? s : s + snb;
+  {
+    // each wave posts its first inadmissible thread with that thread's chain
+    // offset and output start (the admitted bytes when it is the first of all);
+    // the last wave posts "none" (thread WW_T, the end of its last symbol)
+    const uint64_t m = __ballot(!(act && incl <= room && (lit || D <= w.pos + ost + w.whave)));
+    const uint32_t lane = t & 63u;
+    unsigned long long key = ~0ull;
+    if (m) {
+      const int f = __builtin_ctzll(m);
+      const uint32_t sf = (uint32_t)__builtin_amdgcn_readlane((int)s, f);
+      const uint32_t of = (uint32_t)__builtin_amdgcn_readlane((int)min(ost, 0xffffu), f);
+      key = ((unsigned long long)((t & ~63u) + (uint32_t)f) << 32) | (sf << 16) | of;
+    } else if (t >= WW_T - 64u) {
+      const uint32_t el = (uint32_t)__builtin_amdgcn_readlane((int)(s + snb), 63);
+      const uint32_t il = (uint32_t)__builtin_amdgcn_readlane((int)min(incl, 0xffffu), 63);
+      key = ((unsigned long long)WW_T << 32) | (el << 16) | il;
+    }
+    if (lane == 0 && key != ~0ull) atomicMin(&w.nkey, key);
+  }
   if (t == 0) w.carry = 0;
   __syncthreads();
-  const uint32_t T = w.T;
+  const unsigned long long nk = w.nkey;
+  const uint32_t n = (uint32_t)(nk >> 32), T = (uint32_t)nk & 0xffffu;
   [[maybe_unused]] const uint64_t kt2 = KP_NOW();
   KPW0_ADD(KP_W_CYC_DECODE, kt1 - kt0);
   KPW0_ADD(KP_W_CYC_CHAIN, kt2 - kt1);
@@ -1256,7 +1273,8 @@ struct Inflater {
     KPW_ADD(KP_W_CYC_PRE, kw0 - kq0);
     __syncthreads();  // the other waves wait here for a window
     ww_run<D64>(*wide);
-    const uint32_t n = w.n_min, T = w.T, endrel = w.endrel;
+    const unsigned long long nk = w.nkey;  // posted before the window's last barrier
+    const uint32_t n = (uint32_t)(nk >> 32), T = (uint32_t)nk & 0xffffu, endrel = (uint32_t)(nk >> 16) & 0xffffu;
     [[maybe_unused]] const uint64_t kw1 = KP_NOW();
     KPW_ADD(KP_W_CYC_WINDOW, kw1 - kw0);
     KPW_ADD(KP_W_WINDOWS, 1);

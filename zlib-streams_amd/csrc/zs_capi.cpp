@@ -890,7 +890,7 @@ struct StreamState {
   size_t cap_hin = 0, cap_hout = 0;
   int fresh = 0;  // the device state is set up by the next call (ZsStreamIo::fresh)
   int pk_w = -1;  // the persistent worker's mailbox this handle holds (-1: none)
-  uint64_t pk_last_ns = 0;  // its last call's host wait (the next wait sleeps most of it)
+  uint64_t pk_last_ns = 0;  // its last call's time on the worker (the next wait sleeps most of it)
 };
 
 constexpr size_t STAGE_MAX = 4u << 20;
@@ -1339,12 +1339,16 @@ int pk_submit(StreamCall *c, int w) {
     std::this_thread::sleep_for(std::chrono::microseconds(now - t0 < 3 * std::max<int64_t>(expect, 100000) ? 6 : 25));
   }
   const uint64_t waited = (uint64_t)(pk_now_ns() - t0);
-  c->s->pk_last_ns = waited;
+  const uint64_t busy = (uint64_t)__atomic_load_n(&m->busy, __ATOMIC_RELAXED) * 10u;
+  // the next sleep follows the call's own time on the worker, not the wait: a
+  // wait stretched by a relaunch would make every handle sleep long at once,
+  // the worker would see no posts, leave idle, and the stretch would feed itself
+  c->s->pk_last_ns = busy;
   ZsStreamRes r;
   std::memcpy(&r, (const void *)&m->res, sizeof(r));
   c->res = r;
   g_pk.calls.fetch_add(1);
-  g_pk.busy_ns.fetch_add((uint64_t)__atomic_load_n(&m->busy, __ATOMIC_RELAXED) * 10u);
+  g_pk.busy_ns.fetch_add(busy);
   g_pk.wait_ns.fetch_add(waited);
   g_pk.idle_ns.fetch_add((uint64_t)__atomic_load_n(&m->idle, __ATOMIC_RELAXED) * 10u);
   return 0;
