@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 4 final: GPU suite -> driver-shaped bench -> rocprofv3 kernel stats -> PMC traffic,
+# round 4 final: GPU suite -> PMC traffic -> driver-shaped bench (reading that traffic) -> rocprofv3 kernel stats,
 # all on the library in the tree (each GPU step under its own limit; stops at the first failure)
 TAG=${1:-r4final}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -9,8 +9,10 @@ cd $R
 timeout -k 10 600 python -u -m pytest tests -m gpu -q -rf -x --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1; rc=$?
 echo "pytest rc=$rc"; tail -2 $O/pytest_gpu.log
 [ $rc -eq 0 ] || exit $rc
+PMC_TAG=$TAG bash tools/pmc_traffic.sh && [ -s $R/gpurun_out/pmc/pmc_traffic.json ] || exit 1
+cd $R
 t0=$SECONDS
-timeout -k 10 500 python3 bench.py > $O/bench.json 2> $O/bench.err; rc=$?
+timeout -k 10 500 python3 bench.py --traffic-json $R/gpurun_out/pmc/pmc_traffic.json > $O/bench.json 2> $O/bench.err; rc=$?
 echo "bench rc=$rc wall_s=$((SECONDS - t0))"
 [ $rc -eq 0 ] || exit $rc
 python3 -c "
@@ -20,5 +22,4 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pro
 echo "rocprof rc=$rc"
 find $O/prof -name "*kernel_trace.csv" -delete
 [ $rc -eq 0 ] || exit $rc
-cd $R
-PMC_TAG=$TAG bash tools/pmc_traffic.sh
+
