@@ -207,7 +207,8 @@ struct WideLDS {
   uint32_t op, P, W, limit_bits, pos, cap, whave, lmask, dmask;
   uint32_t lt_off, dt_off;     // the code tables: byte offsets in the kernel's StreamLDS
   // results and reductions
-  uint32_t n, cnt_min, carry, open;
+  uint32_t n, cnt_min, carry;
+  uint32_t open[2];            // expansion rounds alternate: one is set while the other is cleared
   // admitted prefix: first inadmissible thread n << 32 | its chain offset << 16 |
   // its output start (= the bytes admitted), by one 64-bit LDS min
   __attribute__((aligned(8))) unsigned long long nkey;
@@ -491,6 +492,9 @@ __device__ void ww_run(StreamLDS<D64> &Ls) {
   const bool lit = (L & 0x80000000u) != 0;
   const uint32_t olen = act ? (lit ? 1u : L) : 0u;
   uint32_t ost;
+  // the first expansion step's marks (they alias J0, whose walks ended before the
+  // last barrier); the scan's barrier orders these stores before the marks
+  reinterpret_cast<uint4 *>(w.ja)[t] = make_uint4(0u, 0u, 0u, 0u);
   const uint32_t incl = ww_scan<false>(w, olen, &ost);
   const uint32_t room = min(w.cap - w.pos, WW_TCAP);
   {
@@ -524,8 +528,17 @@ __device__ void ww_run(StreamLDS<D64> &Ls) {
   uint16_t *marks = w.ja;                                        // WW_STEP u16
   uint32_t *ent = reinterpret_cast<uint32_t *>(w.ja + WW_STEP);  // WW_STEP u32 (into jb / jc)
   for (uint32_t b0 = 0; b0 < T; b0 += WW_STEP) {
-    reinterpret_cast<uint4 *>(marks)[t] = make_uint4(0u, 0u, 0u, 0u);
-    __syncthreads();
+    if (b0) {
+      reinterpret_cast<uint4 *>(marks)[t] = make_uint4(0u, 0u, 0u, 0u);
+      __syncthreads();
+    }
+    // round flags: each round ORs into open[r & 1] before its one barrier, reads
+    // it after, and clears the other (read last round, before this barrier;
+    // next set after the barrier the next round passes first)
+    if (t == 0) {
+      w.open[0] = 0;
+      w.open[1] = 0;
+    }
     if (t < n && ost >= b0 && ost < b0 + WW_STEP) marks[ost - b0] = (uint16_t)(t + 1u);
     __syncthreads();
     const uint4 mk = reinterpret_cast<const uint4 *>(marks)[t];
@@ -556,11 +569,12 @@ __device__ void ww_run(StreamLDS<D64> &Ls) {
     }
     reinterpret_cast<uint4 *>(ent)[2u * t] = make_uint4(e[0], e[1], e[2], e[3]);
     reinterpret_cast<uint4 *>(ent)[2u * t + 1u] = make_uint4(e[4], e[5], e[6], e[7]);
-    if (t == 0) w.open = 0;
+    if (__ballot(open) && (t & 63u) == 0) atomicOr(&w.open[0], 1u);
     __syncthreads();
-    if (__ballot(open) && (t & 63u) == 0) atomicOr(&w.open, 1u);
-    __syncthreads();
-    while (w.open) {
+    uint32_t rp = 0;
+    while (w.open[rp]) {
+      if (t == 0) w.open[rp ^ 1u] = 0;
+      rp ^= 1u;
       KPW0_ADD(KP_W_JUMPS, 1);
       uint32_t g[WW_EB];
 #pragma unroll
@@ -574,9 +588,7 @@ __device__ void ww_run(StreamLDS<D64> &Ls) {
       __syncthreads();
       reinterpret_cast<uint4 *>(ent)[2u * t] = make_uint4(e[0], e[1], e[2], e[3]);
       reinterpret_cast<uint4 *>(ent)[2u * t + 1u] = make_uint4(e[4], e[5], e[6], e[7]);
-      if (t == 0) w.open = 0;
-      __syncthreads();
-      if (__ballot(open) && (t & 63u) == 0) atomicOr(&w.open, 1u);
+      if (__ballot(open) && (t & 63u) == 0) atomicOr(&w.open[rp], 1u);
       __syncthreads();
     }
 #pragma unroll
