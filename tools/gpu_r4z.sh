@@ -1,11 +1,8 @@
-# round 4: stream leg twice with the driver's per-thread split
+# round 4: stream window change -- inflate + stream tests, stream leg, in-kernel phase counters
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-O=$R/gpurun_out/r4z
+O=$R/gpurun_out/r4z5
 mkdir -p $O
 cd $R
-for k in 1 2; do
-ZS_JS_DRIVE_PROF=1 timeout -k 10 300 python3 -u bench.py --only-stream --no-ref-perf > $O/stream$k.json 2> $O/stream$k.err || exit $?
-python3 -c "
-import json;d=json.load(open('$O/stream$k.json'))['stream'];h=d['handles'];print('one',d['one_handle']['value'],{k:h[k] for k in h if k.startswith('persistent') or k=='value'})"
-grep js_drive $O/stream$k.err
-done
+bash tools/gpu_r4x.sh || exit $?
+ZS_LIB=$R/zlib-streams_amd/libzstreams_mi355x_prof.so timeout -k 10 200 python3 tools/stream_probe.py 16 > $O/probe_prof.log 2>&1; rc=$?
+tail -3 $O/probe_prof.log; exit $rc

@@ -360,6 +360,7 @@ __device__ void ww_run(StreamLDS<D64> &Ls) {
   // 1. a complete symbol at every offset of the window: thread t the 8
   //    consecutive offsets 8t .. 8t + 7, whose bits one 128-bit read covers
   uint32_t lv[WW_OFFS], dv[WW_OFFS];
+  uint32_t cur[WW_OFFS];  // the thread's own J0 .. J4 entries, offsets 8t .. 8t + 7
   static_assert(WW_OFFS == 8, "8 consecutive offsets per thread");
   {
     const uint32_t q0 = WW_OFFS * t, b0 = P + q0, wq = b0 >> 5, sh = b0 & 31u;
@@ -376,6 +377,7 @@ __device__ void ww_run(StreamLDS<D64> &Ls) {
       if (q < W) nb = ww_decode_bits<D64>(w, lt, dt, hh, P + q, lv[i], dv[i]);
       nbw[i >> 2] |= nb << (8u * (i & 3u));
       jw[i >> 1] |= (q + nb) << (16u * (i & 1u));
+      cur[i] = q + nb;
     }
     *reinterpret_cast<uint2 *>(&w.nb[q0]) = make_uint2(nbw[0], nbw[1]);
     *reinterpret_cast<uint4 *>(&w.ja[q0]) = make_uint4(jw[0], jw[1], jw[2], jw[3]);
@@ -405,29 +407,28 @@ __device__ void ww_run(StreamLDS<D64> &Ls) {
     // place over J4 (all reads, a barrier, then the writes), so J3 survives:
     // each thread then reaches its symbol from its 32-group's start in <= 3
     // J3 hops and <= 7 J0 hops instead of <= 31 J0 hops
+    // the thread's own entries stay in registers (cur), so a round is 8 gathers
+    // and one 16-byte store
     const uint16_t *src = w.ja;
     uint16_t *dst = w.jb;
+    const uint32_t q0 = WW_OFFS * t;
 #pragma unroll 1
     for (uint32_t k = 0; k < 4; k++) {
       __syncthreads();
 #pragma unroll
-      for (uint32_t i = 0; i < WW_OFFS; i++) {
-        const uint32_t q = t + i * WW_T;
-        dst[q] = src[src[q]];
-      }
+      for (uint32_t i = 0; i < WW_OFFS; i++) cur[i] = src[cur[i]];
+      *reinterpret_cast<uint4 *>(&dst[q0]) =
+          make_uint4(cur[0] | cur[1] << 16, cur[2] | cur[3] << 16, cur[4] | cur[5] << 16, cur[6] | cur[7] << 16);
       if (t < WW_JN - WW_BITS) dst[WW_BITS + t] = (uint16_t)(WW_BITS + t);
       src = dst;
       dst = dst == w.jb ? w.jc : w.jb;
     }
     __syncthreads();
-    {
-      uint16_t j5[WW_OFFS];
 #pragma unroll
-      for (uint32_t i = 0; i < WW_OFFS; i++) j5[i] = w.jc[w.jc[t + i * WW_T]];
-      __syncthreads();
-#pragma unroll
-      for (uint32_t i = 0; i < WW_OFFS; i++) w.jc[t + i * WW_T] = j5[i];
-    }
+    for (uint32_t i = 0; i < WW_OFFS; i++) cur[i] = w.jc[cur[i]];
+    __syncthreads();
+    *reinterpret_cast<uint4 *>(&w.jc[q0]) =
+        make_uint4(cur[0] | cur[1] << 16, cur[2] | cur[3] << 16, cur[4] | cur[5] << 16, cur[6] | cur[7] << 16);
     __syncthreads();
     KPW0_ADD(KP_W_CYC_COMPOSE, KP_NOW() - kt1);
     if (t == 0) {
