@@ -37,6 +37,7 @@ typedef struct {
   uint64_t produced, calls;
   int code;
   double t_total, t_proc, t_init, t_end;  /* env ZS_JS_DRIVE_PROF: per-thread split (stderr) */
+  double t_start;                         /* absolute start (ZS_JS_DRIVE_PROF=2: per-thread lines) */
 } job_t;
 
 static double now_s(void) {
@@ -93,6 +94,7 @@ static void *run_job(void *arg) {
   a->f_end(h);
   const double te1 = now_s();
   j->t_total = te1 - ts;
+  j->t_start = ts;
   j->t_proc = tp;
   j->t_init = ti - ts;
   j->t_end = te1 - te0;
@@ -152,6 +154,13 @@ double zs_js_drive(const char *lib_path, const uint8_t *const *comp, const size_
     fprintf(stderr, "js_drive %d threads: per thread avg total %.2f ms (max %.2f), in process() %.2f ms, init %.3f ms, end %.3f ms; %.1f us per call in process()\n",
             started, 1e3 * tt / started, 1e3 * tmax, 1e3 * tp / started, 1e3 * ti / started, 1e3 * te / started,
             1e6 * tp / (double)(calls ? calls : 1));
+    if (atoi(getenv("ZS_JS_DRIVE_PROF")) >= 2) {
+      const double t0s = (double)t0.tv_sec + 1e-9 * (double)t0.tv_nsec;
+      for (int k = 0; k < started; k++)
+        fprintf(stderr, "  thread %2d: start +%.2f ms, total %.2f ms, %llu calls, %.1f us per call\n", k,
+                1e3 * (js[k].t_start - t0s), 1e3 * js[k].t_total, (unsigned long long)js[k].calls,
+                1e6 * js[k].t_proc / (double)(js[k].calls ? js[k].calls : 1));
+    }
   }
   free(js);
   free(th);
