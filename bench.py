@@ -86,7 +86,7 @@ def parse_args(argv=None):
     ap.add_argument("--stream-leg-mib", type=int, default=16, help="line-text stream of the one-handle run")
     ap.add_argument("--stream-handles", type=int, default=64, help="concurrent handles of the aggregate run")
     ap.add_argument("--stream-handle-mib", type=int, default=4, help="stream size per concurrent handle")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r04", "pmc_traffic.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r05", "pmc_traffic.json"),
                     help="PMC-derived HBM bytes per pipeline launch (null in the line when absent)")
     ap.add_argument("--no-c5-leg", action="store_true",
                     help="skip the configs[4] leg (the fixed 4096 x 4 MiB batch LPT-split across the ranks)")
@@ -210,29 +210,40 @@ def cpu_baseline(comps, raws, wbits_list, sample, cpu, min_seconds):
     while t1 < min_seconds or passes == 0:
         t, b, k = run1(sample, 0)
         t1, b1, ok, passes = t1 + t, b1 + b, ok and k, passes + 1
-    threads = cpu["usable_cores"]
-    ids = (sample * (2 * threads // len(sample) + 1))[:max(len(sample), 2 * threads)]
-    cp, cl, n = arrs(ids)
-    pt_outs = [np.empty(cap, dtype=np.uint8) for _ in range(threads)]
-    op = (ctypes.c_void_p * threads)(*[o.ctypes.data for o in pt_outs])
-    tot, bad = ctypes.c_uint64(), ctypes.c_int()
-    tn = L.zs_cpu_inflate_pt(cp, cl, op, cap, n, threads, wbits, ctypes.byref(tot), ctypes.byref(bad))
-    bn = tot.value
-    last = {k: ids[k + ((n - 1 - k) // threads) * threads] for k in range(min(threads, n))}
-    ok = ok and not bad.value and all(np.array_equal(pt_outs[k][:len(raws[i])], raws[i]) for k, i in last.items())
-    del pt_outs
+    def all_cores(threads):
+        ids = (sample * (2 * threads // len(sample) + 1))[:max(len(sample), 2 * threads)]
+        cp, cl, n = arrs(ids)
+        pt_outs = [np.empty(cap, dtype=np.uint8) for _ in range(threads)]
+        op = (ctypes.c_void_p * threads)(*[o.ctypes.data for o in pt_outs])
+        tot, bad = ctypes.c_uint64(), ctypes.c_int()
+        tn = L.zs_cpu_inflate_pt(cp, cl, op, cap, n, threads, wbits, ctypes.byref(tot), ctypes.byref(bad))
+        last = {k: ids[k + ((n - 1 - k) // threads) * threads] for k in range(min(threads, n))}
+        good = not bad.value and all(np.array_equal(pt_outs[k][:len(raws[i])], raws[i]) for k, i in last.items())
+        return {"threads": threads, "value": round(tot.value / tn / 2**20, 1), "decodes": n,
+                "mib_out": round(tot.value / 2**20), "seconds": round(tn, 2)}, good
+
+    # The host's best all-core figure: one thread per usable core (physical
+    # cores capped by the cgroup quota) AND one per physical core (the
+    # oversubscribed layout measured faster on this host class in round 3);
+    # value_all_cores is the larger.
+    layouts = []
+    for th in sorted({cpu["usable_cores"], cpu["physical_cores"]}):
+        lay, good = all_cores(th)
+        ok = ok and good
+        layouts.append(lay)
+    best = max(layouts, key=lambda x: x["value"])
+    threads, vn = best["threads"], best["value"]
     tp, bp, kp = run1(sample[:8], 1)
     v1 = b1 / t1 / 2**20
-    vn = bn / tn / 2**20
     return {"value": round(v1, 1), "unit": "MiB/s", "cores": 1, "kind": "reference",
             "impl": f"host zlib {L.zs_cpu_zlib_version().decode()} inflate: upstream of the reference's src/inflate.c "
                     f"for windowBits {wbits} (the reference build needs its absent zlib submodule headers)",
             "sample": f"{len(sample)} streams x {passes} pass(es), whole-buffer inflate(Z_FINISH), "
                       f"{b1 / 2**20:.0f} MiB out, {t1:.1f} s on 1 thread",
             "value_all_cores": round(vn, 1), "threads": threads,
-            "all_cores_sample": f"{n} stream decodes dealt round-robin to {threads} threads "
-                                f"(one per core this process may use: physical cores capped by the cgroup quota), "
-                                f"{bn / 2**20:.0f} MiB out, {tn:.1f} s",
+            "all_cores_layouts": layouts,
+            "all_cores_sample": f"the best of {len(layouts)} layouts (one thread per usable core, one per physical "
+                                f"core), stream decodes dealt round-robin, every thread >= 2 streams",
             "value_all_cores_linear": round(v1 * cpu["physical_cores"], 1),
             "linear_note": "1-core rate x every physical core of the host (an upper bound for the whole host)",
             "host": cpu,
@@ -265,24 +276,28 @@ def cpu_deflate_baseline(raws, sample, cpu, level, wbits, min_seconds):
         tot, bad = ctypes.c_uint64(), ctypes.c_int()
         t = L.zs_cpu_deflate(rp, rl, cp, cl, cap, n, 1, level, wbits, ctypes.byref(tot), ctypes.byref(bad))
         t1, b1, c1, ok, passes = t1 + t, b1 + tot.value, c1 + sum(cl), ok and not bad.value, passes + 1
-    threads = cpu["usable_cores"]
-    ids = (sample * (threads // len(sample) + 1))[:max(len(sample), threads)]
-    rp, rl, n = arrs(ids)
-    pt = [np.empty(cap, dtype=np.uint8) for _ in range(threads)]
-    cp = (ctypes.c_void_p * threads)(*[b.ctypes.data for b in pt])
-    cl = (ctypes.c_size_t * threads)()
-    tot, bad = ctypes.c_uint64(), ctypes.c_int()
-    tn = L.zs_cpu_deflate_pt(rp, rl, cp, cl, cap, n, threads, level, wbits, ctypes.byref(tot), ctypes.byref(bad))
-    del pt
+    layouts = []
+    for threads in sorted({cpu["usable_cores"], cpu["physical_cores"]}):
+        ids = (sample * (threads // len(sample) + 1))[:max(len(sample), threads)]
+        rp, rl, n = arrs(ids)
+        pt = [np.empty(cap, dtype=np.uint8) for _ in range(threads)]
+        cp = (ctypes.c_void_p * threads)(*[b.ctypes.data for b in pt])
+        cl = (ctypes.c_size_t * threads)()
+        tot, bad = ctypes.c_uint64(), ctypes.c_int()
+        tn = L.zs_cpu_deflate_pt(rp, rl, cp, cl, cap, n, threads, level, wbits, ctypes.byref(tot), ctypes.byref(bad))
+        del pt
+        ok = ok and not bad.value
+        layouts.append({"threads": threads, "value": round(tot.value / tn / 2**20, 1), "seconds": round(tn, 2)})
+    best = max(layouts, key=lambda x: x["value"])
     v1 = b1 / t1 / 2**20
     return {"value": round(v1, 2), "unit": "MiB/s (input)", "cores": 1, "kind": "reference",
             "impl": f"host zlib {L.zs_cpu_zlib_version().decode()} deflate level {level} memLevel 8 "
                     "(byte-identical to the reference's deflate)",
             "sample": f"{len(sample)} streams x {passes} pass(es), {b1 / 2**20:.0f} MiB in, {t1:.1f} s on 1 thread",
             "ratio": round(b1 / c1, 3) if c1 else None,
-            "value_all_cores": round(tot.value / tn / 2**20, 1), "threads": threads,
+            "value_all_cores": best["value"], "threads": best["threads"], "all_cores_layouts": layouts,
             "value_all_cores_linear": round(v1 * cpu["physical_cores"], 1),
-            "verified": bool(ok and not bad.value)}
+            "verified": bool(ok)}
 
 
 def generate(ids, nbytes, kind, nthreads):
@@ -432,19 +447,23 @@ def main():
     if args.traffic_json and os.path.exists(args.traffic_json) and world == 1 and args.workload == "c2":
         # HBM bytes per pipeline launch from separate rocprofv3 --pmc passes over this same workload
         # (tools/pmc_traffic.sh -> tools/pmc_traffic.py); PMC cannot be read from inside the timed run.
-        # Reported only when those passes ran the library this run loaded (SHA-256 match).
+        # Reported when those passes ran a library built from the same sources as the one this run loaded
+        # (zs_source_hash: csrc + header + hipcc version; hipcc output itself is not bit-reproducible).
         tj = json.load(open(args.traffic_json))
         import hashlib
         so_path = os.environ.get("ZS_LIB") or os.path.join(ROOT, "zlib-streams_amd", "libzstreams_mi355x.so")
         so_sha = hashlib.sha256(open(so_path, "rb").read()).hexdigest()
+        src_sha = zstreams.lib().zs_source_hash().decode()
+        same_src = tj.get("source_sha256") == src_sha
         same = tj.get("library_sha256") == so_sha
-        traffic = tj.get("hbm_bytes_per_launch") if same else None
+        traffic = tj.get("hbm_bytes_per_launch") if same_src else None
         traffic_src = {"file": os.path.relpath(args.traffic_json, ROOT), "checkpoint": tj.get("checkpoint"),
-                       "same_library_build": same, "library_sha256": so_sha,
+                       "same_source_build": same_src, "same_library_build": same, "source_sha256": src_sha,
+                       "library_sha256": so_sha,
                        "how": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, gfx950-corrected, every pipeline kernel"}
-        if not same:
-            traffic_src["reason_null"] = (f"the PMC passes in {traffic_src['file']} measured library "
-                                          f"{str(tj.get('library_sha256'))[:16]}, not this build")
+        if not same_src:
+            traffic_src["reason_null"] = (f"the PMC passes in {traffic_src['file']} measured a library built from "
+                                          f"sources {str(tj.get('source_sha256'))[:16]}, not this build's")
 
     c5_l = None
     if args.workload == "c2" and not args.no_c5_leg and args.sim_world <= 1:
@@ -760,8 +779,15 @@ def stream_leg(args, zstreams, np, cpu):
 
     reps = max(1, int(2e9 // one_bytes))
     c1v, c1ok = cpu_js([comp1] * reps, 1, one_bytes)
-    thr = max(1, min(cpu["usable_cores"], nh))
-    cmv, cmok = cpu_js(cs, thr, each)
+    # the host's best: one thread per usable core and one per handle (<= physical cores)
+    cm_layouts = []
+    cmok = True
+    for th in sorted({max(1, min(cpu["usable_cores"], nh)), max(1, min(cpu["physical_cores"], nh))}):
+        v, k = cpu_js(cs, th, each)
+        cm_layouts.append({"threads": th, "value": round(v, 1)})
+        cmok = cmok and k
+    best = max(cm_layouts, key=lambda x: x["value"])
+    thr, cmv = best["threads"], best["value"]
     mib1 = one_bytes / t1 / 2**20
     mibm = nh * each / tm / 2**20
     return {
@@ -806,6 +832,7 @@ def stream_leg(args, zstreams, np, cpu):
         "reference_perf_workload": None if args.no_ref_perf else guarded("stream.reference_perf_workload",
                                                                          ref_perf_leg, args, zstreams, np),
         "cpu_baseline": {"one_handle": round(c1v, 1), "handles_all_cores": round(cmv, 1), "threads": thr,
+                         "handles_all_cores_layouts": cm_layouts,
                          "unit": "MiB/s", "kind": "reference",
                          "impl": "host zlib 1.2.11 inflate, same call schedule (the shipped WASM runs this loop)",
                          "verified": bool(c1ok and cmok)},

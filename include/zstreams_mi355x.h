@@ -100,9 +100,14 @@ typedef struct zs_result {
 /* Parse mode of the block-parallel path (results are identical; speed differs).
    By default a batch with few decode units (<= 12288 search segments of 32 KiB
    compressed, env ZS_WAVE_SEGS) decodes each unit with a whole wave, a larger
-   one each unit with one lane.  These force one mode (testing, tuning). */
+   one with the split parse (below; env ZS_SPLIT=0: one lane per unit).  These
+   force one mode (testing, tuning). */
 #define ZS_F_PARSE_LANE 8u
 #define ZS_F_PARSE_WAVE 16u
+/* The split parse (default where the lane parse was): a boundary walk of each
+   unit's first block records exact symbol checkpoints, then a wave decodes the
+   block's sub-units in parallel.  This forces it for any batch size. */
+#define ZS_F_PARSE_SPLIT 4096u
 /* Link mode of the block-parallel path (results are identical): groups of at
    most 4 long streams use the parallel-prefix window link by default, larger
    groups the per-stream serial link (zs_link_kernel).  This forces the serial
@@ -225,6 +230,10 @@ int zs_stream_stats_ex(uint64_t out[10]);
  * workgroup of their own and return as soon as that call is done. */
 int zs_stream_persist(int on);
 const char *zs_version(void);
+/* SHA-256 of the sources the library was built from (csrc + this header +
+   the hipcc version; csrc/srchash.py), hex.  Ties measurements such as the
+   bench's PMC traffic to sources rather than to one binary. */
+const char *zs_source_hash(void);
 const char *zs_last_error(void);
 
 #ifdef __cplusplus

@@ -71,7 +71,7 @@ def test_deflate64_reaches_64k_back(zs):
     assert oi["ret"] == 1 and out == data
 
 
-@pytest.mark.parametrize("parse", ["lane", "wave"])
+@pytest.mark.parametrize("parse", ["lane", "wave", "split"])
 def test_deflate64_chunked_block_parallel(zs, parse):
     """Large deflate64 streams take the block-parallel path (64 KiB history
     windows, 32 distance codes, code-285 copies split into tokens) with no

@@ -193,10 +193,11 @@ def _big_cases(rng, n, lo=1 << 20, hi=6 << 20):
     return cases
 
 
-@pytest.mark.parametrize("parse", ["lane", "wave"])
+@pytest.mark.parametrize("parse", ["lane", "wave", "split"])
 def test_chunked_path_exact_and_taken(zs, parse):
-    """Both parse modes of the block-parallel path (a lane per decode unit, a
-    wave per unit) take every stream and give the same exact results."""
+    """Every parse mode of the block-parallel path (a lane per decode unit, a
+    wave per unit, the split parse) takes every stream and gives the same exact
+    results."""
     cases = _big_cases(random.Random(5), 8)
     got = zs.inflate_batch([c[1] for c in cases], [c[2] for c in cases], [len(c[0]) for c in cases], parse=parse)
     st = zs.last_stats()
@@ -207,7 +208,7 @@ def test_chunked_path_exact_and_taken(zs, parse):
     assert st["fallback_jobs"] == 0, st
 
 
-@pytest.mark.parametrize("parse", ["lane", "wave"])
+@pytest.mark.parametrize("parse", ["lane", "wave", "split"])
 def test_chunked_path_errors_match_oracle(zs, parse):
     rng = random.Random(6)
     base = _big_cases(rng, 6, 600 << 10, 2 << 20)
@@ -225,14 +226,17 @@ def test_chunked_path_errors_match_oracle(zs, parse):
     run_and_compare(zs, cases, parse)
 
 
-def test_chunked_random_and_stored(zs):
+@pytest.mark.parametrize("parse", [None, "split"])
+def test_chunked_random_and_stored(zs, parse):
+    """Random bytes and text at levels 0 / 1 / 6: stored first blocks are split
+    parse leftovers (zs_unitw_list_kernel), the rest walks and splits."""
     rng = random.Random(7)
     raw = bytes(rng.getrandbits(8) for _ in range(1 << 20)) + corpus.stream(5, 1 << 20)
     comps = []
     for lvl in (0, 1, 6):
         c = zlib.compressobj(lvl, zlib.DEFLATED, -15)
         comps.append(c.compress(raw) + c.flush())
-    got = zs.inflate_batch(comps, -15, [len(raw)] * 3)
+    got = zs.inflate_batch(comps, -15, [len(raw)] * 3, parse=parse)
     for (out, info), comp in zip(got, comps):
         assert info["ret"] == 1 and info["total_in"] == len(comp) and out == raw
 
@@ -267,7 +271,8 @@ def test_chunked_overprovisioned_out_cap(zs):
     assert st["chunked_jobs"] == 1 and st["fallback_jobs"] == 0, st
 
 
-def test_chunked_fixed_strategy_16mib(zs):
+@pytest.mark.parametrize("parse", [None, "split"])
+def test_chunked_fixed_strategy_16mib(zs, parse):
     """A 16 MiB Z_FIXED stream (fixed-Huffman blocks only, no header to search
     for): zs_find_fixed_kernel records the block starts, the stream splits into
     many units, and output + zlib fields match the oracle."""
@@ -275,7 +280,7 @@ def test_chunked_fixed_strategy_16mib(zs):
     for wb in (-15, 31):
         c = zlib.compressobj(6, zlib.DEFLATED, wb, 8, zlib.Z_FIXED)
         comp = c.compress(raw) + c.flush()
-        got = zs.inflate_batch([comp], wb, [len(raw)])
+        got = zs.inflate_batch([comp], wb, [len(raw)], parse=parse)
         st = zs.last_stats()
         eo, ei = O.oneshot(comp, wb, len(raw))
         assert got[0][0] == eo == raw and got[0][1] == ei, (got[0][1], ei)
@@ -303,7 +308,7 @@ def test_chunked_high_ratio(zs):
     assert st["chunked_jobs"] == 1 and st["fallback_jobs"] == 0 and st["units"] > 1, st
 
 
-@pytest.mark.parametrize("parse", ["lane", "wave"])
+@pytest.mark.parametrize("parse", ["lane", "wave", "split"])
 def test_chunked_token_pool_pages(zs, parse):
     """Streams with several symbols per compressed byte (Huffman-only and RLE
     over a 3-letter alphabet: 1-2 bit literal codes) outgrow the primary token
@@ -514,15 +519,15 @@ def test_c5_rank_share_world8_vs_oracle(zs):
 def test_c2_headline_batch_segmented_link_vs_oracle(zs):
     """configs[1] exactly as the headline bench runs it: 64 x 64 MiB raw-deflate
     streams (Zipf text 0..31, line text 32..63, host zlib L6) in ONE batch with
-    default flags -- lane parse, segmented link with 4 segments per chain of
-    ~720 members -- every job's output and (ret, msg, total_in, total_out,
-    adler) vs the oracle and the generator."""
+    default flags -- split parse (round 5), segmented link with 4 segments per
+    chain of ~720 members -- every job's output and (ret, msg, total_in,
+    total_out, adler) vs the oracle and the generator."""
     raws, comps = corpus.batch(0, 64, 64 << 20, level=6, wbits=-15, nthreads=16)
     cases = [(r, c.tobytes(), -15) for r, c in zip(raws, comps)]
     del comps
     got = zs.inflate_batch([c[1] for c in cases], -15, [64 << 20] * 64)
     st = zs.last_stats()
-    assert st["parse"] == "lane" and st["link"] == "segmented" and st["link_segments"] == 4, st
+    assert st["parse"] == "split" and st["link"] == "segmented" and st["link_segments"] == 4, st
     assert st["chunked_jobs"] == 64 and st["fallback_jobs"] == 0, st
     assert st["units_std"] >= 64 * 400, st  # chains of >= 400 members on average
     _compare_all_with_oracle(cases, got, 64 << 20)
@@ -547,7 +552,7 @@ def test_c2_strong_split_share_world8_vs_oracle(zs):
     _compare_all_with_oracle(cases, got, 64 << 20, nthreads=8)
 
 
-@pytest.mark.parametrize("parse", ["lane", "wave"])
+@pytest.mark.parametrize("parse", ["lane", "wave", "split"])
 def test_c2_pair_forced_link_segments_vs_oracle(zs, parse):
     """ZS_F_LINKSEG(n), n = 2 / 4 / 8, on the C2 pair (one Zipf, one line-text
     64 MiB stream: chains of ~900 / ~500 members) under both parse modes: the
@@ -580,3 +585,71 @@ def test_c2_pair_forced_link_segments_vs_oracle(zs, parse):
     st = zs.last_stats()
     assert st["link"] == "segmented" and st["link_segments"] == 8, st
     _compare_all_with_oracle(small, got, cap)
+
+
+# ---------------------------------------------------------------------------
+# the split parse (round 5): boundary walk + sub-unit decode + leftovers
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("kind", ["zipf", "lines"])
+def test_split_parse_forced_text_vs_oracle(zs, kind):
+    """The split parse forced on 8 x 8 MiB streams of one text kind (Zipf words,
+    or the periodic line text that defeated round 1's self-synchronising split):
+    the walk's checkpoints are exact symbol boundaries, so every job equals the
+    oracle whatever the text; the lane parse gives the same bytes."""
+    base = 0 if kind == "zipf" else 32
+    raws, comps = corpus.batch(base, 8, 8 << 20, level=6, wbits=-15, nthreads=8)
+    cases = [(r, c.tobytes(), -15) for r, c in zip(raws, comps)]
+    got = zs.inflate_batch([c[1] for c in cases], -15, [8 << 20] * 8, parse="split")
+    st = zs.last_stats()
+    assert st["parse"] == "split" and st["chunked_jobs"] == 8 and st["fallback_jobs"] == 0, st
+    _compare_all_with_oracle(cases, got, 8 << 20, nthreads=8)
+    lane = zs.inflate_batch([c[1] for c in cases], -15, [8 << 20] * 8, parse="lane")
+    assert [g[1] for g in lane] == [g[1] for g in got] and all(a[0] == b[0] for a, b in zip(lane, got))
+
+
+def test_split_parse_small_blocks_continue(zs):
+    """Blocks of ~1-3 KiB (a sync flush every few KiB): a 32 KiB search segment
+    holds more block starts than the finder records, so units run past their
+    first block -- the split decodes the first block, the leftover kernel
+    resumes at its end (WK_CONT) -- and more units end with a false start
+    inside; every result field vs the oracle, for raw / zlib / gzip."""
+    rng = random.Random(21)
+    cases = []
+    for k, wb in enumerate((-15, 15, 31, -15)):
+        raw = corpus.stream(k + 3, 3 << 20)
+        c = zlib.compressobj(6, zlib.DEFLATED, wb)
+        parts, i = [], 0
+        while i < len(raw):
+            n = rng.randint(1 << 10, 6 << 10)
+            parts.append(c.compress(raw[i:i + n]))
+            parts.append(c.flush(zlib.Z_SYNC_FLUSH if rng.random() < 0.7 else zlib.Z_FULL_FLUSH))
+            i += n
+        parts.append(c.flush())
+        cases.append((raw, b"".join(parts), wb))
+    got = zs.inflate_batch([c[1] for c in cases], [c[2] for c in cases], [3 << 20] * len(cases), parse="split")
+    st = zs.last_stats()
+    assert st["parse"] == "split" and st["chunked_jobs"] == len(cases) and st["fallback_jobs"] == 0, st
+    for (raw, comp, wb), (out, info) in zip(cases, got):
+        eo, ei = O.oneshot(comp, wb, 3 << 20)
+        assert out == eo == raw and info == ei, (wb, info, ei)
+
+
+def test_split_parse_first_unit_too_far(zs):
+    """A raw stream written against a preset dictionary, inflated without it:
+    its first block reaches before the stream start.  The split parse defers the
+    too-far check of the stream's first unit to its wave scan of sub-unit
+    outputs; the stream goes to the exact decoder, which reports zlib's
+    "invalid distance too far back" -- every field vs the oracle; a clean
+    stream in the same batch still decodes on the chunked path."""
+    zdict = corpus.stream(9, 32 << 10)
+    raw = zdict * 8 + corpus.stream(10, 2 << 20)
+    c = zlib.compressobj(6, zlib.DEFLATED, -15, 8, 0, zdict)
+    bad = c.compress(raw) + c.flush()
+    c2 = zlib.compressobj(6, zlib.DEFLATED, -15)
+    good = c2.compress(raw) + c2.flush()
+    cap = len(raw)
+    got = zs.inflate_batch([bad, good], -15, [cap, cap], parse="split")
+    for comp, (out, info) in zip((bad, good), got):
+        eo, ei = O.oneshot(comp, -15, cap)
+        assert out == eo and info == ei, (info, ei)
+    assert got[0][1]["ret"] == -3 and got[1][0] == raw

@@ -1,10 +1,11 @@
 #!/bin/bash
 # HBM traffic of the inflate pipeline on the bench workload: two rocprofv3 PMC
 # passes (FETCH_SIZE, WRITE_SIZE), kernel trace only (no sys/runtime traces).
-# Run on the GPU box from the repo root; writes gpurun_out/pmc/pmc_traffic.json (copy it into profiles/).
+# Run on the GPU box from the repo root; writes $PMC_OUT (default gpurun_out/pmc)/pmc_traffic.json
+# (copy it into profiles/).
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-OUT=$R/gpurun_out/pmc
+OUT=${PMC_OUT:-$R/gpurun_out/pmc}
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 B="$R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-compress --no-deflate64 --no-stream-leg --no-c5-leg"

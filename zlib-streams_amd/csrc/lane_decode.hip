@@ -95,6 +95,52 @@ __device__ __forceinline__ uint16_t compact_dist_entry(uint32_t z, uint32_t add_
 
 #define OP_ROOT9 15u
 
+// Split parse walk tables (zs_walk_kernel): u8 entries indexed by the next
+// WK_LBITS (literal/length) or WK_DBITS (distance) input bits.  An entry holds
+// the bits the whole element takes -- code plus extra bits -- so the walk
+// needs no symbol values at all: [4:0] bits, WK_HASD a length (a distance
+// follows), WK_BIG deflate64's code 285 (16 extra bits: a length > 65535 is
+// two tokens), WK_EXC anything the walk resolves off its fast path (end of
+// block, an invalid code, a code longer than the table's index).
+#define WK_LBITS 9u
+#define WK_DBITS 7u
+#define WK_HASD 0x20u
+#define WK_EXC 0x40u
+#define WK_BIG 0x80u
+template <bool D64>
+__device__ __forceinline__ uint32_t walk_len_entry(uint32_t ce) {  // from a compact literal/length entry
+  const uint32_t kind = ce & 3u, bits = (ce >> 2) & 15u, sym = ce >> 6;
+  if (kind == CK_SYM) return bits;
+  if (kind != CK_LEN) return WK_EXC;
+  const uint32_t xb = sym < 8u ? 0u : (sym < 28u ? (sym >> 2) - 1u : (D64 ? 16u : 0u));
+  return (bits + xb) | WK_HASD | ((D64 && sym >= 28u) ? WK_BIG : 0u);
+}
+__device__ __forceinline__ uint32_t walk_dist_entry(uint32_t ce) {  // from a compact distance entry
+  if ((ce & 3u) != CK_SYM) return WK_EXC;
+  const uint32_t bits = (ce >> 2) & 15u, dsym = (ce >> 6) & 31u;
+  return bits + (dsym < 4u ? 0u : (dsym >> 1) - 1u);  // extra bits: src/inftrees.c:65-72
+}
+// walk entries from zlib-layout tables (root lbits / dbits) for index i
+template <bool D64>
+__device__ __forceinline__ uint32_t walk_len_z(const uint32_t *zt, uint32_t lbits, uint32_t i) {
+  const uint32_t z = zt[i & ((1u << lbits) - 1u)];
+  const uint32_t op = e_op(z);
+  if (op != 0 && (op & 0xf0u) == 0) return WK_EXC;  // sub-table: longer than WK_LBITS (lbits = 9 here)
+  return walk_len_entry<D64>(compact_len_entry(z));
+}
+__device__ __forceinline__ uint32_t walk_dist_z(const uint32_t *zt, uint32_t dbits, uint32_t i) {
+  const uint32_t z = zt[i & ((1u << dbits) - 1u)];
+  const uint32_t op = e_op(z);
+  if (op & 64u) return WK_EXC;
+  if ((op & 0xf0u) == 0) {  // sub-table: the index's bits past the root pick the entry if the code fits
+    const uint32_t avail = WK_DBITS - dbits;
+    const uint32_t z2 = zt[e_val(z) + ((i >> dbits) & ((1u << min(op, avail)) - 1u))];
+    if ((e_op(z2) & 64u) || dbits + e_bits(z2) > WK_DBITS) return WK_EXC;
+    return walk_dist_entry(compact_dist_entry(z2, dbits));
+  }
+  return walk_dist_entry(compact_dist_entry(z));
+}
+
 // LDS root entry for 8-bit prefix i from a zlib literal/length table with
 // lbits-bit root (lbits <= 9)
 __device__ __forceinline__ uint16_t lds_len_root(const uint32_t *zt, uint32_t lbits, uint32_t i) {
@@ -685,7 +731,7 @@ __device__ void build_dist_tail(const uint16_t *dl, uint32_t n, uint8_t *out) {
 template <bool D64>
 __device__ int wave_dyn_header(BuildLDS &B, const uint32_t *w, uint32_t end_byte, uint32_t &bit, uint32_t *tabg,
                                uint16_t *ctab, uint32_t &lbits, uint32_t &dbits, uint16_t *lroot_out,
-                               uint16_t *droot_out, uint8_t *dtail_out) {
+                               uint16_t *droot_out, uint8_t *dtail_out, uint8_t *walk_out = nullptr) {
   const uint32_t lane = lane_id();
   const uint32_t limit = end_byte * 8u;
   StageBits sb;
@@ -760,6 +806,8 @@ __device__ int wave_dyn_header(BuildLDS &B, const uint32_t *w, uint32_t end_byte
     ctab[i] = compact_len_entry(B.tab[i], i < (1u << lbits) ? 0u : lbits);
   }
   for (uint32_t i = lane; i < LROOT_N; i += WAVE) lroot_out[i] = lds_len_root(B.tab, lbits, i);
+  if (walk_out)
+    for (uint32_t i = lane; i < (1u << WK_LBITS); i += WAVE) walk_out[i] = (uint8_t)walk_len_z<D64>(B.tab, lbits, i);
   __builtin_amdgcn_wave_barrier();
   dbits = 6;
   if (build_table(T_DISTS, B.lens + nlen, ndist, B.tab, &dbits, B.sorted, B.scr, D64 ? 1 : 0)) {
@@ -771,6 +819,9 @@ __device__ int wave_dyn_header(BuildLDS &B, const uint32_t *w, uint32_t end_byte
     ctab[DIST_TABLE_OFF + i] = compact_dist_entry(B.tab[i], i < (1u << dbits) ? 0u : dbits);
   }
   droot_out[lane] = compact_dist_entry(B.tab[lane & ((1u << dbits) - 1u)]);
+  if (walk_out)
+    for (uint32_t i = lane; i < (1u << WK_DBITS); i += WAVE)
+      walk_out[(1u << WK_LBITS) + i] = (uint8_t)walk_dist_z(B.tab, dbits, i);
   if (lane == 0) build_dist_tail(B.lens + nlen, ndist, dtail_out);
   __builtin_amdgcn_wave_barrier();
   return 0;
@@ -1442,16 +1493,27 @@ __device__ __forceinline__ UwSym uw_decode(const uint32_t *lt, const uint32_t *d
 
 __device__ __forceinline__ uint32_t uni32(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// Split parse state of a unit (zs_walk_kernel / zs_split_kernel, below)
+enum { WK_NONE = 0, WK_SPLIT = 1, WK_CONT = 2, WK_LEFT = 3 };
+struct ZsWalkDev {
+  uint32_t status;   // WK_*
+  uint32_t nsub;     // WK_SPLIT: sub-units (checkpoints + 1)
+  uint32_t ntok;     // tokens of the first block (a deflate64 length > 65535 counts two)
+  uint32_t eob_bit;  // where the first block's end-of-block code starts
+  uint32_t end_bit;  // the bit after it
+  uint32_t pos;      // WK_CONT: entries of the first block
+  uint32_t sidx;     // WK_CONT: the first later unit slot starting at or past end_bit ...
+  uint32_t stop;     // ... and its start bit (ZS_NONE: none)
+};
+
+// One unit with a whole wave (the body of zs_unitw_kernel).  wk (split
+// parse leftovers): a WK_CONT unit resumes at its first block's end with the
+// split's output counts, exactly where the lane decoder would be there.
 template <bool D64>
-__global__ void __launch_bounds__(64) zs_unitw_kernel(const ZsJobDev *__restrict__ jobs, const ZsHeadDev *__restrict__ heads,
-                                                       ZsChunkDev *__restrict__ chunks, uint32_t nchunks,
-                                                       uint32_t *__restrict__ tokens, uint32_t *__restrict__ tables,
-                                                       const uint32_t *__restrict__ fixed, const uint32_t *__restrict__ order,
-                                                       ZsTokPool pool) {
-  __shared__ UnitWLDS L;
+__device__ void unitw_unit(UnitWLDS &L, uint32_t c, const ZsJobDev *__restrict__ jobs, const ZsHeadDev *__restrict__ heads,
+                           ZsChunkDev *__restrict__ chunks, uint32_t *__restrict__ tokens, uint32_t *__restrict__ tables,
+                           const uint32_t *__restrict__ fixed, ZsTokPool pool, const ZsWalkDev *wk) {
   const uint32_t lane = threadIdx.x;
-  const uint32_t c = order[blockIdx.x];  // units by decreasing span
-  if (c >= nchunks) return;
   const ZsChunkDev ch = chunks[c];
   if (ch.start_bit == ZS_NONE || heads[ch.job].code != ZD_END) {
     if (lane == 0) {
@@ -1506,6 +1568,15 @@ __global__ void __launch_bounds__(64) zs_unitw_kernel(const ZsJobDev *__restrict
     s.zd = lane_tab + DIST_TABLE_OFF;
     s.lbits = (ch.hdr_info >> 8) & 15u;
     s.dbits = (ch.hdr_info >> 12) & 15u;
+  }
+  if (wk && wk->status == WK_CONT) {  // the split decoded the first block: resume at its end
+    s.mode = LM_BLOCK;
+    s.bit = wk->end_bit;
+    s.pos = wk->pos;
+    s.ntok = wk->ntok;
+    s.last = 0;
+    s.sidx = wk->sidx;
+    s.stop = wk->stop;
   }
   const uint64_t prim = ch.tok;
   for (;;) {
@@ -1711,6 +1782,523 @@ __global__ void __launch_bounds__(64) zs_unitw_kernel(const ZsJobDev *__restrict
     o->end_bit = (s.code == ZD_END || s.code == ZD_STOP) ? s.bit : 0u;
     o->n_out = s.pos;
     o->n_tok = s.ntok;
+  }
+}
+
+template <bool D64>
+__global__ void __launch_bounds__(64) zs_unitw_kernel(const ZsJobDev *__restrict__ jobs, const ZsHeadDev *__restrict__ heads,
+                                                       ZsChunkDev *__restrict__ chunks, uint32_t nchunks,
+                                                       uint32_t *__restrict__ tokens, uint32_t *__restrict__ tables,
+                                                       const uint32_t *__restrict__ fixed, const uint32_t *__restrict__ order,
+                                                       ZsTokPool pool) {
+  __shared__ UnitWLDS L;
+  const uint32_t c = order[blockIdx.x];  // units by decreasing span
+  if (c >= nchunks) return;
+  unitw_unit<D64>(L, c, jobs, heads, chunks, tokens, tables, fixed, pool, nullptr);
+}
+
+// The split parse's leftovers (list[0 .. *count)), a wave per unit over a
+// fixed grid: units whose first block is stored or did not decode, the rest of
+// units that run past their first block (WK_CONT), and any split that failed
+// its own consistency check (WK_LEFT, decoded again from the start).
+template <bool D64>
+__global__ void __launch_bounds__(64) zs_unitw_list_kernel(const ZsJobDev *__restrict__ jobs,
+                                                            const ZsHeadDev *__restrict__ heads,
+                                                            ZsChunkDev *__restrict__ chunks, uint32_t *__restrict__ tokens,
+                                                            uint32_t *__restrict__ tables, const uint32_t *__restrict__ fixed,
+                                                            const uint32_t *__restrict__ list, const uint32_t *__restrict__ count,
+                                                            ZsTokPool pool, const ZsWalkDev *__restrict__ walks) {
+  __shared__ UnitWLDS L;
+  const uint32_t n = *count;
+  for (uint32_t k = blockIdx.x; k < n; k += gridDim.x) {
+    const uint32_t c = list[k];
+    unitw_unit<D64>(L, c, jobs, heads, chunks, tokens, tables, fixed, pool, &walks[c]);
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Split parse (round 5): an EXACT intra-block split of every unit's first block.
+//
+// The lane parse (zs_lane_kernel) decodes one ~16 K-symbol block per lane at
+// one wave per SIMD, so its time is one block's serial decode: ~16 K steps of
+// ~1 260 cycles.  Here the serial part is only a boundary walk, and the token
+// decode runs on many waves:
+//   zs_walk_kernel   one lane per unit: the block's symbols are walked by their
+//                    LENGTHS only (u8 tables: code + extra bits of a literal /
+//                    length, then of a distance; no values, no tokens), and
+//                    every WK_K0 tokens the walk records a checkpoint (bit,
+//                    token index).  Nothing is speculative: the checkpoints are
+//                    true symbol boundaries of the block.
+//   zs_split_kernel  one wave per walked unit, lane j decoding sub-unit j
+//                    (checkpoint j to checkpoint j + 1) into the unit's tokens
+//                    with lane_step_fast's decoder, the block's one table image
+//                    in LDS shared by the whole wave (~9 KiB per wave instead of
+//                    the lane parse's 52 KiB): many waves per SIMD hide latency.
+//                    The checks that need the output position (unit full,
+//                    distance too far back) run after a wave scan of the
+//                    sub-units' output counts; then the unit stops exactly as
+//                    coop_block decides at the block's end.
+//   zs_unitw_list_kernel  the leftovers, a wave per unit: units that run past
+//                    their first block (resumed at its end), stored or
+//                    undecodable first blocks.
+// Results (tokens, n_out, n_tok, end bit, code for STOP / END units) equal the
+// lane decoder's; units that end otherwise only need a code that is neither
+// ZD_STOP nor ZD_END (the chain never uses them: zs_chain_kernel), and get the
+// one the lane decoder would report for the first anomaly the walk meets.
+// Reference: src/inffast.c:100-287 (the symbol loop), src/inflate.c:1037-1193.
+// ---------------------------------------------------------------------------
+#define WK_CP 64u    // checkpoint slots per unit slot: <= 64 sub-units, one wave
+#define WK_K0 256u   // tokens per sub-unit to start with (doubled, checkpoints halved, when WK_CP - 1 run out)
+#define WK_RING (RING + 1)  // words prefetched for the next walk group
+
+struct WalkLDS {
+  uint8_t wl[WAVE][1u << WK_LBITS];
+  uint8_t wd[WAVE][1u << WK_DBITS];
+  uint32_t ring[RING][WAVE];
+};
+
+// literal / length code longer than the walk table (or end of block, invalid):
+// the unit's compact tables, as lane_step reads them.  Returns a walk entry;
+// end of block: 0x100 | WK_EXC | code bits; invalid: WK_EXC alone.
+template <bool D64>
+__device__ __noinline__ uint32_t walk_slow_len(uint32_t h, const uint16_t *cl, uint32_t lbits) {
+  uint32_t ce = cl[h & ((1u << lbits) - 1u)];
+  if ((ce & 3u) == CK_SLOW) {
+    const uint32_t op = (ce >> 2) & 15u;
+    if (op == 0) return WK_EXC;
+    ce = cl[(ce >> 6) + ((h >> lbits) & ((1u << op) - 1u))];
+    if ((ce & 3u) == CK_SLOW) return WK_EXC;
+  }
+  if ((ce & 3u) == CK_EOB) return 0x100u | WK_EXC | ((ce >> 2) & 15u);
+  return walk_len_entry<D64>(ce);
+}
+__device__ __noinline__ uint32_t walk_slow_dist(uint32_t h, const uint16_t *cd, uint32_t dbits) {
+  uint32_t ce = cd[h & ((1u << dbits) - 1u)];
+  if ((ce & 3u) == CK_SLOW) {
+    const uint32_t op = (ce >> 2) & 15u;
+    if (op == 0) return WK_EXC;
+    ce = cd[(ce >> 6) + ((h >> dbits) & ((1u << op) - 1u))];
+  }
+  return walk_dist_entry(ce);
+}
+
+// RING + 1 input words from word wi (masked past the end of the input)
+__device__ __forceinline__ void walk_load(const LaneState &s, uint32_t wi, uint32_t (&v)[WK_RING]) {
+  if (wi + WK_RING <= s.lastw) {
+    const uint32_t *src = (const uint32_t *)(s.w + wi);
+#pragma unroll
+    for (int q = 0; q < RING / 4; q++) {
+      uint4 x;
+      __builtin_memcpy(&x, src + 4 * q, 16);
+      v[4 * q] = x.x;
+      v[4 * q + 1] = x.y;
+      v[4 * q + 2] = x.z;
+      v[4 * q + 3] = x.w;
+    }
+    v[RING] = src[RING];
+  } else {
+#pragma unroll
+    for (int q = 0; q < WK_RING; q++) v[q] = in_word_g(s.w, wi + q, s.end_byte);
+  }
+}
+
+enum { WS_RUN = 0, WS_EOB = 1, WS_BAD = 2, WS_IDLE = 3 };
+
+template <bool D64>
+__global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict__ jobs, const ZsHeadDev *__restrict__ heads,
+                                                      ZsChunkDev *__restrict__ chunks, uint32_t nchunks,
+                                                      const uint32_t *__restrict__ tables, const uint32_t *__restrict__ order,
+                                                      ZsTokPool pool, uint32_t lane_map, ZsWalkDev *__restrict__ walks,
+                                                      uint2 *__restrict__ cps, uint32_t *__restrict__ lists,
+                                                      uint32_t *__restrict__ counts) {
+  __shared__ WalkLDS L;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t ci = lane_map ? (blockIdx.x / lane_map) * lane_map * WAVE +
+                                     lane * min(lane_map, gridDim.x - (blockIdx.x / lane_map) * lane_map) +
+                                     blockIdx.x % lane_map
+                               : blockIdx.x * WAVE + lane;
+  const uint32_t c = ci < nchunks ? order[ci] : ZS_NONE;
+  LaneState s;
+  s.w = nullptr;
+  s.end_byte = s.limit = 0;
+  s.wi = s.nw = s.nkeep = s.nbits = s.lastw = s.rk = 0;
+  s.hold = 0;
+  uint32_t wst = WS_IDLE, code = 0, lbits = 9, dbits = 6, tcap = 0;
+  const uint16_t *cl = nullptr;
+  if (c < nchunks) {
+    const ZsChunkDev ch = chunks[c];
+    if (ch.start_bit != ZS_NONE && heads[ch.job].code == ZD_END) {
+      if (ch.hdr_info & 1u) {
+        const ZsJobDev jb = jobs[ch.job];
+        const uintptr_t ip = reinterpret_cast<uintptr_t>(jb.in);
+        const uint32_t mis = (uint32_t)(ip & 3u);
+        s.w = (gcu32 *)(ip - mis);
+        s.end_byte = mis + (uint32_t)jb.in_len;
+        s.limit = s.end_byte * 8u;
+        tcap = ch.tcap;
+        lbits = (ch.hdr_info >> 8) & 15u;
+        dbits = (ch.hdr_info >> 12) & 15u;
+        const uint32_t *tabg = tables + (size_t)c * TABLE_STRIDE;
+        cl = reinterpret_cast<const uint16_t *>(tabg + TABLE_ENTRIES);
+        const uint4 *wt = reinterpret_cast<const uint4 *>(tabg + TABLE_WALK_OFF);
+        uint4 *wl4 = reinterpret_cast<uint4 *>(L.wl[lane]);
+        uint4 *wd4 = reinterpret_cast<uint4 *>(L.wd[lane]);
+#pragma unroll 8
+        for (uint32_t k = 0; k < (1u << WK_LBITS) / 16u; k++) wl4[k] = wt[k];
+#pragma unroll
+        for (uint32_t k = 0; k < (1u << WK_DBITS) / 16u; k++) wd4[k] = wt[(1u << WK_LBITS) / 16u + k];
+        lane_prime(s, ch.hdr_bit);
+        wst = WS_RUN;
+      } else {  // stored or undecodable first block: a leftover from the start
+        walks[c].status = WK_NONE;
+        const uint32_t k = atomicAdd(&counts[1], 1u);  // lists: [0, nchunks) splits, [nchunks, 2 nchunks) leftovers
+        lists[nchunks + k] = c;
+      }
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  const uint8_t *wl = L.wl[lane];
+  const uint8_t *wd = L.wd[lane];
+  uint32_t *rp = &L.ring[0][lane];
+  const uint16_t *cd = cl ? cl + DIST_TABLE_OFF : nullptr;
+  uint2 *cp = cps + (size_t)(c < nchunks ? c : 0u) * WK_CP;
+  uint32_t ntok = 0, K = WK_K0, ncp = 0, ncut = WK_K0, eob = 0, endb = 0;
+  uint32_t pre[WK_RING];
+  uint32_t pre_wi = ~0u;
+  for (;;) {
+    if (__ballot(wst == WS_RUN) == 0) break;
+    if (wst == WS_RUN) {
+      // group start: ring[0..RING) = words wi .. wi + RING - 1 (prefetched during
+      // the last group when it ended where expected), then the next group's words
+      if (s.wi == pre_wi || s.wi == pre_wi + 1u) {
+        const bool sh = s.wi != pre_wi;
+#pragma unroll
+        for (int q = 0; q < RING; q++) rp[q * WAVE] = sh ? pre[q + 1] : pre[q];
+        s.nw = sh ? pre[1] : pre[0];
+        s.rk = 0;
+      } else {
+        lane_fill_ring(s, rp);
+      }
+      // a group ends with rk in {RING - 2, RING - 1}: its successor starts at
+      // word wi + RING - 2 or one later
+      pre_wi = s.wi + RING - 2u;
+      walk_load(s, pre_wi, pre);
+      while (s.rk + 2 < RING) {
+        const uint32_t p0 = lane_pos(s);
+        lane_refill_bf(s, rp);
+        uint32_t e = wl[(uint32_t)s.hold & ((1u << WK_LBITS) - 1u)];
+        if (__builtin_expect(__ballot(e & WK_EXC) != 0, 0)) {
+          if (e & WK_EXC) e = walk_slow_len<D64>((uint32_t)s.hold, cl, lbits);
+        }
+        const uint32_t n = e & 31u;
+        uint32_t two = 0;
+        if (D64) two = (e & WK_BIG) && ((uint32_t)(s.hold >> (n - 16u)) & 0xffffu) >= 65533u;  // length > 65535
+        s.hold >>= n;
+        s.nbits -= n;
+        lane_refill_bf(s, rp);
+        uint32_t d = wd[(uint32_t)s.hold & ((1u << WK_DBITS) - 1u)];
+        const bool hasd = (e & WK_HASD) != 0;
+        if (__builtin_expect(__ballot(hasd && (d & WK_EXC)) != 0, 0)) {
+          if (hasd && (d & WK_EXC)) d = walk_slow_dist((uint32_t)s.hold, cd, dbits);
+        }
+        const uint32_t dn = hasd ? (d & 31u) : 0u;
+        s.hold >>= dn;
+        s.nbits -= dn;
+        const uint32_t p1 = lane_pos(s);
+        if ((e & WK_EXC) || (hasd && (d & WK_EXC)) || p1 > s.limit) {
+          if (e & 0x100u) {  // end of block
+            eob = p0;
+            endb = p0 + n;
+            wst = endb > s.limit ? WS_BAD : WS_EOB;
+            code = ZD_TRUNC;
+          } else {  // invalid code or truncated: the unit cannot stop at a block boundary
+            wst = WS_BAD;
+            code = p1 > s.limit ? ZD_TRUNC : (ZD_ERROR | (((e & WK_EXC) ? ZM_LITLEN_CODE : ZM_DIST_CODE) << 8));
+          }
+          break;
+        }
+        ntok += 1u + two;
+        if (ntok >= ncut) {  // a checkpoint: the next sub-unit starts here
+          cp[ncp] = make_uint2(p1, ntok);
+          ncp++;
+          ncut += K;
+          if (ncp == WK_CP - 1u) {  // out of slots: keep every second checkpoint, twice the stride
+            for (uint32_t i = 0; i < (WK_CP - 1u) / 2u; i++) cp[i] = cp[2u * i + 1u];
+            ncp = (WK_CP - 1u) / 2u;
+            K *= 2u;
+            ncut = (ncp + 1u) * K;
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // the ring is rewritten by the next group
+  }
+  if (wst == WS_EOB && !tok_ensure(pool, c, tcap, ntok)) {
+    wst = WS_BAD;
+    code = ZD_FULL;
+  }
+  if (wst == WS_EOB) {
+    ZsWalkDev w;
+    w.status = WK_SPLIT;
+    w.nsub = ncp + 1u;
+    w.ntok = ntok;
+    w.eob_bit = eob;
+    w.end_bit = endb;
+    w.pos = 0;
+    w.sidx = 0;
+    w.stop = ZS_NONE;
+    walks[c] = w;
+    const uint32_t k = atomicAdd(&counts[0], 1u);
+    lists[k] = c;
+  } else if (wst == WS_BAD) {
+    chunks[c].code = (int32_t)code;
+    chunks[c].end_bit = 0;
+    chunks[c].n_out = 0;
+    chunks[c].n_tok = 0;
+  }
+}
+
+// lane_step_fast's decoder for a sub-unit of a walked block.  Every symbol
+// before the sub-unit's end is a plain literal or length (the walk met them),
+// so there is no exception path: anything else marks the unit inconsistent
+// (bad: decoded again from its start by zs_unitw_list_kernel).  The checks
+// that depend on the unit's output position are deferred: `need` keeps the
+// most history a distance asks for beyond this sub-unit's own output.
+template <bool D64>
+__device__ __forceinline__ void split_step(LaneState &s, const uint16_t *__restrict__ lt, const uint16_t *__restrict__ dt,
+                                           uint32_t *__restrict__ tb, const uint32_t *__restrict__ dtl,
+                                           const uint32_t *__restrict__ rp, uint32_t &bad, uint32_t &need) {
+  lane_refill_bf(s, rp);
+  uint32_t e = lt[(uint32_t)s.hold & (LROOT_N - 1)];
+  uint32_t kind = e & 3u;
+  if (__builtin_expect(__ballot(kind == CK_SLOW) != 0, 0)) {
+    if (kind == CK_SLOW) {
+      const uint32_t op = (e >> 2) & 15u;
+      uint32_t e2 = CK_SLOW;
+      if (op == OP_ROOT9) {
+        e2 = s.cl[(uint32_t)s.hold & 511u];
+        const uint32_t op2 = (e2 >> 2) & 15u;
+        if ((e2 & 3u) == CK_SLOW && op2) e2 = s.cl[(e2 >> 6) + (((uint32_t)s.hold >> 9) & ((1u << op2) - 1u))];
+      } else if (op) {
+        e2 = s.cl[(e >> 6) + (((uint32_t)s.hold >> s.lbits) & ((1u << op) - 1u))];
+      }
+      e = e2;
+      kind = e & 3u;
+    }
+  }
+  const uint32_t used = (e >> 2) & 15u, sym = e >> 6;
+  const uint32_t isl = kind == CK_LEN;
+  const uint32_t top = sym >= 28u;
+  uint32_t xb = (uint32_t)max((int)(sym >> 2) - 1, 0);
+  xb = top ? (D64 ? 16u : 0u) : xb;
+  xb = isl ? xb : 0u;
+  uint32_t lbase = ((4u + (sym & 3u)) << (xb & 15u)) + 3u - (sym < 4u ? 4u : 0u);
+  lbase = top ? (D64 ? 3u : 258u) : lbase;
+  s.hold >>= used;
+  const uint32_t len = isl ? lbase + ((uint32_t)s.hold & ((1u << xb) - 1u)) : 1u;
+  s.hold >>= xb;
+  s.nbits -= used + xb;
+  lane_refill_bf(s, rp);
+  uint32_t d = dt[(uint32_t)s.hold & (DROOT_N - 1)];
+  const uint32_t dtr = dist_tail_r(s.dta, s.dtb, dtl, (uint32_t)s.hold);
+  const bool dslow = isl && (d & 3u) == CK_SLOW;
+  d = dslow ? (((d >> 2) & 15u) ? dtr : (uint32_t)CK_SLOW) : d;
+  const uint32_t dused = (d >> 2) & 15u, dsym = (d >> 6) & 31u;
+  const uint32_t dx = min((uint32_t)max((int)(dsym >> 1) - 1, 0), 14u);
+  const uint32_t dist = ((2u + (dsym & 1u)) << dx) + 1u - (dsym < 2u ? 2u : 0u) +
+                        ((uint32_t)(s.hold >> dused) & ((1u << dx) - 1u));
+  const uint32_t dcons = isl ? dused + dx : 0u;
+  s.hold >>= dcons;
+  s.nbits -= dcons;
+  bad |= (uint32_t)(kind >= CK_EOB) | (isl & (uint32_t)((d & 3u) == CK_SLOW));
+  need = max(need, (isl && dist > s.pos) ? dist - s.pos : 0u);
+  if (D64 && len > 0xffffu) {  // a deflate64 copy longer than a token holds: two copies, same distance
+    tb[s.gk * WAVE] = (0xffffu << 16) | (dist - 1u);
+    s.gk++;
+    s.ntok++;
+    tb[s.gk * WAVE] = ((len - 0xffffu) << 16) | (dist - 1u);
+  } else {
+    tb[s.gk * WAVE] = isl ? ((len << 16) | (dist - 1u)) : sym;
+  }
+  s.gk++;
+  s.ntok++;
+  s.pos += len;
+}
+
+struct __attribute__((aligned(16))) SplitLDS {
+  uint16_t lroot[LROOT_N];  // the block's table image (zs_unit_header_kernel), shared by the wave
+  uint16_t droot[DROOT_N];
+  uint32_t dtail[DTAIL_BYTES / 4];
+  uint32_t tokbuf[GROUP][WAVE];
+  uint32_t ring[RING][WAVE];
+};
+#define SPLIT_IMG_U4 ((LROOT_N * 2 + DROOT_N * 2 + DTAIL_BYTES) / 16)
+
+template <bool D64>
+__global__ void __launch_bounds__(64) zs_split_kernel(const ZsJobDev *__restrict__ jobs, ZsChunkDev *__restrict__ chunks,
+                                                       uint32_t nchunks, uint32_t *__restrict__ tokens,
+                                                       const uint32_t *__restrict__ tables, ZsTokPool pool,
+                                                       ZsWalkDev *__restrict__ walks, const uint2 *__restrict__ cps,
+                                                       uint32_t *__restrict__ lists, uint32_t *__restrict__ counts) {
+  __shared__ SplitLDS L;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t nsplit = counts[0];
+  constexpr uint32_t HMAX = D64 ? 65536u : HIST;
+  for (uint32_t k = blockIdx.x; k < nsplit; k += gridDim.x) {
+    const uint32_t c = lists[k];
+    const ZsWalkDev wk = walks[c];
+    const ZsChunkDev ch = chunks[c];
+    const ZsJobDev jb = jobs[ch.job];
+    const uint32_t *tabg = tables + (size_t)c * TABLE_STRIDE;
+    __builtin_amdgcn_wave_barrier();  // the previous unit is done with the image
+    if (lane < SPLIT_IMG_U4)
+      reinterpret_cast<uint4 *>(&L)[lane] = reinterpret_cast<const uint4 *>(tabg + TABLE_IMG_OFF)[lane];
+    const bool act = lane < wk.nsub;
+    const uint2 *cpu = cps + (size_t)c * WK_CP;
+    const uint2 a0 = cpu[lane ? lane - 1u : 0u];
+    const uint2 a = lane == 0 ? make_uint2(ch.hdr_bit, 0u) : a0;
+    const uint2 b = lane + 1u == wk.nsub ? make_uint2(wk.eob_bit, wk.ntok) : cpu[lane];
+    LaneState s;
+    const uintptr_t ip = reinterpret_cast<uintptr_t>(jb.in);
+    const uint32_t mis = (uint32_t)(ip & 3u);
+    s.w = (gcu32 *)(ip - mis);
+    s.end_byte = mis + (uint32_t)jb.in_len;
+    s.limit = s.end_byte * 8u;
+    s.tok = (gu32 *)(tokens + ch.tok);
+    s.tcap = ch.tcap;
+    s.unit = c;
+    s.lbits = (ch.hdr_info >> 8) & 15u;
+    s.cl = (gcu16 *)(tabg + TABLE_ENTRIES);
+    s.capx = ch.cap;
+    s.pos = 0;
+    s.ntok = a.y;
+    s.gk = s.rk = 0;
+    s.wi = s.nw = s.nkeep = s.nbits = s.lastw = 0;
+    s.hold = 0;
+    const uint32_t t1 = b.y, b1 = b.x;
+    if (act) lane_prime(s, a.x);
+    __builtin_amdgcn_wave_barrier();
+    s.dta = *reinterpret_cast<const uint4 *>(L.dtail);
+    s.dtb = *reinterpret_cast<const uint4 *>(L.dtail + 4);
+    const uint16_t *lt = L.lroot;
+    const uint16_t *dt = L.droot;
+    uint32_t *tb = &L.tokbuf[0][lane];
+    uint32_t *rp = &L.ring[0][lane];
+    uint32_t bad = 0, need = 0, full = 0;
+    uint32_t pre[RING];
+    uint32_t pre_wi = ~0u;
+    for (;;) {
+      const bool run = act && !bad && !full && s.ntok < t1;
+      if (__ballot(run) == 0) break;
+      s.gk = 0;
+      if (run) {
+        if (s.wi == pre_wi) lane_store_ring(s, rp, pre);
+        else lane_fill_ring(s, rp);
+        while (!bad && !full && s.ntok < t1 && s.gk + (D64 ? 2u : 1u) <= GROUP && s.rk + 2 < RING) {
+          split_step<D64>(s, lt, dt, tb, L.dtail, rp, bad, need);
+          full |= s.pos > s.capx;
+        }
+        if (s.ntok > t1) {  // an inconsistent decode: never write past the walked tokens
+          bad = 1;
+          s.gk -= min(s.gk, s.ntok - t1);
+          s.ntok = t1;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      // the next group's input words, loaded before this group's tokens leave
+      const bool more = run && !bad && !full && s.ntok < t1;
+      pre_wi = more ? s.wi : ~0u;
+      if (more) lane_load_ring(s, pre);
+      const uint32_t g0 = s.ntok - s.gk;
+      {  // 16-byte transposed stores of full token quads (zs_lane_kernel's flush)
+        typedef uint32_t u32x4a4t __attribute__((ext_vector_type(4), aligned(4)));
+        const uint32_t q = lane >> 4;
+        const uint32_t nq = s.ntok <= s.tcap ? (s.gk >> 2) : 0u;
+        const uintptr_t dst = (uintptr_t)(s.tok + g0);
+#pragma unroll
+        for (uint32_t r = 0; r < 4; r++) {
+          const uint32_t src = 16u * r + (lane & 15u);
+          const uint32_t nq_s = (uint32_t)__shfl((int)nq, (int)src);
+          const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)dst, (int)src);
+          const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)((uint64_t)dst >> 32), (int)src);
+          if (q < nq_s) {
+            u32x4a4t v;
+            v.x = L.tokbuf[4 * q][src];
+            v.y = L.tokbuf[4 * q + 1][src];
+            v.z = L.tokbuf[4 * q + 2][src];
+            v.w = L.tokbuf[4 * q + 3][src];
+            *reinterpret_cast<__attribute__((address_space(1))) u32x4a4t *>(((uint64_t)hi << 32 | lo) + 16u * q) = v;
+          }
+        }
+      }
+      if (s.ntok <= s.tcap) {
+        const uint32_t t0 = s.gk & ~3u;
+#pragma unroll
+        for (uint32_t j = 0; j < 3; j++)
+          if (t0 + j < s.gk) s.tok[g0 + t0 + j] = L.tokbuf[t0 + j][lane];
+      } else {  // past the primary region: pool pages (taken by the walk)
+        const uint64_t prim_off = (uint64_t)((const uint32_t *)s.tok - tokens);
+        for (uint32_t j = 0; j < s.gk; j++) *tok_addr(pool, tokens, s.unit, prim_off, s.tcap, g0 + j) = L.tokbuf[j][lane];
+      }
+      __builtin_amdgcn_wave_barrier();  // tokbuf is rewritten by the next group
+    }
+    if (act && !full && (lane_pos(s) != b1 || s.ntok != t1)) bad = 1;
+    const bool anybad = __ballot(bad) != 0, anyfull = __ballot(full) != 0;
+    // output position of every sub-unit: a wave scan of their entry counts
+    uint64_t incl = act ? s.pos : 0u;
+#pragma unroll
+    for (uint32_t o = 1; o < WAVE; o <<= 1) {
+      const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)incl, o);
+      const uint32_t hi = (uint32_t)__shfl_up((int)(uint32_t)(incl >> 32), o);
+      if (lane >= o) incl += ((uint64_t)hi << 32) | lo;
+    }
+    const uint64_t P = incl - (act ? s.pos : 0u);
+    const uint64_t total = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(incl >> 32), WAVE - 1) << 32) |
+                           __builtin_amdgcn_readlane((uint32_t)incl, WAVE - 1);
+    const uint32_t whave = ch.ord == 0 ? ((jb.flags & ZS_JF_CONT) ? min(jb.hist, HMAX) : 0u) : HMAX;
+    const bool far = whave < HMAX && __ballot(act && (uint64_t)need > P + whave) != 0;
+    if (lane == 0) {
+      ZsChunkDev *o = &chunks[c];
+      if (anybad) {  // decode again from the start (never expected)
+        walks[c].status = WK_LEFT;
+        lists[nchunks + atomicAdd(&counts[1], 1u)] = c;
+      } else if (far || anyfull || total > ch.cap) {  // the lane decoder stops inside the block
+        o->code = far ? (ZD_ERROR | (ZM_TOO_FAR << 8)) : ZD_FULL;
+        o->end_bit = 0;
+        o->n_out = 0;
+        o->n_tok = 0;
+      } else {
+        // the block's end, as coop_block meets it: the final block ends the
+        // stream; else a recorded start at this bit ends the unit; else the
+        // unit goes on (a block the finder did not record, or a false start)
+        const uint32_t bit = wk.end_bit;
+        int32_t code = -1;
+        uint32_t si = c + 1u, stop = ZS_NONE;
+        if ((ch.hdr_info >> 1) & 1u) {
+          code = ZD_END;
+        } else {
+          const uint32_t se = ch.first + ch.nunits;
+          while (si < se && chunks[si].start_bit < bit) si++;
+          stop = si < se ? chunks[si].start_bit : ZS_NONE;
+          if (stop == bit) code = ZD_STOP;
+        }
+        if (code >= 0) {
+          o->code = code;
+          o->end_bit = bit;
+          o->n_out = (uint32_t)total;
+          o->n_tok = wk.ntok;
+        } else {
+          ZsWalkDev w = wk;
+          w.status = WK_CONT;
+          w.pos = (uint32_t)total;
+          w.sidx = si;
+          w.stop = stop;
+          walks[c] = w;
+          lists[nchunks + atomicAdd(&counts[1], 1u)] = c;
+        }
+      }
+    }
   }
 }
 
@@ -2304,15 +2892,21 @@ __global__ void __launch_bounds__(EX2_T) zs_expand2_kernel(const ZsJobDev *__res
 // the compact root image next to them; the parse pass then starts each lane
 // directly in symbol mode.  A header that does not decode is left to the parse
 // pass, which redoes it cooperatively and reports exactly.
+//
+// Round 5: the stream's first unit too (ord 0), and fixed-code first blocks
+// (BTYPE 1: the fixed tables are copied into the unit's table area, so every
+// consumer treats them as a prebuilt block), each with the split parse's walk
+// tables (TABLE_WALK_OFF).
 template <bool D64>
 __global__ void __launch_bounds__(64) zs_unit_header_kernel(const ZsJobDev *__restrict__ jobs,
                                                              const ZsHeadDev *__restrict__ heads,
-                                                             ZsChunkDev *__restrict__ units, uint32_t *__restrict__ tables) {
+                                                             ZsChunkDev *__restrict__ units, uint32_t *__restrict__ tables,
+                                                             const uint32_t *__restrict__ fixed) {
   __shared__ BuildLDS B;
   const uint32_t c = blockIdx.x;
   const uint32_t lane = threadIdx.x;
   const ZsChunkDev ch = units[c];
-  if (ch.start_bit == ZS_NONE || ch.ord == 0 || heads[ch.job].code != ZD_END) return;
+  if (ch.start_bit == ZS_NONE || heads[ch.job].code != ZD_END) return;
   const ZsJobDev jb = jobs[ch.job];
   const uintptr_t ip = reinterpret_cast<uintptr_t>(jb.in);
   const uint32_t mis = (uint32_t)(ip & 3u);
@@ -2322,15 +2916,37 @@ __global__ void __launch_bounds__(64) zs_unit_header_kernel(const ZsJobDev *__re
   stage_bits(B, w, end_byte, ch.start_bit, sb);
   if (ch.start_bit + 3 > end_byte * 8u) return;
   const uint32_t hdr3 = sb.peek(ch.start_bit, 3);
-  if ((hdr3 >> 1) != 2u) return;  // BTYPE 2 (BFINAL either way)
+  const uint32_t btype = hdr3 >> 1;
+  if (btype != 2u && btype != 1u) return;  // stored / invalid: the parse pass decides
   uint32_t bit = ch.start_bit + 3;
   uint32_t *tabg = tables + (size_t)c * TABLE_STRIDE;
   uint16_t *ctab = reinterpret_cast<uint16_t *>(tabg + TABLE_ENTRIES);
-  uint16_t *img = reinterpret_cast<uint16_t *>(tabg + TABLE_ENTRIES + TABLE_ENTRIES / 2);
+  uint16_t *img = reinterpret_cast<uint16_t *>(tabg + TABLE_IMG_OFF);
+  uint8_t *walk = reinterpret_cast<uint8_t *>(tabg + TABLE_WALK_OFF);
   uint32_t lbits = 9, dbits = 6;
-  if (wave_dyn_header<D64>(B, w, end_byte, bit, tabg, ctab, lbits, dbits, img, img + LROOT_N,
-                      reinterpret_cast<uint8_t *>(img + LROOT_N + DROOT_N)))
+  if (btype == 1u) {  // fixed codes (src/inflate.c:260-298): lit/len root 9, distance root 5
+    const uint16_t *fc = reinterpret_cast<const uint16_t *>(fixed + FIXED_ZLIB_WORDS);
+    for (uint32_t i = lane; i < 512u; i += WAVE) {
+      tabg[i] = fixed[i];
+      ctab[i] = fc[i];
+      walk[i] = (uint8_t)walk_len_z<D64>(fixed, 9u, i);
+    }
+    if (lane < 32) {
+      tabg[DIST_TABLE_OFF + lane] = fixed[512 + lane];
+      ctab[DIST_TABLE_OFF + lane] = fc[512 + lane];
+      B.lens[lane] = 5;
+    }
+    for (uint32_t i = lane; i < LROOT_N; i += WAVE) img[i] = lds_len_root(fixed, 9u, i);
+    img[LROOT_N + lane] = compact_dist_entry(fixed[512 + (lane & 31u)]);
+    for (uint32_t i = lane; i < (1u << WK_DBITS); i += WAVE) walk[(1u << WK_LBITS) + i] = (uint8_t)walk_dist_z(fixed + 512, 5u, i);
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) build_dist_tail(B.lens, 32, reinterpret_cast<uint8_t *>(img + LROOT_N + DROOT_N));
+    lbits = 9;
+    dbits = 5;
+  } else if (wave_dyn_header<D64>(B, w, end_byte, bit, tabg, ctab, lbits, dbits, img, img + LROOT_N,
+                                  reinterpret_cast<uint8_t *>(img + LROOT_N + DROOT_N), walk)) {
     return;
+  }
   if (lane == 0) {
     units[c].hdr_bit = bit;
     units[c].hdr_info = 1u | ((hdr3 & 1u) << 1) | (lbits << 8) | (dbits << 12);
@@ -2420,18 +3036,85 @@ extern "C" uint32_t zs_lane_resident_waves(void) {
   return v;
 }
 
-// wave_units: decode with a wave per unit (zs_unitw_kernel) instead of a lane
-// per unit -- the host picks it when a batch has few units for the GPU.
+namespace {
+struct SplitWs {  // split parse state per unit slot; grown on demand (the library serializes batches)
+  ZsWalkDev *walks = nullptr;
+  uint2 *cps = nullptr;
+  uint32_t *lists = nullptr;  // [0, cap) walked units, [cap, 2 cap) leftovers; then the two counts
+  size_t cap = 0;
+};
+SplitWs g_split;
+int split_reserve(uint32_t n) {
+  if (n <= g_split.cap) return 0;
+  if (g_split.walks) (void)hipFree(g_split.walks);
+  if (g_split.cps) (void)hipFree(g_split.cps);
+  if (g_split.lists) (void)hipFree(g_split.lists);
+  g_split = SplitWs{};
+  const size_t c = (size_t)n + n / 2;
+  if (hipMalloc(&g_split.walks, c * sizeof(ZsWalkDev)) != hipSuccess ||
+      hipMalloc(&g_split.cps, c * WK_CP * sizeof(uint2)) != hipSuccess ||
+      hipMalloc(&g_split.lists, (2 * c + 2) * sizeof(uint32_t)) != hipSuccess)
+    return -1;
+  g_split.cap = c;
+  return 0;
+}
+// Grid of the split and leftover kernels (they loop over device-side lists):
+// enough waves to fill every SIMD several times over.
+uint32_t split_grid(uint32_t n) {
+  static const uint32_t g = [] {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+    return (uint32_t)cus * 32u;
+  }();
+  return std::max(1u, std::min(n, g));
+}
+}  // namespace
+
+// wave_units: 0 = a lane per unit (zs_lane_kernel), 1 = a wave per unit
+// (zs_unitw_kernel, for batches with few units), 2 = the split parse (walk +
+// sub-unit decode + leftovers, for batches with many units).
 extern "C" void zs_launch_parse(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, ZsChunkDev *d_chunks, uint32_t nchunks,
                                 uint32_t *d_tokens, uint32_t *d_tables, const uint32_t *d_fixed, ZsTokPool pool, int d64,
                                 int wave_units, hipStream_t st) {
   if (!nchunks) return;
   if (d64)
-    hipLaunchKernelGGL(zs_unit_header_kernel<true>, dim3(nchunks), dim3(WAVE), 0, st, d_jobs, d_heads, d_chunks, d_tables);
+    hipLaunchKernelGGL(zs_unit_header_kernel<true>, dim3(nchunks), dim3(WAVE), 0, st, d_jobs, d_heads, d_chunks, d_tables,
+                       d_fixed);
   else
-    hipLaunchKernelGGL(zs_unit_header_kernel<false>, dim3(nchunks), dim3(WAVE), 0, st, d_jobs, d_heads, d_chunks, d_tables);
+    hipLaunchKernelGGL(zs_unit_header_kernel<false>, dim3(nchunks), dim3(WAVE), 0, st, d_jobs, d_heads, d_chunks, d_tables,
+                       d_fixed);
   uint32_t *order = nullptr;
   if (sort_units(d_jobs, d_chunks, nchunks, 0, &order, st)) return;
+  if (wave_units == 2 && split_reserve(nchunks) == 0) {
+    uint32_t *counts = g_split.lists + 2 * g_split.cap;
+    uint32_t *lists = g_split.lists;
+    (void)hipMemsetAsync(counts, 0, 2 * sizeof(uint32_t), st);
+    const uint32_t lane_map = zs_lane_resident_waves();
+    const dim3 wgrid((nchunks + WAVE - 1) / WAVE), sgrid(split_grid(nchunks));
+    // the leftover list lives at lists + nchunks: the kernels index it that way
+    if (d64) {
+      hipLaunchKernelGGL(zs_walk_kernel<true>, wgrid, dim3(WAVE), 0, st, d_jobs, d_heads, d_chunks, nchunks, d_tables,
+                         order, pool, lane_map, g_split.walks, g_split.cps, lists, counts);
+      hipLaunchKernelGGL(zs_split_kernel<true>, sgrid, dim3(WAVE), 0, st, d_jobs, d_chunks, nchunks, d_tokens, d_tables,
+                         pool, g_split.walks, g_split.cps, lists, counts);
+      hipLaunchKernelGGL(zs_unitw_list_kernel<true>, sgrid, dim3(WAVE), 0, st, d_jobs, d_heads, d_chunks, d_tokens,
+                         d_tables, d_fixed, lists + nchunks, counts + 1, pool, g_split.walks);
+    } else {
+      hipLaunchKernelGGL(zs_walk_kernel<false>, wgrid, dim3(WAVE), 0, st, d_jobs, d_heads, d_chunks, nchunks, d_tables,
+                         order, pool, lane_map, g_split.walks, g_split.cps, lists, counts);
+      hipLaunchKernelGGL(zs_split_kernel<false>, sgrid, dim3(WAVE), 0, st, d_jobs, d_chunks, nchunks, d_tokens, d_tables,
+                         pool, g_split.walks, g_split.cps, lists, counts);
+      hipLaunchKernelGGL(zs_unitw_list_kernel<false>, sgrid, dim3(WAVE), 0, st, d_jobs, d_heads, d_chunks, d_tokens,
+                         d_tables, d_fixed, lists + nchunks, counts + 1, pool, g_split.walks);
+    }
+    return;
+  }
+  if (wave_units == 2) {  // no room for the split state: the lane parse
+    (void)hipGetLastError();
+    wave_units = 0;
+  }
   if (wave_units) {
     if (d64)
       hipLaunchKernelGGL(zs_unitw_kernel<true>, dim3(nchunks), dim3(WAVE), 0, st, d_jobs, d_heads, d_chunks, nchunks,

@@ -28,6 +28,7 @@
 
 #include "../../include/zstreams_mi355x.h"
 #include "zs_common.h"
+#include "src_hash.h"  // build/src_hash.h (Makefile, srchash.py)
 
 extern "C" void zs_launch_header(const ZsJobDev *d_jobs, ZsHeadDev *d_heads, uint32_t njobs, hipStream_t stream);
 extern "C" void zs_launch_decode(int d64, const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, const uint32_t *d_ids,
@@ -71,7 +72,7 @@ extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_hea
 
 namespace {
 
-constexpr size_t TABLE_ENTRIES_HOST = 1448 + 724 + 176;  // must match TABLE_STRIDE (zs_device.h)
+constexpr size_t TABLE_ENTRIES_HOST = 1448 + 724 + 176 + 160;  // must match TABLE_STRIDE (zs_device.h)
 constexpr size_t FIXED_WORDS_HOST = 544 + 272;      // must match FIXED_WORDS (zs_device.h)
 constexpr uint64_t MAX_RATIO = 1032;  // deflate's largest expansion: 258 bytes per 2 bits
 // deflate64: code 285 carries 16 extra bits for up to 65538 bytes, so one 1-bit
@@ -216,19 +217,28 @@ uint32_t link_segments(uint32_t njobs, uint32_t max_units, uint32_t flags) {
   if (force > 0) return std::min<uint32_t>(LS_SEGS_MAX_HOST, (uint32_t)force);
   return std::min(LS_SEGS_MAX_HOST, std::max(1u, LS_TARGET_WG / njobs));
 }
+// 0 = lane per unit, 1 = wave per unit, 2 = the split parse (round 5: walk +
+// sub-unit decode, the default where the lane parse was; env ZS_SPLIT=0 keeps
+// the lane parse there).
 int wave_units(size_t nseg, uint32_t flags) {
+  if (flags & ZS_F_PARSE_SPLIT) return 2;
   if (flags & ZS_F_PARSE_LANE) return 0;
   if (flags & ZS_F_PARSE_WAVE) return 1;
   static const int force = [] {
     const char *e = std::getenv("ZS_PARSE");
-    return e ? (std::strcmp(e, "wave") == 0 ? 1 : (std::strcmp(e, "lane") == 0 ? 0 : -1)) : -1;
+    if (!e) return -1;
+    return std::strcmp(e, "wave") == 0 ? 1 : (std::strcmp(e, "lane") == 0 ? 0 : (std::strcmp(e, "split") == 0 ? 2 : -1));
   }();
   static const size_t lim = [] {
     const char *e = std::getenv("ZS_WAVE_SEGS");
     return (size_t)(e ? std::atoll(e) : 12288);
   }();
+  static const bool split = [] {
+    const char *e = std::getenv("ZS_SPLIT");
+    return !(e && e[0] == '0');
+  }();
   if (force >= 0) return force;
-  return nseg <= lim ? 1 : 0;
+  return nseg <= lim ? 1 : (split ? 2 : 0);
 }
 bool chunking_enabled() {
   static bool v = [] {
@@ -3038,7 +3048,8 @@ int dstream_end_code(const DStreamState *s) {
 // ===========================================================================
 extern "C" {
 
-const char *zs_version(void) { return "zstreams-mi355x 0.1 (gfx950)"; }
+const char *zs_version(void) { return "zstreams-mi355x 0.5 (gfx950) src " ZS_SRC_HASH; }
+const char *zs_source_hash(void) { return ZS_SRC_HASH; }
 const char *zs_last_error(void) { return g_err.c_str(); }
 
 int zs_set_stream(void *s) {

@@ -69,7 +69,7 @@ _SIGS = {
     "zs_stream_stats_ex": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64)]),
     "zs_stream_persist": (ctypes.c_int, [ctypes.c_int]),
     "zs_synchronize": (ctypes.c_int, []),
-    "zs_version": (ctypes.c_char_p, []), "zs_last_error": (ctypes.c_char_p, []),
+    "zs_version": (ctypes.c_char_p, []), "zs_source_hash": (ctypes.c_char_p, []), "zs_last_error": (ctypes.c_char_p, []),
 }
 
 
@@ -134,7 +134,7 @@ def _check(rc):
         raise ZStreamsError(f"libzstreams_mi355x error {rc}: {lib().zs_last_error().decode()}")
 
 
-PARSE_FLAGS = {None: 0, "lane": 8, "wave": 16}  # ZS_F_PARSE_LANE / ZS_F_PARSE_WAVE
+PARSE_FLAGS = {None: 0, "lane": 8, "wave": 16, "split": 4096}  # ZS_F_PARSE_LANE / _WAVE / _SPLIT
 LINK_FLAGS = {None: 0, "serial": 32}  # ZS_F_LINK_SERIAL
 
 
@@ -397,12 +397,12 @@ def last_stats():
     k = lib().zs_last_stats_ex(a, 11)
     if k < 0:
         _check(k)
-    mode = {0: "lane", 1: "wave"}
+    mode = {0: "lane", 1: "wave", 2: "split"}
     return {"chunked_jobs": a[0], "units": a[1], "fallback_jobs": a[2], "serial_jobs": a[3],
-            "parse": mode.get(a[4]), "link": None if a[4] > 1 else ("serial" if a[5] == 0 else
+            "parse": mode.get(a[4]), "link": None if a[4] > 2 else ("serial" if a[5] == 0 else
                                                                     "segmented" if a[5] & 0x80000000 else "prefix"),
-            "parse_d64": mode.get(a[6]), "link_d64": None if a[6] > 1 else ("serial" if a[7] == 0 else "prefix"),
-            "link_segments": (a[5] & 0x7fffffff) if a[4] <= 1 and a[5] & 0x80000000 else None,
+            "parse_d64": mode.get(a[6]), "link_d64": None if a[6] > 2 else ("serial" if a[7] == 0 else "prefix"),
+            "link_segments": (a[5] & 0x7fffffff) if a[4] <= 2 and a[5] & 0x80000000 else None,
             "lane_resident_waves": a[8], "units_std": a[9], "units_d64": a[10]}
 
 
