@@ -1936,9 +1936,10 @@ extern "C" void zs_launch_stream(int d64, int run_header, ZsStreamDev *const *d_
 // trailer states, the outcome -- so a call returns when ITS workgroup is done,
 // not when the slowest call of a launch is (the batch path: ~2x the mean call
 // at 64 handles).  Wave 0 polls its mailbox with vector loads at system scope
-// (never the scalar cache), sleeping between polls.  Every workgroup leaves
-// when no call was posted to any mailbox for idle_t ticks (s_memrealtime,
-// 100 MHz), when the host sets ctl[0], or after its current call once the
+// (never the scalar cache), sleeping between polls.  A workgroup leaves when
+// no call was posted to any mailbox for idle_t ticks (s_memrealtime, 100 MHz),
+// and then raises ctl[2] so that every other one leaves after its current
+// call; also when the host sets ctl[0], or after its current call once the
 // launch is older than life_t: the grid always drains; the host relaunches on
 // demand.
 // ---------------------------------------------------------------------------
@@ -1974,7 +1975,7 @@ __global__ void __launch_bounds__(WW_T) zs_stream_pk_kernel(ZsMbox *__restrict__
         // posted -- they stay posted for the relaunch -- so every workgroup
         // goes within one call and no handle waits on the others' streams
         const uint64_t now = __builtin_amdgcn_s_memrealtime();
-        if (now - t0 > life_t || pk_ld(ctw) != 0u) break;
+        if (now - t0 > life_t || pk_ld(ctw) != 0u || pk_ld(ctw + 2) != 0u) break;
         const uint32_t q = pk_ld(mbw);
         if (q != done) {
           cmd = q;
@@ -1985,7 +1986,14 @@ __global__ void __launch_bounds__(WW_T) zs_stream_pk_kernel(ZsMbox *__restrict__
           post = p2;
           last = now;
         }
-        if (now - last > idle_t) break;
+        if (now - last > idle_t) {
+          // leaving idle closes the whole launch: the other workgroups leave
+          // after their current call, so a handle whose workgroup is gone
+          // waits for one call at most, never for the launch's life (the host
+          // relaunches once the grid has drained and clears ctl[2])
+          pk_st(const_cast<uint32_t *>(ctw) + 2, 1u);
+          break;
+        }
         for (uint32_t k = 0; k < nap; k++) __builtin_amdgcn_s_sleep(32);
         nap = min(nap * 2u, 8u);
       }

@@ -900,7 +900,8 @@ struct StreamState {
   size_t cap_hin = 0, cap_hout = 0;
   int fresh = 0;  // the device state is set up by the next call (ZsStreamIo::fresh)
   int pk_w = -1;  // the persistent worker's mailbox this handle holds (-1: none)
-  uint64_t pk_last_ns = 0;  // its last call's time on the worker (the next wait sleeps most of it)
+  uint64_t pk_last_ns = 0;  // its last call's time on the worker (the next wait sleeps most of it) ...
+  uint64_t pk_last_in = 0;  // ... and that call's input bytes
 };
 
 constexpr size_t STAGE_MAX = 4u << 20;
@@ -1276,12 +1277,26 @@ int64_t pk_now_ns() {
   return (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// Device buffers of ended streams that the pool did not take: hipFree
+// synchronises the device, which with the persistent worker resident waits for
+// the launch to end (up to ZS_PK_LIFE_MS).  stream_free defers them while a
+// launch runs; they are freed before the next launch (the grid has drained).
+std::vector<void *> g_defer_dev, g_defer_host;
+void pk_defer_flush_locked() {
+  for (void *p : g_defer_dev) (void)hipFree(p);
+  for (void *p : g_defer_host) (void)hipHostFree(p);
+  g_defer_dev.clear();
+  g_defer_host.clear();
+}
+
 int pk_launch_locked() {
   const uint64_t idle_t = (uint64_t)pk_idle_us() * 100u;  // s_memrealtime ticks (100 MHz)
   static const uint64_t life_t = [] {
     const char *e = std::getenv("ZS_PK_LIFE_MS");
     return (uint64_t)(e ? std::atoll(e) : 250) * 100000u;
   }();
+  __atomic_store_n(&g_pk.h_ctl[2], 0u, __ATOMIC_SEQ_CST);  // the last launch's closing flag (it has drained)
+  pk_defer_flush_locked();  // device frees deferred while a launch ran (stream_free)
   zs_launch_stream_pk(g_pk.d_mb, (uint32_t)g_pk.nw, g_pk.d_ctl, idle_t, life_t, g_pk.st);
   HIP_OK(hipGetLastError());
   HIP_OK(hipEventRecord(g_pk.ev, g_pk.st));
@@ -1294,7 +1309,7 @@ int pk_launch_locked() {
 int pk_attach(StreamState *s) {
   if (s->pk_w >= 0) return s->pk_w;
   std::lock_guard<std::mutex> lk(g_pk.mu);
-  if (pk_init_locked() || g_pk.free_w.empty()) return -1;
+  if (pk_init_locked() || g_pk.broken || g_pk.free_w.empty()) return -1;
   s->pk_w = g_pk.free_w.back();
   g_pk.free_w.pop_back();
   return s->pk_w;
@@ -1305,6 +1320,18 @@ void pk_detach(StreamState *s) {  // the handle's calls are all finished
   std::lock_guard<std::mutex> lk(g_pk.mu);
   g_pk.free_w.push_back(s->pk_w);
   s->pk_w = -1;
+}
+
+// A launch that fails after the call was posted: withdraw the call (seq_in
+// back to the last finished one) and stop using the worker, so the mailbox
+// never goes back to the free list with a call outstanding that a later
+// launch would run against another handle's state.
+int pk_fail_locked(ZsMbox *m, int w, int rc) {
+  const uint32_t prev = __atomic_load_n(&m->seq_out, __ATOMIC_ACQUIRE);
+  __atomic_store_n(&m->seq_in, prev, __ATOMIC_SEQ_CST);
+  g_pk.seq[w] = prev;
+  g_pk.broken = true;
+  return rc;
 }
 
 int pk_submit(StreamCall *c, int w) {
@@ -1322,15 +1349,21 @@ int pk_submit(StreamCall *c, int w) {
   if (t0 - g_pk.last_post.exchange(t0) > pk_idle_us() * 500) {
     std::lock_guard<std::mutex> lk(g_pk.mu);
     if (!pk_running_locked())
-      if (int rc = pk_launch_locked()) return rc;
+      if (int rc = pk_launch_locked()) return pk_fail_locked(m, w, rc);
   }
-  // sleep through most of the expected call (the last one's wait), then poll
-  // with short sleeps: many handles' threads spinning would spend the host's
-  // CPU quota (a cgroup-limited server throttles them for whole periods).  The
-  // waiting thread's timer slack drops to 2 us so the sleeps end on time.
-  static thread_local bool slack = [] { return prctl(PR_SET_TIMERSLACK, 2000UL, 0, 0, 0) == 0; }();
-  (void)slack;
-  const int64_t expect = (int64_t)c->s->pk_last_ns;
+  // sleep through most of the expected call, then poll with short sleeps: many
+  // handles' threads spinning would spend the host's CPU quota (a
+  // cgroup-limited server throttles them for whole periods).  The expected
+  // time is the handle's last call on the worker scaled by this call's input
+  // (a trailer or a 1 KiB call after a 4 MiB one finishes in microseconds),
+  // capped at 2 ms.  The waiting thread's timer slack drops to 2 us for the
+  // wait, so the sleeps end on time, and is restored after it.
+  const int prev_slack = prctl(PR_GET_TIMERSLACK, 0, 0, 0, 0);
+  const bool slack = prev_slack >= 0 && prctl(PR_SET_TIMERSLACK, 2000UL, 0, 0, 0) == 0;
+  const uint64_t last_in = std::max<uint64_t>(c->s->pk_last_in, 1);
+  const int64_t expect = (int64_t)std::min<uint64_t>(
+      std::min<uint64_t>(c->s->pk_last_ns * std::max<uint64_t>(c->jb.in_len, 1) / last_in, 4 * c->s->pk_last_ns),
+      2000000u);
   if (expect > 80000) std::this_thread::sleep_for(std::chrono::nanoseconds(expect * 5 / 8));  // calls vary +-30%
   // the launch may have left (its life ended) before it saw the call: look
   // after three expected calls, then every 500 us
@@ -1343,17 +1376,22 @@ int pk_submit(StreamCall *c, int w) {
       std::lock_guard<std::mutex> lk(g_pk.mu);
       if (!pk_running_locked()) {
         if (__atomic_load_n(&m->seq_out, __ATOMIC_ACQUIRE) == seq) break;
-        if (int rc = pk_launch_locked()) return rc;
+        if (int rc = pk_launch_locked()) {
+          if (slack) (void)prctl(PR_SET_TIMERSLACK, (unsigned long)prev_slack, 0, 0, 0);
+          return pk_fail_locked(m, w, rc);
+        }
       }
     }
     std::this_thread::sleep_for(std::chrono::microseconds(now - t0 < 3 * std::max<int64_t>(expect, 100000) ? 6 : 25));
   }
+  if (slack) (void)prctl(PR_SET_TIMERSLACK, (unsigned long)prev_slack, 0, 0, 0);
   const uint64_t waited = (uint64_t)(pk_now_ns() - t0);
   const uint64_t busy = (uint64_t)__atomic_load_n(&m->busy, __ATOMIC_RELAXED) * 10u;
   // the next sleep follows the call's own time on the worker, not the wait: a
   // wait stretched by a relaunch would make every handle sleep long at once,
   // the worker would see no posts, leave idle, and the stretch would feed itself
   c->s->pk_last_ns = busy;
+  c->s->pk_last_in = c->jb.in_len;
   ZsStreamRes r;
   std::memcpy(&r, (const void *)&m->res, sizeof(r));
   c->res = r;
@@ -1459,6 +1497,19 @@ void stream_free(StreamState *s) {
   pk_detach(s);
   if (s->hs) (void)hipStreamSynchronize(s->hs);
   if (res_give(s)) return;
+  {
+    std::lock_guard<std::mutex> lk(g_pk.mu);
+    if (pk_running_locked()) {  // a free now would wait for the worker's launch to end: defer
+      for (void *p : {(void *)s->d_st, (void *)s->d_in, (void *)s->d_out})
+        if (p) g_defer_dev.push_back(p);
+      for (void *p : {(void *)s->h_in, (void *)s->h_out})
+        if (p) g_defer_host.push_back(p);
+      s->d_st = nullptr;
+      s->d_in = s->d_out = s->h_in = s->h_out = nullptr;
+    } else {
+      pk_defer_flush_locked();
+    }
+  }
   if (s->d_st) (void)hipFree(s->d_st);
   if (s->d_in) (void)hipFree(s->d_in);
   if (s->d_out) (void)hipFree(s->d_out);
