@@ -358,3 +358,56 @@ def test_more_handles_than_worker_mailboxes(zs):
     assert not bad, bad[:3]
     assert after["pk_calls"] > before["pk_calls"]  # the worker took calls
     assert after["calls"] > before["calls"]        # and so did batch launches (headers, deflate64, extra handles)
+
+
+def test_persistent_worker_idle_exit_does_not_strand_a_handle(zs):
+    """one handle makes large calls (2 MiB in, ~8 MiB out: ~30 ms on
+    its workgroup) while another pauses longer than the worker's idle time
+    (ZS_PK_IDLE_US, 2 ms) between small calls.  During a large call nobody
+    posts, so the small handle's workgroup leaves idle; its next call must not
+    wait for the launch's whole life (ZS_PK_LIFE_MS, 250 ms) behind the large
+    handle's busy workgroup: leaving idle closes the launch, the busy
+    workgroup leaves after its call, and the waiter relaunches.  Both streams
+    decode exactly; no small call waits 120 ms."""
+    import threading
+    import time
+    L = zs.lib()
+    prev = zs.stream_persist(True)
+    big_raw = corpus.stream(34, 24 << 20)
+    big = _comp(big_raw, -15)
+    small_raw = corpus.stream(35, 1 << 20)
+    small = _comp(small_raw, -15)
+    res, lat = {}, []
+
+    def run(comp, n_in, n_out, nap, key):
+        h = L.inflate_new()
+        assert L.inflate_init_raw(h) == 0
+        ib = ctypes.create_string_buffer(comp, len(comp))
+        off, got = 0, bytearray()
+        while True:
+            if nap:
+                time.sleep(nap)
+            n = min(n_in, len(comp) - off)
+            ob = ctypes.create_string_buffer(n_out)
+            t0 = time.perf_counter()
+            r = L.inflate_process(h, ctypes.addressof(ib) + off, n, ctypes.addressof(ob), n_out, 0)
+            if nap:
+                lat.append(time.perf_counter() - t0)
+            prod, code = r & 0xffffff, (r >> 24) & 0xff
+            got += ob.raw[:prod]
+            off += L.inflate_last_consumed(h)
+            if code != 0:
+                break
+        res[key] = (code, bytes(got))
+        assert L.inflate_end(h) == 0
+
+    try:
+        tb = threading.Thread(target=run, args=(big, 2 << 20, 8 << 20, 0, "big"))
+        tb.start()
+        time.sleep(0.05)
+        run(small, 32768, 65536, 0.003, "small")
+        tb.join()
+    finally:
+        zs.stream_persist(prev)
+    assert res["big"] == (1, big_raw) and res["small"] == (1, small_raw)
+    assert max(lat) < 0.12, sorted(lat)[-5:]
