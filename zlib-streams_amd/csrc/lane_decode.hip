@@ -1849,14 +1849,50 @@ __global__ void __launch_bounds__(64) zs_unitw_list_kernel(const ZsJobDev *__res
 // Reference: src/inffast.c:100-287 (the symbol loop), src/inflate.c:1037-1193.
 // ---------------------------------------------------------------------------
 #define WK_CP 64u    // checkpoint slots per unit slot: <= 64 sub-units, one wave
+#ifndef WK_K0
 #define WK_K0 256u   // tokens per sub-unit to start with (doubled, checkpoints halved, when WK_CP - 1 run out)
+#endif
 #define WK_RING (RING + 1)  // words prefetched for the next walk group
 
+// index bits of the walk's LDS tables: the stored tables' (WK_LBITS / WK_DBITS)
+// or one fewer, folded at load (an entry whose two halves differ becomes
+// WK_EXC: the walk needs only an element's bit count, so two codes that share
+// the shorter index and take the same bits stay on the fast path)
+#ifndef WKL_BITS
+#define WKL_BITS WK_LBITS
+#endif
+#ifndef WKD_BITS
+#define WKD_BITS WK_DBITS
+#endif
+static_assert(WKL_BITS + 1u >= WK_LBITS && WKL_BITS <= WK_LBITS && WKD_BITS + 1u >= WK_DBITS && WKD_BITS <= WK_DBITS,
+              "walk tables fold by one bit at most");
 struct WalkLDS {
-  uint8_t wl[WAVE][1u << WK_LBITS];
-  uint8_t wd[WAVE][1u << WK_DBITS];
+  uint8_t wl[WAVE][1u << WKL_BITS];
+  uint8_t wd[WAVE][1u << WKD_BITS];
   uint32_t ring[RING][WAVE];
 };
+// n16 uint4 of a walk table into LDS, folded by one index bit when fold (the
+// entries of the upper half n16 uint4 further on)
+__device__ __forceinline__ void walk_table_load(uint4 *dst, const uint4 *src, uint32_t n16, bool fold) {
+  for (uint32_t k = 0; k < n16; k++) {
+    uint4 a = src[k];
+    if (fold) {
+      const uint4 b = src[k + n16];
+      uint32_t *aw = reinterpret_cast<uint32_t *>(&a);
+      const uint32_t bw[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const uint32_t d = aw[q] ^ bw[q];
+        uint32_t r = aw[q];
+#pragma unroll
+        for (int y = 0; y < 4; y++)
+          if ((d >> (8 * y)) & 0xffu) r = (r & ~(0xffu << (8 * y))) | (WK_EXC << (8 * y));
+        aw[q] = r;
+      }
+    }
+    dst[k] = a;
+  }
+}
 
 // literal / length code longer than the walk table (or end of block, invalid):
 // the unit's compact tables, as lane_step reads them.  Returns a walk entry;
@@ -1942,12 +1978,9 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
         const uint32_t *tabg = tables + (size_t)c * TABLE_STRIDE;
         cl = reinterpret_cast<const uint16_t *>(tabg + TABLE_ENTRIES);
         const uint4 *wt = reinterpret_cast<const uint4 *>(tabg + TABLE_WALK_OFF);
-        uint4 *wl4 = reinterpret_cast<uint4 *>(L.wl[lane]);
-        uint4 *wd4 = reinterpret_cast<uint4 *>(L.wd[lane]);
-#pragma unroll 8
-        for (uint32_t k = 0; k < (1u << WK_LBITS) / 16u; k++) wl4[k] = wt[k];
-#pragma unroll
-        for (uint32_t k = 0; k < (1u << WK_DBITS) / 16u; k++) wd4[k] = wt[(1u << WK_LBITS) / 16u + k];
+        walk_table_load(reinterpret_cast<uint4 *>(L.wl[lane]), wt, (1u << WKL_BITS) / 16u, WKL_BITS < WK_LBITS);
+        walk_table_load(reinterpret_cast<uint4 *>(L.wd[lane]), wt + (1u << WK_LBITS) / 16u, (1u << WKD_BITS) / 16u,
+                        WKD_BITS < WK_DBITS);
         lane_prime(s, ch.hdr_bit);
         wst = WS_RUN;
       } else {  // stored or undecodable first block: a leftover from the start
@@ -1987,7 +2020,7 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
       while (s.rk + 2 < RING) {
         const uint32_t p0 = lane_pos(s);
         lane_refill_bf(s, rp);
-        uint32_t e = wl[(uint32_t)s.hold & ((1u << WK_LBITS) - 1u)];
+        uint32_t e = wl[(uint32_t)s.hold & ((1u << WKL_BITS) - 1u)];
         if (__builtin_expect(__ballot(e & WK_EXC) != 0, 0)) {
           if (e & WK_EXC) e = walk_slow_len<D64>((uint32_t)s.hold, cl, lbits);
         }
@@ -1997,7 +2030,7 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
         s.hold >>= n;
         s.nbits -= n;
         lane_refill_bf(s, rp);
-        uint32_t d = wd[(uint32_t)s.hold & ((1u << WK_DBITS) - 1u)];
+        uint32_t d = wd[(uint32_t)s.hold & ((1u << WKD_BITS) - 1u)];
         const bool hasd = (e & WK_HASD) != 0;
         if (__builtin_expect(__ballot(hasd && (d & WK_EXC)) != 0, 0)) {
           if (hasd && (d & WK_EXC)) d = walk_slow_dist((uint32_t)s.hold, cd, dbits);
@@ -2134,6 +2167,9 @@ struct __attribute__((aligned(16))) SplitLDS {
   uint32_t ring[RING][WAVE];
 };
 #define SPLIT_IMG_U4 ((LROOT_N * 2 + DROOT_N * 2 + DTAIL_BYTES) / 16)
+#ifndef SPLIT_PRE
+#define SPLIT_PRE 1  // the next group's input words loaded during the flush (0: at the group start)
+#endif
 
 template <bool D64>
 __global__ void __launch_bounds__(64) zs_split_kernel(const ZsJobDev *__restrict__ jobs, ZsChunkDev *__restrict__ chunks,
@@ -2179,8 +2215,11 @@ __global__ void __launch_bounds__(64) zs_split_kernel(const ZsJobDev *__restrict
     const uint32_t t1 = b.y, b1 = b.x;
     if (act) lane_prime(s, a.x);
     __builtin_amdgcn_wave_barrier();
-    s.dta = *reinterpret_cast<const uint4 *>(L.dtail);
-    s.dtb = *reinterpret_cast<const uint4 *>(L.dtail + 4);
+    {  // the distance tail header is the same for every lane: scalar registers
+      const uint4 x = *reinterpret_cast<const uint4 *>(L.dtail), y = *reinterpret_cast<const uint4 *>(L.dtail + 4);
+      s.dta = make_uint4(uni(x.x), uni(x.y), uni(x.z), uni(x.w));
+      s.dtb = make_uint4(uni(y.x), uni(y.y), uni(y.z), uni(y.w));
+    }
     const uint16_t *lt = L.lroot;
     const uint16_t *dt = L.droot;
     uint32_t *tb = &L.tokbuf[0][lane];
@@ -2208,8 +2247,8 @@ __global__ void __launch_bounds__(64) zs_split_kernel(const ZsJobDev *__restrict
       __builtin_amdgcn_wave_barrier();
       // the next group's input words, loaded before this group's tokens leave
       const bool more = run && !bad && !full && s.ntok < t1;
-      pre_wi = more ? s.wi : ~0u;
-      if (more) lane_load_ring(s, pre);
+      pre_wi = (SPLIT_PRE && more) ? s.wi : ~0u;
+      if (SPLIT_PRE && more) lane_load_ring(s, pre);
       const uint32_t g0 = s.ntok - s.gk;
       {  // 16-byte transposed stores of full token quads (zs_lane_kernel's flush)
         typedef uint32_t u32x4a4t __attribute__((ext_vector_type(4), aligned(4)));
@@ -3091,7 +3130,16 @@ extern "C" void zs_launch_parse(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads
     uint32_t *counts = g_split.lists + 2 * g_split.cap;
     uint32_t *lists = g_split.lists;
     (void)hipMemsetAsync(counts, 0, 2 * sizeof(uint32_t), st);
-    const uint32_t lane_map = zs_lane_resident_waves();
+    // the walk deals its sorted units over the waves resident at once, as the lane parse
+    static const uint32_t lane_map = [] {
+      int dev = 0, cus = 0, lds = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+          hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess ||
+          cus <= 0 || lds <= 0)
+        return 0u;
+      return (uint32_t)cus * std::max<uint32_t>(1u, (uint32_t)lds / (uint32_t)sizeof(WalkLDS));
+    }();
     const dim3 wgrid((nchunks + WAVE - 1) / WAVE), sgrid(split_grid(nchunks));
     // the leftover list lives at lists + nchunks: the kernels index it that way
     if (d64) {
