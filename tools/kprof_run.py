@@ -15,9 +15,10 @@ NAMES = {0: "p_waves", 1: "p_cyc_total", 2: "p_cyc_coop", 3: "p_cyc_steps", 4: "
          11: "p_cyc_max", 12: "p_cyc_init", 13: "p_refills", 14: "p_busy_waves", 15: "p_cyc_busy",
          16: "e_blocks", 17: "e_cyc_total", 18: "e_rounds", 19: "e_jump_iters", 20: "e_cyc_jump", 21: "e_batches",
          22: "e_cyc_max", 23: "e_cyc_init", 24: "e_jump_rounds", 25: "e_cyc_pre",
-         40: "s_refill1", 41: "s_lit", 42: "s_refill2", 43: "s_dist", 44: "s_tail",
+         40: "s_refill1", 41: "s_lit", 42: "s_refill2", 43: "s_dist", 44: "s_tail",  # split parse: units, cycles, wave-steps, group cycles
          26: "d_blocks", 27: "d_cyc_total", 28: "d_cyc_hist", 29: "d_cyc_build", 30: "d_cyc_hdr", 31: "d_cyc_emit",
          32: "d_cyc_out", 33: "d_chunks",
+
          48: "l_streams", 49: "l_steps", 50: "l_cyc_succ", 51: "l_cyc_walk", 52: "l_cyc_winwrite", 53: "l_cyc_resolve",
          54: "l_cyc_barrier", 55: "l_markers_sample", 56: "l_cyc_total", 57: "l_cyc_max"}
 

@@ -28,6 +28,8 @@
 
 #include <hipcub/device/device_radix_sort.hpp>
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 
 #if KP_ON
 __device__ unsigned long long g_kprof[KP_COUNT];
@@ -101,12 +103,15 @@ __device__ __forceinline__ uint16_t compact_dist_entry(uint32_t z, uint32_t add_
 // needs no symbol values at all: [4:0] bits, WK_HASD a length (a distance
 // follows), WK_BIG deflate64's code 285 (16 extra bits: a length > 65535 is
 // two tokens), WK_EXC anything the walk resolves off its fast path (end of
-// block, an invalid code, a code longer than the table's index).
+// block, an invalid code, a code longer than the table's index).  A distance
+// entry WK_BAD (WK_EXC | WK_BIG) is an invalid code; a plain WK_EXC distance
+// entry is a code longer than the index (the walk's canonical tail decodes it).
 #define WK_LBITS 9u
-#define WK_DBITS 7u
+#define WK_DBITS 8u
 #define WK_HASD 0x20u
 #define WK_EXC 0x40u
 #define WK_BIG 0x80u
+#define WK_BAD (WK_EXC | WK_BIG)
 template <bool D64>
 __device__ __forceinline__ uint32_t walk_len_entry(uint32_t ce) {  // from a compact literal/length entry
   const uint32_t kind = ce & 3u, bits = (ce >> 2) & 15u, sym = ce >> 6;
@@ -131,11 +136,12 @@ __device__ __forceinline__ uint32_t walk_len_z(const uint32_t *zt, uint32_t lbit
 __device__ __forceinline__ uint32_t walk_dist_z(const uint32_t *zt, uint32_t dbits, uint32_t i) {
   const uint32_t z = zt[i & ((1u << dbits) - 1u)];
   const uint32_t op = e_op(z);
-  if (op & 64u) return WK_EXC;
+  if (op & 64u) return WK_BAD;
   if ((op & 0xf0u) == 0) {  // sub-table: the index's bits past the root pick the entry if the code fits
     const uint32_t avail = WK_DBITS - dbits;
     const uint32_t z2 = zt[e_val(z) + ((i >> dbits) & ((1u << min(op, avail)) - 1u))];
-    if ((e_op(z2) & 64u) || dbits + e_bits(z2) > WK_DBITS) return WK_EXC;
+    if (dbits + e_bits(z2) > WK_DBITS) return WK_EXC;  // longer than the index: the canonical tail
+    if (e_op(z2) & 64u) return WK_BAD;
     return walk_dist_entry(compact_dist_entry(z2, dbits));
   }
   return walk_dist_entry(compact_dist_entry(z));
@@ -1862,13 +1868,14 @@ __global__ void __launch_bounds__(64) zs_unitw_list_kernel(const ZsJobDev *__res
 #define WKL_BITS WK_LBITS
 #endif
 #ifndef WKD_BITS
-#define WKD_BITS WK_DBITS
+#define WKD_BITS (WK_DBITS - 1u)  // 9 / 7 index bits: 768 B per lane, 3 waves per CU
 #endif
 static_assert(WKL_BITS + 1u >= WK_LBITS && WKL_BITS <= WK_LBITS && WKD_BITS + 1u >= WK_DBITS && WKD_BITS <= WK_DBITS,
               "walk tables fold by one bit at most");
 struct WalkLDS {
   uint8_t wl[WAVE][1u << WKL_BITS];
   uint8_t wd[WAVE][1u << WKD_BITS];
+  uint32_t dtail[WAVE][DTAIL_BYTES / 4];  // the block's canonical distance tail (codes past WKD_BITS)
   uint32_t ring[RING][WAVE];
 };
 // n16 uint4 of a walk table into LDS, folded by one index bit when fold (the
@@ -1898,7 +1905,7 @@ __device__ __forceinline__ void walk_table_load(uint4 *dst, const uint4 *src, ui
 // the unit's compact tables, as lane_step reads them.  Returns a walk entry;
 // end of block: 0x100 | WK_EXC | code bits; invalid: WK_EXC alone.
 template <bool D64>
-__device__ __noinline__ uint32_t walk_slow_len(uint32_t h, const uint16_t *cl, uint32_t lbits) {
+__device__ __forceinline__ uint32_t walk_slow_len(uint32_t h, const uint16_t *cl, uint32_t lbits) {
   uint32_t ce = cl[h & ((1u << lbits) - 1u)];
   if ((ce & 3u) == CK_SLOW) {
     const uint32_t op = (ce >> 2) & 15u;
@@ -1909,17 +1916,11 @@ __device__ __noinline__ uint32_t walk_slow_len(uint32_t h, const uint16_t *cl, u
   if ((ce & 3u) == CK_EOB) return 0x100u | WK_EXC | ((ce >> 2) & 15u);
   return walk_len_entry<D64>(ce);
 }
-__device__ __noinline__ uint32_t walk_slow_dist(uint32_t h, const uint16_t *cd, uint32_t dbits) {
-  uint32_t ce = cd[h & ((1u << dbits) - 1u)];
-  if ((ce & 3u) == CK_SLOW) {
-    const uint32_t op = (ce >> 2) & 15u;
-    if (op == 0) return WK_EXC;
-    ce = cd[(ce >> 6) + ((h >> dbits) & ((1u << op) - 1u))];
-  }
-  return walk_dist_entry(ce);
-}
-
-// RING + 1 input words from word wi (masked past the end of the input)
+// RING + 1 raw input words from word wi (indices clamped to the last input
+// word; the bytes past the input are masked when the words enter the ring, so
+// nothing here uses the loaded values and the loads stay in flight through
+// the group: the walk runs at ~1 wave per SIMD, where a wait costs the whole
+// memory latency)
 __device__ __forceinline__ void walk_load(const LaneState &s, uint32_t wi, uint32_t (&v)[WK_RING]) {
   if (wi + WK_RING <= s.lastw) {
     const uint32_t *src = (const uint32_t *)(s.w + wi);
@@ -1935,11 +1936,22 @@ __device__ __forceinline__ void walk_load(const LaneState &s, uint32_t wi, uint3
     v[RING] = src[RING];
   } else {
 #pragma unroll
-    for (int q = 0; q < WK_RING; q++) v[q] = in_word_g(s.w, wi + q, s.end_byte);
+    for (int q = 0; q < WK_RING; q++) v[q] = s.w[min(wi + (uint32_t)q, s.lastw)];
   }
+}
+// word wi as read raw, with the bytes at or past the input's end zeroed
+__device__ __forceinline__ uint32_t walk_mask(uint32_t v, uint32_t wi, uint32_t end_byte) {
+  const uint32_t b = wi * 4u;
+  const uint32_t keep = b >= end_byte ? 0u : end_byte - b;
+  return keep >= 4u ? v : __builtin_amdgcn_ubfe(v, 0, 8u * keep);
 }
 
 enum { WS_RUN = 0, WS_EOB = 1, WS_BAD = 2, WS_IDLE = 3 };
+
+// keep checkpoints 1, 3, 5, ... (the walk's stride doubles; rare)
+__device__ __forceinline__ void walk_halve(uint2 *cp) {
+  for (uint32_t i = 0; i < (WK_CP - 1u) / 2u; i++) cp[i] = cp[2u * i + 1u];
+}
 
 template <bool D64>
 __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict__ jobs, const ZsHeadDev *__restrict__ heads,
@@ -1960,7 +1972,7 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
   s.end_byte = s.limit = 0;
   s.wi = s.nw = s.nkeep = s.nbits = s.lastw = s.rk = 0;
   s.hold = 0;
-  uint32_t wst = WS_IDLE, code = 0, lbits = 9, dbits = 6, tcap = 0;
+  uint32_t wst = WS_IDLE, code = 0, lbits = 9, tcap = 0;
   const uint16_t *cl = nullptr;
   if (c < nchunks) {
     const ZsChunkDev ch = chunks[c];
@@ -1974,13 +1986,15 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
         s.limit = s.end_byte * 8u;
         tcap = ch.tcap;
         lbits = (ch.hdr_info >> 8) & 15u;
-        dbits = (ch.hdr_info >> 12) & 15u;
         const uint32_t *tabg = tables + (size_t)c * TABLE_STRIDE;
         cl = reinterpret_cast<const uint16_t *>(tabg + TABLE_ENTRIES);
         const uint4 *wt = reinterpret_cast<const uint4 *>(tabg + TABLE_WALK_OFF);
         walk_table_load(reinterpret_cast<uint4 *>(L.wl[lane]), wt, (1u << WKL_BITS) / 16u, WKL_BITS < WK_LBITS);
         walk_table_load(reinterpret_cast<uint4 *>(L.wd[lane]), wt + (1u << WK_LBITS) / 16u, (1u << WKD_BITS) / 16u,
                         WKD_BITS < WK_DBITS);
+        const uint4 *img = reinterpret_cast<const uint4 *>(tabg + TABLE_IMG_OFF) + (LROOT_N + DROOT_N) * 2 / 16;
+#pragma unroll
+        for (uint32_t k = 0; k < DTAIL_BYTES / 16; k++) reinterpret_cast<uint4 *>(L.dtail[lane])[k] = img[k];
         lane_prime(s, ch.hdr_bit);
         wst = WS_RUN;
       } else {  // stored or undecodable first block: a leftover from the start
@@ -1994,9 +2008,14 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
   const uint8_t *wl = L.wl[lane];
   const uint8_t *wd = L.wd[lane];
   uint32_t *rp = &L.ring[0][lane];
-  const uint16_t *cd = cl ? cl + DIST_TABLE_OFF : nullptr;
+  const uint32_t *dtl = L.dtail[lane];
   uint2 *cp = cps + (size_t)(c < nchunks ? c : 0u) * WK_CP;
   uint32_t ntok = 0, K = WK_K0, ncp = 0, ncut = WK_K0, eob = 0, endb = 0;
+#if KP_ON
+  const uint64_t kp_t0 = KP_NOW();
+  uint64_t kp_cyc_l = 0, kp_cyc_d = 0;
+  uint32_t kp_groups = 0, kp_wsteps = 0, kp_slow_l = 0, kp_slow_d = 0;
+#endif
   uint32_t pre[WK_RING];
   uint32_t pre_wi = ~0u;
   for (;;) {
@@ -2006,9 +2025,14 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
       // the last group when it ended where expected), then the next group's words
       if (s.wi == pre_wi || s.wi == pre_wi + 1u) {
         const bool sh = s.wi != pre_wi;
+        uint32_t w0 = 0;
 #pragma unroll
-        for (int q = 0; q < RING; q++) rp[q * WAVE] = sh ? pre[q + 1] : pre[q];
-        s.nw = sh ? pre[1] : pre[0];
+        for (int q = 0; q < RING; q++) {
+          const uint32_t v = walk_mask(sh ? pre[q + 1] : pre[q], s.wi + (uint32_t)q, s.end_byte);
+          rp[q * WAVE] = v;
+          if (q == 0) w0 = v;
+        }
+        s.nw = w0;
         s.rk = 0;
       } else {
         lane_fill_ring(s, rp);
@@ -2017,12 +2041,27 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
       // word wi + RING - 2 or one later
       pre_wi = s.wi + RING - 2u;
       walk_load(s, pre_wi, pre);
+      s.dta = *reinterpret_cast<const uint4 *>(dtl);  // the distance tail's header, in registers for the group
+      s.dtb = *reinterpret_cast<const uint4 *>(dtl + 4);
+#if KP_ON
+      kp_groups++;
+#endif
       while (s.rk + 2 < RING) {
+#if KP_ON
+        kp_wsteps += lane_id() == (uint32_t)__builtin_ctzll(__ballot(1)) ? 1u : 0u;
+#endif
         const uint32_t p0 = lane_pos(s);
         lane_refill_bf(s, rp);
         uint32_t e = wl[(uint32_t)s.hold & ((1u << WKL_BITS) - 1u)];
         if (__builtin_expect(__ballot(e & WK_EXC) != 0, 0)) {
+#if KP_ON
+          const uint64_t kq = KP_NOW();
+          kp_slow_l += lane_id() == (uint32_t)__builtin_ctzll(__ballot(1)) ? 1u : 0u;
+#endif
           if (e & WK_EXC) e = walk_slow_len<D64>((uint32_t)s.hold, cl, lbits);
+#if KP_ON
+          kp_cyc_l += KP_NOW() - kq;
+#endif
         }
         const uint32_t n = e & 31u;
         uint32_t two = 0;
@@ -2032,8 +2071,19 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
         lane_refill_bf(s, rp);
         uint32_t d = wd[(uint32_t)s.hold & ((1u << WKD_BITS) - 1u)];
         const bool hasd = (e & WK_HASD) != 0;
-        if (__builtin_expect(__ballot(hasd && (d & WK_EXC)) != 0, 0)) {
-          if (hasd && (d & WK_EXC)) d = walk_slow_dist((uint32_t)s.hold, cd, dbits);
+        if (__builtin_expect(__ballot(hasd && d == WK_EXC) != 0, 0)) {
+#if KP_ON
+          const uint64_t kq = KP_NOW();
+          kp_slow_d += lane_id() == (uint32_t)__builtin_ctzll(__ballot(1)) ? 1u : 0u;
+#endif
+          // a distance code longer than the table's index: canonical decode from
+          // the lane's tail (header in registers, one LDS read for the symbol)
+          const uint32_t de = dist_tail_r(s.dta, s.dtb, dtl, (uint32_t)s.hold);
+          const uint32_t dsym = (de >> 6) & 31u;
+          if (hasd && d == WK_EXC) d = (!D64 && dsym >= 30u) ? WK_BAD : walk_dist_entry(de);
+#if KP_ON
+          kp_cyc_d += KP_NOW() - kq;
+#endif
         }
         const uint32_t dn = hasd ? (d & 31u) : 0u;
         s.hold >>= dn;
@@ -2057,7 +2107,7 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
           ncp++;
           ncut += K;
           if (ncp == WK_CP - 1u) {  // out of slots: keep every second checkpoint, twice the stride
-            for (uint32_t i = 0; i < (WK_CP - 1u) / 2u; i++) cp[i] = cp[2u * i + 1u];
+            walk_halve(cp);
             ncp = (WK_CP - 1u) / 2u;
             K *= 2u;
             ncut = (ncp + 1u) * K;
@@ -2067,6 +2117,22 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
     }
     __builtin_amdgcn_wave_barrier();  // the ring is rewritten by the next group
   }
+#if KP_ON
+  {  // walk counters in the lane parse's slots (the split parse runs no lane parse)
+    const uint64_t tot = KP_NOW() - kp_t0;
+    KP_ADD(KP_P_WAVES, 1);
+    KP_ADD(KP_P_CYC_TOTAL, tot);
+    KP_MAX(KP_P_CYC_MAX, tot);
+    KP_ADD(KP_P_GROUPS, kp_groups);
+    KP_ADD(KP_P_WAVE_STEPS, kp_wave_sum(kp_wsteps));
+    KP_ADD(KP_P_SLOW_LIT, kp_wave_sum(kp_slow_l));
+    KP_ADD(KP_P_SLOW_DIST, kp_wave_sum(kp_slow_d));
+    KP_ADD(KP_P_CYC_COOP, kp_cyc_l);
+    KP_ADD(KP_P_CYC_FLUSH, kp_cyc_d);
+    KP_ADD(KP_P_LANE_STEPS, kp_wave_sum(ntok));
+    if (kp_groups) KP_ADD(KP_P_BUSY, 1);
+  }
+#endif
   if (wst == WS_EOB && !tok_ensure(pool, c, tcap, ntok)) {
     wst = WS_BAD;
     code = ZD_FULL;
@@ -2159,14 +2225,98 @@ __device__ __forceinline__ void split_step(LaneState &s, const uint16_t *__restr
   s.pos += len;
 }
 
+// Wide tables of the split decode (one copy per wave, so LDS is cheap): u32
+// entries that carry everything a symbol needs -- code bits, extra-bit count
+// and the literal or the length / distance base -- so a step does no base
+// arithmetic; a code longer than the index takes a wave-uniform side branch.
+//   literal / length, 9-bit index: [3:0] code bits, [5:4] kind (SK_*),
+//     [10:6] extra bits, [31:16] literal byte or length base
+//   distance, 8-bit index: [3:0] code bits, [4] long code (canonical tail),
+//     [5] invalid code, [10:6] extra bits, [31:16] distance base
+#define SPL_BITS 9u
+#define SPD_BITS 8u
+enum { SK_LIT = 0, SK_LEN = 1, SK_EOB = 2, SK_SLOW = 3 };
+template <bool D64>
+__device__ __forceinline__ uint32_t split_len_entry(uint32_t ce) {  // from a compact literal/length entry
+  const uint32_t kind = ce & 3u, bits = (ce >> 2) & 15u, sym = ce >> 6;
+  if (kind == CK_SYM) return bits | (SK_LIT << 4) | (sym << 16);
+  if (kind == CK_EOB) return bits | (SK_EOB << 4);
+  if (kind != CK_LEN) return SK_SLOW << 4;
+  // length code sym (0..28), src/inftrees.c:59-64 (deflate64 285: 3 + 16 extra bits)
+  uint32_t xb = sym < 8u ? 0u : (sym < 28u ? (sym >> 2) - 1u : (D64 ? 16u : 0u));
+  uint32_t base = sym < 8u ? sym + 3u : (sym < 28u ? ((4u + (sym & 3u)) << xb) + 3u : (D64 ? 3u : 258u));
+  return bits | (SK_LEN << 4) | (xb << 6) | (base << 16);
+}
+__device__ __forceinline__ uint32_t split_dist_entry(uint32_t ce, bool d64) {  // from a compact distance entry
+  if ((ce & 3u) != CK_SYM) return 0x20u;
+  const uint32_t bits = (ce >> 2) & 15u, dsym = (ce >> 6) & 31u;
+  if (!d64 && dsym >= 30u) return 0x20u;
+  const uint32_t dx = dsym < 4u ? 0u : (dsym >> 1) - 1u;
+  const uint32_t base = dsym < 4u ? dsym + 1u : ((2u + (dsym & 1u)) << dx) + 1u;  // src/inftrees.c:65-72
+  return bits | (dx << 6) | (base << 16);
+}
+
 struct __attribute__((aligned(16))) SplitLDS {
   uint16_t lroot[LROOT_N];  // the block's table image (zs_unit_header_kernel), shared by the wave
   uint16_t droot[DROOT_N];
   uint32_t dtail[DTAIL_BYTES / 4];
+  uint32_t lw[1u << SPL_BITS];  // the wide tables (SPLIT_WIDE)
+  uint32_t dw[1u << SPD_BITS];
   uint32_t tokbuf[GROUP][WAVE];
   uint32_t ring[RING][WAVE];
 };
 #define SPLIT_IMG_U4 ((LROOT_N * 2 + DROOT_N * 2 + DTAIL_BYTES) / 16)
+#ifndef SPLIT_WIDE
+#define SPLIT_WIDE 1  // the wide tables (0: lane_step_fast's compact 8 / 6-bit roots)
+#endif
+
+// the split step on the wide tables
+template <bool D64>
+__device__ __forceinline__ void split_step_w(LaneState &s, const uint32_t *__restrict__ lw, const uint32_t *__restrict__ dw,
+                                             uint32_t *__restrict__ tb, const uint32_t *__restrict__ dtl,
+                                             const uint32_t *__restrict__ rp, uint32_t &bad, uint32_t &need) {
+  lane_refill_bf(s, rp);
+  uint32_t e = lw[(uint32_t)s.hold & ((1u << SPL_BITS) - 1u)];
+  if (__builtin_expect(__ballot(((e >> 4) & 3u) == SK_SLOW) != 0, 0)) {
+    if (((e >> 4) & 3u) == SK_SLOW) {  // longer than 9 bits: zlib's 9-bit root and sub-table (compact, global)
+      uint32_t e2 = s.cl[(uint32_t)s.hold & ((1u << s.lbits) - 1u)];
+      const uint32_t op2 = (e2 >> 2) & 15u;
+      if ((e2 & 3u) == CK_SLOW && op2) e2 = s.cl[(e2 >> 6) + (((uint32_t)s.hold >> s.lbits) & ((1u << op2) - 1u))];
+      e = split_len_entry<D64>(e2);
+    }
+  }
+  const uint32_t cb = e & 15u, kind = (e >> 4) & 3u, xb = (e >> 6) & 31u;
+  const uint32_t isl = kind == SK_LEN;
+  s.hold >>= cb;
+  const uint32_t len = isl ? (e >> 16) + ((uint32_t)s.hold & ((1u << xb) - 1u)) : 1u;
+  s.hold >>= xb;
+  s.nbits -= cb + xb;
+  lane_refill_bf(s, rp);
+  uint32_t d = dw[(uint32_t)s.hold & ((1u << SPD_BITS) - 1u)];
+  if (__builtin_expect(__ballot(isl && (d & 0x10u)) != 0, 0)) {
+    // a distance code longer than 8 bits: canonical decode from the tail
+    const uint32_t de = dist_tail_r(s.dta, s.dtb, dtl, (uint32_t)s.hold);
+    if (isl && (d & 0x10u)) d = split_dist_entry(de, D64);
+  }
+  const uint32_t dcb = d & 15u, dx = (d >> 6) & 31u;
+  const uint32_t dist = (d >> 16) + ((uint32_t)(s.hold >> dcb) & ((1u << dx) - 1u));
+  const uint32_t dcons = isl ? dcb + dx : 0u;
+  s.hold >>= dcons;
+  s.nbits -= dcons;
+  bad |= (uint32_t)(kind >= SK_EOB) | (isl & (uint32_t)((d & 0x30u) != 0));
+  need = max(need, (isl && dist > s.pos) ? dist - s.pos : 0u);
+  if (D64 && len > 0xffffu) {  // a deflate64 copy longer than a token holds: two copies, same distance
+    tb[s.gk * WAVE] = (0xffffu << 16) | (dist - 1u);
+    s.gk++;
+    s.ntok++;
+    tb[s.gk * WAVE] = ((len - 0xffffu) << 16) | (dist - 1u);
+  } else {
+    tb[s.gk * WAVE] = isl ? ((len << 16) | (dist - 1u)) : (e >> 16);
+  }
+  s.gk++;
+  s.ntok++;
+  s.pos += len;
+}
 #ifndef SPLIT_PRE
 #define SPLIT_PRE 1  // the next group's input words loaded during the flush (0: at the group start)
 #endif
@@ -2181,15 +2331,47 @@ __global__ void __launch_bounds__(64) zs_split_kernel(const ZsJobDev *__restrict
   const uint32_t lane = threadIdx.x;
   const uint32_t nsplit = counts[0];
   constexpr uint32_t HMAX = D64 ? 65536u : HIST;
+#if KP_ON
+  const uint64_t kp_t0 = KP_NOW();
+  uint64_t kp_grp = 0;
+  uint32_t kp_units = 0, kp_ws = 0;
+#endif
   for (uint32_t k = blockIdx.x; k < nsplit; k += gridDim.x) {
     const uint32_t c = lists[k];
     const ZsWalkDev wk = walks[c];
+#if KP_ON
+    kp_units++;
+#endif
     const ZsChunkDev ch = chunks[c];
     const ZsJobDev jb = jobs[ch.job];
     const uint32_t *tabg = tables + (size_t)c * TABLE_STRIDE;
     __builtin_amdgcn_wave_barrier();  // the previous unit is done with the image
     if (lane < SPLIT_IMG_U4)
       reinterpret_cast<uint4 *>(&L)[lane] = reinterpret_cast<const uint4 *>(tabg + TABLE_IMG_OFF)[lane];
+    if (SPLIT_WIDE) {  // the wide tables, from the unit's compact tables (zlib layout, roots lbits / dbits)
+      const uint16_t *ccl = reinterpret_cast<const uint16_t *>(tabg + TABLE_ENTRIES), *ccd = ccl + DIST_TABLE_OFF;
+      const uint32_t lb = (ch.hdr_info >> 8) & 15u, db = (ch.hdr_info >> 12) & 15u;
+#pragma unroll
+      for (uint32_t q = 0; q < (1u << SPL_BITS) / WAVE; q++) {
+        const uint32_t i = q * WAVE + lane;
+        const uint32_t ce = ccl[i & ((1u << lb) - 1u)];
+        L.lw[i] = ((ce & 3u) == CK_SLOW) ? (SK_SLOW << 4) : split_len_entry<D64>(ce);
+      }
+#pragma unroll
+      for (uint32_t q = 0; q < (1u << SPD_BITS) / WAVE; q++) {
+        const uint32_t i = q * WAVE + lane;
+        uint32_t ce = ccd[i & ((1u << db) - 1u)];
+        uint32_t v;
+        if ((ce & 3u) == CK_SLOW && ((ce >> 2) & 15u)) {  // sub-table: the index's bits past the root pick it if it fits
+          const uint32_t op = (ce >> 2) & 15u, avail = SPD_BITS - db;
+          ce = ccd[(ce >> 6) + ((i >> db) & ((1u << min(op, avail)) - 1u))];
+          v = ((ce >> 2) & 15u) > SPD_BITS ? 0x10u : split_dist_entry(ce, D64);
+        } else {
+          v = split_dist_entry(ce, D64);
+        }
+        L.dw[i] = v;
+      }
+    }
     const bool act = lane < wk.nsub;
     const uint2 *cpu = cps + (size_t)c * WK_CP;
     const uint2 a0 = cpu[lane ? lane - 1u : 0u];
@@ -2231,11 +2413,24 @@ __global__ void __launch_bounds__(64) zs_split_kernel(const ZsJobDev *__restrict
       const bool run = act && !bad && !full && s.ntok < t1;
       if (__ballot(run) == 0) break;
       s.gk = 0;
+#if KP_ON
+      const uint64_t kg0 = KP_NOW();
+#endif
       if (run) {
         if (s.wi == pre_wi) lane_store_ring(s, rp, pre);
         else lane_fill_ring(s, rp);
+#if KP_ON
+        __builtin_amdgcn_s_waitcnt(0);
+        kp_grp += KP_NOW() - kg0;
+#endif
         while (!bad && !full && s.ntok < t1 && s.gk + (D64 ? 2u : 1u) <= GROUP && s.rk + 2 < RING) {
-          split_step<D64>(s, lt, dt, tb, L.dtail, rp, bad, need);
+#if KP_ON
+          kp_ws += lane_id() == (uint32_t)__builtin_ctzll(__ballot(1)) ? 1u : 0u;
+#endif
+          if (SPLIT_WIDE)
+            split_step_w<D64>(s, L.lw, L.dw, tb, L.dtail, rp, bad, need);
+          else
+            split_step<D64>(s, lt, dt, tb, L.dtail, rp, bad, need);
           full |= s.pos > s.capx;
         }
         if (s.ntok > t1) {  // an inconsistent decode: never write past the walked tokens
@@ -2245,6 +2440,9 @@ __global__ void __launch_bounds__(64) zs_split_kernel(const ZsJobDev *__restrict
         }
       }
       __builtin_amdgcn_wave_barrier();
+#if KP_ON
+      const uint64_t kf0 = KP_NOW();
+#endif
       // the next group's input words, loaded before this group's tokens leave
       const bool more = run && !bad && !full && s.ntok < t1;
       pre_wi = (SPLIT_PRE && more) ? s.wi : ~0u;
@@ -2281,6 +2479,9 @@ __global__ void __launch_bounds__(64) zs_split_kernel(const ZsJobDev *__restrict
         for (uint32_t j = 0; j < s.gk; j++) *tok_addr(pool, tokens, s.unit, prim_off, s.tcap, g0 + j) = L.tokbuf[j][lane];
       }
       __builtin_amdgcn_wave_barrier();  // tokbuf is rewritten by the next group
+#if KP_ON
+      kp_grp += KP_NOW() - kf0;
+#endif
     }
     if (act && !full && (lane_pos(s) != b1 || s.ntok != t1)) bad = 1;
     const bool anybad = __ballot(bad) != 0, anyfull = __ballot(full) != 0;
@@ -2339,6 +2540,14 @@ __global__ void __launch_bounds__(64) zs_split_kernel(const ZsJobDev *__restrict
       }
     }
   }
+#if KP_ON
+  // split counters in the lane parse's step-phase slots (no lane parse runs):
+  // 40 units, 41 cycles, 42 wave-steps, 43 group fill + flush cycles
+  KP_ADD(40, kp_units);
+  KP_ADD(41, KP_NOW() - kp_t0);
+  KP_ADD(42, kp_wave_sum(kp_ws));
+  KP_ADD(43, kp_grp);
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -3156,6 +3365,12 @@ extern "C" void zs_launch_parse(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads
                          pool, g_split.walks, g_split.cps, lists, counts);
       hipLaunchKernelGGL(zs_unitw_list_kernel<false>, sgrid, dim3(WAVE), 0, st, d_jobs, d_heads, d_chunks, d_tokens,
                          d_tables, d_fixed, lists + nchunks, counts + 1, pool, g_split.walks);
+    }
+    static const bool dbg = getenv("ZS_SPLIT_STATS") != nullptr;
+    if (dbg) {  // (diagnostics) walked units and leftovers of this batch, on stderr
+      uint32_t h[2] = {0, 0};
+      if (hipMemcpyAsync(h, counts, sizeof h, hipMemcpyDeviceToHost, st) == hipSuccess && hipStreamSynchronize(st) == hipSuccess)
+        fprintf(stderr, "split: %u unit slots, %u walked, %u leftovers\n", nchunks, h[0], h[1]);
     }
     return;
   }

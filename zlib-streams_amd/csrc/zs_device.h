@@ -7,10 +7,10 @@
 #define TABLE_ENTRIES 1448   // ENOUGH (852 + 594), src/inftrees.h:52-55
 // per unit slot: zlib-layout tables, their compact u16 copy, the LDS image
 // (256 + 64 u16 roots, 64 B dist tail) and the split parse's walk tables
-// (512 + 128 u8 entries, lane_decode.hip zs_walk_kernel)
+// (512 + 256 u8 entries, lane_decode.hip zs_walk_kernel)
 #define TABLE_IMG_OFF (TABLE_ENTRIES + TABLE_ENTRIES / 2)
 #define TABLE_WALK_OFF (TABLE_IMG_OFF + 176)
-#define TABLE_STRIDE (TABLE_WALK_OFF + 160)
+#define TABLE_STRIDE (TABLE_WALK_OFF + 192)
 #define FIXED_ZLIB_WORDS 544                              // fixed tables: 512 lit/len + 32 dist (zlib layout)
 #define FIXED_WORDS (FIXED_ZLIB_WORDS + FIXED_ZLIB_WORDS / 2)  // + compact u16 copy
 #define DIST_TABLE_OFF 852   // distance table follows the literal/length table
