@@ -15,7 +15,8 @@ NAMES = {0: "p_waves", 1: "p_cyc_total", 2: "p_cyc_coop", 3: "p_cyc_steps", 4: "
          11: "p_cyc_max", 12: "p_cyc_init", 13: "p_refills", 14: "p_busy_waves", 15: "p_cyc_busy",
          16: "e_blocks", 17: "e_cyc_total", 18: "e_rounds", 19: "e_jump_iters", 20: "e_cyc_jump", 21: "e_batches",
          22: "e_cyc_max", 23: "e_cyc_init", 24: "e_jump_rounds", 25: "e_cyc_pre",
-         40: "s_refill1", 41: "s_lit", 42: "s_refill2", 43: "s_dist", 44: "s_tail",  # split parse: units, cycles, wave-steps, group cycles
+         44: "w_cyc_total", 45: "w_cyc_max", 46: "w_wave_steps", 47: "w_cyc_exc", 38: "w_cyc_group", 39: "w_exc",
+         40: "s_refill1", 41: "s_lit", 42: "s_refill2", 43: "s_dist",  # split parse: units, cycles, wave-steps, group cycles
          26: "d_blocks", 27: "d_cyc_total", 28: "d_cyc_hist", 29: "d_cyc_build", 30: "d_cyc_hdr", 31: "d_cyc_emit",
          32: "d_cyc_out", 33: "d_chunks",
 
@@ -84,7 +85,14 @@ def main():
                                            ("d_cyc_total", "d_cyc_hist", "d_cyc_build", "d_cyc_hdr", "d_cyc_emit",
                                             "d_cyc_out", "d_chunks")},
         "step_phase_cycles_per_wave_step": {k: d[k] / max(d["p_wave_steps"], 1)
-                                            for k in ("s_refill1", "s_lit", "s_refill2", "s_dist", "s_tail")},
+                                            for k in ("s_refill1", "s_lit", "s_refill2", "s_dist")},
+        # split parse (zs_walk_kernel / zs_split_kernel): cycles per wave-step
+        "walk_cycles_per_step": d.get("w_cyc_total", 0) / max(d.get("w_wave_steps", 0), 1),
+        "walk_max_wave_ms_at_2p4ghz": d.get("w_cyc_max", 0) / 2.4e6,
+        "walk_exc_cycles_per_step": d.get("w_cyc_exc", 0) / max(d.get("w_wave_steps", 0), 1),
+        "walk_group_cycles_per_step": d.get("w_cyc_group", 0) / max(d.get("w_wave_steps", 0), 1),
+        "walk_exc_per_step": d.get("w_exc", 0) / max(d.get("w_wave_steps", 0), 1),
+        "split_cycles_per_wave_step": d.get("s_lit", 0) / max(d.get("s_refill2", 0), 1),
     }
     out = {"raw": d, "derived": derived}
     print(json.dumps(out, indent=1))

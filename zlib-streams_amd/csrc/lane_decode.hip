@@ -33,14 +33,17 @@
 
 #if KP_ON
 __device__ unsigned long long g_kprof[KP_COUNT];
-// wave-uniform value, added once per wave
-#define KP_ADD(i, v)                                                       \
-  do {                                                                     \
-    if (lane_id() == 0) atomicAdd(&g_kprof[i], (unsigned long long)(v));  \
+// wave-uniform value, added once per wave (v is evaluated by every lane, so
+// that a kp_wave_sum inside it sees the whole wave)
+#define KP_ADD(i, v)                                              \
+  do {                                                            \
+    const unsigned long long kp_v_ = (unsigned long long)(v);     \
+    if (lane_id() == 0) atomicAdd(&g_kprof[i], kp_v_);            \
   } while (0)
-#define KP_MAX(i, v)                                                       \
-  do {                                                                     \
-    if (lane_id() == 0) atomicMax(&g_kprof[i], (unsigned long long)(v));  \
+#define KP_MAX(i, v)                                              \
+  do {                                                            \
+    const unsigned long long kp_v_ = (unsigned long long)(v);     \
+    if (lane_id() == 0) atomicMax(&g_kprof[i], kp_v_);            \
   } while (0)
 __device__ __forceinline__ uint32_t kp_wave_sum(uint32_t v) {
   for (int o = 32; o; o >>= 1) v += __shfl_xor(v, o);
@@ -1858,8 +1861,6 @@ __global__ void __launch_bounds__(64) zs_unitw_list_kernel(const ZsJobDev *__res
 #ifndef WK_K0
 #define WK_K0 256u   // tokens per sub-unit to start with (doubled, checkpoints halved, when WK_CP - 1 run out)
 #endif
-#define WK_RING (RING + 1)  // words prefetched for the next walk group
-
 // index bits of the walk's LDS tables: the stored tables' (WK_LBITS / WK_DBITS)
 // or one fewer, folded at load (an entry whose two halves differ becomes
 // WK_EXC: the walk needs only an element's bit count, so two codes that share
@@ -1868,24 +1869,47 @@ __global__ void __launch_bounds__(64) zs_unitw_list_kernel(const ZsJobDev *__res
 #define WKL_BITS WK_LBITS
 #endif
 #ifndef WKD_BITS
-#define WKD_BITS (WK_DBITS - 1u)  // 9 / 7 index bits: 768 B per lane, 3 waves per CU
+#define WKD_BITS (WK_DBITS - 1u)  // 9 / 7 index bits
 #endif
 static_assert(WKL_BITS + 1u >= WK_LBITS && WKL_BITS <= WK_LBITS && WKD_BITS + 1u >= WK_DBITS && WKD_BITS <= WK_DBITS,
               "walk tables fold by one bit at most");
+#define WK_GS(d64) ((d64) ? 7u : 9u)  // steps per group: <= 60 (48) bits each, so a group reads words p / 32 .. p / 32 + 16
+#define WK_PF 16u   // words per prefetch: the ring is two such halves
+#define WK_RW 32u   // input ring words per lane
+#define WK_RS 35u   // a lane's ring row: WK_RW words, words 0 and 1 again (a 3-word read never wraps), odd stride
+#define WK_DT0 6u   // the distance tail's words from here on live in LDS (its symbols: bytes 27 ..)
+#define WK_DTN 9u
+// The tables are lane-interleaved (dword k of lane L at [k][L]): whatever
+// entries the 64 lanes look up, lane L always hits bank L mod 32, so a wave's
+// table read is conflict-free (own tables at a 512-byte stride put every
+// lane's entry i on the same bank: 6 extra LDS cycles per read).  The ring is
+// one row per lane at an odd stride, so that a half (16 consecutive words) is
+// written with 8 two-word stores and the lanes' rows spread over the banks.
 struct WalkLDS {
-  uint8_t wl[WAVE][1u << WKL_BITS];
-  uint8_t wd[WAVE][1u << WKD_BITS];
-  uint32_t dtail[WAVE][DTAIL_BYTES / 4];  // the block's canonical distance tail (codes past WKD_BITS)
-  uint32_t ring[RING][WAVE];
+  uint32_t wl[(1u << WKL_BITS) / 4][WAVE];
+  uint32_t wd[(1u << WKD_BITS) / 4][WAVE];
+  uint32_t dtail[WK_DTN][WAVE];  // words WK_DT0 .. of the block's canonical distance tail (codes past WKD_BITS)
+  uint32_t ring[WAVE][WK_RS];
 };
-// n16 uint4 of a walk table into LDS, folded by one index bit when fold (the
-// entries of the upper half n16 uint4 further on)
-__device__ __forceinline__ void walk_table_load(uint4 *dst, const uint4 *src, uint32_t n16, bool fold) {
+// byte i of a lane's interleaved u8 table (base = &table[0][lane])
+__device__ __forceinline__ uint32_t wk_byte(const uint32_t *base, uint32_t i) {
+  return reinterpret_cast<const uint8_t *>(base)[((i >> 2) * WAVE) * 4u + (i & 3u)];
+}
+// the same from the table's LDS address as an integer (lane column included):
+// the byte address in two independent ops and one combine
+__device__ __forceinline__ uint32_t wk_byte_a(uint32_t base, uint32_t i, uint32_t nbits) {
+  typedef __attribute__((address_space(3))) const uint8_t lds_cu8;
+  const uint32_t a = ((i & ((1u << nbits) - 4u)) << 6) | ((i & 3u) | base);
+  return *(lds_cu8 *)(uintptr_t)a;
+}
+// n16 uint4 of a walk table into the lane's interleaved LDS table, folded by
+// one index bit when fold (the entries of the upper half n16 uint4 further on)
+__device__ __forceinline__ void walk_table_load(uint32_t *dst, const uint4 *src, uint32_t n16, bool fold) {
   for (uint32_t k = 0; k < n16; k++) {
     uint4 a = src[k];
+    uint32_t aw[4] = {a.x, a.y, a.z, a.w};
     if (fold) {
       const uint4 b = src[k + n16];
-      uint32_t *aw = reinterpret_cast<uint32_t *>(&a);
       const uint32_t bw[4] = {b.x, b.y, b.z, b.w};
 #pragma unroll
       for (int q = 0; q < 4; q++) {
@@ -1897,8 +1921,29 @@ __device__ __forceinline__ void walk_table_load(uint4 *dst, const uint4 *src, ui
         aw[q] = r;
       }
     }
-    dst[k] = a;
+#pragma unroll
+    for (int q = 0; q < 4; q++) dst[(4 * k + q) * WAVE] = aw[q];
   }
+}
+// dist_tail_r on a lane-interleaved tail (header in registers)
+__device__ __forceinline__ uint32_t walk_tail(const uint4 a, const uint4 b, const uint32_t *dtl, uint32_t hold) {
+  const uint32_t rev = __builtin_bitreverse32(hold) >> 17;
+  const uint32_t lw[5] = {a.x, a.y, a.z, a.w, b.x};
+  uint32_t L = 7, fl = lw[0] & 0xffffu, of = (b.x >> 16) & 0xffu;
+#pragma unroll
+  for (int k = 1; k < 9; k++) {
+    const uint32_t lim = (lw[k >> 1] >> (16 * (k & 1))) & 0xffffu;
+    const uint32_t ob = 18 + k;
+    const uint32_t ow = ob < 20 ? b.x : (ob < 24 ? b.y : b.z);
+    const uint32_t ofk = (ow >> (8 * (ob & 3))) & 0xffu;
+    const bool ge = rev >= lim;
+    L += ge ? 1u : 0u;
+    fl = ge ? lim : fl;
+    of = ge ? ofk : of;
+  }
+  const uint32_t idx = of + ((rev - fl) >> (15u - L));
+  const uint32_t sym = wk_byte(dtl, 27u - 4u * WK_DT0 + min(idx, 29u));  // dtl holds the tail from word WK_DT0
+  return CK_SYM | (L << 2) | (sym << 6);
 }
 
 // literal / length code longer than the walk table (or end of block, invalid):
@@ -1916,16 +1961,28 @@ __device__ __forceinline__ uint32_t walk_slow_len(uint32_t h, const uint16_t *cl
   if ((ce & 3u) == CK_EOB) return 0x100u | WK_EXC | ((ce >> 2) & 15u);
   return walk_len_entry<D64>(ce);
 }
-// RING + 1 raw input words from word wi (indices clamped to the last input
-// word; the bytes past the input are masked when the words enter the ring, so
-// nothing here uses the loaded values and the loads stay in flight through
-// the group: the walk runs at ~1 wave per SIMD, where a wait costs the whole
-// memory latency)
-__device__ __forceinline__ void walk_load(const LaneState &s, uint32_t wi, uint32_t (&v)[WK_RING]) {
-  if (wi + WK_RING <= s.lastw) {
+// walk entry of a compact literal/length entry that is not a sub-table link
+template <bool D64>
+__device__ __forceinline__ uint32_t walk_ce_entry(uint32_t ce) {
+  if ((ce & 3u) == CK_SLOW) return WK_EXC;  // invalid
+  if ((ce & 3u) == CK_EOB) return 0x100u | WK_EXC | ((ce >> 2) & 15u);
+  return walk_len_entry<D64>(ce);
+}
+// word wi as read raw, with the bytes at or past the input's end zeroed
+__device__ __forceinline__ uint32_t walk_mask(uint32_t v, uint32_t wi, uint32_t end_byte) {
+  const uint32_t b = wi * 4u;
+  const uint32_t keep = b >= end_byte ? 0u : end_byte - b;
+  return keep >= 4u ? v : __builtin_amdgcn_ubfe(v, 0, 8u * keep);
+}
+// WK_PF raw input words from word wi (a multiple of WK_PF): four 16-byte loads
+// when they are all whole input words, else word loads clamped to the last
+// word (masked when written).  Nothing uses the values here, so the loads stay
+// in flight through a group.
+__device__ __forceinline__ void walk_prefetch(const LaneState &s, uint32_t wi, uint32_t (&v)[WK_PF]) {
+  if (wi + WK_PF <= (s.end_byte >> 2)) {
     const uint32_t *src = (const uint32_t *)(s.w + wi);
 #pragma unroll
-    for (int q = 0; q < RING / 4; q++) {
+    for (int q = 0; q < WK_PF / 4; q++) {
       uint4 x;
       __builtin_memcpy(&x, src + 4 * q, 16);
       v[4 * q] = x.x;
@@ -1933,17 +1990,24 @@ __device__ __forceinline__ void walk_load(const LaneState &s, uint32_t wi, uint3
       v[4 * q + 2] = x.z;
       v[4 * q + 3] = x.w;
     }
-    v[RING] = src[RING];
   } else {
 #pragma unroll
-    for (int q = 0; q < WK_RING; q++) v[q] = s.w[min(wi + (uint32_t)q, s.lastw)];
+    for (uint32_t q = 0; q < WK_PF; q++) v[q] = s.w[min(wi + q, s.lastw)];
   }
 }
-// word wi as read raw, with the bytes at or past the input's end zeroed
-__device__ __forceinline__ uint32_t walk_mask(uint32_t v, uint32_t wi, uint32_t end_byte) {
-  const uint32_t b = wi * 4u;
-  const uint32_t keep = b >= end_byte ? 0u : end_byte - b;
-  return keep >= 4u ? v : __builtin_amdgcn_ubfe(v, 0, 8u * keep);
+// a prefetched half into the lane's ring row (the mirror words with half 0)
+__device__ __forceinline__ void walk_put_half(uint32_t *rr, uint32_t wi, uint32_t (&v)[WK_PF], uint32_t end_byte) {
+  if (wi + WK_PF > (end_byte >> 2)) {
+#pragma unroll
+    for (uint32_t q = 0; q < WK_PF; q++) v[q] = walk_mask(v[q], wi + q, end_byte);
+  }
+  uint32_t *h = rr + (wi & WK_PF);
+#pragma unroll
+  for (uint32_t q = 0; q < WK_PF; q++) h[q] = v[q];
+  if (!(wi & WK_PF)) {
+    rr[WK_RW] = v[0];
+    rr[WK_RW + 1] = v[1];
+  }
 }
 
 enum { WS_RUN = 0, WS_EOB = 1, WS_BAD = 2, WS_IDLE = 3 };
@@ -1974,6 +2038,11 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
   s.hold = 0;
   uint32_t wst = WS_IDLE, code = 0, lbits = 9, tcap = 0;
   const uint16_t *cl = nullptr;
+  uint32_t *wl = &L.wl[0][lane];
+  uint32_t *wd = &L.wd[0][lane];
+  uint32_t *dtl = &L.dtail[0][lane];
+  uint32_t *rr = &L.ring[lane][0];
+  s.dta = s.dtb = make_uint4(0, 0, 0, 0);
   if (c < nchunks) {
     const ZsChunkDev ch = chunks[c];
     if (ch.start_bit != ZS_NONE && heads[ch.job].code == ZD_END) {
@@ -1989,13 +2058,15 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
         const uint32_t *tabg = tables + (size_t)c * TABLE_STRIDE;
         cl = reinterpret_cast<const uint16_t *>(tabg + TABLE_ENTRIES);
         const uint4 *wt = reinterpret_cast<const uint4 *>(tabg + TABLE_WALK_OFF);
-        walk_table_load(reinterpret_cast<uint4 *>(L.wl[lane]), wt, (1u << WKL_BITS) / 16u, WKL_BITS < WK_LBITS);
-        walk_table_load(reinterpret_cast<uint4 *>(L.wd[lane]), wt + (1u << WK_LBITS) / 16u, (1u << WKD_BITS) / 16u,
-                        WKD_BITS < WK_DBITS);
-        const uint4 *img = reinterpret_cast<const uint4 *>(tabg + TABLE_IMG_OFF) + (LROOT_N + DROOT_N) * 2 / 16;
+        walk_table_load(wl, wt, (1u << WKL_BITS) / 16u, WKL_BITS < WK_LBITS);
+        walk_table_load(wd, wt + (1u << WK_LBITS) / 16u, (1u << WKD_BITS) / 16u, WKD_BITS < WK_DBITS);
+        // the distance tail: its header in registers for the whole walk, its symbols in LDS
+        const uint32_t *img = tabg + TABLE_IMG_OFF + (LROOT_N + DROOT_N) / 2;
+        s.dta = make_uint4(img[0], img[1], img[2], img[3]);
+        s.dtb = make_uint4(img[4], img[5], img[6], img[7]);
 #pragma unroll
-        for (uint32_t k = 0; k < DTAIL_BYTES / 16; k++) reinterpret_cast<uint4 *>(L.dtail[lane])[k] = img[k];
-        lane_prime(s, ch.hdr_bit);
+        for (uint32_t k = 0; k < WK_DTN; k++) dtl[k * WAVE] = img[WK_DT0 + k];
+        s.lastw = (s.end_byte - 1u) >> 2;
         wst = WS_RUN;
       } else {  // stored or undecodable first block: a leftover from the start
         walks[c].status = WK_NONE;
@@ -2004,133 +2075,205 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
       }
     }
   }
-  __builtin_amdgcn_wave_barrier();
-  const uint8_t *wl = L.wl[lane];
-  const uint8_t *wd = L.wd[lane];
-  uint32_t *rp = &L.ring[0][lane];
-  const uint32_t *dtl = L.dtail[lane];
   uint2 *cp = cps + (size_t)(c < nchunks ? c : 0u) * WK_CP;
   uint32_t ntok = 0, K = WK_K0, ncp = 0, ncut = WK_K0, eob = 0, endb = 0;
+  uint32_t cpp = 0, cpt = 0, cpend = 0;  // a checkpoint taken in the group, stored at the next group start
+  // The bit reader is one absolute bit position per lane, p: each step reads
+  // the three ring words holding bits [p, p + 64) (ring slot = word % WK_RW;
+  // the ring holds words [filled - WK_RW, filled)), looks the literal/length
+  // entry up at p and the distance entry at p + its bits, and advances p by
+  // both elements' bits -- no bit buffer, no refills.  The ring is refilled a
+  // half at a time from a prefetch that stays in flight for groups.
+  uint32_t p = c < nchunks && wst == WS_RUN ? chunks[c].hdr_bit : 0u;
+  uint32_t filled = (p >> 5) & ~(WK_PF - 1u), pre[WK_PF];
+  bool live = wst == WS_RUN;
+  if (live) {  // both halves now (words filled .. filled + 31), then the next prefetch
+    walk_prefetch(s, filled, pre);
+    uint32_t pre2[WK_PF];
+    walk_prefetch(s, filled + WK_PF, pre2);
+    walk_put_half(rr, filled, pre, s.end_byte);
+    walk_put_half(rr, filled + WK_PF, pre2, s.end_byte);
+    filled += WK_RW;
+    walk_prefetch(s, filled, pre);
+  }
+  uint32_t xp = live ? 0u : 1u;  // an exception is pending: the lane stands at its symbol until the next group start
+  uint32_t xs = 0, ce = 0;        // compact-table loads in flight for it (1: root entry, 2: sub-table entry)
+  // the ring row's address, opaque to the compiler (so that a step's ring
+  // address is one shift-and-mask and one add, not folded LDS offsets)
+  typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
+  uint32_t rra = (uint32_t)(uintptr_t)(lds_cu32 *)rr;
+  uint32_t wla = (uint32_t)(uintptr_t)(lds_cu32 *)wl, wda = (uint32_t)(uintptr_t)(lds_cu32 *)wd;
+  asm volatile("" : "+v"(rra), "+v"(wla), "+v"(wda));
+  __builtin_amdgcn_wave_barrier();
 #if KP_ON
   const uint64_t kp_t0 = KP_NOW();
-  uint64_t kp_cyc_l = 0, kp_cyc_d = 0;
-  uint32_t kp_groups = 0, kp_wsteps = 0, kp_slow_l = 0, kp_slow_d = 0;
+  uint64_t kp_cyc_x = 0, kp_cyc_g = 0;
+  uint32_t kp_wsteps = 0, kp_exc = 0, kp_slow_l = 0, kp_slow_d = 0;
 #endif
-  uint32_t pre[WK_RING];
-  uint32_t pre_wi = ~0u;
-  for (;;) {
-    if (__ballot(wst == WS_RUN) == 0) break;
-    if (wst == WS_RUN) {
-      // group start: ring[0..RING) = words wi .. wi + RING - 1 (prefetched during
-      // the last group when it ended where expected), then the next group's words
-      if (s.wi == pre_wi || s.wi == pre_wi + 1u) {
-        const bool sh = s.wi != pre_wi;
-        uint32_t w0 = 0;
-#pragma unroll
-        for (int q = 0; q < RING; q++) {
-          const uint32_t v = walk_mask(sh ? pre[q + 1] : pre[q], s.wi + (uint32_t)q, s.end_byte);
-          rp[q * WAVE] = v;
-          if (q == 0) w0 = v;
-        }
-        s.nw = w0;
-        s.rk = 0;
-      } else {
-        lane_fill_ring(s, rp);
-      }
-      // a group ends with rk in {RING - 2, RING - 1}: its successor starts at
-      // word wi + RING - 2 or one later
-      pre_wi = s.wi + RING - 2u;
-      walk_load(s, pre_wi, pre);
-      s.dta = *reinterpret_cast<const uint4 *>(dtl);  // the distance tail's header, in registers for the group
-      s.dtb = *reinterpret_cast<const uint4 *>(dtl + 4);
+  // The steps are straight-line: a lane whose symbol needs more than the
+  // tables (a long code, the end of the block, an invalid code, deflate64's
+  // symbol 285, or the input's end) stands still with xp set, and the group
+  // start resolves it exactly (the unit's compact tables, the canonical
+  // distance tail); a checkpoint is taken by selects and stored at the next
+  // group start.  Lanes that are done step on harmlessly (LDS reads stay in
+  // bounds; nothing they compute is kept).
+  while (__builtin_amdgcn_ballot_w64(live)) {
 #if KP_ON
-      kp_groups++;
+    const uint64_t kg0 = KP_NOW();
 #endif
-      while (s.rk + 2 < RING) {
-#if KP_ON
-        kp_wsteps += lane_id() == (uint32_t)__builtin_ctzll(__ballot(1)) ? 1u : 0u;
-#endif
-        const uint32_t p0 = lane_pos(s);
-        lane_refill_bf(s, rp);
-        uint32_t e = wl[(uint32_t)s.hold & ((1u << WKL_BITS) - 1u)];
-        if (__builtin_expect(__ballot(e & WK_EXC) != 0, 0)) {
-#if KP_ON
-          const uint64_t kq = KP_NOW();
-          kp_slow_l += lane_id() == (uint32_t)__builtin_ctzll(__ballot(1)) ? 1u : 0u;
-#endif
-          if (e & WK_EXC) e = walk_slow_len<D64>((uint32_t)s.hold, cl, lbits);
-#if KP_ON
-          kp_cyc_l += KP_NOW() - kq;
-#endif
-        }
-        const uint32_t n = e & 31u;
-        uint32_t two = 0;
-        if (D64) two = (e & WK_BIG) && ((uint32_t)(s.hold >> (n - 16u)) & 0xffffu) >= 65533u;  // length > 65535
-        s.hold >>= n;
-        s.nbits -= n;
-        lane_refill_bf(s, rp);
-        uint32_t d = wd[(uint32_t)s.hold & ((1u << WKD_BITS) - 1u)];
-        const bool hasd = (e & WK_HASD) != 0;
-        if (__builtin_expect(__ballot(hasd && d == WK_EXC) != 0, 0)) {
-#if KP_ON
-          const uint64_t kq = KP_NOW();
-          kp_slow_d += lane_id() == (uint32_t)__builtin_ctzll(__ballot(1)) ? 1u : 0u;
-#endif
-          // a distance code longer than the table's index: canonical decode from
-          // the lane's tail (header in registers, one LDS read for the symbol)
-          const uint32_t de = dist_tail_r(s.dta, s.dtb, dtl, (uint32_t)s.hold);
-          const uint32_t dsym = (de >> 6) & 31u;
-          if (hasd && d == WK_EXC) d = (!D64 && dsym >= 30u) ? WK_BAD : walk_dist_entry(de);
-#if KP_ON
-          kp_cyc_d += KP_NOW() - kq;
-#endif
-        }
-        const uint32_t dn = hasd ? (d & 31u) : 0u;
-        s.hold >>= dn;
-        s.nbits -= dn;
-        const uint32_t p1 = lane_pos(s);
-        if ((e & WK_EXC) || (hasd && (d & WK_EXC)) || p1 > s.limit) {
-          if (e & 0x100u) {  // end of block
-            eob = p0;
-            endb = p0 + n;
-            wst = endb > s.limit ? WS_BAD : WS_EOB;
-            code = ZD_TRUNC;
-          } else {  // invalid code or truncated: the unit cannot stop at a block boundary
-            wst = WS_BAD;
-            code = p1 > s.limit ? ZD_TRUNC : (ZD_ERROR | (((e & WK_EXC) ? ZM_LITLEN_CODE : ZM_DIST_CODE) << 8));
-          }
-          break;
-        }
-        ntok += 1u + two;
-        if (ntok >= ncut) {  // a checkpoint: the next sub-unit starts here
-          cp[ncp] = make_uint2(p1, ntok);
-          ncp++;
-          ncut += K;
-          if (ncp == WK_CP - 1u) {  // out of slots: keep every second checkpoint, twice the stride
-            walk_halve(cp);
-            ncp = (WK_CP - 1u) / 2u;
-            K *= 2u;
-            ncut = (ncp + 1u) * K;
-          }
+    if (__builtin_amdgcn_ballot_w64(cpend != 0)) {
+      if (cpend) {  // a checkpoint: the next sub-unit starts here
+        cp[ncp] = make_uint2(cpp, cpt);
+        ncp++;
+        cpend = 0;
+        if (ncp == WK_CP - 1u) {  // out of slots: keep every second checkpoint, twice the stride
+          walk_halve(cp);
+          ncp = (WK_CP - 1u) / 2u;
+          K *= 2u;
+          ncut = (ncp + 1u) * K;
         }
       }
     }
-    __builtin_amdgcn_wave_barrier();  // the ring is rewritten by the next group
+    if (__builtin_amdgcn_ballot_w64(live && xp)) {
+#if KP_ON
+      const uint64_t kq = KP_NOW();
+      kp_exc += lane_id() == (uint32_t)__builtin_ctzll(__ballot(1)) ? 1u : 0u;
+#endif
+      bool ready = true;
+      if (live && xp) {  // the pending symbol, exactly
+        const uint32_t *r = rr + ((p >> 5) & (WK_RW - 1u));
+        const uint32_t x0 = r[0], x1 = r[1], x2 = r[2];
+        const uint32_t bits = __builtin_amdgcn_alignbit(x1, x0, p);
+        uint32_t e2 = wk_byte(wl, bits & ((1u << WKL_BITS) - 1u));
+        if (e2 & WK_EXC) {
+          // past the table: the unit's compact tables (global), one load per
+          // group start so that the lane waits a group instead of the load
+          if (xs == 0) {
+#if KP_ON
+            kp_slow_l++;
+#endif
+            ce = cl[bits & ((1u << lbits) - 1u)];
+            xs = 1;
+            ready = false;
+          } else if (xs == 1 && (ce & 3u) == CK_SLOW && ((ce >> 2) & 15u)) {  // a sub-table link
+            ce = cl[(ce >> 6) + ((bits >> lbits) & ((1u << ((ce >> 2) & 15u)) - 1u))];
+            xs = 2;
+            ready = false;
+          } else {
+            e2 = walk_ce_entry<D64>(ce);
+          }
+        }
+        if (!ready) {
+        } else if (e2 & WK_EXC) {
+          if (e2 & 0x100u) {  // end of block
+            eob = p;
+            endb = p + (e2 & 31u);
+            wst = endb > s.limit ? WS_BAD : WS_EOB;
+            code = ZD_TRUNC;
+          } else {  // invalid literal/length code
+            wst = WS_BAD;
+            code = p > s.limit ? ZD_TRUNC : (ZD_ERROR | (ZM_LITLEN_CODE << 8));
+          }
+          live = false;
+        } else {
+          const uint32_t n2 = e2 & 31u;
+          const uint32_t q2 = (p & 31u) + n2;
+          const uint32_t db2 = __builtin_amdgcn_alignbit(q2 < 32u ? x1 : x2, q2 < 32u ? x0 : x1, q2);
+          uint32_t d2 = 0;
+          if (e2 & WK_HASD) {
+            d2 = wk_byte(wd, db2 & ((1u << WKD_BITS) - 1u));
+            if (d2 == WK_EXC) {  // a distance code longer than the table's index: the canonical tail
+#if KP_ON
+              kp_slow_d++;
+#endif
+              const uint32_t de = walk_tail(s.dta, s.dtb, dtl, db2);
+              const uint32_t dsym = (de >> 6) & 31u;
+              d2 = (!D64 && dsym >= 30u) ? WK_BAD : walk_dist_entry(de);
+            }
+          }
+          const uint32_t pn = p + n2 + (d2 & 31u);
+          if (d2 & WK_EXC) {  // invalid distance code
+            wst = WS_BAD;
+            code = pn > s.limit ? ZD_TRUNC : (ZD_ERROR | (ZM_DIST_CODE << 8));
+            live = false;
+          } else if (pn > s.limit) {
+            wst = WS_BAD;
+            code = ZD_TRUNC;
+            live = false;
+          } else {
+            p = pn;
+            ntok += (D64 && (e2 & WK_BIG) && ((bits >> (n2 - 16u)) & 0xffffu) >= 65533u) ? 2u : 1u;  // deflate64 > 65535: two tokens
+            const bool ck = ntok >= ncut;
+            cpp = ck ? p : cpp;
+            cpt = ck ? ntok : cpt;
+            cpend = ck ? 1u : cpend;
+            ncut = ck ? ncut + K : ncut;
+          }
+        }
+        if (ready) {
+          xs = 0;
+          xp = live ? 0u : 1u;  // a lane that is done stays where it stopped
+        }
+      }
+#if KP_ON
+      kp_cyc_x += KP_NOW() - kq;
+#endif
+    }
+    {  // a lane that has consumed its older half refills it from the prefetch
+      const bool wr = live && filled - (p >> 5) <= WK_RW - WK_PF;
+      if (__builtin_amdgcn_ballot_w64(wr)) {
+        if (wr) {
+          walk_put_half(rr, filled, pre, s.end_byte);
+          filled += WK_PF;
+          walk_prefetch(s, filled, pre);
+        }
+      }
+    }
+    if (!live) ncut = ~0u;  // no checkpoints after the end
+#if KP_ON
+    kp_cyc_g += KP_NOW() - kg0;
+#endif
+#pragma unroll 1
+    for (uint32_t g = 0; g < WK_GS(D64); g++) {
+#if KP_ON
+      kp_wsteps += lane_id() == (uint32_t)__builtin_ctzll(__ballot(1)) ? 1u : 0u;
+#endif
+      lds_cu32 *r = (lds_cu32 *)(uintptr_t)(rra + ((p >> 3) & ((WK_RW - 1u) * 4u)));
+      const uint32_t x0 = r[0], x1 = r[1], x2 = r[2];
+      const uint32_t bits = __builtin_amdgcn_alignbit(x1, x0, p);  // input bits [p, p + 32)
+      const uint32_t e = wk_byte_a(wla, bits, WKL_BITS);
+      const uint32_t n = e & 31u;
+      const uint32_t q = (p & 31u) + n;  // < 64: the distance code's bits from x0:x1, or x1:x2 past 32
+      const uint32_t dbits = __builtin_amdgcn_alignbit(q < 32u ? x1 : x2, q < 32u ? x0 : x1, q);
+      const uint32_t d = wk_byte_a(wda, dbits, WKD_BITS);
+      const uint32_t dd = (e & WK_HASD) ? d : 0u;
+      const uint32_t pn = p + n + (dd & 31u);
+      const uint32_t x = ((e | dd) & (D64 ? (WK_EXC | WK_BIG) : WK_EXC)) | (pn > s.limit ? 1u : 0u) | xp;
+      p = x ? p : pn;
+      ntok += x ? 0u : 1u;
+      xp = x;
+      const bool ck = ntok >= ncut;
+      cpp = ck ? p : cpp;
+      cpt = ck ? ntok : cpt;
+      cpend = ck ? 1u : cpend;
+      ncut = ck ? ncut + K : ncut;
+    }
+  }
+  if (cpend) {  // the last group's checkpoint
+    cp[ncp] = make_uint2(cpp, cpt);
+    ncp++;
   }
 #if KP_ON
-  {  // walk counters in the lane parse's slots (the split parse runs no lane parse)
+  {  // walk counters in slots no other kernel of the split parse writes
     const uint64_t tot = KP_NOW() - kp_t0;
-    KP_ADD(KP_P_WAVES, 1);
-    KP_ADD(KP_P_CYC_TOTAL, tot);
-    KP_MAX(KP_P_CYC_MAX, tot);
-    KP_ADD(KP_P_GROUPS, kp_groups);
-    KP_ADD(KP_P_WAVE_STEPS, kp_wave_sum(kp_wsteps));
+    KP_ADD(44, tot);
+    KP_MAX(45, tot);
+    KP_ADD(46, kp_wave_sum(kp_wsteps));
+    KP_ADD(47, kp_cyc_x);
+    KP_ADD(38, kp_cyc_g);
+    KP_ADD(39, kp_wave_sum(kp_exc));
     KP_ADD(KP_P_SLOW_LIT, kp_wave_sum(kp_slow_l));
     KP_ADD(KP_P_SLOW_DIST, kp_wave_sum(kp_slow_d));
-    KP_ADD(KP_P_CYC_COOP, kp_cyc_l);
-    KP_ADD(KP_P_CYC_FLUSH, kp_cyc_d);
-    KP_ADD(KP_P_LANE_STEPS, kp_wave_sum(ntok));
-    if (kp_groups) KP_ADD(KP_P_BUSY, 1);
   }
 #endif
   if (wst == WS_EOB && !tok_ensure(pool, c, tcap, ntok)) {
