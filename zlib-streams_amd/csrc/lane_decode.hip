@@ -731,6 +731,51 @@ __device__ void build_dist_tail(const uint16_t *dl, uint32_t n, uint8_t *out) {
       if (dl[i] == (uint32_t)L && r < 32) out[27 + r++] = (uint8_t)i;
 }
 
+// The literal/length code's canonical tail for the split parse's walk (codes
+// longer than its 9-bit table): words 0-3 the left-justified 15-bit limits
+// of lengths 9..15 (u16 each, lim[L] = (first[L] + count[L]) << (15 - L)),
+// words 4-5 the literal count of each length 10..15 (u8, capped at 255).
+// Canonical order puts a length's literals first (symbols < 256), so a long
+// code whose index within its length is below that count is a literal --
+// its walk entry is just its length, found without the global tables.
+// Wave-cooperative (every lane calls it): the per-length counts by ballots,
+// 64 code lengths at a time, then lane 0 writes the 8 words.
+__device__ void build_lit_tail(const uint16_t *ll, uint32_t n, uint32_t *out) {
+  const uint32_t lane = lane_id();
+  uint32_t cnt = 0, nl = 0;  // lane L (1..15): codes of length L, and literals among them
+  for (uint32_t b = 0; b < n; b += WAVE) {
+    const uint32_t i = b + lane;
+    const uint32_t len = i < n ? (ll[i] & 15u) : 0u;
+#pragma unroll
+    for (uint32_t L = 1; L < 16; L++) {
+      const uint32_t c = (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(len == L));
+      const uint32_t cl = (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(len == L && i < 256u));
+      cnt += lane == L ? c : 0u;
+      nl += lane == L ? cl : 0u;
+    }
+  }
+  uint32_t code = 0, lim[16], nlit[16];
+  lim[0] = nlit[0] = 0;
+  uint32_t prev = 0;
+#pragma unroll
+  for (int L = 1; L < 16; L++) {
+    const uint32_t cL = __builtin_amdgcn_readlane(cnt, L);
+    nlit[L] = __builtin_amdgcn_readlane(nl, L);
+    code = (code + prev) << 1;
+    lim[L] = min((code + cL) << (15 - L), 0xffffu);
+    prev = cL;
+  }
+  if (lane == 0) {
+    out[0] = lim[9] | (lim[10] << 16);
+    out[1] = lim[11] | (lim[12] << 16);
+    out[2] = lim[13] | (lim[14] << 16);
+    out[3] = lim[15];
+    out[4] = min(nlit[10], 255u) | (min(nlit[11], 255u) << 8) | (min(nlit[12], 255u) << 16) | (min(nlit[13], 255u) << 24);
+    out[5] = min(nlit[14], 255u) | (min(nlit[15], 255u) << 8);
+    out[6] = out[7] = 0;
+  }
+}
+
 // Dynamic block header after the 3 block-type bits (src/inflate.c:905-1033):
 // code-length code, code lengths, then the literal/length and distance tables
 // (src/inftrees.c restated in build_table) into the unit's global table area
@@ -740,7 +785,8 @@ __device__ void build_dist_tail(const uint16_t *dl, uint32_t n, uint8_t *out) {
 template <bool D64>
 __device__ int wave_dyn_header(BuildLDS &B, const uint32_t *w, uint32_t end_byte, uint32_t &bit, uint32_t *tabg,
                                uint16_t *ctab, uint32_t &lbits, uint32_t &dbits, uint16_t *lroot_out,
-                               uint16_t *droot_out, uint8_t *dtail_out, uint8_t *walk_out = nullptr) {
+                               uint16_t *droot_out, uint8_t *dtail_out, uint8_t *walk_out = nullptr,
+                               uint32_t *ltail_out = nullptr) {
   const uint32_t lane = lane_id();
   const uint32_t limit = end_byte * 8u;
   StageBits sb;
@@ -817,6 +863,7 @@ __device__ int wave_dyn_header(BuildLDS &B, const uint32_t *w, uint32_t end_byte
   for (uint32_t i = lane; i < LROOT_N; i += WAVE) lroot_out[i] = lds_len_root(B.tab, lbits, i);
   if (walk_out)
     for (uint32_t i = lane; i < (1u << WK_LBITS); i += WAVE) walk_out[i] = (uint8_t)walk_len_z<D64>(B.tab, lbits, i);
+  if (ltail_out) build_lit_tail(B.lens, nlen, ltail_out);
   __builtin_amdgcn_wave_barrier();
   dbits = 6;
   if (build_table(T_DISTS, B.lens + nlen, ndist, B.tab, &dbits, B.sorted, B.scr, D64 ? 1 : 0)) {
@@ -1873,6 +1920,9 @@ __global__ void __launch_bounds__(64) zs_unitw_list_kernel(const ZsJobDev *__res
 #endif
 static_assert(WKL_BITS + 1u >= WK_LBITS && WKL_BITS <= WK_LBITS && WKD_BITS + 1u >= WK_DBITS && WKD_BITS <= WK_DBITS,
               "walk tables fold by one bit at most");
+#ifndef WK_LTAIL
+#define WK_LTAIL 1  // long literals from the canonical tail in registers (0: always the compact tables)
+#endif
 #define WK_GS(d64) ((d64) ? 7u : 9u)  // steps per group: <= 60 (48) bits each, so a group reads words p / 32 .. p / 32 + 16
 #define WK_PF 16u   // words per prefetch: the ring is two such halves
 #define WK_RW 32u   // input ring words per lane
@@ -1961,6 +2011,24 @@ __device__ __forceinline__ uint32_t walk_slow_len(uint32_t h, const uint16_t *cl
   if ((ce & 3u) == CK_EOB) return 0x100u | WK_EXC | ((ce >> 2) & 15u);
   return walk_len_entry<D64>(ce);
 }
+// a literal/length code past the walk's table from the canonical tail in
+// registers (build_lit_tail): its walk entry when it is a literal, else WK_EXC
+// (end of block, a length code, invalid: the compact tables decide)
+__device__ __forceinline__ uint32_t walk_lit_tail(const uint32_t (&lt)[6], uint32_t bits) {
+  const uint32_t rev = __builtin_bitreverse32(bits) >> 17;  // the next 15 bits, first bit highest
+  const uint32_t lim[7] = {lt[0] & 0xffffu, lt[0] >> 16, lt[1] & 0xffffu, lt[1] >> 16,
+                           lt[2] & 0xffffu, lt[2] >> 16, lt[3] & 0xffffu};  // lengths 9 .. 15
+  uint32_t L = 10, fl = lim[0], nl = lt[4] & 0xffu;
+#pragma unroll
+  for (int k = 1; k < 6; k++) {
+    const bool ge = rev >= lim[k];
+    L += ge ? 1u : 0u;
+    fl = ge ? lim[k] : fl;
+    nl = ge ? ((lt[4 + (k >> 2)] >> (8 * (k & 3))) & 0xffu) : nl;
+  }
+  const uint32_t idx = (rev - fl) >> (15u - L);
+  return (rev >= lim[0] && rev < lim[6] && idx < nl) ? L : WK_EXC;
+}
 // walk entry of a compact literal/length entry that is not a sub-table link
 template <bool D64>
 __device__ __forceinline__ uint32_t walk_ce_entry(uint32_t ce) {
@@ -2043,6 +2111,7 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
   uint32_t *dtl = &L.dtail[0][lane];
   uint32_t *rr = &L.ring[lane][0];
   s.dta = s.dtb = make_uint4(0, 0, 0, 0);
+  uint32_t ltw[6] = {0, 0, 0, 0, 0, 0};  // the literal/length code's canonical tail (registers)
   if (c < nchunks) {
     const ZsChunkDev ch = chunks[c];
     if (ch.start_bit != ZS_NONE && heads[ch.job].code == ZD_END) {
@@ -2065,6 +2134,8 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
         s.dta = make_uint4(img[0], img[1], img[2], img[3]);
         s.dtb = make_uint4(img[4], img[5], img[6], img[7]);
 #pragma unroll
+        for (int k = 0; k < 6; k++) ltw[k] = tabg[TABLE_LTAIL_OFF + k];
+#pragma unroll
         for (uint32_t k = 0; k < WK_DTN; k++) dtl[k * WAVE] = img[WK_DT0 + k];
         s.lastw = (s.end_byte - 1u) >> 2;
         wst = WS_RUN;
@@ -2077,7 +2148,6 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
   }
   uint2 *cp = cps + (size_t)(c < nchunks ? c : 0u) * WK_CP;
   uint32_t ntok = 0, K = WK_K0, ncp = 0, ncut = WK_K0, eob = 0, endb = 0;
-  uint32_t cpp = 0, cpt = 0, cpend = 0;  // a checkpoint taken in the group, stored at the next group start
   // The bit reader is one absolute bit position per lane, p: each step reads
   // the three ring words holding bits [p, p + 64) (ring slot = word % WK_RW;
   // the ring holds words [filled - WK_RW, filled)), looks the literal/length
@@ -2107,7 +2177,7 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
   __builtin_amdgcn_wave_barrier();
 #if KP_ON
   const uint64_t kp_t0 = KP_NOW();
-  uint64_t kp_cyc_x = 0, kp_cyc_g = 0;
+  uint64_t kp_cyc_x = 0, kp_cyc_g = 0, kp_cyc_s = 0;
   uint32_t kp_wsteps = 0, kp_exc = 0, kp_slow_l = 0, kp_slow_d = 0;
 #endif
   // The steps are straight-line: a lane whose symbol needs more than the
@@ -2121,19 +2191,6 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
 #if KP_ON
     const uint64_t kg0 = KP_NOW();
 #endif
-    if (__builtin_amdgcn_ballot_w64(cpend != 0)) {
-      if (cpend) {  // a checkpoint: the next sub-unit starts here
-        cp[ncp] = make_uint2(cpp, cpt);
-        ncp++;
-        cpend = 0;
-        if (ncp == WK_CP - 1u) {  // out of slots: keep every second checkpoint, twice the stride
-          walk_halve(cp);
-          ncp = (WK_CP - 1u) / 2u;
-          K *= 2u;
-          ncut = (ncp + 1u) * K;
-        }
-      }
-    }
     if (__builtin_amdgcn_ballot_w64(live && xp)) {
 #if KP_ON
       const uint64_t kq = KP_NOW();
@@ -2148,7 +2205,10 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
         if (e2 & WK_EXC) {
           // past the table: the unit's compact tables (global), one load per
           // group start so that the lane waits a group instead of the load
-          if (xs == 0) {
+          const uint32_t et = (WK_LTAIL && xs == 0) ? walk_lit_tail(ltw, bits) : WK_EXC;
+          if (et != WK_EXC) {  // a long literal: its length from the tail in registers
+            e2 = et;
+          } else if (xs == 0) {
 #if KP_ON
             kp_slow_l++;
 #endif
@@ -2203,11 +2263,6 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
           } else {
             p = pn;
             ntok += (D64 && (e2 & WK_BIG) && ((bits >> (n2 - 16u)) & 0xffffu) >= 65533u) ? 2u : 1u;  // deflate64 > 65535: two tokens
-            const bool ck = ntok >= ncut;
-            cpp = ck ? p : cpp;
-            cpt = ck ? ntok : cpt;
-            cpend = ck ? 1u : cpend;
-            ncut = ck ? ncut + K : ncut;
           }
         }
         if (ready) {
@@ -2219,6 +2274,21 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
       kp_cyc_x += KP_NOW() - kq;
 #endif
     }
+    // a checkpoint at the first group start past every K tokens (the lane
+    // stands on a symbol boundary here; a pending symbol is not yet counted)
+    if (__builtin_amdgcn_ballot_w64(live && ntok >= ncut)) {
+      if (live && ntok >= ncut) {  // the next sub-unit starts here
+        cp[ncp] = make_uint2(p, ntok);
+        ncp++;
+        ncut += K;
+        if (ncp == WK_CP - 1u) {  // out of slots: keep every second checkpoint, twice the stride
+          walk_halve(cp);
+          ncp = (WK_CP - 1u) / 2u;
+          K *= 2u;
+          ncut = (ncp + 1u) * K;
+        }
+      }
+    }
     {  // a lane that has consumed its older half refills it from the prefetch
       const bool wr = live && filled - (p >> 5) <= WK_RW - WK_PF;
       if (__builtin_amdgcn_ballot_w64(wr)) {
@@ -2229,49 +2299,61 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
         }
       }
     }
-    if (!live) ncut = ~0u;  // no checkpoints after the end
 #if KP_ON
-    kp_cyc_g += KP_NOW() - kg0;
+    const uint64_t ks0 = KP_NOW();
+    kp_cyc_g += ks0 - kg0;
+    kp_wsteps += WK_GS(D64);
 #endif
-#pragma unroll 1
-    for (uint32_t g = 0; g < WK_GS(D64); g++) {
-#if KP_ON
-      kp_wsteps += lane_id() == (uint32_t)__builtin_ctzll(__ballot(1)) ? 1u : 0u;
-#endif
-      lds_cu32 *r = (lds_cu32 *)(uintptr_t)(rra + ((p >> 3) & ((WK_RW - 1u) * 4u)));
-      const uint32_t x0 = r[0], x1 = r[1], x2 = r[2];
-      const uint32_t bits = __builtin_amdgcn_alignbit(x1, x0, p);  // input bits [p, p + 32)
-      const uint32_t e = wk_byte_a(wla, bits, WKL_BITS);
-      const uint32_t n = e & 31u;
-      const uint32_t q = (p & 31u) + n;  // < 64: the distance code's bits from x0:x1, or x1:x2 past 32
-      const uint32_t dbits = __builtin_amdgcn_alignbit(q < 32u ? x1 : x2, q < 32u ? x0 : x1, q);
-      const uint32_t d = wk_byte_a(wda, dbits, WKD_BITS);
-      const uint32_t dd = (e & WK_HASD) ? d : 0u;
-      const uint32_t pn = p + n + (dd & 31u);
-      const uint32_t x = ((e | dd) & (D64 ? (WK_EXC | WK_BIG) : WK_EXC)) | (pn > s.limit ? 1u : 0u) | xp;
-      p = x ? p : pn;
-      ntok += x ? 0u : 1u;
-      xp = x;
-      const bool ck = ntok >= ncut;
-      cpp = ck ? p : cpp;
-      cpt = ck ? ntok : cpt;
-      cpend = ck ? 1u : cpend;
-      ncut = ck ? ncut + K : ncut;
+    // unrolled: the next step's ring read issues before this step's
+    // bookkeeping (a rolled loop serialises them: 472 vs 326 cycles a step).
+    // A step only looks its two entries up and advances p; which step (if
+    // any) met an exception -- an entry past the tables, or the input's end
+    // (p only grows, so the first step past it) -- is found once at the end
+    // of the group from the positions each step started at, and the lane
+    // stands there (the steps after it ran on garbage).
+    {
+      constexpr uint32_t GS = WK_GS(D64);
+      uint32_t pk[GS + 1], xk[GS];
+#pragma unroll
+      for (uint32_t g = 0; g < GS; g++) {
+        pk[g] = p;
+        lds_cu32 *r = (lds_cu32 *)(uintptr_t)(rra + 4u * __builtin_amdgcn_ubfe(p, 5, 5));
+        const uint32_t x0 = r[0], x1 = r[1], x2 = r[2];
+        const uint32_t lo = __builtin_amdgcn_alignbit(x1, x0, p);  // input bits [p, p + 32)
+        const uint32_t hi = __builtin_amdgcn_alignbit(x2, x1, p);  // [p + 32, p + 64)
+        const uint32_t e = wk_byte_a(wla, lo, WKL_BITS);
+        const uint32_t n = e & 31u;  // <= 31: the distance code starts in lo:hi
+        const uint32_t d = wk_byte_a(wda, __builtin_amdgcn_alignbit(hi, lo, n), WKD_BITS);
+        const uint32_t dd = (e & WK_HASD) ? d : 0u;
+        p += n + (dd & 31u);
+        xk[g] = (e | dd) & (D64 ? (WK_EXC | WK_BIG) : WK_EXC);
+      }
+      pk[GS] = p;
+      uint32_t k = GS;  // the first step with an exception (GS: none)
+#pragma unroll
+      for (int g = (int)GS - 1; g >= 0; g--) k = (xk[g] || pk[g + 1] > s.limit) ? (uint32_t)g : k;
+      k = xp ? 0u : k;  // a lane that stood still (pending, or done) stays
+      uint32_t pst = pk[0];
+#pragma unroll
+      for (uint32_t g = 1; g <= GS; g++) pst = k == g ? pk[g] : pst;
+      p = pst;
+      ntok += k;
+      xp = (k < GS) ? 1u : 0u;
     }
-  }
-  if (cpend) {  // the last group's checkpoint
-    cp[ncp] = make_uint2(cpp, cpt);
-    ncp++;
+#if KP_ON
+    kp_cyc_s += KP_NOW() - ks0;
+#endif
   }
 #if KP_ON
   {  // walk counters in slots no other kernel of the split parse writes
     const uint64_t tot = KP_NOW() - kp_t0;
     KP_ADD(44, tot);
     KP_MAX(45, tot);
-    KP_ADD(46, kp_wave_sum(kp_wsteps));
+    KP_ADD(46, kp_wsteps);
     KP_ADD(47, kp_cyc_x);
     KP_ADD(38, kp_cyc_g);
     KP_ADD(39, kp_wave_sum(kp_exc));
+    KP_ADD(KP_P_CYC_STEPS, kp_cyc_s);
     KP_ADD(KP_P_SLOW_LIT, kp_wave_sum(kp_slow_l));
     KP_ADD(KP_P_SLOW_DIST, kp_wave_sum(kp_slow_d));
   }
@@ -2301,73 +2383,6 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
   }
 }
 
-// lane_step_fast's decoder for a sub-unit of a walked block.  Every symbol
-// before the sub-unit's end is a plain literal or length (the walk met them),
-// so there is no exception path: anything else marks the unit inconsistent
-// (bad: decoded again from its start by zs_unitw_list_kernel).  The checks
-// that depend on the unit's output position are deferred: `need` keeps the
-// most history a distance asks for beyond this sub-unit's own output.
-template <bool D64>
-__device__ __forceinline__ void split_step(LaneState &s, const uint16_t *__restrict__ lt, const uint16_t *__restrict__ dt,
-                                           uint32_t *__restrict__ tb, const uint32_t *__restrict__ dtl,
-                                           const uint32_t *__restrict__ rp, uint32_t &bad, uint32_t &need) {
-  lane_refill_bf(s, rp);
-  uint32_t e = lt[(uint32_t)s.hold & (LROOT_N - 1)];
-  uint32_t kind = e & 3u;
-  if (__builtin_expect(__ballot(kind == CK_SLOW) != 0, 0)) {
-    if (kind == CK_SLOW) {
-      const uint32_t op = (e >> 2) & 15u;
-      uint32_t e2 = CK_SLOW;
-      if (op == OP_ROOT9) {
-        e2 = s.cl[(uint32_t)s.hold & 511u];
-        const uint32_t op2 = (e2 >> 2) & 15u;
-        if ((e2 & 3u) == CK_SLOW && op2) e2 = s.cl[(e2 >> 6) + (((uint32_t)s.hold >> 9) & ((1u << op2) - 1u))];
-      } else if (op) {
-        e2 = s.cl[(e >> 6) + (((uint32_t)s.hold >> s.lbits) & ((1u << op) - 1u))];
-      }
-      e = e2;
-      kind = e & 3u;
-    }
-  }
-  const uint32_t used = (e >> 2) & 15u, sym = e >> 6;
-  const uint32_t isl = kind == CK_LEN;
-  const uint32_t top = sym >= 28u;
-  uint32_t xb = (uint32_t)max((int)(sym >> 2) - 1, 0);
-  xb = top ? (D64 ? 16u : 0u) : xb;
-  xb = isl ? xb : 0u;
-  uint32_t lbase = ((4u + (sym & 3u)) << (xb & 15u)) + 3u - (sym < 4u ? 4u : 0u);
-  lbase = top ? (D64 ? 3u : 258u) : lbase;
-  s.hold >>= used;
-  const uint32_t len = isl ? lbase + ((uint32_t)s.hold & ((1u << xb) - 1u)) : 1u;
-  s.hold >>= xb;
-  s.nbits -= used + xb;
-  lane_refill_bf(s, rp);
-  uint32_t d = dt[(uint32_t)s.hold & (DROOT_N - 1)];
-  const uint32_t dtr = dist_tail_r(s.dta, s.dtb, dtl, (uint32_t)s.hold);
-  const bool dslow = isl && (d & 3u) == CK_SLOW;
-  d = dslow ? (((d >> 2) & 15u) ? dtr : (uint32_t)CK_SLOW) : d;
-  const uint32_t dused = (d >> 2) & 15u, dsym = (d >> 6) & 31u;
-  const uint32_t dx = min((uint32_t)max((int)(dsym >> 1) - 1, 0), 14u);
-  const uint32_t dist = ((2u + (dsym & 1u)) << dx) + 1u - (dsym < 2u ? 2u : 0u) +
-                        ((uint32_t)(s.hold >> dused) & ((1u << dx) - 1u));
-  const uint32_t dcons = isl ? dused + dx : 0u;
-  s.hold >>= dcons;
-  s.nbits -= dcons;
-  bad |= (uint32_t)(kind >= CK_EOB) | (isl & (uint32_t)((d & 3u) == CK_SLOW));
-  need = max(need, (isl && dist > s.pos) ? dist - s.pos : 0u);
-  if (D64 && len > 0xffffu) {  // a deflate64 copy longer than a token holds: two copies, same distance
-    tb[s.gk * WAVE] = (0xffffu << 16) | (dist - 1u);
-    s.gk++;
-    s.ntok++;
-    tb[s.gk * WAVE] = ((len - 0xffffu) << 16) | (dist - 1u);
-  } else {
-    tb[s.gk * WAVE] = isl ? ((len << 16) | (dist - 1u)) : sym;
-  }
-  s.gk++;
-  s.ntok++;
-  s.pos += len;
-}
-
 // Wide tables of the split decode (one copy per wave, so LDS is cheap): u32
 // entries that carry everything a symbol needs -- code bits, extra-bit count
 // and the literal or the length / distance base -- so a step does no base
@@ -2375,7 +2390,8 @@ __device__ __forceinline__ void split_step(LaneState &s, const uint16_t *__restr
 //   literal / length, 9-bit index: [3:0] code bits, [5:4] kind (SK_*),
 //     [10:6] extra bits, [31:16] literal byte or length base
 //   distance, 8-bit index: [3:0] code bits, [4] long code (canonical tail),
-//     [5] invalid code, [10:6] extra bits, [31:16] distance base
+//     [5] invalid code, [10:6] extra bits, [31:16] distance base - 1 (the
+//     token's field)
 #define SPL_BITS 9u
 #define SPD_BITS 8u
 enum { SK_LIT = 0, SK_LEN = 1, SK_EOB = 2, SK_SLOW = 3 };
@@ -2396,73 +2412,214 @@ __device__ __forceinline__ uint32_t split_dist_entry(uint32_t ce, bool d64) {  /
   if (!d64 && dsym >= 30u) return 0x20u;
   const uint32_t dx = dsym < 4u ? 0u : (dsym >> 1) - 1u;
   const uint32_t base = dsym < 4u ? dsym + 1u : ((2u + (dsym & 1u)) << dx) + 1u;  // src/inftrees.c:65-72
-  return bits | (dx << 6) | (base << 16);
+  return bits | (dx << 6) | ((base - 1u) << 16);
 }
 
-struct __attribute__((aligned(16))) SplitLDS {
-  uint16_t lroot[LROOT_N];  // the block's table image (zs_unit_header_kernel), shared by the wave
-  uint16_t droot[DROOT_N];
-  uint32_t dtail[DTAIL_BYTES / 4];
-  uint32_t lw[1u << SPL_BITS];  // the wide tables (SPLIT_WIDE)
-  uint32_t dw[1u << SPD_BITS];
-  uint32_t tokbuf[GROUP][WAVE];
-  uint32_t ring[RING][WAVE];
-};
-#define SPLIT_IMG_U4 ((LROOT_N * 2 + DROOT_N * 2 + DTAIL_BYTES) / 16)
-#ifndef SPLIT_WIDE
-#define SPLIT_WIDE 1  // the wide tables (0: lane_step_fast's compact 8 / 6-bit roots)
-#endif
-
-// the split step on the wide tables
+// The split decode reads its input like the walk: an absolute bit position p
+// per lane over a ring row of 32 words (two halves of 16, the older half
+// refilled from a prefetch that stays in flight), three words giving the 64
+// bits from p -- every field of a symbol (code, extra bits, distance code,
+// distance extra bits: <= 48 bits, deflate64 60) is one funnel shift of them.
+#define SP_GS(d64) ((d64) ? 7u : 8u)  // steps per group (<= 17 ring words ahead, as the walk's groups)
 template <bool D64>
-__device__ __forceinline__ void split_step_w(LaneState &s, const uint32_t *__restrict__ lw, const uint32_t *__restrict__ dw,
-                                             uint32_t *__restrict__ tb, const uint32_t *__restrict__ dtl,
-                                             const uint32_t *__restrict__ rp, uint32_t &bad, uint32_t &need) {
-  lane_refill_bf(s, rp);
-  uint32_t e = lw[(uint32_t)s.hold & ((1u << SPL_BITS) - 1u)];
-  if (__builtin_expect(__ballot(((e >> 4) & 3u) == SK_SLOW) != 0, 0)) {
-    if (((e >> 4) & 3u) == SK_SLOW) {  // longer than 9 bits: zlib's 9-bit root and sub-table (compact, global)
-      uint32_t e2 = s.cl[(uint32_t)s.hold & ((1u << s.lbits) - 1u)];
+struct __attribute__((aligned(16))) SplitLDS {
+  uint32_t lw[1u << SPL_BITS];
+  uint32_t dw[1u << SPD_BITS];
+  uint32_t dtail[DTAIL_BYTES / 4];
+  uint32_t tokbuf[D64 ? 2u * SP_GS(true) : 1u][WAVE];  // deflate64: a group's tokens (two per step at most); else in registers
+  uint32_t ring[WAVE][WK_RS];
+};
+struct SplitLane {
+  uint32_t p, ntok, pos, need, bad, gk;
+};
+
+// one symbol of a walked sub-unit.  Every symbol before the sub-unit's end is
+// a literal or a length (the walk met them), so anything else only marks the
+// lane bad (bit 0x20 of t.bad: the unit is decoded again from its start).
+template <bool D64, bool NEEDC>
+__device__ __forceinline__ void split_step3(SplitLane &t, uint32_t rra, const uint32_t *__restrict__ lw,
+                                            const uint32_t *__restrict__ dw, uint32_t *__restrict__ tb, uint32_t *tr,
+                                            uint4 dta, uint4 dtb, const uint32_t *__restrict__ dtl, gcu16 *cl,
+                                            uint32_t lbits) {
+  typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
+  lds_cu32 *r = (lds_cu32 *)(uintptr_t)(rra + ((t.p >> 3) & ((WK_RW - 1u) * 4u)));
+  const uint32_t x0 = r[0], x1 = r[1], x2 = r[2];
+  const uint32_t hl = __builtin_amdgcn_alignbit(x1, x0, t.p), hh = __builtin_amdgcn_alignbit(x2, x1, t.p);
+  uint32_t e = lw[hl & ((1u << SPL_BITS) - 1u)];
+  if (__builtin_expect(__builtin_amdgcn_ballot_w64(((e >> 4) & 3u) == SK_SLOW) != 0, 0)) {
+    if (((e >> 4) & 3u) == SK_SLOW) {  // longer than 9 bits: zlib's root and sub-table (compact, global)
+      uint32_t e2 = cl[hl & ((1u << lbits) - 1u)];
       const uint32_t op2 = (e2 >> 2) & 15u;
-      if ((e2 & 3u) == CK_SLOW && op2) e2 = s.cl[(e2 >> 6) + (((uint32_t)s.hold >> s.lbits) & ((1u << op2) - 1u))];
+      if ((e2 & 3u) == CK_SLOW && op2) e2 = cl[(e2 >> 6) + ((hl >> lbits) & ((1u << op2) - 1u))];
       e = split_len_entry<D64>(e2);
     }
   }
-  const uint32_t cb = e & 15u, kind = (e >> 4) & 3u, xb = (e >> 6) & 31u;
-  const uint32_t isl = kind == SK_LEN;
-  s.hold >>= cb;
-  const uint32_t len = isl ? (e >> 16) + ((uint32_t)s.hold & ((1u << xb) - 1u)) : 1u;
-  s.hold >>= xb;
-  s.nbits -= cb + xb;
-  lane_refill_bf(s, rp);
-  uint32_t d = dw[(uint32_t)s.hold & ((1u << SPD_BITS) - 1u)];
-  if (__builtin_expect(__ballot(isl && (d & 0x10u)) != 0, 0)) {
-    // a distance code longer than 8 bits: canonical decode from the tail
-    const uint32_t de = dist_tail_r(s.dta, s.dtb, dtl, (uint32_t)s.hold);
-    if (isl && (d & 0x10u)) d = split_dist_entry(de, D64);
+  const uint32_t cb = e & 15u, xb = (e >> 6) & 31u;
+  const bool isl = (e & 0x10u) != 0;  // SK_LEN (SK_SLOW is resolved above; what stays invalid is marked bad below)
+  const uint32_t len = (e >> 16) + __builtin_amdgcn_ubfe(__builtin_amdgcn_alignbit(hh, hl, cb), 0, xb);  // literal: its byte
+  const uint32_t k2 = cb + xb;  // <= 31
+  const uint32_t c = __builtin_amdgcn_alignbit(hh, hl, k2);
+  uint32_t d = dw[c & ((1u << SPD_BITS) - 1u)];
+  if (__builtin_expect(__builtin_amdgcn_ballot_w64((d & e & 0x10u) != 0) != 0, 0)) {
+    // a length's distance code longer than 8 bits: canonical decode from the tail
+    if (d & e & 0x10u) d = split_dist_entry(dist_tail_r(dta, dtb, dtl, c), D64);
   }
-  const uint32_t dcb = d & 15u, dx = (d >> 6) & 31u;
-  const uint32_t dist = (d >> 16) + ((uint32_t)(s.hold >> dcb) & ((1u << dx) - 1u));
-  const uint32_t dcons = isl ? dcb + dx : 0u;
-  s.hold >>= dcons;
-  s.nbits -= dcons;
-  bad |= (uint32_t)(kind >= SK_EOB) | (isl & (uint32_t)((d & 0x30u) != 0));
-  need = max(need, (isl && dist > s.pos) ? dist - s.pos : 0u);
-  if (D64 && len > 0xffffu) {  // a deflate64 copy longer than a token holds: two copies, same distance
-    tb[s.gk * WAVE] = (0xffffu << 16) | (dist - 1u);
-    s.gk++;
-    s.ntok++;
-    tb[s.gk * WAVE] = ((len - 0xffffu) << 16) | (dist - 1u);
+  const uint32_t k3 = k2 + (d & 15u), dx = (d >> 6) & 31u;  // k3 <= 46, + dx <= 60
+  const uint32_t dxv = (uint32_t)((((uint64_t)hh << 32) | hl) >> k3);
+  const uint32_t dm1 = (d >> 16) + __builtin_amdgcn_ubfe(dxv, 0, dx);  // distance - 1
+  t.p += isl ? k3 + dx : k2;
+  t.bad |= e | (isl ? d : 0u);  // bit 0x20: end of block / unresolved code / invalid distance
+  if (NEEDC) t.need = max(t.need, (isl && dm1 >= t.pos) ? dm1 + 1u - t.pos : 0u);
+  if (!D64) {
+    *tr = isl ? ((len << 16) | dm1) : len;  // a register of the group (the step index is a constant)
+  } else if (__builtin_expect(__builtin_amdgcn_ballot_w64(isl && len > 0xffffu) != 0, 0)) {
+    // a deflate64 copy longer than a token holds: two copies, same distance
+    if (isl && len > 0xffffu) {
+      tb[t.gk * WAVE] = (0xffffu << 16) | dm1;
+      t.gk++;
+      t.ntok++;
+      tb[t.gk * WAVE] = ((len - 0xffffu) << 16) | dm1;
+    } else {
+      tb[t.gk * WAVE] = isl ? ((len << 16) | dm1) : len;
+    }
   } else {
-    tb[s.gk * WAVE] = isl ? ((len << 16) | (dist - 1u)) : (e >> 16);
+    tb[t.gk * WAVE] = isl ? ((len << 16) | dm1) : len;
   }
-  s.gk++;
-  s.ntok++;
-  s.pos += len;
+  t.gk++;
+  t.ntok++;
+  t.pos += isl ? len : 1u;
 }
-#ifndef SPLIT_PRE
-#define SPLIT_PRE 1  // the next group's input words loaded during the flush (0: at the group start)
+
+// a lane's sub-unit, group by group: refill, SP_GS steps (guarded only when
+// some lane is within a group of its end), then the group's tokens leave in
+// 16-byte transposed stores (zs_lane_kernel's flush)
+template <bool D64, bool NEEDC>
+__device__ __forceinline__ void split_sub3(SplitLDS<D64> &L, SplitLane &t, LaneState &s, uint32_t t1, uint32_t &filled,
+                                           uint32_t (&pre)[WK_PF], uint32_t rra, uint4 dta, uint4 dtb,
+                                           uint32_t *__restrict__ tokens, const ZsTokPool &pool, bool act
+#if KP_ON
+                                           , uint64_t &kp_grp, uint32_t &kp_ws
 #endif
+) {
+  const uint32_t lane = threadIdx.x;
+  uint32_t *tb = &L.tokbuf[0][lane];
+  uint32_t *rr = &L.ring[lane][0];
+  constexpr uint32_t GS = SP_GS(D64), TPS = D64 ? 2u : 1u;
+  for (;;) {
+    const bool run = act && t.ntok < t1 && !(t.bad & 0x20u) && t.pos <= s.capx;
+    if (__builtin_amdgcn_ballot_w64(run) == 0) break;
+#if KP_ON
+    const uint64_t kg0 = KP_NOW();
+#endif
+    {  // a lane that has consumed its older half refills it from the prefetch
+      const bool wr = run && filled - (t.p >> 5) <= WK_RW - WK_PF;
+      if (__builtin_amdgcn_ballot_w64(wr)) {
+        if (wr) {
+          walk_put_half(rr, filled, pre, s.end_byte);
+          filled += WK_PF;
+          walk_prefetch(s, filled, pre);
+        }
+      }
+    }
+#if KP_ON
+    kp_grp += KP_NOW() - kg0;
+    kp_ws += lane == (uint32_t)__builtin_ctzll(__ballot(1)) ? GS : 0u;
+#endif
+    t.gk = 0;
+    const uint32_t g0 = t.ntok;
+    uint32_t tk[GS];  // the group's tokens (!D64: registers; deflate64: tokbuf)
+    if (__builtin_amdgcn_ballot_w64(run && t1 - t.ntok < GS * TPS) == 0) {
+      if (run) {
+#pragma unroll
+        for (uint32_t g = 0; g < GS; g++)
+          split_step3<D64, NEEDC>(t, rra, L.lw, L.dw, tb, &tk[g], dta, dtb, L.dtail, s.cl, s.lbits);
+      }
+    } else {
+      if (run) {
+#pragma unroll
+        for (uint32_t g = 0; g < GS; g++)
+          if (t.ntok < t1) split_step3<D64, NEEDC>(t, rra, L.lw, L.dw, tb, &tk[g], dta, dtb, L.dtail, s.cl, s.lbits);
+      }
+    }
+    if (t.ntok > t1) {  // an inconsistent decode: never write past the walked tokens
+      t.bad |= 0x20u;
+      t.gk -= min(t.gk, t.ntok - t1);
+      t.ntok = t1;
+    }
+    if (!D64) {  // each lane stores its own tokens: two 16-byte stores for a whole group
+#if KP_ON
+      const uint64_t kf0 = KP_NOW();
+#endif
+      if (run) {
+        if (t.gk == GS && t.ntok <= s.tcap) {
+          typedef uint32_t u32x4a4t __attribute__((ext_vector_type(4), aligned(4)));
+          u32x4a4t v0, v1;
+          v0.x = tk[0]; v0.y = tk[1]; v0.z = tk[2]; v0.w = tk[3];
+          v1.x = tk[4]; v1.y = tk[5]; v1.z = tk[6]; v1.w = tk[7];
+          gu32 *dst = s.tok + g0;
+          *reinterpret_cast<__attribute__((address_space(1))) u32x4a4t *>(dst) = v0;
+          *reinterpret_cast<__attribute__((address_space(1))) u32x4a4t *>(dst + 4) = v1;
+        } else {
+          const uint64_t prim_off = (uint64_t)((const uint32_t *)s.tok - tokens);
+#pragma unroll
+          for (uint32_t j = 0; j < GS; j++)
+            if (j < t.gk) {
+              if (g0 + j < s.tcap) s.tok[g0 + j] = tk[j];
+              else *tok_addr(pool, tokens, s.unit, prim_off, s.tcap, g0 + j) = tk[j];
+            }
+        }
+      }
+#if KP_ON
+      kp_grp += KP_NOW() - kf0;
+#endif
+      continue;
+    }
+    __builtin_amdgcn_wave_barrier();
+#if KP_ON
+    const uint64_t kf0 = KP_NOW();
+#endif
+    {  // 16-byte transposed stores of full token quads
+      typedef uint32_t u32x4a4t __attribute__((ext_vector_type(4), aligned(4)));
+      const uint32_t q = lane >> 4;
+      const uint32_t nq = (run && t.ntok <= s.tcap) ? (t.gk >> 2) : 0u;
+      const uintptr_t dst = (uintptr_t)(s.tok + g0);
+#pragma unroll
+      for (uint32_t rq = 0; rq < (GS * TPS + 15u) / 16u; rq++) {
+#pragma unroll
+        for (uint32_t r = 0; r < 4; r++) {
+          const uint32_t src = 16u * r + (lane & 15u);
+          const uint32_t nq_s = (uint32_t)__shfl((int)nq, (int)src);
+          const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)dst, (int)src);
+          const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)((uint64_t)dst >> 32), (int)src);
+          const uint32_t qq = q + 4u * rq;
+          if (qq < nq_s) {
+            u32x4a4t v;
+            v.x = L.tokbuf[4 * qq][src];
+            v.y = L.tokbuf[4 * qq + 1][src];
+            v.z = L.tokbuf[4 * qq + 2][src];
+            v.w = L.tokbuf[4 * qq + 3][src];
+            *reinterpret_cast<__attribute__((address_space(1))) u32x4a4t *>(((uint64_t)hi << 32 | lo) + 16u * qq) = v;
+          }
+        }
+      }
+    }
+    if (run) {
+      if (t.ntok <= s.tcap) {
+        const uint32_t t0 = t.gk & ~3u;
+#pragma unroll
+        for (uint32_t j = 0; j < 3; j++)
+          if (t0 + j < t.gk) s.tok[g0 + t0 + j] = L.tokbuf[t0 + j][lane];
+      } else {  // past the primary region: pool pages (taken by the walk)
+        const uint64_t prim_off = (uint64_t)((const uint32_t *)s.tok - tokens);
+        for (uint32_t j = 0; j < t.gk; j++) *tok_addr(pool, tokens, s.unit, prim_off, s.tcap, g0 + j) = L.tokbuf[j][lane];
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // tokbuf is rewritten by the next group
+#if KP_ON
+    kp_grp += KP_NOW() - kf0;
+#endif
+  }
+}
 
 template <bool D64>
 __global__ void __launch_bounds__(64) zs_split_kernel(const ZsJobDev *__restrict__ jobs, ZsChunkDev *__restrict__ chunks,
@@ -2470,10 +2627,11 @@ __global__ void __launch_bounds__(64) zs_split_kernel(const ZsJobDev *__restrict
                                                        const uint32_t *__restrict__ tables, ZsTokPool pool,
                                                        ZsWalkDev *__restrict__ walks, const uint2 *__restrict__ cps,
                                                        uint32_t *__restrict__ lists, uint32_t *__restrict__ counts) {
-  __shared__ SplitLDS L;
+  __shared__ SplitLDS<D64> L;
   const uint32_t lane = threadIdx.x;
   const uint32_t nsplit = counts[0];
   constexpr uint32_t HMAX = D64 ? 65536u : HIST;
+  typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
 #if KP_ON
   const uint64_t kp_t0 = KP_NOW();
   uint64_t kp_grp = 0;
@@ -2488,10 +2646,8 @@ __global__ void __launch_bounds__(64) zs_split_kernel(const ZsJobDev *__restrict
     const ZsChunkDev ch = chunks[c];
     const ZsJobDev jb = jobs[ch.job];
     const uint32_t *tabg = tables + (size_t)c * TABLE_STRIDE;
-    __builtin_amdgcn_wave_barrier();  // the previous unit is done with the image
-    if (lane < SPLIT_IMG_U4)
-      reinterpret_cast<uint4 *>(&L)[lane] = reinterpret_cast<const uint4 *>(tabg + TABLE_IMG_OFF)[lane];
-    if (SPLIT_WIDE) {  // the wide tables, from the unit's compact tables (zlib layout, roots lbits / dbits)
+    __builtin_amdgcn_wave_barrier();  // the previous unit is done with the tables
+    {  // the wide tables from the unit's compact tables (zlib layout, roots lbits / dbits)
       const uint16_t *ccl = reinterpret_cast<const uint16_t *>(tabg + TABLE_ENTRIES), *ccd = ccl + DIST_TABLE_OFF;
       const uint32_t lb = (ch.hdr_info >> 8) & 15u, db = (ch.hdr_info >> 12) & 15u;
 #pragma unroll
@@ -2514,6 +2670,7 @@ __global__ void __launch_bounds__(64) zs_split_kernel(const ZsJobDev *__restrict
         }
         L.dw[i] = v;
       }
+      if (lane < DTAIL_BYTES / 4) L.dtail[lane] = tabg[TABLE_IMG_OFF + (LROOT_N + DROOT_N) / 2 + lane];
     }
     const bool act = lane < wk.nsub;
     const uint2 *cpu = cps + (size_t)c * WK_CP;
@@ -2526,121 +2683,67 @@ __global__ void __launch_bounds__(64) zs_split_kernel(const ZsJobDev *__restrict
     s.w = (gcu32 *)(ip - mis);
     s.end_byte = mis + (uint32_t)jb.in_len;
     s.limit = s.end_byte * 8u;
+    s.lastw = (s.end_byte - 1u) >> 2;
     s.tok = (gu32 *)(tokens + ch.tok);
     s.tcap = ch.tcap;
     s.unit = c;
     s.lbits = (ch.hdr_info >> 8) & 15u;
     s.cl = (gcu16 *)(tabg + TABLE_ENTRIES);
     s.capx = ch.cap;
-    s.pos = 0;
-    s.ntok = a.y;
-    s.gk = s.rk = 0;
-    s.wi = s.nw = s.nkeep = s.nbits = s.lastw = 0;
-    s.hold = 0;
     const uint32_t t1 = b.y, b1 = b.x;
-    if (act) lane_prime(s, a.x);
+    SplitLane t;
+    t.p = a.x;
+    t.ntok = a.y;
+    t.pos = t.need = t.bad = t.gk = 0;
+    uint32_t *rr = &L.ring[lane][0];
+    uint32_t filled = (t.p >> 5) & ~(WK_PF - 1u), pre[WK_PF];
+    if (act) {  // both halves now (words filled .. filled + 31), then the next prefetch
+      walk_prefetch(s, filled, pre);
+      uint32_t pre2[WK_PF];
+      walk_prefetch(s, filled + WK_PF, pre2);
+      walk_put_half(rr, filled, pre, s.end_byte);
+      walk_put_half(rr, filled + WK_PF, pre2, s.end_byte);
+      filled += WK_RW;
+      walk_prefetch(s, filled, pre);
+    }
+    uint32_t rra = (uint32_t)(uintptr_t)(lds_cu32 *)rr;
+    asm volatile("" : "+v"(rra));
     __builtin_amdgcn_wave_barrier();
+    uint4 dta, dtb;
     {  // the distance tail header is the same for every lane: scalar registers
       const uint4 x = *reinterpret_cast<const uint4 *>(L.dtail), y = *reinterpret_cast<const uint4 *>(L.dtail + 4);
-      s.dta = make_uint4(uni(x.x), uni(x.y), uni(x.z), uni(x.w));
-      s.dtb = make_uint4(uni(y.x), uni(y.y), uni(y.z), uni(y.w));
+      dta = make_uint4(uni(x.x), uni(x.y), uni(x.z), uni(x.w));
+      dtb = make_uint4(uni(y.x), uni(y.y), uni(y.z), uni(y.w));
     }
-    const uint16_t *lt = L.lroot;
-    const uint16_t *dt = L.droot;
-    uint32_t *tb = &L.tokbuf[0][lane];
-    uint32_t *rp = &L.ring[0][lane];
-    uint32_t bad = 0, need = 0, full = 0;
-    uint32_t pre[RING];
-    uint32_t pre_wi = ~0u;
-    for (;;) {
-      const bool run = act && !bad && !full && s.ntok < t1;
-      if (__ballot(run) == 0) break;
-      s.gk = 0;
+    const uint32_t whave = ch.ord == 0 ? ((jb.flags & ZS_JF_CONT) ? min(jb.hist, HMAX) : 0u) : HMAX;
+    if (whave < HMAX)  // only a stream's first unit can reach before its window
+      split_sub3<D64, true>(L, t, s, t1, filled, pre, rra, dta, dtb, tokens, pool, act
 #if KP_ON
-      const uint64_t kg0 = KP_NOW();
+                            , kp_grp, kp_ws
 #endif
-      if (run) {
-        if (s.wi == pre_wi) lane_store_ring(s, rp, pre);
-        else lane_fill_ring(s, rp);
+      );
+    else
+      split_sub3<D64, false>(L, t, s, t1, filled, pre, rra, dta, dtb, tokens, pool, act
 #if KP_ON
-        __builtin_amdgcn_s_waitcnt(0);
-        kp_grp += KP_NOW() - kg0;
+                             , kp_grp, kp_ws
 #endif
-        while (!bad && !full && s.ntok < t1 && s.gk + (D64 ? 2u : 1u) <= GROUP && s.rk + 2 < RING) {
-#if KP_ON
-          kp_ws += lane_id() == (uint32_t)__builtin_ctzll(__ballot(1)) ? 1u : 0u;
-#endif
-          if (SPLIT_WIDE)
-            split_step_w<D64>(s, L.lw, L.dw, tb, L.dtail, rp, bad, need);
-          else
-            split_step<D64>(s, lt, dt, tb, L.dtail, rp, bad, need);
-          full |= s.pos > s.capx;
-        }
-        if (s.ntok > t1) {  // an inconsistent decode: never write past the walked tokens
-          bad = 1;
-          s.gk -= min(s.gk, s.ntok - t1);
-          s.ntok = t1;
-        }
-      }
-      __builtin_amdgcn_wave_barrier();
-#if KP_ON
-      const uint64_t kf0 = KP_NOW();
-#endif
-      // the next group's input words, loaded before this group's tokens leave
-      const bool more = run && !bad && !full && s.ntok < t1;
-      pre_wi = (SPLIT_PRE && more) ? s.wi : ~0u;
-      if (SPLIT_PRE && more) lane_load_ring(s, pre);
-      const uint32_t g0 = s.ntok - s.gk;
-      {  // 16-byte transposed stores of full token quads (zs_lane_kernel's flush)
-        typedef uint32_t u32x4a4t __attribute__((ext_vector_type(4), aligned(4)));
-        const uint32_t q = lane >> 4;
-        const uint32_t nq = s.ntok <= s.tcap ? (s.gk >> 2) : 0u;
-        const uintptr_t dst = (uintptr_t)(s.tok + g0);
-#pragma unroll
-        for (uint32_t r = 0; r < 4; r++) {
-          const uint32_t src = 16u * r + (lane & 15u);
-          const uint32_t nq_s = (uint32_t)__shfl((int)nq, (int)src);
-          const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)dst, (int)src);
-          const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)((uint64_t)dst >> 32), (int)src);
-          if (q < nq_s) {
-            u32x4a4t v;
-            v.x = L.tokbuf[4 * q][src];
-            v.y = L.tokbuf[4 * q + 1][src];
-            v.z = L.tokbuf[4 * q + 2][src];
-            v.w = L.tokbuf[4 * q + 3][src];
-            *reinterpret_cast<__attribute__((address_space(1))) u32x4a4t *>(((uint64_t)hi << 32 | lo) + 16u * q) = v;
-          }
-        }
-      }
-      if (s.ntok <= s.tcap) {
-        const uint32_t t0 = s.gk & ~3u;
-#pragma unroll
-        for (uint32_t j = 0; j < 3; j++)
-          if (t0 + j < s.gk) s.tok[g0 + t0 + j] = L.tokbuf[t0 + j][lane];
-      } else {  // past the primary region: pool pages (taken by the walk)
-        const uint64_t prim_off = (uint64_t)((const uint32_t *)s.tok - tokens);
-        for (uint32_t j = 0; j < s.gk; j++) *tok_addr(pool, tokens, s.unit, prim_off, s.tcap, g0 + j) = L.tokbuf[j][lane];
-      }
-      __builtin_amdgcn_wave_barrier();  // tokbuf is rewritten by the next group
-#if KP_ON
-      kp_grp += KP_NOW() - kf0;
-#endif
-    }
-    if (act && !full && (lane_pos(s) != b1 || s.ntok != t1)) bad = 1;
-    const bool anybad = __ballot(bad) != 0, anyfull = __ballot(full) != 0;
+      );
+    const bool full = act && t.pos > s.capx;
+    uint32_t bad = (t.bad & 0x20u) ? 1u : 0u;
+    if (act && !full && (t.p != b1 || t.ntok != t1)) bad = 1;
+    const bool anybad = __ballot(act && bad) != 0, anyfull = __ballot(full) != 0;
     // output position of every sub-unit: a wave scan of their entry counts
-    uint64_t incl = act ? s.pos : 0u;
+    uint64_t incl = act ? t.pos : 0u;
 #pragma unroll
     for (uint32_t o = 1; o < WAVE; o <<= 1) {
       const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)incl, o);
       const uint32_t hi = (uint32_t)__shfl_up((int)(uint32_t)(incl >> 32), o);
       if (lane >= o) incl += ((uint64_t)hi << 32) | lo;
     }
-    const uint64_t P = incl - (act ? s.pos : 0u);
+    const uint64_t P = incl - (act ? t.pos : 0u);
     const uint64_t total = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(incl >> 32), WAVE - 1) << 32) |
                            __builtin_amdgcn_readlane((uint32_t)incl, WAVE - 1);
-    const uint32_t whave = ch.ord == 0 ? ((jb.flags & ZS_JF_CONT) ? min(jb.hist, HMAX) : 0u) : HMAX;
-    const bool far = whave < HMAX && __ballot(act && (uint64_t)need > P + whave) != 0;
+    const bool far = whave < HMAX && __ballot(act && (uint64_t)t.need > P + whave) != 0;
     if (lane == 0) {
       ZsChunkDev *o = &chunks[c];
       if (anybad) {  // decode again from the start (never expected)
@@ -3332,10 +3435,12 @@ __global__ void __launch_bounds__(64) zs_unit_header_kernel(const ZsJobDev *__re
     for (uint32_t i = lane; i < (1u << WK_DBITS); i += WAVE) walk[(1u << WK_LBITS) + i] = (uint8_t)walk_dist_z(fixed + 512, 5u, i);
     __builtin_amdgcn_wave_barrier();
     if (lane == 0) build_dist_tail(B.lens, 32, reinterpret_cast<uint8_t *>(img + LROOT_N + DROOT_N));
+    if (lane < 8) tabg[TABLE_LTAIL_OFF + lane] = lane < 4 ? 0x80008000u : 0u;  // no code past 9 bits
     lbits = 9;
     dbits = 5;
   } else if (wave_dyn_header<D64>(B, w, end_byte, bit, tabg, ctab, lbits, dbits, img, img + LROOT_N,
-                                  reinterpret_cast<uint8_t *>(img + LROOT_N + DROOT_N), walk)) {
+                                  reinterpret_cast<uint8_t *>(img + LROOT_N + DROOT_N), walk,
+                                  tabg + TABLE_LTAIL_OFF)) {
     return;
   }
   if (lane == 0) {
