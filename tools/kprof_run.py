@@ -92,6 +92,7 @@ def main():
         "walk_exc_cycles_per_step": d.get("w_cyc_exc", 0) / max(d.get("w_wave_steps", 0), 1),
         "walk_group_cycles_per_step": d.get("w_cyc_group", 0) / max(d.get("w_wave_steps", 0), 1),
         "walk_steps_cycles_per_step": d.get("p_cyc_steps", 0) / max(d.get("w_wave_steps", 0), 1),
+        "walk_refill_cycles_per_step": d.get("p_cyc_busy", 0) / max(d.get("w_wave_steps", 0), 1),
         "walk_exc_per_step": d.get("w_exc", 0) / max(d.get("w_wave_steps", 0), 1),
         "split_cycles_per_wave_step": d.get("s_lit", 0) / max(d.get("s_refill2", 0), 1),
     }

@@ -115,10 +115,12 @@ __device__ __forceinline__ uint16_t compact_dist_entry(uint32_t z, uint32_t add_
 #define WK_EXC 0x40u
 #define WK_BIG 0x80u
 #define WK_BAD (WK_EXC | WK_BIG)
+#define WK_EOBE (WK_EXC | WK_HASD)  // end-of-block entry: | its code bits
 template <bool D64>
 __device__ __forceinline__ uint32_t walk_len_entry(uint32_t ce) {  // from a compact literal/length entry
   const uint32_t kind = ce & 3u, bits = (ce >> 2) & 15u, sym = ce >> 6;
   if (kind == CK_SYM) return bits;
+  if (kind == CK_EOB) return WK_EOBE | bits;  // end of block: its code bits (resolved without the tables)
   if (kind != CK_LEN) return WK_EXC;
   const uint32_t xb = sym < 8u ? 0u : (sym < 28u ? (sym >> 2) - 1u : (D64 ? 16u : 0u));
   return (bits + xb) | WK_HASD | ((D64 && sym >= 28u) ? WK_BIG : 0u);
@@ -732,39 +734,70 @@ __device__ void build_dist_tail(const uint16_t *dl, uint32_t n, uint8_t *out) {
 }
 
 // The literal/length code's canonical tail for the split parse's walk (codes
-// longer than its 9-bit table): words 0-3 the left-justified 15-bit limits
-// of lengths 9..15 (u16 each, lim[L] = (first[L] + count[L]) << (15 - L)),
-// words 4-5 the literal count of each length 10..15 (u8, capped at 255).
-// Canonical order puts a length's literals first (symbols < 256), so a long
-// code whose index within its length is below that count is a literal --
-// its walk entry is just its length, found without the global tables.
-// Wave-cooperative (every lane calls it): the per-length counts by ballots,
-// 64 code lengths at a time, then lane 0 writes the 8 words.
+// longer than its 9-bit table), 16 words: 0-3 the left-justified 15-bit
+// limits of lengths 9..15 (u16 each, lim[L] = (first[L] + count[L]) << (15 - L)),
+// 4-5 the literal count of each length 10..15 (u8, capped at 255), 6-7 for
+// each length 10..15 the index in the list below of its first symbol >= 256
+// (u8), 8-15 that list: the symbols >= 256 (end of block, lengths) whose codes
+// are longer than 9 bits, in canonical order, as sym - 256 (u8).  Canonical
+// order puts a length's literals first, then its symbols >= 256 in order, so
+// a long code's index within its length tells a literal from the list entry
+// -- the walk resolves every code from registers and LDS, no global table.
+// Wave-cooperative (every lane calls it): counts by ballots, 64 code lengths
+// at a time; lanes 0..15 write the 16 words.
 __device__ void build_lit_tail(const uint16_t *ll, uint32_t n, uint32_t *out) {
   const uint32_t lane = lane_id();
-  uint32_t cnt = 0, nl = 0;  // lane L (1..15): codes of length L, and literals among them
+  uint32_t cnt = 0, nl = 0, nn = 0;  // lane L (1..15): codes of length L, literals, symbols >= 256 among them
+  uint32_t lst = 0;                  // lane k (0..31): list byte k
+  uint32_t base = 0;                 // running list position (uniform)
   for (uint32_t b = 0; b < n; b += WAVE) {
     const uint32_t i = b + lane;
     const uint32_t len = i < n ? (ll[i] & 15u) : 0u;
 #pragma unroll
     for (uint32_t L = 1; L < 16; L++) {
-      const uint32_t c = (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(len == L));
+      const uint64_t m = __builtin_amdgcn_ballot_w64(len == L);
+      const uint32_t c = (uint32_t)__builtin_popcountll(m);
       const uint32_t cl = (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(len == L && i < 256u));
       cnt += lane == L ? c : 0u;
       nl += lane == L ? cl : 0u;
+      nn += lane == L ? c - cl : 0u;
     }
   }
-  uint32_t code = 0, lim[16], nlit[16];
+  // the list: symbols 256.. sit in the chunk at 256 (lane k: symbol 256 + k);
+  // each lane's rank in canonical order, then list byte t = the lane ranked t
+  {
+    const uint32_t i = 256u + lane;
+    const uint32_t len = i < n ? (ll[i] & 15u) : 0u;
+    uint32_t rank = 64u;
+#pragma unroll
+    for (uint32_t L = 10; L < 16; L++) {
+      const uint64_t m = __builtin_amdgcn_ballot_w64(len == L);
+      if (len == L) rank = base + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull));
+      base += (uint32_t)__builtin_popcountll(m);
+    }
+    for (uint32_t t = 0; t < min(base, 32u); t++) {
+      const uint64_t hit = __builtin_amdgcn_ballot_w64(rank == t);
+      lst = lane == t ? (uint32_t)__builtin_ctzll(hit) : lst;
+    }
+  }
+  uint32_t code = 0, lim[16], nlit[16], nbase[16];
   lim[0] = nlit[0] = 0;
-  uint32_t prev = 0;
+  uint32_t prev = 0, nb = 0;
 #pragma unroll
   for (int L = 1; L < 16; L++) {
     const uint32_t cL = __builtin_amdgcn_readlane(cnt, L);
     nlit[L] = __builtin_amdgcn_readlane(nl, L);
+    nbase[L] = nb;
+    if (L >= 10) nb += __builtin_amdgcn_readlane(nn, L);
     code = (code + prev) << 1;
     lim[L] = min((code + cL) << (15 - L), 0xffffu);
     prev = cL;
   }
+  // list bytes: lane k holds byte k; pack 4 per word
+  const uint32_t b0 = __shfl(lst, (int)((lane & 7u) * 4u)), b1 = __shfl(lst, (int)((lane & 7u) * 4u + 1u));
+  const uint32_t b2 = __shfl(lst, (int)((lane & 7u) * 4u + 2u)), b3 = __shfl(lst, (int)((lane & 7u) * 4u + 3u));
+  const uint32_t lw = (b0 & 0xffu) | ((b1 & 0xffu) << 8) | ((b2 & 0xffu) << 16) | ((b3 & 0xffu) << 24);
+  if (lane < 8u) out[8 + lane] = lw;
   if (lane == 0) {
     out[0] = lim[9] | (lim[10] << 16);
     out[1] = lim[11] | (lim[12] << 16);
@@ -772,7 +805,8 @@ __device__ void build_lit_tail(const uint16_t *ll, uint32_t n, uint32_t *out) {
     out[3] = lim[15];
     out[4] = min(nlit[10], 255u) | (min(nlit[11], 255u) << 8) | (min(nlit[12], 255u) << 16) | (min(nlit[13], 255u) << 24);
     out[5] = min(nlit[14], 255u) | (min(nlit[15], 255u) << 8);
-    out[6] = out[7] = 0;
+    out[6] = nbase[10] | (nbase[11] << 8) | (nbase[12] << 16) | (nbase[13] << 24);
+    out[7] = nbase[14] | (nbase[15] << 8);
   }
 }
 
@@ -1920,9 +1954,6 @@ __global__ void __launch_bounds__(64) zs_unitw_list_kernel(const ZsJobDev *__res
 #endif
 static_assert(WKL_BITS + 1u >= WK_LBITS && WKL_BITS <= WK_LBITS && WKD_BITS + 1u >= WK_DBITS && WKD_BITS <= WK_DBITS,
               "walk tables fold by one bit at most");
-#ifndef WK_LTAIL
-#define WK_LTAIL 1  // long literals from the canonical tail in registers (0: always the compact tables)
-#endif
 #define WK_GS(d64) ((d64) ? 7u : 9u)  // steps per group: <= 60 (48) bits each, so a group reads words p / 32 .. p / 32 + 16
 #define WK_PF 16u   // words per prefetch: the ring is two such halves
 #define WK_RW 32u   // input ring words per lane
@@ -1996,45 +2027,46 @@ __device__ __forceinline__ uint32_t walk_tail(const uint4 a, const uint4 b, cons
   return CK_SYM | (L << 2) | (sym << 6);
 }
 
-// literal / length code longer than the walk table (or end of block, invalid):
-// the unit's compact tables, as lane_step reads them.  Returns a walk entry;
-// end of block: 0x100 | WK_EXC | code bits; invalid: WK_EXC alone.
+// a literal/length code past the walk's table from the canonical tail
+// (build_lit_tail's 16 words, in registers): its walk
+// entry (end of block: 0x100 | WK_EXC | code bits; invalid: WK_EXC)
+// build_lit_tail's 16 words in registers: the header words as an array (only
+// constant indices), the symbol list as named words (an array indexed by a
+// select tree was turned into scratch memory)
+struct WalkLitTail {
+  uint32_t w[8];
+  uint32_t n0, n1, n2, n3, n4, n5, n6, n7;
+};
 template <bool D64>
-__device__ __forceinline__ uint32_t walk_slow_len(uint32_t h, const uint16_t *cl, uint32_t lbits) {
-  uint32_t ce = cl[h & ((1u << lbits) - 1u)];
-  if ((ce & 3u) == CK_SLOW) {
-    const uint32_t op = (ce >> 2) & 15u;
-    if (op == 0) return WK_EXC;
-    ce = cl[(ce >> 6) + ((h >> lbits) & ((1u << op) - 1u))];
-    if ((ce & 3u) == CK_SLOW) return WK_EXC;
-  }
-  if ((ce & 3u) == CK_EOB) return 0x100u | WK_EXC | ((ce >> 2) & 15u);
-  return walk_len_entry<D64>(ce);
-}
-// a literal/length code past the walk's table from the canonical tail in
-// registers (build_lit_tail): its walk entry when it is a literal, else WK_EXC
-// (end of block, a length code, invalid: the compact tables decide)
-__device__ __forceinline__ uint32_t walk_lit_tail(const uint32_t (&lt)[6], uint32_t bits) {
+__device__ __forceinline__ uint32_t walk_lit_tail(const WalkLitTail &T, uint32_t bits) {
+  const uint32_t(&lt)[8] = T.w;
   const uint32_t rev = __builtin_bitreverse32(bits) >> 17;  // the next 15 bits, first bit highest
   const uint32_t lim[7] = {lt[0] & 0xffffu, lt[0] >> 16, lt[1] & 0xffffu, lt[1] >> 16,
                            lt[2] & 0xffffu, lt[2] >> 16, lt[3] & 0xffffu};  // lengths 9 .. 15
-  uint32_t L = 10, fl = lim[0], nl = lt[4] & 0xffu;
+  uint32_t L = 10, fl = lim[0], nl = lt[4] & 0xffu, nb = lt[6] & 0xffu;
 #pragma unroll
   for (int k = 1; k < 6; k++) {
     const bool ge = rev >= lim[k];
     L += ge ? 1u : 0u;
     fl = ge ? lim[k] : fl;
     nl = ge ? ((lt[4 + (k >> 2)] >> (8 * (k & 3))) & 0xffu) : nl;
+    nb = ge ? ((lt[6 + (k >> 2)] >> (8 * (k & 3))) & 0xffu) : nb;
   }
+  if (rev < lim[0] || rev >= lim[6]) return WK_EXC;  // not a long code of this table: invalid
   const uint32_t idx = (rev - fl) >> (15u - L);
-  return (rev >= lim[0] && rev < lim[6] && idx < nl) ? L : WK_EXC;
-}
-// walk entry of a compact literal/length entry that is not a sub-table link
-template <bool D64>
-__device__ __forceinline__ uint32_t walk_ce_entry(uint32_t ce) {
-  if ((ce & 3u) == CK_SLOW) return WK_EXC;  // invalid
-  if ((ce & 3u) == CK_EOB) return 0x100u | WK_EXC | ((ce >> 2) & 15u);
-  return walk_len_entry<D64>(ce);
+  if (idx < nl) return L;  // a literal
+  const uint32_t k = min(nb + idx - nl, 31u);
+  // word k / 4 of the list by a tree of selects on k's bits (a select chain on
+  // k / 4 == j became an indexed private array, i.e. scratch memory)
+  const uint32_t a0 = (k & 4u) ? T.n1 : T.n0, a1 = (k & 4u) ? T.n3 : T.n2;
+  const uint32_t a2 = (k & 4u) ? T.n5 : T.n4, a3 = (k & 4u) ? T.n7 : T.n6;
+  const uint32_t b0 = (k & 8u) ? a1 : a0, b1 = (k & 8u) ? a3 : a2;
+  const uint32_t w = (k & 16u) ? b1 : b0;
+  const uint32_t sym = (w >> (8u * (k & 3u))) & 0xffu;  // symbol - 256
+  if (sym == 0) return 0x100u | WK_EXC | L;  // end of block
+  const uint32_t q = sym - 1u;  // length code 0..28 (src/inftrees.c:59-64; deflate64 285: 16 extra bits)
+  const uint32_t xb = q < 8u ? 0u : (q < 28u ? (q >> 2) - 1u : (D64 ? 16u : 0u));
+  return (L + xb) | WK_HASD | ((D64 && q >= 28u) ? WK_BIG : 0u);
 }
 // word wi as read raw, with the bytes at or past the input's end zeroed
 __device__ __forceinline__ uint32_t walk_mask(uint32_t v, uint32_t wi, uint32_t end_byte) {
@@ -2104,14 +2136,16 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
   s.end_byte = s.limit = 0;
   s.wi = s.nw = s.nkeep = s.nbits = s.lastw = s.rk = 0;
   s.hold = 0;
-  uint32_t wst = WS_IDLE, code = 0, lbits = 9, tcap = 0;
-  const uint16_t *cl = nullptr;
+  uint32_t wst = WS_IDLE, code = 0, tcap = 0;
   uint32_t *wl = &L.wl[0][lane];
   uint32_t *wd = &L.wd[0][lane];
   uint32_t *dtl = &L.dtail[0][lane];
   uint32_t *rr = &L.ring[lane][0];
   s.dta = s.dtb = make_uint4(0, 0, 0, 0);
-  uint32_t ltw[6] = {0, 0, 0, 0, 0, 0};  // the literal/length code's canonical tail (registers)
+  WalkLitTail ltw;  // the literal/length code's canonical tail (registers)
+#pragma unroll
+  for (int k = 0; k < 8; k++) ltw.w[k] = 0;
+  ltw.n0 = ltw.n1 = ltw.n2 = ltw.n3 = ltw.n4 = ltw.n5 = ltw.n6 = ltw.n7 = 0;
   if (c < nchunks) {
     const ZsChunkDev ch = chunks[c];
     if (ch.start_bit != ZS_NONE && heads[ch.job].code == ZD_END) {
@@ -2123,9 +2157,7 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
         s.end_byte = mis + (uint32_t)jb.in_len;
         s.limit = s.end_byte * 8u;
         tcap = ch.tcap;
-        lbits = (ch.hdr_info >> 8) & 15u;
         const uint32_t *tabg = tables + (size_t)c * TABLE_STRIDE;
-        cl = reinterpret_cast<const uint16_t *>(tabg + TABLE_ENTRIES);
         const uint4 *wt = reinterpret_cast<const uint4 *>(tabg + TABLE_WALK_OFF);
         walk_table_load(wl, wt, (1u << WKL_BITS) / 16u, WKL_BITS < WK_LBITS);
         walk_table_load(wd, wt + (1u << WK_LBITS) / 16u, (1u << WKD_BITS) / 16u, WKD_BITS < WK_DBITS);
@@ -2134,7 +2166,16 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
         s.dta = make_uint4(img[0], img[1], img[2], img[3]);
         s.dtb = make_uint4(img[4], img[5], img[6], img[7]);
 #pragma unroll
-        for (int k = 0; k < 6; k++) ltw[k] = tabg[TABLE_LTAIL_OFF + k];
+        for (int k = 0; k < 8; k++) ltw.w[k] = tabg[TABLE_LTAIL_OFF + k];
+        const uint32_t *nlg = tabg + TABLE_LTAIL_OFF + 8;
+        ltw.n0 = nlg[0];
+        ltw.n1 = nlg[1];
+        ltw.n2 = nlg[2];
+        ltw.n3 = nlg[3];
+        ltw.n4 = nlg[4];
+        ltw.n5 = nlg[5];
+        ltw.n6 = nlg[6];
+        ltw.n7 = nlg[7];
 #pragma unroll
         for (uint32_t k = 0; k < WK_DTN; k++) dtl[k * WAVE] = img[WK_DT0 + k];
         s.lastw = (s.end_byte - 1u) >> 2;
@@ -2167,7 +2208,6 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
     walk_prefetch(s, filled, pre);
   }
   uint32_t xp = live ? 0u : 1u;  // an exception is pending: the lane stands at its symbol until the next group start
-  uint32_t xs = 0, ce = 0;        // compact-table loads in flight for it (1: root entry, 2: sub-table entry)
   // the ring row's address, opaque to the compiler (so that a step's ring
   // address is one shift-and-mask and one add, not folded LDS offsets)
   typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
@@ -2177,7 +2217,7 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
   __builtin_amdgcn_wave_barrier();
 #if KP_ON
   const uint64_t kp_t0 = KP_NOW();
-  uint64_t kp_cyc_x = 0, kp_cyc_g = 0, kp_cyc_s = 0;
+  uint64_t kp_cyc_x = 0, kp_cyc_g = 0, kp_cyc_s = 0, kp_cyc_r = 0;
   uint32_t kp_wsteps = 0, kp_exc = 0, kp_slow_l = 0, kp_slow_d = 0;
 #endif
   // The steps are straight-line: a lane whose symbol needs more than the
@@ -2191,40 +2231,63 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
 #if KP_ON
     const uint64_t kg0 = KP_NOW();
 #endif
+    // a checkpoint at the first group start past every K tokens (the lane
+    // stands on a symbol boundary here; a pending symbol is not yet counted)
+    if (__builtin_amdgcn_ballot_w64(live && ntok >= ncut)) {
+      if (live && ntok >= ncut) {  // the next sub-unit starts here
+        cp[ncp] = make_uint2(p, ntok);
+        ncp++;
+        ncut += K;
+        if (ncp == WK_CP - 1u) {  // out of slots: keep every second checkpoint, twice the stride
+          walk_halve(cp);
+          ncp = (WK_CP - 1u) / 2u;
+          K *= 2u;
+          ncut = (ncp + 1u) * K;
+        }
+      }
+    }
+#if KP_ON
+    const uint64_t kr0 = KP_NOW();
+#endif
+    {  // a lane that has consumed its older half refills it from the prefetch
+      const bool wr = live && filled - (p >> 5) <= WK_RW - WK_PF;
+      if (__builtin_amdgcn_ballot_w64(wr)) {
+        if (wr) {
+          walk_put_half(rr, filled, pre, s.end_byte);
+          filled += WK_PF;
+          walk_prefetch(s, filled, pre);
+        }
+      }
+    }
+#if KP_ON
+    kp_cyc_r += KP_NOW() - kr0;
+#endif
+    // the pending symbols, exactly
     if (__builtin_amdgcn_ballot_w64(live && xp)) {
 #if KP_ON
       const uint64_t kq = KP_NOW();
       kp_exc += lane_id() == (uint32_t)__builtin_ctzll(__ballot(1)) ? 1u : 0u;
 #endif
-      bool ready = true;
-      if (live && xp) {  // the pending symbol, exactly
+      const bool pend = live && xp;
+      uint32_t x0 = 0, x1 = 0, x2 = 0, bits = 0, e2 = 0;
+      if (pend) {
         const uint32_t *r = rr + ((p >> 5) & (WK_RW - 1u));
-        const uint32_t x0 = r[0], x1 = r[1], x2 = r[2];
-        const uint32_t bits = __builtin_amdgcn_alignbit(x1, x0, p);
-        uint32_t e2 = wk_byte(wl, bits & ((1u << WKL_BITS) - 1u));
-        if (e2 & WK_EXC) {
-          // past the table: the unit's compact tables (global), one load per
-          // group start so that the lane waits a group instead of the load
-          const uint32_t et = (WK_LTAIL && xs == 0) ? walk_lit_tail(ltw, bits) : WK_EXC;
-          if (et != WK_EXC) {  // a long literal: its length from the tail in registers
-            e2 = et;
-          } else if (xs == 0) {
+        x0 = r[0];
+        x1 = r[1];
+        x2 = r[2];
+        bits = __builtin_amdgcn_alignbit(x1, x0, p);
+        e2 = wk_byte(wl, bits & ((1u << WKL_BITS) - 1u));
+      }
+      // past the table: the end of block from its own entry, every longer
+      // code from the canonical tail (registers and LDS; no global table)
+      if (pend && (e2 & WK_EXC)) {
 #if KP_ON
-            kp_slow_l++;
+        kp_slow_l++;
 #endif
-            ce = cl[bits & ((1u << lbits) - 1u)];
-            xs = 1;
-            ready = false;
-          } else if (xs == 1 && (ce & 3u) == CK_SLOW && ((ce >> 2) & 15u)) {  // a sub-table link
-            ce = cl[(ce >> 6) + ((bits >> lbits) & ((1u << ((ce >> 2) & 15u)) - 1u))];
-            xs = 2;
-            ready = false;
-          } else {
-            e2 = walk_ce_entry<D64>(ce);
-          }
-        }
-        if (!ready) {
-        } else if (e2 & WK_EXC) {
+        e2 = ((e2 & WK_EOBE) == WK_EOBE) ? (0x100u | WK_EXC | (e2 & 31u)) : walk_lit_tail<D64>(ltw, bits);
+      }
+      if (pend) {
+        if (e2 & WK_EXC) {
           if (e2 & 0x100u) {  // end of block
             eob = p;
             endb = p + (e2 & 31u);
@@ -2265,39 +2328,11 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
             ntok += (D64 && (e2 & WK_BIG) && ((bits >> (n2 - 16u)) & 0xffffu) >= 65533u) ? 2u : 1u;  // deflate64 > 65535: two tokens
           }
         }
-        if (ready) {
-          xs = 0;
-          xp = live ? 0u : 1u;  // a lane that is done stays where it stopped
-        }
+        xp = live ? 0u : 1u;  // a lane that is done stays where it stopped
       }
 #if KP_ON
       kp_cyc_x += KP_NOW() - kq;
 #endif
-    }
-    // a checkpoint at the first group start past every K tokens (the lane
-    // stands on a symbol boundary here; a pending symbol is not yet counted)
-    if (__builtin_amdgcn_ballot_w64(live && ntok >= ncut)) {
-      if (live && ntok >= ncut) {  // the next sub-unit starts here
-        cp[ncp] = make_uint2(p, ntok);
-        ncp++;
-        ncut += K;
-        if (ncp == WK_CP - 1u) {  // out of slots: keep every second checkpoint, twice the stride
-          walk_halve(cp);
-          ncp = (WK_CP - 1u) / 2u;
-          K *= 2u;
-          ncut = (ncp + 1u) * K;
-        }
-      }
-    }
-    {  // a lane that has consumed its older half refills it from the prefetch
-      const bool wr = live && filled - (p >> 5) <= WK_RW - WK_PF;
-      if (__builtin_amdgcn_ballot_w64(wr)) {
-        if (wr) {
-          walk_put_half(rr, filled, pre, s.end_byte);
-          filled += WK_PF;
-          walk_prefetch(s, filled, pre);
-        }
-      }
     }
 #if KP_ON
     const uint64_t ks0 = KP_NOW();
@@ -2354,6 +2389,7 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
     KP_ADD(38, kp_cyc_g);
     KP_ADD(39, kp_wave_sum(kp_exc));
     KP_ADD(KP_P_CYC_STEPS, kp_cyc_s);
+    KP_ADD(KP_P_CYC_BUSY, kp_cyc_r);
     KP_ADD(KP_P_SLOW_LIT, kp_wave_sum(kp_slow_l));
     KP_ADD(KP_P_SLOW_DIST, kp_wave_sum(kp_slow_d));
   }
@@ -2420,7 +2456,10 @@ __device__ __forceinline__ uint32_t split_dist_entry(uint32_t ce, bool d64) {  /
 // refilled from a prefetch that stays in flight), three words giving the 64
 // bits from p -- every field of a symbol (code, extra bits, distance code,
 // distance extra bits: <= 48 bits, deflate64 60) is one funnel shift of them.
-#define SP_GS(d64) ((d64) ? 7u : 8u)  // steps per group (<= 17 ring words ahead, as the walk's groups)
+#ifndef SP_GSN
+#define SP_GSN 10u
+#endif
+#define SP_GS(d64) ((d64) ? 7u : SP_GSN)  // steps per group: <= 60 (48) bits each, words p / 32 .. p / 32 + 16
 template <bool D64>
 struct __attribute__((aligned(16))) SplitLDS {
   uint32_t lw[1u << SPL_BITS];
@@ -2551,14 +2590,22 @@ __device__ __forceinline__ void split_sub3(SplitLDS<D64> &L, SplitLane &t, LaneS
       const uint64_t kf0 = KP_NOW();
 #endif
       if (run) {
-        if (t.gk == GS && t.ntok <= s.tcap) {
+        if (t.gk == GS && t.ntok <= s.tcap) {  // 16-byte stores, then 8 / 4 bytes
           typedef uint32_t u32x4a4t __attribute__((ext_vector_type(4), aligned(4)));
-          u32x4a4t v0, v1;
-          v0.x = tk[0]; v0.y = tk[1]; v0.z = tk[2]; v0.w = tk[3];
-          v1.x = tk[4]; v1.y = tk[5]; v1.z = tk[6]; v1.w = tk[7];
+          typedef uint32_t u32x2a4t __attribute__((ext_vector_type(2), aligned(4)));
           gu32 *dst = s.tok + g0;
-          *reinterpret_cast<__attribute__((address_space(1))) u32x4a4t *>(dst) = v0;
-          *reinterpret_cast<__attribute__((address_space(1))) u32x4a4t *>(dst + 4) = v1;
+#pragma unroll
+          for (uint32_t q = 0; q + 4u <= GS; q += 4u) {
+            u32x4a4t v;
+            v.x = tk[q]; v.y = tk[q + 1]; v.z = tk[q + 2]; v.w = tk[q + 3];
+            *reinterpret_cast<__attribute__((address_space(1))) u32x4a4t *>(dst + q) = v;
+          }
+          if (GS % 4u >= 2u) {
+            u32x2a4t v;
+            v.x = tk[GS & ~3u]; v.y = tk[(GS & ~3u) + 1u];
+            *reinterpret_cast<__attribute__((address_space(1))) u32x2a4t *>(dst + (GS & ~3u)) = v;
+          }
+          if (GS % 2u) dst[GS - 1u] = tk[GS - 1u];
         } else {
           const uint64_t prim_off = (uint64_t)((const uint32_t *)s.tok - tokens);
 #pragma unroll
@@ -3435,7 +3482,7 @@ __global__ void __launch_bounds__(64) zs_unit_header_kernel(const ZsJobDev *__re
     for (uint32_t i = lane; i < (1u << WK_DBITS); i += WAVE) walk[(1u << WK_LBITS) + i] = (uint8_t)walk_dist_z(fixed + 512, 5u, i);
     __builtin_amdgcn_wave_barrier();
     if (lane == 0) build_dist_tail(B.lens, 32, reinterpret_cast<uint8_t *>(img + LROOT_N + DROOT_N));
-    if (lane < 8) tabg[TABLE_LTAIL_OFF + lane] = lane < 4 ? 0x80008000u : 0u;  // no code past 9 bits
+    if (lane < 16) tabg[TABLE_LTAIL_OFF + lane] = lane < 4 ? 0x80008000u : 0u;  // no code past 9 bits
     lbits = 9;
     dbits = 5;
   } else if (wave_dyn_header<D64>(B, w, end_byte, bit, tabg, ctab, lbits, dbits, img, img + LROOT_N,

@@ -72,7 +72,7 @@ extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_hea
 
 namespace {
 
-constexpr size_t TABLE_ENTRIES_HOST = 1448 + 724 + 176 + 192 + 8;  // must match TABLE_STRIDE (zs_device.h)
+constexpr size_t TABLE_ENTRIES_HOST = 1448 + 724 + 176 + 192 + 16;  // must match TABLE_STRIDE (zs_device.h)
 constexpr size_t FIXED_WORDS_HOST = 544 + 272;      // must match FIXED_WORDS (zs_device.h)
 constexpr uint64_t MAX_RATIO = 1032;  // deflate's largest expansion: 258 bytes per 2 bits
 // deflate64: code 285 carries 16 extra bits for up to 65538 bytes, so one 1-bit

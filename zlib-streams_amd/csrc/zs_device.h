@@ -10,8 +10,8 @@
 // (512 + 256 u8 entries, lane_decode.hip zs_walk_kernel)
 #define TABLE_IMG_OFF (TABLE_ENTRIES + TABLE_ENTRIES / 2)
 #define TABLE_WALK_OFF (TABLE_IMG_OFF + 176)
-#define TABLE_LTAIL_OFF (TABLE_WALK_OFF + 192)  // the literal/length code's canonical tail (8 words, the walk)
-#define TABLE_STRIDE (TABLE_LTAIL_OFF + 8)
+#define TABLE_LTAIL_OFF (TABLE_WALK_OFF + 192)  // the literal/length code's canonical tail (16 words, the walk)
+#define TABLE_STRIDE (TABLE_LTAIL_OFF + 16)
 #define FIXED_ZLIB_WORDS 544                              // fixed tables: 512 lit/len + 32 dist (zlib layout)
 #define FIXED_WORDS (FIXED_ZLIB_WORDS + FIXED_ZLIB_WORDS / 2)  // + compact u16 copy
 #define DIST_TABLE_OFF 852   // distance table follows the literal/length table
