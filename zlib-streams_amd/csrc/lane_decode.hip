@@ -846,38 +846,48 @@ __device__ int wave_dyn_header(BuildLDS &B, const uint32_t *w, uint32_t end_byte
   }
   const uint32_t total = nlen + ndist;
   const uint32_t cmask = (1u << cbits) - 1u;
+  // the code lengths, a 64-bit window at a time: every lane decodes the
+  // code-length symbol starting at bit + lane, then the true symbols of the
+  // window are followed from lane 0 with readlane (scalar), the checks and
+  // writes in zlib's order (src/inflate.c:1000-1033)
   uint32_t have = 0;
   while (have < total) {
-    if (bit - sb.base > (STAGE_WORDS - 2) * 32u - 64u) stage_bits(B, w, end_byte, bit, sb);
-    const uint32_t x = sb.peek(bit, 14);
-    const uint32_t e = B.tab[x & cmask];
-    const uint32_t eb = e_bits(e), ev = e_val(e);
-    if (ev < 16) {
-      if (bit + eb > limit) {
-        return ZD_TRUNC;
+    if (bit - sb.base > (STAGE_WORDS - 2) * 32u - 128u) stage_bits(B, w, end_byte, bit, sb);
+    const uint32_t xj = sb.peek(bit + lane, 14);
+    const uint32_t ej = B.tab[xj & cmask];
+    const uint32_t ebj = e_bits(ej), evj = e_val(ej);
+    const uint32_t xbj = evj < 16 ? 0u : (evj == 16 ? 2u : (evj == 17 ? 3u : 7u));
+    const uint32_t repj = evj < 16 ? 1u : ((evj == 18 ? 11u : 3u) + ((xj >> ebj) & ((1u << xbj) - 1u)));
+    uint32_t o = 0;
+    while (o < WAVE && have < total) {
+      const uint32_t ev = __builtin_amdgcn_readlane(evj, o), eb = __builtin_amdgcn_readlane(ebj, o);
+      const uint32_t xb = __builtin_amdgcn_readlane(xbj, o);
+      if (ev < 16) {
+        if (bit + o + eb > limit) {
+          return ZD_TRUNC;
+        }
+        if (lane == 0) B.lens[have] = (uint16_t)ev;
+        have++;
+      } else {
+        const uint32_t rep = __builtin_amdgcn_readlane(repj, o);
+        if (bit + o + eb + xb > limit) {
+          return ZD_TRUNC;
+        }
+        if (ev == 16 && have == 0) {
+          return ZD_ERROR | (ZM_REPEAT << 8);
+        }
+        if (have + rep > total) {
+          return ZD_ERROR | (ZM_REPEAT << 8);
+        }
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t fillv = ev == 16 ? uni(B.lens[have - 1]) : 0u;
+        for (uint32_t k = lane; k < rep; k += WAVE) B.lens[have + k] = (uint16_t)fillv;
+        __builtin_amdgcn_wave_barrier();
+        have += rep;
       }
-      bit += eb;
-      if (lane == 0) B.lens[have] = (uint16_t)ev;
-      have++;
-      continue;
+      o += eb + xb;
     }
-    const uint32_t xb = ev == 16 ? 2u : (ev == 17 ? 3u : 7u);
-    if (bit + eb + xb > limit) {
-      return ZD_TRUNC;
-    }
-    if (ev == 16 && have == 0) {
-      return ZD_ERROR | (ZM_REPEAT << 8);
-    }
-    const uint32_t rep = (ev == 18 ? 11u : 3u) + ((x >> eb) & ((1u << xb) - 1u));
-    bit += eb + xb;
-    if (have + rep > total) {
-      return ZD_ERROR | (ZM_REPEAT << 8);
-    }
-    __builtin_amdgcn_wave_barrier();
-    const uint32_t fillv = ev == 16 ? uni(B.lens[have - 1]) : 0u;
-    for (uint32_t k = lane; k < rep; k += WAVE) B.lens[have + k] = (uint16_t)fillv;
-    __builtin_amdgcn_wave_barrier();
-    have += rep;
+    bit += o;
   }
   __builtin_amdgcn_wave_barrier();
   if (uni(B.lens[256]) == 0) {
@@ -1954,6 +1964,9 @@ __global__ void __launch_bounds__(64) zs_unitw_list_kernel(const ZsJobDev *__res
 #endif
 static_assert(WKL_BITS + 1u >= WK_LBITS && WKL_BITS <= WK_LBITS && WKD_BITS + 1u >= WK_DBITS && WKD_BITS <= WK_DBITS,
               "walk tables fold by one bit at most");
+#ifndef WK_RES
+#define WK_RES 2u  // measured: C2 walk 3.92 ms resolving every group, 3.81 every second
+#endif
 #define WK_GS(d64) ((d64) ? 7u : 9u)  // steps per group: <= 60 (48) bits each, so a group reads words p / 32 .. p / 32 + 16
 #define WK_PF 16u   // words per prefetch: the ring is two such halves
 #define WK_RW 32u   // input ring words per lane
@@ -2208,6 +2221,7 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
     walk_prefetch(s, filled, pre);
   }
   uint32_t xp = live ? 0u : 1u;  // an exception is pending: the lane stands at its symbol until the next group start
+  uint32_t gi = 0;                // groups
   // the ring row's address, opaque to the compiler (so that a step's ring
   // address is one shift-and-mask and one add, not folded LDS offsets)
   typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
@@ -2262,8 +2276,10 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
 #if KP_ON
     kp_cyc_r += KP_NOW() - kr0;
 #endif
-    // the pending symbols, exactly
-    if (__builtin_amdgcn_ballot_w64(live && xp)) {
+    // the pending symbols, exactly (every WK_RES groups: a pass costs about
+    // a group's steps, a lane that waits loses half a group on average)
+    gi++;
+    if ((gi % WK_RES) == 0 && __builtin_amdgcn_ballot_w64(live && xp)) {
 #if KP_ON
       const uint64_t kq = KP_NOW();
       kp_exc += lane_id() == (uint32_t)__builtin_ctzll(__ballot(1)) ? 1u : 0u;
@@ -2684,7 +2700,13 @@ __global__ void __launch_bounds__(64) zs_split_kernel(const ZsJobDev *__restrict
   uint64_t kp_grp = 0;
   uint32_t kp_units = 0, kp_ws = 0;
 #endif
-  for (uint32_t k = blockIdx.x; k < nsplit; k += gridDim.x) {
+  for (;;) {
+    // units are taken one at a time from a counter: waves that get the
+    // longest units take fewer (a fixed deal left a tail of 5 vs 6 units)
+    uint32_t k = 0;
+    if (lane == 0) k = atomicAdd(&counts[2], 1u);
+    k = uni(k);
+    if (k >= nsplit) break;
     const uint32_t c = lists[k];
     const ZsWalkDev wk = walks[c];
 #if KP_ON
@@ -3596,7 +3618,7 @@ int split_reserve(uint32_t n) {
   const size_t c = (size_t)n + n / 2;
   if (hipMalloc(&g_split.walks, c * sizeof(ZsWalkDev)) != hipSuccess ||
       hipMalloc(&g_split.cps, c * WK_CP * sizeof(uint2)) != hipSuccess ||
-      hipMalloc(&g_split.lists, (2 * c + 2) * sizeof(uint32_t)) != hipSuccess)
+      hipMalloc(&g_split.lists, (2 * c + 3) * sizeof(uint32_t)) != hipSuccess)
     return -1;
   g_split.cap = c;
   return 0;
@@ -3633,7 +3655,7 @@ extern "C" void zs_launch_parse(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads
   if (wave_units == 2 && split_reserve(nchunks) == 0) {
     uint32_t *counts = g_split.lists + 2 * g_split.cap;
     uint32_t *lists = g_split.lists;
-    (void)hipMemsetAsync(counts, 0, 2 * sizeof(uint32_t), st);
+    (void)hipMemsetAsync(counts, 0, 3 * sizeof(uint32_t), st);  // splits, leftovers, the split's next unit
     // the walk deals its sorted units over the waves resident at once, as the lane parse
     static const uint32_t lane_map = [] {
       int dev = 0, cus = 0, lds = 0;
