@@ -13,6 +13,7 @@
 #   pmc=<checkpoint tag>    HBM traffic of the headline launch (tools/pmc_traffic.sh: one rocprofv3
 #                           --pmc pass per counter) -> NN_pmc/pmc_traffic.json; the following
 #                           bench steps read it (--traffic-json) unless they pass their own
+#   sh=<script args>        bash <script> <args> (e.g. tools/gpu_strong_split_c5.sh TAG)
 #   env=K=V                 export K=V for the following steps
 #   budget=SECONDS          timeout of the following steps (default 600)
 set -o pipefail
@@ -38,6 +39,7 @@ for step in "$@"; do
     bench) timeout -k 10 "$T" python -u bench.py ${ZS_TRAFFIC_JSON:+--traffic-json $ZS_TRAFFIC_JSON} $args > "$p.json" 2> "$p.err" ;;
     prof) (cd /tmp && timeout -k 10 "$T" rocprofv3 --kernel-trace --stats -d "$p" -o run -- python3 "$R/bench.py" $args > "$p.json" 2> "$p.err") ;;
     py) timeout -k 10 "$T" python -u $args > "$p.log" 2>&1 ;;
+    sh) timeout -k 10 "$T" bash $args > "$p.log" 2>&1 ;;
     pmc) PMC_OUT="$p" PMC_TAG="$args" bash tools/pmc_traffic.sh > "$p.log" 2>&1 && [ -s "$p/pmc_traffic.json" ] &&
          export ZS_TRAFFIC_JSON="$p/pmc_traffic.json" ;;
     *) echo "unknown step $step"; exit 2 ;;
@@ -51,7 +53,7 @@ import json,sys
 d=json.loads(open('$p.json').read().strip().splitlines()[-1])
 print('value',d.get('value'),'ms',d.get('ms_per_step'),'exact',d.get('verified_bit_exact'),d.get('path_stats'))
 print('stages',d.get('roofline',{}).get('stages_ms_avg'))" 2>&1 | tail -3 ;;
-    py) tail -5 "$p.log" ;;
+    py|sh) tail -5 "$p.log" ;;
     pmc) python3 -c "import json;d=json.load(open('$p/pmc_traffic.json'));print('traffic',d['hbm_bytes_per_launch'],d.get('source_sha256'))" ;;
   esac
   [ $rc -eq 0 ] || exit $rc

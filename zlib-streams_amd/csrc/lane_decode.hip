@@ -2245,21 +2245,6 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
 #if KP_ON
     const uint64_t kg0 = KP_NOW();
 #endif
-    // a checkpoint at the first group start past every K tokens (the lane
-    // stands on a symbol boundary here; a pending symbol is not yet counted)
-    if (__builtin_amdgcn_ballot_w64(live && ntok >= ncut)) {
-      if (live && ntok >= ncut) {  // the next sub-unit starts here
-        cp[ncp] = make_uint2(p, ntok);
-        ncp++;
-        ncut += K;
-        if (ncp == WK_CP - 1u) {  // out of slots: keep every second checkpoint, twice the stride
-          walk_halve(cp);
-          ncp = (WK_CP - 1u) / 2u;
-          K *= 2u;
-          ncut = (ncp + 1u) * K;
-        }
-      }
-    }
 #if KP_ON
     const uint64_t kr0 = KP_NOW();
 #endif
@@ -2276,6 +2261,22 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
 #if KP_ON
     kp_cyc_r += KP_NOW() - kr0;
 #endif
+    // a checkpoint at the first group start past every K tokens, stored
+    // after the refill's wait (a store before it would make it wait; the lane
+    // stands on a symbol boundary here; a pending symbol is not yet counted)
+    if (__builtin_amdgcn_ballot_w64(live && ntok >= ncut)) {
+      if (live && ntok >= ncut) {  // the next sub-unit starts here
+        cp[ncp] = make_uint2(p, ntok);
+        ncp++;
+        ncut += K;
+        if (ncp == WK_CP - 1u) {  // out of slots: keep every second checkpoint, twice the stride
+          walk_halve(cp);
+          ncp = (WK_CP - 1u) / 2u;
+          K *= 2u;
+          ncut = (ncp + 1u) * K;
+        }
+      }
+    }
     // the pending symbols, exactly (every WK_RES groups: a pass costs about
     // a group's steps, a lane that waits loses half a group on average)
     gi++;
@@ -2475,6 +2476,9 @@ __device__ __forceinline__ uint32_t split_dist_entry(uint32_t ce, bool d64) {  /
 #ifndef SP_GSN
 #define SP_GSN 10u
 #endif
+#ifndef SPLIT_NOSTORE
+#define SPLIT_NOSTORE 0  // (diagnostic builds only: no token stores, wrong output)
+#endif
 #define SP_GS(d64) ((d64) ? 7u : SP_GSN)  // steps per group: <= 60 (48) bits each, words p / 32 .. p / 32 + 16
 template <bool D64>
 struct __attribute__((aligned(16))) SplitLDS {
@@ -2560,6 +2564,47 @@ __device__ __forceinline__ void split_sub3(SplitLDS<D64> &L, SplitLane &t, LaneS
   uint32_t *tb = &L.tokbuf[0][lane];
   uint32_t *rr = &L.ring[lane][0];
   constexpr uint32_t GS = SP_GS(D64), TPS = D64 ? 2u : 1u;
+  // !D64: a group's tokens are stored one group late, right after the next
+  // refill's wait (vmcnt counts stores too: stored at the end of their own
+  // group, they made that wait wait for them -- C2 split 3.2 ms, 2.3 without
+  // stores at all)
+  uint32_t tkp[GS], g0p = 0, gkp = 0;
+  auto store_prev = [&]() {
+#if KP_ON
+    const uint64_t kf0 = KP_NOW();
+#endif
+    if (gkp && !SPLIT_NOSTORE) {
+      if (gkp == GS && g0p + GS <= s.tcap) {  // 16-byte stores, then 8 / 4 bytes
+        typedef uint32_t u32x4a4t __attribute__((ext_vector_type(4), aligned(4)));
+        typedef uint32_t u32x2a4t __attribute__((ext_vector_type(2), aligned(4)));
+        gu32 *dst = s.tok + g0p;
+#pragma unroll
+        for (uint32_t q = 0; q + 4u <= GS; q += 4u) {
+          u32x4a4t v;
+          v.x = tkp[q]; v.y = tkp[q + 1]; v.z = tkp[q + 2]; v.w = tkp[q + 3];
+          *reinterpret_cast<__attribute__((address_space(1))) u32x4a4t *>(dst + q) = v;
+        }
+        if (GS % 4u >= 2u) {
+          u32x2a4t v;
+          v.x = tkp[GS & ~3u]; v.y = tkp[(GS & ~3u) + 1u];
+          *reinterpret_cast<__attribute__((address_space(1))) u32x2a4t *>(dst + (GS & ~3u)) = v;
+        }
+        if (GS % 2u) dst[GS - 1u] = tkp[GS - 1u];
+      } else {
+        const uint64_t prim_off = (uint64_t)((const uint32_t *)s.tok - tokens);
+#pragma unroll
+        for (uint32_t j = 0; j < GS; j++)
+          if (j < gkp) {
+            if (g0p + j < s.tcap) s.tok[g0p + j] = tkp[j];
+            else *tok_addr(pool, tokens, s.unit, prim_off, s.tcap, g0p + j) = tkp[j];
+          }
+      }
+    }
+    gkp = 0;
+#if KP_ON
+    kp_grp += KP_NOW() - kf0;
+#endif
+  };
   for (;;) {
     const bool run = act && t.ntok < t1 && !(t.bad & 0x20u) && t.pos <= s.capx;
     if (__builtin_amdgcn_ballot_w64(run) == 0) break;
@@ -2580,6 +2625,7 @@ __device__ __forceinline__ void split_sub3(SplitLDS<D64> &L, SplitLane &t, LaneS
     kp_grp += KP_NOW() - kg0;
     kp_ws += lane == (uint32_t)__builtin_ctzll(__ballot(1)) ? GS : 0u;
 #endif
+    if (!D64) store_prev();
     t.gk = 0;
     const uint32_t g0 = t.ntok;
     uint32_t tk[GS];  // the group's tokens (!D64: registers; deflate64: tokbuf)
@@ -2601,40 +2647,11 @@ __device__ __forceinline__ void split_sub3(SplitLDS<D64> &L, SplitLane &t, LaneS
       t.gk -= min(t.gk, t.ntok - t1);
       t.ntok = t1;
     }
-    if (!D64) {  // each lane stores its own tokens: two 16-byte stores for a whole group
-#if KP_ON
-      const uint64_t kf0 = KP_NOW();
-#endif
-      if (run) {
-        if (t.gk == GS && t.ntok <= s.tcap) {  // 16-byte stores, then 8 / 4 bytes
-          typedef uint32_t u32x4a4t __attribute__((ext_vector_type(4), aligned(4)));
-          typedef uint32_t u32x2a4t __attribute__((ext_vector_type(2), aligned(4)));
-          gu32 *dst = s.tok + g0;
+    if (!D64) {  // the group's tokens wait in registers: stored after the next group's refill
 #pragma unroll
-          for (uint32_t q = 0; q + 4u <= GS; q += 4u) {
-            u32x4a4t v;
-            v.x = tk[q]; v.y = tk[q + 1]; v.z = tk[q + 2]; v.w = tk[q + 3];
-            *reinterpret_cast<__attribute__((address_space(1))) u32x4a4t *>(dst + q) = v;
-          }
-          if (GS % 4u >= 2u) {
-            u32x2a4t v;
-            v.x = tk[GS & ~3u]; v.y = tk[(GS & ~3u) + 1u];
-            *reinterpret_cast<__attribute__((address_space(1))) u32x2a4t *>(dst + (GS & ~3u)) = v;
-          }
-          if (GS % 2u) dst[GS - 1u] = tk[GS - 1u];
-        } else {
-          const uint64_t prim_off = (uint64_t)((const uint32_t *)s.tok - tokens);
-#pragma unroll
-          for (uint32_t j = 0; j < GS; j++)
-            if (j < t.gk) {
-              if (g0 + j < s.tcap) s.tok[g0 + j] = tk[j];
-              else *tok_addr(pool, tokens, s.unit, prim_off, s.tcap, g0 + j) = tk[j];
-            }
-        }
-      }
-#if KP_ON
-      kp_grp += KP_NOW() - kf0;
-#endif
+      for (uint32_t j = 0; j < GS; j++) tkp[j] = tk[j];
+      g0p = g0;
+      gkp = run ? t.gk : 0u;
       continue;
     }
     __builtin_amdgcn_wave_barrier();
@@ -2682,6 +2699,7 @@ __device__ __forceinline__ void split_sub3(SplitLDS<D64> &L, SplitLane &t, LaneS
     kp_grp += KP_NOW() - kf0;
 #endif
   }
+  if (!D64) store_prev();  // the last group's tokens
 }
 
 template <bool D64>
