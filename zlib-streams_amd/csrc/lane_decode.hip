@@ -2474,7 +2474,10 @@ __device__ __forceinline__ uint32_t split_dist_entry(uint32_t ce, bool d64) {  /
 // bits from p -- every field of a symbol (code, extra bits, distance code,
 // distance extra bits: <= 48 bits, deflate64 60) is one funnel shift of them.
 #ifndef SP_GSN
-#define SP_GSN 10u
+#define SP_GSN 8u
+#endif
+#ifndef SPLIT_ALIGN
+#define SPLIT_ALIGN 1  // measured (C2 split): 3.22 ms with 10-step groups at any token offset, 3.02 aligned 8-step groups
 #endif
 #ifndef SPLIT_NOSTORE
 #define SPLIT_NOSTORE 0  // (diagnostic builds only: no token stores, wrong output)
@@ -2605,6 +2608,9 @@ __device__ __forceinline__ void split_sub3(SplitLDS<D64> &L, SplitLane &t, LaneS
     kp_grp += KP_NOW() - kf0;
 #endif
   };
+  // SPLIT_ALIGN: a first group short enough that every later group's tokens
+  // start on a GS-token (for GS = 8: 32-byte) boundary of the token region
+  uint32_t first_n = (SPLIT_ALIGN && !D64 && act) ? ((GS - (t.ntok % GS)) % GS) : 0u;
   for (;;) {
     const bool run = act && t.ntok < t1 && !(t.bad & 0x20u) && t.pos <= s.capx;
     if (__builtin_amdgcn_ballot_w64(run) == 0) break;
@@ -2629,19 +2635,21 @@ __device__ __forceinline__ void split_sub3(SplitLDS<D64> &L, SplitLane &t, LaneS
     t.gk = 0;
     const uint32_t g0 = t.ntok;
     uint32_t tk[GS];  // the group's tokens (!D64: registers; deflate64: tokbuf)
-    if (__builtin_amdgcn_ballot_w64(run && t1 - t.ntok < GS * TPS) == 0) {
+    if (__builtin_amdgcn_ballot_w64(run && (t1 - t.ntok < GS * TPS || first_n != 0)) == 0) {
       if (run) {
 #pragma unroll
         for (uint32_t g = 0; g < GS; g++)
           split_step3<D64, NEEDC>(t, rra, L.lw, L.dw, tb, &tk[g], dta, dtb, L.dtail, s.cl, s.lbits);
       }
     } else {
+      const uint32_t lim = first_n ? min(t1, t.ntok + first_n) : t1;
       if (run) {
 #pragma unroll
         for (uint32_t g = 0; g < GS; g++)
-          if (t.ntok < t1) split_step3<D64, NEEDC>(t, rra, L.lw, L.dw, tb, &tk[g], dta, dtb, L.dtail, s.cl, s.lbits);
+          if (t.ntok < lim) split_step3<D64, NEEDC>(t, rra, L.lw, L.dw, tb, &tk[g], dta, dtb, L.dtail, s.cl, s.lbits);
       }
     }
+    first_n = 0;
     if (t.ntok > t1) {  // an inconsistent decode: never write past the walked tokens
       t.bad |= 0x20u;
       t.gk -= min(t.gk, t.ntok - t1);
