@@ -1354,16 +1354,17 @@ int pk_submit(StreamCall *c, int w) {
   // sleep through most of the expected call, then poll with short sleeps: many
   // handles' threads spinning would spend the host's CPU quota (a
   // cgroup-limited server throttles them for whole periods).  The expected
-  // time is the handle's last call on the worker scaled by this call's input
-  // (a trailer or a 1 KiB call after a 4 MiB one finishes in microseconds),
-  // capped at 2 ms.  The waiting thread's timer slack drops to 2 us for the
-  // wait, so the sleeps end on time, and is restored after it.
+  // time is the handle's last call on the worker, scaled down when this call
+  // has less input (a trailer or a 1 KiB call after a 4 MiB one finishes in
+  // microseconds) but never up (a call that fills its output ends with input
+  // left: scaling up by input overslept the JS schedule's calls, one handle
+  // 254 -> 213 MiB/s), capped at 2 ms.  The waiting thread's timer slack drops
+  // to 2 us for the wait, so the sleeps end on time, and is restored after it.
   const int prev_slack = prctl(PR_GET_TIMERSLACK, 0, 0, 0, 0);
   const bool slack = prev_slack >= 0 && prctl(PR_SET_TIMERSLACK, 2000UL, 0, 0, 0) == 0;
   const uint64_t last_in = std::max<uint64_t>(c->s->pk_last_in, 1);
-  const int64_t expect = (int64_t)std::min<uint64_t>(
-      std::min<uint64_t>(c->s->pk_last_ns * std::max<uint64_t>(c->jb.in_len, 1) / last_in, 4 * c->s->pk_last_ns),
-      2000000u);
+  const uint64_t in_now = std::min<uint64_t>(std::max<uint64_t>(c->jb.in_len, 1), last_in);
+  const int64_t expect = (int64_t)std::min<uint64_t>(c->s->pk_last_ns * in_now / last_in, 2000000u);
   if (expect > 80000) std::this_thread::sleep_for(std::chrono::nanoseconds(expect * 5 / 8));  // calls vary +-30%
   // the launch may have left (its life ended) before it saw the call: look
   // after three expected calls, then every 500 us
