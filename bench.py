@@ -856,15 +856,27 @@ def ref_perf_leg(args, zstreams, np):
     cap = n + n // 8 + (1 << 20)
     packet = 65536
 
+    calls = {}
+
     def run(lib, phase, data, runs):
         out = np.empty(cap, dtype=np.uint8)
         ol = ctypes.c_size_t()
         ts = []
+        s0 = zstreams.stream_stats() if lib is not None else None
         for _ in range(runs):
             t = J.zs_js_perf(lib, phase, data.ctypes.data, len(data), packet, -1, out.ctypes.data, cap, ctypes.byref(ol))
             if t <= 0:
                 raise RuntimeError(f"zs_js_perf phase {phase} failed ({t})")
             ts.append(t)
+        if s0 is not None:  # the decompress calls on the persistent worker: its time vs the caller's wait
+            s1 = zstreams.stream_stats()
+            n = s1["pk_calls"] - s0["pk_calls"]
+            if n:
+                calls[("compress_only", "decompress_only", "roundtrip")[phase]] = {
+                    "worker_calls_per_run": round(n / runs, 1),
+                    "worker_us_per_call": round((s1["pk_busy_ns"] - s0["pk_busy_ns"]) / n / 1e3, 2),
+                    "caller_wait_us_per_call": round((s1["pk_wait_ns"] - s0["pk_wait_ns"]) / n / 1e3, 2),
+                    "batch_calls_per_run": round((s1["calls"] - s0["calls"]) / runs, 1)}
         return sorted(ts)[len(ts) // 2], out[:ol.value].copy(), ts
 
     res = {}
@@ -882,6 +894,7 @@ def ref_perf_leg(args, zstreams, np):
                      "compressed_bytes": len(comp),
                      "verified": bool(np.array_equal(dec, src) and np.array_equal(rt, src))}
     res["gpu"]["bytes_identical_to_zlib"] = bool(np.array_equal(comps["gpu"], comps["host_zlib"]))
+    res["gpu"]["persistent_worker_calls"] = calls  # (per phase: a stored 32 KiB call's cost on its own)
     res["workload"] = (f"{args.ref_perf_mib} MiB random bytes, {packet >> 10} KiB packets, deflate-raw, default level; "
                        "compress-only / decompress-only / round trip (test_round_trip_stream_perf.js)")
     res["unit"] = "MiB/s (uncompressed)"
