@@ -1206,6 +1206,7 @@ struct PkState {
   std::atomic<uint64_t> calls{0}, busy_ns{0}, wait_ns{0};  // the calls' workgroup time; post to seen-done on the host
   std::atomic<uint64_t> idle_ns{0};  // the workgroups' wait for each call since their previous one
   std::atomic<int64_t> last_post{0};  // steady_clock ns of the last post (the launch outlives it by >= PK_IDLE)
+  std::atomic<int64_t> launch_at{0};  // steady_clock ns of the current launch (its workgroups leave once PK_LIFE old)
 } g_pk;
 std::atomic<int> g_pk_on{-1};  // -1: from env ZS_STREAM_PK (default on)
 
@@ -1273,6 +1274,14 @@ int64_t pk_idle_us() {
   return v;
 }
 
+int64_t pk_life_ms() {
+  static const int64_t v = [] {
+    const char *e = std::getenv("ZS_PK_LIFE_MS");
+    return (int64_t)std::max(1LL, e ? std::atoll(e) : 250LL);
+  }();
+  return v;
+}
+
 int64_t pk_now_ns() {
   return (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -1291,12 +1300,10 @@ void pk_defer_flush_locked() {
 
 int pk_launch_locked() {
   const uint64_t idle_t = (uint64_t)pk_idle_us() * 100u;  // s_memrealtime ticks (100 MHz)
-  static const uint64_t life_t = [] {
-    const char *e = std::getenv("ZS_PK_LIFE_MS");
-    return (uint64_t)(e ? std::atoll(e) : 250) * 100000u;
-  }();
+  const uint64_t life_t = (uint64_t)pk_life_ms() * 100000u;
   __atomic_store_n(&g_pk.h_ctl[2], 0u, __ATOMIC_SEQ_CST);  // the last launch's closing flag (it has drained)
   pk_defer_flush_locked();  // device frees deferred while a launch ran (stream_free)
+  g_pk.launch_at.store(pk_now_ns());
   zs_launch_stream_pk(g_pk.d_mb, (uint32_t)g_pk.nw, g_pk.d_ctl, idle_t, life_t, g_pk.st);
   HIP_OK(hipGetLastError());
   HIP_OK(hipEventRecord(g_pk.ev, g_pk.st));
@@ -1367,13 +1374,20 @@ int pk_submit(StreamCall *c, int w) {
   const int64_t expect = (int64_t)std::min<uint64_t>(c->s->pk_last_ns * in_now / last_in, 2000000u);
   if (expect > 80000) std::this_thread::sleep_for(std::chrono::nanoseconds(expect * 5 / 8));  // calls vary +-30%
   // the launch may have left (its life ended) before it saw the call: look
-  // after three expected calls, then every 500 us
+  // after three expected calls, then every 500 us -- and every 50 us once the
+  // launch is past its life, when its workgroups leave after their current
+  // calls and the posted calls wait for the relaunch (a waiter that looked only
+  // on its own schedule left them waiting ~1 ms, tens under a kernel tracer)
   int64_t next_look = t0 + std::max<int64_t>(3 * expect, 500000);
+  const int64_t life_ns = pk_life_ms() * 1000000;
+  int64_t aged_look = t0 + 50000;
   for (;;) {
     if (__atomic_load_n(&m->seq_out, __ATOMIC_ACQUIRE) == seq) break;
     const int64_t now = pk_now_ns();
-    if (now > next_look) {
+    const bool aged = now - g_pk.launch_at.load(std::memory_order_relaxed) > life_ns;
+    if (now > next_look || (aged && now > aged_look)) {
       next_look = now + 500000;
+      aged_look = now + 50000;
       std::lock_guard<std::mutex> lk(g_pk.mu);
       if (!pk_running_locked()) {
         if (__atomic_load_n(&m->seq_out, __ATOMIC_ACQUIRE) == seq) break;
