@@ -770,9 +770,45 @@ struct Inflater {
   __device__ void copy_stored(uint32_t src, uint32_t n) {
     uint32_t lane = lane_id();
     uint32_t b = 0;
+    // 4 KiB steps: a lane takes four 16-byte pieces, each as five aligned
+    // dword loads funnel-shifted by the (uniform) source misalignment -- 20
+    // loads in flight per lane, one memory latency per 4 KiB (the 1 KiB steps
+    // of byte loads below paid one per KiB: a 32 KiB stored call of the handle
+    // ABI spent ~32 us on its workgroup).  The loads reach at most 3 bytes
+    // before the step's bytes (the block's LEN / NLEN) and 4 after (inside the
+    // block while b + 4 KiB + 4 <= n).
+    if (src >= 4u) {
+      const uint32_t sh = src & 3u;
+      for (; b + 4096u + 4u <= n; b += 4096u) {
+        uint32_t d[4][4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const uint32_t s0 = src + b + (uint32_t)j * 1024u + lane * 16u;
+          const uint32_t *wp = reinterpret_cast<const uint32_t *>(abase + (s0 & ~3u));
+          uint32_t x[5];
+#pragma unroll
+          for (int q = 0; q < 5; q++) x[q] = wp[q];
+#pragma unroll
+          for (int q = 0; q < 4; q++) d[j][q] = __builtin_amdgcn_alignbyte(x[q + 1], x[q], sh);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const uint32_t o = pos + (uint32_t)j * 1024u + lane * 16u;
+          if ((pos & 3u) == 0) {  // whole dwords (RING is a multiple of 4: none straddles the wrap)
+#pragma unroll
+            for (int q = 0; q < 4; q++) *reinterpret_cast<uint32_t *>(&ring[(o + 4u * q) & RMASK]) = d[j][q];
+          } else {
+#pragma unroll
+            for (int q = 0; q < 16; q++) ring[(o + q) & RMASK] = (uint8_t)(d[j][q >> 2] >> (8 * (q & 3)));
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+        pos += 4096u;
+        maybe_flush();
+      }
+    }
     // 1 KiB steps, 16 bytes per lane: the 16 byte loads of a lane are issued
-    // together (one memory latency per KiB instead of one per 64 bytes: a 32
-    // KiB stored call of the handle ABI took ~40 us in the 64-byte loop)
+    // together (one memory latency per KiB instead of one per 64 bytes)
     for (; b + 1024u <= n; b += 1024u) {
       const uint8_t *sp = abase + src + b + lane * 16u;
       uint8_t v[16];
@@ -2029,9 +2065,18 @@ __global__ void __launch_bounds__(WW_T) zs_stream_pk_kernel(ZsMbox *__restrict__
     {  // input: host-mapped staging -> the job's device buffer; the carried restart bit
       const uint64_t n = job->in_len;
       uint8_t *dst = const_cast<uint8_t *>(job->in);
-      if (io.hin) {
+      if (io.hin) {  // four loads over the bus in flight per thread before their stores
         const uint64_t nw = n / 16u;
-        for (uint64_t k = t; k < nw; k += WW_T) reinterpret_cast<uint4 *>(dst)[k] = reinterpret_cast<const uint4 *>(io.hin)[k];
+        const uint4 *hs = reinterpret_cast<const uint4 *>(io.hin);
+        for (uint64_t k0 = t; k0 < nw; k0 += 4u * WW_T) {
+          uint4 v[4];
+#pragma unroll
+          for (int j = 0; j < 4; j++)
+            if (k0 + j * WW_T < nw) v[j] = hs[k0 + j * WW_T];
+#pragma unroll
+          for (int j = 0; j < 4; j++)
+            if (k0 + j * WW_T < nw) reinterpret_cast<uint4 *>(dst)[k0 + j * WW_T] = v[j];
+        }
         if (t < (n & 15u)) dst[nw * 16u + t] = io.hin[nw * 16u + t];
       }
       if (t == 0) {
@@ -2057,9 +2102,18 @@ __global__ void __launch_bounds__(WW_T) zs_stream_pk_kernel(ZsMbox *__restrict__
     const uint64_t n = s_n;
     if (n && s_mode != (uint32_t)ZSM_HEAD) {  // zs_stream_check_kernel for one call, one piece
       const uint8_t *p = job->out;
-      if (uint8_t *h = io.hout) {
+      if (uint8_t *h = io.hout) {  // (the same: the device loads of up to four stores over the bus first)
         const uint64_t nw = n / 16u;
-        for (uint64_t k = t; k < nw; k += WW_T) reinterpret_cast<uint4 *>(h)[k] = reinterpret_cast<const uint4 *>(p)[k];
+        const uint4 *ps = reinterpret_cast<const uint4 *>(p);
+        for (uint64_t k0 = t; k0 < nw; k0 += 4u * WW_T) {
+          uint4 v[4];
+#pragma unroll
+          for (int j = 0; j < 4; j++)
+            if (k0 + j * WW_T < nw) v[j] = ps[k0 + j * WW_T];
+#pragma unroll
+          for (int j = 0; j < 4; j++)
+            if (k0 + j * WW_T < nw) reinterpret_cast<uint4 *>(h)[k0 + j * WW_T] = v[j];
+        }
         if (t < (n & 15u)) h[nw * 16u + t] = p[nw * 16u + t];
       }
       const int gz = s_gz;
