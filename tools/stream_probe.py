@@ -19,13 +19,20 @@ import zstreams  # noqa: E402
 L = zstreams.lib()
 mib = int(sys.argv[1]) if len(sys.argv) > 1 else 16
 sid = int(sys.argv[2]) if len(sys.argv) > 2 else 32
-r, c = corpus.batch(sid, 1, mib << 20, level=6, wbits=-15, nthreads=1)
-raw, comp = r[0], c[0]
+if len(sys.argv) > 3 and sys.argv[3] == "random":  # the perf harness's data: stored blocks
+    import zlib
+    raw = np.random.default_rng(sid).integers(0, 256, mib << 20, dtype=np.uint8)
+    co = zlib.compressobj(6, zlib.DEFLATED, -15)
+    comp = np.frombuffer(co.compress(raw.tobytes()) + co.flush(), dtype=np.uint8)
+else:
+    r, c = corpus.batch(sid, 1, mib << 20, level=6, wbits=-15, nthreads=1)
+    raw, comp = r[0], c[0]
 out = np.empty((mib << 20) + 65536, dtype=np.uint8)
 names = ["waves", "cyc_total", "windows", "empty", "syms", "bytes", "batches", "jumps", "cyc_decode", "cyc_chain",
          "cyc_expand", "serial", "cyc_window", "cyc_compose", "cyc_walk", "cyc_pre", "cyc_post", "cyc_tables", "steps", "redos"]
 for rep in range(2):
     zstreams.kprof_read(reset=True)
+    s0 = zstreams.stream_stats()
     h = L.inflate_new()
     L.inflate_init_raw(h)
     t0 = time.perf_counter()
@@ -34,7 +41,11 @@ for rep in range(2):
     L.inflate_end(h)
     ok = got == len(raw) and np.array_equal(out[:len(raw)], raw)
     k = zstreams.kprof_read(reset=True)
-    print(f"rep {rep}: {len(raw) / dt / 2**20:.1f} MiB/s, {calls} calls, {dt * 1e6 / calls:.1f} us/call, ok={ok}", flush=True)
+    s1 = zstreams.stream_stats()
+    n = max(1, s1["pk_calls"] - s0["pk_calls"])
+    print(f"rep {rep}: {len(raw) / dt / 2**20:.1f} MiB/s, {calls} calls, {dt * 1e6 / calls:.1f} us/call, ok={ok}; "
+          f"worker {s1['pk_calls'] - s0['pk_calls']} calls, {(s1['pk_busy_ns'] - s0['pk_busy_ns']) / n / 1e3:.1f} us busy, "
+          f"{(s1['pk_wait_ns'] - s0['pk_wait_ns']) / n / 1e3:.1f} us wait per call", flush=True)
     if len(k) >= 96:
         w = dict(zip(names, k[64:64 + len(names)]))
         print("  kprof:", w, flush=True)

@@ -201,6 +201,8 @@ __global__ void zs_header_kernel(const ZsJobDev *__restrict__ jobs, ZsHeadDev *_
 #define WW_MIN_ROOM 512u           // output room below which the serial loop runs
 #define WW_RUN 1u
 #define WW_EXIT 2u
+#define WW_COPY 3u                 // a stored block's bytes into the ring, by all WW_T threads
+#define WW_COPY_MIN 4096u          // stored bytes below which wave 0 copies alone
 
 struct WideLDS {
   // command (wave 0 -> all waves)
@@ -213,6 +215,7 @@ struct WideLDS {
   // its output start (= the bytes admitted), by one 64-bit LDS min
   __attribute__((aligned(8))) unsigned long long nkey;
   uint32_t save, save_pos;     // end of the call: the history ring goes to the handle's state
+  __attribute__((aligned(8))) unsigned long long cp_src;  // WW_COPY: the stored bytes' address (W bytes to ring position pos)
   uint32_t tab_in, tab_out;    // cached dynamic tables (ZsStreamDev::tab_bits) loaded / to save
   uint32_t wtot[WW_T / 64];
   uint32_t sk[WW_T / WW_SKIP];   // chain start of symbols 32 m
@@ -343,6 +346,43 @@ __device__ __forceinline__ uint32_t ww_decode_bits(const WideLDS &w, const uint3
   dv = e_val(d) + ((uint32_t)(hd >> dused) & ((1u << dx) - 1u));
   const uint32_t nb = sb + dused + dx;
   return q + nb > w.limit_bits || nb > 63u ? 0u : nb;
+}
+
+// a stored block's W bytes from cp_src into the ring at pos, run by all WW_T
+// threads (wave 0 posted the command; it flushes them afterwards).  A thread
+// takes 16 bytes at a time as five aligned dword loads funnel-shifted by the
+// source's misalignment (the loads reach <= 3 bytes before the piece -- the
+// block's LEN / NLEN -- and 4 after it, inside the block but for the last
+// pieces, which take byte loads); the ring takes bytes (any output alignment).
+template <bool D64>
+__device__ void ww_copy(StreamLDS<D64> &Ls) {
+  constexpr uint32_t RMASK = (D64 ? 65536u : 32768u) - 1u;
+  WideLDS &w = Ls.wide;
+  uint8_t *ring = Ls.ring;
+  const uint8_t *src = reinterpret_cast<const uint8_t *>((uintptr_t)w.cp_src);
+  const uint32_t m = w.W, pos = w.pos;
+  const uint32_t sh = (uint32_t)((uintptr_t)src & 3u);
+  const uint32_t *a = reinterpret_cast<const uint32_t *>((uintptr_t)src & ~(uintptr_t)3);
+  for (uint32_t i = 16u * threadIdx.x; i < m; i += 16u * WW_T) {
+    uint32_t d[4];
+    if (i + 20u <= m) {
+      uint32_t x[5];
+#pragma unroll
+      for (int q = 0; q < 5; q++) x[q] = a[(i >> 2) + q];
+#pragma unroll
+      for (int q = 0; q < 4; q++) d[q] = __builtin_amdgcn_alignbyte(x[q + 1], x[q], sh);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; q++) d[q] = 0;
+#pragma unroll
+      for (uint32_t q = 0; q < 16; q++)
+        if (i + q < m) d[q >> 2] |= (uint32_t)src[i + q] << (8u * (q & 3u));
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < 16; q++)
+      if (i + q < m) ring[(pos + i + q) & RMASK] = (uint8_t)(d[q >> 2] >> (8u * (q & 3u)));
+  }
+  __syncthreads();  // the ring holds the bytes before wave 0 flushes them
 }
 
 // the window, run by all WW_T threads (wave 0 posted the command)
@@ -770,6 +810,29 @@ struct Inflater {
   __device__ void copy_stored(uint32_t src, uint32_t n) {
     uint32_t lane = lane_id();
     uint32_t b = 0;
+    if constexpr (WIDE) {
+      // the stream kernel: the whole workgroup copies (its other waves idle
+      // through a stored block otherwise: a 32 KiB stored call spent ~25 K of
+      // its ~41 K wave-0 cycles here), 16 KiB at a time so that the ring's
+      // unflushed bytes never wrap onto themselves
+      if (wide != nullptr && src >= 4u) {
+        while (n - b >= WW_COPY_MIN) {
+          const uint32_t m = min(n - b, 16384u);
+          WideLDS &w = wide->wide;
+          if (lane == 0) {
+            w.op = WW_COPY;
+            w.W = m;
+            w.pos = pos;
+            w.cp_src = (unsigned long long)(uintptr_t)(abase + src + b);
+          }
+          __syncthreads();  // the other waves wait here for a command
+          ww_copy<D64>(*wide);
+          pos += m;
+          b += m;
+          maybe_flush();
+        }
+      }
+    }
     // 4 KiB steps: a lane takes four 16-byte pieces, each as five aligned
     // dword loads funnel-shifted by the (uniform) source misalignment -- 20
     // loads in flight per lane, one memory latency per 4 KiB (the 1 KiB steps
@@ -777,7 +840,7 @@ struct Inflater {
     // ABI spent ~32 us on its workgroup).  The loads reach at most 3 bytes
     // before the step's bytes (the block's LEN / NLEN) and 4 after (inside the
     // block while b + 4 KiB + 4 <= n).
-    if (src >= 4u) {
+    if (!WIDE && src >= 4u) {  // (the stream kernel's wave 0 took the bulk to its workgroup above)
       const uint32_t sh = src & 3u;
       for (; b + 4096u + 4u <= n; b += 4096u) {
         uint32_t d[4][4];
@@ -1764,9 +1827,11 @@ __device__ __forceinline__ void zs_stream_wg(ZsStreamDev *__restrict__ st, const
   __syncthreads();
   if (t >= WAVE) {
     for (;;) {
-      __syncthreads();  // a window posted by wave 0, or the end of the call
-      if (L.wide.op == WW_EXIT) break;
-      ww_run<D64>(L);
+      __syncthreads();  // a window or a stored copy posted by wave 0, or the end of the call
+      const uint32_t op = L.wide.op;
+      if (op == WW_EXIT) break;
+      if (op == WW_COPY) ww_copy<D64>(L);
+      else ww_run<D64>(L);
     }
   } else {
     zs_stream_call<D64>(st, job, head, L);
@@ -2047,7 +2112,7 @@ __global__ void __launch_bounds__(WW_T) zs_stream_pk_kernel(ZsMbox *__restrict__
           break;
         }
         for (uint32_t k = 0; k < nap; k++) __builtin_amdgcn_s_sleep(32);
-        nap = min(nap * 2u, 8u);
+        nap = min(nap * 2u, 4u);  // <= ~4 us between polls (8: a posted call waited ~4 us on average to be seen)
       }
       if (cmd) {  // the call's fields after its seq_in (system-scope acquire)
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
