@@ -1397,9 +1397,7 @@ int pk_submit(StreamCall *c, int w) {
         }
       }
     }
-    // short calls (stored blocks: ~35 us) poll every 3 us, others every 6 us, long waits every 25 us
-    std::this_thread::sleep_for(
-        std::chrono::microseconds(now - t0 >= 3 * std::max<int64_t>(expect, 100000) ? 25 : (expect < 100000 ? 3 : 6)));
+    std::this_thread::sleep_for(std::chrono::microseconds(now - t0 < 3 * std::max<int64_t>(expect, 100000) ? 6 : 25));
   }
   if (slack) (void)prctl(PR_SET_TIMERSLACK, (unsigned long)prev_slack, 0, 0, 0);
   const uint64_t waited = (uint64_t)(pk_now_ns() - t0);
