@@ -462,3 +462,43 @@ def test_persistent_worker_life_expiry_relaunch(zs):
         assert d["ok"] and d["comp_len"] == len(comp) and d.pop("trace") == etr
     assert short["pk_launches"] >= 4, short
     assert short["seconds"] < base["seconds"] + 0.002 * short["pk_launches"] + 0.05, (short, base)
+
+
+def test_persistent_worker_small_call_after_large_does_not_oversleep(zs):
+    """the waiter sleeps most of the handle's last call on
+    the worker before polling, scaled down by this call's input (never up), so
+    a 1 KiB call right after a 512 KiB one (up to 4 MiB out, milliseconds on the
+    worker) does not sleep for milliseconds.  One handle alternates 512 KiB and
+    1 KiB calls over 24 MiB of line text: the output equals the input and no
+    small call takes 5 ms (the median under 1 ms)."""
+    import time
+    L = zs.lib()
+    prev = zs.stream_persist(True)
+    raw = corpus.stream(37, 24 << 20)
+    comp = _comp(raw, -15)
+    lat = []
+    try:
+        h = L.inflate_new()
+        assert L.inflate_init_raw(h) == 0
+        ib = ctypes.create_string_buffer(comp, len(comp))
+        ob = ctypes.create_string_buffer(4 << 20)  # (calls within the 4 MiB staging stay on the worker)
+        off, got, k = 0, bytearray(), 0
+        while True:
+            n = min((512 << 10) if k % 2 == 0 else 1024, len(comp) - off)
+            t0 = time.perf_counter()
+            r = L.inflate_process(h, ctypes.addressof(ib) + off, n, ctypes.addressof(ob), len(ob), 0)
+            dt = time.perf_counter() - t0
+            if k % 2 == 1:
+                lat.append(dt)
+            k += 1
+            prod, code = r & 0xffffff, (r >> 24) & 0xff
+            got += ob.raw[:prod]
+            off += L.inflate_last_consumed(h)
+            if code != 0:
+                break
+        assert L.inflate_end(h) == 0
+    finally:
+        zs.stream_persist(prev)
+    assert code == 1 and bytes(got) == raw
+    lat.sort()
+    assert len(lat) >= 5 and lat[-1] < 0.005 and lat[len(lat) // 2] < 0.001, lat
