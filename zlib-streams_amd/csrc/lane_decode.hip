@@ -1971,6 +1971,12 @@ static_assert(WKL_BITS + 1u >= WK_LBITS && WKL_BITS <= WK_LBITS && WKD_BITS + 1u
 #define WK_PF 16u   // words per prefetch: the ring is two such halves
 #define WK_RW 32u   // input ring words per lane
 #define WK_RS 35u   // a lane's ring row: WK_RW words, words 0 and 1 again (a 3-word read never wraps), odd stride
+#ifndef WK_RIL
+#define WK_RIL 1    // the lanes' ring rows interleaved (word k of lane L at [k][L]: every ring read conflict-free)
+#endif
+#define WK_WS (WK_RIL ? WAVE : 1u)  // u32 elements between consecutive words of a lane's ring
+// a lane's ring row in a wave's ring of WAVE * WK_RS words
+#define WK_ROW(ring, lane) ((ring) + (WK_RIL ? (lane) : (lane) * WK_RS))
 #define WK_DT0 6u   // the distance tail's words from here on live in LDS (its symbols: bytes 27 ..)
 #define WK_DTN 9u
 // The tables are lane-interleaved (dword k of lane L at [k][L]): whatever
@@ -1983,7 +1989,7 @@ struct WalkLDS {
   uint32_t wl[(1u << WKL_BITS) / 4][WAVE];
   uint32_t wd[(1u << WKD_BITS) / 4][WAVE];
   uint32_t dtail[WK_DTN][WAVE];  // words WK_DT0 .. of the block's canonical distance tail (codes past WKD_BITS)
-  uint32_t ring[WAVE][WK_RS];
+  uint32_t ring[WAVE * WK_RS];
 };
 // byte i of a lane's interleaved u8 table (base = &table[0][lane])
 __device__ __forceinline__ uint32_t wk_byte(const uint32_t *base, uint32_t i) {
@@ -2114,12 +2120,12 @@ __device__ __forceinline__ void walk_put_half(uint32_t *rr, uint32_t wi, uint32_
 #pragma unroll
     for (uint32_t q = 0; q < WK_PF; q++) v[q] = walk_mask(v[q], wi + q, end_byte);
   }
-  uint32_t *h = rr + (wi & WK_PF);
+  uint32_t *h = rr + (wi & WK_PF) * WK_WS;
 #pragma unroll
-  for (uint32_t q = 0; q < WK_PF; q++) h[q] = v[q];
+  for (uint32_t q = 0; q < WK_PF; q++) h[q * WK_WS] = v[q];
   if (!(wi & WK_PF)) {
-    rr[WK_RW] = v[0];
-    rr[WK_RW + 1] = v[1];
+    rr[WK_RW * WK_WS] = v[0];
+    rr[(WK_RW + 1u) * WK_WS] = v[1];
   }
 }
 
@@ -2153,7 +2159,7 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
   uint32_t *wl = &L.wl[0][lane];
   uint32_t *wd = &L.wd[0][lane];
   uint32_t *dtl = &L.dtail[0][lane];
-  uint32_t *rr = &L.ring[lane][0];
+  uint32_t *rr = WK_ROW(L.ring, lane);
   s.dta = s.dtb = make_uint4(0, 0, 0, 0);
   WalkLitTail ltw;  // the literal/length code's canonical tail (registers)
 #pragma unroll
@@ -2288,10 +2294,10 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
       const bool pend = live && xp;
       uint32_t x0 = 0, x1 = 0, x2 = 0, bits = 0, e2 = 0;
       if (pend) {
-        const uint32_t *r = rr + ((p >> 5) & (WK_RW - 1u));
+        const uint32_t *r = rr + ((p >> 5) & (WK_RW - 1u)) * WK_WS;
         x0 = r[0];
-        x1 = r[1];
-        x2 = r[2];
+        x1 = r[WK_WS];
+        x2 = r[2u * WK_WS];
         bits = __builtin_amdgcn_alignbit(x1, x0, p);
         e2 = wk_byte(wl, bits & ((1u << WKL_BITS) - 1u));
       }
@@ -2369,8 +2375,8 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
 #pragma unroll
       for (uint32_t g = 0; g < GS; g++) {
         pk[g] = p;
-        lds_cu32 *r = (lds_cu32 *)(uintptr_t)(rra + 4u * __builtin_amdgcn_ubfe(p, 5, 5));
-        const uint32_t x0 = r[0], x1 = r[1], x2 = r[2];
+        lds_cu32 *r = (lds_cu32 *)(uintptr_t)(rra + 4u * WK_WS * __builtin_amdgcn_ubfe(p, 5, 5));
+        const uint32_t x0 = r[0], x1 = r[WK_WS], x2 = r[2u * WK_WS];
         const uint32_t lo = __builtin_amdgcn_alignbit(x1, x0, p);  // input bits [p, p + 32)
         const uint32_t hi = __builtin_amdgcn_alignbit(x2, x1, p);  // [p + 32, p + 64)
         const uint32_t e = wk_byte_a(wla, lo, WKL_BITS);
@@ -2489,7 +2495,7 @@ struct __attribute__((aligned(16))) SplitLDS {
   uint32_t dw[1u << SPD_BITS];
   uint32_t dtail[DTAIL_BYTES / 4];
   uint32_t tokbuf[D64 ? 2u * SP_GS(true) : 1u][WAVE];  // deflate64: a group's tokens (two per step at most); else in registers
-  uint32_t ring[WAVE][WK_RS];
+  uint32_t ring[WAVE * WK_RS];
 };
 struct SplitLane {
   uint32_t p, ntok, pos, need, bad, gk;
@@ -2504,8 +2510,8 @@ __device__ __forceinline__ void split_step3(SplitLane &t, uint32_t rra, const ui
                                             uint4 dta, uint4 dtb, const uint32_t *__restrict__ dtl, gcu16 *cl,
                                             uint32_t lbits) {
   typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
-  lds_cu32 *r = (lds_cu32 *)(uintptr_t)(rra + ((t.p >> 3) & ((WK_RW - 1u) * 4u)));
-  const uint32_t x0 = r[0], x1 = r[1], x2 = r[2];
+  lds_cu32 *r = (lds_cu32 *)(uintptr_t)(rra + ((t.p >> 5) & (WK_RW - 1u)) * (4u * WK_WS));
+  const uint32_t x0 = r[0], x1 = r[WK_WS], x2 = r[2u * WK_WS];
   const uint32_t hl = __builtin_amdgcn_alignbit(x1, x0, t.p), hh = __builtin_amdgcn_alignbit(x2, x1, t.p);
   uint32_t e = lw[hl & ((1u << SPL_BITS) - 1u)];
   if (__builtin_expect(__builtin_amdgcn_ballot_w64(((e >> 4) & 3u) == SK_SLOW) != 0, 0)) {
@@ -2565,7 +2571,7 @@ __device__ __forceinline__ void split_sub3(SplitLDS<D64> &L, SplitLane &t, LaneS
 ) {
   const uint32_t lane = threadIdx.x;
   uint32_t *tb = &L.tokbuf[0][lane];
-  uint32_t *rr = &L.ring[lane][0];
+  uint32_t *rr = WK_ROW(L.ring, lane);
   constexpr uint32_t GS = SP_GS(D64), TPS = D64 ? 2u : 1u;
   // !D64: a group's tokens are stored one group late, right after the next
   // refill's wait (vmcnt counts stores too: stored at the end of their own
@@ -2790,7 +2796,7 @@ __global__ void __launch_bounds__(64) zs_split_kernel(const ZsJobDev *__restrict
     t.p = a.x;
     t.ntok = a.y;
     t.pos = t.need = t.bad = t.gk = 0;
-    uint32_t *rr = &L.ring[lane][0];
+    uint32_t *rr = WK_ROW(L.ring, lane);
     uint32_t filled = (t.p >> 5) & ~(WK_PF - 1u), pre[WK_PF];
     if (act) {  // both halves now (words filled .. filled + 31), then the next prefetch
       walk_prefetch(s, filled, pre);
