@@ -653,3 +653,25 @@ def test_split_parse_first_unit_too_far(zs):
         eo, ei = O.oneshot(comp, -15, cap)
         assert out == eo and info == ei, (info, ei)
     assert got[0][1]["ret"] == -3 and got[1][0] == raw
+
+
+@pytest.mark.parametrize("parse", ["split", "lane"])
+def test_all_literals_on_one_long_length(zs, parse):
+    """a dynamic code with all 256 literals, end of block and
+    length 257 on 10-bit codes (tests/crafted.py), 0xFF a frequent literal.
+    The walk's canonical tail must count 256 literals of one length (a u8 count
+    read literal 0xFF as the end of block: truncated output, silent for raw
+    deflate); the split decode also checks the code at the walked end of block.
+    Every field vs the oracle and host zlib, raw / zlib / gzip wrappers."""
+    import crafted
+    raw, comp = crafted.long_literal_stream(2 << 20, seed=7)
+    zwrap = bytes([0x78, 0x01]) + comp + zlib.adler32(raw).to_bytes(4, "big")
+    gwrap = (bytes([0x1f, 0x8b, 8, 0, 0, 0, 0, 0, 0, 3]) + comp + zlib.crc32(raw).to_bytes(4, "little")
+             + (len(raw) & 0xffffffff).to_bytes(4, "little"))
+    cases = [(raw, comp, -15), (raw, zwrap, 15), (raw, gwrap, 31), (raw, comp, -15)]
+    got = zs.inflate_batch([c[1] for c in cases], [c[2] for c in cases], [len(raw)] * len(cases), parse=parse)
+    st = zs.last_stats()
+    assert st["parse"] == parse and st["chunked_jobs"] == len(cases) and st["fallback_jobs"] == 0, st
+    for (r, c, wb), (out, info) in zip(cases, got):
+        eo, ei = O.oneshot(c, wb, len(r))
+        assert out == eo == r and info == ei and info["ret"] == 1, (wb, info, ei)

@@ -461,7 +461,9 @@ def test_persistent_worker_life_expiry_relaunch(zs):
     for d in (short, base):
         assert d["ok"] and d["comp_len"] == len(comp) and d.pop("trace") == etr
     assert short["pk_launches"] >= 4, short
-    assert short["seconds"] < base["seconds"] + 0.002 * short["pk_launches"] + 0.05, (short, base)
+    # wall-clock bound with a margin for host scheduling: the bug it
+    # guards against stranded posted calls for ~1 ms (tens under a tracer) per relaunch
+    assert short["seconds"] < base["seconds"] + 0.005 * short["pk_launches"] + 0.25, (short, base)
 
 
 def test_persistent_worker_small_call_after_large_does_not_oversleep(zs):
@@ -501,4 +503,7 @@ def test_persistent_worker_small_call_after_large_does_not_oversleep(zs):
         zs.stream_persist(prev)
     assert code == 1 and bytes(got) == raw
     lat.sort()
-    assert len(lat) >= 5 and lat[-1] < 0.005 and lat[len(lat) // 2] < 0.001, lat
+    # the oversleep this guards against is >= 1.25 ms on EVERY small call (5/8
+    # of the 512 KiB call's worker time, capped at 2 ms): the median tells;
+    # single outliers are host scheduling (margin on the maximum)
+    assert len(lat) >= 5 and lat[-1] < 0.05 and lat[len(lat) // 2] < 0.001, lat

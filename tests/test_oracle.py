@@ -82,3 +82,13 @@ def test_checks_match_zlib():
         b = bytes(rng.getrandbits(8) for _ in range(n))
         assert O.lib().zo_crc32(0, b, n) == zlib.crc32(b)
         assert O.lib().zo_adler32(1, b, n) == zlib.adler32(b)
+
+
+def test_crafted_all_literals_on_one_long_length():
+    """tests/crafted.py's 10-bit-literal dynamic blocks (the GPU test
+    test_all_literals_on_one_long_length): the oracle and host zlib agree."""
+    import crafted
+    raw, comp = crafted.long_literal_stream(200 << 10, seed=3, block_syms=3000)
+    assert zlib.decompress(comp, -15) == raw
+    out, info = O.oneshot(comp, -15, len(raw))
+    assert out == raw and info["ret"] == 1 and info["total_in"] == len(comp)

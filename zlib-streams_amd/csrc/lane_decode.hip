@@ -736,7 +736,8 @@ __device__ void build_dist_tail(const uint16_t *dl, uint32_t n, uint8_t *out) {
 // The literal/length code's canonical tail for the split parse's walk (codes
 // longer than its 9-bit table), 16 words: 0-3 the left-justified 15-bit
 // limits of lengths 9..15 (u16 each, lim[L] = (first[L] + count[L]) << (15 - L)),
-// 4-5 the literal count of each length 10..15 (u8, capped at 255), 6-7 for
+// 4-5 the literal count of each length 10..15 (9 bits each, three per word:
+// 0..256), 6-7 for
 // each length 10..15 the index in the list below of its first symbol >= 256
 // (u8), 8-15 that list: the symbols >= 256 (end of block, lengths) whose codes
 // are longer than 9 bits, in canonical order, as sym - 256 (u8).  Canonical
@@ -803,8 +804,9 @@ __device__ void build_lit_tail(const uint16_t *ll, uint32_t n, uint32_t *out) {
     out[1] = lim[11] | (lim[12] << 16);
     out[2] = lim[13] | (lim[14] << 16);
     out[3] = lim[15];
-    out[4] = min(nlit[10], 255u) | (min(nlit[11], 255u) << 8) | (min(nlit[12], 255u) << 16) | (min(nlit[13], 255u) << 24);
-    out[5] = min(nlit[14], 255u) | (min(nlit[15], 255u) << 8);
+    // 9-bit counts: a complete code may put all 256 literals on one length
+    out[4] = nlit[10] | (nlit[11] << 9) | (nlit[12] << 18);
+    out[5] = nlit[13] | (nlit[14] << 9) | (nlit[15] << 18);
     out[6] = nbase[10] | (nbase[11] << 8) | (nbase[12] << 16) | (nbase[13] << 24);
     out[7] = nbase[14] | (nbase[15] << 8);
   }
@@ -2062,13 +2064,13 @@ __device__ __forceinline__ uint32_t walk_lit_tail(const WalkLitTail &T, uint32_t
   const uint32_t rev = __builtin_bitreverse32(bits) >> 17;  // the next 15 bits, first bit highest
   const uint32_t lim[7] = {lt[0] & 0xffffu, lt[0] >> 16, lt[1] & 0xffffu, lt[1] >> 16,
                            lt[2] & 0xffffu, lt[2] >> 16, lt[3] & 0xffffu};  // lengths 9 .. 15
-  uint32_t L = 10, fl = lim[0], nl = lt[4] & 0xffu, nb = lt[6] & 0xffu;
+  uint32_t L = 10, fl = lim[0], nl = lt[4] & 0x1ffu, nb = lt[6] & 0xffu;
 #pragma unroll
   for (int k = 1; k < 6; k++) {
     const bool ge = rev >= lim[k];
     L += ge ? 1u : 0u;
     fl = ge ? lim[k] : fl;
-    nl = ge ? ((lt[4 + (k >> 2)] >> (8 * (k & 3))) & 0xffu) : nl;
+    nl = ge ? ((lt[4 + k / 3] >> (9 * (k % 3))) & 0x1ffu) : nl;
     nb = ge ? ((lt[6 + (k >> 2)] >> (8 * (k & 3))) & 0xffu) : nb;
   }
   if (rev < lim[0] || rev >= lim[6]) return WK_EXC;  // not a long code of this table: invalid
@@ -2832,6 +2834,20 @@ __global__ void __launch_bounds__(64) zs_split_kernel(const ZsJobDev *__restrict
     const bool full = act && t.pos > s.capx;
     uint32_t bad = (t.bad & 0x20u) ? 1u : 0u;
     if (act && !full && (t.p != b1 || t.ntok != t1)) bad = 1;
+    if (act && !full && !bad && lane + 1u == wk.nsub) {
+      // the walk's end of block, checked: the code at eob_bit must decode to
+      // end-of-block and take end_bit - eob_bit bits (src/inflate.c:1125-1129)
+      const uint32_t *r = rr + ((b1 >> 5) & (WK_RW - 1u)) * WK_WS;
+      const uint32_t hl = __builtin_amdgcn_alignbit(r[WK_WS], r[0], b1);
+      uint32_t e = L.lw[hl & ((1u << SPL_BITS) - 1u)];
+      if (((e >> 4) & 3u) == SK_SLOW) {
+        uint32_t e2 = s.cl[hl & ((1u << s.lbits) - 1u)];
+        const uint32_t op2 = (e2 >> 2) & 15u;
+        if ((e2 & 3u) == CK_SLOW && op2) e2 = s.cl[(e2 >> 6) + ((hl >> s.lbits) & ((1u << op2) - 1u))];
+        e = split_len_entry<D64>(e2);
+      }
+      if (((e >> 4) & 3u) != SK_EOB || b1 + (e & 15u) != wk.end_bit) bad = 1;
+    }
     const bool anybad = __ballot(act && bad) != 0, anyfull = __ballot(full) != 0;
     // output position of every sub-unit: a wave scan of their entry counts
     uint64_t incl = act ? t.pos : 0u;

@@ -1302,7 +1302,6 @@ int pk_launch_locked() {
   const uint64_t idle_t = (uint64_t)pk_idle_us() * 100u;  // s_memrealtime ticks (100 MHz)
   const uint64_t life_t = (uint64_t)pk_life_ms() * 100000u;
   __atomic_store_n(&g_pk.h_ctl[2], 0u, __ATOMIC_SEQ_CST);  // the last launch's closing flag (it has drained)
-  pk_defer_flush_locked();  // device frees deferred while a launch ran (stream_free)
   g_pk.launch_at.store(pk_now_ns());
   zs_launch_stream_pk(g_pk.d_mb, (uint32_t)g_pk.nw, g_pk.d_ctl, idle_t, life_t, g_pk.st);
   HIP_OK(hipGetLastError());
@@ -1312,14 +1311,24 @@ int pk_launch_locked() {
   return 0;
 }
 
-// the handle's mailbox (taken on first use), or -1: the batch path
-int pk_attach(StreamState *s) {
-  if (s->pk_w >= 0) return s->pk_w;
-  std::lock_guard<std::mutex> lk(g_pk.mu);
-  if (pk_init_locked() || g_pk.broken || g_pk.free_w.empty()) return -1;
-  s->pk_w = g_pk.free_w.back();
-  g_pk.free_w.pop_back();
-  return s->pk_w;
+// Relaunch the worker unless it runs (caller holds lk on g_pk.mu).  Device
+// buffers deferred by stream_free are freed first -- the last launch has
+// drained, so hipFree does not wait for it -- with the lock released, so that
+// other handles' waiters do not queue behind the device-wide synchronisation;
+// a launch another thread made meanwhile is taken as this one's.
+int pk_relaunch(std::unique_lock<std::mutex> &lk) {
+  if (pk_running_locked()) return 0;
+  if (!g_defer_dev.empty() || !g_defer_host.empty()) {
+    std::vector<void *> dv, hv;
+    dv.swap(g_defer_dev);
+    hv.swap(g_defer_host);
+    lk.unlock();
+    for (void *p : dv) (void)hipFree(p);
+    for (void *p : hv) (void)hipHostFree(p);
+    lk.lock();
+    if (pk_running_locked()) return 0;
+  }
+  return pk_launch_locked();
 }
 
 void pk_detach(StreamState *s) {  // the handle's calls are all finished
@@ -1327,6 +1336,23 @@ void pk_detach(StreamState *s) {  // the handle's calls are all finished
   std::lock_guard<std::mutex> lk(g_pk.mu);
   g_pk.free_w.push_back(s->pk_w);
   s->pk_w = -1;
+}
+
+// the handle's mailbox (taken on first use), or -1: the batch path.  Once a
+// launch has failed (g_pk.broken) a handle that still holds a mailbox gives it
+// up, so its calls take the batch path like new handles' instead of retrying
+// the launch on every call.
+int pk_attach(StreamState *s) {
+  if (s->pk_w >= 0) {
+    if (!__atomic_load_n(&g_pk.broken, __ATOMIC_ACQUIRE)) return s->pk_w;
+    pk_detach(s);
+    return -1;
+  }
+  std::lock_guard<std::mutex> lk(g_pk.mu);
+  if (pk_init_locked() || g_pk.broken || g_pk.free_w.empty()) return -1;
+  s->pk_w = g_pk.free_w.back();
+  g_pk.free_w.pop_back();
+  return s->pk_w;
 }
 
 // A launch that fails after the call was posted: withdraw the call (seq_in
@@ -1337,7 +1363,7 @@ int pk_fail_locked(ZsMbox *m, int w, int rc) {
   const uint32_t prev = __atomic_load_n(&m->seq_out, __ATOMIC_ACQUIRE);
   __atomic_store_n(&m->seq_in, prev, __ATOMIC_SEQ_CST);
   g_pk.seq[w] = prev;
-  g_pk.broken = true;
+  __atomic_store_n(&g_pk.broken, true, __ATOMIC_RELEASE);
   return rc;
 }
 
@@ -1354,9 +1380,8 @@ int pk_submit(StreamCall *c, int w) {
   // a post within half the idle time of the previous one finds the launch alive
   // (its workgroups saw that post and wait PK_IDLE after it); else look
   if (t0 - g_pk.last_post.exchange(t0) > pk_idle_us() * 500) {
-    std::lock_guard<std::mutex> lk(g_pk.mu);
-    if (!pk_running_locked())
-      if (int rc = pk_launch_locked()) return pk_fail_locked(m, w, rc);
+    std::unique_lock<std::mutex> lk(g_pk.mu);
+    if (int rc = pk_relaunch(lk)) return pk_fail_locked(m, w, rc);
   }
   // sleep through most of the expected call, then poll with short sleeps: many
   // handles' threads spinning would spend the host's CPU quota (a
@@ -1388,10 +1413,10 @@ int pk_submit(StreamCall *c, int w) {
     if (now > next_look || (aged && now > aged_look)) {
       next_look = now + 500000;
       aged_look = now + 50000;
-      std::lock_guard<std::mutex> lk(g_pk.mu);
+      std::unique_lock<std::mutex> lk(g_pk.mu);
       if (!pk_running_locked()) {
         if (__atomic_load_n(&m->seq_out, __ATOMIC_ACQUIRE) == seq) break;
-        if (int rc = pk_launch_locked()) {
+        if (int rc = pk_relaunch(lk)) {
           if (slack) (void)prctl(PR_SET_TIMERSLACK, (unsigned long)prev_slack, 0, 0, 0);
           return pk_fail_locked(m, w, rc);
         }
