@@ -21,7 +21,10 @@ NAMES = {0: "p_waves", 1: "p_cyc_total", 2: "p_cyc_coop", 3: "p_cyc_steps", 4: "
          32: "d_cyc_out", 33: "d_chunks",
 
          48: "l_streams", 49: "l_steps", 50: "l_cyc_succ", 51: "l_cyc_walk", 52: "l_cyc_winwrite", 53: "l_cyc_resolve",
-         54: "l_cyc_barrier", 55: "l_markers_sample", 56: "l_cyc_total", 57: "l_cyc_max"}
+         54: "l_cyc_barrier", 55: "l_markers_sample", 56: "l_cyc_total", 57: "l_cyc_max",
+         # finder validation (zs_findval_kernel, round 6: a pool of candidates per wave): waves, refill
+         # rounds, cycles in symbol steps, wave-steps, lane-steps (lanes with a live candidate), wave cycles
+         58: "fv_waves", 59: "fv_rounds", 60: "fv_cyc_steps", 61: "fv_wave_steps", 62: "fv_lane_steps", 63: "fv_cyc_total"}
 
 
 def main():
@@ -95,6 +98,12 @@ def main():
         "walk_refill_cycles_per_step": d.get("p_cyc_busy", 0) / max(d.get("w_wave_steps", 0), 1),
         "walk_exc_per_step": d.get("w_exc", 0) / max(d.get("w_wave_steps", 0), 1),
         "split_cycles_per_wave_step": d.get("s_lit", 0) / max(d.get("s_refill2", 0), 1),
+        # finder validation pool: lane utilisation, cycles per wave-step, share of the wave's time in steps
+        "fv_lane_util": d.get("fv_lane_steps", 0) / max(64 * d.get("fv_wave_steps", 0), 1),
+        "fv_cycles_per_wave_step": d.get("fv_cyc_steps", 0) / max(d.get("fv_wave_steps", 0), 1),
+        "fv_steps_frac": d.get("fv_cyc_steps", 0) / max(d.get("fv_cyc_total", 0), 1),
+        "fv_wave_steps_per_round": d.get("fv_wave_steps", 0) / max(d.get("fv_rounds", 0), 1),
+        "fv_cycles_per_wave": d.get("fv_cyc_total", 0) / max(d.get("fv_waves", 0), 1),
     }
     out = {"raw": d, "derived": derived}
     print(json.dumps(out, indent=1))

@@ -21,6 +21,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "zs_common.h"
 #include "zs_device.h"
 #include "zs_kprof.h"
@@ -41,137 +43,191 @@ __device__ unsigned long long g_kprof_ck[16];  // KP_L_* - 48
 // (complete code-length code, repeat rules, end-of-block present, literal and
 // distance codes complete or a single 1-bit code, empty distance code allowed).
 // ---------------------------------------------------------------------------
-template <bool D64>
-__device__ bool validate_header(const uint32_t *w, uint32_t end_byte, uint32_t bit, uint8_t *lut) {
-  const uint32_t limit = end_byte * 8u;
-  uint32_t wi = bit >> 5;
-  uint64_t hold = (uint64_t)in_word(w, wi, end_byte) >> (bit & 31);
-  uint32_t n = 32 - (bit & 31);
-  wi++;
-  auto refill = [&]() {
-    while (n <= 32) {
-      hold |= (uint64_t)in_word(w, wi, end_byte) << n;
-      n += 32;
-      wi++;
-    }
-  };
-  auto pos = [&]() { return wi * 32u - n; };
-  refill();
-  hold >>= 3;
-  n -= 3;
-  const uint32_t nlen = (uint32_t)(hold & 31) + 257, ndist = (uint32_t)((hold >> 5) & 31) + 1;
-  const uint32_t ncode = (uint32_t)((hold >> 10) & 15) + 4;
-  hold >>= 14;
-  n -= 14;
-  if (nlen > 286 || ndist > (D64 ? 32u : 30u)) return false;
-  uint8_t cl[19];
+// The input comes from a per-lane window of VWIN words in LDS (win: the
+// lane's column of a [VWIN][WAVE] array, lane-interleaved), loaded by 16-byte
+// loads when the validation starts and again whenever the reader leaves it
+// (a long header): a global load per 32 bits made some lane of the wave
+// refill on nearly every code-length symbol.  The symbol loop is straight
+// line (selects, one reload site): the round-5 loop (a bit buffer refilled by
+// an unrolled inner loop, branches per repeat code) compiled to ~2 000
+// instructions of exec-mask branches and cost ~1 500-2 000 cycles per symbol
+// of the wave's longest lane (profiling build, C2).
+#ifndef VWIN
+#define VWIN 32u
+#endif
+// One candidate's validation state (a lane of zs_findval_kernel).
+// The code-length code is decoded canonically from registers (no per-lane
+// LUT: filling 128 LUT bytes per candidate cost ~60% of the pool's time, and
+// its 8 KiB per wave capped the occupancy): lim_L, the left-justified end of
+// the length-L codes in the 7-bit code space (= the partial Kraft sums), as
+// bytes P1 (L = 1..4) / P2 (5..6); the code's length is 1 + the number of
+// lim_L <= the next 7 bits read first-bit-first (a SWAR byte compare); BA/BB
+// the start of each length's range and OA/OB the rank of its first symbol
+// (bytes, L = 1..4 / 5..7); SL/SH the symbols in canonical order (5 bits
+// each, ranks 0..11 / 12..18).
+struct VState {
+  const uint32_t *w;  // input (4-byte-aligned base)
+  uint32_t end_byte, wb;  // input length from w; window base word
+  uint32_t p, have, prev, eob, lk, lmax, dk, dmax, dn, nlen, total;
+  uint32_t P1, P2, BA, BB, OA, OB;
+  uint64_t SL, SH;
+};
+// the lane's window: VWIN words of input from word `at` rounded down to 4
+__device__ __forceinline__ void vwin_load(VState &v, uint32_t at, uint32_t *win) {
+  v.wb = at & ~3u;
+  if (v.wb + VWIN <= (v.end_byte >> 2)) {
+    const uint32_t *src = v.w + v.wb;
 #pragma unroll
-  for (int i = 0; i < 19; i++) cl[i] = 0;
-  const uint8_t ord[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+    for (uint32_t h = 0; h < VWIN / 16u; h++) {  // 16 words at a time (fewer registers in flight)
+      uint4 x[4];
 #pragma unroll
-  for (int i = 0; i < 19; i++) {
-    if ((uint32_t)i < ncode) {
-      refill();
-      cl[ord[i]] = (uint8_t)(hold & 7);
-      hold >>= 3;
-      n -= 3;
+      for (uint32_t q = 0; q < 4u; q++) __builtin_memcpy(&x[q], src + 16u * h + 4u * q, 16);
+#pragma unroll
+      for (uint32_t q = 0; q < 4u; q++) {
+        win[(16u * h + 4u * q) * WAVE] = x[q].x;
+        win[(16u * h + 4u * q + 1u) * WAVE] = x[q].y;
+        win[(16u * h + 4u * q + 2u) * WAVE] = x[q].z;
+        win[(16u * h + 4u * q + 3u) * WAVE] = x[q].w;
+      }
     }
+  } else {
+#pragma unroll 1
+    for (uint32_t q = 0; q < VWIN; q++) win[q * WAVE] = in_word(v.w, v.wb + q, v.end_byte);
   }
-  // canonical codes of the code-length code -> 7-bit LUT (sym | len << 5)
-  uint32_t cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+}
+enum { VS_RUN = 0, VS_OK = 1, VS_BAD = 2 };
+// header, code-length code and its LUT of the candidate at `bit`
+template <bool D64>
+__device__ uint32_t val_setup(VState &v, uint32_t bit, uint32_t *win) {
+  vwin_load(v, bit >> 5, win);
+  // the header's 14 + 3 * 19 bits lie in the window's first 5 words
+  const uint32_t r0 = (bit >> 5) - v.wb, sh = bit & 31u;
+  const uint32_t h0 = __builtin_amdgcn_alignbit(win[(r0 + 1u) * WAVE], win[r0 * WAVE], sh);
+  const uint32_t h1 = __builtin_amdgcn_alignbit(win[(r0 + 2u) * WAVE], win[(r0 + 1u) * WAVE], sh);
+  const uint32_t h2 = __builtin_amdgcn_alignbit(win[(r0 + 3u) * WAVE], win[(r0 + 2u) * WAVE], sh);
+  v.nlen = ((h0 >> 3) & 31u) + 257u;
+  const uint32_t ndist = ((h0 >> 8) & 31u) + 1u, ncode = ((h0 >> 13) & 15u) + 4u;
+  if (v.nlen > 286 || ndist > (D64 ? 32u : 30u)) return VS_BAD;
+  // the 19 3-bit code-length-code lengths from bit 17, in stream order, masked to ncode
+  const uint64_t cls_s = ((((uint64_t)h1 << 32) | h0) >> 17 | ((uint64_t)h2 << 47)) & (~0ull >> (64u - 3u * ncode));
+  // ... in symbol order (src/inflate.c:975-983 order[])
+  constexpr uint8_t inv[19] = {3, 17, 15, 13, 11, 9, 7, 5, 4, 6, 8, 10, 12, 14, 16, 18, 0, 1, 2};
+  uint64_t cls = 0;
+  uint64_t cntp = 0;  // 5-bit count of each length 1..7 at bits 5L (length 0 not counted)
 #pragma unroll
-  for (int i = 0; i < 19; i++) cnt[cl[i]]++;
-  uint32_t nxt[8];
-  nxt[0] = 0;
-  nxt[1] = 0;
-  uint32_t code = 0;
+  for (int sy = 0; sy < 19; sy++) {
+    const uint32_t L = (uint32_t)(cls_s >> (3 * inv[sy])) & 7u;
+    cls |= (uint64_t)L << (3 * sy);
+    cntp += (1ull << (5u * L)) & ~31ull;
+  }
+  // complete code-length code (src/inftrees.c:137-140 rejects any other for CODES)
+  uint32_t lim = 0, offs = 0;
+  v.P1 = v.P2 = v.BA = v.BB = v.OA = v.OB = 0;
 #pragma unroll
   for (int L = 1; L < 8; L++) {
-    code = (code + (L > 1 ? cnt[L - 1] : 0)) << (L > 1 ? 1 : 0);
-    nxt[L] = code;
+    const uint32_t c = (uint32_t)(cntp >> (5 * L)) & 31u;
+    if (L < 5) {
+      v.BA |= lim << (8 * (L - 1));
+      v.OA |= offs << (8 * (L - 1));
+    } else {
+      v.BB |= lim << (8 * (L - 5));
+      v.OB |= offs << (8 * (L - 5));
+    }
+    lim += c << (7 - L);
+    offs += c;
+    if (L < 5) v.P1 |= min(lim, 255u) << (8 * (L - 1));
+    else if (L < 7) v.P2 |= min(lim, 255u) << (8 * (L - 5));
   }
-  // a complete code-length code (src/inftrees.c:137-140 rejects any other for
-  // CODES) fills all 128 LUT entries: no clearing needed
-  if ((cnt[1] << 6) + (cnt[2] << 5) + (cnt[3] << 4) + (cnt[4] << 3) + (cnt[5] << 2) + (cnt[6] << 1) + cnt[7] != 128u)
-    return false;
+  if (lim != 128u) return VS_BAD;
+  // the symbols in canonical order: symbol order within each length
+  uint64_t seen = 0;
+  v.SL = v.SH = 0;
 #pragma unroll
-  for (int s = 0; s < 19; s++) {
-    uint32_t L = cl[s];
-    if (L) {
-      uint32_t c = 0;
-#pragma unroll
-      for (int x = 1; x < 8; x++)
-        if ((uint32_t)x == L) c = nxt[x]++;
-      uint32_t rev = __builtin_bitreverse32(c) >> (32 - L);
-      for (uint32_t j = rev; j < 128; j += (1u << L)) lut[j] = (uint8_t)(s | (L << 5));
-    }
+  for (int sy = 0; sy < 19; sy++) {
+    const uint32_t L = (uint32_t)(cls >> (3 * sy)) & 7u;
+    const uint32_t sh8 = 8u * ((L - 1u) & 3u);
+    const uint32_t rank = ((((L < 5u) ? v.OA : v.OB) >> sh8) & 255u) + ((uint32_t)(seen >> (5u * L)) & 31u);
+    seen += 1ull << (5u * L);
+    const uint64_t put = L ? (uint64_t)sy : 0ull;
+    v.SL |= rank < 12u ? put << (5u * rank) : 0ull;
+    v.SH |= rank < 12u ? 0ull : put << (5u * (rank - 12u));
   }
-  const uint32_t total = nlen + ndist;
-  uint32_t have = 0, prev = 0, eob = 0;
-  uint32_t lk = 0, lmax = 0, dk = 0, dmax = 0, dn = 0;
-  while (have < total) {
-    refill();
-    uint32_t e = lut[hold & 127];
-    uint32_t L = e >> 5, sym = e & 31;
-    if (L == 0) return false;
-    hold >>= L;
-    n -= L;
-    uint32_t rep = 1, v = sym;
-    if (sym == 16) {
-      if (have == 0) return false;
-      rep = 3 + (uint32_t)(hold & 3);
-      hold >>= 2;
-      n -= 2;
-      v = prev;
-    } else if (sym == 17) {
-      rep = 3 + (uint32_t)(hold & 7);
-      hold >>= 3;
-      n -= 3;
-      v = 0;
-    } else if (sym == 18) {
-      rep = 11 + (uint32_t)(hold & 127);
-      hold >>= 7;
-      n -= 7;
-      v = 0;
-    }
-    if (pos() > limit) return false;
-    if (have + rep > total) return false;
-    if (v) {
-      // split the run between the literal/length and distance code lengths
-      uint32_t nl = have < nlen ? min(rep, nlen - have) : 0u;
-      uint32_t nd = rep - nl;
-      lk += nl << (15 - v);
-      if (nl) lmax = max(lmax, v);
-      dk += nd << (15 - v);
-      dn += nd;
-      if (nd) dmax = max(dmax, v);
-      if (have <= 256 && 256 < have + rep) eob = v;
-      // partial Kraft sums only grow: an over-subscribed code fails now rather
-      // than after all nlen + ndist lengths (most false candidates end here)
-      if (lk > 32768u || dk > 32768u) return false;
-    }
-    prev = v;
-    have += rep;
+  v.total = v.nlen + ndist;
+  v.p = bit + 17u + 3u * ncode;
+  v.have = v.prev = v.eob = v.lk = v.lmax = v.dk = v.dmax = v.dn = 0;
+  return VS_RUN;
+}
+// one code-length symbol (src/inflate.c:1000-1033); at the last one, the
+// completeness checks (src/inftrees.c:131-140, as zlib's table builds)
+template <bool D64>
+__device__ __forceinline__ uint32_t val_step(VState &v, uint32_t *win) {
+  uint32_t i = (v.p >> 5) - v.wb;
+  if (i + 1u >= VWIN) {
+    vwin_load(v, v.p >> 5, win);
+    i = (v.p >> 5) - v.wb;
   }
-  if (eob == 0) return false;
-  if (lk > 32768u || (lk < 32768u && lmax != 1)) return false;
-  if (dn && (dk > 32768u || (dk < 32768u && dmax != 1))) return false;
-  if (D64 && dn == 0) return false;  // deflate64 rejects an empty distance code (src/inftrees.c:131-132)
-  return true;
+  const uint32_t x = __builtin_amdgcn_alignbit(win[(i + 1u) * WAVE], win[i * WAVE], v.p & 31u);
+  // canonical decode of the next code-length symbol (the VState registers)
+  const uint32_t c7 = __builtin_bitreverse32(x) >> 25;
+  const uint32_t L = 1u + (uint32_t)__builtin_popcount(((0x80808080u | (c7 * 0x01010101u)) - v.P1) & 0x80808080u) +
+                     (uint32_t)__builtin_popcount(((0x8080u | (c7 * 0x0101u)) - v.P2) & 0x8080u);
+  const uint32_t sh8 = 8u * ((L - 1u) & 3u);
+  const uint32_t base = (((L < 5u) ? v.BA : v.BB) >> sh8) & 255u, offs = (((L < 5u) ? v.OA : v.OB) >> sh8) & 255u;
+  const uint32_t idx = offs + ((c7 - base) >> (7u - L));
+  const uint32_t sym = idx < 12u ? (uint32_t)(v.SL >> (5u * idx)) & 31u : (uint32_t)(v.SH >> (5u * (idx - 12u))) & 31u;
+  // repeat codes 16 / 17 / 18: 2 / 3 / 7 extra bits, 3 / 3 / 11 + extra copies
+  const uint32_t xb = sym < 16u ? 0u : (sym == 16u ? 2u : (sym == 17u ? 3u : 7u));
+  const uint32_t rep = sym < 16u ? 1u : (sym == 18u ? 11u : 3u) + __builtin_amdgcn_ubfe(x, L, xb);
+  const uint32_t val = sym < 16u ? sym : (sym == 16u ? v.prev : 0u);
+  v.p += L + xb;
+  if (L == 0u || (sym == 16u && v.have == 0u) || v.p > v.end_byte * 8u || v.have + rep > v.total) return VS_BAD;
+  // the run's lengths split between the literal/length and distance codes;
+  // partial Kraft sums only grow, so an over-subscribed code fails now
+  const uint32_t nl = v.have < v.nlen ? min(rep, v.nlen - v.have) : 0u;
+  const uint32_t nd = rep - nl;
+  const uint32_t sv = 15u - val;
+  v.lk += val ? nl << sv : 0u;
+  v.dk += val ? nd << sv : 0u;
+  v.dn += val ? nd : 0u;
+  v.lmax = (val && nl) ? max(v.lmax, val) : v.lmax;
+  v.dmax = (val && nd) ? max(v.dmax, val) : v.dmax;
+  v.eob = (v.have <= 256u && 256u < v.have + rep) ? val : v.eob;
+  if (v.lk > 32768u || v.dk > 32768u) return VS_BAD;
+  v.prev = val;
+  v.have += rep;
+  if (v.have < v.total) return VS_RUN;
+  if (v.eob == 0) return VS_BAD;
+  if (v.lk > 32768u || (v.lk < 32768u && v.lmax != 1)) return VS_BAD;
+  if (v.dn && (v.dk > 32768u || (v.dk < 32768u && v.dmax != 1))) return VS_BAD;
+  if (D64 && v.dn == 0) return VS_BAD;  // deflate64 rejects an empty distance code (src/inftrees.c:131-132)
+  return VS_OK;
 }
 
 // ---------------------------------------------------------------------------
-// Block finder: one wave per search segment; records the first SEG_SLOTS
-// dynamic-block starts in [s_byte, e_byte).
-//   1. every lane tests 32 bit offsets per step with bit-parallel filters
-//      (BFINAL = 0 -- or 1 in a stream's last segments --, BTYPE = 2,
-//      HLIT <= 29, HDIST <= 29, complete code-length
-//      code) and appends the survivors, in offset order, to an LDS queue;
-//   2. the queue is drained 64 candidates at a time, ONE candidate per lane,
-//      through the full header validation, so the expensive check runs
-//      SIMD-parallel instead of stalling the wave lane by lane.
+// Block finder, two kernels (round 6):
+//   zs_find_kernel     one wave per search segment: every lane tests 32 bit
+//                      offsets per step with bit-parallel filters (BFINAL = 0
+//                      -- or 1 in a stream's last segments --, BTYPE = 2,
+//                      HLIT <= 29, HDIST <= 29), the survivors go through an LDS
+//                      queue (one candidate per lane) to the code-length-code
+//                      completeness check, and what passes that is appended, in
+//                      offset order, to the segment's survivor list in global
+//                      memory (<= FV_LIST - 1 per segment; hints only).
+//   zs_findval_kernel  the survivors of all segments, one per lane, through the
+//                      full header validation (a pool: lanes refilled as they
+//                      finish); zs_findsel_kernel keeps each segment's first
+//                      SEG_SLOTS that pass.
+// Measured (C2, round 5, one kernel): the full validation's long per-lane LDS
+// and global chains ran inside the scan loop at 4 waves per SIMD (its 8 KiB of
+// LUTs), 40% of the wave cycles waiting; split, the scan runs at 3.9 KiB of
+// LDS and the validation has its own occupancy.  A C2 segment holds ~220
+// filter candidates per 2048-bit step, ~0.3-0.9 pass the completeness check,
+// a validation decodes ~40-80 code-length symbols (tools/find_probe.c).
 // ---------------------------------------------------------------------------
-#define FQ 256  // validation queue (ring) per wave; a step's surplus past it is dropped (hints only)
+#ifndef FIND_WG
+#define FIND_WG 4u  // segments (waves) per finder workgroup: one-wave workgroups left CUs at ~12 resident waves
+#endif
+#define FQ_LIST 256u  // u32 per segment in the survivor lists: [0] count, then <= FQ_LIST - 1 bit offsets
 
 __device__ __forceinline__ uint32_t find_scan_excl(uint32_t v, uint32_t *total) {
   uint32_t x = v;
@@ -204,35 +260,29 @@ __device__ __forceinline__ bool cl_complete(const uint32_t *st, uint32_t base, u
                          k9[(clb >> 36) & 511u] + k9[(clb >> 45) & 511u] + k9[(clb >> 54) & 511u];
   return kraft == 128u;
 }
+
+// position of this lane among the set lanes of m below it
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
 template <bool D64>
-__global__ void __launch_bounds__(64) zs_find_kernel(const ZsJobDev *__restrict__ jobs, const ZsHeadDev *__restrict__ heads,
-                                                      ZsSegDev *__restrict__ segs) {
-  __shared__ uint32_t s_st[WAVE + 8];  // this step's input words (2048 bits + overlap)
+__global__ void __launch_bounds__(FIND_WG * WAVE) zs_find_kernel(const ZsJobDev *__restrict__ jobs, const ZsHeadDev *__restrict__ heads,
+                                                                const ZsSegDev *__restrict__ segs, uint32_t *__restrict__ vlist,
+                                                                uint32_t nseg) {
+  __shared__ uint32_t s_st_all[FIND_WG][WAVE + 8];  // this step's input words (2048 bits + overlap)
   // this step's candidates passing the bit-parallel filters: ~11% of random
   // bits; past FQC (adversarial bit patterns) the rest of the step is dropped
   // -- starts are hints, the chain check keeps results exact
   constexpr uint32_t FQC = WAVE * 12;
-  // full validations run FV lanes at a time, their LUTs in the queue's space.
-  // Measured on C2 (find): FV 16 6.5 ms, 32 5.0 ms (7 waves/SIMD), 64 4.7 ms
-  // (8 KiB of LUTs, 4 waves/SIMD): each batch's cost is set by its slowest
-  // lane (the per-symbol LUT fill loops, the code-length walk), so half as many
-  // batches beat the lost occupancy
-#ifndef ZS_FV
-  constexpr uint32_t FV = 64;
-#else
-  constexpr uint32_t FV = ZS_FV;
-#endif
-  // the full validation's per-lane code-length LUTs reuse this space: they are
-  // built after the step's candidates have left it
-  __shared__ union {
-    uint32_t q[FQC];
-    uint8_t lut[FV][128];
-  } s_u;
-  uint32_t *const s_q = s_u.q;
-  __shared__ uint32_t s_v[FQ];        // ... and the code-length-code completeness check
-  __shared__ uint8_t s_k9[512];       // Kraft weights of 3 code-length-code lengths (cl_complete), <= 192
-  const uint32_t lane = threadIdx.x;
-  for (uint32_t x = lane; x < 512; x += WAVE) {
+  __shared__ uint32_t s_q_all[FIND_WG][FQC];
+  __shared__ uint8_t s_k9[512];  // Kraft weights of 3 code-length-code lengths (cl_complete), <= 192
+  const uint32_t lane = threadIdx.x & (WAVE - 1u), wv = threadIdx.x / WAVE;
+  uint32_t *const s_st = s_st_all[wv];
+  uint32_t *const s_q = s_q_all[wv];
+  __shared__ uint32_t s_l_all[FIND_WG][FQ_LIST - 1u];  // the segment's survivors (stored to vlist at the end)
+  uint32_t *const s_l = s_l_all[wv];
+  for (uint32_t x = threadIdx.x; x < 512; x += FIND_WG * WAVE) {
     uint32_t k = 0;
     for (int f = 0; f < 3; f++) {
       const uint32_t L = (x >> (3 * f)) & 7u;
@@ -240,12 +290,14 @@ __global__ void __launch_bounds__(64) zs_find_kernel(const ZsJobDev *__restrict_
     }
     s_k9[x] = (uint8_t)k;
   }
-  __builtin_amdgcn_wave_barrier();
-  const uint32_t sg = blockIdx.x;
+  __syncthreads();
+  const uint32_t sg = blockIdx.x * FIND_WG + wv;
+  if (sg >= nseg) return;
   const ZsSegDev seg = segs[sg];
   const ZsJobDev jb = jobs[seg.job];
   const ZsHeadDev hd = heads[seg.job];
-  uint32_t nfound = 0;
+  uint32_t *const out = vlist + (size_t)sg * FQ_LIST;
+  uint32_t nv = 0;  // survivors listed
   if (hd.code == ZD_END) {
     const uintptr_t ip = reinterpret_cast<uintptr_t>(jb.in);
     const uint32_t mis = (uint32_t)(ip & 3u);
@@ -254,26 +306,43 @@ __global__ void __launch_bounds__(64) zs_find_kernel(const ZsJobDev *__restrict_
     // strictly after the stream's first block (that start is unit 0)
     const uint32_t lo = max((mis + seg.s_byte) * 8u, (mis + (uint32_t)hd.start_byte) * 8u + jb.sbit + 1u);
     const uint32_t hi = (mis + seg.e_byte) * 8u;
-    uint32_t vh = 0, vt = 0;
     // input words of a step: lane word (base/32 + lane), the next one, and 8
-    // overlap words (lanes < 8); the next step's are loaded one step ahead
+    // overlap words (lanes < 8), loaded two steps ahead.  The loads are
+    // unconditional (index clamped to the last word, bytes past the input
+    // zeroed when used) and no global store sits in the loop: a conditional
+    // load, or a store after the prefetch, made the compiler wait vmcnt(0) at
+    // the loop top -- one full memory latency per step (C2 scan 2.2 ms)
+    const uint32_t lastw = (end_byte - 1u) >> 2;
+    // (global, not flat: flat loads count in lgkmcnt, so every LDS wait would wait for them)
+    typedef __attribute__((address_space(1))) const uint32_t gcu32f;
+    const gcu32f *gw = (const gcu32f *)w;
     auto fetch = [&](uint32_t bs, uint32_t &a0, uint32_t &a1, uint32_t &a2) {
       const uint32_t wi = (bs >> 5) + lane;
-      a0 = in_word(w, wi, end_byte);
-      a1 = in_word(w, wi + 1, end_byte);
-      a2 = lane < 8 ? in_word(w, (bs >> 5) + WAVE + lane, end_byte) : 0u;
+      a0 = gw[min(wi, lastw)];
+      a1 = gw[min(wi + 1u, lastw)];
+      a2 = gw[min((bs >> 5) + WAVE + (lane & 7u), lastw)];
     };
-    uint32_t nx0, nx1, nx2;
+    auto mask = [&](uint32_t v, uint32_t wi) {
+      const uint32_t b = wi * 4u;
+      const uint32_t keep = b >= end_byte ? 0u : end_byte - b;
+      return keep >= 4u ? v : __builtin_amdgcn_ubfe(v, 0, 8u * keep);
+    };
+    uint32_t nx0, nx1, nx2, ny0, ny1, ny2;
     fetch(lo & ~31u, nx0, nx1, nx2);
-    for (uint32_t base = lo & ~31u;; base += WAVE * 32u) {
-      const bool more = base < hi;
+    fetch((lo & ~31u) + WAVE * 32u, ny0, ny1, ny2);
+    // one step over the 2048 bits at base from buffer (a0, a1, a2), which
+    // then takes the words of the step after next; the loop alternates the two
+    // buffers (a register move between them made the loop wait for the
+    // next step's loads)
+    auto step = [&](uint32_t base, uint32_t &a0, uint32_t &a1, uint32_t &a2) {
       const uint32_t b0 = base + lane * 32u;
-      const uint32_t x0 = nx0, x1 = nx1, x2 = nx2;
-      if (more) fetch(base + WAVE * 32u, nx0, nx1, nx2);
+      const uint32_t wl = b0 >> 5;
+      const uint32_t x0 = mask(a0, wl), x1 = mask(a1, wl + 1u), x2 = mask(a2, (base >> 5) + WAVE + (lane & 7u));
+      fetch(base + 2u * WAVE * 32u, a0, a1, a2);
       s_st[lane] = x0;
       if (lane < 8) s_st[WAVE + lane] = x2;
       uint32_t cand = 0;
-      if (more && b0 < hi) {
+      if (b0 < hi) {
         const uint64_t x = (uint64_t)x0 | ((uint64_t)x1 << 32);
         // bit-parallel over the lane's 32 offsets p: BTYPE = 2 (bit p+1 = 0,
         // bit p+2 = 1), BFINAL (bit p) = 0 unless this is one of the stream's
@@ -299,46 +368,184 @@ __global__ void __launch_bounds__(64) zs_find_kernel(const ZsJobDev *__restrict_
       }
       tot = min(tot, FQC);
       __builtin_amdgcn_wave_barrier();
-      // completeness check on this step's candidates, one per lane; survivors
-      // keep their order in the validation queue
-      for (uint32_t q0 = 0; q0 < tot; q0 += WAVE) {
-        const uint32_t take = min(tot - q0, (uint32_t)WAVE);
-        uint32_t cb = 0;
-        bool ok = false;
-        if (lane < take) {
-          cb = s_q[q0 + lane];
-          ok = cl_complete(s_st, base, cb, s_k9);
+      // completeness check, one candidate per lane, four rounds of the queue
+      // at once (their LDS reads in flight together, not four serial chains);
+      // survivors keep their order in the list
+      for (uint32_t q0 = 0; q0 < tot; q0 += 4u * WAVE) {
+        uint32_t cb[4];
+        bool ok[4];
+#pragma unroll
+        for (uint32_t j = 0; j < 4; j++) {
+          const uint32_t q = q0 + j * WAVE + lane;
+          const uint32_t v = s_q[min(q, FQC - 1u)];
+          cb[j] = q < tot ? v : base;
         }
-        uint32_t vtot;
-        const uint32_t vat = find_scan_excl(ok ? 1u : 0u, &vtot);
-        if (ok && vt + vat - vh < FQ) s_v[(vt + vat) & (FQ - 1)] = cb;
-        vt = min(vt + vtot, vh + FQ);
+#pragma unroll
+        for (uint32_t j = 0; j < 4; j++) ok[j] = cl_complete(s_st, base, cb[j], s_k9) && q0 + j * WAVE + lane < tot;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; j++) {
+          const uint64_t m = __ballot(ok[j]);
+          const uint32_t pos = nv + lanes_below(m);
+          if (ok[j] && pos < FQ_LIST - 1u) s_l[pos] = cb[j];
+          nv = min(nv + (uint32_t)__builtin_popcountll(m), FQ_LIST - 1u);
+        }
       }
       __builtin_amdgcn_wave_barrier();
-      // full header validation, one candidate per lane
-      while (vt - vh >= FV || (!more && vt != vh)) {
-        const uint32_t take = min(vt - vh, FV);
-        uint32_t cb = 0;
-        bool ok = false;
-        if (lane < take) {
-          cb = s_v[(vh + lane) & (FQ - 1)];
-          ok = validate_header<D64>(w, end_byte, cb, s_u.lut[lane]);
-        }
-        uint64_t m = __ballot(ok);
-        while (m && nfound < SEG_SLOTS) {
-          const uint32_t l = (uint32_t)__builtin_ctzll(m);
-          m &= m - 1;
-          const uint32_t f = __builtin_amdgcn_readlane(cb, l);
-          if (lane == 0) segs[sg].cand[nfound] = f;
-          nfound++;
-        }
-        vh += take;
-        if (nfound == SEG_SLOTS) break;
-      }
-      if (!more || nfound == SEG_SLOTS) break;
+    };
+    for (uint32_t base = lo & ~31u; base < hi;) {
+      step(base, nx0, nx1, nx2);
+      base += WAVE * 32u;
+      if (base >= hi) break;
+      step(base, ny0, ny1, ny2);
+      base += WAVE * 32u;
     }
   }
-  if (lane == 0) segs[sg].ncand = nfound;
+  __builtin_amdgcn_wave_barrier();
+  for (uint32_t i = lane; i < nv; i += WAVE) out[1u + i] = s_l[i];
+  if (lane == 0) out[0] = nv;
+  if (lane < 8u) vlist[(size_t)nseg * FQ_LIST + sg * 8u + lane] = 0u;  // zs_findval_kernel's accepted bitmap
+  if (sg == 0 && lane == 0) vlist[(size_t)nseg * (FQ_LIST + 8u)] = 0u;  // its segment counter
+}
+
+// Full header validation of every survivor, one per lane, from ONE pool:
+// each wave takes whole segments' lists from a global counter into an LDS
+// queue, and a lane whose candidate is decided takes the next one; lanes are
+// refilled together once FV_REFILL of them are idle (a setup costs the wave
+// the same whatever number of lanes run it).  Measured (profiling build, C2,
+// round 6): with a wave per segment and 64 candidates per batch, a batch
+// lasted as long as its longest lane (~170 code-length symbols) while the
+// lanes averaged ~40 -- 22% of lane-steps did work.  Accepted candidates set
+// their bit in the segment's bitmap; zs_findsel_kernel keeps the first
+// SEG_SLOTS of each segment (in offset order, as one wave per segment did).
+#define FV_QN 256u     // queue entries per wave (a segment lists <= FQ_LIST - 1)
+#ifndef FV_REFILL
+#define FV_REFILL 24u  // idle lanes that trigger a refill
+#endif
+#define FV_WAVES_PER_CU 16u
+template <bool D64>
+__global__ void __launch_bounds__(WAVE) zs_findval_kernel(const ZsJobDev *__restrict__ jobs, const ZsSegDev *__restrict__ segs,
+                                                         uint32_t *__restrict__ vlist, uint32_t nseg) {
+  __shared__ uint32_t s_win[VWIN][WAVE];  // per-lane input windows
+  __shared__ uint32_t s_qi[FV_QN], s_qb[FV_QN], s_qj[FV_QN];  // queue: segment << 8 | index, bit, job
+  const uint32_t lane = threadIdx.x;
+  uint32_t *const ctr = vlist + (size_t)nseg * (FQ_LIST + 8u);
+  uint32_t *const bmp = vlist + (size_t)nseg * FQ_LIST;
+  uint32_t *win = &s_win[0][lane];
+  uint32_t qh = 0, qt = 0;  // queue head / tail (uniform, monotonic)
+  bool more = true, act = false;
+  uint32_t cur = 0;  // the lane's candidate: segment << 8 | index
+  VState v;
+  v.w = nullptr;
+  v.end_byte = v.wb = v.p = v.have = v.prev = v.eob = v.lk = v.lmax = v.dk = v.dmax = v.dn = v.nlen = v.total = 0;
+  v.P1 = v.P2 = v.BA = v.BB = v.OA = v.OB = 0;
+  v.SL = v.SH = 0;
+#if KP_ON
+  const uint64_t kt0 = KP_NOW();
+  uint64_t kp_st = 0;
+  uint32_t kp_rounds = 0, kp_wsteps = 0, kp_lsteps = 0;
+#endif
+  for (;;) {
+    // whole segments into the queue while one fits
+    while (more && qt - qh + (FQ_LIST - 1u) <= FV_QN) {
+      uint32_t sg = 0;
+      if (lane == 0) sg = atomicAdd(ctr, 1u);
+      sg = __builtin_amdgcn_readfirstlane(sg);
+      if (sg >= nseg) {
+        more = false;
+        break;
+      }
+      const uint32_t *lst = vlist + (size_t)sg * FQ_LIST;
+      const uint32_t n = min(lst[0], FQ_LIST - 1u), job = segs[sg].job;
+      for (uint32_t i = lane; i < n; i += WAVE) {
+        const uint32_t k = (qt + i) & (FV_QN - 1u);
+        s_qi[k] = (sg << 8) | i;
+        s_qb[k] = lst[1u + i];
+        s_qj[k] = job;
+      }
+      qt += n;
+    }
+    __builtin_amdgcn_wave_barrier();
+    // idle lanes take the next candidates, in lane order
+    {
+      const uint64_t m = __ballot(!act);
+      const uint32_t k = lanes_below(m), avail = qt - qh;
+      if (!act && k < avail) {
+        const uint32_t e = (qh + k) & (FV_QN - 1u);
+        cur = s_qi[e];
+        const uint32_t bit = s_qb[e];
+        const ZsJobDev jb = jobs[s_qj[e]];
+        const uintptr_t ip = reinterpret_cast<uintptr_t>(jb.in);
+        const uint32_t mis = (uint32_t)(ip & 3u);
+        v.w = reinterpret_cast<const uint32_t *>(ip - mis);
+        v.end_byte = mis + (uint32_t)jb.in_len;
+        act = val_setup<D64>(v, bit, win) == VS_RUN;
+      }
+      qh += min((uint32_t)__builtin_popcountll(m), avail);
+#if KP_ON
+      kp_rounds++;
+#endif
+    }
+    const bool drain = !more && qh == qt;
+    if (__ballot(act) == 0) {
+      if (drain) break;
+      continue;
+    }
+#if KP_ON
+    const uint64_t ks0 = KP_NOW();
+#endif
+    // steps until enough lanes are idle (or, with nothing left to take, all)
+    const uint32_t keep = drain ? 0u : WAVE - FV_REFILL;
+    do {
+#if KP_ON
+      kp_wsteps++;
+      kp_lsteps += act ? 1u : 0u;
+#endif
+      if (act) {
+        const uint32_t r = val_step<D64>(v, win);
+        if (r != VS_RUN) {
+          act = false;
+          if (r == VS_OK) atomicOr(&bmp[(cur >> 8) * 8u + ((cur & 255u) >> 5)], 1u << (cur & 31u));
+        }
+      }
+    } while ((uint32_t)__builtin_popcountll(__ballot(act)) > keep);
+#if KP_ON
+    kp_st += KP_NOW() - ks0;
+#endif
+  }
+#if KP_ON
+  {
+    uint32_t ls = kp_lsteps;
+    for (uint32_t o = 1; o < WAVE; o <<= 1) ls += (uint32_t)__shfl_xor((int)ls, (int)o);
+    if (lane == 0) {
+      KPC_ADD(58, 1);
+      KPC_ADD(59, kp_rounds);
+      KPC_ADD(60, kp_st);
+      KPC_ADD(61, kp_wsteps);
+      KPC_ADD(62, ls);
+      KPC_ADD(63, KP_NOW() - kt0);
+    }
+  }
+#endif
+}
+
+// The first SEG_SLOTS validated starts of each segment (lowest bitmap bits:
+// the list is in offset order), one thread per segment.
+__global__ void __launch_bounds__(256) zs_findsel_kernel(ZsSegDev *__restrict__ segs, const uint32_t *__restrict__ vlist,
+                                                         uint32_t nseg) {
+  const uint32_t sg = blockIdx.x * 256u + threadIdx.x;
+  if (sg >= nseg) return;
+  const uint32_t *lst = vlist + (size_t)sg * FQ_LIST;
+  const uint32_t *bm = vlist + (size_t)nseg * FQ_LIST + sg * 8u;
+  uint32_t nf = 0;
+  for (uint32_t k = 0; k < 8u && nf < SEG_SLOTS; k++) {
+    uint32_t b = bm[k];
+    while (b && nf < SEG_SLOTS) {
+      const uint32_t i = 32u * k + (uint32_t)__builtin_ctz(b);
+      b &= b - 1u;
+      segs[sg].cand[nf++] = lst[1u + i];
+    }
+  }
+  segs[sg].ncand = nf;
 }
 
 // ---------------------------------------------------------------------------
@@ -1432,10 +1639,25 @@ extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_hea
   // ev (profiling, optional): [0] before find, [1] after find + plan, [2] after
   // parse + chain, [3] after expand, [4] after link, [5] after emit
   if (ev) (void)hipEventRecord(ev[0], st);
-  if (d64)
-    hipLaunchKernelGGL(zs_find_kernel<true>, dim3(nseg), dim3(64), 0, st, d_jobs, d_heads, d_segs);
-  else
-    hipLaunchKernelGGL(zs_find_kernel<false>, dim3(nseg), dim3(64), 0, st, d_jobs, d_heads, d_segs);
+  // the finder's survivor lists (FQ_LIST words per segment) borrow the token
+  // buffer: nothing reads or writes tokens before the parse (a segment is
+  // 32 KiB of input, the token space >= 8 bytes per input byte), and a later
+  // group's finder runs after this group's expand on the same stream
+  const dim3 fgrid((nseg + FIND_WG - 1u) / FIND_WG), fblk(FIND_WG * WAVE);
+  int ncu = 256;
+  {
+    int dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  }
+  const dim3 vgrid(std::min<uint32_t>(nseg, (uint32_t)std::max(ncu, 1) * FV_WAVES_PER_CU));
+  if (d64) {
+    hipLaunchKernelGGL(zs_find_kernel<true>, fgrid, fblk, 0, st, d_jobs, d_heads, d_segs, d_tokens, nseg);
+    hipLaunchKernelGGL(zs_findval_kernel<true>, vgrid, dim3(WAVE), 0, st, d_jobs, d_segs, d_tokens, nseg);
+  } else {
+    hipLaunchKernelGGL(zs_find_kernel<false>, fgrid, fblk, 0, st, d_jobs, d_heads, d_segs, d_tokens, nseg);
+    hipLaunchKernelGGL(zs_findval_kernel<false>, vgrid, dim3(WAVE), 0, st, d_jobs, d_segs, d_tokens, nseg);
+  }
+  hipLaunchKernelGGL(zs_findsel_kernel, dim3((nseg + 255u) / 256u), dim3(256), 0, st, d_segs, d_tokens, nseg);
   hipLaunchKernelGGL(zs_find_fixed_kernel, dim3(nseg), dim3(64), 0, st, d_jobs, d_heads, d_segs, nseg);
   hipLaunchKernelGGL(zs_plan_kernel, dim3(ncjobs), dim3(PLAN_T), 0, st, d_jobs, d_heads, d_segs, d_cjobs, d_units, pool);
   if (ev) (void)hipEventRecord(ev[1], st);
