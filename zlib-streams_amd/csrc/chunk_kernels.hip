@@ -249,15 +249,16 @@ __device__ __forceinline__ uint32_t find_scan_excl(uint32_t v, uint32_t *total) 
 // lengths of x, 0 for L = 0): 7 independent LDS reads instead of 19 serial
 // extract/shift/select/add steps.
 __device__ __forceinline__ bool cl_complete(const uint32_t *st, uint32_t base, uint32_t p, const uint8_t *k9) {
-  const uint32_t r = p - base, wi = r >> 5, sh = r & 31u;
-  const uint64_t a = (uint64_t)st[wi] | ((uint64_t)st[wi + 1] << 32);
-  const uint64_t b = (uint64_t)st[wi + 2] | ((uint64_t)st[wi + 3] << 32);
-  const uint64_t h = sh ? ((a >> sh) | (b << (64 - sh))) : a;
-  const uint64_t h2 = sh ? ((b >> sh) | ((uint64_t)st[wi + 4] << (64 - sh))) : b;
-  const uint32_t ncode = (uint32_t)((h >> 13) & 15) + 4;
-  const uint64_t clb = ((h >> 17) | (h2 << 47)) & (~0ull >> (64 - 3 * ncode));
-  const uint32_t kraft = k9[clb & 511u] + k9[(clb >> 9) & 511u] + k9[(clb >> 18) & 511u] + k9[(clb >> 27) & 511u] +
-                         k9[(clb >> 36) & 511u] + k9[(clb >> 45) & 511u] + k9[(clb >> 54) & 511u];
+  // the 64 bits from p + 13 (HCLEN, then the 19 lengths) from three stage words
+  const uint32_t r = p + 13u - base, wi = r >> 5;
+  const uint32_t a = st[wi], b = st[wi + 1], c = st[wi + 2];
+  const uint32_t lo = __builtin_amdgcn_alignbit(b, a, r), hi = __builtin_amdgcn_alignbit(c, b, r);
+  const uint32_t ncode = (lo & 15u) + 4u;
+  const uint64_t clb = ((((uint64_t)hi << 32) | lo) >> 4) & (~0ull >> (64u - 3u * ncode));
+  const uint32_t l = (uint32_t)clb, h = (uint32_t)(clb >> 32);
+  const uint32_t kraft = k9[l & 511u] + k9[__builtin_amdgcn_ubfe(l, 9, 9)] + k9[__builtin_amdgcn_ubfe(l, 18, 9)] +
+                         k9[__builtin_amdgcn_alignbit(h, l, 27) & 511u] + k9[__builtin_amdgcn_ubfe(h, 4, 9)] +
+                         k9[__builtin_amdgcn_ubfe(h, 13, 9)] + k9[__builtin_amdgcn_ubfe(h, 22, 9)];
   return kraft == 128u;
 }
 
