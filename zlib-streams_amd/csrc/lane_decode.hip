@@ -2274,14 +2274,20 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
     // stands on a symbol boundary here; a pending symbol is not yet counted)
     if (__builtin_amdgcn_ballot_w64(live && ntok >= ncut)) {
       if (live && ntok >= ncut) {  // the next sub-unit starts here
-        cp[ncp] = make_uint2(p, ntok);
-        ncp++;
-        ncut += K;
-        if (ncp == WK_CP - 1u) {  // out of slots: keep every second checkpoint, twice the stride
+        // out of slots (a 65th sub-unit): keep every second checkpoint, twice
+        // the stride.  Round 6: this halved on storing the 63rd checkpoint,
+        // i.e. every unit past 63 x 256 tokens -- zlib's 16 383-symbol blocks,
+        // nearly every C2 unit -- ran as 32 sub-units of 512 tokens
+        if (ncp == WK_CP - 1u) {
           walk_halve(cp);
           ncp = (WK_CP - 1u) / 2u;
           K *= 2u;
           ncut = (ncp + 1u) * K;
+        }
+        if (ntok >= ncut) {
+          cp[ncp] = make_uint2(p, ntok);
+          ncp++;
+          ncut += K;
         }
       }
     }
