@@ -98,6 +98,12 @@ def main():
         "walk_refill_cycles_per_step": d.get("p_cyc_busy", 0) / max(d.get("w_wave_steps", 0), 1),
         "walk_exc_per_step": d.get("w_exc", 0) / max(d.get("w_wave_steps", 0), 1),
         "split_cycles_per_wave_step": d.get("s_lit", 0) / max(d.get("s_refill2", 0), 1),
+        # split kernel phases (shares of its wave cycles): unit prologue, sub-unit decode (of which group
+        # refill + token stores), the rest (epilogue, unit claims)
+        "split_frac_prologue": d.get("p_cyc_flush", 0) / max(d.get("s_lit", 0), 1),
+        "split_frac_decode": d.get("p_groups", 0) / max(d.get("s_lit", 0), 1),
+        "split_frac_group": d.get("s_dist", 0) / max(d.get("s_lit", 0), 1),
+        "split_units": d.get("s_refill1", 0),
         # finder validation pool: lane utilisation, cycles per wave-step, share of the wave's time in steps
         "fv_lane_util": d.get("fv_lane_steps", 0) / max(64 * d.get("fv_wave_steps", 0), 1),
         "fv_cycles_per_wave_step": d.get("fv_cyc_steps", 0) / max(d.get("fv_wave_steps", 0), 1),

@@ -2737,7 +2737,7 @@ __global__ void __launch_bounds__(64) zs_split_kernel(const ZsJobDev *__restrict
   typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
 #if KP_ON
   const uint64_t kp_t0 = KP_NOW();
-  uint64_t kp_grp = 0;
+  uint64_t kp_grp = 0, kp_pro = 0, kp_sub = 0;
   uint32_t kp_units = 0, kp_ws = 0;
 #endif
   for (;;) {
@@ -2751,6 +2751,7 @@ __global__ void __launch_bounds__(64) zs_split_kernel(const ZsJobDev *__restrict
     const ZsWalkDev wk = walks[c];
 #if KP_ON
     kp_units++;
+    const uint64_t ku0 = KP_NOW();
 #endif
     const ZsChunkDev ch = chunks[c];
     const ZsJobDev jb = jobs[ch.job];
@@ -2825,6 +2826,10 @@ __global__ void __launch_bounds__(64) zs_split_kernel(const ZsJobDev *__restrict
       dtb = make_uint4(uni(y.x), uni(y.y), uni(y.z), uni(y.w));
     }
     const uint32_t whave = ch.ord == 0 ? ((jb.flags & ZS_JF_CONT) ? min(jb.hist, HMAX) : 0u) : HMAX;
+#if KP_ON
+    const uint64_t ku1 = KP_NOW();
+    kp_pro += ku1 - ku0;
+#endif
     if (whave < HMAX)  // only a stream's first unit can reach before its window
       split_sub3<D64, true>(L, t, s, t1, filled, pre, rra, dta, dtb, tokens, pool, act
 #if KP_ON
@@ -2837,6 +2842,10 @@ __global__ void __launch_bounds__(64) zs_split_kernel(const ZsJobDev *__restrict
                              , kp_grp, kp_ws
 #endif
       );
+#if KP_ON
+    const uint64_t ku2 = KP_NOW();
+    kp_sub += ku2 - ku1;
+#endif
     const bool full = act && t.pos > s.capx;
     uint32_t bad = (t.bad & 0x20u) ? 1u : 0u;
     if (act && !full && (t.p != b1 || t.ntok != t1)) bad = 1;
@@ -2916,6 +2925,8 @@ __global__ void __launch_bounds__(64) zs_split_kernel(const ZsJobDev *__restrict
   KP_ADD(41, KP_NOW() - kp_t0);
   KP_ADD(42, kp_wave_sum(kp_ws));
   KP_ADD(43, kp_grp);
+  KP_ADD(4, kp_pro);  // (lane-parse slots, unused by the split parse) unit prologue: tables, checkpoints, ring
+  KP_ADD(5, kp_sub);  // the sub-unit decode (steps + group refills / stores)
 #endif
 }
 
