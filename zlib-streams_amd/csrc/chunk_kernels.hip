@@ -891,11 +891,26 @@ struct ZsLinkInfo {
   uint32_t unit;  // unit index (ord 0 <=> first of the job)
 };
 
+// Per stream: each unit's successor (the first later unit starting at its end
+// bit), then the chain from the stream's first unit: exact output offsets and
+// entry ranges of its members.  Round 6: with every unit field staged in LDS,
+// the chain is a parallel prefix over predecessor links (pointer jumping,
+// <= 12 rounds: each unit learns its chain's head, rank and offsets; members
+// are the units headed by the first unit), unless a unit has two
+// predecessors (a false start that resynchronised onto the true symbol grid
+// ends where a true unit ends) or the stream has more than LINK_MAXU units:
+// then thread 0 walks the chain as before.  The walk took 0.38-0.46 ms per C2
+// batch (~720 dependent steps per stream).
 __global__ void __launch_bounds__(LINK_THREADS) zs_chain_kernel(const ZsJobDev *__restrict__ jobs, const ZsHeadDev *__restrict__ heads,
                                                                 ZsChunkDev *__restrict__ chunks, ZsCJobDev *__restrict__ cjobs,
                                                                 ZsLinkInfo *__restrict__ info, ZsDecDev *__restrict__ decs,
                                                                 uint32_t *__restrict__ fallback) {
   __shared__ uint16_t s_succ[LINK_MAXU];  // successor - unit (0: none / end)
+  __shared__ uint8_t s_code[LINK_MAXU];
+  __shared__ uint32_t s_nout[LINK_MAXU], s_endb[LINK_MAXU], s_sb[LINK_MAXU];
+  __shared__ uint32_t s_pj[LINK_MAXU];  // jump pointer (predecessor 2^r back; NONE) | head << 16
+  __shared__ uint32_t s_rk[LINK_MAXU], s_sa[LINK_MAXU], s_st[LINK_MAXU];  // exclusive sums: members, entries (8-aligned), bytes
+  __shared__ uint32_t s_merge, s_r1, s_r2, s_flag;
   const uint32_t t = threadIdx.x;
   const ZsCJobDev cj = cjobs[blockIdx.x];
   const ZsJobDev jb = jobs[cj.job];
@@ -914,14 +929,27 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_chain_kernel(const ZsJobDev *
   }
   const uint32_t u0 = cj.unit0, nu = cj.nunits, last = u0 + nu;
   const bool small = nu <= LINK_MAXU;
-  // A: successors
+  const bool part = (jb.flags & ZS_JF_PART) != 0;
+  constexpr uint32_t PNONE = 0xffffu;
+  if (small) {
+    for (uint32_t i = t; i < nu; i += LINK_THREADS) {
+      s_sb[i] = chunks[u0 + i].start_bit;
+      s_pj[i] = PNONE;
+    }
+    if (t == 0) {
+      s_merge = 0;
+      s_flag = 0;
+    }
+    __syncthreads();
+  }
+  // A: successors (and, staged, every field the chain needs)
   for (uint32_t i = u0 + t; i < last; i += LINK_THREADS) {
     const ZsChunkDev ch = chunks[i];
     const int code = ch.code & 0xff;
     uint32_t k = ZS_NONE;
     if (code == ZD_STOP) {
       for (uint32_t o = i + 1; o < last; o++) {
-        const uint32_t sb = chunks[o].start_bit;
+        const uint32_t sb = small ? s_sb[o - u0] : chunks[o].start_bit;
         if (sb == ch.end_bit) {
           k = o;
           break;
@@ -930,9 +958,125 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_chain_kernel(const ZsJobDev *
       }
     }
     chunks[i].chain_next = k;
-    if (small) s_succ[i - u0] = (k == ZS_NONE || k - i > 0xffffu) ? (uint16_t)0 : (uint16_t)(k - i);
+    if (small) {
+      s_succ[i - u0] = (k == ZS_NONE || k - i > 0xffffu) ? (uint16_t)0 : (uint16_t)(k - i);
+      s_code[i - u0] = (uint8_t)code;
+      s_nout[i - u0] = ch.n_out;
+      s_endb[i - u0] = ch.end_bit;
+      if (k != ZS_NONE && atomicCAS(&s_pj[k - u0], PNONE, i - u0) != PNONE) s_merge = 1;
+    }
   }
   __syncthreads();
+  if (small && !s_merge && cj.scratch_n < 0xf0000000ull) {
+    // initial sums: the predecessor's own values; head = self until resolved
+    for (uint32_t i = t; i < nu; i += LINK_THREADS) {
+      const uint32_t p = s_pj[i];
+      s_rk[i] = p != PNONE ? 1u : 0u;
+      s_sa[i] = p != PNONE ? (s_nout[p] + 7u) & ~7u : 0u;
+      s_st[i] = p != PNONE ? s_nout[p] : 0u;
+      s_pj[i] = p | ((p != PNONE ? p : i) << 16);  // jump | head (the farthest node reached)
+    }
+    __syncthreads();
+    // pointer jumping: read a round's values, then write them (<= 4 units per thread)
+    for (uint32_t r = 0; r < 12; r++) {
+      uint32_t nj[LINK_MAXU / LINK_THREADS], ar[LINK_MAXU / LINK_THREADS], aa[LINK_MAXU / LINK_THREADS],
+          at[LINK_MAXU / LINK_THREADS];
+      bool any = false;
+#pragma unroll
+      for (uint32_t q = 0; q < LINK_MAXU / LINK_THREADS; q++) {
+        const uint32_t i = t + q * LINK_THREADS;
+        nj[q] = 0xffffffffu;
+        if (i < nu) {
+          const uint32_t pj = s_pj[i], j = pj & 0xffffu;
+          if (j != PNONE) {
+            nj[q] = s_pj[j];
+            ar[q] = s_rk[j];
+            aa[q] = s_sa[j];
+            at[q] = s_st[j];
+            any = true;
+          }
+        }
+      }
+      if (!__syncthreads_or(any)) break;
+#pragma unroll
+      for (uint32_t q = 0; q < LINK_MAXU / LINK_THREADS; q++) {
+        const uint32_t i = t + q * LINK_THREADS;
+        if (nj[q] != 0xffffffffu) {
+          s_rk[i] += ar[q];
+          s_sa[i] += aa[q];
+          s_st[i] += at[q];
+          s_pj[i] = nj[q];  // its jump and its head (the head of what j reached)
+        }
+      }
+      __syncthreads();
+    }
+    // the walk's stop, in rank order: r1 = first member rejected before it is
+    // taken (not a block end, or past the entry / piece budget), r2 = first
+    // member after which the chain ends (end of stream, or no successor)
+    if (t == 0) {
+      s_r1 = 0xffffffffu;
+      s_r2 = 0xffffffffu;
+    }
+    __syncthreads();
+    for (uint32_t i = t; i < nu; i += LINK_THREADS) {
+      if ((s_pj[i] >> 16) != 0u) continue;  // not headed by the stream's first unit
+      const uint32_t code = s_code[i], n = s_nout[i], rk = s_rk[i];
+      const uint64_t spos = s_sa[i];
+      if ((code != ZD_STOP && code != ZD_END) || spos + n > cj.scratch_n || (part && (uint64_t)s_st[i] + n > ZS_PART_OUT))
+        atomicMin(&s_r1, rk);
+      if (code == ZD_END || s_succ[i] == 0) atomicMin(&s_r2, rk);
+    }
+    __syncthreads();
+    const uint32_t r1 = s_r1, r2 = s_r2;
+    const uint32_t len = r1 <= r2 ? r1 : r2 + 1u;  // members taken (ranks 0 .. len - 1)
+    for (uint32_t i = t; i < nu; i += LINK_THREADS) {
+      if ((s_pj[i] >> 16) != 0u || s_rk[i] >= len) continue;
+      ZsLinkInfo li;
+      li.scratch = cj.scratch0 + (uint64_t)cj.esz * s_sa[i];
+      li.n_out = s_nout[i];
+      li.unit = u0 + i;
+      info[u0 + s_rk[i]] = li;
+      chunks[u0 + i].out_off = s_st[i];
+      chunks[u0 + i].scratch = li.scratch;
+      if (s_rk[i] + 1u == len) s_flag = i;  // the last member taken
+    }
+    __syncthreads();
+    if (t == 0) {
+      uint32_t ok = 1, cut = 0, end_bit = 0;
+      uint64_t total = 0;
+      if (len) {
+        const uint32_t m = s_flag;
+        total = (uint64_t)s_st[m] + s_nout[m];
+        end_bit = s_endb[m];
+      }
+      if (r1 <= r2) {  // stopped before member r1
+        if (part && len) cut = 1;
+        else ok = 0;
+      } else if (s_code[s_flag] != ZD_END) {  // member r2 has no successor
+        if (part) cut = 1;
+        else ok = 0;
+      }
+      if (total > jb.out_cap) ok = 0;
+      if (ok) {
+        ZsDecDev d;
+        d.code = cut ? ZD_STOP : ZD_END;
+        d.msg = 0;
+        const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(jb.in) & 3u);
+        d.end_bits = end_bit - mis * 8u;
+        d.total_out = total;
+        decs[cj.job] = d;
+      }
+      fallback[cj.job] = ok ? 0u : 1u;
+      cjobs[blockIdx.x].nchain = ok ? len : 0u;
+      cjobs[blockIdx.x].ok = ok;
+      s_r1 = ok;  // (reused: the members are flagged below)
+    }
+    __syncthreads();
+    if (s_r1)
+      for (uint32_t i = t; i < nu; i += LINK_THREADS)
+        if ((s_pj[i] >> 16) == 0u && s_rk[i] < len) chunks[u0 + i].in_chain = 1;
+    return;
+  }
   // B: walk the chain.  A piece of a longer stream (ZS_JF_PART) ends its
   // chain at the last verified block boundary instead of failing: before a
   // member that did not stop at a block boundary (the unit cut off by the
