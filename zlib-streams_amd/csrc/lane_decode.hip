@@ -2116,6 +2116,34 @@ __device__ __forceinline__ void walk_prefetch(const LaneState &s, uint32_t wi, u
     for (uint32_t q = 0; q < WK_PF; q++) v[q] = s.w[min(wi + q, s.lastw)];
   }
 }
+// The walk's per-group prefetch, issued by every lane at every group (round
+// 6): the same vector-memory operations every group let the compiler wait for
+// exactly the previous group's prefetch (vmcnt counts in order; a refill issued
+// by some lanes only made it wait vmcnt(0) -- for every outstanding prefetch
+// and checkpoint store of the wave).  A lane that did not advance reloads the
+// same words (L2 hits); lanes without input read a valid dummy address.  The
+// clamped word loads near the input's end (once per stream) are waited for
+// at once, so they leave nothing outstanding.
+__device__ __forceinline__ void walk_prefetch_u(const gcu32 *base, uint32_t wi, uint32_t fastlim, uint32_t lastw,
+                                                uint32_t (&v)[WK_PF]) {
+  if (__builtin_expect(wi + WK_PF <= fastlim, 1)) {
+    const uint32_t *src = (const uint32_t *)(base + wi);
+#pragma unroll
+    for (int q = 0; q < WK_PF / 4; q++) {
+      uint4 x;
+      __builtin_memcpy(&x, src + 4 * q, 16);
+      v[4 * q] = x.x;
+      v[4 * q + 1] = x.y;
+      v[4 * q + 2] = x.z;
+      v[4 * q + 3] = x.w;
+    }
+  } else {
+#pragma unroll
+    for (uint32_t q = 0; q < WK_PF; q++) v[q] = base[min(wi + q, lastw)];
+#pragma unroll
+    for (uint32_t q = 0; q < WK_PF; q++) __asm__ volatile("" : "+v"(v[q]));  // waited for here
+  }
+}
 // a prefetched half into the lane's ring row (the mirror words with half 0)
 __device__ __forceinline__ void walk_put_half(uint32_t *rr, uint32_t wi, uint32_t (&v)[WK_PF], uint32_t end_byte) {
   if (wi + WK_PF > (end_byte >> 2)) {
@@ -2208,7 +2236,7 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
       }
     }
   }
-  uint2 *cp = cps + (size_t)(c < nchunks ? c : 0u) * WK_CP;
+  uint2 *cp = cps + (size_t)(c < nchunks ? c : nchunks) * WK_CP;  // (slot nchunks: idle lanes' dummy)
   uint32_t ntok = 0, K = WK_K0, ncp = 0, ncut = WK_K0, eob = 0, endb = 0;
   // The bit reader is one absolute bit position per lane, p: each step reads
   // the three ring words holding bits [p, p + 64) (ring slot = word % WK_RW;
@@ -2230,6 +2258,11 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
   }
   uint32_t xp = live ? 0u : 1u;  // an exception is pending: the lane stands at its symbol until the next group start
   uint32_t gi = 0;                // groups
+  // the per-group prefetch's source: the lane's input while it walks, then a
+  // fixed valid address (the tables) through the fast path
+  const gcu32 *pbase = live ? s.w : (const gcu32 *)tables;
+  uint32_t pflim = live ? (s.end_byte >> 2) : 0xffffffffu;
+  if (!live) filled = 0;
   // the ring row's address, opaque to the compiler (so that a step's ring
   // address is one shift-and-mask and one add, not folded LDS offsets)
   typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
@@ -2258,38 +2291,42 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
 #endif
     {  // a lane that has consumed its older half refills it from the prefetch
       const bool wr = live && filled - (p >> 5) <= WK_RW - WK_PF;
-      if (__builtin_amdgcn_ballot_w64(wr)) {
-        if (wr) {
-          walk_put_half(rr, filled, pre, s.end_byte);
-          filled += WK_PF;
-          walk_prefetch(s, filled, pre);
-        }
+      if (wr) {
+        walk_put_half(rr, filled, pre, s.end_byte);
+        filled += WK_PF;
       }
+      if (!live) {  // (a lane that has stopped reads the dummy from here on)
+        pbase = (const gcu32 *)tables;
+        pflim = 0xffffffffu;
+        filled = 0;
+      }
+      walk_prefetch_u(pbase, filled, pflim, s.lastw, pre);
     }
 #if KP_ON
     kp_cyc_r += KP_NOW() - kr0;
 #endif
-    // a checkpoint at the first group start past every K tokens, stored
-    // after the refill's wait (a store before it would make it wait; the lane
-    // stands on a symbol boundary here; a pending symbol is not yet counted)
-    if (__builtin_amdgcn_ballot_w64(live && ntok >= ncut)) {
-      if (live && ntok >= ncut) {  // the next sub-unit starts here
-        // out of slots (a 65th sub-unit): keep every second checkpoint, twice
-        // the stride.  Round 6: this halved on storing the 63rd checkpoint,
-        // i.e. every unit past 63 x 256 tokens -- zlib's 16 383-symbol blocks,
-        // nearly every C2 unit -- ran as 32 sub-units of 512 tokens
-        if (ncp == WK_CP - 1u) {
-          walk_halve(cp);
-          ncp = (WK_CP - 1u) / 2u;
-          K *= 2u;
-          ncut = (ncp + 1u) * K;
-        }
-        if (ntok >= ncut) {
-          cp[ncp] = make_uint2(p, ntok);
-          ncp++;
-          ncut += K;
-        }
+    // a checkpoint at the first group start past every K tokens (the lane
+    // stands on a symbol boundary here; a pending symbol is not yet counted).
+    // The pending slot is stored by every lane at every group, after the
+    // prefetch (one store per group: see walk_prefetch_u); it is kept once the
+    // lane has passed the next K tokens.
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(live && ntok >= ncut && ncp == WK_CP - 1u) != 0, 0)) {
+      // out of slots (a 65th sub-unit): keep every second checkpoint, twice
+      // the stride.  Round 6: this halved on storing the 63rd checkpoint, i.e.
+      // every unit past 63 x 256 tokens -- zlib's 16 383-symbol blocks, nearly
+      // every C2 unit -- ran as 32 sub-units of 512 tokens
+      if (live && ntok >= ncut && ncp == WK_CP - 1u) {
+        walk_halve(cp);
+        ncp = (WK_CP - 1u) / 2u;
+        K *= 2u;
+        ncut = (ncp + 1u) * K;
       }
+      __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): nothing of the rare path left outstanding
+    }
+    cp[ncp] = make_uint2(p, ntok);
+    if (live && ntok >= ncut) {  // the next sub-unit starts here
+      ncp++;
+      ncut += K;
     }
     // the pending symbols, exactly (every WK_RES groups: a pass costs about
     // a group's steps, a lane that waits loses half a group on average)
@@ -3682,7 +3719,7 @@ int split_reserve(uint32_t n) {
   g_split = SplitWs{};
   const size_t c = (size_t)n + n / 2;
   if (hipMalloc(&g_split.walks, c * sizeof(ZsWalkDev)) != hipSuccess ||
-      hipMalloc(&g_split.cps, c * WK_CP * sizeof(uint2)) != hipSuccess ||
+      hipMalloc(&g_split.cps, (c + 1) * WK_CP * sizeof(uint2)) != hipSuccess ||  // + idle lanes' slot (zs_walk_kernel)
       hipMalloc(&g_split.lists, (2 * c + 3) * sizeof(uint32_t)) != hipSuccess)
     return -1;
   g_split.cap = c;
