@@ -514,20 +514,23 @@ def test_c5_rank_share_world8_vs_oracle(zs):
 
 # ---------------------------------------------------------------------------
 # the segmented window link at the configurations the final build runs it
-# (zs_capi.cpp link_segments: S = min(8, 256 / streams) segments per chain)
+# (zs_capi.cpp link_segments: S = min(8, 512 / streams) segments per chain,
+# round 6; 256 / streams before)
 # ---------------------------------------------------------------------------
 def test_c2_headline_batch_segmented_link_vs_oracle(zs):
     """configs[1] exactly as the headline bench runs it: 64 x 64 MiB raw-deflate
     streams (Zipf text 0..31, line text 32..63, host zlib L6) in ONE batch with
-    default flags -- split parse (round 5), segmented link with 4 segments per
-    chain of ~720 members -- every job's output and (ret, msg, total_in,
-    total_out, adler) vs the oracle and the generator."""
+    default flags -- one group (ZS_GROUPS unset), split parse (round 5),
+    segmented link with 8 segments per chain of ~720 members (round 6) -- every
+    job's output and (ret, msg, total_in, total_out, adler) vs the oracle and
+    the generator."""
     raws, comps = corpus.batch(0, 64, 64 << 20, level=6, wbits=-15, nthreads=16)
     cases = [(r, c.tobytes(), -15) for r, c in zip(raws, comps)]
     del comps
     got = zs.inflate_batch([c[1] for c in cases], -15, [64 << 20] * 64)
     st = zs.last_stats()
-    assert st["parse"] == "split" and st["link"] == "segmented" and st["link_segments"] == 4, st
+    assert st["parse"] == "split" and st["link"] == "segmented" and st["link_segments"] == 8, st
+    assert st["groups"] == 1, st
     assert st["chunked_jobs"] == 64 and st["fallback_jobs"] == 0, st
     assert st["units_std"] >= 64 * 400, st  # chains of >= 400 members on average
     _compare_all_with_oracle(cases, got, 64 << 20)

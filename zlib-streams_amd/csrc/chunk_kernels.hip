@@ -1769,25 +1769,32 @@ extern "C" void zs_launch_fixed_tables(uint32_t *fixed, int d64, hipStream_t st)
 
 extern "C" void zs_launch_parse(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, ZsChunkDev *d_chunks, uint32_t nchunks,
                                 uint32_t *d_tokens, uint32_t *d_tables, const uint32_t *d_fixed, ZsTokPool pool, int d64,
-                                int wave_units, hipStream_t st);
+                                int wave_units, hipStream_t st, int ctx);
 extern "C" void zs_launch_expand(const ZsJobDev *d_jobs, ZsChunkDev *d_chunks, uint32_t nchunks, uint16_t *d_scratch,
-                                 const uint32_t *d_tokens, ZsTokPool pool, uint32_t *d_fallback, int d64, hipStream_t st);
+                                 const uint32_t *d_tokens, ZsTokPool pool, uint32_t *d_fallback, int d64, hipStream_t st,
+                                 int ctx);
 
 // One group of chunked jobs, all raw/zlib/gzip (d64 = 0) or all deflate64
-// (d64 = 1: 64 KiB history, so 64 KiB windows per unit slot).
+// (d64 = 1: 64 KiB history, so 64 KiB windows per unit slot).  ctx picks the
+// host-side sort / split workspaces, so that two groups can run at once on two
+// streams (zs_capi.cpp run_jobs); ev_found (optional) is recorded once the
+// group's units are planned.
 extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, ZsSegDev *d_segs, uint32_t nseg,
                                   ZsCJobDev *d_cjobs, uint32_t ncjobs, ZsChunkDev *d_units, uint32_t nunit_slots,
                                   uint16_t *d_scratch, uint32_t *d_tokens, ZsTokPool pool, uint32_t *d_tables,
                                   const uint32_t *d_fixed, uint8_t *d_windows, void *d_linkinfo, ZsDecDev *d_decs,
                                   uint32_t *d_fallback, int d64, int wave_units, void *d_plink, uint32_t plink_levels,
-                                  uint16_t *d_lmaps, uint32_t lsegs, hipStream_t st, hipEvent_t *ev) {
+                                  uint16_t *d_lmaps, uint32_t lsegs, hipStream_t st, hipEvent_t *ev, uint32_t *d_vlist,
+                                  int ctx, hipEvent_t ev_found) {
   // ev (profiling, optional): [0] before find, [1] after find + plan, [2] after
   // parse + chain, [3] after expand, [4] after link, [5] after emit
   if (ev) (void)hipEventRecord(ev[0], st);
   // the finder's survivor lists (FQ_LIST words per segment) borrow the token
-  // buffer: nothing reads or writes tokens before the parse (a segment is
+  // buffer (d_vlist: the group's own token regions, by default the buffer's
+  // start): nothing reads or writes them before the parse (a segment is
   // 32 KiB of input, the token space >= 8 bytes per input byte), and a later
-  // group's finder runs after this group's expand on the same stream
+  // group on the same stream finds after this group's expand
+  uint32_t *const vl = d_vlist ? d_vlist : d_tokens;
   const dim3 fgrid((nseg + FIND_WG - 1u) / FIND_WG), fblk(FIND_WG * WAVE);
   int ncu = 256;
   {
@@ -1796,22 +1803,23 @@ extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_hea
   }
   const dim3 vgrid(std::min<uint32_t>(nseg, (uint32_t)std::max(ncu, 1) * FV_WAVES_PER_CU));
   if (d64) {
-    hipLaunchKernelGGL(zs_find_kernel<true>, fgrid, fblk, 0, st, d_jobs, d_heads, d_segs, d_tokens, nseg);
-    hipLaunchKernelGGL(zs_findval_kernel<true>, vgrid, dim3(WAVE), 0, st, d_jobs, d_segs, d_tokens, nseg);
+    hipLaunchKernelGGL(zs_find_kernel<true>, fgrid, fblk, 0, st, d_jobs, d_heads, d_segs, vl, nseg);
+    hipLaunchKernelGGL(zs_findval_kernel<true>, vgrid, dim3(WAVE), 0, st, d_jobs, d_segs, vl, nseg);
   } else {
-    hipLaunchKernelGGL(zs_find_kernel<false>, fgrid, fblk, 0, st, d_jobs, d_heads, d_segs, d_tokens, nseg);
-    hipLaunchKernelGGL(zs_findval_kernel<false>, vgrid, dim3(WAVE), 0, st, d_jobs, d_segs, d_tokens, nseg);
+    hipLaunchKernelGGL(zs_find_kernel<false>, fgrid, fblk, 0, st, d_jobs, d_heads, d_segs, vl, nseg);
+    hipLaunchKernelGGL(zs_findval_kernel<false>, vgrid, dim3(WAVE), 0, st, d_jobs, d_segs, vl, nseg);
   }
-  hipLaunchKernelGGL(zs_findsel_kernel, dim3((nseg + 255u) / 256u), dim3(256), 0, st, d_segs, d_tokens, nseg);
+  hipLaunchKernelGGL(zs_findsel_kernel, dim3((nseg + 255u) / 256u), dim3(256), 0, st, d_segs, vl, nseg);
   hipLaunchKernelGGL(zs_find_fixed_kernel, dim3(nseg), dim3(64), 0, st, d_jobs, d_heads, d_segs, nseg);
   hipLaunchKernelGGL(zs_plan_kernel, dim3(ncjobs), dim3(PLAN_T), 0, st, d_jobs, d_heads, d_segs, d_cjobs, d_units, pool);
   if (ev) (void)hipEventRecord(ev[1], st);
+  if (ev_found) (void)hipEventRecord(ev_found, st);
   ZsLinkInfo *info = reinterpret_cast<ZsLinkInfo *>(d_linkinfo);
-  zs_launch_parse(d_jobs, d_heads, d_units, nunit_slots, d_tokens, d_tables, d_fixed, pool, d64, wave_units, st);
+  zs_launch_parse(d_jobs, d_heads, d_units, nunit_slots, d_tokens, d_tables, d_fixed, pool, d64, wave_units, st, ctx);
   hipLaunchKernelGGL(zs_chain_kernel, dim3(ncjobs), dim3(LINK_THREADS), 0, st, d_jobs, d_heads, d_units, d_cjobs, info,
                      d_decs, d_fallback);
   if (ev) (void)hipEventRecord(ev[2], st);
-  zs_launch_expand(d_jobs, d_units, nunit_slots, d_scratch, d_tokens, pool, d_fallback, d64, st);
+  zs_launch_expand(d_jobs, d_units, nunit_slots, d_scratch, d_tokens, pool, d_fallback, d64, st, ctx);
   if (ev) (void)hipEventRecord(ev[3], st);
   if (d_plink) {  // few long streams: windows by parallel prefix over each chain
     const dim3 grid((d64 ? 65536u : HIST) / PL_BLK, nunit_slots);

@@ -3657,10 +3657,11 @@ struct SortWs {  // grown on demand; the library serializes batches
   void *tmp = nullptr;
   size_t cap = 0, tmp_bytes = 0;
 };
-SortWs g_sort;
+SortWs g_sorts[2];  // one per concurrent chunked group (zs_launch_chunked ctx)
 // order[0..n) = unit slots by decreasing key (stable)
-int sort_units(const ZsJobDev *d_jobs, const ZsChunkDev *d_chunks, uint32_t n, int after_parse, uint32_t **order,
+int sort_units(int ctx, const ZsJobDev *d_jobs, const ZsChunkDev *d_chunks, uint32_t n, int after_parse, uint32_t **order,
                hipStream_t st) {
+  SortWs &g_sort = g_sorts[ctx & 1];
   if (n > g_sort.cap) {
     if (g_sort.buf) (void)hipFree(g_sort.buf);
     if (g_sort.tmp) (void)hipFree(g_sort.tmp);
@@ -3710,8 +3711,9 @@ struct SplitWs {  // split parse state per unit slot; grown on demand (the libra
   uint32_t *lists = nullptr;  // [0, cap) walked units, [cap, 2 cap) leftovers; then the two counts
   size_t cap = 0;
 };
-SplitWs g_split;
-int split_reserve(uint32_t n) {
+SplitWs g_splits[2];  // one per concurrent chunked group (zs_launch_chunked ctx)
+int split_reserve(int ctx, uint32_t n) {
+  SplitWs &g_split = g_splits[ctx & 1];
   if (n <= g_split.cap) return 0;
   if (g_split.walks) (void)hipFree(g_split.walks);
   if (g_split.cps) (void)hipFree(g_split.cps);
@@ -3744,8 +3746,9 @@ uint32_t split_grid(uint32_t n) {
 // sub-unit decode + leftovers, for batches with many units).
 extern "C" void zs_launch_parse(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads, ZsChunkDev *d_chunks, uint32_t nchunks,
                                 uint32_t *d_tokens, uint32_t *d_tables, const uint32_t *d_fixed, ZsTokPool pool, int d64,
-                                int wave_units, hipStream_t st) {
+                                int wave_units, hipStream_t st, int ctx) {
   if (!nchunks) return;
+  SplitWs &g_split = g_splits[ctx & 1];
   if (d64)
     hipLaunchKernelGGL(zs_unit_header_kernel<true>, dim3(nchunks), dim3(WAVE), 0, st, d_jobs, d_heads, d_chunks, d_tables,
                        d_fixed);
@@ -3753,8 +3756,8 @@ extern "C" void zs_launch_parse(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads
     hipLaunchKernelGGL(zs_unit_header_kernel<false>, dim3(nchunks), dim3(WAVE), 0, st, d_jobs, d_heads, d_chunks, d_tables,
                        d_fixed);
   uint32_t *order = nullptr;
-  if (sort_units(d_jobs, d_chunks, nchunks, 0, &order, st)) return;
-  if (wave_units == 2 && split_reserve(nchunks) == 0) {
+  if (sort_units(ctx, d_jobs, d_chunks, nchunks, 0, &order, st)) return;
+  if (wave_units == 2 && split_reserve(ctx, nchunks) == 0) {
     uint32_t *counts = g_split.lists + 2 * g_split.cap;
     uint32_t *lists = g_split.lists;
     (void)hipMemsetAsync(counts, 0, 3 * sizeof(uint32_t), st);  // splits, leftovers, the split's next unit
@@ -3831,10 +3834,11 @@ static bool expand_v1() {
 
 // expand the verified chain members (after zs_chain_kernel), longest first
 extern "C" void zs_launch_expand(const ZsJobDev *d_jobs, ZsChunkDev *d_chunks, uint32_t nchunks, uint16_t *d_scratch,
-                                 const uint32_t *d_tokens, ZsTokPool pool, uint32_t *d_fallback, int d64, hipStream_t st) {
+                                 const uint32_t *d_tokens, ZsTokPool pool, uint32_t *d_fallback, int d64, hipStream_t st,
+                                 int ctx) {
   if (!nchunks) return;
   uint32_t *order = nullptr;
-  if (sort_units(d_jobs, d_chunks, nchunks, 1, &order, st)) return;
+  if (sort_units(ctx, d_jobs, d_chunks, nchunks, 1, &order, st)) return;
   if (d64)
     hipLaunchKernelGGL(zs_expand_kernel<true>, dim3(nchunks), dim3(EXP_T), 0, st, d_jobs, d_chunks, d_scratch, d_tokens,
                        order, pool, d_fallback);

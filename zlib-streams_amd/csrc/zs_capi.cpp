@@ -68,7 +68,8 @@ extern "C" void zs_launch_chunked(const ZsJobDev *d_jobs, const ZsHeadDev *d_hea
                                   uint16_t *d_scratch, uint32_t *d_tokens, ZsTokPool pool, uint32_t *d_tables,
                                   const uint32_t *d_fixed, uint8_t *d_windows, void *d_linkinfo, ZsDecDev *d_decs,
                                   uint32_t *d_fallback, int d64, int wave_units, void *d_plink, uint32_t plink_levels,
-                                  uint16_t *d_lmaps, uint32_t lsegs, hipStream_t st, hipEvent_t *ev);
+                                  uint16_t *d_lmaps, uint32_t lsegs, hipStream_t st, hipEvent_t *ev, uint32_t *d_vlist,
+                                  int ctx, hipEvent_t ev_found);
 
 namespace {
 
@@ -153,6 +154,11 @@ struct Workspace {
   uint32_t *d_ptab = nullptr;    // pool page table: ZS_TP_MAXPG per unit slot (cap_units)
   uint32_t *d_pool_next = nullptr;
   uint32_t *d_fixed = nullptr;
+  // second chunked group (run_jobs): its stream, and the events that order it
+  // against the launch stream (fork after the header kernel, group A's finder
+  // done, join before the serial decoders)
+  hipStream_t stream_b = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_found = nullptr, ev_join = nullptr;
   // timing (zs_profile): events on the launch stream
   bool prof = false;
   // boundaries: [0] batch start, [1] after header, [2] after find, [3] after
@@ -166,8 +172,9 @@ struct Workspace {
   // to the serial decoder, serial jobs
   uint32_t stats[4] = {0, 0, 0, 0};
   // last launch's block-parallel path: parse mode / link levels of the std and
-  // deflate64 groups, lane-parse resident waves, units per group (zs_last_stats_ex)
-  uint32_t path[7] = {UINT32_MAX, 0, UINT32_MAX, 0, 0, 0, 0};
+  // deflate64 groups, lane-parse resident waves, units per group, raw/zlib/gzip
+  // groups run at once (zs_last_stats_ex)
+  uint32_t path[8] = {UINT32_MAX, 0, UINT32_MAX, 0, 0, 0, 0, 0};
 };
 
 // chunked-path tuning (env: ZS_CHUNK_KB, ZS_NO_CHUNK, ZS_POOL_PER_KB)
@@ -201,9 +208,10 @@ uint32_t plink_levels(uint32_t njobs, uint32_t max_units, uint32_t flags) {
   return lv;
 }
 // Segmented link (zs_linkseg_kernel): a group of at most 64 streams on the
-// serial link cuts each chain into segments so that about one workgroup per CU
-// links; env ZS_LINKSEG = 0 (or ZS_F_LINK_SERIAL) keeps zs_link_kernel.
-constexpr uint32_t LS_SEGS_MAX_HOST = 8, LS_TARGET_WG = 256;
+// serial link cuts each chain into segments so that about two workgroups per
+// CU link; env ZS_LINKSEG = 0 (or ZS_F_LINK_SERIAL) keeps zs_link_kernel.
+// (round 6: LS_TARGET_WG 512, 8 segments for 64 streams: C2 link 1.88 -> 1.77 ms)
+constexpr uint32_t LS_SEGS_MAX_HOST = 8, LS_TARGET_WG = 512;
 uint32_t link_segments(uint32_t njobs, uint32_t max_units, uint32_t flags) {
   // env ZS_LINKSEG: 0 = off, N = N segments per chain (at most LS_SEGS_MAX), unset = auto
   static const int force = [] {
@@ -239,6 +247,20 @@ int wave_units(size_t nseg, uint32_t flags) {
   }();
   if (force >= 0) return force;
   return nseg <= lim ? 1 : (split ? 2 : 0);
+}
+// Two chunked groups on two streams (run_jobs) for a raw/zlib/gzip group of
+// at least 8 streams and TWO_GROUP_SEGS search segments (32 KiB of input
+// each): env ZS_GROUPS=2.  Off by default -- measured (C2): 24.9-25.3 ms with
+// two groups vs 22.0-22.3 with one, also with the walk at the highest wave
+// priority; the groups' kernels squeeze each other's LDS (the walk keeps
+// ~51 KiB per wave resident for its whole ~3.6 ms) and slow the walk's chain.
+constexpr size_t TWO_GROUP_SEGS = 4096;
+bool two_groups_enabled() {
+  static const bool v = [] {
+    const char *e = std::getenv("ZS_GROUPS");
+    return e && e[0] == '2';
+  }();
+  return v;
 }
 bool chunking_enabled() {
   static bool v = [] {
@@ -514,6 +536,27 @@ int batch_locked(const zs_job *jobs, uint32_t n, zs_result *results, uint32_t fl
   return 0;
 }
 
+// the second chunked group's stream and events, created once (0 = ready)
+int ws_stream_b() {
+  if (g_ws.stream_b) return 0;
+  hipStream_t s = nullptr;
+  hipEvent_t e[3] = {nullptr, nullptr, nullptr};
+  bool ok = hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess;
+  for (int i = 0; i < 3 && ok; i++) ok = hipEventCreateWithFlags(&e[i], hipEventDisableTiming) == hipSuccess;
+  if (!ok) {
+    for (int i = 0; i < 3; i++)
+      if (e[i]) (void)hipEventDestroy(e[i]);
+    if (s) (void)hipStreamDestroy(s);
+    (void)hipGetLastError();
+    return -1;
+  }
+  g_ws.stream_b = s;
+  g_ws.ev_fork = e[0];
+  g_ws.ev_found = e[1];
+  g_ws.ev_join = e[2];
+  return 0;
+}
+
 // One launch over the prepared jobs g_ws.h_jobs[0, nv): routing, the chunked
 // pipeline, the serial decoders, then (dec_out == nullptr) the checks and
 // results into g_ws.h_res, or (pieces) each job's header and decode outcome
@@ -551,6 +594,28 @@ int run_jobs(uint32_t nv, uint64_t max_out, uint32_t flags, ZsDecDev *dec_out, Z
   // only sends the jobs to the serial decoder.
   ZsTokPool pool{};
   size_t seg_std = 0, slots_std = 0;
+  // Round 6: a large raw/zlib/gzip group runs as two groups on two streams
+  // (A on the launch stream, B on stream_b once A's finder is done), so that
+  // one group's boundary walk -- a serial chain per unit that keeps well under
+  // one wave per SIMD busy -- overlaps the other group's finder, unit headers,
+  // token decode, expand, link and emit.  n_a = raw/zlib/gzip jobs in group A
+  // (n_cj_std: one group).
+  uint32_t n_a = n_cj_std;
+  size_t seg_a = 0, slots_a = 0;
+  if (two_groups_enabled() && n_cj_std >= 8 && ws_stream_b() == 0) {
+    size_t tot = 0;
+    for (uint32_t q = 0; q < n_cj_std; q++) tot += (g_ws.h_jobs[cj_list[q]].in_len + C - 1) / C;
+    if (tot >= TWO_GROUP_SEGS) {
+      size_t acc = 0;
+      for (uint32_t q = 0; q < n_cj_std; q++) {
+        acc += (g_ws.h_jobs[cj_list[q]].in_len + C - 1) / C;
+        if (2 * acc >= tot) {
+          n_a = q + 1;
+          break;
+        }
+      }
+    }
+  }
   if (!cj_list.empty()) {
     size_t slots = 0, toks = 0, ents = 0, in_sum = 0, win = 0;
     nseg = 0;
@@ -560,6 +625,10 @@ int run_jobs(uint32_t nv, uint64_t max_out, uint32_t flags, ZsDecDev *dec_out, Z
     for (uint32_t q = 0; q < cj_list.size() && !rr; q++) {
       const uint32_t k = cj_list[q];
       const ZsJobDev &jd = g_ws.h_jobs[k];
+      if (q == n_a && n_a < n_cj_std) {
+        seg_a = si;
+        slots_a = slots;
+      }
       if (q == n_cj_std) {
         seg_std = si;
         slots_std = slots;
@@ -568,9 +637,12 @@ int run_jobs(uint32_t nv, uint64_t max_out, uint32_t flags, ZsDecDev *dec_out, Z
       const uint32_t max_units = ns * SEG_SLOTS + 1;
       ZsCJobDev cj{};
       cj.job = k;
-      cj.first_seg = (uint32_t)(si - (q >= n_cj_std ? seg_std : 0));  // group-relative
+      // group-relative: group A from 0, group B from (seg_a, slots_a), deflate64 from (seg_std, slots_std)
+      const size_t gseg = q >= n_cj_std ? seg_std : (q >= n_a ? seg_a : 0);
+      const size_t gslot = q >= n_cj_std ? slots_std : (q >= n_a ? slots_a : 0);
+      cj.first_seg = (uint32_t)(si - gseg);
       cj.nseg = ns;
-      cj.unit0 = (uint32_t)(slots - (q >= n_cj_std ? slots_std : 0));
+      cj.unit0 = (uint32_t)(slots - gslot);
       cj.max_units = max_units;
       // primary token regions (zs_plan_kernel): per unit span x ZS_TOK_PER_BYTE
       // + slack, spans summing to at most the input plus a byte per unit
@@ -637,13 +709,16 @@ int run_jobs(uint32_t nv, uint64_t max_out, uint32_t flags, ZsDecDev *dec_out, Z
   if (ev) HIP_OK(hipEventRecord(ev[0], st));
   zs_launch_header(g_ws.d_jobs, g_ws.d_heads, nv, st);
   const uint32_t n_cjs = n_cj - n_cj64;
+  const uint32_t n_ga = std::min(n_a, n_cjs), n_gb = n_cjs - n_ga;  // the two raw/zlib/gzip groups (n_gb = 0: one)
   // parallel-prefix link buffers (groups of few long streams)
-  uint32_t pl_std = 0, pl_d64 = 0, ls_std = 1;
+  uint32_t pl_std = 0, pl_d64 = 0, ls_std = 1, ls_b = 1;
   {
-    uint32_t mu_std = 0, mu_d64 = 0;
+    uint32_t mu_std = 0, mu_d64 = 0, mu_a = 0, mu_b = 0;
     for (uint32_t q = 0; q < n_cj; q++) (q < n_cjs ? mu_std : mu_d64) = std::max((q < n_cjs ? mu_std : mu_d64), g_ws.h_cjobs[q].max_units);
-    pl_std = n_cjs ? plink_levels(n_cjs, mu_std, flags) : 0;
-    ls_std = n_cjs && !pl_std ? link_segments(n_cjs, mu_std, flags) : 1;
+    for (uint32_t q = 0; q < n_cjs; q++) (q < n_ga ? mu_a : mu_b) = std::max((q < n_ga ? mu_a : mu_b), g_ws.h_cjobs[q].max_units);
+    pl_std = n_cjs && !n_gb ? plink_levels(n_cjs, mu_std, flags) : 0;
+    ls_std = n_cjs && !pl_std ? link_segments(n_ga, mu_a, flags) : 1;
+    ls_b = n_gb ? link_segments(n_gb, mu_b, flags) : 1;
     pl_d64 = n_cj64 ? plink_levels(n_cj64, mu_d64, flags) : 0;
     const size_t need = std::max<size_t>(pl_std ? 2 * slots_std * 32768u * 2u : 0,
                                          pl_d64 ? 2 * (nunit_slots - slots_std) * 65536u * 4u : 0);
@@ -653,9 +728,9 @@ int run_jobs(uint32_t nv, uint64_t max_out, uint32_t flags, ZsDecDev *dec_out, Z
       g_err.clear();
     }
     // segmented link: LS_SEGS_MAX segment-end maps (u16 per window byte) per chain of the group
-    const size_t lneed = ls_std > 1 ? (size_t)n_cjs * LS_SEGS_MAX_HOST * 32768u * 2u : 0;
+    const size_t lneed = (ls_std > 1 || ls_b > 1) ? (size_t)n_cjs * LS_SEGS_MAX_HOST * 32768u * 2u : 0;
     if (lneed && ws_reserve_bytes(&g_ws.d_lmaps, &g_ws.cap_lmaps, lneed)) {
-      ls_std = 1;  // serial link instead
+      ls_std = ls_b = 1;  // serial link instead
       (void)hipGetLastError();
       g_err.clear();
     }
@@ -666,13 +741,32 @@ int run_jobs(uint32_t nv, uint64_t max_out, uint32_t flags, ZsDecDev *dec_out, Z
   g_ws.path[1] = pl_std ? pl_std : (ls_std > 1 ? 0x80000000u | ls_std : 0u);
   g_ws.path[2] = wu_d64;
   g_ws.path[3] = pl_d64;
+  g_ws.path[7] = n_cjs ? (n_gb ? 2u : 1u) : 0u;
   if (n_cjs) {
-    zs_launch_chunked(g_ws.d_jobs, g_ws.d_heads, g_ws.d_segs, (uint32_t)seg_std, g_ws.d_cjobs, n_cjs, g_ws.d_chunks,
-                      (uint32_t)slots_std, g_ws.d_scratch, g_ws.d_tokens, pool, g_ws.d_tables, g_ws.d_fixed,
+    if (n_gb) {  // group B's stream starts after everything so far on the launch stream
+      HIP_OK(hipEventRecord(g_ws.ev_fork, st));
+      HIP_OK(hipStreamWaitEvent(g_ws.stream_b, g_ws.ev_fork, 0));
+    }
+    const size_t sa = n_gb ? seg_a : seg_std, ua = n_gb ? slots_a : slots_std;
+    zs_launch_chunked(g_ws.d_jobs, g_ws.d_heads, g_ws.d_segs, (uint32_t)sa, g_ws.d_cjobs, n_ga, g_ws.d_chunks,
+                      (uint32_t)ua, g_ws.d_scratch, g_ws.d_tokens, pool, g_ws.d_tables, g_ws.d_fixed,
                       g_ws.d_windows, g_ws.d_linkinfo, g_ws.d_decs, g_ws.d_fallback, 0, (int)wu_std,
                       pl_std ? g_ws.d_plink : nullptr, pl_std,
                       ls_std > 1 ? reinterpret_cast<uint16_t *>(g_ws.d_lmaps) : nullptr, ls_std, st,
-                      ev ? ev + 1 : nullptr);
+                      ev ? ev + 1 : nullptr, nullptr, 0, n_gb ? g_ws.ev_found : nullptr);
+    if (n_gb) {  // group B: its own slice of every per-unit array, its finder lists in its own token regions
+      HIP_OK(hipStreamWaitEvent(g_ws.stream_b, g_ws.ev_found, 0));
+      ZsTokPool pb = pool;
+      pb.ptab = pool.ptab + slots_a * ZS_TP_MAXPG;
+      zs_launch_chunked(g_ws.d_jobs, g_ws.d_heads, g_ws.d_segs + seg_a, (uint32_t)(seg_std - seg_a), g_ws.d_cjobs + n_ga,
+                        n_gb, g_ws.d_chunks + slots_a, (uint32_t)(slots_std - slots_a), g_ws.d_scratch, g_ws.d_tokens, pb,
+                        g_ws.d_tables + slots_a * TABLE_ENTRIES_HOST, g_ws.d_fixed, g_ws.d_windows + slots_a * 32768,
+                        g_ws.d_linkinfo + slots_a * 2, g_ws.d_decs, g_ws.d_fallback, 0, (int)wu_std, nullptr, 0,
+                        ls_b > 1 ? reinterpret_cast<uint16_t *>(g_ws.d_lmaps) + (size_t)n_ga * LS_SEGS_MAX_HOST * 32768u
+                                 : nullptr,
+                        ls_b, g_ws.stream_b, nullptr, g_ws.d_tokens + g_ws.h_cjobs[n_ga].tok0, 1, nullptr);
+      HIP_OK(hipEventRecord(g_ws.ev_join, g_ws.stream_b));
+    }
   }
   if (n_cj64) {  // the deflate64 group: its own slice of every per-unit array
     ZsTokPool p64 = pool;
@@ -682,8 +776,9 @@ int run_jobs(uint32_t nv, uint64_t max_out, uint32_t flags, ZsDecDev *dec_out, Z
                       g_ws.d_scratch, g_ws.d_tokens, p64, g_ws.d_tables + slots_std * TABLE_ENTRIES_HOST,
                       g_ws.d_fixed + FIXED_WORDS_HOST, g_ws.d_windows + slots_std * 32768, g_ws.d_linkinfo + slots_std * 2,
                       g_ws.d_decs, g_ws.d_fallback, 1, (int)wu_d64, pl_d64 ? g_ws.d_plink : nullptr,
-                      pl_d64, nullptr, 1, st, (ev && !n_cjs) ? ev + 1 : nullptr);
+                      pl_d64, nullptr, 1, st, (ev && !n_cjs) ? ev + 1 : nullptr, nullptr, 0, nullptr);
   }
+  if (n_gb) HIP_OK(hipStreamWaitEvent(st, g_ws.ev_join, 0));  // group B done before its fallbacks and the results
   if (!n_cj && ev)
     for (int i = 1; i <= 6; i++) HIP_OK(hipEventRecord(ev[i], st));
   zs_launch_decode(0, g_ws.d_jobs, g_ws.d_heads, g_ws.d_ids, n_std, g_ws.d_decs, nullptr, st);
@@ -3227,10 +3322,10 @@ int zs_last_stats(uint32_t out[4]) {
 
 int zs_last_stats_ex(uint32_t *out, uint32_t n) {
   std::lock_guard<std::mutex> lk(g_mu);
-  uint32_t v[11];
+  uint32_t v[12];
   for (int i = 0; i < 4; i++) v[i] = g_ws.stats[i];
-  for (int i = 0; i < 7; i++) v[4 + i] = g_ws.path[i];
-  const uint32_t k = n < 11 ? n : 11;
+  for (int i = 0; i < 8; i++) v[4 + i] = g_ws.path[i];
+  const uint32_t k = n < 12 ? n : 12;
   for (uint32_t i = 0; i < k; i++) out[i] = v[i];
   return (int)k;
 }

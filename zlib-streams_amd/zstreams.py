@@ -393,8 +393,8 @@ def last_stats():
     """Last batch: jobs on the chunked path, decode units planned for them, chunked
     jobs whose chain did not verify (decoded by the serial decoder instead), and
     jobs routed to the serial decoder directly."""
-    a = (ctypes.c_uint32 * 11)()
-    k = lib().zs_last_stats_ex(a, 11)
+    a = (ctypes.c_uint32 * 12)()
+    k = lib().zs_last_stats_ex(a, 12)
     if k < 0:
         _check(k)
     mode = {0: "lane", 1: "wave", 2: "split"}
@@ -403,7 +403,8 @@ def last_stats():
                                                                     "segmented" if a[5] & 0x80000000 else "prefix"),
             "parse_d64": mode.get(a[6]), "link_d64": None if a[6] > 2 else ("serial" if a[7] == 0 else "prefix"),
             "link_segments": (a[5] & 0x7fffffff) if a[4] <= 2 and a[5] & 0x80000000 else None,
-            "lane_resident_waves": a[8], "units_std": a[9], "units_d64": a[10]}
+            "lane_resident_waves": a[8], "units_std": a[9], "units_d64": a[10],
+            "groups": a[11] if k >= 12 else None}  # raw/zlib/gzip groups run at once on two streams (round 6)
 
 
 def stream_stats():
