@@ -51,6 +51,8 @@ def main():
         sys.exit("no counters: ZS_LIB must point at libzstreams_mi355x_prof.so")
     ok = all(r["ret"] == 1 and bytes(o) == bytes(raws[k]) for k, (o, r) in enumerate(res))
     d = {NAMES[i]: v for i, v in enumerate(c) if i in NAMES}
+    # expand2 flush counters in lane-parse slots the split parse leaves unused
+    d.update({"x_pieces": c[6], "x_pieces_marked": c[7], "x_pieces_marked_tail": c[8], "x_markers": c[12]})
     w = max(d["p_waves"], 1)
     b = max(d["e_blocks"], 1)
     derived = {
@@ -110,6 +112,10 @@ def main():
         "fv_steps_frac": d.get("fv_cyc_steps", 0) / max(d.get("fv_cyc_total", 0), 1),
         "fv_wave_steps_per_round": d.get("fv_wave_steps", 0) / max(d.get("fv_rounds", 0), 1),
         "fv_cycles_per_wave": d.get("fv_cyc_total", 0) / max(d.get("fv_waves", 0), 1),
+        # expand2 flush: 256-entry wave pieces holding a history marker (the emit's real work)
+        "x_marked_piece_frac": d.get("x_pieces_marked", 0) / max(d.get("x_pieces", 0), 1),
+        "x_marked_tail_frac": d.get("x_pieces_marked_tail", 0) / max(d.get("x_pieces_marked", 0), 1),
+        "x_marker_entry_frac": d.get("x_markers", 0) / max(256 * d.get("x_pieces", 0), 1),
     }
     out = {"raw": d, "derived": derived}
     print(json.dumps(out, indent=1))

@@ -3352,6 +3352,7 @@ __global__ void __launch_bounds__(EX2_T) zs_expand2_kernel(const ZsJobDev *__res
   const uint64_t kp_t0 = KP_NOW();
   uint64_t kp_batch = 0, kp_pre = 0, kp_spin = 0;
   uint32_t kp_rounds = 0, kp_passes = 0, kp_srounds = 0, kp_batches = 0;
+  uint32_t kp_pc = 0, kp_pf = 0, kp_pt = 0, kp_me = 0;  // wave pieces: all, with a marker, of those in the last HIST; markers
 #endif
   auto load_batch = [&]() {
 #if KP_ON
@@ -3398,6 +3399,20 @@ __global__ void __launch_bounds__(EX2_T) zs_expand2_kernel(const ZsJobDev *__res
   };
   uint32_t R = 0, Rs = 0, carry = 0, flushed = 0, Fs = 0;
   const uint32_t toff = tid * EX2_E;
+#if KP_ON
+  // (profiling) a flushed wave piece (256 entries): does any entry still hold a
+  // history marker?  Round 6 measured 81% of C2's entries and 99.9% of its
+  // pieces do -- an emit that patched only marked pieces could not pay
+  auto kp_piece = [&](uint32_t fs, uint32_t fl) {
+    uint32_t m = 0;
+    for (int k = 0; k < EX2_E; k++) m += ring[fs + toff + k] >= MARK_BASE ? 1u : 0u;
+    kp_pc++;
+    kp_me += kp_wave_sum(m);
+    const bool f = __ballot(m != 0) != 0;
+    kp_pf += f ? 1u : 0u;
+    kp_pt += f && fl + wv * WAVE * EX2_E + WAVE * EX2_E > total - min(total, (uint32_t)HIST) ? 1u : 0u;
+  };
+#endif
   auto place = [&]() {  // marks of the loaded batch's tokens that start in round R
 #pragma unroll
     for (int j = 0; j < EX2_TPT; j++) {
@@ -3421,6 +3436,9 @@ __global__ void __launch_bounds__(EX2_T) zs_expand2_kernel(const ZsJobDev *__res
 #endif
     exp_barrier();  // B1: marks visible; the previous round's entries final
     while (R - flushed >= EX2_N) {
+#if KP_ON
+      kp_piece(Fs, flushed);
+#endif
       ex2_copy(out + flushed + toff, &ring[Fs + toff]);
       flushed += EX2_N;
       Fs = Fs + EX2_N == EX2_RS ? 0u : Fs + EX2_N;
@@ -3528,6 +3546,9 @@ __global__ void __launch_bounds__(EX2_T) zs_expand2_kernel(const ZsJobDev *__res
   }
   exp_barrier();
   while (total - flushed >= EX2_N) {
+#if KP_ON
+    kp_piece(Fs, flushed);
+#endif
     ex2_copy(out + flushed + toff, &ring[Fs + toff]);
     flushed += EX2_N;
     Fs = Fs + EX2_N == EX2_RS ? 0u : Fs + EX2_N;
@@ -3547,6 +3568,10 @@ __global__ void __launch_bounds__(EX2_T) zs_expand2_kernel(const ZsJobDev *__res
     KP_ADD(KP_E_CYC_JUMP, kp_spin);
     KP_ADD(KP_E_BATCHES, kp_batches);
     KP_ADD(KP_E_JUMP_ROUNDS + 1, kp_pre);
+    KP_ADD(6, kp_pc);  // (lane-parse slots the split parse leaves unused)
+    KP_ADD(7, kp_pf);
+    KP_ADD(8, kp_pt);
+    KP_ADD(12, kp_me);
   }
 #endif
 }
