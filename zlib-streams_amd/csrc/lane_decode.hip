@@ -1969,7 +1969,13 @@ static_assert(WKL_BITS + 1u >= WK_LBITS && WKL_BITS <= WK_LBITS && WKD_BITS + 1u
 #ifndef WK_RES
 #define WK_RES 2u  // measured: C2 walk 3.92 ms resolving every group, 3.81 every second
 #endif
-#define WK_GS(d64) ((d64) ? 7u : 9u)  // steps per group: <= 60 (48) bits each, so a group reads words p / 32 .. p / 32 + 16
+#ifndef WK_GSN
+#define WK_GSN 10u  // measured (C2 parse): 9 steps 7.44 ms, 10 steps 7.34
+#endif
+// steps per group: <= 60 (48) bits each, so a group reads words p / 32 .. p / 32 + 16
+// (!D64: 10 steps read at most word p / 32 + 16 too: (31 + 9 x 48) / 32 + 2)
+#define WK_GS(d64) ((d64) ? 7u : WK_GSN)
+static_assert(WK_GSN <= 10u, "a walk group reads at most 17 ring words");
 #define WK_PF 16u   // words per prefetch: the ring is two such halves
 #define WK_RW 32u   // input ring words per lane
 #define WK_RS 35u   // a lane's ring row: WK_RW words, words 0 and 1 again (a 3-word read never wraps), odd stride

@@ -810,6 +810,13 @@ int run_jobs(uint32_t nv, uint64_t max_out, uint32_t flags, ZsDecDev *dec_out, Z
   } else {
     HIP_OK(hipMemcpyAsync(g_ws.h_res, g_ws.d_res, nv * sizeof(ZsResultDev), hipMemcpyDeviceToHost, st));
   }
+  // the chunked path's statistics ride along before the one synchronisation
+  // (round 6: two blocking copies after it left the GPU idle between batches)
+  uint32_t *const h_fb = g_ws.h_ids + nv;  // (pinned, 3 x cap_jobs; [0, nv) held the ids)
+  if (n_cj) {
+    HIP_OK(hipMemcpyAsync(h_fb, g_ws.d_fallback, nv * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(g_ws.h_cjobs, g_ws.d_cjobs, n_cj * sizeof(ZsCJobDev), hipMemcpyDeviceToHost, st));
+  }
   HIP_OK(hipStreamSynchronize(st));
   if (ev) {
     float ms = 0.f, bms = 0.f;
@@ -831,10 +838,7 @@ int run_jobs(uint32_t nv, uint64_t max_out, uint32_t flags, ZsDecDev *dec_out, Z
   g_ws.stats[2] = 0;
   g_ws.stats[3] = n_std + n_d64;
   if (n_cj) {
-    std::vector<uint32_t> fb(nv);
-    HIP_OK(hipMemcpy(fb.data(), g_ws.d_fallback, nv * sizeof(uint32_t), hipMemcpyDeviceToHost));
-    HIP_OK(hipMemcpy(g_ws.h_cjobs, g_ws.d_cjobs, n_cj * sizeof(ZsCJobDev), hipMemcpyDeviceToHost));
-    for (uint32_t k : cj_list) g_ws.stats[2] += fb[k];
+    for (uint32_t k : cj_list) g_ws.stats[2] += h_fb[k];
     for (uint32_t q = 0; q < n_cj; q++) g_ws.stats[1] += g_ws.h_cjobs[q].nunits;
     for (uint32_t q = 0; q < n_cj; q++) g_ws.path[q < n_cjs ? 5 : 6] += g_ws.h_cjobs[q].nunits;
     if (std::getenv("ZS_DEBUG_CHUNKS")) {
