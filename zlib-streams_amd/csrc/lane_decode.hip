@@ -164,6 +164,17 @@ __device__ __forceinline__ uint16_t lds_len_root(const uint32_t *zt, uint32_t lb
 
 typedef __attribute__((address_space(1))) const uint32_t gcu32;
 typedef __attribute__((address_space(1))) uint32_t gu32;
+
+// Raw buffer stores through a wave-uniform resource (round 6): a lane whose
+// byte offset is BUF_SKIP (out of range) stores nothing -- no memory traffic --
+// so a store every lane issues at every iteration (uniform control flow, hence
+// exact vmcnt waits for the loads around it) can still be a conditional one.
+// gfx9 raw buffer resource: word 3 = 0x00020000 (untyped, offsets in bytes);
+// num_records bounds the offsets (< 4 GiB).
+#define BUF_SKIP 0x80000000u
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void *base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, (int)bytes, 0x00020000);
+}
 typedef __attribute__((address_space(1))) const uint16_t gcu16;
 
 // masked input word: bytes at or past end_byte read as zero; never reads a
@@ -2243,6 +2254,9 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
     }
   }
   uint2 *cp = cps + (size_t)(c < nchunks ? c : nchunks) * WK_CP;  // (slot nchunks: idle lanes' dummy)
+  // the per-group checkpoint store: the whole checkpoint array as one buffer
+  const __amdgpu_buffer_rsrc_t cpr = buf_rsrc(cps, (nchunks + 1u) * WK_CP * 8u);
+  const uint32_t cpo = (c < nchunks ? c : nchunks) * WK_CP * 8u;
   uint32_t ntok = 0, K = WK_K0, ncp = 0, ncut = WK_K0, eob = 0, endb = 0;
   // The bit reader is one absolute bit position per lane, p: each step reads
   // the three ring words holding bits [p, p + 64) (ring slot = word % WK_RW;
@@ -2313,9 +2327,10 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
 #endif
     // a checkpoint at the first group start past every K tokens (the lane
     // stands on a symbol boundary here; a pending symbol is not yet counted).
-    // The pending slot is stored by every lane at every group, after the
-    // prefetch (one store per group: see walk_prefetch_u); it is kept once the
-    // lane has passed the next K tokens.
+    // Every lane issues the store at every group, after the prefetch (one
+    // store per group: see walk_prefetch_u); only a lane past the next K tokens
+    // stores (round 6: a buffer store whose other lanes' offsets are out of
+    // range -- storing the pending slot at every group was 0.6 GB of writes).
     if (__builtin_expect(__builtin_amdgcn_ballot_w64(live && ntok >= ncut && ncp == WK_CP - 1u) != 0, 0)) {
       // out of slots (a 65th sub-unit): keep every second checkpoint, twice
       // the stride.  Round 6: this halved on storing the 63rd checkpoint, i.e.
@@ -2329,10 +2344,15 @@ __global__ void __launch_bounds__(64) zs_walk_kernel(const ZsJobDev *__restrict_
       }
       __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): nothing of the rare path left outstanding
     }
-    cp[ncp] = make_uint2(p, ntok);
-    if (live && ntok >= ncut) {  // the next sub-unit starts here
-      ncp++;
-      ncut += K;
+    {  // the checkpoint, stored only by a lane that keeps it (others: out of range, dropped)
+      typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+      const bool keep = live && ntok >= ncut;
+      const u32x2 v = {p, ntok};
+      __builtin_amdgcn_raw_buffer_store_b64(v, cpr, keep ? (cpo + ncp * 8u) : BUF_SKIP, 0, 0);
+      if (keep) {  // the next sub-unit starts here
+        ncp++;
+        ncut += K;
+      }
     }
     // the pending symbols, exactly (every WK_RES groups: a pass costs about
     // a group's steps, a lane that waits loses half a group on average)
