@@ -789,7 +789,9 @@ __global__ void __launch_bounds__(PLAN_T) zs_plan_kernel(const ZsJobDev *__restr
         st = units[cj.unit0 + i].start_bit;
         sp = i + 1 < nunits ? units[cj.unit0 + i + 1].start_bit : ZS_NONE;
         const uint32_t span_bytes = ((sp == ZS_NONE ? end_bit : sp) - st + 7u) / 8u;
-        cap = ((uint64_t)span_bytes * ZS_TOK_PER_BYTE + ZS_TOK_SLACK + 7u) & ~7ull;
+        // whole 128-byte lines: every unit's token region starts line-aligned (the split
+        // decode writes 64-byte halves, round 6)
+        cap = ((uint64_t)span_bytes * ZS_TOK_PER_BYTE + ZS_TOK_SLACK + 31u) & ~31ull;
       }
       // exclusive u64 prefix of the regions (thread 0 walks the tile)
       s_c[t] = cap;

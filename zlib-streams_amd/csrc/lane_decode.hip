@@ -2556,6 +2556,10 @@ __device__ __forceinline__ uint32_t split_dist_entry(uint32_t ce, bool d64) {  /
 #ifndef SPLIT_ALIGN
 #define SPLIT_ALIGN 1  // measured (C2 split): 3.22 ms with 10-step groups at any token offset, 3.02 aligned 8-step groups
 #endif
+#ifndef SPLIT_PAIR
+#define SPLIT_PAIR 1  // token stores in 64-byte pairs of groups (round 6: C2 split writes 5.29 -> 3.99 GB,
+                      // step time within noise; non-temporal stores instead: parse 7.0 -> 13.0 ms)
+#endif
 #ifndef SPLIT_NOSTORE
 #define SPLIT_NOSTORE 0  // (diagnostic builds only: no token stores, wrong output)
 #endif
@@ -2649,9 +2653,52 @@ __device__ __forceinline__ void split_sub3(SplitLDS<D64> &L, SplitLane &t, LaneS
   // group, they made that wait wait for them -- C2 split 3.2 ms, 2.3 without
   // stores at all)
   uint32_t tkp[GS], g0p = 0, gkp = 0;
+#if SPLIT_PAIR
+  // (round 6) a whole group starting a 64-byte half line (token regions are
+  // line-aligned) waits in hold[] for the next one: the pair leaves as one
+  // 64-byte run -- single 32-byte pieces cost 64-byte write-backs (C2 split:
+  // 5.3 GB written for 3.0 GB of tokens)
+  static_assert(D64 || SP_GS(false) == 8u, "pairs of 8-token groups");
+  uint32_t hold[GS], holdp = 0;
+  bool hv = false;
+  auto store32 = [&](uint32_t at, const uint32_t (&v)[GS]) {
+    typedef uint32_t u32x4a4t __attribute__((ext_vector_type(4), aligned(4)));
+    gu32 *dst = s.tok + at;
+#pragma unroll
+    for (uint32_t q = 0; q < GS; q += 4u) {
+      u32x4a4t x;
+      x.x = v[q]; x.y = v[q + 1]; x.z = v[q + 2]; x.w = v[q + 3];
+      *reinterpret_cast<__attribute__((address_space(1))) u32x4a4t *>(dst + q) = x;
+    }
+  };
+  auto flush_hold = [&]() {
+    if (hv) store32(holdp, hold);
+    hv = false;
+  };
+#endif
   auto store_prev = [&]() {
 #if KP_ON
     const uint64_t kf0 = KP_NOW();
+#endif
+#if SPLIT_PAIR
+    if (!D64 && gkp && !SPLIT_NOSTORE) {
+      const bool whole = gkp == GS && g0p + GS <= s.tcap;
+      if (whole && hv && holdp + GS == g0p) {  // the pair: 64 bytes
+        store32(holdp, hold);
+        store32(g0p, tkp);
+        hv = false;
+        gkp = 0;
+      } else {
+        flush_hold();
+        if (whole && (g0p & (2u * GS - 1u)) == 0u) {  // the first half of a pair: wait for the second
+#pragma unroll
+          for (uint32_t j = 0; j < GS; j++) hold[j] = tkp[j];
+          holdp = g0p;
+          hv = true;
+          gkp = 0;
+        }
+      }
+    }
 #endif
     if (gkp && !SPLIT_NOSTORE) {
       if (gkp == GS && g0p + GS <= s.tcap) {  // 16-byte stores, then 8 / 4 bytes
@@ -2785,6 +2832,9 @@ __device__ __forceinline__ void split_sub3(SplitLDS<D64> &L, SplitLane &t, LaneS
 #endif
   }
   if (!D64) store_prev();  // the last group's tokens
+#if SPLIT_PAIR
+  if (!D64) flush_hold();
+#endif
 }
 
 template <bool D64>

@@ -647,7 +647,7 @@ int run_jobs(uint32_t nv, uint64_t max_out, uint32_t flags, ZsDecDev *dec_out, Z
       // primary token regions (zs_plan_kernel): per unit span x ZS_TOK_PER_BYTE
       // + slack, spans summing to at most the input plus a byte per unit
       cj.tok0 = toks;
-      toks += ((jd.in_len + max_units) * ZS_TOK_PER_BYTE + (size_t)max_units * (ZS_TOK_SLACK + 8) + 63) & ~size_t(63);
+      toks += ((jd.in_len + max_units) * ZS_TOK_PER_BYTE + (size_t)max_units * (ZS_TOK_SLACK + 32) + 63) & ~size_t(63);
       // entries: the verified chain's total never exceeds out_cap (else the
       // serial decoder answers); every member starts 8-entry aligned
       // (zs_chain_kernel), hence 8 entries of padding per possible unit
