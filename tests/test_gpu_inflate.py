@@ -8,6 +8,8 @@ import hashlib
 import json
 import os
 import random
+import subprocess
+import sys
 import zlib
 
 import pytest
@@ -678,3 +680,16 @@ def test_all_literals_on_one_long_length(zs, parse):
     for (r, c, wb), (out, info) in zip(cases, got):
         eo, ei = O.oneshot(c, wb, len(r))
         assert out == eo == r and info == ei and info["ret"] == 1, (wb, info, ei)
+
+
+def test_split_leftovers_from_start():
+    """Round 6: a split unit that fails its own check (WK_LEFT) is decoded again
+    from its start by the leftover kernel, header included (the split parse's
+    unit headers write no zlib-layout tables).  ZS_SPLIT_LEFT=1 fails every
+    split unit on purpose; Zipf and line text plus a truncated stream, vs the
+    oracle (tests/split_left_check.py, in a child process: the knob is read
+    once per process)."""
+    env = dict(os.environ, ZS_SPLIT_LEFT="1")
+    r = subprocess.run([sys.executable, os.path.join(HERE, "split_left_check.py")], env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]

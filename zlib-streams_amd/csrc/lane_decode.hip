@@ -833,7 +833,7 @@ template <bool D64>
 __device__ int wave_dyn_header(BuildLDS &B, const uint32_t *w, uint32_t end_byte, uint32_t &bit, uint32_t *tabg,
                                uint16_t *ctab, uint32_t &lbits, uint32_t &dbits, uint16_t *lroot_out,
                                uint16_t *droot_out, uint8_t *dtail_out, uint8_t *walk_out = nullptr,
-                               uint32_t *ltail_out = nullptr) {
+                               uint32_t *ltail_out = nullptr, bool zl_out = true) {
   const uint32_t lane = lane_id();
   const uint32_t limit = end_byte * 8u;
   StageBits sb;
@@ -914,7 +914,7 @@ __device__ int wave_dyn_header(BuildLDS &B, const uint32_t *w, uint32_t end_byte
   }
   __builtin_amdgcn_wave_barrier();
   for (uint32_t i = lane; i < ZBUILD; i += WAVE) {
-    tabg[i] = B.tab[i];
+    if (zl_out) tabg[i] = B.tab[i];
     ctab[i] = compact_len_entry(B.tab[i], i < (1u << lbits) ? 0u : lbits);
   }
   for (uint32_t i = lane; i < LROOT_N; i += WAVE) lroot_out[i] = lds_len_root(B.tab, lbits, i);
@@ -928,7 +928,7 @@ __device__ int wave_dyn_header(BuildLDS &B, const uint32_t *w, uint32_t end_byte
   }
   __builtin_amdgcn_wave_barrier();
   for (uint32_t i = lane; i < (D64 ? 594u : 592u); i += WAVE) {
-    tabg[DIST_TABLE_OFF + i] = B.tab[i];
+    if (zl_out) tabg[DIST_TABLE_OFF + i] = B.tab[i];
     ctab[DIST_TABLE_OFF + i] = compact_dist_entry(B.tab[i], i < (1u << dbits) ? 0u : dbits);
   }
   droot_out[lane] = compact_dist_entry(B.tab[lane & ((1u << dbits) - 1u)]);
@@ -1681,6 +1681,15 @@ __device__ void unitw_unit(UnitWLDS &L, uint32_t c, const ZsJobDev *__restrict__
     s.zd = lane_tab + DIST_TABLE_OFF;
     s.lbits = (ch.hdr_info >> 8) & 15u;
     s.dbits = (ch.hdr_info >> 12) & 15u;
+  }
+  if (wk && wk->status == WK_LEFT) {  // a failed split: from the unit's start, header included (round 6: the
+    s.mode = LM_BLOCK;                 // split parse's unit headers leave no zlib-layout tables)
+    s.bit = ch.start_bit;
+    s.last = 0;
+    s.zl = fixed;
+    s.zd = fixed + 512;
+    s.lbits = 9;
+    s.dbits = 5;
   }
   if (wk && wk->status == WK_CONT) {  // the split decoded the first block: resume at its end
     s.mode = LM_BLOCK;
@@ -2842,7 +2851,8 @@ __global__ void __launch_bounds__(64) zs_split_kernel(const ZsJobDev *__restrict
                                                        uint32_t nchunks, uint32_t *__restrict__ tokens,
                                                        const uint32_t *__restrict__ tables, ZsTokPool pool,
                                                        ZsWalkDev *__restrict__ walks, const uint2 *__restrict__ cps,
-                                                       uint32_t *__restrict__ lists, uint32_t *__restrict__ counts) {
+                                                       uint32_t *__restrict__ lists, uint32_t *__restrict__ counts,
+                                                       int force_left) {
   __shared__ SplitLDS<D64> L;
   const uint32_t lane = threadIdx.x;
   const uint32_t nsplit = counts[0];
@@ -2976,7 +2986,7 @@ __global__ void __launch_bounds__(64) zs_split_kernel(const ZsJobDev *__restrict
       }
       if (((e >> 4) & 3u) != SK_EOB || b1 + (e & 15u) != wk.end_bit) bad = 1;
     }
-    const bool anybad = __ballot(act && bad) != 0, anyfull = __ballot(full) != 0;
+    const bool anybad = __ballot(act && bad) != 0 || force_left, anyfull = __ballot(full) != 0;
     // output position of every sub-unit: a wave scan of their entry counts
     uint64_t incl = act ? t.pos : 0u;
 #pragma unroll
@@ -3667,7 +3677,7 @@ template <bool D64>
 __global__ void __launch_bounds__(64) zs_unit_header_kernel(const ZsJobDev *__restrict__ jobs,
                                                              const ZsHeadDev *__restrict__ heads,
                                                              ZsChunkDev *__restrict__ units, uint32_t *__restrict__ tables,
-                                                             const uint32_t *__restrict__ fixed) {
+                                                             const uint32_t *__restrict__ fixed, int zl_out) {
   __shared__ BuildLDS B;
   const uint32_t c = blockIdx.x;
   const uint32_t lane = threadIdx.x;
@@ -3712,7 +3722,7 @@ __global__ void __launch_bounds__(64) zs_unit_header_kernel(const ZsJobDev *__re
     dbits = 5;
   } else if (wave_dyn_header<D64>(B, w, end_byte, bit, tabg, ctab, lbits, dbits, img, img + LROOT_N,
                                   reinterpret_cast<uint8_t *>(img + LROOT_N + DROOT_N), walk,
-                                  tabg + TABLE_LTAIL_OFF)) {
+                                  tabg + TABLE_LTAIL_OFF, zl_out != 0)) {
     return;
   }
   if (lane == 0) {
@@ -3850,15 +3860,22 @@ extern "C" void zs_launch_parse(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads
                                 int wave_units, hipStream_t st, int ctx) {
   if (!nchunks) return;
   SplitWs &g_split = g_splits[ctx & 1];
+  if (wave_units == 2 && split_reserve(ctx, nchunks) != 0) {  // no room for the split state: the lane parse
+    (void)hipGetLastError();
+    wave_units = 0;
+  }
+  // the split parse reads only the compact and walk tables of a unit's first
+  // block (a failed split decodes its header again): no zlib-layout copy
+  const int zl_out = wave_units == 2 ? 0 : 1;
   if (d64)
     hipLaunchKernelGGL(zs_unit_header_kernel<true>, dim3(nchunks), dim3(WAVE), 0, st, d_jobs, d_heads, d_chunks, d_tables,
-                       d_fixed);
+                       d_fixed, zl_out);
   else
     hipLaunchKernelGGL(zs_unit_header_kernel<false>, dim3(nchunks), dim3(WAVE), 0, st, d_jobs, d_heads, d_chunks, d_tables,
-                       d_fixed);
+                       d_fixed, zl_out);
   uint32_t *order = nullptr;
   if (sort_units(ctx, d_jobs, d_chunks, nchunks, 0, &order, st)) return;
-  if (wave_units == 2 && split_reserve(ctx, nchunks) == 0) {
+  if (wave_units == 2) {
     uint32_t *counts = g_split.lists + 2 * g_split.cap;
     uint32_t *lists = g_split.lists;
     (void)hipMemsetAsync(counts, 0, 3 * sizeof(uint32_t), st);  // splits, leftovers, the split's next unit
@@ -3873,19 +3890,21 @@ extern "C" void zs_launch_parse(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads
       return (uint32_t)cus * std::max<uint32_t>(1u, (uint32_t)lds / (uint32_t)sizeof(WalkLDS));
     }();
     const dim3 wgrid((nchunks + WAVE - 1) / WAVE), sgrid(split_grid(nchunks));
+    // (tests) ZS_SPLIT_LEFT=1: every split unit fails its check and goes to the leftovers
+    static const int force_left = getenv("ZS_SPLIT_LEFT") ? 1 : 0;
     // the leftover list lives at lists + nchunks: the kernels index it that way
     if (d64) {
       hipLaunchKernelGGL(zs_walk_kernel<true>, wgrid, dim3(WAVE), 0, st, d_jobs, d_heads, d_chunks, nchunks, d_tables,
                          order, pool, lane_map, g_split.walks, g_split.cps, lists, counts);
       hipLaunchKernelGGL(zs_split_kernel<true>, sgrid, dim3(WAVE), 0, st, d_jobs, d_chunks, nchunks, d_tokens, d_tables,
-                         pool, g_split.walks, g_split.cps, lists, counts);
+                         pool, g_split.walks, g_split.cps, lists, counts, force_left);
       hipLaunchKernelGGL(zs_unitw_list_kernel<true>, sgrid, dim3(WAVE), 0, st, d_jobs, d_heads, d_chunks, d_tokens,
                          d_tables, d_fixed, lists + nchunks, counts + 1, pool, g_split.walks);
     } else {
       hipLaunchKernelGGL(zs_walk_kernel<false>, wgrid, dim3(WAVE), 0, st, d_jobs, d_heads, d_chunks, nchunks, d_tables,
                          order, pool, lane_map, g_split.walks, g_split.cps, lists, counts);
       hipLaunchKernelGGL(zs_split_kernel<false>, sgrid, dim3(WAVE), 0, st, d_jobs, d_chunks, nchunks, d_tokens, d_tables,
-                         pool, g_split.walks, g_split.cps, lists, counts);
+                         pool, g_split.walks, g_split.cps, lists, counts, force_left);
       hipLaunchKernelGGL(zs_unitw_list_kernel<false>, sgrid, dim3(WAVE), 0, st, d_jobs, d_heads, d_chunks, d_tokens,
                          d_tables, d_fixed, lists + nchunks, counts + 1, pool, g_split.walks);
     }
@@ -3896,10 +3915,6 @@ extern "C" void zs_launch_parse(const ZsJobDev *d_jobs, const ZsHeadDev *d_heads
         fprintf(stderr, "split: %u unit slots, %u walked, %u leftovers\n", nchunks, h[0], h[1]);
     }
     return;
-  }
-  if (wave_units == 2) {  // no room for the split state: the lane parse
-    (void)hipGetLastError();
-    wave_units = 0;
   }
   if (wave_units) {
     if (d64)
