@@ -53,6 +53,9 @@ def main():
     d = {NAMES[i]: v for i, v in enumerate(c) if i in NAMES}
     # expand2 flush counters in lane-parse slots the split parse leaves unused
     d.update({"x_pieces": c[6], "x_pieces_marked": c[7], "x_pieces_marked_tail": c[8], "x_markers": c[12]})
+    # unit headers (zs_unit_header_kernel, dynamic first blocks): cycles by phase
+    d.update({"uh_units": c[0], "uh_cyc": c[1], "uh_cyc_pro": c[2], "uh_cyc_lens": c[11], "uh_cyc_lit": c[13],
+              "uh_cyc_rest": c[14]})
     w = max(d["p_waves"], 1)
     b = max(d["e_blocks"], 1)
     derived = {
@@ -112,6 +115,8 @@ def main():
         "fv_steps_frac": d.get("fv_cyc_steps", 0) / max(d.get("fv_cyc_total", 0), 1),
         "fv_wave_steps_per_round": d.get("fv_wave_steps", 0) / max(d.get("fv_rounds", 0), 1),
         "fv_cycles_per_wave": d.get("fv_cyc_total", 0) / max(d.get("fv_waves", 0), 1),
+        "uh_cycles_per_unit": {k: d.get(k, 0) / max(d.get("uh_units", 0), 1)
+                               for k in ("uh_cyc", "uh_cyc_pro", "uh_cyc_lens", "uh_cyc_lit", "uh_cyc_rest")},
         # expand2 flush: 256-entry wave pieces holding a history marker (the emit's real work)
         "x_marked_piece_frac": d.get("x_pieces_marked", 0) / max(d.get("x_pieces", 0), 1),
         "x_marked_tail_frac": d.get("x_pieces_marked_tail", 0) / max(d.get("x_pieces_marked", 0), 1),

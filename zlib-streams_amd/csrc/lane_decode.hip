@@ -714,34 +714,48 @@ __device__ __forceinline__ uintptr_t readlane_ptr(const void *p, uint32_t ln) {
   return (uintptr_t)(((uint64_t)hi << 32) | lo);
 }
 
-// canonical tail of a distance code (lengths dl[0..n)); one lane writes it
+// canonical tail of a distance code (lengths dl[0..n), n <= 32): limits of
+// lengths 6..14 (u16 [0, 18)), the rank of each length 7..15's first code among
+// the tail codes (u8 [18, 27)), the tail symbols in canonical order (u8 [27,
+// 59)).  Wave-cooperative (round 6; one lane's serial loops over LDS were half
+// of a unit header's time): counts by ballots, lane i places symbol i.
 __device__ void build_dist_tail(const uint16_t *dl, uint32_t n, uint8_t *out) {
+  const uint32_t lane = lane_id();
+  const uint64_t lt_mask = (1ull << lane) - 1ull;
+  const uint32_t len = lane < n ? (dl[lane] & 15u) : 0u;
   uint32_t count[16];
-#pragma unroll
-  for (int L = 0; L < 16; L++) count[L] = 0;
-  for (uint32_t i = 0; i < n; i++) count[dl[i] & 15u]++;
   count[0] = 0;
+#pragma unroll
+  for (int L = 1; L < 16; L++) count[L] = (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(len == (uint32_t)L));
   uint32_t code = 0, first[16];
   first[0] = 0;
+#pragma unroll
   for (int L = 1; L < 16; L++) {
     code = (code + count[L - 1]) << 1;
     first[L] = code;
   }
-  uint16_t *lim = reinterpret_cast<uint16_t *>(out);
+  uint32_t v = 0, off = 0, rank = 0;  // lane k < 9: limit k and rank k; lane i: its rank among the tail
+#pragma unroll
   for (int k = 0; k < 9; k++) {
     const int L = 6 + k;
-    const uint32_t v = (first[L] + count[L]) << (15 - L);
-    lim[k] = (uint16_t)min(v, 0xffffu);
-  }
-  uint32_t rank = 0;
-  for (int k = 0; k < 9; k++) {
-    out[18 + k] = (uint8_t)rank;
+    if (lane == (uint32_t)k) {
+      v = min((first[L] + count[L]) << (15 - L), 0xffffu);
+      off = rank;
+    }
     rank += count[7 + k];
   }
-  uint32_t r = 0;
-  for (int L = 7; L < 16; L++)
-    for (uint32_t i = 0; i < n; i++)
-      if (dl[i] == (uint32_t)L && r < 32) out[27 + r++] = (uint8_t)i;
+  if (lane < 9u) {
+    reinterpret_cast<uint16_t *>(out)[lane] = (uint16_t)v;
+    out[18 + lane] = (uint8_t)off;
+  }
+  uint32_t base = 0, mine = 64u;
+#pragma unroll
+  for (int L = 7; L < 16; L++) {
+    const uint64_t m = __builtin_amdgcn_ballot_w64(len == (uint32_t)L);
+    if (len == (uint32_t)L) mine = base + (uint32_t)__builtin_popcountll(m & lt_mask);
+    base += (uint32_t)__builtin_popcountll(m);
+  }
+  if (mine < 32u) out[27 + mine] = (uint8_t)lane;
 }
 
 // The literal/length code's canonical tail for the split parse's walk (codes
@@ -833,9 +847,12 @@ template <bool D64>
 __device__ int wave_dyn_header(BuildLDS &B, const uint32_t *w, uint32_t end_byte, uint32_t &bit, uint32_t *tabg,
                                uint16_t *ctab, uint32_t &lbits, uint32_t &dbits, uint16_t *lroot_out,
                                uint16_t *droot_out, uint8_t *dtail_out, uint8_t *walk_out = nullptr,
-                               uint32_t *ltail_out = nullptr, bool zl_out = true) {
+                               uint32_t *ltail_out = nullptr, bool zl_out = true, uint64_t *kt = nullptr) {
   const uint32_t lane = lane_id();
   const uint32_t limit = end_byte * 8u;
+#if KP_ON
+  if (kt) kt[0] = KP_NOW();
+#endif
   StageBits sb;
   stage_bits(B, w, end_byte, bit, sb);
   if (bit + 14 > limit) {
@@ -903,6 +920,9 @@ __device__ int wave_dyn_header(BuildLDS &B, const uint32_t *w, uint32_t end_byte
     bit += o;
   }
   __builtin_amdgcn_wave_barrier();
+#if KP_ON
+  if (kt) kt[1] = KP_NOW();
+#endif
   if (uni(B.lens[256]) == 0) {
     return ZD_ERROR | (ZM_MISSING_EOB << 8);
   }
@@ -922,6 +942,9 @@ __device__ int wave_dyn_header(BuildLDS &B, const uint32_t *w, uint32_t end_byte
     for (uint32_t i = lane; i < (1u << WK_LBITS); i += WAVE) walk_out[i] = (uint8_t)walk_len_z<D64>(B.tab, lbits, i);
   if (ltail_out) build_lit_tail(B.lens, nlen, ltail_out);
   __builtin_amdgcn_wave_barrier();
+#if KP_ON
+  if (kt) kt[2] = KP_NOW();
+#endif
   dbits = 6;
   if (build_table(T_DISTS, B.lens + nlen, ndist, B.tab, &dbits, B.sorted, B.scr, D64 ? 1 : 0)) {
     return ZD_ERROR | (ZM_DIST_SET << 8);
@@ -935,7 +958,7 @@ __device__ int wave_dyn_header(BuildLDS &B, const uint32_t *w, uint32_t end_byte
   if (walk_out)
     for (uint32_t i = lane; i < (1u << WK_DBITS); i += WAVE)
       walk_out[(1u << WK_LBITS) + i] = (uint8_t)walk_dist_z(B.tab, dbits, i);
-  if (lane == 0) build_dist_tail(B.lens + nlen, ndist, dtail_out);
+  build_dist_tail(B.lens + nlen, ndist, dtail_out);
   __builtin_amdgcn_wave_barrier();
   return 0;
 }
@@ -3679,6 +3702,10 @@ __global__ void __launch_bounds__(64) zs_unit_header_kernel(const ZsJobDev *__re
                                                              ZsChunkDev *__restrict__ units, uint32_t *__restrict__ tables,
                                                              const uint32_t *__restrict__ fixed, int zl_out) {
   __shared__ BuildLDS B;
+#if KP_ON
+  const uint64_t kt0 = KP_NOW();
+  uint64_t kt[3] = {kt0, kt0, kt0};
+#endif
   const uint32_t c = blockIdx.x;
   const uint32_t lane = threadIdx.x;
   const ZsChunkDev ch = units[c];
@@ -3716,19 +3743,34 @@ __global__ void __launch_bounds__(64) zs_unit_header_kernel(const ZsJobDev *__re
     img[LROOT_N + lane] = compact_dist_entry(fixed[512 + (lane & 31u)]);
     for (uint32_t i = lane; i < (1u << WK_DBITS); i += WAVE) walk[(1u << WK_LBITS) + i] = (uint8_t)walk_dist_z(fixed + 512, 5u, i);
     __builtin_amdgcn_wave_barrier();
-    if (lane == 0) build_dist_tail(B.lens, 32, reinterpret_cast<uint8_t *>(img + LROOT_N + DROOT_N));
+    build_dist_tail(B.lens, 32, reinterpret_cast<uint8_t *>(img + LROOT_N + DROOT_N));
     if (lane < 16) tabg[TABLE_LTAIL_OFF + lane] = lane < 4 ? 0x80008000u : 0u;  // no code past 9 bits
     lbits = 9;
     dbits = 5;
   } else if (wave_dyn_header<D64>(B, w, end_byte, bit, tabg, ctab, lbits, dbits, img, img + LROOT_N,
                                   reinterpret_cast<uint8_t *>(img + LROOT_N + DROOT_N), walk,
-                                  tabg + TABLE_LTAIL_OFF, zl_out != 0)) {
+                                  tabg + TABLE_LTAIL_OFF, zl_out != 0
+#if KP_ON
+                                  , kt
+#endif
+                                  )) {
     return;
   }
   if (lane == 0) {
     units[c].hdr_bit = bit;
     units[c].hdr_info = 1u | ((hdr3 & 1u) << 1) | (lbits << 8) | (dbits << 12);
   }
+#if KP_ON  // (lane-parse slots the split parse leaves unused) units, cycles: all, prologue, code lengths, lit/len tables, rest
+  if (btype == 2u) {
+    const uint64_t te = KP_NOW();
+    KP_ADD(0, 1);
+    KP_ADD(1, te - kt0);
+    KP_ADD(2, kt[0] - kt0);
+    KP_ADD(11, kt[1] - kt[0]);
+    KP_ADD(13, kt[2] - kt[1]);
+    KP_ADD(14, te - kt[2]);
+  }
+#endif
 }
 
 // compact copies of the fixed tables (after zs_fixed_tables_kernel's zlib layout)
