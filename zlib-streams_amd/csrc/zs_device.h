@@ -56,7 +56,13 @@ __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_re
 // the long-code sub-tables keep zlib's allocation order and sizing.
 // Returns 0 ok, -1 bad code set, 1 table space exceeded.  `*root` is in/out.
 // ---------------------------------------------------------------------------
-static __device__ __attribute__((noinline)) int build_table(int type, const uint16_t *lens, uint32_t n, uint32_t *table, uint32_t *root_io,
+#ifndef BUILD_TABLE_ATTR
+// (round 6) inlined: as a call it cost zs_unit_header_kernel 102 VGPRs and
+// scratch (occupancy 4); inlined 49 VGPRs, occupancy 7, no other kernel's
+// occupancy changes
+#define BUILD_TABLE_ATTR __attribute__((always_inline))
+#endif
+static __device__ BUILD_TABLE_ATTR int build_table(int type, const uint16_t *lens, uint32_t n, uint32_t *table, uint32_t *root_io,
                            uint16_t *sorted, uint32_t *scratch16, int d64) {
   const uint32_t lane = lane_id();
   const uint64_t lt_mask = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
