@@ -837,6 +837,96 @@ __device__ void build_lit_tail(const uint16_t *ll, uint32_t n, uint32_t *out) {
   }
 }
 
+// The code lengths of a dynamic header, 64 bit offsets at a time, all in
+// parallel (round 6, for zs_unit_header_kernel): lane l decodes the
+// code-length symbol at bit + l; the true symbols of the window are found by
+// pointer doubling over "next offset" (symbol k at P_k = J^k(0)), their output
+// positions by a prefix sum of their repeat counts, a repeat-previous (16) its
+// value by a max-scan for the last explicit length.  Same B.lens and end bit as
+// the serial loop in wave_dyn_header for every header zlib accepts; on any
+// error it returns nonzero without telling which (the unit header then leaves
+// the unit to the parse pass, which decodes the header again and reports it).
+__device__ int wave_code_lengths_par(BuildLDS &B, const uint32_t *w, uint32_t end_byte, StageBits &sb, uint32_t &bit,
+                                     uint32_t total, uint32_t cmask) {
+  const uint32_t lane = lane_id();
+  const uint32_t limit = end_byte * 8u;
+  uint32_t have = 0, prevlen = 0;
+  while (have < total) {
+    if (bit - sb.base > (STAGE_WORDS - 2) * 32u - 128u) stage_bits(B, w, end_byte, bit, sb);
+    const uint32_t xj = sb.peek(bit + lane, 14);
+    const uint32_t ej = B.tab[xj & cmask];
+    const uint32_t ebj = e_bits(ej), evj = e_val(ej);
+    const uint32_t xbj = evj < 16 ? 0u : (evj == 16 ? 2u : (evj == 17 ? 3u : 7u));
+    const uint32_t repj = evj < 16 ? 1u : ((evj == 18 ? 11u : 3u) + ((xj >> ebj) & ((1u << xbj) - 1u)));
+    const uint32_t lenj = ebj + xbj;
+    if (__builtin_amdgcn_ballot_w64(lenj == 0u)) return -1;  // (a complete code-length code has no 0-bit entry)
+    // J^(2^b): the offset 2^b symbols on (64: past the window)
+    uint32_t Jb[6];
+    Jb[0] = min(lane + lenj, 64u);
+#pragma unroll
+    for (int b = 1; b < 6; b++) {
+      const uint32_t pv = Jb[b - 1];
+      const uint32_t g = (uint32_t)__shfl((int)pv, (int)(pv & 63u));
+      Jb[b] = pv >= 64u ? 64u : g;
+    }
+    uint32_t P = 0;  // symbol k = lane starts at offset P (64: not in this window)
+#pragma unroll
+    for (int b = 0; b < 6; b++) {
+      const uint32_t g = (uint32_t)__shfl((int)Jb[b], (int)(P & 63u));
+      if ((lane >> b) & 1u) P = P >= 64u ? 64u : g;
+    }
+    const bool valid = P < 64u;
+    const uint32_t src = P & 63u;
+    const uint32_t ev = (uint32_t)__shfl((int)evj, (int)src), rep = (uint32_t)__shfl((int)repj, (int)src);
+    const uint32_t ln = (uint32_t)__shfl((int)lenj, (int)src);
+    // output positions: exclusive prefix sum of the repeat counts
+    const uint32_t cnt = valid ? rep : 0u;
+    uint32_t incl = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t t = (uint32_t)__shfl_up((int)incl, o);
+      if (lane >= (uint32_t)o) incl += t;
+    }
+    const uint32_t hk = have + incl - cnt;
+    const bool act = valid && hk < total;
+    const bool err = act && ((bit + P + ln > limit) || (ev == 16u && hk == 0u) || (hk + rep > total));
+    if (__builtin_amdgcn_ballot_w64(err)) return -1;
+    // values: 17 / 18 zeros, 16 the last explicit length before it
+    const uint32_t vbase = ev < 16u ? ev : 0u;
+    int lastx = (act && ev != 16u) ? (int)lane : -1;
+    {  // exclusive max-scan of lastx
+      int m = lastx;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(m, o);
+        if (lane >= (uint32_t)o) m = max(m, t);
+      }
+      const int ex = __shfl_up(m, 1);
+      lastx = lane ? ex : -1;
+    }
+    const uint32_t pvv = (uint32_t)__shfl((int)vbase, lastx < 0 ? 0 : lastx);
+    const uint32_t val = ev == 16u ? (lastx < 0 ? prevlen : pvv) : vbase;
+    if (act && rep == 1u) B.lens[hk] = (uint16_t)val;
+    uint64_t m = __builtin_amdgcn_ballot_w64(act && rep > 1u);
+    while (m) {
+      const uint32_t j = (uint32_t)__builtin_ctzll(m);
+      m &= m - 1ull;
+      const uint32_t b0 = __builtin_amdgcn_readlane(hk, j), r = __builtin_amdgcn_readlane(rep, j);
+      const uint32_t v = __builtin_amdgcn_readlane(val, j);
+      for (uint32_t t = lane; t < r; t += WAVE) B.lens[b0 + t] = (uint16_t)v;
+    }
+    const uint64_t am = __builtin_amdgcn_ballot_w64(act);
+    const uint32_t nk = (uint32_t)__builtin_popcountll(am);  // the active symbols are a prefix
+    if (nk == 0u) return -1;
+    const uint32_t last = nk - 1u;
+    bit += __builtin_amdgcn_readlane(P, last) + __builtin_amdgcn_readlane(ln, last);
+    have = __builtin_amdgcn_readlane(hk, last) + __builtin_amdgcn_readlane(rep, last);
+    prevlen = __builtin_amdgcn_readlane(val, last);
+    __builtin_amdgcn_wave_barrier();
+  }
+  return 0;
+}
+
 // Dynamic block header after the 3 block-type bits (src/inflate.c:905-1033):
 // code-length code, code lengths, then the literal/length and distance tables
 // (src/inftrees.c restated in build_table) into the unit's global table area
@@ -847,7 +937,8 @@ template <bool D64>
 __device__ int wave_dyn_header(BuildLDS &B, const uint32_t *w, uint32_t end_byte, uint32_t &bit, uint32_t *tabg,
                                uint16_t *ctab, uint32_t &lbits, uint32_t &dbits, uint16_t *lroot_out,
                                uint16_t *droot_out, uint8_t *dtail_out, uint8_t *walk_out = nullptr,
-                               uint32_t *ltail_out = nullptr, bool zl_out = true, uint64_t *kt = nullptr) {
+                               uint32_t *ltail_out = nullptr, bool zl_out = true, bool par_lens = false,
+                               uint64_t *kt = nullptr) {
   const uint32_t lane = lane_id();
   const uint32_t limit = end_byte * 8u;
 #if KP_ON
@@ -876,6 +967,9 @@ __device__ int wave_dyn_header(BuildLDS &B, const uint32_t *w, uint32_t end_byte
   }
   const uint32_t total = nlen + ndist;
   const uint32_t cmask = (1u << cbits) - 1u;
+  if (par_lens) {
+    if (wave_code_lengths_par(B, w, end_byte, sb, bit, total, cmask)) return ZD_ERROR | (ZM_REPEAT << 8);
+  } else {
   // the code lengths, a 64-bit window at a time: every lane decodes the
   // code-length symbol starting at bit + lane, then the true symbols of the
   // window are followed from lane 0 with readlane (scalar), the checks and
@@ -918,6 +1012,7 @@ __device__ int wave_dyn_header(BuildLDS &B, const uint32_t *w, uint32_t end_byte
       o += eb + xb;
     }
     bit += o;
+  }
   }
   __builtin_amdgcn_wave_barrier();
 #if KP_ON
@@ -3749,7 +3844,7 @@ __global__ void __launch_bounds__(64) zs_unit_header_kernel(const ZsJobDev *__re
     dbits = 5;
   } else if (wave_dyn_header<D64>(B, w, end_byte, bit, tabg, ctab, lbits, dbits, img, img + LROOT_N,
                                   reinterpret_cast<uint8_t *>(img + LROOT_N + DROOT_N), walk,
-                                  tabg + TABLE_LTAIL_OFF, zl_out != 0
+                                  tabg + TABLE_LTAIL_OFF, zl_out != 0, true
 #if KP_ON
                                   , kt
 #endif
