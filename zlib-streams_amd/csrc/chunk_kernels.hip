@@ -1462,7 +1462,9 @@ __global__ void __launch_bounds__(LINK_THREADS) zs_linkseg_join_kernel(const ZsC
 // ---------------------------------------------------------------------------
 // Emit: u16 entries -> final bytes (one workgroup per chunk)
 // ---------------------------------------------------------------------------
+#ifndef EMIT_THREADS
 #define EMIT_THREADS 256
+#endif
 template <uint32_t HN>
 __global__ void __launch_bounds__(EMIT_THREADS) zs_emit_kernel(const ZsJobDev *__restrict__ jobs, const ZsChunkDev *__restrict__ chunks,
                                                                const uint16_t *__restrict__ scratch, const uint8_t *__restrict__ windows,
