@@ -86,7 +86,7 @@ def parse_args(argv=None):
     ap.add_argument("--stream-leg-mib", type=int, default=16, help="line-text stream of the one-handle run")
     ap.add_argument("--stream-handles", type=int, default=64, help="concurrent handles of the aggregate run")
     ap.add_argument("--stream-handle-mib", type=int, default=4, help="stream size per concurrent handle")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r05", "pmc_traffic.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r06", "pmc_traffic.json"),
                     help="PMC-derived HBM bytes per pipeline launch (null in the line when absent)")
     ap.add_argument("--no-c5-leg", action="store_true",
                     help="skip the configs[4] leg (the fixed 4096 x 4 MiB batch LPT-split across the ranks)")
