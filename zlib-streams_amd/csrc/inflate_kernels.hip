@@ -24,6 +24,10 @@
 #include <stdint.h>
 
 #include "zs_common.h"
+// the stream / wave decoders keep the table builder as a call (round 6: inlined
+// into them, one handle 252 -> 200 MiB/s and the perf harness's decompress
+// 685 -> 411 MiB/s; the block-parallel path's kernels inline it)
+#define BUILD_TABLE_ATTR __attribute__((noinline))
 #include "zs_device.h"
 #include "zs_check.h"
 

@@ -58,8 +58,8 @@ __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_re
 // ---------------------------------------------------------------------------
 #ifndef BUILD_TABLE_ATTR
 // (round 6) inlined: as a call it cost zs_unit_header_kernel 102 VGPRs and
-// scratch (occupancy 4); inlined 49 VGPRs, occupancy 7, no other kernel's
-// occupancy changes
+// scratch (occupancy 4); inlined 49 VGPRs, occupancy 7.  inflate_kernels.hip
+// keeps the call (its stream decoders were slower with it inlined)
 #define BUILD_TABLE_ATTR __attribute__((always_inline))
 #endif
 static __device__ BUILD_TABLE_ATTR int build_table(int type, const uint16_t *lens, uint32_t n, uint32_t *table, uint32_t *root_io,

@@ -364,9 +364,13 @@ def profile_read():
 
 
 PROFILE_STAGES = ("header", "find", "parse", "expand", "link", "emit", "serial_decode", "finalize")
-STAGE_KERNELS = {"header": "zs_header_kernel", "find": "zs_find_kernel + zs_find_fixed_kernel + zs_plan_kernel",
-                 "parse": "zs_unit_header_kernel + zs_lane_kernel + zs_chain_kernel",
-                 "expand": "zs_expand_kernel", "link": "zs_link_kernel", "emit": "zs_emit_kernel",
+STAGE_KERNELS = {"header": "zs_header_kernel",
+                 "find": "zs_find_kernel + zs_findval_kernel + zs_findsel_kernel + zs_find_fixed_kernel + zs_plan_kernel",
+                 "parse": "zs_unit_header_kernel + (split parse) zs_walk_kernel + zs_split_kernel + zs_unitw_list_kernel"
+                          " | zs_lane_kernel | zs_unitw_kernel, + zs_chain_kernel",
+                 "expand": "zs_expand2_kernel (deflate64: zs_expand_kernel)",
+                 "link": "zs_linkseg_kernel + zs_linkseg_join_kernel + zs_link_kernel (or the serial / prefix link)",
+                 "emit": "zs_emit_kernel",
                  "serial_decode": "zs_decode_kernel", "finalize": "zs_check_kernel + zs_finalize_kernel"}
 
 
